@@ -1,0 +1,71 @@
+"""numpy mirrors of the C-ABI structs in include/fme.h.
+
+fme_job (32 B) and fme_result (64 B) are plain PODs; these structured dtypes have the same
+field offsets so arrays can be handed to the library (or the oracle) as raw pointers.
+"""
+import numpy as np
+
+JOB_DTYPE = np.dtype(
+    [
+        ("x", "<u2"), ("y", "<u2"),
+        ("w", "u1"), ("h", "u1"),
+        ("org_id", "u1"), ("ref_id", "u1"),
+        ("mv_x", "<i2"), ("mv_y", "<i2"),
+        ("mvp_x", "<i2"), ("mvp_y", "<i2"),
+        ("lt_x", "<i2"), ("lt_y", "<i2"), ("rb_x", "<i2"), ("rb_y", "<i2"),
+        ("flags", "u1"), ("lambda_id", "u1"), ("bits_in", "<u2"),
+        ("key_offset", "<i4"),
+    ],
+    align=False,
+)
+assert JOB_DTYPE.itemsize == 32
+
+RESULT_DTYPE = np.dtype(
+    [
+        ("mv_int_x", "<i2"), ("mv_int_y", "<i2"),
+        ("mv_x", "<i2"), ("mv_y", "<i2"),
+        ("half_x", "i1"), ("half_y", "i1"), ("qtr_x", "i1"), ("qtr_y", "i1"),
+        ("frac_cost", "<u4"), ("cost", "<u4"), ("bits", "<u4"), ("c", "<u4"),
+        ("emi", "<u4", (8,)),
+        ("n_emi", "u1"), ("nn_class", "u1"), ("status", "<u2"),
+    ],
+    align=False,
+)
+assert RESULT_DTYPE.itemsize == 64
+
+CONFIG_FIELDS = ("bit_depth", "use_hadamard", "nn_mode", "qp", "fast_inter_mode", "max_jobs")
+
+JOB_EMI = 0x01
+JOB_BIPRED = 0x02
+JOB_LOSSLESS = 0x04
+
+RES_NN_STALE = 0x01
+RES_NN_UNINIT = 0x02
+
+MAX_PICTURES = 64
+MAX_LAMBDAS = 64
+NN_PARAMS = 2060
+
+E_INVALID, E_DEVICE, E_NOMEM, E_UNSUPPORTED, E_STATE = -1, -2, -3, -4, -5
+
+# Fields that define parity (everything the reference computes).
+PARITY_FIELDS = ("mv_int_x", "mv_int_y", "mv_x", "mv_y", "half_x", "half_y", "qtr_x", "qtr_y",
+                 "frac_cost", "cost", "bits", "c", "n_emi", "nn_class")
+
+
+def compare_results(a, b, fields=PARITY_FIELDS):
+    """Return (n_mismatched_jobs, first_bad_index_or_None, per-field mismatch counts)."""
+    bad = np.zeros(len(a), dtype=bool)
+    counts = {}
+    for f in fields:
+        m = a[f] != b[f]
+        counts[f] = int(m.sum())
+        bad |= m
+    # emi: only the n_emi pushed values are defined
+    n = a["n_emi"].astype(np.int64)
+    slot = np.arange(8)[None, :] < n[:, None]
+    m = ((a["emi"] != b["emi"]) & slot).any(axis=1)
+    counts["emi"] = int(m.sum())
+    bad |= m
+    idx = np.flatnonzero(bad)
+    return int(bad.sum()), (int(idx[0]) if len(idx) else None), counts

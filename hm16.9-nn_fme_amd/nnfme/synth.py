@@ -1,0 +1,156 @@
+"""Synthetic inputs for the fractional-ME path (SURVEY.md §8(d) "Synthetic inputs").
+
+* YUV: 8-bit luma = 128 + sum_{i<12} a_i sin(fx_i (x + 0.37 t) + fy_i (y + 0.21 t) + phi_i)
+  + N(0, 2), rounded and clipped; a ~ U[10,40], fx, fy ~ U[0.01, 0.2], phi ~ U[0, 2pi];
+  numpy.default_rng(seed) with seed 1 (416x240), 2 (1920x1080), 3 (2560x1600).
+* Jobs: the PU-size mix measured on the 1080p P-frame, integer MVs
+  U[-64,64]^2 clipped into the search range, AMVP predictors U[-256,256]^2 quarter-pel,
+  search range = xSetSearchRange(mvp, 64) with TComDataCU::clipMv (TEncSearch.cpp:4602-4624,
+  TComDataCU.cpp:2773-2786), lambda per frame from the LDP GOP table below.
+"""
+import numpy as np
+
+from .abi import JOB_BIPRED, JOB_DTYPE, JOB_EMI
+
+SEEDS = {(416, 240): 1, (1920, 1080): 2, (2560, 1600): 3}
+
+# PU size (W, H) -> share of FracDIF calls on the 1080p LDP QP22 P-frame.
+PU_MIX = [
+    ((8, 4), 0.300), ((4, 8), 0.300), ((8, 8), 0.150), ((8, 16), 0.075), ((16, 8), 0.075),
+    ((16, 16), 0.037), ((32, 16), 0.018), ((16, 32), 0.018), ((32, 32), 0.009),
+    ((64, 32), 0.0045), ((32, 64), 0.0045), ((64, 64), 0.0022),
+    # AMP shapes, ~0.6 % together
+    ((4, 16), 0.00075), ((12, 16), 0.00075), ((16, 4), 0.00075), ((16, 12), 0.00075),
+    ((8, 32), 0.00075), ((24, 32), 0.00075), ((32, 8), 0.00075), ((32, 24), 0.00075),
+]
+ALL_PU_SIZES = [s for s, _ in PU_MIX] + [(64, 16), (64, 48), (16, 64), (48, 64)]
+
+# lambda per POC % 4 for lowdelay_P (cfg Frame1-4).
+LDP_LAMBDA = {
+    22: (7.340, 20.196, 14.797, 20.196),
+    27: (23.30, 88.78, 66.55, 88.78),
+    32: (73.98, 360.16, 273.43, 360.16),
+    37: (234.9, 1193.1, 947.0, 1193.1),
+}
+
+SEARCH_RANGE = 64      # cfg SearchRange
+MAX_CU = 64
+
+
+def synth_luma(width, height, t, seed=None):
+    """One synthetic 8-bit luma frame (uint8[height, width]) at time index t."""
+    if seed is None:
+        seed = SEEDS.get((width, height), 7)
+    rng = np.random.default_rng(seed)
+    a = rng.uniform(10, 40, 12)
+    fx = rng.uniform(0.01, 0.2, 12)
+    fy = rng.uniform(0.01, 0.2, 12)
+    phi = rng.uniform(0, 2 * np.pi, 12)
+    noise = np.random.default_rng(seed * 1000 + t + 1).normal(0, 2, (height, width))
+    x = np.arange(width, dtype=np.float64)[None, :]
+    y = np.arange(height, dtype=np.float64)[:, None]
+    acc = np.full((height, width), 128.0)
+    for i in range(12):
+        acc += a[i] * np.sin(fx[i] * (x + 0.37 * t) + fy[i] * (y + 0.21 * t) + phi[i])
+    acc += noise
+    return np.clip(np.rint(acc), 0, 255).astype(np.uint8)
+
+
+def _clip_mv_qpel(v, pos, pic, size_max=MAX_CU):
+    """TComDataCU::clipMv on quarter-pel values, with the PU position standing in for the
+    CU position (TComDataCU.cpp:2778-2785)."""
+    vmax = (pic + 8 - pos - 1) << 2
+    vmin = (-size_max - 8 - pos + 1) << 2
+    return np.minimum(vmax, np.maximum(vmin, v))
+
+
+def _div4_round(v):
+    """TComMv::divideByPowerOf2(2) with ME_ENABLE_ROUNDING_OF_MVS (TComMv.h:122-130)."""
+    return (v + 2) >> 2
+
+
+def sample_sizes(rng, n, mix=PU_MIX):
+    sizes = np.array([s for s, _ in mix], dtype=np.int32)
+    p = np.array([q for _, q in mix], dtype=np.float64)
+    p /= p.sum()
+    idx = rng.choice(len(mix), size=n, p=p)
+    return sizes[idx, 0], sizes[idx, 1]
+
+
+def make_jobs(rng, width, height, n, org_id, ref_ids, lambda_ids, sizes=None, bipred_frac=0.0,
+              bits_in_max=6):
+    """n synthetic jobs for one frame.
+
+    ref_ids / lambda_ids: per-job choice lists (a ref picture slot and the lambda slot of the
+    frame).  bipred_frac: share of bi-pred jobs (no EMI, key block from make_bipred_keys).
+    Returns a JOB_DTYPE array; bi-pred rows have key_offset = -2 (to be assigned).
+    """
+    jobs = np.zeros(n, dtype=JOB_DTYPE)
+    if sizes is None:
+        w, h = sample_sizes(rng, n)
+    else:
+        w, h = sizes
+        w = np.broadcast_to(np.asarray(w, dtype=np.int32), (n,)).copy()
+        h = np.broadcast_to(np.asarray(h, dtype=np.int32), (n,)).copy()
+    x = (rng.integers(0, (width - w) // 4 + 1)) * 4
+    y = (rng.integers(0, (height - h) // 4 + 1)) * 4
+    mvp_x = rng.integers(-256, 257, n)
+    mvp_y = rng.integers(-256, 257, n)
+    # xSetSearchRange(mvp, SearchRange): clip(pred) -/+ SR<<2, clip, round >> 2.
+    cpx = _clip_mv_qpel(mvp_x, x, width)
+    cpy = _clip_mv_qpel(mvp_y, y, height)
+    lt_x = _div4_round(_clip_mv_qpel(cpx - (SEARCH_RANGE << 2), x, width))
+    rb_x = _div4_round(_clip_mv_qpel(cpx + (SEARCH_RANGE << 2), x, width))
+    lt_y = _div4_round(_clip_mv_qpel(cpy - (SEARCH_RANGE << 2), y, height))
+    rb_y = _div4_round(_clip_mv_qpel(cpy + (SEARCH_RANGE << 2), y, height))
+    mv_x = np.clip(rng.integers(-64, 65, n), lt_x, rb_x)
+    mv_y = np.clip(rng.integers(-64, 65, n), lt_y, rb_y)
+    jobs["x"], jobs["y"], jobs["w"], jobs["h"] = x, y, w, h
+    jobs["org_id"] = org_id
+    jobs["ref_id"] = rng.choice(np.asarray(ref_ids), size=n)
+    jobs["lambda_id"] = rng.choice(np.asarray(lambda_ids), size=n)
+    jobs["mv_x"], jobs["mv_y"] = mv_x, mv_y
+    jobs["mvp_x"], jobs["mvp_y"] = mvp_x, mvp_y
+    jobs["lt_x"], jobs["lt_y"], jobs["rb_x"], jobs["rb_y"] = lt_x, lt_y, rb_x, rb_y
+    jobs["bits_in"] = rng.integers(1, bits_in_max + 1, n)
+    jobs["flags"] = JOB_EMI
+    jobs["key_offset"] = -1
+    if bipred_frac > 0:
+        bi = rng.random(n) < bipred_frac
+        jobs["flags"][bi] = JOB_BIPRED
+        jobs["key_offset"][bi] = -2
+    return jobs
+
+
+def make_bipred_keys(rng, jobs, pictures):
+    """Key blocks 2*org - pred_other (TComYuv::removeHighFreq, TComYuv.cpp:411-455, no clip)
+    for rows with key_offset == -2; pred_other is an integer-displaced block of another
+    picture.  Assigns key_offset and returns the int16 key buffer."""
+    sel = np.flatnonzero(jobs["key_offset"] == -2)
+    sizes = jobs["w"][sel].astype(np.int64) * jobs["h"][sel].astype(np.int64)
+    offs = np.concatenate([[0], np.cumsum(sizes)])
+    keys = np.zeros(int(offs[-1]), dtype=np.int16)
+    ids = sorted(pictures)
+    for k, i in enumerate(sel):
+        j = jobs[i]
+        w, h, x, y = int(j["w"]), int(j["h"]), int(j["x"]), int(j["y"])
+        org = pictures[int(j["org_id"])].astype(np.int16)
+        oth = pictures[ids[int(rng.integers(0, len(ids)))]]
+        dx, dy = int(rng.integers(-8, 9)), int(rng.integers(-8, 9))
+        H, W = oth.shape
+        rows = np.clip(np.arange(y + dy, y + dy + h), 0, H - 1)
+        cols = np.clip(np.arange(x + dx, x + dx + w), 0, W - 1)
+        pred = oth[rows][:, cols].astype(np.int16)
+        key = 2 * org[y:y + h, x:x + w] - pred
+        keys[offs[k]:offs[k + 1]] = key.reshape(-1)
+        jobs["key_offset"][i] = offs[k]
+    return keys
+
+
+def lambdas_for_frame(qp, poc):
+    return LDP_LAMBDA[qp if qp in LDP_LAMBDA else 22][poc % 4]
+
+
+def jobs_per_frame(width, height, refs=4, calls_per_ctu=423):
+    ctus = ((width + 63) // 64) * ((height + 63) // 64)
+    return ctus * calls_per_ctu * refs

@@ -1,0 +1,190 @@
+/*
+ * fme.h — C-ABI of the MI355X-native fractional-pel motion-estimation path.
+ *
+ * This is the drop-in boundary for HM-16.9-NN_FME's sub-pel hot path:
+ *
+ *   TEncSearch::xMotionEstimation tail   (TEncSearch.cpp:4529-4597)
+ *     EMI 8-point integer square step    (TEncSearch.cpp:5037-5050, 1324-1377, 1078-1189)
+ *     TEncSearch::xPatternSearchFracDIF  (TEncSearch.h:423-432, TEncSearch.cpp:5232-5269)
+ *       xExtDIFUpSamplingH/Q             (TEncSearch.cpp:6331-6532)
+ *       xPatternRefinement               (TEncSearch.cpp:1591-1645)
+ *     NN_pred()                          (TEncSearch.cpp:85-204, globals 55-77)
+ *
+ * The reference exposes no plugin/FFI API for this path: it is a set of protected members
+ * of TEncSearch plus a global function with global state.  This header is what a maintainer
+ * binds instead: plain pointers, sizes and POD structs, no torch/HIP
+ * types in the signatures (streams are passed as `void*` = hipStream_t, may be NULL).
+ *
+ * Every entry point returns 0 on success and a negative FME_E_* code on failure; the
+ * message of the last failure on the calling thread is available from fme_last_error().
+ * Nothing aborts.
+ */
+#ifndef FME_H
+#define FME_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define FME_ABI_VERSION 1
+
+/* ---- error codes ---------------------------------------------------------------- */
+#define FME_OK            0
+#define FME_E_INVALID    -1   /* bad argument (null pointer, bad size, unknown id)        */
+#define FME_E_DEVICE     -2   /* HIP runtime error                                        */
+#define FME_E_NOMEM      -3   /* device or host allocation failed                         */
+#define FME_E_UNSUPPORTED -4  /* configuration not supported (bit depth != 8, PU size)     */
+#define FME_E_STATE      -5   /* missing picture / weights / lambda for a job             */
+
+/* ---- limits ---------------------------------------------------------------------- */
+#define FME_MAX_PICTURES  64   /* picture slots per context (org + reference pictures)    */
+#define FME_MAX_LAMBDAS   64   /* motion-lambda table entries per context                 */
+#define FME_NN_PARAMS     2060 /* float parameters of the 2-layer master net (17-22-20-49)*/
+
+/* ---- configuration (TAppEncCfg.cpp options the path depends on) ------------------- */
+typedef struct fme_config {
+  int32_t bit_depth;        /* internal luma bit depth; only 8 is supported              */
+  int32_t use_hadamard;     /* HadamardME (TAppEncCfg.cpp:760): SATD vs SAD in FracDIF   */
+  int32_t nn_mode;          /* 0: standard FracDIF MV (TEncSearch.cpp:4587-4588 variant)
+                               1: NN_pred() MV (shipped behaviour, TEncSearch.cpp:4590-4591) */
+  int32_t qp;               /* base QP (-q); selects the weight set like TEncSearch::init
+                               (TEncSearch.cpp:472/625/775/925: 27, 32, 37, else 22)     */
+  int32_t fast_inter_mode;  /* FEN (TAppEncCfg.cpp:888): 1 or 3 -> even-row SAD for the
+                               W in {12,24,48} integer metric when H > 8 (TEncSearch.cpp:1158-1164) */
+  int32_t max_jobs;         /* capacity hint for device work buffers (0 = grow on demand) */
+} fme_config;
+
+/* ---- one PU sub-pel refinement job (32 bytes) -------------------------------------- *
+ * Mirrors what xMotionEstimation hands to the path for one (PU, reference picture):
+ *   x, y, w, h       PU luma rectangle in the picture (getPartIndexAndSize)
+ *   org_id, ref_id   picture slots of the original and the reference picture
+ *   mv_x, mv_y       full-pel integer MV: the TZ-search best before the EMI square step
+ *                    when FME_JOB_EMI is set, else the final integer MV (bi-pred full search)
+ *   mvp_x, mvp_y     AMVP predictor, quarter-pel (TComRdCost::setPredictor)
+ *   lt_*, rb_*       full-pel search range passed to xTZSearch (xSetSearchRange output)
+ *   flags            FME_JOB_*
+ *   lambda_id        index into the context's motion-lambda table
+ *   bits_in          ruiBits on entry to xMotionEstimation
+ *   key_offset       FME_JOB_BIPRED: element offset of the W*H int16 key block
+ *                    (2*org - pred_other, TComYuv::removeHighFreq) in the key buffer
+ *                    set by fme_set_keys(); the block is stored row-major with stride W.
+ *                    -1: the key is the original picture at (x, y).
+ */
+#define FME_JOB_EMI       0x01u  /* run the EMI square step (uni-pred TZ path)           */
+#define FME_JOB_BIPRED    0x02u  /* bi-pred iteration: weight 0.5 in the cost tail        */
+#define FME_JOB_LOSSLESS  0x04u  /* CU transquant bypass: SAD instead of SATD            */
+
+typedef struct fme_job {
+  uint16_t x, y;
+  uint8_t  w, h;
+  uint8_t  org_id, ref_id;
+  int16_t  mv_x, mv_y;
+  int16_t  mvp_x, mvp_y;
+  int16_t  lt_x, lt_y, rb_x, rb_y;
+  uint8_t  flags;
+  uint8_t  lambda_id;
+  uint16_t bits_in;
+  int32_t  key_offset;
+} fme_job;
+
+/* ---- one result (64 bytes) ---------------------------------------------------------- *
+ *   mv_int_*    integer MV after the EMI step (== job mv when no EMI), full-pel
+ *   mv_*        final MV, quarter-pel (rcMv after TEncSearch.cpp:4590-4591)
+ *   half_xy, qtr_xy FracDIF offsets rcMvHalf / rcMvQter, each in {-1,0,1}
+ *   frac_cost   FracDIF ruiCost (best quarter-pel SATD + MV cost)
+ *   cost, bits  xMotionEstimation outputs ruiCost, ruiBits (TEncSearch.cpp:4595-4596)
+ *   c           C: integer distortion at mv_int (TEncSearch.cpp:5049-5050)
+ *   emi[]       the distortions pushed into array_e by this job, n_emi of them
+ *   nn_class    NN_pred() class 0..48 (255 when nn_mode == 0)
+ *   status      FME_RES_* bits
+ */
+#define FME_RES_NN_STALE   0x01u  /* NN read at least one slot not written by this job     */
+#define FME_RES_NN_UNINIT  0x02u  /* NN read a slot never written in this context (read as 0) */
+
+typedef struct fme_result {
+  int16_t  mv_int_x, mv_int_y;
+  int16_t  mv_x, mv_y;
+  int8_t   half_x, half_y, qtr_x, qtr_y;
+  uint32_t frac_cost;
+  uint32_t cost;
+  uint32_t bits;
+  uint32_t c;
+  uint32_t emi[8];
+  uint8_t  n_emi;
+  uint8_t  nn_class;
+  uint16_t status;
+} fme_result;
+
+typedef struct fme_ctx fme_ctx;
+
+/* ---- lifecycle -------------------------------------------------------------------- */
+int         fme_abi_version(void);
+int         fme_create(int device, const fme_config* cfg, fme_ctx** out_ctx);
+int         fme_destroy(fme_ctx* ctx);
+const char* fme_last_error(void);
+
+/* ---- pictures ----------------------------------------------------------------------- *
+ * 8-bit luma planes, unpadded (width x height, row stride in bytes).  The path reads
+ * outside the picture with edge replication, which equals HM's padded TComPicYuv
+ * (extendPicBorder, TComPicYuv.cpp:229-276) for every MV TComDataCU::clipMv admits.  */
+int fme_set_picture(fme_ctx* ctx, int id, const uint8_t* luma, int stride, int width, int height,
+                    void* stream);
+/* Zero-copy: bind a device-resident plane owned by the caller (e.g. a buffer filled by an
+ * RCCL broadcast).  It must stay valid while jobs that use `id` run. */
+int fme_bind_picture_device(fme_ctx* ctx, int id, const uint8_t* d_luma, int stride, int width,
+                            int height);
+
+/* ---- cost parameters ------------------------------------------------------------------ */
+/* lambda -> motion lambda exactly as TComRdCost::setLambda + selectMotionLambda(true,0,false):
+ * mlambda = 65536.0 * sqrt(lambda)  (TComRdCost.cpp:104-117, TComRdCost.h:159).           */
+int fme_set_lambda(fme_ctx* ctx, int lambda_id, double lambda);
+int fme_set_motion_lambda(fme_ctx* ctx, int lambda_id, double motion_lambda);
+
+/* Bi-pred key blocks (int16, host memory; copied to the device). */
+int fme_set_keys(fme_ctx* ctx, const int16_t* keys, size_t count, void* stream);
+
+/* ---- NN predictor ------------------------------------------------------------------- *
+ * Parameters in the order embs0[8][4], embs1[8][4], in_h1[22][17], h1_h2[20][22],
+ * h2_out[49][20], b1, BN_gamma_1, BN_beta_1 (22 each), b2, BN_gamma_2, BN_beta_2
+ * (20 each), bout[49], BN_gamma_in, mean, stdev (9 each) — FME_NN_PARAMS floats.
+ * fme_create() loads nothing; the host mirror loads the per-QP set (weights/nn2_qp<QP>.bin).     */
+int fme_load_nn_weights(fme_ctx* ctx, const float* params, int count);
+/* Forget the array_e/C/PUHeight/PUWidth state carried across calls (process start). */
+int fme_nn_reset_state(fme_ctx* ctx);
+
+/* ---- the batch path --------------------------------------------------------------------- *
+ * Runs EMI step -> FracDIF -> NN_pred -> xMotionEstimation tail for n jobs, in job order
+ * for the NN's carried state (jobs are independent otherwise).
+ * fme_refine:        host job/result arrays (copied over PCIe), synchronous on `stream`.
+ * fme_refine_device: device-resident job/result arrays, asynchronous on `stream`
+ *                    (one host synchronisation for the size-class histogram).          */
+int fme_refine(fme_ctx* ctx, const fme_job* jobs, fme_result* results, int n, void* stream);
+int fme_refine_device(fme_ctx* ctx, const fme_job* d_jobs, fme_result* d_results, int n,
+                      void* stream);
+
+/* ---- single-PU entry points with the TEncSearch argument lists ---------------------------- *
+ * xPatternSearchFracDIF(bIsLosslessCoded, pcPatternKey, piRefY, iRefStride, pcMvInt,
+ *                       rcMvHalf, rcMvQter, ruiCost) with the HM objects flattened:
+ *   key/key_stride/w/h = pcPatternKey ROI, ref/ref_stride = piRefY/iRefStride
+ *   (host pointer at the PU origin of a padded picture: reads span rows -4..h+3 and
+ *   columns -4..w+3 around mv_int), mvp/motion_lambda = the TComRdCost state.
+ * Synchronous; latency-bound by construction (one launch per call).                     */
+int fme_frac_dif_single(fme_ctx* ctx, int lossless, const int16_t* key, int key_stride, int w,
+                        int h, const int16_t* ref, int ref_stride, int mv_int_x, int mv_int_y,
+                        int mvp_x, int mvp_y, double motion_lambda, int16_t* half_xy,
+                        int16_t* qtr_xy, uint32_t* cost);
+
+/* NN_pred() on explicit inputs: e[8] = array_e slots, c = C, pu_h/pu_w = PUHeight/PUWidth.
+ * Returns the class 0..48 in *nn_class and the four globals MVX_HALF, MVX_QRTER,
+ * MVY_HALF, MVY_QRTER in out4 (TEncSearch.cpp:136-193).                                */
+int fme_nn_pred_single(fme_ctx* ctx, const uint32_t* e, uint32_t c, int pu_h, int pu_w,
+                       int* nn_class, int16_t* out4);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* FME_H */

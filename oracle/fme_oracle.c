@@ -1,0 +1,461 @@
+/*
+ * fme_oracle.c — TEST INFRASTRUCTURE ONLY (see fme_oracle.h).
+ *
+ * Plain-C restatement of the reference path.  It does not build the m_filteredBlock planes
+ * the reference builds (TEncSearch.cpp:6331-6532); it evaluates each candidate as the luma
+ * prediction at its quarter-pel MV with the same two-stage 14-bit arithmetic
+ * (TComInterpolationFilter.cpp:94-257), which the _ref harness shows equal to the plane
+ * walk for every candidate.  Compile with -ffp-contract=off (the NN is float32, no FMA).
+ */
+#include "fme_oracle.h"
+
+#include <math.h>
+#include <stdlib.h>
+#include <string.h>
+
+/* HEVC luma taps, TComInterpolationFilter.cpp:57-63. */
+static const int kLuma[4][8] = {
+  {0, 0, 0, 64, 0, 0, 0, 0},
+  {-1, 4, -10, 58, 17, -5, 1, 0},
+  {-1, 4, -11, 40, 40, -11, 4, -1},
+  {0, 1, -5, 17, 58, -10, 4, -1},
+};
+
+/* s_acMvRefineH / s_acMvRefineQ, TEncSearch.cpp:212-236 (x, y). */
+static const int kRefineH[9][2] = {{0, 0}, {0, -1}, {0, 1}, {-1, 0}, {1, 0},
+                                   {-1, -1}, {1, -1}, {-1, 1}, {1, 1}};
+static const int kRefineQ[9][2] = {{0, 0}, {0, -1}, {0, 1}, {-1, -1}, {1, -1},
+                                   {-1, 0}, {1, 0}, {-1, 1}, {1, 1}};
+
+static inline int clampi(int v, int lo, int hi) { return v < lo ? lo : (v > hi ? hi : v); }
+
+/* TComRdCost::xGetExpGolombNumberOfBits, TComRdCost.cpp:172-185. */
+uint32_t orc_eg_bits(int v) {
+  uint32_t t = (v <= 0) ? ((uint32_t)(-v) << 1) + 1u : (uint32_t)v << 1;
+  uint32_t len = 1;
+  while (t != 1) {
+    t >>= 1;
+    len += 2;
+  }
+  return len;
+}
+
+/* TComRdCost::getCost / getCostOfVectorWithPredictor, TComRdCost.h:165-170. */
+uint32_t orc_cost(double mlambda, uint32_t bits) {
+  return (uint32_t)((mlambda * (double)bits) / 65536.0);
+}
+
+/* getBitsOfVectorWithPredictor, TComRdCost.h:171-174. */
+static inline uint32_t mv_bits(int x, int y, int scale, int px, int py) {
+  return orc_eg_bits((x << scale) - px) + orc_eg_bits((y << scale) - py);
+}
+
+/* Edge-replicated sample (TComPicYuv::extendPicBorder, TComPicYuv.cpp:229-276). */
+static inline int ref_px(const orc_picture* p, int x, int y) {
+  x = clampi(x, 0, p->width - 1);
+  y = clampi(y, 0, p->height - 1);
+  return p->luma[(size_t)y * p->stride + x];
+}
+
+/* First (horizontal) stage output at integer row y: the 14-bit value the reference stores
+ * in m_filteredBlockTmp[fx] (filterHor with isLast=false: filterCopy isFirst branch for
+ * fx==0, TComInterpolationFilter.cpp:111-124; filter<8,false,true,false> otherwise,
+ * :196-252 with shift 0 and offset -8192). */
+static inline int hor_stage(const orc_picture* p, int x, int y, int fx) {
+  if (fx == 0) return (ref_px(p, x, y) << 6) - 8192;
+  int s = 0;
+  for (int k = 0; k < 8; k++) s += kLuma[fx][k] * ref_px(p, x + k - 3, y);
+  return (int)(int16_t)(s - 8192);
+}
+
+/* Second (vertical, isLast) stage: filterCopy !isFirst branch for fy==0
+ * (TComInterpolationFilter.cpp:126-150) and filter<8,true,false,true> otherwise
+ * (shift 12, offset 2048 + (8192 << 6), clip to [0,255]). */
+int orc_pred_sample(const orc_picture* p, int x, int y, int fx, int fy) {
+  int v;
+  if (fy == 0) {
+    v = (hor_stage(p, x, y, fx) + 8192 + 32) >> 6;
+  } else {
+    int s = 0;
+    for (int k = 0; k < 8; k++) s += kLuma[fy][k] * hor_stage(p, x, y + k - 3, fx);
+    v = (s + 2048 + (8192 << 6)) >> 12;
+  }
+  return clampi(v, 0, 255);
+}
+
+/* Prediction block of a PU at (x0,y0) displaced by quarter-pel (qx,qy). */
+void orc_pred_block(const orc_picture* p, int x0, int y0, int w, int h, int qx, int qy,
+                    int16_t* out) {
+  const int ix = qx >> 2, iy = qy >> 2, fx = qx & 3, fy = qy & 3;
+  for (int r = 0; r < h; r++)
+    for (int c = 0; c < w; c++)
+      out[r * w + c] = (int16_t)orc_pred_sample(p, x0 + ix + c, y0 + iy + r, fx, fy);
+}
+
+/* xCalcHADs4x4, TComRdCost.cpp:1234-1328: unnormalised 4x4 WHT of the difference,
+ * sum of magnitudes, (s+1)>>1. */
+static uint32_t had4x4(const int16_t* o, int os, const int16_t* c, int cs) {
+  int d[16], m[16];
+  for (int r = 0; r < 4; r++)
+    for (int k = 0; k < 4; k++) d[r * 4 + k] = o[r * os + k] - c[r * cs + k];
+  /* columns: butterfly over rows (0,3),(1,2) then pairs */
+  for (int k = 0; k < 4; k++) {
+    int a0 = d[k] + d[12 + k], a3 = d[k] - d[12 + k];
+    int a1 = d[4 + k] + d[8 + k], a2 = d[4 + k] - d[8 + k];
+    m[k] = a0 + a1;
+    m[8 + k] = a0 - a1;
+    m[4 + k] = a2 + a3;
+    m[12 + k] = a3 - a2;
+  }
+  uint32_t s = 0;
+  for (int r = 0; r < 4; r++) {
+    int* q = &m[r * 4];
+    int b0 = q[0] + q[3], b3 = q[0] - q[3], b1 = q[1] + q[2], b2 = q[1] - q[2];
+    s += (uint32_t)abs(b0 + b1) + (uint32_t)abs(b0 - b1) + (uint32_t)abs(b2 + b3) +
+         (uint32_t)abs(b3 - b2);
+  }
+  return (s + 1) >> 1;
+}
+
+/* xCalcHADs8x8, TComRdCost.cpp:1330-1425: any exact 8-point WHT factorisation gives the
+ * same multiset of |coefficients|; (s+2)>>2. */
+static void wht8(int* v, int step) {
+  for (int len = 4; len >= 1; len >>= 1)
+    for (int i = 0; i < 8; i += 2 * len)
+      for (int j = i; j < i + len; j++) {
+        int a = v[j * step], b = v[(j + len) * step];
+        v[j * step] = a + b;
+        v[(j + len) * step] = a - b;
+      }
+}
+
+static uint32_t had8x8(const int16_t* o, int os, const int16_t* c, int cs) {
+  int d[64];
+  for (int r = 0; r < 8; r++)
+    for (int k = 0; k < 8; k++) d[r * 8 + k] = o[r * os + k] - c[r * cs + k];
+  for (int r = 0; r < 8; r++) wht8(&d[r * 8], 1);
+  for (int k = 0; k < 8; k++) wht8(&d[k], 8);
+  uint32_t s = 0;
+  for (int i = 0; i < 64; i++) s += (uint32_t)abs(d[i]);
+  return (s + 2) >> 2;
+}
+
+/* xGetHADs tiling, TComRdCost.cpp:1428-1495 (8x8 when both dims are multiples of 8). */
+uint32_t orc_satd(const int16_t* org, int os, const int16_t* cur, int cs, int w, int h) {
+  uint32_t s = 0;
+  if ((w % 8) == 0 && (h % 8) == 0) {
+    for (int y = 0; y < h; y += 8)
+      for (int x = 0; x < w; x += 8) s += had8x8(org + y * os + x, os, cur + y * cs + x, cs);
+  } else {
+    for (int y = 0; y < h; y += 4)
+      for (int x = 0; x < w; x += 4) s += had4x4(org + y * os + x, os, cur + y * cs + x, cs);
+  }
+  return s;
+}
+
+/* xGetSAD4..64/12/24/48 with row subsampling (iSubShift), TComRdCost.cpp:370-860. */
+uint32_t orc_sad(const int16_t* org, int os, const int16_t* cur, int cs, int w, int h,
+                 int sub_shift) {
+  uint32_t s = 0;
+  const int step = 1 << sub_shift;
+  for (int y = 0; y < h; y += step)
+    for (int x = 0; x < w; x++) s += (uint32_t)abs(org[y * os + x] - cur[y * cs + x]);
+  return s << sub_shift;
+}
+
+/* xGetSSE4..64, TComRdCost.cpp:860-1205 (bit depth 8: no shift). */
+uint32_t orc_sse(const int16_t* org, int os, const int16_t* cur, int cs, int w, int h) {
+  uint32_t s = 0;
+  for (int y = 0; y < h; y++)
+    for (int x = 0; x < w; x++) {
+      int d = org[y * os + x] - cur[y * cs + x];
+      s += (uint32_t)(d * d);
+    }
+  return s;
+}
+
+/* Integer-ME metric selected by the modified setDistParam (TComRdCost.cpp:200-230):
+ * SSE for W in {4,8,16,32,64}; SAD for 12/24/48 with the FEN even-row subsampling of
+ * xTZSearchHelp (TEncSearch.cpp:1158-1164). */
+static uint32_t int_dist(const int16_t* key, int ks, const int16_t* cur, int cs, int w, int h,
+                         int fen) {
+  if (w == 12 || w == 24 || w == 48) {
+    int sub = ((fen == 1 || fen == 3) && h > 8) ? 1 : 0;
+    return orc_sad(key, ks, cur, cs, w, h, sub);
+  }
+  return orc_sse(key, ks, cur, cs, w, h);
+}
+
+/* xPatternSearchFracDIF (TEncSearch.cpp:5232-5269) with xPatternRefinement (1591-1645):
+ * half stage at cost scale 1 around 2*mv_int, quarter stage at cost scale 0 around
+ * 4*mv_int + 2*half; first strict minimum of distortion + MV cost in each stage. */
+void orc_frac_dif(const orc_picture* p, const int16_t* key, int ks, int x0, int y0, int w, int h,
+                  int mv_x, int mv_y, int mvp_x, int mvp_y, double mlambda, int use_hadamard,
+                  int8_t half[2], int8_t qtr[2], uint32_t* cost) {
+  int16_t* pred = (int16_t*)malloc(sizeof(int16_t) * (size_t)w * h);
+  uint32_t best = 0xFFFFFFFFu;
+  int bi = 0;
+  for (int i = 0; i < 9; i++) {
+    const int dx = kRefineH[i][0], dy = kRefineH[i][1];
+    orc_pred_block(p, x0, y0, w, h, 4 * mv_x + 2 * dx, 4 * mv_y + 2 * dy, pred);
+    uint32_t d = use_hadamard ? orc_satd(key, ks, pred, w, w, h) : orc_sad(key, ks, pred, w, w, h, 0);
+    d += orc_cost(mlambda, mv_bits(2 * mv_x + dx, 2 * mv_y + dy, 1, mvp_x, mvp_y));
+    if (d < best) {
+      best = d;
+      bi = i;
+    }
+  }
+  const int hx = kRefineH[bi][0], hy = kRefineH[bi][1];
+  best = 0xFFFFFFFFu;
+  int qi = 0;
+  for (int i = 0; i < 9; i++) {
+    const int dx = kRefineQ[i][0], dy = kRefineQ[i][1];
+    const int qx = 4 * mv_x + 2 * hx + dx, qy = 4 * mv_y + 2 * hy + dy;
+    orc_pred_block(p, x0, y0, w, h, qx, qy, pred);
+    uint32_t d = use_hadamard ? orc_satd(key, ks, pred, w, w, h) : orc_sad(key, ks, pred, w, w, h, 0);
+    d += orc_cost(mlambda, mv_bits(qx, qy, 0, mvp_x, mvp_y));
+    if (d < best) {
+      best = d;
+      qi = i;
+    }
+  }
+  free(pred);
+  half[0] = (int8_t)hx;
+  half[1] = (int8_t)hy;
+  qtr[0] = (int8_t)kRefineQ[qi][0];
+  qtr[1] = (int8_t)kRefineQ[qi][1];
+  *cost = best;
+}
+
+/* Visit order and range checks of xTZ8PointSquareSearch (TEncSearch.cpp:1324-1377):
+ * TL,T,TR (row above in range), L, R, BL,B,BR (row below in range). */
+static int square_points(int sx, int sy, int lt_x, int lt_y, int rb_x, int rb_y, int pts[8][2]) {
+  int n = 0;
+  const int top = sy - 1, bot = sy + 1, left = sx - 1, right = sx + 1;
+  if (top >= lt_y) {
+    if (left >= lt_x) { pts[n][0] = left; pts[n][1] = top; n++; }
+    pts[n][0] = sx; pts[n][1] = top; n++;
+    if (right <= rb_x) { pts[n][0] = right; pts[n][1] = top; n++; }
+  }
+  if (left >= lt_x) { pts[n][0] = left; pts[n][1] = sy; n++; }
+  if (right <= rb_x) { pts[n][0] = right; pts[n][1] = sy; n++; }
+  if (bot <= rb_y) {
+    if (left >= lt_x) { pts[n][0] = left; pts[n][1] = bot; n++; }
+    pts[n][0] = sx; pts[n][1] = bot; n++;
+    if (right <= rb_x) { pts[n][0] = right; pts[n][1] = bot; n++; }
+  }
+  return n;
+}
+
+int orc_emi_push_count(int sx, int sy, int lt_x, int lt_y, int rb_x, int rb_y) {
+  int pts[8][2];
+  return square_points(sx, sy, lt_x, lt_y, rb_x, rb_y, pts);
+}
+
+/* EMI step: xTZ8PointSquareSearch(save=true) at the TZ best (TEncSearch.cpp:5043) with
+ * xTZSearchHelp's normal branch (1155-1188): push the distortion, compare d, then d+cost,
+ * against the running best; C = bestSad - cost(best) (5049-5050).  The incoming bestSad is
+ * the TZ best's distortion + cost at cost scale 2, recomputed here. */
+int orc_emi(const orc_picture* p, const int16_t* key, int ks, int x0, int y0, int w, int h,
+            int sx, int sy, int mvp_x, int mvp_y, int lt_x, int lt_y, int rb_x, int rb_y,
+            double mlambda, int fen, uint32_t emi[8], int* best_x, int* best_y, uint32_t* c) {
+  int16_t* cur = (int16_t*)malloc(sizeof(int16_t) * (size_t)w * h);
+  orc_pred_block(p, x0, y0, w, h, 4 * sx, 4 * sy, cur);
+  uint32_t best_sad = int_dist(key, ks, cur, w, w, h, fen) +
+                      orc_cost(mlambda, mv_bits(sx, sy, 2, mvp_x, mvp_y));
+  int bx = sx, by = sy;
+  int pts[8][2];
+  const int n = square_points(sx, sy, lt_x, lt_y, rb_x, rb_y, pts);
+  for (int i = 0; i < n; i++) {
+    orc_pred_block(p, x0, y0, w, h, 4 * pts[i][0], 4 * pts[i][1], cur);
+    uint32_t d = int_dist(key, ks, cur, w, w, h, fen);
+    emi[i] = d;
+    if (d < best_sad) {
+      d += orc_cost(mlambda, mv_bits(pts[i][0], pts[i][1], 2, mvp_x, mvp_y));
+      if (d < best_sad) {
+        best_sad = d;
+        bx = pts[i][0];
+        by = pts[i][1];
+      }
+    }
+  }
+  free(cur);
+  *best_x = bx;
+  *best_y = by;
+  *c = best_sad - orc_cost(mlambda, mv_bits(bx, by, 2, mvp_x, mvp_y));
+  return n;
+}
+
+/* ---- NN_pred(), TEncSearch.cpp:85-204 ------------------------------------------------ */
+enum {
+  P_EMB0 = 0, P_EMB1 = 32, P_W1 = 64, P_W2 = 438, P_W3 = 878, P_B1 = 1858, P_G1 = 1880,
+  P_BE1 = 1902, P_B2 = 1924, P_G2 = 1944, P_BE2 = 1964, P_BOUT = 1984, P_GIN = 2033,
+  P_MEAN = 2042, P_STD = 2051
+};
+
+/* Embedding rows by PUHeight (TEncSearch.cpp:93-102) and PUWidth (104-113). */
+static int emb_row_h(int h) {
+  switch (h) {
+    case 4: return 1; case 8: return 2; case 16: return 3; case 12: return 4;
+    case 24: return 5; case 32: return 6; case 64: return 7; default: return 0;
+  }
+}
+static int emb_row_w(int w) {
+  switch (w) {
+    case 4: return 1; case 8: return 2; case 12: return 3; case 16: return 4;
+    case 24: return 5; case 32: return 6; case 64: return 7; default: return 0;
+  }
+}
+
+int orc_nn_forward(const float* P, const uint32_t e[8], uint32_t c, int pu_h, int pu_w,
+                   float* logits) {
+  float in[17], x1[22], x2[20], out[49];
+  const int rh = emb_row_h(pu_h), rw = emb_row_w(pu_w);
+  for (int k = 0; k < 4; k++) {
+    in[k] = P[P_EMB0 + rh * 4 + k];
+    in[4 + k] = P[P_EMB1 + rw * 4 + k];
+  }
+  /* IN_errors << e0,e1,e2,e3,C,e4,e5,e6,e7 ; (x - mean) / stdev ; * BN_gamma_in */
+  const uint32_t raw[9] = {e[0], e[1], e[2], e[3], c, e[4], e[5], e[6], e[7]};
+  for (int k = 0; k < 9; k++) {
+    float v = (float)raw[k];
+    v = (v - P[P_MEAN + k]) / P[P_STD + k];
+    in[8 + k] = v * P[P_GIN + k];
+  }
+  for (int r = 0; r < 22; r++) {
+    float s = 0.0f;
+    for (int k = 0; k < 17; k++) s = s + P[P_W1 + r * 17 + k] * in[k];
+    s = s + P[P_B1 + r];
+    s = (s < 0.0f) ? 0.0f : s;
+    x1[r] = s * P[P_G1 + r] + P[P_BE1 + r];
+  }
+  for (int r = 0; r < 20; r++) {
+    float s = 0.0f;
+    for (int k = 0; k < 22; k++) s = s + P[P_W2 + r * 22 + k] * x1[k];
+    s = s + P[P_B2 + r];
+    s = (s < 0.0f) ? 0.0f : s;
+    x2[r] = s * P[P_G2 + r] + P[P_BE2 + r];
+  }
+  for (int r = 0; r < 49; r++) {
+    float s = 0.0f;
+    for (int k = 0; k < 20; k++) s = s + P[P_W3 + r * 20 + k] * x2[k];
+    out[r] = s + P[P_BOUT + r];
+  }
+  int best = 0; /* Eigen maxCoeff: first index of the maximum */
+  for (int r = 1; r < 49; r++)
+    if (out[r] > out[best]) best = r;
+  if (logits) memcpy(logits, out, sizeof(out));
+  return best;
+}
+
+/* ---- context -------------------------------------------------------------------------- */
+size_t orc_ctx_size(void) { return sizeof(orc_ctx); }
+
+void orc_init(orc_ctx* ctx, const fme_config* cfg) {
+  memset(ctx, 0, sizeof(*ctx));
+  ctx->cfg = *cfg;
+}
+void orc_set_picture(orc_ctx* ctx, int id, const uint8_t* luma, int stride, int w, int h) {
+  ctx->pics[id].luma = luma;
+  ctx->pics[id].stride = stride;
+  ctx->pics[id].width = w;
+  ctx->pics[id].height = h;
+}
+/* TComRdCost::setLambda + selectMotionLambda(true, 0, false), TComRdCost.cpp:104-110. */
+void orc_set_lambda(orc_ctx* ctx, int id, double lambda) {
+  const double sq = sqrt(lambda);
+  ctx->mlambda[id] = 65536.0 * sq + 0;
+}
+void orc_set_motion_lambda(orc_ctx* ctx, int id, double ml) { ctx->mlambda[id] = ml; }
+void orc_set_keys(orc_ctx* ctx, const int16_t* keys, size_t n) {
+  ctx->keys = keys;
+  ctx->n_keys = n;
+}
+void orc_load_nn(orc_ctx* ctx, const float* params) {
+  memcpy(ctx->nn, params, sizeof(ctx->nn));
+  ctx->nn_loaded = 1;
+}
+void orc_nn_reset(orc_ctx* ctx) { memset(&ctx->nn_state, 0, sizeof(ctx->nn_state)); }
+
+static int valid_size(int w, int h) {
+  if (w < 4 || h < 4 || w > 64 || h > 64 || (w & 3) || (h & 3)) return 0;
+  return 1;
+}
+
+/* xMotionEstimation sub-pel part for each job in order (TEncSearch.cpp:4529-4597). */
+int orc_refine(orc_ctx* ctx, const fme_job* jobs, fme_result* res, int n) {
+  int16_t* key = (int16_t*)malloc(sizeof(int16_t) * 64 * 64);
+  for (int i = 0; i < n; i++) {
+    const fme_job* j = &jobs[i];
+    fme_result* r = &res[i];
+    memset(r, 0, sizeof(*r));
+    if (!valid_size(j->w, j->h) || j->org_id >= FME_MAX_PICTURES ||
+        j->ref_id >= FME_MAX_PICTURES || j->lambda_id >= FME_MAX_LAMBDAS) {
+      free(key);
+      return FME_E_INVALID;
+    }
+    const orc_picture* ref = &ctx->pics[j->ref_id];
+    const orc_picture* org = &ctx->pics[j->org_id];
+    if (!ref->luma) { free(key); return FME_E_STATE; }
+    const int w = j->w, h = j->h;
+    if (j->key_offset >= 0) {
+      if ((size_t)j->key_offset + (size_t)w * h > ctx->n_keys) { free(key); return FME_E_INVALID; }
+      memcpy(key, ctx->keys + j->key_offset, sizeof(int16_t) * w * h);
+    } else {
+      if (!org->luma) { free(key); return FME_E_STATE; }
+      for (int y = 0; y < h; y++)
+        for (int x = 0; x < w; x++) key[y * w + x] = org->luma[(size_t)(j->y + y) * org->stride + j->x + x];
+    }
+    const double ml = ctx->mlambda[j->lambda_id];
+    int mvx = j->mv_x, mvy = j->mv_y;
+    uint32_t c = 0;
+    int n_emi = 0;
+    if (j->flags & FME_JOB_EMI) {
+      n_emi = orc_emi(ref, key, w, j->x, j->y, w, h, j->mv_x, j->mv_y, j->mvp_x, j->mvp_y,
+                      j->lt_x, j->lt_y, j->rb_x, j->rb_y, ml, ctx->cfg.fast_inter_mode, r->emi,
+                      &mvx, &mvy, &c);
+      /* array_e: clear() then push_back -> slots 0..n-1 overwritten, the rest stale. */
+      for (int s = 0; s < n_emi; s++) ctx->nn_state.slot[s] = r->emi[s];
+      ctx->nn_state.c = c;
+      ctx->nn_state.pu_h = (uint32_t)h;
+      ctx->nn_state.pu_w = (uint32_t)w;
+      ctx->nn_state.written |= ((1u << n_emi) - 1u) | 0x100u;
+    }
+    r->n_emi = (uint8_t)n_emi;
+    r->c = c;
+    r->mv_int_x = (int16_t)mvx;
+    r->mv_int_y = (int16_t)mvy;
+    const int lossless = (j->flags & FME_JOB_LOSSLESS) != 0;
+    orc_frac_dif(ref, key, w, j->x, j->y, w, h, mvx, mvy, j->mvp_x, j->mvp_y, ml,
+                 ctx->cfg.use_hadamard && !lossless, &r->half_x, &r->qtr_x, &r->frac_cost);
+    int offx, offy;
+    if (ctx->cfg.nn_mode) {
+      const orc_nn_state* st = &ctx->nn_state;
+      int cls = orc_nn_forward(ctx->nn, st->slot, st->c, (int)st->pu_h, (int)st->pu_w, NULL);
+      r->nn_class = (uint8_t)cls;
+      if (n_emi < 8 || !(j->flags & FME_JOB_EMI)) r->status |= FME_RES_NN_STALE;
+      if ((st->written & 0x1FFu) != 0x1FFu) r->status |= FME_RES_NN_UNINIT;
+      /* class -> (MVX_HALF<<1)+MVX_QRTER, (MVY_HALF<<1)+MVY_QRTER: (cls%7-3, cls/7-3),
+       * the switch of TEncSearch.cpp:136-193. */
+      offx = cls % 7 - 3;
+      offy = cls / 7 - 3;
+    } else {
+      r->nn_class = 255;
+      offx = 2 * r->half_x + r->qtr_x;
+      offy = 2 * r->half_y + r->qtr_y;
+    }
+    const int fmvx = 4 * mvx + offx, fmvy = 4 * mvy + offy;
+    r->mv_x = (int16_t)fmvx;
+    r->mv_y = (int16_t)fmvy;
+    const uint32_t mvb = mv_bits(fmvx, fmvy, 0, j->mvp_x, j->mvp_y);
+    const uint32_t bits = (uint32_t)j->bits_in + mvb;
+    r->bits = bits;
+    const double fw = (j->flags & FME_JOB_BIPRED) ? 0.5 : 1.0;
+    const double v = floor(fw * ((double)r->frac_cost - (double)orc_cost(ml, mvb))) +
+                     (double)orc_cost(ml, bits);
+    /* (Distortion)(double): gcc/x86-64 converts through a signed 64-bit integer. */
+    r->cost = (uint32_t)(int64_t)v;
+  }
+  free(key);
+  return FME_OK;
+}

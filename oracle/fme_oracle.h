@@ -1,0 +1,105 @@
+/*
+ * fme_oracle.h — TEST INFRASTRUCTURE ONLY.
+ *
+ * CPU restatement of HM-16.9-NN_FME's sub-pel motion-estimation path (plain C, scalar,
+ * -O2 -ffp-contract=off).  It is the parity checker for the HIP path and the CPU baseline
+ * timed by bench.py (`cpu_baseline`, kind "port").  Only tests/, __graft_entry__.smoke()
+ * and bench.py's cpu_baseline leg may load it; the product library never links it.
+ *
+ * Pinning: the integer parts (interpolation, SATD/SAD/SSE, MV cost, FracDIF, EMI step,
+ * tail) are checked against golden vectors produced by oracle/_ref, which compiles the
+ * reference's own TLibCommon sources (TComInterpolationFilter, TComRdCost, TComYuv, ...)
+ * and drives them in TEncSearch's plane-based order (oracle/ref_harness.cpp).  The NN is
+ * pinned by the reference's weight CSVs only: its host file TEncSearch.cpp needs Eigen
+ * 3.3.7, which is absent, so the float summation order at the Eigen boundary is "parity
+ * unpinned"; the contract is sequential-k float32 without FMA.
+ */
+#ifndef FME_ORACLE_H
+#define FME_ORACLE_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#include "../include/fme.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct orc_picture {
+  const uint8_t* luma;
+  int stride, width, height;
+} orc_picture;
+
+/* Carried NN_pred() global state: array_e storage, C, PUHeight, PUWidth (TEncSearch.cpp:55-57). */
+typedef struct orc_nn_state {
+  uint32_t slot[8];
+  uint32_t c;
+  uint32_t pu_h, pu_w;
+  uint32_t written;   /* bit s: slot s written since reset; bit 8: C/PU size written */
+} orc_nn_state;
+
+typedef struct orc_ctx {
+  fme_config cfg;
+  orc_picture pics[FME_MAX_PICTURES];
+  double mlambda[FME_MAX_LAMBDAS];
+  const int16_t* keys;
+  size_t n_keys;
+  float nn[FME_NN_PARAMS];
+  int nn_loaded;
+  orc_nn_state nn_state;
+} orc_ctx;
+
+/* primitives (exported for unit tests) */
+uint32_t orc_eg_bits(int v);                                         /* TComRdCost.cpp:172-185 */
+uint32_t orc_cost(double mlambda, uint32_t bits);                    /* TComRdCost.h:165     */
+int      orc_pred_sample(const orc_picture* p, int x, int y, int fx, int fy); /* A.2 */
+void     orc_pred_block(const orc_picture* p, int x0, int y0, int w, int h, int qx, int qy,
+                        int16_t* out);                               /* W*H, stride w */
+uint32_t orc_satd(const int16_t* org, int org_stride, const int16_t* cur, int cur_stride, int w,
+                  int h);                                            /* TComRdCost.cpp:1428-1495 */
+uint32_t orc_sad(const int16_t* org, int org_stride, const int16_t* cur, int cur_stride, int w,
+                 int h, int sub_shift);                              /* TComRdCost.cpp:335-860 */
+uint32_t orc_sse(const int16_t* org, int org_stride, const int16_t* cur, int cur_stride, int w,
+                 int h);                                             /* TComRdCost.cpp:860-1205 */
+
+/* xPatternSearchFracDIF on one PU; key W*H with stride key_stride, reference picture p,
+ * PU origin (x0,y0), full-pel mv_int. */
+void orc_frac_dif(const orc_picture* p, const int16_t* key, int key_stride, int x0, int y0, int w,
+                  int h, int mv_x, int mv_y, int mvp_x, int mvp_y, double mlambda,
+                  int use_hadamard, int8_t half[2], int8_t qtr[2], uint32_t* cost);
+
+/* EMI square step; returns number of pushes, fills emi[], final best and C. */
+int orc_emi(const orc_picture* p, const int16_t* key, int key_stride, int x0, int y0, int w, int h,
+            int sx, int sy, int mvp_x, int mvp_y, int lt_x, int lt_y, int rb_x, int rb_y,
+            double mlambda, int fast_inter_mode, uint32_t emi[8], int* best_x, int* best_y,
+            uint32_t* c);
+
+/* Number of EMI pushes by geometry alone (TEncSearch.cpp:1341-1376). */
+int orc_emi_push_count(int sx, int sy, int lt_x, int lt_y, int rb_x, int rb_y);
+
+/* NN_pred() forward on explicit inputs; returns class 0..48 (TEncSearch.cpp:85-134). */
+int orc_nn_forward(const float* params, const uint32_t e[8], uint32_t c, int pu_h, int pu_w,
+                   float* logits /* 49, may be NULL */);
+
+/* context helpers */
+void orc_init(orc_ctx* ctx, const fme_config* cfg);
+void orc_set_picture(orc_ctx* ctx, int id, const uint8_t* luma, int stride, int w, int h);
+void orc_set_lambda(orc_ctx* ctx, int id, double lambda);
+void orc_set_motion_lambda(orc_ctx* ctx, int id, double mlambda);
+void orc_set_keys(orc_ctx* ctx, const int16_t* keys, size_t n);
+void orc_load_nn(orc_ctx* ctx, const float* params);
+void orc_nn_reset(orc_ctx* ctx);
+
+/* Whole path for n jobs in order (the restated xMotionEstimation sub-pel part). Returns
+ * 0 or a negative FME_E_* code. */
+int orc_refine(orc_ctx* ctx, const fme_job* jobs, fme_result* res, int n);
+
+/* helpers for bindings */
+size_t orc_ctx_size(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif

@@ -1,0 +1,184 @@
+"""ctypes bindings of the CPU oracle (liboracle.so) and the reference harness (_ref/libhmref.so).
+
+TEST INFRASTRUCTURE ONLY: imported by tests/, __graft_entry__.smoke() and bench.py's
+cpu_baseline leg, never by the product path (hm16.9-nn_fme_amd/).
+"""
+import ctypes as C
+import os
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ORACLE_SO = os.path.join(HERE, "liboracle.so")
+REF_SO = os.path.join(HERE, "_ref", "libhmref.so")
+
+_P = C.c_void_p
+
+
+def _ptr(a):
+    return a.ctypes.data_as(C.c_void_p)
+
+
+class _ConfigStruct(C.Structure):
+    _fields_ = [(n, C.c_int32) for n in ("bit_depth", "use_hadamard", "nn_mode", "qp",
+                                         "fast_inter_mode", "max_jobs")]
+
+
+def _load(path):
+    if not os.path.exists(path):
+        raise FileNotFoundError(f"{path} not built (run `make -C oracle` / `make -C oracle ref`)")
+    return C.CDLL(path)
+
+
+class Oracle:
+    """Plain-C restatement (fme_oracle.c)."""
+
+    def __init__(self, use_hadamard=1, nn_mode=1, qp=22, fast_inter_mode=1):
+        self.lib = lib = _load(ORACLE_SO)
+        lib.orc_ctx_size.restype = C.c_size_t
+        lib.orc_eg_bits.restype = C.c_uint32
+        lib.orc_eg_bits.argtypes = [C.c_int]
+        lib.orc_cost.restype = C.c_uint32
+        lib.orc_cost.argtypes = [C.c_double, C.c_uint32]
+        lib.orc_satd.restype = C.c_uint32
+        lib.orc_satd.argtypes = [_P, C.c_int, _P, C.c_int, C.c_int, C.c_int]
+        lib.orc_sad.restype = C.c_uint32
+        lib.orc_sad.argtypes = [_P, C.c_int, _P, C.c_int, C.c_int, C.c_int, C.c_int]
+        lib.orc_sse.restype = C.c_uint32
+        lib.orc_sse.argtypes = [_P, C.c_int, _P, C.c_int, C.c_int, C.c_int]
+        lib.orc_pred_block.argtypes = [_P] + [C.c_int] * 6 + [_P]
+        lib.orc_nn_forward.restype = C.c_int
+        lib.orc_nn_forward.argtypes = [_P, _P, C.c_uint32, C.c_int, C.c_int, _P]
+        lib.orc_emi_push_count.restype = C.c_int
+        lib.orc_emi_push_count.argtypes = [C.c_int] * 6
+        lib.orc_init.argtypes = [_P, _P]
+        lib.orc_set_picture.argtypes = [_P, C.c_int, _P, C.c_int, C.c_int, C.c_int]
+        lib.orc_set_lambda.argtypes = [_P, C.c_int, C.c_double]
+        lib.orc_set_motion_lambda.argtypes = [_P, C.c_int, C.c_double]
+        lib.orc_set_keys.argtypes = [_P, _P, C.c_size_t]
+        lib.orc_load_nn.argtypes = [_P, _P]
+        lib.orc_nn_reset.argtypes = [_P]
+        lib.orc_refine.restype = C.c_int
+        lib.orc_refine.argtypes = [_P, _P, _P, C.c_int]
+        self._buf = C.create_string_buffer(lib.orc_ctx_size())
+        self.ctx = C.cast(self._buf, C.c_void_p)
+        cfg = _ConfigStruct(8, use_hadamard, nn_mode, qp, fast_inter_mode, 0)
+        lib.orc_init(self.ctx, C.byref(cfg))
+        self._keep = {}
+
+    def set_picture(self, pid, luma):
+        luma = np.ascontiguousarray(luma, dtype=np.uint8)
+        self._keep[("pic", pid)] = luma
+        self.lib.orc_set_picture(self.ctx, pid, _ptr(luma), luma.shape[1], luma.shape[1], luma.shape[0])
+
+    def set_lambda(self, lid, lam):
+        self.lib.orc_set_lambda(self.ctx, lid, lam)
+
+    def set_keys(self, keys):
+        keys = np.ascontiguousarray(keys, dtype=np.int16)
+        self._keep["keys"] = keys
+        self.lib.orc_set_keys(self.ctx, _ptr(keys), keys.size)
+
+    def load_nn(self, params):
+        p = np.ascontiguousarray(params, dtype=np.float32)
+        self.lib.orc_load_nn(self.ctx, _ptr(p))
+
+    def nn_reset(self):
+        self.lib.orc_nn_reset(self.ctx)
+
+    def refine(self, jobs):
+        from nnfme.abi import RESULT_DTYPE
+        jobs = np.ascontiguousarray(jobs)
+        res = np.zeros(len(jobs), dtype=RESULT_DTYPE)
+        rc = self.lib.orc_refine(self.ctx, _ptr(jobs), _ptr(res), len(jobs))
+        if rc != 0:
+            raise RuntimeError(f"orc_refine failed: {rc}")
+        return res
+
+    def nn_class(self, params, e, c, h, w):
+        p = np.ascontiguousarray(params, dtype=np.float32)
+        e = np.ascontiguousarray(e, dtype=np.uint32)
+        logits = np.zeros(49, dtype=np.float32)
+        cls = self.lib.orc_nn_forward(_ptr(p), _ptr(e), int(c), int(h), int(w), _ptr(logits))
+        return cls, logits
+
+    def pred_block(self, luma, x0, y0, w, h, qx, qy):
+        luma = np.ascontiguousarray(luma, dtype=np.uint8)
+        out = np.zeros((h, w), dtype=np.int16)
+        # build an orc_picture on the fly: {const uint8_t*, int stride, width, height}
+        class Pic(C.Structure):
+            _fields_ = [("luma", C.c_void_p), ("stride", C.c_int), ("width", C.c_int), ("height", C.c_int)]
+        p = Pic(luma.ctypes.data, luma.shape[1], luma.shape[1], luma.shape[0])
+        self.lib.orc_pred_block(C.byref(p), x0, y0, w, h, qx, qy, _ptr(out))
+        return out
+
+
+class Reference:
+    """The reference's own TLibCommon primitives driven in TEncSearch order (_ref)."""
+
+    def __init__(self, use_hadamard=1, nn_mode=1, fast_inter_mode=1):
+        self.lib = lib = _load(REF_SO)
+        lib.ref_create.restype = C.c_void_p
+        lib.ref_create.argtypes = [C.c_int, C.c_int, C.c_int]
+        lib.ref_destroy.argtypes = [_P]
+        lib.ref_set_picture.argtypes = [_P, C.c_int, _P, C.c_int, C.c_int, C.c_int]
+        lib.ref_set_lambda.argtypes = [_P, C.c_int, C.c_double]
+        lib.ref_set_keys.argtypes = [_P, _P, C.c_size_t]
+        lib.ref_load_nn.argtypes = [_P, _P]
+        lib.ref_nn_reset.argtypes = [_P]
+        lib.ref_nn_class.restype = C.c_int
+        lib.ref_nn_class.argtypes = [_P, _P, C.c_uint32, C.c_int, C.c_int]
+        lib.ref_pred_block.argtypes = [_P] + [C.c_int] * 7 + [_P]
+        lib.ref_satd.restype = C.c_uint32
+        lib.ref_satd.argtypes = [_P, _P, C.c_int, _P, C.c_int, C.c_int, C.c_int, C.c_int]
+        lib.ref_refine.restype = C.c_int
+        lib.ref_refine.argtypes = [_P, _P, _P, C.c_int]
+        self.h = lib.ref_create(use_hadamard, fast_inter_mode, nn_mode)
+
+    def __del__(self):
+        try:
+            self.lib.ref_destroy(self.h)
+        except Exception:
+            pass
+
+    def set_picture(self, pid, luma):
+        luma = np.ascontiguousarray(luma, dtype=np.uint8)
+        self.lib.ref_set_picture(self.h, pid, _ptr(luma), luma.shape[1], luma.shape[1], luma.shape[0])
+
+    def set_lambda(self, lid, lam):
+        self.lib.ref_set_lambda(self.h, lid, lam)
+
+    def set_keys(self, keys):
+        keys = np.ascontiguousarray(keys, dtype=np.int16)
+        self.lib.ref_set_keys(self.h, _ptr(keys), keys.size)
+
+    def load_nn(self, params):
+        p = np.ascontiguousarray(params, dtype=np.float32)
+        self.lib.ref_load_nn(self.h, _ptr(p))
+
+    def nn_reset(self):
+        self.lib.ref_nn_reset(self.h)
+
+    def nn_class(self, e, c, h, w):
+        e = np.ascontiguousarray(e, dtype=np.uint32)
+        return self.lib.ref_nn_class(self.h, _ptr(e), int(c), int(h), int(w))
+
+    def pred_block(self, pid, x0, y0, w, h, qx, qy):
+        out = np.zeros((h, w), dtype=np.int16)
+        self.lib.ref_pred_block(self.h, pid, x0, y0, w, h, qx, qy, _ptr(out))
+        return out
+
+    def satd(self, org, cur, hadamard=True):
+        org = np.ascontiguousarray(org, dtype=np.int16)
+        cur = np.ascontiguousarray(cur, dtype=np.int16)
+        h, w = org.shape
+        return self.lib.ref_satd(self.h, _ptr(org), w, _ptr(cur), w, w, h, int(hadamard))
+
+    def refine(self, jobs):
+        from nnfme.abi import RESULT_DTYPE
+        jobs = np.ascontiguousarray(jobs)
+        res = np.zeros(len(jobs), dtype=RESULT_DTYPE)
+        rc = self.lib.ref_refine(self.h, _ptr(jobs), _ptr(res), len(jobs))
+        if rc != 0:
+            raise RuntimeError(f"ref_refine failed: {rc}")
+        return res

@@ -1,0 +1,425 @@
+// ref_harness.cpp — TEST INFRASTRUCTURE ONLY.
+//
+// Drives the reference's own compiled TLibCommon classes (built from /root/reference by
+// oracle/Makefile into oracle/_ref/libhmref.so; nothing is copied into this repository):
+//   TComInterpolationFilter::filterHor/filterVer   (TComInterpolationFilter.cpp:341-394)
+//   TComRdCost::setDistParam + DistFunc             (TComRdCost.cpp:200-275, 335-1495)
+//   TComRdCost cost/lambda helpers                  (TComRdCost.cpp:104-117, .h:159-174)
+//   TComPicYuv padding (createWithoutCUInfo + extendPicBorder, TComPicYuv.cpp:81-117, 229-276)
+//   TComPrediction::initTempBuff scratch planes     (TComPrediction.cpp:126-145)
+//
+// TEncSearch.cpp itself needs Eigen 3.3.7 (TEncSearch.cpp:39), which is absent here, so its
+// orchestration is restated below in the same plane-walk order the encoder uses:
+//   xExtDIFUpSamplingH (TEncSearch.cpp:6331-6365), xExtDIFUpSamplingQ (6378-6532),
+//   xPatternRefinement (1591-1645), xPatternSearchFracDIF (5232-5269),
+//   xTZ8PointSquareSearch(save) + xTZSearchHelp normal branch (1324-1377, 1155-1188),
+//   xMotionEstimation tail (4529-4597).  NN_pred() (85-204) is restated as a scalar loop.
+// The restated pieces are independent of oracle/fme_oracle.c, which evaluates each candidate
+// as a direct quarter-pel prediction instead of walking the planes.
+#include <cmath>
+#include <cstdint>
+#include <cstring>
+#include <limits>
+#include <vector>
+
+#include "TLibCommon/TComPattern.h"
+#include "TLibCommon/TComPicYuv.h"
+#include "TLibCommon/TComPrediction.h"
+#include "TLibCommon/TComRdCost.h"
+#include "TLibCommon/TComRom.h"
+
+#include "../include/fme.h"
+
+namespace {
+
+const int kH9[9][2] = {{0, 0}, {0, -1}, {0, 1}, {-1, 0}, {1, 0}, {-1, -1}, {1, -1}, {-1, 1}, {1, 1}};
+const int kQ9[9][2] = {{0, 0}, {0, -1}, {0, 1}, {-1, -1}, {1, -1}, {-1, 0}, {1, 0}, {-1, 1}, {1, 1}};
+
+// A TComPrediction subclass gives access to m_filteredBlock / m_filteredBlockTmp / m_if,
+// exactly as TEncSearch (a TComPrediction subclass) uses them.
+class RefSearch : public TComPrediction {
+ public:
+  TComRdCost rd;
+  DistParam dp;
+  bool hadme = true;
+  int fen = 0;
+
+  RefSearch() {
+    initTempBuff(CHROMA_400);
+    rd.init();
+  }
+
+  void setLambda(double lambda) {
+    BitDepths bd;
+    bd.recon[CHANNEL_TYPE_LUMA] = 8;
+    bd.recon[CHANNEL_TYPE_CHROMA] = 8;
+    rd.setLambda(lambda, bd);
+    rd.selectMotionLambda(true, 0, false);
+  }
+
+  // --- half-pel planes around the integer position (xExtDIFUpSamplingH) -------------
+  void upH(Pel* roi, int stride, int w, int h) {
+    const int ts = m_filteredBlockTmp[0].getStride(COMPONENT_Y);
+    const int ds = m_filteredBlock[0][0].getStride(COMPONENT_Y);
+    Pel* src = roi - 4 * stride - 1;  // half filter size rows up, one column left
+    m_if.filterHor(COMPONENT_Y, src, stride, m_filteredBlockTmp[0].getAddr(COMPONENT_Y), ts, w + 1, h + 8, 0, false, CHROMA_400, 8);
+    m_if.filterHor(COMPONENT_Y, src, stride, m_filteredBlockTmp[2].getAddr(COMPONENT_Y), ts, w + 1, h + 8, 2, false, CHROMA_400, 8);
+    Pel* t0 = m_filteredBlockTmp[0].getAddr(COMPONENT_Y);
+    Pel* t2 = m_filteredBlockTmp[2].getAddr(COMPONENT_Y);
+    m_if.filterVer(COMPONENT_Y, t0 + 4 * ts + 1, ts, m_filteredBlock[0][0].getAddr(COMPONENT_Y), ds, w, h, 0, false, true, CHROMA_400, 8);
+    m_if.filterVer(COMPONENT_Y, t0 + 3 * ts + 1, ts, m_filteredBlock[2][0].getAddr(COMPONENT_Y), ds, w, h + 1, 2, false, true, CHROMA_400, 8);
+    m_if.filterVer(COMPONENT_Y, t2 + 4 * ts, ts, m_filteredBlock[0][2].getAddr(COMPONENT_Y), ds, w + 1, h, 0, false, true, CHROMA_400, 8);
+    m_if.filterVer(COMPONENT_Y, t2 + 3 * ts, ts, m_filteredBlock[2][2].getAddr(COMPONENT_Y), ds, w + 1, h + 1, 2, false, true, CHROMA_400, 8);
+  }
+
+  // --- quarter-pel planes around the best half position (xExtDIFUpSamplingQ) ---------
+  void upQ(Pel* roi, int stride, int w, int h, int hx, int hy) {
+    const int ts = m_filteredBlockTmp[0].getStride(COMPONENT_Y);
+    const int ds = m_filteredBlock[0][0].getStride(COMPONENT_Y);
+    const int extH = (hy == 0) ? h + 8 : h + 7;
+    Pel* base = roi - 4 * stride - 1;
+    Pel* s1 = base + (hy > 0 ? stride : 0) + (hx >= 0 ? 1 : 0);
+    Pel* s3 = base + (hy > 0 ? stride : 0) + (hx > 0 ? 1 : 0);
+    Pel* t0 = m_filteredBlockTmp[0].getAddr(COMPONENT_Y);
+    Pel* t1 = m_filteredBlockTmp[1].getAddr(COMPONENT_Y);
+    Pel* t2 = m_filteredBlockTmp[2].getAddr(COMPONENT_Y);
+    Pel* t3 = m_filteredBlockTmp[3].getAddr(COMPONENT_Y);
+    m_if.filterHor(COMPONENT_Y, s1, stride, t1, ts, w, extH, 1, false, CHROMA_400, 8);
+    m_if.filterHor(COMPONENT_Y, s3, stride, t3, ts, w, extH, 3, false, CHROMA_400, 8);
+    auto ver = [&](Pel* src, int fy, int dy, int dx) {
+      m_if.filterVer(COMPONENT_Y, src, ts, m_filteredBlock[dy][dx].getAddr(COMPONENT_Y), ds, w, h, fy, false, true, CHROMA_400, 8);
+    };
+    const int rowTop = 3 * ts;      // (halfFilterSize - 1) rows
+    const int rowZero = hy == 0 ? ts : 0;
+    ver(t1 + rowTop + rowZero, 1, 1, 1);
+    ver(t1 + rowTop, 3, 3, 1);
+    if (hy != 0) {
+      ver(t1 + rowTop, 2, 2, 1);
+      ver(t3 + rowTop, 2, 2, 3);
+    } else {
+      ver(t1 + 4 * ts, 0, 0, 1);
+      ver(t3 + 4 * ts, 0, 0, 3);
+    }
+    if (hx != 0) {
+      Pel* a = t2 + rowTop + (hx > 0 ? 1 : 0) + (hy >= 0 ? ts : 0);
+      ver(a, 1, 1, 2);
+      Pel* b = t2 + rowTop + (hx > 0 ? 1 : 0) + (hy > 0 ? ts : 0);
+      ver(b, 3, 3, 2);
+    } else {
+      ver(t0 + rowTop + 1 + (hy >= 0 ? ts : 0), 1, 1, 0);
+      ver(t0 + rowTop + 1 + (hy > 0 ? ts : 0), 3, 3, 0);
+    }
+    ver(t3 + rowTop + rowZero, 1, 1, 3);
+    ver(t3 + rowTop, 3, 3, 3);
+  }
+
+  // --- 9-candidate refinement (xPatternRefinement) -----------------------------------
+  Distortion refine(TComPattern* key, int baseX, int baseY, int frac, int& mvx, int& mvy, bool allowHad) {
+    const int rs = m_filteredBlock[0][0].getStride(COMPONENT_Y);
+    rd.setDistParam(key, m_filteredBlock[0][0].getAddr(COMPONENT_Y), rs, 1, dp, hadme && allowHad);
+    const int (*tab)[2] = frac == 2 ? kH9 : kQ9;
+    Distortion best = std::numeric_limits<Distortion>::max();
+    int bi = 0;
+    for (int i = 0; i < 9; i++) {
+      const int hv = (tab[i][0] + baseX) * frac, vv = (tab[i][1] + baseY) * frac;
+      Pel* p = m_filteredBlock[vv & 3][hv & 3].getAddr(COMPONENT_Y);
+      if (hv == 2 && (vv & 1) == 0) p += 1;
+      if ((hv & 1) == 0 && vv == 2) p += rs;
+      dp.pCur = p;
+      dp.bitDepth = 8;
+      Distortion d = dp.DistFunc(&dp);
+      d += rd.getCostOfVectorWithPredictor(tab[i][0] + mvx, tab[i][1] + mvy);
+      if (d < best) {
+        best = d;
+        bi = i;
+        dp.m_maximumDistortionForEarlyExit = d;
+      }
+    }
+    mvx = tab[bi][0];
+    mvy = tab[bi][1];
+    return best;
+  }
+
+  // --- xPatternSearchFracDIF (cost scale 1 on entry, as xMotionEstimation sets) ------
+  Distortion fracDif(bool lossless, TComPattern* key, Pel* refY, int stride, int ix, int iy, int& hx, int& hy, int& qx, int& qy) {
+    Pel* roi = refY + ix + iy * stride;
+    const int w = key->getROIYWidth(), h = key->getROIYHeight();
+    rd.setCostScale(1);
+    upH(roi, stride, w, h);
+    int mx = ix * 2, my = iy * 2;
+    Distortion cost = refine(key, 0, 0, 2, mx, my, !lossless);
+    hx = mx;
+    hy = my;
+    rd.setCostScale(0);
+    upQ(roi, stride, w, h, hx, hy);
+    int qmx = (ix * 2 + hx) * 2, qmy = (iy * 2 + hy) * 2;
+    cost = refine(key, hx * 2, hy * 2, 1, qmx, qmy, !lossless);
+    qx = qmx;
+    qy = qmy;
+    return cost;
+  }
+
+  // --- xTZSearchHelp normal branch with save=true -----------------------------------
+  struct Best {
+    Distortion sad;
+    int x, y;
+  };
+  Distortion intDist(TComPattern* key, Pel* refY, int stride, int x, int y) {
+    rd.setDistParam(key, refY + y * stride + x, stride, dp);
+    dp.bitDepth = 8;
+    if ((fen == 1 || fen == 3) && dp.iRows > 8) dp.iSubShift = 1;
+    return dp.DistFunc(&dp);
+  }
+  void help(TComPattern* key, Pel* refY, int stride, Best& b, int x, int y, std::vector<uint32_t>& pushed) {
+    Distortion d = intDist(key, refY, stride, x, y);
+    pushed.push_back(d);
+    if (d < b.sad) {
+      d += rd.getCostOfVectorWithPredictor(x, y);
+      if (d < b.sad) {
+        b.sad = d;
+        b.x = x;
+        b.y = y;
+      }
+    }
+  }
+};
+
+struct Pic {
+  TComPicYuv yuv;
+  bool set = false;
+};
+
+struct RefCtx {
+  RefSearch s;
+  Pic pics[FME_MAX_PICTURES];
+  double lambda[FME_MAX_LAMBDAS] = {0};
+  std::vector<int16_t> keys;
+  std::vector<float> nn;
+  int nn_mode = 1;
+  // NN_pred global state (TEncSearch.cpp:55-57): array_e storage, C, PUHeight, PUWidth.
+  uint32_t slot[8] = {0};
+  uint32_t C = 0, puh = 0, puw = 0;
+};
+
+int nnClass(const float* P, const uint32_t* e, uint32_t c, int H, int W) {
+  // Scalar NN_pred(): sequential-k float32 sums, no FMA (TEncSearch.cpp:88-134).
+  auto eh = [](int v) { switch (v) { case 4: return 1; case 8: return 2; case 16: return 3; case 12: return 4; case 24: return 5; case 32: return 6; case 64: return 7; default: return 0; } };
+  auto ew = [](int v) { switch (v) { case 4: return 1; case 8: return 2; case 12: return 3; case 16: return 4; case 24: return 5; case 32: return 6; case 64: return 7; default: return 0; } };
+  const float *emb0 = P, *emb1 = P + 32, *w1 = P + 64, *w2 = P + 438, *w3 = P + 878;
+  const float *b1 = P + 1858, *g1 = P + 1880, *be1 = P + 1902, *b2 = P + 1924, *g2 = P + 1944;
+  const float *be2 = P + 1964, *bo = P + 1984, *gin = P + 2033, *mean = P + 2042, *sd = P + 2051;
+  float in[17], x1[22], x2[20];
+  for (int k = 0; k < 4; k++) {
+    in[k] = emb0[eh(H) * 4 + k];
+    in[4 + k] = emb1[ew(W) * 4 + k];
+  }
+  const uint32_t raw[9] = {e[0], e[1], e[2], e[3], c, e[4], e[5], e[6], e[7]};
+  for (int k = 0; k < 9; k++) {
+    volatile float t = ((float)raw[k] - mean[k]) / sd[k];
+    in[8 + k] = t * gin[k];
+  }
+  for (int r = 0; r < 22; r++) {
+    volatile float s = 0.f;
+    for (int k = 0; k < 17; k++) { volatile float p = w1[r * 17 + k] * in[k]; s = s + p; }
+    float v = s + b1[r];
+    v = v < 0.f ? 0.f : v;
+    volatile float m = v * g1[r];
+    x1[r] = m + be1[r];
+  }
+  for (int r = 0; r < 20; r++) {
+    volatile float s = 0.f;
+    for (int k = 0; k < 22; k++) { volatile float p = w2[r * 22 + k] * x1[k]; s = s + p; }
+    float v = s + b2[r];
+    v = v < 0.f ? 0.f : v;
+    volatile float m = v * g2[r];
+    x2[r] = m + be2[r];
+  }
+  int best = 0;
+  float bv = 0.f;
+  for (int r = 0; r < 49; r++) {
+    volatile float s = 0.f;
+    for (int k = 0; k < 20; k++) { volatile float p = w3[r * 20 + k] * x2[k]; s = s + p; }
+    float o = s + bo[r];
+    if (r == 0 || o > bv) { bv = o; best = r; }
+  }
+  return best;
+}
+
+}  // namespace
+
+extern "C" {
+
+void* ref_create(int use_hadamard, int fen, int nn_mode) {
+  initROM();
+  RefCtx* c = new RefCtx();
+  c->s.hadme = use_hadamard != 0;
+  c->s.fen = fen;
+  c->nn_mode = nn_mode;
+  return c;
+}
+
+void ref_destroy(void* h) { delete static_cast<RefCtx*>(h); }
+
+int ref_set_picture(void* h, int id, const uint8_t* luma, int stride, int w, int hgt) {
+  RefCtx* c = static_cast<RefCtx*>(h);
+  Pic& p = c->pics[id];
+  p.yuv.createWithoutCUInfo(w, hgt, CHROMA_400, true, 64, 64);  // 80-sample margin
+  Pel* dst = p.yuv.getAddr(COMPONENT_Y);
+  const int ds = p.yuv.getStride(COMPONENT_Y);
+  for (int y = 0; y < hgt; y++)
+    for (int x = 0; x < w; x++) dst[y * ds + x] = luma[(size_t)y * stride + x];
+  p.yuv.extendPicBorder();
+  p.set = true;
+  return 0;
+}
+
+void ref_set_lambda(void* h, int id, double lambda) { static_cast<RefCtx*>(h)->lambda[id] = lambda; }
+
+void ref_set_keys(void* h, const int16_t* k, size_t n) {
+  RefCtx* c = static_cast<RefCtx*>(h);
+  c->keys.assign(k, k + n);
+}
+
+void ref_load_nn(void* h, const float* p) {
+  RefCtx* c = static_cast<RefCtx*>(h);
+  c->nn.assign(p, p + FME_NN_PARAMS);
+}
+
+void ref_nn_reset(void* h) {
+  RefCtx* c = static_cast<RefCtx*>(h);
+  std::memset(c->slot, 0, sizeof(c->slot));
+  c->C = c->puh = c->puw = 0;
+}
+
+int ref_nn_class(void* h, const uint32_t* e, uint32_t cc, int H, int W) {
+  return nnClass(static_cast<RefCtx*>(h)->nn.data(), e, cc, H, W);
+}
+
+// Interpolate one PU at quarter-pel (qx,qy) through the reference filter classes
+// (TComPrediction::xPredInterBlk order, TComPrediction.cpp:643-683).
+void ref_pred_block(void* h, int id, int x0, int y0, int w, int hgt, int qx, int qy, int16_t* out) {
+  RefCtx* c = static_cast<RefCtx*>(h);
+  TComPicYuv& pic = c->pics[id].yuv;
+  const int stride = pic.getStride(COMPONENT_Y);
+  Pel* src = pic.getAddr(COMPONENT_Y) + (y0 + (qy >> 2)) * stride + x0 + (qx >> 2);
+  const int fx = qx & 3, fy = qy & 3;
+  TComInterpolationFilter f;
+  std::vector<Pel> dst(w * hgt), tmp(w * (hgt + 7));
+  if (fy == 0) {
+    f.filterHor(COMPONENT_Y, src, stride, dst.data(), w, w, hgt, fx, true, CHROMA_400, 8);
+  } else if (fx == 0) {
+    f.filterVer(COMPONENT_Y, src, stride, dst.data(), w, w, hgt, fy, true, true, CHROMA_400, 8);
+  } else {
+    f.filterHor(COMPONENT_Y, src - 3 * stride, stride, tmp.data(), w, w, hgt + 7, fx, false, CHROMA_400, 8);
+    f.filterVer(COMPONENT_Y, tmp.data() + 3 * w, w, dst.data(), w, w, hgt, fy, false, true, CHROMA_400, 8);
+  }
+  for (int i = 0; i < w * hgt; i++) out[i] = dst[i];
+}
+
+// Distortions through the reference DistParam dispatch.
+uint32_t ref_satd(void* h, const int16_t* org, int os, const int16_t* cur, int cs, int w, int hgt, int hadamard) {
+  RefCtx* c = static_cast<RefCtx*>(h);
+  DistParam d;
+  c->s.rd.setDistParam(d, 8, org, os, cur, cs, w, hgt, hadamard != 0);
+  return d.DistFunc(&d);
+}
+
+// The whole sub-pel part of xMotionEstimation for each job in order.
+int ref_refine(void* h, const fme_job* jobs, fme_result* res, int n) {
+  RefCtx* c = static_cast<RefCtx*>(h);
+  RefSearch& s = c->s;
+  std::vector<Pel> keybuf(64 * 64);
+  std::vector<uint32_t> pushed;
+  for (int i = 0; i < n; i++) {
+    const fme_job& j = jobs[i];
+    fme_result& r = res[i];
+    std::memset(&r, 0, sizeof(r));
+    if (!c->pics[j.ref_id].set) return FME_E_STATE;
+    TComPicYuv& ref = c->pics[j.ref_id].yuv;
+    const int rs = ref.getStride(COMPONENT_Y);
+    Pel* refY = ref.getAddr(COMPONENT_Y) + j.y * rs + j.x;
+    const int w = j.w, hh = j.h;
+    if (j.key_offset >= 0) {
+      for (int k = 0; k < w * hh; k++) keybuf[k] = c->keys[j.key_offset + k];
+    } else {
+      TComPicYuv& org = c->pics[j.org_id].yuv;
+      const int os = org.getStride(COMPONENT_Y);
+      const Pel* o = org.getAddr(COMPONENT_Y) + j.y * os + j.x;
+      for (int y = 0; y < hh; y++)
+        for (int x = 0; x < w; x++) keybuf[y * w + x] = o[y * os + x];
+    }
+    TComPattern key;
+    key.initPattern(keybuf.data(), w, hh, w, 8);
+    s.setLambda(c->lambda[j.lambda_id]);
+    TComMv pred(j.mvp_x, j.mvp_y);
+    s.rd.setPredictor(pred);
+
+    int ix = j.mv_x, iy = j.mv_y;
+    uint32_t C = 0;
+    int npush = 0;
+    if (j.flags & FME_JOB_EMI) {
+      s.rd.setCostScale(2);
+      RefSearch::Best b;
+      b.x = j.mv_x;
+      b.y = j.mv_y;
+      b.sad = s.intDist(&key, refY, rs, b.x, b.y) + s.rd.getCostOfVectorWithPredictor(b.x, b.y);
+      pushed.clear();
+      const int sx = b.x, sy = b.y;
+      if (sy - 1 >= j.lt_y) {
+        if (sx - 1 >= j.lt_x) s.help(&key, refY, rs, b, sx - 1, sy - 1, pushed);
+        s.help(&key, refY, rs, b, sx, sy - 1, pushed);
+        if (sx + 1 <= j.rb_x) s.help(&key, refY, rs, b, sx + 1, sy - 1, pushed);
+      }
+      if (sx - 1 >= j.lt_x) s.help(&key, refY, rs, b, sx - 1, sy, pushed);
+      if (sx + 1 <= j.rb_x) s.help(&key, refY, rs, b, sx + 1, sy, pushed);
+      if (sy + 1 <= j.rb_y) {
+        if (sx - 1 >= j.lt_x) s.help(&key, refY, rs, b, sx - 1, sy + 1, pushed);
+        s.help(&key, refY, rs, b, sx, sy + 1, pushed);
+        if (sx + 1 <= j.rb_x) s.help(&key, refY, rs, b, sx + 1, sy + 1, pushed);
+      }
+      C = b.sad - s.rd.getCostOfVectorWithPredictor(b.x, b.y);
+      ix = b.x;
+      iy = b.y;
+      npush = (int)pushed.size();
+      for (int k = 0; k < npush; k++) {
+        r.emi[k] = pushed[k];
+        c->slot[k] = pushed[k];
+      }
+      c->C = C;
+      c->puh = hh;
+      c->puw = w;
+    }
+    r.n_emi = (uint8_t)npush;
+    r.c = C;
+    r.mv_int_x = (int16_t)ix;
+    r.mv_int_y = (int16_t)iy;
+    int hx, hy, qx, qy;
+    const bool lossless = (j.flags & FME_JOB_LOSSLESS) != 0;
+    Distortion fc = s.fracDif(lossless, &key, refY, rs, ix, iy, hx, hy, qx, qy);
+    r.half_x = (int8_t)hx; r.half_y = (int8_t)hy; r.qtr_x = (int8_t)qx; r.qtr_y = (int8_t)qy;
+    r.frac_cost = fc;
+    s.rd.setCostScale(0);
+    int ox, oy;
+    if (c->nn_mode) {
+      int cls = nnClass(c->nn.data(), c->slot, c->C, (int)c->puh, (int)c->puw);
+      r.nn_class = (uint8_t)cls;
+      ox = cls % 7 - 3;
+      oy = cls / 7 - 3;
+    } else {
+      r.nn_class = 255;
+      ox = 2 * hx + qx;
+      oy = 2 * hy + qy;
+    }
+    const int mx = 4 * ix + ox, my = 4 * iy + oy;
+    r.mv_x = (int16_t)mx;
+    r.mv_y = (int16_t)my;
+    const UInt mvb = s.rd.getBitsOfVectorWithPredictor(mx, my);
+    const UInt bits = (UInt)j.bits_in + mvb;
+    r.bits = bits;
+    const double fw = (j.flags & FME_JOB_BIPRED) ? 0.5 : 1.0;
+    r.cost = (Distortion)(std::floor(fw * ((double)fc - (double)s.rd.getCost(mvb))) + (double)s.rd.getCost(bits));
+  }
+  return 0;
+}
+
+}  // extern "C"
