@@ -1,0 +1,248 @@
+#!/usr/bin/env python3
+"""Benchmark: sub-pel PU refinements/s on 1920x1080 lowdelay_P QP22, NN_pred on
+(BASELINE.json metric; configs[2] at QP22).
+
+A step is one frame batch: every (PU, reference picture) sub-pel job of one synthetic 1080p
+P-frame (510 CTUs x 423 calls x 4 references = 862,920 jobs, SURVEY.md §8(d) mix) through
+EMI step -> FracDIF -> NN_pred -> xMotionEstimation tail, jobs and pictures resident in HBM
+when timing starts.  With N ranks (torchrun, one GPU each) every rank refines its own frame
+(frames shard with no data-path collective: weak scaling); rank 0 owns the pictures and
+publishes each step's new frames to all ranks with an RCCL broadcast into a per-rank picture
+ring (nnfme.dist.PictureRing), which is part of the timed step.
+
+Prints one JSON line (rank 0).  `cpu_baseline` times oracle/_ref (the reference's own
+TLibCommon primitives driven in TEncSearch order, compiled -O2 like the reference build) on
+one host core over a bounded sample of the same job mix.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "hm16.9-nn_fme_amd"))
+
+from nnfme import synth  # noqa: E402
+from nnfme.abi import JOB_DTYPE, RESULT_DTYPE  # noqa: E402
+
+W, H, QP = 1920, 1080, 22
+METRIC = "sub-pel PU refinements/sec @ 1080p lowdelay_P QP22; bit-exact MV/SATD vs HM"
+HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md chip table (spec)
+VALU_PEAK_TOPS = 256 * 64 * 2.4e9 / 1e12   # int32 lane-ops/s at 2.4 GHz
+
+
+def algorithmic_bytes(jobs):
+    """W*H (org) + (W+8)(H+8) (reference footprint) + 48 (descriptor + result)."""
+    w = jobs["w"].astype(np.int64)
+    h = jobs["h"].astype(np.int64)
+    return int((w * h + (w + 8) * (h + 8) + 48).sum())
+
+
+def algorithmic_ops(jobs):
+    """SURVEY.md §8(d) integer-op count: 8-tap outputs x16, copies x2, 18 SATDs, 144 cost."""
+    w = jobs["w"].astype(np.int64)
+    h = jobs["h"].astype(np.int64)
+    taps = (w + 1) * (h + 8) + w * (h + 1) + (w + 1) * (h + 1) + 2 * w * (h + 8) + 8 * w * h
+    copies = (w + 1) * (h + 8) + w * h + (w + 1) * h
+    t8 = ((w % 8) == 0) & ((h % 8) == 0)
+    satd = np.where(t8, 575 * (w * h) // 64, 129 * (w * h) // 16)
+    return int((16 * taps + 2 * copies + 18 * satd + 144).sum())
+
+
+def make_frame_jobs(seed):
+    rng = np.random.default_rng(seed)
+    n = synth.jobs_per_frame(W, H)
+    # refs: picture ids 0..3, org: id 4; lambda slot = the frame's POC % 4 (set per step)
+    return synth.make_jobs(rng, W, H, n, 4, [0, 1, 2, 3], [0])
+
+
+def cpu_baseline(jobs_sample, pics):
+    """Time oracle/_ref on one core over `jobs_sample`."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    from oracle import Reference
+    from nnfme import weights
+    ref = Reference(use_hadamard=1, nn_mode=1, fast_inter_mode=1)
+    for k, v in pics.items():
+        ref.set_picture(k, v)
+    ref.set_lambda(0, synth.LDP_LAMBDA[QP][1])
+    ref.load_nn(weights.load_weights(QP))
+    ref.refine(jobs_sample[:2000])   # warm caches
+    t0 = time.perf_counter()
+    ref.refine(jobs_sample)
+    dt = time.perf_counter() - t0
+    return len(jobs_sample) / dt, dt
+
+
+def read_pmc_traffic():
+    """HBM bytes per search launch from the committed rocprofv3 PMC summary (profiles/), if any."""
+    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    if not os.path.exists(path):
+        return None, None
+    try:
+        d = json.load(open(path))
+        return d.get("bytes_per_launch"), d.get("source")
+    except Exception:
+        return None, None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample length")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--check", action="store_true", help="verify one step against the oracle sample")
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+    from nnfme.dist import PictureRing
+    from nnfme.runtime import FmeContext
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    stream = torch.cuda.current_stream(dev)
+
+    # ---- inputs (untimed): jobs of this rank's frames, resident in HBM ----------------------
+    jobs = make_frame_jobs(1000 + rank)
+    n = len(jobs)
+    d_jobs = torch.from_numpy(jobs.view(np.uint8).copy()).to(dev)
+    d_res = torch.empty(n * RESULT_DTYPE.itemsize, dtype=torch.uint8, device=dev)
+
+    # picture pool on the owner (rank 0): 8 distinct synthetic frames, frame f -> pool[f % 8]
+    pool = None
+    if rank == 0:
+        pool = torch.stack([torch.from_numpy(synth.synth_luma(W, H, t)) for t in range(8)]).to(dev)
+    ring = PictureRing(W, H, slots=world + 4, device=dev, world=world, owner=0)
+
+    ctx = FmeContext(device=local, use_hadamard=1, nn_mode=1, qp=QP, fast_inter_mode=1, max_jobs=n)
+    for lid, lam in enumerate(synth.LDP_LAMBDA[QP]):
+        ctx.set_lambda(lid, lam)
+    # lambda slot 0 is rewritten per step to the frame's POC % 4 value
+    base_lambda = synth.LDP_LAMBDA[QP]
+
+    def publish(step):
+        """Frames step*world .. step*world+world-1 become resident on every rank."""
+        first = step * world
+        for f in range(first, first + world):
+            src = pool[f % 8] if rank == 0 else None
+            ring.publish(f, src)
+
+    # prime the ring with the 4 reference frames preceding step 0
+    for f in range(-4, 0):
+        ring.publish(f, pool[f % 8] if rank == 0 else None)
+
+    def run_step(step):
+        publish(step)
+        f = step * world + rank
+        ring.bind(ctx, 4, f)
+        for k in range(4):
+            ring.bind(ctx, k, f - 1 - k)
+        ctx.set_lambda(0, base_lambda[f % 4])
+        ctx.refine_device(d_jobs.data_ptr(), d_res.data_ptr(), n, stream.cuda_stream)
+
+    for s in range(args.warmup):
+        run_step(s)
+    torch.cuda.synchronize(dev)
+
+    # correctness spot-check of the last warm-up step (optional)
+    if args.check and rank == 0:
+        res = d_res.cpu().numpy().view(RESULT_DTYPE)
+        print("check: nn classes", np.bincount(res["nn_class"], minlength=49)[:5], file=sys.stderr)
+
+    # ---- per-kernel timing with HIP events on the batch stream (one profiled step) -----------
+    ctx.set_profiling(True)
+    run_step(args.warmup)
+    tm = ctx.last_timings()
+    ctx.set_profiling(False)
+
+    # ---- timed region --------------------------------------------------------------------------
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for s in range(args.steps):
+        run_step(args.warmup + 1 + s)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    value = world * n * args.steps / elapsed
+    if rank == 0:
+        bytes_launch = algorithmic_bytes(jobs)
+        ops_launch = algorithmic_ops(jobs)
+        search_s = tm["search"] / 1e3
+        achieved = bytes_launch / search_s / 1e9
+        traffic, traffic_src = read_pmc_traffic()
+        out = {
+            "metric": METRIC,
+            "value": value,
+            "unit": "PU/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": elapsed / args.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "int16/int32 (NN f32)",
+            "data": "synthetic (SURVEY.md §8(d) YUV generator + PU-size mix; random-init-free: "
+                    "reference per-QP NN weights)",
+            "config": {"workload": "1920x1080 lowdelay_P QP22, NN_pred 2-layer on, 4 refs, "
+                                   "862920 PU jobs per frame (configs[2] at QP22)",
+                       "jobs_per_step_per_gpu": n, "parallelism": f"frame-sharded x{world}"},
+            "roofline": {
+                "bound": "hbm",
+                "achieved": achieved,
+                "peak": HBM_PEAK_GBS,
+                "unit": "GB/s",
+                "frac": achieved / HBM_PEAK_GBS,
+                "traffic": traffic,
+                "kernel": "fme::k_search (EMI + FracDIF)",
+                "search_ms": tm["search"],
+                "batch_ms": tm["batch"],
+                "kernel_ms": tm,
+                "valu_tops": ops_launch / search_s / 1e12,
+                "valu_peak_tops": VALU_PEAK_TOPS,
+                "valu_frac": ops_launch / search_s / 1e12 / VALU_PEAK_TOPS,
+                "note": "path is integer-VALU-bound (~97 ops/B); valu_frac is the binding roof",
+                "traffic_source": traffic_src,
+            },
+        }
+        if not args.no_cpu_baseline and world == 1:
+            pics = {k: synth.synth_luma(W, H, t) for k, t in zip(range(5), (7, 6, 5, 4, 0))}
+            m = int(min(n, max(20000, args.cpu_seconds * 80000)))
+            sample = jobs[:m]
+            rate, dt = cpu_baseline(sample, pics)
+            out["cpu_baseline"] = {
+                "value": rate, "unit": "PU/s", "cores": 1, "kind": "reference",
+                "sample": f"first {m} jobs of the same 1080p QP22 frame batch, one host core, "
+                          f"{dt:.1f} s (oracle/_ref: reference TLibCommon -O2 + TEncSearch-order "
+                          f"harness, NN restated scalar)",
+            }
+            out["speedup_vs_cpu_1core"] = value / rate
+        print(json.dumps(out), flush=True)
+
+    if world > 1:
+        dist.destroy_process_group()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

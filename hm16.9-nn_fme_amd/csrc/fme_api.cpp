@@ -1,0 +1,498 @@
+// fme_api.cpp — host runtime behind the C-ABI of include/fme.h.
+//
+// A context owns one device's copies of the pictures, the motion-lambda table, the bi-pred key
+// blocks, the NN weights, the NN_pred carried state (array_e slots, C, PUHeight, PUWidth,
+// TEncSearch.cpp:55-57) and the per-batch work buffers.  A batch is
+//   classify -> [one 100-byte D2H: class histogram] -> scatter -> search -> scan -> nn_tail
+// on the caller's stream.  Errors are returned as FME_E_* codes; the text is kept per thread.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "fme_device.h"
+
+using namespace fme;
+
+namespace {
+
+thread_local std::string g_last_error = "";
+
+int fail(int code, const char* fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof(buf), fmt, ap);
+  va_end(ap);
+  g_last_error = buf;
+  return code;
+}
+
+#define HIP_TRY(expr)                                                                       \
+  do {                                                                                      \
+    hipError_t _e = (expr);                                                                 \
+    if (_e != hipSuccess)                                                                   \
+      return fail(_e == hipErrorOutOfMemory ? FME_E_NOMEM : FME_E_DEVICE, "%s: %s (%s:%d)", \
+                  #expr, hipGetErrorString(_e), __FILE__, __LINE__);                        \
+  } while (0)
+
+template <typename T>
+struct DevBuf {
+  T* p = nullptr;
+  size_t cap = 0;
+  hipError_t reserve(size_t n) {
+    if (n <= cap) return hipSuccess;
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    cap = 0;
+    hipError_t e = hipMalloc(reinterpret_cast<void**>(&p), std::max<size_t>(n, 1) * sizeof(T));
+    if (e == hipSuccess) cap = n;
+    return e;
+  }
+  void release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    cap = 0;
+  }
+};
+
+}  // namespace
+
+struct fme_ctx {
+  int device = 0;
+  fme_config cfg{};
+  PicDesc pics[FME_MAX_PICTURES]{};
+  bool pic_owned[FME_MAX_PICTURES]{};
+  size_t pic_bytes[FME_MAX_PICTURES]{};
+  double mlambda[FME_MAX_LAMBDAS]{};
+  bool lambda_set[FME_MAX_LAMBDAS]{};
+  bool tables_dirty = true;
+
+  DevBuf<PicDesc> d_pics;
+  DevBuf<double> d_mlambda;
+  DevBuf<int16_t> d_keys;
+  size_t n_keys = 0;
+  DevBuf<float> d_nn;
+  bool nn_loaded = false;
+
+  DevBuf<fme_job> d_jobs;      // staging for fme_refine (host arrays)
+  DevBuf<fme_result> d_res;
+  DevBuf<uint8_t> cls;
+  DevBuf<int32_t> perm;
+  DevBuf<int32_t> counts;      // 25 counts + 24 cursors, one memset
+  DevBuf<int32_t> blk_agg;
+  DevBuf<int32_t> blk_prefix;
+  DevBuf<uint32_t> nn_state;   // 2 x 12 words
+  int state_cur = 0;
+  int32_t* h_counts = nullptr; // pinned
+
+  std::unique_ptr<fme_ctx> single;  // private context for the single-PU entry points
+  DevBuf<uint8_t> single_pic;
+  DevBuf<fme_job> single_job;
+  DevBuf<fme_result> single_res;
+  DevBuf<uint32_t> single_nn_in;
+  DevBuf<int32_t> single_nn_out;
+
+  bool profiling = false;
+  bool timed = false;
+  hipEvent_t ev[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};
+  hipEvent_t ev_end = nullptr;
+};
+
+namespace fme {
+hipError_t launch_nn_single(const float* nnp, const uint32_t* in, int32_t* out, hipStream_t s);
+}
+
+extern "C" {
+
+int fme_abi_version(void) { return FME_ABI_VERSION; }
+
+const char* fme_last_error(void) { return g_last_error.c_str(); }
+
+int fme_create(int device, const fme_config* cfg, fme_ctx** out_ctx) {
+  if (!cfg || !out_ctx) return fail(FME_E_INVALID, "fme_create: null argument");
+  *out_ctx = nullptr;
+  if (cfg->bit_depth != 8) return fail(FME_E_UNSUPPORTED, "fme_create: bit_depth %d (only 8)", cfg->bit_depth);
+  int ndev = 0;
+  HIP_TRY(hipGetDeviceCount(&ndev));
+  if (device < 0 || device >= ndev) return fail(FME_E_INVALID, "fme_create: device %d of %d", device, ndev);
+  HIP_TRY(hipSetDevice(device));
+  std::unique_ptr<fme_ctx> c(new fme_ctx());
+  c->device = device;
+  c->cfg = *cfg;
+  HIP_TRY(c->d_pics.reserve(FME_MAX_PICTURES));
+  HIP_TRY(c->d_mlambda.reserve(FME_MAX_LAMBDAS));
+  HIP_TRY(c->d_nn.reserve(FME_NN_PARAMS));
+  HIP_TRY(c->counts.reserve(2 * kNumClasses + 1));
+  HIP_TRY(c->nn_state.reserve(24));
+  HIP_TRY(hipMemset(c->nn_state.p, 0, 24 * sizeof(uint32_t)));
+  HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&c->h_counts), (kNumClasses + 1) * sizeof(int32_t), hipHostMallocDefault));
+  if (cfg->max_jobs > 0) {
+    const size_t n = (size_t)cfg->max_jobs;
+    const size_t nb = (n + kJobsPerScanBlock - 1) / kJobsPerScanBlock;
+    HIP_TRY(c->cls.reserve(n));
+    HIP_TRY(c->perm.reserve(n));
+    HIP_TRY(c->blk_agg.reserve(nb * 9));
+    HIP_TRY(c->blk_prefix.reserve(nb * 9));
+  }
+  *out_ctx = c.release();
+  return FME_OK;
+}
+
+int fme_destroy(fme_ctx* c) {
+  if (!c) return FME_OK;
+  (void)hipSetDevice(c->device);
+  (void)hipDeviceSynchronize();
+  for (int i = 0; i < FME_MAX_PICTURES; i++)
+    if (c->pic_owned[i] && c->pics[i].luma) (void)hipFree(const_cast<uint8_t*>(c->pics[i].luma));
+  c->d_pics.release(); c->d_mlambda.release(); c->d_keys.release(); c->d_nn.release();
+  c->d_jobs.release(); c->d_res.release(); c->cls.release(); c->perm.release();
+  c->counts.release(); c->blk_agg.release(); c->blk_prefix.release(); c->nn_state.release();
+  c->single_pic.release(); c->single_job.release(); c->single_res.release();
+  c->single_nn_in.release(); c->single_nn_out.release();
+  if (c->h_counts) (void)hipHostFree(c->h_counts);
+  for (auto& e : c->ev)
+    if (e) (void)hipEventDestroy(e);
+  if (c->ev_end) (void)hipEventDestroy(c->ev_end);
+  if (c->single) fme_destroy(c->single.release());
+  delete c;
+  return FME_OK;
+}
+
+int fme_set_picture(fme_ctx* c, int id, const uint8_t* luma, int stride, int width, int height, void* stream) {
+  if (!c || !luma) return fail(FME_E_INVALID, "fme_set_picture: null argument");
+  if (id < 0 || id >= FME_MAX_PICTURES) return fail(FME_E_INVALID, "fme_set_picture: id %d", id);
+  if (width <= 0 || height <= 0 || stride < width || width > 65535 || height > 65535)
+    return fail(FME_E_INVALID, "fme_set_picture: %dx%d stride %d", width, height, stride);
+  HIP_TRY(hipSetDevice(c->device));
+  const size_t bytes = (size_t)width * height;
+  uint8_t* dst = c->pic_owned[id] ? const_cast<uint8_t*>(c->pics[id].luma) : nullptr;
+  if (!dst || c->pic_bytes[id] < bytes) {
+    if (dst) HIP_TRY(hipFree(dst));
+    dst = nullptr;
+    HIP_TRY(hipMalloc(reinterpret_cast<void**>(&dst), bytes));
+    c->pic_bytes[id] = bytes;
+  }
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  HIP_TRY(hipMemcpy2DAsync(dst, width, luma, stride, width, height, hipMemcpyHostToDevice, s));
+  HIP_TRY(hipStreamSynchronize(s));  // the caller may free its host plane on return
+  c->pics[id] = PicDesc{dst, width, width, height};
+  c->pic_owned[id] = true;
+  c->tables_dirty = true;
+  return FME_OK;
+}
+
+int fme_bind_picture_device(fme_ctx* c, int id, const uint8_t* d_luma, int stride, int width, int height) {
+  if (!c || !d_luma) return fail(FME_E_INVALID, "fme_bind_picture_device: null argument");
+  if (id < 0 || id >= FME_MAX_PICTURES) return fail(FME_E_INVALID, "fme_bind_picture_device: id %d", id);
+  if (width <= 0 || height <= 0 || stride < width) return fail(FME_E_INVALID, "fme_bind_picture_device: geometry");
+  HIP_TRY(hipSetDevice(c->device));
+  if (c->pic_owned[id] && c->pics[id].luma) HIP_TRY(hipFree(const_cast<uint8_t*>(c->pics[id].luma)));
+  c->pic_owned[id] = false;
+  c->pic_bytes[id] = 0;
+  c->pics[id] = PicDesc{d_luma, stride, width, height};
+  c->tables_dirty = true;
+  return FME_OK;
+}
+
+int fme_set_lambda(fme_ctx* c, int id, double lambda) {
+  if (!c || id < 0 || id >= FME_MAX_LAMBDAS || !(lambda >= 0.0)) return fail(FME_E_INVALID, "fme_set_lambda: bad argument");
+  // TComRdCost::setLambda: m_dLambdaMotionSAD[0] = 65536.0 * sqrt(lambda); selectMotionLambda
+  // (true, 0, false) adds iAdd = 0 (TComRdCost.cpp:104-110, TComRdCost.h:159).
+  const double sq = std::sqrt(lambda);
+  c->mlambda[id] = 65536.0 * sq + 0;
+  c->lambda_set[id] = true;
+  c->tables_dirty = true;
+  return FME_OK;
+}
+
+int fme_set_motion_lambda(fme_ctx* c, int id, double ml) {
+  if (!c || id < 0 || id >= FME_MAX_LAMBDAS || !(ml >= 0.0)) return fail(FME_E_INVALID, "fme_set_motion_lambda: bad argument");
+  c->mlambda[id] = ml;
+  c->lambda_set[id] = true;
+  c->tables_dirty = true;
+  return FME_OK;
+}
+
+int fme_set_keys(fme_ctx* c, const int16_t* keys, size_t count, void* stream) {
+  if (!c || (!keys && count)) return fail(FME_E_INVALID, "fme_set_keys: null argument");
+  HIP_TRY(hipSetDevice(c->device));
+  HIP_TRY(c->d_keys.reserve(count));
+  if (count) {
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    HIP_TRY(hipMemcpyAsync(c->d_keys.p, keys, count * sizeof(int16_t), hipMemcpyHostToDevice, s));
+    HIP_TRY(hipStreamSynchronize(s));
+  }
+  c->n_keys = count;
+  return FME_OK;
+}
+
+int fme_load_nn_weights(fme_ctx* c, const float* params, int count) {
+  if (!c || !params) return fail(FME_E_INVALID, "fme_load_nn_weights: null argument");
+  if (count != FME_NN_PARAMS) return fail(FME_E_INVALID, "fme_load_nn_weights: %d params, expected %d", count, FME_NN_PARAMS);
+  HIP_TRY(hipSetDevice(c->device));
+  HIP_TRY(hipMemcpy(c->d_nn.p, params, FME_NN_PARAMS * sizeof(float), hipMemcpyHostToDevice));
+  c->nn_loaded = true;
+  return FME_OK;
+}
+
+int fme_nn_reset_state(fme_ctx* c) {
+  if (!c) return fail(FME_E_INVALID, "fme_nn_reset_state: null ctx");
+  HIP_TRY(hipSetDevice(c->device));
+  HIP_TRY(hipMemset(c->nn_state.p, 0, 24 * sizeof(uint32_t)));
+  c->state_cur = 0;
+  return FME_OK;
+}
+
+int fme_nn_get_state(fme_ctx* c, uint32_t* out12) {
+  if (!c || !out12) return fail(FME_E_INVALID, "fme_nn_get_state: null argument");
+  HIP_TRY(hipSetDevice(c->device));
+  HIP_TRY(hipDeviceSynchronize());
+  HIP_TRY(hipMemcpy(out12, c->nn_state.p + 12 * c->state_cur, 12 * sizeof(uint32_t), hipMemcpyDeviceToHost));
+  return FME_OK;
+}
+
+int fme_nn_set_state(fme_ctx* c, const uint32_t* in12) {
+  if (!c || !in12) return fail(FME_E_INVALID, "fme_nn_set_state: null argument");
+  HIP_TRY(hipSetDevice(c->device));
+  HIP_TRY(hipDeviceSynchronize());
+  HIP_TRY(hipMemcpy(c->nn_state.p + 12 * c->state_cur, in12, 12 * sizeof(uint32_t), hipMemcpyHostToDevice));
+  return FME_OK;
+}
+
+static int ensure_work(fme_ctx* c, int n) {
+  const size_t nb = ((size_t)n + kJobsPerScanBlock - 1) / kJobsPerScanBlock;
+  HIP_TRY(c->cls.reserve(n));
+  HIP_TRY(c->perm.reserve(n));
+  HIP_TRY(c->blk_agg.reserve(nb * 9));
+  HIP_TRY(c->blk_prefix.reserve(nb * 9));
+  return FME_OK;
+}
+
+static int sync_tables(fme_ctx* c, hipStream_t s) {
+  if (!c->tables_dirty) return FME_OK;
+  HIP_TRY(hipMemcpyAsync(c->d_pics.p, c->pics, sizeof(c->pics), hipMemcpyHostToDevice, s));
+  HIP_TRY(hipMemcpyAsync(c->d_mlambda.p, c->mlambda, sizeof(c->mlambda), hipMemcpyHostToDevice, s));
+  c->tables_dirty = false;
+  return FME_OK;
+}
+
+// Device validation covers what the host cannot see for device-resident jobs: a job with an
+// unknown PU shape, an unset picture / lambda slot or a key block outside the key buffer is
+// classified "invalid" and the batch is rejected before any search work is launched.
+int fme_refine_device(fme_ctx* c, const fme_job* d_jobs, fme_result* d_res, int n, void* stream) {
+  if (!c || (n > 0 && (!d_jobs || !d_res))) return fail(FME_E_INVALID, "fme_refine_device: null argument");
+  if (n < 0) return fail(FME_E_INVALID, "fme_refine_device: n = %d", n);
+  if (n == 0) return FME_OK;
+  if (c->cfg.nn_mode && !c->nn_loaded) return fail(FME_E_STATE, "fme_refine_device: nn_mode set but no weights loaded");
+  HIP_TRY(hipSetDevice(c->device));
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  int rc = ensure_work(c, n);
+  if (rc) return rc;
+  rc = sync_tables(c, s);
+  if (rc) return rc;
+
+  BatchArgs a{};
+  a.jobs = d_jobs;
+  a.res = d_res;
+  a.keys = c->d_keys.p;
+  a.n_keys = (int64_t)c->n_keys;
+  a.mlambda = c->d_mlambda.p;
+  a.pics = c->d_pics.p;
+  a.n = n;
+  a.use_hadamard = c->cfg.use_hadamard ? 1 : 0;
+  a.fen = c->cfg.fast_inter_mode;
+  a.nn_mode = c->cfg.nn_mode ? 1 : 0;
+  WorkBufs w{};
+  w.cls = c->cls.p;
+  w.perm = c->perm.p;
+  w.counts = c->counts.p;
+  w.cursor = c->counts.p + kNumClasses + 1;
+  w.blk_agg = c->blk_agg.p;
+  w.blk_prefix = c->blk_prefix.p;
+  w.nn_state = c->nn_state.p;
+
+  const bool prof = c->profiling;
+  if (prof) HIP_TRY(hipEventRecord(c->ev[0], s));
+  HIP_TRY(hipMemsetAsync(c->counts.p, 0, (2 * kNumClasses + 1) * sizeof(int32_t), s));
+  HIP_TRY(launch_classify(a, w, s));
+  if (prof) HIP_TRY(hipEventRecord(c->ev[1], s));
+  HIP_TRY(hipMemcpyAsync(c->h_counts, c->counts.p, (kNumClasses + 1) * sizeof(int32_t), hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipStreamSynchronize(s));
+  if (c->h_counts[kNumClasses] > 0)
+    return fail(FME_E_INVALID, "fme_refine_device: %d job(s) with an unsupported PU size or unset picture/lambda/key",
+                c->h_counts[kNumClasses]);
+
+  Schedule sc{};
+  size_t lds = 0;
+  int off = 0, tiles = 0;
+  for (int k = 0; k < kNumClasses; k++) {
+    const int cnt = c->h_counts[k];
+    sc.class_off[k] = off;
+    sc.class_cnt[k] = cnt;
+    sc.tile_prefix[k] = tiles;
+    if (cnt) {
+      const int p = pus_per_tile(k);
+      tiles += (cnt + p - 1) / p;
+      lds = std::max(lds, lds_bytes_for_class(k));
+    }
+    off += cnt;
+  }
+  sc.tile_prefix[kNumClasses] = tiles;
+  if (prof) HIP_TRY(hipEventRecord(c->ev[2], s));   // host sync above: scatter starts here
+  HIP_TRY(launch_scatter(a, w, sc, s));
+  if (prof) HIP_TRY(hipEventRecord(c->ev[3], s));
+  HIP_TRY(launch_search(a, w, sc, lds, s));
+  if (prof) HIP_TRY(hipEventRecord(c->ev[4], s));
+  HIP_TRY(launch_nn_tail(a, w, c->d_nn.p, c->state_cur, s));
+  if (prof) {
+    HIP_TRY(hipEventRecord(c->ev_end, s));
+    c->timed = true;
+  }
+  if (a.nn_mode) c->state_cur ^= 1;
+  return FME_OK;
+}
+
+int fme_refine(fme_ctx* c, const fme_job* jobs, fme_result* res, int n, void* stream) {
+  if (!c || (n > 0 && (!jobs || !res))) return fail(FME_E_INVALID, "fme_refine: null argument");
+  if (n <= 0) return n == 0 ? FME_OK : fail(FME_E_INVALID, "fme_refine: n = %d", n);
+  HIP_TRY(hipSetDevice(c->device));
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  HIP_TRY(c->d_jobs.reserve(n));
+  HIP_TRY(c->d_res.reserve(n));
+  HIP_TRY(hipMemcpyAsync(c->d_jobs.p, jobs, (size_t)n * sizeof(fme_job), hipMemcpyHostToDevice, s));
+  int rc = fme_refine_device(c, c->d_jobs.p, c->d_res.p, n, stream);
+  if (rc) return rc;
+  HIP_TRY(hipMemcpyAsync(res, c->d_res.p, (size_t)n * sizeof(fme_result), hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipStreamSynchronize(s));
+  return FME_OK;
+}
+
+// xPatternSearchFracDIF for one PU: the reference window around mv_int becomes a private
+// (w+8) x (h+8) picture; the MV predictor is shifted by 4*mv_int so that every MV-cost
+// argument (xPatternRefinement's (cMvTest << scale) - pred) is unchanged.
+int fme_frac_dif_single(fme_ctx* c, int lossless, const int16_t* key, int key_stride, int w, int h,
+                        const int16_t* ref, int ref_stride, int mv_int_x, int mv_int_y, int mvp_x,
+                        int mvp_y, double motion_lambda, int16_t* half_xy, int16_t* qtr_xy,
+                        uint32_t* cost) {
+  if (!c || !key || !ref || !half_xy || !qtr_xy || !cost) return fail(FME_E_INVALID, "fme_frac_dif_single: null argument");
+  if (w < 4 || h < 4 || w > 64 || h > 64 || (w & 3) || (h & 3)) return fail(FME_E_UNSUPPORTED, "fme_frac_dif_single: %dx%d", w, h);
+  HIP_TRY(hipSetDevice(c->device));
+  if (!c->single) {
+    fme_config sc = c->cfg;
+    sc.nn_mode = 0;
+    sc.max_jobs = 1;
+    fme_ctx* sub = nullptr;
+    int rc = fme_create(c->device, &sc, &sub);
+    if (rc) return rc;
+    c->single.reset(sub);
+  }
+  fme_ctx* sub = c->single.get();
+  sub->cfg.use_hadamard = c->cfg.use_hadamard;
+  const int pw = w + 8, ph = h + 8;
+  std::vector<uint8_t> win((size_t)pw * ph);
+  for (int y = 0; y < ph; y++)
+    for (int x = 0; x < pw; x++) {
+      const int v = ref[(ptrdiff_t)(mv_int_y - 4 + y) * ref_stride + (mv_int_x - 4 + x)];
+      win[(size_t)y * pw + x] = (uint8_t)std::min(255, std::max(0, v));
+    }
+  std::vector<int16_t> kb((size_t)w * h);
+  for (int y = 0; y < h; y++)
+    for (int x = 0; x < w; x++) kb[(size_t)y * w + x] = key[(ptrdiff_t)y * key_stride + x];
+  int rc = fme_set_picture(sub, 0, win.data(), pw, pw, ph, nullptr);
+  if (rc) return rc;
+  rc = fme_set_keys(sub, kb.data(), kb.size(), nullptr);
+  if (rc) return rc;
+  rc = fme_set_motion_lambda(sub, 0, motion_lambda);
+  if (rc) return rc;
+  fme_job j{};
+  j.x = 4;
+  j.y = 4;
+  j.w = (uint8_t)w;
+  j.h = (uint8_t)h;
+  j.org_id = 0;
+  j.ref_id = 0;
+  j.mv_x = 0;
+  j.mv_y = 0;
+  const int px = mvp_x - 4 * mv_int_x, py = mvp_y - 4 * mv_int_y;
+  if (px < -32768 || px > 32767 || py < -32768 || py > 32767) return fail(FME_E_INVALID, "fme_frac_dif_single: predictor out of range");
+  j.mvp_x = (int16_t)px;
+  j.mvp_y = (int16_t)py;
+  j.flags = lossless ? FME_JOB_LOSSLESS : 0;
+  j.lambda_id = 0;
+  j.key_offset = 0;
+  fme_result r{};
+  rc = fme_refine(sub, &j, &r, 1, nullptr);
+  if (rc) return rc;
+  half_xy[0] = r.half_x;
+  half_xy[1] = r.half_y;
+  qtr_xy[0] = r.qtr_x;
+  qtr_xy[1] = r.qtr_y;
+  *cost = r.frac_cost;
+  return FME_OK;
+}
+
+int fme_nn_pred_single(fme_ctx* c, const uint32_t* e, uint32_t cc, int pu_h, int pu_w, int* nn_class, int16_t* out4) {
+  if (!c || !e || !nn_class) return fail(FME_E_INVALID, "fme_nn_pred_single: null argument");
+  if (!c->nn_loaded) return fail(FME_E_STATE, "fme_nn_pred_single: no weights loaded");
+  HIP_TRY(hipSetDevice(c->device));
+  HIP_TRY(c->single_nn_in.reserve(11));
+  HIP_TRY(c->single_nn_out.reserve(1));
+  uint32_t in[11];
+  for (int s = 0; s < 8; s++) in[s] = e[s];
+  in[8] = cc;
+  in[9] = (uint32_t)pu_h;
+  in[10] = (uint32_t)pu_w;
+  HIP_TRY(hipMemcpy(c->single_nn_in.p, in, sizeof(in), hipMemcpyHostToDevice));
+  HIP_TRY(launch_nn_single(c->d_nn.p, c->single_nn_in.p, c->single_nn_out.p, nullptr));
+  int32_t cls = 0;
+  HIP_TRY(hipMemcpy(&cls, c->single_nn_out.p, sizeof(cls), hipMemcpyDeviceToHost));
+  *nn_class = cls;
+  if (out4) {
+    // MVX_HALF, MVX_QRTER, MVY_HALF, MVY_QRTER of the switch at TEncSearch.cpp:136-193:
+    // the half/quarter split of the offset (cls % 7 - 3, cls / 7 - 3) with the quarter part
+    // in {-1, 0, 1} and x = 2 * half + quarter.
+    const int ox = cls % 7 - 3, oy = cls / 7 - 3;
+    auto split = [](int o, int16_t& hf, int16_t& qt) {
+      static const int8_t H[7] = {-1, -1, 0, 0, 0, 1, 1}, Q[7] = {-1, 0, -1, 0, 1, 0, 1};
+      hf = H[o + 3];
+      qt = Q[o + 3];
+    };
+    split(ox, out4[0], out4[1]);
+    split(oy, out4[2], out4[3]);
+  }
+  return FME_OK;
+}
+
+int fme_set_profiling(fme_ctx* c, int enable) {
+  if (!c) return fail(FME_E_INVALID, "fme_set_profiling: null ctx");
+  HIP_TRY(hipSetDevice(c->device));
+  if (enable && !c->ev_end) {
+    for (auto& e : c->ev) HIP_TRY(hipEventCreate(&e));
+    HIP_TRY(hipEventCreate(&c->ev_end));
+  }
+  c->profiling = enable != 0;
+  c->timed = false;
+  return FME_OK;
+}
+
+int fme_last_timings(fme_ctx* c, float* ms) {
+  if (!c || !ms) return fail(FME_E_INVALID, "fme_last_timings: null argument");
+  if (!c->timed) return fail(FME_E_STATE, "fme_last_timings: no profiled batch");
+  HIP_TRY(hipSetDevice(c->device));
+  HIP_TRY(hipEventSynchronize(c->ev_end));
+  HIP_TRY(hipEventElapsedTime(&ms[0], c->ev[0], c->ev[1]));
+  HIP_TRY(hipEventElapsedTime(&ms[1], c->ev[2], c->ev[3]));
+  HIP_TRY(hipEventElapsedTime(&ms[2], c->ev[3], c->ev[4]));
+  HIP_TRY(hipEventElapsedTime(&ms[3], c->ev[4], c->ev_end));
+  HIP_TRY(hipEventElapsedTime(&ms[4], c->ev[0], c->ev_end));
+  return FME_OK;
+}
+
+}  // extern "C"

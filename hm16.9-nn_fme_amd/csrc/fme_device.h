@@ -1,0 +1,70 @@
+// fme_device.h — types shared by the HIP kernels (fme_kernels.hip) and the host runtime
+// (fme_api.cpp).  Not part of the public ABI (include/fme.h is).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/fme.h"
+
+namespace fme {
+
+constexpr int kNumClasses = 24;      // HEVC inter PU shapes 4x8 .. 64x64 incl. AMP
+constexpr int kBlock = 256;          // threads per workgroup (4 wavefronts)
+constexpr int kJobsPerScanBlock = 1024;  // classify / NN kernels: 4 jobs per thread
+
+// PU shape of each class (W, H).  Order: by area, then width.
+constexpr int kClassW[kNumClasses] = {4, 8, 8, 4, 16, 8, 16, 12, 16, 16, 8, 32,
+                                      16, 32, 24, 32, 32, 16, 64, 32, 64, 48, 64, 64};
+constexpr int kClassH[kNumClasses] = {8, 4, 8, 16, 4, 16, 8, 16, 12, 16, 32, 8,
+                                      32, 16, 32, 24, 32, 64, 16, 64, 32, 64, 48, 64};
+
+struct PicDesc {
+  const uint8_t* luma;
+  int32_t stride, width, height;
+};
+
+// One batch as the device sees it.
+struct BatchArgs {
+  const fme_job* jobs;
+  fme_result* res;
+  const int16_t* keys;
+  int64_t n_keys;
+  const double* mlambda;      // [FME_MAX_LAMBDAS]
+  const PicDesc* pics;        // [FME_MAX_PICTURES]
+  int32_t n;
+  int32_t use_hadamard;
+  int32_t fen;
+  int32_t nn_mode;
+};
+
+// Work buffers (device) for one batch.
+struct WorkBufs {
+  uint8_t* cls;          // [n] class id, 255 = invalid
+  int32_t* perm;         // [n] jobs grouped by class
+  int32_t* counts;       // [kNumClasses + 1]: per-class count, [24] = invalid jobs
+  int32_t* cursor;       // [kNumClasses]
+  int32_t* blk_agg;      // [nblk * 9] per-block max of the NN writer indices
+  int32_t* blk_prefix;   // [nblk * 9] exclusive prefix (carry-in) per block
+  uint32_t* nn_state;    // 2 x 12 words: slot[8], c, pu_h, pu_w, written
+};
+
+// Tile schedule of the search kernel: blocks [tile_prefix[c], tile_prefix[c+1]) handle
+// class c; class c's jobs are perm[class_off[c] .. class_off[c] + class_cnt[c]).
+struct Schedule {
+  int32_t tile_prefix[kNumClasses + 1];
+  int32_t class_off[kNumClasses];
+  int32_t class_cnt[kNumClasses];
+};
+
+// Host-side launch helpers (fme_kernels.hip).
+int pus_per_tile(int cls);
+size_t lds_bytes_for_class(int cls);
+hipError_t launch_classify(const BatchArgs& a, const WorkBufs& w, hipStream_t s);
+hipError_t launch_scatter(const BatchArgs& a, const WorkBufs& w, const Schedule& sc, hipStream_t s);
+hipError_t launch_search(const BatchArgs& a, const WorkBufs& w, const Schedule& sc, size_t lds,
+                         hipStream_t s);
+hipError_t launch_nn_tail(const BatchArgs& a, const WorkBufs& w, const float* nn_params,
+                          int state_in, hipStream_t s);
+
+}  // namespace fme

@@ -1,0 +1,196 @@
+"""ctypes binding of libfme_amd.so (include/fme.h).
+
+This is the product path: every call lands in the HIP kernels of csrc/fme_kernels.hip.  There
+is no CPU fallback — a missing or unloadable library raises FmeError at import of the
+context, and every failing C call raises FmeError with fme_last_error()'s text.
+"""
+import ctypes as C
+import os
+
+import numpy as np
+
+from .abi import JOB_DTYPE, NN_PARAMS, RESULT_DTYPE
+from .weights import load_weights
+
+PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB_PATH = os.path.join(PKG_ROOT, "libfme_amd.so")
+
+# Every entry point include/fme.h declares (the ABI test checks the .so exports them).
+ABI_SYMBOLS = (
+    "fme_abi_version", "fme_create", "fme_destroy", "fme_last_error", "fme_set_picture",
+    "fme_bind_picture_device", "fme_set_lambda", "fme_set_motion_lambda", "fme_set_keys",
+    "fme_load_nn_weights", "fme_nn_reset_state", "fme_nn_get_state", "fme_nn_set_state", "fme_refine", "fme_refine_device",
+    "fme_frac_dif_single", "fme_nn_pred_single", "fme_set_profiling", "fme_last_timings",
+)
+
+
+class FmeError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__(f"[{code}] {msg}")
+        self.code = code
+
+
+class FmeConfig(C.Structure):
+    _fields_ = [("bit_depth", C.c_int32), ("use_hadamard", C.c_int32), ("nn_mode", C.c_int32),
+                ("qp", C.c_int32), ("fast_inter_mode", C.c_int32), ("max_jobs", C.c_int32)]
+
+
+_lib = None
+
+
+def load_library(path=LIB_PATH):
+    """Load libfme_amd.so once; raise if it has not been built."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise FmeError(-1, f"{path} missing: build it with __graft_entry__.build() or "
+                           f"`make -C hm16.9-nn_fme_amd`")
+    lib = C.CDLL(path)
+    P, I, U32, D = C.c_void_p, C.c_int, C.c_uint32, C.c_double
+    sig = {
+        "fme_abi_version": (I, []),
+        "fme_create": (I, [I, P, P]),
+        "fme_destroy": (I, [P]),
+        "fme_last_error": (C.c_char_p, []),
+        "fme_set_picture": (I, [P, I, P, I, I, I, P]),
+        "fme_bind_picture_device": (I, [P, I, P, I, I, I]),
+        "fme_set_lambda": (I, [P, I, D]),
+        "fme_set_motion_lambda": (I, [P, I, D]),
+        "fme_set_keys": (I, [P, P, C.c_size_t, P]),
+        "fme_load_nn_weights": (I, [P, P, I]),
+        "fme_nn_reset_state": (I, [P]),
+        "fme_nn_get_state": (I, [P, P]),
+        "fme_nn_set_state": (I, [P, P]),
+        "fme_refine": (I, [P, P, P, I, P]),
+        "fme_refine_device": (I, [P, P, P, I, P]),
+        "fme_frac_dif_single": (I, [P, I, P, I, I, I, P, I, I, I, I, I, D, P, P, P]),
+        "fme_nn_pred_single": (I, [P, P, U32, I, I, P, P]),
+        "fme_set_profiling": (I, [P, I]),
+        "fme_last_timings": (I, [P, P]),
+    }
+    for name, (res, args) in sig.items():
+        f = getattr(lib, name)
+        f.restype = res
+        f.argtypes = args
+    if lib.fme_abi_version() != 1:
+        raise FmeError(-1, "ABI version mismatch")
+    _lib = lib
+    return lib
+
+
+def _check(lib, rc):
+    if rc != 0:
+        raise FmeError(rc, lib.fme_last_error().decode(errors="replace"))
+
+
+def _ptr(a):
+    return C.c_void_p(a.ctypes.data)
+
+
+class FmeContext:
+    """One device context: pictures, lambdas, keys, NN weights and the carried NN state."""
+
+    def __init__(self, device=0, use_hadamard=1, nn_mode=1, qp=22, fast_inter_mode=1, max_jobs=0,
+                 load_nn=True):
+        self.lib = load_library()
+        self.cfg = FmeConfig(8, use_hadamard, nn_mode, qp, fast_inter_mode, max_jobs)
+        h = C.c_void_p()
+        _check(self.lib, self.lib.fme_create(device, C.byref(self.cfg), C.byref(h)))
+        self.h = h
+        self.device = device
+        if nn_mode and load_nn:
+            self.load_nn(load_weights(qp))
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.lib.fme_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # -- state --------------------------------------------------------------------------
+    def set_picture(self, pid, luma, stream=None):
+        luma = np.ascontiguousarray(luma, dtype=np.uint8)
+        h, w = luma.shape
+        _check(self.lib, self.lib.fme_set_picture(self.h, pid, _ptr(luma), w, w, h, stream))
+
+    def bind_picture_device(self, pid, data_ptr, stride, width, height):
+        _check(self.lib, self.lib.fme_bind_picture_device(self.h, pid, C.c_void_p(data_ptr), stride, width, height))
+
+    def set_lambda(self, lid, lam):
+        _check(self.lib, self.lib.fme_set_lambda(self.h, lid, float(lam)))
+
+    def set_motion_lambda(self, lid, ml):
+        _check(self.lib, self.lib.fme_set_motion_lambda(self.h, lid, float(ml)))
+
+    def set_keys(self, keys, stream=None):
+        keys = np.ascontiguousarray(keys, dtype=np.int16)
+        _check(self.lib, self.lib.fme_set_keys(self.h, _ptr(keys), keys.size, stream))
+
+    def load_nn(self, params):
+        p = np.ascontiguousarray(params, dtype=np.float32)
+        if p.size != NN_PARAMS:
+            raise FmeError(-1, f"{p.size} NN parameters, expected {NN_PARAMS}")
+        _check(self.lib, self.lib.fme_load_nn_weights(self.h, _ptr(p), p.size))
+
+    def nn_reset(self):
+        _check(self.lib, self.lib.fme_nn_reset_state(self.h))
+
+    def nn_get_state(self):
+        out = np.zeros(12, np.uint32)
+        _check(self.lib, self.lib.fme_nn_get_state(self.h, _ptr(out)))
+        return out
+
+    def nn_set_state(self, state):
+        st = np.ascontiguousarray(state, dtype=np.uint32)
+        assert st.size == 12
+        _check(self.lib, self.lib.fme_nn_set_state(self.h, _ptr(st)))
+
+    # -- work ---------------------------------------------------------------------------
+    def refine(self, jobs, stream=None):
+        jobs = np.ascontiguousarray(jobs, dtype=JOB_DTYPE)
+        res = np.zeros(len(jobs), dtype=RESULT_DTYPE)
+        _check(self.lib, self.lib.fme_refine(self.h, _ptr(jobs), _ptr(res), len(jobs), stream))
+        return res
+
+    def refine_device(self, jobs_ptr, res_ptr, n, stream=None):
+        """Device-resident jobs/results (e.g. torch uint8 tensors' data_ptr())."""
+        _check(self.lib, self.lib.fme_refine_device(self.h, C.c_void_p(jobs_ptr), C.c_void_p(res_ptr), n, stream))
+
+    def frac_dif_single(self, key, ref_window, ref_origin, mv_int, mvp, motion_lambda, lossless=False):
+        """xPatternSearchFracDIF argument list: key block (int16 HxW), a padded reference
+        plane (int16) with the PU origin at ref_origin=(row, col), full-pel mv_int, qpel mvp."""
+        key = np.ascontiguousarray(key, dtype=np.int16)
+        ref = np.ascontiguousarray(ref_window, dtype=np.int16)
+        h, w = key.shape
+        r0, c0 = ref_origin
+        base = ref.ctypes.data + (r0 * ref.shape[1] + c0) * 2
+        half = np.zeros(2, np.int16)
+        qtr = np.zeros(2, np.int16)
+        cost = np.zeros(1, np.uint32)
+        _check(self.lib, self.lib.fme_frac_dif_single(
+            self.h, int(lossless), _ptr(key), w, w, h, C.c_void_p(base), ref.shape[1],
+            int(mv_int[0]), int(mv_int[1]), int(mvp[0]), int(mvp[1]), float(motion_lambda),
+            _ptr(half), _ptr(qtr), _ptr(cost)))
+        return (int(half[0]), int(half[1])), (int(qtr[0]), int(qtr[1])), int(cost[0])
+
+    def set_profiling(self, enable=True):
+        _check(self.lib, self.lib.fme_set_profiling(self.h, int(enable)))
+
+    def last_timings(self):
+        """Device ms of the last batch: classify, scatter, search, nn_tail, whole batch."""
+        ms = np.zeros(5, np.float32)
+        _check(self.lib, self.lib.fme_last_timings(self.h, _ptr(ms)))
+        return dict(zip(("classify", "scatter", "search", "nn_tail", "batch"), ms.tolist()))
+
+    def nn_pred_single(self, e, c, pu_h, pu_w):
+        e = np.ascontiguousarray(e, dtype=np.uint32)
+        cls = C.c_int()
+        out4 = np.zeros(4, np.int16)
+        _check(self.lib, self.lib.fme_nn_pred_single(self.h, _ptr(e), int(c), int(pu_h), int(pu_w), C.byref(cls), _ptr(out4)))
+        return cls.value, tuple(int(v) for v in out4)

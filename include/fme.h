@@ -154,6 +154,11 @@ int fme_set_keys(fme_ctx* ctx, const int16_t* keys, size_t count, void* stream);
 int fme_load_nn_weights(fme_ctx* ctx, const float* params, int count);
 /* Forget the array_e/C/PUHeight/PUWidth state carried across calls (process start). */
 int fme_nn_reset_state(fme_ctx* ctx);
+/* The carried state as 12 words: array_e slots[8], C, PUHeight, PUWidth, and a written mask
+ * (bit s: slot s written since reset, bit 8: C/PU size written).  Lets a frame-sharded run
+ * hand the state of frame f-1 to the rank that refines frame f (nnfme/dist.py).         */
+int fme_nn_get_state(fme_ctx* ctx, uint32_t* out12);
+int fme_nn_set_state(fme_ctx* ctx, const uint32_t* in12);
 
 /* ---- the batch path --------------------------------------------------------------------- *
  * Runs EMI step -> FracDIF -> NN_pred -> xMotionEstimation tail for n jobs, in job order
@@ -182,6 +187,14 @@ int fme_frac_dif_single(fme_ctx* ctx, int lossless, const int16_t* key, int key_
  * MVY_HALF, MVY_QRTER in out4 (TEncSearch.cpp:136-193).                                */
 int fme_nn_pred_single(fme_ctx* ctx, const uint32_t* e, uint32_t c, int pu_h, int pu_w,
                        int* nn_class, int16_t* out4);
+
+/* ---- instrumentation (an extension; the reference has no counterpart) ------------------- *
+ * With profiling on, fme_refine/fme_refine_device record HIP events around each kernel of
+ * the batch on the batch's stream; fme_last_timings() waits for the last batch and returns
+ * device milliseconds: [0] classify, [1] scatter, [2] search (EMI + FracDIF), [3] NN + tail,
+ * [4] whole batch (first kernel start to last kernel end, host sync included).            */
+int fme_set_profiling(fme_ctx* ctx, int enable);
+int fme_last_timings(fme_ctx* ctx, float* ms5);
 
 #ifdef __cplusplus
 }

@@ -376,6 +376,21 @@ void orc_load_nn(orc_ctx* ctx, const float* params) {
   ctx->nn_loaded = 1;
 }
 void orc_nn_reset(orc_ctx* ctx) { memset(&ctx->nn_state, 0, sizeof(ctx->nn_state)); }
+/* 12-word layout of fme_nn_get_state: slots[8], C, PUHeight, PUWidth, written mask. */
+void orc_nn_get_state(const orc_ctx* ctx, uint32_t out[12]) {
+  memcpy(out, ctx->nn_state.slot, 8 * sizeof(uint32_t));
+  out[8] = ctx->nn_state.c;
+  out[9] = ctx->nn_state.pu_h;
+  out[10] = ctx->nn_state.pu_w;
+  out[11] = ctx->nn_state.written;
+}
+void orc_nn_set_state(orc_ctx* ctx, const uint32_t in[12]) {
+  memcpy(ctx->nn_state.slot, in, 8 * sizeof(uint32_t));
+  ctx->nn_state.c = in[8];
+  ctx->nn_state.pu_h = in[9];
+  ctx->nn_state.pu_w = in[10];
+  ctx->nn_state.written = in[11];
+}
 
 static int valid_size(int w, int h) {
   if (w < 4 || h < 4 || w > 64 || h > 64 || (w & 3) || (h & 3)) return 0;

@@ -90,6 +90,8 @@ void orc_set_motion_lambda(orc_ctx* ctx, int id, double mlambda);
 void orc_set_keys(orc_ctx* ctx, const int16_t* keys, size_t n);
 void orc_load_nn(orc_ctx* ctx, const float* params);
 void orc_nn_reset(orc_ctx* ctx);
+void orc_nn_get_state(const orc_ctx* ctx, uint32_t out[12]);
+void orc_nn_set_state(orc_ctx* ctx, const uint32_t in[12]);
 
 /* Whole path for n jobs in order (the restated xMotionEstimation sub-pel part). Returns
  * 0 or a negative FME_E_* code. */

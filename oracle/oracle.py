@@ -58,6 +58,8 @@ class Oracle:
         lib.orc_set_keys.argtypes = [_P, _P, C.c_size_t]
         lib.orc_load_nn.argtypes = [_P, _P]
         lib.orc_nn_reset.argtypes = [_P]
+        lib.orc_nn_get_state.argtypes = [_P, _P]
+        lib.orc_nn_set_state.argtypes = [_P, _P]
         lib.orc_refine.restype = C.c_int
         lib.orc_refine.argtypes = [_P, _P, _P, C.c_int]
         self._buf = C.create_string_buffer(lib.orc_ctx_size())
@@ -85,6 +87,15 @@ class Oracle:
 
     def nn_reset(self):
         self.lib.orc_nn_reset(self.ctx)
+
+    def nn_get_state(self):
+        out = np.zeros(12, np.uint32)
+        self.lib.orc_nn_get_state(self.ctx, _ptr(out))
+        return out
+
+    def nn_set_state(self, st):
+        st = np.ascontiguousarray(st, dtype=np.uint32)
+        self.lib.orc_nn_set_state(self.ctx, _ptr(st))
 
     def refine(self, jobs):
         from nnfme.abi import RESULT_DTYPE

@@ -1,0 +1,50 @@
+"""The C-ABI library loads and exports every entry point include/fme.h declares; the numpy
+struct mirrors match the header.  No compute calls here (no GPU in this container)."""
+import os
+import re
+
+import numpy as np
+import pytest
+
+from conftest import ROOT, gpu_available
+from nnfme import abi, runtime
+
+
+def header_functions():
+    txt = open(os.path.join(ROOT, "include", "fme.h")).read()
+    txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+    return sorted(set(re.findall(r"\b(fme_[a-z_]+)\s*\(", txt)))
+
+
+def test_library_exports_header():
+    lib = runtime.load_library()
+    names = header_functions()
+    assert len(names) == 19
+    assert set(names) == set(runtime.ABI_SYMBOLS)
+    for n in names:
+        assert hasattr(lib, n), n
+    assert lib.fme_abi_version() == 1
+
+
+def test_struct_layouts():
+    assert abi.JOB_DTYPE.itemsize == 32
+    assert abi.RESULT_DTYPE.itemsize == 64
+    assert abi.JOB_DTYPE.fields["key_offset"][1] == 28
+    assert abi.RESULT_DTYPE.fields["frac_cost"][1] == 12
+    assert abi.RESULT_DTYPE.fields["emi"][1] == 28
+    assert abi.RESULT_DTYPE.fields["status"][1] == 62
+
+
+@pytest.mark.skipif(gpu_available(), reason="checks the no-device error path")
+def test_create_without_device_fails_cleanly():
+    with pytest.raises(runtime.FmeError) as e:
+        runtime.FmeContext()
+    assert e.value.code in (-1, -2)
+
+
+def test_null_arguments_rejected():
+    lib = runtime.load_library()
+    assert lib.fme_create(0, None, None) == -1
+    assert b"null" in lib.fme_last_error()
+    assert lib.fme_refine(None, None, None, 1, None) == -1
+    assert lib.fme_destroy(None) == 0

@@ -1,0 +1,112 @@
+"""CPU tests of the oracle: pinned against the golden vectors (made by oracle/_ref, the
+reference's own compiled primitives) and, where the reference is present, re-checked live."""
+import os
+
+import numpy as np
+import pytest
+
+from conftest import golden_cases, load_golden
+from nnfme import synth, weights
+from nnfme.abi import PARITY_FIELDS, compare_results
+from oracle import REF_SO, Oracle, Reference
+
+HAVE_REF = os.path.exists(REF_SO)
+
+
+def _engine(cls, g):
+    hadme, fen, nn_mode, qp = (int(v) for v in g["config"])
+    kw = dict(use_hadamard=hadme, nn_mode=nn_mode, fast_inter_mode=fen)
+    if cls is Oracle:
+        kw["qp"] = qp
+    e = cls(**kw)
+    for i, p in enumerate(g["pictures"]):
+        e.set_picture(i, p)
+    for i, lam in enumerate(g["lambdas"]):
+        e.set_lambda(i, float(lam))
+    e.set_keys(g["keys"] if g["keys"].size else np.zeros(1, np.int16))
+    e.load_nn(weights.load_weights(qp))
+    return e
+
+
+@pytest.mark.parametrize("case", golden_cases())
+def test_oracle_matches_golden(case):
+    g = load_golden(case)
+    res = _engine(Oracle, g).refine(g["jobs"])
+    bad, first, counts = compare_results(res, g["results"])
+    assert bad == 0, f"{case}: {bad} mismatching jobs, first {first}: {counts}"
+
+
+@pytest.mark.skipif(not HAVE_REF, reason="oracle/_ref not built (needs /root/reference)")
+@pytest.mark.parametrize("case", golden_cases())
+def test_reference_harness_matches_golden(case):
+    g = load_golden(case)
+    res = _engine(Reference, g).refine(g["jobs"])
+    bad, first, counts = compare_results(res, g["results"])
+    assert bad == 0, f"{case}: {bad} mismatching jobs, first {first}: {counts}"
+
+
+def test_golden_covers_every_pu_shape_and_flag():
+    seen, flags = set(), 0
+    for case in golden_cases():
+        j = load_golden(case)["jobs"]
+        seen |= set(zip(j["w"].tolist(), j["h"].tolist()))
+        flags |= int(np.bitwise_or.reduce(j["flags"]))
+    assert set(synth.ALL_PU_SIZES) <= seen
+    assert flags == 0x7
+
+
+def test_exp_golomb_bits():
+    o = Oracle()
+    # TComRdCost::xGetExpGolombNumberOfBits: 0 -> 1, 1 -> 3, -1 -> 3, 2 -> 5 ...
+    expect = {0: 1, 1: 3, -1: 3, 2: 5, -2: 5, 3: 5, -3: 5, 4: 7, 255: 17, -255: 17, -256: 19, 256: 19}
+    for v, b in expect.items():
+        assert o.lib.orc_eg_bits(v) == b, v
+
+
+def test_cost_is_truncated_double():
+    o = Oracle()
+    ml = 65536.0 * np.sqrt(20.196)
+    for b in range(0, 80):
+        assert o.lib.orc_cost(ml, b) == int((ml * b) / 65536.0)
+
+
+@pytest.mark.skipif(not HAVE_REF, reason="oracle/_ref not built")
+def test_prediction_matches_reference_filters():
+    rng = np.random.default_rng(3)
+    pic = synth.synth_luma(96, 64, 0, seed=21)
+    o, r = Oracle(), Reference()
+    r.set_picture(0, pic)
+    for _ in range(300):
+        w, h = synth.ALL_PU_SIZES[int(rng.integers(len(synth.ALL_PU_SIZES)))]
+        x, y = int(rng.integers(0, 96 - w + 1)), int(rng.integers(0, 64 - h + 1))
+        qx, qy = int(rng.integers(-200, 200)), int(rng.integers(-200, 200))
+        np.testing.assert_array_equal(o.pred_block(pic, x, y, w, h, qx, qy), r.pred_block(0, x, y, w, h, qx, qy))
+
+
+@pytest.mark.skipif(not HAVE_REF, reason="oracle/_ref not built")
+def test_satd_matches_reference():
+    rng = np.random.default_rng(4)
+    o, r = Oracle(), Reference()
+    for w, h in synth.ALL_PU_SIZES:
+        a = rng.integers(-255, 511, (h, w)).astype(np.int16)
+        b = rng.integers(0, 256, (h, w)).astype(np.int16)
+        assert o.lib.orc_satd(a.ctypes.data, w, b.ctypes.data, w, w, h) == r.satd(a, b, True)
+        assert o.lib.orc_sad(a.ctypes.data, w, b.ctypes.data, w, w, h, 0) == r.satd(a, b, False)
+
+
+@pytest.mark.skipif(not HAVE_REF, reason="oracle/_ref not built")
+@pytest.mark.parametrize("qp", [22, 27, 32, 37])
+def test_nn_class_matches_harness(qp):
+    rng = np.random.default_rng(qp)
+    o, r = Oracle(qp=qp), Reference()
+    wts = weights.load_weights(qp)
+    r.load_nn(wts)
+    for _ in range(500):
+        e = rng.integers(0, 400000, 8).astype(np.uint32)
+        c = int(rng.integers(0, 400000))
+        h, w = synth.ALL_PU_SIZES[int(rng.integers(len(synth.ALL_PU_SIZES)))][::-1]
+        assert o.nn_class(wts, e, c, h, w)[0] == r.nn_class(e, c, h, w)
+
+
+def test_parity_fields_complete():
+    assert {"mv_x", "mv_y", "cost", "frac_cost", "nn_class"} <= set(PARITY_FIELDS)
