@@ -4,10 +4,7 @@
 //   classify   per job: PU-shape class, EMI push count; per block: class histogram and the
 //              max of the NN "last writer" indices (first pass of a prefix-max scan).
 //   scatter    jobs grouped by class (block-aggregated atomics), giving the search tiles.
-//   search     one workgroup = one tile of P same-shape PUs: reference window + key in LDS,
-//              EMI square step (TEncSearch.cpp:5037-5050), 14-bit horizontal planes,
-//              9 half-pel then 9 quarter-pel SATD candidates (xPatternSearchFracDIF,
-//              TEncSearch.cpp:5232-5269), first strict minimum of SATD + MV cost.
+//   search     EMI square step + FracDIF per tile of same-shape PUs (fme_search.hip).
 //   nn_tail    prefix-max over jobs resolves which earlier job last wrote each array_e slot
 //              (the reference's stale global state, TEncSearch.cpp:55-57, 198-201), then
 //              NN_pred() (85-204) and the xMotionEstimation tail (4586-4597), one lane per job.
@@ -62,418 +59,6 @@ __device__ __forceinline__ int refine_dx(int half, int i) {
 }
 __device__ __forceinline__ int refine_dy(int half, int i) {
   return decode_offset(((half ? 0x605au : 0x650au) >> (2 * (8 - i))) & 3u);
-}
-
-// ---------------------------------------------------------------------------------------
-// Hadamard SATD on a tile held in registers (xCalcHADs8x8 / xCalcHADs4x4,
-// TComRdCost.cpp:1234-1425).  Any exact WHT factorisation gives the same |coefficients|.
-// ---------------------------------------------------------------------------------------
-template <int STEP>
-__device__ __forceinline__ void wht8(int* v) {
-#pragma unroll
-  for (int len = 4; len >= 1; len >>= 1)
-#pragma unroll
-    for (int i = 0; i < 8; i += 2 * len)
-#pragma unroll
-      for (int j = i; j < i + len; j++) {
-        const int a = v[j * STEP], b = v[(j + len) * STEP];
-        v[j * STEP] = a + b;
-        v[(j + len) * STEP] = a - b;
-      }
-}
-
-template <int STEP>
-__device__ __forceinline__ void wht4(int* v) {
-  const int a0 = v[0] + v[3 * STEP], a3 = v[0] - v[3 * STEP];
-  const int a1 = v[STEP] + v[2 * STEP], a2 = v[STEP] - v[2 * STEP];
-  v[0] = a0 + a1;
-  v[2 * STEP] = a0 - a1;
-  v[STEP] = a2 + a3;
-  v[3 * STEP] = a3 - a2;
-}
-
-template <int T>
-__device__ __forceinline__ uint32_t satd_tile(int* d) {
-  uint32_t s = 0;
-  if constexpr (T == 8) {
-#pragma unroll
-    for (int r = 0; r < 8; r++) wht8<1>(d + r * 8);
-#pragma unroll
-    for (int c = 0; c < 8; c++) wht8<8>(d + c);
-#pragma unroll
-    for (int i = 0; i < 64; i++) s += (uint32_t)abs(d[i]);
-    return (s + 2) >> 2;
-  } else {
-#pragma unroll
-    for (int r = 0; r < 4; r++) wht4<1>(d + r * 4);
-#pragma unroll
-    for (int c = 0; c < 4; c++) wht4<4>(d + c);
-#pragma unroll
-    for (int i = 0; i < 16; i++) s += (uint32_t)abs(d[i]);
-    return (s + 1) >> 1;
-  }
-}
-
-template <int T>
-__device__ __forceinline__ uint32_t sad_tile(const int* d) {
-  uint32_t s = 0;
-#pragma unroll
-  for (int i = 0; i < T * T; i++) s += (uint32_t)abs(d[i]);
-  return s;
-}
-
-// ---------------------------------------------------------------------------------------
-// Per-class geometry of a search tile.
-//   window  rows -5..H+4, cols -5..W+4 around the TZ integer MV (EMI +-1, 8-tap -4..+4)
-//   planes  fx = 1,2,3 first-stage outputs, rows -4..H+3, cols -1..W-1 around mv_int'
-// ---------------------------------------------------------------------------------------
-struct PuInfo {
-  int32_t job;
-  int32_t flags;
-  int32_t x, y;
-  int32_t ref;
-  int32_t wx0, wy0;       // absolute window origin
-  int32_t mvx, mvy;       // integer MV (after EMI)
-  int32_t ex, ey;         // mv_int' - mv_tz
-  int32_t mvp_x, mvp_y;
-  int32_t lt_x, lt_y, rb_x, rb_y;
-  int32_t had;
-  int32_t hx, hy;
-  int32_t key_off;
-  int32_t pad0;
-  double ml;
-  uint32_t acc[9];
-  uint32_t pad1[3];
-};
-static_assert(sizeof(PuInfo) % 16 == 0, "PuInfo must keep 16-byte alignment");
-
-template <int W, int H>
-struct Geo {
-  static constexpr int WS = W + 10;
-  static constexpr int WR = H + 10;
-  static constexpr int PS = W + 1;
-  static constexpr int PR = H + 8;
-  static constexpr int WIN = WR * WS;
-  static constexpr int KEY = W * H;
-  static constexpr int PLANE = PR * PS;
-  static constexpr int ELEMS = WIN + KEY + 3 * PLANE;
-  static constexpr int BYTES = ((ELEMS * 2) + 15) & ~15;
-  static constexpr int T = ((W % 8) == 0 && (H % 8) == 0) ? 8 : 4;
-  static constexpr int TILES = (W / T) * (H / T);
-  static constexpr int BUDGET = 40 * 1024;
-  static constexpr int P0 = BUDGET / (BYTES + (int)sizeof(PuInfo));
-  static constexpr int P = P0 < 1 ? 1 : (P0 > 32 ? 32 : P0);
-  static constexpr size_t LDS = (size_t)P * (BYTES + sizeof(PuInfo));
-  static constexpr int NCH = (PS + 7) / 8;   // 8-column chunks of a plane row
-};
-
-template <int W, int H>
-struct TileView {
-  using G = Geo<W, H>;
-  PuInfo* info;
-  int16_t* base;
-  __device__ TileView(char* lds) {
-    info = reinterpret_cast<PuInfo*>(lds);
-    base = reinterpret_cast<int16_t*>(lds + G::P * sizeof(PuInfo));
-  }
-  __device__ int16_t* win(int p) const { return base + (size_t)p * (G::BYTES / 2); }
-  __device__ int16_t* key(int p) const { return win(p) + G::WIN; }
-  __device__ int16_t* planes(int p) const { return key(p) + G::KEY; }
-};
-
-// First-stage (horizontal) value at plane coordinates (pr, pc) for fraction fx:
-// fx == 0 is filterCopy's isFirst branch (x << 6) - 8192 (TComInterpolationFilter.cpp:111-124).
-template <int W, int H>
-__device__ __forceinline__ int stage1(const int16_t* win, const int16_t* planes, int ex, int ey,
-                                      int fx, int pr, int pc) {
-  using G = Geo<W, H>;
-  if (fx == 0) return ((int)win[(1 + ey + pr) * G::WS + 4 + ex + pc] << 6) - 8192;
-  return planes[(fx - 1) * G::PLANE + pr * G::PS + pc];
-}
-
-// Distortion of one T x T tile of the PU for the candidate at quarter-pel (qx, qy) relative to
-// mv_int' (|qx|,|qy| <= 3).  Prediction = second stage of the HEVC luma filter
-// (filterVer<8,true,false,true> / filterCopy !isFirst), computed column by column with the
-// first-stage column held in registers.
-template <int W, int H>
-__device__ uint32_t cand_tile_dist(const int16_t* win, const int16_t* planes, const int16_t* key,
-                                   int ex, int ey, int qx, int qy, int tile, int had) {
-  using G = Geo<W, H>;
-  constexpr int T = G::T;
-  constexpr int TX = W / T;
-  const int ty = tile / TX, tx = tile % TX;
-  const int ix = qx >> 2, fx = qx & 3, iy = qy >> 2, fy = qy & 3;
-  int d[T * T];
-  int cf[8];
-  luma_taps(fy, cf);
-#pragma unroll
-  for (int c = 0; c < T; c++) {
-    const int col = tx * T + c;
-    const int pc = col + ix + 1;
-    if (fy == 0) {
-#pragma unroll
-      for (int r = 0; r < T; r++) {
-        const int row = ty * T + r;
-        const int t = stage1<W, H>(win, planes, ex, ey, fx, row + iy + 4, pc);
-        const int p = clamp_i((t + 8192 + 32) >> 6, 0, 255);
-        d[r * T + c] = (int)key[row * W + col] - p;
-      }
-    } else {
-      int v[T + 7];
-#pragma unroll
-      for (int m = 0; m < T + 7; m++) v[m] = stage1<W, H>(win, planes, ex, ey, fx, ty * T + iy + 1 + m, pc);
-#pragma unroll
-      for (int r = 0; r < T; r++) {
-        int s = 0;
-#pragma unroll
-        for (int k = 0; k < 8; k++) s += cf[k] * v[r + k];
-        const int p = clamp_i((s + 2048 + (8192 << 6)) >> 12, 0, 255);
-        d[r * T + c] = (int)key[(ty * T + r) * W + col] - p;
-      }
-    }
-  }
-  return had ? satd_tile<T>(d) : sad_tile<T>(d);
-}
-
-// One tile: P PUs of shape W x H.
-template <int W, int H>
-__device__ void search_tile(const BatchArgs& a, const int32_t* perm, int first, int count, char* lds) {
-  using G = Geo<W, H>;
-  TileView<W, H> v(lds);
-  const int tid = threadIdx.x;
-
-  // ---- descriptors --------------------------------------------------------------------
-  if (tid < G::P) {
-    PuInfo& in = v.info[tid];
-    if (tid < count) {
-      const int jid = perm[first + tid];
-      const fme_job j = a.jobs[jid];
-      in.job = jid;
-      in.flags = j.flags;
-      in.x = j.x;
-      in.y = j.y;
-      in.ref = j.ref_id;
-      in.wx0 = (int)j.x + j.mv_x - 5;
-      in.wy0 = (int)j.y + j.mv_y - 5;
-      in.mvx = j.mv_x;
-      in.mvy = j.mv_y;
-      in.ex = 0;
-      in.ey = 0;
-      in.mvp_x = j.mvp_x;
-      in.mvp_y = j.mvp_y;
-      in.lt_x = j.lt_x;
-      in.lt_y = j.lt_y;
-      in.rb_x = j.rb_x;
-      in.rb_y = j.rb_y;
-      in.had = (a.use_hadamard && !(j.flags & FME_JOB_LOSSLESS)) ? 1 : 0;
-      in.ml = a.mlambda[j.lambda_id];
-      in.key_off = j.key_offset;
-      in.hx = in.hy = 0;
-      // org picture id travels in key_off's place when the key is the picture itself
-      in.pad0 = j.org_id;
-    } else {
-      in.job = -1;
-      in.flags = 0;
-    }
-#pragma unroll
-    for (int k = 0; k < 9; k++) in.acc[k] = 0;
-  }
-  __syncthreads();
-
-  // ---- stage reference window and key into LDS ---------------------------------------
-  for (int e = tid; e < count * G::WIN; e += kBlock) {
-    const int p = e / G::WIN, rem = e - p * G::WIN;
-    const int r = rem / G::WS, c = rem - r * G::WS;
-    const PuInfo& in = v.info[p];
-    const PicDesc pd = a.pics[in.ref];
-    const int ax = clamp_i(in.wx0 + c, 0, pd.width - 1);
-    const int ay = clamp_i(in.wy0 + r, 0, pd.height - 1);
-    v.win(p)[rem] = pd.luma[(size_t)ay * pd.stride + ax];
-  }
-  for (int e = tid; e < count * G::KEY; e += kBlock) {
-    const int p = e / G::KEY, rem = e - p * G::KEY;
-    const int r = rem / W, c = rem - r * W;
-    const PuInfo& in = v.info[p];
-    int16_t val;
-    if (in.key_off >= 0) {
-      val = a.keys[(size_t)in.key_off + rem];
-    } else {
-      const PicDesc pd = a.pics[in.pad0];
-      val = pd.luma[(size_t)(in.y + r) * pd.stride + in.x + c];
-    }
-    v.key(p)[rem] = val;
-  }
-  __syncthreads();
-
-  // ---- EMI: integer distortion of the centre and its 8 neighbours ---------------------
-  // Metric of the modified setDistParam (TComRdCost.cpp:200-230): SSE for W in
-  // {4,8,16,32,64}; SAD for 12/24/48, even rows only when FEN in {1,3} and H > 8.
-  constexpr bool kSad = (W == 12 || W == 24 || W == 48);
-  const int sub = (kSad && (a.fen == 1 || a.fen == 3) && H > 8) ? 1 : 0;
-  for (int e = tid; e < count * 9 * H; e += kBlock) {
-    const int p = e / (9 * H), rem = e - p * 9 * H;
-    const int pos = rem / H, r = rem - pos * H;
-    const PuInfo& in = v.info[p];
-    if (!(in.flags & FME_JOB_EMI)) continue;
-    if (sub && (r & 1)) continue;
-    const int dx = pos == 0 ? 0 : ((pos == 1 || pos == 4 || pos == 6) ? -1 : ((pos == 2 || pos == 7) ? 0 : 1));
-    const int dy = pos == 0 ? 0 : (pos <= 3 ? -1 : (pos <= 5 ? 0 : 1));
-    const int16_t* kr = v.key(p) + r * W;
-    const int16_t* wr = v.win(p) + (5 + dy + r) * G::WS + 5 + dx;
-    uint32_t s = 0;
-#pragma unroll 8
-    for (int c = 0; c < W; c++) {
-      const int d = (int)kr[c] - (int)wr[c];
-      s += kSad ? (uint32_t)abs(d) : (uint32_t)(d * d);
-    }
-    atomicAdd(&v.info[p].acc[pos], s);
-  }
-  __syncthreads();
-
-  // EMI square-step decision (xTZ8PointSquareSearch + xTZSearchHelp, TEncSearch.cpp:1324-1377,
-  // 1155-1188): push every visited distortion, update the best on d + cost < bestSad.
-  if (tid < count) {
-    PuInfo& in = v.info[tid];
-    fme_result* r = a.res + in.job;
-    uint32_t emi[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    int n_emi = 0;
-    uint32_t cval = 0;
-    if (in.flags & FME_JOB_EMI) {
-      uint32_t acc[9];
-#pragma unroll
-      for (int k = 0; k < 9; k++) acc[k] = in.acc[k] << sub;
-      const int sx = in.mvx, sy = in.mvy;
-      uint32_t best = acc[0] + mv_cost(in.ml, mv_bits(sx, sy, 2, in.mvp_x, in.mvp_y));
-      int bx = sx, by = sy;
-      const bool top = sy - 1 >= in.lt_y, bot = sy + 1 <= in.rb_y;
-      const bool left = sx - 1 >= in.lt_x, right = sx + 1 <= in.rb_x;
-      // pos: 1 TL, 2 T, 3 TR, 4 L, 5 R, 6 BL, 7 B, 8 BR
-#pragma unroll
-      for (int pos = 1; pos <= 8; pos++) {
-        const int dx = (pos == 1 || pos == 4 || pos == 6) ? -1 : ((pos == 2 || pos == 7) ? 0 : 1);
-        const int dy = pos <= 3 ? -1 : (pos <= 5 ? 0 : 1);
-        const bool ok = (dy == -1 ? top : (dy == 1 ? bot : true)) &&
-                        (dx == -1 ? left : (dx == 1 ? right : true));
-        if (!ok) continue;
-        uint32_t d = acc[pos];
-        emi[n_emi++] = d;
-        if (d < best) {
-          d += mv_cost(in.ml, mv_bits(sx + dx, sy + dy, 2, in.mvp_x, in.mvp_y));
-          if (d < best) {
-            best = d;
-            bx = sx + dx;
-            by = sy + dy;
-          }
-        }
-      }
-      cval = best - mv_cost(in.ml, mv_bits(bx, by, 2, in.mvp_x, in.mvp_y));
-      in.ex = bx - sx;
-      in.ey = by - sy;
-      in.mvx = bx;
-      in.mvy = by;
-    }
-#pragma unroll
-    for (int k = 0; k < 8; k++) r->emi[k] = emi[k];
-    r->n_emi = (uint8_t)n_emi;
-    r->c = cval;
-    r->mv_int_x = (int16_t)in.mvx;
-    r->mv_int_y = (int16_t)in.mvy;
-#pragma unroll
-    for (int k = 0; k < 9; k++) in.acc[k] = 0;
-  }
-  __syncthreads();
-
-  // ---- first-stage planes fx = 1,2,3 around mv_int' ----------------------------------
-  // filter<8,false,true,false>: sum - 8192, stored as int16 (TComInterpolationFilter.cpp:196-252).
-  for (int e = tid; e < count * G::PR * G::NCH; e += kBlock) {
-    const int p = e / (G::PR * G::NCH), rem = e - p * G::PR * G::NCH;
-    const int pr = rem / G::NCH, ch = rem - pr * G::NCH;
-    const PuInfo& in = v.info[p];
-    const int16_t* wrow = v.win(p) + (1 + in.ey + pr) * G::WS;
-    const int c0 = 1 + in.ex + ch * 8;
-    int w15[15];
-#pragma unroll
-    for (int m = 0; m < 15; m++) w15[m] = wrow[min(c0 + m, G::WS - 1)];
-    int16_t* pl = v.planes(p) + pr * G::PS + ch * 8;
-#pragma unroll
-    for (int f = 1; f <= 3; f++) {
-      int cf[8];
-      luma_taps(f, cf);
-#pragma unroll
-      for (int j = 0; j < 8; j++) {
-        if (ch * 8 + j < G::PS) {
-          int s = 0;
-#pragma unroll
-          for (int k = 0; k < 8; k++) s += cf[k] * w15[j + k];
-          pl[(f - 1) * G::PLANE + j] = (int16_t)(s - 8192);
-        }
-      }
-    }
-  }
-  __syncthreads();
-
-  // ---- half-pel stage: 9 candidates at 2*H9[i] (cost scale 1) --------------------------
-  const int items = count * G::TILES;
-  for (int e = tid; e < 9 * items; e += kBlock) {
-    const int k = e / items, rem = e - k * items;
-    const int p = rem / G::TILES, tile = rem - p * G::TILES;
-    const PuInfo& in = v.info[p];
-    const uint32_t dd = cand_tile_dist<W, H>(v.win(p), v.planes(p), v.key(p), in.ex, in.ey,
-                                             2 * refine_dx(1, k), 2 * refine_dy(1, k), tile, in.had);
-    atomicAdd(&v.info[p].acc[k], dd);
-  }
-  __syncthreads();
-  if (tid < count) {
-    PuInfo& in = v.info[tid];
-    uint32_t best = 0xFFFFFFFFu;
-    int bi = 0;
-#pragma unroll
-    for (int k = 0; k < 9; k++) {
-      const int hx = 2 * in.mvx + refine_dx(1, k), hy = 2 * in.mvy + refine_dy(1, k);
-      const uint32_t d = in.acc[k] + mv_cost(in.ml, mv_bits(hx, hy, 1, in.mvp_x, in.mvp_y));
-      if (d < best) {
-        best = d;
-        bi = k;
-      }
-      in.acc[k] = 0;
-    }
-    in.hx = refine_dx(1, bi);
-    in.hy = refine_dy(1, bi);
-  }
-  __syncthreads();
-
-  // ---- quarter-pel stage: 9 candidates at 2*half + Q9[i] (cost scale 0) --------------
-  for (int e = tid; e < 9 * items; e += kBlock) {
-    const int k = e / items, rem = e - k * items;
-    const int p = rem / G::TILES, tile = rem - p * G::TILES;
-    const PuInfo& in = v.info[p];
-    const uint32_t dd = cand_tile_dist<W, H>(v.win(p), v.planes(p), v.key(p), in.ex, in.ey,
-                                             2 * in.hx + refine_dx(0, k), 2 * in.hy + refine_dy(0, k),
-                                             tile, in.had);
-    atomicAdd(&v.info[p].acc[k], dd);
-  }
-  __syncthreads();
-  if (tid < count) {
-    PuInfo& in = v.info[tid];
-    uint32_t best = 0xFFFFFFFFu;
-    int bi = 0;
-#pragma unroll
-    for (int k = 0; k < 9; k++) {
-      const int qx = 4 * in.mvx + 2 * in.hx + refine_dx(0, k);
-      const int qy = 4 * in.mvy + 2 * in.hy + refine_dy(0, k);
-      const uint32_t d = in.acc[k] + mv_cost(in.ml, mv_bits(qx, qy, 0, in.mvp_x, in.mvp_y));
-      if (d < best) {
-        best = d;
-        bi = k;
-      }
-    }
-    fme_result* r = a.res + in.job;
-    r->half_x = (int8_t)in.hx;
-    r->half_y = (int8_t)in.hy;
-    r->qtr_x = (int8_t)refine_dx(0, bi);
-    r->qtr_y = (int8_t)refine_dy(0, bi);
-    r->frac_cost = best;
-  }
 }
 
 // ---------------------------------------------------------------------------------------
@@ -567,31 +152,6 @@ __global__ __launch_bounds__(kBlock) void k_scatter(BatchArgs a, WorkBufs w, Sch
   for (int q = 0; q < kJobsPerScanBlock / kBlock; q++) {
     const int i = base + q * kBlock + tid;
     if (cls[q] < kNumClasses) w.perm[sc.class_off[cls[q]] + basep[cls[q]] + rank[q]] = i;
-  }
-}
-
-__global__ __launch_bounds__(kBlock) void k_search(BatchArgs a, WorkBufs w, Schedule sc) {
-  extern __shared__ __attribute__((aligned(16))) char lds[];
-  const int b = blockIdx.x;
-  int c = 0;
-  while (c < kNumClasses - 1 && b >= sc.tile_prefix[c + 1]) c++;
-  const int t = b - sc.tile_prefix[c];
-  switch (c) {
-#define FME_CASE(ID, W_, H_)                                                             \
-  case ID: {                                                                             \
-    constexpr int P = Geo<W_, H_>::P;                                                    \
-    const int first = sc.class_off[ID] + t * P;                                          \
-    const int count = min(P, sc.class_cnt[ID] - t * P);                                  \
-    search_tile<W_, H_>(a, w.perm, first, count, lds);                                   \
-  } break;
-    FME_CASE(0, 4, 8) FME_CASE(1, 8, 4) FME_CASE(2, 8, 8) FME_CASE(3, 4, 16)
-    FME_CASE(4, 16, 4) FME_CASE(5, 8, 16) FME_CASE(6, 16, 8) FME_CASE(7, 12, 16)
-    FME_CASE(8, 16, 12) FME_CASE(9, 16, 16) FME_CASE(10, 8, 32) FME_CASE(11, 32, 8)
-    FME_CASE(12, 16, 32) FME_CASE(13, 32, 16) FME_CASE(14, 24, 32) FME_CASE(15, 32, 24)
-    FME_CASE(16, 32, 32) FME_CASE(17, 16, 64) FME_CASE(18, 64, 16) FME_CASE(19, 32, 64)
-    FME_CASE(20, 64, 32) FME_CASE(21, 48, 64) FME_CASE(22, 64, 48) FME_CASE(23, 64, 64)
-#undef FME_CASE
-    default: break;
   }
 }
 
@@ -830,37 +390,6 @@ hipError_t launch_nn_single(const float* nnp, const uint32_t* in, int32_t* out, 
 // ---------------------------------------------------------------------------------------
 // host launch helpers
 // ---------------------------------------------------------------------------------------
-template <int W, int H>
-static int p_of() { return Geo<W, H>::P; }
-template <int W, int H>
-static size_t lds_of() { return Geo<W, H>::LDS; }
-
-int pus_per_tile(int cls) {
-  switch (cls) {
-#define FME_P(ID, W_, H_) case ID: return p_of<W_, H_>();
-    FME_P(0, 4, 8) FME_P(1, 8, 4) FME_P(2, 8, 8) FME_P(3, 4, 16) FME_P(4, 16, 4) FME_P(5, 8, 16)
-    FME_P(6, 16, 8) FME_P(7, 12, 16) FME_P(8, 16, 12) FME_P(9, 16, 16) FME_P(10, 8, 32)
-    FME_P(11, 32, 8) FME_P(12, 16, 32) FME_P(13, 32, 16) FME_P(14, 24, 32) FME_P(15, 32, 24)
-    FME_P(16, 32, 32) FME_P(17, 16, 64) FME_P(18, 64, 16) FME_P(19, 32, 64) FME_P(20, 64, 32)
-    FME_P(21, 48, 64) FME_P(22, 64, 48) FME_P(23, 64, 64)
-#undef FME_P
-    default: return 1;
-  }
-}
-
-size_t lds_bytes_for_class(int cls) {
-  switch (cls) {
-#define FME_L(ID, W_, H_) case ID: return lds_of<W_, H_>();
-    FME_L(0, 4, 8) FME_L(1, 8, 4) FME_L(2, 8, 8) FME_L(3, 4, 16) FME_L(4, 16, 4) FME_L(5, 8, 16)
-    FME_L(6, 16, 8) FME_L(7, 12, 16) FME_L(8, 16, 12) FME_L(9, 16, 16) FME_L(10, 8, 32)
-    FME_L(11, 32, 8) FME_L(12, 16, 32) FME_L(13, 32, 16) FME_L(14, 24, 32) FME_L(15, 32, 24)
-    FME_L(16, 32, 32) FME_L(17, 16, 64) FME_L(18, 64, 16) FME_L(19, 32, 64) FME_L(20, 64, 32)
-    FME_L(21, 48, 64) FME_L(22, 64, 48) FME_L(23, 64, 64)
-#undef FME_L
-    default: return 0;
-  }
-}
-
 static int nblocks(int n) { return (n + kJobsPerScanBlock - 1) / kJobsPerScanBlock; }
 
 hipError_t launch_classify(const BatchArgs& a, const WorkBufs& w, hipStream_t s) {
@@ -870,14 +399,6 @@ hipError_t launch_classify(const BatchArgs& a, const WorkBufs& w, hipStream_t s)
 
 hipError_t launch_scatter(const BatchArgs& a, const WorkBufs& w, const Schedule& sc, hipStream_t s) {
   hipLaunchKernelGGL(k_scatter, dim3(nblocks(a.n)), dim3(kBlock), 0, s, a, w, sc);
-  return hipGetLastError();
-}
-
-hipError_t launch_search(const BatchArgs& a, const WorkBufs& w, const Schedule& sc, size_t lds,
-                         hipStream_t s) {
-  const int tiles = sc.tile_prefix[kNumClasses];
-  if (tiles == 0) return hipSuccess;
-  hipLaunchKernelGGL(k_search, dim3(tiles), dim3(kBlock), lds, s, a, w, sc);
   return hipGetLastError();
 }
 

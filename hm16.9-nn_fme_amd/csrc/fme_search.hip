@@ -1,0 +1,824 @@
+// fme_search.hip — the EMI + FracDIF search kernels (gfx950).
+//
+// One workgroup refines a tile of P same-shape PUs end to end in LDS:
+//   1. stage    reference window (rows -5..H+4, cols -5..W+4 around the TZ MV) as int8
+//               (sample - 128) twice: row-major (horizontal taps) and column-major
+//               (vertical taps of integer columns); the key block column-major int16.
+//   2. EMI      SSE / (FEN-subsampled) SAD of the 9 integer positions around the TZ best,
+//               then the square-step decision (TEncSearch.cpp:1324-1377, 1155-1188, 5043-5050).
+//   3. planes   first-stage (horizontal) outputs for fx = 1,2,3 around mv_int' — the
+//               m_filteredBlockTmp planes of xExtDIFUpSamplingH/Q — column-major int16.
+//               With s' = s - 128 and sum(taps) = 64, sum(c*s) - 8192 == sum(c*s') exactly,
+//               so each value is two v_dot4_i32_i8.
+//   4. half     the shared half-pel planes (m_filteredBlock [2][2], [2][0], [0][2],
+//               TEncSearch.cpp:6331-6365) as 8-bit predictions, then 9 SATD candidates
+//               (xPatternRefinement, 1591-1645), argmin at cost scale 1.
+//   5. quarter  the 8 remaining quarter-pel candidates computed per tile in registers
+//               (v_dot2_i32_i16 on packed row pairs); candidate 0 reuses the half-stage
+//               distortion of the same position; argmin at cost scale 0.
+// SATD runs on packed int16 (|coefficients| <= 16320 before the last butterfly); the last
+// butterfly is folded with |a+b| + |a-b| = 2 max(|a|,|b|).
+#include <hip/hip_runtime.h>
+
+#include "fme_device.h"
+
+namespace fme {
+
+typedef short v2s __attribute__((ext_vector_type(2)));
+typedef unsigned short v2u __attribute__((ext_vector_type(2)));
+
+namespace {
+
+// ---- scalar helpers ------------------------------------------------------------------
+__device__ __forceinline__ int clamp_i(int v, int lo, int hi) { return min(max(v, lo), hi); }
+
+__device__ __forceinline__ uint32_t eg_bits(int v) {  // TComRdCost.cpp:172-185
+  const uint32_t t = v <= 0 ? ((uint32_t)(-v) << 1) + 1u : ((uint32_t)v << 1);
+  return 1u + 2u * (31u - (uint32_t)__clz((int)t));
+}
+__device__ __forceinline__ uint32_t mv_bits(int x, int y, int scale, int px, int py) {
+  return eg_bits((x << scale) - px) + eg_bits((y << scale) - py);
+}
+__device__ __forceinline__ uint32_t mv_cost(double ml, uint32_t bits) {  // TComRdCost.h:165
+  return (uint32_t)((ml * (double)bits) / 65536.0);
+}
+
+// Candidate tables of xPatternRefinement (TEncSearch.cpp:212-236), 2-bit codes.
+__device__ __forceinline__ int dec(uint32_t c) { return c == 1 ? -1 : (c == 2 ? 1 : 0); }
+__device__ __forceinline__ int cand_dx(int i) { return dec((0x666u >> (2 * (8 - i))) & 3u); }
+__device__ __forceinline__ int half_dy(int i) { return dec((0x605au >> (2 * (8 - i))) & 3u); }
+__device__ __forceinline__ int qtr_dy(int i) { return dec((0x650au >> (2 * (8 - i))) & 3u); }
+
+// ---- packed arithmetic -----------------------------------------------------------------
+__device__ __forceinline__ uint32_t pk(v2s v) { return __builtin_bit_cast(uint32_t, v); }
+__device__ __forceinline__ v2s up(uint32_t u) { return __builtin_bit_cast(v2s, u); }
+__device__ __forceinline__ uint32_t pk_add(uint32_t a, uint32_t b) { return pk(up(a) + up(b)); }
+__device__ __forceinline__ uint32_t pk_sub(uint32_t a, uint32_t b) { return pk(up(a) - up(b)); }
+__device__ __forceinline__ uint32_t pk_abs(uint32_t a) {
+  const v2s x = up(a);
+  return pk(__builtin_elementwise_max(x, -x));
+}
+__device__ __forceinline__ int dot2(uint32_t a, uint32_t b, int acc) {
+  return __builtin_amdgcn_sdot2(up(a), up(b), acc, false);
+}
+__device__ __forceinline__ uint32_t udot2(uint32_t a, uint32_t b, uint32_t acc) {
+  return __builtin_amdgcn_udot2(__builtin_bit_cast(v2u, a), __builtin_bit_cast(v2u, b), acc, false);
+}
+__device__ __forceinline__ int dot4(uint32_t a, uint32_t b, int acc) {
+  return __builtin_amdgcn_sdot4((int)a, (int)b, acc, false);
+}
+// bytes b0..b3 of `w` -> (b0, b1) and (b2, b3) as packed u16 pairs
+__device__ __forceinline__ uint32_t lo_pair(uint32_t w) { return __builtin_amdgcn_perm(0u, w, 0x0c010c00u); }
+__device__ __forceinline__ uint32_t hi_pair(uint32_t w) { return __builtin_amdgcn_perm(0u, w, 0x0c030c02u); }
+// 4 bytes starting `sh` bytes into (lo, hi)
+__device__ __forceinline__ uint32_t funnel8(uint32_t hi, uint32_t lo, uint32_t sh) {
+  return __builtin_amdgcn_alignbyte(hi, lo, sh);
+}
+__device__ __forceinline__ uint32_t funnel16(uint32_t hi, uint32_t lo) {
+  return __builtin_amdgcn_alignbit(hi, lo, 16u);
+}
+__device__ __forceinline__ uint32_t lds32(const uint8_t* p) { return *reinterpret_cast<const uint32_t*>(p); }
+__device__ __forceinline__ void sts32(uint8_t* p, uint32_t v) { *reinterpret_cast<uint32_t*>(p) = v; }
+
+// Luma taps as packed int8 quads (t0..t3, t4..t7) and int16 pairs (TComInterpolationFilter.cpp:57-63).
+__device__ __forceinline__ uint32_t q8(int a, int b, int c, int d) {
+  return (uint32_t)(a & 255) | ((uint32_t)(b & 255) << 8) | ((uint32_t)(c & 255) << 16) | ((uint32_t)(d & 255) << 24);
+}
+__device__ __forceinline__ uint32_t p16(int a, int b) { return (uint32_t)(a & 0xffff) | ((uint32_t)(b & 0xffff) << 16); }
+__device__ __forceinline__ void taps8(int f, uint32_t& lo, uint32_t& hi) {
+  if (f == 1) { lo = q8(-1, 4, -10, 58); hi = q8(17, -5, 1, 0); }
+  else if (f == 2) { lo = q8(-1, 4, -11, 40); hi = q8(40, -11, 4, -1); }
+  else { lo = q8(0, 1, -5, 17); hi = q8(58, -10, 4, -1); }
+}
+__device__ __forceinline__ void taps16(int f, uint32_t (&c)[4]) {
+  if (f == 1) { c[0] = p16(-1, 4); c[1] = p16(-10, 58); c[2] = p16(17, -5); c[3] = p16(1, 0); }
+  else if (f == 2) { c[0] = p16(-1, 4); c[1] = p16(-11, 40); c[2] = p16(40, -11); c[3] = p16(4, -1); }
+  else { c[0] = p16(0, 1); c[1] = p16(-5, 17); c[2] = p16(58, -10); c[3] = p16(4, -1); }
+}
+
+// Second-stage rounding of filter<8,true,false,true> (shift 12, offset 2048 + (8192 << 6)).
+__device__ __forceinline__ int round2d(int s) { return clamp_i((s + 526336) >> 12, 0, 255); }
+// 1-D from bytes: (sum(c*s) + 32) >> 6 with sum(c*s) = sum(c*s') + 8192.
+__device__ __forceinline__ int round1d_s8(int s) { return clamp_i((s + 8224) >> 6, 0, 255); }
+
+// ---- SATD on packed tiles ------------------------------------------------------------------
+// X[c][j]: column c, rows (2j, 2j+1) packed.  Returns the xCalcHADs value of the tile.
+template <int T>
+__device__ __forceinline__ uint32_t satd_packed(uint32_t (&X)[T][T / 2]) {
+  // horizontal (across columns) butterflies
+#pragma unroll
+  for (int d = T / 2; d >= 1; d >>= 1)
+#pragma unroll
+    for (int c = 0; c < T; c++)
+      if ((c & d) == 0)
+#pragma unroll
+        for (int j = 0; j < T / 2; j++) {
+          const uint32_t a = X[c][j], b = X[c + d][j];
+          X[c][j] = pk_add(a, b);
+          X[c + d][j] = pk_sub(a, b);
+        }
+  // vertical butterflies between row pairs (distances 4 and 2 rows)
+#pragma unroll
+  for (int d = T / 4; d >= 1; d >>= 1)
+#pragma unroll
+    for (int c = 0; c < T; c++)
+#pragma unroll
+      for (int j = 0; j < T / 2; j++)
+        if ((j & d) == 0) {
+          const uint32_t a = X[c][j], b = X[c][j + d];
+          X[c][j] = pk_add(a, b);
+          X[c][j + d] = pk_sub(a, b);
+        }
+  // last butterfly (rows 2j, 2j+1 in one register): |a+b| + |a-b| = 2 max(|a|, |b|)
+  uint32_t s = 0;
+#pragma unroll
+  for (int c = 0; c < T; c += 2)
+#pragma unroll
+    for (int j = 0; j < T / 2; j++) {
+      const uint32_t a = pk_abs(X[c][j]), b = pk_abs(X[c + 1][j]);
+      const uint32_t los = __builtin_amdgcn_perm(b, a, 0x05040100u);   // (a.lo, b.lo)
+      const uint32_t his = __builtin_amdgcn_perm(b, a, 0x07060302u);   // (a.hi, b.hi)
+      const v2s m = __builtin_elementwise_max(up(los), up(his));
+      s = udot2(pk(m), 0x00010001u, s);
+    }
+  // 8x8: (2s + 2) >> 2 ; 4x4: (2s + 1) >> 1
+  return T == 8 ? (s + 1) >> 1 : s;
+}
+
+template <int T>
+__device__ __forceinline__ uint32_t sad_packed(const uint32_t (&X)[T][T / 2]) {
+  uint32_t s = 0;
+#pragma unroll
+  for (int c = 0; c < T; c++)
+#pragma unroll
+    for (int j = 0; j < T / 2; j++) s = udot2(pk_abs(X[c][j]), 0x00010001u, s);
+  return s;
+}
+
+// ---- per-class layout ----------------------------------------------------------------------
+constexpr int align_up(int v, int a) { return (v + a - 1) / a * a; }
+
+struct PuInfo {
+  int32_t job, flags, x, y, ref, org, key_off;
+  int32_t wx0, wy0;        // absolute window origin (mv_tz - 5)
+  int32_t mvx, mvy;        // integer MV (after EMI)
+  int32_t ex, ey;          // mv_int' - mv_tz
+  int32_t mvp_x, mvp_y;
+  int32_t lt_x, lt_y, rb_x, rb_y;
+  int32_t had, hx, hy, sub;
+  int32_t pad0;
+  double ml;
+  uint32_t acc[9];
+  uint32_t acc_q[9];
+  uint32_t pad1[4];
+};
+static_assert(sizeof(PuInfo) % 16 == 0, "PuInfo alignment");
+
+template <int W, int H>
+struct Lay {
+  static constexpr int T = ((W % 8) == 0 && (H % 8) == 0) ? 8 : 4;
+  static constexpr int TX = W / T, TY = H / T, TILES = TX * TY;
+  static constexpr int WR = H + 10, WC = W + 10;       // window rows / cols
+  static constexpr int RS = align_up(WC, 4) + 8;       // row-major window stride (bytes)
+  static constexpr int CSB = align_up(WR, 4) + 8;      // column-major window stride (bytes)
+  static constexpr int CS = H + 10;                    // stage-1 plane column stride (int16): odd dwords
+  static constexpr int PC = W + 1;                     // plane columns (-1..W-1)
+  static constexpr int PR = H + 8;                     // plane rows (-4..H+3)
+  static constexpr int QS = align_up(H + 1, 8) + 8;    // half-pred byte planes column stride
+  static constexpr int O_WINR = 0;
+  static constexpr int O_WINC = align_up(O_WINR + WR * RS, 16);
+  static constexpr int O_KEY = align_up(O_WINC + WC * CSB, 16);
+  static constexpr int O_PL = align_up(O_KEY + W * H * 2, 16);
+  static constexpr int PLANE_B = PC * CS * 2;
+  static constexpr int O_Q22 = align_up(O_PL + 3 * PLANE_B + 32, 16);
+  static constexpr int O_Q20 = O_Q22 + PC * QS;
+  static constexpr int O_Q02 = O_Q20 + W * QS;
+  static constexpr int BYTES = align_up(O_Q02 + PC * QS + 16, 16);
+};
+
+// Dynamic LDS of a tile: [PuInfo x P][quarter work lists 3 x 8P int32][counts x4][PU regions x P]
+template <int W, int H, int NT, int BUDGET>
+struct Tile {
+  using L = Lay<W, H>;
+  static constexpr int PER_PU = L::BYTES + (int)sizeof(PuInfo) + 3 * 8 * 4;
+  static constexpr int P0 = (BUDGET - 16) / PER_PU;
+  static constexpr int P = P0 < 1 ? 1 : (P0 > 64 ? 64 : P0);
+  static constexpr int O_QLIST = P * (int)sizeof(PuInfo);
+  static constexpr int O_QCOUNT = O_QLIST + 3 * 8 * P * 4;
+  static constexpr int O_REGION = align_up(O_QCOUNT + 16, 16);
+  static constexpr size_t LDS = (size_t)O_REGION + (size_t)P * L::BYTES;
+  static_assert(LDS <= 160 * 1024, "tile exceeds the CU's LDS");
+};
+
+// ---- column loaders -------------------------------------------------------------------------
+// T consecutive bytes of a column starting at byte offset `off` (any alignment) -> T/4 dwords.
+template <int T>
+__device__ __forceinline__ void load_bytes(const uint8_t* base, int off, uint32_t (&out)[T / 4]) {
+  const uint8_t* p = base + (off & ~3);
+  const uint32_t sh = (uint32_t)(off & 3);
+  uint32_t a[T / 4 + 1];
+#pragma unroll
+  for (int j = 0; j <= T / 4; j++) a[j] = lds32(p + 4 * j);
+#pragma unroll
+  for (int j = 0; j < T / 4; j++) out[j] = funnel8(a[j + 1], a[j], sh);
+}
+
+// T outputs of the vertical 8-tap filter on an int16 column starting at value index pr0
+// (any parity): s[m] = sum_k c[k] * v[pr0 + m + k].
+template <int T>
+__device__ __forceinline__ void vert_i16(const uint8_t* col, int pr0, const uint32_t (&c)[4], int (&s)[T]) {
+  constexpr int N = T / 2 + 4;   // dwords read
+  const uint8_t* p = col + 4 * (pr0 >> 1);
+  uint32_t a[N + 1];
+#pragma unroll
+  for (int j = 0; j <= N; j++) a[j] = lds32(p + 4 * j);
+  const bool odd = (pr0 & 1) != 0;
+  uint32_t e[N], o[N];
+#pragma unroll
+  for (int j = 0; j < N; j++) {
+    const uint32_t b = funnel16(a[j + 1], a[j]);
+    e[j] = odd ? b : a[j];
+    o[j] = odd ? a[j + 1] : b;
+  }
+#pragma unroll
+  for (int m = 0; m < T; m++) {
+    const uint32_t* q = (m & 1) ? &o[m >> 1] : &e[m >> 1];
+    int acc = dot2(q[0], c[0], 0);
+    acc = dot2(q[1], c[1], acc);
+    acc = dot2(q[2], c[2], acc);
+    s[m] = dot2(q[3], c[3], acc);
+  }
+}
+
+// T outputs of the vertical 8-tap filter on an int8 (s - 128) byte column starting at byte
+// offset off: s[m] = sum_k c[k] * s'[off + m + k].
+template <int T>
+__device__ __forceinline__ void vert_s8(const uint8_t* base, int off, uint32_t clo, uint32_t chi, int (&s)[T]) {
+  constexpr int N = (T + 7 + 3) / 4 + 1;   // dwords covering T+7 bytes from any alignment
+  const uint8_t* p = base + (off & ~3);
+  const uint32_t sh = (uint32_t)(off & 3);
+  uint32_t a[N];
+#pragma unroll
+  for (int j = 0; j < N; j++) a[j] = lds32(p + 4 * j);
+  uint32_t d[T + 4];
+#pragma unroll
+  for (int m = 0; m < T + 4; m++) {
+    const int q = m >> 2, r = m & 3;
+    // bytes (sh + m) .. (sh + m + 3)
+    const uint32_t x = sh + (uint32_t)r;
+    d[m] = x >= 4 ? funnel8(a[q + 2], a[q + 1], x - 4) : funnel8(a[q + 1], a[q], x);
+  }
+#pragma unroll
+  for (int m = 0; m < T; m++) s[m] = dot4(d[m + 4], chi, dot4(d[m], clo, 0));
+}
+
+}  // namespace
+
+// =============================================================================================
+// The tile body.
+// =============================================================================================
+template <int W, int H, int NT, int BUDGET>
+__device__ __forceinline__ void search_tile2(const BatchArgs& a, const int32_t* perm, int first, int count, char* lds) {
+  using L = Lay<W, H>;
+  using TL = Tile<W, H, NT, BUDGET>;
+  constexpr int T = L::T;
+  constexpr int P = TL::P;
+  PuInfo* info = reinterpret_cast<PuInfo*>(lds);
+  int32_t* qlist = reinterpret_cast<int32_t*>(lds + TL::O_QLIST);     // [3][8P]
+  int32_t* qcount = reinterpret_cast<int32_t*>(lds + TL::O_QCOUNT);   // [3]
+  uint8_t* region0 = reinterpret_cast<uint8_t*>(lds + TL::O_REGION);
+  auto R = [&](int p) { return region0 + (size_t)p * L::BYTES; };
+  const int tid = threadIdx.x;
+
+  // ---- 0. descriptors ----------------------------------------------------------------------
+  if (tid < P) {
+    PuInfo& in = info[tid];
+    if (tid < count) {
+      const int jid = perm[first + tid];
+      const fme_job j = a.jobs[jid];
+      in.job = jid;
+      in.flags = j.flags;
+      in.x = j.x;
+      in.y = j.y;
+      in.ref = j.ref_id;
+      in.org = j.org_id;
+      in.key_off = j.key_offset;
+      in.wx0 = (int)j.x + j.mv_x - 5;
+      in.wy0 = (int)j.y + j.mv_y - 5;
+      in.mvx = j.mv_x;
+      in.mvy = j.mv_y;
+      in.ex = in.ey = 0;
+      in.mvp_x = j.mvp_x;
+      in.mvp_y = j.mvp_y;
+      in.lt_x = j.lt_x;
+      in.lt_y = j.lt_y;
+      in.rb_x = j.rb_x;
+      in.rb_y = j.rb_y;
+      in.had = (a.use_hadamard && !(j.flags & FME_JOB_LOSSLESS)) ? 1 : 0;
+      in.hx = in.hy = 0;
+      in.ml = a.mlambda[j.lambda_id];
+    } else {
+      in.job = -1;
+      in.flags = 0;
+    }
+#pragma unroll
+    for (int k = 0; k < 9; k++) in.acc[k] = in.acc_q[k] = 0;
+  }
+  __syncthreads();
+
+  // ---- 1. stage the window (row- and column-major, int8 s-128) and the key ------------------
+  for (int e = tid; e < count * L::WR * L::WC; e += NT) {
+    const int p = e / (L::WR * L::WC), rem = e - p * (L::WR * L::WC);
+    const int r = rem / L::WC, c = rem - r * L::WC;
+    const PuInfo& in = info[p];
+    const PicDesc pd = a.pics[in.ref];
+    const int ax = clamp_i(in.wx0 + c, 0, pd.width - 1);
+    const int ay = clamp_i(in.wy0 + r, 0, pd.height - 1);
+    const uint8_t v = pd.luma[(size_t)ay * pd.stride + ax] ^ 0x80u;
+    uint8_t* base = R(p);
+    base[L::O_WINR + r * L::RS + c] = v;
+    base[L::O_WINC + c * L::CSB + r] = v;
+  }
+  for (int e = tid; e < count * W * H; e += NT) {
+    const int p = e / (W * H), rem = e - p * (W * H);
+    const int r = rem / W, c = rem - r * W;
+    const PuInfo& in = info[p];
+    int16_t v;
+    if (in.key_off >= 0) {
+      v = a.keys[(size_t)in.key_off + rem];
+    } else {
+      const PicDesc pd = a.pics[in.org];
+      v = pd.luma[(size_t)(in.y + r) * pd.stride + in.x + c];
+    }
+    reinterpret_cast<int16_t*>(R(p) + L::O_KEY)[c * H + r] = v;
+  }
+  __syncthreads();
+
+  // ---- 2. EMI: integer distortion of centre + 8 neighbours, per key column -------------------
+  // Metric of the modified setDistParam (TComRdCost.cpp:200-230): SSE for W in {4,8,16,32,64},
+  // SAD for 12/24/48 over even rows only when FEN is 1 or 3 and H > 8 (TEncSearch.cpp:1158-1164).
+  constexpr bool kSad = (W == 12 || W == 24 || W == 48);
+  const int sub = (kSad && (a.fen == 1 || a.fen == 3) && H > 8) ? 1 : 0;
+  for (int e = tid; e < count * 9 * W; e += NT) {
+    const int p = e / (9 * W), rem = e - p * 9 * W;
+    const int pos = rem / W, c = rem - pos * W;
+    const PuInfo& in = info[p];
+    if (!(in.flags & FME_JOB_EMI)) continue;
+    const int dx = pos == 0 ? 0 : ((pos == 1 || pos == 4 || pos == 6) ? -1 : ((pos == 2 || pos == 7) ? 0 : 1));
+    const int dy = pos == 0 ? 0 : (pos <= 3 ? -1 : (pos <= 5 ? 0 : 1));
+    const uint8_t* base = R(p);
+    const uint8_t* kc = base + L::O_KEY + c * H * 2;
+    const int off = L::O_WINC + (c + 5 + dx) * L::CSB + 5 + dy;
+    const uint32_t wsel = sub ? 0x00000001u : 0x00010001u;
+    uint32_t s = 0;
+#pragma unroll
+    for (int q = 0; q < H / 4; q++) {
+      uint32_t w4[1];
+      load_bytes<4>(base, off + 4 * q, w4);
+      const uint32_t x = w4[0] ^ 0x80808080u;
+      const uint32_t d0 = pk_sub(lds32(kc + 8 * q), lo_pair(x));
+      const uint32_t d1 = pk_sub(lds32(kc + 8 * q + 4), hi_pair(x));
+      if (kSad) {
+        s = udot2(pk_abs(d0), wsel, s);
+        s = udot2(pk_abs(d1), wsel, s);
+      } else {
+        s = (uint32_t)dot2(d0, d0, (int)s);
+        s = (uint32_t)dot2(d1, d1, (int)s);
+      }
+    }
+    atomicAdd(&info[p].acc[pos], s);
+  }
+  __syncthreads();
+  if (tid < count) {
+    PuInfo& in = info[tid];
+    fme_result* r = a.res + in.job;
+    int n_emi = 0;
+    uint32_t cval = 0;
+    if (in.flags & FME_JOB_EMI) {
+      const int sx = in.mvx, sy = in.mvy;
+      uint32_t best = (in.acc[0] << sub) + mv_cost(in.ml, mv_bits(sx, sy, 2, in.mvp_x, in.mvp_y));
+      int bx = sx, by = sy;
+      const bool top = sy - 1 >= in.lt_y, bot = sy + 1 <= in.rb_y;
+      const bool left = sx - 1 >= in.lt_x, right = sx + 1 <= in.rb_x;
+#pragma unroll
+      for (int pos = 1; pos <= 8; pos++) {
+        const int dx = (pos == 1 || pos == 4 || pos == 6) ? -1 : ((pos == 2 || pos == 7) ? 0 : 1);
+        const int dy = pos <= 3 ? -1 : (pos <= 5 ? 0 : 1);
+        const bool ok = (dy == -1 ? top : (dy == 1 ? bot : true)) && (dx == -1 ? left : (dx == 1 ? right : true));
+        if (!ok) continue;
+        uint32_t d = in.acc[pos] << sub;
+        r->emi[n_emi++] = d;
+        if (d < best) {
+          d += mv_cost(in.ml, mv_bits(sx + dx, sy + dy, 2, in.mvp_x, in.mvp_y));
+          if (d < best) {
+            best = d;
+            bx = sx + dx;
+            by = sy + dy;
+          }
+        }
+      }
+      cval = best - mv_cost(in.ml, mv_bits(bx, by, 2, in.mvp_x, in.mvp_y));
+      in.ex = bx - sx;
+      in.ey = by - sy;
+      in.mvx = bx;
+      in.mvy = by;
+    }
+    for (int k = n_emi; k < 8; k++) r->emi[k] = 0;
+    r->n_emi = (uint8_t)n_emi;
+    r->c = cval;
+    r->mv_int_x = (int16_t)in.mvx;
+    r->mv_int_y = (int16_t)in.mvy;
+  }
+  __syncthreads();
+
+  // ---- 3. first-stage planes fx = 1,2,3 (column-major int16), 4 columns x 8 rows per item ---
+  {
+    constexpr int NG = (L::PC + 3) / 4, NCH = (L::PR + 7) / 8;
+    uint32_t tl[3], th[3];
+    taps8(1, tl[0], th[0]);
+    taps8(2, tl[1], th[1]);
+    taps8(3, tl[2], th[2]);
+    for (int e = tid; e < count * NG * NCH; e += NT) {
+      const int p = e / (NG * NCH), rem = e - p * (NG * NCH);
+      const int ch = rem / NG, g = rem - ch * NG;   // columns fastest: neighbouring lanes, neighbouring bytes
+      const PuInfo& in = info[p];
+      uint8_t* base = R(p);
+#pragma unroll
+      for (int rr = 0; rr < 8; rr += 2) {
+        uint32_t out[4][3][2];
+#pragma unroll
+        for (int h = 0; h < 2; h++) {
+          const int pr = ch * 8 + rr + h;
+          const int row = min(1 + in.ey + pr, L::WR - 1);
+          const int off = L::O_WINR + row * L::RS + 1 + in.ex + 4 * g;
+          const uint8_t* q = base + (off & ~3);
+          const uint32_t sh = (uint32_t)(off & 3);
+          uint32_t w[4];
+#pragma unroll
+          for (int j = 0; j < 4; j++) w[j] = lds32(q + 4 * j);
+          uint32_t d[8];
+#pragma unroll
+          for (int m = 0; m < 8; m++) {
+            const uint32_t x = sh + (uint32_t)(m & 3);
+            const int qd = m >> 2;
+            d[m] = x >= 4 ? funnel8(w[qd + 2], w[qd + 1], x - 4) : funnel8(w[qd + 1], w[qd], x);
+          }
+#pragma unroll
+          for (int i = 0; i < 4; i++)
+#pragma unroll
+            for (int f = 0; f < 3; f++) out[i][f][h] = (uint32_t)dot4(d[i + 4], th[f], dot4(d[i], tl[f], 0));
+        }
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+          const int pc = 4 * g + i;
+          if (pc < L::PC && ch * 8 + rr < L::PR) {
+#pragma unroll
+            for (int f = 0; f < 3; f++) {
+              uint8_t* col = base + L::O_PL + f * L::PLANE_B + pc * L::CS * 2;
+              sts32(col + (ch * 8 + rr) * 2, (out[i][f][0] & 0xffffu) | (out[i][f][1] << 16));
+            }
+          }
+        }
+      }
+    }
+  }
+  __syncthreads();
+
+  // ---- 4a. half-pel prediction planes (8-bit, column-major) ----------------------------------
+  // Q22 = [2][2]: vertical half over plane fx=2, cols -1..W-1, rows -1..H-1
+  // Q20 = [2][0]: vertical half over integer columns (bytes), cols 0..W-1, rows -1..H-1
+  // Q02 = [0][2]: plane fx=2 rounded, cols -1..W-1, rows 0..H-1
+  {
+    constexpr int NCH = (H + 1 + 7) / 8;     // Q22 / Q20 row chunks
+    constexpr int NCH2 = (H + 7) / 8;        // Q02 row chunks
+    constexpr int N22 = L::PC * NCH, N20 = W * NCH, N02 = L::PC * NCH2;
+    uint32_t c2[4];
+    taps16(2, c2);
+    uint32_t c2lo, c2hi;
+    taps8(2, c2lo, c2hi);
+    for (int e = tid; e < count * (N22 + N20 + N02); e += NT) {
+      const int p = e / (N22 + N20 + N02);
+      int rem = e - p * (N22 + N20 + N02);
+      const PuInfo& in = info[p];
+      uint8_t* base = R(p);
+      int s[8];
+      uint8_t* dst;
+      if (rem < N22) {
+        const int ch = rem / L::PC, col = rem - ch * L::PC;
+        // outputs rows R = -1 + 8ch + m -> plane rows from R + 1 (taps R-3..R+4 at pr R+1..R+8)
+        vert_i16<8>(base + L::O_PL + 1 * L::PLANE_B + col * L::CS * 2, 8 * ch, c2, s);
+#pragma unroll
+        for (int m = 0; m < 8; m++) s[m] = round2d(s[m]);
+        dst = base + L::O_Q22 + col * L::QS + 8 * ch;
+      } else if (rem < N22 + N20) {
+        rem -= N22;
+        const int ch = rem / W, col = rem - ch * W;
+        // integer column col (rel mv_int') = window column col + 5 + ex; rows R-3.. -> window row R+2+ey
+        const int off = L::O_WINC + (col + 5 + in.ex) * L::CSB + (8 * ch - 1) + 2 + in.ey;
+        vert_s8<8>(base, off, c2lo, c2hi, s);
+#pragma unroll
+        for (int m = 0; m < 8; m++) s[m] = round1d_s8(s[m]);
+        dst = base + L::O_Q20 + col * L::QS + 8 * ch;
+      } else {
+        rem -= N22 + N20;
+        const int ch = rem / L::PC, col = rem - ch * L::PC;
+        const uint8_t* pcol = base + L::O_PL + 1 * L::PLANE_B + col * L::CS * 2 + (8 * ch + 4) * 2;
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+          const uint32_t v = lds32(pcol + 4 * j);
+          s[2 * j] = clamp_i(((int)(int16_t)(v & 0xffffu) + 8224) >> 6, 0, 255);
+          s[2 * j + 1] = clamp_i(((int)(int16_t)(v >> 16) + 8224) >> 6, 0, 255);
+        }
+        dst = base + L::O_Q02 + col * L::QS + 8 * ch;
+      }
+      sts32(dst, (uint32_t)s[0] | ((uint32_t)s[1] << 8) | ((uint32_t)s[2] << 16) | ((uint32_t)s[3] << 24));
+      sts32(dst + 4, (uint32_t)s[4] | ((uint32_t)s[5] << 8) | ((uint32_t)s[6] << 16) | ((uint32_t)s[7] << 24));
+    }
+  }
+  __syncthreads();
+
+  // ---- 4b. half-pel SATD: 9 candidates x tiles ------------------------------------------------
+  {
+    const int items = count * L::TILES;
+    for (int e = tid; e < 9 * items; e += NT) {
+      const int k = e / items, rem = e - k * items;
+      const int p = rem / L::TILES, t = rem - p * L::TILES;
+      const PuInfo& in = info[p];
+      const uint8_t* base = R(p);
+      const int ty = t / L::TX, tx = t - ty * L::TX;
+      const int dx = cand_dx(k), dy = half_dy(k);
+      // pred source for (2dx, 2dy): integer / Q20 / Q02 / Q22 (m_filteredBlock plane walk)
+      int colbase, cstride, rowoff;
+      uint32_t flip = 0;
+      if (dx == 0 && dy == 0) {
+        colbase = L::O_WINC + (5 + in.ex) * L::CSB;
+        cstride = L::CSB;
+        rowoff = 5 + in.ey;
+        flip = 0x80808080u;
+      } else if (dx == 0) {
+        colbase = L::O_Q20;
+        cstride = L::QS;
+        rowoff = dy < 0 ? 0 : 1;
+      } else if (dy == 0) {
+        colbase = L::O_Q02 + (dx < 0 ? 0 : 1) * L::QS;
+        cstride = L::QS;
+        rowoff = 0;
+      } else {
+        colbase = L::O_Q22 + (dx < 0 ? 0 : 1) * L::QS;
+        cstride = L::QS;
+        rowoff = dy < 0 ? 0 : 1;
+      }
+      uint32_t X[T][T / 2];
+#pragma unroll
+      for (int c = 0; c < T; c++) {
+        const int col = tx * T + c;
+        uint32_t b[T / 4];
+        load_bytes<T>(base, colbase + col * cstride + rowoff + ty * T, b);
+        const uint8_t* kc = base + L::O_KEY + (col * H + ty * T) * 2;
+#pragma unroll
+        for (int j = 0; j < T / 4; j++) {
+          const uint32_t x = b[j] ^ flip;
+          X[c][2 * j] = pk_sub(lds32(kc + 8 * j), lo_pair(x));
+          X[c][2 * j + 1] = pk_sub(lds32(kc + 8 * j + 4), hi_pair(x));
+        }
+      }
+      const uint32_t dd = in.had ? satd_packed<T>(X) : sad_packed<T>(X);
+      atomicAdd(&info[p].acc_q[k], dd);
+    }
+  }
+  __syncthreads();
+
+  // ---- 4c. half argmin (cost scale 1), quarter work list sorted by code path -------------------
+  if (tid < 3) qcount[tid] = 0;
+  __syncthreads();
+  if (tid < count) {
+    PuInfo& in = info[tid];
+    uint32_t best = 0xFFFFFFFFu;
+    int bi = 0;
+#pragma unroll
+    for (int k = 0; k < 9; k++) {
+      const int hx = 2 * in.mvx + cand_dx(k), hy = 2 * in.mvy + half_dy(k);
+      const uint32_t d = in.acc_q[k] + mv_cost(in.ml, mv_bits(hx, hy, 1, in.mvp_x, in.mvp_y));
+      if (d < best) {
+        best = d;
+        bi = k;
+      }
+    }
+    in.hx = cand_dx(bi);
+    in.hy = half_dy(bi);
+    in.acc[0] = in.acc_q[bi];   // quarter candidate 0 == the best half position
+#pragma unroll
+    for (int k = 1; k < 9; k++) {
+      in.acc[k] = 0;
+      const int qx = 2 * in.hx + cand_dx(k), qy = 2 * in.hy + qtr_dy(k);
+      const int path = (qy & 3) == 0 ? 0 : ((qx & 3) == 0 ? 1 : 2);
+      const int slot = atomicAdd(&qcount[path], 1);
+      qlist[path * 8 * P + slot] = tid * 16 + k;
+    }
+  }
+  __syncthreads();
+
+  // ---- 5. quarter-pel SATD: 8 candidates x tiles, grouped by path ------------------------------
+  {
+    const int n0 = qcount[0] * L::TILES, n1 = qcount[1] * L::TILES, n2 = qcount[2] * L::TILES;
+    for (int e = tid; e < n0 + n1 + n2; e += NT) {
+      int path, idx;
+      if (e < n0) { path = 0; idx = e; }
+      else if (e < n0 + n1) { path = 1; idx = e - n0; }
+      else { path = 2; idx = e - n0 - n1; }
+      const int entry = qlist[path * 8 * P + idx / L::TILES];
+      const int t = idx - (idx / L::TILES) * L::TILES;
+      const int p = entry >> 4, k = entry & 15;
+      const PuInfo& in = info[p];
+      const uint8_t* base = R(p);
+      const int ty = t / L::TX, tx = t - ty * L::TX;
+      const int qx = 2 * in.hx + cand_dx(k), qy = 2 * in.hy + qtr_dy(k);
+      const int ix = qx >> 2, fx = qx & 3, iy = qy >> 2, fy = qy & 3;
+      uint32_t X[T][T / 2];
+      if (path == 0) {
+        // fy == 0 (iy == 0): horizontal only, plane fx rounded (filterCopy !isFirst)
+#pragma unroll
+        for (int c = 0; c < T; c++) {
+          const int col = tx * T + c;
+          const uint8_t* pcol = base + L::O_PL + (fx - 1) * L::PLANE_B + (col + ix + 1) * L::CS * 2 + (ty * T + 4) * 2;
+          const uint8_t* kc = base + L::O_KEY + (col * H + ty * T) * 2;
+#pragma unroll
+          for (int j = 0; j < T / 2; j++) {
+            const v2s t16 = up(lds32(pcol + 4 * j));
+            v2s pr = (t16 + (v2s)(8224)) >> (v2s)(6);
+            pr = __builtin_elementwise_min(__builtin_elementwise_max(pr, (v2s)(0)), (v2s)(255));
+            X[c][j] = pk_sub(lds32(kc + 4 * j), pk(pr));
+          }
+        }
+      } else if (path == 1) {
+        // fx == 0: vertical only on the integer column (bytes)
+        uint32_t clo, chi;
+        taps8(fy, clo, chi);
+#pragma unroll
+        for (int c = 0; c < T; c++) {
+          const int col = tx * T + c;
+          const int off = L::O_WINC + (col + 5 + in.ex) * L::CSB + ty * T + iy + 2 + in.ey;
+          int s[T];
+          vert_s8<T>(base, off, clo, chi, s);
+          const uint8_t* kc = base + L::O_KEY + (col * H + ty * T) * 2;
+#pragma unroll
+          for (int j = 0; j < T / 2; j++) {
+            const uint32_t pr = (uint32_t)round1d_s8(s[2 * j]) | ((uint32_t)round1d_s8(s[2 * j + 1]) << 16);
+            X[c][j] = pk_sub(lds32(kc + 4 * j), pr);
+          }
+        }
+      } else {
+        // 2-D: vertical fy over plane fx
+        uint32_t cv[4];
+        taps16(fy, cv);
+#pragma unroll
+        for (int c = 0; c < T; c++) {
+          const int col = tx * T + c;
+          const uint8_t* pcol = base + L::O_PL + (fx - 1) * L::PLANE_B + (col + ix + 1) * L::CS * 2;
+          int s[T];
+          vert_i16<T>(pcol, ty * T + iy + 1, cv, s);
+          const uint8_t* kc = base + L::O_KEY + (col * H + ty * T) * 2;
+#pragma unroll
+          for (int j = 0; j < T / 2; j++) {
+            const uint32_t pr = (uint32_t)round2d(s[2 * j]) | ((uint32_t)round2d(s[2 * j + 1]) << 16);
+            X[c][j] = pk_sub(lds32(kc + 4 * j), pr);
+          }
+        }
+      }
+      const uint32_t dd = in.had ? satd_packed<T>(X) : sad_packed<T>(X);
+      atomicAdd(&info[p].acc[k], dd);
+    }
+  }
+  __syncthreads();
+
+  // ---- 6. quarter argmin (cost scale 0) and results ---------------------------------------------
+  if (tid < count) {
+    PuInfo& in = info[tid];
+    uint32_t best = 0xFFFFFFFFu;
+    int bi = 0;
+#pragma unroll
+    for (int k = 0; k < 9; k++) {
+      const int qx = 4 * in.mvx + 2 * in.hx + cand_dx(k), qy = 4 * in.mvy + 2 * in.hy + qtr_dy(k);
+      const uint32_t d = in.acc[k] + mv_cost(in.ml, mv_bits(qx, qy, 0, in.mvp_x, in.mvp_y));
+      if (d < best) {
+        best = d;
+        bi = k;
+      }
+    }
+    fme_result* r = a.res + in.job;
+    r->half_x = (int8_t)in.hx;
+    r->half_y = (int8_t)in.hy;
+    r->qtr_x = (int8_t)cand_dx(bi);
+    r->qtr_y = (int8_t)qtr_dy(bi);
+    r->frac_cost = best;
+  }
+}
+
+// =============================================================================================
+// kernels: small shapes (256 lanes, <= 40 KB LDS per tile) and large shapes (512 lanes)
+// =============================================================================================
+#define FME_SMALL_CLASSES(X)                                                                       \
+  X(0, 4, 8) X(1, 8, 4) X(2, 8, 8) X(3, 4, 16) X(4, 16, 4) X(5, 8, 16) X(6, 16, 8) X(7, 12, 16)      \
+  X(8, 16, 12) X(9, 16, 16) X(10, 8, 32) X(11, 32, 8) X(12, 16, 32) X(13, 32, 16) X(14, 24, 32)     \
+  X(15, 32, 24) X(16, 32, 32) X(17, 16, 64) X(18, 64, 16)
+#define FME_LARGE_CLASSES(X) X(19, 32, 64) X(20, 64, 32) X(21, 48, 64) X(22, 64, 48) X(23, 64, 64)
+
+constexpr int kSmallNT = 256, kSmallBudget = 40 * 1024;
+constexpr int kLargeNT = 512, kLargeBudget = 76 * 1024;
+
+__device__ __forceinline__ int find_class(const Schedule& sc, int b, int lo, int hi) {
+  int c = lo;
+  while (c < hi - 1 && b >= sc.tile_prefix[c + 1]) c++;
+  return c;
+}
+
+__global__ __launch_bounds__(kSmallNT) void k_search_small(BatchArgs a, WorkBufs w, Schedule sc) {
+  extern __shared__ __attribute__((aligned(16))) char lds[];
+  const int b = blockIdx.x + sc.tile_prefix[0];
+  const int c = find_class(sc, b, 0, 19);
+  const int t = b - sc.tile_prefix[c];
+  switch (c) {
+#define FME_CASE(ID, W_, H_)                                                                  \
+  case ID: {                                                                                  \
+    constexpr int P = Tile<W_, H_, kSmallNT, kSmallBudget>::P;                                \
+    search_tile2<W_, H_, kSmallNT, kSmallBudget>(a, w.perm, sc.class_off[ID] + t * P,         \
+                                                 min(P, sc.class_cnt[ID] - t * P), lds);      \
+  } break;
+    FME_SMALL_CLASSES(FME_CASE)
+#undef FME_CASE
+    default: break;
+  }
+}
+
+__global__ __launch_bounds__(kLargeNT) void k_search_large(BatchArgs a, WorkBufs w, Schedule sc) {
+  extern __shared__ __attribute__((aligned(16))) char lds[];
+  const int b = blockIdx.x + sc.tile_prefix[19];
+  const int c = find_class(sc, b, 19, kNumClasses);
+  const int t = b - sc.tile_prefix[c];
+  switch (c) {
+#define FME_CASE(ID, W_, H_)                                                                  \
+  case ID: {                                                                                  \
+    constexpr int P = Tile<W_, H_, kLargeNT, kLargeBudget>::P;                                \
+    search_tile2<W_, H_, kLargeNT, kLargeBudget>(a, w.perm, sc.class_off[ID] + t * P,         \
+                                                 min(P, sc.class_cnt[ID] - t * P), lds);      \
+  } break;
+    FME_LARGE_CLASSES(FME_CASE)
+#undef FME_CASE
+    default: break;
+  }
+}
+
+// ---- host helpers ----------------------------------------------------------------------------
+int pus_per_tile(int cls) {
+  switch (cls) {
+#define FME_PS(ID, W_, H_) case ID: return Tile<W_, H_, kSmallNT, kSmallBudget>::P;
+#define FME_PL(ID, W_, H_) case ID: return Tile<W_, H_, kLargeNT, kLargeBudget>::P;
+    FME_SMALL_CLASSES(FME_PS)
+    FME_LARGE_CLASSES(FME_PL)
+#undef FME_PS
+#undef FME_PL
+    default: return 1;
+  }
+}
+
+size_t lds_bytes_for_class(int cls) {
+  switch (cls) {
+#define FME_LS(ID, W_, H_) case ID: return Tile<W_, H_, kSmallNT, kSmallBudget>::LDS;
+#define FME_LL(ID, W_, H_) case ID: return Tile<W_, H_, kLargeNT, kLargeBudget>::LDS;
+    FME_SMALL_CLASSES(FME_LS)
+    FME_LARGE_CLASSES(FME_LL)
+#undef FME_LS
+#undef FME_LL
+    default: return 0;
+  }
+}
+
+hipError_t launch_search(const BatchArgs& a, const WorkBufs& w, const Schedule& sc, size_t /*lds*/,
+                         hipStream_t s) {
+  size_t lds_s = 0, lds_l = 0;
+  for (int c = 0; c < kNumClasses; c++) {
+    if (!sc.class_cnt[c]) continue;
+    if (c < 19) lds_s = lds_s > lds_bytes_for_class(c) ? lds_s : lds_bytes_for_class(c);
+    else lds_l = lds_l > lds_bytes_for_class(c) ? lds_l : lds_bytes_for_class(c);
+  }
+  const int small_tiles = sc.tile_prefix[19] - sc.tile_prefix[0];
+  const int large_tiles = sc.tile_prefix[kNumClasses] - sc.tile_prefix[19];
+  if (large_tiles > 0) {
+    static bool attr_set = false;
+    if (!attr_set) {
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_search_large),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+      attr_set = true;
+    }
+    hipLaunchKernelGGL(k_search_large, dim3(large_tiles), dim3(kLargeNT), lds_l, s, a, w, sc);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+  }
+  if (small_tiles > 0) {
+    hipLaunchKernelGGL(k_search_small, dim3(small_tiles), dim3(kSmallNT), lds_s, s, a, w, sc);
+    return hipGetLastError();
+  }
+  return hipSuccess;
+}
+
+}  // namespace fme
