@@ -52,11 +52,14 @@ def algorithmic_ops(jobs):
     return int((16 * taps + 2 * copies + 18 * satd + 144).sum())
 
 
-def make_frame_jobs(seed):
+def make_frame_jobs(seed, kind="ctu"):
+    """One frame's jobs.  "ctu": HM order (CTU raster, PUs on the CU grid, coherent motion);
+    "uniform": every PU at a uniformly random frame position (no cache locality, stress)."""
     rng = np.random.default_rng(seed)
-    n = synth.jobs_per_frame(W, H)
-    # refs: picture ids 0..3, org: id 4; lambda slot = the frame's POC % 4 (set per step)
-    return synth.make_jobs(rng, W, H, n, 4, [0, 1, 2, 3], [0])
+    # refs: picture ids 0..3, org: id 4; lambda slot 0 = the frame's value (set per step)
+    if kind == "uniform":
+        return synth.make_jobs(rng, W, H, synth.jobs_per_frame(W, H), 4, [0, 1, 2, 3], [0])
+    return synth.make_ctu_jobs(rng, W, H, 423, 4, [0, 1, 2, 3], [0])
 
 
 def cpu_baseline(jobs_sample, pics):
@@ -96,6 +99,8 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample length")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--check", action="store_true", help="verify one step against the oracle sample")
+    ap.add_argument("--jobs", choices=("ctu", "uniform"), default="ctu",
+                    help="job stream: HM CTU order (default) or uniformly scattered PUs (stress)")
     args = ap.parse_args()
 
     import torch
@@ -115,7 +120,7 @@ def main():
     stream = torch.cuda.current_stream(dev)
 
     # ---- inputs (untimed): jobs of this rank's frames, resident in HBM ----------------------
-    jobs = make_frame_jobs(1000 + rank)
+    jobs = make_frame_jobs(1000 + rank, args.jobs)
     n = len(jobs)
     d_jobs = torch.from_numpy(jobs.view(np.uint8).copy()).to(dev)
     d_res = torch.empty(n * RESULT_DTYPE.itemsize, dtype=torch.uint8, device=dev)
@@ -206,6 +211,7 @@ def main():
                     "reference per-QP NN weights)",
             "config": {"workload": "1920x1080 lowdelay_P QP22, NN_pred 2-layer on, 4 refs, "
                                    "862920 PU jobs per frame (configs[2] at QP22)",
+                       "job_stream": args.jobs,
                        "jobs_per_step_per_gpu": n, "parallelism": f"frame-sharded x{world}"},
             "roofline": {
                 "bound": "hbm",

@@ -9,6 +9,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
@@ -85,6 +86,7 @@ struct fme_ctx {
   DevBuf<fme_result> d_res;
   DevBuf<uint8_t> cls;
   DevBuf<int32_t> perm;
+  DevBuf<fme_job> sjobs;
   DevBuf<int32_t> counts;      // 25 counts + 24 cursors, one memset
   DevBuf<int32_t> blk_agg;
   DevBuf<int32_t> blk_prefix;
@@ -103,9 +105,15 @@ struct fme_ctx {
   bool timed = false;
   hipEvent_t ev[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};
   hipEvent_t ev_end = nullptr;
+
+  // the large-shape search kernel runs beside the small-shape one on its own stream
+  hipStream_t aux = nullptr;
+  hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+  bool concurrent_search = true;   // FME_SERIAL_SEARCH=1 runs the two search kernels back to back
 };
 
 namespace fme {
+hipError_t debug_phase_cycles(unsigned long long* out16, bool reset);
 hipError_t launch_nn_single(const float* nnp, const uint32_t* in, int32_t* out, hipStream_t s);
 }
 
@@ -133,11 +141,16 @@ int fme_create(int device, const fme_config* cfg, fme_ctx** out_ctx) {
   HIP_TRY(c->nn_state.reserve(24));
   HIP_TRY(hipMemset(c->nn_state.p, 0, 24 * sizeof(uint32_t)));
   HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&c->h_counts), (kNumClasses + 1) * sizeof(int32_t), hipHostMallocDefault));
+  HIP_TRY(hipStreamCreateWithFlags(&c->aux, hipStreamNonBlocking));
+  if (const char* e = getenv("FME_SERIAL_SEARCH")) c->concurrent_search = (e[0] == '0');
+  HIP_TRY(hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming));
+  HIP_TRY(hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming));
   if (cfg->max_jobs > 0) {
     const size_t n = (size_t)cfg->max_jobs;
     const size_t nb = (n + kJobsPerScanBlock - 1) / kJobsPerScanBlock;
     HIP_TRY(c->cls.reserve(n));
     HIP_TRY(c->perm.reserve(n));
+    HIP_TRY(c->sjobs.reserve(n));
     HIP_TRY(c->blk_agg.reserve(nb * 9));
     HIP_TRY(c->blk_prefix.reserve(nb * 9));
   }
@@ -152,7 +165,7 @@ int fme_destroy(fme_ctx* c) {
   for (int i = 0; i < FME_MAX_PICTURES; i++)
     if (c->pic_owned[i] && c->pics[i].luma) (void)hipFree(const_cast<uint8_t*>(c->pics[i].luma));
   c->d_pics.release(); c->d_mlambda.release(); c->d_keys.release(); c->d_nn.release();
-  c->d_jobs.release(); c->d_res.release(); c->cls.release(); c->perm.release();
+  c->d_jobs.release(); c->d_res.release(); c->cls.release(); c->perm.release(); c->sjobs.release();
   c->counts.release(); c->blk_agg.release(); c->blk_prefix.release(); c->nn_state.release();
   c->single_pic.release(); c->single_job.release(); c->single_res.release();
   c->single_nn_in.release(); c->single_nn_out.release();
@@ -160,6 +173,9 @@ int fme_destroy(fme_ctx* c) {
   for (auto& e : c->ev)
     if (e) (void)hipEventDestroy(e);
   if (c->ev_end) (void)hipEventDestroy(c->ev_end);
+  if (c->ev_fork) (void)hipEventDestroy(c->ev_fork);
+  if (c->ev_join) (void)hipEventDestroy(c->ev_join);
+  if (c->aux) (void)hipStreamDestroy(c->aux);
   if (c->single) fme_destroy(c->single.release());
   delete c;
   return FME_OK;
@@ -270,6 +286,7 @@ static int ensure_work(fme_ctx* c, int n) {
   const size_t nb = ((size_t)n + kJobsPerScanBlock - 1) / kJobsPerScanBlock;
   HIP_TRY(c->cls.reserve(n));
   HIP_TRY(c->perm.reserve(n));
+  HIP_TRY(c->sjobs.reserve(n));
   HIP_TRY(c->blk_agg.reserve(nb * 9));
   HIP_TRY(c->blk_prefix.reserve(nb * 9));
   return FME_OK;
@@ -312,6 +329,7 @@ int fme_refine_device(fme_ctx* c, const fme_job* d_jobs, fme_result* d_res, int 
   WorkBufs w{};
   w.cls = c->cls.p;
   w.perm = c->perm.p;
+  w.sjobs = c->sjobs.p;
   w.counts = c->counts.p;
   w.cursor = c->counts.p + kNumClasses + 1;
   w.blk_agg = c->blk_agg.p;
@@ -330,25 +348,34 @@ int fme_refine_device(fme_ctx* c, const fme_job* d_jobs, fme_result* d_res, int 
                 c->h_counts[kNumClasses]);
 
   Schedule sc{};
-  size_t lds = 0;
-  int off = 0, tiles = 0;
+  int off = 0, blocks = 0;
+  const int tpb = tiles_per_block();
   for (int k = 0; k < kNumClasses; k++) {
     const int cnt = c->h_counts[k];
     sc.class_off[k] = off;
     sc.class_cnt[k] = cnt;
-    sc.tile_prefix[k] = tiles;
+    sc.tile_prefix[k] = blocks;
     if (cnt) {
       const int p = pus_per_tile(k);
-      tiles += (cnt + p - 1) / p;
-      lds = std::max(lds, lds_bytes_for_class(k));
+      const int tiles = (cnt + p - 1) / p;
+      blocks += (tiles + tpb - 1) / tpb;
     }
     off += cnt;
   }
-  sc.tile_prefix[kNumClasses] = tiles;
+  sc.tile_prefix[kNumClasses] = blocks;
   if (prof) HIP_TRY(hipEventRecord(c->ev[2], s));   // host sync above: scatter starts here
   HIP_TRY(launch_scatter(a, w, sc, s));
   if (prof) HIP_TRY(hipEventRecord(c->ev[3], s));
-  HIP_TRY(launch_search(a, w, sc, lds, s));
+  if (!c->concurrent_search) {
+    HIP_TRY(launch_search_large(a, w, sc, s));
+  } else if (search_large_blocks(sc) > 0) {
+    HIP_TRY(hipEventRecord(c->ev_fork, s));
+    HIP_TRY(hipStreamWaitEvent(c->aux, c->ev_fork, 0));
+    HIP_TRY(launch_search_large(a, w, sc, c->aux));
+    HIP_TRY(hipEventRecord(c->ev_join, c->aux));
+  }
+  HIP_TRY(launch_search_small(a, w, sc, s));
+  if (c->concurrent_search && search_large_blocks(sc) > 0) HIP_TRY(hipStreamWaitEvent(s, c->ev_join, 0));
   if (prof) HIP_TRY(hipEventRecord(c->ev[4], s));
   HIP_TRY(launch_nn_tail(a, w, c->d_nn.p, c->state_cur, s));
   if (prof) {
@@ -479,6 +506,13 @@ int fme_set_profiling(fme_ctx* c, int enable) {
   }
   c->profiling = enable != 0;
   c->timed = false;
+  return FME_OK;
+}
+
+int fme_debug_phase_cycles(uint64_t* out16, int reset) {
+  if (!out16) return fail(FME_E_INVALID, "fme_debug_phase_cycles: null argument");
+  HIP_TRY(hipDeviceSynchronize());
+  HIP_TRY(debug_phase_cycles(reinterpret_cast<unsigned long long*>(out16), reset != 0));
   return FME_OK;
 }
 

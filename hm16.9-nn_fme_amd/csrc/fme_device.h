@@ -41,7 +41,8 @@ struct BatchArgs {
 // Work buffers (device) for one batch.
 struct WorkBufs {
   uint8_t* cls;          // [n] class id, 255 = invalid
-  int32_t* perm;         // [n] jobs grouped by class
+  int32_t* perm;         // [n] jobs grouped by class (original index)
+  fme_job* sjobs;        // [n] copies of the jobs in class order (search reads them contiguously)
   int32_t* counts;       // [kNumClasses + 1]: per-class count, [24] = invalid jobs
   int32_t* cursor;       // [kNumClasses]
   int32_t* blk_agg;      // [nblk * 9] per-block max of the NN writer indices
@@ -49,8 +50,9 @@ struct WorkBufs {
   uint32_t* nn_state;    // 2 x 12 words: slot[8], c, pu_h, pu_w, written
 };
 
-// Tile schedule of the search kernel: blocks [tile_prefix[c], tile_prefix[c+1]) handle
-// class c; class c's jobs are perm[class_off[c] .. class_off[c] + class_cnt[c]).
+// Schedule of the search kernels: blocks [tile_prefix[c], tile_prefix[c+1]) serve class c
+// (each strides over the class's tiles of pus_per_tile(c) PUs); class c's jobs are
+// sjobs/perm[class_off[c] .. class_off[c] + class_cnt[c]).
 struct Schedule {
   int32_t tile_prefix[kNumClasses + 1];
   int32_t class_off[kNumClasses];
@@ -62,8 +64,11 @@ int pus_per_tile(int cls);
 size_t lds_bytes_for_class(int cls);
 hipError_t launch_classify(const BatchArgs& a, const WorkBufs& w, hipStream_t s);
 hipError_t launch_scatter(const BatchArgs& a, const WorkBufs& w, const Schedule& sc, hipStream_t s);
-hipError_t launch_search(const BatchArgs& a, const WorkBufs& w, const Schedule& sc, size_t lds,
-                         hipStream_t s);
+int tiles_per_block();
+int search_large_blocks(const Schedule& sc);
+int search_small_blocks(const Schedule& sc);
+hipError_t launch_search_large(const BatchArgs& a, const WorkBufs& w, const Schedule& sc, hipStream_t s);
+hipError_t launch_search_small(const BatchArgs& a, const WorkBufs& w, const Schedule& sc, hipStream_t s);
 hipError_t launch_nn_tail(const BatchArgs& a, const WorkBufs& w, const float* nn_params,
                           int state_in, hipStream_t s);
 

@@ -151,7 +151,11 @@ __global__ __launch_bounds__(kBlock) void k_scatter(BatchArgs a, WorkBufs w, Sch
 #pragma unroll
   for (int q = 0; q < kJobsPerScanBlock / kBlock; q++) {
     const int i = base + q * kBlock + tid;
-    if (cls[q] < kNumClasses) w.perm[sc.class_off[cls[q]] + basep[cls[q]] + rank[q]] = i;
+    if (cls[q] < kNumClasses) {
+      const int dst = sc.class_off[cls[q]] + basep[cls[q]] + rank[q];
+      w.perm[dst] = i;
+      w.sjobs[dst] = a.jobs[i];
+    }
   }
 }
 
@@ -203,7 +207,7 @@ __device__ __forceinline__ int emb_row_w(int w) {
   return w == 4 ? 1 : w == 8 ? 2 : w == 12 ? 3 : w == 16 ? 4 : w == 24 ? 5 : w == 32 ? 6 : w == 64 ? 7 : 0;
 }
 
-__device__ int nn_forward(const float* __restrict__ P, const uint32_t (&e)[8], uint32_t c, int pu_h,
+__device__ __forceinline__ int nn_forward(const float* __restrict__ P, const uint32_t (&e)[8], uint32_t c, int pu_h,
                           int pu_w) {
   float in[17], x1[22], x2[20];
   const int rh = emb_row_h(pu_h), rw = emb_row_w(pu_w);
@@ -227,6 +231,7 @@ __device__ int nn_forward(const float* __restrict__ P, const uint32_t (&e)[8], u
     s = s + P[P_B1 + r];
     s = s < 0.0f ? 0.0f : s;
     x1[r] = s * P[P_G1 + r] + P[P_BE1 + r];
+    __builtin_amdgcn_sched_barrier(0);   // keep the weight reads of one row together
   }
 #pragma unroll
   for (int r = 0; r < 20; r++) {
@@ -236,14 +241,16 @@ __device__ int nn_forward(const float* __restrict__ P, const uint32_t (&e)[8], u
     s = s + P[P_B2 + r];
     s = s < 0.0f ? 0.0f : s;
     x2[r] = s * P[P_G2 + r] + P[P_BE2 + r];
+    __builtin_amdgcn_sched_barrier(0);
   }
   int best = 0;
   float bv = 0.0f;
-#pragma unroll
+#pragma unroll 1
   for (int r = 0; r < 49; r++) {
+    const float* wr = P + P_W3 + r * 20;
     float s = 0.0f;
 #pragma unroll
-    for (int k = 0; k < 20; k++) s = s + P[P_W3 + r * 20 + k] * x2[k];
+    for (int k = 0; k < 20; k++) s = s + wr[k] * x2[k];
     s = s + P[P_BOUT + r];
     if (r == 0 || s > bv) {  // Eigen maxCoeff: first index of the maximum
       bv = s;
@@ -254,17 +261,20 @@ __device__ int nn_forward(const float* __restrict__ P, const uint32_t (&e)[8], u
 }
 
 __global__ __launch_bounds__(kBlock) void k_nn_tail(BatchArgs a, WorkBufs w,
-                                                    const float* __restrict__ nnp, int state_in) {
+                                                    const float* __restrict__ nnp_g, int state_in) {
   __shared__ int32_t wave_tot[kBlock / 64][9];
+  // weights in LDS: every lane reads the same address (broadcast), no scalar-register pressure
+  __shared__ __attribute__((aligned(16))) float nnp[FME_NN_PARAMS + 4];
+  if (a.nn_mode)
+    for (int i = threadIdx.x; i < FME_NN_PARAMS; i += kBlock) nnp[i] = nnp_g[i];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   constexpr int Q = kJobsPerScanBlock / kBlock;   // consecutive jobs per lane
   const int i0 = blockIdx.x * kJobsPerScanBlock + tid * Q;
 
-  // writer indices of this lane's jobs (inclusive running max)
+  // writer indices of this lane's jobs (inclusive running max over its Q consecutive jobs)
   int run[9];
 #pragma unroll
   for (int f = 0; f < 9; f++) run[f] = -1;
-  int srcs[Q][9];
 #pragma unroll
   for (int q = 0; q < Q; q++) {
     const int i = i0 + q;
@@ -278,8 +288,6 @@ __global__ __launch_bounds__(kBlock) void k_nn_tail(BatchArgs a, WorkBufs w,
         run[8] = i;
       }
     }
-#pragma unroll
-    for (int f = 0; f < 9; f++) srcs[q][f] = run[f];
   }
   // exclusive prefix-max of the lane totals across the block
   int excl[9];
@@ -305,13 +313,23 @@ __global__ __launch_bounds__(kBlock) void k_nn_tail(BatchArgs a, WorkBufs w,
 
   const uint32_t* st_in = w.nn_state + 12 * state_in;
   uint32_t* st_out = w.nn_state + 12 * (state_in ^ 1);
+  int src[9];
 #pragma unroll
+  for (int f = 0; f < 9; f++) src[f] = excl[f];
+#pragma unroll 1
   for (int q = 0; q < Q; q++) {
     const int i = i0 + q;
     if (i >= a.n) break;
-    int src[9];
+    {
+      const fme_job jj = a.jobs[i];
+      if (jj.flags & FME_JOB_EMI) {
+        const int np = emi_pushes(jj);
 #pragma unroll
-    for (int f = 0; f < 9; f++) src[f] = max(srcs[q][f], excl[f]);
+        for (int s = 0; s < 8; s++)
+          if (np > s) src[s] = i;
+        src[8] = i;
+      }
+    }
     const fme_job j = a.jobs[i];
     fme_result* r = a.res + i;
     const double ml = a.mlambda[j.lambda_id];

@@ -22,10 +22,33 @@
 
 #include "fme_device.h"
 
+// Timing-only ablation knob (never set in the product build): bit 0 EMI, 1 planes,
+// 2 half planes, 3 half SATD, 4 quarter SATD, 5 staging.
+#ifndef FME_SKIP
+#define FME_SKIP 0
+#endif
+// Diagnostic build only: per-phase s_memtime deltas of lane 0, summed over workgroups.
+#ifndef FME_STAMPS
+#define FME_STAMPS 0
+#endif
+// Tuning knobs: LDS budget per workgroup (KB) of the 256- and 512-lane kernels, and tiles per
+// workgroup (> 1 turns on the software-pipelined tile loop).
+#ifndef FME_SMALL_BUDGET_KB
+#define FME_SMALL_BUDGET_KB 24
+#endif
+#ifndef FME_LARGE_BUDGET_KB
+#define FME_LARGE_BUDGET_KB 76
+#endif
+#ifndef FME_TILES_PER_BLOCK
+#define FME_TILES_PER_BLOCK 1
+#endif
+
 namespace fme {
 
 typedef short v2s __attribute__((ext_vector_type(2)));
 typedef unsigned short v2u __attribute__((ext_vector_type(2)));
+
+__device__ unsigned long long g_fme_stamps[16];
 
 namespace {
 
@@ -78,7 +101,45 @@ __device__ __forceinline__ uint32_t funnel16(uint32_t hi, uint32_t lo) {
   return __builtin_amdgcn_alignbit(hi, lo, 16u);
 }
 __device__ __forceinline__ uint32_t lds32(const uint8_t* p) { return *reinterpret_cast<const uint32_t*>(p); }
+// Global loads through pointers the compiler cannot classify (e.g. read from an LDS table):
+// address space 1 makes them global_load (vmcnt only, in order) instead of flat_load, which
+// forces s_waitcnt vmcnt(0) lgkmcnt(0) at every control-flow join.
+typedef __attribute__((address_space(1))) const uint32_t gu32c;
+typedef __attribute__((address_space(1))) const uint8_t gu8c;
+__device__ __forceinline__ uint32_t gld32(const void* p) { return *(gu32c*)(p); }
+__device__ __forceinline__ uint32_t gld8(const void* p) { return *(gu8c*)(p); }
 __device__ __forceinline__ void sts32(uint8_t* p, uint32_t v) { *reinterpret_cast<uint32_t*>(p) = v; }
+
+// 4x4 byte transpose: r[i] holds row i (byte j = column j); c[j] = column j (byte i = row i).
+__device__ __forceinline__ void transpose4x4(const uint32_t (&r)[4], uint32_t (&c)[4]) {
+  const uint32_t a = __builtin_amdgcn_perm(r[1], r[0], 0x05010400u);
+  const uint32_t b = __builtin_amdgcn_perm(r[1], r[0], 0x07030602u);
+  const uint32_t d = __builtin_amdgcn_perm(r[3], r[2], 0x05010400u);
+  const uint32_t e = __builtin_amdgcn_perm(r[3], r[2], 0x07030602u);
+  c[0] = __builtin_amdgcn_perm(d, a, 0x05040100u);
+  c[1] = __builtin_amdgcn_perm(d, a, 0x07060302u);
+  c[2] = __builtin_amdgcn_perm(e, b, 0x05040100u);
+  c[3] = __builtin_amdgcn_perm(e, b, 0x07060302u);
+}
+
+// Four picture bytes at (x, y) .. (x+3, y) with edge replication (TComPicYuv::extendPicBorder
+// semantics), branch-free: the 4-byte run xa = clamp(x, 0, W-4) is read with at most two
+// aligned dword loads, then v_perm picks byte clamp(x+i, 0, W-1) - xa for lane byte i.
+// Needs width >= 4 (HEVC luma width is a multiple of 8).
+__device__ __forceinline__ uint32_t pic4(const uint8_t* luma, int stride, int width, int height, int x, int y) {
+  const int yc = clamp_i(y, 0, height - 1);
+  const int xa = clamp_i(x, 0, width - 4);
+  const uintptr_t addr = reinterpret_cast<uintptr_t>(luma + (size_t)yc * stride + xa);
+  const uint32_t sh = (uint32_t)(addr & 3);
+  const uint32_t* q = reinterpret_cast<const uint32_t*>(addr & ~(uintptr_t)3);
+  const uint32_t lo = gld32(q);
+  const uint32_t hi = gld32(sh ? q + 1 : q);      // second dword only when the run straddles
+  const uint32_t run = funnel8(hi, lo, sh);       // pixels xa .. xa+3
+  uint32_t sel = 0;
+#pragma unroll
+  for (int i = 0; i < 4; i++) sel |= (uint32_t)(clamp_i(x + i, 0, width - 1) - xa) << (8 * i);
+  return __builtin_amdgcn_perm(0u, run, sel);
+}
 
 // Luma taps as packed int8 quads (t0..t3, t4..t7) and int16 pairs (TComInterpolationFilter.cpp:57-63).
 __device__ __forceinline__ uint32_t q8(int a, int b, int c, int d) {
@@ -170,7 +231,8 @@ struct PuInfo {
   double ml;
   uint32_t acc[9];
   uint32_t acc_q[9];
-  uint32_t pad1[4];
+  uint32_t cost_e[9];      // EMI: MV cost of each integer position (cost scale 2)
+  uint32_t pad1[3];
 };
 static_assert(sizeof(PuInfo) % 16 == 0, "PuInfo alignment");
 
@@ -187,7 +249,7 @@ struct Lay {
   static constexpr int QS = align_up(H + 1, 8) + 8;    // half-pred byte planes column stride
   static constexpr int O_WINR = 0;
   static constexpr int O_WINC = align_up(O_WINR + WR * RS, 16);
-  static constexpr int O_KEY = align_up(O_WINC + WC * CSB, 16);
+  static constexpr int O_KEY = align_up(O_WINC + align_up(WC, 4) * CSB, 16);   // transposes write align4(WC) columns
   static constexpr int O_PL = align_up(O_KEY + W * H * 2, 16);
   static constexpr int PLANE_B = PC * CS * 2;
   static constexpr int O_Q22 = align_up(O_PL + 3 * PLANE_B + 32, 16);
@@ -196,14 +258,17 @@ struct Lay {
   static constexpr int BYTES = align_up(O_Q02 + PC * QS + 16, 16);
 };
 
-// Dynamic LDS of a tile: [PuInfo x P][quarter work lists 3 x 8P int32][counts x4][PU regions x P]
+// Dynamic LDS of a tile: [PuInfo x 2P][quarter work lists 3 x 8P int32][counts x4][PU regions x P]
 template <int W, int H, int NT, int BUDGET>
 struct Tile {
   using L = Lay<W, H>;
-  static constexpr int PER_PU = L::BYTES + (int)sizeof(PuInfo) + 3 * 8 * 4;
-  static constexpr int P0 = (BUDGET - 16) / PER_PU;
+  static constexpr int PER_PU = L::BYTES + 2 * (int)sizeof(PuInfo) + 3 * 8 * 4;
+  static constexpr int FIXED = FME_MAX_PICTURES * (int)sizeof(PicDesc) + FME_MAX_LAMBDAS * 8 + 32;
+  static constexpr int P0 = (BUDGET - FIXED) / PER_PU;
   static constexpr int P = P0 < 1 ? 1 : (P0 > 64 ? 64 : P0);
-  static constexpr int O_QLIST = P * (int)sizeof(PuInfo);
+  static constexpr int O_PICS = 2 * P * (int)sizeof(PuInfo);               // PicDesc[64]
+  static constexpr int O_ML = O_PICS + FME_MAX_PICTURES * (int)sizeof(PicDesc);   // double[64]
+  static constexpr int O_QLIST = O_ML + FME_MAX_LAMBDAS * 8;
   static constexpr int O_QCOUNT = O_QLIST + 3 * 8 * P * 4;
   static constexpr int O_REGION = align_up(O_QCOUNT + 16, 16);
   static constexpr size_t LDS = (size_t)O_REGION + (size_t)P * L::BYTES;
@@ -275,447 +340,614 @@ __device__ __forceinline__ void vert_s8(const uint8_t* base, int off, uint32_t c
 }  // namespace
 
 // =============================================================================================
-// The tile body.
+// The tile loop: one workgroup owns tiles tile0, tile0 + stride, ... of one PU shape.  While
+// tile t is searched, tile t+stride's descriptors and reference/key samples are in flight in
+// registers (issued after the EMI phase, stored to LDS after the quarter stage).
 // =============================================================================================
 template <int W, int H, int NT, int BUDGET>
-__device__ __forceinline__ void search_tile2(const BatchArgs& a, const int32_t* perm, int first, int count, char* lds) {
+struct Pipe {
+  using L = Lay<W, H>;
+  static constexpr int P = Tile<W, H, NT, BUDGET>::P;
+  static constexpr int G = (L::WC + 3) / 4;                 // 4-sample groups per window row
+  static constexpr int NWIN = P * L::WR * G;                 // window loads per tile
+  static constexpr int UW = (NWIN + NT - 1) / NT;            // per lane
+  static constexpr int NKEY = P * (W / 4) * (H / 4);         // 4x4 key blocks per tile
+  static constexpr int UK = (NKEY + NT - 1) / NT;
+};
+
+// Fill a descriptor from a (class-sorted) job.
+__device__ __forceinline__ void fill_info(PuInfo& in, const fme_job& j, int jid, const BatchArgs& a,
+                                          const double* ml) {
+  in.job = jid;
+  in.flags = j.flags;
+  in.x = j.x;
+  in.y = j.y;
+  in.ref = j.ref_id;
+  in.org = j.org_id;
+  in.key_off = j.key_offset;
+  in.wx0 = (int)j.x + j.mv_x - 5;
+  in.wy0 = (int)j.y + j.mv_y - 5;
+  in.mvx = j.mv_x;
+  in.mvy = j.mv_y;
+  in.ex = in.ey = 0;
+  in.mvp_x = j.mvp_x;
+  in.mvp_y = j.mvp_y;
+  in.lt_x = j.lt_x;
+  in.lt_y = j.lt_y;
+  in.rb_x = j.rb_x;
+  in.rb_y = j.rb_y;
+  in.had = (a.use_hadamard && !(j.flags & FME_JOB_LOSSLESS)) ? 1 : 0;
+  in.hx = in.hy = 0;
+  in.ml = ml[j.lambda_id];
+#pragma unroll
+  for (int k = 0; k < 9; k++) in.acc[k] = in.acc_q[k] = 0;
+}
+
+template <int W, int H, int NT, int BUDGET>
+__device__ __forceinline__ void search_class(const BatchArgs& a, const fme_job* __restrict__ sjobs,
+                                             const int32_t* __restrict__ perm, int cls_off, int cls_cnt,
+                                             int tile0, int stride, char* lds) {
   using L = Lay<W, H>;
   using TL = Tile<W, H, NT, BUDGET>;
+  using PP = Pipe<W, H, NT, BUDGET>;
   constexpr int T = L::T;
   constexpr int P = TL::P;
-  PuInfo* info = reinterpret_cast<PuInfo*>(lds);
+  PuInfo* infos = reinterpret_cast<PuInfo*>(lds);                     // [2][P] (double-buffered)
   int32_t* qlist = reinterpret_cast<int32_t*>(lds + TL::O_QLIST);     // [3][8P]
   int32_t* qcount = reinterpret_cast<int32_t*>(lds + TL::O_QCOUNT);   // [3]
   uint8_t* region0 = reinterpret_cast<uint8_t*>(lds + TL::O_REGION);
+  PicDesc* lpics = reinterpret_cast<PicDesc*>(lds + TL::O_PICS);
+  double* lml = reinterpret_cast<double*>(lds + TL::O_ML);
   auto R = [&](int p) { return region0 + (size_t)p * L::BYTES; };
   const int tid = threadIdx.x;
+  const int ntiles = (cls_cnt + P - 1) / P;
+  if (tile0 >= ntiles) return;
+  // picture and motion-lambda tables in LDS (read per sample / per PU below)
+  if (tid < FME_MAX_PICTURES) lpics[tid] = a.pics[tid];
+  if (tid < FME_MAX_LAMBDAS) lml[tid] = a.mlambda[tid];
+  unsigned long long stamp[11], pst[4];
+  if (FME_STAMPS && threadIdx.x == 0) stamp[0] = __builtin_amdgcn_s_memtime();
 
-  // ---- 0. descriptors ----------------------------------------------------------------------
-  if (tid < P) {
-    PuInfo& in = info[tid];
-    if (tid < count) {
-      const int jid = perm[first + tid];
-      const fme_job j = a.jobs[jid];
-      in.job = jid;
-      in.flags = j.flags;
-      in.x = j.x;
-      in.y = j.y;
-      in.ref = j.ref_id;
-      in.org = j.org_id;
-      in.key_off = j.key_offset;
-      in.wx0 = (int)j.x + j.mv_x - 5;
-      in.wy0 = (int)j.y + j.mv_y - 5;
-      in.mvx = j.mv_x;
-      in.mvy = j.mv_y;
-      in.ex = in.ey = 0;
-      in.mvp_x = j.mvp_x;
-      in.mvp_y = j.mvp_y;
-      in.lt_x = j.lt_x;
-      in.lt_y = j.lt_y;
-      in.rb_x = j.rb_x;
-      in.rb_y = j.rb_y;
-      in.had = (a.use_hadamard && !(j.flags & FME_JOB_LOSSLESS)) ? 1 : 0;
-      in.hx = in.hy = 0;
-      in.ml = a.mlambda[j.lambda_id];
-    } else {
-      in.job = -1;
-      in.flags = 0;
-    }
+  // ---- staging helpers ---------------------------------------------------------------------
+  uint32_t wreg[PP::UW];
+  uint32_t kreg[PP::UK][4];
+  auto issue_loads = [&](const PuInfo* inf, int cnt, int tid) {
 #pragma unroll
-    for (int k = 0; k < 9; k++) in.acc[k] = in.acc_q[k] = 0;
-  }
-  __syncthreads();
-
-  // ---- 1. stage the window (row- and column-major, int8 s-128) and the key ------------------
-  for (int e = tid; e < count * L::WR * L::WC; e += NT) {
-    const int p = e / (L::WR * L::WC), rem = e - p * (L::WR * L::WC);
-    const int r = rem / L::WC, c = rem - r * L::WC;
-    const PuInfo& in = info[p];
-    const PicDesc pd = a.pics[in.ref];
-    const int ax = clamp_i(in.wx0 + c, 0, pd.width - 1);
-    const int ay = clamp_i(in.wy0 + r, 0, pd.height - 1);
-    const uint8_t v = pd.luma[(size_t)ay * pd.stride + ax] ^ 0x80u;
-    uint8_t* base = R(p);
-    base[L::O_WINR + r * L::RS + c] = v;
-    base[L::O_WINC + c * L::CSB + r] = v;
-  }
-  for (int e = tid; e < count * W * H; e += NT) {
-    const int p = e / (W * H), rem = e - p * (W * H);
-    const int r = rem / W, c = rem - r * W;
-    const PuInfo& in = info[p];
-    int16_t v;
-    if (in.key_off >= 0) {
-      v = a.keys[(size_t)in.key_off + rem];
-    } else {
-      const PicDesc pd = a.pics[in.org];
-      v = pd.luma[(size_t)(in.y + r) * pd.stride + in.x + c];
-    }
-    reinterpret_cast<int16_t*>(R(p) + L::O_KEY)[c * H + r] = v;
-  }
-  __syncthreads();
-
-  // ---- 2. EMI: integer distortion of centre + 8 neighbours, per key column -------------------
-  // Metric of the modified setDistParam (TComRdCost.cpp:200-230): SSE for W in {4,8,16,32,64},
-  // SAD for 12/24/48 over even rows only when FEN is 1 or 3 and H > 8 (TEncSearch.cpp:1158-1164).
-  constexpr bool kSad = (W == 12 || W == 24 || W == 48);
-  const int sub = (kSad && (a.fen == 1 || a.fen == 3) && H > 8) ? 1 : 0;
-  for (int e = tid; e < count * 9 * W; e += NT) {
-    const int p = e / (9 * W), rem = e - p * 9 * W;
-    const int pos = rem / W, c = rem - pos * W;
-    const PuInfo& in = info[p];
-    if (!(in.flags & FME_JOB_EMI)) continue;
-    const int dx = pos == 0 ? 0 : ((pos == 1 || pos == 4 || pos == 6) ? -1 : ((pos == 2 || pos == 7) ? 0 : 1));
-    const int dy = pos == 0 ? 0 : (pos <= 3 ? -1 : (pos <= 5 ? 0 : 1));
-    const uint8_t* base = R(p);
-    const uint8_t* kc = base + L::O_KEY + c * H * 2;
-    const int off = L::O_WINC + (c + 5 + dx) * L::CSB + 5 + dy;
-    const uint32_t wsel = sub ? 0x00000001u : 0x00010001u;
-    uint32_t s = 0;
-#pragma unroll
-    for (int q = 0; q < H / 4; q++) {
-      uint32_t w4[1];
-      load_bytes<4>(base, off + 4 * q, w4);
-      const uint32_t x = w4[0] ^ 0x80808080u;
-      const uint32_t d0 = pk_sub(lds32(kc + 8 * q), lo_pair(x));
-      const uint32_t d1 = pk_sub(lds32(kc + 8 * q + 4), hi_pair(x));
-      if (kSad) {
-        s = udot2(pk_abs(d0), wsel, s);
-        s = udot2(pk_abs(d1), wsel, s);
-      } else {
-        s = (uint32_t)dot2(d0, d0, (int)s);
-        s = (uint32_t)dot2(d1, d1, (int)s);
+    for (int u = 0; u < PP::UW; u++) {
+      const int e = tid + u * NT;
+      wreg[u] = 0;
+      if (!(FME_SKIP & 32) && e < cnt * L::WR * PP::G) {
+        const int p = e / (L::WR * PP::G), rem = e - p * (L::WR * PP::G);
+        const int r = rem / PP::G, g = rem - r * PP::G;
+        const PicDesc& pd = lpics[inf[p].ref];
+        wreg[u] = pic4(pd.luma, pd.stride, pd.width, pd.height, inf[p].wx0 + 4 * g, inf[p].wy0 + r);
       }
     }
-    atomicAdd(&info[p].acc[pos], s);
-  }
-  __syncthreads();
-  if (tid < count) {
-    PuInfo& in = info[tid];
-    fme_result* r = a.res + in.job;
-    int n_emi = 0;
-    uint32_t cval = 0;
-    if (in.flags & FME_JOB_EMI) {
-      const int sx = in.mvx, sy = in.mvy;
-      uint32_t best = (in.acc[0] << sub) + mv_cost(in.ml, mv_bits(sx, sy, 2, in.mvp_x, in.mvp_y));
-      int bx = sx, by = sy;
-      const bool top = sy - 1 >= in.lt_y, bot = sy + 1 <= in.rb_y;
-      const bool left = sx - 1 >= in.lt_x, right = sx + 1 <= in.rb_x;
 #pragma unroll
-      for (int pos = 1; pos <= 8; pos++) {
-        const int dx = (pos == 1 || pos == 4 || pos == 6) ? -1 : ((pos == 2 || pos == 7) ? 0 : 1);
-        const int dy = pos <= 3 ? -1 : (pos <= 5 ? 0 : 1);
-        const bool ok = (dy == -1 ? top : (dy == 1 ? bot : true)) && (dx == -1 ? left : (dx == 1 ? right : true));
-        if (!ok) continue;
-        uint32_t d = in.acc[pos] << sub;
-        r->emi[n_emi++] = d;
-        if (d < best) {
-          d += mv_cost(in.ml, mv_bits(sx + dx, sy + dy, 2, in.mvp_x, in.mvp_y));
-          if (d < best) {
-            best = d;
-            bx = sx + dx;
-            by = sy + dy;
+    for (int u = 0; u < PP::UK; u++) {
+      const int e = tid + u * NT;
+      if (!(FME_SKIP & 32) && e < cnt * (W / 4) * (H / 4)) {
+        const int p = e / ((W / 4) * (H / 4)), rem = e - p * ((W / 4) * (H / 4));
+        const int rb = rem / (W / 4), cb = rem - rb * (W / 4);
+        const PuInfo& in = inf[p];
+        if (in.key_off < 0) {   // bi-pred key blocks (int16) are read at store time
+          const PicDesc& pd = lpics[in.org];
+#pragma unroll
+          for (int i = 0; i < 4; i++) {
+            const uint8_t* q = pd.luma + (size_t)(in.y + 4 * rb + i) * pd.stride + in.x + 4 * cb;
+            const uintptr_t addr = reinterpret_cast<uintptr_t>(q);
+            kreg[u][i] = (addr & 3) == 0 ? gld32(q)
+                                         : (gld8(q) | (gld8(q + 1) << 8) | (gld8(q + 2) << 16) | (gld8(q + 3) << 24));
           }
         }
       }
-      cval = best - mv_cost(in.ml, mv_bits(bx, by, 2, in.mvp_x, in.mvp_y));
-      in.ex = bx - sx;
-      in.ey = by - sy;
-      in.mvx = bx;
-      in.mvy = by;
     }
-    for (int k = n_emi; k < 8; k++) r->emi[k] = 0;
-    r->n_emi = (uint8_t)n_emi;
-    r->c = cval;
-    r->mv_int_x = (int16_t)in.mvx;
-    r->mv_int_y = (int16_t)in.mvy;
-  }
-  __syncthreads();
-
-  // ---- 3. first-stage planes fx = 1,2,3 (column-major int16), 4 columns x 8 rows per item ---
-  {
-    constexpr int NG = (L::PC + 3) / 4, NCH = (L::PR + 7) / 8;
-    uint32_t tl[3], th[3];
-    taps8(1, tl[0], th[0]);
-    taps8(2, tl[1], th[1]);
-    taps8(3, tl[2], th[2]);
-    for (int e = tid; e < count * NG * NCH; e += NT) {
-      const int p = e / (NG * NCH), rem = e - p * (NG * NCH);
-      const int ch = rem / NG, g = rem - ch * NG;   // columns fastest: neighbouring lanes, neighbouring bytes
-      const PuInfo& in = info[p];
+  };
+  auto store_loads = [&](const PuInfo* inf, int cnt, int tid) {
+#pragma unroll
+    for (int u = 0; u < PP::UW; u++) {
+      const int e = tid + u * NT;
+      if (e < cnt * L::WR * PP::G) {
+        const int p = e / (L::WR * PP::G), rem = e - p * (L::WR * PP::G);
+        const int r = rem / PP::G, g = rem - r * PP::G;
+        sts32(R(p) + L::O_WINR + r * L::RS + 4 * g, wreg[u] ^ 0x80808080u);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < PP::UK; u++) {
+      const int e = tid + u * NT;
+      if (e < cnt * (W / 4) * (H / 4)) {
+        const int p = e / ((W / 4) * (H / 4)), rem = e - p * ((W / 4) * (H / 4));
+        const int rb = rem / (W / 4), cb = rem - rb * (W / 4);
+        uint8_t* kb = R(p) + L::O_KEY;
+        if (inf[p].key_off >= 0) {
+          const int16_t* src = a.keys + (size_t)inf[p].key_off + (4 * rb) * W + 4 * cb;
+#pragma unroll
+          for (int j = 0; j < 4; j++) {
+            uint8_t* dst = kb + ((4 * cb + j) * H + 4 * rb) * 2;
+            sts32(dst, (uint32_t)(uint16_t)src[j] | ((uint32_t)(uint16_t)src[W + j] << 16));
+            sts32(dst + 4, (uint32_t)(uint16_t)src[2 * W + j] | ((uint32_t)(uint16_t)src[3 * W + j] << 16));
+          }
+        } else {
+          uint32_t rows[4] = {kreg[u][0], kreg[u][1], kreg[u][2], kreg[u][3]}, cols[4];
+          transpose4x4(rows, cols);
+#pragma unroll
+          for (int j = 0; j < 4; j++) {
+            uint8_t* dst = kb + ((4 * cb + j) * H + 4 * rb) * 2;
+            sts32(dst, lo_pair(cols[j]));
+            sts32(dst + 4, hi_pair(cols[j]));
+          }
+        }
+      }
+    }
+  };
+  auto transpose_window = [&](int cnt, int tid) {
+    constexpr int RG = (L::WR + 3) / 4, CG = (L::WC + 3) / 4;
+    const int total = (FME_SKIP & 32) ? 0 : cnt * RG * CG;
+    for (int e = tid; e < total; e += NT) {
+      const int p = e / (RG * CG), rem = e - p * (RG * CG);
+      const int rg = rem / CG, cg = rem - rg * CG;
       uint8_t* base = R(p);
+      uint32_t rows[4], cols[4];
 #pragma unroll
-      for (int rr = 0; rr < 8; rr += 2) {
-        uint32_t out[4][3][2];
+      for (int i = 0; i < 4; i++) rows[i] = lds32(base + L::O_WINR + (4 * rg + i) * L::RS + 4 * cg);
+      transpose4x4(rows, cols);
 #pragma unroll
-        for (int h = 0; h < 2; h++) {
-          const int pr = ch * 8 + rr + h;
-          const int row = min(1 + in.ey + pr, L::WR - 1);
-          const int off = L::O_WINR + row * L::RS + 1 + in.ex + 4 * g;
-          const uint8_t* q = base + (off & ~3);
-          const uint32_t sh = (uint32_t)(off & 3);
-          uint32_t w[4];
+      for (int j = 0; j < 4; j++) sts32(base + L::O_WINC + (4 * cg + j) * L::CSB + 4 * rg, cols[j]);
+    }
+  };
+
+  // ---- prologue: the first tile ---------------------------------------------------------------
+  int cur = 0;
+  int t = tile0;
+  int count = min(P, cls_cnt - t * P);
+  {
+    fme_job j0{};
+    int id0 = -1;
+    if (tid < count) {
+      const int k = cls_off + t * P + tid;
+      j0 = sjobs[k];
+      id0 = perm[k];
+    }
+    __syncthreads();   // tables visible
+    if (FME_STAMPS && threadIdx.x == 0) pst[0] = __builtin_amdgcn_s_memtime();
+    if (tid < P) {
+      if (tid < count) {
+        fill_info(infos[tid], j0, id0, a, lml);
+      } else {
+        infos[tid].job = -1;
+        infos[tid].flags = 0;
+      }
+    }
+  }
+  __syncthreads();
+  if (FME_STAMPS && threadIdx.x == 0) pst[1] = __builtin_amdgcn_s_memtime();
+  issue_loads(infos, count, tid);
+  store_loads(infos, count, tid);
+  if (FME_STAMPS && threadIdx.x == 0) pst[2] = __builtin_amdgcn_s_memtime();
+  __syncthreads();
+  if (FME_STAMPS && threadIdx.x == 0) pst[3] = __builtin_amdgcn_s_memtime();
+  transpose_window(count, tid);
+  __syncthreads();
+  if (FME_STAMPS && threadIdx.x == 0) stamp[1] = __builtin_amdgcn_s_memtime();
+
+  for (;;) {
+    // an opaque copy of the lane id per iteration keeps LICM from hoisting the per-lane index
+    // arithmetic of every phase out of the tile loop (and keeping it live in VGPRs)
+    int tid = threadIdx.x;
+    asm volatile("" : "+v"(tid));
+    PuInfo* info = infos + cur * P;
+    PuInfo* info_n = infos + (cur ^ 1) * P;
+    const int tn = t + stride;
+    const int count_n = (FME_TILES_PER_BLOCK > 1 && tn < ntiles) ? min(P, cls_cnt - tn * P) : 0;
+    // next tile's descriptors: issued now, consumed after the EMI phase
+    fme_job nj{};
+    int nid = -1;
+    if (tid < count_n) {
+      const int k = cls_off + tn * P + tid;
+      nj = sjobs[k];
+      nid = perm[k];
+    }
+
+    // ---- 2. EMI: integer distortion of centre + 8 neighbours, per key column ----------------
+    // Metric of the modified setDistParam (TComRdCost.cpp:200-230): SSE for W in {4,8,16,32,64},
+    // SAD for 12/24/48 over even rows only when FEN is 1 or 3 and H > 8 (TEncSearch.cpp:1158-1164).
+    constexpr bool kSad = (W == 12 || W == 24 || W == 48);
+    const int sub = (kSad && (a.fen == 1 || a.fen == 3) && H > 8) ? 1 : 0;
+    for (int e = tid; e < ((FME_SKIP & 1) ? 0 : count * 9 * W); e += NT) {
+      const int p = e / (9 * W), rem = e - p * 9 * W;
+      const int pos = rem / W, c = rem - pos * W;
+      const PuInfo& in = info[p];
+      if (!(in.flags & FME_JOB_EMI)) continue;
+      const int dx = pos == 0 ? 0 : ((pos == 1 || pos == 4 || pos == 6) ? -1 : ((pos == 2 || pos == 7) ? 0 : 1));
+      const int dy = pos == 0 ? 0 : (pos <= 3 ? -1 : (pos <= 5 ? 0 : 1));
+      const uint8_t* base = R(p);
+      const uint8_t* kc = base + L::O_KEY + c * H * 2;
+      const int off = L::O_WINC + (c + 5 + dx) * L::CSB + 5 + dy;
+      const uint32_t wsel = sub ? 0x00000001u : 0x00010001u;
+      uint32_t s = 0;
 #pragma unroll
-          for (int j = 0; j < 4; j++) w[j] = lds32(q + 4 * j);
-          uint32_t d[8];
+      for (int q = 0; q < H / 4; q++) {
+        uint32_t w4[1];
+        load_bytes<4>(base, off + 4 * q, w4);
+        const uint32_t x = w4[0] ^ 0x80808080u;
+        const uint32_t d0 = pk_sub(lds32(kc + 8 * q), lo_pair(x));
+        const uint32_t d1 = pk_sub(lds32(kc + 8 * q + 4), hi_pair(x));
+        if (kSad) {
+          s = udot2(pk_abs(d0), wsel, s);
+          s = udot2(pk_abs(d1), wsel, s);
+        } else {
+          s = (uint32_t)dot2(d0, d0, (int)s);
+          s = (uint32_t)dot2(d1, d1, (int)s);
+        }
+      }
+      atomicAdd(&info[p].acc[pos], s);
+      if (c == 0)
+        info[p].cost_e[pos] = mv_cost(in.ml, mv_bits(in.mvx + dx, in.mvy + dy, 2, in.mvp_x, in.mvp_y));
+    }
+    __syncthreads();
+    if (FME_STAMPS && threadIdx.x == 0) stamp[2] = __builtin_amdgcn_s_memtime();
+    if (tid < 3) qcount[tid] = 0;
+    if (tid < count) {
+      PuInfo& in = info[tid];
+      fme_result* r = (FME_SKIP & 128) ? reinterpret_cast<fme_result*>(lds + TL::O_QLIST) : a.res + in.job;
+      int n_emi = 0;
+      uint32_t cval = 0;
+      if (in.flags & FME_JOB_EMI) {
+        const int sx = in.mvx, sy = in.mvy;
+        uint32_t best = (in.acc[0] << sub) + in.cost_e[0];
+        int bx = sx, by = sy, bpos = 0;
+        const bool top = sy - 1 >= in.lt_y, bot = sy + 1 <= in.rb_y;
+        const bool left = sx - 1 >= in.lt_x, right = sx + 1 <= in.rb_x;
 #pragma unroll
-          for (int m = 0; m < 8; m++) {
-            const uint32_t x = sh + (uint32_t)(m & 3);
-            const int qd = m >> 2;
-            d[m] = x >= 4 ? funnel8(w[qd + 2], w[qd + 1], x - 4) : funnel8(w[qd + 1], w[qd], x);
+        for (int pos = 1; pos <= 8; pos++) {
+          const int dx = (pos == 1 || pos == 4 || pos == 6) ? -1 : ((pos == 2 || pos == 7) ? 0 : 1);
+          const int dy = pos <= 3 ? -1 : (pos <= 5 ? 0 : 1);
+          const bool ok = (dy == -1 ? top : (dy == 1 ? bot : true)) && (dx == -1 ? left : (dx == 1 ? right : true));
+          if (!ok) continue;
+          uint32_t d = in.acc[pos] << sub;
+          r->emi[n_emi++] = d;
+          if (d < best) {
+            d += in.cost_e[pos];
+            if (d < best) {
+              best = d;
+              bx = sx + dx;
+              by = sy + dy;
+              bpos = pos;
+            }
+          }
+        }
+        cval = best - in.cost_e[bpos];
+        in.ex = bx - sx;
+        in.ey = by - sy;
+        in.mvx = bx;
+        in.mvy = by;
+      }
+      for (int k = n_emi; k < 8; k++) r->emi[k] = 0;
+      r->n_emi = (uint8_t)n_emi;
+      r->c = cval;
+      r->mv_int_x = (int16_t)in.mvx;
+      r->mv_int_y = (int16_t)in.mvy;
+    }
+    if (tid < P) {
+      if (tid < count_n) {
+        fill_info(info_n[tid], nj, nid, a, lml);
+      } else {
+        info_n[tid].job = -1;
+        info_n[tid].flags = 0;
+      }
+    }
+    __syncthreads();
+    if (FME_STAMPS && threadIdx.x == 0) stamp[3] = __builtin_amdgcn_s_memtime();
+    // next tile's samples: in flight through the rest of this tile
+    issue_loads(info_n, count_n, tid);
+
+    // ---- 3. first-stage planes fx = 1,2,3 (column-major int16), 4 columns x 8 rows per item -
+    {
+      constexpr int NG = (L::PC + 3) / 4, NCH = (L::PR + 7) / 8;
+      uint32_t tl[3], th[3];
+      taps8(1, tl[0], th[0]);
+      taps8(2, tl[1], th[1]);
+      taps8(3, tl[2], th[2]);
+      for (int e = tid; e < ((FME_SKIP & 2) ? 0 : count * NG * NCH); e += NT) {
+        const int p = e / (NG * NCH), rem = e - p * (NG * NCH);
+        const int ch = rem / NG, g = rem - ch * NG;
+        const PuInfo& in = info[p];
+        uint8_t* base = R(p);
+#pragma unroll
+        for (int rr = 0; rr < 8; rr += 2) {
+          uint32_t out[4][3][2];
+#pragma unroll
+          for (int h = 0; h < 2; h++) {
+            const int pr = ch * 8 + rr + h;
+            const int row = min(1 + in.ey + pr, L::WR - 1);
+            const int off = L::O_WINR + row * L::RS + 1 + in.ex + 4 * g;
+            const uint8_t* q = base + (off & ~3);
+            const uint32_t sh = (uint32_t)(off & 3);
+            uint32_t w[4];
+#pragma unroll
+            for (int j = 0; j < 4; j++) w[j] = lds32(q + 4 * j);
+            uint32_t d[8];
+#pragma unroll
+            for (int m = 0; m < 8; m++) {
+              const uint32_t x = sh + (uint32_t)(m & 3);
+              const int qd = m >> 2;
+              d[m] = x >= 4 ? funnel8(w[qd + 2], w[qd + 1], x - 4) : funnel8(w[qd + 1], w[qd], x);
+            }
+#pragma unroll
+            for (int i = 0; i < 4; i++)
+#pragma unroll
+              for (int f = 0; f < 3; f++) out[i][f][h] = (uint32_t)dot4(d[i + 4], th[f], dot4(d[i], tl[f], 0));
           }
 #pragma unroll
-          for (int i = 0; i < 4; i++)
+          for (int i = 0; i < 4; i++) {
+            const int pc = 4 * g + i;
+            if (pc < L::PC && ch * 8 + rr < L::PR) {
 #pragma unroll
-            for (int f = 0; f < 3; f++) out[i][f][h] = (uint32_t)dot4(d[i + 4], th[f], dot4(d[i], tl[f], 0));
-        }
-#pragma unroll
-        for (int i = 0; i < 4; i++) {
-          const int pc = 4 * g + i;
-          if (pc < L::PC && ch * 8 + rr < L::PR) {
-#pragma unroll
-            for (int f = 0; f < 3; f++) {
-              uint8_t* col = base + L::O_PL + f * L::PLANE_B + pc * L::CS * 2;
-              sts32(col + (ch * 8 + rr) * 2, (out[i][f][0] & 0xffffu) | (out[i][f][1] << 16));
+              for (int f = 0; f < 3; f++) {
+                uint8_t* col = base + L::O_PL + f * L::PLANE_B + pc * L::CS * 2;
+                sts32(col + (ch * 8 + rr) * 2, (out[i][f][0] & 0xffffu) | (out[i][f][1] << 16));
+              }
             }
           }
         }
       }
     }
-  }
-  __syncthreads();
+    __syncthreads();
 
-  // ---- 4a. half-pel prediction planes (8-bit, column-major) ----------------------------------
-  // Q22 = [2][2]: vertical half over plane fx=2, cols -1..W-1, rows -1..H-1
-  // Q20 = [2][0]: vertical half over integer columns (bytes), cols 0..W-1, rows -1..H-1
-  // Q02 = [0][2]: plane fx=2 rounded, cols -1..W-1, rows 0..H-1
-  {
-    constexpr int NCH = (H + 1 + 7) / 8;     // Q22 / Q20 row chunks
-    constexpr int NCH2 = (H + 7) / 8;        // Q02 row chunks
-    constexpr int N22 = L::PC * NCH, N20 = W * NCH, N02 = L::PC * NCH2;
-    uint32_t c2[4];
-    taps16(2, c2);
-    uint32_t c2lo, c2hi;
-    taps8(2, c2lo, c2hi);
-    for (int e = tid; e < count * (N22 + N20 + N02); e += NT) {
-      const int p = e / (N22 + N20 + N02);
-      int rem = e - p * (N22 + N20 + N02);
-      const PuInfo& in = info[p];
-      uint8_t* base = R(p);
-      int s[8];
-      uint8_t* dst;
-      if (rem < N22) {
-        const int ch = rem / L::PC, col = rem - ch * L::PC;
-        // outputs rows R = -1 + 8ch + m -> plane rows from R + 1 (taps R-3..R+4 at pr R+1..R+8)
-        vert_i16<8>(base + L::O_PL + 1 * L::PLANE_B + col * L::CS * 2, 8 * ch, c2, s);
+    if (FME_STAMPS && threadIdx.x == 0) stamp[4] = __builtin_amdgcn_s_memtime();
+    // ---- 4a. half-pel prediction planes (8-bit, column-major) --------------------------------
+    // Q22 = [2][2]: vertical half over plane fx=2, cols -1..W-1, rows -1..H-1
+    // Q20 = [2][0]: vertical half over integer columns (bytes), cols 0..W-1, rows -1..H-1
+    // Q02 = [0][2]: plane fx=2 rounded, cols -1..W-1, rows 0..H-1
+    {
+      constexpr int NCH = (H + 1 + 7) / 8;
+      constexpr int NCH2 = (H + 7) / 8;
+      constexpr int N22 = L::PC * NCH, N20 = W * NCH, N02 = L::PC * NCH2;
+      uint32_t c2[4];
+      taps16(2, c2);
+      uint32_t c2lo, c2hi;
+      taps8(2, c2lo, c2hi);
+      for (int e = tid; e < ((FME_SKIP & 4) ? 0 : count * (N22 + N20 + N02)); e += NT) {
+        const int p = e / (N22 + N20 + N02);
+        int rem = e - p * (N22 + N20 + N02);
+        const PuInfo& in = info[p];
+        uint8_t* base = R(p);
+        int s[8];
+        uint8_t* dst;
+        if (rem < N22) {
+          const int ch = rem / L::PC, col = rem - ch * L::PC;
+          vert_i16<8>(base + L::O_PL + 1 * L::PLANE_B + col * L::CS * 2, 8 * ch, c2, s);
 #pragma unroll
-        for (int m = 0; m < 8; m++) s[m] = round2d(s[m]);
-        dst = base + L::O_Q22 + col * L::QS + 8 * ch;
-      } else if (rem < N22 + N20) {
-        rem -= N22;
-        const int ch = rem / W, col = rem - ch * W;
-        // integer column col (rel mv_int') = window column col + 5 + ex; rows R-3.. -> window row R+2+ey
-        const int off = L::O_WINC + (col + 5 + in.ex) * L::CSB + (8 * ch - 1) + 2 + in.ey;
-        vert_s8<8>(base, off, c2lo, c2hi, s);
+          for (int m = 0; m < 8; m++) s[m] = round2d(s[m]);
+          dst = base + L::O_Q22 + col * L::QS + 8 * ch;
+        } else if (rem < N22 + N20) {
+          rem -= N22;
+          const int ch = rem / W, col = rem - ch * W;
+          const int off = L::O_WINC + (col + 5 + in.ex) * L::CSB + (8 * ch - 1) + 2 + in.ey;
+          vert_s8<8>(base, off, c2lo, c2hi, s);
 #pragma unroll
-        for (int m = 0; m < 8; m++) s[m] = round1d_s8(s[m]);
-        dst = base + L::O_Q20 + col * L::QS + 8 * ch;
-      } else {
-        rem -= N22 + N20;
-        const int ch = rem / L::PC, col = rem - ch * L::PC;
-        const uint8_t* pcol = base + L::O_PL + 1 * L::PLANE_B + col * L::CS * 2 + (8 * ch + 4) * 2;
+          for (int m = 0; m < 8; m++) s[m] = round1d_s8(s[m]);
+          dst = base + L::O_Q20 + col * L::QS + 8 * ch;
+        } else {
+          rem -= N22 + N20;
+          const int ch = rem / L::PC, col = rem - ch * L::PC;
+          const uint8_t* pcol = base + L::O_PL + 1 * L::PLANE_B + col * L::CS * 2 + (8 * ch + 4) * 2;
 #pragma unroll
-        for (int j = 0; j < 4; j++) {
-          const uint32_t v = lds32(pcol + 4 * j);
-          s[2 * j] = clamp_i(((int)(int16_t)(v & 0xffffu) + 8224) >> 6, 0, 255);
-          s[2 * j + 1] = clamp_i(((int)(int16_t)(v >> 16) + 8224) >> 6, 0, 255);
+          for (int j = 0; j < 4; j++) {
+            const uint32_t v = lds32(pcol + 4 * j);
+            s[2 * j] = clamp_i(((int)(int16_t)(v & 0xffffu) + 8224) >> 6, 0, 255);
+            s[2 * j + 1] = clamp_i(((int)(int16_t)(v >> 16) + 8224) >> 6, 0, 255);
+          }
+          dst = base + L::O_Q02 + col * L::QS + 8 * ch;
         }
-        dst = base + L::O_Q02 + col * L::QS + 8 * ch;
+        sts32(dst, (uint32_t)s[0] | ((uint32_t)s[1] << 8) | ((uint32_t)s[2] << 16) | ((uint32_t)s[3] << 24));
+        sts32(dst + 4, (uint32_t)s[4] | ((uint32_t)s[5] << 8) | ((uint32_t)s[6] << 16) | ((uint32_t)s[7] << 24));
       }
-      sts32(dst, (uint32_t)s[0] | ((uint32_t)s[1] << 8) | ((uint32_t)s[2] << 16) | ((uint32_t)s[3] << 24));
-      sts32(dst + 4, (uint32_t)s[4] | ((uint32_t)s[5] << 8) | ((uint32_t)s[6] << 16) | ((uint32_t)s[7] << 24));
     }
-  }
-  __syncthreads();
+    __syncthreads();
 
-  // ---- 4b. half-pel SATD: 9 candidates x tiles ------------------------------------------------
-  {
-    const int items = count * L::TILES;
-    for (int e = tid; e < 9 * items; e += NT) {
-      const int k = e / items, rem = e - k * items;
-      const int p = rem / L::TILES, t = rem - p * L::TILES;
-      const PuInfo& in = info[p];
-      const uint8_t* base = R(p);
-      const int ty = t / L::TX, tx = t - ty * L::TX;
-      const int dx = cand_dx(k), dy = half_dy(k);
-      // pred source for (2dx, 2dy): integer / Q20 / Q02 / Q22 (m_filteredBlock plane walk)
-      int colbase, cstride, rowoff;
-      uint32_t flip = 0;
-      if (dx == 0 && dy == 0) {
-        colbase = L::O_WINC + (5 + in.ex) * L::CSB;
-        cstride = L::CSB;
-        rowoff = 5 + in.ey;
-        flip = 0x80808080u;
-      } else if (dx == 0) {
-        colbase = L::O_Q20;
-        cstride = L::QS;
-        rowoff = dy < 0 ? 0 : 1;
-      } else if (dy == 0) {
-        colbase = L::O_Q02 + (dx < 0 ? 0 : 1) * L::QS;
-        cstride = L::QS;
-        rowoff = 0;
-      } else {
-        colbase = L::O_Q22 + (dx < 0 ? 0 : 1) * L::QS;
-        cstride = L::QS;
-        rowoff = dy < 0 ? 0 : 1;
-      }
-      uint32_t X[T][T / 2];
-#pragma unroll
-      for (int c = 0; c < T; c++) {
-        const int col = tx * T + c;
-        uint32_t b[T / 4];
-        load_bytes<T>(base, colbase + col * cstride + rowoff + ty * T, b);
-        const uint8_t* kc = base + L::O_KEY + (col * H + ty * T) * 2;
-#pragma unroll
-        for (int j = 0; j < T / 4; j++) {
-          const uint32_t x = b[j] ^ flip;
-          X[c][2 * j] = pk_sub(lds32(kc + 8 * j), lo_pair(x));
-          X[c][2 * j + 1] = pk_sub(lds32(kc + 8 * j + 4), hi_pair(x));
+    if (FME_STAMPS && threadIdx.x == 0) stamp[5] = __builtin_amdgcn_s_memtime();
+    // ---- 4b. half-pel SATD: 9 candidates x tiles ------------------------------------------------
+    {
+      const int items = count * L::TILES;
+      for (int e = tid; e < ((FME_SKIP & 8) ? 0 : 9 * items); e += NT) {
+        const int k = e / items, rem = e - k * items;
+        const int p = rem / L::TILES, tt = rem - p * L::TILES;
+        const PuInfo& in = info[p];
+        const uint8_t* base = R(p);
+        const int ty = tt / L::TX, tx = tt - ty * L::TX;
+        const int dx = cand_dx(k), dy = half_dy(k);
+        int colbase, cstride, rowoff;
+        uint32_t flip = 0;
+        if (dx == 0 && dy == 0) {
+          colbase = L::O_WINC + (5 + in.ex) * L::CSB;
+          cstride = L::CSB;
+          rowoff = 5 + in.ey;
+          flip = 0x80808080u;
+        } else if (dx == 0) {
+          colbase = L::O_Q20;
+          cstride = L::QS;
+          rowoff = dy < 0 ? 0 : 1;
+        } else if (dy == 0) {
+          colbase = L::O_Q02 + (dx < 0 ? 0 : 1) * L::QS;
+          cstride = L::QS;
+          rowoff = 0;
+        } else {
+          colbase = L::O_Q22 + (dx < 0 ? 0 : 1) * L::QS;
+          cstride = L::QS;
+          rowoff = dy < 0 ? 0 : 1;
         }
-      }
-      const uint32_t dd = in.had ? satd_packed<T>(X) : sad_packed<T>(X);
-      atomicAdd(&info[p].acc_q[k], dd);
-    }
-  }
-  __syncthreads();
-
-  // ---- 4c. half argmin (cost scale 1), quarter work list sorted by code path -------------------
-  if (tid < 3) qcount[tid] = 0;
-  __syncthreads();
-  if (tid < count) {
-    PuInfo& in = info[tid];
-    uint32_t best = 0xFFFFFFFFu;
-    int bi = 0;
-#pragma unroll
-    for (int k = 0; k < 9; k++) {
-      const int hx = 2 * in.mvx + cand_dx(k), hy = 2 * in.mvy + half_dy(k);
-      const uint32_t d = in.acc_q[k] + mv_cost(in.ml, mv_bits(hx, hy, 1, in.mvp_x, in.mvp_y));
-      if (d < best) {
-        best = d;
-        bi = k;
-      }
-    }
-    in.hx = cand_dx(bi);
-    in.hy = half_dy(bi);
-    in.acc[0] = in.acc_q[bi];   // quarter candidate 0 == the best half position
-#pragma unroll
-    for (int k = 1; k < 9; k++) {
-      in.acc[k] = 0;
-      const int qx = 2 * in.hx + cand_dx(k), qy = 2 * in.hy + qtr_dy(k);
-      const int path = (qy & 3) == 0 ? 0 : ((qx & 3) == 0 ? 1 : 2);
-      const int slot = atomicAdd(&qcount[path], 1);
-      qlist[path * 8 * P + slot] = tid * 16 + k;
-    }
-  }
-  __syncthreads();
-
-  // ---- 5. quarter-pel SATD: 8 candidates x tiles, grouped by path ------------------------------
-  {
-    const int n0 = qcount[0] * L::TILES, n1 = qcount[1] * L::TILES, n2 = qcount[2] * L::TILES;
-    for (int e = tid; e < n0 + n1 + n2; e += NT) {
-      int path, idx;
-      if (e < n0) { path = 0; idx = e; }
-      else if (e < n0 + n1) { path = 1; idx = e - n0; }
-      else { path = 2; idx = e - n0 - n1; }
-      const int entry = qlist[path * 8 * P + idx / L::TILES];
-      const int t = idx - (idx / L::TILES) * L::TILES;
-      const int p = entry >> 4, k = entry & 15;
-      const PuInfo& in = info[p];
-      const uint8_t* base = R(p);
-      const int ty = t / L::TX, tx = t - ty * L::TX;
-      const int qx = 2 * in.hx + cand_dx(k), qy = 2 * in.hy + qtr_dy(k);
-      const int ix = qx >> 2, fx = qx & 3, iy = qy >> 2, fy = qy & 3;
-      uint32_t X[T][T / 2];
-      if (path == 0) {
-        // fy == 0 (iy == 0): horizontal only, plane fx rounded (filterCopy !isFirst)
+        uint32_t X[T][T / 2];
 #pragma unroll
         for (int c = 0; c < T; c++) {
           const int col = tx * T + c;
-          const uint8_t* pcol = base + L::O_PL + (fx - 1) * L::PLANE_B + (col + ix + 1) * L::CS * 2 + (ty * T + 4) * 2;
+          uint32_t b[T / 4];
+          load_bytes<T>(base, colbase + col * cstride + rowoff + ty * T, b);
           const uint8_t* kc = base + L::O_KEY + (col * H + ty * T) * 2;
 #pragma unroll
-          for (int j = 0; j < T / 2; j++) {
-            const v2s t16 = up(lds32(pcol + 4 * j));
-            v2s pr = (t16 + (v2s)(8224)) >> (v2s)(6);
-            pr = __builtin_elementwise_min(__builtin_elementwise_max(pr, (v2s)(0)), (v2s)(255));
-            X[c][j] = pk_sub(lds32(kc + 4 * j), pk(pr));
+          for (int j = 0; j < T / 4; j++) {
+            const uint32_t x = b[j] ^ flip;
+            X[c][2 * j] = pk_sub(lds32(kc + 8 * j), lo_pair(x));
+            X[c][2 * j + 1] = pk_sub(lds32(kc + 8 * j + 4), hi_pair(x));
           }
         }
-      } else if (path == 1) {
-        // fx == 0: vertical only on the integer column (bytes)
-        uint32_t clo, chi;
-        taps8(fy, clo, chi);
-#pragma unroll
-        for (int c = 0; c < T; c++) {
-          const int col = tx * T + c;
-          const int off = L::O_WINC + (col + 5 + in.ex) * L::CSB + ty * T + iy + 2 + in.ey;
-          int s[T];
-          vert_s8<T>(base, off, clo, chi, s);
-          const uint8_t* kc = base + L::O_KEY + (col * H + ty * T) * 2;
-#pragma unroll
-          for (int j = 0; j < T / 2; j++) {
-            const uint32_t pr = (uint32_t)round1d_s8(s[2 * j]) | ((uint32_t)round1d_s8(s[2 * j + 1]) << 16);
-            X[c][j] = pk_sub(lds32(kc + 4 * j), pr);
-          }
-        }
-      } else {
-        // 2-D: vertical fy over plane fx
-        uint32_t cv[4];
-        taps16(fy, cv);
-#pragma unroll
-        for (int c = 0; c < T; c++) {
-          const int col = tx * T + c;
-          const uint8_t* pcol = base + L::O_PL + (fx - 1) * L::PLANE_B + (col + ix + 1) * L::CS * 2;
-          int s[T];
-          vert_i16<T>(pcol, ty * T + iy + 1, cv, s);
-          const uint8_t* kc = base + L::O_KEY + (col * H + ty * T) * 2;
-#pragma unroll
-          for (int j = 0; j < T / 2; j++) {
-            const uint32_t pr = (uint32_t)round2d(s[2 * j]) | ((uint32_t)round2d(s[2 * j + 1]) << 16);
-            X[c][j] = pk_sub(lds32(kc + 4 * j), pr);
-          }
-        }
+        uint32_t dd = in.had ? satd_packed<T>(X) : sad_packed<T>(X);
+        if (tt == 0) dd += mv_cost(in.ml, mv_bits(2 * in.mvx + dx, 2 * in.mvy + dy, 1, in.mvp_x, in.mvp_y));
+        atomicAdd(&info[p].acc_q[k], dd);
       }
-      const uint32_t dd = in.had ? satd_packed<T>(X) : sad_packed<T>(X);
-      atomicAdd(&info[p].acc[k], dd);
     }
-  }
-  __syncthreads();
+    __syncthreads();
 
-  // ---- 6. quarter argmin (cost scale 0) and results ---------------------------------------------
-  if (tid < count) {
-    PuInfo& in = info[tid];
-    uint32_t best = 0xFFFFFFFFu;
-    int bi = 0;
+    if (FME_STAMPS && threadIdx.x == 0) stamp[6] = __builtin_amdgcn_s_memtime();
+    // ---- 4c. half argmin (cost scale 1; costs already added), quarter work list by code path --
+    if (tid < count) {
+      PuInfo& in = info[tid];
+      uint32_t best = 0xFFFFFFFFu;
+      int bi = 0;
 #pragma unroll
-    for (int k = 0; k < 9; k++) {
-      const int qx = 4 * in.mvx + 2 * in.hx + cand_dx(k), qy = 4 * in.mvy + 2 * in.hy + qtr_dy(k);
-      const uint32_t d = in.acc[k] + mv_cost(in.ml, mv_bits(qx, qy, 0, in.mvp_x, in.mvp_y));
-      if (d < best) {
-        best = d;
-        bi = k;
+      for (int k = 0; k < 9; k++) {
+        const uint32_t d = in.acc_q[k];
+        if (d < best) {
+          best = d;
+          bi = k;
+        }
+      }
+      in.hx = cand_dx(bi);
+      in.hy = half_dy(bi);
+      in.acc[0] = in.acc_q[bi];   // quarter candidate 0 == the best half position (same bits, same cost)
+#pragma unroll
+      for (int k = 1; k < 9; k++) {
+        in.acc[k] = 0;
+        const int qx = 2 * in.hx + cand_dx(k), qy = 2 * in.hy + qtr_dy(k);
+        const int path = (qy & 3) == 0 ? 0 : ((qx & 3) == 0 ? 1 : 2);
+        const int slot = atomicAdd(&qcount[path], 1);
+        qlist[path * 8 * P + slot] = tid * 16 + k;
       }
     }
-    fme_result* r = a.res + in.job;
-    r->half_x = (int8_t)in.hx;
-    r->half_y = (int8_t)in.hy;
-    r->qtr_x = (int8_t)cand_dx(bi);
-    r->qtr_y = (int8_t)qtr_dy(bi);
-    r->frac_cost = best;
+    __syncthreads();
+
+    if (FME_STAMPS && threadIdx.x == 0) stamp[7] = __builtin_amdgcn_s_memtime();
+    // ---- 5. quarter-pel SATD: 8 candidates x tiles, grouped by path ----------------------------
+    {
+      const int n0 = qcount[0] * L::TILES, n1 = qcount[1] * L::TILES, n2 = qcount[2] * L::TILES;
+      for (int e = tid; e < ((FME_SKIP & 16) ? 0 : n0 + n1 + n2); e += NT) {
+        int path, idx;
+        if (e < n0) { path = 0; idx = e; }
+        else if (e < n0 + n1) { path = 1; idx = e - n0; }
+        else { path = 2; idx = e - n0 - n1; }
+        const int entry = qlist[path * 8 * P + idx / L::TILES];
+        const int tt = idx - (idx / L::TILES) * L::TILES;
+        const int p = entry >> 4, k = entry & 15;
+        const PuInfo& in = info[p];
+        const uint8_t* base = R(p);
+        const int ty = tt / L::TX, tx = tt - ty * L::TX;
+        const int qx = 2 * in.hx + cand_dx(k), qy = 2 * in.hy + qtr_dy(k);
+        const int ix = qx >> 2, fx = qx & 3, iy = qy >> 2, fy = qy & 3;
+        uint32_t X[T][T / 2];
+        if (path == 0) {
+          // fy == 0 (iy == 0): horizontal only, plane fx rounded (filterCopy !isFirst)
+#pragma unroll
+          for (int c = 0; c < T; c++) {
+            const int col = tx * T + c;
+            const uint8_t* pcol = base + L::O_PL + (fx - 1) * L::PLANE_B + (col + ix + 1) * L::CS * 2 + (ty * T + 4) * 2;
+            const uint8_t* kc = base + L::O_KEY + (col * H + ty * T) * 2;
+#pragma unroll
+            for (int j = 0; j < T / 2; j++) {
+              const v2s t16 = up(lds32(pcol + 4 * j));
+              v2s pr = (t16 + (v2s)(8224)) >> (v2s)(6);
+              pr = __builtin_elementwise_min(__builtin_elementwise_max(pr, (v2s)(0)), (v2s)(255));
+              X[c][j] = pk_sub(lds32(kc + 4 * j), pk(pr));
+            }
+          }
+        } else if (path == 1) {
+          // fx == 0: vertical only on the integer column (bytes)
+          uint32_t clo, chi;
+          taps8(fy, clo, chi);
+#pragma unroll
+          for (int c = 0; c < T; c++) {
+            const int col = tx * T + c;
+            const int off = L::O_WINC + (col + 5 + in.ex) * L::CSB + ty * T + iy + 2 + in.ey;
+            int s[T];
+            vert_s8<T>(base, off, clo, chi, s);
+            const uint8_t* kc = base + L::O_KEY + (col * H + ty * T) * 2;
+#pragma unroll
+            for (int j = 0; j < T / 2; j++) {
+              const uint32_t pr = (uint32_t)round1d_s8(s[2 * j]) | ((uint32_t)round1d_s8(s[2 * j + 1]) << 16);
+              X[c][j] = pk_sub(lds32(kc + 4 * j), pr);
+            }
+          }
+        } else {
+          // 2-D: vertical fy over plane fx
+          uint32_t cv[4];
+          taps16(fy, cv);
+#pragma unroll
+          for (int c = 0; c < T; c++) {
+            const int col = tx * T + c;
+            const uint8_t* pcol = base + L::O_PL + (fx - 1) * L::PLANE_B + (col + ix + 1) * L::CS * 2;
+            int s[T];
+            vert_i16<T>(pcol, ty * T + iy + 1, cv, s);
+            const uint8_t* kc = base + L::O_KEY + (col * H + ty * T) * 2;
+#pragma unroll
+            for (int j = 0; j < T / 2; j++) {
+              const uint32_t pr = (uint32_t)round2d(s[2 * j]) | ((uint32_t)round2d(s[2 * j + 1]) << 16);
+              X[c][j] = pk_sub(lds32(kc + 4 * j), pr);
+            }
+          }
+        }
+        uint32_t dd = in.had ? satd_packed<T>(X) : sad_packed<T>(X);
+        if (tt == 0) dd += mv_cost(in.ml, mv_bits(4 * in.mvx + qx, 4 * in.mvy + qy, 0, in.mvp_x, in.mvp_y));
+        atomicAdd(&info[p].acc[k], dd);
+      }
+    }
+    __syncthreads();
+
+    if (FME_STAMPS && threadIdx.x == 0) stamp[8] = __builtin_amdgcn_s_memtime();
+    // ---- 6. quarter argmin (cost scale 0) and results ---------------------------------------------
+    if (tid < count) {
+      PuInfo& in = info[tid];
+      uint32_t best = 0xFFFFFFFFu;
+      int bi = 0;
+#pragma unroll
+      for (int k = 0; k < 9; k++) {
+        const uint32_t d = in.acc[k];
+        if (d < best) {
+          best = d;
+          bi = k;
+        }
+      }
+      fme_result* r = (FME_SKIP & 128) ? reinterpret_cast<fme_result*>(lds + TL::O_QLIST) : a.res + in.job;
+      r->half_x = (int8_t)in.hx;
+      r->half_y = (int8_t)in.hy;
+      r->qtr_x = (int8_t)cand_dx(bi);
+      r->qtr_y = (int8_t)qtr_dy(bi);
+      r->frac_cost = best;
+    }
+    if (FME_STAMPS && threadIdx.x == 0) {
+      stamp[9] = __builtin_amdgcn_s_memtime();
+      for (int i = 0; i < 9; i++) atomicAdd(&g_fme_stamps[i], stamp[i + 1] - stamp[i]);
+      atomicAdd(&g_fme_stamps[9], pst[0] - stamp[0]);    // descriptor loads + table copy
+      atomicAdd(&g_fme_stamps[10], pst[1] - pst[0]);     // fill_info + barrier
+      atomicAdd(&g_fme_stamps[11], pst[2] - pst[1]);     // sample loads issued .. stored (lane 0's wave)
+      atomicAdd(&g_fme_stamps[12], pst[3] - pst[2]);     // waiting for the other waves' samples
+      atomicAdd(&g_fme_stamps[13], stamp[1] - pst[3]);   // window transpose + barrier
+      atomicAdd(&g_fme_stamps[15], 1ull);
+    }
+    if (count_n == 0) break;
+    // ---- hand over to the next tile ---------------------------------------------------------------
+    store_loads(info_n, count_n, tid);
+    __syncthreads();
+    transpose_window(count_n, tid);
+    __syncthreads();
+    cur ^= 1;
+    t = tn;
+    count = count_n;
   }
 }
 
 // =============================================================================================
-// kernels: small shapes (256 lanes, <= 40 KB LDS per tile) and large shapes (512 lanes)
+// kernels: small shapes (256 lanes) and large shapes (512 lanes).  Blocks of one launch are
+// dealt to classes by sc.tile_prefix (block ranges); a block strides over its class's tiles.
 // =============================================================================================
 #define FME_SMALL_CLASSES(X)                                                                       \
   X(0, 4, 8) X(1, 8, 4) X(2, 8, 8) X(3, 4, 16) X(4, 16, 4) X(5, 8, 16) X(6, 16, 8) X(7, 12, 16)      \
@@ -723,8 +955,8 @@ __device__ __forceinline__ void search_tile2(const BatchArgs& a, const int32_t* 
   X(15, 32, 24) X(16, 32, 32) X(17, 16, 64) X(18, 64, 16)
 #define FME_LARGE_CLASSES(X) X(19, 32, 64) X(20, 64, 32) X(21, 48, 64) X(22, 64, 48) X(23, 64, 64)
 
-constexpr int kSmallNT = 256, kSmallBudget = 40 * 1024;
-constexpr int kLargeNT = 512, kLargeBudget = 76 * 1024;
+constexpr int kSmallNT = 256, kSmallBudget = FME_SMALL_BUDGET_KB * 1024;
+constexpr int kLargeNT = 512, kLargeBudget = FME_LARGE_BUDGET_KB * 1024;
 
 __device__ __forceinline__ int find_class(const Schedule& sc, int b, int lo, int hi) {
   int c = lo;
@@ -736,14 +968,13 @@ __global__ __launch_bounds__(kSmallNT) void k_search_small(BatchArgs a, WorkBufs
   extern __shared__ __attribute__((aligned(16))) char lds[];
   const int b = blockIdx.x + sc.tile_prefix[0];
   const int c = find_class(sc, b, 0, 19);
-  const int t = b - sc.tile_prefix[c];
+  const int blk = b - sc.tile_prefix[c], nblk = sc.tile_prefix[c + 1] - sc.tile_prefix[c];
   switch (c) {
-#define FME_CASE(ID, W_, H_)                                                                  \
-  case ID: {                                                                                  \
-    constexpr int P = Tile<W_, H_, kSmallNT, kSmallBudget>::P;                                \
-    search_tile2<W_, H_, kSmallNT, kSmallBudget>(a, w.perm, sc.class_off[ID] + t * P,         \
-                                                 min(P, sc.class_cnt[ID] - t * P), lds);      \
-  } break;
+#define FME_CASE(ID, W_, H_)                                                                        \
+  case ID:                                                                                          \
+    search_class<W_, H_, kSmallNT, kSmallBudget>(a, w.sjobs, w.perm, sc.class_off[ID],               \
+                                                 sc.class_cnt[ID], blk, nblk, lds);                 \
+    break;
     FME_SMALL_CLASSES(FME_CASE)
 #undef FME_CASE
     default: break;
@@ -754,14 +985,13 @@ __global__ __launch_bounds__(kLargeNT) void k_search_large(BatchArgs a, WorkBufs
   extern __shared__ __attribute__((aligned(16))) char lds[];
   const int b = blockIdx.x + sc.tile_prefix[19];
   const int c = find_class(sc, b, 19, kNumClasses);
-  const int t = b - sc.tile_prefix[c];
+  const int blk = b - sc.tile_prefix[c], nblk = sc.tile_prefix[c + 1] - sc.tile_prefix[c];
   switch (c) {
-#define FME_CASE(ID, W_, H_)                                                                  \
-  case ID: {                                                                                  \
-    constexpr int P = Tile<W_, H_, kLargeNT, kLargeBudget>::P;                                \
-    search_tile2<W_, H_, kLargeNT, kLargeBudget>(a, w.perm, sc.class_off[ID] + t * P,         \
-                                                 min(P, sc.class_cnt[ID] - t * P), lds);      \
-  } break;
+#define FME_CASE(ID, W_, H_)                                                                        \
+  case ID:                                                                                          \
+    search_class<W_, H_, kLargeNT, kLargeBudget>(a, w.sjobs, w.perm, sc.class_off[ID],               \
+                                                 sc.class_cnt[ID], blk, nblk, lds);                 \
+    break;
     FME_LARGE_CLASSES(FME_CASE)
 #undef FME_CASE
     default: break;
@@ -793,32 +1023,44 @@ size_t lds_bytes_for_class(int cls) {
   }
 }
 
-hipError_t launch_search(const BatchArgs& a, const WorkBufs& w, const Schedule& sc, size_t /*lds*/,
-                         hipStream_t s) {
-  size_t lds_s = 0, lds_l = 0;
-  for (int c = 0; c < kNumClasses; c++) {
-    if (!sc.class_cnt[c]) continue;
-    if (c < 19) lds_s = lds_s > lds_bytes_for_class(c) ? lds_s : lds_bytes_for_class(c);
-    else lds_l = lds_l > lds_bytes_for_class(c) ? lds_l : lds_bytes_for_class(c);
-  }
-  const int small_tiles = sc.tile_prefix[19] - sc.tile_prefix[0];
-  const int large_tiles = sc.tile_prefix[kNumClasses] - sc.tile_prefix[19];
-  if (large_tiles > 0) {
-    static bool attr_set = false;
-    if (!attr_set) {
-      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_search_large),
-                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-      attr_set = true;
-    }
-    hipLaunchKernelGGL(k_search_large, dim3(large_tiles), dim3(kLargeNT), lds_l, s, a, w, sc);
-    hipError_t e = hipGetLastError();
+int tiles_per_block() { return FME_TILES_PER_BLOCK; }
+
+hipError_t debug_phase_cycles(unsigned long long* out16, bool reset) {
+  hipError_t e = hipMemcpyFromSymbol(out16, HIP_SYMBOL(g_fme_stamps), 16 * sizeof(unsigned long long));
+  if (e != hipSuccess || !reset) return e;
+  unsigned long long z[16] = {0};
+  return hipMemcpyToSymbol(HIP_SYMBOL(g_fme_stamps), z, sizeof(z));
+}
+
+int search_large_blocks(const Schedule& sc) { return sc.tile_prefix[kNumClasses] - sc.tile_prefix[19]; }
+int search_small_blocks(const Schedule& sc) { return sc.tile_prefix[19] - sc.tile_prefix[0]; }
+
+static size_t lds_max(const Schedule& sc, int lo, int hi) {
+  size_t m = 0;
+  for (int c = lo; c < hi; c++)
+    if (sc.class_cnt[c] && lds_bytes_for_class(c) > m) m = lds_bytes_for_class(c);
+  return m;
+}
+
+hipError_t launch_search_large(const BatchArgs& a, const WorkBufs& w, const Schedule& sc, hipStream_t s) {
+  const int blocks = search_large_blocks(sc);
+  if (blocks <= 0) return hipSuccess;
+  static bool attr_set = false;
+  if (!attr_set) {
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_search_large),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     if (e != hipSuccess) return e;
+    attr_set = true;
   }
-  if (small_tiles > 0) {
-    hipLaunchKernelGGL(k_search_small, dim3(small_tiles), dim3(kSmallNT), lds_s, s, a, w, sc);
-    return hipGetLastError();
-  }
-  return hipSuccess;
+  hipLaunchKernelGGL(k_search_large, dim3(blocks), dim3(kLargeNT), lds_max(sc, 19, kNumClasses), s, a, w, sc);
+  return hipGetLastError();
+}
+
+hipError_t launch_search_small(const BatchArgs& a, const WorkBufs& w, const Schedule& sc, hipStream_t s) {
+  const int blocks = search_small_blocks(sc);
+  if (blocks <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_search_small, dim3(blocks), dim3(kSmallNT), lds_max(sc, 0, 19), s, a, w, sc);
+  return hipGetLastError();
 }
 
 }  // namespace fme

@@ -13,7 +13,7 @@ from .abi import JOB_DTYPE, NN_PARAMS, RESULT_DTYPE
 from .weights import load_weights
 
 PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-LIB_PATH = os.path.join(PKG_ROOT, "libfme_amd.so")
+LIB_PATH = os.environ.get("FME_LIB_PATH") or os.path.join(PKG_ROOT, "libfme_amd.so")
 
 # Every entry point include/fme.h declares (the ABI test checks the .so exports them).
 ABI_SYMBOLS = (
@@ -21,6 +21,7 @@ ABI_SYMBOLS = (
     "fme_bind_picture_device", "fme_set_lambda", "fme_set_motion_lambda", "fme_set_keys",
     "fme_load_nn_weights", "fme_nn_reset_state", "fme_nn_get_state", "fme_nn_set_state", "fme_refine", "fme_refine_device",
     "fme_frac_dif_single", "fme_nn_pred_single", "fme_set_profiling", "fme_last_timings",
+    "fme_debug_phase_cycles",
 )
 
 
@@ -35,14 +36,14 @@ class FmeConfig(C.Structure):
                 ("qp", C.c_int32), ("fast_inter_mode", C.c_int32), ("max_jobs", C.c_int32)]
 
 
-_lib = None
+_libs = {}
 
 
-def load_library(path=LIB_PATH):
-    """Load libfme_amd.so once; raise if it has not been built."""
-    global _lib
-    if _lib is not None:
-        return _lib
+def load_library(path=None):
+    """Load libfme_amd.so (once per path); raise if it has not been built."""
+    path = path or LIB_PATH
+    if path in _libs:
+        return _libs[path]
     if not os.path.exists(path):
         raise FmeError(-1, f"{path} missing: build it with __graft_entry__.build() or "
                            f"`make -C hm16.9-nn_fme_amd`")
@@ -68,6 +69,7 @@ def load_library(path=LIB_PATH):
         "fme_nn_pred_single": (I, [P, P, U32, I, I, P, P]),
         "fme_set_profiling": (I, [P, I]),
         "fme_last_timings": (I, [P, P]),
+        "fme_debug_phase_cycles": (I, [P, I]),
     }
     for name, (res, args) in sig.items():
         f = getattr(lib, name)
@@ -75,7 +77,7 @@ def load_library(path=LIB_PATH):
         f.argtypes = args
     if lib.fme_abi_version() != 1:
         raise FmeError(-1, "ABI version mismatch")
-    _lib = lib
+    _libs[path] = lib
     return lib
 
 
@@ -92,8 +94,8 @@ class FmeContext:
     """One device context: pictures, lambdas, keys, NN weights and the carried NN state."""
 
     def __init__(self, device=0, use_hadamard=1, nn_mode=1, qp=22, fast_inter_mode=1, max_jobs=0,
-                 load_nn=True):
-        self.lib = load_library()
+                 load_nn=True, lib_path=None):
+        self.lib = load_library(lib_path)
         self.cfg = FmeConfig(8, use_hadamard, nn_mode, qp, fast_inter_mode, max_jobs)
         h = C.c_void_p()
         _check(self.lib, self.lib.fme_create(device, C.byref(self.cfg), C.byref(h)))
@@ -187,6 +189,11 @@ class FmeContext:
         ms = np.zeros(5, np.float32)
         _check(self.lib, self.lib.fme_last_timings(self.h, _ptr(ms)))
         return dict(zip(("classify", "scatter", "search", "nn_tail", "batch"), ms.tolist()))
+
+    def debug_phase_cycles(self, reset=True):
+        out = np.zeros(16, np.uint64)
+        _check(self.lib, self.lib.fme_debug_phase_cycles(_ptr(out), int(reset)))
+        return out
 
     def nn_pred_single(self, e, c, pu_h, pu_w):
         e = np.ascontiguousarray(e, dtype=np.uint32)

@@ -122,6 +122,80 @@ def make_jobs(rng, width, height, n, org_id, ref_ids, lambda_ids, sizes=None, bi
     return jobs
 
 
+def cu_size_for(w, h):
+    """Smallest square CU (8..64) that holds a PU of w x h (HEVC partition shapes)."""
+    s = max(w, h)
+    return 8 if s <= 8 else (16 if s <= 16 else (32 if s <= 32 else 64))
+
+
+def motion_field(rng, ctus_x, ctus_y, amp=12.0):
+    """Smooth per-CTU motion (full-pel per frame of distance): two low-frequency waves."""
+    fx = rng.uniform(0.1, 0.5, 2)
+    fy = rng.uniform(0.1, 0.5, 2)
+    ph = rng.uniform(0, 2 * np.pi, 4)
+    cx = np.arange(ctus_x)[None, :]
+    cy = np.arange(ctus_y)[:, None]
+    vx = amp * np.sin(fx[0] * cx + fy[0] * cy + ph[0]) + 0.5 * amp * np.sin(fx[1] * cx - fy[1] * cy + ph[1])
+    vy = 0.6 * amp * np.sin(fx[0] * cy - fy[0] * cx + ph[2]) + 0.3 * amp * np.sin(fx[1] * cy + ph[3])
+    return vx, vy
+
+
+def make_ctu_jobs(rng, width, height, calls_per_ctu, org_id, ref_ids, lambda_ids, mix=PU_MIX,
+                  bipred_frac=0.0, bits_in_max=6):
+    """Jobs in HM's order: CTUs in raster order, every PU of a CTU inside it on the CU /
+    partition grid (TEncCu quadtree, TComDataCU::getPartIndexAndSize), for every reference
+    picture.  Integer MVs follow a smooth per-CTU motion field scaled by the reference distance
+    plus a local deviation, the AMVP predictor is near the true motion; the search range and
+    the TZ start obey the same clipping rules as make_jobs().  Realistic cache locality: the
+    windows of one CTU's jobs overlap, as in the encoder."""
+    ctus_x, ctus_y = (width + MAX_CU - 1) // MAX_CU, (height + MAX_CU - 1) // MAX_CU
+    vx, vy = motion_field(rng, ctus_x, ctus_y)
+    ref_ids = np.asarray(ref_ids)
+    nref = len(ref_ids)
+    per = calls_per_ctu * nref
+    n = ctus_x * ctus_y * per
+    w, h = sample_sizes(rng, n, mix)
+    ctu = np.repeat(np.arange(ctus_x * ctus_y), per)
+    cux = (ctu % ctus_x) * MAX_CU
+    cuy = (ctu // ctus_x) * MAX_CU
+    cs = np.where(np.maximum(w, h) <= 8, 8, np.where(np.maximum(w, h) <= 16, 16, np.where(np.maximum(w, h) <= 32, 32, 64)))
+    # CU position inside the CTU (aligned to its size), PU at either end of the CU
+    ncu = MAX_CU // cs
+    x = cux + rng.integers(0, ncu) * cs + rng.integers(0, 2, n) * (cs - w)
+    y = cuy + rng.integers(0, ncu) * cs + rng.integers(0, 2, n) * (cs - h)
+    x = np.minimum(x, (width - w) // 4 * 4)
+    y = np.minimum(y, (height - h) // 4 * 4)
+    ref_k = np.tile(np.arange(nref), n // nref)          # every PU against each reference
+    dist = ref_k + 1
+    tx = np.rint(vx.reshape(-1)[ctu] * dist).astype(np.int64) + rng.integers(-4, 5, n)
+    ty = np.rint(vy.reshape(-1)[ctu] * dist).astype(np.int64) + rng.integers(-4, 5, n)
+    mvp_x = 4 * tx + rng.integers(-16, 17, n)
+    mvp_y = 4 * ty + rng.integers(-16, 17, n)
+    cpx = _clip_mv_qpel(mvp_x, x, width)
+    cpy = _clip_mv_qpel(mvp_y, y, height)
+    lt_x = _div4_round(_clip_mv_qpel(cpx - (SEARCH_RANGE << 2), x, width))
+    rb_x = _div4_round(_clip_mv_qpel(cpx + (SEARCH_RANGE << 2), x, width))
+    lt_y = _div4_round(_clip_mv_qpel(cpy - (SEARCH_RANGE << 2), y, height))
+    rb_y = _div4_round(_clip_mv_qpel(cpy + (SEARCH_RANGE << 2), y, height))
+    jobs = np.zeros(n, dtype=JOB_DTYPE)
+    jobs["x"], jobs["y"], jobs["w"], jobs["h"] = x, y, w, h
+    jobs["org_id"] = org_id
+    jobs["ref_id"] = ref_ids[ref_k]
+    jobs["lambda_id"] = rng.choice(np.asarray(lambda_ids), size=n)
+    jobs["mv_x"] = np.clip(tx, lt_x, rb_x)
+    jobs["mv_y"] = np.clip(ty, lt_y, rb_y)
+    jobs["mvp_x"], jobs["mvp_y"] = mvp_x, mvp_y
+    jobs["lt_x"], jobs["lt_y"], jobs["rb_x"], jobs["rb_y"] = lt_x, lt_y, rb_x, rb_y
+    jobs["bits_in"] = rng.integers(1, bits_in_max + 1, n)
+    jobs["flags"] = JOB_EMI
+    jobs["key_offset"] = -1
+    if bipred_frac > 0:
+        bi = rng.random(n) < bipred_frac
+        jobs["flags"][bi] = JOB_BIPRED
+        jobs["key_offset"][bi] = -2
+    return jobs
+
+
 def make_bipred_keys(rng, jobs, pictures):
     """Key blocks 2*org - pred_other (TComYuv::removeHighFreq, TComYuv.cpp:411-455, no clip)
     for rows with key_offset == -2; pred_other is an integer-displaced block of another

@@ -195,6 +195,9 @@ int fme_nn_pred_single(fme_ctx* ctx, const uint32_t* e, uint32_t c, int pu_h, in
  * [4] whole batch (first kernel start to last kernel end, host sync included).            */
 int fme_set_profiling(fme_ctx* ctx, int enable);
 int fme_last_timings(fme_ctx* ctx, float* ms5);
+/* Diagnostic builds (FME_STAMPS=1) only: per-phase shader cycles of the search kernels summed
+ * over workgroups ([0..8] phases, [15] workgroups); zeros otherwise.  Resets when reset != 0. */
+int fme_debug_phase_cycles(uint64_t* out16, int reset);
 
 #ifdef __cplusplus
 }
