@@ -12,10 +12,19 @@ ring (nnfme.dist.PictureRing), which is part of the timed step.
 
 Prints one JSON line (rank 0).  `cpu_baseline` times oracle/_ref (the reference's own
 TLibCommon primitives driven in TEncSearch order, compiled -O2 like the reference build) on
-one host core over a bounded sample of the same job mix.
+one host core (HM is single-threaded) over a bounded sample of the same job mix;
+`cpu_baseline_all_cores` runs one job stream per host core.  Both run
+before the GPU is initialised.
+
+`roofline` is for the dominant kernel, fme::k_search_small (EMI + FracDIF of the 19 PU shapes
+up to 64x16/16x64, ~99 % of the jobs): its algorithmic bytes (SURVEY.md §8(d) per-PU figure
+summed over the jobs it processes) over its average duration, from HIP events recorded
+around it on its own stream during the timed steps.  The path is integer-VALU bound, so the
+VALU roof (reference integer ops, §8(d)) is reported beside the HBM one.
 """
 import argparse
 import json
+import multiprocessing as mp
 import os
 import sys
 import time
@@ -31,7 +40,11 @@ from nnfme.abi import JOB_DTYPE, RESULT_DTYPE  # noqa: E402
 W, H, QP = 1920, 1080, 22
 METRIC = "sub-pel PU refinements/sec @ 1080p lowdelay_P QP22; bit-exact MV/SATD vs HM"
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md chip table (spec)
-VALU_PEAK_TOPS = 256 * 64 * 2.4e9 / 1e12   # int32 lane-ops/s at 2.4 GHz
+# int32 VALU lane-ops/s: 256 CUs x 4 SIMDs x 32 lanes/clk (a wave64 op issues over 2 clk) x
+# 2.4 GHz = 78.6 T (MI355X_MICROARCH.md; = the 157.3 TFLOP/s f32 vector peak / 2)
+VALU_PEAK_TOPS = 256 * 4 * 32 * 2.4e9 / 1e12
+# PU shapes (w, h) served by fme::k_search_large (fme_device.h classes 19..23)
+LARGE_SHAPES = {(32, 64), (64, 32), (48, 64), (64, 48), (64, 64)}
 
 
 def algorithmic_bytes(jobs):
@@ -39,6 +52,13 @@ def algorithmic_bytes(jobs):
     w = jobs["w"].astype(np.int64)
     h = jobs["h"].astype(np.int64)
     return int((w * h + (w + 8) * (h + 8) + 48).sum())
+
+
+def large_mask(jobs):
+    m = np.zeros(len(jobs), bool)
+    for w, h in LARGE_SHAPES:
+        m |= (jobs["w"] == w) & (jobs["h"] == h)
+    return m
 
 
 def algorithmic_ops(jobs):
@@ -62,21 +82,60 @@ def make_frame_jobs(seed, kind="ctu"):
     return synth.make_ctu_jobs(rng, W, H, 423, 4, [0, 1, 2, 3], [0])
 
 
-def cpu_baseline(jobs_sample, pics):
-    """Time oracle/_ref on one core over `jobs_sample`."""
+_CPU = {}   # set before forking the all-cores workers
+
+
+def _cpu_reference():
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     from oracle import Reference
     from nnfme import weights
     ref = Reference(use_hadamard=1, nn_mode=1, fast_inter_mode=1)
-    for k, v in pics.items():
+    for k, v in _CPU["pics"].items():
         ref.set_picture(k, v)
     ref.set_lambda(0, synth.LDP_LAMBDA[QP][1])
     ref.load_nn(weights.load_weights(QP))
-    ref.refine(jobs_sample[:2000])   # warm caches
-    t0 = time.perf_counter()
-    ref.refine(jobs_sample)
+    return ref
+
+
+def cpu_baseline(jobs, pics, seconds):
+    """oracle/_ref on one core: whole passes over the frame's jobs (in HM order) until
+    `seconds` have elapsed (the last pass partial, in 20k-job chunks)."""
+    _CPU["pics"] = pics
+    ref = _cpu_reference()
+    ref.refine(jobs[:2000])   # warm caches
+    done, t0 = 0, time.perf_counter()
+    while time.perf_counter() - t0 < seconds:
+        i = done % len(jobs)
+        chunk = jobs[i:i + 20000]
+        ref.refine(chunk)
+        done += len(chunk)
     dt = time.perf_counter() - t0
-    return len(jobs_sample) / dt, dt
+    return done / dt, dt, done
+
+
+def _cpu_worker(args):
+    lo, hi, reps = args
+    ref = _cpu_reference()
+    jobs = _CPU["jobs"][lo:hi]
+    ref.refine(jobs[:500])
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        ref.refine(jobs)
+    return len(jobs) * reps, time.perf_counter() - t0
+
+
+def cpu_baseline_all_cores(jobs, pics, rate1, seconds, cores):
+    """One job stream per core (fork workers, each its own slice of the frame, repeated so each
+    runs about `seconds`); value = all jobs / wall time of the slowest worker."""
+    _CPU["pics"], _CPU["jobs"] = pics, jobs
+    per = len(jobs) // cores
+    reps = max(1, int(round(seconds * rate1 / max(per, 1))))
+    tasks = [(i * per, (i + 1) * per, reps) for i in range(cores)]
+    with mp.get_context("fork").Pool(cores) as pool:
+        out = pool.map(_cpu_worker, tasks)
+    total = sum(o[0] for o in out)
+    wall = max(o[1] for o in out)
+    return total / wall, wall, total
 
 
 def read_pmc_traffic():
@@ -98,19 +157,47 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample length")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--check", action="store_true", help="verify one step against the oracle sample")
     ap.add_argument("--jobs", choices=("ctu", "uniform"), default="ctu",
                     help="job stream: HM CTU order (default) or uniformly scattered PUs (stress)")
+    ap.add_argument("--cpu-cores", type=int, default=0,
+                    help="cores for cpu_baseline_all_cores (0: all available, at most 16; -1: skip)")
     args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+
+    # ---- inputs (untimed): jobs of this rank's frames ----------------------------------------
+    jobs = make_frame_jobs(1000 + rank, args.jobs)
+    n = len(jobs)
+
+    # ---- CPU baselines first, before anything touches the GPU (fork-safe) -------------------
+    cpu = {}
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        pics = {k: synth.synth_luma(W, H, t) for k, t in zip(range(5), (7, 6, 5, 4, 0))}
+        rate, dt, done = cpu_baseline(jobs, pics, args.cpu_seconds)
+        cpu["cpu_baseline"] = {
+            "value": rate, "unit": "PU/s", "cores": 1, "kind": "reference",
+            "sample": f"{done} jobs ({done / n:.2f} passes over the same 1080p QP22 frame batch, "
+                      f"HM order) on one host core, {dt:.1f} s; oracle/_ref = the reference's "
+                      f"TLibCommon (interpolation, RdCost) -O2 driven in TEncSearch order, NN "
+                      f"restated scalar",
+        }
+        avail = len(os.sched_getaffinity(0))
+        cores = min(16, avail) if args.cpu_cores == 0 else args.cpu_cores
+        if cores > 1:
+            rate_all, wall, total = cpu_baseline_all_cores(jobs, pics, rate, args.cpu_seconds * 0.75, cores)
+            cpu["cpu_baseline_all_cores"] = {
+                "value": rate_all, "unit": "PU/s", "cores": cores, "kind": "reference",
+                "sample": f"{total} jobs, one stream per core over 1/{cores} slices of the frame, "
+                          f"{wall:.1f} s wall",
+            }
 
     import torch
     import torch.distributed as dist
     from nnfme.dist import PictureRing
     from nnfme.runtime import FmeContext
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         torch.cuda.set_device(local)
@@ -119,9 +206,7 @@ def main():
     dev = torch.device("cuda", local)
     stream = torch.cuda.current_stream(dev)
 
-    # ---- inputs (untimed): jobs of this rank's frames, resident in HBM ----------------------
-    jobs = make_frame_jobs(1000 + rank, args.jobs)
-    n = len(jobs)
+    # jobs and results resident in HBM
     d_jobs = torch.from_numpy(jobs.view(np.uint8).copy()).to(dev)
     d_res = torch.empty(n * RESULT_DTYPE.itemsize, dtype=torch.uint8, device=dev)
 
@@ -161,24 +246,15 @@ def main():
         run_step(s)
     torch.cuda.synchronize(dev)
 
-    # correctness spot-check of the last warm-up step (optional)
-    if args.check and rank == 0:
-        res = d_res.cpu().numpy().view(RESULT_DTYPE)
-        print("check: nn classes", np.bincount(res["nn_class"], minlength=49)[:5], file=sys.stderr)
-
-    # ---- per-kernel timing with HIP events on the batch stream (one profiled step) -----------
+    # ---- timed region (HIP events around each kernel, read at the next batch's own sync) ------
     ctx.set_profiling(True)
-    run_step(args.warmup)
-    tm = ctx.last_timings()
-    ctx.set_profiling(False)
-
-    # ---- timed region --------------------------------------------------------------------------
+    ctx.accumulated_timings(reset=True)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     for s in range(args.steps):
-        run_step(args.warmup + 1 + s)
+        run_step(args.warmup + s)
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
@@ -187,13 +263,41 @@ def main():
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
+    nb, acc = ctx.accumulated_timings(reset=True)
+    ctx.set_profiling(False)
+    tm = {k: v / max(nb, 1) for k, v in acc.items()}
+
+    # ---- PCIe-inclusive leg (untimed for `value`): host jobs -> host results, new org frame
+    # uploaded from host memory each step (pinned buffers) -------------------------------------
+    pcie = None
+    if rank == 0 and world == 1:
+        h_jobs = torch.from_numpy(jobs.view(np.uint8).copy()).pin_memory()
+        h_res = torch.empty(n * RESULT_DTYPE.itemsize, dtype=torch.uint8).pin_memory()
+        h_org = torch.from_numpy(synth.synth_luma(W, H, 0)).pin_memory()
+        d_org = torch.empty_like(h_org, device=dev)
+        reps = 3
+        torch.cuda.synchronize(dev)
+        t1 = time.perf_counter()
+        for _ in range(reps):
+            d_org.copy_(h_org, non_blocking=True)
+            ctx.bind_picture_device(4, d_org.data_ptr(), W, W, H)
+            d_jobs.copy_(h_jobs, non_blocking=True)
+            ctx.refine_device(d_jobs.data_ptr(), d_res.data_ptr(), n, stream.cuda_stream)
+            h_res.copy_(d_res, non_blocking=True)
+        torch.cuda.synchronize(dev)
+        dt = (time.perf_counter() - t1) / reps
+        pcie = {"value": n / dt, "unit": "PU/s", "ms_per_step": dt * 1e3,
+                "note": "jobs H2D + org frame H2D + refine + results D2H, pinned host buffers"}
 
     value = world * n * args.steps / elapsed
     if rank == 0:
-        bytes_launch = algorithmic_bytes(jobs)
-        ops_launch = algorithmic_ops(jobs)
+        lm = large_mask(jobs)
+        small_jobs = jobs[~lm]
+        bytes_small = algorithmic_bytes(small_jobs)
+        small_s = tm["search_small"] / 1e3
+        achieved = bytes_small / small_s / 1e9
+        ops_small = algorithmic_ops(small_jobs)
         search_s = tm["search"] / 1e3
-        achieved = bytes_launch / search_s / 1e9
         traffic, traffic_src = read_pmc_traffic()
         out = {
             "metric": METRIC,
@@ -207,8 +311,8 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "int16/int32 (NN f32)",
-            "data": "synthetic (SURVEY.md §8(d) YUV generator + PU-size mix; random-init-free: "
-                    "reference per-QP NN weights)",
+            "data": "synthetic (SURVEY.md §8(d) YUV generator + PU-size mix; reference per-QP "
+                    "NN weights, no random init)",
             "config": {"workload": "1920x1080 lowdelay_P QP22, NN_pred 2-layer on, 4 refs, "
                                    "862920 PU jobs per frame (configs[2] at QP22)",
                        "job_stream": args.jobs,
@@ -220,29 +324,28 @@ def main():
                 "unit": "GB/s",
                 "frac": achieved / HBM_PEAK_GBS,
                 "traffic": traffic,
-                "kernel": "fme::k_search (EMI + FracDIF)",
-                "search_ms": tm["search"],
-                "batch_ms": tm["batch"],
-                "kernel_ms": tm,
-                "valu_tops": ops_launch / search_s / 1e12,
+                "kernel": "fme::k_search_small (EMI + FracDIF, 19 PU shapes)",
+                "kernel_jobs": int(len(small_jobs)),
+                "algorithmic_bytes_per_launch": bytes_small,
+                "kernel_ms": tm["search_small"],
+                "profiled_batches": nb,
+                "valu_tops": ops_small / small_s / 1e12,
                 "valu_peak_tops": VALU_PEAK_TOPS,
-                "valu_frac": ops_launch / search_s / 1e12 / VALU_PEAK_TOPS,
-                "note": "path is integer-VALU-bound (~97 ops/B); valu_frac is the binding roof",
+                "valu_frac": ops_small / small_s / 1e12 / VALU_PEAK_TOPS,
+                "note": "integer-VALU bound (~97 reference int ops per algorithmic byte); "
+                        "valu_frac counts the reference's arithmetic (SURVEY.md §8(d))",
                 "traffic_source": traffic_src,
+                "batch_kernel_ms": tm,
+                "search_phase_achieved_gbs": algorithmic_bytes(jobs) / search_s / 1e9,
             },
         }
-        if not args.no_cpu_baseline and world == 1:
-            pics = {k: synth.synth_luma(W, H, t) for k, t in zip(range(5), (7, 6, 5, 4, 0))}
-            m = int(min(n, max(20000, args.cpu_seconds * 80000)))
-            sample = jobs[:m]
-            rate, dt = cpu_baseline(sample, pics)
-            out["cpu_baseline"] = {
-                "value": rate, "unit": "PU/s", "cores": 1, "kind": "reference",
-                "sample": f"first {m} jobs of the same 1080p QP22 frame batch, one host core, "
-                          f"{dt:.1f} s (oracle/_ref: reference TLibCommon -O2 + TEncSearch-order "
-                          f"harness, NN restated scalar)",
-            }
-            out["speedup_vs_cpu_1core"] = value / rate
+        out.update(cpu)
+        if "cpu_baseline" in cpu:
+            out["speedup_vs_cpu_1core"] = value / cpu["cpu_baseline"]["value"]
+        if "cpu_baseline_all_cores" in cpu:
+            out["speedup_vs_cpu_all_cores"] = value / cpu["cpu_baseline_all_cores"]["value"]
+        if pcie:
+            out["pcie_inclusive"] = pcie
         print(json.dumps(out), flush=True)
 
     if world > 1:

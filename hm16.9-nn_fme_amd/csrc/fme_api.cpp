@@ -101,10 +101,22 @@ struct fme_ctx {
   DevBuf<uint32_t> single_nn_in;
   DevBuf<int32_t> single_nn_out;
 
+  // Profiling: two event sets used alternately, so batch k's set is read (without an extra
+  // sync) at batch k+1's histogram synchronisation.  Per set: 0 start, 1 classify end,
+  // 2 scatter begin, 3 scatter end, 4 small-shape search end, 5 search end, 6 batch end,
+  // 7/8 large-shape search begin/end (aux stream when concurrent).
+  static constexpr int kEv = 9;
   bool profiling = false;
+  bool events_made = false;
+  hipEvent_t ev[2][kEv] = {};
+  int ev_cur = 0;               // set the next profiled batch records into
+  int ev_pending = -1;          // set recorded but not yet harvested
+  bool ev_has_large[2] = {false, false};
+  bool ev_serial[2] = {false, false};
   bool timed = false;
-  hipEvent_t ev[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};
-  hipEvent_t ev_end = nullptr;
+  float last_ms[FME_NUM_TIMINGS] = {};
+  double acc_ms[FME_NUM_TIMINGS] = {};
+  int acc_batches = 0;
 
   // the large-shape search kernel runs beside the small-shape one on its own stream
   hipStream_t aux = nullptr;
@@ -115,6 +127,29 @@ struct fme_ctx {
 namespace fme {
 hipError_t debug_phase_cycles(unsigned long long* out16, bool reset);
 hipError_t launch_nn_single(const float* nnp, const uint32_t* in, int32_t* out, hipStream_t s);
+}
+
+// Reads a recorded (complete or to-be-waited-for) event set into last_ms and adds it to the
+// accumulators.
+static int harvest_events(fme_ctx* c, bool wait) {
+  if (c->ev_pending < 0) return FME_OK;
+  const int b = c->ev_pending;
+  hipEvent_t* e = c->ev[b];
+  if (wait) HIP_TRY(hipEventSynchronize(e[6]));
+  float* ms = c->last_ms;
+  HIP_TRY(hipEventElapsedTime(&ms[0], e[0], e[1]));
+  HIP_TRY(hipEventElapsedTime(&ms[1], e[2], e[3]));
+  HIP_TRY(hipEventElapsedTime(&ms[2], e[3], e[5]));
+  HIP_TRY(hipEventElapsedTime(&ms[3], e[5], e[6]));
+  HIP_TRY(hipEventElapsedTime(&ms[4], e[0], e[6]));
+  HIP_TRY(hipEventElapsedTime(&ms[5], c->ev_serial[b] && c->ev_has_large[b] ? e[8] : e[3], e[4]));
+  ms[6] = 0.f;
+  if (c->ev_has_large[b]) HIP_TRY(hipEventElapsedTime(&ms[6], e[7], e[8]));
+  for (int i = 0; i < FME_NUM_TIMINGS; i++) c->acc_ms[i] += ms[i];
+  c->acc_batches++;
+  c->ev_pending = -1;
+  c->timed = true;
+  return FME_OK;
 }
 
 extern "C" {
@@ -170,9 +205,9 @@ int fme_destroy(fme_ctx* c) {
   c->single_pic.release(); c->single_job.release(); c->single_res.release();
   c->single_nn_in.release(); c->single_nn_out.release();
   if (c->h_counts) (void)hipHostFree(c->h_counts);
-  for (auto& e : c->ev)
-    if (e) (void)hipEventDestroy(e);
-  if (c->ev_end) (void)hipEventDestroy(c->ev_end);
+  for (auto& set : c->ev)
+    for (auto& e : set)
+      if (e) (void)hipEventDestroy(e);
   if (c->ev_fork) (void)hipEventDestroy(c->ev_fork);
   if (c->ev_join) (void)hipEventDestroy(c->ev_join);
   if (c->aux) (void)hipStreamDestroy(c->aux);
@@ -337,12 +372,19 @@ int fme_refine_device(fme_ctx* c, const fme_job* d_jobs, fme_result* d_res, int 
   w.nn_state = c->nn_state.p;
 
   const bool prof = c->profiling;
-  if (prof) HIP_TRY(hipEventRecord(c->ev[0], s));
+  const int eb = c->ev_cur;
+  hipEvent_t* ev = c->ev[eb];
+  if (prof) HIP_TRY(hipEventRecord(ev[0], s));
   HIP_TRY(hipMemsetAsync(c->counts.p, 0, (2 * kNumClasses + 1) * sizeof(int32_t), s));
   HIP_TRY(launch_classify(a, w, s));
-  if (prof) HIP_TRY(hipEventRecord(c->ev[1], s));
+  if (prof) HIP_TRY(hipEventRecord(ev[1], s));
   HIP_TRY(hipMemcpyAsync(c->h_counts, c->counts.p, (kNumClasses + 1) * sizeof(int32_t), hipMemcpyDeviceToHost, s));
   HIP_TRY(hipStreamSynchronize(s));
+  // the previous profiled batch ran on this stream before the sync: its events are complete
+  if (c->ev_pending >= 0 && c->ev_pending != eb) {
+    rc = harvest_events(c, false);
+    if (rc) return rc;
+  }
   if (c->h_counts[kNumClasses] > 0)
     return fail(FME_E_INVALID, "fme_refine_device: %d job(s) with an unsupported PU size or unset picture/lambda/key",
                 c->h_counts[kNumClasses]);
@@ -363,24 +405,33 @@ int fme_refine_device(fme_ctx* c, const fme_job* d_jobs, fme_result* d_res, int 
     off += cnt;
   }
   sc.tile_prefix[kNumClasses] = blocks;
-  if (prof) HIP_TRY(hipEventRecord(c->ev[2], s));   // host sync above: scatter starts here
+  const bool has_large = search_large_blocks(sc) > 0;
+  if (prof) HIP_TRY(hipEventRecord(ev[2], s));   // host sync above: scatter starts here
   HIP_TRY(launch_scatter(a, w, sc, s));
-  if (prof) HIP_TRY(hipEventRecord(c->ev[3], s));
+  if (prof) HIP_TRY(hipEventRecord(ev[3], s));
   if (!c->concurrent_search) {
+    if (prof && has_large) HIP_TRY(hipEventRecord(ev[7], s));
     HIP_TRY(launch_search_large(a, w, sc, s));
-  } else if (search_large_blocks(sc) > 0) {
+    if (prof && has_large) HIP_TRY(hipEventRecord(ev[8], s));
+  } else if (has_large) {
     HIP_TRY(hipEventRecord(c->ev_fork, s));
     HIP_TRY(hipStreamWaitEvent(c->aux, c->ev_fork, 0));
+    if (prof) HIP_TRY(hipEventRecord(ev[7], c->aux));
     HIP_TRY(launch_search_large(a, w, sc, c->aux));
+    if (prof) HIP_TRY(hipEventRecord(ev[8], c->aux));
     HIP_TRY(hipEventRecord(c->ev_join, c->aux));
   }
   HIP_TRY(launch_search_small(a, w, sc, s));
-  if (c->concurrent_search && search_large_blocks(sc) > 0) HIP_TRY(hipStreamWaitEvent(s, c->ev_join, 0));
-  if (prof) HIP_TRY(hipEventRecord(c->ev[4], s));
+  if (prof) HIP_TRY(hipEventRecord(ev[4], s));
+  if (c->concurrent_search && has_large) HIP_TRY(hipStreamWaitEvent(s, c->ev_join, 0));
+  if (prof) HIP_TRY(hipEventRecord(ev[5], s));
   HIP_TRY(launch_nn_tail(a, w, c->d_nn.p, c->state_cur, s));
   if (prof) {
-    HIP_TRY(hipEventRecord(c->ev_end, s));
-    c->timed = true;
+    HIP_TRY(hipEventRecord(ev[6], s));
+    c->ev_has_large[eb] = has_large;
+    c->ev_serial[eb] = !c->concurrent_search;
+    c->ev_pending = eb;
+    c->ev_cur ^= 1;
   }
   if (a.nn_mode) c->state_cur ^= 1;
   return FME_OK;
@@ -500,12 +551,16 @@ int fme_nn_pred_single(fme_ctx* c, const uint32_t* e, uint32_t cc, int pu_h, int
 int fme_set_profiling(fme_ctx* c, int enable) {
   if (!c) return fail(FME_E_INVALID, "fme_set_profiling: null ctx");
   HIP_TRY(hipSetDevice(c->device));
-  if (enable && !c->ev_end) {
-    for (auto& e : c->ev) HIP_TRY(hipEventCreate(&e));
-    HIP_TRY(hipEventCreate(&c->ev_end));
+  if (enable && !c->events_made) {
+    for (auto& set : c->ev)
+      for (auto& e : set) HIP_TRY(hipEventCreate(&e));
+    c->events_made = true;
+  }
+  if (!enable && c->ev_pending >= 0) {
+    const int rc = harvest_events(c, true);
+    if (rc) return rc;
   }
   c->profiling = enable != 0;
-  c->timed = false;
   return FME_OK;
 }
 
@@ -516,17 +571,28 @@ int fme_debug_phase_cycles(uint64_t* out16, int reset) {
   return FME_OK;
 }
 
-int fme_last_timings(fme_ctx* c, float* ms) {
-  if (!c || !ms) return fail(FME_E_INVALID, "fme_last_timings: null argument");
-  if (!c->timed) return fail(FME_E_STATE, "fme_last_timings: no profiled batch");
+int fme_last_timings(fme_ctx* c, float* ms, int count) {
+  if (!c || !ms || count < 0) return fail(FME_E_INVALID, "fme_last_timings: null argument");
   HIP_TRY(hipSetDevice(c->device));
-  HIP_TRY(hipEventSynchronize(c->ev_end));
-  HIP_TRY(hipEventElapsedTime(&ms[0], c->ev[0], c->ev[1]));
-  HIP_TRY(hipEventElapsedTime(&ms[1], c->ev[2], c->ev[3]));
-  HIP_TRY(hipEventElapsedTime(&ms[2], c->ev[3], c->ev[4]));
-  HIP_TRY(hipEventElapsedTime(&ms[3], c->ev[4], c->ev_end));
-  HIP_TRY(hipEventElapsedTime(&ms[4], c->ev[0], c->ev_end));
+  const int rc = harvest_events(c, true);
+  if (rc) return rc;
+  if (!c->timed) return fail(FME_E_STATE, "fme_last_timings: no profiled batch");
+  for (int i = 0; i < count && i < FME_NUM_TIMINGS; i++) ms[i] = c->last_ms[i];
   return FME_OK;
+}
+
+int fme_accumulated_timings(fme_ctx* c, double* ms, int count, int reset) {
+  if (!c || (count > 0 && !ms) || count < 0) return fail(FME_E_INVALID, "fme_accumulated_timings: null argument");
+  HIP_TRY(hipSetDevice(c->device));
+  const int rc = harvest_events(c, true);
+  if (rc) return rc;
+  const int n = c->acc_batches;
+  for (int i = 0; i < count && i < FME_NUM_TIMINGS; i++) ms[i] = c->acc_ms[i];
+  if (reset) {
+    for (double& v : c->acc_ms) v = 0.0;
+    c->acc_batches = 0;
+  }
+  return n;
 }
 
 }  // extern "C"

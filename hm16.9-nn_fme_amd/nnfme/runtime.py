@@ -15,13 +15,16 @@ from .weights import load_weights
 PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB_PATH = os.environ.get("FME_LIB_PATH") or os.path.join(PKG_ROOT, "libfme_amd.so")
 
+ABI_VERSION = 2
+TIMING_NAMES = ("classify", "scatter", "search", "nn_tail", "batch", "search_small", "search_large")
+
 # Every entry point include/fme.h declares (the ABI test checks the .so exports them).
 ABI_SYMBOLS = (
     "fme_abi_version", "fme_create", "fme_destroy", "fme_last_error", "fme_set_picture",
     "fme_bind_picture_device", "fme_set_lambda", "fme_set_motion_lambda", "fme_set_keys",
     "fme_load_nn_weights", "fme_nn_reset_state", "fme_nn_get_state", "fme_nn_set_state", "fme_refine", "fme_refine_device",
     "fme_frac_dif_single", "fme_nn_pred_single", "fme_set_profiling", "fme_last_timings",
-    "fme_debug_phase_cycles",
+    "fme_accumulated_timings", "fme_debug_phase_cycles",
 )
 
 
@@ -68,14 +71,15 @@ def load_library(path=None):
         "fme_frac_dif_single": (I, [P, I, P, I, I, I, P, I, I, I, I, I, D, P, P, P]),
         "fme_nn_pred_single": (I, [P, P, U32, I, I, P, P]),
         "fme_set_profiling": (I, [P, I]),
-        "fme_last_timings": (I, [P, P]),
+        "fme_last_timings": (I, [P, P, I]),
+        "fme_accumulated_timings": (I, [P, P, I, I]),
         "fme_debug_phase_cycles": (I, [P, I]),
     }
     for name, (res, args) in sig.items():
         f = getattr(lib, name)
         f.restype = res
         f.argtypes = args
-    if lib.fme_abi_version() != 1:
+    if lib.fme_abi_version() != ABI_VERSION:
         raise FmeError(-1, "ABI version mismatch")
     _libs[path] = lib
     return lib
@@ -185,10 +189,18 @@ class FmeContext:
         _check(self.lib, self.lib.fme_set_profiling(self.h, int(enable)))
 
     def last_timings(self):
-        """Device ms of the last batch: classify, scatter, search, nn_tail, whole batch."""
-        ms = np.zeros(5, np.float32)
-        _check(self.lib, self.lib.fme_last_timings(self.h, _ptr(ms)))
-        return dict(zip(("classify", "scatter", "search", "nn_tail", "batch"), ms.tolist()))
+        """Device ms of the last profiled batch, keyed by TIMING_NAMES."""
+        ms = np.zeros(len(TIMING_NAMES), np.float32)
+        _check(self.lib, self.lib.fme_last_timings(self.h, _ptr(ms), ms.size))
+        return dict(zip(TIMING_NAMES, ms.tolist()))
+
+    def accumulated_timings(self, reset=True):
+        """(batches, {name: summed device ms}) over the profiled batches since the last reset."""
+        ms = np.zeros(len(TIMING_NAMES), np.float64)
+        n = self.lib.fme_accumulated_timings(self.h, _ptr(ms), ms.size, int(reset))
+        if n < 0:
+            _check(self.lib, n)
+        return n, dict(zip(TIMING_NAMES, ms.tolist()))
 
     def debug_phase_cycles(self, reset=True):
         out = np.zeros(16, np.uint64)

@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define FME_ABI_VERSION 1
+#define FME_ABI_VERSION 2
 
 /* ---- error codes ---------------------------------------------------------------- */
 #define FME_OK            0
@@ -190,11 +190,18 @@ int fme_nn_pred_single(fme_ctx* ctx, const uint32_t* e, uint32_t c, int pu_h, in
 
 /* ---- instrumentation (an extension; the reference has no counterpart) ------------------- *
  * With profiling on, fme_refine/fme_refine_device record HIP events around each kernel of
- * the batch on the batch's stream; fme_last_timings() waits for the last batch and returns
- * device milliseconds: [0] classify, [1] scatter, [2] search (EMI + FracDIF), [3] NN + tail,
- * [4] whole batch (first kernel start to last kernel end, host sync included).            */
+ * the batch on the streams the kernels run on.  Device milliseconds, FME_NUM_TIMINGS values:
+ * [0] classify, [1] scatter, [2] search phase (EMI + FracDIF, both shape kernels),
+ * [3] NN + tail, [4] whole batch (first kernel start to last kernel end, host sync included),
+ * [5] small-shape search kernel, [6] large-shape search kernel (0 if not launched).
+ * fme_last_timings waits for the last profiled batch.  fme_accumulated_timings returns the
+ * sums over every profiled batch since the last reset (the return value is the batch count);
+ * a batch's events are read at the next batch's own host synchronisation, so profiling a
+ * run of batches adds no synchronisation.                                                  */
+#define FME_NUM_TIMINGS 7
 int fme_set_profiling(fme_ctx* ctx, int enable);
-int fme_last_timings(fme_ctx* ctx, float* ms5);
+int fme_last_timings(fme_ctx* ctx, float* ms, int count);
+int fme_accumulated_timings(fme_ctx* ctx, double* ms, int count, int reset);
 /* Diagnostic builds (FME_STAMPS=1) only: per-phase shader cycles of the search kernels summed
  * over workgroups ([0..8] phases, [15] workgroups); zeros otherwise.  Resets when reset != 0. */
 int fme_debug_phase_cycles(uint64_t* out16, int reset);

@@ -1,0 +1,254 @@
+// test_hm_adapter.cpp — GPU test of the C++ TEncSearch-shaped adapter (include/fme_hm.hpp).
+//
+// Drives fme_hm::CtuRowBatcher the way an encoder would (jobs of one CTU row queued, the row
+// submitted, the next row filled while it runs) over a synthetic 416x240 P-frame with 4
+// references, uni- and bi-pred jobs, and checks every result bit-exactly against the CPU
+// oracle (oracle/fme_oracle.c, test infrastructure) run over the same job sequence.  Also
+// checks the single-PU xPatternSearchFracDIF / NN_pred entry points and the error path.
+// Exit status 0 = all equal.  Run by tests/test_gpu_parity.py::test_cpp_hm_adapter.
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <memory>
+#include <random>
+#include <vector>
+
+#include "../../include/fme_hm.hpp"
+#include "../../oracle/fme_oracle.h"
+
+namespace {
+
+const int W = 416, H = 240, CTU = 64, PAD = 80;
+const double kLambda[4] = {7.340, 20.196, 14.797, 20.196};   // LDP QP22
+const int kSizes[][2] = {{8, 4}, {4, 8}, {8, 8}, {16, 8}, {8, 16}, {16, 16}, {32, 16}, {16, 32},
+                         {32, 32}, {64, 32}, {32, 64}, {64, 64}, {4, 16}, {12, 16}, {16, 4},
+                         {16, 12}, {8, 32}, {24, 32}, {32, 8}, {32, 24}, {64, 16}, {48, 64}};
+const int kNumSizes = sizeof(kSizes) / sizeof(kSizes[0]);
+
+int failures = 0;
+#define EXPECT(cond, ...)                 \
+  do {                                    \
+    if (!(cond)) {                        \
+      if (failures < 20) {                \
+        fprintf(stderr, "FAIL: " __VA_ARGS__); \
+        fprintf(stderr, "\n");            \
+      }                                   \
+      failures++;                         \
+    }                                     \
+  } while (0)
+
+std::vector<int16_t> make_picture(int t, uint32_t seed) {
+  std::mt19937 rng(seed);
+  std::uniform_real_distribution<double> U(0.0, 1.0);
+  double a[8], fx[8], fy[8], ph[8];
+  for (int i = 0; i < 8; i++) {
+    a[i] = 10 + 30 * U(rng);
+    fx[i] = 0.01 + 0.19 * U(rng);
+    fy[i] = 0.01 + 0.19 * U(rng);
+    ph[i] = 6.2831853 * U(rng);
+  }
+  std::normal_distribution<double> N(0.0, 2.0);
+  std::vector<int16_t> p((size_t)W * H);
+  for (int y = 0; y < H; y++)
+    for (int x = 0; x < W; x++) {
+      double v = 128;
+      for (int i = 0; i < 8; i++) v += a[i] * std::sin(fx[i] * (x + 0.37 * t) + fy[i] * (y + 0.21 * t) + ph[i]) / 3;
+      v += N(rng);
+      p[(size_t)y * W + x] = (int16_t)std::min(255.0, std::max(0.0, std::round(v)));
+    }
+  return p;
+}
+
+int clip_qpel(int v, int pos, int pic) {   // TComDataCU::clipMv (TComDataCU.cpp:2778-2785)
+  const int vmax = (pic + 8 - pos - 1) << 2, vmin = (-64 - 8 - pos + 1) << 2;
+  return std::min(vmax, std::max(vmin, v));
+}
+int div4_round(int v) { return (v + 2) >> 2; }   // TComMv::divideByPowerOf2 with rounding
+
+bool same(const fme_result& a, const fme_result& b) {
+  return a.mv_int_x == b.mv_int_x && a.mv_int_y == b.mv_int_y && a.mv_x == b.mv_x && a.mv_y == b.mv_y &&
+         a.half_x == b.half_x && a.half_y == b.half_y && a.qtr_x == b.qtr_x && a.qtr_y == b.qtr_y &&
+         a.frac_cost == b.frac_cost && a.cost == b.cost && a.bits == b.bits && a.c == b.c &&
+         a.n_emi == b.n_emi && !memcmp(a.emi, b.emi, sizeof(a.emi)) && a.nn_class == b.nn_class &&
+         a.status == b.status;
+}
+
+}  // namespace
+
+static int run() {
+  using namespace fme_hm;
+  std::vector<std::vector<int16_t>> pics;
+  for (int i = 0; i < 5; i++) pics.push_back(make_picture(i == 4 ? 0 : 4 - i, 7 + i));
+
+  SearchConfig cfg;
+  cfg.qp = 22;
+  cfg.maxJobs = 4096;
+  FracSearch search(cfg);
+  for (int i = 0; i < 5; i++) search.setPicture(i, pics[i].data(), W, W, H);
+  for (int l = 0; l < 4; l++) search.setLambdaSlot(l, kLambda[l]);
+
+  // oracle context over the same inputs
+  fme_config oc{8, 1, 1, 22, 1, 0};
+  std::unique_ptr<orc_ctx> orc(new orc_ctx());
+  orc_init(orc.get(), &oc);
+  std::vector<std::vector<uint8_t>> pics8(5);
+  for (int i = 0; i < 5; i++) {
+    pics8[i].assign(pics[i].begin(), pics[i].end());
+    orc_set_picture(orc.get(), i, pics8[i].data(), W, W, H);
+  }
+  for (int l = 0; l < 4; l++) orc_set_lambda(orc.get(), l, kLambda[l]);
+  const std::vector<float> wts = loadWeights("", 22);
+  orc_load_nn(orc.get(), wts.data());
+
+  // ---- batch path: one row of CTUs at a time ------------------------------------------------
+  std::mt19937 rng(1234);
+  auto R = [&](int lo, int hi) { return std::uniform_int_distribution<int>(lo, hi)(rng); };
+  CtuRowBatcher batcher(search, 2);
+  std::vector<CtuRowBatcher::Ticket> tickets;
+  std::vector<std::vector<fme_job>> row_jobs;
+  std::vector<std::vector<int16_t>> row_keys;
+  const int rows = (H + CTU - 1) / CTU, cols = (W + CTU - 1) / CTU;
+  for (int ry = 0; ry < rows; ry++) {
+    std::vector<fme_job> jobs;
+    std::vector<int16_t> keys;   // oracle copy of the row's key blocks
+    for (int cx = 0; cx < cols; cx++) {
+      for (int k = 0; k < 60; k++) {
+        const int* s = kSizes[R(0, kNumSizes - 1)];
+        const int w = s[0], h = s[1];
+        const int x0 = cx * CTU, y0 = ry * CTU;
+        const int x = std::min(W - w, x0 + 4 * R(0, (CTU - w) / 4)), y = std::min(H - h, y0 + 4 * R(0, (CTU - h) / 4));
+        fme_job j{};
+        j.x = (uint16_t)(x & ~3);
+        j.y = (uint16_t)(y & ~3);
+        j.w = (uint8_t)w;
+        j.h = (uint8_t)h;
+        j.org_id = 4;
+        j.ref_id = (uint8_t)R(0, 3);
+        j.lambda_id = (uint8_t)R(0, 3);
+        j.mvp_x = (int16_t)R(-256, 256);
+        j.mvp_y = (int16_t)R(-256, 256);
+        const int cpx = clip_qpel(j.mvp_x, j.x, W), cpy = clip_qpel(j.mvp_y, j.y, H);
+        j.lt_x = (int16_t)div4_round(clip_qpel(cpx - (64 << 2), j.x, W));
+        j.rb_x = (int16_t)div4_round(clip_qpel(cpx + (64 << 2), j.x, W));
+        j.lt_y = (int16_t)div4_round(clip_qpel(cpy - (64 << 2), j.y, H));
+        j.rb_y = (int16_t)div4_round(clip_qpel(cpy + (64 << 2), j.y, H));
+        j.mv_x = (int16_t)std::min<int>(j.rb_x, std::max<int>(j.lt_x, R(-64, 64)));
+        j.mv_y = (int16_t)std::min<int>(j.rb_y, std::max<int>(j.lt_y, R(-64, 64)));
+        j.bits_in = (uint16_t)R(1, 6);
+        j.flags = FME_JOB_EMI;
+        j.key_offset = -1;
+        if (R(0, 9) == 0) {
+          // bi-pred: key = 2*org - pred_other, unclipped (TComYuv::removeHighFreq)
+          std::vector<int16_t> key((size_t)w * h);
+          const std::vector<int16_t>& org = pics[4];
+          const std::vector<int16_t>& oth = pics[R(0, 3)];
+          const int ox = std::min(W - w, std::max(0, j.x + R(-3, 3))), oy = std::min(H - h, std::max(0, j.y + R(-3, 3)));
+          for (int yy = 0; yy < h; yy++)
+            for (int xx = 0; xx < w; xx++)
+              key[(size_t)yy * w + xx] = (int16_t)(2 * org[(size_t)(j.y + yy) * W + j.x + xx] - oth[(size_t)(oy + yy) * W + ox + xx]);
+          batcher.addBiPred(j, key.data(), w);
+          j.flags = FME_JOB_BIPRED;
+          j.key_offset = (int32_t)keys.size();
+          keys.insert(keys.end(), key.begin(), key.end());
+        } else {
+          batcher.add(j);
+        }
+        jobs.push_back(j);
+      }
+    }
+    tickets.push_back(batcher.submit());   // row ry runs while row ry+1 is built
+    row_jobs.push_back(jobs);
+    row_keys.push_back(keys);
+  }
+  int total = 0;
+  for (int ry = 0; ry < rows; ry++) {
+    const std::vector<fme_result> got = batcher.wait(tickets[ry]);
+    std::vector<fme_result> want(row_jobs[ry].size());
+    orc_set_keys(orc.get(), row_keys[ry].data(), row_keys[ry].size());
+    EXPECT(orc_refine(orc.get(), row_jobs[ry].data(), want.data(), (int)want.size()) == 0, "oracle row %d", ry);
+    EXPECT(got.size() == want.size(), "row %d size", ry);
+    for (size_t i = 0; i < got.size() && i < want.size(); i++)
+      EXPECT(same(got[i], want[i]), "row %d job %zu (%dx%d): mv %d,%d vs %d,%d cost %u vs %u", ry, i,
+             row_jobs[ry][i].w, row_jobs[ry][i].h, got[i].mv_x, got[i].mv_y, want[i].mv_x, want[i].mv_y,
+             got[i].cost, want[i].cost);
+    total += (int)got.size();
+  }
+
+  // ---- error path: an unsupported PU shape rejects the row, the context stays usable --------
+  {
+    fme_job bad = row_jobs[0][0];
+    bad.w = 6;
+    batcher.add(bad);
+    const CtuRowBatcher::Ticket t = batcher.submit();
+    bool threw = false;
+    try {
+      batcher.wait(t);
+    } catch (const Error& e) {
+      threw = e.code() == FME_E_INVALID;
+    }
+    EXPECT(threw, "invalid row did not throw FME_E_INVALID");
+    fme_job ok = row_jobs[0][1];
+    if (ok.flags & FME_JOB_BIPRED) ok = row_jobs[0][2];
+    batcher.add(ok);
+    EXPECT(batcher.wait(batcher.submit()).size() == 1, "row after the error");
+  }
+
+  // ---- single-PU entry points ---------------------------------------------------------------
+  const int PW = W + 2 * PAD;
+  std::vector<std::vector<int16_t>> padded(4, std::vector<int16_t>((size_t)PW * (H + 2 * PAD)));
+  for (int r = 0; r < 4; r++)
+    for (int y = -PAD; y < H + PAD; y++)
+      for (int x = -PAD; x < W + PAD; x++)
+        padded[r][(size_t)(y + PAD) * PW + x + PAD] =
+            pics[r][(size_t)std::min(H - 1, std::max(0, y)) * W + std::min(W - 1, std::max(0, x))];
+  int singles = 0;
+  for (size_t i = 0; i < row_jobs[1].size(); i += 7) {
+    const fme_job& j = row_jobs[1][i];
+    if (j.flags & FME_JOB_BIPRED) continue;
+    std::vector<int16_t> key((size_t)j.w * j.h);
+    for (int yy = 0; yy < j.h; yy++)
+      for (int xx = 0; xx < j.w; xx++) key[(size_t)yy * j.w + xx] = pics[4][(size_t)(j.y + yy) * W + j.x + xx];
+    search.setLambda(kLambda[j.lambda_id]);
+    search.setPredictor(Mv(j.mvp_x, j.mvp_y));
+    Mv mvInt(j.mv_x, j.mv_y), mh, mq;
+    Distortion cost = 0;
+    const int16_t* refY = padded[j.ref_id].data() + (size_t)(j.y + PAD) * PW + j.x + PAD;
+    search.xPatternSearchFracDIF(false, key.data(), j.w, j.w, j.h, refY, PW, &mvInt, mh, mq, cost);
+    orc_picture p{pics8[j.ref_id].data(), W, W, H};
+    int8_t oh[2], oq[2];
+    uint32_t ocost = 0;
+    orc_frac_dif(&p, key.data(), j.w, j.x, j.y, j.w, j.h, j.mv_x, j.mv_y, j.mvp_x, j.mvp_y,
+                 65536.0 * std::sqrt(kLambda[j.lambda_id]), 1, oh, oq, &ocost);
+    EXPECT(mh.hor == oh[0] && mh.ver == oh[1] && mq.hor == oq[0] && mq.ver == oq[1] && cost == ocost,
+           "xPatternSearchFracDIF job %zu: (%d,%d)(%d,%d) %u vs (%d,%d)(%d,%d) %u", i, mh.hor, mh.ver,
+           mq.hor, mq.ver, cost, oh[0], oh[1], oq[0], oq[1], ocost);
+    singles++;
+  }
+  for (int k = 0; k < 100; k++) {
+    uint32_t e[8];
+    for (uint32_t& v : e) v = (uint32_t)R(0, 200000);
+    const uint32_t C = (uint32_t)R(0, 200000);
+    const int* s = kSizes[R(0, kNumSizes - 1)];
+    int xh, xq, yh, yq;
+    const int cls = search.NN_pred(e, C, s[1], s[0], xh, xq, yh, yq);
+    EXPECT(cls == orc_nn_forward(wts.data(), e, C, s[1], s[0], nullptr), "NN_pred %d", k);
+    EXPECT(2 * xh + xq == cls % 7 - 3 && 2 * yh + yq == cls / 7 - 3, "NN_pred offsets %d", k);
+  }
+
+  if (failures) {
+    fprintf(stderr, "hm adapter: %d failure(s)\n", failures);
+    return 1;
+  }
+  printf("hm adapter ok: %d jobs in %d CTU rows, %d single-PU FracDIF calls, 100 NN_pred calls bit-exact\n",
+         total, rows, singles);
+  return 0;
+}
+
+int main() {
+  try {
+    return run();
+  } catch (const fme_hm::Error& e) {
+    fprintf(stderr, "hm adapter: error %d: %s\n", e.code(), e.what());
+    return 2;
+  }
+}

@@ -19,11 +19,11 @@ def header_functions():
 def test_library_exports_header():
     lib = runtime.load_library()
     names = header_functions()
-    assert len(names) == 20
+    assert len(names) == 21
     assert set(names) == set(runtime.ABI_SYMBOLS)
     for n in names:
         assert hasattr(lib, n), n
-    assert lib.fme_abi_version() == 1
+    assert lib.fme_abi_version() == runtime.ABI_VERSION == 2
 
 
 def test_struct_layouts():
@@ -48,3 +48,20 @@ def test_null_arguments_rejected():
     assert b"null" in lib.fme_last_error()
     assert lib.fme_refine(None, None, None, 1, None) == -1
     assert lib.fme_destroy(None) == 0
+
+
+def test_hm_adapter_library_exports():
+    """libfme_hm.so (the C++ TEncSearch-shaped adapter) links against libfme_amd.so and
+    exports the FracSearch / CtuRowBatcher surface include/fme_hm.hpp declares."""
+    import subprocess
+    so = os.path.join(os.path.dirname(runtime.LIB_PATH), "libfme_hm.so")
+    if not os.path.exists(so):
+        pytest.skip("libfme_hm.so not built")
+    out = subprocess.run(["nm", "-DC", "--defined-only", so], capture_output=True, text=True, check=True).stdout
+    for sym in ("fme_hm::FracSearch::xPatternSearchFracDIF", "fme_hm::FracSearch::NN_pred",
+                "fme_hm::FracSearch::setPicture", "fme_hm::CtuRowBatcher::submit",
+                "fme_hm::CtuRowBatcher::wait", "fme_hm::CtuRowBatcher::addBiPred",
+                "fme_hm::loadWeights"):
+        assert sym in out, sym
+    deps = subprocess.run(["ldd", so], capture_output=True, text=True).stdout
+    assert "libfme_amd.so" in deps

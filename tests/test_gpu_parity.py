@@ -6,10 +6,12 @@ size-independent properties: run-to-run determinism, batch-split invariance of t
 NN state, the oracle on a random sample of jobs, and a vectorised float32 NN restatement
 over every job.
 """
+import os
+
 import numpy as np
 import pytest
 
-from conftest import golden_cases, load_golden
+from conftest import ROOT, golden_cases, load_golden
 from nnfme import synth, weights
 from nnfme.abi import (JOB_BIPRED, JOB_DTYPE, JOB_EMI, RESULT_DTYPE, compare_results)
 
@@ -254,3 +256,14 @@ def test_1080p_frame_full_size_properties(frame_1080p):
     # the tail follows from the class
     assert np.array_equal(a["mv_x"], 4 * a["mv_int_x"].astype(np.int32) + a["nn_class"] % 7 - 3)
     assert np.array_equal(a["mv_y"], 4 * a["mv_int_y"].astype(np.int32) + a["nn_class"] // 7 - 3)
+
+
+def test_cpp_hm_adapter():
+    """The C++ TEncSearch-shaped adapter (include/fme_hm.hpp): CTU-row batcher, single-PU
+    xPatternSearchFracDIF and NN_pred, bit-exact against the oracle (tests/cpp)."""
+    import subprocess
+    exe = os.path.join(ROOT, "hm16.9-nn_fme_amd", "host", "test_hm_adapter")
+    assert os.path.exists(exe), "build it with __graft_entry__.build() (make host-test)"
+    p = subprocess.run([exe], capture_output=True, text=True, timeout=300)
+    assert p.returncode == 0, p.stdout + p.stderr
+    assert "hm adapter ok" in p.stdout

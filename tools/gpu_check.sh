@@ -15,6 +15,13 @@ run() {  # name, timeout, command...
 }
 [ "${SKIP_TESTS:-0}" = 1 ] || run pytest_gpu 900 python -m pytest tests -m gpu -x -q -p no:cacheprovider
 [ "${SKIP_TESTS:-0}" = 1 ] || run smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
+if [ "${PMC:-1}" = 1 ]; then
+  # HBM traffic of the search kernels: FETCH_SIZE and WRITE_SIZE in separate passes
+  for c in fetch:FETCH_SIZE write:WRITE_SIZE; do
+    run pmc_${c%%:*} 600 rocprofv3 --pmc ${c##*:} --output-format csv -d gpurun_out/pmc_traffic/${c%%:*} -o run -- python bench.py --steps 2 --warmup 1 --no-cpu-baseline
+  done
+  python3 tools/pmc_traffic.py gpurun_out/pmc_traffic gpurun_out/pmc_traffic.json && cp gpurun_out/pmc_traffic.json profiles/pmc_traffic.json
+fi
 run bench 600 python bench.py --steps "$STEPS" --warmup 3
 if [ "${PROFILE:-1}" = 1 ]; then
   run rocprof 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python bench.py --steps 5 --warmup 2 --no-cpu-baseline
