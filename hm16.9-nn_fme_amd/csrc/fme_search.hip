@@ -42,6 +42,10 @@
 #ifndef FME_TILES_PER_BLOCK
 #define FME_TILES_PER_BLOCK 1
 #endif
+// XCD-aware tile order (see xcd_tile below); 0 = tiles in block order.
+#ifndef FME_XCD_SWIZZLE
+#define FME_XCD_SWIZZLE 1
+#endif
 
 namespace fme {
 
@@ -964,11 +968,26 @@ __device__ __forceinline__ int find_class(const Schedule& sc, int b, int lo, int
   return c;
 }
 
+// Workgroups are dealt round-robin to the 8 XCDs (each with its own L2), so block r of a
+// class runs on XCD (first + r) % 8.  Giving XCD k the k-th contiguous eighth of the class's
+// tiles (tiles follow the CTU-ordered job stream) keeps each XCD on one spatial band of the
+// pictures instead of all eight XCDs fetching every region.
+__device__ __forceinline__ int xcd_tile(int r, int n) {
+#if FME_XCD_SWIZZLE
+  const int k = r & 7;
+  return k * (n >> 3) + min(k, n & 7) + (r >> 3);
+#else
+  (void)n;
+  return r;
+#endif
+}
+
 __global__ __launch_bounds__(kSmallNT) void k_search_small(BatchArgs a, WorkBufs w, Schedule sc) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
   const int b = blockIdx.x + sc.tile_prefix[0];
   const int c = find_class(sc, b, 0, 19);
-  const int blk = b - sc.tile_prefix[c], nblk = sc.tile_prefix[c + 1] - sc.tile_prefix[c];
+  const int nblk = sc.tile_prefix[c + 1] - sc.tile_prefix[c];
+  const int blk = xcd_tile(b - sc.tile_prefix[c], nblk);
   switch (c) {
 #define FME_CASE(ID, W_, H_)                                                                        \
   case ID:                                                                                          \
@@ -985,7 +1004,8 @@ __global__ __launch_bounds__(kLargeNT) void k_search_large(BatchArgs a, WorkBufs
   extern __shared__ __attribute__((aligned(16))) char lds[];
   const int b = blockIdx.x + sc.tile_prefix[19];
   const int c = find_class(sc, b, 19, kNumClasses);
-  const int blk = b - sc.tile_prefix[c], nblk = sc.tile_prefix[c + 1] - sc.tile_prefix[c];
+  const int nblk = sc.tile_prefix[c + 1] - sc.tile_prefix[c];
+  const int blk = xcd_tile(b - sc.tile_prefix[c], nblk);
   switch (c) {
 #define FME_CASE(ID, W_, H_)                                                                        \
   case ID:                                                                                          \

@@ -7,11 +7,13 @@ ring of picture slots.  Ranks keep the last 4 frames (lowdelay_P references) res
 step moves world x 2.07 MB at 1080p, overlapping nothing else on the data path.
 
 NN_pred's carried state (array_e slots, C, PUHeight, PUWidth) crosses frame boundaries in
-the reference.  A rank refines each of its frames from a fresh state; the jobs that read the
-carried state form a prefix of the frame (status FME_RES_NN_UNINIT).  `chain_states` composes
-the per-frame end states in encode order, and the prefix is re-run with the true carry-in
-(fix_frame_prefix).  On real traces the prefix is empty: a frame's first job is a uni-pred
-2Nx2N PU whose EMI step writes all eight slots.
+the reference.  A rank refines each of its frames from a fresh state; jobs that read a slot
+no earlier job of the frame wrote carry status FME_RES_NN_UNINIT.  `chain_states` composes the
+per-frame end states in encode order (an all_gather of 12 words per frame), and the jobs up
+to the last such reader are re-run with the true carry-in (fix_frame_prefix): every later
+job reads only state written inside the frame, which the re-run leaves unchanged.  On real
+traces the re-run is empty or a few jobs: a frame's first job is a uni-pred 2Nx2N PU whose
+EMI step writes all eight slots unless the search range clips it.
 """
 import numpy as np
 
@@ -49,6 +51,12 @@ class PictureRing:
             dist.broadcast(dst, src=self.owner, group=self.group)
         self.frame_of_slot[s] = frame
 
+    def tensor(self, frame):
+        s = self.slot(frame)
+        if self.frame_of_slot[s] != frame:
+            raise RuntimeError(f"frame {frame} is not resident (slot {s} holds {self.frame_of_slot[s]})")
+        return self.buf[s]
+
     def bind(self, ctx, pid, frame):
         s = self.slot(frame)
         if self.frame_of_slot[s] != frame:
@@ -82,18 +90,16 @@ def chain_states(frame_states, initial=None):
 
 
 def uninit_prefix(results):
-    """Number of leading jobs that read the carried state (they form a prefix)."""
+    """Length of the shortest prefix holding every job that read the carried state."""
     m = (results["status"] & RES_NN_UNINIT) != 0
     if not m.any():
         return 0
-    k = int(np.flatnonzero(m)[-1]) + 1
-    if not m[:k].all():
-        raise AssertionError("carried-state readers do not form a prefix")
-    return k
+    return int(np.flatnonzero(m)[-1]) + 1
 
 
 def fix_frame_prefix(engine, jobs, results, carry):
-    """Re-run the carried-state prefix of a frame with its true carry-in."""
+    """Re-run the carried-state prefix of a frame with its true carry-in (engine: anything
+    with nn_set_state/refine over host arrays — FmeContext, or the oracle in tests)."""
     k = uninit_prefix(results)
     if k == 0 or not int(np.asarray(carry)[11]):
         return results
