@@ -16,9 +16,9 @@ one host core (HM is single-threaded) over a bounded sample of the same job mix;
 `cpu_baseline_all_cores` runs one job stream per host core.  Both run
 before the GPU is initialised.
 
-`roofline` is for the dominant kernel, fme::k_search_small (EMI + FracDIF of the 19 PU shapes
-up to 64x16/16x64, ~99 % of the jobs): its algorithmic bytes (SURVEY.md §8(d) per-PU figure
-summed over the jobs it processes) over its average duration, from HIP events recorded
+`roofline` is for the main search launch (the lane-per-unit EMI + FracDIF kernels of the 18
+power-of-two PU shapes, ~99.4 % of the jobs): its algorithmic bytes (SURVEY.md §8(d) per-PU
+figure summed over the jobs it processes) over its average duration, from HIP events recorded
 around it on its own stream during the timed steps.  The path is integer-VALU bound, so the
 VALU roof (reference integer ops, §8(d)) is reported beside the HBM one.
 """
@@ -43,8 +43,6 @@ HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md chip table (spec)
 # int32 VALU lane-ops/s: 256 CUs x 4 SIMDs x 32 lanes/clk (a wave64 op issues over 2 clk) x
 # 2.4 GHz = 78.6 T (MI355X_MICROARCH.md; = the 157.3 TFLOP/s f32 vector peak / 2)
 VALU_PEAK_TOPS = 256 * 4 * 32 * 2.4e9 / 1e12
-# PU shapes (w, h) served by fme::k_search_large (fme_device.h classes 19..23)
-LARGE_SHAPES = {(32, 64), (64, 32), (48, 64), (64, 48), (64, 64)}
 
 
 def algorithmic_bytes(jobs):
@@ -54,10 +52,13 @@ def algorithmic_bytes(jobs):
     return int((w * h + (w + 8) * (h + 8) + 48).sum())
 
 
-def large_mask(jobs):
+def main_kernel_mask(ctx, jobs):
+    """Jobs the main search launch serves (fme_search_kernel_of_shape == 0)."""
     m = np.zeros(len(jobs), bool)
-    for w, h in LARGE_SHAPES:
-        m |= (jobs["w"] == w) & (jobs["h"] == h)
+    shapes = set(zip(jobs["w"].tolist(), jobs["h"].tolist()))
+    for w, h in shapes:
+        if ctx.search_kernel_of_shape(w, h) == 0:
+            m |= (jobs["w"] == w) & (jobs["h"] == h)
     return m
 
 
@@ -291,10 +292,9 @@ def main():
 
     value = world * n * args.steps / elapsed
     if rank == 0:
-        lm = large_mask(jobs)
-        small_jobs = jobs[~lm]
+        small_jobs = jobs[main_kernel_mask(ctx, jobs)]
         bytes_small = algorithmic_bytes(small_jobs)
-        small_s = tm["search_small"] / 1e3
+        small_s = tm["search_main"] / 1e3
         achieved = bytes_small / small_s / 1e9
         ops_small = algorithmic_ops(small_jobs)
         search_s = tm["search"] / 1e3
@@ -324,10 +324,10 @@ def main():
                 "unit": "GB/s",
                 "frac": achieved / HBM_PEAK_GBS,
                 "traffic": traffic,
-                "kernel": "fme::k_search_small (EMI + FracDIF, 19 PU shapes)",
+                "kernel": "main search launch: fme::k_search_lane{48,84,88} (EMI + FracDIF)",
                 "kernel_jobs": int(len(small_jobs)),
                 "algorithmic_bytes_per_launch": bytes_small,
-                "kernel_ms": tm["search_small"],
+                "kernel_ms": tm["search_main"],
                 "profiled_batches": nb,
                 "valu_tops": ops_small / small_s / 1e12,
                 "valu_peak_tops": VALU_PEAK_TOPS,

@@ -390,45 +390,53 @@ int fme_refine_device(fme_ctx* c, const fme_job* d_jobs, fme_result* d_res, int 
                 c->h_counts[kNumClasses]);
 
   Schedule sc{};
-  int off = 0, blocks = 0;
-  const int tpb = tiles_per_block();
+  int off = 0;
+  int nb[kSearchKernels] = {0, 0, 0};
   for (int k = 0; k < kNumClasses; k++) {
     const int cnt = c->h_counts[k];
     sc.class_off[k] = off;
     sc.class_cnt[k] = cnt;
-    sc.tile_prefix[k] = blocks;
-    if (cnt) {
-      const int p = pus_per_tile(k);
-      const int tiles = (cnt + p - 1) / p;
-      blocks += (tiles + tpb - 1) / tpb;
-    }
+    const int kern = search_kernel_of(k);
+    for (int q = 0; q < kSearchKernels; q++) sc.prefix[q][k] = nb[q];
+    nb[kern] += search_blocks_for(k, cnt);
     off += cnt;
   }
-  sc.tile_prefix[kNumClasses] = blocks;
-  const bool has_large = search_large_blocks(sc) > 0;
+  for (int q = 0; q < kSearchKernels; q++) sc.prefix[q][kNumClasses] = nb[q];
+  // main search kernel on the batch stream: the lane-per-unit kernel (or, in -DFME_NO_LANE
+  // builds, the 256-lane cooperative one); the remaining cooperative shapes run beside it on
+  // the auxiliary stream
+  const bool lane_main = nb[kSearchLane48] + nb[kSearchLane84] + nb[kSearchLane88] > 0 || nb[kSearchCoop] == 0;
+  const bool has_aux = lane_main ? (nb[kSearchCoop] + nb[kSearchCoopLarge] > 0) : nb[kSearchCoopLarge] > 0;
+  auto launch_aux = [&](hipStream_t st) -> hipError_t {
+    if (lane_main) {
+      const hipError_t e = launch_search_small(a, w, sc, st);
+      if (e != hipSuccess) return e;
+    }
+    return launch_search_large(a, w, sc, st);
+  };
   if (prof) HIP_TRY(hipEventRecord(ev[2], s));   // host sync above: scatter starts here
   HIP_TRY(launch_scatter(a, w, sc, s));
   if (prof) HIP_TRY(hipEventRecord(ev[3], s));
   if (!c->concurrent_search) {
-    if (prof && has_large) HIP_TRY(hipEventRecord(ev[7], s));
-    HIP_TRY(launch_search_large(a, w, sc, s));
-    if (prof && has_large) HIP_TRY(hipEventRecord(ev[8], s));
-  } else if (has_large) {
+    if (prof && has_aux) HIP_TRY(hipEventRecord(ev[7], s));
+    HIP_TRY(launch_aux(s));
+    if (prof && has_aux) HIP_TRY(hipEventRecord(ev[8], s));
+  } else if (has_aux) {
     HIP_TRY(hipEventRecord(c->ev_fork, s));
     HIP_TRY(hipStreamWaitEvent(c->aux, c->ev_fork, 0));
     if (prof) HIP_TRY(hipEventRecord(ev[7], c->aux));
-    HIP_TRY(launch_search_large(a, w, sc, c->aux));
+    HIP_TRY(launch_aux(c->aux));
     if (prof) HIP_TRY(hipEventRecord(ev[8], c->aux));
     HIP_TRY(hipEventRecord(c->ev_join, c->aux));
   }
-  HIP_TRY(launch_search_small(a, w, sc, s));
+  HIP_TRY(lane_main ? launch_search_lane(a, w, sc, s) : launch_search_small(a, w, sc, s));
   if (prof) HIP_TRY(hipEventRecord(ev[4], s));
-  if (c->concurrent_search && has_large) HIP_TRY(hipStreamWaitEvent(s, c->ev_join, 0));
+  if (c->concurrent_search && has_aux) HIP_TRY(hipStreamWaitEvent(s, c->ev_join, 0));
   if (prof) HIP_TRY(hipEventRecord(ev[5], s));
   HIP_TRY(launch_nn_tail(a, w, c->d_nn.p, c->state_cur, s));
   if (prof) {
     HIP_TRY(hipEventRecord(ev[6], s));
-    c->ev_has_large[eb] = has_large;
+    c->ev_has_large[eb] = has_aux;
     c->ev_serial[eb] = !c->concurrent_search;
     c->ev_pending = eb;
     c->ev_cur ^= 1;
@@ -546,6 +554,17 @@ int fme_nn_pred_single(fme_ctx* c, const uint32_t* e, uint32_t cc, int pu_h, int
     split(oy, out4[2], out4[3]);
   }
   return FME_OK;
+}
+
+int fme_search_kernel_of_shape(int width, int height) {
+  for (int k = 0; k < kNumClasses; k++)
+    if (kClassW[k] == width && kClassH[k] == height) {
+      const int kern = search_kernel_of(k);
+      const bool lane_build = lane_lanes_per_pu(0) > 0;
+      if (lane_build) return kern <= kSearchLane88 ? 0 : 1;
+      return kern == kSearchCoop ? 0 : 1;
+    }
+  return -1;
 }
 
 int fme_set_profiling(fme_ctx* c, int enable) {

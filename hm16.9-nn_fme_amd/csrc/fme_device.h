@@ -50,11 +50,16 @@ struct WorkBufs {
   uint32_t* nn_state;    // 2 x 12 words: slot[8], c, pu_h, pu_w, written
 };
 
-// Schedule of the search kernels: blocks [tile_prefix[c], tile_prefix[c+1]) serve class c
-// (each strides over the class's tiles of pus_per_tile(c) PUs); class c's jobs are
-// sjobs/perm[class_off[c] .. class_off[c] + class_cnt[c]).
+// Schedule of the search kernels.  Kernel k (lane-per-unit with 4x8 / 8x4 / 8x8 units,
+// cooperative 256-lane, cooperative 512-lane) serves class c with its blocks
+// [prefix[k][c], prefix[k][c+1]); every class belongs to exactly one kernel
+// (search_kernel_of).  Class c's jobs are sjobs/perm[class_off[c] .. + class_cnt[c]).
+enum {
+  kSearchLane48 = 0, kSearchLane84 = 1, kSearchLane88 = 2, kSearchCoop = 3, kSearchCoopLarge = 4,
+  kSearchKernels = 5
+};
 struct Schedule {
-  int32_t tile_prefix[kNumClasses + 1];
+  int32_t prefix[kSearchKernels][kNumClasses + 1];
   int32_t class_off[kNumClasses];
   int32_t class_cnt[kNumClasses];
 };
@@ -65,10 +70,14 @@ size_t lds_bytes_for_class(int cls);
 hipError_t launch_classify(const BatchArgs& a, const WorkBufs& w, hipStream_t s);
 hipError_t launch_scatter(const BatchArgs& a, const WorkBufs& w, const Schedule& sc, hipStream_t s);
 int tiles_per_block();
-int search_large_blocks(const Schedule& sc);
-int search_small_blocks(const Schedule& sc);
+int search_kernel_of(int cls);                      // kSearchLane48 .. kSearchCoopLarge
+int search_blocks_for(int cls, int cnt);           // blocks of its kernel for cnt jobs
+hipError_t launch_search_lane(const BatchArgs& a, const WorkBufs& w, const Schedule& sc, hipStream_t s);
 hipError_t launch_search_large(const BatchArgs& a, const WorkBufs& w, const Schedule& sc, hipStream_t s);
 hipError_t launch_search_small(const BatchArgs& a, const WorkBufs& w, const Schedule& sc, hipStream_t s);
+int lane_lanes_per_pu(int cls);                    // 0: not a lane-kernel class
+int lane_kernel_of(int cls);                       // kSearchLane48/84/88, -1: not a lane class
+int lane_blocks_for(int cls, int cnt);
 hipError_t launch_nn_tail(const BatchArgs& a, const WorkBufs& w, const float* nn_params,
                           int state_in, hipStream_t s);
 

@@ -1,0 +1,719 @@
+// fme_lane.hip — lane-per-unit EMI + FracDIF search kernel (gfx950).
+//
+// One lane owns one unit of a PU: the whole PU for 8x4 / 4x8, an 8x4 / 4x8 half for
+// 16x4 / 4x16, an 8x8 block for the power-of-two 8x8-tiled shapes (8x8 .. 64x64).  A PU's
+// L units sit in L consecutive lanes of one wavefront; SATD / SSE partials are summed over
+// those lanes with xor shuffles, so every lane of the group takes the same decisions.  Each
+// lane keeps its reference window in VGPRs as (sample - 128) bytes and never touches LDS:
+//
+//   1. load     window rows -5..UH+4, cols -5..UW+4 around the TZ MV (clamped rows, edge-
+//               replicated columns near the picture border), the key block (org bytes, or
+//               the job's int16 key block for bi-pred), re-aligned to byte 0.
+//   2. EMI      9 integer distortions (SSE = So2 - 2 Sop + Spp with v_dot4_i32_i8 on the
+//               s-128 bytes) and the square-step decision (TEncSearch.cpp:1324-1377,
+//               1155-1188, 5043-5050), then the window is re-centred on mv_int' in place.
+//   3. half     the 9 candidates of xPatternRefinement (TEncSearch.cpp:1591-1645) around
+//               mv_int' in three triples that share their filtered columns: {(0,0),(0,-1),
+//               (0,1)} from the transposed window, {(-1,0),(-1,-1),(-1,1)} and {(1,0),(1,-1),
+//               (1,1)} from the horizontal first stage (xExtDIFUpSamplingH, 6331-6365).
+//   4. quarter  the 8 candidates around the half best (xExtDIFUpSamplingQ, 6378-6532) as
+//               separable 2-D filters with per-lane taps: a phase with fraction 0 uses the
+//               tap set {0,0,0,64,0,0,0,0}, which reproduces HM's copy / 1-D paths exactly
+//               ((64 A + 2048) >> 12 == (A + 32) >> 6).
+// All predictions are formed in the (p - 128) domain: the rounding offsets absorb the 128
+// ((s + 8224) >> 6 - 128 == (s + 32) >> 6 for 1-D, (s + 526336) >> 12 - 128 == (s + 2048)
+// >> 12 for 2-D), and key - pred is unchanged.
+#include <hip/hip_runtime.h>
+
+#include <type_traits>
+
+#include "fme_device.h"
+#include "fme_simd.h"
+
+#ifndef FME_XCD_SWIZZLE
+#define FME_XCD_SWIZZLE 1
+#endif
+// register-pressure experiments only: bit 0 skip quarter stage, 1 skip half sides, 2 skip EMI
+#ifndef FME_LANE_SKIP
+#define FME_LANE_SKIP 0
+#endif
+// occupancy targets (waves per SIMD) that bound the register allocation of each kernel
+#ifndef FME_LANE_WAVES_SMALL
+#define FME_LANE_WAVES_SMALL 2
+#endif
+#ifndef FME_LANE_WAVES_88
+#define FME_LANE_WAVES_88 1
+#endif
+
+namespace fme {
+namespace {
+using namespace simd;
+
+constexpr int kLaneNT = 256;
+
+// ---- small helpers -------------------------------------------------------------------------
+template <int L>
+__device__ __forceinline__ uint32_t group_sum(uint32_t v) {
+#pragma unroll
+  for (int o = L / 2; o >= 1; o >>= 1) v += (uint32_t)__shfl_xor((int)v, o, 64);
+  return v;
+}
+
+// low 16 bits of a and b -> one packed pair (a in the low half)
+__device__ __forceinline__ uint32_t pack2(int a, int b) { return __builtin_amdgcn_perm((uint32_t)b, (uint32_t)a, 0x05040100u); }
+__device__ __forceinline__ int clamp_s8(int v) { return min(max(v, -128), 127); }
+
+// Bytes (b, b+1) of two dwords (row r0 in src1, row r1 in src0) -> sign-extended int16 pair.
+__device__ __forceinline__ uint32_t sext_pair(uint32_t hi_row, uint32_t lo_row, int byte) {
+  const uint32_t sel = (uint32_t)byte | 0x0c00u | ((uint32_t)(4 + byte) << 16) | 0x0c000000u;
+  const uint32_t z = __builtin_amdgcn_perm(hi_row, lo_row, sel);    // zero-extended s' bytes
+  return pk_sub(z ^ 0x00800080u, 0x00800080u);                       // sign extension
+}
+
+// Opaque to the optimiser (no instructions): values derived from the window before this point
+// are not reused after it, so common subexpressions do not stay live across passes.
+template <int R, int N>
+__device__ __forceinline__ void launder(uint32_t (&v)[R][N]) {
+#pragma unroll
+  for (int r = 0; r < R; r++)
+#pragma unroll
+    for (int k = 0; k < N; k++) asm volatile("" : "+v"(v[r][k]));
+}
+
+// 4 bytes starting at byte b of a row held in dwords v[0..N).  Every caller passes a b that
+// is a compile-time constant after unrolling, so the register indices fold.
+template <int N>
+__device__ __forceinline__ uint32_t rbytes(const uint32_t (&v)[N], int b) {
+  const int q = b >> 2, r = b & 3;
+  return r == 0 ? v[q] : __builtin_amdgcn_alignbyte(v[q + 1], v[q], (uint32_t)r);
+}
+// 4 bytes starting at byte b + d, d in {0, 1} per lane (b constant after unrolling)
+template <int N>
+__device__ __forceinline__ uint32_t rbytes_d(const uint32_t (&v)[N], int b, uint32_t d) {
+  const int q = b >> 2, r = b & 3;
+  const uint32_t lo = v[q], hi = v[q + 1];
+  return r == 3 ? (d ? hi : __builtin_amdgcn_alignbyte(hi, lo, 3u))
+                : __builtin_amdgcn_alignbyte(hi, lo, (uint32_t)r + d);
+}
+// bytes b, b+1 of one dword -> sign-extended int16 pair
+__device__ __forceinline__ uint32_t sext_bytes(uint32_t d, int b) {
+  const uint32_t sel = (uint32_t)b | 0x0c00u | ((uint32_t)(b + 1) << 16) | 0x0c000000u;
+  return pk_sub(__builtin_amdgcn_perm(0u, d, sel) ^ 0x00800080u, 0x00800080u);
+}
+
+// 8-tap luma filter taps for fraction f in 0..3 as int8 quads (f = 0: 64 at tap 3).
+__device__ __forceinline__ void taps8_any(int f, uint32_t& lo, uint32_t& hi) {
+  const uint32_t l1 = q8(-1, 4, -10, 58), h1 = q8(17, -5, 1, 0);
+  const uint32_t l2 = q8(-1, 4, -11, 40), h2 = q8(40, -11, 4, -1);
+  const uint32_t l3 = q8(0, 1, -5, 17), h3 = q8(58, -10, 4, -1);
+  const uint32_t l0 = q8(0, 0, 0, 64), h0 = 0u;
+  lo = f == 0 ? l0 : (f == 1 ? l1 : (f == 2 ? l2 : l3));
+  hi = f == 0 ? h0 : (f == 1 ? h1 : (f == 2 ? h2 : h3));
+}
+// tap k of fraction f (k outside 0..7 -> 0)
+__device__ __forceinline__ int tap(int f, int k) {
+  // rows: f = 0..3, taps 0..7 (TComInterpolationFilter.cpp:57-63)
+  const int t0 = k == 3 ? 64 : 0;
+  const int t1 = k == 0 ? -1 : k == 1 ? 4 : k == 2 ? -10 : k == 3 ? 58 : k == 4 ? 17 : k == 5 ? -5 : k == 6 ? 1 : 0;
+  const int t2 = k == 0 ? -1 : k == 1 ? 4 : k == 2 ? -11 : k == 3 ? 40 : k == 4 ? 40 : k == 5 ? -11 : k == 6 ? 4 : k == 7 ? -1 : 0;
+  const int t3 = k == 1 ? 1 : k == 2 ? -5 : k == 3 ? 17 : k == 4 ? 58 : k == 5 ? -10 : k == 6 ? 4 : k == 7 ? -1 : 0;
+  if (k < 0 || k > 7) return 0;
+  return f == 0 ? t0 : (f == 1 ? t1 : (f == 2 ? t2 : t3));
+}
+// Coefficient pairs for a vertical 8-tap filter of fraction f whose taps start `o` rows into
+// a span of 10 rows read as 5 packed row pairs: pair t = (tap(2t - o), tap(2t + 1 - o)).
+__device__ __forceinline__ void vpairs(int f, int o, uint32_t (&c)[5]) {
+#pragma unroll
+  for (int t = 0; t < 5; t++) c[t] = p16(tap(f, 2 * t - o), tap(f, 2 * t + 1 - o));
+}
+
+// ---- distortion of one unit for one candidate ------------------------------------------------
+// X[c][j]: key - pred, column c, rows (2j, 2j+1) packed.  Sum over the unit's T x T tiles of
+// xCalcHADs (had) or SAD.
+template <int UW, int UH, int T>
+__device__ __forceinline__ uint32_t unit_dist(uint32_t (&X)[UW][UH / 2], bool had) {
+  uint32_t s = 0;
+#pragma unroll
+  for (int ty = 0; ty < UH / T; ty++)
+#pragma unroll
+    for (int tx = 0; tx < UW / T; tx++) {
+      uint32_t Y[T][T / 2];
+#pragma unroll
+      for (int c = 0; c < T; c++)
+#pragma unroll
+        for (int j = 0; j < T / 2; j++) Y[c][j] = X[tx * T + c][ty * (T / 2) + j];
+      if (had) {
+        s += satd_packed<T>(Y);
+      } else {
+        s += sad_packed<T>(Y);
+      }
+    }
+  return s;
+}
+
+// Candidate offsets (xPatternRefinement tables, TEncSearch.cpp:212-236).
+__device__ __forceinline__ constexpr int h9_dx(int i) { return (i == 3 || i == 5 || i == 7) ? -1 : ((i == 4 || i == 6 || i == 8) ? 1 : 0); }
+__device__ __forceinline__ constexpr int h9_dy(int i) { return (i == 1 || i == 5 || i == 6) ? -1 : ((i == 2 || i == 7 || i == 8) ? 1 : 0); }
+__device__ __forceinline__ constexpr int q9_dx(int i) { return (i == 3 || i == 5 || i == 7) ? -1 : ((i == 4 || i == 6 || i == 8) ? 1 : 0); }
+__device__ __forceinline__ constexpr int q9_dy(int i) { return (i == 1 || i == 3 || i == 4) ? -1 : ((i == 2 || i == 7 || i == 8) ? 1 : 0); }
+// Q9 index of (dqx, dqy)
+__device__ __forceinline__ constexpr int q9_index(int dx, int dy) {
+  return dy == 0 ? (dx == 0 ? 0 : (dx < 0 ? 5 : 6)) : dy < 0 ? (dx == 0 ? 1 : (dx < 0 ? 3 : 4)) : (dx == 0 ? 2 : (dx < 0 ? 7 : 8));
+}
+// EMI positions: 0 centre, then TL, T, TR, L, R, BL, B, BR (xTZ8PointSquareSearch order)
+__device__ __forceinline__ constexpr int emi_dx(int p) { return (p == 1 || p == 4 || p == 6) ? -1 : ((p == 3 || p == 5 || p == 8) ? 1 : 0); }
+__device__ __forceinline__ constexpr int emi_dy(int p) { return p >= 1 && p <= 3 ? -1 : (p >= 6 ? 1 : 0); }
+
+typedef uint32_t u32x4a __attribute__((ext_vector_type(4), aligned(4)));
+typedef uint32_t u32x2a __attribute__((ext_vector_type(2), aligned(4)));
+typedef __attribute__((address_space(1))) const u32x4a gu4;
+typedef __attribute__((address_space(1))) const u32x2a gu2;
+typedef __attribute__((address_space(1))) const uint16_t gu16;
+
+// N dwords of picture row `row` from byte xb (4-aligned); edge-replicated when not inside.
+template <int N>
+__device__ __forceinline__ void load_row(const uint8_t* row, int xb, int width, bool inside, uint32_t (&out)[N]) {
+  if (inside) {
+    const uint8_t* p = row + xb;
+    int k = 0;
+#pragma unroll
+    for (; k + 4 <= N; k += 4) {
+      const u32x4a v = *(gu4*)(p + 4 * k);
+      out[k] = v.x; out[k + 1] = v.y; out[k + 2] = v.z; out[k + 3] = v.w;
+    }
+#pragma unroll
+    for (; k + 2 <= N; k += 2) {
+      const u32x2a v = *(gu2*)(p + 4 * k);
+      out[k] = v.x; out[k + 1] = v.y;
+    }
+#pragma unroll
+    for (; k < N; k++) out[k] = gld32(p + 4 * k);
+  } else {
+#pragma unroll
+    for (int k = 0; k < N; k++) {
+      uint32_t v = 0;
+#pragma unroll
+      for (int b = 0; b < 4; b++) v |= gld8(row + clamp_i(xb + 4 * k + b, 0, width - 1)) << (8 * b);
+      out[k] = v;
+    }
+  }
+}
+
+// =============================================================================================
+// One lane: unit (ux, uy) of PU p of class (PW x PH), unit UW x UH.
+// =============================================================================================
+template <int PW, int PH, int UW, int UH>
+__device__ __forceinline__ void lane_unit(const BatchArgs& a, const fme_job* __restrict__ sjobs,
+                                          const int32_t* __restrict__ perm, int cls_off, int cls_cnt,
+                                          int blk) {
+  constexpr int T = ((PW % 8) == 0 && (PH % 8) == 0) ? 8 : 4;
+  static_assert(UW % T == 0 && UH % T == 0, "unit must hold whole SATD tiles");
+  constexpr int UX = PW / UW, L = UX * (PH / UH);
+  static_assert((L & (L - 1)) == 0 && L <= 64, "lanes per PU must be a power of two");
+  constexpr int RW = UH + 10;                 // window rows (-5 .. UH+4)
+  constexpr int NWL = (UW + 13 + 3) / 4;      // dwords loaded per row (any start alignment)
+  constexpr int NW = (UW + 10 + 3) / 4;       // dwords per row after re-alignment
+  constexpr int RV = UH + 8;                  // re-centred window rows (-4 .. UH+3)
+  constexpr int NV = UW / 4 + 2;              // re-centred dwords per row (cols -4 .. UW+3)
+  constexpr int UJ = UH / 2;                  // packed row pairs per column
+
+  const int gl = blk * kLaneNT + (int)threadIdx.x;
+  int p = gl / L;
+  const int u = gl - p * L;
+  const bool active = p < cls_cnt;
+  if (!active) p = cls_cnt - 1;              // duplicate work, no stores (keeps the group whole)
+  const int ux = u % UX, uy = u / UX;
+
+  const fme_job j = sjobs[cls_off + p];
+  const int jid = perm[cls_off + p];
+  const PicDesc ref = a.pics[j.ref_id];
+  const double ml = a.mlambda[j.lambda_id];
+  const bool had = a.use_hadamard && !(j.flags & FME_JOB_LOSSLESS);
+  const bool kbuf = j.key_offset >= 0;
+  const int ox = (int)j.x + ux * UW, oy = (int)j.y + uy * UH;   // unit origin
+  const int mvp_x = j.mvp_x, mvp_y = j.mvp_y;
+
+  // ---- 1. loads ------------------------------------------------------------------------------
+  uint32_t w[RW][NW];
+  {
+    const int px0 = ox + j.mv_x - 5, py0 = oy + j.mv_y - 5;
+    const int xb = px0 & ~3;
+    const uint32_t s0 = (uint32_t)(px0 - xb);
+    const bool inside = xb >= 0 && xb + 4 * NWL <= ref.width;
+    uint32_t raw[RW][NWL];
+#pragma unroll
+    for (int r = 0; r < RW; r++) {
+      const int yy = clamp_i(py0 + r, 0, ref.height - 1);
+      load_row<NWL>(ref.luma + (size_t)yy * ref.stride, xb, ref.width, inside, raw[r]);
+    }
+#pragma unroll
+    for (int r = 0; r < RW; r++)
+#pragma unroll
+      for (int k = 0; k < NW; k++) w[r][k] = __builtin_amdgcn_alignbyte(raw[r][k + 1], raw[r][k], s0) ^ 0x80808080u;
+  }
+  // key: org bytes (s - 128) or the job's int16 key block
+  uint32_t o[UH][UW / 4];      // org bytes, rows
+  uint32_t kr[UH][UW / 2];     // key int16 pairs (cols 2k, 2k+1), rows
+  if (!kbuf) {
+    const PicDesc org = a.pics[j.org_id];
+#pragma unroll
+    for (int r = 0; r < UH; r++) {
+      const uint8_t* q = org.luma + (size_t)(oy + r) * org.stride + ox;
+      if constexpr (UW == 8) {
+        const u32x2a v = *(gu2*)q;
+        o[r][0] = v.x ^ 0x80808080u;
+        o[r][1] = v.y ^ 0x80808080u;
+      } else {
+        o[r][0] = gld32(q) ^ 0x80808080u;
+      }
+#pragma unroll
+      for (int k = 0; k < UW / 2; k++) kr[r][k] = 0;
+    }
+  } else {
+    const int16_t* kb = a.keys + (size_t)j.key_offset + (size_t)(uy * UH) * PW + ux * UW;
+#pragma unroll
+    for (int r = 0; r < UH; r++) {
+#pragma unroll
+      for (int k = 0; k < UW / 2; k++) {
+        const uint32_t lo = *(gu16*)(kb + r * PW + 2 * k), hi = *(gu16*)(kb + r * PW + 2 * k + 1);
+        kr[r][k] = lo | (hi << 16);
+      }
+#pragma unroll
+      for (int k = 0; k < UW / 4; k++) o[r][k] = 0;
+    }
+  }
+
+  // ---- 2. EMI square step -----------------------------------------------------------------------
+  int mvx = j.mv_x, mvy = j.mv_y;
+  int ex = 0, ey = 0, n_emi = 0;
+  uint32_t cval = 0, emi[8];
+#pragma unroll
+  for (int k = 0; k < 8; k++) emi[k] = 0;
+  if (!(FME_LANE_SKIP & 4) && (j.flags & FME_JOB_EMI)) {
+    uint32_t e9[9];
+    if (!kbuf) {
+      int so2 = 0;
+#pragma unroll
+      for (int r = 0; r < UH; r++)
+#pragma unroll
+        for (int k = 0; k < UW / 4; k++) so2 = dot4(o[r][k], o[r][k], so2);
+#pragma unroll
+      for (int pos = 0; pos < 9; pos++) {
+        const int dx = emi_dx(pos), dy = emi_dy(pos);
+        int sop = 0, spp = 0;
+#pragma unroll
+        for (int r = 0; r < UH; r++) {
+          const uint32_t(&row)[NW] = w[5 + dy + r];
+#pragma unroll
+          for (int k = 0; k < UW / 4; k++) {
+            const uint32_t pv = rbytes(row, 5 + dx + 4 * k);
+            sop = dot4(o[r][k], pv, sop);
+            spp = dot4(pv, pv, spp);
+          }
+        }
+        e9[pos] = (uint32_t)(so2 - 2 * sop + spp);
+      }
+    } else {
+#pragma unroll
+      for (int pos = 0; pos < 9; pos++) {
+        const int dx = emi_dx(pos), dy = emi_dy(pos);
+        int s = 0;
+#pragma unroll
+        for (int r = 0; r < UH; r++) {
+          const uint32_t(&row)[NW] = w[5 + dy + r];
+#pragma unroll
+          for (int k = 0; k < UW / 4; k++) {
+            const uint32_t x = rbytes(row, 5 + dx + 4 * k) ^ 0x80808080u;   // samples 0..255
+            const uint32_t d0 = pk_sub(kr[r][2 * k], lo_pair(x));
+            const uint32_t d1 = pk_sub(kr[r][2 * k + 1], hi_pair(x));
+            s = dot2(d0, d0, s);
+            s = dot2(d1, d1, s);
+          }
+        }
+        e9[pos] = (uint32_t)s;
+      }
+    }
+#pragma unroll
+    for (int pos = 0; pos < 9; pos++) e9[pos] = group_sum<L>(e9[pos]);
+    // decision (TEncSearch.cpp:1341-1376 visiting order and range checks, 1155-1188 update)
+    const int sx = mvx, sy = mvy;
+    uint32_t best = e9[0] + mv_cost(ml, mv_bits(sx, sy, 2, mvp_x, mvp_y));
+    uint32_t best_cost = best - e9[0];
+    int bx = sx, by = sy;
+    const bool top = sy - 1 >= j.lt_y, bot = sy + 1 <= j.rb_y;
+    const bool left = sx - 1 >= j.lt_x, right = sx + 1 <= j.rb_x;
+#pragma unroll
+    for (int pos = 1; pos <= 8; pos++) {
+      const int dx = emi_dx(pos), dy = emi_dy(pos);
+      const bool ok = (dy == -1 ? top : (dy == 1 ? bot : true)) && (dx == -1 ? left : (dx == 1 ? right : true));
+      if (ok) {
+        const uint32_t d = e9[pos];
+        // emi[n_emi++] = d with a static register index
+#pragma unroll
+        for (int k = 0; k < 8; k++)
+          if (k == n_emi) emi[k] = d;
+        n_emi++;
+        if (d < best) {
+          const uint32_t cst = mv_cost(ml, mv_bits(sx + dx, sy + dy, 2, mvp_x, mvp_y));
+          const uint32_t dc = d + cst;
+          if (dc < best) {
+            best = dc;
+            best_cost = cst;
+            bx = sx + dx;
+            by = sy + dy;
+          }
+        }
+      }
+    }
+    cval = best - best_cost;
+    ex = bx - sx;
+    ey = by - sy;
+    mvx = bx;
+    mvy = by;
+  }
+  typedef __attribute__((address_space(1))) u32x4a gw4;
+  uint8_t* const rec = reinterpret_cast<uint8_t*>(a.res + jid);
+  if (active && u == 0) {   // bytes 16..63 of the record: cost, bits (NN tail), c, emi[8], n_emi
+    u32x4a q0, q1, q2;
+    q0.x = 0; q0.y = 0; q0.z = cval; q0.w = emi[0];
+    q1.x = emi[1]; q1.y = emi[2]; q1.z = emi[3]; q1.w = emi[4];
+    q2.x = emi[5]; q2.y = emi[6]; q2.z = emi[7]; q2.w = (uint32_t)n_emi;
+    *(gw4*)(rec + 16) = q0;
+    *(gw4*)(rec + 32) = q1;
+    *(gw4*)(rec + 48) = q2;
+  }
+
+  // ---- re-centre the window on mv_int': rows -4..UH+3, cols -4..UW+3 ---------------------------
+  uint32_t v[RV][NV];
+  {
+    const uint32_t sh = (uint32_t)(1 + ex);
+#pragma unroll
+    for (int r = 0; r < RV; r++) {
+      uint32_t srow[NV + 1];
+#pragma unroll
+      for (int k = 0; k <= NV; k++) srow[k] = ey < 0 ? w[r][k] : (ey == 0 ? w[r + 1][k] : w[r + 2][k]);
+#pragma unroll
+      for (int k = 0; k < NV; k++) v[r][k] = __builtin_amdgcn_alignbyte(srow[k + 1], srow[k], sh);
+    }
+  }
+
+  // ---- key as signed int16 (key - 128) pairs: K[c][j] = (row 2j, row 2j+1) of column c ------------
+  uint32_t K[UW][UJ];
+#pragma unroll
+  for (int c = 0; c < UW; c++)
+#pragma unroll
+    for (int jj = 0; jj < UJ; jj++) {
+      const uint32_t ko = sext_pair(o[2 * jj + 1][c >> 2], o[2 * jj][c >> 2], c & 3);
+      const uint32_t hs = (c & 1) ? 0x07060302u : 0x05040100u;   // 16-bit half c&1 of each row
+      const uint32_t kb = pk_sub(__builtin_amdgcn_perm(kr[2 * jj + 1][c >> 1], kr[2 * jj][c >> 1], hs), 0x00800080u);
+      K[c][jj] = kbuf ? kb : ko;
+    }
+
+  // ---- 3. half-pel stage (H9 order: (0,0),(0,-1),(0,1),(-1,0),(1,0),(-1,-1),(1,-1),(-1,1),(1,1)) ---
+  // At most two candidates' key - pred arrays are live at a time (register budget).
+  // candidates arrive out of H9 order: keep the first strict minimum in H9 order with an index
+  // tie-break (d < best, or d == best at a lower index)
+  uint32_t hbest = 0xFFFFFFFFu;
+  int hbi = 9;
+  auto half_cand = [&](int i, uint32_t part) {
+    const uint32_t d = group_sum<L>(part) + mv_cost(ml, mv_bits(2 * mvx + h9_dx(i), 2 * mvy + h9_dy(i), 1, mvp_x, mvp_y));
+    if (d < hbest || (d == hbest && i < hbi)) {
+      hbest = d;
+      hbi = i;
+    }
+  };
+  {
+    uint32_t c2lo, c2hi;
+    taps8(2, c2lo, c2hi);
+    // (0,0): integer samples, window' rows 4+y, cols 4+x
+    if (!(FME_LANE_SKIP & 16)) {
+      uint32_t X[UW][UJ];
+#pragma unroll
+      for (int x = 0; x < UW; x++)
+#pragma unroll
+        for (int jj = 0; jj < UJ; jj++)
+          X[x][jj] = pk_sub(K[x][jj], sext_pair(v[5 + 2 * jj][(x + 4) >> 2], v[4 + 2 * jj][(x + 4) >> 2], (x + 4) & 3));
+      half_cand(0, unit_dist<UW, UH, T>(X, had));
+    }
+    // (0,-1), (0,1): vertical half-pel on integer columns (transposed window')
+    if (!(FME_LANE_SKIP & 8)) {
+      launder(v);
+      uint32_t X1[UW][UJ], X2[UW][UJ];
+#pragma unroll
+      for (int g = 0; g < UW / 4; g++) {
+        uint32_t CB[4][RV / 4];   // columns 4g..4g+3 (window' cols 4g+4 ..), 4 rows per dword
+#pragma unroll
+        for (int q = 0; q < RV / 4; q++) {
+          const uint32_t rows[4] = {v[4 * q][g + 1], v[4 * q + 1][g + 1], v[4 * q + 2][g + 1], v[4 * q + 3][g + 1]};
+          uint32_t cols[4];
+          transpose4x4(rows, cols);
+#pragma unroll
+          for (int c = 0; c < 4; c++) CB[c][q] = cols[c];
+        }
+#pragma unroll
+        for (int c4 = 0; c4 < 4; c4++) {
+          const int x = 4 * g + c4;
+          int v1[UH + 1];   // half rows i = 0..UH (between rows i-1, i): taps on window' rows i..i+7
+#pragma unroll
+          for (int i = 0; i <= UH; i++) {
+            const int acc = dot4(rbytes(CB[c4], i), c2lo, 32);
+            v1[i] = clamp_s8(dot4(rbytes(CB[c4], i + 4), c2hi, acc) >> 6);
+          }
+#pragma unroll
+          for (int jj = 0; jj < UJ; jj++) {
+            X1[x][jj] = pk_sub(K[x][jj], pack2(v1[2 * jj], v1[2 * jj + 1]));
+            X2[x][jj] = pk_sub(K[x][jj], pack2(v1[2 * jj + 1], v1[2 * jj + 2]));
+          }
+        }
+      }
+      half_cand(1, unit_dist<UW, UH, T>(X1, had));
+      half_cand(2, unit_dist<UW, UH, T>(X2, had));
+    }
+    const uint32_t c16[4] = {p16(-1, 4), p16(-11, 40), p16(40, -11), p16(4, -1)};
+    const uint32_t c16o[5] = {p16(0, -1), p16(4, -11), p16(40, 40), p16(-11, 4), p16(-1, 0)};
+    // passes instantiated per side (a rolled loop would index the window registers dynamically)
+    auto side_pass = [&](auto side_c) {
+      constexpr int side = decltype(side_c)::value;
+      // (s,0): horizontal half-pel, half column jc = x + side (window' bytes jc .. jc+7)
+      {
+        launder(v);
+        uint32_t X[UW][UJ];
+#pragma unroll
+        for (int x = 0; x < UW; x++) {
+          const int jc = x + side;
+          int h1[UH];
+#pragma unroll
+          for (int y = 0; y < UH; y++) {
+            const uint32_t(&row)[NV] = v[y + 4];
+            h1[y] = clamp_s8(dot4(rbytes(row, jc + 4), c2hi, dot4(rbytes(row, jc), c2lo, 32)) >> 6);
+          }
+#pragma unroll
+          for (int jj = 0; jj < UJ; jj++) X[x][jj] = pk_sub(K[x][jj], pack2(h1[2 * jj], h1[2 * jj + 1]));
+        }
+        half_cand(3 + side, unit_dist<UW, UH, T>(X, had));
+      }
+      // (s,-1), (s,1): 2-D half-pel (first stage rows -4..UH+3 of half column jc, then vertical)
+      {
+        launder(v);
+        uint32_t XB[UW][UJ], XC[UW][UJ];
+#pragma unroll
+        for (int x = 0; x < UW; x++) {
+          const int jc = x + side;
+          launder(v);
+          uint32_t HP[RV / 2];
+#pragma unroll
+          for (int r = 0; r < RV; r += 2) {
+            const int h0 = dot4(rbytes(v[r], jc + 4), c2hi, dot4(rbytes(v[r], jc), c2lo, 0));
+            const int h1 = dot4(rbytes(v[r + 1], jc + 4), c2hi, dot4(rbytes(v[r + 1], jc), c2lo, 0));
+            HP[r / 2] = pack2(h0, h1);
+          }
+          int v2[UH + 1];
+#pragma unroll
+          for (int i = 0; i <= UH; i++) {
+            int acc = 2048;
+            if ((i & 1) == 0) {
+#pragma unroll
+              for (int t = 0; t < 4; t++) acc = dot2(HP[i / 2 + t], c16[t], acc);
+            } else {
+#pragma unroll
+              for (int t = 0; t < 5; t++) acc = dot2(HP[(i - 1) / 2 + t], c16o[t], acc);
+            }
+            v2[i] = clamp_s8(acc >> 12);
+          }
+#pragma unroll
+          for (int jj = 0; jj < UJ; jj++) {
+            XB[x][jj] = pk_sub(K[x][jj], pack2(v2[2 * jj], v2[2 * jj + 1]));
+            XC[x][jj] = pk_sub(K[x][jj], pack2(v2[2 * jj + 1], v2[2 * jj + 2]));
+          }
+          __builtin_amdgcn_sched_barrier(0);   // one column at a time (register pressure)
+        }
+        half_cand(5 + side, unit_dist<UW, UH, T>(XB, had));
+        half_cand(7 + side, unit_dist<UW, UH, T>(XC, had));
+      }
+    };
+    if (!(FME_LANE_SKIP & 2)) {
+      side_pass(std::integral_constant<int, 0>{});
+      side_pass(std::integral_constant<int, 1>{});
+    }
+  }
+  const int hx = h9_dx(hbi), hy = h9_dy(hbi);
+
+  // ---- 4. quarter-pel stage: column phase k (dqx = k-1), row phase l (dqy = l-1) ----------------
+  // Passes of at most two candidates sharing a column phase: k0{l0,l1} k0{l2} k1{l0,l2}
+  // k2{l0,l1} k2{l2}; candidate (k1,l1) is the half best itself.
+  uint32_t qbest = hbest;   // Q9 candidate 0 is the half best: same distortion, same bits
+  int qbi = 0;
+  auto qtr_cand = [&](int i, uint32_t part) {
+    const int qx = 2 * hx + q9_dx(i), qy = 2 * hy + q9_dy(i);
+    const uint32_t d = group_sum<L>(part) + mv_cost(ml, mv_bits(4 * mvx + qx, 4 * mvy + qy, 0, mvp_x, mvp_y));
+    if (d < qbest || (d == qbest && i < qbi)) {
+      qbest = d;
+      qbi = i;
+    }
+  };
+  {
+    auto qpass = [&](auto ps_c) {
+      constexpr int ps = decltype(ps_c)::value;
+      constexpr int PK[5] = {0, 0, 1, 2, 2};
+      constexpr int PL0[5] = {0, 2, 0, 0, 2};
+      constexpr int PL1[5] = {1, -1, 2, 1, -1};
+      constexpr int k = PK[ps];
+      const int qx = 2 * hx + (k - 1);
+      const int ix = qx >> 2, fx = qx & 3;
+      const uint32_t dlt = (uint32_t)(1 + ix);
+      uint32_t clo, chi;
+      taps8_any(fx, clo, chi);
+      constexpr int NPASS = PL1[ps] < 0 ? 1 : 2;
+      constexpr int ls[2] = {PL0[ps], PL1[ps]};
+      uint32_t cpe[NPASS][5], cpo[NPASS][5];
+#pragma unroll
+      for (int m = 0; m < NPASS; m++) {
+        const int l = ls[m];
+        const int qy = 2 * hy + (l - 1);
+        const int iy = qy >> 2, fy = qy & 3;
+        vpairs(fy, 1 + iy, cpe[m]);
+        vpairs(fy, 2 + iy, cpo[m]);
+      }
+      uint32_t XQ[NPASS][UW][UJ];
+#pragma unroll
+      for (int x = 0; x < UW; x++) {
+        launder(v);
+        uint32_t HQ[RV / 2];
+#pragma unroll
+        for (int r = 0; r < RV; r += 2) {
+          const int h0 = dot4(rbytes_d(v[r], x + 4, dlt), chi, dot4(rbytes_d(v[r], x, dlt), clo, 0));
+          const int h1 = dot4(rbytes_d(v[r + 1], x + 4, dlt), chi, dot4(rbytes_d(v[r + 1], x, dlt), clo, 0));
+          HQ[r / 2] = pack2(h0, h1);
+        }
+#pragma unroll
+        for (int m = 0; m < NPASS; m++) {
+          int vq[UH];
+#pragma unroll
+          for (int y = 0; y < UH; y++) {
+            const int m0 = (y & 1) ? (y - 1) / 2 : y / 2;
+            int acc = 2048;
+#pragma unroll
+            for (int t = 0; t < 5; t++) acc = dot2(HQ[m0 + t], (y & 1) ? cpo[m][t] : cpe[m][t], acc);
+            vq[y] = clamp_s8(acc >> 12);
+          }
+#pragma unroll
+          for (int jj = 0; jj < UJ; jj++) XQ[m][x][jj] = pk_sub(K[x][jj], pack2(vq[2 * jj], vq[2 * jj + 1]));
+        }
+        __builtin_amdgcn_sched_barrier(0);   // one column at a time (register pressure)
+      }
+#pragma unroll
+      for (int m = 0; m < NPASS; m++) qtr_cand(q9_index(k - 1, ls[m] - 1), unit_dist<UW, UH, T>(XQ[m], had));
+    };
+    if (!(FME_LANE_SKIP & 1)) {
+      qpass(std::integral_constant<int, 0>{});
+      qpass(std::integral_constant<int, 1>{});
+      qpass(std::integral_constant<int, 2>{});
+      qpass(std::integral_constant<int, 3>{});
+      qpass(std::integral_constant<int, 4>{});
+    }
+  }
+  const int bq = qbi;
+
+  // ---- results: bytes 0..15 (mv_int, mv (NN tail), half, qtr, frac_cost) ------------------------
+  if (active && u == 0) {
+    u32x4a q;
+    q.x = (uint32_t)(uint16_t)mvx | ((uint32_t)(uint16_t)mvy << 16);
+    q.y = 0;
+    q.z = (uint32_t)(uint8_t)hx | ((uint32_t)(uint8_t)hy << 8) | ((uint32_t)(uint8_t)q9_dx(bq) << 16) |
+          ((uint32_t)(uint8_t)q9_dy(bq) << 24);
+    q.w = qbest;
+    *(gw4*)rec = q;
+  }
+}
+
+// Workgroups go round-robin to the 8 XCDs: give XCD k the k-th contiguous eighth of a class's
+// blocks (one spatial band of the CTU-ordered job stream) so each L2 sees one band.
+__device__ __forceinline__ int xcd_block(int r, int n) {
+#if FME_XCD_SWIZZLE
+  const int k = r & 7;
+  return k * (n >> 3) + min(k, n & 7) + (r >> 3);
+#else
+  (void)n;
+  return r;
+#endif
+}
+
+}  // namespace
+
+// (class id, PU W, PU H, unit W, unit H) — fme_device.h class table; one kernel per unit
+// shape, since a kernel's register allocation is the maximum over its cases.
+#define FME_LANE48_CLASSES(X) X(0, 4, 8, 4, 8) X(3, 4, 16, 4, 8)
+#define FME_LANE84_CLASSES(X) X(1, 8, 4, 8, 4) X(4, 16, 4, 8, 4)
+#define FME_LANE88_CLASSES(X)                                                                        \
+  X(2, 8, 8, 8, 8) X(5, 8, 16, 8, 8) X(6, 16, 8, 8, 8) X(9, 16, 16, 8, 8) X(10, 8, 32, 8, 8)         \
+  X(11, 32, 8, 8, 8) X(12, 16, 32, 8, 8) X(13, 32, 16, 8, 8) X(16, 32, 32, 8, 8) X(17, 16, 64, 8, 8) \
+  X(18, 64, 16, 8, 8) X(19, 32, 64, 8, 8) X(20, 64, 32, 8, 8) X(23, 64, 64, 8, 8)
+#define FME_LANE_CLASSES(X) FME_LANE48_CLASSES(X) FME_LANE84_CLASSES(X) FME_LANE88_CLASSES(X)
+
+#define FME_CASE(ID, PW_, PH_, UW_, UH_)                                                             \
+  case ID:                                                                                           \
+    lane_unit<PW_, PH_, UW_, UH_>(a, w.sjobs, w.perm, sc.class_off[ID], sc.class_cnt[ID], blk);      \
+    break;
+#define FME_LANE_KERNEL(NAME, KID, LIST, WAVES)                                                      \
+  __global__ __launch_bounds__(kLaneNT) __attribute__((amdgpu_waves_per_eu(WAVES)))                 \
+  void NAME(BatchArgs a, WorkBufs w, Schedule sc) {                                                  \
+    const int b = blockIdx.x;                                                                        \
+    int c = 0;                                                                                       \
+    while (c < kNumClasses - 1 && b >= sc.prefix[KID][c + 1]) c++;                                   \
+    const int nblk = sc.prefix[KID][c + 1] - sc.prefix[KID][c];                                      \
+    const int blk = xcd_block(b - sc.prefix[KID][c], nblk);                                          \
+    switch (c) {                                                                                     \
+      LIST(FME_CASE)                                                                                 \
+      default: break;                                                                                \
+    }                                                                                                \
+  }
+FME_LANE_KERNEL(k_search_lane48, kSearchLane48, FME_LANE48_CLASSES, FME_LANE_WAVES_SMALL)
+#ifndef FME_LANE_ONLY48
+FME_LANE_KERNEL(k_search_lane84, kSearchLane84, FME_LANE84_CLASSES, FME_LANE_WAVES_SMALL)
+FME_LANE_KERNEL(k_search_lane88, kSearchLane88, FME_LANE88_CLASSES, FME_LANE_WAVES_88)
+#endif
+#undef FME_CASE
+#undef FME_LANE_KERNEL
+
+// Lanes per PU of a lane-kernel class, 0 for classes the cooperative kernels serve.
+int lane_lanes_per_pu(int cls) {
+#ifdef FME_NO_LANE
+  (void)cls;
+  return 0;
+#else
+  switch (cls) {
+#define FME_L(ID, PW_, PH_, UW_, UH_) case ID: return (PW_ / UW_) * (PH_ / UH_);
+    FME_LANE_CLASSES(FME_L)
+#undef FME_L
+    default: return 0;
+  }
+#endif
+}
+
+int lane_blocks_for(int cls, int cnt) {
+  const int l = lane_lanes_per_pu(cls);
+  return l ? (int)(((long long)cnt * l + kLaneNT - 1) / kLaneNT) : 0;
+}
+
+int lane_kernel_of(int cls) {
+  switch (cls) {
+#define FME_K(ID, PW_, PH_, UW_, UH_) case ID: return UW_ == 4 ? kSearchLane48 : (UH_ == 4 ? kSearchLane84 : kSearchLane88);
+    FME_LANE_CLASSES(FME_K)
+#undef FME_K
+    default: return -1;
+  }
+}
+
+hipError_t launch_search_lane(const BatchArgs& a, const WorkBufs& w, const Schedule& sc, hipStream_t s) {
+  int blocks = sc.prefix[kSearchLane48][kNumClasses];
+  if (blocks > 0) hipLaunchKernelGGL(k_search_lane48, dim3(blocks), dim3(kLaneNT), 0, s, a, w, sc);
+#ifndef FME_LANE_ONLY48
+  blocks = sc.prefix[kSearchLane88][kNumClasses];
+  if (blocks > 0) hipLaunchKernelGGL(k_search_lane88, dim3(blocks), dim3(kLaneNT), 0, s, a, w, sc);
+  blocks = sc.prefix[kSearchLane84][kNumClasses];
+  if (blocks > 0) hipLaunchKernelGGL(k_search_lane84, dim3(blocks), dim3(kLaneNT), 0, s, a, w, sc);
+#endif
+  return hipGetLastError();
+}
+
+}  // namespace fme

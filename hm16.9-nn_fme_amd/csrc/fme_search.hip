@@ -21,6 +21,7 @@
 #include <hip/hip_runtime.h>
 
 #include "fme_device.h"
+#include "fme_simd.h"
 
 // Timing-only ablation knob (never set in the product build): bit 0 EMI, 1 planes,
 // 2 half planes, 3 half SATD, 4 quarter SATD, 5 staging.
@@ -49,177 +50,10 @@
 
 namespace fme {
 
-typedef short v2s __attribute__((ext_vector_type(2)));
-typedef unsigned short v2u __attribute__((ext_vector_type(2)));
-
 __device__ unsigned long long g_fme_stamps[16];
 
 namespace {
-
-// ---- scalar helpers ------------------------------------------------------------------
-__device__ __forceinline__ int clamp_i(int v, int lo, int hi) { return min(max(v, lo), hi); }
-
-__device__ __forceinline__ uint32_t eg_bits(int v) {  // TComRdCost.cpp:172-185
-  const uint32_t t = v <= 0 ? ((uint32_t)(-v) << 1) + 1u : ((uint32_t)v << 1);
-  return 1u + 2u * (31u - (uint32_t)__clz((int)t));
-}
-__device__ __forceinline__ uint32_t mv_bits(int x, int y, int scale, int px, int py) {
-  return eg_bits((x << scale) - px) + eg_bits((y << scale) - py);
-}
-__device__ __forceinline__ uint32_t mv_cost(double ml, uint32_t bits) {  // TComRdCost.h:165
-  return (uint32_t)((ml * (double)bits) / 65536.0);
-}
-
-// Candidate tables of xPatternRefinement (TEncSearch.cpp:212-236), 2-bit codes.
-__device__ __forceinline__ int dec(uint32_t c) { return c == 1 ? -1 : (c == 2 ? 1 : 0); }
-__device__ __forceinline__ int cand_dx(int i) { return dec((0x666u >> (2 * (8 - i))) & 3u); }
-__device__ __forceinline__ int half_dy(int i) { return dec((0x605au >> (2 * (8 - i))) & 3u); }
-__device__ __forceinline__ int qtr_dy(int i) { return dec((0x650au >> (2 * (8 - i))) & 3u); }
-
-// ---- packed arithmetic -----------------------------------------------------------------
-__device__ __forceinline__ uint32_t pk(v2s v) { return __builtin_bit_cast(uint32_t, v); }
-__device__ __forceinline__ v2s up(uint32_t u) { return __builtin_bit_cast(v2s, u); }
-__device__ __forceinline__ uint32_t pk_add(uint32_t a, uint32_t b) { return pk(up(a) + up(b)); }
-__device__ __forceinline__ uint32_t pk_sub(uint32_t a, uint32_t b) { return pk(up(a) - up(b)); }
-__device__ __forceinline__ uint32_t pk_abs(uint32_t a) {
-  const v2s x = up(a);
-  return pk(__builtin_elementwise_max(x, -x));
-}
-__device__ __forceinline__ int dot2(uint32_t a, uint32_t b, int acc) {
-  return __builtin_amdgcn_sdot2(up(a), up(b), acc, false);
-}
-__device__ __forceinline__ uint32_t udot2(uint32_t a, uint32_t b, uint32_t acc) {
-  return __builtin_amdgcn_udot2(__builtin_bit_cast(v2u, a), __builtin_bit_cast(v2u, b), acc, false);
-}
-__device__ __forceinline__ int dot4(uint32_t a, uint32_t b, int acc) {
-  return __builtin_amdgcn_sdot4((int)a, (int)b, acc, false);
-}
-// bytes b0..b3 of `w` -> (b0, b1) and (b2, b3) as packed u16 pairs
-__device__ __forceinline__ uint32_t lo_pair(uint32_t w) { return __builtin_amdgcn_perm(0u, w, 0x0c010c00u); }
-__device__ __forceinline__ uint32_t hi_pair(uint32_t w) { return __builtin_amdgcn_perm(0u, w, 0x0c030c02u); }
-// 4 bytes starting `sh` bytes into (lo, hi)
-__device__ __forceinline__ uint32_t funnel8(uint32_t hi, uint32_t lo, uint32_t sh) {
-  return __builtin_amdgcn_alignbyte(hi, lo, sh);
-}
-__device__ __forceinline__ uint32_t funnel16(uint32_t hi, uint32_t lo) {
-  return __builtin_amdgcn_alignbit(hi, lo, 16u);
-}
-__device__ __forceinline__ uint32_t lds32(const uint8_t* p) { return *reinterpret_cast<const uint32_t*>(p); }
-// Global loads through pointers the compiler cannot classify (e.g. read from an LDS table):
-// address space 1 makes them global_load (vmcnt only, in order) instead of flat_load, which
-// forces s_waitcnt vmcnt(0) lgkmcnt(0) at every control-flow join.
-typedef __attribute__((address_space(1))) const uint32_t gu32c;
-typedef __attribute__((address_space(1))) const uint8_t gu8c;
-__device__ __forceinline__ uint32_t gld32(const void* p) { return *(gu32c*)(p); }
-__device__ __forceinline__ uint32_t gld8(const void* p) { return *(gu8c*)(p); }
-__device__ __forceinline__ void sts32(uint8_t* p, uint32_t v) { *reinterpret_cast<uint32_t*>(p) = v; }
-
-// 4x4 byte transpose: r[i] holds row i (byte j = column j); c[j] = column j (byte i = row i).
-__device__ __forceinline__ void transpose4x4(const uint32_t (&r)[4], uint32_t (&c)[4]) {
-  const uint32_t a = __builtin_amdgcn_perm(r[1], r[0], 0x05010400u);
-  const uint32_t b = __builtin_amdgcn_perm(r[1], r[0], 0x07030602u);
-  const uint32_t d = __builtin_amdgcn_perm(r[3], r[2], 0x05010400u);
-  const uint32_t e = __builtin_amdgcn_perm(r[3], r[2], 0x07030602u);
-  c[0] = __builtin_amdgcn_perm(d, a, 0x05040100u);
-  c[1] = __builtin_amdgcn_perm(d, a, 0x07060302u);
-  c[2] = __builtin_amdgcn_perm(e, b, 0x05040100u);
-  c[3] = __builtin_amdgcn_perm(e, b, 0x07060302u);
-}
-
-// Four picture bytes at (x, y) .. (x+3, y) with edge replication (TComPicYuv::extendPicBorder
-// semantics), branch-free: the 4-byte run xa = clamp(x, 0, W-4) is read with at most two
-// aligned dword loads, then v_perm picks byte clamp(x+i, 0, W-1) - xa for lane byte i.
-// Needs width >= 4 (HEVC luma width is a multiple of 8).
-__device__ __forceinline__ uint32_t pic4(const uint8_t* luma, int stride, int width, int height, int x, int y) {
-  const int yc = clamp_i(y, 0, height - 1);
-  const int xa = clamp_i(x, 0, width - 4);
-  const uintptr_t addr = reinterpret_cast<uintptr_t>(luma + (size_t)yc * stride + xa);
-  const uint32_t sh = (uint32_t)(addr & 3);
-  const uint32_t* q = reinterpret_cast<const uint32_t*>(addr & ~(uintptr_t)3);
-  const uint32_t lo = gld32(q);
-  const uint32_t hi = gld32(sh ? q + 1 : q);      // second dword only when the run straddles
-  const uint32_t run = funnel8(hi, lo, sh);       // pixels xa .. xa+3
-  uint32_t sel = 0;
-#pragma unroll
-  for (int i = 0; i < 4; i++) sel |= (uint32_t)(clamp_i(x + i, 0, width - 1) - xa) << (8 * i);
-  return __builtin_amdgcn_perm(0u, run, sel);
-}
-
-// Luma taps as packed int8 quads (t0..t3, t4..t7) and int16 pairs (TComInterpolationFilter.cpp:57-63).
-__device__ __forceinline__ uint32_t q8(int a, int b, int c, int d) {
-  return (uint32_t)(a & 255) | ((uint32_t)(b & 255) << 8) | ((uint32_t)(c & 255) << 16) | ((uint32_t)(d & 255) << 24);
-}
-__device__ __forceinline__ uint32_t p16(int a, int b) { return (uint32_t)(a & 0xffff) | ((uint32_t)(b & 0xffff) << 16); }
-__device__ __forceinline__ void taps8(int f, uint32_t& lo, uint32_t& hi) {
-  if (f == 1) { lo = q8(-1, 4, -10, 58); hi = q8(17, -5, 1, 0); }
-  else if (f == 2) { lo = q8(-1, 4, -11, 40); hi = q8(40, -11, 4, -1); }
-  else { lo = q8(0, 1, -5, 17); hi = q8(58, -10, 4, -1); }
-}
-__device__ __forceinline__ void taps16(int f, uint32_t (&c)[4]) {
-  if (f == 1) { c[0] = p16(-1, 4); c[1] = p16(-10, 58); c[2] = p16(17, -5); c[3] = p16(1, 0); }
-  else if (f == 2) { c[0] = p16(-1, 4); c[1] = p16(-11, 40); c[2] = p16(40, -11); c[3] = p16(4, -1); }
-  else { c[0] = p16(0, 1); c[1] = p16(-5, 17); c[2] = p16(58, -10); c[3] = p16(4, -1); }
-}
-
-// Second-stage rounding of filter<8,true,false,true> (shift 12, offset 2048 + (8192 << 6)).
-__device__ __forceinline__ int round2d(int s) { return clamp_i((s + 526336) >> 12, 0, 255); }
-// 1-D from bytes: (sum(c*s) + 32) >> 6 with sum(c*s) = sum(c*s') + 8192.
-__device__ __forceinline__ int round1d_s8(int s) { return clamp_i((s + 8224) >> 6, 0, 255); }
-
-// ---- SATD on packed tiles ------------------------------------------------------------------
-// X[c][j]: column c, rows (2j, 2j+1) packed.  Returns the xCalcHADs value of the tile.
-template <int T>
-__device__ __forceinline__ uint32_t satd_packed(uint32_t (&X)[T][T / 2]) {
-  // horizontal (across columns) butterflies
-#pragma unroll
-  for (int d = T / 2; d >= 1; d >>= 1)
-#pragma unroll
-    for (int c = 0; c < T; c++)
-      if ((c & d) == 0)
-#pragma unroll
-        for (int j = 0; j < T / 2; j++) {
-          const uint32_t a = X[c][j], b = X[c + d][j];
-          X[c][j] = pk_add(a, b);
-          X[c + d][j] = pk_sub(a, b);
-        }
-  // vertical butterflies between row pairs (distances 4 and 2 rows)
-#pragma unroll
-  for (int d = T / 4; d >= 1; d >>= 1)
-#pragma unroll
-    for (int c = 0; c < T; c++)
-#pragma unroll
-      for (int j = 0; j < T / 2; j++)
-        if ((j & d) == 0) {
-          const uint32_t a = X[c][j], b = X[c][j + d];
-          X[c][j] = pk_add(a, b);
-          X[c][j + d] = pk_sub(a, b);
-        }
-  // last butterfly (rows 2j, 2j+1 in one register): |a+b| + |a-b| = 2 max(|a|, |b|)
-  uint32_t s = 0;
-#pragma unroll
-  for (int c = 0; c < T; c += 2)
-#pragma unroll
-    for (int j = 0; j < T / 2; j++) {
-      const uint32_t a = pk_abs(X[c][j]), b = pk_abs(X[c + 1][j]);
-      const uint32_t los = __builtin_amdgcn_perm(b, a, 0x05040100u);   // (a.lo, b.lo)
-      const uint32_t his = __builtin_amdgcn_perm(b, a, 0x07060302u);   // (a.hi, b.hi)
-      const v2s m = __builtin_elementwise_max(up(los), up(his));
-      s = udot2(pk(m), 0x00010001u, s);
-    }
-  // 8x8: (2s + 2) >> 2 ; 4x4: (2s + 1) >> 1
-  return T == 8 ? (s + 1) >> 1 : s;
-}
-
-template <int T>
-__device__ __forceinline__ uint32_t sad_packed(const uint32_t (&X)[T][T / 2]) {
-  uint32_t s = 0;
-#pragma unroll
-  for (int c = 0; c < T; c++)
-#pragma unroll
-    for (int j = 0; j < T / 2; j++) s = udot2(pk_abs(X[c][j]), 0x00010001u, s);
-  return s;
-}
-
+using namespace simd;
 // ---- per-class layout ----------------------------------------------------------------------
 constexpr int align_up(int v, int a) { return (v + a - 1) / a * a; }
 
@@ -951,20 +785,28 @@ __device__ __forceinline__ void search_class(const BatchArgs& a, const fme_job* 
 
 // =============================================================================================
 // kernels: small shapes (256 lanes) and large shapes (512 lanes).  Blocks of one launch are
-// dealt to classes by sc.tile_prefix (block ranges); a block strides over its class's tiles.
+// dealt to classes by sc.prefix (block ranges); a block strides over its class's tiles.
 // =============================================================================================
+// With the lane-per-unit kernel (fme_lane.hip) these kernels serve only the AMP shapes whose
+// lane groups are not a power of two (12x16, 16x12, 24x32, 32x24, 48x64, 64x48 — the
+// SAD12/24/48 EMI metric); -DFME_NO_LANE routes every class here (A/B builds).
+#ifdef FME_NO_LANE
 #define FME_SMALL_CLASSES(X)                                                                       \
   X(0, 4, 8) X(1, 8, 4) X(2, 8, 8) X(3, 4, 16) X(4, 16, 4) X(5, 8, 16) X(6, 16, 8) X(7, 12, 16)      \
   X(8, 16, 12) X(9, 16, 16) X(10, 8, 32) X(11, 32, 8) X(12, 16, 32) X(13, 32, 16) X(14, 24, 32)     \
   X(15, 32, 24) X(16, 32, 32) X(17, 16, 64) X(18, 64, 16)
 #define FME_LARGE_CLASSES(X) X(19, 32, 64) X(20, 64, 32) X(21, 48, 64) X(22, 64, 48) X(23, 64, 64)
+#else
+#define FME_SMALL_CLASSES(X) X(7, 12, 16) X(8, 16, 12) X(14, 24, 32) X(15, 32, 24)
+#define FME_LARGE_CLASSES(X) X(21, 48, 64) X(22, 64, 48)
+#endif
 
 constexpr int kSmallNT = 256, kSmallBudget = FME_SMALL_BUDGET_KB * 1024;
 constexpr int kLargeNT = 512, kLargeBudget = FME_LARGE_BUDGET_KB * 1024;
 
-__device__ __forceinline__ int find_class(const Schedule& sc, int b, int lo, int hi) {
-  int c = lo;
-  while (c < hi - 1 && b >= sc.tile_prefix[c + 1]) c++;
+__device__ __forceinline__ int find_class(const int32_t (&prefix)[kNumClasses + 1], int b) {
+  int c = 0;
+  while (c < kNumClasses - 1 && b >= prefix[c + 1]) c++;
   return c;
 }
 
@@ -984,10 +826,10 @@ __device__ __forceinline__ int xcd_tile(int r, int n) {
 
 __global__ __launch_bounds__(kSmallNT) void k_search_small(BatchArgs a, WorkBufs w, Schedule sc) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
-  const int b = blockIdx.x + sc.tile_prefix[0];
-  const int c = find_class(sc, b, 0, 19);
-  const int nblk = sc.tile_prefix[c + 1] - sc.tile_prefix[c];
-  const int blk = xcd_tile(b - sc.tile_prefix[c], nblk);
+  const int b = blockIdx.x;
+  const int c = find_class(sc.prefix[kSearchCoop], b);
+  const int nblk = sc.prefix[kSearchCoop][c + 1] - sc.prefix[kSearchCoop][c];
+  const int blk = xcd_tile(b - sc.prefix[kSearchCoop][c], nblk);
   switch (c) {
 #define FME_CASE(ID, W_, H_)                                                                        \
   case ID:                                                                                          \
@@ -1002,10 +844,10 @@ __global__ __launch_bounds__(kSmallNT) void k_search_small(BatchArgs a, WorkBufs
 
 __global__ __launch_bounds__(kLargeNT) void k_search_large(BatchArgs a, WorkBufs w, Schedule sc) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
-  const int b = blockIdx.x + sc.tile_prefix[19];
-  const int c = find_class(sc, b, 19, kNumClasses);
-  const int nblk = sc.tile_prefix[c + 1] - sc.tile_prefix[c];
-  const int blk = xcd_tile(b - sc.tile_prefix[c], nblk);
+  const int b = blockIdx.x;
+  const int c = find_class(sc.prefix[kSearchCoopLarge], b);
+  const int nblk = sc.prefix[kSearchCoopLarge][c + 1] - sc.prefix[kSearchCoopLarge][c];
+  const int blk = xcd_tile(b - sc.prefix[kSearchCoopLarge][c], nblk);
   switch (c) {
 #define FME_CASE(ID, W_, H_)                                                                        \
   case ID:                                                                                          \
@@ -1052,18 +894,28 @@ hipError_t debug_phase_cycles(unsigned long long* out16, bool reset) {
   return hipMemcpyToSymbol(HIP_SYMBOL(g_fme_stamps), z, sizeof(z));
 }
 
-int search_large_blocks(const Schedule& sc) { return sc.tile_prefix[kNumClasses] - sc.tile_prefix[19]; }
-int search_small_blocks(const Schedule& sc) { return sc.tile_prefix[19] - sc.tile_prefix[0]; }
+int search_kernel_of(int cls) {
+  if (lane_lanes_per_pu(cls) > 0) return lane_kernel_of(cls);
+  return cls >= 19 ? kSearchCoopLarge : kSearchCoop;
+}
 
-static size_t lds_max(const Schedule& sc, int lo, int hi) {
+int search_blocks_for(int cls, int cnt) {
+  if (cnt <= 0) return 0;
+  if (lane_lanes_per_pu(cls) > 0) return lane_blocks_for(cls, cnt);
+  const int p = pus_per_tile(cls), tpb = tiles_per_block();
+  const int tiles = (cnt + p - 1) / p;
+  return (tiles + tpb - 1) / tpb;
+}
+
+static size_t lds_max(const Schedule& sc, int kernel) {
   size_t m = 0;
-  for (int c = lo; c < hi; c++)
-    if (sc.class_cnt[c] && lds_bytes_for_class(c) > m) m = lds_bytes_for_class(c);
+  for (int c = 0; c < kNumClasses; c++)
+    if (sc.class_cnt[c] && search_kernel_of(c) == kernel && lds_bytes_for_class(c) > m) m = lds_bytes_for_class(c);
   return m;
 }
 
 hipError_t launch_search_large(const BatchArgs& a, const WorkBufs& w, const Schedule& sc, hipStream_t s) {
-  const int blocks = search_large_blocks(sc);
+  const int blocks = sc.prefix[kSearchCoopLarge][kNumClasses];
   if (blocks <= 0) return hipSuccess;
   static bool attr_set = false;
   if (!attr_set) {
@@ -1072,14 +924,14 @@ hipError_t launch_search_large(const BatchArgs& a, const WorkBufs& w, const Sche
     if (e != hipSuccess) return e;
     attr_set = true;
   }
-  hipLaunchKernelGGL(k_search_large, dim3(blocks), dim3(kLargeNT), lds_max(sc, 19, kNumClasses), s, a, w, sc);
+  hipLaunchKernelGGL(k_search_large, dim3(blocks), dim3(kLargeNT), lds_max(sc, kSearchCoopLarge), s, a, w, sc);
   return hipGetLastError();
 }
 
 hipError_t launch_search_small(const BatchArgs& a, const WorkBufs& w, const Schedule& sc, hipStream_t s) {
-  const int blocks = search_small_blocks(sc);
+  const int blocks = sc.prefix[kSearchCoop][kNumClasses];
   if (blocks <= 0) return hipSuccess;
-  hipLaunchKernelGGL(k_search_small, dim3(blocks), dim3(kSmallNT), lds_max(sc, 0, 19), s, a, w, sc);
+  hipLaunchKernelGGL(k_search_small, dim3(blocks), dim3(kSmallNT), lds_max(sc, kSearchCoop), s, a, w, sc);
   return hipGetLastError();
 }
 

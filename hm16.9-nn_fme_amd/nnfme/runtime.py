@@ -16,7 +16,7 @@ PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB_PATH = os.environ.get("FME_LIB_PATH") or os.path.join(PKG_ROOT, "libfme_amd.so")
 
 ABI_VERSION = 2
-TIMING_NAMES = ("classify", "scatter", "search", "nn_tail", "batch", "search_small", "search_large")
+TIMING_NAMES = ("classify", "scatter", "search", "nn_tail", "batch", "search_main", "search_aux")
 
 # Every entry point include/fme.h declares (the ABI test checks the .so exports them).
 ABI_SYMBOLS = (
@@ -24,7 +24,7 @@ ABI_SYMBOLS = (
     "fme_bind_picture_device", "fme_set_lambda", "fme_set_motion_lambda", "fme_set_keys",
     "fme_load_nn_weights", "fme_nn_reset_state", "fme_nn_get_state", "fme_nn_set_state", "fme_refine", "fme_refine_device",
     "fme_frac_dif_single", "fme_nn_pred_single", "fme_set_profiling", "fme_last_timings",
-    "fme_accumulated_timings", "fme_debug_phase_cycles",
+    "fme_accumulated_timings", "fme_search_kernel_of_shape", "fme_debug_phase_cycles",
 )
 
 
@@ -73,6 +73,7 @@ def load_library(path=None):
         "fme_set_profiling": (I, [P, I]),
         "fme_last_timings": (I, [P, P, I]),
         "fme_accumulated_timings": (I, [P, P, I, I]),
+        "fme_search_kernel_of_shape": (I, [I, I]),
         "fme_debug_phase_cycles": (I, [P, I]),
     }
     for name, (res, args) in sig.items():
@@ -184,6 +185,10 @@ class FmeContext:
             int(mv_int[0]), int(mv_int[1]), int(mvp[0]), int(mvp[1]), float(motion_lambda),
             _ptr(half), _ptr(qtr), _ptr(cost)))
         return (int(half[0]), int(half[1])), (int(qtr[0]), int(qtr[1])), int(cost[0])
+
+    def search_kernel_of_shape(self, w, h):
+        """0: the main search kernel serves w x h PUs, 1: an auxiliary one, -1: unsupported."""
+        return int(self.lib.fme_search_kernel_of_shape(int(w), int(h)))
 
     def set_profiling(self, enable=True):
         _check(self.lib, self.lib.fme_set_profiling(self.h, int(enable)))

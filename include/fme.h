@@ -193,13 +193,17 @@ int fme_nn_pred_single(fme_ctx* ctx, const uint32_t* e, uint32_t c, int pu_h, in
  * the batch on the streams the kernels run on.  Device milliseconds, FME_NUM_TIMINGS values:
  * [0] classify, [1] scatter, [2] search phase (EMI + FracDIF, both shape kernels),
  * [3] NN + tail, [4] whole batch (first kernel start to last kernel end, host sync included),
- * [5] small-shape search kernel, [6] large-shape search kernel (0 if not launched).
+ * [5] main search kernel (batch stream), [6] auxiliary search kernels (their own stream; 0 if
+ * not launched).
  * fme_last_timings waits for the last profiled batch.  fme_accumulated_timings returns the
  * sums over every profiled batch since the last reset (the return value is the batch count);
  * a batch's events are read at the next batch's own host synchronisation, so profiling a
  * run of batches adds no synchronisation.                                                  */
 #define FME_NUM_TIMINGS 7
 int fme_set_profiling(fme_ctx* ctx, int enable);
+/* Which search kernel serves PU shape width x height: 0 the main one (timings[5]), 1 an
+ * auxiliary one (timings[6]), -1 unsupported shape. */
+int fme_search_kernel_of_shape(int width, int height);
 int fme_last_timings(fme_ctx* ctx, float* ms, int count);
 int fme_accumulated_timings(fme_ctx* ctx, double* ms, int count, int reset);
 /* Diagnostic builds (FME_STAMPS=1) only: per-phase shader cycles of the search kernels summed

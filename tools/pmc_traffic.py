@@ -38,10 +38,10 @@ def main():
         f = fetch.get(k, 0.0) * 1024 * 2
         w = write.get(k, 0.0) * 1024
         kernels[k] = {"fetch_bytes": f, "write_bytes": w, "bytes_per_launch": f + w}
-    main_k = "fme::k_search_small"
+    main_ks = [k for k in kernels if k.startswith("fme::k_search_lane")] or ["fme::k_search_small"]
     d = {
-        "kernel": main_k,
-        "bytes_per_launch": kernels.get(main_k, {}).get("bytes_per_launch"),
+        "kernel": "+".join(main_ks),
+        "bytes_per_launch": sum(kernels.get(k, {}).get("bytes_per_launch") or 0 for k in main_ks) or None,
         "source": "rocprofv3 --pmc FETCH_SIZE (x2, gfx950) + WRITE_SIZE, separate passes, "
                   "bench.py --steps 2 --warmup 1 (profiles/pmc_traffic.json)",
         "kernels": kernels,
