@@ -25,7 +25,6 @@
 // >> 12 for 2-D), and key - pred is unchanged.
 #include <hip/hip_runtime.h>
 
-#include <type_traits>
 
 #include "fme_device.h"
 #include "fme_simd.h"
@@ -152,17 +151,217 @@ __device__ __forceinline__ uint32_t unit_dist(uint32_t (&X)[UW][UH / 2], bool ha
 }
 
 // Candidate offsets (xPatternRefinement tables, TEncSearch.cpp:212-236).
-__device__ __forceinline__ constexpr int h9_dx(int i) { return (i == 3 || i == 5 || i == 7) ? -1 : ((i == 4 || i == 6 || i == 8) ? 1 : 0); }
-__device__ __forceinline__ constexpr int h9_dy(int i) { return (i == 1 || i == 5 || i == 6) ? -1 : ((i == 2 || i == 7 || i == 8) ? 1 : 0); }
-__device__ __forceinline__ constexpr int q9_dx(int i) { return (i == 3 || i == 5 || i == 7) ? -1 : ((i == 4 || i == 6 || i == 8) ? 1 : 0); }
-__device__ __forceinline__ constexpr int q9_dy(int i) { return (i == 1 || i == 3 || i == 4) ? -1 : ((i == 2 || i == 7 || i == 8) ? 1 : 0); }
+__host__ __device__ constexpr int h9_dx(int i) { return (i == 3 || i == 5 || i == 7) ? -1 : ((i == 4 || i == 6 || i == 8) ? 1 : 0); }
+__host__ __device__ constexpr int h9_dy(int i) { return (i == 1 || i == 5 || i == 6) ? -1 : ((i == 2 || i == 7 || i == 8) ? 1 : 0); }
+__host__ __device__ constexpr int q9_dx(int i) { return (i == 3 || i == 5 || i == 7) ? -1 : ((i == 4 || i == 6 || i == 8) ? 1 : 0); }
+__host__ __device__ constexpr int q9_dy(int i) { return (i == 1 || i == 3 || i == 4) ? -1 : ((i == 2 || i == 7 || i == 8) ? 1 : 0); }
 // Q9 index of (dqx, dqy)
-__device__ __forceinline__ constexpr int q9_index(int dx, int dy) {
+__host__ __device__ constexpr int q9_index(int dx, int dy) {
   return dy == 0 ? (dx == 0 ? 0 : (dx < 0 ? 5 : 6)) : dy < 0 ? (dx == 0 ? 1 : (dx < 0 ? 3 : 4)) : (dx == 0 ? 2 : (dx < 0 ? 7 : 8));
 }
 // EMI positions: 0 centre, then TL, T, TR, L, R, BL, B, BR (xTZ8PointSquareSearch order)
-__device__ __forceinline__ constexpr int emi_dx(int p) { return (p == 1 || p == 4 || p == 6) ? -1 : ((p == 3 || p == 5 || p == 8) ? 1 : 0); }
-__device__ __forceinline__ constexpr int emi_dy(int p) { return p >= 1 && p <= 3 ? -1 : (p >= 6 ? 1 : 0); }
+__host__ __device__ constexpr int emi_dx(int p) { return (p == 1 || p == 4 || p == 6) ? -1 : ((p == 3 || p == 5 || p == 8) ? 1 : 0); }
+__host__ __device__ constexpr int emi_dy(int p) { return p >= 1 && p <= 3 ? -1 : (p >= 6 ? 1 : 0); }
+
+// =============================================================================================
+// Candidate passes of one unit.  v: re-centred window (rows -4..UH+3, cols -4..UW+3, s - 128
+// bytes), K: key - 128 as packed column pairs.  Each pass keeps at most two key - pred arrays.
+// =============================================================================================
+template <int L>
+__device__ __forceinline__ void take_half(int i, uint32_t part, double ml, int mvx, int mvy, int px, int py,
+                                          uint32_t& best, int& bi) {
+  const uint32_t d = group_sum<L>(part) + mv_cost(ml, mv_bits(2 * mvx + h9_dx(i), 2 * mvy + h9_dy(i), 1, px, py));
+  if (d < best || (d == best && i < bi)) {
+    best = d;
+    bi = i;
+  }
+}
+template <int L>
+__device__ __forceinline__ void take_qtr(int i, uint32_t part, double ml, int mvx, int mvy, int hx, int hy,
+                                         int px, int py, uint32_t& best, int& bi) {
+  const int qx = 2 * hx + q9_dx(i), qy = 2 * hy + q9_dy(i);
+  const uint32_t d = group_sum<L>(part) + mv_cost(ml, mv_bits(4 * mvx + qx, 4 * mvy + qy, 0, px, py));
+  if (d < best || (d == best && i < bi)) {
+    best = d;
+    bi = i;
+  }
+}
+
+// (0,0), (0,-1), (0,1)
+template <int UW, int UH, int T>
+__device__ __forceinline__ void half_center(uint32_t (&v)[UH + 8][UW / 4 + 2], const uint32_t (&K)[UW][UH / 2],
+                                            bool had, uint32_t (&d)[3]) {
+  constexpr int RV = UH + 8, UJ = UH / 2;
+  uint32_t c2lo, c2hi;
+  taps8(2, c2lo, c2hi);
+  {   // (0,0): integer samples, window' rows 4+y, cols 4+x
+    uint32_t X[UW][UJ];
+#pragma unroll
+    for (int x = 0; x < UW; x++)
+#pragma unroll
+      for (int jj = 0; jj < UJ; jj++)
+        X[x][jj] = pk_sub(K[x][jj], sext_pair(v[5 + 2 * jj][(x + 4) >> 2], v[4 + 2 * jj][(x + 4) >> 2], (x + 4) & 3));
+    d[0] = unit_dist<UW, UH, T>(X, had);
+  }
+  launder(v);
+  {   // (0,-1), (0,1): vertical half-pel on integer columns (transposed window')
+    uint32_t X1[UW][UJ], X2[UW][UJ];
+#pragma unroll
+    for (int g = 0; g < UW / 4; g++) {
+      uint32_t CB[4][RV / 4];   // columns 4g..4g+3 (window' cols 4g+4 ..), 4 rows per dword
+#pragma unroll
+      for (int q = 0; q < RV / 4; q++) {
+        const uint32_t rows[4] = {v[4 * q][g + 1], v[4 * q + 1][g + 1], v[4 * q + 2][g + 1], v[4 * q + 3][g + 1]};
+        uint32_t cols[4];
+        transpose4x4(rows, cols);
+#pragma unroll
+        for (int c = 0; c < 4; c++) CB[c][q] = cols[c];
+      }
+#pragma unroll
+      for (int c4 = 0; c4 < 4; c4++) {
+        const int x = 4 * g + c4;
+        int v1[UH + 1];   // half rows i = 0..UH (between rows i-1, i): taps on window' rows i..i+7
+#pragma unroll
+        for (int i = 0; i <= UH; i++) {
+          const int acc = dot4(rbytes(CB[c4], i), c2lo, 32);
+          v1[i] = clamp_s8(dot4(rbytes(CB[c4], i + 4), c2hi, acc) >> 6);
+        }
+#pragma unroll
+        for (int jj = 0; jj < UJ; jj++) {
+          X1[x][jj] = pk_sub(K[x][jj], pack2(v1[2 * jj], v1[2 * jj + 1]));
+          X2[x][jj] = pk_sub(K[x][jj], pack2(v1[2 * jj + 1], v1[2 * jj + 2]));
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+    d[1] = unit_dist<UW, UH, T>(X1, had);
+    d[2] = unit_dist<UW, UH, T>(X2, had);
+  }
+}
+
+// (s,0), (s,-1), (s,1) for s = -1 (SIDE 0: half column x) or +1 (SIDE 1: half column x+1)
+template <int UW, int UH, int T, int SIDE>
+__device__ __forceinline__ void half_side(uint32_t (&v)[UH + 8][UW / 4 + 2], const uint32_t (&K)[UW][UH / 2],
+                                          bool had, uint32_t (&d)[3]) {
+  constexpr int RV = UH + 8, UJ = UH / 2;
+  uint32_t c2lo, c2hi;
+  taps8(2, c2lo, c2hi);
+  launder(v);
+  {   // (s,0): horizontal half-pel, half column jc = x + SIDE (window' bytes jc .. jc+7)
+    uint32_t X[UW][UJ];
+#pragma unroll
+    for (int x = 0; x < UW; x++) {
+      const int jc = x + SIDE;
+      int h1[UH];
+#pragma unroll
+      for (int y = 0; y < UH; y++)
+        h1[y] = clamp_s8(dot4(rbytes(v[y + 4], jc + 4), c2hi, dot4(rbytes(v[y + 4], jc), c2lo, 32)) >> 6);
+#pragma unroll
+      for (int jj = 0; jj < UJ; jj++) X[x][jj] = pk_sub(K[x][jj], pack2(h1[2 * jj], h1[2 * jj + 1]));
+    }
+    d[0] = unit_dist<UW, UH, T>(X, had);
+  }
+  launder(v);
+  {   // (s,-1), (s,1): 2-D half-pel (first stage rows -4..UH+3 of half column jc, then vertical)
+    const uint32_t c16[4] = {p16(-1, 4), p16(-11, 40), p16(40, -11), p16(4, -1)};
+    const uint32_t c16o[5] = {p16(0, -1), p16(4, -11), p16(40, 40), p16(-11, 4), p16(-1, 0)};
+    uint32_t XB[UW][UJ], XC[UW][UJ];
+#pragma unroll
+    for (int x = 0; x < UW; x++) {
+      const int jc = x + SIDE;
+      launder(v);
+      uint32_t HP[RV / 2];
+#pragma unroll
+      for (int r = 0; r < RV; r += 2) {
+        const int h0 = dot4(rbytes(v[r], jc + 4), c2hi, dot4(rbytes(v[r], jc), c2lo, 0));
+        const int h1 = dot4(rbytes(v[r + 1], jc + 4), c2hi, dot4(rbytes(v[r + 1], jc), c2lo, 0));
+        HP[r / 2] = pack2(h0, h1);
+      }
+      int v2[UH + 1];
+#pragma unroll
+      for (int i = 0; i <= UH; i++) {
+        int acc = 2048;
+        if ((i & 1) == 0) {
+#pragma unroll
+          for (int t = 0; t < 4; t++) acc = dot2(HP[i / 2 + t], c16[t], acc);
+        } else {
+#pragma unroll
+          for (int t = 0; t < 5; t++) acc = dot2(HP[(i - 1) / 2 + t], c16o[t], acc);
+        }
+        v2[i] = clamp_s8(acc >> 12);
+      }
+#pragma unroll
+      for (int jj = 0; jj < UJ; jj++) {
+        XB[x][jj] = pk_sub(K[x][jj], pack2(v2[2 * jj], v2[2 * jj + 1]));
+        XC[x][jj] = pk_sub(K[x][jj], pack2(v2[2 * jj + 1], v2[2 * jj + 2]));
+      }
+      __builtin_amdgcn_sched_barrier(0);   // one column at a time (register pressure)
+    }
+    d[1] = unit_dist<UW, UH, T>(XB, had);
+    d[2] = unit_dist<UW, UH, T>(XC, had);
+  }
+}
+
+// Quarter passes: pass PS covers column phase k = QP_K[PS] (dqx = k-1) and one or two row
+// phases l (dqy = l-1); candidate (k1, l1) is the half best.  A phase with fraction 0 filters
+// with {0,0,0,64,0,0,0,0}, which equals HM's copy / 1-D paths after rounding.
+__host__ __device__ constexpr int qp_k(int ps) { return ps < 2 ? 0 : (ps == 2 ? 1 : 2); }
+__host__ __device__ constexpr int qp_l0(int ps) { return (ps == 1 || ps == 4) ? 2 : 0; }
+__host__ __device__ constexpr int qp_l1(int ps) { return ps == 0 ? 1 : (ps == 2 ? 2 : (ps == 3 ? 1 : -1)); }
+// Q9 index of pass ps's first / second candidate
+__host__ __device__ constexpr int qp_idx0(int ps) { return q9_index(qp_k(ps) - 1, qp_l0(ps) - 1); }
+__host__ __device__ constexpr int qp_idx1(int ps) { return q9_index(qp_k(ps) - 1, qp_l1(ps) - 1); }
+
+template <int UW, int UH, int T, int PS>
+__device__ __forceinline__ void qtr_pass(uint32_t (&v)[UH + 8][UW / 4 + 2], const uint32_t (&K)[UW][UH / 2],
+                                         bool had, int hx, int hy, uint32_t (&d)[2]) {
+  constexpr int RV = UH + 8, UJ = UH / 2;
+  constexpr int k = qp_k(PS);
+  constexpr int NP = qp_l1(PS) < 0 ? 1 : 2;
+  const int LS[2] = {qp_l0(PS), qp_l1(PS) < 0 ? 0 : qp_l1(PS)};
+  const int qx = 2 * hx + (k - 1);
+  const int ix = qx >> 2, fx = qx & 3;
+  const uint32_t dlt = (uint32_t)(1 + ix);
+  uint32_t clo, chi;
+  taps8_any(fx, clo, chi);
+  uint32_t cpe[NP][5], cpo[NP][5];
+#pragma unroll
+  for (int m = 0; m < NP; m++) {
+    const int qy = 2 * hy + (LS[m] - 1);
+    const int iy = qy >> 2, fy = qy & 3;
+    vpairs(fy, 1 + iy, cpe[m]);
+    vpairs(fy, 2 + iy, cpo[m]);
+  }
+  uint32_t XQ[NP][UW][UJ];
+#pragma unroll
+  for (int x = 0; x < UW; x++) {
+    launder(v);
+    uint32_t HQ[RV / 2];
+#pragma unroll
+    for (int r = 0; r < RV; r += 2) {
+      const int h0 = dot4(rbytes_d(v[r], x + 4, dlt), chi, dot4(rbytes_d(v[r], x, dlt), clo, 0));
+      const int h1 = dot4(rbytes_d(v[r + 1], x + 4, dlt), chi, dot4(rbytes_d(v[r + 1], x, dlt), clo, 0));
+      HQ[r / 2] = pack2(h0, h1);
+    }
+#pragma unroll
+    for (int m = 0; m < NP; m++) {
+      int vq[UH];
+#pragma unroll
+      for (int y = 0; y < UH; y++) {
+        const int m0 = (y & 1) ? (y - 1) / 2 : y / 2;
+        int acc = 2048;
+#pragma unroll
+        for (int t = 0; t < 5; t++) acc = dot2(HQ[m0 + t], (y & 1) ? cpo[m][t] : cpe[m][t], acc);
+        vq[y] = clamp_s8(acc >> 12);
+      }
+#pragma unroll
+      for (int jj = 0; jj < UJ; jj++) XQ[m][x][jj] = pk_sub(K[x][jj], pack2(vq[2 * jj], vq[2 * jj + 1]));
+    }
+    __builtin_amdgcn_sched_barrier(0);   // one column at a time (register pressure)
+  }
+  d[0] = unit_dist<UW, UH, T>(XQ[0], had);
+  d[1] = NP > 1 ? unit_dist<UW, UH, T>(XQ[NP - 1], had) : 0u;
+}
 
 typedef uint32_t u32x4a __attribute__((ext_vector_type(4), aligned(4)));
 typedef uint32_t u32x2a __attribute__((ext_vector_type(2), aligned(4)));
@@ -251,36 +450,33 @@ __device__ __forceinline__ void lane_unit(const BatchArgs& a, const fme_job* __r
 #pragma unroll
       for (int k = 0; k < NW; k++) w[r][k] = __builtin_amdgcn_alignbyte(raw[r][k + 1], raw[r][k], s0) ^ 0x80808080u;
   }
-  // key: org bytes (s - 128) or the job's int16 key block
-  uint32_t o[UH][UW / 4];      // org bytes, rows
-  uint32_t kr[UH][UW / 2];     // key int16 pairs (cols 2k, 2k+1), rows
+  // key block, one register array for either form: org bytes (s - 128) in kraw[r][0 .. UW/4)
+  // (uni-pred), or the job's int16 key pairs (cols 2k, 2k+1) in kraw[r][0 .. UW/2)
+  uint32_t kraw[UH][UW / 2];
   if (!kbuf) {
     const PicDesc org = a.pics[j.org_id];
 #pragma unroll
     for (int r = 0; r < UH; r++) {
       const uint8_t* q = org.luma + (size_t)(oy + r) * org.stride + ox;
       if constexpr (UW == 8) {
-        const u32x2a v = *(gu2*)q;
-        o[r][0] = v.x ^ 0x80808080u;
-        o[r][1] = v.y ^ 0x80808080u;
+        const u32x2a ov = *(gu2*)q;
+        kraw[r][0] = ov.x ^ 0x80808080u;
+        kraw[r][1] = ov.y ^ 0x80808080u;
       } else {
-        o[r][0] = gld32(q) ^ 0x80808080u;
+        kraw[r][0] = gld32(q) ^ 0x80808080u;
       }
 #pragma unroll
-      for (int k = 0; k < UW / 2; k++) kr[r][k] = 0;
+      for (int k = UW / 4; k < UW / 2; k++) kraw[r][k] = 0;
     }
   } else {
     const int16_t* kb = a.keys + (size_t)j.key_offset + (size_t)(uy * UH) * PW + ux * UW;
 #pragma unroll
-    for (int r = 0; r < UH; r++) {
+    for (int r = 0; r < UH; r++)
 #pragma unroll
       for (int k = 0; k < UW / 2; k++) {
         const uint32_t lo = *(gu16*)(kb + r * PW + 2 * k), hi = *(gu16*)(kb + r * PW + 2 * k + 1);
-        kr[r][k] = lo | (hi << 16);
+        kraw[r][k] = lo | (hi << 16);
       }
-#pragma unroll
-      for (int k = 0; k < UW / 4; k++) o[r][k] = 0;
-    }
   }
 
   // ---- 2. EMI square step -----------------------------------------------------------------------
@@ -290,47 +486,70 @@ __device__ __forceinline__ void lane_unit(const BatchArgs& a, const fme_job* __r
 #pragma unroll
   for (int k = 0; k < 8; k++) emi[k] = 0;
   if (!(FME_LANE_SKIP & 4) && (j.flags & FME_JOB_EMI)) {
+    // Row-major: window row R (= 5 + dy + r) serves positions (dx, dy) with org row r = R-5-dy;
+    // its byte groups at dx = -1, 0, 1 are formed once.
     uint32_t e9[9];
-    if (!kbuf) {
-      int so2 = 0;
+    if (!kbuf) {   // SSE = So2 - 2 Sop + Spp on the s - 128 bytes
+      int so2 = 0, sop[9], spp[3][3];   // spp[dx][dy]
+#pragma unroll
+      for (int i = 0; i < 9; i++) sop[i] = 0;
+#pragma unroll
+      for (int i = 0; i < 3; i++)
+#pragma unroll
+        for (int q = 0; q < 3; q++) spp[i][q] = 0;
 #pragma unroll
       for (int r = 0; r < UH; r++)
 #pragma unroll
-        for (int k = 0; k < UW / 4; k++) so2 = dot4(o[r][k], o[r][k], so2);
+        for (int k = 0; k < UW / 4; k++) so2 = dot4(kraw[r][k], kraw[r][k], so2);
 #pragma unroll
-      for (int pos = 0; pos < 9; pos++) {
-        const int dx = emi_dx(pos), dy = emi_dy(pos);
-        int sop = 0, spp = 0;
+      for (int R = 4; R < UH + 6; R++) {
 #pragma unroll
-        for (int r = 0; r < UH; r++) {
-          const uint32_t(&row)[NW] = w[5 + dy + r];
+        for (int dx = -1; dx <= 1; dx++)
 #pragma unroll
           for (int k = 0; k < UW / 4; k++) {
-            const uint32_t pv = rbytes(row, 5 + dx + 4 * k);
-            sop = dot4(o[r][k], pv, sop);
-            spp = dot4(pv, pv, spp);
+            const uint32_t pv = rbytes(w[R], 5 + dx + 4 * k);
+            const int pp = dot4(pv, pv, 0);
+#pragma unroll
+            for (int dy = -1; dy <= 1; dy++) {
+              const int r = R - 5 - dy;
+              if (r < 0 || r >= UH) continue;
+              int pos = 0;
+#pragma unroll
+              for (int q = 0; q < 9; q++)
+                if (emi_dx(q) == dx && emi_dy(q) == dy) pos = q;
+              sop[pos] = dot4(kraw[r][k], pv, sop[pos]);
+              spp[dx + 1][dy + 1] += pp;
+            }
           }
-        }
-        e9[pos] = (uint32_t)(so2 - 2 * sop + spp);
+        __builtin_amdgcn_sched_barrier(0);
       }
+#pragma unroll
+      for (int q = 0; q < 9; q++) e9[q] = (uint32_t)(so2 - 2 * sop[q] + spp[emi_dx(q) + 1][emi_dy(q) + 1]);
     } else {
 #pragma unroll
-      for (int pos = 0; pos < 9; pos++) {
-        const int dx = emi_dx(pos), dy = emi_dy(pos);
-        int s = 0;
+      for (int q = 0; q < 9; q++) e9[q] = 0;
 #pragma unroll
-        for (int r = 0; r < UH; r++) {
-          const uint32_t(&row)[NW] = w[5 + dy + r];
+      for (int R = 4; R < UH + 6; R++) {
+#pragma unroll
+        for (int dx = -1; dx <= 1; dx++)
 #pragma unroll
           for (int k = 0; k < UW / 4; k++) {
-            const uint32_t x = rbytes(row, 5 + dx + 4 * k) ^ 0x80808080u;   // samples 0..255
-            const uint32_t d0 = pk_sub(kr[r][2 * k], lo_pair(x));
-            const uint32_t d1 = pk_sub(kr[r][2 * k + 1], hi_pair(x));
-            s = dot2(d0, d0, s);
-            s = dot2(d1, d1, s);
+            const uint32_t x = rbytes(w[R], 5 + dx + 4 * k) ^ 0x80808080u;   // samples 0..255
+            const uint32_t lo = lo_pair(x), hi = hi_pair(x);
+#pragma unroll
+            for (int dy = -1; dy <= 1; dy++) {
+              const int r = R - 5 - dy;
+              if (r < 0 || r >= UH) continue;
+              int pos = 0;
+#pragma unroll
+              for (int q = 0; q < 9; q++)
+                if (emi_dx(q) == dx && emi_dy(q) == dy) pos = q;
+              const uint32_t d0 = pk_sub(kraw[r][2 * k], lo);
+              const uint32_t d1 = pk_sub(kraw[r][2 * k + 1], hi);
+              e9[pos] = (uint32_t)dot2(d1, d1, dot2(d0, d0, (int)e9[pos]));
+            }
           }
-        }
-        e9[pos] = (uint32_t)s;
+        __builtin_amdgcn_sched_barrier(0);
       }
     }
 #pragma unroll
@@ -403,214 +622,55 @@ __device__ __forceinline__ void lane_unit(const BatchArgs& a, const fme_job* __r
   for (int c = 0; c < UW; c++)
 #pragma unroll
     for (int jj = 0; jj < UJ; jj++) {
-      const uint32_t ko = sext_pair(o[2 * jj + 1][c >> 2], o[2 * jj][c >> 2], c & 3);
+      const uint32_t ko = sext_pair(kraw[2 * jj + 1][c >> 2], kraw[2 * jj][c >> 2], c & 3);
       const uint32_t hs = (c & 1) ? 0x07060302u : 0x05040100u;   // 16-bit half c&1 of each row
-      const uint32_t kb = pk_sub(__builtin_amdgcn_perm(kr[2 * jj + 1][c >> 1], kr[2 * jj][c >> 1], hs), 0x00800080u);
+      const uint32_t kb = pk_sub(__builtin_amdgcn_perm(kraw[2 * jj + 1][c >> 1], kraw[2 * jj][c >> 1], hs), 0x00800080u);
       K[c][jj] = kbuf ? kb : ko;
     }
 
   // ---- 3. half-pel stage (H9 order: (0,0),(0,-1),(0,1),(-1,0),(1,0),(-1,-1),(1,-1),(-1,1),(1,1)) ---
-  // At most two candidates' key - pred arrays are live at a time (register budget).
-  // candidates arrive out of H9 order: keep the first strict minimum in H9 order with an index
-  // tie-break (d < best, or d == best at a lower index)
+  // Candidates arrive out of H9 order: keep the first strict minimum in H9 order with an index
+  // tie-break (d < best, or d == best at a lower index).
   uint32_t hbest = 0xFFFFFFFFu;
   int hbi = 9;
-  auto half_cand = [&](int i, uint32_t part) {
-    const uint32_t d = group_sum<L>(part) + mv_cost(ml, mv_bits(2 * mvx + h9_dx(i), 2 * mvy + h9_dy(i), 1, mvp_x, mvp_y));
-    if (d < hbest || (d == hbest && i < hbi)) {
-      hbest = d;
-      hbi = i;
-    }
-  };
   {
-    uint32_t c2lo, c2hi;
-    taps8(2, c2lo, c2hi);
-    // (0,0): integer samples, window' rows 4+y, cols 4+x
-    if (!(FME_LANE_SKIP & 16)) {
-      uint32_t X[UW][UJ];
-#pragma unroll
-      for (int x = 0; x < UW; x++)
-#pragma unroll
-        for (int jj = 0; jj < UJ; jj++)
-          X[x][jj] = pk_sub(K[x][jj], sext_pair(v[5 + 2 * jj][(x + 4) >> 2], v[4 + 2 * jj][(x + 4) >> 2], (x + 4) & 3));
-      half_cand(0, unit_dist<UW, UH, T>(X, had));
-    }
-    // (0,-1), (0,1): vertical half-pel on integer columns (transposed window')
-    if (!(FME_LANE_SKIP & 8)) {
-      launder(v);
-      uint32_t X1[UW][UJ], X2[UW][UJ];
-#pragma unroll
-      for (int g = 0; g < UW / 4; g++) {
-        uint32_t CB[4][RV / 4];   // columns 4g..4g+3 (window' cols 4g+4 ..), 4 rows per dword
-#pragma unroll
-        for (int q = 0; q < RV / 4; q++) {
-          const uint32_t rows[4] = {v[4 * q][g + 1], v[4 * q + 1][g + 1], v[4 * q + 2][g + 1], v[4 * q + 3][g + 1]};
-          uint32_t cols[4];
-          transpose4x4(rows, cols);
-#pragma unroll
-          for (int c = 0; c < 4; c++) CB[c][q] = cols[c];
-        }
-#pragma unroll
-        for (int c4 = 0; c4 < 4; c4++) {
-          const int x = 4 * g + c4;
-          int v1[UH + 1];   // half rows i = 0..UH (between rows i-1, i): taps on window' rows i..i+7
-#pragma unroll
-          for (int i = 0; i <= UH; i++) {
-            const int acc = dot4(rbytes(CB[c4], i), c2lo, 32);
-            v1[i] = clamp_s8(dot4(rbytes(CB[c4], i + 4), c2hi, acc) >> 6);
-          }
-#pragma unroll
-          for (int jj = 0; jj < UJ; jj++) {
-            X1[x][jj] = pk_sub(K[x][jj], pack2(v1[2 * jj], v1[2 * jj + 1]));
-            X2[x][jj] = pk_sub(K[x][jj], pack2(v1[2 * jj + 1], v1[2 * jj + 2]));
-          }
-        }
-      }
-      half_cand(1, unit_dist<UW, UH, T>(X1, had));
-      half_cand(2, unit_dist<UW, UH, T>(X2, had));
-    }
-    const uint32_t c16[4] = {p16(-1, 4), p16(-11, 40), p16(40, -11), p16(4, -1)};
-    const uint32_t c16o[5] = {p16(0, -1), p16(4, -11), p16(40, 40), p16(-11, 4), p16(-1, 0)};
-    // passes instantiated per side (a rolled loop would index the window registers dynamically)
-    auto side_pass = [&](auto side_c) {
-      constexpr int side = decltype(side_c)::value;
-      // (s,0): horizontal half-pel, half column jc = x + side (window' bytes jc .. jc+7)
-      {
-        launder(v);
-        uint32_t X[UW][UJ];
-#pragma unroll
-        for (int x = 0; x < UW; x++) {
-          const int jc = x + side;
-          int h1[UH];
-#pragma unroll
-          for (int y = 0; y < UH; y++) {
-            const uint32_t(&row)[NV] = v[y + 4];
-            h1[y] = clamp_s8(dot4(rbytes(row, jc + 4), c2hi, dot4(rbytes(row, jc), c2lo, 32)) >> 6);
-          }
-#pragma unroll
-          for (int jj = 0; jj < UJ; jj++) X[x][jj] = pk_sub(K[x][jj], pack2(h1[2 * jj], h1[2 * jj + 1]));
-        }
-        half_cand(3 + side, unit_dist<UW, UH, T>(X, had));
-      }
-      // (s,-1), (s,1): 2-D half-pel (first stage rows -4..UH+3 of half column jc, then vertical)
-      {
-        launder(v);
-        uint32_t XB[UW][UJ], XC[UW][UJ];
-#pragma unroll
-        for (int x = 0; x < UW; x++) {
-          const int jc = x + side;
-          launder(v);
-          uint32_t HP[RV / 2];
-#pragma unroll
-          for (int r = 0; r < RV; r += 2) {
-            const int h0 = dot4(rbytes(v[r], jc + 4), c2hi, dot4(rbytes(v[r], jc), c2lo, 0));
-            const int h1 = dot4(rbytes(v[r + 1], jc + 4), c2hi, dot4(rbytes(v[r + 1], jc), c2lo, 0));
-            HP[r / 2] = pack2(h0, h1);
-          }
-          int v2[UH + 1];
-#pragma unroll
-          for (int i = 0; i <= UH; i++) {
-            int acc = 2048;
-            if ((i & 1) == 0) {
-#pragma unroll
-              for (int t = 0; t < 4; t++) acc = dot2(HP[i / 2 + t], c16[t], acc);
-            } else {
-#pragma unroll
-              for (int t = 0; t < 5; t++) acc = dot2(HP[(i - 1) / 2 + t], c16o[t], acc);
-            }
-            v2[i] = clamp_s8(acc >> 12);
-          }
-#pragma unroll
-          for (int jj = 0; jj < UJ; jj++) {
-            XB[x][jj] = pk_sub(K[x][jj], pack2(v2[2 * jj], v2[2 * jj + 1]));
-            XC[x][jj] = pk_sub(K[x][jj], pack2(v2[2 * jj + 1], v2[2 * jj + 2]));
-          }
-          __builtin_amdgcn_sched_barrier(0);   // one column at a time (register pressure)
-        }
-        half_cand(5 + side, unit_dist<UW, UH, T>(XB, had));
-        half_cand(7 + side, unit_dist<UW, UH, T>(XC, had));
-      }
-    };
-    if (!(FME_LANE_SKIP & 2)) {
-      side_pass(std::integral_constant<int, 0>{});
-      side_pass(std::integral_constant<int, 1>{});
-    }
+    uint32_t d[3];
+    half_center<UW, UH, T>(v, K, had, d);
+    take_half<L>(0, d[0], ml, mvx, mvy, mvp_x, mvp_y, hbest, hbi);
+    take_half<L>(1, d[1], ml, mvx, mvy, mvp_x, mvp_y, hbest, hbi);
+    take_half<L>(2, d[2], ml, mvx, mvy, mvp_x, mvp_y, hbest, hbi);
+  }
+  if (!(FME_LANE_SKIP & 2)) {
+    uint32_t d[3];
+    half_side<UW, UH, T, 0>(v, K, had, d);
+    take_half<L>(3, d[0], ml, mvx, mvy, mvp_x, mvp_y, hbest, hbi);
+    take_half<L>(5, d[1], ml, mvx, mvy, mvp_x, mvp_y, hbest, hbi);
+    take_half<L>(7, d[2], ml, mvx, mvy, mvp_x, mvp_y, hbest, hbi);
+    half_side<UW, UH, T, 1>(v, K, had, d);
+    take_half<L>(4, d[0], ml, mvx, mvy, mvp_x, mvp_y, hbest, hbi);
+    take_half<L>(6, d[1], ml, mvx, mvy, mvp_x, mvp_y, hbest, hbi);
+    take_half<L>(8, d[2], ml, mvx, mvy, mvp_x, mvp_y, hbest, hbi);
   }
   const int hx = h9_dx(hbi), hy = h9_dy(hbi);
 
-  // ---- 4. quarter-pel stage: column phase k (dqx = k-1), row phase l (dqy = l-1) ----------------
-  // Passes of at most two candidates sharing a column phase: k0{l0,l1} k0{l2} k1{l0,l2}
-  // k2{l0,l1} k2{l2}; candidate (k1,l1) is the half best itself.
-  uint32_t qbest = hbest;   // Q9 candidate 0 is the half best: same distortion, same bits
+  // ---- 4. quarter-pel stage: passes over column phases (Q9 candidate 0 = the half best) -------
+  uint32_t qbest = hbest;
   int qbi = 0;
-  auto qtr_cand = [&](int i, uint32_t part) {
-    const int qx = 2 * hx + q9_dx(i), qy = 2 * hy + q9_dy(i);
-    const uint32_t d = group_sum<L>(part) + mv_cost(ml, mv_bits(4 * mvx + qx, 4 * mvy + qy, 0, mvp_x, mvp_y));
-    if (d < qbest || (d == qbest && i < qbi)) {
-      qbest = d;
-      qbi = i;
-    }
-  };
-  {
-    auto qpass = [&](auto ps_c) {
-      constexpr int ps = decltype(ps_c)::value;
-      constexpr int PK[5] = {0, 0, 1, 2, 2};
-      constexpr int PL0[5] = {0, 2, 0, 0, 2};
-      constexpr int PL1[5] = {1, -1, 2, 1, -1};
-      constexpr int k = PK[ps];
-      const int qx = 2 * hx + (k - 1);
-      const int ix = qx >> 2, fx = qx & 3;
-      const uint32_t dlt = (uint32_t)(1 + ix);
-      uint32_t clo, chi;
-      taps8_any(fx, clo, chi);
-      constexpr int NPASS = PL1[ps] < 0 ? 1 : 2;
-      constexpr int ls[2] = {PL0[ps], PL1[ps]};
-      uint32_t cpe[NPASS][5], cpo[NPASS][5];
-#pragma unroll
-      for (int m = 0; m < NPASS; m++) {
-        const int l = ls[m];
-        const int qy = 2 * hy + (l - 1);
-        const int iy = qy >> 2, fy = qy & 3;
-        vpairs(fy, 1 + iy, cpe[m]);
-        vpairs(fy, 2 + iy, cpo[m]);
-      }
-      uint32_t XQ[NPASS][UW][UJ];
-#pragma unroll
-      for (int x = 0; x < UW; x++) {
-        launder(v);
-        uint32_t HQ[RV / 2];
-#pragma unroll
-        for (int r = 0; r < RV; r += 2) {
-          const int h0 = dot4(rbytes_d(v[r], x + 4, dlt), chi, dot4(rbytes_d(v[r], x, dlt), clo, 0));
-          const int h1 = dot4(rbytes_d(v[r + 1], x + 4, dlt), chi, dot4(rbytes_d(v[r + 1], x, dlt), clo, 0));
-          HQ[r / 2] = pack2(h0, h1);
-        }
-#pragma unroll
-        for (int m = 0; m < NPASS; m++) {
-          int vq[UH];
-#pragma unroll
-          for (int y = 0; y < UH; y++) {
-            const int m0 = (y & 1) ? (y - 1) / 2 : y / 2;
-            int acc = 2048;
-#pragma unroll
-            for (int t = 0; t < 5; t++) acc = dot2(HQ[m0 + t], (y & 1) ? cpo[m][t] : cpe[m][t], acc);
-            vq[y] = clamp_s8(acc >> 12);
-          }
-#pragma unroll
-          for (int jj = 0; jj < UJ; jj++) XQ[m][x][jj] = pk_sub(K[x][jj], pack2(vq[2 * jj], vq[2 * jj + 1]));
-        }
-        __builtin_amdgcn_sched_barrier(0);   // one column at a time (register pressure)
-      }
-#pragma unroll
-      for (int m = 0; m < NPASS; m++) qtr_cand(q9_index(k - 1, ls[m] - 1), unit_dist<UW, UH, T>(XQ[m], had));
-    };
-    if (!(FME_LANE_SKIP & 1)) {
-      qpass(std::integral_constant<int, 0>{});
-      qpass(std::integral_constant<int, 1>{});
-      qpass(std::integral_constant<int, 2>{});
-      qpass(std::integral_constant<int, 3>{});
-      qpass(std::integral_constant<int, 4>{});
-    }
+  if (!(FME_LANE_SKIP & 1)) {
+    uint32_t d[2];
+    qtr_pass<UW, UH, T, 0>(v, K, had, hx, hy, d);
+    take_qtr<L>(qp_idx0(0), d[0], ml, mvx, mvy, hx, hy, mvp_x, mvp_y, qbest, qbi);
+    take_qtr<L>(qp_idx1(0), d[1], ml, mvx, mvy, hx, hy, mvp_x, mvp_y, qbest, qbi);
+    qtr_pass<UW, UH, T, 1>(v, K, had, hx, hy, d);
+    take_qtr<L>(qp_idx0(1), d[0], ml, mvx, mvy, hx, hy, mvp_x, mvp_y, qbest, qbi);
+    qtr_pass<UW, UH, T, 2>(v, K, had, hx, hy, d);
+    take_qtr<L>(qp_idx0(2), d[0], ml, mvx, mvy, hx, hy, mvp_x, mvp_y, qbest, qbi);
+    take_qtr<L>(qp_idx1(2), d[1], ml, mvx, mvy, hx, hy, mvp_x, mvp_y, qbest, qbi);
+    qtr_pass<UW, UH, T, 3>(v, K, had, hx, hy, d);
+    take_qtr<L>(qp_idx0(3), d[0], ml, mvx, mvy, hx, hy, mvp_x, mvp_y, qbest, qbi);
+    take_qtr<L>(qp_idx1(3), d[1], ml, mvx, mvy, hx, hy, mvp_x, mvp_y, qbest, qbi);
+    qtr_pass<UW, UH, T, 4>(v, K, had, hx, hy, d);
+    take_qtr<L>(qp_idx0(4), d[0], ml, mvx, mvy, hx, hy, mvp_x, mvp_y, qbest, qbi);
   }
   const int bq = qbi;
 
@@ -667,9 +727,13 @@ __device__ __forceinline__ int xcd_block(int r, int n) {
       default: break;                                                                                \
     }                                                                                                \
   }
+#ifndef FME_LANE_ONLY88
 FME_LANE_KERNEL(k_search_lane48, kSearchLane48, FME_LANE48_CLASSES, FME_LANE_WAVES_SMALL)
+#endif
 #ifndef FME_LANE_ONLY48
+#ifndef FME_LANE_ONLY88
 FME_LANE_KERNEL(k_search_lane84, kSearchLane84, FME_LANE84_CLASSES, FME_LANE_WAVES_SMALL)
+#endif
 FME_LANE_KERNEL(k_search_lane88, kSearchLane88, FME_LANE88_CLASSES, FME_LANE_WAVES_88)
 #endif
 #undef FME_CASE
@@ -705,13 +769,18 @@ int lane_kernel_of(int cls) {
 }
 
 hipError_t launch_search_lane(const BatchArgs& a, const WorkBufs& w, const Schedule& sc, hipStream_t s) {
-  int blocks = sc.prefix[kSearchLane48][kNumClasses];
+  int blocks = 0;
+#ifndef FME_LANE_ONLY88
+  blocks = sc.prefix[kSearchLane48][kNumClasses];
   if (blocks > 0) hipLaunchKernelGGL(k_search_lane48, dim3(blocks), dim3(kLaneNT), 0, s, a, w, sc);
+#endif
 #ifndef FME_LANE_ONLY48
   blocks = sc.prefix[kSearchLane88][kNumClasses];
   if (blocks > 0) hipLaunchKernelGGL(k_search_lane88, dim3(blocks), dim3(kLaneNT), 0, s, a, w, sc);
+#ifndef FME_LANE_ONLY88
   blocks = sc.prefix[kSearchLane84][kNumClasses];
   if (blocks > 0) hipLaunchKernelGGL(k_search_lane84, dim3(blocks), dim3(kLaneNT), 0, s, a, w, sc);
+#endif
 #endif
   return hipGetLastError();
 }
