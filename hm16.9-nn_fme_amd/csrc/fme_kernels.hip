@@ -260,37 +260,32 @@ __device__ __forceinline__ int nn_forward(const float* __restrict__ P, const uin
   return best;
 }
 
-__global__ __launch_bounds__(kBlock) void k_nn_tail(BatchArgs a, WorkBufs w,
-                                                    const float* __restrict__ nnp_g, int state_in) {
-  __shared__ int32_t wave_tot[kBlock / 64][9];
+// One lane per job, 1024 lanes per block = one 1024-job scan block (kJobsPerScanBlock).
+constexpr int kTailNT = kJobsPerScanBlock;
+
+__global__ __launch_bounds__(kTailNT) void k_nn_tail(BatchArgs a, WorkBufs w,
+                                                     const float* __restrict__ nnp_g, int state_in) {
+  __shared__ int32_t wave_tot[kTailNT / 64][9];
   // weights in LDS: every lane reads the same address (broadcast), no scalar-register pressure
   __shared__ __attribute__((aligned(16))) float nnp[FME_NN_PARAMS + 4];
   if (a.nn_mode)
-    for (int i = threadIdx.x; i < FME_NN_PARAMS; i += kBlock) nnp[i] = nnp_g[i];
+    for (int i = threadIdx.x; i < FME_NN_PARAMS; i += kTailNT) nnp[i] = nnp_g[i];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  constexpr int Q = kJobsPerScanBlock / kBlock;   // consecutive jobs per lane
-  const int i0 = blockIdx.x * kJobsPerScanBlock + tid * Q;
+  const int i = blockIdx.x * kJobsPerScanBlock + tid;
+  const bool valid = i < a.n;
+  fme_job j{};
+  if (valid) j = a.jobs[i];
 
-  // writer indices of this lane's jobs (inclusive running max over its Q consecutive jobs)
+  // writer indices of this job (slots it pushes, C/PU size), prefix-max across the block
   int run[9];
+  {
+    const bool emi = valid && (j.flags & FME_JOB_EMI);
+    const int np = emi ? emi_pushes(j) : 0;
 #pragma unroll
-  for (int f = 0; f < 9; f++) run[f] = -1;
-#pragma unroll
-  for (int q = 0; q < Q; q++) {
-    const int i = i0 + q;
-    if (i < a.n) {
-      const fme_job j = a.jobs[i];
-      if (j.flags & FME_JOB_EMI) {
-        const int np = emi_pushes(j);
-#pragma unroll
-        for (int s = 0; s < 8; s++)
-          if (np > s) run[s] = i;
-        run[8] = i;
-      }
-    }
+    for (int s = 0; s < 8; s++) run[s] = (np > s) ? i : -1;
+    run[8] = emi ? i : -1;
   }
-  // exclusive prefix-max of the lane totals across the block
-  int excl[9];
+  int incl[9];
 #pragma unroll
   for (int f = 0; f < 9; f++) {
     int v = run[f];
@@ -299,96 +294,78 @@ __global__ __launch_bounds__(kBlock) void k_nn_tail(BatchArgs a, WorkBufs w,
       const int o = __shfl_up(v, off, 64);
       if (lane >= off) v = max(v, o);
     }
-    const int ex = __shfl_up(v, 1, 64);
-    excl[f] = lane == 0 ? -1 : ex;
+    incl[f] = v;
     if (lane == 63) wave_tot[wid][f] = v;
   }
   __syncthreads();
+  int src[9];
 #pragma unroll
   for (int f = 0; f < 9; f++) {
     int carry = w.blk_prefix[blockIdx.x * 9 + f];
     for (int u = 0; u < wid; u++) carry = max(carry, wave_tot[u][f]);
-    excl[f] = max(excl[f], carry);
+    src[f] = max(incl[f], carry);   // inclusive: this job's own pushes count
   }
+  if (!valid) return;
 
   const uint32_t* st_in = w.nn_state + 12 * state_in;
   uint32_t* st_out = w.nn_state + 12 * (state_in ^ 1);
-  int src[9];
+  fme_result* r = a.res + i;
+  const double ml = a.mlambda[j.lambda_id];
+  const int mvx = r->mv_int_x, mvy = r->mv_int_y;
+  int offx, offy;
+  uint16_t status = 0;
+  if (a.nn_mode) {
+    uint32_t e[8];
+    uint32_t written = st_in[11];
 #pragma unroll
-  for (int f = 0; f < 9; f++) src[f] = excl[f];
-#pragma unroll 1
-  for (int q = 0; q < Q; q++) {
-    const int i = i0 + q;
-    if (i >= a.n) break;
-    {
-      const fme_job jj = a.jobs[i];
-      if (jj.flags & FME_JOB_EMI) {
-        const int np = emi_pushes(jj);
-#pragma unroll
-        for (int s = 0; s < 8; s++)
-          if (np > s) src[s] = i;
-        src[8] = i;
-      }
-    }
-    const fme_job j = a.jobs[i];
-    fme_result* r = a.res + i;
-    const double ml = a.mlambda[j.lambda_id];
-    const int mvx = r->mv_int_x, mvy = r->mv_int_y;
-    int offx, offy;
-    uint16_t status = 0;
-    if (a.nn_mode) {
-      uint32_t e[8];
-      uint32_t written = st_in[11];
-#pragma unroll
-      for (int s = 0; s < 8; s++) {
-        if (src[s] >= 0) {
-          e[s] = a.res[src[s]].emi[s];
-          written |= 1u << s;
-        } else {
-          e[s] = st_in[s];
-        }
-      }
-      uint32_t c, ph, pw;
-      if (src[8] >= 0) {
-        c = a.res[src[8]].c;
-        ph = a.jobs[src[8]].h;
-        pw = a.jobs[src[8]].w;
-        written |= 0x100u;
+    for (int s = 0; s < 8; s++) {
+      if (src[s] >= 0) {
+        e[s] = a.res[src[s]].emi[s];
+        written |= 1u << s;
       } else {
-        c = st_in[8];
-        ph = st_in[9];
-        pw = st_in[10];
+        e[s] = st_in[s];
       }
-      const int cls = nn_forward(nnp, e, c, (int)ph, (int)pw);
-      r->nn_class = (uint8_t)cls;
-      if (!(j.flags & FME_JOB_EMI) || r->n_emi < 8) status |= FME_RES_NN_STALE;
-      if ((written & 0x1FFu) != 0x1FFu) status |= FME_RES_NN_UNINIT;
-      offx = cls % 7 - 3;
-      offy = cls / 7 - 3;
-      if (i == a.n - 1) {  // carry the global state to the next batch
-#pragma unroll
-        for (int s = 0; s < 8; s++) st_out[s] = e[s];
-        st_out[8] = c;
-        st_out[9] = ph;
-        st_out[10] = pw;
-        st_out[11] = written;
-      }
-    } else {
-      r->nn_class = 255;
-      offx = 2 * r->half_x + r->qtr_x;
-      offy = 2 * r->half_y + r->qtr_y;
     }
-    const int fx = 4 * mvx + offx, fy = 4 * mvy + offy;
-    r->mv_x = (int16_t)fx;
-    r->mv_y = (int16_t)fy;
-    const uint32_t mvb = mv_bits(fx, fy, 0, j.mvp_x, j.mvp_y);
-    const uint32_t bits = (uint32_t)j.bits_in + mvb;
-    r->bits = bits;
-    const double fw = (j.flags & FME_JOB_BIPRED) ? 0.5 : 1.0;
-    const double val = floor(fw * ((double)r->frac_cost - (double)mv_cost(ml, mvb))) + (double)mv_cost(ml, bits);
-    r->cost = (uint32_t)(int64_t)val;   // gcc/x86-64 (Distortion)(double) semantics
-    r->status = status;
+    uint32_t c, ph, pw;
+    if (src[8] >= 0) {
+      c = a.res[src[8]].c;
+      ph = a.jobs[src[8]].h;
+      pw = a.jobs[src[8]].w;
+      written |= 0x100u;
+    } else {
+      c = st_in[8];
+      ph = st_in[9];
+      pw = st_in[10];
+    }
+    const int cls = nn_forward(nnp, e, c, (int)ph, (int)pw);
+    r->nn_class = (uint8_t)cls;
+    if (!(j.flags & FME_JOB_EMI) || r->n_emi < 8) status |= FME_RES_NN_STALE;
+    if ((written & 0x1FFu) != 0x1FFu) status |= FME_RES_NN_UNINIT;
+    offx = cls % 7 - 3;
+    offy = cls / 7 - 3;
+    if (i == a.n - 1) {  // carry the global state to the next batch
+#pragma unroll
+      for (int s = 0; s < 8; s++) st_out[s] = e[s];
+      st_out[8] = c;
+      st_out[9] = ph;
+      st_out[10] = pw;
+      st_out[11] = written;
+    }
+  } else {
+    r->nn_class = 255;
+    offx = 2 * r->half_x + r->qtr_x;
+    offy = 2 * r->half_y + r->qtr_y;
   }
+  const int fx = 4 * mvx + offx, fy = 4 * mvy + offy;
+  r->mv_x = (int16_t)fx;
+  r->mv_y = (int16_t)fy;
+  const uint32_t mvb = mv_bits(fx, fy, 0, j.mvp_x, j.mvp_y);
+  const uint32_t bits = (uint32_t)j.bits_in + mvb;
+  r->bits = bits;
+  const double fw = (j.flags & FME_JOB_BIPRED) ? 0.5 : 1.0;
+  const double val = floor(fw * ((double)r->frac_cost - (double)mv_cost(ml, mvb))) + (double)mv_cost(ml, bits);
+  r->cost = (uint32_t)(int64_t)val;   // gcc/x86-64 (Distortion)(double) semantics
+  r->status = status;
 }
 
 // NN_pred() on one explicit input (fme_nn_pred_single): e[8], C, PUHeight, PUWidth.
@@ -426,7 +403,7 @@ hipError_t launch_nn_tail(const BatchArgs& a, const WorkBufs& w, const float* nn
   hipLaunchKernelGGL(k_scan_blocks, dim3(1), dim3(1024), 0, s, w, nb);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(k_nn_tail, dim3(nb), dim3(kBlock), 0, s, a, w, nn_params, state_in);
+  hipLaunchKernelGGL(k_nn_tail, dim3(nb), dim3(kTailNT), 0, s, a, w, nn_params, state_in);
   return hipGetLastError();
 }
 

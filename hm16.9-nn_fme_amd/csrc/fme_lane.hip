@@ -36,12 +36,22 @@
 #ifndef FME_LANE_SKIP
 #define FME_LANE_SKIP 0
 #endif
+// Candidates per quarter pass (2: column-phase pairs, 1: one candidate per pass — fewer live
+// registers, the first-stage column recomputed per candidate)
+#ifndef FME_LANE_QPAIR
+#define FME_LANE_QPAIR 1
+#endif
+// Half-stage vertical pairs {(0,-1),(0,1)} and {(s,-1),(s,1)} in one pass (2) or one
+// candidate per pass (1)
+#ifndef FME_LANE_HPAIR
+#define FME_LANE_HPAIR 1
+#endif
 // occupancy targets (waves per SIMD) that bound the register allocation of each kernel
 #ifndef FME_LANE_WAVES_SMALL
 #define FME_LANE_WAVES_SMALL 2
 #endif
 #ifndef FME_LANE_WAVES_88
-#define FME_LANE_WAVES_88 1
+#define FME_LANE_WAVES_88 2
 #endif
 
 namespace fme {
@@ -204,7 +214,9 @@ __device__ __forceinline__ void half_center(uint32_t (&v)[UH + 8][UW / 4 + 2], c
     d[0] = unit_dist<UW, UH, T>(X, had);
   }
   launder(v);
-  {   // (0,-1), (0,1): vertical half-pel on integer columns (transposed window')
+  // (0,-1), (0,1): vertical half-pel on integer columns (transposed window')
+  auto vpass = [&](auto sel_c) {   // sel 1: (0,-1) only, 2: (0,1) only, 3: both
+    constexpr int sel = decltype(sel_c)::value;
     uint32_t X1[UW][UJ], X2[UW][UJ];
 #pragma unroll
     for (int g = 0; g < UW / 4; g++) {
@@ -222,21 +234,28 @@ __device__ __forceinline__ void half_center(uint32_t (&v)[UH + 8][UW / 4 + 2], c
         const int x = 4 * g + c4;
         int v1[UH + 1];   // half rows i = 0..UH (between rows i-1, i): taps on window' rows i..i+7
 #pragma unroll
-        for (int i = 0; i <= UH; i++) {
+        for (int i = (sel == 2 ? 1 : 0); i <= (sel == 1 ? UH - 1 : UH); i++) {
           const int acc = dot4(rbytes(CB[c4], i), c2lo, 32);
           v1[i] = clamp_s8(dot4(rbytes(CB[c4], i + 4), c2hi, acc) >> 6);
         }
 #pragma unroll
         for (int jj = 0; jj < UJ; jj++) {
-          X1[x][jj] = pk_sub(K[x][jj], pack2(v1[2 * jj], v1[2 * jj + 1]));
-          X2[x][jj] = pk_sub(K[x][jj], pack2(v1[2 * jj + 1], v1[2 * jj + 2]));
+          if (sel & 1) X1[x][jj] = pk_sub(K[x][jj], pack2(v1[2 * jj], v1[2 * jj + 1]));
+          if (sel & 2) X2[x][jj] = pk_sub(K[x][jj], pack2(v1[2 * jj + 1], v1[2 * jj + 2]));
         }
         __builtin_amdgcn_sched_barrier(0);
       }
     }
-    d[1] = unit_dist<UW, UH, T>(X1, had);
-    d[2] = unit_dist<UW, UH, T>(X2, had);
-  }
+    if (sel & 1) d[1] = unit_dist<UW, UH, T>(X1, had);
+    if (sel & 2) d[2] = unit_dist<UW, UH, T>(X2, had);
+  };
+#if FME_LANE_HPAIR == 2
+  vpass(std::integral_constant<int, 3>{});
+#else
+  vpass(std::integral_constant<int, 1>{});
+  launder(v);
+  vpass(std::integral_constant<int, 2>{});
+#endif
 }
 
 // (s,0), (s,-1), (s,1) for s = -1 (SIDE 0: half column x) or +1 (SIDE 1: half column x+1)
@@ -262,7 +281,9 @@ __device__ __forceinline__ void half_side(uint32_t (&v)[UH + 8][UW / 4 + 2], con
     d[0] = unit_dist<UW, UH, T>(X, had);
   }
   launder(v);
-  {   // (s,-1), (s,1): 2-D half-pel (first stage rows -4..UH+3 of half column jc, then vertical)
+  // (s,-1), (s,1): 2-D half-pel (first stage rows -4..UH+3 of half column jc, then vertical)
+  auto dpass = [&](auto sel_c) {   // sel 1: (s,-1) only, 2: (s,1) only, 3: both
+    constexpr int sel = decltype(sel_c)::value;
     const uint32_t c16[4] = {p16(-1, 4), p16(-11, 40), p16(40, -11), p16(4, -1)};
     const uint32_t c16o[5] = {p16(0, -1), p16(4, -11), p16(40, 40), p16(-11, 4), p16(-1, 0)};
     uint32_t XB[UW][UJ], XC[UW][UJ];
@@ -279,7 +300,7 @@ __device__ __forceinline__ void half_side(uint32_t (&v)[UH + 8][UW / 4 + 2], con
       }
       int v2[UH + 1];
 #pragma unroll
-      for (int i = 0; i <= UH; i++) {
+      for (int i = (sel == 2 ? 1 : 0); i <= (sel == 1 ? UH - 1 : UH); i++) {
         int acc = 2048;
         if ((i & 1) == 0) {
 #pragma unroll
@@ -292,25 +313,39 @@ __device__ __forceinline__ void half_side(uint32_t (&v)[UH + 8][UW / 4 + 2], con
       }
 #pragma unroll
       for (int jj = 0; jj < UJ; jj++) {
-        XB[x][jj] = pk_sub(K[x][jj], pack2(v2[2 * jj], v2[2 * jj + 1]));
-        XC[x][jj] = pk_sub(K[x][jj], pack2(v2[2 * jj + 1], v2[2 * jj + 2]));
+        if (sel & 1) XB[x][jj] = pk_sub(K[x][jj], pack2(v2[2 * jj], v2[2 * jj + 1]));
+        if (sel & 2) XC[x][jj] = pk_sub(K[x][jj], pack2(v2[2 * jj + 1], v2[2 * jj + 2]));
       }
       __builtin_amdgcn_sched_barrier(0);   // one column at a time (register pressure)
     }
-    d[1] = unit_dist<UW, UH, T>(XB, had);
-    d[2] = unit_dist<UW, UH, T>(XC, had);
-  }
+    if (sel & 1) d[1] = unit_dist<UW, UH, T>(XB, had);
+    if (sel & 2) d[2] = unit_dist<UW, UH, T>(XC, had);
+  };
+#if FME_LANE_HPAIR == 2
+  dpass(std::integral_constant<int, 3>{});
+#else
+  dpass(std::integral_constant<int, 1>{});
+  dpass(std::integral_constant<int, 2>{});
+#endif
 }
 
 // Quarter passes: pass PS covers column phase k = QP_K[PS] (dqx = k-1) and one or two row
 // phases l (dqy = l-1); candidate (k1, l1) is the half best.  A phase with fraction 0 filters
 // with {0,0,0,64,0,0,0,0}, which equals HM's copy / 1-D paths after rounding.
+#if FME_LANE_QPAIR == 2
+constexpr int kQPasses = 5;
 __host__ __device__ constexpr int qp_k(int ps) { return ps < 2 ? 0 : (ps == 2 ? 1 : 2); }
 __host__ __device__ constexpr int qp_l0(int ps) { return (ps == 1 || ps == 4) ? 2 : 0; }
 __host__ __device__ constexpr int qp_l1(int ps) { return ps == 0 ? 1 : (ps == 2 ? 2 : (ps == 3 ? 1 : -1)); }
+#else
+constexpr int kQPasses = 8;   // (k,l) for k, l in 0..2 without (1,1)
+__host__ __device__ constexpr int qp_k(int ps) { return (ps + (ps >= 4 ? 1 : 0)) / 3; }
+__host__ __device__ constexpr int qp_l0(int ps) { return (ps + (ps >= 4 ? 1 : 0)) % 3; }
+__host__ __device__ constexpr int qp_l1(int ps) { return -1; }
+#endif
 // Q9 index of pass ps's first / second candidate
 __host__ __device__ constexpr int qp_idx0(int ps) { return q9_index(qp_k(ps) - 1, qp_l0(ps) - 1); }
-__host__ __device__ constexpr int qp_idx1(int ps) { return q9_index(qp_k(ps) - 1, qp_l1(ps) - 1); }
+__host__ __device__ constexpr int qp_idx1(int ps) { return qp_l1(ps) < 0 ? -1 : q9_index(qp_k(ps) - 1, qp_l1(ps) - 1); }
 
 template <int UW, int UH, int T, int PS>
 __device__ __forceinline__ void qtr_pass(uint32_t (&v)[UH + 8][UW / 4 + 2], const uint32_t (&K)[UW][UH / 2],
@@ -361,6 +396,20 @@ __device__ __forceinline__ void qtr_pass(uint32_t (&v)[UH + 8][UW / 4 + 2], cons
   }
   d[0] = unit_dist<UW, UH, T>(XQ[0], had);
   d[1] = NP > 1 ? unit_dist<UW, UH, T>(XQ[NP - 1], had) : 0u;
+}
+
+template <int L, int UW, int UH, int T, int... PS>
+__device__ __forceinline__ void qtr_all(uint32_t (&v)[UH + 8][UW / 4 + 2], const uint32_t (&K)[UW][UH / 2],
+                                        bool had, int hx, int hy, double ml, int mvx, int mvy, int px, int py,
+                                        uint32_t& best, int& bi, std::integer_sequence<int, PS...>) {
+  auto one = [&](auto ps_c) {
+    constexpr int ps = decltype(ps_c)::value;
+    uint32_t d[2];
+    qtr_pass<UW, UH, T, ps>(v, K, had, hx, hy, d);
+    take_qtr<L>(qp_idx0(ps), d[0], ml, mvx, mvy, hx, hy, px, py, best, bi);
+    if constexpr (qp_l1(ps) >= 0) take_qtr<L>(qp_idx1(ps), d[1], ml, mvx, mvy, hx, hy, px, py, best, bi);
+  };
+  (one(std::integral_constant<int, PS>{}), ...);
 }
 
 typedef uint32_t u32x4a __attribute__((ext_vector_type(4), aligned(4)));
@@ -657,20 +706,8 @@ __device__ __forceinline__ void lane_unit(const BatchArgs& a, const fme_job* __r
   uint32_t qbest = hbest;
   int qbi = 0;
   if (!(FME_LANE_SKIP & 1)) {
-    uint32_t d[2];
-    qtr_pass<UW, UH, T, 0>(v, K, had, hx, hy, d);
-    take_qtr<L>(qp_idx0(0), d[0], ml, mvx, mvy, hx, hy, mvp_x, mvp_y, qbest, qbi);
-    take_qtr<L>(qp_idx1(0), d[1], ml, mvx, mvy, hx, hy, mvp_x, mvp_y, qbest, qbi);
-    qtr_pass<UW, UH, T, 1>(v, K, had, hx, hy, d);
-    take_qtr<L>(qp_idx0(1), d[0], ml, mvx, mvy, hx, hy, mvp_x, mvp_y, qbest, qbi);
-    qtr_pass<UW, UH, T, 2>(v, K, had, hx, hy, d);
-    take_qtr<L>(qp_idx0(2), d[0], ml, mvx, mvy, hx, hy, mvp_x, mvp_y, qbest, qbi);
-    take_qtr<L>(qp_idx1(2), d[1], ml, mvx, mvy, hx, hy, mvp_x, mvp_y, qbest, qbi);
-    qtr_pass<UW, UH, T, 3>(v, K, had, hx, hy, d);
-    take_qtr<L>(qp_idx0(3), d[0], ml, mvx, mvy, hx, hy, mvp_x, mvp_y, qbest, qbi);
-    take_qtr<L>(qp_idx1(3), d[1], ml, mvx, mvy, hx, hy, mvp_x, mvp_y, qbest, qbi);
-    qtr_pass<UW, UH, T, 4>(v, K, had, hx, hy, d);
-    take_qtr<L>(qp_idx0(4), d[0], ml, mvx, mvy, hx, hy, mvp_x, mvp_y, qbest, qbi);
+    qtr_all<L, UW, UH, T>(v, K, had, hx, hy, ml, mvx, mvy, mvp_x, mvp_y, qbest, qbi,
+                          std::make_integer_sequence<int, kQPasses>{});
   }
   const int bq = qbi;
 
