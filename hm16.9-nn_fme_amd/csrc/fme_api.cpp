@@ -79,7 +79,7 @@ struct fme_ctx {
   DevBuf<double> d_mlambda;
   DevBuf<int16_t> d_keys;
   size_t n_keys = 0;
-  DevBuf<float> d_nn;
+  DevBuf<float> d_nn;         // packed layout (nn_pack, kNnPkFloats)
   bool nn_loaded = false;
 
   DevBuf<fme_job> d_jobs;      // staging for fme_refine (host arrays)
@@ -171,7 +171,7 @@ int fme_create(int device, const fme_config* cfg, fme_ctx** out_ctx) {
   c->cfg = *cfg;
   HIP_TRY(c->d_pics.reserve(FME_MAX_PICTURES));
   HIP_TRY(c->d_mlambda.reserve(FME_MAX_LAMBDAS));
-  HIP_TRY(c->d_nn.reserve(FME_NN_PARAMS));
+  HIP_TRY(c->d_nn.reserve(kNnPkFloats));
   HIP_TRY(c->counts.reserve(2 * kNumClasses + 1));
   HIP_TRY(c->nn_state.reserve(24));
   HIP_TRY(hipMemset(c->nn_state.p, 0, 24 * sizeof(uint32_t)));
@@ -288,7 +288,9 @@ int fme_load_nn_weights(fme_ctx* c, const float* params, int count) {
   if (!c || !params) return fail(FME_E_INVALID, "fme_load_nn_weights: null argument");
   if (count != FME_NN_PARAMS) return fail(FME_E_INVALID, "fme_load_nn_weights: %d params, expected %d", count, FME_NN_PARAMS);
   HIP_TRY(hipSetDevice(c->device));
-  HIP_TRY(hipMemcpy(c->d_nn.p, params, FME_NN_PARAMS * sizeof(float), hipMemcpyHostToDevice));
+  std::vector<float> packed(kNnPkFloats);
+  nn_pack(params, packed.data());
+  HIP_TRY(hipMemcpy(c->d_nn.p, packed.data(), kNnPkFloats * sizeof(float), hipMemcpyHostToDevice));
   c->nn_loaded = true;
   return FME_OK;
 }

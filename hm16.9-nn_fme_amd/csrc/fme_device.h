@@ -78,6 +78,27 @@ hipError_t launch_search_small(const BatchArgs& a, const WorkBufs& w, const Sche
 int lane_lanes_per_pu(int cls);                    // 0: not a lane-kernel class
 int lane_kernel_of(int cls);                       // kSearchLane48/84/88, -1: not a lane class
 int lane_blocks_for(int cls, int cnt);
+// Packed NN layout for the tail kernel (nn_pack, fme_kernels.hip): offsets in floats, every
+// pair region 8-byte aligned.
+constexpr int kNnPkPfx = 0;                       // [64 shapes][22] layer-1 prefix (k = 0..7)
+constexpr int kNnPkW1 = kNnPkPfx + 64 * 22;       // [11 row pairs][9 k][2]   (k = 8..16)
+constexpr int kNnPkW2 = kNnPkW1 + 11 * 9 * 2;     // [10][22][2]
+constexpr int kNnPkW3 = kNnPkW2 + 10 * 22 * 2;    // [25][20][2] (row 49 zero)
+constexpr int kNnPkB1 = kNnPkW3 + 25 * 20 * 2;    // 22
+constexpr int kNnPkG1 = kNnPkB1 + 22;
+constexpr int kNnPkBE1 = kNnPkG1 + 22;
+constexpr int kNnPkB2 = kNnPkBE1 + 22;            // 20
+constexpr int kNnPkG2 = kNnPkB2 + 20;
+constexpr int kNnPkBE2 = kNnPkG2 + 20;
+constexpr int kNnPkBout = kNnPkBE2 + 20;          // 50 (row 49 zero)
+constexpr int kNnPkGin = kNnPkBout + 50;          // 9 each
+constexpr int kNnPkMean = kNnPkGin + 9;
+constexpr int kNnPkStd = kNnPkMean + 9;
+constexpr int kNnPkFloats = kNnPkStd + 9 + 1;
+static_assert(kNnPkW1 % 2 == 0 && kNnPkW2 % 2 == 0 && kNnPkW3 % 2 == 0 && kNnPkB1 % 2 == 0 &&
+              kNnPkG1 % 2 == 0 && kNnPkBE1 % 2 == 0 && kNnPkB2 % 2 == 0 && kNnPkG2 % 2 == 0 &&
+              kNnPkBE2 % 2 == 0 && kNnPkBout % 2 == 0, "pair regions must be 8-byte aligned");
+void nn_pack(const float* params, float* packed);   // FME_NN_PARAMS floats -> kNnPkFloats
 hipError_t launch_nn_tail(const BatchArgs& a, const WorkBufs& w, const float* nn_params,
                           int state_in, hipStream_t s);
 

@@ -207,54 +207,108 @@ __device__ __forceinline__ int emb_row_w(int w) {
   return w == 4 ? 1 : w == 8 ? 2 : w == 12 ? 3 : w == 16 ? 4 : w == 24 ? 5 : w == 32 ? 6 : w == 64 ? 7 : 0;
 }
 
-__device__ __forceinline__ int nn_forward(const float* __restrict__ P, const uint32_t (&e)[8], uint32_t c, int pu_h,
-                          int pu_w) {
-  float in[17], x1[22], x2[20];
-  const int rh = emb_row_h(pu_h), rw = emb_row_w(pu_w);
-#pragma unroll
-  for (int k = 0; k < 4; k++) {
-    in[k] = P[P_EMB0 + rh * 4 + k];
-    in[4 + k] = P[P_EMB1 + rw * 4 + k];
+// Device layout of the net for the tail (built once per weight load by nn_pack, fme_device.h
+// kNnPk*): rows paired for packed f32 math (row r in .x, row r+1 in .y, so both halves run
+// the reference's sequential k order), and the 8 embedding terms of layer 1 folded into a
+// per-PU-shape prefix: the partial sums after k = 0..7 depend only on (PUHeight, PUWidth).
+typedef float f2 __attribute__((ext_vector_type(2)));
+
+void nn_pack(const float* P, float* Q) {
+  for (int i = 0; i < kNnPkFloats; i++) Q[i] = 0.0f;
+  for (int rh = 0; rh < 8; rh++)
+    for (int rw = 0; rw < 8; rw++)
+      for (int r = 0; r < 22; r++) {
+        float s = 0.0f;   // TEncSearch.cpp:120 row r, terms k = 0..7 (embeddings), in order
+        for (int k = 0; k < 4; k++) s = s + P[P_W1 + r * 17 + k] * P[P_EMB0 + rh * 4 + k];
+        for (int k = 0; k < 4; k++) s = s + P[P_W1 + r * 17 + 4 + k] * P[P_EMB1 + rw * 4 + k];
+        Q[kNnPkPfx + (rh * 8 + rw) * 22 + r] = s;
+      }
+  for (int r = 0; r < 22; r++)
+    for (int k = 0; k < 9; k++) Q[kNnPkW1 + ((r / 2) * 9 + k) * 2 + (r & 1)] = P[P_W1 + r * 17 + 8 + k];
+  for (int r = 0; r < 20; r++)
+    for (int k = 0; k < 22; k++) Q[kNnPkW2 + ((r / 2) * 22 + k) * 2 + (r & 1)] = P[P_W2 + r * 22 + k];
+  for (int r = 0; r < 49; r++)
+    for (int k = 0; k < 20; k++) Q[kNnPkW3 + ((r / 2) * 20 + k) * 2 + (r & 1)] = P[P_W3 + r * 20 + k];
+  for (int r = 0; r < 22; r++) {
+    Q[kNnPkB1 + r] = P[P_B1 + r];
+    Q[kNnPkG1 + r] = P[P_G1 + r];
+    Q[kNnPkBE1 + r] = P[P_BE1 + r];
   }
+  for (int r = 0; r < 20; r++) {
+    Q[kNnPkB2 + r] = P[P_B2 + r];
+    Q[kNnPkG2 + r] = P[P_G2 + r];
+    Q[kNnPkBE2 + r] = P[P_BE2 + r];
+  }
+  for (int r = 0; r < 49; r++) Q[kNnPkBout + r] = P[P_BOUT + r];
+  for (int k = 0; k < 9; k++) {
+    Q[kNnPkGin + k] = P[P_GIN + k];
+    Q[kNnPkMean + k] = P[P_MEAN + k];
+    Q[kNnPkStd + k] = P[P_STD + k];
+  }
+}
+
+__device__ __forceinline__ f2 ld2(const float* __restrict__ Q, int o) { return *(const f2*)(Q + o); }
+__device__ __forceinline__ f2 relu2(f2 s) {
+  s.x = s.x < 0.0f ? 0.0f : s.x;
+  s.y = s.y < 0.0f ? 0.0f : s.y;
+  return s;
+}
+
+// NN_pred() (TEncSearch.cpp:85-134) on the packed layout: float32, every dot product summed in
+// k order without contraction (the sequential-k contract), BN as x*g + b.  The
+// weights are wave-uniform, so they stream through the scalar cache into SGPR operands.
+__device__ __forceinline__ int nn_forward(const float* __restrict__ Q, const uint32_t (&e)[8], uint32_t c, int pu_h,
+                                          int pu_w) {
+  const int t = emb_row_h(pu_h) * 8 + emb_row_w(pu_w);
+  float in[9];
   const uint32_t raw[9] = {e[0], e[1], e[2], e[3], c, e[4], e[5], e[6], e[7]};
 #pragma unroll
   for (int k = 0; k < 9; k++) {
     float v = (float)raw[k];
-    v = (v - P[P_MEAN + k]) / P[P_STD + k];
-    in[8 + k] = v * P[P_GIN + k];
+    v = (v - Q[kNnPkMean + k]) / Q[kNnPkStd + k];
+    in[k] = v * Q[kNnPkGin + k];
   }
+  const float* pfx = Q + kNnPkPfx + t * 22;
+  f2 x1[11];
 #pragma unroll
-  for (int r = 0; r < 22; r++) {
-    float s = 0.0f;
+  for (int rp = 0; rp < 11; rp++) {
+    f2 s = {pfx[2 * rp], pfx[2 * rp + 1]};
 #pragma unroll
-    for (int k = 0; k < 17; k++) s = s + P[P_W1 + r * 17 + k] * in[k];
-    s = s + P[P_B1 + r];
-    s = s < 0.0f ? 0.0f : s;
-    x1[r] = s * P[P_G1 + r] + P[P_BE1 + r];
-    __builtin_amdgcn_sched_barrier(0);   // keep the weight reads of one row together
+    for (int k = 0; k < 9; k++) s = s + ld2(Q, kNnPkW1 + (rp * 9 + k) * 2) * (f2){in[k], in[k]};
+    s = relu2(s + ld2(Q, kNnPkB1 + 2 * rp));
+    x1[rp] = s * ld2(Q, kNnPkG1 + 2 * rp) + ld2(Q, kNnPkBE1 + 2 * rp);
   }
+  f2 x2[10];
 #pragma unroll
-  for (int r = 0; r < 20; r++) {
-    float s = 0.0f;
+  for (int rp = 0; rp < 10; rp++) {
+    f2 s = {0.0f, 0.0f};
 #pragma unroll
-    for (int k = 0; k < 22; k++) s = s + P[P_W2 + r * 22 + k] * x1[k];
-    s = s + P[P_B2 + r];
-    s = s < 0.0f ? 0.0f : s;
-    x2[r] = s * P[P_G2 + r] + P[P_BE2 + r];
-    __builtin_amdgcn_sched_barrier(0);
+    for (int k = 0; k < 22; k++) {
+      const float xk = (k & 1) ? x1[k / 2].y : x1[k / 2].x;
+      s = s + ld2(Q, kNnPkW2 + (rp * 22 + k) * 2) * (f2){xk, xk};
+    }
+    s = relu2(s + ld2(Q, kNnPkB2 + 2 * rp));
+    x2[rp] = s * ld2(Q, kNnPkG2 + 2 * rp) + ld2(Q, kNnPkBE2 + 2 * rp);
   }
   int best = 0;
   float bv = 0.0f;
-#pragma unroll 1
-  for (int r = 0; r < 49; r++) {
-    const float* wr = P + P_W3 + r * 20;
-    float s = 0.0f;
+#pragma unroll 1   // the weights of one row pair per iteration (scalar loads, few SGPRs)
+  for (int rp = 0; rp < 25; rp++) {
+    f2 s = {0.0f, 0.0f};
 #pragma unroll
-    for (int k = 0; k < 20; k++) s = s + wr[k] * x2[k];
-    s = s + P[P_BOUT + r];
-    if (r == 0 || s > bv) {  // Eigen maxCoeff: first index of the maximum
-      bv = s;
-      best = r;
+    for (int k = 0; k < 20; k++) {
+      const float xk = (k & 1) ? x2[k / 2].y : x2[k / 2].x;
+      s = s + ld2(Q, kNnPkW3 + (rp * 20 + k) * 2) * (f2){xk, xk};
+    }
+    s = s + ld2(Q, kNnPkBout + 2 * rp);
+    // Eigen maxCoeff: first index of the maximum (strict >), rows in order
+    if (rp == 0 || s.x > bv) {
+      bv = s.x;
+      best = 2 * rp;
+    }
+    if (rp < 24 && s.y > bv) {
+      bv = s.y;
+      best = 2 * rp + 1;
     }
   }
   return best;
@@ -266,10 +320,6 @@ constexpr int kTailNT = kJobsPerScanBlock;
 __global__ __launch_bounds__(kTailNT) void k_nn_tail(BatchArgs a, WorkBufs w,
                                                      const float* __restrict__ nnp_g, int state_in) {
   __shared__ int32_t wave_tot[kTailNT / 64][9];
-  // weights in LDS: every lane reads the same address (broadcast), no scalar-register pressure
-  __shared__ __attribute__((aligned(16))) float nnp[FME_NN_PARAMS + 4];
-  if (a.nn_mode)
-    for (int i = threadIdx.x; i < FME_NN_PARAMS; i += kTailNT) nnp[i] = nnp_g[i];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int i = blockIdx.x * kJobsPerScanBlock + tid;
   const bool valid = i < a.n;
@@ -337,7 +387,7 @@ __global__ __launch_bounds__(kTailNT) void k_nn_tail(BatchArgs a, WorkBufs w,
       ph = st_in[9];
       pw = st_in[10];
     }
-    const int cls = nn_forward(nnp, e, c, (int)ph, (int)pw);
+    const int cls = nn_forward(nnp_g, e, c, (int)ph, (int)pw);
     r->nn_class = (uint8_t)cls;
     if (!(j.flags & FME_JOB_EMI) || r->n_emi < 8) status |= FME_RES_NN_STALE;
     if ((written & 0x1FFu) != 0x1FFu) status |= FME_RES_NN_UNINIT;

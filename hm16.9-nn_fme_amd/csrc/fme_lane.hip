@@ -61,10 +61,23 @@ using namespace simd;
 constexpr int kLaneNT = 256;
 
 // ---- small helpers -------------------------------------------------------------------------
+template <int CTRL>
+__device__ __forceinline__ uint32_t dpp(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, CTRL, 0xF, 0xF, true);
+}
+// Sum over the L lanes of a PU's group (L a power of two <= 64): every lane of the group ends
+// with the total.  Offsets 1, 2 swap within a quad (DPP quad_perm); once each quad / octet
+// holds its sum, the half-mirror / mirror partner of a lane (DPP row_half_mirror / row_mirror,
+// lane i <-> 7-i / 15-i) lies in the other quad / octet; 16 is a ds_swizzle xor, 32 a
+// bpermute.  (A/B on the 1080p batch: -1 % search time against bpermute for every step.)
 template <int L>
 __device__ __forceinline__ uint32_t group_sum(uint32_t v) {
-#pragma unroll
-  for (int o = L / 2; o >= 1; o >>= 1) v += (uint32_t)__shfl_xor((int)v, o, 64);
+  if (L >= 2) v += dpp<0xB1>(v);
+  if (L >= 4) v += dpp<0x4E>(v);
+  if (L >= 8) v += dpp<0x141>(v);
+  if (L >= 16) v += dpp<0x140>(v);
+  if (L >= 32) v += (uint32_t)__builtin_amdgcn_ds_swizzle((int)v, 0x401F);
+  if (L >= 64) v += (uint32_t)__shfl_xor((int)v, 32, 64);
   return v;
 }
 
