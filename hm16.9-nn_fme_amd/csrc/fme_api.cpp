@@ -94,6 +94,15 @@ struct fme_ctx {
   int state_cur = 0;
   int32_t* h_counts = nullptr; // pinned
 
+  // motion compensation: owned chroma planes (cb then cr, one allocation per slot), staging
+  uint8_t* chroma_owned[FME_MAX_PICTURES]{};
+  size_t chroma_bytes[FME_MAX_PICTURES]{};
+  DevBuf<fme_mc_job> d_mc_jobs;
+  DevBuf<uint8_t> d_mc_planes;
+  DevBuf<int32_t> d_mc_invalid;
+  hipEvent_t ev_mc[2] = {nullptr, nullptr};
+  bool mc_timed = false;
+
   std::unique_ptr<fme_ctx> single;  // private context for the single-PU entry points
   DevBuf<uint8_t> single_pic;
   DevBuf<fme_job> single_job;
@@ -199,6 +208,11 @@ int fme_destroy(fme_ctx* c) {
   (void)hipDeviceSynchronize();
   for (int i = 0; i < FME_MAX_PICTURES; i++)
     if (c->pic_owned[i] && c->pics[i].luma) (void)hipFree(const_cast<uint8_t*>(c->pics[i].luma));
+  for (int i = 0; i < FME_MAX_PICTURES; i++)
+    if (c->chroma_owned[i]) (void)hipFree(c->chroma_owned[i]);
+  c->d_mc_jobs.release(); c->d_mc_planes.release(); c->d_mc_invalid.release();
+  for (auto& e : c->ev_mc)
+    if (e) (void)hipEventDestroy(e);
   c->d_pics.release(); c->d_mlambda.release(); c->d_keys.release(); c->d_nn.release();
   c->d_jobs.release(); c->d_res.release(); c->cls.release(); c->perm.release(); c->sjobs.release();
   c->counts.release(); c->blk_agg.release(); c->blk_prefix.release(); c->nn_state.release();
@@ -214,6 +228,17 @@ int fme_destroy(fme_ctx* c) {
   if (c->single) fme_destroy(c->single.release());
   delete c;
   return FME_OK;
+}
+
+// A new luma plane with other dimensions invalidates the slot's chroma planes.
+static void keep_chroma(fme_ctx* c, int id, int width, int height) {
+  const PicDesc& o = c->pics[id];
+  if (o.luma && o.width == width && o.height == height) return;
+  if (c->chroma_owned[id]) (void)hipFree(c->chroma_owned[id]);
+  c->chroma_owned[id] = nullptr;
+  c->chroma_bytes[id] = 0;
+  c->pics[id].cb = c->pics[id].cr = nullptr;
+  c->pics[id].cstride = 0;
 }
 
 int fme_set_picture(fme_ctx* c, int id, const uint8_t* luma, int stride, int width, int height, void* stream) {
@@ -233,7 +258,8 @@ int fme_set_picture(fme_ctx* c, int id, const uint8_t* luma, int stride, int wid
   hipStream_t s = static_cast<hipStream_t>(stream);
   HIP_TRY(hipMemcpy2DAsync(dst, width, luma, stride, width, height, hipMemcpyHostToDevice, s));
   HIP_TRY(hipStreamSynchronize(s));  // the caller may free its host plane on return
-  c->pics[id] = PicDesc{dst, width, width, height};
+  keep_chroma(c, id, width, height);
+  c->pics[id] = PicDesc{dst, width, width, height, c->pics[id].cb, c->pics[id].cr, c->pics[id].cstride, 0};
   c->pic_owned[id] = true;
   c->tables_dirty = true;
   return FME_OK;
@@ -247,7 +273,51 @@ int fme_bind_picture_device(fme_ctx* c, int id, const uint8_t* d_luma, int strid
   if (c->pic_owned[id] && c->pics[id].luma) HIP_TRY(hipFree(const_cast<uint8_t*>(c->pics[id].luma)));
   c->pic_owned[id] = false;
   c->pic_bytes[id] = 0;
-  c->pics[id] = PicDesc{d_luma, stride, width, height};
+  keep_chroma(c, id, width, height);
+  c->pics[id] = PicDesc{d_luma, stride, width, height, c->pics[id].cb, c->pics[id].cr, c->pics[id].cstride, 0};
+  c->tables_dirty = true;
+  return FME_OK;
+}
+
+int fme_set_picture_chroma(fme_ctx* c, int id, const uint8_t* cb, const uint8_t* cr, int stride, void* stream) {
+  if (!c || !cb || !cr) return fail(FME_E_INVALID, "fme_set_picture_chroma: null argument");
+  if (id < 0 || id >= FME_MAX_PICTURES) return fail(FME_E_INVALID, "fme_set_picture_chroma: id %d", id);
+  if (!c->pics[id].luma) return fail(FME_E_STATE, "fme_set_picture_chroma: picture %d has no luma plane", id);
+  const int cw = c->pics[id].width >> 1, ch = c->pics[id].height >> 1;
+  if (stride < cw) return fail(FME_E_INVALID, "fme_set_picture_chroma: stride %d < %d", stride, cw);
+  HIP_TRY(hipSetDevice(c->device));
+  const size_t bytes = 2 * (size_t)cw * ch;
+  if (!c->chroma_owned[id] || c->chroma_bytes[id] < bytes) {
+    if (c->chroma_owned[id]) HIP_TRY(hipFree(c->chroma_owned[id]));
+    c->chroma_owned[id] = nullptr;
+    HIP_TRY(hipMalloc(reinterpret_cast<void**>(&c->chroma_owned[id]), bytes));
+    c->chroma_bytes[id] = bytes;
+  }
+  uint8_t* dcb = c->chroma_owned[id];
+  uint8_t* dcr = dcb + (size_t)cw * ch;
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  HIP_TRY(hipMemcpy2DAsync(dcb, cw, cb, stride, cw, ch, hipMemcpyHostToDevice, s));
+  HIP_TRY(hipMemcpy2DAsync(dcr, cw, cr, stride, cw, ch, hipMemcpyHostToDevice, s));
+  HIP_TRY(hipStreamSynchronize(s));
+  c->pics[id].cb = dcb;
+  c->pics[id].cr = dcr;
+  c->pics[id].cstride = cw;
+  c->tables_dirty = true;
+  return FME_OK;
+}
+
+int fme_bind_picture_chroma_device(fme_ctx* c, int id, const uint8_t* d_cb, const uint8_t* d_cr, int stride) {
+  if (!c || !d_cb || !d_cr) return fail(FME_E_INVALID, "fme_bind_picture_chroma_device: null argument");
+  if (id < 0 || id >= FME_MAX_PICTURES) return fail(FME_E_INVALID, "fme_bind_picture_chroma_device: id %d", id);
+  if (!c->pics[id].luma) return fail(FME_E_STATE, "fme_bind_picture_chroma_device: picture %d has no luma plane", id);
+  if (stride < (c->pics[id].width >> 1)) return fail(FME_E_INVALID, "fme_bind_picture_chroma_device: stride %d", stride);
+  HIP_TRY(hipSetDevice(c->device));
+  if (c->chroma_owned[id]) HIP_TRY(hipFree(c->chroma_owned[id]));
+  c->chroma_owned[id] = nullptr;
+  c->chroma_bytes[id] = 0;
+  c->pics[id].cb = d_cb;
+  c->pics[id].cr = d_cr;
+  c->pics[id].cstride = stride;
   c->tables_dirty = true;
   return FME_OK;
 }
@@ -567,6 +637,113 @@ int fme_search_kernel_of_shape(int width, int height) {
       return kern == kSearchCoop ? 0 : 1;
     }
   return -1;
+}
+
+// ---- motion compensation ---------------------------------------------------------------------
+static const char* mc_job_problem(const fme_ctx* c, const fme_mc_job& j, int width, int height) {
+  if (j.w < 4 || j.h < 4 || j.w > 64 || j.h > 64 || (j.w & 3) || (j.h & 3)) return "PU size";
+  if (!(j.flags & (FME_MC_L0 | FME_MC_L1)) || (j.flags & ~(FME_MC_L0 | FME_MC_L1))) return "list flags";
+  if ((int)j.x + j.w > width || (int)j.y + j.h > height) return "PU outside the picture";
+  for (int l = 0; l < 2; l++) {
+    if (!(j.flags & (1u << l))) continue;
+    if (j.ref_id[l] >= FME_MAX_PICTURES) return "reference id";
+    const PicDesc& p = c->pics[j.ref_id[l]];
+    if (!p.luma || !p.cb || !p.cr) return "reference picture without luma + chroma";
+    if (p.width != width || p.height != height) return "reference picture dimensions";
+  }
+  return nullptr;
+}
+
+static int mc_launch(fme_ctx* c, const fme_mc_job* d_jobs, int n, uint8_t* y, int ys, uint8_t* cb, uint8_t* cr,
+                     int cs, int width, int height, hipStream_t s) {
+  HIP_TRY(c->d_mc_invalid.reserve(1));
+  HIP_TRY(hipMemsetAsync(c->d_mc_invalid.p, 0, sizeof(int32_t), s));
+  if (int e = sync_tables(c, s)) return e;
+  McArgs a{};
+  a.jobs = d_jobs;
+  a.pics = c->d_pics.p;
+  a.y = y;
+  a.cb = cb;
+  a.cr = cr;
+  a.invalid = c->d_mc_invalid.p;
+  a.n = n;
+  a.y_stride = ys;
+  a.c_stride = cs;
+  a.width = width;
+  a.height = height;
+  if (c->profiling) {
+    if (!c->ev_mc[0]) {
+      HIP_TRY(hipEventCreate(&c->ev_mc[0]));
+      HIP_TRY(hipEventCreate(&c->ev_mc[1]));
+    }
+    HIP_TRY(hipEventRecord(c->ev_mc[0], s));
+  }
+  HIP_TRY(launch_mc(a, s));
+  if (c->profiling) HIP_TRY(hipEventRecord(c->ev_mc[1], s));
+  c->mc_timed = c->profiling;
+  return FME_OK;
+}
+
+static int mc_check_planes(const void* y, int ys, const void* cb, const void* cr, int cs, int width, int height) {
+  if (!y || !cb || !cr) return fail(FME_E_INVALID, "motion compensation: null plane");
+  if (width <= 0 || height <= 0 || (width & 1) || (height & 1) || ys < width || cs < width / 2)
+    return fail(FME_E_INVALID, "motion compensation: geometry %dx%d strides %d/%d", width, height, ys, cs);
+  return FME_OK;
+}
+
+int fme_motion_compensate(fme_ctx* c, const fme_mc_job* jobs, int n, uint8_t* y, int ys, uint8_t* cb, uint8_t* cr,
+                          int cs, int width, int height, void* stream) {
+  if (!c || (n > 0 && !jobs) || n < 0) return fail(FME_E_INVALID, "fme_motion_compensate: bad argument");
+  if (int e = mc_check_planes(y, ys, cb, cr, cs, width, height)) return e;
+  for (int i = 0; i < n; i++)
+    if (const char* why = mc_job_problem(c, jobs[i], width, height))
+      return fail(FME_E_INVALID, "fme_motion_compensate: job %d: %s", i, why);
+  if (n == 0) return FME_OK;
+  HIP_TRY(hipSetDevice(c->device));
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  const size_t ly = (size_t)width * height, lc = ly / 4;
+  HIP_TRY(c->d_mc_jobs.reserve(n));
+  HIP_TRY(c->d_mc_planes.reserve(ly + 2 * lc));
+  uint8_t* dy = c->d_mc_planes.p;
+  uint8_t* dcb = dy + ly;
+  uint8_t* dcr = dcb + lc;
+  const int cw = width / 2, ch = height / 2;
+  HIP_TRY(hipMemcpyAsync(c->d_mc_jobs.p, jobs, n * sizeof(fme_mc_job), hipMemcpyHostToDevice, s));
+  HIP_TRY(hipMemcpy2DAsync(dy, width, y, ys, width, height, hipMemcpyHostToDevice, s));
+  HIP_TRY(hipMemcpy2DAsync(dcb, cw, cb, cs, cw, ch, hipMemcpyHostToDevice, s));
+  HIP_TRY(hipMemcpy2DAsync(dcr, cw, cr, cs, cw, ch, hipMemcpyHostToDevice, s));
+  if (int e = mc_launch(c, c->d_mc_jobs.p, n, dy, width, dcb, dcr, cw, width, height, s)) return e;
+  HIP_TRY(hipMemcpy2DAsync(y, ys, dy, width, width, height, hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipMemcpy2DAsync(cb, cs, dcb, cw, cw, ch, hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipMemcpy2DAsync(cr, cs, dcr, cw, cw, ch, hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipStreamSynchronize(s));
+  return FME_OK;
+}
+
+int fme_motion_compensate_device(fme_ctx* c, const fme_mc_job* d_jobs, int n, uint8_t* d_y, int ys, uint8_t* d_cb,
+                                 uint8_t* d_cr, int cs, int width, int height, void* stream) {
+  if (!c || (n > 0 && !d_jobs) || n < 0) return fail(FME_E_INVALID, "fme_motion_compensate_device: bad argument");
+  if (int e = mc_check_planes(d_y, ys, d_cb, d_cr, cs, width, height)) return e;
+  HIP_TRY(hipSetDevice(c->device));
+  return mc_launch(c, d_jobs, n, d_y, ys, d_cb, d_cr, cs, width, height, static_cast<hipStream_t>(stream));
+}
+
+int fme_mc_invalid_count(fme_ctx* c) {
+  if (!c) return fail(FME_E_INVALID, "fme_mc_invalid_count: null ctx");
+  if (!c->d_mc_invalid.p) return 0;
+  HIP_TRY(hipSetDevice(c->device));
+  int32_t v = 0;
+  HIP_TRY(hipDeviceSynchronize());
+  HIP_TRY(hipMemcpy(&v, c->d_mc_invalid.p, sizeof(v), hipMemcpyDeviceToHost));
+  return v;
+}
+
+int fme_mc_last_ms(fme_ctx* c, float* ms) {
+  if (!c || !ms) return fail(FME_E_INVALID, "fme_mc_last_ms: null argument");
+  if (!c->mc_timed) return fail(FME_E_STATE, "fme_mc_last_ms: no profiled motion compensation");
+  HIP_TRY(hipEventSynchronize(c->ev_mc[1]));
+  HIP_TRY(hipEventElapsedTime(ms, c->ev_mc[0], c->ev_mc[1]));
+  return FME_OK;
 }
 
 int fme_set_profiling(fme_ctx* c, int enable) {

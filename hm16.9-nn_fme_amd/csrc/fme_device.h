@@ -22,7 +22,23 @@ constexpr int kClassH[kNumClasses] = {8, 4, 8, 16, 4, 16, 8, 16, 12, 16, 32, 8,
 struct PicDesc {
   const uint8_t* luma;
   int32_t stride, width, height;
+  const uint8_t* cb;          // 4:2:0 chroma (motion compensation only); null when unset
+  const uint8_t* cr;
+  int32_t cstride;
+  int32_t pad_;
 };
+
+// One motion-compensation launch (fme_mc.hip).
+struct McArgs {
+  const fme_mc_job* jobs;
+  const PicDesc* pics;
+  uint8_t* y;
+  uint8_t* cb;
+  uint8_t* cr;
+  int32_t* invalid;           // count of skipped jobs
+  int32_t n, y_stride, c_stride, width, height;
+};
+hipError_t launch_mc(const McArgs& a, hipStream_t s);
 
 // One batch as the device sees it.
 struct BatchArgs {

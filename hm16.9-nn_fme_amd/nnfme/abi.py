@@ -33,6 +33,24 @@ RESULT_DTYPE = np.dtype(
 )
 assert RESULT_DTYPE.itemsize == 64
 
+# fme_mc_job (24 B): one PU of motion compensation (include/fme.h)
+MC_JOB_DTYPE = np.dtype(
+    [
+        ("x", "<u2"), ("y", "<u2"),
+        ("w", "u1"), ("h", "u1"),
+        ("flags", "u1"), ("reserved", "u1"),
+        ("ref_id", "u1", (2,)),
+        ("cu_x", "<u2"), ("cu_y", "<u2"),
+        ("mv", "<i2", (2, 2)),
+        ("reserved2", "<u2"),
+    ],
+    align=False,
+)
+assert MC_JOB_DTYPE.itemsize == 24
+
+MC_L0 = 0x01
+MC_L1 = 0x02
+
 CONFIG_FIELDS = ("bit_depth", "use_hadamard", "nn_mode", "qp", "fast_inter_mode", "max_jobs")
 
 JOB_EMI = 0x01

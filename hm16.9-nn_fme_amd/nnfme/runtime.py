@@ -15,7 +15,7 @@ from .weights import load_weights
 PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB_PATH = os.environ.get("FME_LIB_PATH") or os.path.join(PKG_ROOT, "libfme_amd.so")
 
-ABI_VERSION = 2
+ABI_VERSION = 3
 TIMING_NAMES = ("classify", "scatter", "search", "nn_tail", "batch", "search_main", "search_aux")
 
 # Every entry point include/fme.h declares (the ABI test checks the .so exports them).
@@ -25,6 +25,8 @@ ABI_SYMBOLS = (
     "fme_load_nn_weights", "fme_nn_reset_state", "fme_nn_get_state", "fme_nn_set_state", "fme_refine", "fme_refine_device",
     "fme_frac_dif_single", "fme_nn_pred_single", "fme_set_profiling", "fme_last_timings",
     "fme_accumulated_timings", "fme_search_kernel_of_shape", "fme_debug_phase_cycles",
+    "fme_set_picture_chroma", "fme_bind_picture_chroma_device", "fme_motion_compensate",
+    "fme_motion_compensate_device", "fme_mc_invalid_count", "fme_mc_last_ms",
 )
 
 
@@ -75,6 +77,12 @@ def load_library(path=None):
         "fme_accumulated_timings": (I, [P, P, I, I]),
         "fme_search_kernel_of_shape": (I, [I, I]),
         "fme_debug_phase_cycles": (I, [P, I]),
+        "fme_set_picture_chroma": (I, [P, I, P, P, I, P]),
+        "fme_bind_picture_chroma_device": (I, [P, I, P, P, I]),
+        "fme_motion_compensate": (I, [P, P, I, P, I, P, P, I, I, I, P]),
+        "fme_motion_compensate_device": (I, [P, P, I, P, I, P, P, I, I, I, P]),
+        "fme_mc_invalid_count": (I, [P]),
+        "fme_mc_last_ms": (I, [P, P]),
     }
     for name, (res, args) in sig.items():
         f = getattr(lib, name)
@@ -128,6 +136,47 @@ class FmeContext:
 
     def bind_picture_device(self, pid, data_ptr, stride, width, height):
         _check(self.lib, self.lib.fme_bind_picture_device(self.h, pid, C.c_void_p(data_ptr), stride, width, height))
+
+    def set_picture_chroma(self, pid, cb, cr, stream=None):
+        cb = np.ascontiguousarray(cb, dtype=np.uint8)
+        cr = np.ascontiguousarray(cr, dtype=np.uint8)
+        assert cb.shape == cr.shape
+        _check(self.lib, self.lib.fme_set_picture_chroma(self.h, pid, _ptr(cb), _ptr(cr), cb.shape[1], stream))
+
+    def set_picture_yuv(self, pid, y, cb, cr, stream=None):
+        self.set_picture(pid, y, stream)
+        self.set_picture_chroma(pid, cb, cr, stream)
+
+    def bind_picture_chroma_device(self, pid, cb_ptr, cr_ptr, stride):
+        _check(self.lib, self.lib.fme_bind_picture_chroma_device(self.h, pid, C.c_void_p(cb_ptr), C.c_void_p(cr_ptr),
+                                                                 stride))
+
+    # -- motion compensation ----------------------------------------------------------------
+    def motion_compensate(self, mc_jobs, y, cb, cr, stream=None):
+        """Predict every job into the (host) planes y, cb, cr in place (fme_motion_compensate)."""
+        from .abi import MC_JOB_DTYPE
+        jobs = np.ascontiguousarray(mc_jobs, dtype=MC_JOB_DTYPE)
+        for a in (y, cb, cr):
+            assert a.dtype == np.uint8 and a.flags["C_CONTIGUOUS"]
+        h, w = y.shape
+        _check(self.lib, self.lib.fme_motion_compensate(self.h, _ptr(jobs), len(jobs), _ptr(y), y.shape[1], _ptr(cb),
+                                                        _ptr(cr), cb.shape[1], w, h, stream))
+
+    def motion_compensate_device(self, d_jobs, n, d_y, y_stride, d_cb, d_cr, c_stride, width, height, stream=None):
+        _check(self.lib, self.lib.fme_motion_compensate_device(self.h, C.c_void_p(d_jobs), n, C.c_void_p(d_y), y_stride,
+                                                               C.c_void_p(d_cb), C.c_void_p(d_cr), c_stride, width,
+                                                               height, stream))
+
+    def mc_invalid_count(self):
+        rc = self.lib.fme_mc_invalid_count(self.h)
+        if rc < 0:
+            _check(self.lib, rc)
+        return rc
+
+    def mc_last_ms(self):
+        ms = C.c_float()
+        _check(self.lib, self.lib.fme_mc_last_ms(self.h, C.byref(ms)))
+        return ms.value
 
     def set_lambda(self, lid, lam):
         _check(self.lib, self.lib.fme_set_lambda(self.h, lid, float(lam)))

@@ -228,3 +228,73 @@ def lambdas_for_frame(qp, poc):
 def jobs_per_frame(width, height, refs=4, calls_per_ctu=423):
     ctus = ((width + 63) // 64) * ((height + 63) // 64)
     return ctus * calls_per_ctu * refs
+
+
+# ---- motion compensation inputs ---------------------------------
+def synth_chroma(width, height, t, seed=None):
+    """4:2:0 chroma planes (Cb, Cr) of a synthetic frame: the luma generator at half size with
+    its own draws (SURVEY.md §8(d) uses flat 128 chroma; textured planes exercise the 4-tap
+    filter)."""
+    base = SEEDS.get((width, height), 7) if seed is None else seed
+    return (synth_luma(width // 2, height // 2, t, seed=base * 31 + 11),
+            synth_luma(width // 2, height // 2, t, seed=base * 37 + 13))
+
+
+# PU partitions of a CU of size s: PartSize (TComDataCU::getPartIndexAndSize) -> PU rectangles
+def _cu_parts(rng, s, amp):
+    modes = ["2Nx2N", "2NxN", "Nx2N"]
+    if s == 8:
+        modes = ["2Nx2N", "2NxN", "Nx2N"]          # 8x4 / 4x8 (inter NxN is off)
+    elif amp:
+        modes += ["2NxnU", "2NxnD", "nLx2N", "nRx2N"]
+    m = modes[rng.integers(len(modes))]
+    q, h = s // 4, s // 2
+    return {
+        "2Nx2N": [(0, 0, s, s)],
+        "2NxN": [(0, 0, s, h), (0, h, s, h)],
+        "Nx2N": [(0, 0, h, s), (h, 0, h, s)],
+        "2NxnU": [(0, 0, s, q), (0, q, s, s - q)],
+        "2NxnD": [(0, 0, s, s - q), (0, s - q, s, q)],
+        "nLx2N": [(0, 0, q, s), (q, 0, s - q, s)],
+        "nRx2N": [(0, 0, s - q, s), (s - q, 0, q, s)],
+    }[m]
+
+
+def make_mc_partition(rng, width, height, ref_ids, bi_frac=0.0, mv_amp=64, p_split=(0.35, 0.55, 0.6), amp=True,
+                      identical_frac=0.0):
+    """One frame's decided inter PUs for motion compensation: every CTU split into CUs by a random
+    quad-tree (forced where a CU crosses the picture border, as TEncCu does), each CU into PUs by
+    a random PartSize, each PU with quarter-pel MVs U[-4 mv_amp, 4 mv_amp] on 1 or 2 lists.
+    Returns an MC_JOB_DTYPE array that tiles the picture (width, height multiples of 8)."""
+    from .abi import MC_JOB_DTYPE, MC_L0, MC_L1
+    out = []
+
+    def cu(x, y, s, depth):
+        if x >= width or y >= height:
+            return
+        inside = x + s <= width and y + s <= height
+        if s > 8 and (not inside or rng.random() < p_split[min(depth, 2)]):
+            for dy in (0, s // 2):
+                for dx in (0, s // 2):
+                    cu(x + dx, y + dy, s // 2, depth + 1)
+            return
+        for (px, py, pw, ph) in _cu_parts(rng, s, amp):
+            out.append((x + px, y + py, pw, ph, x, y))
+
+    for cy in range(0, height, MAX_CU):
+        for cx in range(0, width, MAX_CU):
+            cu(cx, cy, MAX_CU, 0)
+    n = len(out)
+    jobs = np.zeros(n, dtype=MC_JOB_DTYPE)
+    a = np.array(out, dtype=np.int64)
+    jobs["x"], jobs["y"], jobs["w"], jobs["h"], jobs["cu_x"], jobs["cu_y"] = a.T
+    bi = rng.random(n) < bi_frac
+    one = rng.integers(0, 2, n)   # uni-pred: list 0 or 1
+    jobs["flags"] = np.where(bi, MC_L0 | MC_L1, np.where(one == 0, MC_L0, MC_L1))
+    ids = np.asarray(ref_ids, dtype=np.int64)
+    jobs["ref_id"] = ids[rng.integers(0, len(ids), (n, 2))]
+    jobs["mv"] = rng.integers(-4 * mv_amp, 4 * mv_amp + 1, (n, 2, 2))
+    same = bi & (rng.random(n) < identical_frac)   # xCheckIdenticalMotion cases
+    jobs["ref_id"][same, 1] = jobs["ref_id"][same, 0]
+    jobs["mv"][same, 1] = jobs["mv"][same, 0]
+    return jobs

@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define FME_ABI_VERSION 2
+#define FME_ABI_VERSION 3
 
 /* ---- error codes ---------------------------------------------------------------- */
 #define FME_OK            0
@@ -137,6 +137,14 @@ int fme_set_picture(fme_ctx* ctx, int id, const uint8_t* luma, int stride, int w
 int fme_bind_picture_device(fme_ctx* ctx, int id, const uint8_t* d_luma, int stride, int width,
                             int height);
 
+/* 4:2:0 chroma planes of picture `id` (8-bit, (width/2) x (height/2) of its luma plane, which
+ * must be set first; setting the luma plane again with other dimensions drops them).  Only
+ * motion compensation reads chroma.                                                         */
+int fme_set_picture_chroma(fme_ctx* ctx, int id, const uint8_t* cb, const uint8_t* cr, int stride,
+                           void* stream);
+int fme_bind_picture_chroma_device(fme_ctx* ctx, int id, const uint8_t* d_cb, const uint8_t* d_cr,
+                                   int stride);
+
 /* ---- cost parameters ------------------------------------------------------------------ */
 /* lambda -> motion lambda exactly as TComRdCost::setLambda + selectMotionLambda(true,0,false):
  * mlambda = 65536.0 * sqrt(lambda)  (TComRdCost.cpp:104-117, TComRdCost.h:159).           */
@@ -187,6 +195,53 @@ int fme_frac_dif_single(fme_ctx* ctx, int lossless, const int16_t* key, int key_
  * MVY_HALF, MVY_QRTER in out4 (TEncSearch.cpp:136-193).                                */
 int fme_nn_pred_single(fme_ctx* ctx, const uint32_t* e, uint32_t c, int pu_h, int pu_w,
                        int* nn_class, int16_t* out4);
+
+/* ---- motion compensation of decided MVs (luma 8-tap + 4:2:0 chroma 4-tap) ------------------ *
+ * TComPrediction::motionCompensation for one PU per job (TComPrediction.cpp:495-560):
+ *   xPredInterUni / xPredInterBi (562-614) -> xPredInterBlk (616-668) on the luma plane
+ *   (8-tap, quarter-pel) and both chroma planes (4-tap, eighth-pel; TComInterpolationFilter.cpp
+ *   :65-75, 341-394), each MV first clipped by TComDataCU::clipMv (TComDataCU.cpp:2773-2786)
+ *   against the CU origin; bi-prediction keeps both lists at 14-bit precision and averages them
+ *   with TComYuv::addAvg (TComYuv.cpp:354-415); L0 and L1 with the same picture and the same MV
+ *   are predicted from L0 alone (xCheckIdenticalMotion, TComPrediction.cpp:476-492).
+ * Weighted prediction (xWeightedPredictionUni/Bi) is not supported: the shipped configurations
+ * leave WeightedPredP/B off.
+ *   x, y, w, h   PU luma rectangle (w, h in 4..64, multiples of 4)
+ *   flags        FME_MC_L0 and/or FME_MC_L1 (both: bi-prediction)
+ *   ref_id[l]    picture slot of list l's reference (luma and chroma set)
+ *   cu_x, cu_y   luma origin of the CU the PU belongs to (clipMv bounds)
+ *   mv[l]        list l's MV in quarter-pel luma units (hor, ver), as stored in the CU          */
+#define FME_MC_L0 0x01u
+#define FME_MC_L1 0x02u
+
+typedef struct fme_mc_job {
+  uint16_t x, y;
+  uint8_t  w, h;
+  uint8_t  flags;
+  uint8_t  reserved;
+  uint8_t  ref_id[2];
+  uint16_t cu_x, cu_y;
+  int16_t  mv[2][2];
+  uint16_t reserved2;
+} fme_mc_job;   /* 24 bytes */
+
+/* Writes each job's prediction into the destination planes at the PU position (luma
+ * width x height, chroma (width/2) x (height/2)); other samples are left as they are.  Jobs
+ * must not overlap.  Every reference picture must have the destination's dimensions.
+ * fme_motion_compensate: host planes (copied to the device and back), synchronous; a batch
+ *   with any invalid job is rejected before anything runs.
+ * fme_motion_compensate_device: device planes and jobs, asynchronous on `stream`; invalid jobs
+ *   are skipped and counted, fme_mc_invalid_count() waits and returns the count of the last
+ *   such call.                                                                              */
+int fme_motion_compensate(fme_ctx* ctx, const fme_mc_job* jobs, int n, uint8_t* y, int y_stride,
+                          uint8_t* cb, uint8_t* cr, int c_stride, int width, int height, void* stream);
+int fme_motion_compensate_device(fme_ctx* ctx, const fme_mc_job* d_jobs, int n, uint8_t* d_y,
+                                 int y_stride, uint8_t* d_cb, uint8_t* d_cr, int c_stride, int width,
+                                 int height, void* stream);
+int fme_mc_invalid_count(fme_ctx* ctx);
+/* With profiling on: device milliseconds of the last motion-compensation launch (HIP events on
+ * its stream); waits for it. */
+int fme_mc_last_ms(fme_ctx* ctx, float* ms);
 
 /* ---- instrumentation (an extension; the reference has no counterpart) ------------------- *
  * With profiling on, fme_refine/fme_refine_device record HIP events around each kernel of

@@ -474,3 +474,147 @@ int orc_refine(orc_ctx* ctx, const fme_job* jobs, fme_result* res, int n) {
   free(key);
   return FME_OK;
 }
+
+/* =====================================================================================
+ * Motion compensation of decided MVs: luma 8-tap + 4:2:0 chroma 4-tap.
+ * ===================================================================================== */
+
+/* m_chromaFilter, TComInterpolationFilter.cpp:65-75 (eighth-pel, 4 taps). */
+static const int kChroma[8][4] = {{0, 64, 0, 0},    {-2, 58, 10, -2}, {-4, 54, 16, -2},
+                                  {-6, 46, 28, -4}, {-4, 36, 36, -4}, {-4, 28, 46, -6},
+                                  {-2, 16, 54, -4}, {-2, 10, 58, -2}};
+
+/* A block of `Pel` samples with its stride: the reference planes are staged into a padded
+ * window (edge replication = TComPicYuv::extendPicBorder) so the filters below can walk raw
+ * pointers the way TComInterpolationFilter does. */
+typedef struct orc_win {
+  int16_t* p;     /* sample (0,0) of the block */
+  int stride;
+} orc_win;
+
+/* TComInterpolationFilter::filterCopy (TComInterpolationFilter.cpp:94-154), bit depth 8:
+ * isFirst == isLast -> copy; isFirst -> (x << 6) - 8192; else ((x + 8192 + 32) >> 6) clipped. */
+static void mc_copy(const int16_t* src, int ss, int16_t* dst, int ds, int w, int h, int first, int last) {
+  for (int r = 0; r < h; r++)
+    for (int c = 0; c < w; c++) {
+      int v = src[r * ss + c];
+      if (first == last) {
+      } else if (first) {
+        v = (v << 6) - 8192;
+      } else {
+        v = clampi((v + 8192 + 32) >> 6, 0, 255);
+      }
+      dst[r * ds + c] = (int16_t)v;
+    }
+}
+
+/* filter<N, isVertical, isFirst, isLast> (TComInterpolationFilter.cpp:172-257), bit depth 8:
+ * headRoom 6; isLast: shift 6 (+6 when !isFirst), offset 1 << (shift-1) (+ 8192 << 6 when
+ * !isFirst), clip; else shift 6 - 6 (isFirst) or 6, offset -8192 (isFirst) or 0. */
+static void mc_filter(int ntaps, const int* coef, int vert, int first, int last, const int16_t* src, int ss,
+                      int16_t* dst, int ds, int w, int h) {
+  const int cstride = vert ? ss : 1;
+  const int16_t* s0 = src - (ntaps / 2 - 1) * cstride;
+  int shift = 6, offset;
+  if (last) {
+    shift += first ? 0 : 6;
+    offset = 1 << (shift - 1);
+    offset += first ? 0 : 8192 << 6;
+  } else {
+    shift -= first ? 6 : 0;
+    offset = first ? -8192 << shift : 0;
+  }
+  for (int r = 0; r < h; r++)
+    for (int c = 0; c < w; c++) {
+      int sum = 0;
+      for (int k = 0; k < ntaps; k++) sum += s0[r * ss + c + k * cstride] * coef[k];
+      int v = (sum + offset) >> shift;
+      if (last) v = clampi(v, 0, 255);
+      dst[r * ds + c] = (int16_t)v;
+    }
+}
+
+/* TComDataCU::clipMv (TComDataCU.cpp:2773-2786), max CU 64. */
+static void mc_clip_mv(int* mx, int* my, int pic_w, int pic_h, int cu_x, int cu_y) {
+  const int hor_max = (pic_w + 8 - cu_x - 1) << 2, hor_min = (-64 - 8 - cu_x + 1) * 4;
+  const int ver_max = (pic_h + 8 - cu_y - 1) << 2, ver_min = (-64 - 8 - cu_y + 1) * 4;
+  *mx = *mx < hor_min ? hor_min : (*mx > hor_max ? hor_max : *mx);
+  *my = *my < ver_min ? ver_min : (*my > ver_max ? ver_max : *my);
+}
+
+/* xPredInterBlk (TComPrediction.cpp:616-668) for one component: W x H at (x0,y0) of a plane
+ * (pw x ph), MV in units of 1 << shift samples; bi keeps 14-bit output. */
+static void mc_pred_blk(const uint8_t* plane, int stride, int pw, int ph, int chroma, int x0, int y0, int w, int h,
+                        int mx, int my, int bi, int16_t* dst, int ds) {
+  const int ntaps = chroma ? 4 : 8, sh = chroma ? 3 : 2;
+  const int ix = mx >> sh, iy = my >> sh, fx = mx & ((1 << sh) - 1), fy = my & ((1 << sh) - 1);
+  /* padded window: rows -ntaps/2+1 .. h+ntaps/2, cols likewise, around the displaced block */
+  const int pad = ntaps / 2, ww = w + 2 * pad, wh = h + 2 * pad;
+  int16_t* win = (int16_t*)malloc(sizeof(int16_t) * ww * wh);
+  int16_t* tmp = (int16_t*)malloc(sizeof(int16_t) * w * (h + ntaps));
+  for (int r = 0; r < wh; r++)
+    for (int c = 0; c < ww; c++) {
+      const int yy = clampi(y0 + iy + r - pad, 0, ph - 1), xx = clampi(x0 + ix + c - pad, 0, pw - 1);
+      win[r * ww + c] = plane[(size_t)yy * stride + xx];
+    }
+  const int16_t* ref = win + pad * ww + pad;
+  int ch[8], cv[8];
+  for (int k = 0; k < ntaps; k++) {
+    ch[k] = chroma ? kChroma[fx][k] : kLuma[fx][k];
+    cv[k] = chroma ? kChroma[fy][k] : kLuma[fy][k];
+  }
+  if (fy == 0) {         /* filterHor(frac = fx, isLast = !bi); fx == 0 -> filterCopy */
+    if (fx == 0) mc_copy(ref, ww, dst, ds, w, h, 1, !bi);
+    else mc_filter(ntaps, ch, 0, 1, !bi, ref, ww, dst, ds, w, h);
+  } else if (fx == 0) {  /* filterVer(frac = fy, isFirst = true, isLast = !bi) */
+    mc_filter(ntaps, cv, 1, 1, !bi, ref, ww, dst, ds, w, h);
+  } else {               /* filterHor over h + ntaps - 1 rows, then filterVer(isFirst = false) */
+    mc_filter(ntaps, ch, 0, 1, 0, ref - (ntaps / 2 - 1) * ww, ww, tmp, w, w, h + ntaps - 1);
+    mc_filter(ntaps, cv, 1, 0, !bi, tmp + (ntaps / 2 - 1) * w, w, dst, ds, w, h);
+  }
+  free(win);
+  free(tmp);
+}
+
+int orc_mc(const orc_yuv* pics, const fme_mc_job* jobs, int n, uint8_t* y, int ys, uint8_t* cb, uint8_t* cr,
+           int cs, int width, int height) {
+  for (int i = 0; i < n; i++) {
+    const fme_mc_job* j = &jobs[i];
+    if (j->w < 4 || j->h < 4 || j->w > 64 || j->h > 64 || (j->w & 3) || (j->h & 3)) return -1 - i;
+    if (!(j->flags & 3u) || (j->flags & ~3u)) return -1 - i;
+    if (j->x + j->w > width || j->y + j->h > height) return -1 - i;
+    for (int l = 0; l < 2; l++)
+      if ((j->flags & (1u << l)) &&
+          (j->ref_id[l] >= FME_MAX_PICTURES || !pics[j->ref_id[l]].y || pics[j->ref_id[l]].width != width ||
+           pics[j->ref_id[l]].height != height))
+        return -1 - i;
+    int lists[2], nl = 0;
+    if (j->flags & FME_MC_L0) lists[nl++] = 0;
+    if (j->flags & FME_MC_L1) lists[nl++] = 1;
+    /* xCheckIdenticalMotion (TComPrediction.cpp:476-492) */
+    if (nl == 2 && j->ref_id[0] == j->ref_id[1] && j->mv[0][0] == j->mv[1][0] && j->mv[0][1] == j->mv[1][1]) nl = 1;
+    for (int comp = 0; comp < 3; comp++) {
+      const int c = comp ? 1 : 0;
+      const int w = j->w >> c, h = j->h >> c, x0 = j->x >> c, y0 = j->y >> c;
+      int16_t pred[2][64 * 64];
+      for (int k = 0; k < nl; k++) {
+        const orc_yuv* p = &pics[j->ref_id[lists[k]]];
+        int mx = j->mv[lists[k]][0], my = j->mv[lists[k]][1];
+        mc_clip_mv(&mx, &my, p->width, p->height, j->cu_x, j->cu_y);
+        const uint8_t* plane = comp == 0 ? p->y : (comp == 1 ? p->cb : p->cr);
+        mc_pred_blk(plane, comp ? p->c_stride : p->y_stride, p->width >> c, p->height >> c, c, x0, y0, w, h, mx, my,
+                    nl == 2, pred[k], w);
+      }
+      uint8_t* out = comp == 0 ? y : (comp == 1 ? cb : cr);
+      const int os = comp ? cs : ys;
+      for (int r = 0; r < h; r++)
+        for (int q = 0; q < w; q++) {
+          int v = pred[0][r * w + q];
+          /* TComYuv::addAvg (TComYuv.cpp:354-415): shiftNum 7, offset 64 + 2 * 8192 */
+          if (nl == 2) v = clampi((pred[0][r * w + q] + pred[1][r * w + q] + 16448) >> 7, 0, 255);
+          out[(size_t)(y0 + r) * os + x0 + q] = (uint8_t)v;
+        }
+    }
+  }
+  return 0;
+}

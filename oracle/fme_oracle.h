@@ -97,6 +97,18 @@ void orc_nn_set_state(orc_ctx* ctx, const uint32_t in[12]);
  * 0 or a negative FME_E_* code. */
 int orc_refine(orc_ctx* ctx, const fme_job* jobs, fme_result* res, int n);
 
+/* ---- motion compensation ------------------------------------ */
+typedef struct orc_yuv {
+  const uint8_t *y, *cb, *cr;   /* 8-bit 4:2:0 planes; chroma (width/2) x (height/2) */
+  int y_stride, c_stride, width, height;
+} orc_yuv;
+
+/* TComPrediction::motionCompensation per job into the planes (TComPrediction.cpp:476-668,
+ * TComInterpolationFilter.cpp:94-394, TComYuv.cpp:354-415, TComDataCU.cpp:2773-2786).
+ * pics[ref_id] are the reference pictures.  Returns 0, or -1-i for an invalid job i. */
+int orc_mc(const orc_yuv* pics, const fme_mc_job* jobs, int n, uint8_t* y, int y_stride,
+           uint8_t* cb, uint8_t* cr, int c_stride, int width, int height);
+
 /* helpers for bindings */
 size_t orc_ctx_size(void);
 

@@ -96,6 +96,66 @@ def build_case(name, seed, width, height, n_jobs, hadme, fen, nn_mode, qp, bipre
           f"{int((r_ref['n_emi'] < 8).sum())} with < 8 EMI pushes")
 
 
+def build_mc_case(name, seed, width, height, bi_frac, mv_amp, identical_frac, keep_frac=1.0, fill=0):
+    """Motion compensation (TComPrediction::motionCompensation): reference pictures with 4:2:0
+    chroma, one frame partition of decided PUs, the predicted planes from _ref (the oracle must
+    agree).  keep_frac < 1 drops PUs: their samples must keep the initial `fill`."""
+    from nnfme.abi import MC_JOB_DTYPE  # noqa: F401
+    rng = np.random.default_rng(seed)
+    pics = {}
+    for k in range(3):
+        cb, cr = synth.synth_chroma(width, height, k, seed=seed)
+        pics[k] = (synth.synth_luma(width, height, k, seed=seed), cb, cr)
+    if name == "mc_shapes":   # every HEVC inter PU shape once, each in its own 64x64 cell
+        shapes = synth.ALL_PU_SIZES
+        jobs = synth.make_mc_partition(rng, 64 * 6, 64 * 4, [0, 1, 2], bi_frac=bi_frac, mv_amp=mv_amp)[:len(shapes)]
+        for i, (w, h) in enumerate(shapes):
+            jobs[i]["x"], jobs[i]["y"] = 64 * (i % 6) + (64 - w), 64 * (i // 6)
+            jobs[i]["cu_x"], jobs[i]["cu_y"] = 64 * (i % 6), 64 * (i // 6)
+            jobs[i]["w"], jobs[i]["h"] = w, h
+    else:
+        jobs = synth.make_mc_partition(rng, width, height, [0, 1, 2], bi_frac=bi_frac, mv_amp=mv_amp,
+                                       identical_frac=identical_frac)
+    if keep_frac < 1.0:
+        jobs = jobs[rng.random(len(jobs)) < keep_frac]
+    ref, orc = Reference(), Oracle()
+    for k, (y, cb, cr) in pics.items():
+        ref.set_picture_yuv(k, y, cb, cr)
+    outs = []
+    for eng in (ref, orc):
+        y = np.full((height, width), fill, np.uint8)
+        cb = np.full((height // 2, width // 2), fill, np.uint8)
+        cr = cb.copy()
+        if eng is ref:
+            eng.mc(jobs, y, cb, cr)
+        else:
+            eng.mc(pics, jobs, y, cb, cr)
+        outs.append((y, cb, cr))
+    for a, b, comp in zip(outs[0], outs[1], "Y Cb Cr".split()):
+        if not np.array_equal(a, b):
+            raise SystemExit(f"{name}: oracle disagrees with _ref on {comp} ({int((a != b).sum())} samples)")
+    path = os.path.join(OUT, f"{name}.npz")
+    np.savez_compressed(
+        path,
+        ref_y=np.stack([pics[k][0] for k in range(3)]),
+        ref_cb=np.stack([pics[k][1] for k in range(3)]),
+        ref_cr=np.stack([pics[k][2] for k in range(3)]),
+        jobs=jobs,
+        fill=np.array([fill], np.uint8),
+        pred_y=outs[0][0], pred_cb=outs[0][1], pred_cr=outs[0][2],
+    )
+    nbi = int(((jobs["flags"] & 3) == 3).sum())
+    print(f"{path}: {len(jobs)} PUs, {nbi} bi-pred, {len(set(zip(jobs['w'], jobs['h'])))} PU shapes")
+
+
+MC_CASES = [
+    # name, seed, W, H, bi_frac, mv_amp (pel), identical_frac, keep_frac, fill
+    ("mc_ldp_uni", 21, 160, 104, 0.0, 40, 0.0, 1.0, 0),
+    ("mc_ra_bi_clip", 22, 168, 96, 0.5, 200, 0.2, 1.0, 0),
+    ("mc_sparse", 23, 128, 80, 0.3, 16, 0.1, 0.5, 77),
+    ("mc_shapes", 24, 384, 256, 0.5, 24, 0.0, 1.0, 9),
+]
+
 CASES = [
     # name, seed, W, H, jobs, HADME, FEN, nn_mode, QP
     ("ldp_qp22_hadme_fen1_nn", 11, 160, 96, 1200, 1, 1, 1, 22),
@@ -108,8 +168,11 @@ CASES = [
 
 def main():
     os.makedirs(OUT, exist_ok=True)
-    for c in CASES:
-        build_case(*c)
+    if "--mc-only" not in sys.argv:
+        for c in CASES:
+            build_case(*c)
+    for c in MC_CASES:
+        build_mc_case(*c)
     return 0
 
 

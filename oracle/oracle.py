@@ -62,6 +62,8 @@ class Oracle:
         lib.orc_nn_set_state.argtypes = [_P, _P]
         lib.orc_refine.restype = C.c_int
         lib.orc_refine.argtypes = [_P, _P, _P, C.c_int]
+        lib.orc_mc.restype = C.c_int
+        lib.orc_mc.argtypes = [_P, _P, C.c_int, _P, C.c_int, _P, _P, C.c_int, C.c_int, C.c_int]
         self._buf = C.create_string_buffer(lib.orc_ctx_size())
         self.ctx = C.cast(self._buf, C.c_void_p)
         cfg = _ConfigStruct(8, use_hadamard, nn_mode, qp, fast_inter_mode, 0)
@@ -113,6 +115,25 @@ class Oracle:
         cls = self.lib.orc_nn_forward(_ptr(p), _ptr(e), int(c), int(h), int(w), _ptr(logits))
         return cls, logits
 
+    def mc(self, pics, mc_jobs, y, cb, cr):
+        """orc_mc: pics = {id: (Y, Cb, Cr)} reference pictures; predicts into y/cb/cr in place."""
+        class Yuv(C.Structure):
+            _fields_ = [("y", C.c_void_p), ("cb", C.c_void_p), ("cr", C.c_void_p), ("y_stride", C.c_int),
+                        ("c_stride", C.c_int), ("width", C.c_int), ("height", C.c_int)]
+        arr = (Yuv * 64)()
+        keep = []
+        for pid, (py, pcb, pcr) in pics.items():
+            py, pcb, pcr = (np.ascontiguousarray(a, dtype=np.uint8) for a in (py, pcb, pcr))
+            keep += [py, pcb, pcr]
+            arr[pid] = Yuv(py.ctypes.data, pcb.ctypes.data, pcr.ctypes.data, py.shape[1], pcb.shape[1],
+                           py.shape[1], py.shape[0])
+        jobs = np.ascontiguousarray(mc_jobs)
+        h, w = y.shape
+        rc = self.lib.orc_mc(C.cast(arr, C.c_void_p), _ptr(jobs), len(jobs), _ptr(y), y.shape[1], _ptr(cb), _ptr(cr),
+                             cb.shape[1], w, h)
+        if rc != 0:
+            raise RuntimeError(f"orc_mc: invalid job {-1 - rc}")
+
     def pred_block(self, luma, x0, y0, w, h, qx, qy):
         luma = np.ascontiguousarray(luma, dtype=np.uint8)
         out = np.zeros((h, w), dtype=np.int16)
@@ -144,6 +165,10 @@ class Reference:
         lib.ref_satd.argtypes = [_P, _P, C.c_int, _P, C.c_int, C.c_int, C.c_int, C.c_int]
         lib.ref_refine.restype = C.c_int
         lib.ref_refine.argtypes = [_P, _P, _P, C.c_int]
+        lib.ref_set_picture_yuv.restype = C.c_int
+        lib.ref_set_picture_yuv.argtypes = [_P, C.c_int, _P, C.c_int, _P, _P, C.c_int, C.c_int, C.c_int]
+        lib.ref_mc.restype = C.c_int
+        lib.ref_mc.argtypes = [_P, _P, C.c_int, _P, C.c_int, _P, _P, C.c_int, C.c_int, C.c_int]
         self.h = lib.ref_create(use_hadamard, fast_inter_mode, nn_mode)
 
     def __del__(self):
@@ -155,6 +180,18 @@ class Reference:
     def set_picture(self, pid, luma):
         luma = np.ascontiguousarray(luma, dtype=np.uint8)
         self.lib.ref_set_picture(self.h, pid, _ptr(luma), luma.shape[1], luma.shape[1], luma.shape[0])
+
+    def set_picture_yuv(self, pid, y, cb, cr):
+        y, cb, cr = (np.ascontiguousarray(a, dtype=np.uint8) for a in (y, cb, cr))
+        self.lib.ref_set_picture_yuv(self.h, pid, _ptr(y), y.shape[1], _ptr(cb), _ptr(cr), cb.shape[1], y.shape[1],
+                                     y.shape[0])
+
+    def mc(self, mc_jobs, y, cb, cr):
+        jobs = np.ascontiguousarray(mc_jobs)
+        h, w = y.shape
+        rc = self.lib.ref_mc(self.h, _ptr(jobs), len(jobs), _ptr(y), y.shape[1], _ptr(cb), _ptr(cr), cb.shape[1], w, h)
+        if rc != 0:
+            raise RuntimeError(f"ref_mc: invalid job {-1 - rc}")
 
     def set_lambda(self, lid, lam):
         self.lib.ref_set_lambda(self.h, lid, lam)

@@ -16,6 +16,7 @@
 //   xMotionEstimation tail (4529-4597).  NN_pred() (85-204) is restated as a scalar loop.
 // The restated pieces are independent of oracle/fme_oracle.c, which evaluates each candidate
 // as a direct quarter-pel prediction instead of walking the planes.
+#include <algorithm>
 #include <cmath>
 #include <cstdint>
 #include <cstring>
@@ -27,6 +28,7 @@
 #include "TLibCommon/TComPrediction.h"
 #include "TLibCommon/TComRdCost.h"
 #include "TLibCommon/TComRom.h"
+#include "TLibCommon/TComYuv.h"
 
 #include "../include/fme.h"
 
@@ -187,6 +189,8 @@ class RefSearch : public TComPrediction {
 struct Pic {
   TComPicYuv yuv;
   bool set = false;
+  TComPicYuv yuv420;    // 4:2:0 picture with its 80 / 40-sample margins (motion compensation)
+  bool set420 = false;
 };
 
 struct RefCtx {
@@ -418,6 +422,103 @@ int ref_refine(void* h, const fme_job* jobs, fme_result* res, int n) {
     r.bits = bits;
     const double fw = (j.flags & FME_JOB_BIPRED) ? 0.5 : 1.0;
     r.cost = (Distortion)(std::floor(fw * ((double)fc - (double)s.rd.getCost(mvb))) + (double)s.rd.getCost(bits));
+  }
+  return 0;
+}
+
+// ---- motion compensation ---------------------------------------------------------------------
+// 4:2:0 picture for motion compensation: TComPicYuv with margins + extendPicBorder.
+int ref_set_picture_yuv(void* h, int id, const uint8_t* y, int ys, const uint8_t* cb, const uint8_t* cr, int cs,
+                        int w, int hgt) {
+  RefCtx* c = static_cast<RefCtx*>(h);
+  Pic& p = c->pics[id];
+  p.yuv420.destroy();
+  p.yuv420.createWithoutCUInfo(w, hgt, CHROMA_420, true, 64, 64);
+  for (int comp = 0; comp < 3; comp++) {
+    const ComponentID id_ = ComponentID(comp);
+    Pel* dst = p.yuv420.getAddr(id_);
+    const int ds = p.yuv420.getStride(id_);
+    const uint8_t* src = comp == 0 ? y : (comp == 1 ? cb : cr);
+    const int ss = comp ? cs : ys, pw = comp ? w / 2 : w, ph = comp ? hgt / 2 : hgt;
+    for (int yy = 0; yy < ph; yy++)
+      for (int xx = 0; xx < pw; xx++) dst[yy * ds + xx] = src[(size_t)yy * ss + xx];
+  }
+  p.yuv420.extendPicBorder();
+  p.set420 = true;
+  return 0;
+}
+
+// TComPrediction::motionCompensation per job (TComPrediction.cpp:495-560).  TComDataCU /
+// TComPic are not built here, so the CU-level steps are restated: clipMv (TComDataCU.cpp
+// :2773-2786), xCheckIdenticalMotion (TComPrediction.cpp:476-492) and xPredInterBlk's
+// offset / fraction / filter order (616-668) over the reference's TComInterpolationFilter
+// (filterHor / filterVer with the component id and CHROMA_420, TComInterpolationFilter.cpp
+// :341-394) on the padded TComPicYuv; bi-prediction averages with TComYuv::addAvg.
+int ref_mc(void* h, const fme_mc_job* jobs, int n, uint8_t* y, int ys, uint8_t* cb, uint8_t* cr, int cs, int width,
+           int height) {
+  RefCtx* c = static_cast<RefCtx*>(h);
+  TComInterpolationFilter f;
+  BitDepths bd;
+  bd.recon[CHANNEL_TYPE_LUMA] = 8;
+  bd.recon[CHANNEL_TYPE_CHROMA] = 8;
+  for (int i = 0; i < n; i++) {
+    const fme_mc_job& j = jobs[i];
+    int lists[2], nl = 0;
+    if (j.flags & FME_MC_L0) lists[nl++] = 0;
+    if (j.flags & FME_MC_L1) lists[nl++] = 1;
+    for (int k = 0; k < nl; k++)
+      if (!c->pics[j.ref_id[lists[k]]].set420) return -1 - i;
+    if (nl == 2 && j.ref_id[0] == j.ref_id[1] && j.mv[0][0] == j.mv[1][0] && j.mv[0][1] == j.mv[1][1]) nl = 1;
+    const bool bi = nl == 2;
+    TComYuv pred[2], out;
+    for (int k = 0; k < 2; k++) pred[k].create(j.w, j.h, CHROMA_420);
+    out.create(j.w, j.h, CHROMA_420);
+    for (int k = 0; k < nl; k++) {
+      TComPicYuv& ref = c->pics[j.ref_id[lists[k]]].yuv420;
+      int mx = j.mv[lists[k]][0], my = j.mv[lists[k]][1];
+      {   // clipMv
+        const int hmax = (width + 8 - j.cu_x - 1) << 2, hmin = (-64 - 8 - j.cu_x + 1) * 4;
+        const int vmax = (height + 8 - j.cu_y - 1) << 2, vmin = (-64 - 8 - j.cu_y + 1) * 4;
+        mx = std::min(hmax, std::max(hmin, mx));
+        my = std::min(vmax, std::max(vmin, my));
+      }
+      TComYuv& dstYuv = bi ? pred[k] : out;
+      for (int comp = 0; comp < 3; comp++) {
+        const ComponentID cid = ComponentID(comp);
+        const int csx = comp ? 1 : 0;
+        const int shH = 2 + csx, shV = 2 + csx;
+        const int rs = ref.getStride(cid);
+        Pel* src = ref.getAddr(cid) + ((j.y >> csx) + (my >> shV)) * rs + (j.x >> csx) + (mx >> shH);
+        Pel* dst = dstYuv.getAddr(cid);
+        const int dstS = dstYuv.getStride(cid);
+        const int xf = mx & ((1 << shH) - 1), yf = my & ((1 << shV) - 1);
+        const int cw = j.w >> csx, ch = j.h >> csx;
+        if (yf == 0) {
+          f.filterHor(cid, src, rs, dst, dstS, cw, ch, xf, !bi, CHROMA_420, 8);
+        } else if (xf == 0) {
+          f.filterVer(cid, src, rs, dst, dstS, cw, ch, yf, true, !bi, CHROMA_420, 8);
+        } else {
+          const int nt = comp ? NTAPS_CHROMA : NTAPS_LUMA;
+          std::vector<Pel> tmp((size_t)cw * (ch + nt - 1));
+          f.filterHor(cid, src - ((nt >> 1) - 1) * rs, rs, tmp.data(), cw, cw, ch + nt - 1, xf, false, CHROMA_420, 8);
+          f.filterVer(cid, tmp.data() + ((nt >> 1) - 1) * cw, cw, dst, dstS, cw, ch, yf, false, !bi, CHROMA_420, 8);
+        }
+      }
+    }
+    if (bi) out.addAvg(&pred[0], &pred[1], 0, j.w, j.h, bd);
+    for (int comp = 0; comp < 3; comp++) {
+      const ComponentID cid = ComponentID(comp);
+      const int csx = comp ? 1 : 0;
+      const Pel* o = out.getAddr(cid);
+      const int os = out.getStride(cid);
+      uint8_t* d = comp == 0 ? y : (comp == 1 ? cb : cr);
+      const int dsd = comp ? cs : ys;
+      for (int r = 0; r < (j.h >> csx); r++)
+        for (int q = 0; q < (j.w >> csx); q++)
+          d[(size_t)((j.y >> csx) + r) * dsd + (j.x >> csx) + q] = (uint8_t)o[r * os + q];
+    }
+    for (int k = 0; k < 2; k++) pred[k].destroy();
+    out.destroy();
   }
   return 0;
 }

@@ -33,7 +33,24 @@ def pytest_collection_modifyitems(config, items):
 
 
 def golden_cases():
-    return sorted(f[:-4] for f in os.listdir(GOLDEN) if f.endswith(".npz"))
+    """Sub-pel refinement fixtures (fme_job -> fme_result)."""
+    return sorted(f[:-4] for f in os.listdir(GOLDEN) if f.endswith(".npz") and not f.startswith("mc_"))
+
+
+def mc_golden_cases():
+    """Motion-compensation fixtures (fme_mc_job + reference YUV -> predicted planes)."""
+    return sorted(f[:-4] for f in os.listdir(GOLDEN) if f.endswith(".npz") and f.startswith("mc_"))
+
+
+def mc_inputs(g):
+    """(pictures {id: (Y, Cb, Cr)}, jobs, fresh output planes filled like the fixture's)."""
+    import numpy as np
+    pics = {k: (g["ref_y"][k], g["ref_cb"][k], g["ref_cr"][k]) for k in range(len(g["ref_y"]))}
+    fill = int(g["fill"][0])
+    h, w = g["pred_y"].shape
+    planes = (np.full((h, w), fill, np.uint8), np.full((h // 2, w // 2), fill, np.uint8),
+              np.full((h // 2, w // 2), fill, np.uint8))
+    return pics, g["jobs"], planes
 
 
 def load_golden(name):

@@ -19,11 +19,11 @@ def header_functions():
 def test_library_exports_header():
     lib = runtime.load_library()
     names = header_functions()
-    assert len(names) == 22
+    assert len(names) == 28
     assert set(names) == set(runtime.ABI_SYMBOLS)
     for n in names:
         assert hasattr(lib, n), n
-    assert lib.fme_abi_version() == runtime.ABI_VERSION == 2
+    assert lib.fme_abi_version() == runtime.ABI_VERSION == 3
 
 
 def test_struct_layouts():
@@ -33,6 +33,28 @@ def test_struct_layouts():
     assert abi.RESULT_DTYPE.fields["frac_cost"][1] == 12
     assert abi.RESULT_DTYPE.fields["emi"][1] == 28
     assert abi.RESULT_DTYPE.fields["status"][1] == 62
+    # fme_mc_job: x,y @0, w,h @4, flags @6, ref_id[2] @8, cu_x,cu_y @10, mv[2][2] @14
+    assert abi.MC_JOB_DTYPE.itemsize == 24
+    assert abi.MC_JOB_DTYPE.fields["ref_id"][1] == 8
+    assert abi.MC_JOB_DTYPE.fields["cu_x"][1] == 10
+    assert abi.MC_JOB_DTYPE.fields["mv"][1] == 14
+
+
+def test_mc_struct_matches_header():
+    """Compile a probe against include/fme.h: sizeof / offsetof of fme_mc_job."""
+    import subprocess
+    import tempfile
+    src = ('#include <stdio.h>\n#include <stddef.h>\n#include "fme.h"\nint main(void){printf("%zu %zu %zu %zu %zu",'
+           'sizeof(fme_mc_job), offsetof(fme_mc_job, ref_id), offsetof(fme_mc_job, cu_x), offsetof(fme_mc_job, mv),'
+           'offsetof(fme_mc_job, flags));return 0;}')
+    with tempfile.TemporaryDirectory() as d:
+        c = os.path.join(d, "p.c")
+        open(c, "w").write(src)
+        exe = os.path.join(d, "p")
+        subprocess.run(["gcc", "-I", os.path.join(ROOT, "include"), c, "-o", exe], check=True)
+        got = [int(v) for v in subprocess.run([exe], capture_output=True, text=True, check=True).stdout.split()]
+    d = abi.MC_JOB_DTYPE.fields
+    assert got == [abi.MC_JOB_DTYPE.itemsize, d["ref_id"][1], d["cu_x"][1], d["mv"][1], d["flags"][1]]
 
 
 @pytest.mark.skipif(gpu_available(), reason="checks the no-device error path")

@@ -5,7 +5,7 @@ import os
 import numpy as np
 import pytest
 
-from conftest import golden_cases, load_golden
+from conftest import mc_golden_cases, mc_inputs, golden_cases, load_golden
 from nnfme import synth, weights
 from nnfme.abi import PARITY_FIELDS, compare_results
 from oracle import REF_SO, Oracle, Reference
@@ -53,6 +53,55 @@ def test_golden_covers_every_pu_shape_and_flag():
         flags |= int(np.bitwise_or.reduce(j["flags"]))
     assert set(synth.ALL_PU_SIZES) <= seen
     assert flags == 0x7
+
+
+@pytest.mark.parametrize("case", mc_golden_cases())
+def test_mc_oracle_matches_golden(case):
+    """orc_mc (plain-C restatement) against the reference's motion compensation."""
+    g = load_golden(case)
+    pics, jobs, (y, cb, cr) = mc_inputs(g)
+    Oracle().mc(pics, jobs, y, cb, cr)
+    for got, exp, comp in ((y, g["pred_y"], "Y"), (cb, g["pred_cb"], "Cb"), (cr, g["pred_cr"], "Cr")):
+        assert np.array_equal(got, exp), f"{case} {comp}: {int((got != exp).sum())} samples differ"
+
+
+@pytest.mark.skipif(not HAVE_REF, reason="oracle/_ref not built")
+@pytest.mark.parametrize("seed,bi,amp", [(31, 0.0, 8), (32, 0.5, 64), (33, 0.8, 600)])
+def test_mc_oracle_matches_reference_random(seed, bi, amp):
+    """Random frame partitions (every PU shape, bi-pred, identical motion, MVs far outside the
+    picture so clipMv bites) through orc_mc and the reference's filters + addAvg."""
+    from nnfme import synth
+    W, H = 200, 136
+    rng = np.random.default_rng(seed)
+    pics = {}
+    ref = Reference()
+    for k in range(4):
+        cb, cr = synth.synth_chroma(W, H, k, seed=seed)
+        pics[k] = (synth.synth_luma(W, H, k, seed=seed), cb, cr)
+        ref.set_picture_yuv(k, *pics[k])
+    jobs = synth.make_mc_partition(rng, W, H, [0, 1, 2, 3], bi_frac=bi, mv_amp=amp, identical_frac=0.2)
+    outs = []
+    for eng in ("orc", "ref"):
+        y, cb, cr = np.zeros((H, W), np.uint8), np.zeros((H // 2, W // 2), np.uint8), np.zeros((H // 2, W // 2), np.uint8)
+        if eng == "orc":
+            Oracle().mc(pics, jobs, y, cb, cr)
+        else:
+            ref.mc(jobs, y, cb, cr)
+        outs.append((y, cb, cr))
+    for a, b in zip(*outs):
+        assert np.array_equal(a, b)
+
+
+def test_mc_golden_covers_cases():
+    shapes, flags, clipped = set(), set(), False
+    for case in mc_golden_cases():
+        g = load_golden(case)
+        j = g["jobs"]
+        shapes |= set(zip(j["w"].tolist(), j["h"].tolist()))
+        flags |= set(j["flags"].tolist())
+        W = g["pred_y"].shape[1]
+        clipped |= bool(((j["mv"][:, :, 0] >> 2) + j["x"][:, None] > W + 8).any())
+    assert len(shapes) >= 20 and flags == {1, 2, 3} and clipped
 
 
 def test_exp_golomb_bits():
