@@ -139,6 +139,63 @@ def cpu_baseline_all_cores(jobs, pics, rate1, seconds, cores):
     return total / wall, wall, total
 
 
+def mc_algorithmic_bytes(jobs):
+    """Motion compensation, per PU and list: the luma 8-tap footprint (w+7)(h+7) and the two
+    chroma 4-tap footprints (w/2+3)(h/2+3); per PU: the predicted samples (1.5 w h, written) and
+    the 24-byte job."""
+    w = jobs["w"].astype(np.int64)
+    h = jobs["h"].astype(np.int64)
+    lists = np.where((jobs["flags"] & 3) == 3, 2, 1)
+    same = ((jobs["flags"] & 3) == 3) & (jobs["ref_id"][:, 0] == jobs["ref_id"][:, 1]) & \
+        (jobs["mv"][:, 0, 0] == jobs["mv"][:, 1, 0]) & (jobs["mv"][:, 0, 1] == jobs["mv"][:, 1, 1])
+    lists = np.where(same, 1, lists)
+    ref = (w + 7) * (h + 7) + 2 * (w // 2 + 3) * (h // 2 + 3)
+    return int((lists * ref + (3 * w * h) // 2 + 24).sum())
+
+
+def mc_leg(dev, stream, reps):
+    """Motion compensation of one 1080p frame's decided PUs (TComPrediction::motionCompensation:
+    luma 8-tap + 4:2:0 chroma 4-tap), device-resident jobs / pictures / planes; HIP events around
+    each launch.  Two partitions: lowdelay_P (uni-pred, 4 refs) and a random-access-like one
+    (50 % bi-pred)."""
+    import torch
+    from nnfme.runtime import FmeContext
+    ctx = FmeContext(device=dev.index, nn_mode=0)
+    for k, t in zip(range(4), (7, 6, 5, 4)):
+        cb, cr = synth.synth_chroma(W, H, t)
+        ctx.set_picture_yuv(k, synth.synth_luma(W, H, t), cb, cr)
+    dy = torch.zeros((H, W), dtype=torch.uint8, device=dev)
+    dcb = torch.zeros((H // 2, W // 2), dtype=torch.uint8, device=dev)
+    dcr = torch.zeros_like(dcb)
+    out = {}
+    for name, bi in (("ldp_uni", 0.0), ("ra_bi50", 0.5)):
+        jobs = synth.make_mc_partition(np.random.default_rng(5), W, H, [0, 1, 2, 3], bi_frac=bi, mv_amp=64)
+        dj = torch.from_numpy(jobs.view(np.uint8).copy()).to(dev)
+
+        def run():
+            ctx.motion_compensate_device(dj.data_ptr(), len(jobs), dy.data_ptr(), W, dcb.data_ptr(), dcr.data_ptr(),
+                                         W // 2, W, H, stream.cuda_stream)
+        for _ in range(3):
+            run()
+        ctx.set_profiling(True)
+        ms = []
+        for _ in range(reps):
+            run()
+            ms.append(ctx.mc_last_ms())
+        ctx.set_profiling(False)
+        t = float(np.mean(ms))
+        nbytes = mc_algorithmic_bytes(jobs)
+        gbs = nbytes / (t / 1e3) / 1e9
+        out[name] = {"pus": int(len(jobs)), "bi_pred": int(((jobs["flags"] & 3) == 3).sum()),
+                     "kernel_ms": t, "pu_per_s": len(jobs) / (t / 1e3),
+                     "luma_mpix_per_s": W * H / (t / 1e3) / 1e6,
+                     "roofline": {"bound": "hbm", "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                                  "frac": gbs / HBM_PEAK_GBS, "algorithmic_bytes_per_launch": nbytes,
+                                  "kernel": "fme::k_mc"}}
+    ctx.close()
+    return out
+
+
 def read_pmc_traffic():
     """HBM bytes per search launch from the committed rocprofv3 PMC summary (profiles/), if any."""
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
@@ -158,6 +215,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample length")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-mc", action="store_true", help="skip the motion-compensation leg")
     ap.add_argument("--jobs", choices=("ctu", "uniform"), default="ctu",
                     help="job stream: HM CTU order (default) or uniformly scattered PUs (stress)")
     ap.add_argument("--cpu-cores", type=int, default=0,
@@ -290,6 +348,8 @@ def main():
         pcie = {"value": n / dt, "unit": "PU/s", "ms_per_step": dt * 1e3,
                 "note": "jobs H2D + org frame H2D + refine + results D2H, pinned host buffers"}
 
+    mc = mc_leg(dev, stream, reps=max(5, args.steps)) if rank == 0 and not args.no_mc else None
+
     value = world * n * args.steps / elapsed
     if rank == 0:
         small_jobs = jobs[main_kernel_mask(ctx, jobs)]
@@ -346,6 +406,8 @@ def main():
             out["speedup_vs_cpu_all_cores"] = value / cpu["cpu_baseline_all_cores"]["value"]
         if pcie:
             out["pcie_inclusive"] = pcie
+        if mc:
+            out["motion_compensation"] = mc
         print(json.dumps(out), flush=True)
 
     if world > 1:

@@ -1,51 +1,70 @@
 // fme_mc.hip — motion compensation of decided MVs (gfx950): luma 8-tap + 4:2:0 chroma 4-tap.
 //
-// TComPrediction::motionCompensation (TComPrediction.cpp:495-560) for one PU per workgroup
-// (one wavefront):
+// TComPrediction::motionCompensation (TComPrediction.cpp:495-560): a few PUs per workgroup, one
+// 4x4 luma unit (+ the co-sited 2x2 Cb and Cr units) per lane, reference windows in VGPRs:
 //   * clipMv of each list's MV against the CU origin (TComDataCU.cpp:2773-2786);
 //   * xCheckIdenticalMotion (TComPrediction.cpp:476-492): both lists on one picture with one MV
 //     -> uni-prediction from L0;
 //   * xPredInterBlk (616-668) per component: integer offset mv >> (2 + csx), fraction
-//     mv & ((4 << csx) - 1); fraction (0,0) copies, (fx,0) / (0,fy) filter once, otherwise a
-//     horizontal first stage over H + N - 1 rows into LDS, then the vertical stage
-//     (TComInterpolationFilter.cpp:94-154 filterCopy, 172-257 filter<N, isVert, isFirst, isLast>);
-//     uni-prediction ends at 8 bits (isLast), bi-prediction keeps 14-bit intermediates;
+//     mv & ((4 << csx) - 1); HM copies at fraction (0,0), filters once at (fx,0) / (0,fy) and
+//     twice otherwise (TComInterpolationFilter.cpp:94-154 filterCopy, 172-257 filter<N, isVert,
+//     isFirst, isLast>).  Here every case runs the two-stage form with the identity filter
+//     (64 at the centre tap) for a zero fraction, which gives the same integers: with
+//     S = sum c.s and s' = s - 128 (sum c = 64), stage 1 = S - 8192 = sum c.s'; a zero vertical
+//     fraction multiplies it by 64, and (64 (S - 8192) + 2048 + (8192 << 6)) >> 12 = (S + 32)
+//     >> 6 (uni), (64 (S - 8192)) >> 6 = S - 8192 (bi); a zero horizontal fraction gives
+//     stage 1 = 64 s' = (s << 6) - 8192, filterCopy's isFirst output.  Uni-prediction ends at
+//     8 bits, bi-prediction keeps the 14-bit values;
 //   * TComYuv::addAvg (TComYuv.cpp:354-415): (p0 + p1 + 16448) >> 7, clipped to 8 bits.
 // Samples outside a plane are read with edge replication, which equals HM's padded picture for
 // every clipped MV (luma margin 80, chroma margin 40: the clipped reads stay within 75 / 38).
 #include <hip/hip_runtime.h>
 
 #include "fme_device.h"
+#include "fme_simd.h"
 
 namespace fme {
 namespace {
 
-constexpr int kMcNT = 64;                 // one wavefront per PU
-constexpr int kMcTmp = (64 + 7) * 64;     // first-stage rows of the largest luma PU
-constexpr int kInternalOffs = 8192;       // IF_INTERNAL_OFFS (1 << IF_INTERNAL_PREC-1), 14-bit
+using namespace simd;
 
-// TComInterpolationFilter.cpp:57-75
-__device__ __forceinline__ int luma_tap(int f, int k) {
-  constexpr signed char t[4][8] = {{0, 0, 0, 64, 0, 0, 0, 0},
-                                   {-1, 4, -10, 58, 17, -5, 1, 0},
-                                   {-1, 4, -11, 40, 40, -11, 4, -1},
-                                   {0, 1, -5, 17, 58, -10, 4, -1}};
-  return t[f][k];
+#ifndef FME_MC_PROBE
+#define FME_MC_PROBE 0
+#endif
+
+
+// TComInterpolationFilter.cpp:57-75 as int8 quads (luma: taps 0-3, 4-7; chroma: taps 0-3).
+// Fraction 0 uses the identity filter (64 at the centre tap): through the two-stage form below
+// it reproduces filterCopy and the 1-D filters exactly (module header).
+__device__ __forceinline__ void luma_taps(int f, uint32_t& lo, uint32_t& hi) {
+  lo = f == 0 ? q8(0, 0, 0, 64) : f == 1 ? q8(-1, 4, -10, 58) : f == 2 ? q8(-1, 4, -11, 40) : q8(0, 1, -5, 17);
+  hi = f == 0 ? 0u : f == 1 ? q8(17, -5, 1, 0) : f == 2 ? q8(40, -11, 4, -1) : q8(58, -10, 4, -1);
 }
-__device__ __forceinline__ int chroma_tap(int f, int k) {
-  constexpr signed char t[8][4] = {{0, 64, 0, 0},    {-2, 58, 10, -2}, {-4, 54, 16, -2}, {-6, 46, 28, -4},
-                                   {-4, 36, 36, -4}, {-4, 28, 46, -6}, {-2, 16, 54, -4}, {-2, 10, 58, -2}};
-  return t[f][k];
+__device__ __forceinline__ uint32_t chroma_taps(int f) {
+  switch (f) {
+    case 0: return q8(0, 64, 0, 0);
+    case 1: return q8(-2, 58, 10, -2);
+    case 2: return q8(-4, 54, 16, -2);
+    case 3: return q8(-6, 46, 28, -4);
+    case 4: return q8(-4, 36, 36, -4);
+    case 5: return q8(-4, 28, 46, -6);
+    case 6: return q8(-2, 16, 54, -4);
+    default: return q8(-2, 10, 58, -2);
+  }
 }
+__device__ __forceinline__ int tap_of(uint32_t lo, uint32_t hi, int k) {   // signed byte k of (lo, hi)
+  const uint32_t w = k < 4 ? lo : hi;
+  return (int)(int8_t)(w >> (8 * (k & 3)));
+}
+
+typedef uint32_t u32x4a __attribute__((ext_vector_type(4), aligned(4)));
+typedef uint32_t u32x3a __attribute__((ext_vector_type(3), aligned(4)));
+typedef __attribute__((address_space(1))) const u32x4a gu4;
+typedef __attribute__((address_space(1))) const u32x3a gu3;
 
 struct Plane {
   const uint8_t* p;
   int stride, w, h;
-  __device__ __forceinline__ int at(int x, int y) const {
-    x = min(max(x, 0), w - 1);
-    y = min(max(y, 0), h - 1);
-    return p[(size_t)y * stride + x];
-  }
 };
 
 // TComDataCU::clipMv (TComDataCU.cpp:2773-2786), max CU 64 (sps.getMaxCUWidth/Height)
@@ -56,67 +75,96 @@ __device__ __forceinline__ void clip_mv(int& mx, int& my, int pic_w, int pic_h, 
   my = min(ver_max, max(ver_min, my));
 }
 
-// One list's prediction of one component block (W x H at (x0, y0) of the plane, integer offset
-// (ix, iy), fractions (fx, fy)) -> 8-bit into dst (uni) or 14-bit into acc (bi; second list
-// averages into dst).  mode: 0 uni, 1 bi first list, 2 bi second list.
-template <int N>
-__device__ void pred_block(const Plane& ref, int x0, int y0, int W, int H, int ix, int iy, int fx, int fy,
-                           int mode, int16_t* tmp, int16_t* acc, uint8_t* dst, int dst_stride) {
-  const int lane = threadIdx.x;
-  const int bx = x0 + ix, by = y0 + iy;
-  const bool last = mode == 0;
-  auto tapf = [](int f, int k) { return N == 8 ? luma_tap(f, k) : chroma_tap(f, k); };
-  auto emit = [&](int x, int y, int v) {   // v: 8-bit sample (uni) or 14-bit intermediate (bi)
-    if (mode == 0) {
-      dst[y * dst_stride + x] = (uint8_t)v;
-    } else if (mode == 1) {
-      acc[y * W + x] = (int16_t)v;
-    } else {   // TComYuv::addAvg, shiftNum = 7, offset = (1 << 6) + 2 * IF_INTERNAL_OFFS
-      const int s = (acc[y * W + x] + v + 16448) >> 7;
-      dst[y * dst_stride + x] = (uint8_t)min(max(s, 0), 255);
-    }
-  };
-  if (fx == 0 && fy == 0) {   // filterCopy(isFirst = true, isLast)
-    for (int i = lane; i < W * H; i += kMcNT) {
-      const int x = i % W, y = i / W;
-      const int s = ref.at(bx + x, by + y);
-      emit(x, y, last ? s : (s << 6) - kInternalOffs);
-    }
-  } else if (fy == 0 || fx == 0) {   // one 1-D filter<N, isVert, isFirst = true, isLast>
-    const bool vert = fy != 0;
-    const int f = vert ? fy : fx;
-    for (int i = lane; i < W * H; i += kMcNT) {
-      const int x = i % W, y = i / W;
-      int sum = 0;
+// Rows of (s - 128) bytes of a window: R rows from plane row y0, ND dwords from byte x0 & ~3
+// (edge-replicated), and the byte shift of x0 inside the first dword.
+template <int R, int ND>
+__device__ __forceinline__ uint32_t load_window(const Plane& pl, int x0, int y0, bool aligned, uint32_t (&w)[R][ND]) {
+  const int xa = x0 & ~3;
+  const bool inside = aligned && xa >= 0 && xa + 4 * ND <= pl.w && y0 >= 0 && y0 + R <= pl.h;
+  if (inside) {
 #pragma unroll
-      for (int k = 0; k < N; k++) {
-        const int o = k - (N / 2 - 1);
-        sum += ref.at(bx + x + (vert ? 0 : o), by + y + (vert ? o : 0)) * tapf(f, k);
+    for (int r = 0; r < R; r++) {
+      const uint8_t* row = pl.p + (size_t)(y0 + r) * pl.stride + xa;
+      if constexpr (ND == 4) {
+        const u32x4a v = *(gu4*)row;
+        w[r][0] = v.x ^ 0x80808080u; w[r][1] = v.y ^ 0x80808080u;
+        w[r][2] = v.z ^ 0x80808080u; w[r][3] = v.w ^ 0x80808080u;
+      } else if constexpr (ND == 3) {
+        const u32x3a v = *(gu3*)row;
+        w[r][0] = v.x ^ 0x80808080u; w[r][1] = v.y ^ 0x80808080u; w[r][2] = v.z ^ 0x80808080u;
+      } else {
+#pragma unroll
+        for (int k = 0; k < ND; k++) w[r][k] = gld32(row + 4 * k) ^ 0x80808080u;
       }
-      // isLast: shift 6, offset 32, clip; else shift 0, offset -IF_INTERNAL_OFFS
-      emit(x, y, last ? min(max((sum + 32) >> 6, 0), 255) : sum - kInternalOffs);
     }
-  } else {   // filterHor(isFirst, !isLast) over H + N - 1 rows, then filterVer(!isFirst, isLast)
-    const int HT = H + N - 1;
-    for (int i = lane; i < W * HT; i += kMcNT) {
-      const int x = i % W, r = i / W;
-      int sum = 0;
+  } else {
 #pragma unroll
-      for (int k = 0; k < N; k++) sum += ref.at(bx + x + k - (N / 2 - 1), by + r - (N / 2 - 1)) * tapf(fx, k);
-      tmp[r * W + x] = (int16_t)(sum - kInternalOffs);
-    }
-    __syncthreads();
-    for (int i = lane; i < W * H; i += kMcNT) {
-      const int x = i % W, y = i / W;
-      int sum = 0;
+    for (int r = 0; r < R; r++) {
+      const uint8_t* row = pl.p + (size_t)clamp_i(y0 + r, 0, pl.h - 1) * pl.stride;
 #pragma unroll
-      for (int k = 0; k < N; k++) sum += tmp[(y + k) * W + x] * tapf(fy, k);
-      // isLast: shift 12, offset 2048 + (IF_INTERNAL_OFFS << 6), clip; else shift 6, offset 0
-      emit(x, y, last ? min(max((sum + 2048 + (kInternalOffs << 6)) >> 12, 0), 255) : (sum >> 6));
+      for (int k = 0; k < ND; k++) {
+        uint32_t v = 0;
+#pragma unroll
+        for (int b = 0; b < 4; b++) v |= gld8(row + clamp_i(xa + 4 * k + b, 0, pl.w - 1)) << (8 * b);
+        w[r][k] = v ^ 0x80808080u;
+      }
     }
   }
-  __syncthreads();   // tmp / acc reuse by the next call
+  return (uint32_t)(x0 - xa);
 }
+
+// One U x U output unit of one list (N taps; U = 4 luma, 2 chroma): its window of R = U + N - 1
+// rows of (s - 128) bytes around plane position (bx, by) (integer MV applied).
+template <int N, int U>
+struct UnitWin {
+  static constexpr int R = U + N - 1;                   // window rows and columns
+  static constexpr int NA = ((U - 1 + N - 4) >> 2) + 2; // re-aligned dwords the dot4 groups read
+  static constexpr int ND = NA + 1;                     // dwords loaded per row (any alignment)
+  uint32_t w[R][ND];
+  uint32_t s0;
+  __device__ __forceinline__ void load(const Plane& pl, bool aligned, int bx, int by) {
+#if FME_MC_PROBE == 1   // timing probe only: no reference reads
+    for (int r = 0; r < R; r++)
+      for (int k = 0; k < ND; k++) w[r][k] = (uint32_t)(bx * 7 + by * 13 + r + k);
+    s0 = (uint32_t)bx & 3;
+#else
+    s0 = load_window<R, ND>(pl, bx - (N / 2 - 1), by - (N / 2 - 1), aligned, w);
+#endif
+  }
+  // Two stages in the (s - 128) domain, which absorbs filterCopy / filter<N, ., isFirst = true,
+  // .>'s -IF_INTERNAL_OFFS: stage 1 = sum c.s - 8192; stage 2 uni (isLast): (sum + 2048 +
+  // (8192 << 6)) >> 12 clipped, bi: sum >> 6 (14-bit).
+  __device__ __forceinline__ void pred(uint32_t hlo, uint32_t hhi, uint32_t vlo, uint32_t vhi, bool uni,
+                                       int (&out)[U][U]) const {
+    int t[R][U];
+#pragma unroll
+    for (int r = 0; r < R; r++) {
+      uint32_t a[NA];
+#pragma unroll
+      for (int k = 0; k < NA; k++) a[k] = __builtin_amdgcn_alignbyte(w[r][k + 1], w[r][k], s0);
+#pragma unroll
+      for (int c = 0; c < U; c++) {   // bytes c .. c+N-1 of the re-aligned row
+        const uint32_t b0 = (c & 3) ? __builtin_amdgcn_alignbyte(a[(c >> 2) + 1], a[c >> 2], (uint32_t)(c & 3)) : a[c >> 2];
+        int acc = dot4(b0, hlo, 0);
+        if constexpr (N == 8) {
+          const int q = c + 4;
+          const uint32_t b1 = (q & 3) ? __builtin_amdgcn_alignbyte(a[(q >> 2) + 1], a[q >> 2], (uint32_t)(q & 3)) : a[q >> 2];
+          acc = dot4(b1, hhi, acc);
+        }
+        t[r][c] = acc;
+      }
+    }
+#pragma unroll
+    for (int y = 0; y < U; y++)
+#pragma unroll
+      for (int c = 0; c < U; c++) {
+        int sum = 0;
+#pragma unroll
+        for (int k = 0; k < N; k++) sum += t[y + k][c] * tap_of(vlo, vhi, k);
+        out[y][c] = uni ? clamp_i((sum + 2048 + (8192 << 6)) >> 12, 0, 255) : (sum >> 6);
+      }
+  }
+};
 
 __device__ __forceinline__ bool mc_job_valid(const McArgs& a, const fme_mc_job& j) {
   if (j.w < 4 || j.h < 4 || j.w > 64 || j.h > 64 || (j.w & 3) || (j.h & 3)) return false;
@@ -131,38 +179,141 @@ __device__ __forceinline__ bool mc_job_valid(const McArgs& a, const fme_mc_job& 
   return true;
 }
 
-__global__ __launch_bounds__(kMcNT) void k_mc(McArgs a) {
-  __shared__ int16_t tmp[kMcTmp];
-  __shared__ int16_t acc[64 * 64];
-  const fme_mc_job j = a.jobs[blockIdx.x];
-  if (!mc_job_valid(a, j)) {
-    if (threadIdx.x == 0) atomicAdd(a.invalid, 1);
-    return;
+__device__ __forceinline__ void store_row(uint8_t* d, const int* v, int n, bool aligned) {
+  if (n == 4 && aligned) {
+    *(uint32_t*)d = (uint32_t)v[0] | ((uint32_t)v[1] << 8) | ((uint32_t)v[2] << 16) | ((uint32_t)v[3] << 24);
+  } else if (n == 2 && aligned) {
+    *(uint16_t*)d = (uint16_t)((uint32_t)v[0] | ((uint32_t)v[1] << 8));
+  } else {
+    for (int i = 0; i < n; i++) d[i] = (uint8_t)v[i];
   }
-  int nl = 0, lists[2];
-  if (j.flags & FME_MC_L0) lists[nl++] = 0;
-  if (j.flags & FME_MC_L1) lists[nl++] = 1;
-  if (nl == 2 && j.ref_id[0] == j.ref_id[1] && j.mv[0][0] == j.mv[1][0] && j.mv[0][1] == j.mv[1][1])
-    nl = 1;   // xCheckIdenticalMotion: same picture, same MV -> xPredInterUni(REF_PIC_LIST_0)
-  for (int comp = 0; comp < 3; comp++) {
-    const int cs = comp ? 1 : 0;   // getComponentScaleX/Y for 4:2:0 chroma
-    const int W = j.w >> cs, H = j.h >> cs, x0 = j.x >> cs, y0 = j.y >> cs;
-    uint8_t* dst = comp == 0 ? a.y + (size_t)y0 * a.y_stride + x0
-                             : (comp == 1 ? a.cb : a.cr) + (size_t)y0 * a.c_stride + x0;
-    const int dst_stride = comp ? a.c_stride : a.y_stride;
-    for (int k = 0; k < nl; k++) {
-      const int l = lists[k];
-      const PicDesc& pd = a.pics[j.ref_id[l]];
-      int mx = j.mv[l][0], my = j.mv[l][1];
-      clip_mv(mx, my, pd.width, pd.height, j.cu_x, j.cu_y);
-      const int sh = 2 + cs, mask = (1 << sh) - 1;
-      const Plane ref = comp == 0 ? Plane{pd.luma, pd.stride, pd.width, pd.height}
-                                  : Plane{comp == 1 ? pd.cb : pd.cr, pd.cstride, pd.width >> 1, pd.height >> 1};
-      const int mode = nl == 1 ? 0 : (k == 0 ? 1 : 2);
-      if (comp == 0)
-        pred_block<8>(ref, x0, y0, W, H, mx >> sh, my >> sh, mx & mask, my & mask, mode, tmp, acc, dst, dst_stride);
-      else
-        pred_block<4>(ref, x0, y0, W, H, mx >> sh, my >> sh, mx & mask, my & mask, mode, tmp, acc, dst, dst_stride);
+}
+
+// Per-job state shared by the workgroup (LDS), filled by one thread per job.
+struct McJobInfo {
+  int units;          // 4x4 luma units, 0 when invalid
+  int ux_n;           // units per PU row
+  int x, y;           // PU luma origin
+  int nl;             // lists predicted (2: bi)
+  int lix[2], liy[2], lfx[2], lfy[2];   // luma integer offsets / fractions per list
+  int cix[2], ciy[2], cfx[2], cfy[2];   // chroma (eighth-pel) per list
+  PicDesc pic[2];
+};
+
+#ifndef FME_MC_JOBS
+#define FME_MC_JOBS 8
+#endif
+constexpr int kMcJobs = FME_MC_JOBS;   // consecutive jobs per workgroup
+constexpr int kMcBlock = 256;
+
+// kMcJobs consecutive jobs per workgroup; their 4x4 luma units (each with the co-sited 2x2 Cb and
+// Cr units) are dealt to the 256 lanes, so small and large PUs fill the waves alike; a lane
+// predicts both lists of its unit in registers and averages them.
+__global__ __launch_bounds__(kMcBlock) void k_mc(McArgs a) {
+  __shared__ McJobInfo info[kMcJobs];
+  __shared__ int first_unit[kMcJobs + 1];
+  const int j0 = blockIdx.x * kMcJobs;
+  const int t = threadIdx.x;
+  if (t < kMcJobs) {
+    McJobInfo& in = info[t];
+    in.units = 0;
+    const int ji = j0 + t;
+    if (ji < a.n) {
+      const fme_mc_job j = a.jobs[ji];
+      if (!mc_job_valid(a, j)) {
+        atomicAdd(a.invalid, 1);
+      } else {
+        int nl = 0, lists[2] = {0, 0};
+        if (j.flags & FME_MC_L0) lists[nl++] = 0;
+        if (j.flags & FME_MC_L1) lists[nl++] = 1;
+        if (nl == 2 && j.ref_id[0] == j.ref_id[1] && j.mv[0][0] == j.mv[1][0] && j.mv[0][1] == j.mv[1][1])
+          nl = 1;   // xCheckIdenticalMotion: same picture, same MV -> xPredInterUni(REF_PIC_LIST_0)
+        in.nl = nl;
+        for (int k = 0; k < nl; k++) {
+          const int l = lists[k];
+          const PicDesc p = a.pics[j.ref_id[l]];
+          int mx = j.mv[l][0], my = j.mv[l][1];
+          clip_mv(mx, my, p.width, p.height, j.cu_x, j.cu_y);
+          in.lix[k] = mx >> 2;   // xPredInterBlk: shift 2 + csx, fraction mask (4 << csx) - 1
+          in.liy[k] = my >> 2;
+          in.lfx[k] = mx & 3;
+          in.lfy[k] = my & 3;
+          in.cix[k] = mx >> 3;
+          in.ciy[k] = my >> 3;
+          in.cfx[k] = mx & 7;
+          in.cfy[k] = my & 7;
+          in.pic[k] = p;
+        }
+        in.x = j.x;
+        in.y = j.y;
+        in.ux_n = j.w >> 2;
+        in.units = (j.w >> 2) * (j.h >> 2);
+      }
+    }
+  }
+  __syncthreads();
+  if (t == 0) {
+    int acc = 0;
+    for (int k = 0; k < kMcJobs; k++) {
+      first_unit[k] = acc;
+      acc += info[k].units;
+    }
+    first_unit[kMcJobs] = acc;
+  }
+  __syncthreads();
+  const int total = first_unit[kMcJobs];
+  const bool ys_al = ((a.y_stride | (int)(uintptr_t)a.y) & 3) == 0;
+  const bool cs_al = ((a.c_stride | (int)(uintptr_t)a.cb | (int)(uintptr_t)a.cr) & 1) == 0;
+  for (int g = t; g < total; g += kMcBlock) {
+    int q = 0;
+#pragma unroll
+    for (int k = 1; k < kMcJobs; k++) q += g >= first_unit[k] ? 1 : 0;
+    const McJobInfo& in = info[q];
+    const int u = g - first_unit[q];
+    const int ux = u % in.ux_n, uy = u / in.ux_n;
+    const bool uni = in.nl == 1;
+    {   // luma 4x4
+      const int x = in.x + 4 * ux, y = in.y + 4 * uy;
+      int acc[4][4], o[4][4];
+#pragma unroll
+      for (int k = 0; k < 2; k++) {
+        if (k >= in.nl) break;
+        const PicDesc& p = in.pic[k];
+        UnitWin<8, 4> w;
+        w.load(Plane{p.luma, p.stride, p.width, p.height}, ((p.stride | (int)(uintptr_t)p.luma) & 3) == 0,
+               x + in.lix[k], y + in.liy[k]);
+        uint32_t hlo, hhi, vlo, vhi;
+        luma_taps(in.lfx[k], hlo, hhi);
+        luma_taps(in.lfy[k], vlo, vhi);
+        w.pred(hlo, hhi, vlo, vhi, uni, o);
+#pragma unroll
+        for (int r = 0; r < 4; r++)
+#pragma unroll
+          for (int c = 0; c < 4; c++) acc[r][c] = k == 0 ? o[r][c] : clamp_i((acc[r][c] + o[r][c] + 16448) >> 7, 0, 255);
+      }
+#pragma unroll
+      for (int r = 0; r < 4; r++) store_row(a.y + (size_t)(y + r) * a.y_stride + x, acc[r], 4, ys_al);
+    }
+#pragma unroll
+    for (int comp = 1; comp <= 2; comp++) {   // chroma 2x2 of Cb and Cr (4:2:0)
+      const int x = (in.x >> 1) + 2 * ux, y = (in.y >> 1) + 2 * uy;
+      int acc[2][2], o[2][2];
+#pragma unroll
+      for (int k = 0; k < 2; k++) {
+        if (k >= in.nl) break;
+        const PicDesc& p = in.pic[k];
+        const Plane pl{comp == 1 ? p.cb : p.cr, p.cstride, p.width >> 1, p.height >> 1};
+        UnitWin<4, 2> w;
+        w.load(pl, ((p.cstride | (int)(uintptr_t)pl.p) & 3) == 0, x + in.cix[k], y + in.ciy[k]);
+        w.pred(chroma_taps(in.cfx[k]), 0u, chroma_taps(in.cfy[k]), 0u, uni, o);
+#pragma unroll
+        for (int r = 0; r < 2; r++)
+#pragma unroll
+          for (int c = 0; c < 2; c++) acc[r][c] = k == 0 ? o[r][c] : clamp_i((acc[r][c] + o[r][c] + 16448) >> 7, 0, 255);
+      }
+      uint8_t* base = comp == 1 ? a.cb : a.cr;
+#pragma unroll
+      for (int r = 0; r < 2; r++) store_row(base + (size_t)(y + r) * a.c_stride + x, acc[r], 2, cs_al);
     }
   }
 }
@@ -170,7 +321,7 @@ __global__ __launch_bounds__(kMcNT) void k_mc(McArgs a) {
 }  // namespace
 
 hipError_t launch_mc(const McArgs& a, hipStream_t s) {
-  if (a.n > 0) hipLaunchKernelGGL(k_mc, dim3(a.n), dim3(kMcNT), 0, s, a);
+  if (a.n > 0) hipLaunchKernelGGL(k_mc, dim3((a.n + kMcJobs - 1) / kMcJobs), dim3(kMcBlock), 0, s, a);
   return hipGetLastError();
 }
 
