@@ -39,6 +39,20 @@ from nnfme.abi import JOB_DTYPE, RESULT_DTYPE  # noqa: E402
 
 W, H, QP = 1920, 1080, 22
 METRIC = "sub-pel PU refinements/sec @ 1080p lowdelay_P QP22; bit-exact MV/SATD vs HM"
+# BASELINE.json configs as bench workloads (default: the headline, configs[2] at QP22).
+#   name: (W, H, QP, nn_mode, calls per CTU per reference, references, bi-pred share, description)
+WORKLOADS = {
+    "c3_qp22": (1920, 1080, 22, 1, 423, 4, 0.0,
+                "1920x1080 lowdelay_P QP22, NN_pred 2-layer on, 4 refs, 862920 PU jobs per frame (configs[2] at QP22)"),
+    "c3_qp27": (1920, 1080, 27, 1, 423, 4, 0.0, "1920x1080 lowdelay_P QP27, NN_pred on, 4 refs (configs[2] at QP27)"),
+    "c3_qp32": (1920, 1080, 32, 1, 423, 4, 0.0, "1920x1080 lowdelay_P QP32, NN_pred on, 4 refs (configs[2] at QP32)"),
+    "c3_qp37": (1920, 1080, 37, 1, 423, 4, 0.0, "1920x1080 lowdelay_P QP37, NN_pred on, 4 refs (configs[2] at QP37)"),
+    "c2": (416, 240, 22, 0, 331, 4, 0.0,
+           "416x240 lowdelay_P QP22, interpolation + SATD only (NN_pred off), 4 refs, 331 calls/CTU/ref (configs[1])"),
+    "c4": (2560, 1600, 27, 1, 333, 4, 0.205,
+           "2560x1600 random-access QP27 B-frame, NN_pred on, 2+2 refs, ~1331 calls/CTU, 20.5 % bi-pred with "
+           "2*org - pred keys (configs[3]; lambdas from the LDP QP27 table)"),
+}
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md chip table (spec)
 # int32 VALU lane-ops/s: 256 CUs x 4 SIMDs x 32 lanes/clk (a wave64 op issues over 2 clk) x
 # 2.4 GHz = 78.6 T (MI355X_MICROARCH.md; = the 157.3 TFLOP/s f32 vector peak / 2)
@@ -73,14 +87,15 @@ def algorithmic_ops(jobs):
     return int((16 * taps + 2 * copies + 18 * satd + 144).sum())
 
 
-def make_frame_jobs(seed, kind="ctu"):
+def make_frame_jobs(seed, kind="ctu", calls=423, bipred=0.0):
     """One frame's jobs.  "ctu": HM order (CTU raster, PUs on the CU grid, coherent motion);
     "uniform": every PU at a uniformly random frame position (no cache locality, stress)."""
     rng = np.random.default_rng(seed)
     # refs: picture ids 0..3, org: id 4; lambda slot 0 = the frame's value (set per step)
     if kind == "uniform":
-        return synth.make_jobs(rng, W, H, synth.jobs_per_frame(W, H), 4, [0, 1, 2, 3], [0])
-    return synth.make_ctu_jobs(rng, W, H, 423, 4, [0, 1, 2, 3], [0])
+        return synth.make_jobs(rng, W, H, synth.jobs_per_frame(W, H, calls_per_ctu=calls), 4, [0, 1, 2, 3], [0],
+                               bipred_frac=bipred)
+    return synth.make_ctu_jobs(rng, W, H, calls, 4, [0, 1, 2, 3], [0], bipred_frac=bipred)
 
 
 _CPU = {}   # set before forking the all-cores workers
@@ -90,11 +105,13 @@ def _cpu_reference():
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     from oracle import Reference
     from nnfme import weights
-    ref = Reference(use_hadamard=1, nn_mode=1, fast_inter_mode=1)
+    ref = Reference(use_hadamard=1, nn_mode=_CPU.get("nn", 1), fast_inter_mode=1)
     for k, v in _CPU["pics"].items():
         ref.set_picture(k, v)
     ref.set_lambda(0, synth.LDP_LAMBDA[QP][1])
     ref.load_nn(weights.load_weights(QP))
+    if _CPU.get("keys") is not None:
+        ref.set_keys(_CPU["keys"])
     return ref
 
 
@@ -216,28 +233,39 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample length")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-mc", action="store_true", help="skip the motion-compensation leg")
+    ap.add_argument("--workload", choices=sorted(WORKLOADS), default="c3_qp22",
+                    help="BASELINE.json config to run (default: the headline configs[2] at QP22)")
     ap.add_argument("--jobs", choices=("ctu", "uniform"), default="ctu",
                     help="job stream: HM CTU order (default) or uniformly scattered PUs (stress)")
     ap.add_argument("--cpu-cores", type=int, default=0,
                     help="cores for cpu_baseline_all_cores (0: all available, at most 16; -1: skip)")
     args = ap.parse_args()
 
+    global W, H, QP, METRIC
+    W, H, QP, NN, CALLS, _, BIPRED, WDESC = WORKLOADS[args.workload]
+    if args.workload != "c3_qp22":
+        METRIC = f"sub-pel PU refinements/sec @ {args.workload}: {WDESC.split(',')[0]}; bit-exact MV/SATD vs HM"
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
 
     # ---- inputs (untimed): jobs of this rank's frames ----------------------------------------
-    jobs = make_frame_jobs(1000 + rank, args.jobs)
+    jobs = make_frame_jobs(1000 + rank, args.jobs, CALLS, BIPRED)
     n = len(jobs)
+    keys = None
+    if BIPRED > 0:   # bi-pred key blocks (2*org - pred_other), resident with the jobs
+        kpics = {k: synth.synth_luma(W, H, t) for k, t in zip(range(5), (7, 6, 5, 4, 0))}
+        keys = synth.make_bipred_keys_fast(np.random.default_rng(77 + rank), jobs, kpics)
 
     # ---- CPU baselines first, before anything touches the GPU (fork-safe) -------------------
     cpu = {}
+    _CPU["nn"], _CPU["keys"] = NN, keys
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         pics = {k: synth.synth_luma(W, H, t) for k, t in zip(range(5), (7, 6, 5, 4, 0))}
         rate, dt, done = cpu_baseline(jobs, pics, args.cpu_seconds)
         cpu["cpu_baseline"] = {
             "value": rate, "unit": "PU/s", "cores": 1, "kind": "reference",
-            "sample": f"{done} jobs ({done / n:.2f} passes over the same 1080p QP22 frame batch, "
+            "sample": f"{done} jobs ({done / n:.2f} passes over the same {args.workload} frame batch, "
                       f"HM order) on one host core, {dt:.1f} s; oracle/_ref = the reference's "
                       f"TLibCommon (interpolation, RdCost) -O2 driven in TEncSearch order, NN "
                       f"restated scalar",
@@ -275,7 +303,9 @@ def main():
         pool = torch.stack([torch.from_numpy(synth.synth_luma(W, H, t)) for t in range(8)]).to(dev)
     ring = PictureRing(W, H, slots=world + 4, device=dev, world=world, owner=0)
 
-    ctx = FmeContext(device=local, use_hadamard=1, nn_mode=1, qp=QP, fast_inter_mode=1, max_jobs=n)
+    ctx = FmeContext(device=local, use_hadamard=1, nn_mode=NN, qp=QP, fast_inter_mode=1, max_jobs=n)
+    if keys is not None:
+        ctx.set_keys(keys)
     for lid, lam in enumerate(synth.LDP_LAMBDA[QP]):
         ctx.set_lambda(lid, lam)
     # lambda slot 0 is rewritten per step to the frame's POC % 4 value
@@ -348,7 +378,7 @@ def main():
         pcie = {"value": n / dt, "unit": "PU/s", "ms_per_step": dt * 1e3,
                 "note": "jobs H2D + org frame H2D + refine + results D2H, pinned host buffers"}
 
-    mc = mc_leg(dev, stream, reps=max(5, args.steps)) if rank == 0 and not args.no_mc else None
+    mc = mc_leg(dev, stream, reps=max(5, args.steps)) if rank == 0 and not args.no_mc and W == 1920 else None
 
     value = world * n * args.steps / elapsed
     if rank == 0:
@@ -373,8 +403,10 @@ def main():
             "dtype": "int16/int32 (NN f32)",
             "data": "synthetic (SURVEY.md §8(d) YUV generator + PU-size mix; reference per-QP "
                     "NN weights, no random init)",
-            "config": {"workload": "1920x1080 lowdelay_P QP22, NN_pred 2-layer on, 4 refs, "
-                                   "862920 PU jobs per frame (configs[2] at QP22)",
+            "config": {"workload": WDESC if args.workload != "c3_qp22" else
+                       "1920x1080 lowdelay_P QP22, NN_pred 2-layer on, 4 refs, "
+                       "862920 PU jobs per frame (configs[2] at QP22)",
+                       "workload_id": args.workload,
                        "job_stream": args.jobs,
                        "jobs_per_step_per_gpu": n, "parallelism": f"frame-sharded x{world}"},
             "roofline": {

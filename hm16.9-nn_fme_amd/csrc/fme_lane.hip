@@ -149,6 +149,32 @@ __device__ __forceinline__ void vpairs(int f, int o, uint32_t (&c)[5]) {
   for (int t = 0; t < 5; t++) c[t] = p16(tap(f, 2 * t - o), tap(f, 2 * t + 1 - o));
 }
 
+// ---- the key block (key - 128 as packed int16 row pairs): K(x, j) = rows (2j, 2j+1) of column x --
+// In registers, or (FME_LANE_KLDS) in LDS at [(x*UJ + j) / 4][lane][(x*UJ + j) % 4] dwords: 16-byte
+// groups of consecutive lanes are contiguous (conflict-free ds_read_b128) and the key's VGPRs
+// are freed for occupancy.
+#ifndef FME_LANE_KLDS
+#define FME_LANE_KLDS 0
+#endif
+template <int UW, int UJ>
+struct KeySrc {
+#if FME_LANE_KLDS
+  uint32_t* lds;   // this lane's base: &klds[lane * 4]
+  __device__ __forceinline__ uint32_t at(int x, int j) const {
+    const int e = x * UJ + j;
+    return lds[(e >> 2) * (kLaneNT * 4) + (e & 3)];
+  }
+  __device__ __forceinline__ void set(int x, int j, uint32_t v) {
+    const int e = x * UJ + j;
+    lds[(e >> 2) * (kLaneNT * 4) + (e & 3)] = v;
+  }
+#else
+  uint32_t k[UW][UJ];
+  __device__ __forceinline__ uint32_t at(int x, int j) const { return k[x][j]; }
+  __device__ __forceinline__ void set(int x, int j, uint32_t v) { k[x][j] = v; }
+#endif
+};
+
 // ---- distortion of one unit for one candidate ------------------------------------------------
 // X[c][j]: key - pred, column c, rows (2j, 2j+1) packed.  Sum over the unit's T x T tiles of
 // xCalcHADs (had) or SAD.
@@ -212,7 +238,7 @@ __device__ __forceinline__ void take_qtr(int i, uint32_t part, double ml, int mv
 
 // (0,0), (0,-1), (0,1)
 template <int UW, int UH, int T>
-__device__ __forceinline__ void half_center(uint32_t (&v)[UH + 8][UW / 4 + 2], const uint32_t (&K)[UW][UH / 2],
+__device__ __forceinline__ void half_center(uint32_t (&v)[UH + 8][UW / 4 + 2], const KeySrc<UW, UH / 2>& K,
                                             bool had, uint32_t (&d)[3]) {
   constexpr int RV = UH + 8, UJ = UH / 2;
   uint32_t c2lo, c2hi;
@@ -223,7 +249,7 @@ __device__ __forceinline__ void half_center(uint32_t (&v)[UH + 8][UW / 4 + 2], c
     for (int x = 0; x < UW; x++)
 #pragma unroll
       for (int jj = 0; jj < UJ; jj++)
-        X[x][jj] = pk_sub(K[x][jj], sext_pair(v[5 + 2 * jj][(x + 4) >> 2], v[4 + 2 * jj][(x + 4) >> 2], (x + 4) & 3));
+        X[x][jj] = pk_sub(K.at(x, jj), sext_pair(v[5 + 2 * jj][(x + 4) >> 2], v[4 + 2 * jj][(x + 4) >> 2], (x + 4) & 3));
     d[0] = unit_dist<UW, UH, T>(X, had);
   }
   launder(v);
@@ -253,8 +279,8 @@ __device__ __forceinline__ void half_center(uint32_t (&v)[UH + 8][UW / 4 + 2], c
         }
 #pragma unroll
         for (int jj = 0; jj < UJ; jj++) {
-          if (sel & 1) X1[x][jj] = pk_sub(K[x][jj], pack2(v1[2 * jj], v1[2 * jj + 1]));
-          if (sel & 2) X2[x][jj] = pk_sub(K[x][jj], pack2(v1[2 * jj + 1], v1[2 * jj + 2]));
+          if (sel & 1) X1[x][jj] = pk_sub(K.at(x, jj), pack2(v1[2 * jj], v1[2 * jj + 1]));
+          if (sel & 2) X2[x][jj] = pk_sub(K.at(x, jj), pack2(v1[2 * jj + 1], v1[2 * jj + 2]));
         }
         __builtin_amdgcn_sched_barrier(0);
       }
@@ -273,7 +299,7 @@ __device__ __forceinline__ void half_center(uint32_t (&v)[UH + 8][UW / 4 + 2], c
 
 // (s,0), (s,-1), (s,1) for s = -1 (SIDE 0: half column x) or +1 (SIDE 1: half column x+1)
 template <int UW, int UH, int T, int SIDE>
-__device__ __forceinline__ void half_side(uint32_t (&v)[UH + 8][UW / 4 + 2], const uint32_t (&K)[UW][UH / 2],
+__device__ __forceinline__ void half_side(uint32_t (&v)[UH + 8][UW / 4 + 2], const KeySrc<UW, UH / 2>& K,
                                           bool had, uint32_t (&d)[3]) {
   constexpr int RV = UH + 8, UJ = UH / 2;
   uint32_t c2lo, c2hi;
@@ -289,7 +315,7 @@ __device__ __forceinline__ void half_side(uint32_t (&v)[UH + 8][UW / 4 + 2], con
       for (int y = 0; y < UH; y++)
         h1[y] = clamp_s8(dot4(rbytes(v[y + 4], jc + 4), c2hi, dot4(rbytes(v[y + 4], jc), c2lo, 32)) >> 6);
 #pragma unroll
-      for (int jj = 0; jj < UJ; jj++) X[x][jj] = pk_sub(K[x][jj], pack2(h1[2 * jj], h1[2 * jj + 1]));
+      for (int jj = 0; jj < UJ; jj++) X[x][jj] = pk_sub(K.at(x, jj), pack2(h1[2 * jj], h1[2 * jj + 1]));
     }
     d[0] = unit_dist<UW, UH, T>(X, had);
   }
@@ -326,8 +352,8 @@ __device__ __forceinline__ void half_side(uint32_t (&v)[UH + 8][UW / 4 + 2], con
       }
 #pragma unroll
       for (int jj = 0; jj < UJ; jj++) {
-        if (sel & 1) XB[x][jj] = pk_sub(K[x][jj], pack2(v2[2 * jj], v2[2 * jj + 1]));
-        if (sel & 2) XC[x][jj] = pk_sub(K[x][jj], pack2(v2[2 * jj + 1], v2[2 * jj + 2]));
+        if (sel & 1) XB[x][jj] = pk_sub(K.at(x, jj), pack2(v2[2 * jj], v2[2 * jj + 1]));
+        if (sel & 2) XC[x][jj] = pk_sub(K.at(x, jj), pack2(v2[2 * jj + 1], v2[2 * jj + 2]));
       }
       __builtin_amdgcn_sched_barrier(0);   // one column at a time (register pressure)
     }
@@ -361,7 +387,7 @@ __host__ __device__ constexpr int qp_idx0(int ps) { return q9_index(qp_k(ps) - 1
 __host__ __device__ constexpr int qp_idx1(int ps) { return qp_l1(ps) < 0 ? -1 : q9_index(qp_k(ps) - 1, qp_l1(ps) - 1); }
 
 template <int UW, int UH, int T, int PS>
-__device__ __forceinline__ void qtr_pass(uint32_t (&v)[UH + 8][UW / 4 + 2], const uint32_t (&K)[UW][UH / 2],
+__device__ __forceinline__ void qtr_pass(uint32_t (&v)[UH + 8][UW / 4 + 2], const KeySrc<UW, UH / 2>& K,
                                          bool had, int hx, int hy, uint32_t (&d)[2]) {
   constexpr int RV = UH + 8, UJ = UH / 2;
   constexpr int k = qp_k(PS);
@@ -403,7 +429,7 @@ __device__ __forceinline__ void qtr_pass(uint32_t (&v)[UH + 8][UW / 4 + 2], cons
         vq[y] = clamp_s8(acc >> 12);
       }
 #pragma unroll
-      for (int jj = 0; jj < UJ; jj++) XQ[m][x][jj] = pk_sub(K[x][jj], pack2(vq[2 * jj], vq[2 * jj + 1]));
+      for (int jj = 0; jj < UJ; jj++) XQ[m][x][jj] = pk_sub(K.at(x, jj), pack2(vq[2 * jj], vq[2 * jj + 1]));
     }
     __builtin_amdgcn_sched_barrier(0);   // one column at a time (register pressure)
   }
@@ -412,7 +438,7 @@ __device__ __forceinline__ void qtr_pass(uint32_t (&v)[UH + 8][UW / 4 + 2], cons
 }
 
 template <int L, int UW, int UH, int T, int... PS>
-__device__ __forceinline__ void qtr_all(uint32_t (&v)[UH + 8][UW / 4 + 2], const uint32_t (&K)[UW][UH / 2],
+__device__ __forceinline__ void qtr_all(uint32_t (&v)[UH + 8][UW / 4 + 2], const KeySrc<UW, UH / 2>& K,
                                         bool had, int hx, int hy, double ml, int mvx, int mvy, int px, int py,
                                         uint32_t& best, int& bi, std::integer_sequence<int, PS...>) {
   auto one = [&](auto ps_c) {
@@ -466,7 +492,7 @@ __device__ __forceinline__ void load_row(const uint8_t* row, int xb, int width, 
 template <int PW, int PH, int UW, int UH>
 __device__ __forceinline__ void lane_unit(const BatchArgs& a, const fme_job* __restrict__ sjobs,
                                           const int32_t* __restrict__ perm, int cls_off, int cls_cnt,
-                                          int blk) {
+                                          int blk, uint32_t* klds) {
   constexpr int T = ((PW % 8) == 0 && (PH % 8) == 0) ? 8 : 4;
   static_assert(UW % T == 0 && UH % T == 0, "unit must hold whole SATD tiles");
   constexpr int UX = PW / UW, L = UX * (PH / UH);
@@ -679,7 +705,10 @@ __device__ __forceinline__ void lane_unit(const BatchArgs& a, const fme_job* __r
   }
 
   // ---- key as signed int16 (key - 128) pairs: K[c][j] = (row 2j, row 2j+1) of column c ------------
-  uint32_t K[UW][UJ];
+  KeySrc<UW, UJ> K;
+#if FME_LANE_KLDS
+  K.lds = klds + threadIdx.x * 4;
+#endif
 #pragma unroll
   for (int c = 0; c < UW; c++)
 #pragma unroll
@@ -687,7 +716,7 @@ __device__ __forceinline__ void lane_unit(const BatchArgs& a, const fme_job* __r
       const uint32_t ko = sext_pair(kraw[2 * jj + 1][c >> 2], kraw[2 * jj][c >> 2], c & 3);
       const uint32_t hs = (c & 1) ? 0x07060302u : 0x05040100u;   // 16-bit half c&1 of each row
       const uint32_t kb = pk_sub(__builtin_amdgcn_perm(kraw[2 * jj + 1][c >> 1], kraw[2 * jj][c >> 1], hs), 0x00800080u);
-      K[c][jj] = kbuf ? kb : ko;
+      K.set(c, jj, kbuf ? kb : ko);
     }
 
   // ---- 3. half-pel stage (H9 order: (0,0),(0,-1),(0,1),(-1,0),(1,0),(-1,-1),(1,-1),(-1,1),(1,1)) ---
@@ -696,8 +725,8 @@ __device__ __forceinline__ void lane_unit(const BatchArgs& a, const fme_job* __r
   uint32_t hbest = 0xFFFFFFFFu;
   int hbi = 9;
   {
-    uint32_t d[3];
-    half_center<UW, UH, T>(v, K, had, d);
+    uint32_t d[3] = {0u, 0u, 0u};
+    if (!(FME_LANE_SKIP & 8)) half_center<UW, UH, T>(v, K, had, d);
     take_half<L>(0, d[0], ml, mvx, mvy, mvp_x, mvp_y, hbest, hbi);
     take_half<L>(1, d[1], ml, mvx, mvy, mvp_x, mvp_y, hbest, hbi);
     take_half<L>(2, d[2], ml, mvx, mvy, mvp_x, mvp_y, hbest, hbi);
@@ -762,11 +791,13 @@ __device__ __forceinline__ int xcd_block(int r, int n) {
 
 #define FME_CASE(ID, PW_, PH_, UW_, UH_)                                                             \
   case ID:                                                                                           \
-    lane_unit<PW_, PH_, UW_, UH_>(a, w.sjobs, w.perm, sc.class_off[ID], sc.class_cnt[ID], blk);      \
+    lane_unit<PW_, PH_, UW_, UH_>(a, w.sjobs, w.perm, sc.class_off[ID], sc.class_cnt[ID], blk, klds); \
     break;
 #define FME_LANE_KERNEL(NAME, KID, LIST, WAVES)                                                      \
   __global__ __launch_bounds__(kLaneNT) __attribute__((amdgpu_waves_per_eu(WAVES)))                 \
   void NAME(BatchArgs a, WorkBufs w, Schedule sc) {                                                  \
+    __shared__ uint32_t klds_[FME_LANE_KLDS ? 8 * kLaneNT * 4 : 1];                                  \
+    uint32_t* klds = klds_;                                                                          \
     const int b = blockIdx.x;                                                                        \
     int c = 0;                                                                                       \
     while (c < kNumClasses - 1 && b >= sc.prefix[KID][c + 1]) c++;                                   \
