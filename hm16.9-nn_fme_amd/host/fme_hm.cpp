@@ -129,6 +129,68 @@ void FracSearch::setLambdaSlot(int lambdaId, double lambda) {
   check(fme_set_lambda(ctx_, lambdaId, lambda), "fme_set_lambda");
 }
 
+// ---- MotionCompensator ---------------------------------------------------------------------
+
+void MotionCompensator::setPictureYuv(int id, const Pel* y, int ys, const Pel* cb, const Pel* cr, int cs, int width,
+                                      int height) {
+  const int cw = width / 2, ch = height / 2;
+  stage_.resize((size_t)width * height + 2 * (size_t)cw * ch);
+  auto to8 = [&](const Pel* src, int stride, int w, int h, uint8_t* dst) {
+    for (int r = 0; r < h; r++)
+      for (int c = 0; c < w; c++) {
+        const int v = src[(ptrdiff_t)r * stride + c];
+        if (v < 0 || v > 255) throw Error(FME_E_UNSUPPORTED, "setPictureYuv: sample outside 8-bit range");
+        dst[(size_t)r * w + c] = (uint8_t)v;
+      }
+  };
+  uint8_t* dy = stage_.data();
+  uint8_t* dcb = dy + (size_t)width * height;
+  uint8_t* dcr = dcb + (size_t)cw * ch;
+  to8(y, ys, width, height, dy);
+  to8(cb, cs, cw, ch, dcb);
+  to8(cr, cs, cw, ch, dcr);
+  setPictureYuv8(id, dy, width, dcb, dcr, cw, width, height);
+}
+
+void MotionCompensator::setPictureYuv8(int id, const uint8_t* y, int ys, const uint8_t* cb, const uint8_t* cr, int cs,
+                                       int width, int height) {
+  std::lock_guard<std::mutex> lk(search_.mutex());
+  check(fme_set_picture(search_.ctx(), id, y, ys, width, height, nullptr), "fme_set_picture");
+  check(fme_set_picture_chroma(search_.ctx(), id, cb, cr, cs, nullptr), "fme_set_picture_chroma");
+}
+
+void MotionCompensator::add(int x, int y, int w, int h, int cuX, int cuY, int refIdL0, const Mv& mvL0, int refIdL1,
+                            const Mv& mvL1) {
+  fme_mc_job j = {};
+  j.x = (uint16_t)x;
+  j.y = (uint16_t)y;
+  j.w = (uint8_t)w;
+  j.h = (uint8_t)h;
+  j.cu_x = (uint16_t)cuX;
+  j.cu_y = (uint16_t)cuY;
+  if (refIdL0 >= 0) {
+    j.flags |= FME_MC_L0;
+    j.ref_id[0] = (uint8_t)refIdL0;
+    j.mv[0][0] = (int16_t)mvL0.hor;
+    j.mv[0][1] = (int16_t)mvL0.ver;
+  }
+  if (refIdL1 >= 0) {
+    j.flags |= FME_MC_L1;
+    j.ref_id[1] = (uint8_t)refIdL1;
+    j.mv[1][0] = (int16_t)mvL1.hor;
+    j.mv[1][1] = (int16_t)mvL1.ver;
+  }
+  jobs_.push_back(j);
+}
+
+void MotionCompensator::run(uint8_t* y, int ys, uint8_t* cb, uint8_t* cr, int cs, int width, int height) {
+  std::lock_guard<std::mutex> lk(search_.mutex());
+  check(fme_motion_compensate(search_.ctx(), jobs_.data(), (int)jobs_.size(), y, ys, cb, cr, cs, width, height,
+                              nullptr),
+        "fme_motion_compensate");
+  jobs_.clear();
+}
+
 // ---- CtuRowBatcher -----------------------------------------------------------------------
 
 CtuRowBatcher::CtuRowBatcher(FracSearch& search, int maxRowsInFlight)

@@ -105,6 +105,30 @@ class FracSearch {
   std::mutex mu_;
 };
 
+// TComPrediction::motionCompensation-shaped surface (TComPrediction.cpp:495-668) over the
+// FracSearch's context: pictures with 4:2:0 chroma, one fme_mc_job per PU (the CU's
+// TComCUMvField entries for the partition, unclipped, plus the CU origin for clipMv), and
+// a batch predicted into caller planes.  PUs of a batch must not overlap.
+class MotionCompensator {
+ public:
+  explicit MotionCompensator(FracSearch& search) : search_(search) {}
+  // A reconstructed reference picture (TComPicYuv planes at the picture origin).
+  void setPictureYuv(int id, const Pel* y, int yStride, const Pel* cb, const Pel* cr, int cStride, int width,
+                     int height);
+  void setPictureYuv8(int id, const uint8_t* y, int yStride, const uint8_t* cb, const uint8_t* cr, int cStride,
+                      int width, int height);
+  // Queue one PU: uni-pred when only one of mvL0 / mvL1 is given (refIdL* < 0 for the other).
+  void add(int x, int y, int w, int h, int cuX, int cuY, int refIdL0, const Mv& mvL0, int refIdL1, const Mv& mvL1);
+  int pending() const { return (int)jobs_.size(); }
+  // Predict every queued PU into the 8-bit planes (width x height luma) and clear the queue.
+  void run(uint8_t* y, int yStride, uint8_t* cb, uint8_t* cr, int cStride, int width, int height);
+
+ private:
+  FracSearch& search_;
+  std::vector<fme_mc_job> jobs_;
+  std::vector<uint8_t> stage_;
+};
+
 // Per-CTU-row batch producer (double-buffered: the caller fills row k+1 while row k runs).
 class CtuRowBatcher {
  public:

@@ -235,10 +235,65 @@ static int run() {
     EXPECT(2 * xh + xq == cls % 7 - 3 && 2 * yh + yq == cls / 7 - 3, "NN_pred offsets %d", k);
   }
 
+  // ---- MotionCompensator: one CTU-quadtree partition of the frame, uni + bi, against orc_mc --------
+  int mc_pus = 0;
+  {
+    fme_hm::MotionCompensator mc(search);
+    std::vector<std::vector<int16_t>> cbs, crs;
+    orc_yuv yuv[FME_MAX_PICTURES] = {};
+    std::vector<std::vector<uint8_t>> y8(3), cb8(3), cr8(3);
+    for (int i = 0; i < 3; i++) {
+      std::vector<int16_t> cb((size_t)(W / 2) * (H / 2)), cr(cb.size());
+      for (int y = 0; y < H / 2; y++)
+        for (int x = 0; x < W / 2; x++) {   // chroma: subsampled luma of another frame, flipped
+          cb[(size_t)y * (W / 2) + x] = pics[(i + 1) % 5][(size_t)(2 * y) * W + 2 * x];
+          cr[(size_t)y * (W / 2) + x] = (int16_t)(255 - pics[(i + 2) % 5][(size_t)(2 * y + 1) * W + 2 * x + 1]);
+        }
+      mc.setPictureYuv(10 + i, pics[i].data(), W, cb.data(), cr.data(), W / 2, W, H);
+      y8[i].assign(pics[i].begin(), pics[i].end());
+      cb8[i].assign(cb.begin(), cb.end());
+      cr8[i].assign(cr.begin(), cr.end());
+      yuv[10 + i] = orc_yuv{y8[i].data(), cb8[i].data(), cr8[i].data(), W, W / 2, W, H};
+    }
+    std::vector<fme_mc_job> jobs;
+    std::mt19937 rng(99);
+    for (int cy = 0; cy < H; cy += 16)   // 16x16 CUs: 2Nx2N, 2NxN or Nx2N
+      for (int cx = 0; cx < W; cx += 16) {
+        const int mode = (int)(rng() % 3);
+        const int parts = mode == 0 ? 1 : 2;
+        for (int p = 0; p < parts; p++) {
+          const int pw = mode == 2 ? 8 : 16, ph = mode == 1 ? 8 : 16;
+          const int px = cx + (mode == 2 ? 8 * p : 0), py = cy + (mode == 1 ? 8 * p : 0);
+          const bool bi = rng() % 3 == 0;
+          fme_hm::Mv m0((int)(rng() % 257) - 128, (int)(rng() % 257) - 128), m1((int)(rng() % 257) - 128, (int)(rng() % 257) - 128);
+          const int r0 = 10 + (int)(rng() % 3), r1 = 10 + (int)(rng() % 3);
+          mc.add(px, py, pw, ph, cx, cy, r0, m0, bi ? r1 : -1, m1);
+          fme_mc_job j = {};
+          j.x = (uint16_t)px; j.y = (uint16_t)py; j.w = (uint8_t)pw; j.h = (uint8_t)ph;
+          j.cu_x = (uint16_t)cx; j.cu_y = (uint16_t)cy;
+          j.flags = FME_MC_L0 | (bi ? FME_MC_L1 : 0);
+          j.ref_id[0] = (uint8_t)r0; j.ref_id[1] = (uint8_t)(bi ? r1 : 0);
+          j.mv[0][0] = (int16_t)m0.hor; j.mv[0][1] = (int16_t)m0.ver;
+          if (bi) { j.mv[1][0] = (int16_t)m1.hor; j.mv[1][1] = (int16_t)m1.ver; }
+          jobs.push_back(j);
+        }
+      }
+    mc_pus = (int)jobs.size();
+    std::vector<uint8_t> gy((size_t)W * H), gcb((size_t)W * H / 4), gcr(gcb.size());
+    std::vector<uint8_t> oy(gy.size()), ocb(gcb.size()), ocr(gcb.size());
+    mc.run(gy.data(), W, gcb.data(), gcr.data(), W / 2, W, H);
+    EXPECT(mc.pending() == 0, "MotionCompensator queue not cleared");
+    EXPECT(orc_mc(yuv, jobs.data(), (int)jobs.size(), oy.data(), W, ocb.data(), ocr.data(), W / 2, W, H) == 0,
+           "orc_mc rejected the jobs");
+    EXPECT(gy == oy, "MotionCompensator luma differs from orc_mc");
+    EXPECT(gcb == ocb && gcr == ocr, "MotionCompensator chroma differs from orc_mc");
+  }
+
   if (failures) {
     fprintf(stderr, "hm adapter: %d failure(s)\n", failures);
     return 1;
   }
+  printf("hm adapter ok: %d PU motion compensations (Y/Cb/Cr) bit-exact\n", mc_pus);
   printf("hm adapter ok: %d jobs in %d CTU rows, %d single-PU FracDIF calls, 100 NN_pred calls bit-exact\n",
          total, rows, singles);
   return 0;
