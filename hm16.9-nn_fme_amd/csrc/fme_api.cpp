@@ -102,6 +102,11 @@ struct fme_ctx {
   DevBuf<int32_t> d_mc_invalid;
   hipEvent_t ev_mc[2] = {nullptr, nullptr};
   bool mc_timed = false;
+  // integer search: staging for the host entry point, timing events
+  DevBuf<fme_tz_ext> d_tz_ext;
+  DevBuf<uint32_t> d_tz_sad;
+  hipEvent_t ev_tz[2] = {nullptr, nullptr};
+  bool tz_timed = false;
 
   std::unique_ptr<fme_ctx> single;  // private context for the single-PU entry points
   DevBuf<uint8_t> single_pic;
@@ -211,6 +216,9 @@ int fme_destroy(fme_ctx* c) {
   for (int i = 0; i < FME_MAX_PICTURES; i++)
     if (c->chroma_owned[i]) (void)hipFree(c->chroma_owned[i]);
   c->d_mc_jobs.release(); c->d_mc_planes.release(); c->d_mc_invalid.release();
+  c->d_tz_ext.release(); c->d_tz_sad.release();
+  for (auto& e : c->ev_tz)
+    if (e) (void)hipEventDestroy(e);
   for (auto& e : c->ev_mc)
     if (e) (void)hipEventDestroy(e);
   c->d_pics.release(); c->d_mlambda.release(); c->d_keys.release(); c->d_nn.release();
@@ -514,6 +522,103 @@ int fme_refine_device(fme_ctx* c, const fme_job* d_jobs, fme_result* d_res, int 
     c->ev_cur ^= 1;
   }
   if (a.nn_mode) c->state_cur ^= 1;
+  return FME_OK;
+}
+
+// ---- integer motion estimation (xTZSearch / xPatternSearch) -----------------------------------
+// classify (validation + class histogram, one host sync) -> scatter (jobs grouped by PU shape)
+// -> one search launch per unit shape (fme_tz.hip) writing mv_x / mv_y (and ruiSAD) in place.
+int fme_integer_search_device(fme_ctx* c, fme_job* d_jobs, const fme_tz_ext* d_ext, uint32_t* d_sad, int n,
+                              void* stream) {
+  if (!c || (n > 0 && (!d_jobs || !d_ext))) return fail(FME_E_INVALID, "fme_integer_search_device: null argument");
+  if (n < 0) return fail(FME_E_INVALID, "fme_integer_search_device: n = %d", n);
+  if (n == 0) return FME_OK;
+  HIP_TRY(hipSetDevice(c->device));
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  int rc = ensure_work(c, n);
+  if (rc) return rc;
+  rc = sync_tables(c, s);
+  if (rc) return rc;
+  BatchArgs a{};
+  a.jobs = d_jobs;
+  a.keys = c->d_keys.p;
+  a.n_keys = (int64_t)c->n_keys;
+  a.mlambda = c->d_mlambda.p;
+  a.pics = c->d_pics.p;
+  a.n = n;
+  a.use_hadamard = c->cfg.use_hadamard ? 1 : 0;
+  a.fen = c->cfg.fast_inter_mode;
+  WorkBufs w{};
+  w.cls = c->cls.p;
+  w.perm = c->perm.p;
+  w.sjobs = c->sjobs.p;
+  w.counts = c->counts.p;
+  w.cursor = c->counts.p + kNumClasses + 1;
+  w.blk_agg = c->blk_agg.p;
+  w.blk_prefix = c->blk_prefix.p;
+  w.nn_state = c->nn_state.p;
+  if (c->profiling) {
+    if (!c->ev_tz[0]) {
+      HIP_TRY(hipEventCreate(&c->ev_tz[0]));
+      HIP_TRY(hipEventCreate(&c->ev_tz[1]));
+    }
+  }
+  HIP_TRY(hipMemsetAsync(c->counts.p, 0, (2 * kNumClasses + 1) * sizeof(int32_t), s));
+  HIP_TRY(launch_classify(a, w, s));
+  HIP_TRY(hipMemcpyAsync(c->h_counts, c->counts.p, (kNumClasses + 1) * sizeof(int32_t), hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipStreamSynchronize(s));
+  if (c->h_counts[kNumClasses] > 0)
+    return fail(FME_E_INVALID, "fme_integer_search_device: %d job(s) with an unsupported PU size or unset picture/lambda/key",
+                c->h_counts[kNumClasses]);
+  Schedule sc{};
+  int off = 0, nb[3] = {0, 0, 0};
+  for (int k = 0; k < kNumClasses; k++) {
+    const int cnt = c->h_counts[k];
+    sc.class_off[k] = off;
+    sc.class_cnt[k] = cnt;
+    for (int q = 0; q < 3; q++) sc.prefix[q][k] = nb[q];
+    nb[tz_kernel_of(k)] += (int)(((long long)cnt * tz_lanes_per_pu(k) + 255) / 256);
+    off += cnt;
+  }
+  for (int q = 0; q < 3; q++) sc.prefix[q][kNumClasses] = nb[q];
+  HIP_TRY(launch_scatter(a, w, sc, s));
+  TzArgs ta{};
+  ta.a = a;
+  ta.sjobs = c->sjobs.p;
+  ta.perm = c->perm.p;
+  ta.jobs_out = d_jobs;
+  ta.ext = d_ext;
+  ta.sad = d_sad;
+  if (c->profiling) HIP_TRY(hipEventRecord(c->ev_tz[0], s));
+  HIP_TRY(launch_tz(ta, sc, s));
+  if (c->profiling) HIP_TRY(hipEventRecord(c->ev_tz[1], s));
+  c->tz_timed = c->profiling;
+  return FME_OK;
+}
+
+int fme_integer_search(fme_ctx* c, fme_job* jobs, const fme_tz_ext* ext, uint32_t* sad, int n, void* stream) {
+  if (!c || (n > 0 && (!jobs || !ext))) return fail(FME_E_INVALID, "fme_integer_search: null argument");
+  if (n <= 0) return n == 0 ? FME_OK : fail(FME_E_INVALID, "fme_integer_search: n = %d", n);
+  HIP_TRY(hipSetDevice(c->device));
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  HIP_TRY(c->d_jobs.reserve(n));
+  HIP_TRY(c->d_tz_ext.reserve(n));
+  HIP_TRY(c->d_tz_sad.reserve(n));
+  HIP_TRY(hipMemcpyAsync(c->d_jobs.p, jobs, (size_t)n * sizeof(fme_job), hipMemcpyHostToDevice, s));
+  HIP_TRY(hipMemcpyAsync(c->d_tz_ext.p, ext, (size_t)n * sizeof(fme_tz_ext), hipMemcpyHostToDevice, s));
+  int rc = fme_integer_search_device(c, c->d_jobs.p, c->d_tz_ext.p, c->d_tz_sad.p, n, stream);
+  if (rc) return rc;
+  HIP_TRY(hipMemcpyAsync(jobs, c->d_jobs.p, (size_t)n * sizeof(fme_job), hipMemcpyDeviceToHost, s));
+  if (sad) HIP_TRY(hipMemcpyAsync(sad, c->d_tz_sad.p, (size_t)n * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipStreamSynchronize(s));
+  return FME_OK;
+}
+
+int fme_integer_search_last_ms(fme_ctx* c, float* ms) {
+  if (!c || !ms) return fail(FME_E_INVALID, "fme_integer_search_last_ms: null argument");
+  if (!c->tz_timed) return fail(FME_E_STATE, "fme_integer_search_last_ms: no profiled integer search");
+  HIP_TRY(hipEventSynchronize(c->ev_tz[1]));
+  HIP_TRY(hipEventElapsedTime(ms, c->ev_tz[0], c->ev_tz[1]));
   return FME_OK;
 }
 

@@ -40,6 +40,7 @@ struct McArgs {
 };
 hipError_t launch_mc(const McArgs& a, hipStream_t s);
 
+
 // One batch as the device sees it.
 struct BatchArgs {
   const fme_job* jobs;
@@ -79,6 +80,19 @@ struct Schedule {
   int32_t class_off[kNumClasses];
   int32_t class_cnt[kNumClasses];
 };
+
+// One integer-search launch (fme_tz.hip): the batch, its class-ordered copy and the outputs.
+struct TzArgs {
+  BatchArgs a;
+  const fme_job* sjobs;
+  const int32_t* perm;
+  fme_job* jobs_out;          // mv_x / mv_y written per job
+  const fme_tz_ext* ext;
+  uint32_t* sad;              // may be null
+};
+int tz_kernel_of(int cls);    // 0: 4x8 units, 1: 8x4, 2: 8x8
+int tz_lanes_per_pu(int cls);
+hipError_t launch_tz(const TzArgs& ta, const Schedule& sc, hipStream_t s);
 
 // Host-side launch helpers (fme_kernels.hip).
 int pus_per_tile(int cls);

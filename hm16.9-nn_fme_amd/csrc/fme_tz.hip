@@ -1,0 +1,472 @@
+// fme_tz.hip — integer motion estimation on gfx950.
+//
+// xMotionEstimation's integer search (TEncSearch.cpp:4504-4527):
+//   uni-pred  xPatternSearchFast -> xTZSearch (4737-5036) with the shipped settings: FastSearch 1
+//             (diamond, not extended), FastMEAssumingSmootherMV (first search stops 3 rounds after
+//             the best), raster step 5, star refinement; up to, not including, the EMI square step
+//             (that is the first step of the sub-pel kernels);
+//   bi-pred   xPatternSearch (4627-4680): every point of the range in raster order.
+// Helpers restated: xTZSearchHelp's normal branch (1078-1188), xTZ8PointDiamondSearch (1379-1589),
+// xTZ2PointSearch (1191-1322), xSetSearchRange (4602-4624), TComDataCU::clipMv
+// (TComDataCU.cpp:2773-2786), TComMv::divideByPowerOf2 (TComMv.h:122-130).
+//
+// Mapping: one lane per unit of a PU (8x8, 8x4 or 4x8; a PU of W x H has (W/UW)(H/UH) units,
+// the group padded to a power of two), as in fme_lane.hip.  The search is a state machine every
+// lane of a group steps in lock-step: it yields the next candidate the reference would test (range
+// checks and phase changes without a test are folded into the step), the group sums its units'
+// distortions with DPP, and every lane applies xTZSearchHelp's update.  Groups of one wave advance
+// together; a finished group idles until the wave's last group is done.
+// Metric (the NN_FME integer-ME setDistParam, TComRdCost.cpp:200-230): SSE for widths 4..64, SAD
+// for 12/24/48 with the FEN even-row subsampling when H > 8; uni-pred keys as (s - 128) bytes
+// (SSE = Sk2 - 2 Sks + Sss with v_dot4_i32_i8, SAD with v_sad_u8), bi-pred keys (2 org - pred,
+// int16) as packed pairs.
+#include <hip/hip_runtime.h>
+
+#include "fme_device.h"
+#include "fme_simd.h"
+
+namespace fme {
+namespace {
+using namespace simd;
+
+constexpr int kTzNT = 256;
+
+template <int CTRL>
+__device__ __forceinline__ uint32_t dpp(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, CTRL, 0xF, 0xF, true);
+}
+// Sum over the L lanes of a group (L a power of two <= 64, uniform over the workgroup).
+__device__ __forceinline__ uint32_t group_sum(uint32_t v, int L) {
+  if (L >= 2) v += dpp<0xB1>(v);    // quad_perm [1,0,3,2]
+  if (L >= 4) v += dpp<0x4E>(v);    // quad_perm [2,3,0,1]
+  if (L >= 8) v += dpp<0x141>(v);   // row_half_mirror
+  if (L >= 16) v += dpp<0x140>(v);  // row_mirror
+  if (L >= 32) v += (uint32_t)__builtin_amdgcn_ds_swizzle((int)v, 0x401F);
+  if (L >= 64) v += (uint32_t)__shfl_xor((int)v, 32, 64);
+  return v;
+}
+
+__device__ __forceinline__ int round4(int v) { return (v + 2) >> 2; }   // divideByPowerOf2(2)
+
+__device__ __forceinline__ void clip_qpel(int& x, int& y, int pw, int ph, int cu_x, int cu_y) {
+  x = min((pw + 8 - cu_x - 1) << 2, max((-64 - 8 - cu_x + 1) * 4, x));
+  y = min((ph + 8 - cu_y - 1) << 2, max((-64 - 8 - cu_y + 1) * 4, y));
+}
+
+struct Range {
+  int l, r, t, b;
+};
+
+enum Phase {
+  P_START, P_ZERO, P_PRED, P_RANGE, P_FIRST, P_TWO1, P_TWO, P_RASTER_CHK, P_RASTER, P_STAR_CHK, P_STAR,
+  P_STAR_END, P_FULL, P_DONE
+};
+
+struct Tz {
+  // IntTZSearchStruct
+  uint32_t best_sad;
+  int bx, by, bdist, bround, pnr;
+  // state machine
+  int phase, ret;
+  int sx, sy;           // rounded start (the AMVP predictor)
+  int px, py;           // 2Nx2N integer MV
+  bool has_pred;
+  int ox, oy;           // origin of the running diamond / two-point search
+  int dist, k, opnr;
+  int rx, ry;           // raster iterators
+  Range R, RR;          // search range, raster range
+  int range;            // m_iSearchRange
+};
+
+// Point k of xTZ8PointDiamondSearch(origin, dist) in call order, with the range check the
+// reference applies before testing it (the "inside" fast path tests the same points in the same
+// order, and every per-point check holds there).  Returns false past the last point.
+__device__ __forceinline__ bool diamond_point(const Tz& s, int k, bool& ok, int& x, int& y, int& pnr, int& pd) {
+  const int d = s.dist, ox = s.ox, oy = s.oy;
+  const Range& R = s.R;
+  if (d == 1) {
+    if (k >= 4) return false;
+    const int dx = k == 1 ? -1 : (k == 2 ? 1 : 0), dy = k == 0 ? -1 : (k == 3 ? 1 : 0);
+    x = ox + dx;
+    y = oy + dy;
+    pnr = k == 0 ? 2 : (k == 1 ? 4 : (k == 2 ? 5 : 7));
+    pd = 1;
+    ok = (dy < 0 ? y >= R.t : true) && (dy > 0 ? y <= R.b : true) && (dx < 0 ? x >= R.l : true) &&
+         (dx > 0 ? x <= R.r : true);
+    return true;
+  }
+  if (d <= 8) {
+    if (k >= 8) return false;
+    const int h = d >> 1;
+    // 2:(0,-d) 1:(-h,-h) 3:(h,-h) 4:(-d,0) 5:(d,0) 6:(-h,h) 8:(h,h) 7:(0,d)
+    const int dx = k == 0 || k == 7 ? 0 : (k == 1 || k == 5 ? -h : (k == 2 || k == 6 ? h : (k == 3 ? -d : d)));
+    const int dy = k == 0 ? -d : (k == 7 ? d : (k == 1 || k == 2 ? -h : (k == 5 || k == 6 ? h : 0)));
+    const int nr[8] = {2, 1, 3, 4, 5, 6, 8, 7};
+    pnr = nr[k];
+    pd = (k == 1 || k == 2 || k == 5 || k == 6) ? h : d;
+    x = ox + dx;
+    y = oy + dy;
+    ok = (dy < 0 ? y >= R.t : true) && (dy > 0 ? y <= R.b : true) && (dx < 0 ? x >= R.l : true) &&
+         (dx > 0 ? x <= R.r : true);
+    return true;
+  }
+  if (k >= 16) return false;
+  pnr = 0;
+  pd = d;
+  if (k < 4) {
+    const int dx = k == 1 ? -d : (k == 2 ? d : 0), dy = k == 0 ? -d : (k == 3 ? d : 0);
+    x = ox + dx;
+    y = oy + dy;
+    ok = (dy < 0 ? y >= R.t : true) && (dy > 0 ? y <= R.b : true) && (dx < 0 ? x >= R.l : true) &&
+         (dx > 0 ? x <= R.r : true);
+    return true;
+  }
+  const int idx = 1 + ((k - 4) >> 2), m = (k - 4) & 3, q = (d >> 2) * idx;
+  const int yt = oy - d + q, yb = oy + d - q, xl = ox - q, xr = ox + q;
+  x = (m & 1) ? xr : xl;
+  y = (m & 2) ? yb : yt;
+  ok = ((m & 2) ? yb <= R.b : yt >= R.t) && ((m & 1) ? xr <= R.r : xl >= R.l);
+  return true;
+}
+
+// xTZ2PointSearch: the two neighbours of a distance-1 best the diamond did not test.
+__device__ __forceinline__ bool two_point(const Tz& s, int k, bool& ok, int& x, int& y) {
+  if (k >= 2 || s.opnr < 1 || s.opnr > 8) return false;
+  // per point_nr: (dx0, dy0, dx1, dy1), 2-bit codes 0 -> 0, 1 -> -1, 2 -> +1
+  const uint32_t tab[9] = {0u, 0x41u, 0x65u, 0x24u, 0x59u, 0xa6u, 0x81u, 0xa9u, 0x82u};
+  const uint32_t c = (tab[s.opnr] >> (4 * k)) & 0xFu;
+  const int dx = dec(c & 3u), dy = dec(c >> 2);
+  x = s.ox + dx;
+  y = s.oy + dy;
+  ok = (dx < 0 ? x >= s.R.l : true) && (dx > 0 ? x <= s.R.r : true) && (dy < 0 ? y >= s.R.t : true) &&
+       (dy > 0 ? y <= s.R.b : true);
+  return true;
+}
+
+// Next candidate of the search (x, y, point number, distance for xTZSearchHelp); false = done.
+__device__ __forceinline__ bool next_candidate(Tz& s, int pw, int ph, int cu_x, int cu_y, int& x, int& y, int& pnr,
+                                               int& pd) {
+  for (int guard = 0; guard < 64; guard++) {   // phase changes between two tests are bounded
+    switch (s.phase) {
+      case P_START:
+        s.phase = P_ZERO;
+        x = s.sx; y = s.sy; pnr = 0; pd = 0;
+        return true;
+      case P_ZERO:
+        s.phase = P_PRED;
+        if ((s.sx != 0 || s.sy != 0) && (s.bx != 0 || s.by != 0)) {
+          x = 0; y = 0; pnr = 0; pd = 0;
+          return true;
+        }
+        break;
+      case P_PRED:
+        s.phase = P_RANGE;
+        if (s.has_pred && (s.sx != s.px || s.sy != s.py) && (s.px != s.bx || s.py != s.by)) {
+          x = s.px; y = s.py; pnr = 0; pd = 0;
+          return true;
+        }
+        break;
+      case P_RANGE:
+        s.RR = s.R;
+        if (s.has_pred) {   // xSetSearchRange(currBest << 2, m_iSearchRange): raster range only
+          int cx = s.bx * 4, cy = s.by * 4;
+          clip_qpel(cx, cy, pw, ph, cu_x, cu_y);
+          int lx = cx - (s.range << 2), ly = cy - (s.range << 2), rx = cx + (s.range << 2), ry = cy + (s.range << 2);
+          clip_qpel(lx, ly, pw, ph, cu_x, cu_y);
+          clip_qpel(rx, ry, pw, ph, cu_x, cu_y);
+          s.RR = Range{round4(lx), round4(rx), round4(ly), round4(ry)};
+        }
+        s.phase = P_FIRST;
+        s.ox = s.bx; s.oy = s.by; s.dist = 1; s.k = -1;
+        break;
+      case P_FIRST:
+      case P_STAR: {
+        if (s.k < 0) {
+          s.bround += 1;
+          s.k = 0;
+        }
+        bool ok;
+        while (diamond_point(s, s.k, ok, x, y, pnr, pd)) {
+          s.k++;
+          if (ok) return true;
+        }
+        if (s.phase == P_FIRST) {
+          if (s.bround >= 3 || 2 * s.dist > s.range) s.phase = P_TWO1;
+          else { s.dist *= 2; s.k = -1; }
+        } else {
+          if (2 * s.dist > s.range) s.phase = P_STAR_END;
+          else { s.dist *= 2; s.k = -1; }
+        }
+        break;
+      }
+      case P_TWO1:
+        s.phase = P_RASTER_CHK;
+        if (s.bdist == 1) {
+          s.bdist = 0;
+          s.ox = s.bx; s.oy = s.by; s.opnr = s.pnr; s.k = 0;
+          s.ret = P_RASTER_CHK;
+          s.phase = P_TWO;
+        }
+        break;
+      case P_TWO: {
+        bool ok;
+        while (two_point(s, s.k, ok, x, y)) {
+          s.k++;
+          if (ok) {
+            pnr = 0; pd = 2;
+            return true;
+          }
+        }
+        s.phase = s.ret;
+        break;
+      }
+      case P_RASTER_CHK:
+        s.phase = P_STAR_CHK;
+        if (s.bdist > 5) {
+          s.bdist = 5;
+          if (s.RR.l <= s.RR.r && s.RR.t <= s.RR.b) {
+            s.rx = s.RR.l; s.ry = s.RR.t;
+            s.phase = P_RASTER;
+          }
+        }
+        break;
+      case P_RASTER:
+        if (s.ry > s.RR.b) {
+          s.phase = P_STAR_CHK;
+          break;
+        }
+        x = s.rx; y = s.ry; pnr = 0; pd = 5;
+        s.rx += 5;
+        if (s.rx > s.RR.r) { s.rx = s.RR.l; s.ry += 5; }
+        return true;
+      case P_STAR_CHK:
+        if (s.bdist > 0) {
+          s.ox = s.bx; s.oy = s.by; s.bdist = 0; s.pnr = 0; s.dist = 1; s.k = -1;
+          s.phase = P_STAR;
+        } else {
+          s.phase = P_DONE;
+        }
+        break;
+      case P_STAR_END:
+        s.phase = P_STAR_CHK;
+        if (s.bdist == 1) {
+          s.bdist = 0;
+          if (s.pnr != 0) {
+            s.ox = s.bx; s.oy = s.by; s.opnr = s.pnr; s.k = 0;
+            s.ret = P_STAR_CHK;
+            s.phase = P_TWO;
+          }
+        }
+        break;
+      case P_FULL:   // xPatternSearch: raster order over the whole range
+        if (s.ry > s.R.b || s.R.l > s.R.r) {
+          s.phase = P_DONE;
+          break;
+        }
+        x = s.rx; y = s.ry; pnr = 0; pd = 0;
+        if (++s.rx > s.R.r) { s.rx = s.R.l; s.ry++; }
+        return true;
+      default:
+        return false;
+    }
+  }
+  return false;
+}
+
+// One lane: unit (ux, uy) of a PU of class geometry (PW x PH, units UW x UH).
+template <int UW, int UH>
+__device__ __forceinline__ void tz_unit(const TzArgs& ta, int cls_off, int cls_cnt, int blk, int PW, int PH) {
+  const BatchArgs& a = ta.a;
+  const int UX = PW / UW, LR = UX * (PH / UH);
+  int L = 1;
+  while (L < LR) L <<= 1;
+  const int gl = blk * kTzNT + (int)threadIdx.x;
+  int p = gl / L;
+  const int u = gl - p * L;
+  const bool active = p < cls_cnt;
+  if (!active) p = cls_cnt - 1;
+  const bool real = u < LR;                 // padding lanes contribute 0
+  const int uu = real ? u : 0;
+  const int ux = uu % UX, uy = uu / UX;
+
+  const fme_job j = ta.sjobs[cls_off + p];
+  const int jid = ta.perm[cls_off + p];
+  const fme_tz_ext e = ta.ext[jid];
+  const PicDesc ref = a.pics[j.ref_id];
+  const double ml = a.mlambda[j.lambda_id];
+  const bool kbuf = j.key_offset >= 0;
+  const bool sad_metric = PW == 12 || PW == 24 || PW == 48;
+  const bool sub = sad_metric && (a.fen == 1 || a.fen == 3) && PH > 8;
+  const int ox = (int)j.x + ux * UW, oy = (int)j.y + uy * UH;
+
+  // key of this unit: (s - 128) bytes (uni-pred) or int16 pairs (bi-pred key block)
+  uint32_t k8[UH][UW / 4], k16[UH][UW / 2];
+  int sk2 = 0;
+  if (!kbuf) {
+    const PicDesc org = a.pics[j.org_id];
+#pragma unroll
+    for (int r = 0; r < UH; r++)
+#pragma unroll
+      for (int c = 0; c < UW / 4; c++) {
+        const uint32_t v = gld32(org.luma + (size_t)(oy + r) * org.stride + ox + 4 * c);
+        k8[r][c] = v;   // raw bytes (SAD) ; signed form below (SSE)
+        sk2 = dot4(v ^ 0x80808080u, v ^ 0x80808080u, sk2);
+      }
+  } else {
+    const int16_t* kb = a.keys + (size_t)j.key_offset + (size_t)(uy * UH) * PW + ux * UW;
+#pragma unroll
+    for (int r = 0; r < UH; r++)
+#pragma unroll
+      for (int c = 0; c < UW / 2; c++)
+        k16[r][c] = (uint32_t)(uint16_t)kb[r * PW + 2 * c] | ((uint32_t)(uint16_t)kb[r * PW + 2 * c + 1] << 16);
+  }
+
+  Tz s;
+  s.best_sad = 0xFFFFFFFFu;
+  s.bx = s.by = s.bdist = s.bround = s.pnr = 0;
+  s.R = Range{j.lt_x, j.rb_x, j.lt_y, j.rb_y};
+  s.RR = s.R;
+  s.range = e.search_range ? e.search_range : 64;
+  s.k = -1; s.dist = 1; s.ox = s.oy = 0; s.opnr = 0; s.ret = P_DONE;
+  if (j.flags & FME_JOB_BIPRED) {
+    s.phase = P_FULL;
+    s.rx = j.lt_x; s.ry = j.lt_y;
+    s.sx = s.sy = 0; s.px = s.py = 0; s.has_pred = false;
+  } else {
+    int mx = j.mvp_x, my = j.mvp_y;
+    clip_qpel(mx, my, ref.width, ref.height, e.cu_x, e.cu_y);
+    s.sx = round4(mx);
+    s.sy = round4(my);
+    s.has_pred = (e.flags & FME_TZ_PRED2NX2N) != 0;
+    int qx = e.pred2n_x * 4, qy = e.pred2n_y * 4;
+    clip_qpel(qx, qy, ref.width, ref.height, e.cu_x, e.cu_y);
+    s.px = round4(qx);
+    s.py = round4(qy);
+    s.phase = P_START;
+    s.rx = s.ry = 0;
+  }
+
+  for (int step = 0; step < (1 << 16); step++) {   // bound: a search tests < 2,000 points
+    int x = 0, y = 0, pnr = 0, pd = 0;
+    const bool has = next_candidate(s, ref.width, ref.height, e.cu_x, e.cu_y, x, y, pnr, pd);
+    if (!__any(has ? 1 : 0)) break;
+    if (!has) continue;   // this group is done; the wave's other groups still search
+    // ---- distortion of this unit at integer displacement (x, y) ----------------------------
+    uint32_t part = 0;
+    if (real) {
+      const int bx = ox + x, by = oy + y;
+      const int xa = bx & ~3;
+      const uint32_t s0 = (uint32_t)(bx - xa);
+      constexpr int ND = UW / 4 + 1;
+      const bool inside = xa >= 0 && xa + 4 * ND <= ref.width;
+      int sop = 0, spp = 0;
+      uint32_t acc = 0;
+#pragma unroll
+      for (int r = 0; r < UH; r++) {
+        if (sub && (r & 1)) continue;   // FEN: even rows of the PU (UH is even)
+        const uint8_t* row = ref.luma + (size_t)clamp_i(by + r, 0, ref.height - 1) * ref.stride;
+        uint32_t w[ND];
+        if (inside) {
+#pragma unroll
+          for (int q = 0; q < ND; q++) w[q] = gld32(row + xa + 4 * q);
+        } else {
+#pragma unroll
+          for (int q = 0; q < ND; q++) {
+            uint32_t v = 0;
+#pragma unroll
+            for (int b = 0; b < 4; b++) v |= gld8(row + clamp_i(xa + 4 * q + b, 0, ref.width - 1)) << (8 * b);
+            w[q] = v;
+          }
+        }
+#pragma unroll
+        for (int c = 0; c < UW / 4; c++) {
+          const uint32_t pv = __builtin_amdgcn_alignbyte(w[c + 1], w[c], s0);   // reference bytes
+          if (!kbuf) {
+            if (sad_metric) {
+              acc = __builtin_amdgcn_sad_u8(pv, k8[r][c], acc);
+            } else {
+              const uint32_t ps = pv ^ 0x80808080u;
+              sop = dot4(k8[r][c] ^ 0x80808080u, ps, sop);
+              spp = dot4(ps, ps, spp);
+            }
+          } else {
+            const uint32_t d0 = pk_sub(k16[r][2 * c], lo_pair(pv));
+            const uint32_t d1 = pk_sub(k16[r][2 * c + 1], hi_pair(pv));
+            if (sad_metric) {
+              acc = udot2(pk_abs(d0), 0x00010001u, udot2(pk_abs(d1), 0x00010001u, acc));
+            } else {
+              acc = (uint32_t)dot2(d1, d1, dot2(d0, d0, (int)acc));
+            }
+          }
+        }
+      }
+      part = (!kbuf && !sad_metric) ? (uint32_t)(sk2 - 2 * sop + spp) : acc;
+      if (sub) part <<= 1;
+    }
+    uint32_t d = group_sum(part, L);
+    // ---- xTZSearchHelp's update -------------------------------------------------------------
+    if (d < s.best_sad) {
+      d += mv_cost(ml, mv_bits(x, y, 2, j.mvp_x, j.mvp_y));
+      if (d < s.best_sad) {
+        s.best_sad = d;
+        s.bx = x;
+        s.by = y;
+        s.bdist = pd;
+        s.bround = 0;
+        s.pnr = pnr;
+      }
+    }
+  }
+  if (active && u == 0) {
+    fme_job* out = ta.jobs_out + jid;
+    out->mv_x = (int16_t)s.bx;
+    out->mv_y = (int16_t)s.by;
+    if (ta.sad) ta.sad[jid] = s.best_sad - mv_cost(ml, mv_bits(s.bx, s.by, 2, j.mvp_x, j.mvp_y));
+  }
+}
+
+__device__ __forceinline__ int xcd_block(int r, int n) {
+  const int k = r & 7;
+  return k * (n >> 3) + min(k, n & 7) + (r >> 3);
+}
+
+template <int UW, int UH>
+__global__ __launch_bounds__(kTzNT) void k_tz(TzArgs ta, Schedule sc, int kid) {
+  const int b = blockIdx.x;
+  int c = 0;
+  while (c < kNumClasses - 1 && b >= sc.prefix[kid][c + 1]) c++;
+  const int nblk = sc.prefix[kid][c + 1] - sc.prefix[kid][c];
+  const int blk = xcd_block(b - sc.prefix[kid][c], nblk);
+  const int W[kNumClasses] = {4, 8, 8, 4, 16, 8, 16, 12, 16, 16, 8, 32, 16, 32, 24, 32, 32, 16, 64, 32, 64, 48, 64, 64};
+  const int H[kNumClasses] = {8, 4, 8, 16, 4, 16, 8, 16, 12, 16, 32, 8, 32, 16, 32, 24, 32, 64, 16, 64, 32, 64, 48, 64};
+  tz_unit<UW, UH>(ta, sc.class_off[c], sc.class_cnt[c], blk, W[c], H[c]);
+}
+
+}  // namespace
+
+// Unit shape of a class for the integer search: 8 wide / tall where the PU allows, else 4.
+int tz_kernel_of(int cls) {
+  const int w = kClassW[cls], h = kClassH[cls];
+  const int uw = (w % 8) == 0 ? 8 : 4, uh = (h % 8) == 0 ? 8 : 4;
+  return uw == 4 ? 0 : (uh == 4 ? 1 : 2);
+}
+int tz_lanes_per_pu(int cls) {
+  const int w = kClassW[cls], h = kClassH[cls];
+  const int uw = (w % 8) == 0 ? 8 : 4, uh = (h % 8) == 0 ? 8 : 4;
+  const int lr = (w / uw) * (h / uh);
+  int l = 1;
+  while (l < lr) l <<= 1;
+  return l;
+}
+
+hipError_t launch_tz(const TzArgs& ta, const Schedule& sc, hipStream_t s) {
+  int blocks = sc.prefix[0][kNumClasses];
+  if (blocks > 0) hipLaunchKernelGGL((k_tz<4, 8>), dim3(blocks), dim3(kTzNT), 0, s, ta, sc, 0);
+  blocks = sc.prefix[1][kNumClasses];
+  if (blocks > 0) hipLaunchKernelGGL((k_tz<8, 4>), dim3(blocks), dim3(kTzNT), 0, s, ta, sc, 1);
+  blocks = sc.prefix[2][kNumClasses];
+  if (blocks > 0) hipLaunchKernelGGL((k_tz<8, 8>), dim3(blocks), dim3(kTzNT), 0, s, ta, sc, 2);
+  return hipGetLastError();
+}
+
+}  // namespace fme

@@ -48,6 +48,18 @@ MC_JOB_DTYPE = np.dtype(
 )
 assert MC_JOB_DTYPE.itemsize == 24
 
+# fme_tz_ext (12 B): per-job extension of the integer TZ search (include/fme.h)
+TZ_EXT_DTYPE = np.dtype(
+    [
+        ("cu_x", "<u2"), ("cu_y", "<u2"),
+        ("pred2n_x", "<i2"), ("pred2n_y", "<i2"),
+        ("flags", "u1"), ("search_range", "u1"), ("reserved", "<u2"),
+    ],
+    align=False,
+)
+assert TZ_EXT_DTYPE.itemsize == 12
+TZ_PRED2NX2N = 0x01
+
 MC_L0 = 0x01
 MC_L1 = 0x02
 

@@ -27,6 +27,7 @@ ABI_SYMBOLS = (
     "fme_accumulated_timings", "fme_search_kernel_of_shape", "fme_debug_phase_cycles",
     "fme_set_picture_chroma", "fme_bind_picture_chroma_device", "fme_motion_compensate",
     "fme_motion_compensate_device", "fme_mc_invalid_count", "fme_mc_last_ms",
+    "fme_integer_search", "fme_integer_search_device", "fme_integer_search_last_ms",
 )
 
 
@@ -83,6 +84,9 @@ def load_library(path=None):
         "fme_motion_compensate_device": (I, [P, P, I, P, I, P, P, I, I, I, P]),
         "fme_mc_invalid_count": (I, [P]),
         "fme_mc_last_ms": (I, [P, P]),
+        "fme_integer_search": (I, [P, P, P, P, I, P]),
+        "fme_integer_search_device": (I, [P, P, P, P, I, P]),
+        "fme_integer_search_last_ms": (I, [P, P]),
     }
     for name, (res, args) in sig.items():
         f = getattr(lib, name)
@@ -150,6 +154,26 @@ class FmeContext:
     def bind_picture_chroma_device(self, pid, cb_ptr, cr_ptr, stride):
         _check(self.lib, self.lib.fme_bind_picture_chroma_device(self.h, pid, C.c_void_p(cb_ptr), C.c_void_p(cr_ptr),
                                                                  stride))
+
+    # -- integer motion estimation ------------------------------------------------------------
+    def integer_search(self, jobs, ext, stream=None):
+        """xTZSearch / xPatternSearch per job (fme_integer_search): returns (jobs with mv_x/mv_y
+        = the integer MV, ruiSAD per job)."""
+        from .abi import TZ_EXT_DTYPE
+        jobs = np.array(jobs, dtype=JOB_DTYPE, copy=True)
+        ext = np.ascontiguousarray(ext, dtype=TZ_EXT_DTYPE)
+        sad = np.zeros(len(jobs), np.uint32)
+        _check(self.lib, self.lib.fme_integer_search(self.h, _ptr(jobs), _ptr(ext), _ptr(sad), len(jobs), stream))
+        return jobs, sad
+
+    def integer_search_device(self, d_jobs, d_ext, d_sad, n, stream=None):
+        _check(self.lib, self.lib.fme_integer_search_device(self.h, C.c_void_p(d_jobs), C.c_void_p(d_ext),
+                                                            C.c_void_p(d_sad), n, stream))
+
+    def integer_search_last_ms(self):
+        ms = C.c_float()
+        _check(self.lib, self.lib.fme_integer_search_last_ms(self.h, C.byref(ms)))
+        return ms.value
 
     # -- motion compensation ----------------------------------------------------------------
     def motion_compensate(self, mc_jobs, y, cb, cr, stream=None):

@@ -331,3 +331,67 @@ def make_bipred_keys_fast(rng, jobs, pictures):
         keys[idx] = blk
         jobs["key_offset"][sel[m]] = offs[m]
     return keys
+
+
+# ---- integer motion estimation inputs -----------------------------------
+def _clip_cu_qpel(v, cu, pic):
+    """TComDataCU::clipMv with the CU origin (TComDataCU.cpp:2778-2785), quarter-pel."""
+    return np.minimum((pic + 8 - cu - 1) << 2, np.maximum((-MAX_CU - 8 - cu + 1) << 2, v))
+
+
+def make_tz_jobs(rng, width, height, calls_per_ctu, org_id, ref_ids, lambda_ids, mix=PU_MIX, bipred_frac=0.0,
+                 pred2n_frac=0.5, search_range=SEARCH_RANGE, bipred_range=4, amp=12.0, mvp_noise=24):
+    """Jobs for the integer search in HM's CTU order: PUs on the CU grid with their CU origin
+    (clipMv), the AMVP predictor near a smooth motion field, the search range from
+    xSetSearchRange(mvp, SearchRange) (bi-pred: xSetSearchRange(current MV, BipredSearchRange)),
+    and for a share of non-2Nx2N PUs the 2Nx2N integer MV as an extra start candidate.
+    Returns (fme_job array with FME_JOB_EMI / FME_JOB_BIPRED flags, fme_tz_ext array)."""
+    from .abi import TZ_EXT_DTYPE, TZ_PRED2NX2N
+    ctus_x, ctus_y = (width + MAX_CU - 1) // MAX_CU, (height + MAX_CU - 1) // MAX_CU
+    vx, vy = motion_field(rng, ctus_x, ctus_y, amp)
+    ref_ids = np.asarray(ref_ids)
+    nref = len(ref_ids)
+    per = calls_per_ctu * nref
+    n = ctus_x * ctus_y * per
+    w, h = sample_sizes(rng, n, mix)
+    ctu = np.repeat(np.arange(ctus_x * ctus_y), per)
+    cs = np.where(np.maximum(w, h) <= 8, 8, np.where(np.maximum(w, h) <= 16, 16, np.where(np.maximum(w, h) <= 32, 32, 64)))
+    ncu = MAX_CU // cs
+    cu_x = (ctu % ctus_x) * MAX_CU + rng.integers(0, ncu) * cs
+    cu_y = (ctu // ctus_x) * MAX_CU + rng.integers(0, ncu) * cs
+    cu_x = np.minimum(cu_x, (width - cs) // 8 * 8)
+    cu_y = np.minimum(cu_y, (height - cs) // 8 * 8)
+    x = np.minimum(cu_x + rng.integers(0, 2, n) * (cs - w), (width - w) // 4 * 4)
+    y = np.minimum(cu_y + rng.integers(0, 2, n) * (cs - h), (height - h) // 4 * 4)
+    ref_k = np.tile(np.arange(nref), n // nref)
+    dist = ref_k + 1
+    mvp_x = 4 * np.rint(vx.reshape(-1)[ctu] * dist).astype(np.int64) + rng.integers(-mvp_noise, mvp_noise + 1, n)
+    mvp_y = 4 * np.rint(vy.reshape(-1)[ctu] * dist).astype(np.int64) + rng.integers(-mvp_noise, mvp_noise + 1, n)
+    bi = rng.random(n) < bipred_frac
+    # bi-pred: the range is centred on the current MV of the list (rcMv), near the predictor
+    cen_x = np.where(bi, mvp_x + 4 * rng.integers(-3, 4, n), mvp_x)
+    cen_y = np.where(bi, mvp_y + 4 * rng.integers(-3, 4, n), mvp_y)
+    rng_pel = np.where(bi, bipred_range, search_range)
+    cx = _clip_cu_qpel(cen_x, cu_x, width)
+    cy = _clip_cu_qpel(cen_y, cu_y, height)
+    jobs = np.zeros(n, dtype=JOB_DTYPE)
+    jobs["x"], jobs["y"], jobs["w"], jobs["h"] = x, y, w, h
+    jobs["org_id"] = org_id
+    jobs["ref_id"] = ref_ids[ref_k]
+    jobs["lambda_id"] = rng.choice(np.asarray(lambda_ids), size=n)
+    jobs["mvp_x"], jobs["mvp_y"] = mvp_x, mvp_y
+    jobs["lt_x"] = _div4_round(_clip_cu_qpel(cx - (rng_pel << 2), cu_x, width))
+    jobs["rb_x"] = _div4_round(_clip_cu_qpel(cx + (rng_pel << 2), cu_x, width))
+    jobs["lt_y"] = _div4_round(_clip_cu_qpel(cy - (rng_pel << 2), cu_y, height))
+    jobs["rb_y"] = _div4_round(_clip_cu_qpel(cy + (rng_pel << 2), cu_y, height))
+    jobs["bits_in"] = rng.integers(1, 7, n)
+    jobs["flags"] = np.where(bi, JOB_BIPRED, JOB_EMI)
+    jobs["key_offset"] = np.where(bi, -2, -1)
+    ext = np.zeros(n, dtype=TZ_EXT_DTYPE)
+    ext["cu_x"], ext["cu_y"] = cu_x, cu_y
+    ext["search_range"] = search_range
+    p2 = (~bi) & ((w != cs) | (h != cs)) & (rng.random(n) < pred2n_frac)
+    ext["flags"] = np.where(p2, TZ_PRED2NX2N, 0)
+    ext["pred2n_x"] = np.where(p2, np.rint(vx.reshape(-1)[ctu] * dist).astype(np.int64) + rng.integers(-6, 7, n), 0)
+    ext["pred2n_y"] = np.where(p2, np.rint(vy.reshape(-1)[ctu] * dist).astype(np.int64) + rng.integers(-6, 7, n), 0)
+    return jobs, ext

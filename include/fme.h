@@ -178,6 +178,37 @@ int fme_refine(fme_ctx* ctx, const fme_job* jobs, fme_result* results, int n, vo
 int fme_refine_device(fme_ctx* ctx, const fme_job* d_jobs, fme_result* d_results, int n,
                       void* stream);
 
+/* ---- integer motion estimation ----------------------------------------- *
+ * The integer search xMotionEstimation runs before the sub-pel path (TEncSearch.cpp:4504-4527):
+ *   uni-pred jobs (no FME_JOB_BIPRED): xPatternSearchFast -> xTZSearch (TEncSearch.cpp:4737-5036)
+ *     with the shipped settings (FastSearch = 1 diamond, not extended; FastMEAssumingSmootherMV:
+ *     first search stops 3 rounds after the best; raster step 5; star refinement), from the
+ *     AMVP predictor job.mvp (clipMv'd against the CU origin, rounded to full-pel), the zero
+ *     vector and, with FME_TZ_PRED2NX2N, the 2Nx2N PU's integer MV; diamond / star points are
+ *     limited to the job's lt/rb range, the raster to the range re-centred on the best after the
+ *     2Nx2N test (xSetSearchRange).  The final EMI square step is NOT run here: it is the first
+ *     step of fme_refine (FME_JOB_EMI), so the result is the TZ best before it.
+ *   bi-pred jobs: xPatternSearch (TEncSearch.cpp:4627-4680), every point of lt..rb in raster order.
+ * The metric is the modified integer-ME one of the batch path (SSE, SAD12/24/48 with FEN row
+ * subsampling) plus the MV cost at cost scale 2.  On return job.mv_x/mv_y hold the integer MV
+ * (ready for fme_refine) and sad[i] = ruiSAD (distortion at that MV).                             */
+#define FME_TZ_PRED2NX2N 0x01u
+
+typedef struct fme_tz_ext {
+  uint16_t cu_x, cu_y;          /* luma origin of the PU's CU (TComDataCU::clipMv)              */
+  int16_t  pred2n_x, pred2n_y;  /* m_integerMv2Nx2N[list][ref] (full-pel), with FME_TZ_PRED2NX2N */
+  uint8_t  flags;               /* FME_TZ_*                                                     */
+  uint8_t  search_range;        /* m_iSearchRange (cfg SearchRange, 64): diamond / star bound    */
+  uint16_t reserved;
+} fme_tz_ext;   /* 12 bytes */
+
+int fme_integer_search(fme_ctx* ctx, fme_job* jobs, const fme_tz_ext* ext, uint32_t* sad, int n,
+                       void* stream);
+int fme_integer_search_device(fme_ctx* ctx, fme_job* d_jobs, const fme_tz_ext* d_ext, uint32_t* d_sad,
+                              int n, void* stream);
+/* With profiling on: device milliseconds of the last integer-search launches; waits for them. */
+int fme_integer_search_last_ms(fme_ctx* ctx, float* ms);
+
 /* ---- single-PU entry points with the TEncSearch argument lists ---------------------------- *
  * xPatternSearchFracDIF(bIsLosslessCoded, pcPatternKey, piRefY, iRefStride, pcMvInt,
  *                       rcMvHalf, rcMvQter, ruiCost) with the HM objects flattened:

@@ -618,3 +618,269 @@ int orc_mc(const orc_yuv* pics, const fme_mc_job* jobs, int n, uint8_t* y, int y
   }
   return 0;
 }
+
+/* =====================================================================================
+ * Integer motion estimation: xTZSearch with the shipped settings and
+ * xPatternSearch for bi-pred jobs (TEncSearch.cpp:4627-5036, helpers 1078-1589).
+ * ===================================================================================== */
+
+/* TComMv::divideByPowerOf2(2) with ME_ENABLE_ROUNDING_OF_MVS (TComMv.h:122-130). */
+static int mv_round4(int v) { return (v + 2) >> 2; }
+
+/* TComDataCU::clipMv (TComDataCU.cpp:2773-2786), quarter-pel, max CU 64. */
+static void tz_clip(int* x, int* y, int pw, int ph, int cu_x, int cu_y) {
+  const int hmax = (pw + 8 - cu_x - 1) << 2, hmin = (-64 - 8 - cu_x + 1) * 4;
+  const int vmax = (ph + 8 - cu_y - 1) << 2, vmin = (-64 - 8 - cu_y + 1) * 4;
+  *x = *x < hmin ? hmin : (*x > hmax ? hmax : *x);
+  *y = *y < vmin ? vmin : (*y > vmax ? vmax : *y);
+}
+
+/* IntTZSearchStruct (TEncSearch.h) and the state xTZSearchHelp reads. */
+typedef struct tz_state {
+  const orc_picture* ref;
+  const int16_t* key;
+  int x0, y0, w, h, fen, mvp_x, mvp_y;
+  double ml;
+  int16_t* cur;
+  uint32_t best_sad;
+  int best_x, best_y, best_dist, best_round, point_nr;
+} tz_state;
+
+/* xTZSearchHelp normal branch (TEncSearch.cpp:1155-1188, save = false). */
+static void tz_help(tz_state* s, int x, int y, int point_nr, int dist) {
+  orc_pred_block(s->ref, s->x0, s->y0, s->w, s->h, 4 * x, 4 * y, s->cur);
+  uint32_t d = int_dist(s->key, s->w, s->cur, s->w, s->w, s->h, s->fen);
+  if (d < s->best_sad) {
+    d += orc_cost(s->ml, mv_bits(x, y, 2, s->mvp_x, s->mvp_y));
+    if (d < s->best_sad) {
+      s->best_sad = d;
+      s->best_x = x;
+      s->best_y = y;
+      s->best_dist = dist;
+      s->best_round = 0;
+      s->point_nr = point_nr;
+    }
+  }
+}
+
+typedef struct tz_range { int l, r, t, b; } tz_range;
+
+/* xTZ8PointDiamondSearch (TEncSearch.cpp:1379-1589), bCheckCornersAtDist1 = false. */
+static void tz_diamond(tz_state* s, const tz_range* R, int sx, int sy, int dist) {
+  const int top = sy - dist, bot = sy + dist, left = sx - dist, right = sx + dist;
+  s->best_round += 1;
+  if (dist == 1) {
+    if (top >= R->t) tz_help(s, sx, top, 2, dist);
+    if (left >= R->l) tz_help(s, left, sy, 4, dist);
+    if (right <= R->r) tz_help(s, right, sy, 5, dist);
+    if (bot <= R->b) tz_help(s, sx, bot, 7, dist);
+  } else if (dist <= 8) {
+    const int t2 = sy - (dist >> 1), b2 = sy + (dist >> 1), l2 = sx - (dist >> 1), r2 = sx + (dist >> 1);
+    if (top >= R->t && left >= R->l && right <= R->r && bot <= R->b) {
+      tz_help(s, sx, top, 2, dist);
+      tz_help(s, l2, t2, 1, dist >> 1);
+      tz_help(s, r2, t2, 3, dist >> 1);
+      tz_help(s, left, sy, 4, dist);
+      tz_help(s, right, sy, 5, dist);
+      tz_help(s, l2, b2, 6, dist >> 1);
+      tz_help(s, r2, b2, 8, dist >> 1);
+      tz_help(s, sx, bot, 7, dist);
+    } else {
+      if (top >= R->t) tz_help(s, sx, top, 2, dist);
+      if (t2 >= R->t) {
+        if (l2 >= R->l) tz_help(s, l2, t2, 1, dist >> 1);
+        if (r2 <= R->r) tz_help(s, r2, t2, 3, dist >> 1);
+      }
+      if (left >= R->l) tz_help(s, left, sy, 4, dist);
+      if (right <= R->r) tz_help(s, right, sy, 5, dist);
+      if (b2 <= R->b) {
+        if (l2 >= R->l) tz_help(s, l2, b2, 6, dist >> 1);
+        if (r2 <= R->r) tz_help(s, r2, b2, 8, dist >> 1);
+      }
+      if (bot <= R->b) tz_help(s, sx, bot, 7, dist);
+    }
+  } else {
+    const int q = dist >> 2;
+    if (top >= R->t && left >= R->l && right <= R->r && bot <= R->b) {
+      tz_help(s, sx, top, 0, dist);
+      tz_help(s, left, sy, 0, dist);
+      tz_help(s, right, sy, 0, dist);
+      tz_help(s, sx, bot, 0, dist);
+      for (int k = 1; k < 4; k++) {
+        const int yt = top + q * k, yb = bot - q * k, xl = sx - q * k, xr = sx + q * k;
+        tz_help(s, xl, yt, 0, dist);
+        tz_help(s, xr, yt, 0, dist);
+        tz_help(s, xl, yb, 0, dist);
+        tz_help(s, xr, yb, 0, dist);
+      }
+    } else {
+      if (top >= R->t) tz_help(s, sx, top, 0, dist);
+      if (left >= R->l) tz_help(s, left, sy, 0, dist);
+      if (right <= R->r) tz_help(s, right, sy, 0, dist);
+      if (bot <= R->b) tz_help(s, sx, bot, 0, dist);
+      for (int k = 1; k < 4; k++) {
+        const int yt = top + q * k, yb = bot - q * k, xl = sx - q * k, xr = sx + q * k;
+        if (yt >= R->t) {
+          if (xl >= R->l) tz_help(s, xl, yt, 0, dist);
+          if (xr <= R->r) tz_help(s, xr, yt, 0, dist);
+        }
+        if (yb <= R->b) {
+          if (xl >= R->l) tz_help(s, xl, yb, 0, dist);
+          if (xr <= R->r) tz_help(s, xr, yb, 0, dist);
+        }
+      }
+    }
+  }
+}
+
+/* xTZ2PointSearch (TEncSearch.cpp:1191-1322): the 2 untested neighbours of a distance-1 best. */
+static void tz_two_point(tz_state* s, const tz_range* R) {
+  const int sx = s->best_x, sy = s->best_y;
+  switch (s->point_nr) {
+    case 1:
+      if (sx - 1 >= R->l) tz_help(s, sx - 1, sy, 0, 2);
+      if (sy - 1 >= R->t) tz_help(s, sx, sy - 1, 0, 2);
+      break;
+    case 2:
+      if (sy - 1 >= R->t) {
+        if (sx - 1 >= R->l) tz_help(s, sx - 1, sy - 1, 0, 2);
+        if (sx + 1 <= R->r) tz_help(s, sx + 1, sy - 1, 0, 2);
+      }
+      break;
+    case 3:
+      if (sy - 1 >= R->t) tz_help(s, sx, sy - 1, 0, 2);
+      if (sx + 1 <= R->r) tz_help(s, sx + 1, sy, 0, 2);
+      break;
+    case 4:
+      if (sx - 1 >= R->l) {
+        if (sy + 1 <= R->b) tz_help(s, sx - 1, sy + 1, 0, 2);
+        if (sy - 1 >= R->t) tz_help(s, sx - 1, sy - 1, 0, 2);
+      }
+      break;
+    case 5:
+      if (sx + 1 <= R->r) {
+        if (sy - 1 >= R->t) tz_help(s, sx + 1, sy - 1, 0, 2);
+        if (sy + 1 <= R->b) tz_help(s, sx + 1, sy + 1, 0, 2);
+      }
+      break;
+    case 6:
+      if (sx - 1 >= R->l) tz_help(s, sx - 1, sy, 0, 2);
+      if (sy + 1 <= R->b) tz_help(s, sx, sy + 1, 0, 2);
+      break;
+    case 7:
+      if (sy + 1 <= R->b) {
+        if (sx - 1 >= R->l) tz_help(s, sx - 1, sy + 1, 0, 2);
+        if (sx + 1 <= R->r) tz_help(s, sx + 1, sy + 1, 0, 2);
+      }
+      break;
+    case 8:
+      if (sx + 1 <= R->r) tz_help(s, sx + 1, sy, 0, 2);
+      if (sy + 1 <= R->b) tz_help(s, sx, sy + 1, 0, 2);
+      break;
+    default:   /* assert(false) in the reference: unreachable with distance-1 bests */
+      break;
+  }
+}
+
+/* xTZSearch (TEncSearch.cpp:4737-5036) up to the EMI square step. */
+static void tz_search(tz_state* s, const fme_job* j, const fme_tz_ext* e, int pw, int ph) {
+  const int range = e->search_range ? e->search_range : 64;
+  int sx = j->mvp_x, sy = j->mvp_y;
+  tz_clip(&sx, &sy, pw, ph, e->cu_x, e->cu_y);
+  sx = mv_round4(sx);
+  sy = mv_round4(sy);
+  s->best_sad = 0xFFFFFFFFu;
+  tz_help(s, sx, sy, 0, 0);
+  if ((sx != 0 || sy != 0) && (s->best_x != 0 || s->best_y != 0)) tz_help(s, 0, 0, 0, 0);
+  const tz_range R = {j->lt_x, j->rb_x, j->lt_y, j->rb_y};
+  tz_range raster = R;
+  if (e->flags & FME_TZ_PRED2NX2N) {
+    int px = e->pred2n_x * 4, py = e->pred2n_y * 4;
+    tz_clip(&px, &py, pw, ph, e->cu_x, e->cu_y);
+    px = mv_round4(px);
+    py = mv_round4(py);
+    if ((sx != px || sy != py) && (px != s->best_x || py != s->best_y)) tz_help(s, px, py, 0, 0);
+    /* xSetSearchRange(currBest << 2, m_iSearchRange) for the raster search (4602-4624) */
+    int cx = s->best_x * 4, cy = s->best_y * 4;
+    tz_clip(&cx, &cy, pw, ph, e->cu_x, e->cu_y);
+    int lx = cx - (range << 2), ly = cy - (range << 2), rx = cx + (range << 2), ry = cy + (range << 2);
+    tz_clip(&lx, &ly, pw, ph, e->cu_x, e->cu_y);
+    tz_clip(&rx, &ry, pw, ph, e->cu_x, e->cu_y);
+    raster.l = mv_round4(lx);
+    raster.t = mv_round4(ly);
+    raster.r = mv_round4(rx);
+    raster.b = mv_round4(ry);
+  }
+  const int startx = s->best_x, starty = s->best_y;
+  for (int d = 1; d <= range; d *= 2) {   /* first search, stops 3 rounds after the best */
+    tz_diamond(s, &R, startx, starty, d);
+    if (s->best_round >= 3) break;
+  }
+  if (s->best_dist == 1) {
+    s->best_dist = 0;
+    tz_two_point(s, &R);
+  }
+  if (s->best_dist > 5) {   /* raster search, iRaster = 5 */
+    s->best_dist = 5;
+    for (int y = raster.t; y <= raster.b; y += 5)
+      for (int x = raster.l; x <= raster.r; x += 5) tz_help(s, x, y, 0, 5);
+  }
+  while (s->best_dist > 0) {   /* star refinement */
+    const int bx = s->best_x, by = s->best_y;
+    s->best_dist = 0;
+    s->point_nr = 0;
+    for (int d = 1; d < range + 1; d *= 2) tz_diamond(s, &R, bx, by, d);
+    if (s->best_dist == 1) {
+      s->best_dist = 0;
+      if (s->point_nr != 0) tz_two_point(s, &R);
+    }
+  }
+}
+
+int orc_integer_search(orc_ctx* ctx, fme_job* jobs, const fme_tz_ext* ext, uint32_t* sad, int n) {
+  int16_t* key = (int16_t*)malloc(sizeof(int16_t) * 64 * 64);
+  int16_t* cur = (int16_t*)malloc(sizeof(int16_t) * 64 * 64);
+  for (int i = 0; i < n; i++) {
+    fme_job* j = &jobs[i];
+    if (!valid_size(j->w, j->h) || j->ref_id >= FME_MAX_PICTURES || j->org_id >= FME_MAX_PICTURES ||
+        j->lambda_id >= FME_MAX_LAMBDAS) {
+      free(key); free(cur);
+      return FME_E_INVALID;
+    }
+    const orc_picture* ref = &ctx->pics[j->ref_id];
+    const orc_picture* org = &ctx->pics[j->org_id];
+    if (!ref->luma) { free(key); free(cur); return FME_E_STATE; }
+    const int w = j->w, h = j->h;
+    if (j->key_offset >= 0) {
+      if ((size_t)j->key_offset + (size_t)w * h > ctx->n_keys) { free(key); free(cur); return FME_E_INVALID; }
+      memcpy(key, ctx->keys + j->key_offset, sizeof(int16_t) * w * h);
+    } else {
+      if (!org->luma) { free(key); free(cur); return FME_E_STATE; }
+      for (int y = 0; y < h; y++)
+        for (int x = 0; x < w; x++) key[y * w + x] = org->luma[(size_t)(j->y + y) * org->stride + j->x + x];
+    }
+    tz_state s;
+    memset(&s, 0, sizeof(s));
+    s.ref = ref; s.key = key; s.x0 = j->x; s.y0 = j->y; s.w = w; s.h = h;
+    s.fen = ctx->cfg.fast_inter_mode; s.mvp_x = j->mvp_x; s.mvp_y = j->mvp_y;
+    s.ml = ctx->mlambda[j->lambda_id]; s.cur = cur;
+    if (j->flags & FME_JOB_BIPRED) {
+      /* xPatternSearch (TEncSearch.cpp:4627-4680): raster order, strict minimum */
+      s.best_sad = 0xFFFFFFFFu;
+      for (int y = j->lt_y; y <= j->rb_y; y++)
+        for (int x = j->lt_x; x <= j->rb_x; x++) {
+          orc_pred_block(ref, j->x, j->y, w, h, 4 * x, 4 * y, cur);
+          const uint32_t d = int_dist(key, w, cur, w, w, h, s.fen) + orc_cost(s.ml, mv_bits(x, y, 2, s.mvp_x, s.mvp_y));
+          if (d < s.best_sad) { s.best_sad = d; s.best_x = x; s.best_y = y; }
+        }
+    } else {
+      tz_search(&s, j, &ext[i], ref->width, ref->height);
+    }
+    j->mv_x = (int16_t)s.best_x;
+    j->mv_y = (int16_t)s.best_y;
+    if (sad) sad[i] = s.best_sad - orc_cost(s.ml, mv_bits(s.best_x, s.best_y, 2, s.mvp_x, s.mvp_y));
+  }
+  free(key);
+  free(cur);
+  return FME_OK;
+}

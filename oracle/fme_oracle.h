@@ -97,6 +97,10 @@ void orc_nn_set_state(orc_ctx* ctx, const uint32_t in[12]);
  * 0 or a negative FME_E_* code. */
 int orc_refine(orc_ctx* ctx, const fme_job* jobs, fme_result* res, int n);
 
+/* ---- integer motion estimation: xTZSearch / xPatternSearch per job;
+ * writes jobs[i].mv_x/mv_y and sad[i].  Returns 0 or a negative FME_E_* code. */
+int orc_integer_search(orc_ctx* ctx, fme_job* jobs, const fme_tz_ext* ext, uint32_t* sad, int n);
+
 /* ---- motion compensation ------------------------------------ */
 typedef struct orc_yuv {
   const uint8_t *y, *cb, *cr;   /* 8-bit 4:2:0 planes; chroma (width/2) x (height/2) */

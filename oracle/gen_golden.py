@@ -148,6 +148,42 @@ def build_mc_case(name, seed, width, height, bi_frac, mv_amp, identical_frac, ke
     print(f"{path}: {len(jobs)} PUs, {nbi} bi-pred, {len(set(zip(jobs['w'], jobs['h'])))} PU shapes")
 
 
+def build_tz_case(name, seed, width, height, calls, fen, search_range, bipred, mvp_noise):
+    """Integer motion estimation (xTZSearch / xPatternSearch) from _ref; the oracle must agree."""
+    rng = np.random.default_rng(seed)
+    pics = {i: synth.synth_luma(width, height, i, seed=seed) for i in range(5)}
+    lambdas = np.array(synth.LDP_LAMBDA[22], dtype=np.float64)
+    jobs, ext = synth.make_tz_jobs(rng, width, height, calls, 4, [0, 1, 2, 3], [0, 1, 2, 3], bipred_frac=bipred,
+                                   search_range=search_range, mvp_noise=mvp_noise)
+    keys = synth.make_bipred_keys(rng, jobs, pics)
+    ref = Reference(fast_inter_mode=fen)
+    orc = Oracle(fast_inter_mode=fen)
+    for eng in (ref, orc):
+        for k, v in pics.items():
+            eng.set_picture(k, v)
+        for lid, lam in enumerate(lambdas):
+            eng.set_lambda(lid, float(lam))
+        eng.set_keys(keys if keys.size else np.zeros(1, np.int16))
+    out_r, sad_r = ref.integer_search(jobs, ext)
+    out_o, sad_o = orc.integer_search(jobs, ext)
+    bad = (out_r["mv_x"] != out_o["mv_x"]) | (out_r["mv_y"] != out_o["mv_y"]) | (sad_r != sad_o)
+    if bad.any():
+        raise SystemExit(f"{name}: oracle disagrees with _ref on {int(bad.sum())} jobs")
+    path = os.path.join(OUT, f"{name}.npz")
+    np.savez_compressed(path, pictures=np.stack([pics[i] for i in range(5)]), lambdas=lambdas, keys=keys,
+                        jobs=jobs, ext=ext, mv_x=out_r["mv_x"], mv_y=out_r["mv_y"], sad=sad_r,
+                        config=np.array([fen, search_range], dtype=np.int32))
+    far = np.abs(out_r["mv_x"] * 4 - jobs["mvp_x"]) + np.abs(out_r["mv_y"] * 4 - jobs["mvp_y"])
+    print(f"{path}: {len(jobs)} jobs, {int((jobs['flags'] & JOB_BIPRED != 0).sum())} bi-pred, "
+          f"{int((ext['flags'] != 0).sum())} with a 2Nx2N start, {int((far > 4 * 20).sum())} ending > 20 px from the predictor")
+
+
+TZ_CASES = [
+    # name, seed, W, H, calls/CTU/ref, FEN, SearchRange, bi-pred share, predictor noise (qpel)
+    ("tz_ldp_fen1", 31, 160, 96, 40, 1, 64, 0.15, 24),
+    ("tz_far_fen0_sr32", 32, 160, 96, 40, 0, 32, 0.1, 200),
+]
+
 MC_CASES = [
     # name, seed, W, H, bi_frac, mv_amp (pel), identical_frac, keep_frac, fill
     ("mc_ldp_uni", 21, 160, 104, 0.0, 40, 0.0, 1.0, 0),
@@ -168,11 +204,14 @@ CASES = [
 
 def main():
     os.makedirs(OUT, exist_ok=True)
-    if "--mc-only" not in sys.argv:
+    if "--mc-only" not in sys.argv and "--tz-only" not in sys.argv:
         for c in CASES:
             build_case(*c)
-    for c in MC_CASES:
-        build_mc_case(*c)
+    if "--tz-only" not in sys.argv:
+        for c in MC_CASES:
+            build_mc_case(*c)
+    for c in TZ_CASES:
+        build_tz_case(*c)
     return 0
 
 

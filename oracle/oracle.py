@@ -62,6 +62,8 @@ class Oracle:
         lib.orc_nn_set_state.argtypes = [_P, _P]
         lib.orc_refine.restype = C.c_int
         lib.orc_refine.argtypes = [_P, _P, _P, C.c_int]
+        lib.orc_integer_search.restype = C.c_int
+        lib.orc_integer_search.argtypes = [_P, _P, _P, _P, C.c_int]
         lib.orc_mc.restype = C.c_int
         lib.orc_mc.argtypes = [_P, _P, C.c_int, _P, C.c_int, _P, _P, C.c_int, C.c_int, C.c_int]
         self._buf = C.create_string_buffer(lib.orc_ctx_size())
@@ -115,6 +117,16 @@ class Oracle:
         cls = self.lib.orc_nn_forward(_ptr(p), _ptr(e), int(c), int(h), int(w), _ptr(logits))
         return cls, logits
 
+    def integer_search(self, jobs, ext):
+        """orc_integer_search: returns (jobs with mv_x/mv_y = the integer MV, sad)."""
+        jobs = np.array(jobs, copy=True)
+        ext = np.ascontiguousarray(ext)
+        sad = np.zeros(len(jobs), np.uint32)
+        rc = self.lib.orc_integer_search(self.ctx, _ptr(jobs), _ptr(ext), _ptr(sad), len(jobs))
+        if rc != 0:
+            raise RuntimeError(f"orc_integer_search failed: {rc}")
+        return jobs, sad
+
     def mc(self, pics, mc_jobs, y, cb, cr):
         """orc_mc: pics = {id: (Y, Cb, Cr)} reference pictures; predicts into y/cb/cr in place."""
         class Yuv(C.Structure):
@@ -167,6 +179,8 @@ class Reference:
         lib.ref_refine.argtypes = [_P, _P, _P, C.c_int]
         lib.ref_set_picture_yuv.restype = C.c_int
         lib.ref_set_picture_yuv.argtypes = [_P, C.c_int, _P, C.c_int, _P, _P, C.c_int, C.c_int, C.c_int]
+        lib.ref_integer_search.restype = C.c_int
+        lib.ref_integer_search.argtypes = [_P, _P, _P, _P, C.c_int]
         lib.ref_mc.restype = C.c_int
         lib.ref_mc.argtypes = [_P, _P, C.c_int, _P, C.c_int, _P, _P, C.c_int, C.c_int, C.c_int]
         self.h = lib.ref_create(use_hadamard, fast_inter_mode, nn_mode)
@@ -185,6 +199,15 @@ class Reference:
         y, cb, cr = (np.ascontiguousarray(a, dtype=np.uint8) for a in (y, cb, cr))
         self.lib.ref_set_picture_yuv(self.h, pid, _ptr(y), y.shape[1], _ptr(cb), _ptr(cr), cb.shape[1], y.shape[1],
                                      y.shape[0])
+
+    def integer_search(self, jobs, ext):
+        jobs = np.array(jobs, copy=True)
+        ext = np.ascontiguousarray(ext)
+        sad = np.zeros(len(jobs), np.uint32)
+        rc = self.lib.ref_integer_search(self.h, _ptr(jobs), _ptr(ext), _ptr(sad), len(jobs))
+        if rc != 0:
+            raise RuntimeError(f"ref_integer_search failed: {rc}")
+        return jobs, sad
 
     def mc(self, mc_jobs, y, cb, cr):
         jobs = np.ascontiguousarray(mc_jobs)

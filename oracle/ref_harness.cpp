@@ -524,3 +524,226 @@ int ref_mc(void* h, const fme_mc_job* jobs, int n, uint8_t* y, int ys, uint8_t* 
 }
 
 }  // extern "C"
+
+// ---- integer motion estimation ----------------------------------------
+// xTZSearch (TEncSearch.cpp:4737-5036, FastSearch = 1 diamond, bExtendedSettings = false,
+// FastMEAssumingSmootherMV = true) and xPatternSearch (4627-4680) restated over the reference's
+// TComRdCost distortion (setDistParam + DistFunc, the same dispatch as the EMI step) and TComMv
+// (divideByPowerOf2).  TEncSearch.cpp itself is unbuildable here (Eigen), TComDataCU is not
+// built, so clipMv (TComDataCU.cpp:2773-2786) is restated.
+namespace {
+struct TzStruct {   // IntTZSearchStruct
+  Distortion uiBestSad;
+  int iBestX, iBestY;
+  unsigned uiBestDistance, uiBestRound;
+  int ucPointNr;
+};
+struct Tz {
+  RefSearch& s;
+  TComPattern* key;
+  Pel* refY;
+  int stride;
+  int lt_x, lt_y, rb_x, rb_y;
+  void clipMv(TComMv& mv, int pw, int ph, int cux, int cuy) {
+    const int hmax = (pw + 8 - cux - 1) << 2, hmin = (-64 - 8 - cux + 1) << 2;
+    const int vmax = (ph + 8 - cuy - 1) << 2, vmin = (-64 - 8 - cuy + 1) << 2;
+    mv.setHor(std::min(hmax, std::max(hmin, mv.getHor())));
+    mv.setVer(std::min(vmax, std::max(vmin, mv.getVer())));
+  }
+  void help(TzStruct& t, int x, int y, int pnr, unsigned dist) {   // xTZSearchHelp, normal branch
+    Distortion d = s.intDist(key, refY, stride, x, y);
+    if (d < t.uiBestSad) {
+      d += s.rd.getCostOfVectorWithPredictor(x, y);
+      if (d < t.uiBestSad) {
+        t.uiBestSad = d;
+        t.iBestX = x;
+        t.iBestY = y;
+        t.uiBestDistance = dist;
+        t.uiBestRound = 0;
+        t.ucPointNr = pnr;
+      }
+    }
+  }
+  void diamond(TzStruct& t, int sx, int sy, int iDist) {   // xTZ8PointDiamondSearch, corners off
+    const int iTop = sy - iDist, iBottom = sy + iDist, iLeft = sx - iDist, iRight = sx + iDist;
+    t.uiBestRound += 1;
+    if (iDist == 1) {
+      if (iTop >= lt_y) help(t, sx, iTop, 2, iDist);
+      if (iLeft >= lt_x) help(t, iLeft, sy, 4, iDist);
+      if (iRight <= rb_x) help(t, iRight, sy, 5, iDist);
+      if (iBottom <= rb_y) help(t, sx, iBottom, 7, iDist);
+      return;
+    }
+    if (iDist <= 8) {
+      const int iTop_2 = sy - (iDist >> 1), iBottom_2 = sy + (iDist >> 1);
+      const int iLeft_2 = sx - (iDist >> 1), iRight_2 = sx + (iDist >> 1);
+      if (iTop >= lt_y && iLeft >= lt_x && iRight <= rb_x && iBottom <= rb_y) {
+        help(t, sx, iTop, 2, iDist);
+        help(t, iLeft_2, iTop_2, 1, iDist >> 1);
+        help(t, iRight_2, iTop_2, 3, iDist >> 1);
+        help(t, iLeft, sy, 4, iDist);
+        help(t, iRight, sy, 5, iDist);
+        help(t, iLeft_2, iBottom_2, 6, iDist >> 1);
+        help(t, iRight_2, iBottom_2, 8, iDist >> 1);
+        help(t, sx, iBottom, 7, iDist);
+      } else {
+        if (iTop >= lt_y) help(t, sx, iTop, 2, iDist);
+        if (iTop_2 >= lt_y) {
+          if (iLeft_2 >= lt_x) help(t, iLeft_2, iTop_2, 1, iDist >> 1);
+          if (iRight_2 <= rb_x) help(t, iRight_2, iTop_2, 3, iDist >> 1);
+        }
+        if (iLeft >= lt_x) help(t, iLeft, sy, 4, iDist);
+        if (iRight <= rb_x) help(t, iRight, sy, 5, iDist);
+        if (iBottom_2 <= rb_y) {
+          if (iLeft_2 >= lt_x) help(t, iLeft_2, iBottom_2, 6, iDist >> 1);
+          if (iRight_2 <= rb_x) help(t, iRight_2, iBottom_2, 8, iDist >> 1);
+        }
+        if (iBottom <= rb_y) help(t, sx, iBottom, 7, iDist);
+      }
+      return;
+    }
+    if (iTop >= lt_y && iLeft >= lt_x && iRight <= rb_x && iBottom <= rb_y) {
+      help(t, sx, iTop, 0, iDist);
+      help(t, iLeft, sy, 0, iDist);
+      help(t, iRight, sy, 0, iDist);
+      help(t, sx, iBottom, 0, iDist);
+      for (int index = 1; index < 4; index++) {
+        const int iPosYT = iTop + ((iDist >> 2) * index), iPosYB = iBottom - ((iDist >> 2) * index);
+        const int iPosXL = sx - ((iDist >> 2) * index), iPosXR = sx + ((iDist >> 2) * index);
+        help(t, iPosXL, iPosYT, 0, iDist);
+        help(t, iPosXR, iPosYT, 0, iDist);
+        help(t, iPosXL, iPosYB, 0, iDist);
+        help(t, iPosXR, iPosYB, 0, iDist);
+      }
+    } else {
+      if (iTop >= lt_y) help(t, sx, iTop, 0, iDist);
+      if (iLeft >= lt_x) help(t, iLeft, sy, 0, iDist);
+      if (iRight <= rb_x) help(t, iRight, sy, 0, iDist);
+      if (iBottom <= rb_y) help(t, sx, iBottom, 0, iDist);
+      for (int index = 1; index < 4; index++) {
+        const int iPosYT = iTop + ((iDist >> 2) * index), iPosYB = iBottom - ((iDist >> 2) * index);
+        const int iPosXL = sx - ((iDist >> 2) * index), iPosXR = sx + ((iDist >> 2) * index);
+        if (iPosYT >= lt_y) {
+          if (iPosXL >= lt_x) help(t, iPosXL, iPosYT, 0, iDist);
+          if (iPosXR <= rb_x) help(t, iPosXR, iPosYT, 0, iDist);
+        }
+        if (iPosYB <= rb_y) {
+          if (iPosXL >= lt_x) help(t, iPosXL, iPosYB, 0, iDist);
+          if (iPosXR <= rb_x) help(t, iPosXR, iPosYB, 0, iDist);
+        }
+      }
+    }
+  }
+  void twoPoint(TzStruct& t) {   // xTZ2PointSearch: the two neighbours not yet tested
+    const int sx = t.iBestX, sy = t.iBestY;
+    static const int kPts[9][2][2] = {{{0, 0}, {0, 0}},   {{-1, 0}, {0, -1}}, {{-1, -1}, {1, -1}},
+                                      {{0, -1}, {1, 0}},  {{-1, 1}, {-1, -1}}, {{1, -1}, {1, 1}},
+                                      {{-1, 0}, {0, 1}},  {{-1, 1}, {1, 1}},   {{1, 0}, {0, 1}}};
+    if (t.ucPointNr < 1 || t.ucPointNr > 8) return;
+    for (int k = 0; k < 2; k++) {
+      const int dx = kPts[t.ucPointNr][k][0], dy = kPts[t.ucPointNr][k][1];
+      const int x = sx + dx, y = sy + dy;
+      if (dx < 0 && x < lt_x) continue;
+      if (dx > 0 && x > rb_x) continue;
+      if (dy < 0 && y < lt_y) continue;
+      if (dy > 0 && y > rb_y) continue;
+      help(t, x, y, 0, 2);
+    }
+  }
+};
+}  // namespace
+
+extern "C" int ref_integer_search(void* h, fme_job* jobs, const fme_tz_ext* ext, uint32_t* sad, int n) {
+  RefCtx* c = static_cast<RefCtx*>(h);
+  RefSearch& s = c->s;
+  std::vector<Pel> keybuf(64 * 64);
+  for (int i = 0; i < n; i++) {
+    fme_job& j = jobs[i];
+    if (!c->pics[j.ref_id].set) return FME_E_STATE;
+    TComPicYuv& ref = c->pics[j.ref_id].yuv;
+    const int rs = ref.getStride(COMPONENT_Y);
+    Pel* refY = ref.getAddr(COMPONENT_Y) + j.y * rs + j.x;
+    const int w = j.w, hh = j.h;
+    if (j.key_offset >= 0) {
+      for (int k = 0; k < w * hh; k++) keybuf[k] = c->keys[j.key_offset + k];
+    } else {
+      TComPicYuv& org = c->pics[j.org_id].yuv;
+      const int os = org.getStride(COMPONENT_Y);
+      const Pel* o = org.getAddr(COMPONENT_Y) + j.y * os + j.x;
+      for (int y = 0; y < hh; y++)
+        for (int x = 0; x < w; x++) keybuf[y * w + x] = o[y * os + x];
+    }
+    TComPattern key;
+    key.initPattern(keybuf.data(), w, hh, w, 8);
+    s.setLambda(c->lambda[j.lambda_id]);
+    TComMv pred(j.mvp_x, j.mvp_y);
+    s.rd.setPredictor(pred);
+    s.rd.setCostScale(2);
+    Tz tz{s, &key, refY, rs, j.lt_x, j.lt_y, j.rb_x, j.rb_y};
+    TzStruct t{std::numeric_limits<Distortion>::max(), 0, 0, 0, 0, 0};
+    const int pw = ref.getWidth(COMPONENT_Y), ph = ref.getHeight(COMPONENT_Y);
+    if (j.flags & FME_JOB_BIPRED) {   // xPatternSearch
+      for (int y = j.lt_y; y <= j.rb_y; y++)
+        for (int x = j.lt_x; x <= j.rb_x; x++) {
+          Distortion d = s.intDist(&key, refY, rs, x, y) + s.rd.getCostOfVectorWithPredictor(x, y);
+          if (d < t.uiBestSad) { t.uiBestSad = d; t.iBestX = x; t.iBestY = y; }
+        }
+    } else {
+      const fme_tz_ext& e = ext[i];
+      const int uiSearchRange = e.search_range ? e.search_range : 64;
+      TComMv rcMv(j.mvp_x, j.mvp_y);
+      tz.clipMv(rcMv, pw, ph, e.cu_x, e.cu_y);
+      rcMv.divideByPowerOf2(2);
+      tz.help(t, rcMv.getHor(), rcMv.getVer(), 0, 0);
+      if ((rcMv.getHor() != 0 || rcMv.getVer() != 0) && (0 != t.iBestX || 0 != t.iBestY)) tz.help(t, 0, 0, 0, 0);
+      int rL = j.lt_x, rR = j.rb_x, rT = j.lt_y, rB = j.rb_y;
+      if (e.flags & FME_TZ_PRED2NX2N) {
+        TComMv p(e.pred2n_x, e.pred2n_y);
+        p <<= 2;
+        tz.clipMv(p, pw, ph, e.cu_x, e.cu_y);
+        p.divideByPowerOf2(2);
+        if ((rcMv != p) && (p.getHor() != t.iBestX || p.getVer() != t.iBestY)) tz.help(t, p.getHor(), p.getVer(), 0, 0);
+        TComMv cur(t.iBestX, t.iBestY);   // xSetSearchRange(currBestMv << 2, m_iSearchRange)
+        cur <<= 2;
+        TComMv tmp = cur;
+        tz.clipMv(tmp, pw, ph, e.cu_x, e.cu_y);
+        TComMv lt(tmp.getHor() - (uiSearchRange << 2), tmp.getVer() - (uiSearchRange << 2));
+        TComMv rb(tmp.getHor() + (uiSearchRange << 2), tmp.getVer() + (uiSearchRange << 2));
+        tz.clipMv(lt, pw, ph, e.cu_x, e.cu_y);
+        tz.clipMv(rb, pw, ph, e.cu_x, e.cu_y);
+        lt.divideByPowerOf2(2);
+        rb.divideByPowerOf2(2);
+        rL = lt.getHor(); rR = rb.getHor(); rT = lt.getVer(); rB = rb.getVer();
+      }
+      int iStartX = t.iBestX, iStartY = t.iBestY;
+      for (int iDist = 1; iDist <= uiSearchRange; iDist *= 2) {
+        tz.diamond(t, iStartX, iStartY, iDist);
+        if (t.uiBestRound >= 3) break;
+      }
+      if (t.uiBestDistance == 1) {
+        t.uiBestDistance = 0;
+        tz.twoPoint(t);
+      }
+      if ((int)t.uiBestDistance > 5) {
+        t.uiBestDistance = 5;
+        for (iStartY = rT; iStartY <= rB; iStartY += 5)
+          for (iStartX = rL; iStartX <= rR; iStartX += 5) tz.help(t, iStartX, iStartY, 0, 5);
+      }
+      while (t.uiBestDistance > 0) {
+        iStartX = t.iBestX;
+        iStartY = t.iBestY;
+        t.uiBestDistance = 0;
+        t.ucPointNr = 0;
+        for (int iDist = 1; iDist < uiSearchRange + 1; iDist *= 2) tz.diamond(t, iStartX, iStartY, iDist);
+        if (t.uiBestDistance == 1) {
+          t.uiBestDistance = 0;
+          if (t.ucPointNr != 0) tz.twoPoint(t);
+        }
+      }
+    }
+    j.mv_x = (int16_t)t.iBestX;
+    j.mv_y = (int16_t)t.iBestY;
+    if (sad) sad[i] = t.uiBestSad - s.rd.getCostOfVectorWithPredictor(t.iBestX, t.iBestY);
+  }
+  return 0;
+}

@@ -34,7 +34,12 @@ def pytest_collection_modifyitems(config, items):
 
 def golden_cases():
     """Sub-pel refinement fixtures (fme_job -> fme_result)."""
-    return sorted(f[:-4] for f in os.listdir(GOLDEN) if f.endswith(".npz") and not f.startswith("mc_"))
+    return sorted(f[:-4] for f in os.listdir(GOLDEN) if f.endswith(".npz") and not f.startswith(("mc_", "tz_")))
+
+
+def tz_golden_cases():
+    """Integer motion-estimation fixtures (fme_job + fme_tz_ext -> integer MV, ruiSAD)."""
+    return sorted(f[:-4] for f in os.listdir(GOLDEN) if f.endswith(".npz") and f.startswith("tz_"))
 
 
 def mc_golden_cases():

@@ -19,7 +19,7 @@ def header_functions():
 def test_library_exports_header():
     lib = runtime.load_library()
     names = header_functions()
-    assert len(names) == 28
+    assert len(names) == 31
     assert set(names) == set(runtime.ABI_SYMBOLS)
     for n in names:
         assert hasattr(lib, n), n
@@ -38,6 +38,8 @@ def test_struct_layouts():
     assert abi.MC_JOB_DTYPE.fields["ref_id"][1] == 8
     assert abi.MC_JOB_DTYPE.fields["cu_x"][1] == 10
     assert abi.MC_JOB_DTYPE.fields["mv"][1] == 14
+    assert abi.TZ_EXT_DTYPE.itemsize == 12
+    assert abi.TZ_EXT_DTYPE.fields["flags"][1] == 8
 
 
 def test_mc_struct_matches_header():

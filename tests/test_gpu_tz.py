@@ -1,0 +1,114 @@
+"""GPU parity of the integer motion estimation: fme_integer_search
+(xTZSearch for uni-pred jobs, xPatternSearch for bi-pred jobs) against the golden vectors made by
+the reference harness (oracle/_ref) and the C restatement (orc_integer_search).  Integer output
+(MV, ruiSAD): bit-exact."""
+import numpy as np
+import pytest
+
+from conftest import load_golden, tz_golden_cases
+from nnfme import synth
+from nnfme.abi import JOB_BIPRED, TZ_EXT_DTYPE
+
+pytestmark = pytest.mark.gpu
+
+
+def _ctx(g=None, fen=1):
+    from nnfme.runtime import FmeContext
+    if g is not None:
+        fen = int(g["config"][0])
+    ctx = FmeContext(nn_mode=0, fast_inter_mode=fen)
+    if g is not None:
+        for i, p in enumerate(g["pictures"]):
+            ctx.set_picture(i, p)
+        for i, lam in enumerate(g["lambdas"]):
+            ctx.set_lambda(i, float(lam))
+        if g["keys"].size:
+            ctx.set_keys(g["keys"])
+    return ctx
+
+
+@pytest.mark.parametrize("case", tz_golden_cases())
+def test_tz_golden(case):
+    g = load_golden(case)
+    jobs, sad = _ctx(g).integer_search(g["jobs"], g["ext"])
+    bad = (jobs["mv_x"] != g["mv_x"]) | (jobs["mv_y"] != g["mv_y"]) | (sad != g["sad"])
+    assert not bad.any(), f"{case}: {int(bad.sum())} of {len(bad)} jobs differ (first {int(np.flatnonzero(bad)[0])})"
+    # only the MV fields change
+    for f in ("x", "y", "w", "h", "mvp_x", "mvp_y", "lt_x", "rb_y", "flags", "key_offset"):
+        assert np.array_equal(jobs[f], g["jobs"][f])
+
+
+def test_tz_1080p_sample_matches_oracle():
+    """A 1080p frame of integer-search jobs (4 refs, 15 % bi-pred full searches, 2Nx2N starts,
+    predictors up to 40 px off so raster searches run) on the GPU; a 2,500-job random sample
+    against the C oracle, and run-to-run determinism of the whole frame."""
+    from oracle import Oracle
+    W, H = 1920, 1080
+    rng = np.random.default_rng(17)
+    pics = {i: synth.synth_luma(W, H, t) for i, t in zip(range(5), (7, 6, 5, 4, 0))}
+    jobs, ext = synth.make_tz_jobs(rng, W, H, 60, 4, [0, 1, 2, 3], [0, 1, 2, 3], bipred_frac=0.15, mvp_noise=160)
+    keys = synth.make_bipred_keys_fast(rng, jobs, pics)
+    ctx = _ctx()
+    orc = Oracle(fast_inter_mode=1)
+    for eng in (ctx, orc):
+        for k, v in pics.items():
+            eng.set_picture(k, v)
+        for lid, lam in enumerate(synth.LDP_LAMBDA[22]):
+            eng.set_lambda(lid, lam)
+        eng.set_keys(keys)
+    got, sad = ctx.integer_search(jobs, ext)
+    got2, sad2 = ctx.integer_search(jobs, ext)
+    assert np.array_equal(got, got2) and np.array_equal(sad, sad2)
+    idx = np.sort(rng.choice(len(jobs), 2500, replace=False))
+    exp, esad = orc.integer_search(jobs[idx], ext[idx])
+    bad = (got["mv_x"][idx] != exp["mv_x"]) | (got["mv_y"][idx] != exp["mv_y"]) | (sad[idx] != esad)
+    assert not bad.any(), f"{int(bad.sum())} of {len(idx)} sampled jobs differ"
+    assert ((jobs["flags"][idx] & JOB_BIPRED) != 0).sum() > 100
+
+
+def test_tz_then_refine_matches_oracle_chain():
+    """xMotionEstimation end to end on the GPU: integer search, then the sub-pel path (EMI step,
+    FracDIF, NN, tail) on its output, against the oracle chain."""
+    from nnfme import weights
+    from nnfme.abi import compare_results
+    from nnfme.runtime import FmeContext
+    from oracle import Oracle
+    g = load_golden("tz_ldp_fen1")
+    ctx = FmeContext(nn_mode=1, qp=22, fast_inter_mode=1)
+    orc = Oracle(nn_mode=1, qp=22, fast_inter_mode=1)
+    orc.load_nn(weights.load_weights(22))
+    for eng in (ctx, orc):
+        for i, p in enumerate(g["pictures"]):
+            eng.set_picture(i, p)
+        for i, lam in enumerate(g["lambdas"]):
+            eng.set_lambda(i, float(lam))
+        eng.set_keys(g["keys"])
+    jobs, _ = ctx.integer_search(g["jobs"], g["ext"])
+    ojobs, _ = orc.integer_search(g["jobs"], g["ext"])
+    bad, first, counts = compare_results(ctx.refine(jobs), orc.refine(ojobs))
+    assert bad == 0, f"{bad} jobs differ, first {first}: {counts}"
+
+
+def test_tz_device_and_timing():
+    import torch
+    g = load_golden("tz_far_fen0_sr32")
+    ctx = _ctx(g)
+    dev = torch.device("cuda", 0)
+    dj = torch.from_numpy(g["jobs"].view(np.uint8).copy()).to(dev)
+    de = torch.from_numpy(np.ascontiguousarray(g["ext"]).view(np.uint8).copy()).to(dev)
+    ds = torch.zeros(len(g["jobs"]), dtype=torch.int32, device=dev)
+    ctx.set_profiling(True)
+    ctx.integer_search_device(dj.data_ptr(), de.data_ptr(), ds.data_ptr(), len(g["jobs"]),
+                              torch.cuda.current_stream(dev).cuda_stream)
+    assert ctx.integer_search_last_ms() > 0
+    from nnfme.abi import JOB_DTYPE
+    out = dj.cpu().numpy().view(JOB_DTYPE)
+    assert np.array_equal(out["mv_x"], g["mv_x"]) and np.array_equal(out["mv_y"], g["mv_y"])
+    assert np.array_equal(ds.cpu().numpy().view(np.uint32), g["sad"])
+    # invalid job -> rejected, nothing written
+    from nnfme.runtime import FmeError
+    bad = g["jobs"].copy()
+    bad["w"][3] = 6
+    with pytest.raises(FmeError):
+        ctx.integer_search(bad, g["ext"])
+    assert TZ_EXT_DTYPE.itemsize == 12

@@ -5,7 +5,7 @@ import os
 import numpy as np
 import pytest
 
-from conftest import mc_golden_cases, mc_inputs, golden_cases, load_golden
+from conftest import tz_golden_cases, mc_golden_cases, mc_inputs, golden_cases, load_golden
 from nnfme import synth, weights
 from nnfme.abi import PARITY_FIELDS, compare_results
 from oracle import REF_SO, Oracle, Reference
@@ -102,6 +102,49 @@ def test_mc_golden_covers_cases():
         W = g["pred_y"].shape[1]
         clipped |= bool(((j["mv"][:, :, 0] >> 2) + j["x"][:, None] > W + 8).any())
     assert len(shapes) >= 20 and flags == {1, 2, 3} and clipped
+
+
+def _tz_engine(cls, g):
+    fen, _ = (int(v) for v in g["config"])
+    eng = cls(fast_inter_mode=fen)
+    for i, p in enumerate(g["pictures"]):
+        eng.set_picture(i, p)
+    for i, lam in enumerate(g["lambdas"]):
+        eng.set_lambda(i, float(lam))
+    eng.set_keys(g["keys"] if g["keys"].size else np.zeros(1, np.int16))
+    return eng
+
+
+@pytest.mark.parametrize("case", tz_golden_cases())
+def test_tz_oracle_matches_golden(case):
+    """orc_integer_search (xTZSearch / xPatternSearch restated) against the reference harness's run."""
+    g = load_golden(case)
+    jobs, sad = _tz_engine(Oracle, g).integer_search(g["jobs"], g["ext"])
+    assert np.array_equal(jobs["mv_x"], g["mv_x"]) and np.array_equal(jobs["mv_y"], g["mv_y"])
+    assert np.array_equal(sad, g["sad"])
+
+
+@pytest.mark.skipif(not HAVE_REF, reason="oracle/_ref not built")
+@pytest.mark.parametrize("case", tz_golden_cases())
+def test_tz_reference_harness_matches_golden(case):
+    g = load_golden(case)
+    jobs, sad = _tz_engine(Reference, g).integer_search(g["jobs"], g["ext"])
+    assert np.array_equal(jobs["mv_x"], g["mv_x"]) and np.array_equal(jobs["mv_y"], g["mv_y"])
+    assert np.array_equal(sad, g["sad"])
+
+
+def test_tz_golden_covers_cases():
+    from nnfme.abi import JOB_BIPRED, TZ_PRED2NX2N
+    shapes, bi, pred, far, sr = set(), 0, 0, 0, set()
+    for case in tz_golden_cases():
+        g = load_golden(case)
+        j = g["jobs"]
+        shapes |= set(zip(j["w"].tolist(), j["h"].tolist()))
+        bi += int(((j["flags"] & JOB_BIPRED) != 0).sum())
+        pred += int(((g["ext"]["flags"] & TZ_PRED2NX2N) != 0).sum())
+        far += int((np.abs(g["mv_x"] * 4 - j["mvp_x"]) > 4 * 32).sum())   # raster-search territory
+        sr.add(int(g["config"][1]))
+    assert len(shapes) >= 18 and bi > 100 and pred > 300 and far > 50 and sr == {32, 64}
 
 
 def test_exp_golomb_bits():
