@@ -213,6 +213,74 @@ def mc_leg(dev, stream, reps):
     return out
 
 
+def tz_cpu_rate(jobs, ext, keys, pics, seconds):
+    """oracle/_ref integer search (the reference's TComRdCost distortion, xTZSearch restated) on one
+    host core over a bounded prefix of the frame's jobs (HM order)."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    from oracle import Reference
+    ref = Reference(fast_inter_mode=1)
+    for k, v in pics.items():
+        ref.set_picture(k, v)
+    for lid, lam in enumerate(synth.LDP_LAMBDA[QP]):
+        ref.set_lambda(lid, lam)
+    if keys is not None and keys.size:
+        ref.set_keys(keys)
+    done, t0 = 0, time.perf_counter()
+    while time.perf_counter() - t0 < seconds and done < len(jobs):
+        ref.integer_search(jobs[done:done + 5000], ext[done:done + 5000])
+        done += min(5000, len(jobs) - done)
+    return done / (time.perf_counter() - t0), done
+
+
+def tz_leg(dev, stream, reps, cpu_seconds):
+    """Integer motion estimation (xTZSearch / bi-pred xPatternSearch) of one 1080p frame's jobs:
+    510 CTUs x 423 calls x 4 refs in HM order, HBM-resident jobs, HIP events around the launches."""
+    import torch
+    from nnfme.runtime import FmeContext
+    rng = np.random.default_rng(2024)
+    pics = {k: synth.synth_luma(W, H, t) for k, t in zip(range(5), (7, 6, 5, 4, 0))}
+    jobs, ext = synth.make_tz_jobs(rng, W, H, 423, 4, [0, 1, 2, 3], [0, 1, 2, 3])
+    out = {"workload": f"{W}x{H} lowdelay_P QP{QP}: {len(jobs)} integer searches (xTZSearch from the AMVP "
+                       f"predictor, 2Nx2N starts for half the non-2Nx2N PUs, SearchRange 64)"}
+    if cpu_seconds > 0:
+        rate, done = tz_cpu_rate(jobs, ext, None, pics, cpu_seconds)
+        out["cpu_baseline"] = {"value": rate, "unit": "PU/s", "cores": 1, "kind": "reference",
+                               "sample": f"first {done} jobs of the frame on one host core (oracle/_ref)"}
+    ctx = FmeContext(device=dev.index, nn_mode=0, fast_inter_mode=1, max_jobs=len(jobs))
+    for k, v in pics.items():
+        ctx.set_picture(k, v)
+    for lid, lam in enumerate(synth.LDP_LAMBDA[QP]):
+        ctx.set_lambda(lid, lam)
+    src = torch.from_numpy(jobs.view(np.uint8).copy()).to(dev)
+    dj = src.clone()
+    de = torch.from_numpy(np.ascontiguousarray(ext).view(np.uint8).copy()).to(dev)
+    ds = torch.zeros(len(jobs), dtype=torch.int32, device=dev)
+
+    def run():
+        ctx.integer_search_device(dj.data_ptr(), de.data_ptr(), ds.data_ptr(), len(jobs), stream.cuda_stream)
+    run()
+    ctx.set_profiling(True)
+    ms = []
+    for _ in range(reps):
+        dj.copy_(src)
+        run()
+        ms.append(ctx.integer_search_last_ms())
+    ctx.set_profiling(False)
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        run()
+    torch.cuda.synchronize(dev)
+    wall = (time.perf_counter() - t0) / reps
+    t = float(np.median(ms))
+    out.update({"kernel_ms": t, "pu_per_s_kernels": len(jobs) / (t / 1e3), "ms_per_frame": wall * 1e3,
+                "pu_per_s": len(jobs) / wall, "kernels": "fme::k_tz<4,8>, <8,4>, <8,8> (+ classify, scatter)"})
+    if "cpu_baseline" in out:
+        out["speedup_vs_cpu_1core"] = out["pu_per_s"] / out["cpu_baseline"]["value"]
+    ctx.close()
+    return out
+
+
 def read_pmc_traffic():
     """HBM bytes per search launch from the committed rocprofv3 PMC summary (profiles/), if any."""
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
@@ -233,6 +301,7 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample length")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-mc", action="store_true", help="skip the motion-compensation leg")
+    ap.add_argument("--no-tz", action="store_true", help="skip the integer-search leg")
     ap.add_argument("--workload", choices=sorted(WORKLOADS), default="c3_qp22",
                     help="BASELINE.json config to run (default: the headline configs[2] at QP22)")
     ap.add_argument("--jobs", choices=("ctu", "uniform"), default="ctu",
@@ -379,6 +448,9 @@ def main():
                 "note": "jobs H2D + org frame H2D + refine + results D2H, pinned host buffers"}
 
     mc = mc_leg(dev, stream, reps=max(5, args.steps)) if rank == 0 and not args.no_mc and W == 1920 else None
+    tz = None
+    if rank == 0 and not args.no_tz and W == 1920 and world == 1:
+        tz = tz_leg(dev, stream, reps=max(3, args.steps // 2), cpu_seconds=0.0 if args.no_cpu_baseline else 6.0)
 
     value = world * n * args.steps / elapsed
     if rank == 0:
@@ -440,6 +512,8 @@ def main():
             out["pcie_inclusive"] = pcie
         if mc:
             out["motion_compensation"] = mc
+        if tz:
+            out["integer_search"] = tz
         print(json.dumps(out), flush=True)
 
     if world > 1:
