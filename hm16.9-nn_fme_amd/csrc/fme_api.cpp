@@ -134,6 +134,8 @@ struct fme_ctx {
 
   // the large-shape search kernel runs beside the small-shape one on its own stream
   hipStream_t aux = nullptr;
+  hipStream_t aux2 = nullptr;            // second auxiliary stream (integer search)
+  hipEvent_t ev_join2 = nullptr;
   hipEvent_t ev_fork = nullptr, ev_join = nullptr;
   bool concurrent_search = true;   // FME_SERIAL_SEARCH=1 runs the two search kernels back to back
 };
@@ -231,6 +233,8 @@ int fme_destroy(fme_ctx* c) {
     for (auto& e : set)
       if (e) (void)hipEventDestroy(e);
   if (c->ev_fork) (void)hipEventDestroy(c->ev_fork);
+  if (c->ev_join2) (void)hipEventDestroy(c->ev_join2);
+  if (c->aux2) (void)hipStreamDestroy(c->aux2);
   if (c->ev_join) (void)hipEventDestroy(c->ev_join);
   if (c->aux) (void)hipStreamDestroy(c->aux);
   if (c->single) fme_destroy(c->single.release());
@@ -590,7 +594,20 @@ int fme_integer_search_device(fme_ctx* c, fme_job* d_jobs, const fme_tz_ext* d_e
   ta.ext = d_ext;
   ta.sad = d_sad;
   if (c->profiling) HIP_TRY(hipEventRecord(c->ev_tz[0], s));
-  HIP_TRY(launch_tz(ta, sc, s));
+  // the three unit-shape kernels are latency-bound and independent: 4x8 and 8x4 units on the two
+  // auxiliary streams, 8x8 units on the caller's stream, joined before returning
+  if (!c->aux2) HIP_TRY(hipStreamCreateWithFlags(&c->aux2, hipStreamNonBlocking));
+  if (!c->ev_join2) HIP_TRY(hipEventCreateWithFlags(&c->ev_join2, hipEventDisableTiming));
+  HIP_TRY(hipEventRecord(c->ev_fork, s));
+  HIP_TRY(hipStreamWaitEvent(c->aux, c->ev_fork, 0));
+  HIP_TRY(hipStreamWaitEvent(c->aux2, c->ev_fork, 0));
+  HIP_TRY(launch_tz(ta, sc, 0, c->aux));
+  HIP_TRY(launch_tz(ta, sc, 1, c->aux2));
+  HIP_TRY(launch_tz(ta, sc, 2, s));
+  HIP_TRY(hipEventRecord(c->ev_join, c->aux));
+  HIP_TRY(hipEventRecord(c->ev_join2, c->aux2));
+  HIP_TRY(hipStreamWaitEvent(s, c->ev_join, 0));
+  HIP_TRY(hipStreamWaitEvent(s, c->ev_join2, 0));
   if (c->profiling) HIP_TRY(hipEventRecord(c->ev_tz[1], s));
   c->tz_timed = c->profiling;
   return FME_OK;

@@ -92,7 +92,7 @@ struct TzArgs {
 };
 int tz_kernel_of(int cls);    // 0: 4x8 units, 1: 8x4, 2: 8x8
 int tz_lanes_per_pu(int cls);
-hipError_t launch_tz(const TzArgs& ta, const Schedule& sc, hipStream_t s);
+hipError_t launch_tz(const TzArgs& ta, const Schedule& sc, int kid, hipStream_t s);
 
 // Host-side launch helpers (fme_kernels.hip).
 int pus_per_tile(int cls);

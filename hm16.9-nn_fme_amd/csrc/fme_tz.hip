@@ -143,9 +143,27 @@ __device__ __forceinline__ bool two_point(const Tz& s, int k, bool& ok, int& x, 
   return true;
 }
 
+__device__ __forceinline__ bool diamond_has_more(const Tz& s) {
+  bool ok;
+  int x, y, pnr, pd;
+  for (int j = s.k; diamond_point(s, j, ok, x, y, pnr, pd); j++)
+    if (ok) return true;
+  return false;
+}
+__device__ __forceinline__ bool two_point_has_more(const Tz& s) {
+  bool ok;
+  int x, y;
+  for (int j = s.k; two_point(s, j, ok, x, y); j++)
+    if (ok) return true;
+  return false;
+}
+
 // Next candidate of the search (x, y, point number, distance for xTZSearchHelp); false = done.
+// `more`: the following call continues the same list (diamond, two-point, raster, full search)
+// without a decision that depends on this candidate's result, so the two can be evaluated together.
 __device__ __forceinline__ bool next_candidate(Tz& s, int pw, int ph, int cu_x, int cu_y, int& x, int& y, int& pnr,
-                                               int& pd) {
+                                               int& pd, bool& more) {
+  more = false;
   for (int guard = 0; guard < 64; guard++) {   // phase changes between two tests are bounded
     switch (s.phase) {
       case P_START:
@@ -188,7 +206,10 @@ __device__ __forceinline__ bool next_candidate(Tz& s, int pw, int ph, int cu_x, 
         bool ok;
         while (diamond_point(s, s.k, ok, x, y, pnr, pd)) {
           s.k++;
-          if (ok) return true;
+          if (ok) {
+            more = diamond_has_more(s);
+            return true;
+          }
         }
         if (s.phase == P_FIRST) {
           if (s.bround >= 3 || 2 * s.dist > s.range) s.phase = P_TWO1;
@@ -214,6 +235,7 @@ __device__ __forceinline__ bool next_candidate(Tz& s, int pw, int ph, int cu_x, 
           s.k++;
           if (ok) {
             pnr = 0; pd = 2;
+            more = two_point_has_more(s);
             return true;
           }
         }
@@ -238,6 +260,7 @@ __device__ __forceinline__ bool next_candidate(Tz& s, int pw, int ph, int cu_x, 
         x = s.rx; y = s.ry; pnr = 0; pd = 5;
         s.rx += 5;
         if (s.rx > s.RR.r) { s.rx = s.RR.l; s.ry += 5; }
+        more = s.ry <= s.RR.b;
         return true;
       case P_STAR_CHK:
         if (s.bdist > 0) {
@@ -265,6 +288,7 @@ __device__ __forceinline__ bool next_candidate(Tz& s, int pw, int ph, int cu_x, 
         }
         x = s.rx; y = s.ry; pnr = 0; pd = 0;
         if (++s.rx > s.R.r) { s.rx = s.R.l; s.ry++; }
+        more = s.ry <= s.R.b;
         return true;
       default:
         return false;
@@ -299,26 +323,30 @@ __device__ __forceinline__ void tz_unit(const TzArgs& ta, int cls_off, int cls_c
   const bool sub = sad_metric && (a.fen == 1 || a.fen == 3) && PH > 8;
   const int ox = (int)j.x + ux * UW, oy = (int)j.y + uy * UH;
 
-  // key of this unit: (s - 128) bytes (uni-pred) or int16 pairs (bi-pred key block)
-  uint32_t k8[UH][UW / 4], k16[UH][UW / 2];
+  // key of this unit in one register array: uni-pred org bytes in kk[r][0 .. UW/4) (raw; the SSE
+  // path flips them to s - 128), bi-pred int16 key pairs in kk[r][0 .. UW/2)
+  uint32_t kk[UH][UW / 2];
   int sk2 = 0;
   if (!kbuf) {
     const PicDesc org = a.pics[j.org_id];
 #pragma unroll
-    for (int r = 0; r < UH; r++)
+    for (int r = 0; r < UH; r++) {
 #pragma unroll
       for (int c = 0; c < UW / 4; c++) {
         const uint32_t v = gld32(org.luma + (size_t)(oy + r) * org.stride + ox + 4 * c);
-        k8[r][c] = v;   // raw bytes (SAD) ; signed form below (SSE)
+        kk[r][c] = v;
         sk2 = dot4(v ^ 0x80808080u, v ^ 0x80808080u, sk2);
       }
+#pragma unroll
+      for (int c = UW / 4; c < UW / 2; c++) kk[r][c] = 0;
+    }
   } else {
     const int16_t* kb = a.keys + (size_t)j.key_offset + (size_t)(uy * UH) * PW + ux * UW;
 #pragma unroll
     for (int r = 0; r < UH; r++)
 #pragma unroll
       for (int c = 0; c < UW / 2; c++)
-        k16[r][c] = (uint32_t)(uint16_t)kb[r * PW + 2 * c] | ((uint32_t)(uint16_t)kb[r * PW + 2 * c + 1] << 16);
+        kk[r][c] = (uint32_t)(uint16_t)kb[r * PW + 2 * c] | ((uint32_t)(uint16_t)kb[r * PW + 2 * c + 1] << 16);
   }
 
   Tz s;
@@ -346,74 +374,114 @@ __device__ __forceinline__ void tz_unit(const TzArgs& ta, int cls_off, int cls_c
     s.rx = s.ry = 0;
   }
 
+  // Up to B candidates per step: consecutive points of one list (a diamond, the two-point pair,
+  // the raster) do not depend on each other's results, so their windows are loaded together
+  // (one memory latency per batch instead of per point) and xTZSearchHelp's updates are then
+  // applied in the reference's order.
+  // Measured on the 1080p frame (tools/tz_probe.py): B = 1 at 3 waves/SIMD 20.6 ms, B = 2 29.7 ms,
+  // B = 4/6 65.9 ms — the batch's windows cost more occupancy than the saved latency is worth.
+#ifdef FME_TZ_BATCH
+  constexpr int B = FME_TZ_BATCH;
+#else
+  constexpr int B = 1;
+#endif
+  constexpr int ND = UW / 4 + 1;
   for (int step = 0; step < (1 << 16); step++) {   // bound: a search tests < 2,000 points
-    int x = 0, y = 0, pnr = 0, pd = 0;
-    const bool has = next_candidate(s, ref.width, ref.height, e.cu_x, e.cu_y, x, y, pnr, pd);
-    if (!__any(has ? 1 : 0)) break;
-    if (!has) continue;   // this group is done; the wave's other groups still search
-    // ---- distortion of this unit at integer displacement (x, y) ----------------------------
-    uint32_t part = 0;
-    if (real) {
-      const int bx = ox + x, by = oy + y;
-      const int xa = bx & ~3;
-      const uint32_t s0 = (uint32_t)(bx - xa);
-      constexpr int ND = UW / 4 + 1;
-      const bool inside = xa >= 0 && xa + 4 * ND <= ref.width;
-      int sop = 0, spp = 0;
-      uint32_t acc = 0;
+    int cx[B], cy[B], cp[B], cd[B];
+    int nc = 0;
+    bool more = true;
 #pragma unroll
-      for (int r = 0; r < UH; r++) {
-        if (sub && (r & 1)) continue;   // FEN: even rows of the PU (UH is even)
-        const uint8_t* row = ref.luma + (size_t)clamp_i(by + r, 0, ref.height - 1) * ref.stride;
-        uint32_t w[ND];
-        if (inside) {
-#pragma unroll
-          for (int q = 0; q < ND; q++) w[q] = gld32(row + xa + 4 * q);
+    for (int b = 0; b < B; b++) {
+      cx[b] = cy[b] = cp[b] = cd[b] = 0;
+      if (more) {
+        bool m = false;
+        if (next_candidate(s, ref.width, ref.height, e.cu_x, e.cu_y, cx[b], cy[b], cp[b], cd[b], m)) {
+          nc = b + 1;
+          more = m;
         } else {
-#pragma unroll
-          for (int q = 0; q < ND; q++) {
-            uint32_t v = 0;
-#pragma unroll
-            for (int b = 0; b < 4; b++) v |= gld8(row + clamp_i(xa + 4 * q + b, 0, ref.width - 1)) << (8 * b);
-            w[q] = v;
-          }
+          more = false;
         }
+      }
+    }
+    if (!__any(nc > 0 ? 1 : 0)) break;
+    if (nc == 0) continue;   // this group is done; the wave's other groups still search
+    // ---- windows of this unit at the batch's displacements: all loads in flight ----------------
+    uint32_t w[B][UH][ND];
+    uint32_t s0[B];
 #pragma unroll
-        for (int c = 0; c < UW / 4; c++) {
-          const uint32_t pv = __builtin_amdgcn_alignbyte(w[c + 1], w[c], s0);   // reference bytes
-          if (!kbuf) {
-            if (sad_metric) {
-              acc = __builtin_amdgcn_sad_u8(pv, k8[r][c], acc);
-            } else {
-              const uint32_t ps = pv ^ 0x80808080u;
-              sop = dot4(k8[r][c] ^ 0x80808080u, ps, sop);
-              spp = dot4(ps, ps, spp);
-            }
+    for (int b = 0; b < B; b++) {
+      s0[b] = 0;
+      if (b < nc && real) {
+        const int bx = ox + cx[b], by = oy + cy[b];
+        const int xa = bx & ~3;
+        s0[b] = (uint32_t)(bx - xa);
+        const bool inside = xa >= 0 && xa + 4 * ND <= ref.width;
+#pragma unroll
+        for (int r = 0; r < UH; r++) {
+          if (sub && (r & 1)) continue;   // FEN: even rows of the PU (UH is even)
+          const uint8_t* row = ref.luma + (size_t)clamp_i(by + r, 0, ref.height - 1) * ref.stride;
+          if (inside) {
+#pragma unroll
+            for (int q = 0; q < ND; q++) w[b][r][q] = gld32(row + xa + 4 * q);
           } else {
-            const uint32_t d0 = pk_sub(k16[r][2 * c], lo_pair(pv));
-            const uint32_t d1 = pk_sub(k16[r][2 * c + 1], hi_pair(pv));
-            if (sad_metric) {
-              acc = udot2(pk_abs(d0), 0x00010001u, udot2(pk_abs(d1), 0x00010001u, acc));
-            } else {
-              acc = (uint32_t)dot2(d1, d1, dot2(d0, d0, (int)acc));
+#pragma unroll
+            for (int q = 0; q < ND; q++) {
+              uint32_t v = 0;
+#pragma unroll
+              for (int k = 0; k < 4; k++) v |= gld8(row + clamp_i(xa + 4 * q + k, 0, ref.width - 1)) << (8 * k);
+              w[b][r][q] = v;
             }
           }
         }
       }
-      part = (!kbuf && !sad_metric) ? (uint32_t)(sk2 - 2 * sop + spp) : acc;
-      if (sub) part <<= 1;
     }
-    uint32_t d = group_sum(part, L);
-    // ---- xTZSearchHelp's update -------------------------------------------------------------
-    if (d < s.best_sad) {
-      d += mv_cost(ml, mv_bits(x, y, 2, j.mvp_x, j.mvp_y));
+    // ---- distortions, then xTZSearchHelp's updates in order --------------------------------------
+#pragma unroll
+    for (int b = 0; b < B; b++) {
+      if (b >= nc) break;
+      uint32_t part = 0;
+      if (real) {
+        int sop = 0, spp = 0;
+        uint32_t acc = 0;
+#pragma unroll
+        for (int r = 0; r < UH; r++) {
+          if (sub && (r & 1)) continue;
+#pragma unroll
+          for (int c = 0; c < UW / 4; c++) {
+            const uint32_t pv = __builtin_amdgcn_alignbyte(w[b][r][c + 1], w[b][r][c], s0[b]);   // reference bytes
+            if (!kbuf) {
+              if (sad_metric) {
+                acc = __builtin_amdgcn_sad_u8(pv, kk[r][c], acc);
+              } else {
+                const uint32_t ps = pv ^ 0x80808080u;
+                sop = dot4(kk[r][c] ^ 0x80808080u, ps, sop);
+                spp = dot4(ps, ps, spp);
+              }
+            } else {
+              const uint32_t d0 = pk_sub(kk[r][2 * c], lo_pair(pv));
+              const uint32_t d1 = pk_sub(kk[r][2 * c + 1], hi_pair(pv));
+              if (sad_metric) {
+                acc = udot2(pk_abs(d0), 0x00010001u, udot2(pk_abs(d1), 0x00010001u, acc));
+              } else {
+                acc = (uint32_t)dot2(d1, d1, dot2(d0, d0, (int)acc));
+              }
+            }
+          }
+        }
+        part = (!kbuf && !sad_metric) ? (uint32_t)(sk2 - 2 * sop + spp) : acc;
+        if (sub) part <<= 1;
+      }
+      uint32_t d = group_sum(part, L);
       if (d < s.best_sad) {
-        s.best_sad = d;
-        s.bx = x;
-        s.by = y;
-        s.bdist = pd;
-        s.bround = 0;
-        s.pnr = pnr;
+        d += mv_cost(ml, mv_bits(cx[b], cy[b], 2, j.mvp_x, j.mvp_y));
+        if (d < s.best_sad) {
+          s.best_sad = d;
+          s.bx = cx[b];
+          s.by = cy[b];
+          s.bdist = cd[b];
+          s.bround = 0;
+          s.pnr = cp[b];
+        }
       }
     }
   }
@@ -431,7 +499,11 @@ __device__ __forceinline__ int xcd_block(int r, int n) {
 }
 
 template <int UW, int UH>
-__global__ __launch_bounds__(kTzNT) void k_tz(TzArgs ta, Schedule sc, int kid) {
+#ifndef FME_TZ_WAVES
+#define FME_TZ_WAVES 3   // occupancy target: 3 waves/SIMD (<= 168 VGPRs) measured best (1: 23.5, 4: 26.3 ms)
+#endif
+__global__ __launch_bounds__(kTzNT) __attribute__((amdgpu_waves_per_eu(FME_TZ_WAVES)))
+void k_tz(TzArgs ta, Schedule sc, int kid) {
   const int b = blockIdx.x;
   int c = 0;
   while (c < kNumClasses - 1 && b >= sc.prefix[kid][c + 1]) c++;
@@ -459,13 +531,14 @@ int tz_lanes_per_pu(int cls) {
   return l;
 }
 
-hipError_t launch_tz(const TzArgs& ta, const Schedule& sc, hipStream_t s) {
-  int blocks = sc.prefix[0][kNumClasses];
-  if (blocks > 0) hipLaunchKernelGGL((k_tz<4, 8>), dim3(blocks), dim3(kTzNT), 0, s, ta, sc, 0);
-  blocks = sc.prefix[1][kNumClasses];
-  if (blocks > 0) hipLaunchKernelGGL((k_tz<8, 4>), dim3(blocks), dim3(kTzNT), 0, s, ta, sc, 1);
-  blocks = sc.prefix[2][kNumClasses];
-  if (blocks > 0) hipLaunchKernelGGL((k_tz<8, 8>), dim3(blocks), dim3(kTzNT), 0, s, ta, sc, 2);
+// One unit-shape kernel (kid 0: 4x8 units, 1: 8x4, 2: 8x8); the three are independent and the
+// runtime runs them on separate streams.
+hipError_t launch_tz(const TzArgs& ta, const Schedule& sc, int kid, hipStream_t s) {
+  const int blocks = sc.prefix[kid][kNumClasses];
+  if (blocks <= 0) return hipSuccess;
+  if (kid == 0) hipLaunchKernelGGL((k_tz<4, 8>), dim3(blocks), dim3(kTzNT), 0, s, ta, sc, 0);
+  else if (kid == 1) hipLaunchKernelGGL((k_tz<8, 4>), dim3(blocks), dim3(kTzNT), 0, s, ta, sc, 1);
+  else hipLaunchKernelGGL((k_tz<8, 8>), dim3(blocks), dim3(kTzNT), 0, s, ta, sc, 2);
   return hipGetLastError();
 }
 
