@@ -19,6 +19,10 @@
 
 #include "fme_device.h"
 
+#ifndef FME_LANE_STREAMS_DEFAULT
+#define FME_LANE_STREAMS_DEFAULT 1
+#endif
+
 using namespace fme;
 
 namespace {
@@ -138,6 +142,7 @@ struct fme_ctx {
   hipEvent_t ev_join2 = nullptr;
   hipEvent_t ev_fork = nullptr, ev_join = nullptr;
   bool concurrent_search = true;   // FME_SERIAL_SEARCH=1 runs the two search kernels back to back
+  bool lane_streams = FME_LANE_STREAMS_DEFAULT;  // FME_LANE_STREAMS=0/1: 4x8 / 8x4 lane kernels on aux streams
 };
 
 namespace fme {
@@ -194,6 +199,7 @@ int fme_create(int device, const fme_config* cfg, fme_ctx** out_ctx) {
   HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&c->h_counts), (kNumClasses + 1) * sizeof(int32_t), hipHostMallocDefault));
   HIP_TRY(hipStreamCreateWithFlags(&c->aux, hipStreamNonBlocking));
   if (const char* e = getenv("FME_SERIAL_SEARCH")) c->concurrent_search = (e[0] == '0');
+  if (const char* e = getenv("FME_LANE_STREAMS")) c->lane_streams = (e[0] == '1');
   HIP_TRY(hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming));
   HIP_TRY(hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming));
   if (cfg->max_jobs > 0) {
@@ -501,6 +507,38 @@ int fme_refine_device(fme_ctx* c, const fme_job* d_jobs, fme_result* d_res, int 
   if (prof) HIP_TRY(hipEventRecord(ev[2], s));   // host sync above: scatter starts here
   HIP_TRY(launch_scatter(a, w, sc, s));
   if (prof) HIP_TRY(hipEventRecord(ev[3], s));
+  if (c->concurrent_search && c->lane_streams && lane_main) {
+    // the three lane kernels are independent: 8x8 units on the batch stream, 4x8 units on aux2,
+    // the cooperative shapes then 8x4 units on aux; joined before the NN tail
+    if (!c->aux2) HIP_TRY(hipStreamCreateWithFlags(&c->aux2, hipStreamNonBlocking));
+    if (!c->ev_join2) HIP_TRY(hipEventCreateWithFlags(&c->ev_join2, hipEventDisableTiming));
+    HIP_TRY(hipEventRecord(c->ev_fork, s));
+    HIP_TRY(hipStreamWaitEvent(c->aux, c->ev_fork, 0));
+    HIP_TRY(hipStreamWaitEvent(c->aux2, c->ev_fork, 0));
+    HIP_TRY(launch_search_lane_one(a, w, sc, kSearchLane48, c->aux2));
+    if (prof) HIP_TRY(hipEventRecord(ev[7], c->aux));
+    HIP_TRY(launch_aux(c->aux));
+    HIP_TRY(launch_search_lane_one(a, w, sc, kSearchLane84, c->aux));
+    if (prof) HIP_TRY(hipEventRecord(ev[8], c->aux));
+    HIP_TRY(hipEventRecord(c->ev_join, c->aux));
+    HIP_TRY(hipEventRecord(c->ev_join2, c->aux2));
+    HIP_TRY(launch_search_lane_one(a, w, sc, kSearchLane88, s));
+    HIP_TRY(hipStreamWaitEvent(s, c->ev_join, 0));
+    HIP_TRY(hipStreamWaitEvent(s, c->ev_join2, 0));
+    // "main search" spans all three lane kernels here (and the cooperative shapes beside them)
+    if (prof) HIP_TRY(hipEventRecord(ev[4], s));
+    if (prof) HIP_TRY(hipEventRecord(ev[5], s));
+    HIP_TRY(launch_nn_tail(a, w, c->d_nn.p, c->state_cur, s));
+    if (prof) {
+      HIP_TRY(hipEventRecord(ev[6], s));
+      c->ev_has_large[eb] = true;
+      c->ev_serial[eb] = false;
+      c->ev_pending = eb;
+      c->ev_cur ^= 1;
+    }
+    if (a.nn_mode) c->state_cur ^= 1;
+    return FME_OK;
+  }
   if (!c->concurrent_search) {
     if (prof && has_aux) HIP_TRY(hipEventRecord(ev[7], s));
     HIP_TRY(launch_aux(s));

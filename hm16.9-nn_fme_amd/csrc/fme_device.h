@@ -103,6 +103,9 @@ int tiles_per_block();
 int search_kernel_of(int cls);                      // kSearchLane48 .. kSearchCoopLarge
 int search_blocks_for(int cls, int cnt);           // blocks of its kernel for cnt jobs
 hipError_t launch_search_lane(const BatchArgs& a, const WorkBufs& w, const Schedule& sc, hipStream_t s);
+// one lane kernel (kSearchLane48 / 84 / 88) on stream s
+hipError_t launch_search_lane_one(const BatchArgs& a, const WorkBufs& w, const Schedule& sc, int kern,
+                                  hipStream_t s);
 hipError_t launch_search_large(const BatchArgs& a, const WorkBufs& w, const Schedule& sc, hipStream_t s);
 hipError_t launch_search_small(const BatchArgs& a, const WorkBufs& w, const Schedule& sc, hipStream_t s);
 int lane_lanes_per_pu(int cls);                    // 0: not a lane-kernel class

@@ -81,43 +81,71 @@ __device__ __forceinline__ int emi_pushes(const fme_job& j) {
 // ---------------------------------------------------------------------------------------
 // classify: class histogram + first pass of the NN writer prefix-max
 // ---------------------------------------------------------------------------------------
+// PU shape -> class: [(w/4 - 1) * 16 + h/4 - 1], 255 = not an HEVC inter PU shape
+struct ClassLut {
+  uint8_t v[256];
+  constexpr ClassLut() : v() {
+    for (int i = 0; i < 256; i++) v[i] = 255;
+    for (int c = 0; c < kNumClasses; c++) v[((kClassW[c] >> 2) - 1) * 16 + (kClassH[c] >> 2) - 1] = (uint8_t)c;
+  }
+};
+__constant__ ClassLut kClassLut = ClassLut();
+
+// All of a block's loads (its 4 jobs per lane, the class table, the picture descriptors) are
+// issued before any of them is used: the kernel is a few dependent memory latencies long.
 __global__ __launch_bounds__(kBlock) void k_classify(BatchArgs a, WorkBufs w) {
+  constexpr int Q = kJobsPerScanBlock / kBlock;
   __shared__ int32_t hist[kNumClasses + 1];
   __shared__ int32_t agg[9];
+  __shared__ uint8_t lut[256];
+  __shared__ int32_t pic_w[FME_MAX_PICTURES], pic_h[FME_MAX_PICTURES];  // pic_w -1: slot unset
   const int tid = threadIdx.x;
+  const int base = blockIdx.x * kJobsPerScanBlock;
+  fme_job jb[Q];
+#pragma unroll
+  for (int q = 0; q < Q; q++) {
+    const int i = base + q * kBlock + tid;
+    if (i < a.n) jb[q] = a.jobs[i];
+  }
+  lut[tid] = kClassLut.v[tid];
+  if (tid < FME_MAX_PICTURES) {
+    const PicDesc p = a.pics[tid];
+    pic_w[tid] = p.luma ? p.width : -1;
+    pic_h[tid] = p.height;
+  }
   if (tid < kNumClasses + 1) hist[tid] = 0;
   if (tid < 9) agg[tid] = -1;
   __syncthreads();
   int mx[9];
 #pragma unroll
   for (int f = 0; f < 9; f++) mx[f] = -1;
-  const int base = blockIdx.x * kJobsPerScanBlock;
 #pragma unroll
-  for (int q = 0; q < kJobsPerScanBlock / kBlock; q++) {
+  for (int q = 0; q < Q; q++) {
     const int i = base + q * kBlock + tid;
-    if (i >= a.n) break;
-    const fme_job j = a.jobs[i];
-    int c = class_of(j.w, j.h);
-    // reject what would make the search read undefined memory
-    bool ok = j.ref_id < FME_MAX_PICTURES && j.lambda_id < FME_MAX_LAMBDAS &&
-              a.pics[j.ref_id].luma != nullptr;
-    if (ok) {
-      if (j.key_offset >= 0) {
-        ok = (int64_t)j.key_offset + (int64_t)j.w * j.h <= a.n_keys;
-      } else {
-        ok = j.org_id < FME_MAX_PICTURES && a.pics[j.org_id].luma != nullptr &&
-             (int)j.x + j.w <= a.pics[j.org_id].width && (int)j.y + j.h <= a.pics[j.org_id].height;
+    if (i < a.n) {
+      const fme_job& j = jb[q];
+      int c = ((j.w | j.h) & 3) == 0 && j.w >= 4 && j.w <= 64 && j.h >= 4 && j.h <= 64
+                  ? lut[((j.w >> 2) - 1) * 16 + (j.h >> 2) - 1] : 255;
+      // reject what would make the search read undefined memory
+      bool ok = j.ref_id < FME_MAX_PICTURES && j.lambda_id < FME_MAX_LAMBDAS && pic_w[j.ref_id] >= 0;
+      if (ok) {
+        if (j.key_offset >= 0) {
+          ok = (int64_t)j.key_offset + (int64_t)j.w * j.h <= a.n_keys;
+        } else {
+          ok = j.org_id < FME_MAX_PICTURES && pic_w[j.org_id] >= 0 &&
+               (int)j.x + j.w <= pic_w[j.org_id] && (int)j.y + j.h <= pic_h[j.org_id];
+        }
       }
-    }
-    if (!ok) c = 255;
-    w.cls[i] = (uint8_t)c;
-    atomicAdd(&hist[c == 255 ? kNumClasses : c], 1);
-    if (j.flags & FME_JOB_EMI) {
-      const int np = emi_pushes(j);
+      if (!ok) c = 255;
+      w.cls[i] = (uint8_t)c;
+      atomicAdd(&hist[c == 255 ? kNumClasses : c], 1);
+      if (j.flags & FME_JOB_EMI) {
+        const int np = emi_pushes(j);
 #pragma unroll
-      for (int s = 0; s < 8; s++)
-        if (np > s) mx[s] = max(mx[s], i);
-      mx[8] = max(mx[8], i);
+        for (int s = 0; s < 8; s++)
+          if (np > s) mx[s] = max(mx[s], i);
+        mx[8] = max(mx[8], i);
+      }
     }
   }
 #pragma unroll
@@ -136,15 +164,19 @@ __global__ __launch_bounds__(kBlock) void k_scatter(BatchArgs a, WorkBufs w, Sch
   const int base = blockIdx.x * kJobsPerScanBlock;
   int rank[kJobsPerScanBlock / kBlock];
   int cls[kJobsPerScanBlock / kBlock];
+  fme_job jb[kJobsPerScanBlock / kBlock];   // loaded up front, beside the class bytes
 #pragma unroll
   for (int q = 0; q < kJobsPerScanBlock / kBlock; q++) {
     const int i = base + q * kBlock + tid;
     cls[q] = 255;
     if (i < a.n) {
       cls[q] = w.cls[i];
-      if (cls[q] < kNumClasses) rank[q] = atomicAdd(&cnt[cls[q]], 1);
+      jb[q] = a.jobs[i];
     }
   }
+#pragma unroll
+  for (int q = 0; q < kJobsPerScanBlock / kBlock; q++)
+    if (cls[q] < kNumClasses) rank[q] = atomicAdd(&cnt[cls[q]], 1);
   __syncthreads();
   if (tid < kNumClasses) basep[tid] = cnt[tid] ? atomicAdd(&w.cursor[tid], cnt[tid]) : 0;
   __syncthreads();
@@ -154,40 +186,35 @@ __global__ __launch_bounds__(kBlock) void k_scatter(BatchArgs a, WorkBufs w, Sch
     if (cls[q] < kNumClasses) {
       const int dst = sc.class_off[cls[q]] + basep[cls[q]] + rank[q];
       w.perm[dst] = i;
-      w.sjobs[dst] = a.jobs[i];
+      w.sjobs[dst] = jb[q];
     }
   }
-}
-
-// Exclusive prefix-max over the per-block aggregates (one workgroup of 1024 lanes).
-__global__ __launch_bounds__(1024) void k_scan_blocks(WorkBufs w, int nblk) {
-  __shared__ int32_t buf[1024];
-  const int tid = threadIdx.x;
-  const int per = (nblk + 1023) / 1024;
+  // Exclusive prefix-max of the NN-writer aggregates over the blocks before this one: k_nn_tail's
+  // carry-in of the stale-state scan.  It depends on k_classify only, so it is computed here,
+  // before the search, instead of by a serial pass between the search and the tail.
+  __shared__ int32_t red[kBlock / 64][9];
+  int m[9];
+#pragma unroll
+  for (int f = 0; f < 9; f++) m[f] = -1;
+  for (int b = tid; b < (int)blockIdx.x; b += kBlock) {
+#pragma unroll
+    for (int f = 0; f < 9; f++) m[f] = max(m[f], w.blk_agg[b * 9 + f]);
+  }
+#pragma unroll
   for (int f = 0; f < 9; f++) {
-    // local inclusive over this thread's consecutive blocks
-    int m = -1;
-    for (int q = 0; q < per; q++) {
-      const int b = tid * per + q;
-      if (b < nblk) m = max(m, w.blk_agg[b * 9 + f]);
-    }
-    buf[tid] = m;
-    __syncthreads();
-    for (int off = 1; off < 1024; off <<= 1) {
-      const int o = tid >= off ? buf[tid - off] : -1;
-      __syncthreads();
-      buf[tid] = max(buf[tid], o);
-      __syncthreads();
-    }
-    int run = tid > 0 ? buf[tid - 1] : -1;  // exclusive carry into this thread's first block
-    for (int q = 0; q < per; q++) {
-      const int b = tid * per + q;
-      if (b < nblk) {
-        w.blk_prefix[b * 9 + f] = run;
-        run = max(run, w.blk_agg[b * 9 + f]);
-      }
-    }
-    __syncthreads();
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) m[f] = max(m[f], __shfl_xor(m[f], off));
+  }
+  if ((tid & 63) == 0) {
+#pragma unroll
+    for (int f = 0; f < 9; f++) red[tid >> 6][f] = m[f];
+  }
+  __syncthreads();
+  if (tid < 9) {
+    int r = red[0][tid];
+#pragma unroll
+    for (int q = 1; q < kBlock / 64; q++) r = max(r, red[q][tid]);
+    w.blk_prefix[blockIdx.x * 9 + tid] = r;
   }
 }
 
@@ -450,9 +477,6 @@ hipError_t launch_scatter(const BatchArgs& a, const WorkBufs& w, const Schedule&
 hipError_t launch_nn_tail(const BatchArgs& a, const WorkBufs& w, const float* nn_params,
                           int state_in, hipStream_t s) {
   const int nb = nblocks(a.n);
-  hipLaunchKernelGGL(k_scan_blocks, dim3(1), dim3(1024), 0, s, w, nb);
-  hipError_t e = hipGetLastError();
-  if (e != hipSuccess) return e;
   hipLaunchKernelGGL(k_nn_tail, dim3(nb), dim3(kTailNT), 0, s, a, w, nn_params, state_in);
   return hipGetLastError();
 }

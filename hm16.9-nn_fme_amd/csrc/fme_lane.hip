@@ -866,4 +866,15 @@ hipError_t launch_search_lane(const BatchArgs& a, const WorkBufs& w, const Sched
   return hipGetLastError();
 }
 
+hipError_t launch_search_lane_one(const BatchArgs& a, const WorkBufs& w, const Schedule& sc, int kern,
+                                  hipStream_t s) {
+  const int blocks = sc.prefix[kern][kNumClasses];
+  if (blocks <= 0) return hipSuccess;
+  if (kern == kSearchLane48) hipLaunchKernelGGL(k_search_lane48, dim3(blocks), dim3(kLaneNT), 0, s, a, w, sc);
+  else if (kern == kSearchLane84) hipLaunchKernelGGL(k_search_lane84, dim3(blocks), dim3(kLaneNT), 0, s, a, w, sc);
+  else if (kern == kSearchLane88) hipLaunchKernelGGL(k_search_lane88, dim3(blocks), dim3(kLaneNT), 0, s, a, w, sc);
+  else return hipErrorInvalidValue;
+  return hipGetLastError();
+}
+
 }  // namespace fme
