@@ -16,10 +16,11 @@ one host core (HM is single-threaded) over a bounded sample of the same job mix;
 `cpu_baseline_all_cores` runs one job stream per host core.  Both run
 before the GPU is initialised.
 
-`roofline` is for the main search launch (the lane-per-unit EMI + FracDIF kernels of the 18
-power-of-two PU shapes, ~99.4 % of the jobs): its algorithmic bytes (SURVEY.md §8(d) per-PU
-figure summed over the jobs it processes) over its average duration, from HIP events recorded
-around it on its own stream during the timed steps.  The path is integer-VALU bound, so the
+`roofline` is for the main search phase (the lane-per-unit EMI + FracDIF kernels of the 18
+power-of-two PU shapes, ~99.4 % of the jobs; the 8x8-, 8x4- and 4x8-unit kernels run
+concurrently on three streams, k_search_lane88 dominant): its algorithmic bytes (SURVEY.md §8(d)
+per-PU figure summed over the jobs it processes) over the phase's average duration, from HIP
+events recorded on the batch stream at the fork and after the join during the timed steps.  The path is integer-VALU bound, so the
 VALU roof (reference integer ops, §8(d)) is reported beside the HBM one.
 """
 import argparse
@@ -488,7 +489,8 @@ def main():
                 "unit": "GB/s",
                 "frac": achieved / HBM_PEAK_GBS,
                 "traffic": traffic,
-                "kernel": "main search launch: fme::k_search_lane{48,84,88} (EMI + FracDIF)",
+                "kernel": "main search phase: fme::k_search_lane{48,84,88} (EMI + FracDIF) on three "
+                          "concurrent streams, fork to join; k_search_lane88 dominant",
                 "kernel_jobs": int(len(small_jobs)),
                 "algorithmic_bytes_per_launch": bytes_small,
                 "kernel_ms": tm["search_main"],

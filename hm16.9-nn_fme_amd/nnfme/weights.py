@@ -41,3 +41,104 @@ def unpack(params):
         out[name] = np.asarray(params[o:o + n]).reshape(shape)
         o += n
     return out
+
+
+# ---- the reference's weight files ------------------------------------
+# DL/<name>/<qp>/*.csv as NN_training.ipynb's export_parameters / export_mapper write them and
+# DL/edit.sh renumbers and indents them for pasting into TEncSearch::init: one line per matrix
+# row, "\t\t\t" indent, "," separated, ";" after the last value; mapper_<qp>.csv holds the mean
+# and std rows of the nine distortions.
+CSV_FILES = [
+    ("embs0", "1.emb0-weight"), ("embs1", "2.emb1-weight"), ("in_h1", "3.lins0-weight"),
+    ("h1_h2", "4.lins1-weight"), ("h2_out", "5.outp-weight"), ("b1", "6.lins0-bias"),
+    ("b2", "7.lins1-bias"), ("bout", "8.outp-bias"), ("BN_gamma_in", "9.bn-weight"),
+    ("BN_gamma_1", "10.bns0-weight"), ("BN_gamma_2", "11.bns1-weight"),
+    ("BN_beta_1", "12.bns0-bias"), ("BN_beta_2", "13.bns1-bias"),
+]
+# fastai v0.7 MixedInputModel state_dict keys (DL/models/QP<qp>_*.h5 are torch.save'd dicts)
+STATE_DICT_KEYS = {
+    "embs0": "embs.0.weight", "embs1": "embs.1.weight", "in_h1": "lins.0.weight",
+    "h1_h2": "lins.1.weight", "h2_out": "outp.weight", "b1": "lins.0.bias", "b2": "lins.1.bias",
+    "bout": "outp.bias", "BN_gamma_1": "bns.0.weight", "BN_beta_1": "bns.0.bias",
+    "BN_gamma_2": "bns.1.weight", "BN_beta_2": "bns.1.bias", "BN_gamma_in": "bn.weight",
+}
+_NUM = None
+
+
+def _numbers(text):
+    global _NUM
+    if _NUM is None:
+        import re
+        _NUM = re.compile(r"[-+]?(?:\d+\.\d*|\.\d+|\d+)(?:[eE][-+]?\d+)?")
+    return [float(t) for t in _NUM.findall(text)]
+
+
+def pack(tensors):
+    """{name: array} in LAYOUT -> float32[2060] (the fme_load_nn_weights order)."""
+    flat = []
+    for name, shape in LAYOUT:
+        a = np.asarray(tensors[name], dtype=np.float64)
+        if a.size != int(np.prod(shape)):
+            raise ValueError(f"{name}: {a.size} values, expected {int(np.prod(shape))}")
+        flat.append(a.reshape(-1))
+    return np.concatenate(flat).astype(np.float32)
+
+
+def load_csv_dir(path, qp):
+    """A DL/<name>/<qp>/ directory (edit.sh layout) -> float32[2060].  The values are parsed as
+    double and cast to float, as TEncSearch::init's comma initialisers do."""
+    t = {}
+    for name, stem in CSV_FILES:
+        with open(os.path.join(path, stem + ".csv")) as f:
+            t[name] = _numbers(f.read())
+    with open(os.path.join(path, f"14.mapper_{qp}.csv")) as f:
+        rows = [l for l in f.read().splitlines() if l.strip()]
+    if len(rows) != 2:
+        raise ValueError(f"{path}: mapper_{qp}.csv has {len(rows)} rows, expected mean and std")
+    t["mean"], t["stdev"] = _numbers(rows[0]), _numbers(rows[1])
+    return pack(t)
+
+
+def _fmt(v):
+    return np.format_float_positional(np.float32(v), unique=True, trim="-")
+
+
+def write_csv_dir(path, params, qp):
+    """float32[2060] -> a DL/<name>/<qp>/ directory in edit.sh's layout (load_csv_dir reads it
+    back bit-exactly: every value is the shortest decimal that round-trips its float32)."""
+    os.makedirs(path, exist_ok=True)
+    t = unpack(np.asarray(params, np.float32))
+    for name, stem in CSV_FILES:
+        a = np.atleast_2d(t[name])
+        sep = ", " if a.shape[0] == 1 else ","
+        rows = ["\t\t\t" + sep.join(_fmt(v) for v in row) for row in a]
+        with open(os.path.join(path, stem + ".csv"), "w") as f:
+            f.write((sep + "\n").join(rows) + ";\n")
+    with open(os.path.join(path, f"14.mapper_{qp}.csv"), "w") as f:
+        for row in (t["mean"], t["stdev"]):
+            f.write(",".join(repr(float(v)) for v in np.asarray(row, np.float64)) + ";\n")
+
+
+def from_state_dict(sd, mean, stdev):
+    """fastai v0.7 MixedInputModel state_dict (+ the mapper's mean / std) -> float32[2060].
+    NN_pred() uses the BatchNorm weights and biases only (TEncSearch.cpp:139-186): running
+    statistics and the input BatchNorm's bias are not read."""
+    t = {name: np.asarray(sd[key].detach().cpu().numpy() if hasattr(sd[key], "detach") else sd[key])
+         for name, key in STATE_DICT_KEYS.items()}
+    t["mean"], t["stdev"] = mean, stdev
+    return pack(t)
+
+
+def to_state_dict(params):
+    """float32[2060] -> {state_dict key: torch tensor} (the inverse of from_state_dict)."""
+    import torch
+    t = unpack(np.asarray(params, np.float32))
+    return {key: torch.from_numpy(np.ascontiguousarray(t[name])) for name, key in STATE_DICT_KEYS.items()}
+
+
+def load_checkpoint(path, mean, stdev):
+    """DL/models/QP<qp>_*.h5 (a torch.save'd state_dict despite the suffix) -> float32[2060].
+    Loaded with torch.load(weights_only=True): nothing in the file is executed."""
+    import torch
+    sd = torch.load(path, map_location="cpu", weights_only=True)
+    return from_state_dict(sd, mean, stdev)
