@@ -19,6 +19,9 @@
 
 #include "fme_device.h"
 
+#ifndef FME_TZ_DEFER_DEFAULT
+#define FME_TZ_DEFER_DEFAULT 1
+#endif
 #ifndef FME_LANE_STREAMS_DEFAULT
 #define FME_LANE_STREAMS_DEFAULT 1
 #endif
@@ -109,8 +112,15 @@ struct fme_ctx {
   // integer search: staging for the host entry point, timing events
   DevBuf<fme_tz_ext> d_tz_ext;
   DevBuf<uint32_t> d_tz_sad;
+  DevBuf<uint32_t> d_tz_rst;   // raster hand-off records [n][8]
+  DevBuf<int32_t> d_tz_rq;     // raster queues [3][n] + 3 lengths
+  bool tz_defer = FME_TZ_DEFER_DEFAULT;   // FME_TZ_DEFER=0/1: raster searches in a second pass
   hipEvent_t ev_tz[2] = {nullptr, nullptr};
   bool tz_timed = false;
+  // predInterSearch producer: m_integerMv2Nx2N[REF_PIC_LIST_0][k] (TEncSearch.h:118), AMVP staging
+  int16_t int_mv_2n[FME_MAX_REFS][2] = {};
+  DevBuf<AmvpTask> d_amvp;
+  DevBuf<uint32_t> d_amvp_sad;
 
   std::unique_ptr<fme_ctx> single;  // private context for the single-PU entry points
   DevBuf<uint8_t> single_pic;
@@ -200,6 +210,7 @@ int fme_create(int device, const fme_config* cfg, fme_ctx** out_ctx) {
   HIP_TRY(hipStreamCreateWithFlags(&c->aux, hipStreamNonBlocking));
   if (const char* e = getenv("FME_SERIAL_SEARCH")) c->concurrent_search = (e[0] == '0');
   if (const char* e = getenv("FME_LANE_STREAMS")) c->lane_streams = (e[0] == '1');
+  if (const char* e = getenv("FME_TZ_DEFER")) c->tz_defer = (e[0] == '1');
   HIP_TRY(hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming));
   HIP_TRY(hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming));
   if (cfg->max_jobs > 0) {
@@ -224,7 +235,8 @@ int fme_destroy(fme_ctx* c) {
   for (int i = 0; i < FME_MAX_PICTURES; i++)
     if (c->chroma_owned[i]) (void)hipFree(c->chroma_owned[i]);
   c->d_mc_jobs.release(); c->d_mc_planes.release(); c->d_mc_invalid.release();
-  c->d_tz_ext.release(); c->d_tz_sad.release();
+  c->d_tz_ext.release(); c->d_tz_sad.release(); c->d_tz_rst.release(); c->d_tz_rq.release();
+  c->d_amvp.release(); c->d_amvp_sad.release();
   for (auto& e : c->ev_tz)
     if (e) (void)hipEventDestroy(e);
   for (auto& e : c->ev_mc)
@@ -631,6 +643,15 @@ int fme_integer_search_device(fme_ctx* c, fme_job* d_jobs, const fme_tz_ext* d_e
   ta.jobs_out = d_jobs;
   ta.ext = d_ext;
   ta.sad = d_sad;
+  ta.defer = c->tz_defer ? 1 : 0;
+  if (c->tz_defer) {
+    HIP_TRY(c->d_tz_rst.reserve((size_t)n * 8));
+    HIP_TRY(c->d_tz_rq.reserve((size_t)3 * n + 4));
+    ta.rst = c->d_tz_rst.p;
+    ta.rq = c->d_tz_rq.p;
+    ta.rqn = c->d_tz_rq.p + (size_t)3 * n;
+    HIP_TRY(hipMemsetAsync(ta.rqn, 0, 4 * sizeof(int32_t), s));
+  }
   if (c->profiling) HIP_TRY(hipEventRecord(c->ev_tz[0], s));
   // the three unit-shape kernels are latency-bound and independent: 4x8 and 8x4 units on the two
   // auxiliary streams, 8x8 units on the caller's stream, joined before returning
@@ -646,6 +667,22 @@ int fme_integer_search_device(fme_ctx* c, fme_job* d_jobs, const fme_tz_ext* d_e
   HIP_TRY(hipEventRecord(c->ev_join2, c->aux2));
   HIP_TRY(hipStreamWaitEvent(s, c->ev_join, 0));
   HIP_TRY(hipStreamWaitEvent(s, c->ev_join2, 0));
+  if (c->tz_defer) {
+    // pass 2: the queued raster searches, one PU per wave (queue lengths read back: one sync)
+    HIP_TRY(hipMemcpyAsync(c->h_counts, ta.rqn, 3 * sizeof(int32_t), hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    const int nq[3] = {c->h_counts[0], c->h_counts[1], c->h_counts[2]};
+    HIP_TRY(hipEventRecord(c->ev_fork, s));
+    HIP_TRY(hipStreamWaitEvent(c->aux, c->ev_fork, 0));
+    HIP_TRY(hipStreamWaitEvent(c->aux2, c->ev_fork, 0));
+    HIP_TRY(launch_tz_raster(ta, sc, 0, nq[0], c->aux));
+    HIP_TRY(launch_tz_raster(ta, sc, 1, nq[1], c->aux2));
+    HIP_TRY(launch_tz_raster(ta, sc, 2, nq[2], s));
+    HIP_TRY(hipEventRecord(c->ev_join, c->aux));
+    HIP_TRY(hipEventRecord(c->ev_join2, c->aux2));
+    HIP_TRY(hipStreamWaitEvent(s, c->ev_join, 0));
+    HIP_TRY(hipStreamWaitEvent(s, c->ev_join2, 0));
+  }
   if (c->profiling) HIP_TRY(hipEventRecord(c->ev_tz[1], s));
   c->tz_timed = c->profiling;
   return FME_OK;
@@ -951,6 +988,294 @@ int fme_accumulated_timings(fme_ctx* c, double* ms, int count, int reset) {
     c->acc_batches = 0;
   }
   return n;
+}
+
+}  // extern "C"
+
+// ---- predInterSearch's P-slice PU / reference loop ---------------------------
+namespace {
+
+// xGetMvpIdxBits (TEncSearch.cpp:4258-4284); m_auiMVPIdxCost[idx][num] (412-425)
+uint32_t mvp_idx_bits(int idx, int num) {
+  if (num == 1) return 0;
+  if (idx == 0) return 1;
+  return 1u + (uint32_t)(idx - 1) + (num - 1 > idx ? 1u : 0u);
+}
+// xGetBlkBits (TEncSearch.cpp:4286-4333), P slice: uiBlkBit[0]
+uint32_t blk_bits_p(int part_size) {
+  return (part_size == FME_PART_2Nx2N || part_size == FME_PART_NxN) ? 1u : 3u;
+}
+// TComRdCost::xGetExpGolombNumberOfBits (TComRdCost.cpp:172-185)
+uint32_t eg_bits(int v) {
+  uint32_t t = v <= 0 ? ((uint32_t)(-v) << 1) + 1u : (uint32_t)v << 1;
+  uint32_t len = 1;
+  while (t != 1) {
+    t >>= 1;
+    len += 2;
+  }
+  return len;
+}
+// TComRdCost::getCost (TComRdCost.h:165)
+uint32_t rd_cost(double ml, uint32_t bits) { return (uint32_t)((ml * (double)bits) / 65536.0); }
+// TComDataCU::clipMv (TComDataCU.cpp:2773-2786), max CU 64, quarter-pel
+void clip_qpel(int& x, int& y, int pw, int ph, int cu_x, int cu_y) {
+  x = std::min((pw + 8 - cu_x - 1) << 2, std::max((-64 - 8 - cu_x + 1) * 4, x));
+  y = std::min((ph + 8 - cu_y - 1) << 2, std::max((-64 - 8 - cu_y + 1) * 4, y));
+}
+int round4(int v) { return (v + 2) >> 2; }   // TComMv::divideByPowerOf2(2)
+
+bool valid_pu_shape(int w, int h) {
+  for (int k = 0; k < kNumClasses; k++)
+    if (kClassW[k] == w && kClassH[k] == h) return true;
+  return false;
+}
+
+}  // namespace
+
+extern "C" {
+
+int fme_pred_inter_reset(fme_ctx* c) {
+  if (!c) return fail(FME_E_INVALID, "fme_pred_inter_reset: null ctx");
+  std::memset(c->int_mv_2n, 0, sizeof(c->int_mv_2n));
+  return FME_OK;
+}
+
+// The requests run in call order as far as anything observable goes; the GPU sees them as
+//   1. one AMVP template-cost launch over every (request, reference, candidate) with two candidates;
+//   2. integer searches by dependency level: a request that reads m_integerMv2Nx2N[k] waits for the
+//      level of the 2Nx2N request that last wrote it (per CTU the chain of 2Nx2N CUs in xCompressCU
+//      order; CTUs are independent), and the writers of a level run the EMI step (through
+//      fme_refine, with the NN state saved and restored) to publish their post-EMI integer MV;
+//   3. one fme_refine over all jobs in request order (the NN's carried state as in the reference);
+//   4. xCheckBestMVP and the reference choice on the host.
+int fme_pred_inter_p(fme_ctx* c, const fme_pu_req* reqs, fme_pu_res* res, int n, void* stream) {
+  if (!c || (n > 0 && (!reqs || !res))) return fail(FME_E_INVALID, "fme_pred_inter_p: null argument");
+  if (n <= 0) return n == 0 ? FME_OK : fail(FME_E_INVALID, "fme_pred_inter_p: n = %d", n);
+  HIP_TRY(hipSetDevice(c->device));
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  // ---- validation (nothing runs on a bad batch) ----
+  for (int i = 0; i < n; i++) {
+    const fme_pu_req& q = reqs[i];
+    const PicDesc& org = c->pics[q.org_id < FME_MAX_PICTURES ? q.org_id : 0];
+    if (!valid_pu_shape(q.w, q.h) || q.part_size > FME_PART_nRx2N || q.num_refs < 1 || q.num_refs > FME_MAX_REFS ||
+        q.org_id >= FME_MAX_PICTURES || !org.luma || q.x + q.w > org.width || q.y + q.h > org.height ||
+        q.lambda_id >= FME_MAX_LAMBDAS || !c->lambda_set[q.lambda_id] || (q.flags & ~FME_PU_LOSSLESS))
+      return fail(FME_E_INVALID, "fme_pred_inter_p: request %d invalid (shape %dx%d, part %d, refs %d)", i, q.w, q.h,
+                  q.part_size, q.num_refs);
+    for (int k = 0; k < q.num_refs; k++) {
+      if (q.ref_id[k] >= FME_MAX_PICTURES || !c->pics[q.ref_id[k]].luma || q.n_cand[k] < 1 || q.n_cand[k] > 2)
+        return fail(FME_E_INVALID, "fme_pred_inter_p: request %d reference %d invalid", i, k);
+      const PicDesc& r = c->pics[q.ref_id[k]];
+      if (r.width != org.width || r.height != org.height)
+        return fail(FME_E_INVALID, "fme_pred_inter_p: request %d reference %d size differs from the original", i, k);
+    }
+  }
+  int rc = sync_tables(c, s);
+  if (rc) return rc;
+  // ---- 1. xEstimateMvPredAMVP template costs ----
+  std::vector<int> base(n + 1, 0);
+  for (int i = 0; i < n; i++) base[i + 1] = base[i] + reqs[i].num_refs;
+  const int nj = base[n];
+  std::vector<AmvpTask> tasks;
+  std::vector<int> task_of((size_t)nj, -1);
+  for (int i = 0; i < n; i++) {
+    const fme_pu_req& q = reqs[i];
+    for (int k = 0; k < q.num_refs; k++) {
+      if (q.n_cand[k] < 2) continue;
+      task_of[base[i] + k] = (int)tasks.size();
+      for (int m = 0; m < 2; m++)
+        tasks.push_back(AmvpTask{q.x, q.y, q.w, q.h, q.org_id, q.ref_id[k], q.cu_x, q.cu_y, q.cand[k][m][0],
+                                 q.cand[k][m][1]});
+    }
+  }
+  std::vector<uint32_t> tsad(tasks.size());
+  if (!tasks.empty()) {
+    HIP_TRY(c->d_amvp.reserve(tasks.size()));
+    HIP_TRY(c->d_amvp_sad.reserve(tasks.size()));
+    HIP_TRY(hipMemcpyAsync(c->d_amvp.p, tasks.data(), tasks.size() * sizeof(AmvpTask), hipMemcpyHostToDevice, s));
+    AmvpArgs aa{c->d_amvp.p, c->d_pics.p, c->d_amvp_sad.p, (int32_t)tasks.size()};
+    HIP_TRY(launch_amvp_sad(aa, s));
+    HIP_TRY(hipMemcpyAsync(tsad.data(), c->d_amvp_sad.p, tasks.size() * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+  }
+  // ---- jobs: one xMotionEstimation per (request, reference) ----
+  std::vector<fme_job> jobs((size_t)nj);
+  std::vector<fme_tz_ext> ext((size_t)nj);
+  std::vector<uint8_t> amvp_idx((size_t)nj, 0);
+  for (int i = 0; i < n; i++) {
+    const fme_pu_req& q = reqs[i];
+    const PicDesc& org = c->pics[q.org_id];
+    const double ml = c->mlambda[q.lambda_id];
+    const int range = q.search_range ? q.search_range : 64;
+    for (int k = 0; k < q.num_refs; k++) {
+      const int jx = base[i] + k;
+      int idx = 0;
+      if (task_of[jx] >= 0) {   // uiBestCost > uiTmpCost: the first least cost wins
+        uint32_t best = 0xFFFFFFFFu;
+        for (int m = 0; m < 2; m++) {
+          const uint32_t cost =
+              (uint32_t)((double)tsad[task_of[jx] + m] + ((double)mvp_idx_bits(m, 2) * ml) / 65536.0);
+          if (best > cost) {
+            best = cost;
+            idx = m;
+          }
+        }
+      }
+      amvp_idx[jx] = (uint8_t)idx;
+      uint32_t bits = blk_bits_p(q.part_size);
+      if (q.num_refs > 1) bits += (uint32_t)k + 1u - (k == q.num_refs - 1 ? 1u : 0u);
+      bits += mvp_idx_bits(idx, 2);
+      const int px = q.cand[k][idx][0], py = q.cand[k][idx][1];
+      // xSetSearchRange (TEncSearch.cpp:4602-4624)
+      int cx = px, cy = py;
+      clip_qpel(cx, cy, org.width, org.height, q.cu_x, q.cu_y);
+      int lx = cx - (range << 2), ly = cy - (range << 2), rx = cx + (range << 2), ry = cy + (range << 2);
+      clip_qpel(lx, ly, org.width, org.height, q.cu_x, q.cu_y);
+      clip_qpel(rx, ry, org.width, org.height, q.cu_x, q.cu_y);
+      fme_job& j = jobs[jx];
+      j = fme_job{};
+      j.x = q.x; j.y = q.y; j.w = q.w; j.h = q.h;
+      j.org_id = q.org_id; j.ref_id = q.ref_id[k];
+      j.mvp_x = (int16_t)px; j.mvp_y = (int16_t)py;
+      j.lt_x = (int16_t)round4(lx); j.lt_y = (int16_t)round4(ly);
+      j.rb_x = (int16_t)round4(rx); j.rb_y = (int16_t)round4(ry);
+      j.flags = (uint8_t)(FME_JOB_EMI | ((q.flags & FME_PU_LOSSLESS) ? FME_JOB_LOSSLESS : 0u));
+      j.lambda_id = q.lambda_id;
+      j.bits_in = (uint16_t)bits;
+      j.key_offset = -1;
+      fme_tz_ext& e = ext[jx];
+      e = fme_tz_ext{};
+      e.cu_x = q.cu_x; e.cu_y = q.cu_y;
+      e.search_range = (uint8_t)range;
+      const bool reads = !(q.part_size == FME_PART_2Nx2N && q.depth == 0);
+      e.flags = reads ? FME_TZ_PRED2NX2N : 0;
+    }
+  }
+  // ---- 2. dependency levels of m_integerMv2Nx2N ----
+  std::vector<int> level((size_t)n, 0), src((size_t)nj, -1);   // src: job whose post-EMI MV is read
+  int last[FME_MAX_REFS] = {-1, -1, -1, -1};
+  int max_level = 0;
+  for (int i = 0; i < n; i++) {
+    const fme_pu_req& q = reqs[i];
+    const bool reads = !(q.part_size == FME_PART_2Nx2N && q.depth == 0);
+    if (reads)
+      for (int k = 0; k < q.num_refs; k++)
+        if (last[k] >= 0) {
+          level[i] = std::max(level[i], level[last[k]] + 1);
+          src[base[i] + k] = base[last[k]] + k;
+        }
+    if (q.part_size == FME_PART_2Nx2N)
+      for (int k = 0; k < q.num_refs; k++) last[k] = i;
+    max_level = std::max(max_level, level[i]);
+  }
+  std::vector<std::vector<int>> by_level((size_t)max_level + 1);
+  for (int i = 0; i < n; i++) by_level[level[i]].push_back(i);
+  std::vector<int16_t> emi_mv((size_t)nj * 2, 0);   // post-EMI integer MV of 2Nx2N jobs
+  std::vector<fme_job> lj;
+  std::vector<fme_tz_ext> le;
+  std::vector<int> lidx;
+  std::vector<fme_result> lres;
+  for (int L = 0; L <= max_level; L++) {
+    lj.clear(); le.clear(); lidx.clear();
+    for (int i : by_level[L])
+      for (int k = 0; k < reqs[i].num_refs; k++) {
+        const int jx = base[i] + k;
+        fme_tz_ext e = ext[jx];
+        if (e.flags & FME_TZ_PRED2NX2N) {
+          const int sj = src[jx];
+          e.pred2n_x = sj >= 0 ? emi_mv[2 * sj] : c->int_mv_2n[k][0];
+          e.pred2n_y = sj >= 0 ? emi_mv[2 * sj + 1] : c->int_mv_2n[k][1];
+        }
+        lj.push_back(jobs[jx]);
+        le.push_back(e);
+        lidx.push_back(jx);
+      }
+    rc = fme_integer_search(c, lj.data(), le.data(), nullptr, (int)lj.size(), stream);
+    if (rc) return rc;
+    for (size_t m = 0; m < lj.size(); m++) jobs[lidx[m]] = lj[m];
+    if (L == max_level) break;
+    // writers of this level publish their post-EMI integer MV for the levels above
+    lj.clear(); lidx.clear();
+    for (int i : by_level[L])
+      if (reqs[i].part_size == FME_PART_2Nx2N)
+        for (int k = 0; k < reqs[i].num_refs; k++) {
+          lj.push_back(jobs[base[i] + k]);
+          lidx.push_back(base[i] + k);
+        }
+    if (lj.empty()) continue;
+    uint32_t st[12];
+    rc = fme_nn_get_state(c, st);
+    if (rc) return rc;
+    lres.resize(lj.size());
+    rc = fme_refine(c, lj.data(), lres.data(), (int)lj.size(), stream);
+    if (rc) return rc;
+    rc = fme_nn_set_state(c, st);
+    if (rc) return rc;
+    for (size_t m = 0; m < lj.size(); m++) {
+      emi_mv[2 * lidx[m]] = lres[m].mv_int_x;
+      emi_mv[2 * lidx[m] + 1] = lres[m].mv_int_y;
+    }
+  }
+  // ---- 3. the sub-pel path over every job in request order ----
+  std::vector<fme_result> r((size_t)nj);
+  rc = fme_refine(c, jobs.data(), r.data(), nj, stream);
+  if (rc) return rc;
+  // ---- 4. xCheckBestMVP, reference choice, m_integerMv2Nx2N ----
+  for (int i = 0; i < n; i++) {
+    const fme_pu_req& q = reqs[i];
+    const double ml = c->mlambda[q.lambda_id];
+    fme_pu_res& o = res[i];
+    o = fme_pu_res{};
+    uint32_t best = 0xFFFFFFFFu;
+    for (int k = 0; k < q.num_refs; k++) {
+      const int jx = base[i] + k;
+      const fme_result& rr = r[jx];
+      const int mx = rr.mv_x, my = rr.mv_y;
+      int idx = amvp_idx[jx];
+      uint32_t bits = rr.bits, cost = rr.cost;
+      if (q.n_cand[k] >= 2) {
+        const int org_bits = (int)(eg_bits(mx - q.cand[k][idx][0]) + eg_bits(my - q.cand[k][idx][1]) +
+                                   mvp_idx_bits(idx, 2));
+        int best_bits = org_bits, best_idx = idx;
+        for (int m = 0; m < q.n_cand[k]; m++) {
+          if (m == idx) continue;
+          const int b = (int)(eg_bits(mx - q.cand[k][m][0]) + eg_bits(my - q.cand[k][m][1]) + mvp_idx_bits(m, 2));
+          if (b < best_bits) {
+            best_bits = b;
+            best_idx = m;
+          }
+        }
+        if (best_idx != idx) {
+          idx = best_idx;
+          const uint32_t org_total = bits;
+          bits = org_total - (uint32_t)org_bits + (uint32_t)best_bits;
+          cost = (cost - rd_cost(ml, org_total)) + rd_cost(ml, bits);
+        }
+      }
+      o.ref_cost[k] = cost;
+      o.ref_bits[k] = bits;
+      o.ref_mv[k][0] = (int16_t)mx;
+      o.ref_mv[k][1] = (int16_t)my;
+      o.ref_mvp_idx[k] = (uint8_t)idx;
+      if (cost < best) {
+        best = cost;
+        o.cost = cost;
+        o.bits = bits;
+        o.mv_x = (int16_t)mx;
+        o.mv_y = (int16_t)my;
+        o.ref_idx = (uint8_t)k;
+        o.mvp_idx = (uint8_t)idx;
+        o.mvp_x = q.cand[k][idx][0];
+        o.mvp_y = q.cand[k][idx][1];
+      }
+    }
+    if (q.part_size == FME_PART_2Nx2N)
+      for (int k = 0; k < q.num_refs; k++) {
+        c->int_mv_2n[k][0] = r[base[i] + k].mv_int_x;
+        c->int_mv_2n[k][1] = r[base[i] + k].mv_int_y;
+      }
+  }
+  return FME_OK;
 }
 
 }  // extern "C"

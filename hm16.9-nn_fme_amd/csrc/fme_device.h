@@ -40,6 +40,23 @@ struct McArgs {
 };
 hipError_t launch_mc(const McArgs& a, hipStream_t s);
 
+// xGetTemplateCost's distortion (fme_mc.hip): SAD of the uni-pred luma prediction at one AMVP
+// candidate (clipMv'd against the CU origin) against the original, one task per wave.
+struct AmvpTask {
+  uint16_t x, y;
+  uint8_t w, h, org_id, ref_id;
+  uint16_t cu_x, cu_y;
+  int16_t mv_x, mv_y;
+};
+static_assert(sizeof(AmvpTask) == 16, "AmvpTask layout");
+struct AmvpArgs {
+  const AmvpTask* tasks;
+  const PicDesc* pics;
+  uint32_t* sad;
+  int32_t n;
+};
+hipError_t launch_amvp_sad(const AmvpArgs& a, hipStream_t s);
+
 
 // One batch as the device sees it.
 struct BatchArgs {
@@ -89,10 +106,15 @@ struct TzArgs {
   fme_job* jobs_out;          // mv_x / mv_y written per job
   const fme_tz_ext* ext;
   uint32_t* sad;              // may be null
+  int32_t defer;              // 1: pass 1 queues raster searches for pass 2 (k_tz_raster)
+  uint32_t* rst;              // [n][8] raster hand-off records, by job index
+  int32_t* rq;                // [3][n] queued job indices per kernel
+  int32_t* rqn;               // [3] queue lengths
 };
 int tz_kernel_of(int cls);    // 0: 4x8 units, 1: 8x4, 2: 8x8
 int tz_lanes_per_pu(int cls);
 hipError_t launch_tz(const TzArgs& ta, const Schedule& sc, int kid, hipStream_t s);
+hipError_t launch_tz_raster(const TzArgs& ta, const Schedule& sc, int kid, int nq, hipStream_t s);
 
 // Host-side launch helpers (fme_kernels.hip).
 int pus_per_tile(int cls);

@@ -318,10 +318,51 @@ __global__ __launch_bounds__(kMcBlock) void k_mc(McArgs a) {
   }
 }
 
+// xGetTemplateCost (TEncSearch.cpp:4397-4436) distortion: clipMv of the candidate, the uni-pred
+// luma prediction xPredInterBlk(COMPONENT_Y, ..., bi = false) and getDistPart(DF_SAD) against the
+// original (plain SAD at every width: setDistParam(UInt, UInt, DFunc) sets no subsampling,
+// TComRdCost.cpp:187-197).  One task per wave: the lanes walk the PU's 4x4 units.
+__global__ __launch_bounds__(kMcBlock) void k_amvp_sad(AmvpArgs a) {
+  const int task = (int)(blockIdx.x * (kMcBlock / 64) + (threadIdx.x >> 6));
+  if (task >= a.n) return;   // wave-uniform
+  const int lane = (int)(threadIdx.x & 63);
+  const AmvpTask t = a.tasks[task];
+  const PicDesc ref = a.pics[t.ref_id], org = a.pics[t.org_id];
+  int mx = t.mv_x, my = t.mv_y;
+  clip_mv(mx, my, ref.width, ref.height, t.cu_x, t.cu_y);
+  uint32_t hlo, hhi, vlo, vhi;
+  luma_taps(mx & 3, hlo, hhi);
+  luma_taps(my & 3, vlo, vhi);
+  const bool al = ((ref.stride | (int)(uintptr_t)ref.luma) & 3) == 0;
+  const int uxn = t.w >> 2, units = uxn * (t.h >> 2);
+  uint32_t sad = 0;
+  for (int u = lane; u < units; u += 64) {
+    const int x = t.x + 4 * (u % uxn), y = t.y + 4 * (u / uxn);
+    UnitWin<8, 4> w;
+    w.load(Plane{ref.luma, ref.stride, ref.width, ref.height}, al, x + (mx >> 2), y + (my >> 2));
+    int o[4][4];
+    w.pred(hlo, hhi, vlo, vhi, true, o);
+#pragma unroll
+    for (int r = 0; r < 4; r++) {
+      const uint8_t* op = org.luma + (size_t)(y + r) * org.stride + x;
+#pragma unroll
+      for (int c = 0; c < 4; c++) sad += (uint32_t)abs(o[r][c] - (int)gld8(op + c));
+    }
+  }
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) sad += (uint32_t)__shfl_xor((int)sad, off, 64);
+  if (lane == 0) a.sad[task] = sad;
+}
+
 }  // namespace
 
 hipError_t launch_mc(const McArgs& a, hipStream_t s) {
   if (a.n > 0) hipLaunchKernelGGL(k_mc, dim3((a.n + kMcJobs - 1) / kMcJobs), dim3(kMcBlock), 0, s, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_amvp_sad(const AmvpArgs& a, hipStream_t s) {
+  if (a.n > 0) hipLaunchKernelGGL(k_amvp_sad, dim3((a.n + kMcBlock / 64 - 1) / (kMcBlock / 64)), dim3(kMcBlock), 0, s, a);
   return hipGetLastError();
 }
 

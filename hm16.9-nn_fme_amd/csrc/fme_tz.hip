@@ -59,7 +59,7 @@ struct Range {
 
 enum Phase {
   P_START, P_ZERO, P_PRED, P_RANGE, P_FIRST, P_TWO1, P_TWO, P_RASTER_CHK, P_RASTER, P_STAR_CHK, P_STAR,
-  P_STAR_END, P_FULL, P_DONE
+  P_STAR_END, P_FULL, P_DONE, P_DEFER
 };
 
 struct Tz {
@@ -161,8 +161,9 @@ __device__ __forceinline__ bool two_point_has_more(const Tz& s) {
 // Next candidate of the search (x, y, point number, distance for xTZSearchHelp); false = done.
 // `more`: the following call continues the same list (diamond, two-point, raster, full search)
 // without a decision that depends on this candidate's result, so the two can be evaluated together.
+// `defer` (wave-uniform): stop at the raster (P_DEFER) and leave it to the second pass.
 __device__ __forceinline__ bool next_candidate(Tz& s, int pw, int ph, int cu_x, int cu_y, int& x, int& y, int& pnr,
-                                               int& pd, bool& more) {
+                                               int& pd, bool& more, bool defer) {
   more = false;
   for (int guard = 0; guard < 64; guard++) {   // phase changes between two tests are bounded
     switch (s.phase) {
@@ -248,7 +249,7 @@ __device__ __forceinline__ bool next_candidate(Tz& s, int pw, int ph, int cu_x, 
           s.bdist = 5;
           if (s.RR.l <= s.RR.r && s.RR.t <= s.RR.b) {
             s.rx = s.RR.l; s.ry = s.RR.t;
-            s.phase = P_RASTER;
+            s.phase = defer ? P_DEFER : P_RASTER;
           }
         }
         break;
@@ -297,24 +298,95 @@ __device__ __forceinline__ bool next_candidate(Tz& s, int pw, int ph, int cu_x, 
   return false;
 }
 
-// One lane: unit (ux, uy) of a PU of class geometry (PW x PH, units UW x UH).
+// Reference window of one unit at displacement (bx, by) from its origin: UH rows (FEN: even rows
+// only) of ND dwords from the aligned column, and the byte shift s0 of the first sample.
 template <int UW, int UH>
-__device__ __forceinline__ void tz_unit(const TzArgs& ta, int cls_off, int cls_cnt, int blk, int PW, int PH) {
+__device__ __forceinline__ void load_window(uint32_t (&w)[UH][UW / 4 + 1], uint32_t& s0, const PicDesc& ref, int bx,
+                                            int by, bool sub) {
+  constexpr int ND = UW / 4 + 1;
+  const int xa = bx & ~3;
+  s0 = (uint32_t)(bx - xa);
+  const bool inside = xa >= 0 && xa + 4 * ND <= ref.width;
+#pragma unroll
+  for (int r = 0; r < UH; r++) {
+    if (sub && (r & 1)) continue;   // FEN: even rows of the PU (UH is even)
+    const uint8_t* row = ref.luma + (size_t)clamp_i(by + r, 0, ref.height - 1) * ref.stride;
+    if (inside) {
+#pragma unroll
+      for (int q = 0; q < ND; q++) w[r][q] = gld32(row + xa + 4 * q);
+    } else {
+#pragma unroll
+      for (int q = 0; q < ND; q++) {
+        uint32_t v = 0;
+#pragma unroll
+        for (int k = 0; k < 4; k++) v |= gld8(row + clamp_i(xa + 4 * q + k, 0, ref.width - 1)) << (8 * k);
+        w[r][q] = v;
+      }
+    }
+  }
+}
+
+// One unit's share of the distortion (TComRdCost metric of the integer search) for a window.
+template <int UW, int UH>
+__device__ __forceinline__ uint32_t unit_part(const uint32_t (&w)[UH][UW / 4 + 1], uint32_t s0,
+                                              const uint32_t (&kk)[UH][UW / 2], int sk2, bool kbuf,
+                                              bool sad_metric, bool sub) {
+  int sop = 0, spp = 0;
+  uint32_t acc = 0;
+#pragma unroll
+  for (int r = 0; r < UH; r++) {
+    if (sub && (r & 1)) continue;
+#pragma unroll
+    for (int c = 0; c < UW / 4; c++) {
+      const uint32_t pv = __builtin_amdgcn_alignbyte(w[r][c + 1], w[r][c], s0);   // reference bytes
+      if (!kbuf) {
+        if (sad_metric) {
+          acc = __builtin_amdgcn_sad_u8(pv, kk[r][c], acc);
+        } else {
+          const uint32_t ps = pv ^ 0x80808080u;
+          sop = dot4(kk[r][c] ^ 0x80808080u, ps, sop);
+          spp = dot4(ps, ps, spp);
+        }
+      } else {
+        const uint32_t d0 = pk_sub(kk[r][2 * c], lo_pair(pv));
+        const uint32_t d1 = pk_sub(kk[r][2 * c + 1], hi_pair(pv));
+        if (sad_metric) {
+          acc = udot2(pk_abs(d0), 0x00010001u, udot2(pk_abs(d1), 0x00010001u, acc));
+        } else {
+          acc = (uint32_t)dot2(d1, d1, dot2(d0, d0, (int)acc));
+        }
+      }
+    }
+  }
+  uint32_t part = (!kbuf && !sad_metric) ? (uint32_t)(sk2 - 2 * sop + spp) : acc;
+  if (sub) part <<= 1;
+  return part;
+}
+
+// Raster hand-off record (pass 1 -> pass 2), by job index: the search state when
+// xTZSearch reaches its raster (bdist is 5 from there on, the round count is no longer read).
+constexpr int kTzRec = 8;   // best_sad, bx, by, pnr, RR.l, RR.r, RR.t, RR.b
+
+// One lane: unit u of a PU of class geometry (PW x PH, units UW x UH).
+//   RASTER = false: pass 1, groups of L lanes per PU (p = the group's PU in the class).  With
+//                   ta.defer a search that reaches its raster stops there and is queued.
+//   RASTER = true:  pass 2, one queued PU per wave: its raster points are spread over the wave's
+//                   64 / L groups (their (cost, scan index) minimum is the sequential scan's best),
+//                   then every group finishes the star refinement of the same PU in lock-step.
+template <int UW, int UH, bool RASTER>
+__device__ __forceinline__ void tz_unit(const TzArgs& ta, int cls_off, int cls_cnt, int p, int u, int L, int PW,
+                                        int PH, int rjid) {
+  constexpr int KID = UW == 4 ? 0 : (UH == 4 ? 1 : 2);
   const BatchArgs& a = ta.a;
   const int UX = PW / UW, LR = UX * (PH / UH);
-  int L = 1;
-  while (L < LR) L <<= 1;
-  const int gl = blk * kTzNT + (int)threadIdx.x;
-  int p = gl / L;
-  const int u = gl - p * L;
   const bool active = p < cls_cnt;
   if (!active) p = cls_cnt - 1;
   const bool real = u < LR;                 // padding lanes contribute 0
   const int uu = real ? u : 0;
   const int ux = uu % UX, uy = uu / UX;
 
-  const fme_job j = ta.sjobs[cls_off + p];
-  const int jid = ta.perm[cls_off + p];
+  const int jid = RASTER ? rjid : ta.perm[cls_off + p];
+  const fme_job j = RASTER ? a.jobs[jid] : ta.sjobs[cls_off + p];
   const fme_tz_ext e = ta.ext[jid];
   const PicDesc ref = a.pics[j.ref_id];
   const double ml = a.mlambda[j.lambda_id];
@@ -356,10 +428,53 @@ __device__ __forceinline__ void tz_unit(const TzArgs& ta, int cls_off, int cls_c
   s.RR = s.R;
   s.range = e.search_range ? e.search_range : 64;
   s.k = -1; s.dist = 1; s.ox = s.oy = 0; s.opnr = 0; s.ret = P_DONE;
-  if (j.flags & FME_JOB_BIPRED) {
+  const bool defer = !RASTER && ta.defer;
+  s.sx = s.sy = 0; s.px = s.py = 0; s.has_pred = false;
+  s.rx = s.ry = 0;
+  constexpr int ND = UW / 4 + 1;
+  if (RASTER) {
+    const uint32_t* rec = ta.rst + (size_t)jid * kTzRec;
+    s.best_sad = rec[0];
+    s.bx = (int)rec[1]; s.by = (int)rec[2]; s.pnr = (int)rec[3];
+    s.RR = Range{(int)rec[4], (int)rec[5], (int)rec[6], (int)rec[7]};
+    s.bdist = 5;
+    s.phase = P_STAR_CHK;
+    // the raster: point i of the scan is (RR.l + 5 (i % nx), RR.t + 5 (i / nx))
+    const int nx = (s.RR.r - s.RR.l) / 5 + 1, npts = nx * ((s.RR.b - s.RR.t) / 5 + 1);
+    const int g = ((int)threadIdx.x & 63) / L, G = 64 / L;
+    uint64_t best = ~0ull;
+    for (int base = 0; base < npts; base += G) {
+      const int i = base + g;
+      const bool valid = i < npts;
+      const int iy = valid ? i / nx : 0;
+      const int cx = s.RR.l + 5 * (valid ? i - iy * nx : 0), cy = s.RR.t + 5 * iy;
+      uint32_t part = 0;
+      if (valid && real) {
+        uint32_t w[UH][ND];
+        uint32_t s0;
+        load_window<UW, UH>(w, s0, ref, ox + cx, oy + cy, sub);
+        part = unit_part<UW, UH>(w, s0, kk, sk2, kbuf, sad_metric, sub);
+      }
+      const uint32_t d = group_sum(part, L);
+      const uint32_t cost = valid ? d + mv_cost(ml, mv_bits(cx, cy, 2, j.mvp_x, j.mvp_y)) : 0xFFFFFFFFu;
+      uint64_t key = ((uint64_t)cost << 32) | (uint32_t)i;
+      for (int off = L; off < 64; off <<= 1) {
+        const uint64_t o = (uint64_t)__shfl_xor((unsigned long long)key, off, 64);
+        key = o < key ? o : key;
+      }
+      best = key < best ? key : best;
+    }
+    if (npts > 0 && (uint32_t)(best >> 32) < s.best_sad) {
+      const int bi = (int)(uint32_t)best, iy = bi / nx;
+      s.best_sad = (uint32_t)(best >> 32);
+      s.bx = s.RR.l + 5 * (bi - iy * nx);
+      s.by = s.RR.t + 5 * iy;
+      s.bround = 0;
+      s.pnr = 0;
+    }
+  } else if (j.flags & FME_JOB_BIPRED) {
     s.phase = P_FULL;
     s.rx = j.lt_x; s.ry = j.lt_y;
-    s.sx = s.sy = 0; s.px = s.py = 0; s.has_pred = false;
   } else {
     int mx = j.mvp_x, my = j.mvp_y;
     clip_qpel(mx, my, ref.width, ref.height, e.cu_x, e.cu_y);
@@ -371,7 +486,6 @@ __device__ __forceinline__ void tz_unit(const TzArgs& ta, int cls_off, int cls_c
     s.px = round4(qx);
     s.py = round4(qy);
     s.phase = P_START;
-    s.rx = s.ry = 0;
   }
 
   // Up to B candidates per step: consecutive points of one list (a diamond, the two-point pair,
@@ -385,7 +499,6 @@ __device__ __forceinline__ void tz_unit(const TzArgs& ta, int cls_off, int cls_c
 #else
   constexpr int B = 1;
 #endif
-  constexpr int ND = UW / 4 + 1;
   for (int step = 0; step < (1 << 16); step++) {   // bound: a search tests < 2,000 points
     int cx[B], cy[B], cp[B], cd[B];
     int nc = 0;
@@ -395,7 +508,7 @@ __device__ __forceinline__ void tz_unit(const TzArgs& ta, int cls_off, int cls_c
       cx[b] = cy[b] = cp[b] = cd[b] = 0;
       if (more) {
         bool m = false;
-        if (next_candidate(s, ref.width, ref.height, e.cu_x, e.cu_y, cx[b], cy[b], cp[b], cd[b], m)) {
+        if (next_candidate(s, ref.width, ref.height, e.cu_x, e.cu_y, cx[b], cy[b], cp[b], cd[b], m, defer)) {
           nc = b + 1;
           more = m;
         } else {
@@ -411,66 +524,13 @@ __device__ __forceinline__ void tz_unit(const TzArgs& ta, int cls_off, int cls_c
 #pragma unroll
     for (int b = 0; b < B; b++) {
       s0[b] = 0;
-      if (b < nc && real) {
-        const int bx = ox + cx[b], by = oy + cy[b];
-        const int xa = bx & ~3;
-        s0[b] = (uint32_t)(bx - xa);
-        const bool inside = xa >= 0 && xa + 4 * ND <= ref.width;
-#pragma unroll
-        for (int r = 0; r < UH; r++) {
-          if (sub && (r & 1)) continue;   // FEN: even rows of the PU (UH is even)
-          const uint8_t* row = ref.luma + (size_t)clamp_i(by + r, 0, ref.height - 1) * ref.stride;
-          if (inside) {
-#pragma unroll
-            for (int q = 0; q < ND; q++) w[b][r][q] = gld32(row + xa + 4 * q);
-          } else {
-#pragma unroll
-            for (int q = 0; q < ND; q++) {
-              uint32_t v = 0;
-#pragma unroll
-              for (int k = 0; k < 4; k++) v |= gld8(row + clamp_i(xa + 4 * q + k, 0, ref.width - 1)) << (8 * k);
-              w[b][r][q] = v;
-            }
-          }
-        }
-      }
+      if (b < nc && real) load_window<UW, UH>(w[b], s0[b], ref, ox + cx[b], oy + cy[b], sub);
     }
     // ---- distortions, then xTZSearchHelp's updates in order --------------------------------------
 #pragma unroll
     for (int b = 0; b < B; b++) {
       if (b >= nc) break;
-      uint32_t part = 0;
-      if (real) {
-        int sop = 0, spp = 0;
-        uint32_t acc = 0;
-#pragma unroll
-        for (int r = 0; r < UH; r++) {
-          if (sub && (r & 1)) continue;
-#pragma unroll
-          for (int c = 0; c < UW / 4; c++) {
-            const uint32_t pv = __builtin_amdgcn_alignbyte(w[b][r][c + 1], w[b][r][c], s0[b]);   // reference bytes
-            if (!kbuf) {
-              if (sad_metric) {
-                acc = __builtin_amdgcn_sad_u8(pv, kk[r][c], acc);
-              } else {
-                const uint32_t ps = pv ^ 0x80808080u;
-                sop = dot4(kk[r][c] ^ 0x80808080u, ps, sop);
-                spp = dot4(ps, ps, spp);
-              }
-            } else {
-              const uint32_t d0 = pk_sub(kk[r][2 * c], lo_pair(pv));
-              const uint32_t d1 = pk_sub(kk[r][2 * c + 1], hi_pair(pv));
-              if (sad_metric) {
-                acc = udot2(pk_abs(d0), 0x00010001u, udot2(pk_abs(d1), 0x00010001u, acc));
-              } else {
-                acc = (uint32_t)dot2(d1, d1, dot2(d0, d0, (int)acc));
-              }
-            }
-          }
-        }
-        part = (!kbuf && !sad_metric) ? (uint32_t)(sk2 - 2 * sop + spp) : acc;
-        if (sub) part <<= 1;
-      }
+      const uint32_t part = real ? unit_part<UW, UH>(w[b], s0[b], kk, sk2, kbuf, sad_metric, sub) : 0u;
       uint32_t d = group_sum(part, L);
       if (d < s.best_sad) {
         d += mv_cost(ml, mv_bits(cx[b], cy[b], 2, j.mvp_x, j.mvp_y));
@@ -485,7 +545,16 @@ __device__ __forceinline__ void tz_unit(const TzArgs& ta, int cls_off, int cls_c
       }
     }
   }
-  if (active && u == 0) {
+  if (active && u == 0 && (!RASTER || ((int)threadIdx.x & 63) == 0)) {
+    if (!RASTER && s.phase == P_DEFER) {
+      uint32_t* rec = ta.rst + (size_t)jid * kTzRec;
+      rec[0] = s.best_sad;
+      rec[1] = (uint32_t)s.bx; rec[2] = (uint32_t)s.by; rec[3] = (uint32_t)s.pnr;
+      rec[4] = (uint32_t)s.RR.l; rec[5] = (uint32_t)s.RR.r; rec[6] = (uint32_t)s.RR.t; rec[7] = (uint32_t)s.RR.b;
+      const int slot = atomicAdd(ta.rqn + KID, 1);
+      ta.rq[(size_t)KID * ta.a.n + slot] = jid;
+      return;
+    }
     fme_job* out = ta.jobs_out + jid;
     out->mv_x = (int16_t)s.bx;
     out->mv_y = (int16_t)s.by;
@@ -498,10 +567,21 @@ __device__ __forceinline__ int xcd_block(int r, int n) {
   return k * (n >> 3) + min(k, n & 7) + (r >> 3);
 }
 
-template <int UW, int UH>
 #ifndef FME_TZ_WAVES
 #define FME_TZ_WAVES 3   // occupancy target: 3 waves/SIMD (<= 168 VGPRs) measured best (1: 23.5, 4: 26.3 ms)
 #endif
+__constant__ int kTzW[kNumClasses] = {4, 8, 8, 4, 16, 8, 16, 12, 16, 16, 8, 32, 16, 32, 24, 32, 32, 16, 64, 32, 64, 48, 64, 64};
+__constant__ int kTzH[kNumClasses] = {8, 4, 8, 16, 4, 16, 8, 16, 12, 16, 32, 8, 32, 16, 32, 24, 32, 64, 16, 64, 32, 64, 48, 64};
+
+__device__ __forceinline__ int tz_group_lanes(int PW, int PH, int UW, int UH) {
+  const int LR = (PW / UW) * (PH / UH);
+  int L = 1;
+  while (L < LR) L <<= 1;
+  return L;
+}
+
+// pass 1: the class's PUs in groups of L lanes, blocks dealt to the XCDs in contiguous ranges
+template <int UW, int UH>
 __global__ __launch_bounds__(kTzNT) __attribute__((amdgpu_waves_per_eu(FME_TZ_WAVES)))
 void k_tz(TzArgs ta, Schedule sc, int kid) {
   const int b = blockIdx.x;
@@ -509,9 +589,26 @@ void k_tz(TzArgs ta, Schedule sc, int kid) {
   while (c < kNumClasses - 1 && b >= sc.prefix[kid][c + 1]) c++;
   const int nblk = sc.prefix[kid][c + 1] - sc.prefix[kid][c];
   const int blk = xcd_block(b - sc.prefix[kid][c], nblk);
-  const int W[kNumClasses] = {4, 8, 8, 4, 16, 8, 16, 12, 16, 16, 8, 32, 16, 32, 24, 32, 32, 16, 64, 32, 64, 48, 64, 64};
-  const int H[kNumClasses] = {8, 4, 8, 16, 4, 16, 8, 16, 12, 16, 32, 8, 32, 16, 32, 24, 32, 64, 16, 64, 32, 64, 48, 64};
-  tz_unit<UW, UH>(ta, sc.class_off[c], sc.class_cnt[c], blk, W[c], H[c]);
+  const int PW = kTzW[c], PH = kTzH[c];
+  const int L = tz_group_lanes(PW, PH, UW, UH);
+  const int gl = blk * kTzNT + (int)threadIdx.x;
+  const int p = gl / L;
+  tz_unit<UW, UH, false>(ta, sc.class_off[c], sc.class_cnt[c], p, gl - p * L, L, PW, PH, 0);
+}
+
+// pass 2: one queued PU (job index) per wave
+#ifndef FME_TZR_WAVES
+#define FME_TZR_WAVES FME_TZ_WAVES
+#endif
+template <int UW, int UH>
+__global__ __launch_bounds__(kTzNT) __attribute__((amdgpu_waves_per_eu(FME_TZR_WAVES)))
+void k_tz_raster(TzArgs ta, Schedule sc, int kid, int nq) {
+  const int wv = (int)(blockIdx.x * (kTzNT / 64) + (threadIdx.x >> 6));
+  if (wv >= nq) return;
+  const int jid = ta.rq[(size_t)kid * ta.a.n + wv];
+  const int PW = ta.a.jobs[jid].w, PH = ta.a.jobs[jid].h;   // validated by k_classify
+  const int L = tz_group_lanes(PW, PH, UW, UH);
+  tz_unit<UW, UH, true>(ta, 0, 1, 0, (int)(threadIdx.x & 63) & (L - 1), L, PW, PH, jid);
 }
 
 }  // namespace
@@ -539,6 +636,16 @@ hipError_t launch_tz(const TzArgs& ta, const Schedule& sc, int kid, hipStream_t 
   if (kid == 0) hipLaunchKernelGGL((k_tz<4, 8>), dim3(blocks), dim3(kTzNT), 0, s, ta, sc, 0);
   else if (kid == 1) hipLaunchKernelGGL((k_tz<8, 4>), dim3(blocks), dim3(kTzNT), 0, s, ta, sc, 1);
   else hipLaunchKernelGGL((k_tz<8, 8>), dim3(blocks), dim3(kTzNT), 0, s, ta, sc, 2);
+  return hipGetLastError();
+}
+
+// The raster searches pass 1 queued for kernel kid (nq of them, read back by the host).
+hipError_t launch_tz_raster(const TzArgs& ta, const Schedule& sc, int kid, int nq, hipStream_t s) {
+  if (nq <= 0) return hipSuccess;
+  const int blocks = (nq + kTzNT / 64 - 1) / (kTzNT / 64);
+  if (kid == 0) hipLaunchKernelGGL((k_tz_raster<4, 8>), dim3(blocks), dim3(kTzNT), 0, s, ta, sc, 0, nq);
+  else if (kid == 1) hipLaunchKernelGGL((k_tz_raster<8, 4>), dim3(blocks), dim3(kTzNT), 0, s, ta, sc, 1, nq);
+  else hipLaunchKernelGGL((k_tz_raster<8, 8>), dim3(blocks), dim3(kTzNT), 0, s, ta, sc, 2, nq);
   return hipGetLastError();
 }
 

@@ -60,6 +60,36 @@ TZ_EXT_DTYPE = np.dtype(
 assert TZ_EXT_DTYPE.itemsize == 12
 TZ_PRED2NX2N = 0x01
 
+# fme_pu_req (64 B) / fme_pu_res (80 B): predInterSearch's P-slice PU / reference loop (include/fme.h)
+MAX_REFS = 4
+PU_REQ_DTYPE = np.dtype(
+    [
+        ("x", "<u2"), ("y", "<u2"), ("w", "u1"), ("h", "u1"),
+        ("cu_x", "<u2"), ("cu_y", "<u2"),
+        ("part_size", "u1"), ("depth", "u1"), ("org_id", "u1"), ("num_refs", "u1"),
+        ("ref_id", "u1", (MAX_REFS,)), ("n_cand", "u1", (MAX_REFS,)),
+        ("cand", "<i2", (MAX_REFS, 2, 2)),
+        ("lambda_id", "u1"), ("search_range", "u1"), ("flags", "u1"), ("reserved", "u1"),
+        ("reserved2", "<u2", (3,)),
+    ],
+    align=False,
+)
+assert PU_REQ_DTYPE.itemsize == 64
+PU_RES_DTYPE = np.dtype(
+    [
+        ("mv_x", "<i2"), ("mv_y", "<i2"), ("mvp_x", "<i2"), ("mvp_y", "<i2"),
+        ("ref_idx", "u1"), ("mvp_idx", "u1"), ("reserved", "<u2"),
+        ("bits", "<u4"), ("cost", "<u4"),
+        ("ref_cost", "<u4", (MAX_REFS,)), ("ref_bits", "<u4", (MAX_REFS,)),
+        ("ref_mv", "<i2", (MAX_REFS, 2)), ("ref_mvp_idx", "u1", (MAX_REFS,)),
+        ("reserved2", "<u4", (2,)),
+    ],
+    align=False,
+)
+assert PU_RES_DTYPE.itemsize == 80
+PU_LOSSLESS = 0x01
+PART_2Nx2N, PART_2NxN, PART_Nx2N, PART_NxN, PART_2NxnU, PART_2NxnD, PART_nLx2N, PART_nRx2N = range(8)
+
 MC_L0 = 0x01
 MC_L1 = 0x02
 

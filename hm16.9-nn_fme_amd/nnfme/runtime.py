@@ -28,6 +28,7 @@ ABI_SYMBOLS = (
     "fme_set_picture_chroma", "fme_bind_picture_chroma_device", "fme_motion_compensate",
     "fme_motion_compensate_device", "fme_mc_invalid_count", "fme_mc_last_ms",
     "fme_integer_search", "fme_integer_search_device", "fme_integer_search_last_ms",
+    "fme_pred_inter_p", "fme_pred_inter_reset",
 )
 
 
@@ -87,6 +88,8 @@ def load_library(path=None):
         "fme_integer_search": (I, [P, P, P, P, I, P]),
         "fme_integer_search_device": (I, [P, P, P, P, I, P]),
         "fme_integer_search_last_ms": (I, [P, P]),
+        "fme_pred_inter_p": (I, [P, P, P, I, P]),
+        "fme_pred_inter_reset": (I, [P]),
     }
     for name, (res, args) in sig.items():
         f = getattr(lib, name)
@@ -174,6 +177,19 @@ class FmeContext:
         ms = C.c_float()
         _check(self.lib, self.lib.fme_integer_search_last_ms(self.h, C.byref(ms)))
         return ms.value
+
+    # -- predInterSearch P-slice PU / reference loop ------------------------
+    def pred_inter_p(self, reqs, stream=None):
+        """fme_pred_inter_p: one fme_pu_res per fme_pu_req, in request order."""
+        from .abi import PU_REQ_DTYPE, PU_RES_DTYPE
+        reqs = np.ascontiguousarray(reqs, dtype=PU_REQ_DTYPE)
+        res = np.zeros(len(reqs), dtype=PU_RES_DTYPE)
+        if len(reqs):
+            _check(self.lib, self.lib.fme_pred_inter_p(self.h, _ptr(reqs), _ptr(res), len(reqs), stream))
+        return res
+
+    def pred_inter_reset(self):
+        _check(self.lib, self.lib.fme_pred_inter_reset(self.h))
 
     # -- motion compensation ----------------------------------------------------------------
     def motion_compensate(self, mc_jobs, y, cb, cr, stream=None):

@@ -395,3 +395,111 @@ def make_tz_jobs(rng, width, height, calls_per_ctu, org_id, ref_ids, lambda_ids,
     ext["pred2n_x"] = np.where(p2, np.rint(vx.reshape(-1)[ctu] * dist).astype(np.int64) + rng.integers(-6, 7, n), 0)
     ext["pred2n_y"] = np.where(p2, np.rint(vy.reshape(-1)[ctu] * dist).astype(np.int64) + rng.integers(-6, 7, n), 0)
     return jobs, ext
+
+
+# ---- predInterSearch producer inputs -----------------------------------------
+def _cu_partitions(x0, y0, s):
+    """(part_size, [(x, y, w, h) per PU]) of one CU in TEncCu::xCompressCU's order (TEncCu.cpp:
+    2Nx2N, 2NxN, Nx2N, then the AMP shapes for CUs above 8x8)."""
+    from .abi import PART_2Nx2N, PART_2NxN, PART_2NxnD, PART_2NxnU, PART_Nx2N, PART_nLx2N, PART_nRx2N
+    h, q = s // 2, s // 4
+    parts = [(PART_2Nx2N, [(x0, y0, s, s)]),
+             (PART_2NxN, [(x0, y0, s, h), (x0, y0 + h, s, h)]),
+             (PART_Nx2N, [(x0, y0, h, s), (x0 + h, y0, h, s)])]
+    if s > 8:
+        parts += [(PART_2NxnU, [(x0, y0, s, q), (x0, y0 + q, s, s - q)]),
+                  (PART_2NxnD, [(x0, y0, s, s - q), (x0, y0 + s - q, s, q)]),
+                  (PART_nLx2N, [(x0, y0, q, s), (x0 + q, y0, s - q, s)]),
+                  (PART_nRx2N, [(x0, y0, s - q, s), (x0 + s - q, y0, q, s)])]
+    return parts
+
+
+def make_pu_requests(rng, width, height, org_id, ref_ids, lambda_id, max_depth=3, amp=12.0, cand_noise=24,
+                     one_cand_frac=0.1, lossless_frac=0.0, search_range=SEARCH_RANGE):
+    """fme_pu_req stream of a P frame in encoder call order: CTUs in raster order, each CU quadtree
+    depth-first (64 -> 8), per CU every partition's PUs (PU0 then PU1).  AMVP candidates per
+    reference index k lie near a smooth motion field scaled by the POC distance k + 1 (the second
+    one sometimes equal to the first or zero, as fillMvpCand pads); one_cand_frac of the lists
+    hold a single candidate."""
+    from .abi import MAX_REFS, PU_LOSSLESS, PU_REQ_DTYPE
+    ctus_x, ctus_y = (width + MAX_CU - 1) // MAX_CU, (height + MAX_CU - 1) // MAX_CU
+    vx, vy = motion_field(rng, ctus_x, ctus_y, amp)
+    rows = []
+
+    def cu(x0, y0, s, d, ctu):
+        if x0 >= width or y0 >= height:
+            return
+        if x0 + s > width or y0 + s > height:   # boundary CUs are split
+            if s > 8:
+                for cy in (y0, y0 + s // 2):
+                    for cx in (x0, x0 + s // 2):
+                        cu(cx, cy, s // 2, d + 1, ctu)
+            return
+        for ps, pus in _cu_partitions(x0, y0, s):
+            for (x, y, w, h) in pus:
+                rows.append((x, y, w, h, x0, y0, ps, d, ctu))
+        if d < max_depth and s > 8:
+            for cy in (y0, y0 + s // 2):
+                for cx in (x0, x0 + s // 2):
+                    cu(cx, cy, s // 2, d + 1, ctu)
+
+    for t in range(ctus_x * ctus_y):
+        cu((t % ctus_x) * MAX_CU, (t // ctus_x) * MAX_CU, MAX_CU, 0, t)
+    a = np.array(rows, dtype=np.int64).reshape(-1, 9)
+    n = len(a)
+    nref = len(ref_ids)
+    reqs = np.zeros(n, dtype=PU_REQ_DTYPE)
+    reqs["x"], reqs["y"], reqs["w"], reqs["h"] = a[:, 0], a[:, 1], a[:, 2], a[:, 3]
+    reqs["cu_x"], reqs["cu_y"], reqs["part_size"], reqs["depth"] = a[:, 4], a[:, 5], a[:, 6], a[:, 7]
+    reqs["org_id"] = org_id
+    reqs["num_refs"] = nref
+    reqs["ref_id"][:, :nref] = np.asarray(ref_ids)
+    reqs["lambda_id"] = lambda_id
+    reqs["search_range"] = search_range
+    reqs["flags"] = np.where(rng.random(n) < lossless_frac, PU_LOSSLESS, 0)
+    ctu = a[:, 8]
+    for k in range(nref):
+        bx = 4 * np.rint(vx.reshape(-1)[ctu] * (k + 1)).astype(np.int64)
+        by = 4 * np.rint(vy.reshape(-1)[ctu] * (k + 1)).astype(np.int64)
+        c0x = bx + rng.integers(-cand_noise, cand_noise + 1, n)
+        c0y = by + rng.integers(-cand_noise, cand_noise + 1, n)
+        kind = rng.integers(0, 4, n)   # second candidate: 0/1 near the field, 2 equal, 3 zero
+        c1x = np.where(kind < 2, bx + rng.integers(-cand_noise, cand_noise + 1, n), np.where(kind == 2, c0x, 0))
+        c1y = np.where(kind < 2, by + rng.integers(-cand_noise, cand_noise + 1, n), np.where(kind == 2, c0y, 0))
+        reqs["cand"][:, k, 0, 0], reqs["cand"][:, k, 0, 1] = c0x, c0y
+        reqs["cand"][:, k, 1, 0], reqs["cand"][:, k, 1, 1] = c1x, c1y
+        reqs["n_cand"][:, k] = np.where(rng.random(n) < one_cand_frac, 1, 2)
+    assert nref <= MAX_REFS
+    return reqs
+
+
+def pu_requests_to_jobs(reqs, width, height):
+    """The xMotionEstimation jobs of single-reference, single-candidate requests whose
+    m_integerMv2Nx2N reads see the initial (0, 0): mvp = cand[0][0], xSetSearchRange(mvp, range)
+    (TEncSearch.cpp:4602-4624), bits_in = xGetBlkBits + m_auiMVPIdxCost[0][2]."""
+    from .abi import PART_2Nx2N, PART_NxN, PU_LOSSLESS, TZ_EXT_DTYPE, TZ_PRED2NX2N
+    from .abi import JOB_LOSSLESS
+    n = len(reqs)
+    jobs = np.zeros(n, dtype=JOB_DTYPE)
+    ext = np.zeros(n, dtype=TZ_EXT_DTYPE)
+    for f in ("x", "y", "w", "h", "org_id"):
+        jobs[f] = reqs[f]
+    jobs["ref_id"] = reqs["ref_id"][:, 0]
+    mx, my = reqs["cand"][:, 0, 0, 0].astype(np.int64), reqs["cand"][:, 0, 0, 1].astype(np.int64)
+    jobs["mvp_x"], jobs["mvp_y"] = mx, my
+    rng_pel = np.where(reqs["search_range"] == 0, 64, reqs["search_range"]).astype(np.int64)
+    cux, cuy = reqs["cu_x"].astype(np.int64), reqs["cu_y"].astype(np.int64)
+    cx, cy = _clip_cu_qpel(mx, cux, width), _clip_cu_qpel(my, cuy, height)
+    jobs["lt_x"] = _div4_round(_clip_cu_qpel(cx - (rng_pel << 2), cux, width))
+    jobs["rb_x"] = _div4_round(_clip_cu_qpel(cx + (rng_pel << 2), cux, width))
+    jobs["lt_y"] = _div4_round(_clip_cu_qpel(cy - (rng_pel << 2), cuy, height))
+    jobs["rb_y"] = _div4_round(_clip_cu_qpel(cy + (rng_pel << 2), cuy, height))
+    jobs["flags"] = JOB_EMI | np.where(reqs["flags"] & PU_LOSSLESS, JOB_LOSSLESS, 0)
+    jobs["lambda_id"] = reqs["lambda_id"]
+    jobs["bits_in"] = np.where(np.isin(reqs["part_size"], (PART_2Nx2N, PART_NxN)), 1, 3) + 1
+    jobs["key_offset"] = -1
+    ext["cu_x"], ext["cu_y"] = reqs["cu_x"], reqs["cu_y"]
+    ext["search_range"] = rng_pel
+    reads = ~((reqs["part_size"] == PART_2Nx2N) & (reqs["depth"] == 0))
+    ext["flags"] = np.where(reads, TZ_PRED2NX2N, 0)
+    return jobs, ext

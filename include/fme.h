@@ -209,6 +209,73 @@ int fme_integer_search_device(fme_ctx* ctx, fme_job* d_jobs, const fme_tz_ext* d
 /* With profiling on: device milliseconds of the last integer-search launches; waits for them. */
 int fme_integer_search_last_ms(fme_ctx* ctx, float* ms);
 
+/* ---- predInterSearch's P-slice PU / reference loop --------------------- *
+ * TEncSearch::predInterSearch, uni-directional part for P slices (TEncSearch.cpp:3746-3866), as a
+ * batch producer.  Per PU request and reference index k < num_refs, in the encoder's call order:
+ *   bits_in = xGetBlkBits(part_size, P slice)[0] (4286-4333) + the reference-index bits
+ *             (3792-3800) + m_auiMVPIdxCost[mvp_idx][AMVP_MAX_NUM_CANDS] (3812, 412-425);
+ *   xEstimateMvPredAMVP (4186-4256): with two candidates, the first with the least
+ *             xGetTemplateCost (4397-4436: luma prediction at the clipMv'd candidate, SAD against
+ *             the original, cost (UInt)(SAD + bits * mlambda / 65536.0) with bits = 1);
+ *   xMotionEstimation (4439-4599): xSetSearchRange around the predictor, xTZSearch from it and
+ *             from m_integerMv2Nx2N[k] when the PU is not a depth-0 2Nx2N PU, the EMI step,
+ *             FracDIF, NN_pred, the cost tail; a 2Nx2N PU stores its integer MV (after the EMI
+ *             step) in m_integerMv2Nx2N[k] (4511-4526), state this context keeps like TEncSearch;
+ *   xCheckBestMVP (4344-4394), then the strict-minimum reference choice (3845-3853).
+ * The AMVP candidates are the caller's (TComDataCU::fillMvpCand reads CUs the encoder has already
+ * decided); merge, bi-prediction and the mode decision stay with the caller.  The NN state and
+ * m_integerMv2Nx2N follow request order exactly; internally requests are grouped into dependency
+ * levels so that each GPU batch holds every request whose inputs are known.                       */
+#define FME_MAX_REFS     4
+#define FME_PU_LOSSLESS  0x01u   /* CU transquant bypass                                          */
+/* HM PartSize (TypeDef.h) */
+#define FME_PART_2Nx2N 0
+#define FME_PART_2NxN  1
+#define FME_PART_Nx2N  2
+#define FME_PART_NxN   3
+#define FME_PART_2NxnU 4
+#define FME_PART_2NxnD 5
+#define FME_PART_nLx2N 6
+#define FME_PART_nRx2N 7
+
+typedef struct fme_pu_req {
+  uint16_t x, y;              /* PU luma rectangle (getPartIndexAndSize)                        */
+  uint8_t  w, h;
+  uint16_t cu_x, cu_y;        /* luma origin of the CU (clipMv)                                 */
+  uint8_t  part_size;         /* FME_PART_*                                                     */
+  uint8_t  depth;             /* CU depth (0: CTU-sized CU)                                     */
+  uint8_t  org_id;            /* original picture slot                                          */
+  uint8_t  num_refs;          /* getNumRefIdx(REF_PIC_LIST_0), 1..FME_MAX_REFS                 */
+  uint8_t  ref_id[FME_MAX_REFS];    /* picture slot of reference index k                       */
+  uint8_t  n_cand[FME_MAX_REFS];    /* AMVPInfo::iN of reference index k (1 or 2)              */
+  int16_t  cand[FME_MAX_REFS][2][2];/* AMVPInfo::m_acMvCand, quarter-pel (hor, ver)            */
+  uint8_t  lambda_id;         /* motion-lambda slot                                             */
+  uint8_t  search_range;      /* m_aaiAdaptSR = cfg SearchRange (0 -> 64)                       */
+  uint8_t  flags;             /* FME_PU_*                                                       */
+  uint8_t  reserved;
+  uint16_t reserved2[3];
+} fme_pu_req;   /* 64 bytes */
+
+typedef struct fme_pu_res {
+  int16_t  mv_x, mv_y;        /* cMv[0]: MV of the chosen reference, quarter-pel                */
+  int16_t  mvp_x, mvp_y;      /* its predictor after xCheckBestMVP                              */
+  uint8_t  ref_idx;           /* iRefIdx[0]                                                     */
+  uint8_t  mvp_idx;           /* aaiMvpIdx[0][ref_idx]                                          */
+  uint16_t reserved;
+  uint32_t bits, cost;        /* uiBits[0], uiCost[0]                                           */
+  uint32_t ref_cost[FME_MAX_REFS];  /* uiCostTempL0 per reference index (after xCheckBestMVP)  */
+  uint32_t ref_bits[FME_MAX_REFS];  /* uiBitsTempL0                                            */
+  int16_t  ref_mv[FME_MAX_REFS][2]; /* cMvTemp[0][k], quarter-pel                              */
+  uint8_t  ref_mvp_idx[FME_MAX_REFS];
+  uint32_t reserved2[2];
+} fme_pu_res;   /* 80 bytes */
+
+/* Host arrays, synchronous on `stream`.  A batch with an invalid request is rejected before any
+ * work runs. */
+int fme_pred_inter_p(fme_ctx* ctx, const fme_pu_req* reqs, fme_pu_res* res, int n, void* stream);
+/* Forget m_integerMv2Nx2N (TEncSearch construction: every entry (0, 0)). */
+int fme_pred_inter_reset(fme_ctx* ctx);
+
 /* ---- single-PU entry points with the TEncSearch argument lists ---------------------------- *
  * xPatternSearchFracDIF(bIsLosslessCoded, pcPatternKey, piRefY, iRefStride, pcMvInt,
  *                       rcMvHalf, rcMvQter, ruiCost) with the HM objects flattened:

@@ -884,3 +884,163 @@ int orc_integer_search(orc_ctx* ctx, fme_job* jobs, const fme_tz_ext* ext, uint3
   free(cur);
   return FME_OK;
 }
+
+/* =====================================================================================
+ * predInterSearch's P-slice PU / reference loop, sequential.
+ * ===================================================================================== */
+
+/* xGetMvpIdxBits (TEncSearch.cpp:4258-4284) = m_auiMVPIdxCost[idx][num] (412-425). */
+static uint32_t pi_mvp_idx_bits(int idx, int num) {
+  if (num == 1) return 0;
+  uint32_t len = 1;
+  if (idx == 0) return len;
+  len += (uint32_t)(idx - 1);
+  if (num - 1 > idx) len++;
+  return len;
+}
+
+/* xGetBlkBits (TEncSearch.cpp:4286-4333) for a P slice: uiBlkBit[0]. */
+static uint32_t pi_blk_bits(int part_size) {
+  if (part_size == FME_PART_2Nx2N || part_size == FME_PART_NxN) return 1;
+  return 3;   /* 2NxN, 2NxnU, 2NxnD, Nx2N, nLx2N, nRx2N */
+}
+
+/* xGetTemplateCost (TEncSearch.cpp:4397-4436): clipMv, xPredInterBlk(COMPONENT_Y, bi = false),
+ * getDistPart(DF_SAD) (plain SAD, TComRdCost.cpp:187-197, 327-349), calcRdCost(bits, SAD, DF_SAD)
+ * (TComRdCost.cpp:57-102, COST_STANDARD_LOSSY: SAD + bits * lambdaMotionSAD / 65536). */
+static uint32_t pi_template_cost(const orc_ctx* ctx, const fme_pu_req* q, int k, int m, int16_t* pred) {
+  const orc_picture* ref = &ctx->pics[q->ref_id[k]];
+  const orc_picture* org = &ctx->pics[q->org_id];
+  int mx = q->cand[k][m][0], my = q->cand[k][m][1];
+  mc_clip_mv(&mx, &my, ref->width, ref->height, q->cu_x, q->cu_y);
+  mc_pred_blk(ref->luma, ref->stride, ref->width, ref->height, 0, q->x, q->y, q->w, q->h, mx, my, 0, pred, q->w);
+  uint32_t sad = 0;
+  for (int y = 0; y < q->h; y++)
+    for (int x = 0; x < q->w; x++) {
+      const int d = pred[y * q->w + x] - org->luma[(size_t)(q->y + y) * org->stride + q->x + x];
+      sad += (uint32_t)(d < 0 ? -d : d);
+    }
+  const double ml = ctx->mlambda[q->lambda_id];
+  return (uint32_t)((double)sad + ((double)pi_mvp_idx_bits(m, 2) * ml) / 65536.0);
+}
+
+void orc_pred_inter_reset(orc_ctx* ctx) { memset(ctx->int_mv_2n, 0, sizeof(ctx->int_mv_2n)); }
+
+int orc_pred_inter_p(orc_ctx* ctx, const fme_pu_req* reqs, fme_pu_res* res, int n) {
+  int16_t* pred = (int16_t*)malloc(sizeof(int16_t) * 64 * 64);
+  for (int i = 0; i < n; i++) {
+    const fme_pu_req* q = &reqs[i];
+    fme_pu_res* o = &res[i];
+    memset(o, 0, sizeof(*o));
+    if (q->num_refs < 1 || q->num_refs > FME_MAX_REFS || q->org_id >= FME_MAX_PICTURES ||
+        !ctx->pics[q->org_id].luma || q->lambda_id >= FME_MAX_LAMBDAS) {
+      free(pred);
+      return FME_E_INVALID;
+    }
+    const orc_picture* org = &ctx->pics[q->org_id];
+    const double ml = ctx->mlambda[q->lambda_id];
+    const int range = q->search_range ? q->search_range : 64;
+    uint32_t best_cost = 0xFFFFFFFFu;   /* uiCost[0] = max */
+    for (int k = 0; k < q->num_refs; k++) {
+      if (q->ref_id[k] >= FME_MAX_PICTURES || !ctx->pics[q->ref_id[k]].luma || q->n_cand[k] < 1 || q->n_cand[k] > 2) {
+        free(pred);
+        return FME_E_INVALID;
+      }
+      /* uiBitsTemp = uiMbBits[0] + reference-index bits (3792-3800) */
+      uint32_t bits = pi_blk_bits(q->part_size);
+      if (q->num_refs > 1) {
+        bits += (uint32_t)k + 1;
+        if (k == q->num_refs - 1) bits--;
+      }
+      /* xEstimateMvPredAMVP (4186-4256) */
+      int idx = 0;
+      if (q->n_cand[k] > 1) {
+        uint32_t best = 0xFFFFFFFFu;
+        for (int m = 0; m < q->n_cand[k]; m++) {
+          const uint32_t c = pi_template_cost(ctx, q, k, m, pred);
+          if (best > c) {
+            best = c;
+            idx = m;
+          }
+        }
+      }
+      bits += pi_mvp_idx_bits(idx, 2);   /* m_auiMVPIdxCost[idx][AMVP_MAX_NUM_CANDS] (3812) */
+      /* xMotionEstimation (4439-4599): xSetSearchRange, xTZSearch (+ EMI), FracDIF, NN, tail */
+      fme_job j;
+      memset(&j, 0, sizeof(j));
+      j.x = q->x; j.y = q->y; j.w = q->w; j.h = q->h;
+      j.org_id = q->org_id; j.ref_id = q->ref_id[k];
+      j.mvp_x = q->cand[k][idx][0]; j.mvp_y = q->cand[k][idx][1];
+      int cx = j.mvp_x, cy = j.mvp_y;
+      tz_clip(&cx, &cy, org->width, org->height, q->cu_x, q->cu_y);
+      int lx = cx - (range << 2), ly = cy - (range << 2), rx = cx + (range << 2), ry = cy + (range << 2);
+      tz_clip(&lx, &ly, org->width, org->height, q->cu_x, q->cu_y);
+      tz_clip(&rx, &ry, org->width, org->height, q->cu_x, q->cu_y);
+      j.lt_x = (int16_t)mv_round4(lx); j.lt_y = (int16_t)mv_round4(ly);
+      j.rb_x = (int16_t)mv_round4(rx); j.rb_y = (int16_t)mv_round4(ry);
+      j.flags = (uint8_t)(FME_JOB_EMI | ((q->flags & FME_PU_LOSSLESS) ? FME_JOB_LOSSLESS : 0u));
+      j.lambda_id = q->lambda_id;
+      j.bits_in = (uint16_t)bits;
+      j.key_offset = -1;
+      fme_tz_ext e;
+      memset(&e, 0, sizeof(e));
+      e.cu_x = q->cu_x; e.cu_y = q->cu_y;
+      e.search_range = (uint8_t)range;
+      if (!(q->part_size == FME_PART_2Nx2N && q->depth == 0)) {   /* pIntegerMv2Nx2NPred (4511-4515) */
+        e.flags = FME_TZ_PRED2NX2N;
+        e.pred2n_x = ctx->int_mv_2n[k][0];
+        e.pred2n_y = ctx->int_mv_2n[k][1];
+      }
+      fme_result r;
+      int rc = orc_integer_search(ctx, &j, &e, NULL, 1);
+      if (!rc) rc = orc_refine(ctx, &j, &r, 1);
+      if (rc) {
+        free(pred);
+        return rc;
+      }
+      if (q->part_size == FME_PART_2Nx2N) {   /* m_integerMv2Nx2N = rcMv after the TZ search (4523-4526) */
+        ctx->int_mv_2n[k][0] = r.mv_int_x;
+        ctx->int_mv_2n[k][1] = r.mv_int_y;
+      }
+      /* xCheckBestMVP (4344-4394), cost scale 0 */
+      uint32_t rbits = r.bits, rcost = r.cost;
+      if (q->n_cand[k] >= 2) {
+        const int org_bits = (int)(mv_bits(r.mv_x, r.mv_y, 0, q->cand[k][idx][0], q->cand[k][idx][1]) +
+                                   pi_mvp_idx_bits(idx, 2));
+        int best_bits = org_bits, best_idx = idx;
+        for (int m = 0; m < q->n_cand[k]; m++) {
+          if (m == idx) continue;
+          const int b = (int)(mv_bits(r.mv_x, r.mv_y, 0, q->cand[k][m][0], q->cand[k][m][1]) + pi_mvp_idx_bits(m, 2));
+          if (b < best_bits) {
+            best_bits = b;
+            best_idx = m;
+          }
+        }
+        if (best_idx != idx) {
+          idx = best_idx;
+          const uint32_t org_total = rbits;
+          rbits = org_total - (uint32_t)org_bits + (uint32_t)best_bits;
+          rcost = (rcost - orc_cost(ml, org_total)) + orc_cost(ml, rbits);
+        }
+      }
+      o->ref_cost[k] = rcost;
+      o->ref_bits[k] = rbits;
+      o->ref_mv[k][0] = r.mv_x;
+      o->ref_mv[k][1] = r.mv_y;
+      o->ref_mvp_idx[k] = (uint8_t)idx;
+      if (rcost < best_cost) {   /* 3845-3853 */
+        best_cost = rcost;
+        o->cost = rcost;
+        o->bits = rbits;
+        o->mv_x = r.mv_x;
+        o->mv_y = r.mv_y;
+        o->ref_idx = (uint8_t)k;
+        o->mvp_idx = (uint8_t)idx;
+        o->mvp_x = q->cand[k][idx][0];
+        o->mvp_y = q->cand[k][idx][1];
+      }
+    }
+  }
+  free(pred);
+  return FME_OK;
+}

@@ -48,6 +48,7 @@ typedef struct orc_ctx {
   float nn[FME_NN_PARAMS];
   int nn_loaded;
   orc_nn_state nn_state;
+  int16_t int_mv_2n[FME_MAX_REFS][2];   /* m_integerMv2Nx2N[REF_PIC_LIST_0] (TEncSearch.h:118) */
 } orc_ctx;
 
 /* primitives (exported for unit tests) */
@@ -112,6 +113,13 @@ typedef struct orc_yuv {
  * pics[ref_id] are the reference pictures.  Returns 0, or -1-i for an invalid job i. */
 int orc_mc(const orc_yuv* pics, const fme_mc_job* jobs, int n, uint8_t* y, int y_stride,
            uint8_t* cb, uint8_t* cr, int c_stride, int width, int height);
+
+/* ---- predInterSearch's P-slice PU / reference loop: each request in
+ * order, each reference index in order, exactly as TEncSearch.cpp:3746-3866 runs them (AMVP
+ * template choice, xMotionEstimation = orc_integer_search + orc_refine on one job, xCheckBestMVP,
+ * the reference choice, m_integerMv2Nx2N).  Returns 0 or a negative FME_E_* code. */
+int orc_pred_inter_p(orc_ctx* ctx, const fme_pu_req* reqs, fme_pu_res* res, int n);
+void orc_pred_inter_reset(orc_ctx* ctx);
 
 /* helpers for bindings */
 size_t orc_ctx_size(void);

@@ -64,6 +64,9 @@ class Oracle:
         lib.orc_refine.argtypes = [_P, _P, _P, C.c_int]
         lib.orc_integer_search.restype = C.c_int
         lib.orc_integer_search.argtypes = [_P, _P, _P, _P, C.c_int]
+        lib.orc_pred_inter_p.restype = C.c_int
+        lib.orc_pred_inter_p.argtypes = [_P, _P, _P, C.c_int]
+        lib.orc_pred_inter_reset.argtypes = [_P]
         lib.orc_mc.restype = C.c_int
         lib.orc_mc.argtypes = [_P, _P, C.c_int, _P, C.c_int, _P, _P, C.c_int, C.c_int, C.c_int]
         self._buf = C.create_string_buffer(lib.orc_ctx_size())
@@ -126,6 +129,19 @@ class Oracle:
         if rc != 0:
             raise RuntimeError(f"orc_integer_search failed: {rc}")
         return jobs, sad
+
+    def pred_inter_p(self, reqs):
+        """orc_pred_inter_p: predInterSearch's P-slice PU / reference loop, one fme_pu_res per request."""
+        from nnfme.abi import PU_REQ_DTYPE, PU_RES_DTYPE
+        reqs = np.ascontiguousarray(reqs, dtype=PU_REQ_DTYPE)
+        res = np.zeros(len(reqs), dtype=PU_RES_DTYPE)
+        rc = self.lib.orc_pred_inter_p(self.ctx, _ptr(reqs), _ptr(res), len(reqs))
+        if rc != 0:
+            raise RuntimeError(f"orc_pred_inter_p failed: {rc}")
+        return res
+
+    def pred_inter_reset(self):
+        self.lib.orc_pred_inter_reset(self.ctx)
 
     def mc(self, pics, mc_jobs, y, cb, cr):
         """orc_mc: pics = {id: (Y, Cb, Cr)} reference pictures; predicts into y/cb/cr in place."""
