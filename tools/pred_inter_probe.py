@@ -2,7 +2,7 @@
 """predInterSearch producer (fme_pred_inter_p) on one 1080p P frame of CTU-quadtree requests
 (64 -> 8 CUs, AMP, 4 references, NN on): wall time per frame and requests / jobs per second.
 
-usage: python tools/pred_inter_probe.py [max_depth]"""
+usage: python tools/pred_inter_probe.py [max_depth] [height]"""
 import os
 import sys
 import time
@@ -16,8 +16,8 @@ sys.path[:0] = [os.path.join(ROOT, "hm16.9-nn_fme_amd"), os.path.join(ROOT, "ora
 def main():
     from nnfme import synth
     from nnfme.runtime import FmeContext
-    W, H = 1920, 1080
     depth = int(sys.argv[1]) if len(sys.argv) > 1 else 3
+    W, H = 1920, int(sys.argv[2]) if len(sys.argv) > 2 else 1080
     rng = np.random.default_rng(2)
     pics = {i: synth.synth_luma(W, H, t) for i, t in zip(range(5), (7, 6, 5, 4, 0))}
     reqs = synth.make_pu_requests(rng, W, H, org_id=4, ref_ids=[0, 1, 2, 3], lambda_id=0, max_depth=depth)
@@ -35,7 +35,7 @@ def main():
         ts.append(time.perf_counter() - t0)
     t = float(np.median(ts))
     nj = int(reqs["num_refs"].astype(np.int64).sum())
-    print(f"pred_inter_p 1080p depth {depth}: {len(reqs)} PU requests ({nj} xMotionEstimation jobs) in {t * 1e3:.1f} ms "
+    print(f"pred_inter_p {W}x{H} depth {depth}: {len(reqs)} PU requests ({nj} xMotionEstimation jobs) in {t * 1e3:.1f} ms "
           f"-> {len(reqs) / t / 1e6:.2f} M requests/s, {nj / t / 1e6:.2f} M jobs/s; ref_idx histogram "
           f"{np.bincount(res['ref_idx'], minlength=4).tolist()}", flush=True)
     # CPU: the oracle's sequential restatement on a bounded sample (first CTU rows)
