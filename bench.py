@@ -282,6 +282,58 @@ def tz_leg(dev, stream, reps, cpu_seconds):
     return out
 
 
+def pred_inter_leg(dev, reps, cpu_seconds):
+    """predInterSearch's P-slice PU / reference loop over one 1080p P frame:
+    every PU of a full 64 -> 8 CU quadtree with AMP in xCompressCU order, 4 references, the AMVP
+    candidate lists of nnfme.synth.make_pu_requests, NN on (fme_pred_inter_p, host request arrays).
+    Wall time per frame; the oracle's sequential loop (orc_pred_inter_p) on one host core over a
+    bounded prefix of the same stream is the CPU baseline."""
+    from nnfme import weights
+    from nnfme.runtime import FmeContext
+    rng = np.random.default_rng(2)
+    pics = {i: synth.synth_luma(W, H, t) for i, t in zip(range(5), (7, 6, 5, 4, 0))}
+    reqs = synth.make_pu_requests(rng, W, H, org_id=4, ref_ids=[0, 1, 2, 3], lambda_id=0, max_depth=3)
+    nj = int(reqs["num_refs"].astype(np.int64).sum())
+    out = {"workload": f"{W}x{H} P frame QP{QP}: {len(reqs)} PU requests = {nj} xMotionEstimation jobs (full 64->8 "
+                       f"quadtree with AMP, 4 refs, AMVP template choice, xCheckBestMVP, reference choice, NN on)"}
+    if cpu_seconds > 0:
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        from oracle import Oracle
+        orc = Oracle(nn_mode=1, qp=QP, fast_inter_mode=1)
+        orc.load_nn(weights.load_weights(QP))
+        for k, v in pics.items():
+            orc.set_picture(k, v)
+        for lid, lam in enumerate(synth.LDP_LAMBDA[QP]):
+            orc.set_lambda(lid, lam)
+        done, t0 = 0, time.perf_counter()
+        while time.perf_counter() - t0 < cpu_seconds and done < len(reqs):
+            orc.pred_inter_p(reqs[done:done + 1000])
+            done += min(1000, len(reqs) - done)
+        rate = done / (time.perf_counter() - t0)
+        out["cpu_baseline"] = {"value": rate, "unit": "PU requests/s", "cores": 1, "kind": "port",
+                               "sample": f"first {done} requests of the frame, sequential (oracle/fme_oracle.c)"}
+    ctx = FmeContext(device=dev.index, nn_mode=1, qp=QP, fast_inter_mode=1, max_jobs=nj)
+    for k, v in pics.items():
+        ctx.set_picture(k, v)
+    for lid, lam in enumerate(synth.LDP_LAMBDA[QP]):
+        ctx.set_lambda(lid, lam)
+    ctx.pred_inter_p(reqs)
+    ts = []
+    for _ in range(reps):
+        ctx.pred_inter_reset()
+        t0 = time.perf_counter()
+        ctx.pred_inter_p(reqs)
+        ts.append(time.perf_counter() - t0)
+    t = float(np.median(ts))
+    out.update({"ms_per_frame": t * 1e3, "requests_per_s": len(reqs) / t, "jobs_per_s": nj / t,
+                "note": "bounded by the reference's m_integerMv2Nx2N chain: the bottom CTU row (56 rows) has no "
+                        "depth-0 CU, so its 30 CTUs form one sequential chain of 2Nx2N searches (DESIGN.md section 4)"})
+    if "cpu_baseline" in out:
+        out["speedup_vs_cpu_1core"] = out["requests_per_s"] / out["cpu_baseline"]["value"]
+    ctx.close()
+    return out
+
+
 def read_pmc_traffic():
     """HBM bytes per search launch from the committed rocprofv3 PMC summary (profiles/), if any."""
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
@@ -303,6 +355,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-mc", action="store_true", help="skip the motion-compensation leg")
     ap.add_argument("--no-tz", action="store_true", help="skip the integer-search leg")
+    ap.add_argument("--no-pi", action="store_true", help="skip the predInterSearch producer leg")
     ap.add_argument("--workload", choices=sorted(WORKLOADS), default="c3_qp22",
                     help="BASELINE.json config to run (default: the headline configs[2] at QP22)")
     ap.add_argument("--jobs", choices=("ctu", "uniform"), default="ctu",
@@ -449,6 +502,9 @@ def main():
                 "note": "jobs H2D + org frame H2D + refine + results D2H, pinned host buffers"}
 
     mc = mc_leg(dev, stream, reps=max(5, args.steps)) if rank == 0 and not args.no_mc and W == 1920 else None
+    pi = None
+    if rank == 0 and not args.no_pi and W == 1920 and world == 1:
+        pi = pred_inter_leg(dev, reps=2, cpu_seconds=0.0 if args.no_cpu_baseline else 4.0)
     tz = None
     if rank == 0 and not args.no_tz and W == 1920 and world == 1:
         tz = tz_leg(dev, stream, reps=max(3, args.steps // 2), cpu_seconds=0.0 if args.no_cpu_baseline else 6.0)
@@ -516,6 +572,8 @@ def main():
             out["motion_compensation"] = mc
         if tz:
             out["integer_search"] = tz
+        if pi:
+            out["pred_inter_search"] = pi
         print(json.dumps(out), flush=True)
 
     if world > 1:

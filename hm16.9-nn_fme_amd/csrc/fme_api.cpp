@@ -120,6 +120,7 @@ struct fme_ctx {
   // predInterSearch producer: m_integerMv2Nx2N[REF_PIC_LIST_0][k] (TEncSearch.h:118), AMVP staging
   int16_t int_mv_2n[FME_MAX_REFS][2] = {};
   DevBuf<AmvpTask> d_amvp;
+  DevBuf<int16_t> d_tz_emi;   // [n][2] post-EMI integer MVs (producer levels)
   DevBuf<uint32_t> d_amvp_sad;
 
   std::unique_ptr<fme_ctx> single;  // private context for the single-PU entry points
@@ -236,7 +237,7 @@ int fme_destroy(fme_ctx* c) {
     if (c->chroma_owned[i]) (void)hipFree(c->chroma_owned[i]);
   c->d_mc_jobs.release(); c->d_mc_planes.release(); c->d_mc_invalid.release();
   c->d_tz_ext.release(); c->d_tz_sad.release(); c->d_tz_rst.release(); c->d_tz_rq.release();
-  c->d_amvp.release(); c->d_amvp_sad.release();
+  c->d_amvp.release(); c->d_amvp_sad.release(); c->d_tz_emi.release();
   for (auto& e : c->ev_tz)
     if (e) (void)hipEventDestroy(e);
   for (auto& e : c->ev_mc)
@@ -582,8 +583,12 @@ int fme_refine_device(fme_ctx* c, const fme_job* d_jobs, fme_result* d_res, int 
 // ---- integer motion estimation (xTZSearch / xPatternSearch) -----------------------------------
 // classify (validation + class histogram, one host sync) -> scatter (jobs grouped by PU shape)
 // -> one search launch per unit shape (fme_tz.hip) writing mv_x / mv_y (and ruiSAD) in place.
-int fme_integer_search_device(fme_ctx* c, fme_job* d_jobs, const fme_tz_ext* d_ext, uint32_t* d_sad, int n,
-                              void* stream) {
+}  // extern "C"
+
+// d_emi (may be null): also run the EMI square step of uni-pred EMI jobs and write the resulting
+// integer MV there (the producer's m_integerMv2Nx2N), leaving jobs' mv_x / mv_y at the TZ best.
+static int tz_run(fme_ctx* c, fme_job* d_jobs, const fme_tz_ext* d_ext, uint32_t* d_sad, int n, void* stream,
+                  int16_t* d_emi) {
   if (!c || (n > 0 && (!d_jobs || !d_ext))) return fail(FME_E_INVALID, "fme_integer_search_device: null argument");
   if (n < 0) return fail(FME_E_INVALID, "fme_integer_search_device: n = %d", n);
   if (n == 0) return FME_OK;
@@ -643,6 +648,7 @@ int fme_integer_search_device(fme_ctx* c, fme_job* d_jobs, const fme_tz_ext* d_e
   ta.jobs_out = d_jobs;
   ta.ext = d_ext;
   ta.sad = d_sad;
+  ta.emi_mv = d_emi;
   ta.defer = c->tz_defer ? 1 : 0;
   if (c->tz_defer) {
     HIP_TRY(c->d_tz_rst.reserve((size_t)n * 8));
@@ -688,7 +694,8 @@ int fme_integer_search_device(fme_ctx* c, fme_job* d_jobs, const fme_tz_ext* d_e
   return FME_OK;
 }
 
-int fme_integer_search(fme_ctx* c, fme_job* jobs, const fme_tz_ext* ext, uint32_t* sad, int n, void* stream) {
+static int tz_run_host(fme_ctx* c, fme_job* jobs, const fme_tz_ext* ext, uint32_t* sad, int n, void* stream,
+                       int16_t* emi) {
   if (!c || (n > 0 && (!jobs || !ext))) return fail(FME_E_INVALID, "fme_integer_search: null argument");
   if (n <= 0) return n == 0 ? FME_OK : fail(FME_E_INVALID, "fme_integer_search: n = %d", n);
   HIP_TRY(hipSetDevice(c->device));
@@ -696,14 +703,27 @@ int fme_integer_search(fme_ctx* c, fme_job* jobs, const fme_tz_ext* ext, uint32_
   HIP_TRY(c->d_jobs.reserve(n));
   HIP_TRY(c->d_tz_ext.reserve(n));
   HIP_TRY(c->d_tz_sad.reserve(n));
+  if (emi) HIP_TRY(c->d_tz_emi.reserve((size_t)2 * n));
   HIP_TRY(hipMemcpyAsync(c->d_jobs.p, jobs, (size_t)n * sizeof(fme_job), hipMemcpyHostToDevice, s));
   HIP_TRY(hipMemcpyAsync(c->d_tz_ext.p, ext, (size_t)n * sizeof(fme_tz_ext), hipMemcpyHostToDevice, s));
-  int rc = fme_integer_search_device(c, c->d_jobs.p, c->d_tz_ext.p, c->d_tz_sad.p, n, stream);
+  int rc = tz_run(c, c->d_jobs.p, c->d_tz_ext.p, c->d_tz_sad.p, n, stream, emi ? c->d_tz_emi.p : nullptr);
   if (rc) return rc;
   HIP_TRY(hipMemcpyAsync(jobs, c->d_jobs.p, (size_t)n * sizeof(fme_job), hipMemcpyDeviceToHost, s));
   if (sad) HIP_TRY(hipMemcpyAsync(sad, c->d_tz_sad.p, (size_t)n * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+  if (emi) HIP_TRY(hipMemcpyAsync(emi, c->d_tz_emi.p, (size_t)n * 2 * sizeof(int16_t), hipMemcpyDeviceToHost, s));
   HIP_TRY(hipStreamSynchronize(s));
   return FME_OK;
+}
+
+extern "C" {
+
+int fme_integer_search_device(fme_ctx* c, fme_job* d_jobs, const fme_tz_ext* d_ext, uint32_t* d_sad, int n,
+                              void* stream) {
+  return tz_run(c, d_jobs, d_ext, d_sad, n, stream, nullptr);
+}
+
+int fme_integer_search(fme_ctx* c, fme_job* jobs, const fme_tz_ext* ext, uint32_t* sad, int n, void* stream) {
+  return tz_run_host(c, jobs, ext, sad, n, stream, nullptr);
 }
 
 int fme_integer_search_last_ms(fme_ctx* c, float* ms) {
@@ -1044,8 +1064,8 @@ int fme_pred_inter_reset(fme_ctx* c) {
 //   1. one AMVP template-cost launch over every (request, reference, candidate) with two candidates;
 //   2. integer searches by dependency level: a request that reads m_integerMv2Nx2N[k] waits for the
 //      level of the 2Nx2N request that last wrote it (per CTU the chain of 2Nx2N CUs in xCompressCU
-//      order; CTUs are independent), and the writers of a level run the EMI step (through
-//      fme_refine, with the NN state saved and restored) to publish their post-EMI integer MV;
+//      order); the search kernels also run the EMI square step and return the post-EMI integer MV
+//      that the 2Nx2N requests publish to the levels above;
 //   3. one fme_refine over all jobs in request order (the NN's carried state as in the reference);
 //   4. xCheckBestMVP and the reference choice on the host.
 int fme_pred_inter_p(fme_ctx* c, const fme_pu_req* reqs, fme_pu_res* res, int n, void* stream) {
@@ -1174,7 +1194,7 @@ int fme_pred_inter_p(fme_ctx* c, const fme_pu_req* reqs, fme_pu_res* res, int n,
   std::vector<fme_job> lj;
   std::vector<fme_tz_ext> le;
   std::vector<int> lidx;
-  std::vector<fme_result> lres;
+  std::vector<int16_t> lemi;
   for (int L = 0; L <= max_level; L++) {
     lj.clear(); le.clear(); lidx.clear();
     for (int i : by_level[L])
@@ -1190,30 +1210,14 @@ int fme_pred_inter_p(fme_ctx* c, const fme_pu_req* reqs, fme_pu_res* res, int n,
         le.push_back(e);
         lidx.push_back(jx);
       }
-    rc = fme_integer_search(c, lj.data(), le.data(), nullptr, (int)lj.size(), stream);
-    if (rc) return rc;
-    for (size_t m = 0; m < lj.size(); m++) jobs[lidx[m]] = lj[m];
-    if (L == max_level) break;
-    // writers of this level publish their post-EMI integer MV for the levels above
-    lj.clear(); lidx.clear();
-    for (int i : by_level[L])
-      if (reqs[i].part_size == FME_PART_2Nx2N)
-        for (int k = 0; k < reqs[i].num_refs; k++) {
-          lj.push_back(jobs[base[i] + k]);
-          lidx.push_back(base[i] + k);
-        }
-    if (lj.empty()) continue;
-    uint32_t st[12];
-    rc = fme_nn_get_state(c, st);
-    if (rc) return rc;
-    lres.resize(lj.size());
-    rc = fme_refine(c, lj.data(), lres.data(), (int)lj.size(), stream);
-    if (rc) return rc;
-    rc = fme_nn_set_state(c, st);
+    lemi.resize(2 * lj.size());
+    // the integer searches of this level, with the EMI square step's result for the levels above
+    rc = tz_run_host(c, lj.data(), le.data(), nullptr, (int)lj.size(), stream, lemi.data());
     if (rc) return rc;
     for (size_t m = 0; m < lj.size(); m++) {
-      emi_mv[2 * lidx[m]] = lres[m].mv_int_x;
-      emi_mv[2 * lidx[m] + 1] = lres[m].mv_int_y;
+      jobs[lidx[m]] = lj[m];
+      emi_mv[2 * lidx[m]] = lemi[2 * m];
+      emi_mv[2 * lidx[m] + 1] = lemi[2 * m + 1];
     }
   }
   // ---- 3. the sub-pel path over every job in request order ----

@@ -110,6 +110,7 @@ struct TzArgs {
   uint32_t* rst;              // [n][8] raster hand-off records, by job index
   int32_t* rq;                // [3][n] queued job indices per kernel
   int32_t* rqn;               // [3] queue lengths
+  int16_t* emi_mv;            // [n][2] or null: the MV after the EMI square step (uni-pred EMI jobs)
 };
 int tz_kernel_of(int cls);    // 0: 4x8 units, 1: 8x4, 2: 8x8
 int tz_lanes_per_pu(int cls);

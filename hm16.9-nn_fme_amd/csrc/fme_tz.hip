@@ -59,7 +59,7 @@ struct Range {
 
 enum Phase {
   P_START, P_ZERO, P_PRED, P_RANGE, P_FIRST, P_TWO1, P_TWO, P_RASTER_CHK, P_RASTER, P_STAR_CHK, P_STAR,
-  P_STAR_END, P_FULL, P_DONE, P_DEFER
+  P_STAR_END, P_FULL, P_DONE, P_DEFER, P_SQUARE
 };
 
 struct Tz {
@@ -76,7 +76,23 @@ struct Tz {
   int rx, ry;           // raster iterators
   Range R, RR;          // search range, raster range
   int range;            // m_iSearchRange
+  bool square;          // run the EMI square step after the search (ta.emi_mv)
+  int tx, ty;           // the TZ best before the square step
+  uint32_t tsad;
 };
+
+// xTZ8PointSquareSearch (TEncSearch.cpp:1324-1377) at distance 1: point k of (1 2 3 / 4 . 5 / 6 7 8) in
+// call order with the reference's range checks (the middle column is only checked vertically).
+__device__ __forceinline__ bool square_point(const Tz& s, int k, bool& ok, int& x, int& y) {
+  if (k >= 8) return false;
+  const int dx = (k == 0 || k == 3 || k == 5) ? -1 : ((k == 1 || k == 6) ? 0 : 1);
+  const int dy = k < 3 ? -1 : (k < 5 ? 0 : 1);
+  x = s.ox + dx;
+  y = s.oy + dy;
+  ok = (dy < 0 ? y >= s.R.t : true) && (dy > 0 ? y <= s.R.b : true) && (dx < 0 ? x >= s.R.l : true) &&
+       (dx > 0 ? x <= s.R.r : true);
+  return true;
+}
 
 // Point k of xTZ8PointDiamondSearch(origin, dist) in call order, with the range check the
 // reference applies before testing it (the "inside" fast path tests the same points in the same
@@ -267,10 +283,31 @@ __device__ __forceinline__ bool next_candidate(Tz& s, int pw, int ph, int cu_x, 
         if (s.bdist > 0) {
           s.ox = s.bx; s.oy = s.by; s.bdist = 0; s.pnr = 0; s.dist = 1; s.k = -1;
           s.phase = P_STAR;
+        } else if (s.square) {
+          s.tx = s.bx; s.ty = s.by; s.tsad = s.best_sad;
+          s.ox = s.bx; s.oy = s.by; s.k = 0;
+          s.phase = P_SQUARE;
         } else {
           s.phase = P_DONE;
         }
         break;
+      case P_SQUARE: {
+        bool ok;
+        while (square_point(s, s.k, ok, x, y)) {
+          s.k++;
+          if (ok) {
+            pnr = s.k; pd = 1;
+            bool o2;
+            int x2, y2;
+            more = false;
+            for (int j = s.k; square_point(s, j, o2, x2, y2); j++)
+              if (o2) { more = true; break; }
+            return true;
+          }
+        }
+        s.phase = P_DONE;
+        break;
+      }
       case P_STAR_END:
         s.phase = P_STAR_CHK;
         if (s.bdist == 1) {
@@ -431,6 +468,8 @@ __device__ __forceinline__ void tz_unit(const TzArgs& ta, int cls_off, int cls_c
   const bool defer = !RASTER && ta.defer;
   s.sx = s.sy = 0; s.px = s.py = 0; s.has_pred = false;
   s.rx = s.ry = 0;
+  s.square = ta.emi_mv != nullptr && (j.flags & FME_JOB_EMI) && !(j.flags & FME_JOB_BIPRED);
+  s.tx = s.ty = 0; s.tsad = 0;
   constexpr int ND = UW / 4 + 1;
   if (RASTER) {
     const uint32_t* rec = ta.rst + (size_t)jid * kTzRec;
@@ -556,9 +595,15 @@ __device__ __forceinline__ void tz_unit(const TzArgs& ta, int cls_off, int cls_c
       return;
     }
     fme_job* out = ta.jobs_out + jid;
-    out->mv_x = (int16_t)s.bx;
-    out->mv_y = (int16_t)s.by;
-    if (ta.sad) ta.sad[jid] = s.best_sad - mv_cost(ml, mv_bits(s.bx, s.by, 2, j.mvp_x, j.mvp_y));
+    const int bx = s.square ? s.tx : s.bx, by = s.square ? s.ty : s.by;
+    const uint32_t bsad = s.square ? s.tsad : s.best_sad;
+    out->mv_x = (int16_t)bx;
+    out->mv_y = (int16_t)by;
+    if (ta.sad) ta.sad[jid] = bsad - mv_cost(ml, mv_bits(bx, by, 2, j.mvp_x, j.mvp_y));
+    if (ta.emi_mv) {   // the integer MV after the square step (rcMv of xTZSearch, TEncSearch.cpp:5037-5048)
+      ta.emi_mv[2 * jid] = (int16_t)s.bx;
+      ta.emi_mv[2 * jid + 1] = (int16_t)s.by;
+    }
   }
 }
 
