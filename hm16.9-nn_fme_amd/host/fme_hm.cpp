@@ -191,6 +191,27 @@ void MotionCompensator::run(uint8_t* y, int ys, uint8_t* cb, uint8_t* cr, int cs
   jobs_.clear();
 }
 
+// ---- InterSearchP -------------------------------------------------------------------------
+
+int InterSearchP::add(const fme_pu_req& req) {
+  reqs_.push_back(req);
+  return (int)reqs_.size() - 1;
+}
+
+std::vector<fme_pu_res> InterSearchP::run() {
+  std::vector<fme_pu_res> res(reqs_.size());
+  std::lock_guard<std::mutex> lk(search_.mutex());
+  if (!reqs_.empty())
+    check(fme_pred_inter_p(search_.ctx(), reqs_.data(), res.data(), (int)reqs_.size(), nullptr), "fme_pred_inter_p");
+  reqs_.clear();
+  return res;
+}
+
+void InterSearchP::reset() {
+  std::lock_guard<std::mutex> lk(search_.mutex());
+  check(fme_pred_inter_reset(search_.ctx()), "fme_pred_inter_reset");
+}
+
 // ---- CtuRowBatcher -----------------------------------------------------------------------
 
 CtuRowBatcher::CtuRowBatcher(FracSearch& search, int maxRowsInFlight)

@@ -129,6 +129,26 @@ class MotionCompensator {
   std::vector<uint8_t> stage_;
 };
 
+// TEncSearch::predInterSearch's uni-directional PU / reference loop for P slices
+// (TEncSearch.cpp:3746-3866) over the FracSearch's context: AMVP template choice, bits,
+// xMotionEstimation, xCheckBestMVP and the reference choice per partition PU, with
+// m_integerMv2Nx2N kept like TEncSearch keeps it.  The caller queues one fme_pu_req per PU in
+// call order (AMVP candidates from TComDataCU::fillMvpCand) and gets one fme_pu_res per request.
+// A queue of one request is the live encoder's path; a frame's worth is trace replay (the
+// library batches it by its m_integerMv2Nx2N dependency levels).
+class InterSearchP {
+ public:
+  explicit InterSearchP(FracSearch& search) : search_(search) {}
+  int add(const fme_pu_req& req);        // index of the request in the pending batch
+  int pending() const { return (int)reqs_.size(); }
+  std::vector<fme_pu_res> run();         // the queued requests in order; clears the queue
+  void reset();                          // m_integerMv2Nx2N = (0, 0), as a new TEncSearch
+
+ private:
+  FracSearch& search_;
+  std::vector<fme_pu_req> reqs_;
+};
+
 // Per-CTU-row batch producer (double-buffered: the caller fills row k+1 while row k runs).
 class CtuRowBatcher {
  public:

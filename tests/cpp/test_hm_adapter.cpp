@@ -65,6 +65,10 @@ int clip_qpel(int v, int pos, int pic) {   // TComDataCU::clipMv (TComDataCU.cpp
 }
 int div4_round(int v) { return (v + 2) >> 2; }   // TComMv::divideByPowerOf2 with rounding
 
+void check_rc(int rc) {
+  if (rc != FME_OK) throw fme_hm::Error(rc, fme_last_error());
+}
+
 bool same(const fme_result& a, const fme_result& b) {
   return a.mv_int_x == b.mv_int_x && a.mv_int_y == b.mv_int_y && a.mv_x == b.mv_x && a.mv_y == b.mv_y &&
          a.half_x == b.half_x && a.half_y == b.half_y && a.qtr_x == b.qtr_x && a.qtr_y == b.qtr_y &&
@@ -289,11 +293,65 @@ static int run() {
     EXPECT(gcb == ocb && gcr == ocr, "MotionCompensator chroma differs from orc_mc");
   }
 
+  // ---- InterSearchP: predInterSearch's P-slice PU / reference loop ----------
+  int pi_reqs = 0;
+  {
+    InterSearchP inter(search);
+    inter.reset();
+    orc_pred_inter_reset(orc.get());
+    check_rc(fme_nn_reset_state(search.ctx()));
+    orc_nn_reset(orc.get());
+    std::mt19937 rq(7);
+    auto Q = [&](int lo, int hi) { return std::uniform_int_distribution<int>(lo, hi)(rq); };
+    std::vector<fme_pu_req> reqs;
+    auto add_cu = [&](int x0, int y0, int s, int depth) {
+      const int parts[3][2][4] = {{{0, 0, s, s}, {-1, 0, 0, 0}},
+                                  {{0, 0, s, s / 2}, {0, s / 2, s, s / 2}},
+                                  {{0, 0, s / 2, s}, {s / 2, 0, s / 2, s}}};
+      for (int ps = 0; ps < 3; ps++)
+        for (int p = 0; p < 2; p++) {
+          if (parts[ps][p][0] < 0) continue;
+          fme_pu_req q = {};
+          q.x = (uint16_t)(x0 + parts[ps][p][0]); q.y = (uint16_t)(y0 + parts[ps][p][1]);
+          q.w = (uint8_t)parts[ps][p][2]; q.h = (uint8_t)parts[ps][p][3];
+          q.cu_x = (uint16_t)x0; q.cu_y = (uint16_t)y0;
+          q.part_size = (uint8_t)ps;   // FME_PART_2Nx2N, _2NxN, _Nx2N
+          q.depth = (uint8_t)depth;
+          q.org_id = 4; q.num_refs = 4; q.lambda_id = 0; q.search_range = 64;
+          for (int k = 0; k < 4; k++) {
+            q.ref_id[k] = (uint8_t)k;
+            q.n_cand[k] = (uint8_t)(Q(0, 9) == 0 ? 1 : 2);
+            for (int m = 0; m < 2; m++) {
+              q.cand[k][m][0] = (int16_t)(4 * (k + 1) * 3 + Q(-24, 24));
+              q.cand[k][m][1] = (int16_t)(-4 * (k + 1) * 2 + Q(-24, 24));
+            }
+          }
+          reqs.push_back(q);
+          inter.add(q);
+        }
+    };
+    for (int cy = 0; cy + CTU <= H; cy += CTU)
+      for (int cx = 0; cx + CTU <= W; cx += CTU) {
+        add_cu(cx, cy, 64, 0);
+        for (int k = 0; k < 4; k++) add_cu(cx + 32 * (k & 1), cy + 32 * (k >> 1), 32, 1);
+      }
+    pi_reqs = (int)reqs.size();
+    EXPECT(inter.pending() == pi_reqs, "InterSearchP queue size");
+    const std::vector<fme_pu_res> got = inter.run();
+    std::vector<fme_pu_res> want(reqs.size());
+    EXPECT(orc_pred_inter_p(orc.get(), reqs.data(), want.data(), (int)reqs.size()) == 0, "orc_pred_inter_p failed");
+    int bad = 0;
+    for (size_t i = 0; i < reqs.size(); i++) bad += memcmp(&got[i], &want[i], sizeof(fme_pu_res)) != 0;
+    EXPECT(bad == 0, "InterSearchP: %d of %d requests differ from orc_pred_inter_p", bad, pi_reqs);
+    EXPECT(inter.pending() == 0, "InterSearchP queue not cleared");
+  }
+
   if (failures) {
     fprintf(stderr, "hm adapter: %d failure(s)\n", failures);
     return 1;
   }
   printf("hm adapter ok: %d PU motion compensations (Y/Cb/Cr) bit-exact\n", mc_pus);
+  printf("hm adapter ok: %d predInterSearch PU requests (4 refs) bit-exact\n", pi_reqs);
   printf("hm adapter ok: %d jobs in %d CTU rows, %d single-PU FracDIF calls, 100 NN_pred calls bit-exact\n",
          total, rows, singles);
   return 0;
