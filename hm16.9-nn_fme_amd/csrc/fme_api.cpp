@@ -115,6 +115,7 @@ struct fme_ctx {
   DevBuf<uint32_t> d_tz_rst;   // raster hand-off records [n][8]
   DevBuf<int32_t> d_tz_rq;     // raster queues [3][n] + 3 lengths
   bool tz_defer = FME_TZ_DEFER_DEFAULT;   // FME_TZ_DEFER=0/1: raster searches in a second pass
+  int tz_defer_min = 4096;                 // FME_TZ_DEFER_MIN: batches below this size run in one pass
   hipEvent_t ev_tz[2] = {nullptr, nullptr};
   bool tz_timed = false;
   // predInterSearch producer: m_integerMv2Nx2N[REF_PIC_LIST_0][k] (TEncSearch.h:118), AMVP staging
@@ -212,6 +213,7 @@ int fme_create(int device, const fme_config* cfg, fme_ctx** out_ctx) {
   if (const char* e = getenv("FME_SERIAL_SEARCH")) c->concurrent_search = (e[0] == '0');
   if (const char* e = getenv("FME_LANE_STREAMS")) c->lane_streams = (e[0] == '1');
   if (const char* e = getenv("FME_TZ_DEFER")) c->tz_defer = (e[0] == '1');
+  if (const char* e = getenv("FME_TZ_DEFER_MIN")) c->tz_defer_min = atoi(e);
   HIP_TRY(hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming));
   HIP_TRY(hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming));
   if (cfg->max_jobs > 0) {
@@ -649,8 +651,11 @@ static int tz_run(fme_ctx* c, fme_job* d_jobs, const fme_tz_ext* d_ext, uint32_t
   ta.ext = d_ext;
   ta.sad = d_sad;
   ta.emi_mv = d_emi;
-  ta.defer = c->tz_defer ? 1 : 0;
-  if (c->tz_defer) {
+  // small batches (the producer's dependency levels) skip the second pass: its extra host
+  // synchronisation costs more than the raster divergence it removes
+  const bool defer = c->tz_defer && n >= c->tz_defer_min;
+  ta.defer = defer ? 1 : 0;
+  if (defer) {
     HIP_TRY(c->d_tz_rst.reserve((size_t)n * 8));
     HIP_TRY(c->d_tz_rq.reserve((size_t)3 * n + 4));
     ta.rst = c->d_tz_rst.p;
@@ -673,7 +678,7 @@ static int tz_run(fme_ctx* c, fme_job* d_jobs, const fme_tz_ext* d_ext, uint32_t
   HIP_TRY(hipEventRecord(c->ev_join2, c->aux2));
   HIP_TRY(hipStreamWaitEvent(s, c->ev_join, 0));
   HIP_TRY(hipStreamWaitEvent(s, c->ev_join2, 0));
-  if (c->tz_defer) {
+  if (defer) {
     // pass 2: the queued raster searches, one PU per wave (queue lengths read back: one sync)
     HIP_TRY(hipMemcpyAsync(c->h_counts, ta.rqn, 3 * sizeof(int32_t), hipMemcpyDeviceToHost, s));
     HIP_TRY(hipStreamSynchronize(s));
