@@ -24,7 +24,7 @@ if [ "${PMC:-1}" = 1 ]; then
 fi
 run bench 600 python bench.py --steps "$STEPS" --warmup 3
 if [ "${PROFILE:-1}" = 1 ]; then
-  run rocprof 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python bench.py --steps 5 --warmup 2 --no-cpu-baseline
+  run rocprof 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-pi
   find gpurun_out/prof -name "*kernel_stats.csv" -exec cp {} gpurun_out/kernel_stats.csv \;
   cat gpurun_out/kernel_stats.csv | cut -c1-200
 fi
