@@ -197,6 +197,8 @@ class Reference:
         lib.ref_set_picture_yuv.argtypes = [_P, C.c_int, _P, C.c_int, _P, _P, C.c_int, C.c_int, C.c_int]
         lib.ref_integer_search.restype = C.c_int
         lib.ref_integer_search.argtypes = [_P, _P, _P, _P, C.c_int]
+        lib.ref_template_cost.restype = C.c_uint32
+        lib.ref_template_cost.argtypes = [_P] + [C.c_int] * 12
         lib.ref_mc.restype = C.c_int
         lib.ref_mc.argtypes = [_P, _P, C.c_int, _P, C.c_int, _P, _P, C.c_int, C.c_int, C.c_int]
         self.h = lib.ref_create(use_hadamard, fast_inter_mode, nn_mode)
@@ -234,6 +236,10 @@ class Reference:
 
     def set_lambda(self, lid, lam):
         self.lib.ref_set_lambda(self.h, lid, lam)
+
+    def template_cost(self, org_id, ref_id, x, y, w, h, cu_x, cu_y, mvx, mvy, bits, lambda_id):
+        """xGetTemplateCost over the reference's TComInterpolationFilter / TComRdCost."""
+        return self.lib.ref_template_cost(self.h, org_id, ref_id, x, y, w, h, cu_x, cu_y, mvx, mvy, bits, lambda_id)
 
     def set_keys(self, keys):
         keys = np.ascontiguousarray(keys, dtype=np.int16)

@@ -523,6 +523,44 @@ int ref_mc(void* h, const fme_mc_job* jobs, int n, uint8_t* y, int ys, uint8_t* 
   return 0;
 }
 
+// xGetTemplateCost (TEncSearch.cpp:4397-4436) over the reference's own pieces: clipMv, xPredInterBlk's
+// luma filter order (uni-prediction, isLast) on the padded TComPicYuv, TComRdCost::getDistPart(DF_SAD)
+// (TComRdCost.cpp:327-349) and calcRdCost(bits, SAD, DF_SAD) (57-102) with the slot's lambda.
+uint32_t ref_template_cost(void* h, int org_id, int ref_id, int x, int y, int w, int hgt, int cu_x, int cu_y,
+                           int mvx, int mvy, int bits, int lambda_id) {
+  RefCtx* c = static_cast<RefCtx*>(h);
+  TComPicYuv& ref = c->pics[ref_id].yuv;
+  TComPicYuv& org = c->pics[org_id].yuv;
+  const int W = ref.getWidth(COMPONENT_Y), H = ref.getHeight(COMPONENT_Y);
+  {   // TComDataCU::clipMv (TComDataCU.cpp:2773-2786)
+    const int hmax = (W + 8 - cu_x - 1) << 2, hmin = (-64 - 8 - cu_x + 1) * 4;
+    const int vmax = (H + 8 - cu_y - 1) << 2, vmin = (-64 - 8 - cu_y + 1) * 4;
+    mvx = std::min(hmax, std::max(hmin, mvx));
+    mvy = std::min(vmax, std::max(vmin, mvy));
+  }
+  TComInterpolationFilter f;
+  const int rs = ref.getStride(COMPONENT_Y);
+  Pel* src = ref.getAddr(COMPONENT_Y) + (y + (mvy >> 2)) * rs + x + (mvx >> 2);
+  std::vector<Pel> dst((size_t)w * hgt);
+  const int xf = mvx & 3, yf = mvy & 3;
+  if (yf == 0) {
+    f.filterHor(COMPONENT_Y, src, rs, dst.data(), w, w, hgt, xf, true, CHROMA_400, 8);
+  } else if (xf == 0) {
+    f.filterVer(COMPONENT_Y, src, rs, dst.data(), w, w, hgt, yf, true, true, CHROMA_400, 8);
+  } else {
+    std::vector<Pel> tmp((size_t)w * (hgt + NTAPS_LUMA - 1));
+    f.filterHor(COMPONENT_Y, src - ((NTAPS_LUMA >> 1) - 1) * rs, rs, tmp.data(), w, w, hgt + NTAPS_LUMA - 1, xf, false,
+                CHROMA_400, 8);
+    f.filterVer(COMPONENT_Y, tmp.data() + ((NTAPS_LUMA >> 1) - 1) * w, w, dst.data(), w, w, hgt, yf, false, true,
+                CHROMA_400, 8);
+  }
+  const int os = org.getStride(COMPONENT_Y);
+  const Pel* o = org.getAddr(COMPONENT_Y) + y * os + x;
+  c->s.setLambda(c->lambda[lambda_id]);
+  const Distortion sad = c->s.rd.getDistPart(8, dst.data(), w, o, os, w, hgt, COMPONENT_Y, DF_SAD);
+  return (UInt)c->s.rd.calcRdCost(bits, sad, DF_SAD);
+}
+
 }  // extern "C"
 
 // ---- integer motion estimation ----------------------------------------

@@ -214,3 +214,43 @@ def test_pred_inter_reset_and_rejection():
     with pytest.raises(FmeError):
         ctx.pred_inter_p(bad)
     assert len(ctx.pred_inter_p(reqs[:0])) == 0
+
+
+def test_template_cost_matches_reference_harness():
+    """xGetTemplateCost (TEncSearch.cpp:4397-4436) as the producer and oracle compute it (clipMv'd
+    luma prediction, SAD, SAD + bits * mlambda / 65536) against the reference's own
+    TComInterpolationFilter / TComRdCost::getDistPart / calcRdCost (oracle/_ref), on every PU shape,
+    every quarter-pel phase and MVs far enough out for clipMv to act."""
+    from oracle import REF_SO, Oracle, Reference
+    if not os.path.exists(REF_SO):
+        pytest.skip("oracle/_ref not built (needs /root/reference)")
+    pics = _pics()
+    ref = Reference(fast_inter_mode=1)
+    orc = Oracle(nn_mode=0)
+    for k, v in pics.items():
+        ref.set_picture(k, v)
+    for lid, lam in enumerate(synth.LDP_LAMBDA[22]):
+        ref.set_lambda(lid, lam)
+    rng = np.random.default_rng(31)
+    org = pics[4].astype(np.int64)
+    n = 0
+    for (w, h) in synth.ALL_PU_SIZES:
+        for _ in range(12):
+            # a PU inside its (64x64) CU, as getPartIndexAndSize gives it: clipMv keeps the reads
+            # inside the padded picture only for such geometry
+            cu_x, cu_y = 64 * int(rng.integers(0, W // 64)), 64 * int(rng.integers(0, H // 64))
+            x = cu_x + 4 * int(rng.integers(0, (64 - w) // 4 + 1))
+            y = cu_y + 4 * int(rng.integers(0, (64 - h) // 4 + 1))
+            span = 200 if rng.random() < 0.3 else 40
+            mvx, mvy = (int(v) for v in rng.integers(-4 * span, 4 * span + 1, 2))
+            lid, bits, rid = int(rng.integers(0, 4)), int(rng.integers(0, 3)), int(rng.integers(0, 4))
+            cx = int(synth._clip_cu_qpel(mvx, cu_x, W))
+            cy = int(synth._clip_cu_qpel(mvy, cu_y, H))
+            pred = orc.pred_block(pics[rid], x, y, w, h, cx, cy)
+            sad = int(np.abs(pred.astype(np.int64) - org[y:y + h, x:x + w]).sum())
+            ml = 65536.0 * np.sqrt(synth.LDP_LAMBDA[22][lid])
+            want = int(sad + (bits * ml) / 65536.0)
+            got = ref.template_cost(4, rid, x, y, w, h, cu_x, cu_y, mvx, mvy, bits, lid)
+            assert got == want, (w, h, x, y, mvx, mvy, got, want)
+            n += 1
+    assert n == 12 * len(synth.ALL_PU_SIZES)
