@@ -88,6 +88,12 @@ struct fme_ctx {
   size_t n_keys = 0;
   DevBuf<float> d_nn;         // packed layout (nn_pack, kNnPkFloats)
   bool nn_loaded = false;
+  // nn_mode 2: a generic net (fme_load_nn_net), packed by nn_deep_pack
+  fme_nn_net net{};
+  DevBuf<uint8_t> d_net;
+  bool net_loaded = false;
+  int nn_engine = FME_NN_ENGINE_EXACT;
+  float* nn_margin = nullptr;  // caller-owned device array (fme_set_nn_margin_output)
 
   DevBuf<fme_job> d_jobs;      // staging for fme_refine (host arrays)
   DevBuf<fme_result> d_res;
@@ -158,6 +164,12 @@ struct fme_ctx {
 };
 
 namespace fme {
+size_t nn_deep_packed_bytes(const fme_nn_net& n);
+void nn_deep_pack(const fme_nn_net& n, const double* params, void* out);
+hipError_t launch_nn_deep_tail(const fme_nn_net& n, const void* packed, float* margin, const BatchArgs& a,
+                               const WorkBufs& w, int state_in, int engine, hipStream_t s);
+hipError_t launch_nn_deep_single(const fme_nn_net& n, const void* packed, const uint32_t* in11, int32_t* out,
+                                 hipStream_t s);
 hipError_t debug_phase_cycles(unsigned long long* out16, bool reset);
 hipError_t launch_nn_single(const float* nnp, const uint32_t* in, int32_t* out, hipStream_t s);
 }
@@ -195,6 +207,7 @@ int fme_create(int device, const fme_config* cfg, fme_ctx** out_ctx) {
   if (!cfg || !out_ctx) return fail(FME_E_INVALID, "fme_create: null argument");
   *out_ctx = nullptr;
   if (cfg->bit_depth != 8) return fail(FME_E_UNSUPPORTED, "fme_create: bit_depth %d (only 8)", cfg->bit_depth);
+  if (cfg->nn_mode < 0 || cfg->nn_mode > 2) return fail(FME_E_INVALID, "fme_create: nn_mode %d", cfg->nn_mode);
   int ndev = 0;
   HIP_TRY(hipGetDeviceCount(&ndev));
   if (device < 0 || device >= ndev) return fail(FME_E_INVALID, "fme_create: device %d of %d", device, ndev);
@@ -244,7 +257,7 @@ int fme_destroy(fme_ctx* c) {
     if (e) (void)hipEventDestroy(e);
   for (auto& e : c->ev_mc)
     if (e) (void)hipEventDestroy(e);
-  c->d_pics.release(); c->d_mlambda.release(); c->d_keys.release(); c->d_nn.release();
+  c->d_pics.release(); c->d_mlambda.release(); c->d_keys.release(); c->d_nn.release(); c->d_net.release();
   c->d_jobs.release(); c->d_res.release(); c->cls.release(); c->perm.release(); c->sjobs.release();
   c->counts.release(); c->blk_agg.release(); c->blk_prefix.release(); c->nn_state.release();
   c->single_pic.release(); c->single_job.release(); c->single_res.release();
@@ -398,6 +411,61 @@ int fme_load_nn_weights(fme_ctx* c, const float* params, int count) {
   return FME_OK;
 }
 
+int fme_nn_param_count(const fme_nn_net* n) {
+  if (!n) return fail(FME_E_INVALID, "fme_nn_param_count: null descriptor");
+  if (n->n_hidden < 1 || n->n_hidden > FME_NN_MAX_HIDDEN)
+    return fail(FME_E_INVALID, "fme_nn_param_count: n_hidden %d", n->n_hidden);
+  if (n->precision != FME_NN_F32 && n->precision != FME_NN_F64)
+    return fail(FME_E_INVALID, "fme_nn_param_count: precision %d", n->precision);
+  if (n->embedding < FME_NN_EMB_NONE || n->embedding > FME_NN_EMB_SWAP)
+    return fail(FME_E_INVALID, "fme_nn_param_count: embedding %d", n->embedding);
+  if (n->out_act != FME_NN_OUT_LINEAR && n->out_act != FME_NN_OUT_SIGMOID)
+    return fail(FME_E_INVALID, "fme_nn_param_count: out_act %d", n->out_act);
+  if (n->carry_hidden >> n->n_hidden) return fail(FME_E_INVALID, "fme_nn_param_count: carry_hidden 0x%x", n->carry_hidden);
+  int count = n->embedding ? 64 : 0, fan = n->embedding ? 17 : 9;
+  for (int l = 0; l < n->n_hidden; l++) {
+    const int w = n->width[l];
+    if (w < 1 || w > FME_NN_MAX_WIDTH) return fail(FME_E_INVALID, "fme_nn_param_count: width[%d] = %d", l, w);
+    count += w * fan + 3 * w;
+    fan = w;
+  }
+  return count + 49 * fan + 49 + 27;
+}
+
+int fme_load_nn_net(fme_ctx* c, const fme_nn_net* n, const double* params, int count) {
+  if (!c || !n || !params) return fail(FME_E_INVALID, "fme_load_nn_net: null argument");
+  const int need = fme_nn_param_count(n);
+  if (need < 0) return need;
+  if (count != need) return fail(FME_E_INVALID, "fme_load_nn_net: %d params, the descriptor needs %d", count, need);
+  if (n->carry_hidden)
+    return fail(FME_E_UNSUPPORTED, "fme_load_nn_net: carry_hidden 0x%x (hidden layers carried across calls) is not "
+                "supported by the batch engines", n->carry_hidden);
+  HIP_TRY(hipSetDevice(c->device));
+  const size_t bytes = nn_deep_packed_bytes(*n);
+  if (!bytes) return fail(FME_E_UNSUPPORTED, "fme_load_nn_net: no kernel for this net");
+  std::vector<unsigned char> packed(bytes);
+  nn_deep_pack(*n, params, packed.data());
+  HIP_TRY(hipDeviceSynchronize());   // a batch in flight may still read the previous net
+  HIP_TRY(c->d_net.reserve(bytes));
+  HIP_TRY(hipMemcpy(c->d_net.p, packed.data(), bytes, hipMemcpyHostToDevice));
+  c->net = *n;
+  c->net_loaded = true;
+  return FME_OK;
+}
+
+int fme_set_nn_engine(fme_ctx* c, int engine) {
+  if (!c || (engine != FME_NN_ENGINE_EXACT && engine != FME_NN_ENGINE_MFMA))
+    return fail(FME_E_INVALID, "fme_set_nn_engine: bad argument");
+  c->nn_engine = engine;
+  return FME_OK;
+}
+
+int fme_set_nn_margin_output(fme_ctx* c, float* d_margin) {
+  if (!c) return fail(FME_E_INVALID, "fme_set_nn_margin_output: null ctx");
+  c->nn_margin = d_margin;
+  return FME_OK;
+}
+
 int fme_nn_reset_state(fme_ctx* c) {
   if (!c) return fail(FME_E_INVALID, "fme_nn_reset_state: null ctx");
   HIP_TRY(hipSetDevice(c->device));
@@ -447,7 +515,8 @@ int fme_refine_device(fme_ctx* c, const fme_job* d_jobs, fme_result* d_res, int 
   if (!c || (n > 0 && (!d_jobs || !d_res))) return fail(FME_E_INVALID, "fme_refine_device: null argument");
   if (n < 0) return fail(FME_E_INVALID, "fme_refine_device: n = %d", n);
   if (n == 0) return FME_OK;
-  if (c->cfg.nn_mode && !c->nn_loaded) return fail(FME_E_STATE, "fme_refine_device: nn_mode set but no weights loaded");
+  if (c->cfg.nn_mode == 1 && !c->nn_loaded) return fail(FME_E_STATE, "fme_refine_device: nn_mode set but no weights loaded");
+  if (c->cfg.nn_mode == 2 && !c->net_loaded) return fail(FME_E_STATE, "fme_refine_device: nn_mode 2 but no net loaded");
   HIP_TRY(hipSetDevice(c->device));
   hipStream_t s = static_cast<hipStream_t>(stream);
   int rc = ensure_work(c, n);
@@ -543,7 +612,9 @@ int fme_refine_device(fme_ctx* c, const fme_job* d_jobs, fme_result* d_res, int 
     // "main search" spans all three lane kernels here (and the cooperative shapes beside them)
     if (prof) HIP_TRY(hipEventRecord(ev[4], s));
     if (prof) HIP_TRY(hipEventRecord(ev[5], s));
-    HIP_TRY(launch_nn_tail(a, w, c->d_nn.p, c->state_cur, s));
+    HIP_TRY(c->cfg.nn_mode == 2
+                ? launch_nn_deep_tail(c->net, c->d_net.p, c->nn_margin, a, w, c->state_cur, c->nn_engine, s)
+                : launch_nn_tail(a, w, c->d_nn.p, c->state_cur, s));
     if (prof) {
       HIP_TRY(hipEventRecord(ev[6], s));
       c->ev_has_large[eb] = true;
@@ -570,7 +641,9 @@ int fme_refine_device(fme_ctx* c, const fme_job* d_jobs, fme_result* d_res, int 
   if (prof) HIP_TRY(hipEventRecord(ev[4], s));
   if (c->concurrent_search && has_aux) HIP_TRY(hipStreamWaitEvent(s, c->ev_join, 0));
   if (prof) HIP_TRY(hipEventRecord(ev[5], s));
-  HIP_TRY(launch_nn_tail(a, w, c->d_nn.p, c->state_cur, s));
+  HIP_TRY(c->cfg.nn_mode == 2
+              ? launch_nn_deep_tail(c->net, c->d_net.p, c->nn_margin, a, w, c->state_cur, c->nn_engine, s)
+              : launch_nn_tail(a, w, c->d_nn.p, c->state_cur, s));
   if (prof) {
     HIP_TRY(hipEventRecord(ev[6], s));
     c->ev_has_large[eb] = has_aux;
@@ -820,7 +893,8 @@ int fme_frac_dif_single(fme_ctx* c, int lossless, const int16_t* key, int key_st
 
 int fme_nn_pred_single(fme_ctx* c, const uint32_t* e, uint32_t cc, int pu_h, int pu_w, int* nn_class, int16_t* out4) {
   if (!c || !e || !nn_class) return fail(FME_E_INVALID, "fme_nn_pred_single: null argument");
-  if (!c->nn_loaded) return fail(FME_E_STATE, "fme_nn_pred_single: no weights loaded");
+  const bool deep = c->cfg.nn_mode == 2;
+  if (deep ? !c->net_loaded : !c->nn_loaded) return fail(FME_E_STATE, "fme_nn_pred_single: no weights loaded");
   HIP_TRY(hipSetDevice(c->device));
   HIP_TRY(c->single_nn_in.reserve(11));
   HIP_TRY(c->single_nn_out.reserve(1));
@@ -830,7 +904,8 @@ int fme_nn_pred_single(fme_ctx* c, const uint32_t* e, uint32_t cc, int pu_h, int
   in[9] = (uint32_t)pu_h;
   in[10] = (uint32_t)pu_w;
   HIP_TRY(hipMemcpy(c->single_nn_in.p, in, sizeof(in), hipMemcpyHostToDevice));
-  HIP_TRY(launch_nn_single(c->d_nn.p, c->single_nn_in.p, c->single_nn_out.p, nullptr));
+  HIP_TRY(deep ? launch_nn_deep_single(c->net, c->d_net.p, c->single_nn_in.p, c->single_nn_out.p, nullptr)
+               : launch_nn_single(c->d_nn.p, c->single_nn_in.p, c->single_nn_out.p, nullptr));
   int32_t cls = 0;
   HIP_TRY(hipMemcpy(&cls, c->single_nn_out.p, sizeof(cls), hipMemcpyDeviceToHost));
   *nn_class = cls;

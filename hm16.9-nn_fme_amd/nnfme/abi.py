@@ -129,3 +129,16 @@ def compare_results(a, b, fields=PARITY_FIELDS):
     bad |= m
     idx = np.flatnonzero(bad)
     return int(bad.sum()), (int(idx[0]) if len(idx) else None), counts
+
+
+# fme_nn_net (40 B): descriptor of a generic NN_pred net (include/fme.h, fme_load_nn_net)
+import ctypes as _C
+
+
+class NnNetStruct(_C.Structure):
+    _fields_ = [("precision", _C.c_int32), ("n_hidden", _C.c_int32), ("width", _C.c_int32 * 4),
+                ("embedding", _C.c_int32), ("out_act", _C.c_int32), ("carry_hidden", _C.c_uint32),
+                ("reserved", _C.c_int32)]
+
+
+assert _C.sizeof(NnNetStruct) == 40

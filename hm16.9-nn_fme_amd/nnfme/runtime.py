@@ -15,7 +15,7 @@ from .weights import load_weights
 PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB_PATH = os.environ.get("FME_LIB_PATH") or os.path.join(PKG_ROOT, "libfme_amd.so")
 
-ABI_VERSION = 3
+ABI_VERSION = 4
 TIMING_NAMES = ("classify", "scatter", "search", "nn_tail", "batch", "search_main", "search_aux")
 
 # Every entry point include/fme.h declares (the ABI test checks the .so exports them).
@@ -28,7 +28,8 @@ ABI_SYMBOLS = (
     "fme_set_picture_chroma", "fme_bind_picture_chroma_device", "fme_motion_compensate",
     "fme_motion_compensate_device", "fme_mc_invalid_count", "fme_mc_last_ms",
     "fme_integer_search", "fme_integer_search_device", "fme_integer_search_last_ms",
-    "fme_pred_inter_p", "fme_pred_inter_reset",
+    "fme_pred_inter_p", "fme_pred_inter_reset", "fme_nn_param_count", "fme_load_nn_net",
+    "fme_set_nn_engine", "fme_set_nn_margin_output",
 )
 
 
@@ -90,6 +91,10 @@ def load_library(path=None):
         "fme_integer_search_last_ms": (I, [P, P]),
         "fme_pred_inter_p": (I, [P, P, P, I, P]),
         "fme_pred_inter_reset": (I, [P]),
+        "fme_nn_param_count": (I, [P]),
+        "fme_load_nn_net": (I, [P, P, P, I]),
+        "fme_set_nn_engine": (I, [P, I]),
+        "fme_set_nn_margin_output": (I, [P, P]),
     }
     for name, (res, args) in sig.items():
         f = getattr(lib, name)
@@ -114,15 +119,19 @@ class FmeContext:
     """One device context: pictures, lambdas, keys, NN weights and the carried NN state."""
 
     def __init__(self, device=0, use_hadamard=1, nn_mode=1, qp=22, fast_inter_mode=1, max_jobs=0,
-                 load_nn=True, lib_path=None):
+                 load_nn=True, lib_path=None, net=None, nn_engine=0):
         self.lib = load_library(lib_path)
         self.cfg = FmeConfig(8, use_hadamard, nn_mode, qp, fast_inter_mode, max_jobs)
         h = C.c_void_p()
         _check(self.lib, self.lib.fme_create(device, C.byref(self.cfg), C.byref(h)))
         self.h = h
         self.device = device
-        if nn_mode and load_nn:
+        if nn_mode == 1 and load_nn:
             self.load_nn(load_weights(qp))
+        if nn_mode == 2 and net is not None:
+            self.load_nn_net(net)
+        if nn_engine:
+            self.set_nn_engine(nn_engine)
 
     def close(self):
         if getattr(self, "h", None):
@@ -233,6 +242,20 @@ class FmeContext:
         if p.size != NN_PARAMS:
             raise FmeError(-1, f"{p.size} NN parameters, expected {NN_PARAMS}")
         _check(self.lib, self.lib.fme_load_nn_weights(self.h, _ptr(p), p.size))
+
+    def load_nn_net(self, net):
+        """A generic NN_pred net (nnfme.weights.NnNet) for nn_mode 2 (fme_load_nn_net)."""
+        d = net.desc_struct()
+        p = np.ascontiguousarray(net.params, dtype=np.float64)
+        _check(self.lib, self.lib.fme_load_nn_net(self.h, C.byref(d), _ptr(p), p.size))
+
+    def set_nn_engine(self, engine):
+        """0: exact (bit-exact to the reference's loops), 1: MFMA GEMM (k-ordered FMA chain)."""
+        _check(self.lib, self.lib.fme_set_nn_engine(self.h, int(engine)))
+
+    def set_nn_margin_output(self, d_ptr):
+        """Device float[n] receiving top-1 minus top-2 of each later batch's NN outputs (0: off)."""
+        _check(self.lib, self.lib.fme_set_nn_margin_output(self.h, C.c_void_p(d_ptr) if d_ptr else None))
 
     def nn_reset(self):
         _check(self.lib, self.lib.fme_nn_reset_state(self.h))

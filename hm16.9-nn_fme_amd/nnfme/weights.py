@@ -142,3 +142,106 @@ def load_checkpoint(path, mean, stdev):
     import torch
     sd = torch.load(path, map_location="cpu", weights_only=True)
     return from_state_dict(sd, mean, stdev)
+
+
+# ---- generic (deeper) NN_pred nets: fme_load_nn_net, BASELINE.json configs[4] ---------------------
+# Blobs written by tools/convert_deep_weights.py from the reference's in-tree backups:
+#   nn3x40_scr.nnd   Backups/4 "SCR 3 layers" (9 -> 3 x 40 -> 49, double, sigmoid output)
+#   nn4x40_qp22.nnd  Backups/15 "blowing 4 lyrs qp 22" (17 -> 4 x 40 -> 49, float, X3/X4 carried)
+F32, F64 = 0, 1
+EMB_NONE, EMB_MASTER, EMB_SWAP = 0, 1, 2
+OUT_LINEAR, OUT_SIGMOID = 0, 1
+NET_FILES = {"scr3x40": "nn3x40_scr.nnd", "blowing4x40": "nn4x40_qp22.nnd"}
+
+
+class NnNet:
+    """A generic net: the fme_nn_net descriptor fields plus float64 parameters in
+    fme_load_nn_net order (include/fme.h)."""
+
+    def __init__(self, precision, widths, embedding, out_act, carry_hidden, params):
+        self.precision = int(precision)
+        self.widths = [int(w) for w in widths]
+        self.embedding = int(embedding)
+        self.out_act = int(out_act)
+        self.carry_hidden = int(carry_hidden)
+        self.params = np.ascontiguousarray(params, dtype=np.float64)
+        if self.params.size != param_count(self):
+            raise ValueError(f"{self.params.size} parameters, descriptor needs {param_count(self)}")
+
+    @property
+    def n_hidden(self):
+        return len(self.widths)
+
+    def desc_struct(self):
+        from .abi import NnNetStruct
+        w = (self.widths + [0] * 4)[:4]
+        return NnNetStruct(self.precision, self.n_hidden, (C_INT4)(*w), self.embedding, self.out_act,
+                           self.carry_hidden, 0)
+
+    def with_carry(self, carry_hidden):
+        return NnNet(self.precision, self.widths, self.embedding, self.out_act, carry_hidden, self.params)
+
+    def __repr__(self):
+        return (f"NnNet({'f64' if self.precision else 'f32'}, {self.widths}, emb={self.embedding}, "
+                f"out_act={self.out_act}, carry=0b{self.carry_hidden:b})")
+
+
+def _c_int4():
+    import ctypes
+    return ctypes.c_int32 * 4
+
+
+C_INT4 = _c_int4()
+
+
+def param_count(net):
+    n = 64 if net.embedding else 0
+    fan = 17 if net.embedding else 9
+    for w in net.widths:
+        n += w * fan + 3 * w
+        fan = w
+    return n + 49 * fan + 49 + 27
+
+
+def load_net(name_or_path):
+    """Read an .nnd blob (tools/convert_deep_weights.py)."""
+    path = name_or_path
+    if not os.path.exists(path):
+        path = os.path.join(WEIGHTS_DIR, NET_FILES.get(name_or_path, name_or_path))
+    raw = open(path, "rb").read()
+    if raw[:8] != b"FMENND01":
+        raise ValueError(f"{path}: not an FMENND01 blob")
+    hdr = np.frombuffer(raw, dtype="<i4", count=12, offset=8)
+    prec, nh = int(hdr[0]), int(hdr[1])
+    widths = [int(v) for v in hdr[2:2 + nh]]
+    emb, out_act, carry, count = int(hdr[6]), int(hdr[7]), int(hdr[8]) & 0xFFFFFFFF, int(hdr[10])
+    params = np.frombuffer(raw, dtype="<f8", count=count, offset=56)
+    return NnNet(prec, widths, emb, out_act, carry, params)
+
+
+def master_net(qp=22):
+    """The shipped 2-layer master net (nn2_qp<QP>) in the generic layout: the generic path must
+    reproduce nn_mode 1 bit for bit with it."""
+    blob = np.fromfile(os.path.join(WEIGHTS_DIR, f"nn2_qp{weight_set_for_qp(qp)}.bin"), dtype="<f8")
+    t = {}
+    o = 0
+    for name, shape in LAYOUT:
+        n = int(np.prod(shape))
+        t[name] = blob[o:o + n]
+        o += n
+    params = np.concatenate([
+        t["embs0"], t["embs1"],
+        t["in_h1"], t["b1"], t["BN_gamma_1"], t["BN_beta_1"],
+        t["h1_h2"], t["b2"], t["BN_gamma_2"], t["BN_beta_2"],
+        t["h2_out"], t["bout"], t["BN_gamma_in"], t["mean"], t["stdev"]])
+    return NnNet(F32, [22, 20], EMB_MASTER, OUT_LINEAR, 0, params)
+
+
+def case_net(name):
+    """Nets named by fixtures and bench workloads: an .nnd blob (NET_FILES key), "<name>+rezero" =
+    that net with carry_hidden cleared, "master" = the shipped QP22 2-layer net, generic layout."""
+    if name == "master":
+        return master_net(22)
+    base, _, mod = str(name).partition("+")
+    net = load_net(base)
+    return net.with_carry(0) if mod == "rezero" else net

@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define FME_ABI_VERSION 3
+#define FME_ABI_VERSION 4
 
 /* ---- error codes ---------------------------------------------------------------- */
 #define FME_OK            0
@@ -49,7 +49,8 @@ typedef struct fme_config {
   int32_t bit_depth;        /* internal luma bit depth; only 8 is supported              */
   int32_t use_hadamard;     /* HadamardME (TAppEncCfg.cpp:760): SATD vs SAD in FracDIF   */
   int32_t nn_mode;          /* 0: standard FracDIF MV (TEncSearch.cpp:4587-4588 variant)
-                               1: NN_pred() MV (shipped behaviour, TEncSearch.cpp:4590-4591) */
+                               1: NN_pred() MV (shipped behaviour, TEncSearch.cpp:4590-4591)
+                               2: the same with a generic net (fme_load_nn_net, configs[4]) */
   int32_t qp;               /* base QP (-q); selects the weight set like TEncSearch::init
                                (TEncSearch.cpp:472/625/775/925: 27, 32, 37, else 22)     */
   int32_t fast_inter_mode;  /* FEN (TAppEncCfg.cpp:888): 1 or 3 -> even-row SAD for the
@@ -160,6 +161,58 @@ int fme_set_keys(fme_ctx* ctx, const int16_t* keys, size_t count, void* stream);
  * (20 each), bout[49], BN_gamma_in, mean, stdev (9 each) — FME_NN_PARAMS floats.
  * fme_create() loads nothing; the host mirror loads the per-QP set (weights/nn2_qp<QP>.bin).     */
 int fme_load_nn_weights(fme_ctx* ctx, const float* params, int count);
+/* ---- generic (deeper) NN_pred nets: BASELINE.json configs[4] ------------------------------- *
+ * nn_mode 2 runs a net loaded with fme_load_nn_net in NN_pred()'s place, with the same inputs
+ * (array_e slots, C, PUHeight, PUWidth carried across calls exactly as in nn_mode 1) and the same
+ * class -> MV offset switch.  The shape follows the reference's deeper nets:
+ *   Backups/4 "SCR 3 layers" (9 -> 40 -> 40 -> 40 -> 49, double, sigmoid output,
+ *     TEncSearch - SCR 3 layers - no normalization.cpp:57-299, forward :4427-4480),
+ *   Backups/15 "blowing 4 lyrs qp 22" (17 -> 4 x 40 -> 49, float, H-embedding rows 12->3, 16->4,
+ *     TEncSearch - blowing - 4 lyrs qp 22.cpp:57-75, 849-1160, forward :4954-5052),
+ *   and the master net itself (17 -> 22 -> 20 -> 49, float).
+ * Per call: x = ((double|float)raw - mean) / stdev * gamma_in for raw = e0,e1,e2,e3,C,e4,e5,e6,e7;
+ * IN = [emb0[rowH] | emb1[rowW] | x] (embedding != NONE) or x; per hidden layer
+ * X[i] = relu(sum_k W[i][k] * IN[k] + b[i]) * gamma[i] + beta[i], summed k = 0.. in order with a
+ * separate rounding per product and per add (no FMA), starting from 0 - or, for a layer whose bit
+ * is set in carry_hidden, from that layer's X of the previous call (Backups/15 never re-zeroes X3,
+ * X4: :4957-4961); OUT = Wout * X + bout, then sigmoid with out_act; class = first maximum.
+ * Parameters (double, fme_nn_param_count of them), in this order:
+ *   [embs0[8][4], embs1[8][4]]            (embedding != NONE)
+ *   per hidden layer l: W_l[width_l][in_l], b_l, gamma_l, beta_l   (in_0 = 17 or 9)
+ *   Wout[49][width_last], bout[49], gamma_in[9], mean[9], stdev[9]
+ * A float net takes each value as (float)value, like the reference's float initialisers.         */
+#define FME_NN_MAX_HIDDEN  4
+#define FME_NN_MAX_WIDTH   40
+#define FME_NN_F32         0
+#define FME_NN_F64         1
+#define FME_NN_EMB_NONE    0   /* 9 inputs, no PU-size embeddings                             */
+#define FME_NN_EMB_MASTER  1   /* rows by H 4,8,16,12,24,32,64 -> 1..7 (TEncSearch.cpp:93-102) */
+#define FME_NN_EMB_SWAP    2   /* rows by H 4,8,12,16,24,32,64 -> 1..7 (Backups/15:4979-4988)  */
+#define FME_NN_OUT_LINEAR  0
+#define FME_NN_OUT_SIGMOID 1   /* 1 / (1 + exp(-x)) before the argmax (Backups/4:297-299)      */
+#define FME_NN_ENGINE_EXACT 0  /* one lane per job, the reference's arithmetic bit for bit      */
+#define FME_NN_ENGINE_MFMA  1  /* batched GEMM on v_mfma_{f32_16x16x4_f32,f64_16x16x4_f64}: a
+                                  k-ordered FMA chain, so classes may differ on near-ties       */
+
+typedef struct fme_nn_net {
+  int32_t  precision;                   /* FME_NN_F32 / FME_NN_F64                              */
+  int32_t  n_hidden;                    /* 1..FME_NN_MAX_HIDDEN                                 */
+  int32_t  width[FME_NN_MAX_HIDDEN];    /* 1..FME_NN_MAX_WIDTH each (unused entries 0)          */
+  int32_t  embedding;                   /* FME_NN_EMB_*                                          */
+  int32_t  out_act;                     /* FME_NN_OUT_*                                          */
+  uint32_t carry_hidden;                /* bit l: hidden layer l starts from the previous call's */
+  int32_t  reserved;
+} fme_nn_net;   /* 40 bytes */
+
+/* Number of parameters of `net`, or a negative FME_E_* code for an invalid descriptor. */
+int fme_nn_param_count(const fme_nn_net* net);
+int fme_load_nn_net(fme_ctx* ctx, const fme_nn_net* net, const double* params, int count);
+/* FME_NN_ENGINE_EXACT (default) or FME_NN_ENGINE_MFMA for nn_mode 2. */
+int fme_set_nn_engine(fme_ctx* ctx, int engine);
+/* Optional diagnostic output of nn_mode 2: a device array of n floats that each later batch fills
+ * with top-1 minus top-2 of OUT (after the output activation) per job; NULL turns it off. */
+int fme_set_nn_margin_output(fme_ctx* ctx, float* d_margin);
+
 /* Forget the array_e/C/PUHeight/PUWidth state carried across calls (process start). */
 int fme_nn_reset_state(fme_ctx* ctx);
 /* The carried state as 12 words: array_e slots[8], C, PUHeight, PUWidth, and a written mask

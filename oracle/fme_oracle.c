@@ -348,6 +348,116 @@ int orc_nn_forward(const float* P, const uint32_t e[8], uint32_t c, int pu_h, in
   return best;
 }
 
+/* ---- generic nets (nn_mode 2) -------------------------------------------------------------
+ * The reference's deeper nets, restated literally:
+ *   Backups/4 "SCR 3 layers" (double): IN[k] = (U - mean) / stdev (:4427-4435), IN_norm = IN *
+ *     BN_gamma_in (:4439-4441), X_l[i] += w * x for j in order from the memset 0 (:4445-4470),
+ *     += b, relu * gamma + beta, OUT[i] += w * X3[j], += bout, sigmoid (:4472-4480),
+ *     std::max_element (:4486);
+ *   Backups/15 "blowing 4 lyrs qp 22" (float): the same per layer (:5007-5045) with embeddings
+ *     (:4979-5000), no sigmoid, and X3 / X4 left out of the per-call memset (:4957-4961), so they
+ *     start from the previous call's values.
+ * relu is `x > 0 ? x : 0` (Backups/4:292-295, Backups/15:80-83). */
+int orc_nn_param_count(const fme_nn_net* d) {
+  if (!d || d->n_hidden < 1 || d->n_hidden > FME_NN_MAX_HIDDEN) return FME_E_INVALID;
+  if (d->precision != FME_NN_F32 && d->precision != FME_NN_F64) return FME_E_INVALID;
+  if (d->embedding < FME_NN_EMB_NONE || d->embedding > FME_NN_EMB_SWAP) return FME_E_INVALID;
+  if (d->out_act != FME_NN_OUT_LINEAR && d->out_act != FME_NN_OUT_SIGMOID) return FME_E_INVALID;
+  if (d->carry_hidden >> d->n_hidden) return FME_E_INVALID;
+  int n = d->embedding ? 64 : 0, in = d->embedding ? 17 : 9;
+  for (int l = 0; l < d->n_hidden; l++) {
+    const int w = d->width[l];
+    if (w < 1 || w > FME_NN_MAX_WIDTH) return FME_E_INVALID;
+    n += w * in + 3 * w;
+    in = w;
+  }
+  return n + 49 * in + 49 + 27;
+}
+
+int orc_load_nn_net(orc_ctx* ctx, const fme_nn_net* d, const double* params, int count) {
+  const int n = orc_nn_param_count(d);
+  if (n < 0 || n != count || n > ORC_NN_NET_MAX_PARAMS) return FME_E_INVALID;
+  ctx->net.d = *d;
+  ctx->net.count = n;
+  for (int i = 0; i < n; i++) {
+    ctx->net.pd[i] = params[i];
+    ctx->net.pf[i] = (float)params[i];
+  }
+  memset(ctx->net.carry_d, 0, sizeof(ctx->net.carry_d));
+  memset(ctx->net.carry_f, 0, sizeof(ctx->net.carry_f));
+  ctx->net.loaded = 1;
+  return 0;
+}
+
+#define ORC_RELU(x) ((x) > 0 ? (x) : 0)
+#define ORC_DEEP_FORWARD(NAME, T, EXPF)                                                          \
+  static int NAME(const fme_nn_net* d, const T* P, T carry[][FME_NN_MAX_WIDTH], const uint32_t e[8], \
+                  uint32_t c, int pu_h, int pu_w, double* logits) {                               \
+    T in[17], xa[FME_NN_MAX_WIDTH], xb[FME_NN_MAX_WIDTH], out[49];                                \
+    const T* p = P;                                                                               \
+    int nin = 0;                                                                                  \
+    if (d->embedding) {                                                                           \
+      const int rh = d->embedding == FME_NN_EMB_SWAP ? emb_row_w(pu_h) : emb_row_h(pu_h);         \
+      const int rw = emb_row_w(pu_w);                                                             \
+      for (int k = 0; k < 4; k++) {                                                               \
+        in[k] = p[rh * 4 + k];                                                                    \
+        in[4 + k] = p[32 + rw * 4 + k];                                                           \
+      }                                                                                           \
+      p += 64;                                                                                    \
+      nin = 8;                                                                                    \
+    }                                                                                             \
+    const T* tail = P + orc_nn_param_count(d) - 27;                                               \
+    const uint32_t raw[9] = {e[0], e[1], e[2], e[3], c, e[4], e[5], e[6], e[7]};                  \
+    for (int k = 0; k < 9; k++) {                                                                 \
+      T v = (T)raw[k];                                                                            \
+      v = (v - tail[9 + k]) / tail[18 + k];                                                       \
+      in[nin + k] = v * tail[k];                                                                  \
+    }                                                                                             \
+    nin += 9;                                                                                     \
+    const T* x = in;                                                                              \
+    T* y = xa;                                                                                    \
+    for (int l = 0; l < d->n_hidden; l++) {                                                       \
+      const int w = d->width[l];                                                                  \
+      const T *W = p, *b = p + w * nin, *g = b + w, *be = g + w;                                  \
+      const int carried = (d->carry_hidden >> l) & 1;                                             \
+      for (int i = 0; i < w; i++) {                                                               \
+        T s = carried ? carry[l][i] : (T)0;                                                       \
+        for (int k = 0; k < nin; k++) s = s + W[i * nin + k] * x[k];                              \
+        s = s + b[i];                                                                             \
+        s = ORC_RELU(s) * g[i] + be[i];                                                           \
+        y[i] = s;                                                                                 \
+        if (carried) carry[l][i] = s;                                                             \
+      }                                                                                           \
+      p = be + w;                                                                                 \
+      x = y;                                                                                      \
+      y = (y == xa) ? xb : xa;                                                                    \
+      nin = w;                                                                                    \
+    }                                                                                             \
+    for (int i = 0; i < 49; i++) {                                                                \
+      T s = 0;                                                                                    \
+      for (int k = 0; k < nin; k++) s = s + p[i * nin + k] * x[k];                                \
+      s = s + p[49 * nin + i];                                                                    \
+      if (d->out_act == FME_NN_OUT_SIGMOID) s = (T)1 / ((T)1 + EXPF(-s));                         \
+      out[i] = s;                                                                                 \
+    }                                                                                             \
+    int best = 0;                                                                                 \
+    for (int i = 1; i < 49; i++)                                                                  \
+      if (out[best] < out[i]) best = i;                                                           \
+    if (logits)                                                                                   \
+      for (int i = 0; i < 49; i++) logits[i] = (double)out[i];                                    \
+    return best;                                                                                  \
+  }
+ORC_DEEP_FORWARD(deep_forward_f32, float, expf)
+ORC_DEEP_FORWARD(deep_forward_f64, double, exp)
+
+int orc_nn_net_forward(orc_ctx* ctx, const uint32_t e[8], uint32_t c, int pu_h, int pu_w,
+                       double* logits) {
+  if (!ctx->net.loaded) return FME_E_STATE;
+  if (ctx->net.d.precision == FME_NN_F64)
+    return deep_forward_f64(&ctx->net.d, ctx->net.pd, ctx->net.carry_d, e, c, pu_h, pu_w, logits);
+  return deep_forward_f32(&ctx->net.d, ctx->net.pf, ctx->net.carry_f, e, c, pu_h, pu_w, logits);
+}
+
 /* ---- context -------------------------------------------------------------------------- */
 size_t orc_ctx_size(void) { return sizeof(orc_ctx); }
 
@@ -375,7 +485,11 @@ void orc_load_nn(orc_ctx* ctx, const float* params) {
   memcpy(ctx->nn, params, sizeof(ctx->nn));
   ctx->nn_loaded = 1;
 }
-void orc_nn_reset(orc_ctx* ctx) { memset(&ctx->nn_state, 0, sizeof(ctx->nn_state)); }
+void orc_nn_reset(orc_ctx* ctx) {
+  memset(&ctx->nn_state, 0, sizeof(ctx->nn_state));
+  memset(ctx->net.carry_d, 0, sizeof(ctx->net.carry_d));
+  memset(ctx->net.carry_f, 0, sizeof(ctx->net.carry_f));
+}
 /* 12-word layout of fme_nn_get_state: slots[8], C, PUHeight, PUWidth, written mask. */
 void orc_nn_get_state(const orc_ctx* ctx, uint32_t out[12]) {
   memcpy(out, ctx->nn_state.slot, 8 * sizeof(uint32_t));
@@ -399,6 +513,7 @@ static int valid_size(int w, int h) {
 
 /* xMotionEstimation sub-pel part for each job in order (TEncSearch.cpp:4529-4597). */
 int orc_refine(orc_ctx* ctx, const fme_job* jobs, fme_result* res, int n) {
+  if (ctx->cfg.nn_mode == 2 && !ctx->net.loaded) return FME_E_STATE;
   int16_t* key = (int16_t*)malloc(sizeof(int16_t) * 64 * 64);
   for (int i = 0; i < n; i++) {
     const fme_job* j = &jobs[i];
@@ -446,7 +561,9 @@ int orc_refine(orc_ctx* ctx, const fme_job* jobs, fme_result* res, int n) {
     int offx, offy;
     if (ctx->cfg.nn_mode) {
       const orc_nn_state* st = &ctx->nn_state;
-      int cls = orc_nn_forward(ctx->nn, st->slot, st->c, (int)st->pu_h, (int)st->pu_w, NULL);
+      int cls = ctx->cfg.nn_mode == 2
+                    ? orc_nn_net_forward(ctx, st->slot, st->c, (int)st->pu_h, (int)st->pu_w, NULL)
+                    : orc_nn_forward(ctx->nn, st->slot, st->c, (int)st->pu_h, (int)st->pu_w, NULL);
       r->nn_class = (uint8_t)cls;
       if (n_emi < 8 || !(j->flags & FME_JOB_EMI)) r->status |= FME_RES_NN_STALE;
       if ((st->written & 0x1FFu) != 0x1FFu) r->status |= FME_RES_NN_UNINIT;

@@ -39,6 +39,18 @@ typedef struct orc_nn_state {
   uint32_t written;   /* bit s: slot s written since reset; bit 8: C/PU size written */
 } orc_nn_state;
 
+/* A generic NN_pred net (nn_mode 2, fme_load_nn_net): descriptor, parameters in the net's own
+ * precision, and the hidden layers a carry_hidden net keeps between calls. */
+#define ORC_NN_NET_MAX_PARAMS 8060
+typedef struct orc_nn_net {
+  fme_nn_net d;
+  int loaded, count;
+  double pd[ORC_NN_NET_MAX_PARAMS];
+  float pf[ORC_NN_NET_MAX_PARAMS];
+  double carry_d[FME_NN_MAX_HIDDEN][FME_NN_MAX_WIDTH];
+  float carry_f[FME_NN_MAX_HIDDEN][FME_NN_MAX_WIDTH];
+} orc_nn_net;
+
 typedef struct orc_ctx {
   fme_config cfg;
   orc_picture pics[FME_MAX_PICTURES];
@@ -48,6 +60,7 @@ typedef struct orc_ctx {
   float nn[FME_NN_PARAMS];
   int nn_loaded;
   orc_nn_state nn_state;
+  orc_nn_net net;
   int16_t int_mv_2n[FME_MAX_REFS][2];   /* m_integerMv2Nx2N[REF_PIC_LIST_0] (TEncSearch.h:118) */
 } orc_ctx;
 
@@ -82,6 +95,14 @@ int orc_emi_push_count(int sx, int sy, int lt_x, int lt_y, int rb_x, int rb_y);
 /* NN_pred() forward on explicit inputs; returns class 0..48 (TEncSearch.cpp:85-134). */
 int orc_nn_forward(const float* params, const uint32_t e[8], uint32_t c, int pu_h, int pu_w,
                    float* logits /* 49, may be NULL */);
+
+/* Generic nets (nn_mode 2).  orc_nn_net_forward runs one NN_pred() call on explicit inputs
+ * (updating the carried hidden layers of a carry_hidden net) and returns the class; logits
+ * (49, may be NULL) receive OUT after the output activation, as double. */
+int orc_nn_param_count(const fme_nn_net* d);
+int orc_load_nn_net(orc_ctx* ctx, const fme_nn_net* d, const double* params, int count);
+int orc_nn_net_forward(orc_ctx* ctx, const uint32_t e[8], uint32_t c, int pu_h, int pu_w,
+                       double* logits);
 
 /* context helpers */
 void orc_init(orc_ctx* ctx, const fme_config* cfg);

@@ -57,7 +57,7 @@ def edge_jobs(rng, width, height, n):
     return j
 
 
-def build_case(name, seed, width, height, n_jobs, hadme, fen, nn_mode, qp, bipred=0.15, n_edge=96):
+def build_case(name, seed, width, height, n_jobs, hadme, fen, nn_mode, qp, bipred=0.15, n_edge=96, net=None):
     rng = np.random.default_rng(seed)
     pics = {i: synth.synth_luma(width, height, i, seed=seed) for i in range(5)}
     lambdas = np.array(synth.LDP_LAMBDA[qp if qp in synth.LDP_LAMBDA else 22], dtype=np.float64)
@@ -77,6 +77,8 @@ def build_case(name, seed, width, height, n_jobs, hadme, fen, nn_mode, qp, bipre
             eng.set_lambda(lid, float(lam))
         eng.set_keys(keys if keys.size else np.zeros(1, np.int16))
         eng.load_nn(wts)
+        if net is not None:
+            eng.load_nn_net(weights.case_net(net))
     r_ref = ref.refine(jobs)
     r_orc = orc.refine(jobs)
     bad, first, counts = compare_results(r_ref, r_orc)
@@ -91,6 +93,7 @@ def build_case(name, seed, width, height, n_jobs, hadme, fen, nn_mode, qp, bipre
         jobs=jobs,
         results=r_ref,
         config=np.array([hadme, fen, nn_mode, qp], dtype=np.int32),
+        **({"net": np.array(net)} if net is not None else {}),
     )
     print(f"{path}: {len(jobs)} jobs, {int((jobs['flags'] & JOB_BIPRED != 0).sum())} bi-pred, "
           f"{int((r_ref['n_emi'] < 8).sum())} with < 8 EMI pushes")
@@ -202,8 +205,24 @@ CASES = [
 ]
 
 
+# nn_mode 2: the reference's deeper nets (BASELINE.json configs[4]) and the master net through the
+# generic path.  nn4x40 runs with its X3/X4 carry cleared ("+rezero"): the batch engines do not run
+# carried hidden layers (fme_load_nn_net rejects carry_hidden); the oracle and _ref cover both.
+DEEP_CASES = [
+    ("deep_scr3x40_qp22", 16, 160, 96, 900, 1, 1, 2, 22, 0.15, 96, "scr3x40"),
+    ("deep_blowing4x40_qp22", 17, 128, 96, 600, 1, 1, 2, 22, 0.15, 96, "blowing4x40+rezero"),
+    ("deep_master_qp22", 11, 160, 96, 1200, 1, 1, 2, 22, 0.15, 96, "master"),
+]
+
+
 def main():
     os.makedirs(OUT, exist_ok=True)
+    if "--deep-only" in sys.argv:
+        for c in DEEP_CASES:
+            build_case(*c)
+        return 0
+    for c in DEEP_CASES:
+        build_case(*c)
     if "--mc-only" not in sys.argv and "--tz-only" not in sys.argv:
         for c in CASES:
             build_case(*c)

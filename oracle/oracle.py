@@ -69,6 +69,12 @@ class Oracle:
         lib.orc_pred_inter_reset.argtypes = [_P]
         lib.orc_mc.restype = C.c_int
         lib.orc_mc.argtypes = [_P, _P, C.c_int, _P, C.c_int, _P, _P, C.c_int, C.c_int, C.c_int]
+        lib.orc_nn_param_count.restype = C.c_int
+        lib.orc_nn_param_count.argtypes = [_P]
+        lib.orc_load_nn_net.restype = C.c_int
+        lib.orc_load_nn_net.argtypes = [_P, _P, _P, C.c_int]
+        lib.orc_nn_net_forward.restype = C.c_int
+        lib.orc_nn_net_forward.argtypes = [_P, _P, C.c_uint32, C.c_int, C.c_int, _P]
         self._buf = C.create_string_buffer(lib.orc_ctx_size())
         self.ctx = C.cast(self._buf, C.c_void_p)
         cfg = _ConfigStruct(8, use_hadamard, nn_mode, qp, fast_inter_mode, 0)
@@ -94,6 +100,24 @@ class Oracle:
 
     def nn_reset(self):
         self.lib.orc_nn_reset(self.ctx)
+
+    def load_nn_net(self, net):
+        """net: nnfme.weights.NnNet (descriptor + float64 parameters), nn_mode 2."""
+        d = net.desc_struct()
+        p = np.ascontiguousarray(net.params, dtype=np.float64)
+        self._keep["net"] = (d, p)
+        rc = self.lib.orc_load_nn_net(self.ctx, C.byref(d), _ptr(p), p.size)
+        if rc != 0:
+            raise RuntimeError(f"orc_load_nn_net failed: {rc}")
+
+    def nn_net_forward(self, e, c, h, w):
+        """One NN_pred() call of the loaded generic net: (class, OUT[49] as float64)."""
+        e = np.ascontiguousarray(e, dtype=np.uint32)
+        logits = np.zeros(49, np.float64)
+        cls = self.lib.orc_nn_net_forward(self.ctx, _ptr(e), int(c), int(h), int(w), _ptr(logits))
+        if cls < 0:
+            raise RuntimeError(f"orc_nn_net_forward failed: {cls}")
+        return cls, logits
 
     def nn_get_state(self):
         out = np.zeros(12, np.uint32)
@@ -188,7 +212,11 @@ class Reference:
         lib.ref_nn_reset.argtypes = [_P]
         lib.ref_nn_class.restype = C.c_int
         lib.ref_nn_class.argtypes = [_P, _P, C.c_uint32, C.c_int, C.c_int]
+        lib.ref_pred_block.restype = C.c_int
         lib.ref_pred_block.argtypes = [_P] + [C.c_int] * 7 + [_P]
+        lib.ref_load_nn_net.argtypes = [_P, _P, _P, C.c_int]
+        lib.ref_nn_net_class.restype = C.c_int
+        lib.ref_nn_net_class.argtypes = [_P, _P, C.c_uint32, C.c_int, C.c_int, _P]
         lib.ref_satd.restype = C.c_uint32
         lib.ref_satd.argtypes = [_P, _P, C.c_int, _P, C.c_int, C.c_int, C.c_int, C.c_int]
         lib.ref_refine.restype = C.c_int
@@ -239,7 +267,10 @@ class Reference:
 
     def template_cost(self, org_id, ref_id, x, y, w, h, cu_x, cu_y, mvx, mvy, bits, lambda_id):
         """xGetTemplateCost over the reference's TComInterpolationFilter / TComRdCost."""
-        return self.lib.ref_template_cost(self.h, org_id, ref_id, x, y, w, h, cu_x, cu_y, mvx, mvy, bits, lambda_id)
+        v = self.lib.ref_template_cost(self.h, org_id, ref_id, x, y, w, h, cu_x, cu_y, mvx, mvy, bits, lambda_id)
+        if v == 0xFFFFFFFF:
+            raise RuntimeError("ref_template_cost: unset picture or bad slot")
+        return v
 
     def set_keys(self, keys):
         keys = np.ascontiguousarray(keys, dtype=np.int16)
@@ -252,13 +283,24 @@ class Reference:
     def nn_reset(self):
         self.lib.ref_nn_reset(self.h)
 
+    def load_nn_net(self, net):
+        d = net.desc_struct()
+        p = np.ascontiguousarray(net.params, dtype=np.float64)
+        self.lib.ref_load_nn_net(self.h, C.byref(d), _ptr(p), p.size)
+
+    def nn_net_class(self, e, c, h, w):
+        e = np.ascontiguousarray(e, dtype=np.uint32)
+        logits = np.zeros(49, np.float64)
+        return self.lib.ref_nn_net_class(self.h, _ptr(e), int(c), int(h), int(w), _ptr(logits)), logits
+
     def nn_class(self, e, c, h, w):
         e = np.ascontiguousarray(e, dtype=np.uint32)
         return self.lib.ref_nn_class(self.h, _ptr(e), int(c), int(h), int(w))
 
     def pred_block(self, pid, x0, y0, w, h, qx, qy):
         out = np.zeros((h, w), dtype=np.int16)
-        self.lib.ref_pred_block(self.h, pid, x0, y0, w, h, qx, qy, _ptr(out))
+        if self.lib.ref_pred_block(self.h, pid, x0, y0, w, h, qx, qy, _ptr(out)) != 0:
+            raise RuntimeError("ref_pred_block: unset picture or bad size")
         return out
 
     def satd(self, org, cur, hadamard=True):

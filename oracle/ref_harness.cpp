@@ -193,8 +193,94 @@ struct Pic {
   bool set420 = false;
 };
 
+// A generic NN_pred net (nn_mode 2) restated in the style of the reference's backups: global-like
+// activation arrays X[l][40], memset per call except the carried layers (Backups/15:4957-4961),
+// `X[i] += w * x` in j order, `+= b`, relu * gamma + beta, OUT += w * X, += bout, [sigmoid],
+// std::max_element (Backups/4:4437-4486, Backups/15:4954-5052).  Independent of fme_oracle.c's
+// forward (which walks a parameter pointer); both take the parameters in fme_load_nn_net order.
+struct DeepNet {
+  fme_nn_net d{};
+  std::vector<double> p;
+  double Xd[FME_NN_MAX_HIDDEN][FME_NN_MAX_WIDTH] = {};
+  float Xf[FME_NN_MAX_HIDDEN][FME_NN_MAX_WIDTH] = {};
+
+  template <typename T>
+  int run(T X[][FME_NN_MAX_WIDTH], const uint32_t* e, uint32_t C, int H, int W, double* logits) {
+    auto rowMaster = [](int v) { switch (v) { case 4: return 1; case 8: return 2; case 16: return 3; case 12: return 4; case 24: return 5; case 32: return 6; case 64: return 7; default: return 0; } };
+    auto rowW = [](int v) { switch (v) { case 4: return 1; case 8: return 2; case 12: return 3; case 16: return 4; case 24: return 5; case 32: return 6; case 64: return 7; default: return 0; } };
+    const bool emb = d.embedding != FME_NN_EMB_NONE;
+    // offsets of every tensor
+    size_t o = emb ? 64 : 0;
+    size_t wOff[FME_NN_MAX_HIDDEN], bOff[FME_NN_MAX_HIDDEN], gOff[FME_NN_MAX_HIDDEN], beOff[FME_NN_MAX_HIDDEN];
+    int nin = emb ? 17 : 9;
+    int fan[FME_NN_MAX_HIDDEN + 1];
+    for (int l = 0; l < d.n_hidden; l++) {
+      fan[l] = nin;
+      wOff[l] = o; o += (size_t)d.width[l] * nin;
+      bOff[l] = o; o += d.width[l];
+      gOff[l] = o; o += d.width[l];
+      beOff[l] = o; o += d.width[l];
+      nin = d.width[l];
+    }
+    fan[d.n_hidden] = nin;
+    const size_t outW = o, outB = o + 49 * (size_t)nin, gin = outB + 49, mean = gin + 9, sd = mean + 9;
+    auto P = [&](size_t i) { return (T)p[i]; };
+    T IN[17] = {};
+    const uint32_t errs[9] = {e[0], e[1], e[2], e[3], C, e[4], e[5], e[6], e[7]};
+    const int base = emb ? 8 : 0;
+    for (int i = 0; i < 9; i++) {
+      T v = (T)errs[i];
+      IN[base + i] = (v - P(mean + i)) / P(sd + i);
+    }
+    if (emb) {
+      const int rh = d.embedding == FME_NN_EMB_SWAP ? rowW(H) : rowMaster(H);
+      for (int k = 0; k < 4; k++) {
+        IN[k] = P(rh * 4 + k);
+        IN[4 + k] = P(32 + rowW(W) * 4 + k);
+      }
+    }
+    for (int i = 0; i < 9; i++) IN[base + i] = IN[base + i] * P(gin + i);
+    for (int l = 0; l < d.n_hidden; l++)
+      if (!((d.carry_hidden >> l) & 1)) std::memset(X[l], 0, sizeof(X[l]));
+    for (int l = 0; l < d.n_hidden; l++) {
+      const T* src = l == 0 ? IN : X[l - 1];
+      for (int i = 0; i < d.width[l]; i++) {
+        for (int j = 0; j < fan[l]; j++) {
+          volatile T prod = P(wOff[l] + (size_t)i * fan[l] + j) * src[j];
+          X[l][i] += prod;
+        }
+        X[l][i] += P(bOff[l] + i);
+        const T r = X[l][i] > 0 ? X[l][i] : (T)0;
+        volatile T m = r * P(gOff[l] + i);
+        X[l][i] = m + P(beOff[l] + i);
+      }
+    }
+    T OUT[49] = {};
+    const T* last = X[d.n_hidden - 1];
+    for (int i = 0; i < 49; i++) {
+      for (int j = 0; j < nin; j++) {
+        volatile T prod = P(outW + (size_t)i * nin + j) * last[j];
+        OUT[i] += prod;
+      }
+      OUT[i] += P(outB + i);
+      if (d.out_act == FME_NN_OUT_SIGMOID) OUT[i] = (T)1 / ((T)1 + std::exp(-OUT[i]));
+    }
+    if (logits)
+      for (int i = 0; i < 49; i++) logits[i] = (double)OUT[i];
+    return (int)std::distance(OUT, std::max_element(OUT, OUT + 49));
+  }
+  int forward(const uint32_t* e, uint32_t C, int H, int W, double* logits) {
+    return d.precision == FME_NN_F64 ? run<double>(Xd, e, C, H, W, logits) : run<float>(Xf, e, C, H, W, logits);
+  }
+  void reset() {
+    std::memset(Xd, 0, sizeof(Xd));
+    std::memset(Xf, 0, sizeof(Xf));
+  }
+};
+
 struct RefCtx {
   RefSearch s;
+  DeepNet net;
   Pic pics[FME_MAX_PICTURES];
   double lambda[FME_MAX_LAMBDAS] = {0};
   std::vector<int16_t> keys;
@@ -293,6 +379,19 @@ void ref_nn_reset(void* h) {
   RefCtx* c = static_cast<RefCtx*>(h);
   std::memset(c->slot, 0, sizeof(c->slot));
   c->C = c->puh = c->puw = 0;
+  c->net.reset();
+}
+
+void ref_load_nn_net(void* h, const fme_nn_net* d, const double* p, int count) {
+  RefCtx* c = static_cast<RefCtx*>(h);
+  c->net.d = *d;
+  c->net.p.assign(p, p + count);
+  c->net.reset();
+}
+
+// One NN_pred() call of the generic net on explicit inputs (updates carried layers).
+int ref_nn_net_class(void* h, const uint32_t* e, uint32_t cc, int H, int W, double* logits) {
+  return static_cast<RefCtx*>(h)->net.forward(e, cc, H, W, logits);
 }
 
 int ref_nn_class(void* h, const uint32_t* e, uint32_t cc, int H, int W) {
@@ -301,8 +400,10 @@ int ref_nn_class(void* h, const uint32_t* e, uint32_t cc, int H, int W) {
 
 // Interpolate one PU at quarter-pel (qx,qy) through the reference filter classes
 // (TComPrediction::xPredInterBlk order, TComPrediction.cpp:643-683).
-void ref_pred_block(void* h, int id, int x0, int y0, int w, int hgt, int qx, int qy, int16_t* out) {
+int ref_pred_block(void* h, int id, int x0, int y0, int w, int hgt, int qx, int qy, int16_t* out) {
   RefCtx* c = static_cast<RefCtx*>(h);
+  if (id < 0 || id >= FME_MAX_PICTURES || !c->pics[id].set || w < 1 || w > 64 || hgt < 1 || hgt > 64)
+    return FME_E_STATE;
   TComPicYuv& pic = c->pics[id].yuv;
   const int stride = pic.getStride(COMPONENT_Y);
   Pel* src = pic.getAddr(COMPONENT_Y) + (y0 + (qy >> 2)) * stride + x0 + (qx >> 2);
@@ -318,6 +419,7 @@ void ref_pred_block(void* h, int id, int x0, int y0, int w, int hgt, int qx, int
     f.filterVer(COMPONENT_Y, tmp.data() + 3 * w, w, dst.data(), w, w, hgt, fy, false, true, CHROMA_400, 8);
   }
   for (int i = 0; i < w * hgt; i++) out[i] = dst[i];
+  return 0;
 }
 
 // Distortions through the reference DistParam dispatch.
@@ -405,7 +507,8 @@ int ref_refine(void* h, const fme_job* jobs, fme_result* res, int n) {
     s.rd.setCostScale(0);
     int ox, oy;
     if (c->nn_mode) {
-      int cls = nnClass(c->nn.data(), c->slot, c->C, (int)c->puh, (int)c->puw);
+      int cls = c->nn_mode == 2 ? c->net.forward(c->slot, c->C, (int)c->puh, (int)c->puw, nullptr)
+                                : nnClass(c->nn.data(), c->slot, c->C, (int)c->puh, (int)c->puw);
       r.nn_class = (uint8_t)cls;
       ox = cls % 7 - 3;
       oy = cls / 7 - 3;
@@ -529,6 +632,9 @@ int ref_mc(void* h, const fme_mc_job* jobs, int n, uint8_t* y, int ys, uint8_t* 
 uint32_t ref_template_cost(void* h, int org_id, int ref_id, int x, int y, int w, int hgt, int cu_x, int cu_y,
                            int mvx, int mvy, int bits, int lambda_id) {
   RefCtx* c = static_cast<RefCtx*>(h);
+  if (org_id < 0 || org_id >= FME_MAX_PICTURES || ref_id < 0 || ref_id >= FME_MAX_PICTURES ||
+      !c->pics[org_id].set || !c->pics[ref_id].set || lambda_id < 0 || lambda_id >= FME_MAX_LAMBDAS)
+    return 0xFFFFFFFFu;   // the Python wrapper raises on this sentinel
   TComPicYuv& ref = c->pics[ref_id].yuv;
   TComPicYuv& org = c->pics[org_id].yuv;
   const int W = ref.getWidth(COMPONENT_Y), H = ref.getHeight(COMPONENT_Y);

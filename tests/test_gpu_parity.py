@@ -22,6 +22,8 @@ def _ctx(g, **over):
     from nnfme.runtime import FmeContext
     hadme, fen, nn_mode, qp = (int(v) for v in g["config"])
     kw = dict(use_hadamard=hadme, nn_mode=nn_mode, qp=qp, fast_inter_mode=fen)
+    if "net" in g:
+        kw["net"] = weights.case_net(str(g["net"]))
     kw.update(over)
     ctx = FmeContext(**kw)
     for i, p in enumerate(g["pictures"]):
@@ -150,9 +152,9 @@ def test_nn_pred_single_matches_oracle(qp):
 # ---------------------------------------------------------------------------------------
 # full-size: one 1080p LDP QP22 frame (≈863 K jobs, 4 reference pictures)
 # ---------------------------------------------------------------------------------------
-def nn_host_emulation(jobs, res, params, state=None):
-    """Vectorised restatement of NN_pred's inputs (last writer per array_e slot, in job
-    order) and its float32 forward (sequential-k, no FMA: numpy float32 ops round each step)."""
+def nn_host_inputs(jobs, res):
+    """Vectorised restatement of NN_pred's inputs: the last writer per array_e slot and of C /
+    PUHeight / PUWidth, in job order, from a fresh state (unwritten -> 0)."""
     n = len(jobs)
     emi_job = (jobs["flags"] & JOB_EMI) != 0
     idx = np.arange(n)
@@ -172,6 +174,14 @@ def nn_host_emulation(jobs, res, params, state=None):
     c[ok] = res["c"][src[8][ok]]
     ph[ok] = jobs["h"][src[8][ok]]
     pw[ok] = jobs["w"][src[8][ok]]
+    return e, c, ph, pw
+
+
+def nn_host_emulation(jobs, res, params, state=None):
+    """NN_pred's float32 forward (sequential-k, no FMA: numpy float32 ops round each step) on the
+    inputs of nn_host_inputs."""
+    n = len(jobs)
+    e, c, ph, pw = nn_host_inputs(jobs, res)
     t = weights.unpack(params)
     f32 = np.float32
     rowh = {4: 1, 8: 2, 16: 3, 12: 4, 24: 5, 32: 6, 64: 7}

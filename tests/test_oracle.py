@@ -25,6 +25,8 @@ def _engine(cls, g):
         e.set_lambda(i, float(lam))
     e.set_keys(g["keys"] if g["keys"].size else np.zeros(1, np.int16))
     e.load_nn(weights.load_weights(qp))
+    if "net" in g:
+        e.load_nn_net(weights.case_net(str(g["net"])))
     return e
 
 
