@@ -173,6 +173,14 @@ __device__ __forceinline__ void layer_mfma(T* act, const T* __restrict__ W, cons
         acc[nt] = M::mma(a, bw, acc[nt]);
       }
     }
+    if constexpr (sizeof(T) == 8) {
+      // v_mfma_f64_16x16x4_f64 on gfx950 writes its upper accumulator registers (rows 8..15 of
+      // the tile) later than the compiler's hazard model pads for: measured on the box, those
+      // rows were read stale in every tile but the last (tools/deep_probe.py).  Pad explicitly:
+      // the accumulators are operands of the pad, so no read of them is placed before it.
+#pragma unroll
+      for (int nt = 0; nt < NT; nt++) asm volatile("s_nop 15\n\ts_nop 15" : "+a"(acc[nt]));
+    }
 #pragma unroll
     for (int nt = 0; nt < NT; nt++) {
       const int col = nt * 16 + c16;
