@@ -1,14 +1,19 @@
 #!/usr/bin/env python3
 """Benchmark: sub-pel PU refinements/s on 1920x1080 lowdelay_P QP22, NN_pred on
-(BASELINE.json metric; configs[2] at QP22).
+(BASELINE.json metric; configs[2] at QP22; other configs with --workload).
 
 A step is one frame batch: every (PU, reference picture) sub-pel job of one synthetic 1080p
 P-frame (510 CTUs x 423 calls x 4 references = 862,920 jobs, SURVEY.md §8(d) mix) through
-EMI step -> FracDIF -> NN_pred -> xMotionEstimation tail, jobs and pictures resident in HBM
-when timing starts.  With N ranks (torchrun, one GPU each) every rank refines its own frame
-(frames shard with no data-path collective: weak scaling); rank 0 owns the pictures and
-publishes each step's new frames to all ranks with an RCCL broadcast into a per-rank picture
-ring (nnfme.dist.PictureRing), which is part of the timed step.
+EMI step -> FracDIF -> NN_pred -> xMotionEstimation tail.  As SURVEY.md §8(d) defines the metric,
+the timed region runs from the first H2D of job descriptors to the last D2H of results: per step
+the jobs (32 B each), the frame's original and one reconstructed reference picture go over PCIe
+from pinned host memory, and the 16-byte fme_mv_result per job comes back (nnfme.pipeline.
+FrameReplay: two steps in flight on separate copy / compute streams, no host synchronisation
+inside a batch).  With N ranks (torchrun, one GPU each) rank r replays frames r, r+N, ... (weak
+scaling); each reconstruction is uploaded by one rank and RCCL-broadcast to all, and the NN
+carried state is chained across ranks at the end (all_gather of 12 words per frame + prefix
+re-run), all inside the timed region.  `device_resident` reports the same batches with inputs
+and outputs already in HBM.
 
 Prints one JSON line (rank 0).  `cpu_baseline` times oracle/_ref (the reference's own
 TLibCommon primitives driven in TEncSearch order, compiled -O2 like the reference build) on
@@ -17,11 +22,10 @@ one host core (HM is single-threaded) over a bounded sample of the same job mix;
 before the GPU is initialised.
 
 `roofline` is for the main search phase (the lane-per-unit EMI + FracDIF kernels of the 18
-power-of-two PU shapes, ~99.4 % of the jobs; the 8x8-, 8x4- and 4x8-unit kernels run
-concurrently on three streams, k_search_lane88 dominant): its algorithmic bytes (SURVEY.md §8(d)
-per-PU figure summed over the jobs it processes) over the phase's average duration, from HIP
-events recorded on the batch stream at the fork and after the join during the timed steps.  The path is integer-VALU bound, so the
-VALU roof (reference integer ops, §8(d)) is reported beside the HBM one.
+power-of-two PU shapes, ~99.4 % of the jobs, on three concurrent streams, k_search_lane88
+dominant), timed by HIP events recorded on the batch stream at the fork and after the join: the
+path is integer-VALU bound, so `bound` is "valu" with the reference's integer ops (§8(d)) per
+second over the VALU peak; the HBM roof of the same phase is the `hbm` entry.
 """
 import argparse
 import json
@@ -41,18 +45,37 @@ from nnfme.abi import JOB_DTYPE, RESULT_DTYPE  # noqa: E402
 W, H, QP = 1920, 1080, 22
 METRIC = "sub-pel PU refinements/sec @ 1080p lowdelay_P QP22; bit-exact MV/SATD vs HM"
 # BASELINE.json configs as bench workloads (default: the headline, configs[2] at QP22).
-#   name: (W, H, QP, nn_mode, calls per CTU per reference, references, bi-pred share, description)
+#   name: W, H, QP, nn (nn_mode), net (nn_mode 2), engine (0 exact, 1 MFMA), calls (per CTU per
+#   reference), refs, bipred (share of bi-pred key jobs), gop ("ldp" / "ra" lambdas), frames (per
+#   batch: small frames are batched so a launch fills the chip), desc
 WORKLOADS = {
-    "c3_qp22": (1920, 1080, 22, 1, 423, 4, 0.0,
-                "1920x1080 lowdelay_P QP22, NN_pred 2-layer on, 4 refs, 862920 PU jobs per frame (configs[2] at QP22)"),
-    "c3_qp27": (1920, 1080, 27, 1, 423, 4, 0.0, "1920x1080 lowdelay_P QP27, NN_pred on, 4 refs (configs[2] at QP27)"),
-    "c3_qp32": (1920, 1080, 32, 1, 423, 4, 0.0, "1920x1080 lowdelay_P QP32, NN_pred on, 4 refs (configs[2] at QP32)"),
-    "c3_qp37": (1920, 1080, 37, 1, 423, 4, 0.0, "1920x1080 lowdelay_P QP37, NN_pred on, 4 refs (configs[2] at QP37)"),
-    "c2": (416, 240, 22, 0, 331, 4, 0.0,
-           "416x240 lowdelay_P QP22, interpolation + SATD only (NN_pred off), 4 refs, 331 calls/CTU/ref (configs[1])"),
-    "c4": (2560, 1600, 27, 1, 333, 4, 0.205,
-           "2560x1600 random-access QP27 B-frame, NN_pred on, 2+2 refs, ~1331 calls/CTU, 20.5 % bi-pred with "
-           "2*org - pred keys (configs[3]; lambdas from the LDP QP27 table)"),
+    "c3_qp22": dict(W=1920, H=1080, QP=22, nn=1, calls=423, bipred=0.0, gop="ldp", frames=1,
+                    desc="1920x1080 lowdelay_P QP22, NN_pred 2-layer on, 4 refs, 862920 PU jobs per frame "
+                         "(configs[2] at QP22)"),
+    "c3_qp27": dict(W=1920, H=1080, QP=27, nn=1, calls=423, bipred=0.0, gop="ldp", frames=1,
+                    desc="1920x1080 lowdelay_P QP27, NN_pred on, 4 refs (configs[2] at QP27)"),
+    "c3_qp32": dict(W=1920, H=1080, QP=32, nn=1, calls=423, bipred=0.0, gop="ldp", frames=1,
+                    desc="1920x1080 lowdelay_P QP32, NN_pred on, 4 refs (configs[2] at QP32)"),
+    "c3_qp37": dict(W=1920, H=1080, QP=37, nn=1, calls=423, bipred=0.0, gop="ldp", frames=1,
+                    desc="1920x1080 lowdelay_P QP37, NN_pred on, 4 refs (configs[2] at QP37)"),
+    "c1": dict(W=416, H=240, QP=22, nn=1, calls=331, bipred=0.0, gop="ldp", frames=8,
+               desc="416x240 lowdelay_P QP22, NN_pred on, 4 refs (configs[0]: the CPU plumbing baseline's "
+                    "workload; 8 frames per batch on the GPU)"),
+    "c2": dict(W=416, H=240, QP=22, nn=0, calls=331, bipred=0.0, gop="ldp", frames=8,
+               desc="416x240 lowdelay_P QP22, interpolation + SATD only (NN_pred off), 4 refs, 331 calls/CTU/ref, "
+                    "8 frames per batch (configs[1])"),
+    "c4": dict(W=2560, H=1600, QP=27, nn=1, calls=333, bipred=0.205, gop="ra", frames=1,
+               desc="2560x1600 random-access QP27 B-frames, NN_pred on, 2+2 refs, ~1331 calls/CTU, 20.5 % bi-pred "
+                    "with 2*org - pred keys, RA GOP-8 lambdas (configs[3])"),
+    "c5": dict(W=1920, H=1080, QP=22, nn=2, net="scr3x40", engine=1, calls=423, bipred=0.0, gop="ldp", frames=1,
+               desc="1920x1080 lowdelay_P QP22 with the 3-hidden-layer NN_pred (Backups/4 SCR 9-40-40-40-49, "
+                    "double) as a batched MFMA GEMM (v_mfma_f64_16x16x4) (configs[4])"),
+    "c5_exact": dict(W=1920, H=1080, QP=22, nn=2, net="scr3x40", engine=0, calls=423, bipred=0.0, gop="ldp",
+                     frames=1, desc="configs[4] net through the exact (scalar, reference-order) engine"),
+    "c5_b4x40": dict(W=1920, H=1080, QP=22, nn=2, net="blowing4x40+rezero", engine=1, calls=423, bipred=0.0,
+                     gop="ldp", frames=1,
+                     desc="1920x1080 QP22 with the 4x40 blowing net (Backups/15, float, hidden layers re-zeroed) "
+                          "as a batched MFMA GEMM (v_mfma_f32_16x16x4)"),
 }
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md chip table (spec)
 # int32 VALU lane-ops/s: 256 CUs x 4 SIMDs x 32 lanes/clk (a wave64 op issues over 2 clk) x
@@ -334,10 +357,11 @@ def pred_inter_leg(dev, reps, cpu_seconds):
     return out
 
 
-def read_pmc_traffic():
-    """HBM bytes per search launch from the committed rocprofv3 PMC summary (profiles/), if any."""
+def read_pmc_traffic(workload):
+    """HBM bytes per main search launch from the committed rocprofv3 PMC summary of this workload
+    (profiles/pmc_traffic.json, regenerated by tools/gpu_check.sh from the current tree)."""
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-    if not os.path.exists(path):
+    if workload != "c3_qp22" or not os.path.exists(path):
         return None, None
     try:
         d = json.load(open(path))
@@ -346,10 +370,41 @@ def read_pmc_traffic():
         return None, None
 
 
+def frame_lambda(wl, f):
+    """Lambda of frame f: lowdelay_P by POC % 4 (cfg Frame1-4), random access by GOP-8 entry."""
+    if wl["gop"] == "ra":
+        return synth.ra_lambda(wl["QP"], f % 8)
+    return synth.LDP_LAMBDA[wl["QP"]][(f + 1) % 4]
+
+
+def nn_tail_roofline(wl, tm, n):
+    """configs[4]: the NN tail of nn_mode 2 as a batched GEMM (FLOPs of the hidden and output
+    layers per job) over its measured time, against the dense MFMA peak of its dtype."""
+    from nnfme import weights
+    net = weights.case_net(wl["net"])
+    fan = 17 if net.embedding else 9
+    flops = 0
+    for wdt in net.widths:
+        flops += 2 * fan * wdt
+        fan = wdt
+    flops += 2 * fan * 49
+    t = tm["nn_tail"] / 1e3
+    achieved = n * flops / t / 1e12
+    f64 = net.precision == weights.F64
+    # dense matrix peaks: f32 157.3 TF (MI355X_MICROARCH.md); f64 78.6 TF (AMD MI355X spec sheet)
+    peak = 78.6 if f64 else 157.3
+    return {"bound": "mfma", "achieved": achieved, "peak": peak, "unit": "TFLOP/s", "frac": achieved / peak,
+            "kernel": "fme::k_nn_deep_tail<%s, %d, %s, %s>" % ("double" if f64 else "float", len(net.widths),
+                                                              "emb" if net.embedding else "noemb",
+                                                              "mfma" if wl.get("engine") else "exact"),
+            "flops_per_job": flops, "kernel_ms": tm["nn_tail"],
+            "dtype": "f64" if f64 else "f32"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample length")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -357,41 +412,45 @@ def main():
     ap.add_argument("--no-tz", action="store_true", help="skip the integer-search leg")
     ap.add_argument("--no-pi", action="store_true", help="skip the predInterSearch producer leg")
     ap.add_argument("--workload", choices=sorted(WORKLOADS), default="c3_qp22",
-                    help="BASELINE.json config to run (default: the headline configs[2] at QP22)")
+                    help="BASELINE.json config to run (default: the headline, configs[2] at QP22)")
     ap.add_argument("--jobs", choices=("ctu", "uniform"), default="ctu",
                     help="job stream: HM CTU order (default) or uniformly scattered PUs (stress)")
     ap.add_argument("--cpu-cores", type=int, default=0,
                     help="cores for cpu_baseline_all_cores (0: all available, at most 16; -1: skip)")
+    ap.add_argument("--dist-backend", default="nccl", help="torch.distributed backend for N > 1 (nccl = RCCL)")
     args = ap.parse_args()
 
     global W, H, QP, METRIC
-    W, H, QP, NN, CALLS, _, BIPRED, WDESC = WORKLOADS[args.workload]
+    wl = WORKLOADS[args.workload]
+    W, H, QP = wl["W"], wl["H"], wl["QP"]
+    NN, CALLS, BIPRED, WDESC, FPS = wl["nn"], wl["calls"], wl["bipred"], wl["desc"], wl["frames"]
     if args.workload != "c3_qp22":
         METRIC = f"sub-pel PU refinements/sec @ {args.workload}: {WDESC.split(',')[0]}; bit-exact MV/SATD vs HM"
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
 
-    # ---- inputs (untimed): jobs of this rank's frames ----------------------------------------
-    jobs = make_frame_jobs(1000 + rank, args.jobs, CALLS, BIPRED)
-    n = len(jobs)
+    # ---- inputs (untimed): one frame's jobs in HM order -----------------------------------------
+    jobs = make_frame_jobs(1000, args.jobs, CALLS, BIPRED)
+    n1 = len(jobs)
     keys = None
     if BIPRED > 0:   # bi-pred key blocks (2*org - pred_other), resident with the jobs
         kpics = {k: synth.synth_luma(W, H, t) for k, t in zip(range(5), (7, 6, 5, 4, 0))}
-        keys = synth.make_bipred_keys_fast(np.random.default_rng(77 + rank), jobs, kpics)
+        keys = synth.make_bipred_keys_fast(np.random.default_rng(77), jobs, kpics)
 
     # ---- CPU baselines first, before anything touches the GPU (fork-safe) -------------------
     cpu = {}
-    _CPU["nn"], _CPU["keys"] = NN, keys
+    _CPU["nn"], _CPU["keys"] = min(NN, 1), keys
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         pics = {k: synth.synth_luma(W, H, t) for k, t in zip(range(5), (7, 6, 5, 4, 0))}
         rate, dt, done = cpu_baseline(jobs, pics, args.cpu_seconds)
         cpu["cpu_baseline"] = {
             "value": rate, "unit": "PU/s", "cores": 1, "kind": "reference",
-            "sample": f"{done} jobs ({done / n:.2f} passes over the same {args.workload} frame batch, "
+            "sample": f"{done} jobs ({done / n1:.2f} passes over one {args.workload} frame's jobs, "
                       f"HM order) on one host core, {dt:.1f} s; oracle/_ref = the reference's "
                       f"TLibCommon (interpolation, RdCost) -O2 driven in TEncSearch order, NN "
-                      f"restated scalar",
+                      f"restated scalar" + (" (the 2-layer master net: the deeper nets' backups do not "
+                                            "build)" if NN == 2 else ""),
         }
         avail = len(os.sched_getaffinity(0))
         cores = min(16, avail) if args.cpu_cores == 0 else args.cpu_cores
@@ -405,119 +464,102 @@ def main():
 
     import torch
     import torch.distributed as dist
-    from nnfme.dist import PictureRing
+    from nnfme import weights
+    from nnfme.pipeline import FrameReplay
     from nnfme.runtime import FmeContext
 
+    ndev = torch.cuda.device_count()
+    dev_index = local % max(ndev, 1)
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
-    stream = torch.cuda.current_stream(dev)
+        torch.cuda.set_device(dev_index)
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", dev_index))
+        else:
+            dist.init_process_group(args.dist_backend)
+    torch.cuda.set_device(dev_index)
+    dev = torch.device("cuda", dev_index)
 
-    # jobs and results resident in HBM
-    d_jobs = torch.from_numpy(jobs.view(np.uint8).copy()).to(dev)
-    d_res = torch.empty(n * RESULT_DTYPE.itemsize, dtype=torch.uint8, device=dev)
-
-    # picture pool on the owner (rank 0): 8 distinct synthetic frames, frame f -> pool[f % 8]
-    pool = None
-    if rank == 0:
-        pool = torch.stack([torch.from_numpy(synth.synth_luma(W, H, t)) for t in range(8)]).to(dev)
-    ring = PictureRing(W, H, slots=world + 4, device=dev, world=world, owner=0)
-
-    ctx = FmeContext(device=local, use_hadamard=1, nn_mode=NN, qp=QP, fast_inter_mode=1, max_jobs=n)
+    net = weights.case_net(wl["net"]) if NN == 2 else None
+    ctx = FmeContext(device=dev_index, use_hadamard=1, nn_mode=NN, qp=QP, fast_inter_mode=1,
+                     max_jobs=n1 * FPS, net=net, nn_engine=wl.get("engine", 0))
     if keys is not None:
         ctx.set_keys(keys)
-    for lid, lam in enumerate(synth.LDP_LAMBDA[QP]):
-        ctx.set_lambda(lid, lam)
-    # lambda slot 0 is rewritten per step to the frame's POC % 4 value
-    base_lambda = synth.LDP_LAMBDA[QP]
 
-    def publish(step):
-        """Frames step*world .. step*world+world-1 become resident on every rank."""
-        first = step * world
-        for f in range(first, first + world):
-            src = pool[f % 8] if rank == 0 else None
-            ring.publish(f, src)
-
-    # prime the ring with the 4 reference frames preceding step 0
-    for f in range(-4, 0):
-        ring.publish(f, pool[f % 8] if rank == 0 else None)
-
-    def run_step(step):
-        publish(step)
-        f = step * world + rank
-        ring.bind(ctx, 4, f)
-        for k in range(4):
-            ring.bind(ctx, k, f - 1 - k)
-        ctx.set_lambda(0, base_lambda[f % 4])
-        ctx.refine_device(d_jobs.data_ptr(), d_res.data_ptr(), n, stream.cuda_stream)
+    # synthetic frame pool (the trace's originals / reconstructions): frame g -> pool[g % 8]
+    pool = np.stack([synth.synth_luma(W, H, t) for t in range(8)])
+    steps_total = args.warmup + args.steps
+    rep = FrameReplay(ctx, jobs, pool, lambda f: frame_lambda(wl, f), steps_total, frames_per_step=FPS,
+                      world=world, rank=rank, device=dev)
+    n = rep.n
+    rep.prime()
 
     for s in range(args.warmup):
-        run_step(s)
-    torch.cuda.synchronize(dev)
+        rep.issue(s, prefetch=s + 1 < args.warmup)   # the first timed step uploads its own inputs
+    rep.s_copy.synchronize()
+    rep.s_comp.synchronize()
 
-    # ---- timed region (HIP events around each kernel, read at the next batch's own sync) ------
+    # ---- timed region: H2D (jobs, originals, reconstructions + RCCL broadcast) -> refine ->
+    # D2H of the 16-byte results, two steps in flight; the NN-state chain fix-up when sharded ----
     ctx.set_profiling(True)
     ctx.accumulated_timings(reset=True)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
-    for s in range(args.steps):
-        run_step(args.warmup + s)
+    for s in range(args.warmup, steps_total):
+        rep.issue(s)
+    fixed = rep.finish(first_step=args.warmup)
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        if args.dist_backend == "gloo":
+            t = t.cpu()
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     nb, acc = ctx.accumulated_timings(reset=True)
     ctx.set_profiling(False)
     tm = {k: v / max(nb, 1) for k, v in acc.items()}
+    value = world * n * args.steps / elapsed
 
-    # ---- PCIe-inclusive leg (untimed for `value`): host jobs -> host results, new org frame
-    # uploaded from host memory each step (pinned buffers) -------------------------------------
-    pcie = None
-    if rank == 0 and world == 1:
-        h_jobs = torch.from_numpy(jobs.view(np.uint8).copy()).pin_memory()
-        h_res = torch.empty(n * RESULT_DTYPE.itemsize, dtype=torch.uint8).pin_memory()
-        h_org = torch.from_numpy(synth.synth_luma(W, H, 0)).pin_memory()
-        d_org = torch.empty_like(h_org, device=dev)
-        reps = 3
-        torch.cuda.synchronize(dev)
-        t1 = time.perf_counter()
-        for _ in range(reps):
-            d_org.copy_(h_org, non_blocking=True)
-            ctx.bind_picture_device(4, d_org.data_ptr(), W, W, H)
-            d_jobs.copy_(h_jobs, non_blocking=True)
-            ctx.refine_device(d_jobs.data_ptr(), d_res.data_ptr(), n, stream.cuda_stream)
-            h_res.copy_(d_res, non_blocking=True)
-        torch.cuda.synchronize(dev)
-        dt = (time.perf_counter() - t1) / reps
-        pcie = {"value": n / dt, "unit": "PU/s", "ms_per_step": dt * 1e3,
-                "note": "jobs H2D + org frame H2D + refine + results D2H, pinned host buffers"}
+    # ---- device-resident rate (extra key): the same batches with jobs, pictures and results
+    # already in HBM, back to back on one stream (no PCIe in the loop) ---------------------------
+    dres = None
+    if rank == 0:
+        comp = rep.s_comp
+        with torch.cuda.stream(comp):
+            rep._bind(args.warmup)
+            torch.cuda.synchronize(dev)
+            t1 = time.perf_counter()
+            for s in range(args.steps):
+                ctx.refine_mv_device(rep.d_jobs[s & 1].data_ptr(), rep.d_out[s & 1].data_ptr(), n, comp.cuda_stream)
+            comp.synchronize()
+            dt = (time.perf_counter() - t1) / args.steps
+        dres = {"value": n / dt, "unit": "PU/s", "ms_per_step": dt * 1e3,
+                "note": "jobs, pictures and results HBM-resident, one GPU, batches back to back"}
 
-    mc = mc_leg(dev, stream, reps=max(5, args.steps)) if rank == 0 and not args.no_mc and W == 1920 else None
+    mc = mc_leg(dev, torch.cuda.current_stream(dev), reps=max(5, args.steps // 2)) \
+        if rank == 0 and not args.no_mc and W == 1920 and NN != 2 else None
     pi = None
-    if rank == 0 and not args.no_pi and W == 1920 and world == 1:
+    if rank == 0 and not args.no_pi and W == 1920 and world == 1 and NN == 1:
         pi = pred_inter_leg(dev, reps=2, cpu_seconds=0.0 if args.no_cpu_baseline else 4.0)
     tz = None
-    if rank == 0 and not args.no_tz and W == 1920 and world == 1:
-        tz = tz_leg(dev, stream, reps=max(3, args.steps // 2), cpu_seconds=0.0 if args.no_cpu_baseline else 6.0)
+    if rank == 0 and not args.no_tz and W == 1920 and world == 1 and NN == 1:
+        tz = tz_leg(dev, torch.cuda.current_stream(dev), reps=max(3, args.steps // 4),
+                    cpu_seconds=0.0 if args.no_cpu_baseline else 6.0)
 
-    value = world * n * args.steps / elapsed
     if rank == 0:
-        small_jobs = jobs[main_kernel_mask(ctx, jobs)]
+        gj = rep.jobs
+        small_jobs = gj[main_kernel_mask(ctx, gj)]
         bytes_small = algorithmic_bytes(small_jobs)
         small_s = tm["search_main"] / 1e3
-        achieved = bytes_small / small_s / 1e9
         ops_small = algorithmic_ops(small_jobs)
-        search_s = tm["search"] / 1e3
-        traffic, traffic_src = read_pmc_traffic()
+        valu = ops_small / small_s / 1e12
+        gbs = bytes_small / small_s / 1e9
+        traffic, traffic_src = read_pmc_traffic(args.workload)
         out = {
             "metric": METRIC,
             "value": value,
@@ -529,45 +571,53 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "int16/int32 (NN f32)",
+            "dtype": "int16/int32 (NN f32)" if NN != 2 else
+                     "int16/int32 (NN %s)" % ("f64" if net.precision == weights.F64 else "f32"),
             "data": "synthetic (SURVEY.md §8(d) YUV generator + PU-size mix; reference per-QP "
                     "NN weights, no random init)",
-            "config": {"workload": WDESC if args.workload != "c3_qp22" else
-                       "1920x1080 lowdelay_P QP22, NN_pred 2-layer on, 4 refs, "
-                       "862920 PU jobs per frame (configs[2] at QP22)",
+            "config": {"workload": WDESC,
                        "workload_id": args.workload,
                        "job_stream": args.jobs,
-                       "jobs_per_step_per_gpu": n, "parallelism": f"frame-sharded x{world}"},
+                       "frames_per_step": FPS,
+                       "jobs_per_step_per_gpu": n, "parallelism": f"frame-sharded x{world}",
+                       "timed": "per step: H2D of the jobs (32 B each), of the frames' originals and of one "
+                                "reconstructed reference per frame (RCCL broadcast when sharded), refine, D2H of "
+                                "the 16-byte fme_mv_result per job; two steps in flight on separate copy / "
+                                "compute streams" + ("; NN-state chain fix-up included" if world > 1 else "")},
             "roofline": {
-                "bound": "hbm",
-                "achieved": achieved,
-                "peak": HBM_PEAK_GBS,
-                "unit": "GB/s",
-                "frac": achieved / HBM_PEAK_GBS,
+                "bound": "valu",
+                "achieved": valu,
+                "peak": VALU_PEAK_TOPS,
+                "unit": "Tops/s (int32 VALU lane-ops)",
+                "frac": valu / VALU_PEAK_TOPS,
                 "traffic": traffic,
                 "kernel": "main search phase: fme::k_search_lane{48,84,88} (EMI + FracDIF) on three "
                           "concurrent streams, fork to join; k_search_lane88 dominant",
                 "kernel_jobs": int(len(small_jobs)),
+                "algorithmic_ops_per_launch": ops_small,
                 "algorithmic_bytes_per_launch": bytes_small,
                 "kernel_ms": tm["search_main"],
                 "profiled_batches": nb,
-                "valu_tops": ops_small / small_s / 1e12,
-                "valu_peak_tops": VALU_PEAK_TOPS,
-                "valu_frac": ops_small / small_s / 1e12 / VALU_PEAK_TOPS,
-                "note": "integer-VALU bound (~97 reference int ops per algorithmic byte); "
-                        "valu_frac counts the reference's arithmetic (SURVEY.md §8(d))",
+                "note": "integer-VALU bound (~97 reference int ops per algorithmic byte, SURVEY.md §8(d)); "
+                        "achieved counts the reference's arithmetic, not the instructions issued",
                 "traffic_source": traffic_src,
                 "batch_kernel_ms": tm,
-                "search_phase_achieved_gbs": algorithmic_bytes(jobs) / search_s / 1e9,
+                "hbm": {"bound": "hbm", "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                        "frac": gbs / HBM_PEAK_GBS,
+                        "traffic_frac_of_algorithmic": (traffic / bytes_small) if traffic else None},
             },
         }
+        if NN == 2:
+            out["nn_tail_roofline"] = nn_tail_roofline(wl, tm, n)
         out.update(cpu)
         if "cpu_baseline" in cpu:
             out["speedup_vs_cpu_1core"] = value / cpu["cpu_baseline"]["value"]
         if "cpu_baseline_all_cores" in cpu:
             out["speedup_vs_cpu_all_cores"] = value / cpu["cpu_baseline_all_cores"]["value"]
-        if pcie:
-            out["pcie_inclusive"] = pcie
+        if dres:
+            out["device_resident"] = dres
+        if world > 1:
+            out["nn_state_fixup_jobs_rank0"] = int(fixed)
         if mc:
             out["motion_compensation"] = mc
         if tz:
@@ -576,6 +626,7 @@ def main():
             out["pred_inter_search"] = pi
         print(json.dumps(out), flush=True)
 
+    ctx.close()
     if world > 1:
         dist.destroy_process_group()
     return 0

@@ -22,15 +22,15 @@
 #ifndef FME_TZ_DEFER_DEFAULT
 #define FME_TZ_DEFER_DEFAULT 1
 #endif
-#ifndef FME_LANE_STREAMS_DEFAULT
-#define FME_LANE_STREAMS_DEFAULT 1
-#endif
 
 using namespace fme;
 
 namespace {
 
 thread_local std::string g_last_error = "";
+
+// counts buffer: 25 class counts (+ invalid), 24 scatter cursors, 3 x 8 lane tile-queue heads
+constexpr int kCountWords = 2 * kNumClasses + 1 + 24;
 
 int fail(int code, const char* fmt, ...) {
   char buf[512];
@@ -97,14 +97,19 @@ struct fme_ctx {
 
   DevBuf<fme_job> d_jobs;      // staging for fme_refine (host arrays)
   DevBuf<fme_result> d_res;
+  DevBuf<fme_mv_result> d_mv;   // staging for fme_refine_mv
   DevBuf<uint8_t> cls;
   DevBuf<int32_t> perm;
   DevBuf<fme_job> sjobs;
-  DevBuf<int32_t> counts;      // 25 counts + 24 cursors, one memset
+  DevBuf<int32_t> counts;      // 25 counts, 24 cursors, 24 tile-queue heads: one memset
   DevBuf<int32_t> blk_agg;
   DevBuf<int32_t> blk_prefix;
   DevBuf<uint32_t> nn_state;   // 2 x 12 words
   int state_cur = 0;
+  bool state_pending = false;   // reset / set_state not yet applied (next batch, stream order)
+  uint32_t pending_state[12] = {};
+  DevBuf<Schedule> d_sched;     // built by k_schedule each batch
+  SchedParams sched_p{};
   int32_t* h_counts = nullptr; // pinned
 
   // motion compensation: owned chroma planes (cb then cr, one allocation per slot), staging
@@ -137,30 +142,31 @@ struct fme_ctx {
   DevBuf<uint32_t> single_nn_in;
   DevBuf<int32_t> single_nn_out;
 
-  // Profiling: two event sets used alternately, so batch k's set is read (without an extra
-  // sync) at batch k+1's histogram synchronisation.  Per set: 0 start, 1 classify end,
-  // 2 scatter begin, 3 scatter end, 4 small-shape search end, 5 search end, 6 batch end,
-  // 7/8 large-shape search begin/end (aux stream when concurrent).
+  // Profiling: a ring of event sets, one per profiled batch, read once the batch has finished
+  // (harvest_events), so profiling a run of batches adds no synchronisation.  Per set: 0 start,
+  // 1 classify end, 2 schedule end = scatter begin, 3 scatter end, 4 main search end, 5 search
+  // end, 6 batch end, 7/8 auxiliary search begin/end (aux stream).
   static constexpr int kEv = 9;
+  static constexpr int kEvSets = 32;
   bool profiling = false;
   bool events_made = false;
-  hipEvent_t ev[2][kEv] = {};
-  int ev_cur = 0;               // set the next profiled batch records into
-  int ev_pending = -1;          // set recorded but not yet harvested
-  bool ev_has_large[2] = {false, false};
-  bool ev_serial[2] = {false, false};
+  hipEvent_t ev[kEvSets][kEv] = {};
+  long long ev_head = 0;        // sets recorded
+  long long ev_tail = 0;        // sets harvested
+  bool ev_has_large[kEvSets] = {};
+  bool ev_serial[kEvSets] = {};
   bool timed = false;
+  hipEvent_t ev_done = nullptr; // end of the last batch (fme_refine_status)
+  bool batch_issued = false;
   float last_ms[FME_NUM_TIMINGS] = {};
   double acc_ms[FME_NUM_TIMINGS] = {};
   int acc_batches = 0;
 
-  // the large-shape search kernel runs beside the small-shape one on its own stream
+  // auxiliary streams: the search kernels of one batch run on three streams
   hipStream_t aux = nullptr;
-  hipStream_t aux2 = nullptr;            // second auxiliary stream (integer search)
+  hipStream_t aux2 = nullptr;
   hipEvent_t ev_join2 = nullptr;
   hipEvent_t ev_fork = nullptr, ev_join = nullptr;
-  bool concurrent_search = true;   // FME_SERIAL_SEARCH=1 runs the two search kernels back to back
-  bool lane_streams = FME_LANE_STREAMS_DEFAULT;  // FME_LANE_STREAMS=0/1: 4x8 / 8x4 lane kernels on aux streams
 };
 
 namespace fme {
@@ -172,29 +178,6 @@ hipError_t launch_nn_deep_single(const fme_nn_net& n, const void* packed, const 
                                  hipStream_t s);
 hipError_t debug_phase_cycles(unsigned long long* out16, bool reset);
 hipError_t launch_nn_single(const float* nnp, const uint32_t* in, int32_t* out, hipStream_t s);
-}
-
-// Reads a recorded (complete or to-be-waited-for) event set into last_ms and adds it to the
-// accumulators.
-static int harvest_events(fme_ctx* c, bool wait) {
-  if (c->ev_pending < 0) return FME_OK;
-  const int b = c->ev_pending;
-  hipEvent_t* e = c->ev[b];
-  if (wait) HIP_TRY(hipEventSynchronize(e[6]));
-  float* ms = c->last_ms;
-  HIP_TRY(hipEventElapsedTime(&ms[0], e[0], e[1]));
-  HIP_TRY(hipEventElapsedTime(&ms[1], e[2], e[3]));
-  HIP_TRY(hipEventElapsedTime(&ms[2], e[3], e[5]));
-  HIP_TRY(hipEventElapsedTime(&ms[3], e[5], e[6]));
-  HIP_TRY(hipEventElapsedTime(&ms[4], e[0], e[6]));
-  HIP_TRY(hipEventElapsedTime(&ms[5], c->ev_serial[b] && c->ev_has_large[b] ? e[8] : e[3], e[4]));
-  ms[6] = 0.f;
-  if (c->ev_has_large[b]) HIP_TRY(hipEventElapsedTime(&ms[6], e[7], e[8]));
-  for (int i = 0; i < FME_NUM_TIMINGS; i++) c->acc_ms[i] += ms[i];
-  c->acc_batches++;
-  c->ev_pending = -1;
-  c->timed = true;
-  return FME_OK;
 }
 
 extern "C" {
@@ -218,13 +201,16 @@ int fme_create(int device, const fme_config* cfg, fme_ctx** out_ctx) {
   HIP_TRY(c->d_pics.reserve(FME_MAX_PICTURES));
   HIP_TRY(c->d_mlambda.reserve(FME_MAX_LAMBDAS));
   HIP_TRY(c->d_nn.reserve(kNnPkFloats));
-  HIP_TRY(c->counts.reserve(2 * kNumClasses + 1));
+  HIP_TRY(c->counts.reserve(kCountWords));
+  HIP_TRY(c->d_sched.reserve(1));
+  c->sched_p = sched_params();
+  HIP_TRY(hipEventCreateWithFlags(&c->ev_done, hipEventDisableTiming));
+  HIP_TRY(hipStreamCreateWithFlags(&c->aux2, hipStreamNonBlocking));
+  HIP_TRY(hipEventCreateWithFlags(&c->ev_join2, hipEventDisableTiming));
   HIP_TRY(c->nn_state.reserve(24));
   HIP_TRY(hipMemset(c->nn_state.p, 0, 24 * sizeof(uint32_t)));
   HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&c->h_counts), (kNumClasses + 1) * sizeof(int32_t), hipHostMallocDefault));
   HIP_TRY(hipStreamCreateWithFlags(&c->aux, hipStreamNonBlocking));
-  if (const char* e = getenv("FME_SERIAL_SEARCH")) c->concurrent_search = (e[0] == '0');
-  if (const char* e = getenv("FME_LANE_STREAMS")) c->lane_streams = (e[0] == '1');
   if (const char* e = getenv("FME_TZ_DEFER")) c->tz_defer = (e[0] == '1');
   if (const char* e = getenv("FME_TZ_DEFER_MIN")) c->tz_defer_min = atoi(e);
   HIP_TRY(hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming));
@@ -258,8 +244,10 @@ int fme_destroy(fme_ctx* c) {
   for (auto& e : c->ev_mc)
     if (e) (void)hipEventDestroy(e);
   c->d_pics.release(); c->d_mlambda.release(); c->d_keys.release(); c->d_nn.release(); c->d_net.release();
-  c->d_jobs.release(); c->d_res.release(); c->cls.release(); c->perm.release(); c->sjobs.release();
+  c->d_jobs.release(); c->d_res.release(); c->d_mv.release(); c->cls.release(); c->perm.release(); c->sjobs.release();
   c->counts.release(); c->blk_agg.release(); c->blk_prefix.release(); c->nn_state.release();
+  c->d_sched.release();
+  if (c->ev_done) (void)hipEventDestroy(c->ev_done);
   c->single_pic.release(); c->single_job.release(); c->single_res.release();
   c->single_nn_in.release(); c->single_nn_out.release();
   if (c->h_counts) (void)hipHostFree(c->h_counts);
@@ -468,14 +456,17 @@ int fme_set_nn_margin_output(fme_ctx* c, float* d_margin) {
 
 int fme_nn_reset_state(fme_ctx* c) {
   if (!c) return fail(FME_E_INVALID, "fme_nn_reset_state: null ctx");
-  HIP_TRY(hipSetDevice(c->device));
-  HIP_TRY(hipMemset(c->nn_state.p, 0, 24 * sizeof(uint32_t)));
-  c->state_cur = 0;
+  for (uint32_t& v : c->pending_state) v = 0;
+  c->state_pending = true;
   return FME_OK;
 }
 
 int fme_nn_get_state(fme_ctx* c, uint32_t* out12) {
   if (!c || !out12) return fail(FME_E_INVALID, "fme_nn_get_state: null argument");
+  if (c->state_pending) {
+    std::memcpy(out12, c->pending_state, sizeof(c->pending_state));
+    return FME_OK;
+  }
   HIP_TRY(hipSetDevice(c->device));
   HIP_TRY(hipDeviceSynchronize());
   HIP_TRY(hipMemcpy(out12, c->nn_state.p + 12 * c->state_cur, 12 * sizeof(uint32_t), hipMemcpyDeviceToHost));
@@ -484,9 +475,20 @@ int fme_nn_get_state(fme_ctx* c, uint32_t* out12) {
 
 int fme_nn_set_state(fme_ctx* c, const uint32_t* in12) {
   if (!c || !in12) return fail(FME_E_INVALID, "fme_nn_set_state: null argument");
+  std::memcpy(c->pending_state, in12, sizeof(c->pending_state));
+  c->state_pending = true;
+  return FME_OK;
+}
+
+int fme_nn_copy_state_device(fme_ctx* c, uint32_t* d_out12, void* stream) {
+  if (!c || !d_out12) return fail(FME_E_INVALID, "fme_nn_copy_state_device: null argument");
   HIP_TRY(hipSetDevice(c->device));
-  HIP_TRY(hipDeviceSynchronize());
-  HIP_TRY(hipMemcpy(c->nn_state.p + 12 * c->state_cur, in12, 12 * sizeof(uint32_t), hipMemcpyHostToDevice));
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  if (c->state_pending)
+    HIP_TRY(launch_put_state(d_out12, c->pending_state, s));
+  else
+    HIP_TRY(hipMemcpyAsync(d_out12, c->nn_state.p + 12 * c->state_cur, 12 * sizeof(uint32_t),
+                           hipMemcpyDeviceToDevice, s));
   return FME_OK;
 }
 
@@ -500,28 +502,85 @@ static int ensure_work(fme_ctx* c, int n) {
   return FME_OK;
 }
 
+static WorkBufs work_bufs(fme_ctx* c) {
+  WorkBufs w{};
+  w.cls = c->cls.p;
+  w.perm = c->perm.p;
+  w.sjobs = c->sjobs.p;
+  w.counts = c->counts.p;
+  w.cursor = c->counts.p + kNumClasses + 1;
+  w.tile_ctr = c->counts.p + 2 * kNumClasses + 1;
+  w.blk_agg = c->blk_agg.p;
+  w.blk_prefix = c->blk_prefix.p;
+  w.nn_state = c->nn_state.p;
+  w.sched = c->d_sched.p;
+  w.mv_out = nullptr;
+  return w;
+}
+
+// The picture / lambda tables go to the device in stream order as the argument of a one-block
+// kernel: rebinding pictures for the next frame never waits for the batch in flight, and the
+// batch stream holds no copy-engine transfer (which would queue behind bulk uploads).
 static int sync_tables(fme_ctx* c, hipStream_t s) {
   if (!c->tables_dirty) return FME_OK;
-  HIP_TRY(hipMemcpyAsync(c->d_pics.p, c->pics, sizeof(c->pics), hipMemcpyHostToDevice, s));
-  HIP_TRY(hipMemcpyAsync(c->d_mlambda.p, c->mlambda, sizeof(c->mlambda), hipMemcpyHostToDevice, s));
+  HIP_TRY(launch_put_tables(c->d_pics.p, c->d_mlambda.p, c->pics, c->mlambda, s));
   c->tables_dirty = false;
   return FME_OK;
 }
 
+// Applies a reset / set of the NN state requested since the last batch, in stream order.
+static int apply_pending_state(fme_ctx* c, hipStream_t s) {
+  if (!c->state_pending) return FME_OK;
+  HIP_TRY(launch_put_state(c->nn_state.p + 12 * c->state_cur, c->pending_state, s));
+  c->state_pending = false;
+  return FME_OK;
+}
+
+// Profiling: a ring of event sets; a set is read once its batch has finished (polled at the next
+// batch, waited for only when the ring is full or the caller asks for the timings).
+static int harvest_events(fme_ctx* c, bool wait_all) {
+  while (c->ev_tail != c->ev_head) {
+    const int b = c->ev_tail % fme_ctx::kEvSets;
+    hipEvent_t* e = c->ev[b];
+    if (wait_all) {
+      HIP_TRY(hipEventSynchronize(e[6]));
+    } else {
+      const hipError_t q = hipEventQuery(e[6]);
+      if (q == hipErrorNotReady) break;
+      HIP_TRY(q);
+    }
+    float* ms = c->last_ms;
+    HIP_TRY(hipEventElapsedTime(&ms[0], e[0], e[1]));
+    HIP_TRY(hipEventElapsedTime(&ms[1], e[2], e[3]));
+    HIP_TRY(hipEventElapsedTime(&ms[2], e[3], e[5]));
+    HIP_TRY(hipEventElapsedTime(&ms[3], e[5], e[6]));
+    HIP_TRY(hipEventElapsedTime(&ms[4], e[0], e[6]));
+    HIP_TRY(hipEventElapsedTime(&ms[5], c->ev_serial[b] && c->ev_has_large[b] ? e[8] : e[3], e[4]));
+    ms[6] = 0.f;
+    if (c->ev_has_large[b]) HIP_TRY(hipEventElapsedTime(&ms[6], e[7], e[8]));
+    for (int i = 0; i < FME_NUM_TIMINGS; i++) c->acc_ms[i] += ms[i];
+    c->acc_batches++;
+    c->timed = true;
+    c->ev_tail++;
+  }
+  return FME_OK;
+}
+
+// One batch: classify -> schedule (device) -> scatter -> search (lane kernels on three streams,
+// cooperative AMP kernels beside them) -> NN + tail, all enqueued without waiting for the device.
 // Device validation covers what the host cannot see for device-resident jobs: a job with an
-// unknown PU shape, an unset picture / lambda slot or a key block outside the key buffer is
-// classified "invalid" and the batch is rejected before any search work is launched.
-int fme_refine_device(fme_ctx* c, const fme_job* d_jobs, fme_result* d_res, int n, void* stream) {
-  if (!c || (n > 0 && (!d_jobs || !d_res))) return fail(FME_E_INVALID, "fme_refine_device: null argument");
-  if (n < 0) return fail(FME_E_INVALID, "fme_refine_device: n = %d", n);
-  if (n == 0) return FME_OK;
+// unknown PU shape, an unset picture / lambda slot or a key block outside the key buffer makes
+// k_schedule mark the batch rejected; every later kernel then skips its work.
+static int refine_batch(fme_ctx* c, const fme_job* d_jobs, fme_result* d_res, fme_mv_result* d_mv, int n,
+                        hipStream_t s) {
   if (c->cfg.nn_mode == 1 && !c->nn_loaded) return fail(FME_E_STATE, "fme_refine_device: nn_mode set but no weights loaded");
   if (c->cfg.nn_mode == 2 && !c->net_loaded) return fail(FME_E_STATE, "fme_refine_device: nn_mode 2 but no net loaded");
   HIP_TRY(hipSetDevice(c->device));
-  hipStream_t s = static_cast<hipStream_t>(stream);
   int rc = ensure_work(c, n);
   if (rc) return rc;
   rc = sync_tables(c, s);
+  if (rc) return rc;
+  rc = apply_pending_state(c, s);
   if (rc) return rc;
 
   BatchArgs a{};
@@ -535,124 +594,91 @@ int fme_refine_device(fme_ctx* c, const fme_job* d_jobs, fme_result* d_res, int 
   a.use_hadamard = c->cfg.use_hadamard ? 1 : 0;
   a.fen = c->cfg.fast_inter_mode;
   a.nn_mode = c->cfg.nn_mode ? 1 : 0;
-  WorkBufs w{};
-  w.cls = c->cls.p;
-  w.perm = c->perm.p;
-  w.sjobs = c->sjobs.p;
-  w.counts = c->counts.p;
-  w.cursor = c->counts.p + kNumClasses + 1;
-  w.blk_agg = c->blk_agg.p;
-  w.blk_prefix = c->blk_prefix.p;
-  w.nn_state = c->nn_state.p;
+  WorkBufs w = work_bufs(c);
+  w.mv_out = d_mv;
 
   const bool prof = c->profiling;
-  const int eb = c->ev_cur;
-  hipEvent_t* ev = c->ev[eb];
-  if (prof) HIP_TRY(hipEventRecord(ev[0], s));
-  HIP_TRY(hipMemsetAsync(c->counts.p, 0, (2 * kNumClasses + 1) * sizeof(int32_t), s));
-  HIP_TRY(launch_classify(a, w, s));
-  if (prof) HIP_TRY(hipEventRecord(ev[1], s));
-  HIP_TRY(hipMemcpyAsync(c->h_counts, c->counts.p, (kNumClasses + 1) * sizeof(int32_t), hipMemcpyDeviceToHost, s));
-  HIP_TRY(hipStreamSynchronize(s));
-  // the previous profiled batch ran on this stream before the sync: its events are complete
-  if (c->ev_pending >= 0 && c->ev_pending != eb) {
+  hipEvent_t* ev = nullptr;
+  int eb = 0;
+  if (prof) {
     rc = harvest_events(c, false);
     if (rc) return rc;
-  }
-  if (c->h_counts[kNumClasses] > 0)
-    return fail(FME_E_INVALID, "fme_refine_device: %d job(s) with an unsupported PU size or unset picture/lambda/key",
-                c->h_counts[kNumClasses]);
-
-  Schedule sc{};
-  int off = 0;
-  int nb[kSearchKernels] = {0, 0, 0};
-  for (int k = 0; k < kNumClasses; k++) {
-    const int cnt = c->h_counts[k];
-    sc.class_off[k] = off;
-    sc.class_cnt[k] = cnt;
-    const int kern = search_kernel_of(k);
-    for (int q = 0; q < kSearchKernels; q++) sc.prefix[q][k] = nb[q];
-    nb[kern] += search_blocks_for(k, cnt);
-    off += cnt;
-  }
-  for (int q = 0; q < kSearchKernels; q++) sc.prefix[q][kNumClasses] = nb[q];
-  // main search kernel on the batch stream: the lane-per-unit kernel (or, in -DFME_NO_LANE
-  // builds, the 256-lane cooperative one); the remaining cooperative shapes run beside it on
-  // the auxiliary stream
-  const bool lane_main = nb[kSearchLane48] + nb[kSearchLane84] + nb[kSearchLane88] > 0 || nb[kSearchCoop] == 0;
-  const bool has_aux = lane_main ? (nb[kSearchCoop] + nb[kSearchCoopLarge] > 0) : nb[kSearchCoopLarge] > 0;
-  auto launch_aux = [&](hipStream_t st) -> hipError_t {
-    if (lane_main) {
-      const hipError_t e = launch_search_small(a, w, sc, st);
-      if (e != hipSuccess) return e;
+    if (c->ev_head - c->ev_tail == fme_ctx::kEvSets) {   // ring full: wait for the oldest set
+      HIP_TRY(hipEventSynchronize(c->ev[c->ev_tail % fme_ctx::kEvSets][6]));
+      rc = harvest_events(c, false);
+      if (rc) return rc;
     }
-    return launch_search_large(a, w, sc, st);
-  };
-  if (prof) HIP_TRY(hipEventRecord(ev[2], s));   // host sync above: scatter starts here
-  HIP_TRY(launch_scatter(a, w, sc, s));
+    eb = c->ev_head % fme_ctx::kEvSets;
+    ev = c->ev[eb];
+    HIP_TRY(hipEventRecord(ev[0], s));
+  }
+  HIP_TRY(hipMemsetAsync(c->counts.p, 0, kCountWords * sizeof(int32_t), s));
+  HIP_TRY(launch_classify(a, w, s));
+  if (prof) HIP_TRY(hipEventRecord(ev[1], s));
+  HIP_TRY(launch_schedule(w, c->sched_p, s));
+  if (prof) HIP_TRY(hipEventRecord(ev[2], s));
+  HIP_TRY(launch_scatter(a, w, s));
   if (prof) HIP_TRY(hipEventRecord(ev[3], s));
-  if (c->concurrent_search && c->lane_streams && lane_main) {
-    // the three lane kernels are independent: 8x8 units on the batch stream, 4x8 units on aux2,
-    // the cooperative shapes then 8x4 units on aux; joined before the NN tail
-    if (!c->aux2) HIP_TRY(hipStreamCreateWithFlags(&c->aux2, hipStreamNonBlocking));
-    if (!c->ev_join2) HIP_TRY(hipEventCreateWithFlags(&c->ev_join2, hipEventDisableTiming));
-    HIP_TRY(hipEventRecord(c->ev_fork, s));
-    HIP_TRY(hipStreamWaitEvent(c->aux, c->ev_fork, 0));
-    HIP_TRY(hipStreamWaitEvent(c->aux2, c->ev_fork, 0));
-    HIP_TRY(launch_search_lane_one(a, w, sc, kSearchLane48, c->aux2));
-    if (prof) HIP_TRY(hipEventRecord(ev[7], c->aux));
-    HIP_TRY(launch_aux(c->aux));
-    HIP_TRY(launch_search_lane_one(a, w, sc, kSearchLane84, c->aux));
-    if (prof) HIP_TRY(hipEventRecord(ev[8], c->aux));
-    HIP_TRY(hipEventRecord(c->ev_join, c->aux));
-    HIP_TRY(hipEventRecord(c->ev_join2, c->aux2));
-    HIP_TRY(launch_search_lane_one(a, w, sc, kSearchLane88, s));
-    HIP_TRY(hipStreamWaitEvent(s, c->ev_join, 0));
-    HIP_TRY(hipStreamWaitEvent(s, c->ev_join2, 0));
-    // "main search" spans all three lane kernels here (and the cooperative shapes beside them)
-    if (prof) HIP_TRY(hipEventRecord(ev[4], s));
-    if (prof) HIP_TRY(hipEventRecord(ev[5], s));
-    HIP_TRY(c->cfg.nn_mode == 2
-                ? launch_nn_deep_tail(c->net, c->d_net.p, c->nn_margin, a, w, c->state_cur, c->nn_engine, s)
-                : launch_nn_tail(a, w, c->d_nn.p, c->state_cur, s));
-    if (prof) {
-      HIP_TRY(hipEventRecord(ev[6], s));
-      c->ev_has_large[eb] = true;
-      c->ev_serial[eb] = false;
-      c->ev_pending = eb;
-      c->ev_cur ^= 1;
-    }
-    if (a.nn_mode) c->state_cur ^= 1;
-    return FME_OK;
-  }
-  if (!c->concurrent_search) {
-    if (prof && has_aux) HIP_TRY(hipEventRecord(ev[7], s));
-    HIP_TRY(launch_aux(s));
-    if (prof && has_aux) HIP_TRY(hipEventRecord(ev[8], s));
-  } else if (has_aux) {
-    HIP_TRY(hipEventRecord(c->ev_fork, s));
-    HIP_TRY(hipStreamWaitEvent(c->aux, c->ev_fork, 0));
-    if (prof) HIP_TRY(hipEventRecord(ev[7], c->aux));
-    HIP_TRY(launch_aux(c->aux));
-    if (prof) HIP_TRY(hipEventRecord(ev[8], c->aux));
-    HIP_TRY(hipEventRecord(c->ev_join, c->aux));
-  }
-  HIP_TRY(lane_main ? launch_search_lane(a, w, sc, s) : launch_search_small(a, w, sc, s));
+  // the three lane kernels are independent: 8x8 units on the batch stream, 4x8 units on aux2, 8x4
+  // units then the cooperative AMP shapes on aux; joined before the NN tail
+  HIP_TRY(hipEventRecord(c->ev_fork, s));
+  HIP_TRY(hipStreamWaitEvent(c->aux, c->ev_fork, 0));
+  HIP_TRY(hipStreamWaitEvent(c->aux2, c->ev_fork, 0));
+  // (the lane kernels' workgroups stay resident until their queues drain, so every lane kernel is
+  // launched before the cooperative AMP kernels, which then fill in as the lane workgroups exit)
+  HIP_TRY(launch_search_lane_one(a, w, kSearchLane48, c->aux2));
+  if (prof) HIP_TRY(hipEventRecord(ev[7], c->aux));
+  HIP_TRY(launch_search_lane_one(a, w, kSearchLane84, c->aux));
+  HIP_TRY(launch_search_small(a, w, c->aux));
+  HIP_TRY(launch_search_large(a, w, c->aux));
+  if (prof) HIP_TRY(hipEventRecord(ev[8], c->aux));
+  HIP_TRY(hipEventRecord(c->ev_join, c->aux));
+  HIP_TRY(hipEventRecord(c->ev_join2, c->aux2));
+  HIP_TRY(launch_search_lane_one(a, w, kSearchLane88, s));
+  HIP_TRY(hipStreamWaitEvent(s, c->ev_join, 0));
+  HIP_TRY(hipStreamWaitEvent(s, c->ev_join2, 0));
+  // "main search" spans all three lane kernels (and the cooperative shapes beside them)
   if (prof) HIP_TRY(hipEventRecord(ev[4], s));
-  if (c->concurrent_search && has_aux) HIP_TRY(hipStreamWaitEvent(s, c->ev_join, 0));
   if (prof) HIP_TRY(hipEventRecord(ev[5], s));
   HIP_TRY(c->cfg.nn_mode == 2
               ? launch_nn_deep_tail(c->net, c->d_net.p, c->nn_margin, a, w, c->state_cur, c->nn_engine, s)
               : launch_nn_tail(a, w, c->d_nn.p, c->state_cur, s));
   if (prof) {
     HIP_TRY(hipEventRecord(ev[6], s));
-    c->ev_has_large[eb] = has_aux;
-    c->ev_serial[eb] = !c->concurrent_search;
-    c->ev_pending = eb;
-    c->ev_cur ^= 1;
+    c->ev_has_large[eb] = true;
+    c->ev_serial[eb] = false;
+    c->ev_head++;
   }
+  HIP_TRY(hipEventRecord(c->ev_done, s));
+  c->batch_issued = true;
   if (a.nn_mode) c->state_cur ^= 1;
   return FME_OK;
+}
+
+int fme_refine_device(fme_ctx* c, const fme_job* d_jobs, fme_result* d_res, int n, void* stream) {
+  if (!c || (n > 0 && (!d_jobs || !d_res))) return fail(FME_E_INVALID, "fme_refine_device: null argument");
+  if (n < 0) return fail(FME_E_INVALID, "fme_refine_device: n = %d", n);
+  if (n == 0) return FME_OK;
+  return refine_batch(c, d_jobs, d_res, nullptr, n, static_cast<hipStream_t>(stream));
+}
+
+int fme_refine_mv_device(fme_ctx* c, const fme_job* d_jobs, fme_mv_result* d_out, int n, void* stream) {
+  if (!c || (n > 0 && (!d_jobs || !d_out))) return fail(FME_E_INVALID, "fme_refine_mv_device: null argument");
+  if (n < 0) return fail(FME_E_INVALID, "fme_refine_mv_device: n = %d", n);
+  if (n == 0) return FME_OK;
+  HIP_TRY(hipSetDevice(c->device));
+  HIP_TRY(c->d_res.reserve(n));   // full records: context scratch
+  return refine_batch(c, d_jobs, c->d_res.p, d_out, n, static_cast<hipStream_t>(stream));
+}
+
+int fme_refine_status(fme_ctx* c) {
+  if (!c) return fail(FME_E_INVALID, "fme_refine_status: null ctx");
+  if (!c->batch_issued) return 0;
+  HIP_TRY(hipSetDevice(c->device));
+  HIP_TRY(hipEventSynchronize(c->ev_done));
+  int32_t v = 0;
+  HIP_TRY(hipMemcpy(&v, &c->d_sched.p->invalid, sizeof(v), hipMemcpyDeviceToHost));
+  return v;
 }
 
 // ---- integer motion estimation (xTZSearch / xPatternSearch) -----------------------------------
@@ -682,29 +708,22 @@ static int tz_run(fme_ctx* c, fme_job* d_jobs, const fme_tz_ext* d_ext, uint32_t
   a.n = n;
   a.use_hadamard = c->cfg.use_hadamard ? 1 : 0;
   a.fen = c->cfg.fast_inter_mode;
-  WorkBufs w{};
-  w.cls = c->cls.p;
-  w.perm = c->perm.p;
-  w.sjobs = c->sjobs.p;
-  w.counts = c->counts.p;
-  w.cursor = c->counts.p + kNumClasses + 1;
-  w.blk_agg = c->blk_agg.p;
-  w.blk_prefix = c->blk_prefix.p;
-  w.nn_state = c->nn_state.p;
+  WorkBufs w = work_bufs(c);
   if (c->profiling) {
     if (!c->ev_tz[0]) {
       HIP_TRY(hipEventCreate(&c->ev_tz[0]));
       HIP_TRY(hipEventCreate(&c->ev_tz[1]));
     }
   }
-  HIP_TRY(hipMemsetAsync(c->counts.p, 0, (2 * kNumClasses + 1) * sizeof(int32_t), s));
+  HIP_TRY(hipMemsetAsync(c->counts.p, 0, kCountWords * sizeof(int32_t), s));
   HIP_TRY(launch_classify(a, w, s));
+  HIP_TRY(launch_schedule(w, c->sched_p, s));   // class offsets for the scatter
   HIP_TRY(hipMemcpyAsync(c->h_counts, c->counts.p, (kNumClasses + 1) * sizeof(int32_t), hipMemcpyDeviceToHost, s));
   HIP_TRY(hipStreamSynchronize(s));
   if (c->h_counts[kNumClasses] > 0)
     return fail(FME_E_INVALID, "fme_integer_search_device: %d job(s) with an unsupported PU size or unset picture/lambda/key",
                 c->h_counts[kNumClasses]);
-  Schedule sc{};
+  TzSchedule sc{};
   int off = 0, nb[3] = {0, 0, 0};
   for (int k = 0; k < kNumClasses; k++) {
     const int cnt = c->h_counts[k];
@@ -715,7 +734,7 @@ static int tz_run(fme_ctx* c, fme_job* d_jobs, const fme_tz_ext* d_ext, uint32_t
     off += cnt;
   }
   for (int q = 0; q < 3; q++) sc.prefix[q][kNumClasses] = nb[q];
-  HIP_TRY(launch_scatter(a, w, sc, s));
+  HIP_TRY(launch_scatter(a, w, s));
   TzArgs ta{};
   ta.a = a;
   ta.sjobs = c->sjobs.p;
@@ -812,19 +831,38 @@ int fme_integer_search_last_ms(fme_ctx* c, float* ms) {
   return FME_OK;
 }
 
-int fme_refine(fme_ctx* c, const fme_job* jobs, fme_result* res, int n, void* stream) {
-  if (!c || (n > 0 && (!jobs || !res))) return fail(FME_E_INVALID, "fme_refine: null argument");
-  if (n <= 0) return n == 0 ? FME_OK : fail(FME_E_INVALID, "fme_refine: n = %d", n);
+// Host arrays: H2D of the jobs, the batch, D2H of the outputs and of the rejected-job count,
+// one synchronisation at the end.
+static int refine_host(fme_ctx* c, const fme_job* jobs, fme_result* res, fme_mv_result* mv, int n, void* stream,
+                       const char* name) {
+  if (!c || (n > 0 && (!jobs || (!res && !mv)))) return fail(FME_E_INVALID, "%s: null argument", name);
+  if (n <= 0) return n == 0 ? FME_OK : fail(FME_E_INVALID, "%s: n = %d", name, n);
   HIP_TRY(hipSetDevice(c->device));
   hipStream_t s = static_cast<hipStream_t>(stream);
   HIP_TRY(c->d_jobs.reserve(n));
   HIP_TRY(c->d_res.reserve(n));
+  if (mv) HIP_TRY(c->d_mv.reserve(n));
   HIP_TRY(hipMemcpyAsync(c->d_jobs.p, jobs, (size_t)n * sizeof(fme_job), hipMemcpyHostToDevice, s));
-  int rc = fme_refine_device(c, c->d_jobs.p, c->d_res.p, n, stream);
+  int rc = refine_batch(c, c->d_jobs.p, c->d_res.p, mv ? c->d_mv.p : nullptr, n, s);
   if (rc) return rc;
-  HIP_TRY(hipMemcpyAsync(res, c->d_res.p, (size_t)n * sizeof(fme_result), hipMemcpyDeviceToHost, s));
+  if (mv)
+    HIP_TRY(hipMemcpyAsync(mv, c->d_mv.p, (size_t)n * sizeof(fme_mv_result), hipMemcpyDeviceToHost, s));
+  else
+    HIP_TRY(hipMemcpyAsync(res, c->d_res.p, (size_t)n * sizeof(fme_result), hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipMemcpyAsync(c->h_counts, &c->d_sched.p->invalid, sizeof(int32_t), hipMemcpyDeviceToHost, s));
   HIP_TRY(hipStreamSynchronize(s));
+  if (c->h_counts[0] > 0)
+    return fail(FME_E_INVALID, "%s: %d job(s) with an unsupported PU size or unset picture/lambda/key", name,
+                c->h_counts[0]);
   return FME_OK;
+}
+
+int fme_refine(fme_ctx* c, const fme_job* jobs, fme_result* res, int n, void* stream) {
+  return refine_host(c, jobs, res, nullptr, n, stream, "fme_refine");
+}
+
+int fme_refine_mv(fme_ctx* c, const fme_job* jobs, fme_mv_result* out, int n, void* stream) {
+  return refine_host(c, jobs, nullptr, out, n, stream, "fme_refine_mv");
 }
 
 // xPatternSearchFracDIF for one PU: the reference window around mv_int becomes a private
@@ -1051,7 +1089,7 @@ int fme_set_profiling(fme_ctx* c, int enable) {
       for (auto& e : set) HIP_TRY(hipEventCreate(&e));
     c->events_made = true;
   }
-  if (!enable && c->ev_pending >= 0) {
+  if (!enable) {
     const int rc = harvest_events(c, true);
     if (rc) return rc;
   }

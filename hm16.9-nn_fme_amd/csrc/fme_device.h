@@ -72,6 +72,8 @@ struct BatchArgs {
   int32_t nn_mode;
 };
 
+struct Schedule;
+
 // Work buffers (device) for one batch.
 struct WorkBufs {
   uint8_t* cls;          // [n] class id, 255 = invalid
@@ -82,6 +84,9 @@ struct WorkBufs {
   int32_t* blk_agg;      // [nblk * 9] per-block max of the NN writer indices
   int32_t* blk_prefix;   // [nblk * 9] exclusive prefix (carry-in) per block
   uint32_t* nn_state;    // 2 x 12 words: slot[8], c, pu_h, pu_w, written
+  Schedule* sched;       // built on the device by k_schedule from counts
+  int32_t* tile_ctr;     // [3][8] lane-kernel tile queue heads (zeroed with counts)
+  fme_mv_result* mv_out; // compact per-job output (fme_refine_mv*), or null
 };
 
 // Schedule of the search kernels.  Kernel k (lane-per-unit with 4x8 / 8x4 / 8x8 units,
@@ -96,7 +101,21 @@ struct Schedule {
   int32_t prefix[kSearchKernels][kNumClasses + 1];
   int32_t class_off[kNumClasses];
   int32_t class_cnt[kNumClasses];
+  // Device-built schedules only (k_schedule): the lane kernels' per-XCD tile queues.  XCD x
+  // owns the x-th contiguous eighth of every class's blocks; its queue lists them class by
+  // class, xq[k][x][c] = its tiles before class c (xq[k][x][kNumClasses] = queue length).
+  int32_t xq[3][8][kNumClasses + 1];
+  int32_t invalid;            // jobs rejected by k_classify (the whole batch is then skipped)
+  int32_t pad_[3];
 };
+
+// What k_schedule needs to know about the search kernels (host tables, one per build).
+struct SchedParams {
+  int8_t kern[kNumClasses];       // search_kernel_of(c)
+  int32_t lanes[kNumClasses];     // lane kernels: lanes per PU; cooperative: PUs per tile
+  int32_t tiles_per_block;        // cooperative kernels
+};
+SchedParams sched_params();
 
 // One integer-search launch (fme_tz.hip): the batch, its class-ordered copy and the outputs.
 struct TzArgs {
@@ -114,26 +133,39 @@ struct TzArgs {
 };
 int tz_kernel_of(int cls);    // 0: 4x8 units, 1: 8x4, 2: 8x8
 int tz_lanes_per_pu(int cls);
-hipError_t launch_tz(const TzArgs& ta, const Schedule& sc, int kid, hipStream_t s);
-hipError_t launch_tz_raster(const TzArgs& ta, const Schedule& sc, int kid, int nq, hipStream_t s);
+// Host-built schedule of the integer-search kernels (passed by value).
+struct TzSchedule {
+  int32_t prefix[3][kNumClasses + 1];
+  int32_t class_off[kNumClasses];
+  int32_t class_cnt[kNumClasses];
+};
+hipError_t launch_tz(const TzArgs& ta, const TzSchedule& sc, int kid, hipStream_t s);
+hipError_t launch_tz_raster(const TzArgs& ta, const TzSchedule& sc, int kid, int nq, hipStream_t s);
 
 // Host-side launch helpers (fme_kernels.hip).
 int pus_per_tile(int cls);
 size_t lds_bytes_for_class(int cls);
 hipError_t launch_classify(const BatchArgs& a, const WorkBufs& w, hipStream_t s);
-hipError_t launch_scatter(const BatchArgs& a, const WorkBufs& w, const Schedule& sc, hipStream_t s);
+// one block: w.counts -> *w.sched (class offsets, block ranges, XCD queues, invalid count)
+hipError_t launch_schedule(const WorkBufs& w, const SchedParams& p, hipStream_t s);
+hipError_t launch_scatter(const BatchArgs& a, const WorkBufs& w, hipStream_t s);
+// 12 words of NN state written to dst in stream order (reset / set_state)
+hipError_t launch_put_state(uint32_t* dst, const uint32_t* v12, hipStream_t s);
+// the picture / lambda tables written in stream order from kernel arguments
+hipError_t launch_put_tables(PicDesc* d_pics, double* d_ml, const PicDesc* pics, const double* ml, hipStream_t s);
 int tiles_per_block();
 int search_kernel_of(int cls);                      // kSearchLane48 .. kSearchCoopLarge
 int search_blocks_for(int cls, int cnt);           // blocks of its kernel for cnt jobs
-hipError_t launch_search_lane(const BatchArgs& a, const WorkBufs& w, const Schedule& sc, hipStream_t s);
-// one lane kernel (kSearchLane48 / 84 / 88) on stream s
-hipError_t launch_search_lane_one(const BatchArgs& a, const WorkBufs& w, const Schedule& sc, int kern,
-                                  hipStream_t s);
-hipError_t launch_search_large(const BatchArgs& a, const WorkBufs& w, const Schedule& sc, hipStream_t s);
-hipError_t launch_search_small(const BatchArgs& a, const WorkBufs& w, const Schedule& sc, hipStream_t s);
+// The search kernels read their schedule from *w.sched (no host round trip).  A lane kernel is
+// launched with enough workgroups to fill the chip, each pulling tiles from its XCD's queue
+// (then the other XCDs'); a cooperative kernel strides over its blocks.  `n` bounds the work.
+hipError_t launch_search_lane_one(const BatchArgs& a, const WorkBufs& w, int kern, hipStream_t s);
+hipError_t launch_search_large(const BatchArgs& a, const WorkBufs& w, hipStream_t s);
+hipError_t launch_search_small(const BatchArgs& a, const WorkBufs& w, hipStream_t s);
 int lane_lanes_per_pu(int cls);                    // 0: not a lane-kernel class
 int lane_kernel_of(int cls);                       // kSearchLane48/84/88, -1: not a lane class
 int lane_blocks_for(int cls, int cnt);
+int cu_count(int device);                          // compute units (workgroup budget of a launch)
 // Packed NN layout for the tail kernel (nn_pack, fme_kernels.hip): offsets in floats, every
 // pair region 8-byte aligned.
 constexpr int kNnPkPfx = 0;                       // [64 shapes][22] layer-1 prefix (k = 0..7)
@@ -158,4 +190,38 @@ void nn_pack(const float* params, float* packed);   // FME_NN_PARAMS floats -> k
 hipError_t launch_nn_tail(const BatchArgs& a, const WorkBufs& w, const float* nn_params,
                           int state_in, hipStream_t s);
 
+// The tail kernels' output: xMotionEstimation's MV / cost / bits with the NN class and status,
+// into the full record or, for fme_refine_mv*, the compact one alone.
+__device__ __forceinline__ void store_outputs(fme_result* r, fme_mv_result* mv_out, int i, int fx, int fy,
+                                              uint32_t cost, uint32_t bits, uint8_t cls, uint16_t status) {
+  if (mv_out) {
+    fme_mv_result o;
+    o.mv_x = (int16_t)fx;
+    o.mv_y = (int16_t)fy;
+    o.cost = cost;
+    o.bits = bits;
+    o.nn_class = cls;
+    o.reserved = 0;
+    o.status = status;
+    mv_out[i] = o;
+  } else {
+    r->mv_x = (int16_t)fx;
+    r->mv_y = (int16_t)fy;
+    r->cost = cost;
+    r->bits = bits;
+    r->nn_class = cls;
+    r->status = status;
+  }
+}
+
+// A batch k_classify rejected: every job is marked, nothing else is written, and the NN state
+// is carried through unchanged (the host flips the state slot after every batch).
+__device__ __forceinline__ void reject_job(const BatchArgs& a, const WorkBufs& w, int i, int state_in) {
+  if (w.mv_out)
+    w.mv_out[i].status = FME_RES_REJECTED;
+  else
+    a.res[i].status = FME_RES_REJECTED;
+  if (i == 0)
+    for (int k = 0; k < 12; k++) w.nn_state[12 * (state_in ^ 1) + k] = w.nn_state[12 * state_in + k];
+}
 }  // namespace fme

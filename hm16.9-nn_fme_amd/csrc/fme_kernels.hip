@@ -156,8 +156,61 @@ __global__ __launch_bounds__(kBlock) void k_classify(BatchArgs a, WorkBufs w) {
   if (tid < 9) w.blk_agg[blockIdx.x * 9 + tid] = agg[tid];
 }
 
-__global__ __launch_bounds__(kBlock) void k_scatter(BatchArgs a, WorkBufs w, Schedule sc) {
+// ---------------------------------------------------------------------------------------
+// schedule: the class histogram -> class offsets, each search kernel's block ranges and the
+// lane kernels' per-XCD tile queues, all on the device (one wave, one lane per class), so a
+// batch needs no host round trip between classify and search.
+// ---------------------------------------------------------------------------------------
+__device__ __forceinline__ int wave_excl_scan(int v) {
+  int s = v;
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const int o = __shfl_up(s, off, 64);
+    if ((int)threadIdx.x >= off) s += o;
+  }
+  return s - v;
+}
+
+__global__ __launch_bounds__(64) void k_schedule(WorkBufs w, SchedParams p) {
+  const int c = threadIdx.x;
+  Schedule* sc = w.sched;
+  const int inv = w.counts[kNumClasses];
+  const int cnt = (c < kNumClasses && inv == 0) ? w.counts[c] : 0;
+  int kern = -1, nb = 0;
+  if (cnt > 0) {
+    kern = p.kern[c];
+    if (kern <= kSearchLane88) {
+      nb = (int)(((long long)cnt * p.lanes[c] + 255) / 256);
+    } else {
+      const int tiles = (cnt + p.lanes[c] - 1) / p.lanes[c];
+      nb = (tiles + p.tiles_per_block - 1) / p.tiles_per_block;
+    }
+  }
+  const int off = wave_excl_scan(cnt);
+  if (c < kNumClasses) {
+    sc->class_off[c] = off;
+    sc->class_cnt[c] = cnt;
+  }
+#pragma unroll
+  for (int q = 0; q < kSearchKernels; q++) {
+    const int ex = wave_excl_scan(kern == q ? nb : 0);
+    if (c <= kNumClasses) sc->prefix[q][c] = ex;     // [kNumClasses] = the kernel's total
+  }
+#pragma unroll
+  for (int q = 0; q < 3; q++)
+#pragma unroll
+    for (int x = 0; x < 8; x++) {
+      const int mine = kern == q ? (nb >> 3) + (x < (nb & 7) ? 1 : 0) : 0;
+      const int ex = wave_excl_scan(mine);
+      if (c <= kNumClasses) sc->xq[q][x][c] = ex;
+    }
+  if (c == 0) sc->invalid = inv;
+}
+
+__global__ __launch_bounds__(kBlock) void k_scatter(BatchArgs a, WorkBufs w) {
   __shared__ int32_t cnt[kNumClasses], basep[kNumClasses];
+  const Schedule* __restrict__ sc = w.sched;
+  if (sc->invalid) return;   // rejected batch: nothing downstream reads the grouping
   const int tid = threadIdx.x;
   if (tid < kNumClasses) cnt[tid] = 0;
   __syncthreads();
@@ -184,7 +237,7 @@ __global__ __launch_bounds__(kBlock) void k_scatter(BatchArgs a, WorkBufs w, Sch
   for (int q = 0; q < kJobsPerScanBlock / kBlock; q++) {
     const int i = base + q * kBlock + tid;
     if (cls[q] < kNumClasses) {
-      const int dst = sc.class_off[cls[q]] + basep[cls[q]] + rank[q];
+      const int dst = sc->class_off[cls[q]] + basep[cls[q]] + rank[q];
       w.perm[dst] = i;
       w.sjobs[dst] = jb[q];
     }
@@ -350,6 +403,10 @@ __global__ __launch_bounds__(kTailNT) void k_nn_tail(BatchArgs a, WorkBufs w,
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int i = blockIdx.x * kJobsPerScanBlock + tid;
   const bool valid = i < a.n;
+  if (w.sched->invalid) {
+    if (valid) reject_job(a, w, i, state_in);
+    return;
+  }
   fme_job j{};
   if (valid) j = a.jobs[i];
 
@@ -389,7 +446,7 @@ __global__ __launch_bounds__(kTailNT) void k_nn_tail(BatchArgs a, WorkBufs w,
   fme_result* r = a.res + i;
   const double ml = a.mlambda[j.lambda_id];
   const int mvx = r->mv_int_x, mvy = r->mv_int_y;
-  int offx, offy;
+  int offx, offy, cls = 255;
   uint16_t status = 0;
   if (a.nn_mode) {
     uint32_t e[8];
@@ -414,8 +471,7 @@ __global__ __launch_bounds__(kTailNT) void k_nn_tail(BatchArgs a, WorkBufs w,
       ph = st_in[9];
       pw = st_in[10];
     }
-    const int cls = nn_forward(nnp_g, e, c, (int)ph, (int)pw);
-    r->nn_class = (uint8_t)cls;
+    cls = nn_forward(nnp_g, e, c, (int)ph, (int)pw);
     if (!(j.flags & FME_JOB_EMI) || r->n_emi < 8) status |= FME_RES_NN_STALE;
     if ((written & 0x1FFu) != 0x1FFu) status |= FME_RES_NN_UNINIT;
     offx = cls % 7 - 3;
@@ -429,20 +485,16 @@ __global__ __launch_bounds__(kTailNT) void k_nn_tail(BatchArgs a, WorkBufs w,
       st_out[11] = written;
     }
   } else {
-    r->nn_class = 255;
     offx = 2 * r->half_x + r->qtr_x;
     offy = 2 * r->half_y + r->qtr_y;
   }
   const int fx = 4 * mvx + offx, fy = 4 * mvy + offy;
-  r->mv_x = (int16_t)fx;
-  r->mv_y = (int16_t)fy;
   const uint32_t mvb = mv_bits(fx, fy, 0, j.mvp_x, j.mvp_y);
   const uint32_t bits = (uint32_t)j.bits_in + mvb;
-  r->bits = bits;
   const double fw = (j.flags & FME_JOB_BIPRED) ? 0.5 : 1.0;
   const double val = floor(fw * ((double)r->frac_cost - (double)mv_cost(ml, mvb))) + (double)mv_cost(ml, bits);
-  r->cost = (uint32_t)(int64_t)val;   // gcc/x86-64 (Distortion)(double) semantics
-  r->status = status;
+  // gcc/x86-64 (Distortion)(double) semantics for the cost
+  store_outputs(r, w.mv_out, i, fx, fy, (uint32_t)(int64_t)val, bits, (uint8_t)cls, status);
 }
 
 // NN_pred() on one explicit input (fme_nn_pred_single): e[8], C, PUHeight, PUWidth.
@@ -469,9 +521,67 @@ hipError_t launch_classify(const BatchArgs& a, const WorkBufs& w, hipStream_t s)
   return hipGetLastError();
 }
 
-hipError_t launch_scatter(const BatchArgs& a, const WorkBufs& w, const Schedule& sc, hipStream_t s) {
-  hipLaunchKernelGGL(k_scatter, dim3(nblocks(a.n)), dim3(kBlock), 0, s, a, w, sc);
+// fme_nn_reset_state / fme_nn_set_state, applied in stream order: the 12 words travel as a
+// kernel argument, so the host copy is free as soon as the launch returns.
+struct State12 {
+  uint32_t v[12];
+};
+__global__ void k_put_state(uint32_t* dst, State12 st) {
+  if (threadIdx.x < 12) dst[threadIdx.x] = st.v[threadIdx.x];
+}
+
+// The picture / lambda tables of a batch, likewise as a kernel argument (3 KB < the 4 KB limit):
+// no copy-engine transfer on the batch stream, which would queue behind bulk uploads.
+struct TablesArg {
+  PicDesc pics[FME_MAX_PICTURES];
+  double ml[FME_MAX_LAMBDAS];
+};
+static_assert(sizeof(TablesArg) <= 3584, "tables must fit the kernel-argument segment");
+__global__ __launch_bounds__(256) void k_put_tables(PicDesc* __restrict__ pics, double* __restrict__ ml, TablesArg t) {
+  const int i = threadIdx.x;
+  if (i < FME_MAX_PICTURES) pics[i] = t.pics[i];
+  if (i < FME_MAX_LAMBDAS) ml[i] = t.ml[i];
+}
+
+hipError_t launch_put_tables(PicDesc* d_pics, double* d_ml, const PicDesc* pics, const double* ml, hipStream_t s) {
+  TablesArg t;
+  for (int i = 0; i < FME_MAX_PICTURES; i++) t.pics[i] = pics[i];
+  for (int i = 0; i < FME_MAX_LAMBDAS; i++) t.ml[i] = ml[i];
+  hipLaunchKernelGGL(k_put_tables, dim3(1), dim3(256), 0, s, d_pics, d_ml, t);
   return hipGetLastError();
+}
+
+hipError_t launch_put_state(uint32_t* dst, const uint32_t* v12, hipStream_t s) {
+  State12 st;
+  for (int k = 0; k < 12; k++) st.v[k] = v12[k];
+  hipLaunchKernelGGL(k_put_state, dim3(1), dim3(64), 0, s, dst, st);
+  return hipGetLastError();
+}
+
+hipError_t launch_schedule(const WorkBufs& w, const SchedParams& p, hipStream_t s) {
+  hipLaunchKernelGGL(k_schedule, dim3(1), dim3(64), 0, s, w, p);
+  return hipGetLastError();
+}
+
+hipError_t launch_scatter(const BatchArgs& a, const WorkBufs& w, hipStream_t s) {
+  hipLaunchKernelGGL(k_scatter, dim3(nblocks(a.n)), dim3(kBlock), 0, s, a, w);
+  return hipGetLastError();
+}
+
+SchedParams sched_params() {
+  SchedParams p{};
+  for (int c = 0; c < kNumClasses; c++) {
+    p.kern[c] = (int8_t)search_kernel_of(c);
+    p.lanes[c] = lane_lanes_per_pu(c) > 0 ? lane_lanes_per_pu(c) : pus_per_tile(c);
+  }
+  p.tiles_per_block = tiles_per_block();
+  return p;
+}
+
+int cu_count(int device) {
+  int v = 0;
+  if (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || v <= 0) v = 256;
+  return v;
 }
 
 hipError_t launch_nn_tail(const BatchArgs& a, const WorkBufs& w, const float* nn_params,

@@ -25,6 +25,7 @@
 // >> 12 for 2-D), and key - pred is unchanged.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 
 #include "fme_device.h"
 #include "fme_simd.h"
@@ -765,15 +766,12 @@ __device__ __forceinline__ void lane_unit(const BatchArgs& a, const fme_job* __r
   }
 }
 
-// Workgroups go round-robin to the 8 XCDs: give XCD k the k-th contiguous eighth of a class's
-// blocks (one spatial band of the CTU-ordered job stream) so each L2 sees one band.
-__device__ __forceinline__ int xcd_block(int r, int n) {
+// The XCD this wave runs on (HW_REG_XCC_ID, gfx940+: bits 3:0).
+__device__ __forceinline__ int xcc_id() {
 #if FME_XCD_SWIZZLE
-  const int k = r & 7;
-  return k * (n >> 3) + min(k, n & 7) + (r >> 3);
+  return __builtin_amdgcn_s_getreg((20) | (0 << 6) | ((4 - 1) << 11)) & 7;
 #else
-  (void)n;
-  return r;
+  return 0;
 #endif
 }
 
@@ -789,34 +787,57 @@ __device__ __forceinline__ int xcd_block(int r, int n) {
   X(18, 64, 16, 8, 8) X(19, 32, 64, 8, 8) X(20, 64, 32, 8, 8) X(23, 64, 64, 8, 8)
 #define FME_LANE_CLASSES(X) FME_LANE48_CLASSES(X) FME_LANE84_CLASSES(X) FME_LANE88_CLASSES(X)
 
+// A workgroup pulls 256-lane tiles from its XCD's queue (Schedule::xq: the XCD's contiguous
+// eighth of every class = one spatial band of the CTU-ordered job stream, so each L2 sees one
+// band), then from the other XCDs' queues; the claim of the next tile is issued before the
+// current one is searched.  The grid is sized to fill the chip, not to the (device-computed)
+// tile count, so the host never waits for the class histogram.
 #define FME_CASE(ID, PW_, PH_, UW_, UH_)                                                             \
   case ID:                                                                                           \
-    lane_unit<PW_, PH_, UW_, UH_>(a, w.sjobs, w.perm, sc.class_off[ID], sc.class_cnt[ID], blk, klds); \
+    lane_unit<PW_, PH_, UW_, UH_>(a, w.sjobs, w.perm, sc->class_off[ID], sc->class_cnt[ID], blk, klds); \
     break;
 #define FME_LANE_KERNEL(NAME, KID, LIST, WAVES)                                                      \
   __global__ __launch_bounds__(kLaneNT) __attribute__((amdgpu_waves_per_eu(WAVES)))                 \
-  void NAME(BatchArgs a, WorkBufs w, Schedule sc) {                                                  \
+  void NAME(BatchArgs a, WorkBufs w) {                                                               \
     __shared__ uint32_t klds_[FME_LANE_KLDS ? 8 * kLaneNT * 4 : 1];                                  \
+    __shared__ int32_t claim[2];                                                                     \
     uint32_t* klds = klds_;                                                                          \
-    const int b = blockIdx.x;                                                                        \
-    int c = 0;                                                                                       \
-    while (c < kNumClasses - 1 && b >= sc.prefix[KID][c + 1]) c++;                                   \
-    const int nblk = sc.prefix[KID][c + 1] - sc.prefix[KID][c];                                      \
-    const int blk = xcd_block(b - sc.prefix[KID][c], nblk);                                          \
-    switch (c) {                                                                                     \
-      LIST(FME_CASE)                                                                                 \
-      default: break;                                                                                \
+    const Schedule* __restrict__ sc = w.sched;                                                       \
+    int32_t* ctr = w.tile_ctr + KID * 8;                                                             \
+    const int home = xcc_id();                                                                       \
+    int x = home, tried = 0, par = 0;                                                                \
+    if (threadIdx.x == 0) claim[0] = atomicAdd(&ctr[x], 1);                                          \
+    __syncthreads();                                                                                 \
+    int t = __builtin_amdgcn_readfirstlane(claim[0]);                                                \
+    while (true) {                                                                                   \
+      if (t >= sc->xq[KID][x][kNumClasses]) {   /* queue drained: the next XCD's */                  \
+        if (++tried == 8) break;                                                                     \
+        x = (home + tried) & 7;                                                                      \
+        par ^= 1;                                                                                    \
+        if (threadIdx.x == 0) claim[par] = atomicAdd(&ctr[x], 1);                                    \
+        __syncthreads();                                                                             \
+        t = __builtin_amdgcn_readfirstlane(claim[par]);                                              \
+        continue;                                                                                    \
+      }                                                                                              \
+      int nxt = 0;                                                                                   \
+      if (threadIdx.x == 0) nxt = atomicAdd(&ctr[x], 1);                                             \
+      int c = 0;                                                                                     \
+      while (c < kNumClasses - 1 && t >= sc->xq[KID][x][c + 1]) c++;                                 \
+      const int nblk = sc->prefix[KID][c + 1] - sc->prefix[KID][c];                                  \
+      const int blk = x * (nblk >> 3) + min(x, nblk & 7) + (t - sc->xq[KID][x][c]);                  \
+      switch (c) {                                                                                   \
+        LIST(FME_CASE)                                                                               \
+        default: break;                                                                              \
+      }                                                                                              \
+      par ^= 1;                                                                                      \
+      if (threadIdx.x == 0) claim[par] = nxt;                                                        \
+      __syncthreads();                                                                               \
+      t = __builtin_amdgcn_readfirstlane(claim[par]);                                                \
     }                                                                                                \
   }
-#ifndef FME_LANE_ONLY88
 FME_LANE_KERNEL(k_search_lane48, kSearchLane48, FME_LANE48_CLASSES, FME_LANE_WAVES_SMALL)
-#endif
-#ifndef FME_LANE_ONLY48
-#ifndef FME_LANE_ONLY88
 FME_LANE_KERNEL(k_search_lane84, kSearchLane84, FME_LANE84_CLASSES, FME_LANE_WAVES_SMALL)
-#endif
 FME_LANE_KERNEL(k_search_lane88, kSearchLane88, FME_LANE88_CLASSES, FME_LANE_WAVES_88)
-#endif
 #undef FME_CASE
 #undef FME_LANE_KERNEL
 
@@ -849,30 +870,33 @@ int lane_kernel_of(int cls) {
   }
 }
 
-hipError_t launch_search_lane(const BatchArgs& a, const WorkBufs& w, const Schedule& sc, hipStream_t s) {
-  int blocks = 0;
-#ifndef FME_LANE_ONLY88
-  blocks = sc.prefix[kSearchLane48][kNumClasses];
-  if (blocks > 0) hipLaunchKernelGGL(k_search_lane48, dim3(blocks), dim3(kLaneNT), 0, s, a, w, sc);
-#endif
-#ifndef FME_LANE_ONLY48
-  blocks = sc.prefix[kSearchLane88][kNumClasses];
-  if (blocks > 0) hipLaunchKernelGGL(k_search_lane88, dim3(blocks), dim3(kLaneNT), 0, s, a, w, sc);
-#ifndef FME_LANE_ONLY88
-  blocks = sc.prefix[kSearchLane84][kNumClasses];
-  if (blocks > 0) hipLaunchKernelGGL(k_search_lane84, dim3(blocks), dim3(kLaneNT), 0, s, a, w, sc);
-#endif
-#endif
-  return hipGetLastError();
+// Workgroups of one lane-kernel launch: at most the tiles n jobs could need, at most what the
+// chip holds at 4 workgroups per CU (the kernels reach 2-3; spare workgroups find the queues
+// drained and exit).
+static int lane_grid(int kern, int n) {
+  static int cus = 0;
+  if (!cus) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    cus = cu_count(dev);
+  }
+  int max_l = 0, classes = 0;
+  for (int c = 0; c < kNumClasses; c++)
+    if (lane_kernel_of(c) == kern) {
+      max_l = std::max(max_l, lane_lanes_per_pu(c));
+      classes++;
+    }
+  if (!classes) return 0;
+  const long long bound = ((long long)n * max_l + kLaneNT - 1) / kLaneNT + classes;
+  return (int)std::min<long long>(bound, 4LL * cus);
 }
 
-hipError_t launch_search_lane_one(const BatchArgs& a, const WorkBufs& w, const Schedule& sc, int kern,
-                                  hipStream_t s) {
-  const int blocks = sc.prefix[kern][kNumClasses];
+hipError_t launch_search_lane_one(const BatchArgs& a, const WorkBufs& w, int kern, hipStream_t s) {
+  const int blocks = lane_grid(kern, a.n);
   if (blocks <= 0) return hipSuccess;
-  if (kern == kSearchLane48) hipLaunchKernelGGL(k_search_lane48, dim3(blocks), dim3(kLaneNT), 0, s, a, w, sc);
-  else if (kern == kSearchLane84) hipLaunchKernelGGL(k_search_lane84, dim3(blocks), dim3(kLaneNT), 0, s, a, w, sc);
-  else if (kern == kSearchLane88) hipLaunchKernelGGL(k_search_lane88, dim3(blocks), dim3(kLaneNT), 0, s, a, w, sc);
+  if (kern == kSearchLane48) hipLaunchKernelGGL(k_search_lane48, dim3(blocks), dim3(kLaneNT), 0, s, a, w);
+  else if (kern == kSearchLane84) hipLaunchKernelGGL(k_search_lane84, dim3(blocks), dim3(kLaneNT), 0, s, a, w);
+  else if (kern == kSearchLane88) hipLaunchKernelGGL(k_search_lane88, dim3(blocks), dim3(kLaneNT), 0, s, a, w);
   else return hipErrorInvalidValue;
   return hipGetLastError();
 }

@@ -283,6 +283,13 @@ __global__ __launch_bounds__(kRound) void k_nn_deep_tail(BatchArgs a, WorkBufs w
   T* act = reinterpret_cast<T*>(smem_raw) + (MFMA ? wid * 64 * kAS : 0);
   const uint32_t* st_in = w.nn_state + 12 * state_in;
   uint32_t* st_out = w.nn_state + 12 * (state_in ^ 1);
+  if (w.sched->invalid) {
+    for (int rnd = 0; rnd < kRounds; rnd++) {
+      const int i = blockIdx.x * kJobsPerScanBlock + rnd * kRound + tid;
+      if (i < a.n) reject_job(a, w, i, state_in);
+    }
+    return;
+  }
 
   int carry[9];
 #pragma unroll
@@ -366,7 +373,6 @@ __global__ __launch_bounds__(kRound) void k_nn_deep_tail(BatchArgs a, WorkBufs w
     uint16_t status = 0;
     if (!(j.flags & FME_JOB_EMI) || r->n_emi < 8) status |= FME_RES_NN_STALE;
     if ((written & 0x1FFu) != 0x1FFu) status |= FME_RES_NN_UNINIT;
-    r->nn_class = (uint8_t)cls;
     if (i == a.n - 1) {
 #pragma unroll
       for (int s = 0; s < 8; s++) st_out[s] = e[s];
@@ -376,16 +382,13 @@ __global__ __launch_bounds__(kRound) void k_nn_deep_tail(BatchArgs a, WorkBufs w
       st_out[11] = written;
     }
     const int fx = 4 * r->mv_int_x + cls % 7 - 3, fy = 4 * r->mv_int_y + cls / 7 - 3;
-    r->mv_x = (int16_t)fx;
-    r->mv_y = (int16_t)fy;
     const double ml = a.mlambda[j.lambda_id];
     const uint32_t mvb = mv_bits(fx, fy, 0, j.mvp_x, j.mvp_y);
     const uint32_t bits = (uint32_t)j.bits_in + mvb;
-    r->bits = bits;
     const double fw = (j.flags & FME_JOB_BIPRED) ? 0.5 : 1.0;
     const double val = floor(fw * ((double)r->frac_cost - (double)mv_cost(ml, mvb))) + (double)mv_cost(ml, bits);
-    r->cost = (uint32_t)(int64_t)val;   // gcc/x86-64 (Distortion)(double) semantics
-    r->status = status;
+    // gcc/x86-64 (Distortion)(double) semantics for the cost
+    store_outputs(r, w.mv_out, i, fx, fy, (uint32_t)(int64_t)val, bits, (uint8_t)cls, status);
   }
 }
 

@@ -20,6 +20,8 @@
 // butterfly is folded with |a+b| + |a-b| = 2 max(|a|,|b|).
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+
 #include "fme_device.h"
 #include "fme_simd.h"
 
@@ -824,39 +826,49 @@ __device__ __forceinline__ int xcd_tile(int r, int n) {
 #endif
 }
 
-__global__ __launch_bounds__(kSmallNT) void k_search_small(BatchArgs a, WorkBufs w, Schedule sc) {
+// The schedule is device-built (k_schedule), so the grid is a fixed multiple of 8 workgroups
+// that strides over the kernel's blocks (block b keeps XCD b % 8, as with one block each).
+__global__ __launch_bounds__(kSmallNT) void k_search_small(BatchArgs a, WorkBufs w) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
-  const int b = blockIdx.x;
-  const int c = find_class(sc.prefix[kSearchCoop], b);
-  const int nblk = sc.prefix[kSearchCoop][c + 1] - sc.prefix[kSearchCoop][c];
-  const int blk = xcd_tile(b - sc.prefix[kSearchCoop][c], nblk);
-  switch (c) {
+  const Schedule* __restrict__ sc = w.sched;
+  const int total = sc->prefix[kSearchCoop][kNumClasses];
+  for (int b = blockIdx.x; b < total; b += gridDim.x) {
+    const int c = find_class(sc->prefix[kSearchCoop], b);
+    const int nblk = sc->prefix[kSearchCoop][c + 1] - sc->prefix[kSearchCoop][c];
+    const int blk = xcd_tile(b - sc->prefix[kSearchCoop][c], nblk);
+    switch (c) {
 #define FME_CASE(ID, W_, H_)                                                                        \
   case ID:                                                                                          \
-    search_class<W_, H_, kSmallNT, kSmallBudget>(a, w.sjobs, w.perm, sc.class_off[ID],               \
-                                                 sc.class_cnt[ID], blk, nblk, lds);                 \
+    search_class<W_, H_, kSmallNT, kSmallBudget>(a, w.sjobs, w.perm, sc->class_off[ID],              \
+                                                 sc->class_cnt[ID], blk, nblk, lds);                \
     break;
-    FME_SMALL_CLASSES(FME_CASE)
+      FME_SMALL_CLASSES(FME_CASE)
 #undef FME_CASE
-    default: break;
+      default: break;
+    }
+    __syncthreads();   // LDS is reused by the next block's tiles
   }
 }
 
-__global__ __launch_bounds__(kLargeNT) void k_search_large(BatchArgs a, WorkBufs w, Schedule sc) {
+__global__ __launch_bounds__(kLargeNT) void k_search_large(BatchArgs a, WorkBufs w) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
-  const int b = blockIdx.x;
-  const int c = find_class(sc.prefix[kSearchCoopLarge], b);
-  const int nblk = sc.prefix[kSearchCoopLarge][c + 1] - sc.prefix[kSearchCoopLarge][c];
-  const int blk = xcd_tile(b - sc.prefix[kSearchCoopLarge][c], nblk);
-  switch (c) {
+  const Schedule* __restrict__ sc = w.sched;
+  const int total = sc->prefix[kSearchCoopLarge][kNumClasses];
+  for (int b = blockIdx.x; b < total; b += gridDim.x) {
+    const int c = find_class(sc->prefix[kSearchCoopLarge], b);
+    const int nblk = sc->prefix[kSearchCoopLarge][c + 1] - sc->prefix[kSearchCoopLarge][c];
+    const int blk = xcd_tile(b - sc->prefix[kSearchCoopLarge][c], nblk);
+    switch (c) {
 #define FME_CASE(ID, W_, H_)                                                                        \
   case ID:                                                                                          \
-    search_class<W_, H_, kLargeNT, kLargeBudget>(a, w.sjobs, w.perm, sc.class_off[ID],               \
-                                                 sc.class_cnt[ID], blk, nblk, lds);                 \
+    search_class<W_, H_, kLargeNT, kLargeBudget>(a, w.sjobs, w.perm, sc->class_off[ID],              \
+                                                 sc->class_cnt[ID], blk, nblk, lds);                \
     break;
-    FME_LARGE_CLASSES(FME_CASE)
+      FME_LARGE_CLASSES(FME_CASE)
 #undef FME_CASE
-    default: break;
+      default: break;
+    }
+    __syncthreads();
   }
 }
 
@@ -907,15 +919,37 @@ int search_blocks_for(int cls, int cnt) {
   return (tiles + tpb - 1) / tpb;
 }
 
-static size_t lds_max(const Schedule& sc, int kernel) {
+static size_t lds_max(int kernel) {
   size_t m = 0;
   for (int c = 0; c < kNumClasses; c++)
-    if (sc.class_cnt[c] && search_kernel_of(c) == kernel && lds_bytes_for_class(c) > m) m = lds_bytes_for_class(c);
+    if (search_kernel_of(c) == kernel && lds_bytes_for_class(c) > m) m = lds_bytes_for_class(c);
   return m;
 }
 
-hipError_t launch_search_large(const BatchArgs& a, const WorkBufs& w, const Schedule& sc, hipStream_t s) {
-  const int blocks = sc.prefix[kSearchCoopLarge][kNumClasses];
+// Workgroups of a cooperative launch: at most the blocks n jobs could need (the smallest tile of
+// the kernel's classes), at most 2 per CU, a multiple of 8 (XCD round robin).
+static int coop_grid(int kernel, int n) {
+  static int cus = 0;
+  if (!cus) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    cus = cu_count(dev);
+  }
+  int min_p = 1 << 30, classes = 0;
+  for (int c = 0; c < kNumClasses; c++)
+    if (search_kernel_of(c) == kernel) {
+      min_p = std::min(min_p, pus_per_tile(c));
+      classes++;
+    }
+  if (!classes) return 0;
+  const long long tiles = (long long)n / min_p + classes;
+  const long long bound = (tiles + tiles_per_block() - 1) / tiles_per_block() + classes;
+  const long long g = std::min<long long>(bound, 2LL * cus);
+  return (int)((g + 7) / 8 * 8);
+}
+
+hipError_t launch_search_large(const BatchArgs& a, const WorkBufs& w, hipStream_t s) {
+  const int blocks = coop_grid(kSearchCoopLarge, a.n);
   if (blocks <= 0) return hipSuccess;
   static bool attr_set = false;
   if (!attr_set) {
@@ -924,14 +958,14 @@ hipError_t launch_search_large(const BatchArgs& a, const WorkBufs& w, const Sche
     if (e != hipSuccess) return e;
     attr_set = true;
   }
-  hipLaunchKernelGGL(k_search_large, dim3(blocks), dim3(kLargeNT), lds_max(sc, kSearchCoopLarge), s, a, w, sc);
+  hipLaunchKernelGGL(k_search_large, dim3(blocks), dim3(kLargeNT), lds_max(kSearchCoopLarge), s, a, w);
   return hipGetLastError();
 }
 
-hipError_t launch_search_small(const BatchArgs& a, const WorkBufs& w, const Schedule& sc, hipStream_t s) {
-  const int blocks = sc.prefix[kSearchCoop][kNumClasses];
+hipError_t launch_search_small(const BatchArgs& a, const WorkBufs& w, hipStream_t s) {
+  const int blocks = coop_grid(kSearchCoop, a.n);
   if (blocks <= 0) return hipSuccess;
-  hipLaunchKernelGGL(k_search_small, dim3(blocks), dim3(kSmallNT), lds_max(sc, kSearchCoop), s, a, w, sc);
+  hipLaunchKernelGGL(k_search_small, dim3(blocks), dim3(kSmallNT), lds_max(kSearchCoop), s, a, w);
   return hipGetLastError();
 }
 

@@ -628,7 +628,7 @@ __device__ __forceinline__ int tz_group_lanes(int PW, int PH, int UW, int UH) {
 // pass 1: the class's PUs in groups of L lanes, blocks dealt to the XCDs in contiguous ranges
 template <int UW, int UH>
 __global__ __launch_bounds__(kTzNT) __attribute__((amdgpu_waves_per_eu(FME_TZ_WAVES)))
-void k_tz(TzArgs ta, Schedule sc, int kid) {
+void k_tz(TzArgs ta, TzSchedule sc, int kid) {
   const int b = blockIdx.x;
   int c = 0;
   while (c < kNumClasses - 1 && b >= sc.prefix[kid][c + 1]) c++;
@@ -647,7 +647,7 @@ void k_tz(TzArgs ta, Schedule sc, int kid) {
 #endif
 template <int UW, int UH>
 __global__ __launch_bounds__(kTzNT) __attribute__((amdgpu_waves_per_eu(FME_TZR_WAVES)))
-void k_tz_raster(TzArgs ta, Schedule sc, int kid, int nq) {
+void k_tz_raster(TzArgs ta, TzSchedule sc, int kid, int nq) {
   const int wv = (int)(blockIdx.x * (kTzNT / 64) + (threadIdx.x >> 6));
   if (wv >= nq) return;
   const int jid = ta.rq[(size_t)kid * ta.a.n + wv];
@@ -675,7 +675,7 @@ int tz_lanes_per_pu(int cls) {
 
 // One unit-shape kernel (kid 0: 4x8 units, 1: 8x4, 2: 8x8); the three are independent and the
 // runtime runs them on separate streams.
-hipError_t launch_tz(const TzArgs& ta, const Schedule& sc, int kid, hipStream_t s) {
+hipError_t launch_tz(const TzArgs& ta, const TzSchedule& sc, int kid, hipStream_t s) {
   const int blocks = sc.prefix[kid][kNumClasses];
   if (blocks <= 0) return hipSuccess;
   if (kid == 0) hipLaunchKernelGGL((k_tz<4, 8>), dim3(blocks), dim3(kTzNT), 0, s, ta, sc, 0);
@@ -685,7 +685,7 @@ hipError_t launch_tz(const TzArgs& ta, const Schedule& sc, int kid, hipStream_t 
 }
 
 // The raster searches pass 1 queued for kernel kid (nq of them, read back by the host).
-hipError_t launch_tz_raster(const TzArgs& ta, const Schedule& sc, int kid, int nq, hipStream_t s) {
+hipError_t launch_tz_raster(const TzArgs& ta, const TzSchedule& sc, int kid, int nq, hipStream_t s) {
   if (nq <= 0) return hipSuccess;
   const int blocks = (nq + kTzNT / 64 - 1) / (kTzNT / 64);
   if (kid == 0) hipLaunchKernelGGL((k_tz_raster<4, 8>), dim3(blocks), dim3(kTzNT), 0, s, ta, sc, 0, nq);

@@ -33,6 +33,15 @@ RESULT_DTYPE = np.dtype(
 )
 assert RESULT_DTYPE.itemsize == 64
 
+# fme_mv_result (16 B): xMotionEstimation's outputs alone (fme_refine_mv*)
+MV_RESULT_DTYPE = np.dtype(
+    [("mv_x", "<i2"), ("mv_y", "<i2"), ("cost", "<u4"), ("bits", "<u4"),
+     ("nn_class", "u1"), ("reserved", "u1"), ("status", "<u2")],
+    align=False,
+)
+assert MV_RESULT_DTYPE.itemsize == 16
+MV_FIELDS = ("mv_x", "mv_y", "cost", "bits", "nn_class", "status")
+
 # fme_mc_job (24 B): one PU of motion compensation (include/fme.h)
 MC_JOB_DTYPE = np.dtype(
     [
@@ -101,6 +110,7 @@ JOB_LOSSLESS = 0x04
 
 RES_NN_STALE = 0x01
 RES_NN_UNINIT = 0x02
+RES_REJECTED = 0x8000
 
 MAX_PICTURES = 64
 MAX_LAMBDAS = 64

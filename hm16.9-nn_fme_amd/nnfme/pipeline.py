@@ -1,0 +1,232 @@
+"""Frame replay: the sub-pel path over a stream of frames, as SURVEY.md §8(d) times it.
+
+Per step (one batch of xMotionEstimation jobs = one frame, or a group of F small frames so that
+a launch fills the chip):
+  * H2D of the batch's job descriptors, of the frames' original pictures and of one
+    reconstructed reference picture per frame (trace replay: frame f's references are the
+    reconstructions of f-1..f-4; each is uploaded once, by the rank that publishes it, and
+    broadcast to every rank over RCCL/xGMI when the run is sharded);
+  * fme_refine_mv_device (EMI step -> FracDIF -> NN_pred -> cost tail, no host synchronisation);
+  * D2H of the 16-byte fme_mv_result per job.
+Two steps are in flight: the uploads of step k+1 and the download of step k-1 run on their own
+streams while step k computes (events order the double-buffered job / output slots).
+
+Sharding (world > 1): rank r replays batches r, r + world, ... (weak scaling; no collective on
+the data path besides the picture broadcasts).  NN_pred's carried state crosses frames in the
+reference, so every batch starts from a reset state, each batch's end state is copied on the
+device (fme_nn_copy_state_device), and after the run the states are all-gathered (12 words per
+batch), chained in encode order (nnfme.dist.chain_states) and the jobs up to each batch's last
+carried-state reader are refined again with the true carry-in: the result equals a sequential
+run bit for bit (tests/test_gpu_dist.py).  Every picture stays resident in HBM for the run
+(288 GB per GPU), so the fix-up moves nothing over PCIe but the prefix's jobs.
+
+Picture slots of a batch of F frames (frames G*F .. G*F+F-1 of batch G): reconstruction of
+frame G*F - 4 + s in slot s (s < F + 3), original of frame G*F + j in slot ORG0 + j; frame j's
+reference at distance d (the base job's ref_id = d - 1) is slot j + 4 - d, its lambda slot j.
+"""
+import ctypes
+
+import numpy as np
+
+from . import dist as fdist
+from .abi import JOB_DTYPE, MV_RESULT_DTYPE
+
+_hip = None
+
+
+def _memcpy_async(dst, src, nbytes, kind, stream):
+    """hipMemcpyAsync between pinned host and device memory on `stream` (a torch stream): the
+    copy engines (SDMA) carry it.  (A torch D2H copy_ runs as a blit kernel on the CUs, which
+    then waits for the search kernels' workgroups.)"""
+    global _hip
+    if _hip is None:
+        _hip = ctypes.CDLL("libamdhip64.so.7")   # by SONAME: the runtime torch and libfme_amd.so share
+        _hip.hipMemcpyAsync.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int,
+                                        ctypes.c_void_p]
+        _hip.hipMemcpyAsync.restype = ctypes.c_int
+    rc = _hip.hipMemcpyAsync(dst.data_ptr(), src.data_ptr(), nbytes, kind, stream.cuda_stream)
+    if rc != 0:
+        raise RuntimeError(f"hipMemcpyAsync failed ({rc})")
+
+
+H2D, D2H = 1, 2
+
+
+def torch_current_stream(t):
+    import torch
+    return torch.cuda.current_stream(t.device)
+
+
+ORG0 = 32      # first original-picture slot
+REFS = 4       # lowdelay_P / the workloads' reference count
+
+
+def group_jobs(base, frames):
+    """The job batch of a group of `frames` frames: the base frame's jobs (org_id anything,
+    ref_id = reference distance - 1 in 0..3, lambda slot 0) once per frame, slots remapped."""
+    out = []
+    for j in range(frames):
+        g = np.array(base, dtype=JOB_DTYPE, copy=True)
+        g["org_id"] = ORG0 + j
+        g["ref_id"] = j + 3 - base["ref_id"].astype(np.int64)
+        g["lambda_id"] = j
+        out.append(g)
+    return np.concatenate(out)
+
+
+class FrameReplay:
+    def __init__(self, ctx, base_jobs, pool, lambda_of, n_steps, frames_per_step=1, world=1, rank=0, device=None,
+                 group=None):
+        """ctx: an FmeContext on `device`; base_jobs: one frame's jobs (ref_id = reference
+        distance - 1); pool: uint8 [P, H, W] host frames, frame g's pictures are pool[g % P];
+        lambda_of(g): frame g's lambda."""
+        import torch
+        self.torch, self.ctx = torch, ctx
+        self.world, self.rank, self.group = world, rank, group
+        self.F = F = frames_per_step
+        self.lambda_of = lambda_of
+        self.steps = n_steps
+        P, H, W = pool.shape
+        self.P, self.H, self.W = P, H, W
+        self.pool = torch.from_numpy(np.ascontiguousarray(pool)).pin_memory()
+        self.jobs = group_jobs(base_jobs, F)
+        self.n = n = len(self.jobs)
+        self.h_jobs = torch.from_numpy(self.jobs.view(np.uint8).copy()).pin_memory()
+        self.d_jobs = [torch.empty(n * JOB_DTYPE.itemsize, dtype=torch.uint8, device=device) for _ in range(2)]
+        self.d_out = [torch.empty(n * MV_RESULT_DTYPE.itemsize, dtype=torch.uint8, device=device) for _ in range(2)]
+        self.h_out = torch.empty((n_steps, n * MV_RESULT_DTYPE.itemsize), dtype=torch.uint8).pin_memory()
+        frames = n_steps * world * F
+        # every reconstructed picture of the run (frames -4 .. frames - 1) and this rank's originals
+        self.recon = torch.empty((frames + REFS, H, W), dtype=torch.uint8, device=device)
+        self.org = torch.empty((n_steps * F, H, W), dtype=torch.uint8, device=device)
+        self.states = torch.zeros((n_steps, 12), dtype=torch.int32, device=device)
+        self.s_comp = torch.cuda.default_stream(device)
+        self.s_copy = torch.cuda.Stream(device)
+        self.uploaded = -1
+        self.ev_in = [torch.cuda.Event() for _ in range(2)]
+        self.ev_comp = [torch.cuda.Event() for _ in range(2)]
+        self.ev_out = [torch.cuda.Event() for _ in range(2)]
+        self.fixed_jobs = 0
+
+    def first_frame(self, k):
+        """First frame of this rank's step k."""
+        return (k * self.world + self.rank) * self.F
+
+    # -- pictures ---------------------------------------------------------------------------
+    def _publish(self, g, src_rank):
+        """Reconstruction of frame g: uploaded by src_rank, broadcast to every rank."""
+        dst = self.recon[g + REFS]
+        if self.rank == src_rank:
+            _memcpy_async(dst, self.pool[g % self.P], self.H * self.W, H2D, torch_current_stream(dst))
+        if self.world > 1:
+            import torch.distributed as dist
+            if dist.get_backend(self.group) == "gloo":   # CPU rehearsal of the sharded path
+                tmp = dst.cpu()
+                dist.broadcast(tmp, src=src_rank, group=self.group)
+                dst.copy_(tmp, non_blocking=False)
+            else:
+                dist.broadcast(dst, src=src_rank, group=self.group)
+
+    def prime(self):
+        """References of the first frames (recon -4 .. -2), before the run (untimed)."""
+        with self.torch.cuda.stream(self.s_copy):
+            for g in range(-REFS, -1):
+                self._publish(g, 0)
+        self.s_copy.synchronize()
+
+    def _bind(self, k):
+        ctx, W, H, F = self.ctx, self.W, self.H, self.F
+        f0 = self.first_frame(k)
+        for j in range(F):
+            ctx.bind_picture_device(ORG0 + j, self.org[k * F + j].data_ptr(), W, W, H)
+            ctx.set_lambda(j, self.lambda_of(f0 + j))
+        for s in range(F + REFS - 1):
+            ctx.bind_picture_device(s, self.recon[f0 - REFS + s + REFS].data_ptr(), W, W, H)
+
+    # -- one step -----------------------------------------------------------------------------
+    # Streams: the batch runs on the device's default stream, every copy on one copy stream, in
+    # the order U(0), U(1), D(0), U(2), D(1), ...: the upload of step k+1 is queued before the
+    # download of step k, so it overlaps step k's batch, and the download overlaps step k+1's.
+    # (With the library's two auxiliary streams that is four streams = the process's four hardware
+    # queues (GPU_MAX_HW_QUEUES): more streams share queues, and a copy stream's event waits then
+    # block kernels queued behind them.)
+    def _upload(self, k):
+        F = self.F
+        b = k & 1
+        f0 = self.first_frame(k)
+        cp = self.s_copy
+        with self.torch.cuda.stream(cp):
+            if k >= 2:
+                cp.wait_event(self.ev_comp[b])            # step k-2 is done with the slot
+            _memcpy_async(self.d_jobs[b], self.h_jobs, self.h_jobs.numel(), H2D, cp)
+            for j in range(F):
+                _memcpy_async(self.org[k * F + j], self.pool[(f0 + j) % self.P], self.H * self.W, H2D, cp)
+            base = k * self.world * F
+            for r in range(self.world):   # recon(first frame of rank r's batch - 1 + j), by rank r
+                for j in range(F):
+                    self._publish(base + r * F + j - 1, r)
+            self.ev_in[b].record(cp)
+        self.uploaded = k
+
+    def issue(self, k, prefetch=True):
+        """Enqueue step k (and, with prefetch, the upload of step k+1); returns without waiting
+        for the device."""
+        ctx = self.ctx
+        b = k & 1
+        if self.uploaded < k:
+            self._upload(k)
+        comp = self.s_comp
+        comp.wait_event(self.ev_in[b])
+        if k >= 2:
+            comp.wait_event(self.ev_out[b])                # step k-2's results have left
+        self._bind(k)
+        if self.world > 1:
+            ctx.nn_reset()                                 # stream-ordered: this batch starts fresh
+        ctx.refine_mv_device(self.d_jobs[b].data_ptr(), self.d_out[b].data_ptr(), self.n, comp.cuda_stream)
+        if self.world > 1:
+            ctx.nn_copy_state_device(self.states[k].data_ptr(), comp.cuda_stream)
+        self.ev_comp[b].record(comp)
+        if prefetch and k + 1 < self.steps:
+            self._upload(k + 1)
+        cp = self.s_copy
+        cp.wait_event(self.ev_comp[b])
+        _memcpy_async(self.h_out[k], self.d_out[b], self.h_out.shape[1], D2H, cp)
+        self.ev_out[b].record(cp)
+
+    def results(self, k):
+        return self.h_out[k].numpy().view(MV_RESULT_DTYPE)
+
+    # -- end of the run -----------------------------------------------------------------------
+    def finish(self, first_step=0):
+        """Wait for every step; when sharded, chain the NN states and refine each batch's
+        carried-state prefix again (steps >= first_step).  Returns the number of re-run jobs."""
+        torch = self.torch
+        self.s_copy.synchronize()
+        self.s_comp.synchronize()
+        if self.world == 1:
+            return 0
+        import torch.distributed as dist
+        st = self.states if dist.get_backend(self.group) != "gloo" else self.states.cpu()
+        gathered = [torch.zeros_like(st) for _ in range(self.world)]
+        dist.all_gather(gathered, st, group=self.group)
+        bs = np.zeros((self.steps * self.world, 12), np.uint32)
+        for r in range(self.world):
+            g = gathered[r].cpu().numpy().view(np.uint32)
+            for k in range(self.steps):
+                bs[k * self.world + r] = g[k]
+        carries, _ = fdist.chain_states(bs)
+        fixed = 0
+        ctx, comp = self.ctx, self.s_comp
+        for k in range(first_step, self.steps):
+            out = self.results(k)
+            p = fdist.uninit_prefix(out)
+            carry = carries[k * self.world + self.rank]
+            if p == 0 or not int(carry[11]):
+                continue
+            with torch.cuda.stream(comp):
+                self._bind(k)
+                ctx.nn_set_state(carry)
+                out[:p] = ctx.refine_mv(self.jobs[:p], comp.cuda_stream)
+            fixed += p
+        self.fixed_jobs = fixed
+        return fixed

@@ -9,13 +9,13 @@ import os
 
 import numpy as np
 
-from .abi import JOB_DTYPE, NN_PARAMS, RESULT_DTYPE
+from .abi import JOB_DTYPE, MV_RESULT_DTYPE, NN_PARAMS, RESULT_DTYPE
 from .weights import load_weights
 
 PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB_PATH = os.environ.get("FME_LIB_PATH") or os.path.join(PKG_ROOT, "libfme_amd.so")
 
-ABI_VERSION = 4
+ABI_VERSION = 5
 TIMING_NAMES = ("classify", "scatter", "search", "nn_tail", "batch", "search_main", "search_aux")
 
 # Every entry point include/fme.h declares (the ABI test checks the .so exports them).
@@ -29,7 +29,8 @@ ABI_SYMBOLS = (
     "fme_motion_compensate_device", "fme_mc_invalid_count", "fme_mc_last_ms",
     "fme_integer_search", "fme_integer_search_device", "fme_integer_search_last_ms",
     "fme_pred_inter_p", "fme_pred_inter_reset", "fme_nn_param_count", "fme_load_nn_net",
-    "fme_set_nn_engine", "fme_set_nn_margin_output",
+    "fme_set_nn_engine", "fme_set_nn_margin_output", "fme_refine_mv", "fme_refine_mv_device",
+    "fme_refine_status", "fme_nn_copy_state_device",
 )
 
 
@@ -95,6 +96,10 @@ def load_library(path=None):
         "fme_load_nn_net": (I, [P, P, P, I]),
         "fme_set_nn_engine": (I, [P, I]),
         "fme_set_nn_margin_output": (I, [P, P]),
+        "fme_refine_mv": (I, [P, P, P, I, P]),
+        "fme_refine_mv_device": (I, [P, P, P, I, P]),
+        "fme_refine_status": (I, [P]),
+        "fme_nn_copy_state_device": (I, [P, P, P]),
     }
     for name, (res, args) in sig.items():
         f = getattr(lib, name)
@@ -278,8 +283,30 @@ class FmeContext:
         return res
 
     def refine_device(self, jobs_ptr, res_ptr, n, stream=None):
-        """Device-resident jobs/results (e.g. torch uint8 tensors' data_ptr())."""
+        """Device-resident jobs/results (e.g. torch uint8 tensors' data_ptr()); asynchronous on
+        `stream` (no host synchronisation).  A rejected batch shows in refine_status()."""
         _check(self.lib, self.lib.fme_refine_device(self.h, C.c_void_p(jobs_ptr), C.c_void_p(res_ptr), n, stream))
+
+    def refine_mv(self, jobs, stream=None):
+        """fme_refine_mv: the 16-byte xMotionEstimation outputs (MV_RESULT_DTYPE) per job."""
+        jobs = np.ascontiguousarray(jobs, dtype=JOB_DTYPE)
+        out = np.zeros(len(jobs), dtype=MV_RESULT_DTYPE)
+        _check(self.lib, self.lib.fme_refine_mv(self.h, _ptr(jobs), _ptr(out), len(jobs), stream))
+        return out
+
+    def refine_mv_device(self, jobs_ptr, out_ptr, n, stream=None):
+        _check(self.lib, self.lib.fme_refine_mv_device(self.h, C.c_void_p(jobs_ptr), C.c_void_p(out_ptr), n, stream))
+
+    def refine_status(self):
+        """Waits for the last batch: the number of jobs that made the device reject it (0: ran)."""
+        rc = self.lib.fme_refine_status(self.h)
+        if rc < 0:
+            _check(self.lib, rc)
+        return rc
+
+    def nn_copy_state_device(self, d_ptr, stream=None):
+        """Enqueue a copy of the carried NN state (12 words) to device memory at d_ptr."""
+        _check(self.lib, self.lib.fme_nn_copy_state_device(self.h, C.c_void_p(d_ptr), stream))
 
     def frac_dif_single(self, key, ref_window, ref_origin, mv_int, mvp, motion_lambda, lossless=False):
         """xPatternSearchFracDIF argument list: key block (int16 HxW), a padded reference

@@ -225,6 +225,40 @@ def lambdas_for_frame(qp, poc):
     return LDP_LAMBDA[qp if qp in LDP_LAMBDA else 22][poc % 4]
 
 
+# randomaccess_main GOP (cfg/encoder_randomaccess_main.cfg Frame1..8): (POC, QPoffset, QPFactor)
+RA_GOP = ((8, 1, 0.442), (4, 2, 0.3536), (2, 3, 0.3536), (1, 4, 0.68), (3, 4, 0.68), (6, 3, 0.3536),
+          (5, 4, 0.68), (7, 4, 0.68))
+
+
+def ra_depth(poc, gop=8):
+    """TEncSlice.cpp:165-199: depth of a POC in a GOP (0 for the GOP's key POC; the loop also
+    counts the level at which the POC is found)."""
+    poc %= gop
+    if poc == 0:
+        return 0
+    depth, step, i = 0, gop, gop >> 1
+    while i >= 1:
+        found = any(j == poc for j in range(i, gop, step))
+        step >>= 1
+        depth += 1
+        if found:
+            break
+        i >>= 1
+    return depth
+
+
+def ra_lambda(qp, gop_entry):
+    """Lambda of a random-access B slice (TEncSlice.cpp:246-325 with HadamardME on: no 0.95):
+    QPFactor * 2^((QP + QPoffset - 12) / 3), times Clip3(2, 4, (QP + QPoffset - 12) / 6) below the
+    GOP's top layer."""
+    poc, off, factor = RA_GOP[gop_entry % 8]
+    qp_temp = float(qp + off - 12)
+    lam = factor * 2.0 ** (qp_temp / 3.0)
+    if ra_depth(poc) > 0:
+        lam *= min(4.0, max(2.0, qp_temp / 6.0))
+    return lam
+
+
 def jobs_per_frame(width, height, refs=4, calls_per_ctu=423):
     ctus = ((width + 63) // 64) * ((height + 63) // 64)
     return ctus * calls_per_ctu * refs

@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define FME_ABI_VERSION 4
+#define FME_ABI_VERSION 5
 
 /* ---- error codes ---------------------------------------------------------------- */
 #define FME_OK            0
@@ -104,6 +104,8 @@ typedef struct fme_job {
  */
 #define FME_RES_NN_STALE   0x01u  /* NN read at least one slot not written by this job     */
 #define FME_RES_NN_UNINIT  0x02u  /* NN read a slot never written in this context (read as 0) */
+#define FME_RES_REJECTED   0x8000u /* device batch rejected (an invalid job): nothing else of the
+                                      record was written and the NN state is unchanged          */
 
 typedef struct fme_result {
   int16_t  mv_int_x, mv_int_y;
@@ -118,6 +120,19 @@ typedef struct fme_result {
   uint8_t  nn_class;
   uint16_t status;
 } fme_result;
+
+/* ---- the xMotionEstimation outputs alone (16 bytes) ------------------------------------- *
+ * What TEncSearch::xMotionEstimation hands back to predInterSearch (rcMv, ruiBits, ruiCost,
+ * TEncSearch.cpp:4590-4597) plus the NN class and status: the record a caller copies back over
+ * PCIe per job when it needs no FracDIF / EMI internals (fme_refine_mv*).                     */
+typedef struct fme_mv_result {
+  int16_t  mv_x, mv_y;        /* final MV, quarter-pel                                         */
+  uint32_t cost;              /* ruiCost                                                       */
+  uint32_t bits;              /* ruiBits                                                       */
+  uint8_t  nn_class;          /* 0..48, 255 when nn_mode == 0                                  */
+  uint8_t  reserved;
+  uint16_t status;            /* FME_RES_*                                                     */
+} fme_mv_result;
 
 typedef struct fme_ctx fme_ctx;
 
@@ -213,23 +228,43 @@ int fme_set_nn_engine(fme_ctx* ctx, int engine);
  * with top-1 minus top-2 of OUT (after the output activation) per job; NULL turns it off. */
 int fme_set_nn_margin_output(fme_ctx* ctx, float* d_margin);
 
-/* Forget the array_e/C/PUHeight/PUWidth state carried across calls (process start). */
+/* Forget the array_e/C/PUHeight/PUWidth state carried across calls (process start).  Stream-
+ * ordered: it takes effect at the start of the next batch, after every batch already issued. */
 int fme_nn_reset_state(fme_ctx* ctx);
 /* The carried state as 12 words: array_e slots[8], C, PUHeight, PUWidth, and a written mask
  * (bit s: slot s written since reset, bit 8: C/PU size written).  Lets a frame-sharded run
- * hand the state of frame f-1 to the rank that refines frame f (nnfme/dist.py).         */
+ * hand the state of frame f-1 to the rank that refines frame f (nnfme/dist.py).
+ * get: waits for the device.  set: stream-ordered like reset (takes effect at the next batch). */
 int fme_nn_get_state(fme_ctx* ctx, uint32_t* out12);
 int fme_nn_set_state(fme_ctx* ctx, const uint32_t* in12);
+/* Enqueue on `stream` a device-to-device copy of the state after every batch issued so far
+ * (12 words to d_out12): per-frame end states without a host round trip.                    */
+int fme_nn_copy_state_device(fme_ctx* ctx, uint32_t* d_out12, void* stream);
 
 /* ---- the batch path --------------------------------------------------------------------- *
  * Runs EMI step -> FracDIF -> NN_pred -> xMotionEstimation tail for n jobs, in job order
  * for the NN's carried state (jobs are independent otherwise).
  * fme_refine:        host job/result arrays (copied over PCIe), synchronous on `stream`.
- * fme_refine_device: device-resident job/result arrays, asynchronous on `stream`
- *                    (one host synchronisation for the size-class histogram).          */
+ *                    A batch with an invalid job returns FME_E_INVALID (nothing computed, the
+ *                    NN state unchanged).
+ * fme_refine_device: device-resident job/result arrays, asynchronous on `stream`: no host
+ *                    synchronisation at all (the PU-shape schedule is built on the device), so
+ *                    successive batches, and copies on other streams, overlap.  Invalid jobs
+ *                    are found on the device: the batch is then skipped (every result gets
+ *                    FME_RES_REJECTED, the NN state is unchanged) and fme_refine_status()
+ *                    reports it.
+ * fme_refine_mv / fme_refine_mv_device: the same batch writing only the 16-byte
+ *                    fme_mv_result per job (xMotionEstimation's outputs); the full records
+ *                    stay in context-owned device memory.                                     */
 int fme_refine(fme_ctx* ctx, const fme_job* jobs, fme_result* results, int n, void* stream);
 int fme_refine_device(fme_ctx* ctx, const fme_job* d_jobs, fme_result* d_results, int n,
                       void* stream);
+int fme_refine_mv(fme_ctx* ctx, const fme_job* jobs, fme_mv_result* out, int n, void* stream);
+int fme_refine_mv_device(fme_ctx* ctx, const fme_job* d_jobs, fme_mv_result* d_out, int n,
+                         void* stream);
+/* Waits for the last refinement batch; returns the number of jobs k_classify rejected in it
+ * (0: the batch ran), or a negative FME_E_* code. */
+int fme_refine_status(fme_ctx* ctx);
 
 /* ---- integer motion estimation ----------------------------------------- *
  * The integer search xMotionEstimation runs before the sub-pel path (TEncSearch.cpp:4504-4527):

@@ -19,11 +19,11 @@ def header_functions():
 def test_library_exports_header():
     lib = runtime.load_library()
     names = header_functions()
-    assert len(names) == 37
+    assert len(names) == 41
     assert set(names) == set(runtime.ABI_SYMBOLS)
     for n in names:
         assert hasattr(lib, n), n
-    assert lib.fme_abi_version() == runtime.ABI_VERSION == 4
+    assert lib.fme_abi_version() == runtime.ABI_VERSION == 5
 
 
 def test_struct_layouts():
@@ -38,6 +38,9 @@ def test_struct_layouts():
     assert abi.MC_JOB_DTYPE.fields["ref_id"][1] == 8
     assert abi.MC_JOB_DTYPE.fields["cu_x"][1] == 10
     assert abi.MC_JOB_DTYPE.fields["mv"][1] == 14
+    assert abi.MV_RESULT_DTYPE.itemsize == 16
+    assert abi.MV_RESULT_DTYPE.fields["cost"][1] == 4
+    assert abi.MV_RESULT_DTYPE.fields["status"][1] == 14
     assert abi.TZ_EXT_DTYPE.itemsize == 12
     assert abi.TZ_EXT_DTYPE.fields["flags"][1] == 8
 
@@ -71,6 +74,10 @@ def test_null_arguments_rejected():
     assert lib.fme_create(0, None, None) == -1
     assert b"null" in lib.fme_last_error()
     assert lib.fme_refine(None, None, None, 1, None) == -1
+    assert lib.fme_refine_mv(None, None, None, 1, None) == -1
+    assert lib.fme_refine_mv_device(None, None, None, 1, None) == -1
+    assert lib.fme_refine_status(None) == -1
+    assert lib.fme_nn_copy_state_device(None, None, None) == -1
     assert lib.fme_destroy(None) == 0
 
 
