@@ -29,8 +29,8 @@ namespace {
 
 thread_local std::string g_last_error = "";
 
-// counts buffer: 25 class counts (+ invalid), 24 scatter cursors, 3 x 8 lane tile-queue heads
-constexpr int kCountWords = 2 * kNumClasses + 1 + 24;
+// counts buffer: 25 class counts (+ invalid), 24 scatter cursors, 8 lane tile-queue heads
+constexpr int kCountWords = 2 * kNumClasses + 1 + 8;
 
 int fail(int code, const char* fmt, ...) {
   char buf[512];
@@ -205,8 +205,6 @@ int fme_create(int device, const fme_config* cfg, fme_ctx** out_ctx) {
   HIP_TRY(c->d_sched.reserve(1));
   c->sched_p = sched_params();
   HIP_TRY(hipEventCreateWithFlags(&c->ev_done, hipEventDisableTiming));
-  HIP_TRY(hipStreamCreateWithFlags(&c->aux2, hipStreamNonBlocking));
-  HIP_TRY(hipEventCreateWithFlags(&c->ev_join2, hipEventDisableTiming));
   HIP_TRY(c->nn_state.reserve(24));
   HIP_TRY(hipMemset(c->nn_state.p, 0, 24 * sizeof(uint32_t)));
   HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&c->h_counts), (kNumClasses + 1) * sizeof(int32_t), hipHostMallocDefault));
@@ -619,26 +617,18 @@ static int refine_batch(fme_ctx* c, const fme_job* d_jobs, fme_result* d_res, fm
   if (prof) HIP_TRY(hipEventRecord(ev[2], s));
   HIP_TRY(launch_scatter(a, w, s));
   if (prof) HIP_TRY(hipEventRecord(ev[3], s));
-  // the three lane kernels are independent: 8x8 units on the batch stream, 4x8 units on aux2, 8x4
-  // units then the cooperative AMP shapes on aux; joined before the NN tail
+  // the lane kernel (every power-of-two shape) on the batch stream, the cooperative AMP kernels
+  // beside it on the auxiliary stream, joined before the NN tail
   HIP_TRY(hipEventRecord(c->ev_fork, s));
   HIP_TRY(hipStreamWaitEvent(c->aux, c->ev_fork, 0));
-  HIP_TRY(hipStreamWaitEvent(c->aux2, c->ev_fork, 0));
-  // (the lane kernels' workgroups stay resident until their queues drain, so every lane kernel is
-  // launched before the cooperative AMP kernels, which then fill in as the lane workgroups exit)
-  HIP_TRY(launch_search_lane_one(a, w, kSearchLane48, c->aux2));
+  HIP_TRY(launch_search_lane(a, w, s));
+  if (prof) HIP_TRY(hipEventRecord(ev[4], s));
   if (prof) HIP_TRY(hipEventRecord(ev[7], c->aux));
-  HIP_TRY(launch_search_lane_one(a, w, kSearchLane84, c->aux));
   HIP_TRY(launch_search_small(a, w, c->aux));
   HIP_TRY(launch_search_large(a, w, c->aux));
   if (prof) HIP_TRY(hipEventRecord(ev[8], c->aux));
   HIP_TRY(hipEventRecord(c->ev_join, c->aux));
-  HIP_TRY(hipEventRecord(c->ev_join2, c->aux2));
-  HIP_TRY(launch_search_lane_one(a, w, kSearchLane88, s));
   HIP_TRY(hipStreamWaitEvent(s, c->ev_join, 0));
-  HIP_TRY(hipStreamWaitEvent(s, c->ev_join2, 0));
-  // "main search" spans all three lane kernels (and the cooperative shapes beside them)
-  if (prof) HIP_TRY(hipEventRecord(ev[4], s));
   if (prof) HIP_TRY(hipEventRecord(ev[5], s));
   HIP_TRY(c->cfg.nn_mode == 2
               ? launch_nn_deep_tail(c->net, c->d_net.p, c->nn_margin, a, w, c->state_cur, c->nn_engine, s)
@@ -966,10 +956,7 @@ int fme_nn_pred_single(fme_ctx* c, const uint32_t* e, uint32_t cc, int pu_h, int
 int fme_search_kernel_of_shape(int width, int height) {
   for (int k = 0; k < kNumClasses; k++)
     if (kClassW[k] == width && kClassH[k] == height) {
-      const int kern = search_kernel_of(k);
-      const bool lane_build = lane_lanes_per_pu(0) > 0;
-      if (lane_build) return kern <= kSearchLane88 ? 0 : 1;
-      return kern == kSearchCoop ? 0 : 1;
+      return search_kernel_of(k) == kSearchLane ? 0 : 1;
     }
   return -1;
 }
@@ -1171,6 +1158,54 @@ bool valid_pu_shape(int w, int h) {
 }  // namespace
 
 extern "C" {
+
+// xGetTemplateCost (TEncSearch.cpp:4397-4436) of every AMVP candidate of every request, one launch:
+// costs[(i * FME_MAX_REFS + k) * 2 + m]; 0xFFFFFFFF for k >= num_refs or m >= n_cand[k].
+int fme_template_costs(fme_ctx* c, const fme_pu_req* reqs, uint32_t* costs, int n, void* stream) {
+  if (!c || (n > 0 && (!reqs || !costs))) return fail(FME_E_INVALID, "fme_template_costs: null argument");
+  if (n <= 0) return n == 0 ? FME_OK : fail(FME_E_INVALID, "fme_template_costs: n = %d", n);
+  HIP_TRY(hipSetDevice(c->device));
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  std::vector<AmvpTask> tasks;
+  std::vector<int> slot;
+  for (int i = 0; i < n; i++) {
+    const fme_pu_req& q = reqs[i];
+    const PicDesc& org = c->pics[q.org_id < FME_MAX_PICTURES ? q.org_id : 0];
+    if (!valid_pu_shape(q.w, q.h) || q.num_refs < 1 || q.num_refs > FME_MAX_REFS || q.org_id >= FME_MAX_PICTURES ||
+        !org.luma || q.x + q.w > org.width || q.y + q.h > org.height || q.lambda_id >= FME_MAX_LAMBDAS ||
+        !c->lambda_set[q.lambda_id])
+      return fail(FME_E_INVALID, "fme_template_costs: request %d invalid", i);
+    for (int k = 0; k < FME_MAX_REFS; k++)
+      for (int m = 0; m < 2; m++) {
+        costs[((size_t)i * FME_MAX_REFS + k) * 2 + m] = 0xFFFFFFFFu;
+        if (k >= q.num_refs || m >= q.n_cand[k]) continue;
+        if (q.ref_id[k] >= FME_MAX_PICTURES || !c->pics[q.ref_id[k]].luma || q.n_cand[k] > 2 ||
+            c->pics[q.ref_id[k]].width != org.width || c->pics[q.ref_id[k]].height != org.height)
+          return fail(FME_E_INVALID, "fme_template_costs: request %d reference %d invalid", i, k);
+        slot.push_back((i * FME_MAX_REFS + k) * 2 + m);
+        tasks.push_back(AmvpTask{q.x, q.y, q.w, q.h, q.org_id, q.ref_id[k], q.cu_x, q.cu_y, q.cand[k][m][0],
+                                 q.cand[k][m][1]});
+      }
+  }
+  if (tasks.empty()) return FME_OK;
+  int rc = sync_tables(c, s);
+  if (rc) return rc;
+  std::vector<uint32_t> tsad(tasks.size());
+  HIP_TRY(c->d_amvp.reserve(tasks.size()));
+  HIP_TRY(c->d_amvp_sad.reserve(tasks.size()));
+  HIP_TRY(hipMemcpyAsync(c->d_amvp.p, tasks.data(), tasks.size() * sizeof(AmvpTask), hipMemcpyHostToDevice, s));
+  AmvpArgs aa{c->d_amvp.p, c->d_pics.p, c->d_amvp_sad.p, (int32_t)tasks.size()};
+  HIP_TRY(launch_amvp_sad(aa, s));
+  HIP_TRY(hipMemcpyAsync(tsad.data(), c->d_amvp_sad.p, tasks.size() * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipStreamSynchronize(s));
+  for (size_t t = 0; t < tasks.size(); t++) {
+    const int i = slot[t] / (2 * FME_MAX_REFS), m = slot[t] & 1;
+    const double ml = c->mlambda[reqs[i].lambda_id];
+    // calcRdCost(bits, SAD, DF_SAD) with bits = m_auiMVPIdxCost[m][AMVP_MAX_NUM_CANDS] (4423-4433)
+    costs[slot[t]] = (uint32_t)((double)tsad[t] + ((double)mvp_idx_bits(m, 2) * ml) / 65536.0);
+  }
+  return FME_OK;
+}
 
 int fme_pred_inter_reset(fme_ctx* c) {
   if (!c) return fail(FME_E_INVALID, "fme_pred_inter_reset: null ctx");

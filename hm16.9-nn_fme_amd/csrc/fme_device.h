@@ -85,26 +85,23 @@ struct WorkBufs {
   int32_t* blk_prefix;   // [nblk * 9] exclusive prefix (carry-in) per block
   uint32_t* nn_state;    // 2 x 12 words: slot[8], c, pu_h, pu_w, written
   Schedule* sched;       // built on the device by k_schedule from counts
-  int32_t* tile_ctr;     // [3][8] lane-kernel tile queue heads (zeroed with counts)
+  int32_t* tile_ctr;     // [8] lane-kernel tile queue heads (zeroed with counts)
   fme_mv_result* mv_out; // compact per-job output (fme_refine_mv*), or null
 };
 
-// Schedule of the search kernels.  Kernel k (lane-per-unit with 4x8 / 8x4 / 8x8 units,
-// cooperative 256-lane, cooperative 512-lane) serves class c with its blocks
-// [prefix[k][c], prefix[k][c+1]); every class belongs to exactly one kernel
-// (search_kernel_of).  Class c's jobs are sjobs/perm[class_off[c] .. + class_cnt[c]).
-enum {
-  kSearchLane48 = 0, kSearchLane84 = 1, kSearchLane88 = 2, kSearchCoop = 3, kSearchCoopLarge = 4,
-  kSearchKernels = 5
-};
+// Schedule of the search kernels.  Kernel k (lane-per-unit, cooperative 256-lane, cooperative
+// 512-lane) serves class c with its tiles [prefix[k][c], prefix[k][c+1]) (lane kernel: 64-lane
+// wave tiles; cooperative: blocks); every class belongs to exactly one kernel (search_kernel_of).
+// Class c's jobs are sjobs/perm[class_off[c] .. + class_cnt[c]).
+enum { kSearchLane = 0, kSearchCoop = 1, kSearchCoopLarge = 2, kSearchKernels = 3 };
 struct Schedule {
   int32_t prefix[kSearchKernels][kNumClasses + 1];
   int32_t class_off[kNumClasses];
   int32_t class_cnt[kNumClasses];
-  // Device-built schedules only (k_schedule): the lane kernels' per-XCD tile queues.  XCD x
-  // owns the x-th contiguous eighth of every class's blocks; its queue lists them class by
-  // class, xq[k][x][c] = its tiles before class c (xq[k][x][kNumClasses] = queue length).
-  int32_t xq[3][8][kNumClasses + 1];
+  // The lane kernel's per-XCD tile queues: XCD x owns the x-th contiguous eighth of every
+  // class's wave tiles; its queue lists them class by class, xq[x][c] = its tiles before class c
+  // (xq[x][kNumClasses] = queue length).
+  int32_t xq[8][kNumClasses + 1];
   int32_t invalid;            // jobs rejected by k_classify (the whole batch is then skipped)
   int32_t pad_[3];
 };
@@ -112,7 +109,7 @@ struct Schedule {
 // What k_schedule needs to know about the search kernels (host tables, one per build).
 struct SchedParams {
   int8_t kern[kNumClasses];       // search_kernel_of(c)
-  int32_t lanes[kNumClasses];     // lane kernels: lanes per PU; cooperative: PUs per tile
+  int32_t lanes[kNumClasses];     // lane kernel: lanes per PU; cooperative: PUs per tile
   int32_t tiles_per_block;        // cooperative kernels
 };
 SchedParams sched_params();
@@ -154,17 +151,14 @@ hipError_t launch_put_state(uint32_t* dst, const uint32_t* v12, hipStream_t s);
 // the picture / lambda tables written in stream order from kernel arguments
 hipError_t launch_put_tables(PicDesc* d_pics, double* d_ml, const PicDesc* pics, const double* ml, hipStream_t s);
 int tiles_per_block();
-int search_kernel_of(int cls);                      // kSearchLane48 .. kSearchCoopLarge
-int search_blocks_for(int cls, int cnt);           // blocks of its kernel for cnt jobs
-// The search kernels read their schedule from *w.sched (no host round trip).  A lane kernel is
-// launched with enough workgroups to fill the chip, each pulling tiles from its XCD's queue
-// (then the other XCDs'); a cooperative kernel strides over its blocks.  `n` bounds the work.
-hipError_t launch_search_lane_one(const BatchArgs& a, const WorkBufs& w, int kern, hipStream_t s);
+int search_kernel_of(int cls);                      // kSearchLane .. kSearchCoopLarge
+// The search kernels read their schedule from *w.sched (no host round trip).  The lane kernel is
+// launched with enough workgroups to fill the chip, each wave pulling tiles from its XCD's queue
+// (then the other XCDs'); a cooperative kernel strides over its blocks.  `a.n` bounds the work.
+hipError_t launch_search_lane(const BatchArgs& a, const WorkBufs& w, hipStream_t s);
 hipError_t launch_search_large(const BatchArgs& a, const WorkBufs& w, hipStream_t s);
 hipError_t launch_search_small(const BatchArgs& a, const WorkBufs& w, hipStream_t s);
 int lane_lanes_per_pu(int cls);                    // 0: not a lane-kernel class
-int lane_kernel_of(int cls);                       // kSearchLane48/84/88, -1: not a lane class
-int lane_blocks_for(int cls, int cnt);
 int cu_count(int device);                          // compute units (workgroup budget of a launch)
 // Packed NN layout for the tail kernel (nn_pack, fme_kernels.hip): offsets in floats, every
 // pair region 8-byte aligned.

@@ -179,8 +179,8 @@ __global__ __launch_bounds__(64) void k_schedule(WorkBufs w, SchedParams p) {
   int kern = -1, nb = 0;
   if (cnt > 0) {
     kern = p.kern[c];
-    if (kern <= kSearchLane88) {
-      nb = (int)(((long long)cnt * p.lanes[c] + 255) / 256);
+    if (kern == kSearchLane) {
+      nb = (int)(((long long)cnt * p.lanes[c] + 63) / 64);   // 64-lane wave tiles
     } else {
       const int tiles = (cnt + p.lanes[c] - 1) / p.lanes[c];
       nb = (tiles + p.tiles_per_block - 1) / p.tiles_per_block;
@@ -197,13 +197,11 @@ __global__ __launch_bounds__(64) void k_schedule(WorkBufs w, SchedParams p) {
     if (c <= kNumClasses) sc->prefix[q][c] = ex;     // [kNumClasses] = the kernel's total
   }
 #pragma unroll
-  for (int q = 0; q < 3; q++)
-#pragma unroll
-    for (int x = 0; x < 8; x++) {
-      const int mine = kern == q ? (nb >> 3) + (x < (nb & 7) ? 1 : 0) : 0;
-      const int ex = wave_excl_scan(mine);
-      if (c <= kNumClasses) sc->xq[q][x][c] = ex;
-    }
+  for (int x = 0; x < 8; x++) {
+    const int mine = kern == kSearchLane ? (nb >> 3) + (x < (nb & 7) ? 1 : 0) : 0;
+    const int ex = wave_excl_scan(mine);
+    if (c <= kNumClasses) sc->xq[x][c] = ex;
+  }
   if (c == 0) sc->invalid = inv;
 }
 

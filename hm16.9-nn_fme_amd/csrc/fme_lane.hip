@@ -33,10 +33,6 @@
 #ifndef FME_XCD_SWIZZLE
 #define FME_XCD_SWIZZLE 1
 #endif
-// register-pressure experiments only: bit 0 skip quarter stage, 1 skip half sides, 2 skip EMI
-#ifndef FME_LANE_SKIP
-#define FME_LANE_SKIP 0
-#endif
 // Candidates per quarter pass (2: column-phase pairs, 1: one candidate per pass — fewer live
 // registers, the first-stage column recomputed per candidate)
 #ifndef FME_LANE_QPAIR
@@ -47,12 +43,9 @@
 #ifndef FME_LANE_HPAIR
 #define FME_LANE_HPAIR 1
 #endif
-// occupancy targets (waves per SIMD) that bound the register allocation of each kernel
-#ifndef FME_LANE_WAVES_SMALL
-#define FME_LANE_WAVES_SMALL 2
-#endif
-#ifndef FME_LANE_WAVES_88
-#define FME_LANE_WAVES_88 2
+// occupancy target (waves per SIMD) that bounds the register allocation
+#ifndef FME_LANE_WAVES
+#define FME_LANE_WAVES 2
 #endif
 
 namespace fme {
@@ -151,29 +144,11 @@ __device__ __forceinline__ void vpairs(int f, int o, uint32_t (&c)[5]) {
 }
 
 // ---- the key block (key - 128 as packed int16 row pairs): K(x, j) = rows (2j, 2j+1) of column x --
-// In registers, or (FME_LANE_KLDS) in LDS at [(x*UJ + j) / 4][lane][(x*UJ + j) % 4] dwords: 16-byte
-// groups of consecutive lanes are contiguous (conflict-free ds_read_b128) and the key's VGPRs
-// are freed for occupancy.
-#ifndef FME_LANE_KLDS
-#define FME_LANE_KLDS 0
-#endif
 template <int UW, int UJ>
 struct KeySrc {
-#if FME_LANE_KLDS
-  uint32_t* lds;   // this lane's base: &klds[lane * 4]
-  __device__ __forceinline__ uint32_t at(int x, int j) const {
-    const int e = x * UJ + j;
-    return lds[(e >> 2) * (kLaneNT * 4) + (e & 3)];
-  }
-  __device__ __forceinline__ void set(int x, int j, uint32_t v) {
-    const int e = x * UJ + j;
-    lds[(e >> 2) * (kLaneNT * 4) + (e & 3)] = v;
-  }
-#else
   uint32_t k[UW][UJ];
   __device__ __forceinline__ uint32_t at(int x, int j) const { return k[x][j]; }
   __device__ __forceinline__ void set(int x, int j, uint32_t v) { k[x][j] = v; }
-#endif
 };
 
 // ---- distortion of one unit for one candidate ------------------------------------------------
@@ -493,7 +468,7 @@ __device__ __forceinline__ void load_row(const uint8_t* row, int xb, int width, 
 template <int PW, int PH, int UW, int UH>
 __device__ __forceinline__ void lane_unit(const BatchArgs& a, const fme_job* __restrict__ sjobs,
                                           const int32_t* __restrict__ perm, int cls_off, int cls_cnt,
-                                          int blk, uint32_t* klds) {
+                                          int wt) {
   constexpr int T = ((PW % 8) == 0 && (PH % 8) == 0) ? 8 : 4;
   static_assert(UW % T == 0 && UH % T == 0, "unit must hold whole SATD tiles");
   constexpr int UX = PW / UW, L = UX * (PH / UH);
@@ -505,7 +480,7 @@ __device__ __forceinline__ void lane_unit(const BatchArgs& a, const fme_job* __r
   constexpr int NV = UW / 4 + 2;              // re-centred dwords per row (cols -4 .. UW+3)
   constexpr int UJ = UH / 2;                  // packed row pairs per column
 
-  const int gl = blk * kLaneNT + (int)threadIdx.x;
+  const int gl = wt * 64 + ((int)threadIdx.x & 63);   // wave tile wt: 64 lanes = 64 / L PUs
   int p = gl / L;
   const int u = gl - p * L;
   const bool active = p < cls_cnt;
@@ -574,7 +549,7 @@ __device__ __forceinline__ void lane_unit(const BatchArgs& a, const fme_job* __r
   uint32_t cval = 0, emi[8];
 #pragma unroll
   for (int k = 0; k < 8; k++) emi[k] = 0;
-  if (!(FME_LANE_SKIP & 4) && (j.flags & FME_JOB_EMI)) {
+  if (j.flags & FME_JOB_EMI) {
     // Row-major: window row R (= 5 + dy + r) serves positions (dx, dy) with org row r = R-5-dy;
     // its byte groups at dx = -1, 0, 1 are formed once.
     uint32_t e9[9];
@@ -707,9 +682,6 @@ __device__ __forceinline__ void lane_unit(const BatchArgs& a, const fme_job* __r
 
   // ---- key as signed int16 (key - 128) pairs: K[c][j] = (row 2j, row 2j+1) of column c ------------
   KeySrc<UW, UJ> K;
-#if FME_LANE_KLDS
-  K.lds = klds + threadIdx.x * 4;
-#endif
 #pragma unroll
   for (int c = 0; c < UW; c++)
 #pragma unroll
@@ -727,12 +699,12 @@ __device__ __forceinline__ void lane_unit(const BatchArgs& a, const fme_job* __r
   int hbi = 9;
   {
     uint32_t d[3] = {0u, 0u, 0u};
-    if (!(FME_LANE_SKIP & 8)) half_center<UW, UH, T>(v, K, had, d);
+    half_center<UW, UH, T>(v, K, had, d);
     take_half<L>(0, d[0], ml, mvx, mvy, mvp_x, mvp_y, hbest, hbi);
     take_half<L>(1, d[1], ml, mvx, mvy, mvp_x, mvp_y, hbest, hbi);
     take_half<L>(2, d[2], ml, mvx, mvy, mvp_x, mvp_y, hbest, hbi);
   }
-  if (!(FME_LANE_SKIP & 2)) {
+  {
     uint32_t d[3];
     half_side<UW, UH, T, 0>(v, K, had, d);
     take_half<L>(3, d[0], ml, mvx, mvy, mvp_x, mvp_y, hbest, hbi);
@@ -748,10 +720,8 @@ __device__ __forceinline__ void lane_unit(const BatchArgs& a, const fme_job* __r
   // ---- 4. quarter-pel stage: passes over column phases (Q9 candidate 0 = the half best) -------
   uint32_t qbest = hbest;
   int qbi = 0;
-  if (!(FME_LANE_SKIP & 1)) {
-    qtr_all<L, UW, UH, T>(v, K, had, hx, hy, ml, mvx, mvy, mvp_x, mvp_y, qbest, qbi,
-                          std::make_integer_sequence<int, kQPasses>{});
-  }
+  qtr_all<L, UW, UH, T>(v, K, had, hx, hy, ml, mvx, mvy, mvp_x, mvp_y, qbest, qbi,
+                        std::make_integer_sequence<int, kQPasses>{});
   const int bq = qbi;
 
   // ---- results: bytes 0..15 (mv_int, mv (NN tail), half, qtr, frac_cost) ------------------------
@@ -787,93 +757,76 @@ __device__ __forceinline__ int xcc_id() {
   X(18, 64, 16, 8, 8) X(19, 32, 64, 8, 8) X(20, 64, 32, 8, 8) X(23, 64, 64, 8, 8)
 #define FME_LANE_CLASSES(X) FME_LANE48_CLASSES(X) FME_LANE84_CLASSES(X) FME_LANE88_CLASSES(X)
 
-// A workgroup pulls 256-lane tiles from its XCD's queue (Schedule::xq: the XCD's contiguous
-// eighth of every class = one spatial band of the CTU-ordered job stream, so each L2 sees one
-// band), then from the other XCDs' queues; the claim of the next tile is issued before the
-// current one is searched.  The grid is sized to fill the chip, not to the (device-computed)
-// tile count, so the host never waits for the class histogram.
+// One kernel serves every lane class.  A workgroup claims four consecutive 64-lane wave tiles
+// (one per wave; a tile holds 64 / L PUs of one class) per atomic from its XCD's queue
+// (Schedule::xq: the XCD's contiguous eighth of every class's tiles = one spatial band of the
+// CTU-ordered job stream, so each L2 sees one band, and the four waves of a CU search neighbouring
+// PUs whose reference windows share L1 lines), then from the other XCDs' queues.  The next claim
+// is issued before the current tiles are searched.  The grid is sized to fill the chip, not to
+// the (device-computed) tile count, so the host never waits for the class histogram.
+// Measured (1080p frame, tools/ab_bench.py): per-wave claims 1.48 ms, four tiles per workgroup
+// 1.21 ms, eight 1.24, sixteen 1.29; without the XCD queues 1.25.
 #define FME_CASE(ID, PW_, PH_, UW_, UH_)                                                             \
   case ID:                                                                                           \
-    lane_unit<PW_, PH_, UW_, UH_>(a, w.sjobs, w.perm, sc->class_off[ID], sc->class_cnt[ID], blk, klds); \
+    lane_unit<PW_, PH_, UW_, UH_>(a, w.sjobs, w.perm, sc->class_off[ID], sc->class_cnt[ID], wt);     \
     break;
-#define FME_LANE_KERNEL(NAME, KID, LIST, WAVES)                                                      \
-  __global__ __launch_bounds__(kLaneNT) __attribute__((amdgpu_waves_per_eu(WAVES)))                 \
-  void NAME(BatchArgs a, WorkBufs w) {                                                               \
-    __shared__ uint32_t klds_[FME_LANE_KLDS ? 8 * kLaneNT * 4 : 1];                                  \
-    __shared__ int32_t claim[2];                                                                     \
-    uint32_t* klds = klds_;                                                                          \
-    const Schedule* __restrict__ sc = w.sched;                                                       \
-    int32_t* ctr = w.tile_ctr + KID * 8;                                                             \
-    const int home = xcc_id();                                                                       \
-    int x = home, tried = 0, par = 0;                                                                \
-    if (threadIdx.x == 0) claim[0] = atomicAdd(&ctr[x], 1);                                          \
-    __syncthreads();                                                                                 \
-    int t = __builtin_amdgcn_readfirstlane(claim[0]);                                                \
-    while (true) {                                                                                   \
-      if (t >= sc->xq[KID][x][kNumClasses]) {   /* queue drained: the next XCD's */                  \
-        if (++tried == 8) break;                                                                     \
-        x = (home + tried) & 7;                                                                      \
-        par ^= 1;                                                                                    \
-        if (threadIdx.x == 0) claim[par] = atomicAdd(&ctr[x], 1);                                    \
-        __syncthreads();                                                                             \
-        t = __builtin_amdgcn_readfirstlane(claim[par]);                                              \
-        continue;                                                                                    \
-      }                                                                                              \
-      int nxt = 0;                                                                                   \
-      if (threadIdx.x == 0) nxt = atomicAdd(&ctr[x], 1);                                             \
-      int c = 0;                                                                                     \
-      while (c < kNumClasses - 1 && t >= sc->xq[KID][x][c + 1]) c++;                                 \
-      const int nblk = sc->prefix[KID][c + 1] - sc->prefix[KID][c];                                  \
-      const int blk = x * (nblk >> 3) + min(x, nblk & 7) + (t - sc->xq[KID][x][c]);                  \
-      switch (c) {                                                                                   \
-        LIST(FME_CASE)                                                                               \
-        default: break;                                                                              \
-      }                                                                                              \
-      par ^= 1;                                                                                      \
-      if (threadIdx.x == 0) claim[par] = nxt;                                                        \
-      __syncthreads();                                                                               \
-      t = __builtin_amdgcn_readfirstlane(claim[par]);                                                \
-    }                                                                                                \
+__global__ __launch_bounds__(kLaneNT) __attribute__((amdgpu_waves_per_eu(FME_LANE_WAVES)))
+void k_search_lane(BatchArgs a, WorkBufs w) {
+  constexpr int kGroup = kLaneNT / 64;   // wave tiles per claim
+  __shared__ int32_t claim[2];
+  const Schedule* __restrict__ sc = w.sched;
+  int32_t* ctr = w.tile_ctr;
+  const int home = xcc_id(), wid = threadIdx.x >> 6;
+  int x = home, tried = 0, par = 0;
+  if (threadIdx.x == 0) claim[0] = atomicAdd(&ctr[x], 1);
+  __syncthreads();
+  int t = __builtin_amdgcn_readfirstlane(claim[0]);
+  while (true) {
+    const int len = sc->xq[x][kNumClasses];
+    if (kGroup * t >= len) {   // queue drained: the next XCD's
+      if (++tried == 8) break;
+      x = (home + tried) & 7;
+      par ^= 1;
+      if (threadIdx.x == 0) claim[par] = atomicAdd(&ctr[x], 1);
+      __syncthreads();
+      t = __builtin_amdgcn_readfirstlane(claim[par]);
+      continue;
+    }
+    int nxt = 0;
+    if (threadIdx.x == 0) nxt = atomicAdd(&ctr[x], 1);
+    const int tw = kGroup * t + wid;
+    if (tw < len) {
+      int c = 0;
+      while (c < kNumClasses - 1 && tw >= sc->xq[x][c + 1]) c++;
+      const int nt = sc->prefix[kSearchLane][c + 1] - sc->prefix[kSearchLane][c];
+      const int wt = x * (nt >> 3) + min(x, nt & 7) + (tw - sc->xq[x][c]);
+      switch (c) {
+        FME_LANE_CLASSES(FME_CASE)
+        default: break;
+      }
+    }
+    par ^= 1;   // claim[par] is rewritten only after every wave has passed the barrier below
+    if (threadIdx.x == 0) claim[par] = nxt;
+    __syncthreads();
+    t = __builtin_amdgcn_readfirstlane(claim[par]);
   }
-FME_LANE_KERNEL(k_search_lane48, kSearchLane48, FME_LANE48_CLASSES, FME_LANE_WAVES_SMALL)
-FME_LANE_KERNEL(k_search_lane84, kSearchLane84, FME_LANE84_CLASSES, FME_LANE_WAVES_SMALL)
-FME_LANE_KERNEL(k_search_lane88, kSearchLane88, FME_LANE88_CLASSES, FME_LANE_WAVES_88)
+}
 #undef FME_CASE
-#undef FME_LANE_KERNEL
 
 // Lanes per PU of a lane-kernel class, 0 for classes the cooperative kernels serve.
 int lane_lanes_per_pu(int cls) {
-#ifdef FME_NO_LANE
-  (void)cls;
-  return 0;
-#else
   switch (cls) {
 #define FME_L(ID, PW_, PH_, UW_, UH_) case ID: return (PW_ / UW_) * (PH_ / UH_);
     FME_LANE_CLASSES(FME_L)
 #undef FME_L
     default: return 0;
   }
-#endif
 }
 
-int lane_blocks_for(int cls, int cnt) {
-  const int l = lane_lanes_per_pu(cls);
-  return l ? (int)(((long long)cnt * l + kLaneNT - 1) / kLaneNT) : 0;
-}
-
-int lane_kernel_of(int cls) {
-  switch (cls) {
-#define FME_K(ID, PW_, PH_, UW_, UH_) case ID: return UW_ == 4 ? kSearchLane48 : (UH_ == 4 ? kSearchLane84 : kSearchLane88);
-    FME_LANE_CLASSES(FME_K)
-#undef FME_K
-    default: return -1;
-  }
-}
-
-// Workgroups of one lane-kernel launch: at most the tiles n jobs could need, at most what the
-// chip holds at 4 workgroups per CU (the kernels reach 2-3; spare workgroups find the queues
-// drained and exit).
-static int lane_grid(int kern, int n) {
+// Workgroups of the lane-kernel launch: at most the wave tiles n jobs could need (4 per
+// workgroup), at most 4 per CU (the kernel holds 2; spare workgroups find the queues drained
+// and exit).
+static int lane_grid(int n) {
   static int cus = 0;
   if (!cus) {
     int dev = 0;
@@ -882,22 +835,18 @@ static int lane_grid(int kern, int n) {
   }
   int max_l = 0, classes = 0;
   for (int c = 0; c < kNumClasses; c++)
-    if (lane_kernel_of(c) == kern) {
+    if (lane_lanes_per_pu(c)) {
       max_l = std::max(max_l, lane_lanes_per_pu(c));
       classes++;
     }
-  if (!classes) return 0;
-  const long long bound = ((long long)n * max_l + kLaneNT - 1) / kLaneNT + classes;
-  return (int)std::min<long long>(bound, 4LL * cus);
+  const long long waves = ((long long)n * max_l + 63) / 64 + classes;
+  return (int)std::min<long long>((waves + kLaneNT / 64 - 1) / (kLaneNT / 64), 4LL * cus);
 }
 
-hipError_t launch_search_lane_one(const BatchArgs& a, const WorkBufs& w, int kern, hipStream_t s) {
-  const int blocks = lane_grid(kern, a.n);
+hipError_t launch_search_lane(const BatchArgs& a, const WorkBufs& w, hipStream_t s) {
+  const int blocks = lane_grid(a.n);
   if (blocks <= 0) return hipSuccess;
-  if (kern == kSearchLane48) hipLaunchKernelGGL(k_search_lane48, dim3(blocks), dim3(kLaneNT), 0, s, a, w);
-  else if (kern == kSearchLane84) hipLaunchKernelGGL(k_search_lane84, dim3(blocks), dim3(kLaneNT), 0, s, a, w);
-  else if (kern == kSearchLane88) hipLaunchKernelGGL(k_search_lane88, dim3(blocks), dim3(kLaneNT), 0, s, a, w);
-  else return hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_search_lane, dim3(blocks), dim3(kLaneNT), 0, s, a, w);
   return hipGetLastError();
 }
 

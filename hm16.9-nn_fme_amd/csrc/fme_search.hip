@@ -791,17 +791,9 @@ __device__ __forceinline__ void search_class(const BatchArgs& a, const fme_job* 
 // =============================================================================================
 // With the lane-per-unit kernel (fme_lane.hip) these kernels serve only the AMP shapes whose
 // lane groups are not a power of two (12x16, 16x12, 24x32, 32x24, 48x64, 64x48 — the
-// SAD12/24/48 EMI metric); -DFME_NO_LANE routes every class here (A/B builds).
-#ifdef FME_NO_LANE
-#define FME_SMALL_CLASSES(X)                                                                       \
-  X(0, 4, 8) X(1, 8, 4) X(2, 8, 8) X(3, 4, 16) X(4, 16, 4) X(5, 8, 16) X(6, 16, 8) X(7, 12, 16)      \
-  X(8, 16, 12) X(9, 16, 16) X(10, 8, 32) X(11, 32, 8) X(12, 16, 32) X(13, 32, 16) X(14, 24, 32)     \
-  X(15, 32, 24) X(16, 32, 32) X(17, 16, 64) X(18, 64, 16)
-#define FME_LARGE_CLASSES(X) X(19, 32, 64) X(20, 64, 32) X(21, 48, 64) X(22, 64, 48) X(23, 64, 64)
-#else
+// SAD12/24/48 EMI metric).
 #define FME_SMALL_CLASSES(X) X(7, 12, 16) X(8, 16, 12) X(14, 24, 32) X(15, 32, 24)
 #define FME_LARGE_CLASSES(X) X(21, 48, 64) X(22, 64, 48)
-#endif
 
 constexpr int kSmallNT = 256, kSmallBudget = FME_SMALL_BUDGET_KB * 1024;
 constexpr int kLargeNT = 512, kLargeBudget = FME_LARGE_BUDGET_KB * 1024;
@@ -907,16 +899,8 @@ hipError_t debug_phase_cycles(unsigned long long* out16, bool reset) {
 }
 
 int search_kernel_of(int cls) {
-  if (lane_lanes_per_pu(cls) > 0) return lane_kernel_of(cls);
+  if (lane_lanes_per_pu(cls) > 0) return kSearchLane;
   return cls >= 19 ? kSearchCoopLarge : kSearchCoop;
-}
-
-int search_blocks_for(int cls, int cnt) {
-  if (cnt <= 0) return 0;
-  if (lane_lanes_per_pu(cls) > 0) return lane_blocks_for(cls, cnt);
-  const int p = pus_per_tile(cls), tpb = tiles_per_block();
-  const int tiles = (cnt + p - 1) / p;
-  return (tiles + tpb - 1) / tpb;
 }
 
 static size_t lds_max(int kernel) {

@@ -30,7 +30,7 @@ ABI_SYMBOLS = (
     "fme_integer_search", "fme_integer_search_device", "fme_integer_search_last_ms",
     "fme_pred_inter_p", "fme_pred_inter_reset", "fme_nn_param_count", "fme_load_nn_net",
     "fme_set_nn_engine", "fme_set_nn_margin_output", "fme_refine_mv", "fme_refine_mv_device",
-    "fme_refine_status", "fme_nn_copy_state_device",
+    "fme_refine_status", "fme_nn_copy_state_device", "fme_template_costs",
 )
 
 
@@ -100,6 +100,7 @@ def load_library(path=None):
         "fme_refine_mv_device": (I, [P, P, P, I, P]),
         "fme_refine_status": (I, [P]),
         "fme_nn_copy_state_device": (I, [P, P, P]),
+        "fme_template_costs": (I, [P, P, P, I, P]),
     }
     for name, (res, args) in sig.items():
         f = getattr(lib, name)
@@ -201,6 +202,16 @@ class FmeContext:
         if len(reqs):
             _check(self.lib, self.lib.fme_pred_inter_p(self.h, _ptr(reqs), _ptr(res), len(reqs), stream))
         return res
+
+    def template_costs(self, reqs, stream=None):
+        """fme_template_costs: xGetTemplateCost per (request, reference, candidate) -> uint32
+        [n, MAX_REFS, 2] (0xFFFFFFFF where there is no candidate)."""
+        from .abi import MAX_REFS, PU_REQ_DTYPE
+        reqs = np.ascontiguousarray(reqs, dtype=PU_REQ_DTYPE)
+        out = np.zeros((len(reqs), MAX_REFS, 2), np.uint32)
+        if len(reqs):
+            _check(self.lib, self.lib.fme_template_costs(self.h, _ptr(reqs), _ptr(out), len(reqs), stream))
+        return out
 
     def pred_inter_reset(self):
         _check(self.lib, self.lib.fme_pred_inter_reset(self.h))

@@ -363,6 +363,11 @@ typedef struct fme_pu_res {
 int fme_pred_inter_p(fme_ctx* ctx, const fme_pu_req* reqs, fme_pu_res* res, int n, void* stream);
 /* Forget m_integerMv2Nx2N (TEncSearch construction: every entry (0, 0)). */
 int fme_pred_inter_reset(fme_ctx* ctx);
+/* xEstimateMvPredAMVP's template costs alone: xGetTemplateCost (TEncSearch.cpp:4397-4436) of every
+ * AMVP candidate m < n_cand[k] of every reference k < num_refs of every request, in one launch:
+ * costs[(i * FME_MAX_REFS + k) * 2 + m] (0xFFFFFFFF where there is no candidate).  Host arrays,
+ * synchronous. */
+int fme_template_costs(fme_ctx* ctx, const fme_pu_req* reqs, uint32_t* costs, int n, void* stream);
 
 /* ---- single-PU entry points with the TEncSearch argument lists ---------------------------- *
  * xPatternSearchFracDIF(bIsLosslessCoded, pcPatternKey, piRefY, iRefStride, pcMvInt,

@@ -1041,6 +1041,12 @@ static uint32_t pi_template_cost(const orc_ctx* ctx, const fme_pu_req* q, int k,
   return (uint32_t)((double)sad + ((double)pi_mvp_idx_bits(m, 2) * ml) / 65536.0);
 }
 
+/* xGetTemplateCost of AMVP candidate m of reference k of one request (exported for the tests). */
+uint32_t orc_template_cost(const orc_ctx* ctx, const fme_pu_req* q, int k, int m) {
+  int16_t pred[64 * 64];
+  return pi_template_cost(ctx, q, k, m, pred);
+}
+
 void orc_pred_inter_reset(orc_ctx* ctx) { memset(ctx->int_mv_2n, 0, sizeof(ctx->int_mv_2n)); }
 
 int orc_pred_inter_p(orc_ctx* ctx, const fme_pu_req* reqs, fme_pu_res* res, int n) {

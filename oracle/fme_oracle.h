@@ -141,6 +141,7 @@ int orc_mc(const orc_yuv* pics, const fme_mc_job* jobs, int n, uint8_t* y, int y
  * the reference choice, m_integerMv2Nx2N).  Returns 0 or a negative FME_E_* code. */
 int orc_pred_inter_p(orc_ctx* ctx, const fme_pu_req* reqs, fme_pu_res* res, int n);
 void orc_pred_inter_reset(orc_ctx* ctx);
+uint32_t orc_template_cost(const orc_ctx* ctx, const fme_pu_req* q, int k, int m);   /* TEncSearch.cpp:4397-4436 */
 
 /* helpers for bindings */
 size_t orc_ctx_size(void);

@@ -67,6 +67,8 @@ class Oracle:
         lib.orc_pred_inter_p.restype = C.c_int
         lib.orc_pred_inter_p.argtypes = [_P, _P, _P, C.c_int]
         lib.orc_pred_inter_reset.argtypes = [_P]
+        lib.orc_template_cost.restype = C.c_uint32
+        lib.orc_template_cost.argtypes = [_P, _P, C.c_int, C.c_int]
         lib.orc_mc.restype = C.c_int
         lib.orc_mc.argtypes = [_P, _P, C.c_int, _P, C.c_int, _P, _P, C.c_int, C.c_int, C.c_int]
         lib.orc_nn_param_count.restype = C.c_int
@@ -166,6 +168,12 @@ class Oracle:
 
     def pred_inter_reset(self):
         self.lib.orc_pred_inter_reset(self.ctx)
+
+    def template_cost(self, req, k, m):
+        """orc_template_cost: xGetTemplateCost of candidate m of reference k of one fme_pu_req."""
+        from nnfme.abi import PU_REQ_DTYPE
+        r = np.ascontiguousarray(np.asarray(req, dtype=PU_REQ_DTYPE).reshape(1))
+        return int(self.lib.orc_template_cost(self.ctx, _ptr(r), int(k), int(m)))
 
     def mc(self, pics, mc_jobs, y, cb, cr):
         """orc_mc: pics = {id: (Y, Cb, Cr)} reference pictures; predicts into y/cb/cr in place."""

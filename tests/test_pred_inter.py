@@ -254,3 +254,89 @@ def test_template_cost_matches_reference_harness():
             assert got == want, (w, h, x, y, mvx, mvy, got, want)
             n += 1
     assert n == 12 * len(synth.ALL_PU_SIZES)
+
+
+def _template_requests(rng, n):
+    """Requests whose CU sits at any depth of the quadtree (origins on the 64/32/16/8 grid, so not
+    64-aligned below depth 0), every PU shape that fits the CU, two candidates per reference with
+    MVs near and far (clipMv active)."""
+    reqs = np.zeros(n, dtype=abi.PU_REQ_DTYPE)
+    sizes = [s for s in synth.ALL_PU_SIZES]
+    for i in range(n):
+        w, h = sizes[int(rng.integers(len(sizes)))]
+        cu = max(8, 1 << int(np.ceil(np.log2(max(w, h)))))
+        cu_x = cu * int(rng.integers(0, W // cu))
+        cu_y = cu * int(rng.integers(0, H // cu))
+        x = cu_x + 4 * int(rng.integers(0, (cu - w) // 4 + 1))
+        y = cu_y + 4 * int(rng.integers(0, (cu - h) // 4 + 1))
+        reqs[i]["x"], reqs[i]["y"], reqs[i]["w"], reqs[i]["h"] = x, y, w, h
+        reqs[i]["cu_x"], reqs[i]["cu_y"] = cu_x, cu_y
+        reqs[i]["depth"] = {64: 0, 32: 1, 16: 2, 8: 3}[cu]
+        reqs[i]["org_id"] = 4
+        reqs[i]["num_refs"] = 4
+        reqs[i]["ref_id"] = [0, 1, 2, 3]
+        reqs[i]["n_cand"] = [2, 2, 1, 2]
+        span = 220 if rng.random() < 0.3 else 40
+        reqs[i]["cand"] = rng.integers(-4 * span, 4 * span + 1, (4, 2, 2))
+        reqs[i]["lambda_id"] = int(rng.integers(0, 4))
+    return reqs
+
+
+def test_oracle_template_cost_matches_reference_harness():
+    """The oracle's own xGetTemplateCost (the one its predInterSearch loop uses: clipMv +
+    mc_pred_blk + SAD + calcRdCost) against oracle/_ref's, which drives the reference's
+    TComInterpolationFilter and TComRdCost, per (request, reference, candidate), CUs at every depth."""
+    from oracle import REF_SO, Oracle, Reference
+    if not os.path.exists(REF_SO):
+        pytest.skip("oracle/_ref not built (needs /root/reference)")
+    pics = _pics()
+    ref, orc = Reference(fast_inter_mode=1), Oracle(nn_mode=0)
+    _setup(orc, pics)
+    for k, v in pics.items():
+        ref.set_picture(k, v)
+    for lid, lam in enumerate(synth.LDP_LAMBDA[22]):
+        ref.set_lambda(lid, lam)
+    reqs = _template_requests(np.random.default_rng(44), 300)
+    n = 0
+    for q in reqs:
+        for k in range(4):
+            for m in range(int(q["n_cand"][k])):
+                mx, my = (int(v) for v in q["cand"][k][m])
+                want = ref.template_cost(4, int(q["ref_id"][k]), int(q["x"]), int(q["y"]), int(q["w"]), int(q["h"]),
+                                         int(q["cu_x"]), int(q["cu_y"]), mx, my, 1, int(q["lambda_id"]))   # m_auiMVPIdxCost[m][2] = 1
+                assert orc.template_cost(q, k, m) == want, (q, k, m)
+                n += 1
+    assert n > 1500
+
+
+@pytest.mark.gpu
+def test_gpu_template_costs_match_reference_harness():
+    """fme_template_costs (the producer's AMVP stage, k_amvp_sad) against oracle/_ref's
+    xGetTemplateCost over the reference's own filters and RdCost, CUs at every depth."""
+    from oracle import REF_SO, Reference
+    from nnfme.runtime import FmeContext
+    if not os.path.exists(REF_SO):
+        pytest.skip("oracle/_ref not built")
+    pics = _pics()
+    ctx = FmeContext(nn_mode=0)
+    _setup(ctx, pics)
+    ref = Reference(fast_inter_mode=1)
+    for k, v in pics.items():
+        ref.set_picture(k, v)
+    for lid, lam in enumerate(synth.LDP_LAMBDA[22]):
+        ref.set_lambda(lid, lam)
+    reqs = _template_requests(np.random.default_rng(45), 400)
+    got = ctx.template_costs(reqs)
+    n = 0
+    for i, q in enumerate(reqs):
+        for k in range(4):
+            for m in range(2):
+                if m >= int(q["n_cand"][k]):
+                    assert got[i, k, m] == 0xFFFFFFFF
+                    continue
+                mx, my = (int(v) for v in q["cand"][k][m])
+                want = ref.template_cost(4, int(q["ref_id"][k]), int(q["x"]), int(q["y"]), int(q["w"]), int(q["h"]),
+                                         int(q["cu_x"]), int(q["cu_y"]), mx, my, 1, int(q["lambda_id"]))
+                assert got[i, k, m] == want, (i, k, m)
+                n += 1
+    assert n > 2000
