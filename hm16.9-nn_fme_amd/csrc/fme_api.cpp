@@ -145,7 +145,7 @@ struct fme_ctx {
   // Profiling: a ring of event sets, one per profiled batch, read once the batch has finished
   // (harvest_events), so profiling a run of batches adds no synchronisation.  Per set: 0 start,
   // 1 classify end, 2 schedule end = scatter begin, 3 scatter end, 4 main search end, 5 search
-  // end, 6 batch end, 7/8 auxiliary search begin/end (aux stream).
+  // end, 6 batch end.
   static constexpr int kEv = 9;
   static constexpr int kEvSets = 32;
   bool profiling = false;
@@ -153,8 +153,6 @@ struct fme_ctx {
   hipEvent_t ev[kEvSets][kEv] = {};
   long long ev_head = 0;        // sets recorded
   long long ev_tail = 0;        // sets harvested
-  bool ev_has_large[kEvSets] = {};
-  bool ev_serial[kEvSets] = {};
   bool timed = false;
   hipEvent_t ev_done = nullptr; // end of the last batch (fme_refine_status)
   bool batch_issued = false;
@@ -162,7 +160,7 @@ struct fme_ctx {
   double acc_ms[FME_NUM_TIMINGS] = {};
   int acc_batches = 0;
 
-  // auxiliary streams: the search kernels of one batch run on three streams
+  // auxiliary streams of the integer search (created on first use)
   hipStream_t aux = nullptr;
   hipStream_t aux2 = nullptr;
   hipEvent_t ev_join2 = nullptr;
@@ -176,7 +174,6 @@ hipError_t launch_nn_deep_tail(const fme_nn_net& n, const void* packed, float* m
                                const WorkBufs& w, int state_in, int engine, hipStream_t s);
 hipError_t launch_nn_deep_single(const fme_nn_net& n, const void* packed, const uint32_t* in11, int32_t* out,
                                  hipStream_t s);
-hipError_t debug_phase_cycles(unsigned long long* out16, bool reset);
 hipError_t launch_nn_single(const float* nnp, const uint32_t* in, int32_t* out, hipStream_t s);
 }
 
@@ -208,11 +205,8 @@ int fme_create(int device, const fme_config* cfg, fme_ctx** out_ctx) {
   HIP_TRY(c->nn_state.reserve(24));
   HIP_TRY(hipMemset(c->nn_state.p, 0, 24 * sizeof(uint32_t)));
   HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&c->h_counts), (kNumClasses + 1) * sizeof(int32_t), hipHostMallocDefault));
-  HIP_TRY(hipStreamCreateWithFlags(&c->aux, hipStreamNonBlocking));
   if (const char* e = getenv("FME_TZ_DEFER")) c->tz_defer = (e[0] == '1');
   if (const char* e = getenv("FME_TZ_DEFER_MIN")) c->tz_defer_min = atoi(e);
-  HIP_TRY(hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming));
-  HIP_TRY(hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming));
   if (cfg->max_jobs > 0) {
     const size_t n = (size_t)cfg->max_jobs;
     const size_t nb = (n + kJobsPerScanBlock - 1) / kJobsPerScanBlock;
@@ -553,9 +547,8 @@ static int harvest_events(fme_ctx* c, bool wait_all) {
     HIP_TRY(hipEventElapsedTime(&ms[2], e[3], e[5]));
     HIP_TRY(hipEventElapsedTime(&ms[3], e[5], e[6]));
     HIP_TRY(hipEventElapsedTime(&ms[4], e[0], e[6]));
-    HIP_TRY(hipEventElapsedTime(&ms[5], c->ev_serial[b] && c->ev_has_large[b] ? e[8] : e[3], e[4]));
-    ms[6] = 0.f;
-    if (c->ev_has_large[b]) HIP_TRY(hipEventElapsedTime(&ms[6], e[7], e[8]));
+    HIP_TRY(hipEventElapsedTime(&ms[5], e[3], e[4]));
+    ms[6] = 0.f;   // no auxiliary search kernel any more (every shape runs in the lane kernel)
     for (int i = 0; i < FME_NUM_TIMINGS; i++) c->acc_ms[i] += ms[i];
     c->acc_batches++;
     c->timed = true;
@@ -617,26 +610,15 @@ static int refine_batch(fme_ctx* c, const fme_job* d_jobs, fme_result* d_res, fm
   if (prof) HIP_TRY(hipEventRecord(ev[2], s));
   HIP_TRY(launch_scatter(a, w, s));
   if (prof) HIP_TRY(hipEventRecord(ev[3], s));
-  // the lane kernel (every power-of-two shape) on the batch stream, the cooperative AMP kernels
-  // beside it on the auxiliary stream, joined before the NN tail
-  HIP_TRY(hipEventRecord(c->ev_fork, s));
-  HIP_TRY(hipStreamWaitEvent(c->aux, c->ev_fork, 0));
+  // the lane kernel: every PU shape, one launch on the batch stream
   HIP_TRY(launch_search_lane(a, w, s));
   if (prof) HIP_TRY(hipEventRecord(ev[4], s));
-  if (prof) HIP_TRY(hipEventRecord(ev[7], c->aux));
-  HIP_TRY(launch_search_small(a, w, c->aux));
-  HIP_TRY(launch_search_large(a, w, c->aux));
-  if (prof) HIP_TRY(hipEventRecord(ev[8], c->aux));
-  HIP_TRY(hipEventRecord(c->ev_join, c->aux));
-  HIP_TRY(hipStreamWaitEvent(s, c->ev_join, 0));
   if (prof) HIP_TRY(hipEventRecord(ev[5], s));
   HIP_TRY(c->cfg.nn_mode == 2
               ? launch_nn_deep_tail(c->net, c->d_net.p, c->nn_margin, a, w, c->state_cur, c->nn_engine, s)
               : launch_nn_tail(a, w, c->d_nn.p, c->state_cur, s));
   if (prof) {
     HIP_TRY(hipEventRecord(ev[6], s));
-    c->ev_has_large[eb] = true;
-    c->ev_serial[eb] = false;
     c->ev_head++;
   }
   HIP_TRY(hipEventRecord(c->ev_done, s));
@@ -748,7 +730,11 @@ static int tz_run(fme_ctx* c, fme_job* d_jobs, const fme_tz_ext* d_ext, uint32_t
   if (c->profiling) HIP_TRY(hipEventRecord(c->ev_tz[0], s));
   // the three unit-shape kernels are latency-bound and independent: 4x8 and 8x4 units on the two
   // auxiliary streams, 8x8 units on the caller's stream, joined before returning
+  // the integer search's own auxiliary streams (the refinement batch uses none)
+  if (!c->aux) HIP_TRY(hipStreamCreateWithFlags(&c->aux, hipStreamNonBlocking));
   if (!c->aux2) HIP_TRY(hipStreamCreateWithFlags(&c->aux2, hipStreamNonBlocking));
+  if (!c->ev_fork) HIP_TRY(hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming));
+  if (!c->ev_join) HIP_TRY(hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming));
   if (!c->ev_join2) HIP_TRY(hipEventCreateWithFlags(&c->ev_join2, hipEventDisableTiming));
   HIP_TRY(hipEventRecord(c->ev_fork, s));
   HIP_TRY(hipStreamWaitEvent(c->aux, c->ev_fork, 0));
@@ -956,7 +942,7 @@ int fme_nn_pred_single(fme_ctx* c, const uint32_t* e, uint32_t cc, int pu_h, int
 int fme_search_kernel_of_shape(int width, int height) {
   for (int k = 0; k < kNumClasses; k++)
     if (kClassW[k] == width && kClassH[k] == height) {
-      return search_kernel_of(k) == kSearchLane ? 0 : 1;
+      return 0;   // every shape runs in the lane kernel
     }
   return -1;
 }
@@ -1081,13 +1067,6 @@ int fme_set_profiling(fme_ctx* c, int enable) {
     if (rc) return rc;
   }
   c->profiling = enable != 0;
-  return FME_OK;
-}
-
-int fme_debug_phase_cycles(uint64_t* out16, int reset) {
-  if (!out16) return fail(FME_E_INVALID, "fme_debug_phase_cycles: null argument");
-  HIP_TRY(hipDeviceSynchronize());
-  HIP_TRY(debug_phase_cycles(reinterpret_cast<unsigned long long*>(out16), reset != 0));
   return FME_OK;
 }
 

@@ -89,13 +89,10 @@ struct WorkBufs {
   fme_mv_result* mv_out; // compact per-job output (fme_refine_mv*), or null
 };
 
-// Schedule of the search kernels.  Kernel k (lane-per-unit, cooperative 256-lane, cooperative
-// 512-lane) serves class c with its tiles [prefix[k][c], prefix[k][c+1]) (lane kernel: 64-lane
-// wave tiles; cooperative: blocks); every class belongs to exactly one kernel (search_kernel_of).
-// Class c's jobs are sjobs/perm[class_off[c] .. + class_cnt[c]).
-enum { kSearchLane = 0, kSearchCoop = 1, kSearchCoopLarge = 2, kSearchKernels = 3 };
+// Schedule of the search kernel (k_schedule builds it on the device): class c's jobs are
+// sjobs/perm[class_off[c] .. + class_cnt[c]) and its 64-lane wave tiles [prefix[c], prefix[c+1]).
 struct Schedule {
-  int32_t prefix[kSearchKernels][kNumClasses + 1];
+  int32_t prefix[kNumClasses + 1];
   int32_t class_off[kNumClasses];
   int32_t class_cnt[kNumClasses];
   // The lane kernel's per-XCD tile queues: XCD x owns the x-th contiguous eighth of every
@@ -106,11 +103,10 @@ struct Schedule {
   int32_t pad_[3];
 };
 
-// What k_schedule needs to know about the search kernels (host tables, one per build).
+// What k_schedule needs to know about the search kernel: lanes per PU of each class (its unit
+// count rounded up to a power of two).
 struct SchedParams {
-  int8_t kern[kNumClasses];       // search_kernel_of(c)
-  int32_t lanes[kNumClasses];     // lane kernel: lanes per PU; cooperative: PUs per tile
-  int32_t tiles_per_block;        // cooperative kernels
+  int32_t lanes[kNumClasses];
 };
 SchedParams sched_params();
 
@@ -140,8 +136,6 @@ hipError_t launch_tz(const TzArgs& ta, const TzSchedule& sc, int kid, hipStream_
 hipError_t launch_tz_raster(const TzArgs& ta, const TzSchedule& sc, int kid, int nq, hipStream_t s);
 
 // Host-side launch helpers (fme_kernels.hip).
-int pus_per_tile(int cls);
-size_t lds_bytes_for_class(int cls);
 hipError_t launch_classify(const BatchArgs& a, const WorkBufs& w, hipStream_t s);
 // one block: w.counts -> *w.sched (class offsets, block ranges, XCD queues, invalid count)
 hipError_t launch_schedule(const WorkBufs& w, const SchedParams& p, hipStream_t s);
@@ -150,15 +144,11 @@ hipError_t launch_scatter(const BatchArgs& a, const WorkBufs& w, hipStream_t s);
 hipError_t launch_put_state(uint32_t* dst, const uint32_t* v12, hipStream_t s);
 // the picture / lambda tables written in stream order from kernel arguments
 hipError_t launch_put_tables(PicDesc* d_pics, double* d_ml, const PicDesc* pics, const double* ml, hipStream_t s);
-int tiles_per_block();
-int search_kernel_of(int cls);                      // kSearchLane .. kSearchCoopLarge
-// The search kernels read their schedule from *w.sched (no host round trip).  The lane kernel is
-// launched with enough workgroups to fill the chip, each wave pulling tiles from its XCD's queue
-// (then the other XCDs'); a cooperative kernel strides over its blocks.  `a.n` bounds the work.
+// The search kernel reads its schedule from *w.sched (no host round trip); it is launched with
+// enough workgroups to fill the chip, each pulling tiles from its XCD's queue (then the other
+// XCDs').  `a.n` bounds the work.
 hipError_t launch_search_lane(const BatchArgs& a, const WorkBufs& w, hipStream_t s);
-hipError_t launch_search_large(const BatchArgs& a, const WorkBufs& w, hipStream_t s);
-hipError_t launch_search_small(const BatchArgs& a, const WorkBufs& w, hipStream_t s);
-int lane_lanes_per_pu(int cls);                    // 0: not a lane-kernel class
+int lane_lanes_per_pu(int cls);                    // lanes of a class's PU group (pow2), 0: none
 int cu_count(int device);                          // compute units (workgroup budget of a launch)
 // Packed NN layout for the tail kernel (nn_pack, fme_kernels.hip): offsets in floats, every
 // pair region 8-byte aligned.

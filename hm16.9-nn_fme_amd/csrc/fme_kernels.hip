@@ -176,29 +176,19 @@ __global__ __launch_bounds__(64) void k_schedule(WorkBufs w, SchedParams p) {
   Schedule* sc = w.sched;
   const int inv = w.counts[kNumClasses];
   const int cnt = (c < kNumClasses && inv == 0) ? w.counts[c] : 0;
-  int kern = -1, nb = 0;
-  if (cnt > 0) {
-    kern = p.kern[c];
-    if (kern == kSearchLane) {
-      nb = (int)(((long long)cnt * p.lanes[c] + 63) / 64);   // 64-lane wave tiles
-    } else {
-      const int tiles = (cnt + p.lanes[c] - 1) / p.lanes[c];
-      nb = (tiles + p.tiles_per_block - 1) / p.tiles_per_block;
-    }
-  }
+  const int nb = cnt > 0 ? (int)(((long long)cnt * p.lanes[c] + 63) / 64) : 0;   // 64-lane wave tiles
   const int off = wave_excl_scan(cnt);
   if (c < kNumClasses) {
     sc->class_off[c] = off;
     sc->class_cnt[c] = cnt;
   }
-#pragma unroll
-  for (int q = 0; q < kSearchKernels; q++) {
-    const int ex = wave_excl_scan(kern == q ? nb : 0);
-    if (c <= kNumClasses) sc->prefix[q][c] = ex;     // [kNumClasses] = the kernel's total
+  {
+    const int ex = wave_excl_scan(nb);
+    if (c <= kNumClasses) sc->prefix[c] = ex;     // [kNumClasses] = the total
   }
 #pragma unroll
   for (int x = 0; x < 8; x++) {
-    const int mine = kern == kSearchLane ? (nb >> 3) + (x < (nb & 7) ? 1 : 0) : 0;
+    const int mine = (nb >> 3) + (x < (nb & 7) ? 1 : 0);
     const int ex = wave_excl_scan(mine);
     if (c <= kNumClasses) sc->xq[x][c] = ex;
   }
@@ -568,11 +558,7 @@ hipError_t launch_scatter(const BatchArgs& a, const WorkBufs& w, hipStream_t s) 
 
 SchedParams sched_params() {
   SchedParams p{};
-  for (int c = 0; c < kNumClasses; c++) {
-    p.kern[c] = (int8_t)search_kernel_of(c);
-    p.lanes[c] = lane_lanes_per_pu(c) > 0 ? lane_lanes_per_pu(c) : pus_per_tile(c);
-  }
-  p.tiles_per_block = tiles_per_block();
+  for (int c = 0; c < kNumClasses; c++) p.lanes[c] = lane_lanes_per_pu(c);
   return p;
 }
 

@@ -75,6 +75,8 @@ __device__ __forceinline__ uint32_t group_sum(uint32_t v) {
   return v;
 }
 
+__host__ __device__ constexpr int pow2_at_least(int v) { return v <= 1 ? 1 : 2 * pow2_at_least((v + 1) / 2); }
+
 // low 16 bits of a and b -> one packed pair (a in the low half)
 __device__ __forceinline__ uint32_t pack2(int a, int b) { return __builtin_amdgcn_perm((uint32_t)b, (uint32_t)a, 0x05040100u); }
 __device__ __forceinline__ int clamp_s8(int v) { return min(max(v, -128), 127); }
@@ -192,20 +194,22 @@ __host__ __device__ constexpr int emi_dy(int p) { return p >= 1 && p <= 3 ? -1 :
 // Candidate passes of one unit.  v: re-centred window (rows -4..UH+3, cols -4..UW+3, s - 128
 // bytes), K: key - 128 as packed column pairs.  Each pass keeps at most two key - pred arrays.
 // =============================================================================================
+// `live`: ~0 on the lanes of a PU's units, 0 on the idle lanes that pad a group of 6 / 12 / 48
+// units (AMP shapes) to a power of two, so they add nothing to the group's sum.
 template <int L>
-__device__ __forceinline__ void take_half(int i, uint32_t part, double ml, int mvx, int mvy, int px, int py,
-                                          uint32_t& best, int& bi) {
-  const uint32_t d = group_sum<L>(part) + mv_cost(ml, mv_bits(2 * mvx + h9_dx(i), 2 * mvy + h9_dy(i), 1, px, py));
+__device__ __forceinline__ void take_half(int i, uint32_t part, uint32_t live, double ml, int mvx, int mvy, int px,
+                                          int py, uint32_t& best, int& bi) {
+  const uint32_t d = group_sum<L>(part & live) + mv_cost(ml, mv_bits(2 * mvx + h9_dx(i), 2 * mvy + h9_dy(i), 1, px, py));
   if (d < best || (d == best && i < bi)) {
     best = d;
     bi = i;
   }
 }
 template <int L>
-__device__ __forceinline__ void take_qtr(int i, uint32_t part, double ml, int mvx, int mvy, int hx, int hy,
-                                         int px, int py, uint32_t& best, int& bi) {
+__device__ __forceinline__ void take_qtr(int i, uint32_t part, uint32_t live, double ml, int mvx, int mvy, int hx,
+                                         int hy, int px, int py, uint32_t& best, int& bi) {
   const int qx = 2 * hx + q9_dx(i), qy = 2 * hy + q9_dy(i);
-  const uint32_t d = group_sum<L>(part) + mv_cost(ml, mv_bits(4 * mvx + qx, 4 * mvy + qy, 0, px, py));
+  const uint32_t d = group_sum<L>(part & live) + mv_cost(ml, mv_bits(4 * mvx + qx, 4 * mvy + qy, 0, px, py));
   if (d < best || (d == best && i < bi)) {
     best = d;
     bi = i;
@@ -415,14 +419,14 @@ __device__ __forceinline__ void qtr_pass(uint32_t (&v)[UH + 8][UW / 4 + 2], cons
 
 template <int L, int UW, int UH, int T, int... PS>
 __device__ __forceinline__ void qtr_all(uint32_t (&v)[UH + 8][UW / 4 + 2], const KeySrc<UW, UH / 2>& K,
-                                        bool had, int hx, int hy, double ml, int mvx, int mvy, int px, int py,
-                                        uint32_t& best, int& bi, std::integer_sequence<int, PS...>) {
+                                        bool had, uint32_t live, int hx, int hy, double ml, int mvx, int mvy, int px,
+                                        int py, uint32_t& best, int& bi, std::integer_sequence<int, PS...>) {
   auto one = [&](auto ps_c) {
     constexpr int ps = decltype(ps_c)::value;
     uint32_t d[2];
     qtr_pass<UW, UH, T, ps>(v, K, had, hx, hy, d);
-    take_qtr<L>(qp_idx0(ps), d[0], ml, mvx, mvy, hx, hy, px, py, best, bi);
-    if constexpr (qp_l1(ps) >= 0) take_qtr<L>(qp_idx1(ps), d[1], ml, mvx, mvy, hx, hy, px, py, best, bi);
+    take_qtr<L>(qp_idx0(ps), d[0], live, ml, mvx, mvy, hx, hy, px, py, best, bi);
+    if constexpr (qp_l1(ps) >= 0) take_qtr<L>(qp_idx1(ps), d[1], live, ml, mvx, mvy, hx, hy, px, py, best, bi);
   };
   (one(std::integral_constant<int, PS>{}), ...);
 }
@@ -471,8 +475,13 @@ __device__ __forceinline__ void lane_unit(const BatchArgs& a, const fme_job* __r
                                           int wt) {
   constexpr int T = ((PW % 8) == 0 && (PH % 8) == 0) ? 8 : 4;
   static_assert(UW % T == 0 && UH % T == 0, "unit must hold whole SATD tiles");
-  constexpr int UX = PW / UW, L = UX * (PH / UH);
-  static_assert((L & (L - 1)) == 0 && L <= 64, "lanes per PU must be a power of two");
+  static_assert(PW % UW == 0 && PH % UH == 0, "units tile the PU");
+  constexpr int UX = PW / UW, LR = UX * (PH / UH);   // units of the PU
+  constexpr int L = pow2_at_least(LR);                // lanes of its group (AMP: 6 -> 8, 12 -> 16, 48 -> 64)
+  static_assert(L <= 64, "a PU's group fits one wave");
+  // the modified setDistParam's integer metric (TComRdCost.cpp:200-230): SAD for W in {12, 24, 48},
+  // with xTZSearchHelp's FEN row subsampling (TEncSearch.cpp:1158-1164); SSE otherwise
+  constexpr bool kSadEmi = PW == 12 || PW == 24 || PW == 48;
   constexpr int RW = UH + 10;                 // window rows (-5 .. UH+4)
   constexpr int NWL = (UW + 13 + 3) / 4;      // dwords loaded per row (any start alignment)
   constexpr int NW = (UW + 10 + 3) / 4;       // dwords per row after re-alignment
@@ -485,7 +494,9 @@ __device__ __forceinline__ void lane_unit(const BatchArgs& a, const fme_job* __r
   const int u = gl - p * L;
   const bool active = p < cls_cnt;
   if (!active) p = cls_cnt - 1;              // duplicate work, no stores (keeps the group whole)
-  const int ux = u % UX, uy = u / UX;
+  const uint32_t live = u < LR ? ~0u : 0u;   // padding lanes repeat the last unit, summed as 0
+  const int uu = u < LR ? u : LR - 1;
+  const int ux = uu % UX, uy = uu / UX;
 
   const fme_job j = sjobs[cls_off + p];
   const int jid = perm[cls_off + p];
@@ -553,7 +564,36 @@ __device__ __forceinline__ void lane_unit(const BatchArgs& a, const fme_job* __r
     // Row-major: window row R (= 5 + dy + r) serves positions (dx, dy) with org row r = R-5-dy;
     // its byte groups at dx = -1, 0, 1 are formed once.
     uint32_t e9[9];
-    if (!kbuf) {   // SSE = So2 - 2 Sop + Spp on the s - 128 bytes
+    if constexpr (kSadEmi) {   // SAD of the (even, with FEN) rows, doubled when subsampled
+      const bool sub = a.fen == 1 || a.fen == 3;   // and PH > 8: every 12/24/48-wide shape
+#pragma unroll
+      for (int q = 0; q < 9; q++) e9[q] = 0;
+#pragma unroll
+      for (int r = 0; r < UH; r++) {
+        if ((r & 1) && sub) continue;   // unit rows start on even PU rows
+#pragma unroll
+        for (int pos = 0; pos < 9; pos++) {
+          const int R = r + 5 + emi_dy(pos);
+#pragma unroll
+          for (int k = 0; k < UW / 4; k++) {
+            const uint32_t pv = rbytes(w[R], 5 + emi_dx(pos) + 4 * k) ^ 0x80808080u;   // samples 0..255
+            if (!kbuf) {
+              e9[pos] = __builtin_amdgcn_sad_u8(kraw[r][k] ^ 0x80808080u, pv, e9[pos]);
+            } else {   // int16 key: |key - pred| per sample
+              const int k0 = (int16_t)(kraw[r][2 * k] & 0xFFFF), k1 = (int16_t)(kraw[r][2 * k] >> 16);
+              const int k2 = (int16_t)(kraw[r][2 * k + 1] & 0xFFFF), k3 = (int16_t)(kraw[r][2 * k + 1] >> 16);
+              e9[pos] += (uint32_t)(abs(k0 - (int)(pv & 0xFF)) + abs(k1 - (int)((pv >> 8) & 0xFF)) +
+                                    abs(k2 - (int)((pv >> 16) & 0xFF)) + abs(k3 - (int)(pv >> 24)));
+            }
+          }
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      if (sub) {
+#pragma unroll
+        for (int q = 0; q < 9; q++) e9[q] <<= 1;
+      }
+    } else if (!kbuf) {   // SSE = So2 - 2 Sop + Spp on the s - 128 bytes
       int so2 = 0, sop[9], spp[3][3];   // spp[dx][dy]
 #pragma unroll
       for (int i = 0; i < 9; i++) sop[i] = 0;
@@ -617,7 +657,7 @@ __device__ __forceinline__ void lane_unit(const BatchArgs& a, const fme_job* __r
       }
     }
 #pragma unroll
-    for (int pos = 0; pos < 9; pos++) e9[pos] = group_sum<L>(e9[pos]);
+    for (int pos = 0; pos < 9; pos++) e9[pos] = group_sum<L>(e9[pos] & live);
     // decision (TEncSearch.cpp:1341-1376 visiting order and range checks, 1155-1188 update)
     const int sx = mvx, sy = mvy;
     uint32_t best = e9[0] + mv_cost(ml, mv_bits(sx, sy, 2, mvp_x, mvp_y));
@@ -700,27 +740,27 @@ __device__ __forceinline__ void lane_unit(const BatchArgs& a, const fme_job* __r
   {
     uint32_t d[3] = {0u, 0u, 0u};
     half_center<UW, UH, T>(v, K, had, d);
-    take_half<L>(0, d[0], ml, mvx, mvy, mvp_x, mvp_y, hbest, hbi);
-    take_half<L>(1, d[1], ml, mvx, mvy, mvp_x, mvp_y, hbest, hbi);
-    take_half<L>(2, d[2], ml, mvx, mvy, mvp_x, mvp_y, hbest, hbi);
+    take_half<L>(0, d[0], live, ml, mvx, mvy, mvp_x, mvp_y, hbest, hbi);
+    take_half<L>(1, d[1], live, ml, mvx, mvy, mvp_x, mvp_y, hbest, hbi);
+    take_half<L>(2, d[2], live, ml, mvx, mvy, mvp_x, mvp_y, hbest, hbi);
   }
   {
     uint32_t d[3];
     half_side<UW, UH, T, 0>(v, K, had, d);
-    take_half<L>(3, d[0], ml, mvx, mvy, mvp_x, mvp_y, hbest, hbi);
-    take_half<L>(5, d[1], ml, mvx, mvy, mvp_x, mvp_y, hbest, hbi);
-    take_half<L>(7, d[2], ml, mvx, mvy, mvp_x, mvp_y, hbest, hbi);
+    take_half<L>(3, d[0], live, ml, mvx, mvy, mvp_x, mvp_y, hbest, hbi);
+    take_half<L>(5, d[1], live, ml, mvx, mvy, mvp_x, mvp_y, hbest, hbi);
+    take_half<L>(7, d[2], live, ml, mvx, mvy, mvp_x, mvp_y, hbest, hbi);
     half_side<UW, UH, T, 1>(v, K, had, d);
-    take_half<L>(4, d[0], ml, mvx, mvy, mvp_x, mvp_y, hbest, hbi);
-    take_half<L>(6, d[1], ml, mvx, mvy, mvp_x, mvp_y, hbest, hbi);
-    take_half<L>(8, d[2], ml, mvx, mvy, mvp_x, mvp_y, hbest, hbi);
+    take_half<L>(4, d[0], live, ml, mvx, mvy, mvp_x, mvp_y, hbest, hbi);
+    take_half<L>(6, d[1], live, ml, mvx, mvy, mvp_x, mvp_y, hbest, hbi);
+    take_half<L>(8, d[2], live, ml, mvx, mvy, mvp_x, mvp_y, hbest, hbi);
   }
   const int hx = h9_dx(hbi), hy = h9_dy(hbi);
 
   // ---- 4. quarter-pel stage: passes over column phases (Q9 candidate 0 = the half best) -------
   uint32_t qbest = hbest;
   int qbi = 0;
-  qtr_all<L, UW, UH, T>(v, K, had, hx, hy, ml, mvx, mvy, mvp_x, mvp_y, qbest, qbi,
+  qtr_all<L, UW, UH, T>(v, K, had, live, hx, hy, ml, mvx, mvy, mvp_x, mvp_y, qbest, qbi,
                         std::make_integer_sequence<int, kQPasses>{});
   const int bq = qbi;
 
@@ -755,7 +795,13 @@ __device__ __forceinline__ int xcc_id() {
   X(2, 8, 8, 8, 8) X(5, 8, 16, 8, 8) X(6, 16, 8, 8, 8) X(9, 16, 16, 8, 8) X(10, 8, 32, 8, 8)         \
   X(11, 32, 8, 8, 8) X(12, 16, 32, 8, 8) X(13, 32, 16, 8, 8) X(16, 32, 32, 8, 8) X(17, 16, 64, 8, 8) \
   X(18, 64, 16, 8, 8) X(19, 32, 64, 8, 8) X(20, 64, 32, 8, 8) X(23, 64, 64, 8, 8)
-#define FME_LANE_CLASSES(X) FME_LANE48_CLASSES(X) FME_LANE84_CLASSES(X) FME_LANE88_CLASSES(X)
+// the AMP shapes whose unit count is not a power of two: 12x16 / 16x12 in 4x8 / 8x4 units (6 of 8
+// lanes), 24x32 / 32x24 in 8x8 units (12 of 16), 48x64 / 64x48 (48 of 64)
+#define FME_LANE_AMP_CLASSES(X)                                                                      \
+  X(7, 12, 16, 4, 8) X(8, 16, 12, 8, 4) X(14, 24, 32, 8, 8) X(15, 32, 24, 8, 8) X(21, 48, 64, 8, 8)   \
+  X(22, 64, 48, 8, 8)
+#define FME_LANE_CLASSES(X) \
+  FME_LANE48_CLASSES(X) FME_LANE84_CLASSES(X) FME_LANE88_CLASSES(X) FME_LANE_AMP_CLASSES(X)
 
 // One kernel serves every lane class.  A workgroup claims four consecutive 64-lane wave tiles
 // (one per wave; a tile holds 64 / L PUs of one class) per atomic from its XCD's queue
@@ -798,7 +844,7 @@ void k_search_lane(BatchArgs a, WorkBufs w) {
     if (tw < len) {
       int c = 0;
       while (c < kNumClasses - 1 && tw >= sc->xq[x][c + 1]) c++;
-      const int nt = sc->prefix[kSearchLane][c + 1] - sc->prefix[kSearchLane][c];
+      const int nt = sc->prefix[c + 1] - sc->prefix[c];
       const int wt = x * (nt >> 3) + min(x, nt & 7) + (tw - sc->xq[x][c]);
       switch (c) {
         FME_LANE_CLASSES(FME_CASE)
@@ -816,7 +862,7 @@ void k_search_lane(BatchArgs a, WorkBufs w) {
 // Lanes per PU of a lane-kernel class, 0 for classes the cooperative kernels serve.
 int lane_lanes_per_pu(int cls) {
   switch (cls) {
-#define FME_L(ID, PW_, PH_, UW_, UH_) case ID: return (PW_ / UW_) * (PH_ / UH_);
+#define FME_L(ID, PW_, PH_, UW_, UH_) case ID: return pow2_at_least((PW_ / UW_) * (PH_ / UH_));
     FME_LANE_CLASSES(FME_L)
 #undef FME_L
     default: return 0;

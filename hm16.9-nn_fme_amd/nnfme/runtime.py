@@ -24,7 +24,7 @@ ABI_SYMBOLS = (
     "fme_bind_picture_device", "fme_set_lambda", "fme_set_motion_lambda", "fme_set_keys",
     "fme_load_nn_weights", "fme_nn_reset_state", "fme_nn_get_state", "fme_nn_set_state", "fme_refine", "fme_refine_device",
     "fme_frac_dif_single", "fme_nn_pred_single", "fme_set_profiling", "fme_last_timings",
-    "fme_accumulated_timings", "fme_search_kernel_of_shape", "fme_debug_phase_cycles",
+    "fme_accumulated_timings", "fme_search_kernel_of_shape",
     "fme_set_picture_chroma", "fme_bind_picture_chroma_device", "fme_motion_compensate",
     "fme_motion_compensate_device", "fme_mc_invalid_count", "fme_mc_last_ms",
     "fme_integer_search", "fme_integer_search_device", "fme_integer_search_last_ms",
@@ -80,7 +80,6 @@ def load_library(path=None):
         "fme_last_timings": (I, [P, P, I]),
         "fme_accumulated_timings": (I, [P, P, I, I]),
         "fme_search_kernel_of_shape": (I, [I, I]),
-        "fme_debug_phase_cycles": (I, [P, I]),
         "fme_set_picture_chroma": (I, [P, I, P, P, I, P]),
         "fme_bind_picture_chroma_device": (I, [P, I, P, P, I]),
         "fme_motion_compensate": (I, [P, P, I, P, I, P, P, I, I, I, P]),
@@ -356,11 +355,6 @@ class FmeContext:
         if n < 0:
             _check(self.lib, n)
         return n, dict(zip(TIMING_NAMES, ms.tolist()))
-
-    def debug_phase_cycles(self, reset=True):
-        out = np.zeros(16, np.uint64)
-        _check(self.lib, self.lib.fme_debug_phase_cycles(_ptr(out), int(reset)))
-        return out
 
     def nn_pred_single(self, e, c, pu_h, pu_w):
         e = np.ascontiguousarray(e, dtype=np.uint32)

@@ -437,24 +437,20 @@ int fme_mc_last_ms(fme_ctx* ctx, float* ms);
 /* ---- instrumentation (an extension; the reference has no counterpart) ------------------- *
  * With profiling on, fme_refine/fme_refine_device record HIP events around each kernel of
  * the batch on the streams the kernels run on.  Device milliseconds, FME_NUM_TIMINGS values:
- * [0] classify, [1] scatter, [2] search phase (EMI + FracDIF, both shape kernels),
- * [3] NN + tail, [4] whole batch (first kernel start to last kernel end, host sync included),
- * [5] main search kernel (batch stream), [6] auxiliary search kernels (their own stream; 0 if
- * not launched).
+ * [0] classify, [1] schedule + scatter, [2] search phase (EMI + FracDIF), [3] NN + tail,
+ * [4] whole batch (first kernel start to last kernel end), [5] the search kernel, [6] 0 (an
+ * auxiliary search kernel in earlier versions; every PU shape now runs in the one kernel).
  * fme_last_timings waits for the last profiled batch.  fme_accumulated_timings returns the
  * sums over every profiled batch since the last reset (the return value is the batch count);
  * a batch's events are read at the next batch's own host synchronisation, so profiling a
  * run of batches adds no synchronisation.                                                  */
 #define FME_NUM_TIMINGS 7
 int fme_set_profiling(fme_ctx* ctx, int enable);
-/* Which search kernel serves PU shape width x height: 0 the main one (timings[5]), 1 an
- * auxiliary one (timings[6]), -1 unsupported shape. */
+/* Which search kernel serves PU shape width x height: 0 the lane kernel (timings[5]; every HEVC
+ * inter PU shape), -1 unsupported shape. */
 int fme_search_kernel_of_shape(int width, int height);
 int fme_last_timings(fme_ctx* ctx, float* ms, int count);
 int fme_accumulated_timings(fme_ctx* ctx, double* ms, int count, int reset);
-/* Diagnostic builds (FME_STAMPS=1) only: per-phase shader cycles of the search kernels summed
- * over workgroups ([0..8] phases, [15] workgroups); zeros otherwise.  Resets when reset != 0. */
-int fme_debug_phase_cycles(uint64_t* out16, int reset);
 
 #ifdef __cplusplus
 }
