@@ -1,4 +1,5 @@
-"""Frame sharding across GPUs (one process per GPU, torch.distributed over RCCL/xGMI).
+"""Frame sharding across GPUs (one process per GPU, torch.distributed over RCCL/xGMI): the
+picture ring and the NN-state chaining (nnfme.pipeline.FrameReplay drives them for the bench).
 
 Sub-pel jobs are independent given (original picture, reference pictures) — SURVEY.md §8(e).
 Frames are dealt round-robin to ranks; the only exchange is the rank that owns the pictures
@@ -103,8 +104,10 @@ def fix_frame_prefix(engine, jobs, results, carry):
     k = uninit_prefix(results)
     if k == 0 or not int(np.asarray(carry)[11]):
         return results
+    saved = engine.nn_get_state()   # the engine's own state is left as it was
     engine.nn_set_state(carry)
     fixed = engine.refine(jobs[:k])
+    engine.nn_set_state(saved)
     out = results.copy()
     out[:k] = fixed
     # status bits are relative to the context, keep the sequential meaning

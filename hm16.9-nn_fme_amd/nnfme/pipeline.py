@@ -127,6 +127,25 @@ class FrameReplay:
             else:
                 dist.broadcast(dst, src=src_rank, group=self.group)
 
+    def _upload_run(self, dst, d0, g0, count, stream):
+        """Planes of frames g0 .. g0+count-1 into dst[d0 ..]: one copy per run of frames that is
+        contiguous in the pool (a small-frame batch is a few large copies, not many small ones)."""
+        i = 0
+        while i < count:
+            s = (g0 + i) % self.P
+            run = min(count - i, self.P - s)
+            _memcpy_async(dst[d0 + i], self.pool[s], run * self.H * self.W, H2D, stream)
+            i += run
+
+    def _publish_run(self, g0, count, src_rank, stream):
+        """Reconstructions of frames g0 .. g0+count-1, uploaded by src_rank (one copy per pool
+        run), broadcast to every rank."""
+        if self.world == 1:
+            self._upload_run(self.recon, g0 + REFS, g0, count, stream)
+            return
+        for j in range(count):
+            self._publish(g0 + j, src_rank)
+
     def prime(self):
         """References of the first frames (recon -4 .. -2), before the run (untimed)."""
         with self.torch.cuda.stream(self.s_copy):
@@ -159,12 +178,10 @@ class FrameReplay:
             if k >= 2:
                 cp.wait_event(self.ev_comp[b])            # step k-2 is done with the slot
             _memcpy_async(self.d_jobs[b], self.h_jobs, self.h_jobs.numel(), H2D, cp)
-            for j in range(F):
-                _memcpy_async(self.org[k * F + j], self.pool[(f0 + j) % self.P], self.H * self.W, H2D, cp)
+            self._upload_run(self.org, k * F, f0, F, cp)
             base = k * self.world * F
             for r in range(self.world):   # recon(first frame of rank r's batch - 1 + j), by rank r
-                for j in range(F):
-                    self._publish(base + r * F + j - 1, r)
+                self._publish_run(base + r * F - 1, F, r, cp)
             self.ev_in[b].record(cp)
         self.uploaded = k
 
