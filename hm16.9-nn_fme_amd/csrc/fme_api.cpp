@@ -130,10 +130,11 @@ struct fme_ctx {
   hipEvent_t ev_tz[2] = {nullptr, nullptr};
   bool tz_timed = false;
   // predInterSearch producer: m_integerMv2Nx2N[REF_PIC_LIST_0][k] (TEncSearch.h:118), AMVP staging
-  int16_t int_mv_2n[FME_MAX_REFS][2] = {};
+  int16_t int_mv_2n[2][FME_MAX_REFS][2] = {};   // m_integerMv2Nx2N[list][ref]
   DevBuf<AmvpTask> d_amvp;
   DevBuf<int16_t> d_tz_emi;   // [n][2] post-EMI integer MVs (producer levels)
   DevBuf<uint32_t> d_amvp_sad;
+  DevBuf<BiKeyTask> d_bikey;
 
   std::unique_ptr<fme_ctx> single;  // private context for the single-PU entry points
   DevBuf<uint8_t> single_pic;
@@ -230,7 +231,7 @@ int fme_destroy(fme_ctx* c) {
     if (c->chroma_owned[i]) (void)hipFree(c->chroma_owned[i]);
   c->d_mc_jobs.release(); c->d_mc_planes.release(); c->d_mc_invalid.release();
   c->d_tz_ext.release(); c->d_tz_sad.release(); c->d_tz_rst.release(); c->d_tz_rq.release();
-  c->d_amvp.release(); c->d_amvp_sad.release(); c->d_tz_emi.release();
+  c->d_amvp.release(); c->d_amvp_sad.release(); c->d_bikey.release(); c->d_tz_emi.release();
   for (auto& e : c->ev_tz)
     if (e) (void)hipEventDestroy(e);
   for (auto& e : c->ev_mc)
@@ -1128,12 +1129,78 @@ void clip_qpel(int& x, int& y, int pw, int ph, int cu_x, int cu_y) {
 }
 int round4(int v) { return (v + 2) >> 2; }   // TComMv::divideByPowerOf2(2)
 
+// xGetBlkBits (TEncSearch.cpp:4286-4333), B slice: uiBlkBit[0..2]
+void blk_bits_b(int part_size, int part_idx, int last_mode, uint32_t out[3]) {
+  static const uint32_t hor[2][3][3] = {{{0, 0, 3}, {0, 0, 0}, {0, 0, 0}}, {{5, 7, 7}, {7, 5, 7}, {6, 6, 6}}};
+  static const uint32_t ver[2][3][3] = {{{0, 2, 3}, {0, 0, 0}, {0, 0, 0}}, {{5, 7, 7}, {5, 5, 7}, {6, 6, 6}}};
+  if (part_size == FME_PART_2Nx2N || part_size == FME_PART_NxN) {
+    out[0] = 3; out[1] = 3; out[2] = 5;
+    return;
+  }
+  const bool hz = part_size == FME_PART_2NxN || part_size == FME_PART_2NxnU || part_size == FME_PART_2NxnD;
+  const uint32_t* t = hz ? hor[part_idx][last_mode] : ver[part_idx][last_mode];
+  out[0] = t[0]; out[1] = t[1]; out[2] = t[2];
+}
+uint32_t ref_bits(int k, int num_refs) {   // TEncSearch.cpp:3792-3800
+  return num_refs <= 1 ? 0u : (uint32_t)k + 1u - (k == num_refs - 1 ? 1u : 0u);
+}
+// xCheckBestMVP (TEncSearch.cpp:4344-4394), cost scale 0
+void check_best_mvp(double ml, const int16_t cand[2][2], int n_cand, int mx, int my, int& idx, uint32_t& bits,
+                    uint32_t& cost) {
+  if (n_cand < 2) return;
+  const int org_bits = (int)(eg_bits(mx - cand[idx][0]) + eg_bits(my - cand[idx][1]) + mvp_idx_bits(idx, 2));
+  int best_bits = org_bits, best_idx = idx;
+  for (int m = 0; m < n_cand; m++) {
+    if (m == idx) continue;
+    const int b = (int)(eg_bits(mx - cand[m][0]) + eg_bits(my - cand[m][1]) + mvp_idx_bits(m, 2));
+    if (b < best_bits) {
+      best_bits = b;
+      best_idx = m;
+    }
+  }
+  if (best_idx != idx) {
+    idx = best_idx;
+    const uint32_t org_total = bits;
+    bits = org_total - (uint32_t)org_bits + (uint32_t)best_bits;
+    cost = (cost - rd_cost(ml, org_total)) + rd_cost(ml, bits);
+  }
+}
+// xMotionEstimation's cost tail (TEncSearch.cpp:4594-4597) re-priced for bits_in + extra bits: the
+// searches do not read bits_in, so a job run with a provisional bits_in gives the exact result.
+uint32_t tail_cost(double ml, const fme_result& r, uint32_t bits_in, uint32_t extra, double fw) {
+  const uint32_t mvb = r.bits - bits_in;
+  const double v = floor(fw * ((double)r.frac_cost - (double)rd_cost(ml, mvb))) + (double)rd_cost(ml, r.bits + extra);
+  return (uint32_t)(int64_t)v;
+}
+
 bool valid_pu_shape(int w, int h) {
   for (int k = 0; k < kNumClasses; k++)
     if (kClassW[k] == w && kClassH[k] == h) return true;
   return false;
 }
 
+}  // namespace
+
+namespace {
+struct BPu {
+  uint32_t mb[3];
+  uint32_t cost[2], bits[2];
+  int16_t mv[2][2];
+  int ridx[2];
+  int mvpi[2][FME_MAX_REFS];
+  int16_t mvt[2][FME_MAX_REFS][2];
+  uint32_t cost_v1, bits_v1;
+  int16_t mv_v1[2];
+  int ridx_v1;
+  int L;            // list of the bi-pred search
+  uint32_t mot[2];  // uiMotBits
+  int bi0;          // first bi job of this request in the round's list
+  int stage;        // 0 waiting, 1 bi-pred search issued, 2 decided
+  int last_mode;    // uiLastMode after this request's decision
+};
+
+int two_part(int part_size) { return part_size != FME_PART_2Nx2N && part_size != FME_PART_NxN; }
+int num_parts(int part_size) { return part_size == FME_PART_2Nx2N ? 1 : (part_size == FME_PART_NxN ? 4 : 2); }
 }  // namespace
 
 extern "C" {
@@ -1335,8 +1402,8 @@ int fme_pred_inter_p(fme_ctx* c, const fme_pu_req* reqs, fme_pu_res* res, int n,
         fme_tz_ext e = ext[jx];
         if (e.flags & FME_TZ_PRED2NX2N) {
           const int sj = src[jx];
-          e.pred2n_x = sj >= 0 ? emi_mv[2 * sj] : c->int_mv_2n[k][0];
-          e.pred2n_y = sj >= 0 ? emi_mv[2 * sj + 1] : c->int_mv_2n[k][1];
+          e.pred2n_x = sj >= 0 ? emi_mv[2 * sj] : c->int_mv_2n[0][k][0];
+          e.pred2n_y = sj >= 0 ? emi_mv[2 * sj + 1] : c->int_mv_2n[0][k][1];
         }
         lj.push_back(jobs[jx]);
         le.push_back(e);
@@ -1407,10 +1474,446 @@ int fme_pred_inter_p(fme_ctx* c, const fme_pu_req* reqs, fme_pu_res* res, int n,
     }
     if (q.part_size == FME_PART_2Nx2N)
       for (int k = 0; k < q.num_refs; k++) {
-        c->int_mv_2n[k][0] = r[base[i] + k].mv_int_x;
-        c->int_mv_2n[k][1] = r[base[i] + k].mv_int_y;
+        c->int_mv_2n[0][k][0] = r[base[i] + k].mv_int_x;
+        c->int_mv_2n[0][k][1] = r[base[i] + k].mv_int_y;
       }
   }
+  return FME_OK;
+}
+
+
+// predInterSearch on a B slice (TEncSearch.cpp:3746-4105).  The GPU sees:
+//   1. one AMVP template-cost launch over every (request, list, reference) with two candidates;
+//   2. the uni-pred integer searches by m_integerMv2Nx2N dependency level (per list and reference);
+//   3. one fme_refine over the uni-pred jobs in call order.  Their bits_in leave out uiMbBits,
+//      which depends on the previous PU's decision (uiLastMode); the searches never read bits_in,
+//      so the host re-prices each tail exactly (tail_cost);
+//   4. rounds: every request whose uiLastMode is known gets its uni-pred outcome on the host, then
+//      its bi-pred key (k_bi_key), its bi-pred integer searches (xPatternSearch jobs) and one
+//      fme_refine over the uni jobs plus the round's bi jobs in call order: bi jobs read the carried
+//      NN state and write none, so the uni jobs repeat their results and each bi job sees the state
+//      of its position.  The round's decisions give the next requests their uiLastMode (two rounds
+//      at most: only the second PU of a two-PU CU waits).
+
+int fme_pred_inter_b(fme_ctx* c, const fme_pu_req_b* reqs, fme_pu_res_b* res, int n, void* stream) {
+  if (!c || (n > 0 && (!reqs || !res))) return fail(FME_E_INVALID, "fme_pred_inter_b: null argument");
+  if (n <= 0) return n == 0 ? FME_OK : fail(FME_E_INVALID, "fme_pred_inter_b: n = %d", n);
+  if (c->cfg.fast_inter_mode != 1 && c->cfg.fast_inter_mode != 2)
+    return fail(FME_E_UNSUPPORTED, "fme_pred_inter_b: FEN %d (only FEN 1/2: one bi-pred iteration)",
+                c->cfg.fast_inter_mode);
+  HIP_TRY(hipSetDevice(c->device));
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  // ---- validation (nothing runs on a bad batch) ----
+  for (int i = 0; i < n; i++) {
+    const fme_pu_req_b& q = reqs[i];
+    const PicDesc& org = c->pics[q.org_id < FME_MAX_PICTURES ? q.org_id : 0];
+    if (!valid_pu_shape(q.w, q.h) || q.part_size > FME_PART_nRx2N || q.part_idx >= num_parts(q.part_size) ||
+        q.org_id >= FME_MAX_PICTURES || !org.luma || q.x + q.w > org.width || q.y + q.h > org.height ||
+        q.lambda_id >= FME_MAX_LAMBDAS || !c->lambda_set[q.lambda_id] ||
+        (q.flags & ~(FME_PU_LOSSLESS | FME_PU_FAST_ME_GEN_B | FME_PU_CLIP_BIPRED)))
+      return fail(FME_E_INVALID, "fme_pred_inter_b: request %d invalid (shape %dx%d, part %d/%d)", i, q.w, q.h,
+                  q.part_size, q.part_idx);
+    if (two_part(q.part_size) && q.part_idx == 1 &&
+        (i == 0 || reqs[i - 1].part_idx != 0 || reqs[i - 1].part_size != q.part_size ||
+         reqs[i - 1].cu_x != q.cu_x || reqs[i - 1].cu_y != q.cu_y))
+      return fail(FME_E_INVALID, "fme_pred_inter_b: request %d (second PU) does not follow its CU's first PU", i);
+    for (int l = 0; l < 2; l++) {
+      if (q.num_refs[l] < 1 || q.num_refs[l] > FME_MAX_REFS)
+        return fail(FME_E_INVALID, "fme_pred_inter_b: request %d list %d: %d references", i, l, q.num_refs[l]);
+      for (int k = 0; k < q.num_refs[l]; k++) {
+        const int rid = q.ref_id[l][k];
+        if (rid >= FME_MAX_PICTURES || !c->pics[rid].luma || q.n_cand[l][k] < 1 || q.n_cand[l][k] > 2 ||
+            c->pics[rid].width != org.width || c->pics[rid].height != org.height ||
+            (l == 1 && (q.l1_to_l0[k] < -1 || q.l1_to_l0[k] >= q.num_refs[0])))
+          return fail(FME_E_INVALID, "fme_pred_inter_b: request %d list %d reference %d invalid", i, l, k);
+      }
+    }
+  }
+  int rc = sync_tables(c, s);
+  if (rc) return rc;
+  auto copied = [&](const fme_pu_req_b& q, int l, int k) {
+    return l == 1 && (q.flags & FME_PU_FAST_ME_GEN_B) && q.l1_to_l0[k] >= 0;
+  };
+  // ---- 1. xEstimateMvPredAMVP template costs over every (request, list, reference) ----
+  std::vector<int> amvp((size_t)n * 8, 0);   // chosen AMVP index of (i, l, k) = [i * 8 + l * 4 + k]
+  {
+    std::vector<AmvpTask> tasks;
+    std::vector<int> slot;
+    for (int i = 0; i < n; i++) {
+      const fme_pu_req_b& q = reqs[i];
+      for (int l = 0; l < 2; l++)
+        for (int k = 0; k < q.num_refs[l]; k++) {
+          if (q.n_cand[l][k] < 2) continue;
+          slot.push_back(i * 8 + l * 4 + k);
+          for (int m = 0; m < 2; m++)
+            tasks.push_back(AmvpTask{q.x, q.y, q.w, q.h, q.org_id, q.ref_id[l][k], q.cu_x, q.cu_y,
+                                     q.cand[l][k][m][0], q.cand[l][k][m][1]});
+        }
+    }
+    if (!tasks.empty()) {
+      std::vector<uint32_t> tsad(tasks.size());
+      HIP_TRY(c->d_amvp.reserve(tasks.size()));
+      HIP_TRY(c->d_amvp_sad.reserve(tasks.size()));
+      HIP_TRY(hipMemcpyAsync(c->d_amvp.p, tasks.data(), tasks.size() * sizeof(AmvpTask), hipMemcpyHostToDevice, s));
+      AmvpArgs aa{c->d_amvp.p, c->d_pics.p, c->d_amvp_sad.p, (int32_t)tasks.size()};
+      HIP_TRY(launch_amvp_sad(aa, s));
+      HIP_TRY(hipMemcpyAsync(tsad.data(), c->d_amvp_sad.p, tasks.size() * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+      HIP_TRY(hipStreamSynchronize(s));
+      for (size_t t = 0; t < slot.size(); t++) {
+        const double ml = c->mlambda[reqs[slot[t] / 8].lambda_id];
+        uint32_t best = 0xFFFFFFFFu;
+        for (int m = 0; m < 2; m++) {   // uiBestCost > uiTmpCost: the first least cost wins
+          const uint32_t cost = (uint32_t)((double)tsad[2 * t + m] + ((double)mvp_idx_bits(m, 2) * ml) / 65536.0);
+          if (best > cost) {
+            best = cost;
+            amvp[slot[t]] = m;
+          }
+        }
+      }
+    }
+  }
+  // ---- 2. uni-pred jobs in call order, integer searches by m_integerMv2Nx2N level ----
+  std::vector<int> ujob((size_t)n * 8, -1), ubeg(n + 1, 0);
+  std::vector<fme_job> uj;
+  std::vector<fme_tz_ext> ue;
+  std::vector<int> ukey;   // (list, reference) of each uni job
+  for (int i = 0; i < n; i++) {
+    const fme_pu_req_b& q = reqs[i];
+    const PicDesc& org = c->pics[q.org_id];
+    const int range = q.search_range ? q.search_range : 64;
+    ubeg[i] = (int)uj.size();
+    for (int l = 0; l < 2; l++)
+      for (int k = 0; k < q.num_refs[l]; k++) {
+        if (copied(q, l, k)) continue;
+        const int idx = amvp[i * 8 + l * 4 + k];
+        const int px = q.cand[l][k][idx][0], py = q.cand[l][k][idx][1];
+        int cx = px, cy = py;
+        clip_qpel(cx, cy, org.width, org.height, q.cu_x, q.cu_y);
+        int lx = cx - (range << 2), ly = cy - (range << 2), rx = cx + (range << 2), ry = cy + (range << 2);
+        clip_qpel(lx, ly, org.width, org.height, q.cu_x, q.cu_y);
+        clip_qpel(rx, ry, org.width, org.height, q.cu_x, q.cu_y);
+        fme_job j{};
+        j.x = q.x; j.y = q.y; j.w = q.w; j.h = q.h;
+        j.org_id = q.org_id; j.ref_id = q.ref_id[l][k];
+        j.mvp_x = (int16_t)px; j.mvp_y = (int16_t)py;
+        j.lt_x = (int16_t)round4(lx); j.lt_y = (int16_t)round4(ly);
+        j.rb_x = (int16_t)round4(rx); j.rb_y = (int16_t)round4(ry);
+        j.flags = (uint8_t)(FME_JOB_EMI | ((q.flags & FME_PU_LOSSLESS) ? FME_JOB_LOSSLESS : 0u));
+        j.lambda_id = q.lambda_id;
+        j.bits_in = (uint16_t)(ref_bits(k, q.num_refs[l]) + mvp_idx_bits(idx, 2));   // + uiMbBits[l] later
+        j.key_offset = -1;
+        fme_tz_ext e{};
+        e.cu_x = q.cu_x; e.cu_y = q.cu_y;
+        e.search_range = (uint8_t)range;
+        e.flags = (q.part_size == FME_PART_2Nx2N && q.depth == 0) ? 0 : FME_TZ_PRED2NX2N;
+        ujob[i * 8 + l * 4 + k] = (int)uj.size();
+        uj.push_back(j);
+        ue.push_back(e);
+        ukey.push_back(l * 4 + k);
+      }
+  }
+  ubeg[n] = (int)uj.size();
+  const int nu = (int)uj.size();
+  {
+    std::vector<int> level((size_t)n, 0), src((size_t)nu, -1);
+    int last[8] = {-1, -1, -1, -1, -1, -1, -1, -1};   // last 2Nx2N writer of m_integerMv2Nx2N[l][k]
+    int max_level = 0;
+    for (int i = 0; i < n; i++) {
+      for (int u = ubeg[i]; u < ubeg[i + 1]; u++)
+        if ((ue[u].flags & FME_TZ_PRED2NX2N) && last[ukey[u]] >= 0) {
+          level[i] = std::max(level[i], level[last[ukey[u]]] + 1);
+          src[u] = ujob[last[ukey[u]] * 8 + ukey[u]];
+        }
+      if (reqs[i].part_size == FME_PART_2Nx2N)
+        for (int u = ubeg[i]; u < ubeg[i + 1]; u++) last[ukey[u]] = i;
+      max_level = std::max(max_level, level[i]);
+    }
+    std::vector<std::vector<int>> by_level((size_t)max_level + 1);
+    for (int i = 0; i < n; i++) by_level[level[i]].push_back(i);
+    std::vector<int16_t> emi_mv((size_t)nu * 2, 0), lemi;
+    std::vector<fme_job> lj;
+    std::vector<fme_tz_ext> le;
+    std::vector<int> lidx;
+    for (int L = 0; L <= max_level; L++) {
+      lj.clear(); le.clear(); lidx.clear();
+      for (int i : by_level[L])
+        for (int u = ubeg[i]; u < ubeg[i + 1]; u++) {
+          fme_tz_ext e = ue[u];
+          if (e.flags & FME_TZ_PRED2NX2N) {
+            const int sj = src[u];
+            e.pred2n_x = sj >= 0 ? emi_mv[2 * sj] : c->int_mv_2n[ukey[u] >> 2][ukey[u] & 3][0];
+            e.pred2n_y = sj >= 0 ? emi_mv[2 * sj + 1] : c->int_mv_2n[ukey[u] >> 2][ukey[u] & 3][1];
+          }
+          lj.push_back(uj[u]);
+          le.push_back(e);
+          lidx.push_back(u);
+        }
+      if (lj.empty()) continue;
+      lemi.resize(2 * lj.size());
+      rc = tz_run_host(c, lj.data(), le.data(), nullptr, (int)lj.size(), stream, lemi.data());
+      if (rc) return rc;
+      for (size_t m = 0; m < lj.size(); m++) {
+        uj[lidx[m]] = lj[m];
+        emi_mv[2 * lidx[m]] = lemi[2 * m];
+        emi_mv[2 * lidx[m] + 1] = lemi[2 * m + 1];
+      }
+    }
+  }
+  // ---- 3. the uni-pred sub-pel path in call order ----
+  uint32_t s0[12];
+  rc = fme_nn_get_state(c, s0);
+  if (rc) return rc;
+  std::vector<fme_result> ru((size_t)nu);
+  rc = fme_refine(c, uj.data(), ru.data(), nu, stream);
+  if (rc) return rc;
+  // ---- 4. rounds of host decisions and bi-pred searches ----
+  std::vector<BPu> st((size_t)n);
+  for (int i = 0; i < n; i++) st[i].stage = 0;
+  auto uni_phase = [&](int i, int last_mode) {
+    const fme_pu_req_b& q = reqs[i];
+    BPu& p = st[i];
+    fme_pu_res_b& o = res[i];
+    o = fme_pu_res_b{};
+    const double ml = c->mlambda[q.lambda_id];
+    blk_bits_b(q.part_size, q.part_idx, last_mode, p.mb);
+    p.cost[0] = p.cost[1] = 0xFFFFFFFFu;
+    p.bits[0] = p.bits[1] = 0;
+    std::memset(p.mv, 0, sizeof(p.mv));
+    p.ridx[0] = p.ridx[1] = 0;
+    p.cost_v1 = 0xFFFFFFFFu;
+    p.bits_v1 = 0xFFFFFFFFu;
+    p.mv_v1[0] = p.mv_v1[1] = 0;
+    p.ridx_v1 = 0;
+    uint32_t cost_l0[FME_MAX_REFS] = {}, bits_l0[FME_MAX_REFS] = {};
+    for (int l = 0; l < 2; l++)
+      for (int k = 0; k < q.num_refs[l]; k++) {
+        int idx = amvp[i * 8 + l * 4 + k];
+        uint32_t b = p.mb[l] + ref_bits(k, q.num_refs[l]) + mvp_idx_bits(idx, 2), cst;
+        if (copied(q, l, k)) {   // TEncSearch.cpp:3814-3827
+          const int k0 = q.l1_to_l0[k];
+          p.mvt[1][k][0] = p.mvt[0][k0][0];
+          p.mvt[1][k][1] = p.mvt[0][k0][1];
+          cst = cost_l0[k0] - rd_cost(ml, bits_l0[k0]);
+          b += eg_bits(p.mvt[1][k][0] - q.cand[1][k][idx][0]) + eg_bits(p.mvt[1][k][1] - q.cand[1][k][idx][1]);
+          cst += rd_cost(ml, b);
+        } else {
+          const int u = ujob[i * 8 + l * 4 + k];
+          const fme_result& r = ru[u];
+          p.mvt[l][k][0] = r.mv_x;
+          p.mvt[l][k][1] = r.mv_y;
+          cst = tail_cost(ml, r, uj[u].bits_in, p.mb[l], 1.0);
+          b = r.bits + p.mb[l];
+        }
+        check_best_mvp(ml, q.cand[l][k], q.n_cand[l][k], p.mvt[l][k][0], p.mvt[l][k][1], idx, b, cst);
+        p.mvpi[l][k] = idx;
+        o.ref_cost[l][k] = cst;
+        o.ref_mv[l][k][0] = p.mvt[l][k][0];
+        o.ref_mv[l][k][1] = p.mvt[l][k][1];
+        o.ref_mvp_idx[l][k] = (uint8_t)idx;
+        if (l == 0) {
+          cost_l0[k] = cst;
+          bits_l0[k] = b;
+        }
+        if (cst < p.cost[l]) {
+          p.cost[l] = cst;
+          p.bits[l] = b;
+          p.mv[l][0] = p.mvt[l][k][0];
+          p.mv[l][1] = p.mvt[l][k][1];
+          p.ridx[l] = k;
+        }
+        if (l == 1 && cst < p.cost_v1 && q.l1_to_l0[k] < 0) {
+          p.cost_v1 = cst;
+          p.bits_v1 = b;
+          p.mv_v1[0] = p.mvt[1][k][0];
+          p.mv_v1[1] = p.mvt[1][k][1];
+          p.ridx_v1 = k;
+        }
+      }
+    o.bi_list = 0xFF;
+    o.bi_cost = 0xFFFFFFFFu;
+    o.uni_cost[0] = p.cost[0];
+    o.uni_bits[0] = p.bits[0];
+    o.uni_cost[1] = p.cost_v1;
+    o.uni_bits[1] = p.bits_v1;
+  };
+  // the decision (4041-4105); bi-pred outcome already in o.bi_* and mvbi/ridxbi/mvpibi
+  auto decide = [&](int i, const int16_t mvbi[2][2], const int ridxbi[2], const int mvpibi[2][FME_MAX_REFS]) {
+    const fme_pu_req_b& q = reqs[i];
+    BPu& p = st[i];
+    fme_pu_res_b& o = res[i];
+    if (o.bi_cost <= p.cost[0] && o.bi_cost <= p.cost_v1) {
+      p.last_mode = 2;
+      o.inter_dir = 3;
+      o.bits = o.bi_bits;
+      o.cost = o.bi_cost;
+      for (int l = 0; l < 2; l++) {
+        const int k = ridxbi[l], m = mvpibi[l][k];
+        o.ref_idx[l] = (uint8_t)k;
+        o.mvp_idx[l] = (uint8_t)m;
+        o.mv[l][0] = mvbi[l][0];
+        o.mv[l][1] = mvbi[l][1];
+        o.mvp[l][0] = q.cand[l][k][m][0];
+        o.mvp[l][1] = q.cand[l][k][m][1];
+      }
+    } else if (p.cost[0] <= p.cost_v1) {
+      const int k = p.ridx[0], m = p.mvpi[0][k];
+      p.last_mode = 0;
+      o.inter_dir = 1;
+      o.bits = p.bits[0];
+      o.cost = p.cost[0];
+      o.ref_idx[0] = (uint8_t)k;
+      o.mvp_idx[0] = (uint8_t)m;
+      o.mv[0][0] = p.mv[0][0];
+      o.mv[0][1] = p.mv[0][1];
+      o.mvp[0][0] = q.cand[0][k][m][0];
+      o.mvp[0][1] = q.cand[0][k][m][1];
+    } else {
+      const int k = p.ridx_v1, m = p.mvpi[1][k];
+      p.last_mode = 1;
+      o.inter_dir = 2;
+      o.bits = p.bits_v1;
+      o.cost = p.cost_v1;
+      o.ref_idx[1] = (uint8_t)k;
+      o.mvp_idx[1] = (uint8_t)m;
+      o.mv[1][0] = p.mv_v1[0];
+      o.mv[1][1] = p.mv_v1[1];
+      o.mvp[1][0] = q.cand[1][k][m][0];
+      o.mvp[1][1] = q.cand[1][k][m][1];
+    }
+    p.stage = 2;
+  };
+  std::vector<fme_job> bj, seq;
+  std::vector<fme_tz_ext> be;
+  std::vector<BiKeyTask> keyt;
+  std::vector<int> issued;
+  std::vector<fme_result> rs;
+  for (;;) {
+    bj.clear(); be.clear(); keyt.clear(); issued.clear();
+    size_t key_total = 0;
+    for (int i = 0; i < n; i++) {
+      const fme_pu_req_b& q = reqs[i];
+      BPu& p = st[i];
+      if (p.stage != 0) continue;
+      const bool dep = two_part(q.part_size) && q.part_idx == 1;
+      if (dep && st[i - 1].stage != 2) continue;   // uiLastMode not known yet
+      uni_phase(i, dep ? st[i - 1].last_mode : 0);
+      const bool restricted = q.cu_w == 8 && (q.w < 8 || q.h < 8);   // isBipredRestriction
+      if (restricted) {
+        const int16_t mvbi[2][2] = {{p.mv[0][0], p.mv[0][1]}, {p.mv[1][0], p.mv[1][1]}};
+        decide(i, mvbi, p.ridx, p.mvpi);
+        continue;
+      }
+      // bi-pred setup (3871-3916) and the other list's prediction -> key (3946-3952, 4461-4471)
+      p.mot[0] = p.bits[0] - p.mb[0];
+      p.mot[1] = p.bits[1] - p.mb[1];
+      const int L = p.cost[0] <= p.cost[1] ? 1 : 0;   // FASTINTERSEARCH_MODE1/2 (3931-3941)
+      p.L = L;
+      const int key_off = (int)key_total;
+      key_total += (size_t)q.w * q.h;
+      keyt.push_back(BiKeyTask{q.x, q.y, q.w, q.h, q.org_id, q.ref_id[1 - L][p.ridx[1 - L]], q.cu_x, q.cu_y,
+                               p.mv[1 - L][0], p.mv[1 - L][1], key_off,
+                               (q.flags & FME_PU_CLIP_BIPRED) ? 1u : 0u});
+      const PicDesc& org = c->pics[q.org_id];
+      const int brange = q.bipred_range ? q.bipred_range : 4;
+      p.bi0 = (int)bj.size();
+      for (int k = 0; k < q.num_refs[L]; k++) {
+        const int m = p.mvpi[L][k];
+        // xSetSearchRange around the reference's uni-pred MV (4486-4490)
+        int cx = p.mvt[L][k][0], cy = p.mvt[L][k][1];
+        clip_qpel(cx, cy, org.width, org.height, q.cu_x, q.cu_y);
+        int lx = cx - (brange << 2), ly = cy - (brange << 2), rx = cx + (brange << 2), ry = cy + (brange << 2);
+        clip_qpel(lx, ly, org.width, org.height, q.cu_x, q.cu_y);
+        clip_qpel(rx, ry, org.width, org.height, q.cu_x, q.cu_y);
+        fme_job j{};
+        j.x = q.x; j.y = q.y; j.w = q.w; j.h = q.h;
+        j.org_id = q.org_id; j.ref_id = q.ref_id[L][k];
+        j.mvp_x = q.cand[L][k][m][0]; j.mvp_y = q.cand[L][k][m][1];
+        j.lt_x = (int16_t)round4(lx); j.lt_y = (int16_t)round4(ly);
+        j.rb_x = (int16_t)round4(rx); j.rb_y = (int16_t)round4(ry);
+        j.flags = (uint8_t)(FME_JOB_BIPRED | ((q.flags & FME_PU_LOSSLESS) ? FME_JOB_LOSSLESS : 0u));
+        j.lambda_id = q.lambda_id;
+        j.bits_in = (uint16_t)(p.mb[2] + p.mot[1 - L] + ref_bits(k, q.num_refs[L]) + mvp_idx_bits(m, 2));
+        j.key_offset = key_off;
+        fme_tz_ext e{};
+        e.cu_x = q.cu_x; e.cu_y = q.cu_y;
+        e.search_range = (uint8_t)brange;
+        bj.push_back(j);
+        be.push_back(e);
+      }
+      p.stage = 1;
+      issued.push_back(i);
+    }
+    if (issued.empty()) break;
+    // keys, bi-pred integer searches, then the sub-pel path over uni + bi jobs in call order
+    HIP_TRY(c->d_keys.reserve(key_total));
+    c->n_keys = key_total;
+    HIP_TRY(c->d_bikey.reserve(keyt.size()));
+    HIP_TRY(hipMemcpyAsync(c->d_bikey.p, keyt.data(), keyt.size() * sizeof(BiKeyTask), hipMemcpyHostToDevice, s));
+    BiKeyArgs ka{c->d_bikey.p, c->d_pics.p, c->d_keys.p, (int32_t)keyt.size()};
+    HIP_TRY(launch_bi_key(ka, s));
+    rc = tz_run_host(c, bj.data(), be.data(), nullptr, (int)bj.size(), stream, nullptr);
+    if (rc) return rc;
+    seq.clear();
+    std::vector<int> pos(issued.size());
+    size_t t = 0;
+    for (int i = 0; i < n; i++) {
+      seq.insert(seq.end(), uj.begin() + ubeg[i], uj.begin() + ubeg[i + 1]);
+      if (t < issued.size() && issued[t] == i) {
+        pos[t] = (int)seq.size();
+        const int nb = reqs[i].num_refs[st[i].L];
+        seq.insert(seq.end(), bj.begin() + st[i].bi0, bj.begin() + st[i].bi0 + nb);
+        t++;
+      }
+    }
+    rc = fme_nn_set_state(c, s0);
+    if (!rc) {
+      rs.resize(seq.size());
+      rc = fme_refine(c, seq.data(), rs.data(), (int)seq.size(), stream);
+    }
+    if (rc) return rc;
+    for (size_t t2 = 0; t2 < issued.size(); t2++) {
+      const int i = issued[t2];
+      const fme_pu_req_b& q = reqs[i];
+      BPu& p = st[i];
+      fme_pu_res_b& o = res[i];
+      const double ml = c->mlambda[q.lambda_id];
+      const int L = p.L;
+      int16_t mvbi[2][2] = {{p.mv[0][0], p.mv[0][1]}, {p.mv[1][0], p.mv[1][1]}};
+      int ridxbi[2] = {p.ridx[0], p.ridx[1]};
+      int mvpibi[2][FME_MAX_REFS];
+      std::memcpy(mvpibi, p.mvpi, sizeof(mvpibi));
+      uint32_t cost_bi = 0xFFFFFFFFu, bits_bi = p.mb[2] + p.mot[0] + p.mot[1];
+      for (int k = 0; k < q.num_refs[L]; k++) {
+        const fme_result& r = rs[pos[t2] + k];
+        uint32_t b = r.bits, cst = r.cost;
+        int idx = mvpibi[L][k];
+        check_best_mvp(ml, q.cand[L][k], q.n_cand[L][k], r.mv_x, r.mv_y, idx, b, cst);
+        mvpibi[L][k] = idx;
+        o.bi_ref_cost[k] = cst;
+        o.bi_ref_mv[k][0] = r.mv_x;
+        o.bi_ref_mv[k][1] = r.mv_y;
+        if (cst < cost_bi) {   // 3985-3995
+          mvbi[L][0] = r.mv_x;
+          mvbi[L][1] = r.mv_y;
+          ridxbi[L] = k;
+          cost_bi = cst;
+          p.mot[L] = b - p.mb[2] - p.mot[1 - L];
+          bits_bi = b;
+        }
+      }
+      o.bi_list = (uint8_t)L;
+      o.bi_cost = cost_bi;
+      o.bi_bits = bits_bi;
+      decide(i, mvbi, ridxbi, mvpibi);
+    }
+  }
+  // ---- m_integerMv2Nx2N: the last 2Nx2N request's post-EMI integer MV per (list, reference) ----
+  for (int i = 0; i < n; i++)
+    if (reqs[i].part_size == FME_PART_2Nx2N)
+      for (int u = ubeg[i]; u < ubeg[i + 1]; u++) {
+        c->int_mv_2n[ukey[u] >> 2][ukey[u] & 3][0] = ru[u].mv_int_x;
+        c->int_mv_2n[ukey[u] >> 2][ukey[u] & 3][1] = ru[u].mv_int_y;
+      }
   return FME_OK;
 }
 

@@ -57,6 +57,26 @@ struct AmvpArgs {
 };
 hipError_t launch_amvp_sad(const AmvpArgs& a, hipStream_t s);
 
+// xMotionEstimation(bBi)'s search key (fme_mc.hip): the other list's uni-pred luma prediction at
+// its MV (clipMv'd against the CU origin), key = 2 * org - pred (TComYuv::removeHighFreq), clipped
+// to 8 bits with ClipForBiPredMe; w*h int16 at keys + key_off.  One task per wave.
+struct BiKeyTask {
+  uint16_t x, y;
+  uint8_t w, h, org_id, ref_id;
+  uint16_t cu_x, cu_y;
+  int16_t mv_x, mv_y;
+  int32_t key_off;
+  uint32_t clip;
+};
+static_assert(sizeof(BiKeyTask) == 24, "BiKeyTask layout");
+struct BiKeyArgs {
+  const BiKeyTask* tasks;
+  const PicDesc* pics;
+  int16_t* keys;
+  int32_t n;
+};
+hipError_t launch_bi_key(const BiKeyArgs& a, hipStream_t s);
+
 
 // One batch as the device sees it.
 struct BatchArgs {

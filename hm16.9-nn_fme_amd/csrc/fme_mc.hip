@@ -354,7 +354,52 @@ __global__ __launch_bounds__(kMcBlock) void k_amvp_sad(AmvpArgs a) {
   if (lane == 0) a.sad[task] = sad;
 }
 
+// xMotionEstimation(bBi) (TEncSearch.cpp:4461-4471): motionCompensation of the other list (luma,
+// uni-pred, 8-bit) and TComYuv::removeHighFreq (TComYuv.cpp:411-455) into the key buffer.  One
+// task per wave: the lanes walk the PU's 4x4 units.
+__global__ __launch_bounds__(kMcBlock) void k_bi_key(BiKeyArgs a) {
+  const int task = (int)(blockIdx.x * (kMcBlock / 64) + (threadIdx.x >> 6));
+  if (task >= a.n) return;   // wave-uniform
+  const int lane = (int)(threadIdx.x & 63);
+  const BiKeyTask t = a.tasks[task];
+  const PicDesc ref = a.pics[t.ref_id], org = a.pics[t.org_id];
+  int mx = t.mv_x, my = t.mv_y;
+  clip_mv(mx, my, ref.width, ref.height, t.cu_x, t.cu_y);
+  uint32_t hlo, hhi, vlo, vhi;
+  luma_taps(mx & 3, hlo, hhi);
+  luma_taps(my & 3, vlo, vhi);
+  const bool al = ((ref.stride | (int)(uintptr_t)ref.luma) & 3) == 0;
+  const int uxn = t.w >> 2, units = uxn * (t.h >> 2);
+  for (int u = lane; u < units; u += 64) {
+    const int ux = u % uxn, uy = u / uxn;
+    const int x = t.x + 4 * ux, y = t.y + 4 * uy;
+    UnitWin<8, 4> w;
+    w.load(Plane{ref.luma, ref.stride, ref.width, ref.height}, al, x + (mx >> 2), y + (my >> 2));
+    int o[4][4];
+    w.pred(hlo, hhi, vlo, vhi, true, o);
+#pragma unroll
+    for (int r = 0; r < 4; r++) {
+      const uint8_t* op = org.luma + (size_t)(y + r) * org.stride + x;
+      int16_t* kp = a.keys + t.key_off + (size_t)(4 * uy + r) * t.w + 4 * ux;
+      int v[4];
+#pragma unroll
+      for (int c = 0; c < 4; c++) {
+        v[c] = 2 * (int)gld8(op + c) - o[r][c];
+        if (t.clip) v[c] = clamp_i(v[c], 0, 255);
+      }
+      // 4 int16 = 8 bytes; key_off and w are multiples of 4, so the store is 8-byte aligned
+      *(uint2*)kp = make_uint2((uint32_t)(uint16_t)v[0] | ((uint32_t)(uint16_t)v[1] << 16),
+                               (uint32_t)(uint16_t)v[2] | ((uint32_t)(uint16_t)v[3] << 16));
+    }
+  }
+}
+
 }  // namespace
+
+hipError_t launch_bi_key(const BiKeyArgs& a, hipStream_t s) {
+  if (a.n > 0) hipLaunchKernelGGL(k_bi_key, dim3((a.n + kMcBlock / 64 - 1) / (kMcBlock / 64)), dim3(kMcBlock), 0, s, a);
+  return hipGetLastError();
+}
 
 hipError_t launch_mc(const McArgs& a, hipStream_t s) {
   if (a.n > 0) hipLaunchKernelGGL(k_mc, dim3((a.n + kMcJobs - 1) / kMcJobs), dim3(kMcBlock), 0, s, a);

@@ -97,6 +97,38 @@ PU_RES_DTYPE = np.dtype(
 )
 assert PU_RES_DTYPE.itemsize == 80
 PU_LOSSLESS = 0x01
+PU_FAST_ME_GEN_B = 0x02
+PU_CLIP_BIPRED = 0x04
+# fme_pu_req_b / fme_pu_res_b (include/fme.h): predInterSearch on a B slice
+PU_REQ_B_DTYPE = np.dtype(
+    [
+        ("x", "<u2"), ("y", "<u2"), ("w", "u1"), ("h", "u1"),
+        ("cu_x", "<u2"), ("cu_y", "<u2"),
+        ("part_size", "u1"), ("depth", "u1"), ("org_id", "u1"), ("part_idx", "u1"),
+        ("cu_w", "u1"), ("lambda_id", "u1"), ("search_range", "u1"), ("bipred_range", "u1"),
+        ("flags", "u1"), ("num_refs", "u1", (2,)),
+        ("ref_id", "u1", (2, MAX_REFS)), ("n_cand", "u1", (2, MAX_REFS)),
+        ("l1_to_l0", "i1", (MAX_REFS,)), ("reserved", "u1", (7,)),
+        ("cand", "<i2", (2, MAX_REFS, 2, 2)),
+    ],
+    align=False,
+)
+assert PU_REQ_B_DTYPE.itemsize == 112
+PU_RES_B_DTYPE = np.dtype(
+    [
+        ("inter_dir", "u1"), ("ref_idx", "u1", (2,)), ("mvp_idx", "u1", (2,)), ("bi_list", "u1"),
+        ("reserved", "<u2"),
+        ("mv", "<i2", (2, 2)), ("mvp", "<i2", (2, 2)),
+        ("bits", "<u4"), ("cost", "<u4"),
+        ("uni_cost", "<u4", (2,)), ("uni_bits", "<u4", (2,)),
+        ("bi_cost", "<u4"), ("bi_bits", "<u4"),
+        ("ref_cost", "<u4", (2, MAX_REFS)), ("ref_mv", "<i2", (2, MAX_REFS, 2)),
+        ("bi_ref_cost", "<u4", (MAX_REFS,)), ("bi_ref_mv", "<i2", (MAX_REFS, 2)),
+        ("ref_mvp_idx", "u1", (2, MAX_REFS)),
+    ],
+    align=False,
+)
+assert PU_RES_B_DTYPE.itemsize == 160
 PART_2Nx2N, PART_2NxN, PART_Nx2N, PART_NxN, PART_2NxnU, PART_2NxnD, PART_nLx2N, PART_nRx2N = range(8)
 
 MC_L0 = 0x01

@@ -15,7 +15,7 @@ from .weights import load_weights
 PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB_PATH = os.environ.get("FME_LIB_PATH") or os.path.join(PKG_ROOT, "libfme_amd.so")
 
-ABI_VERSION = 5
+ABI_VERSION = 6
 TIMING_NAMES = ("classify", "scatter", "search", "nn_tail", "batch", "search_main", "search_aux")
 
 # Every entry point include/fme.h declares (the ABI test checks the .so exports them).
@@ -30,7 +30,7 @@ ABI_SYMBOLS = (
     "fme_integer_search", "fme_integer_search_device", "fme_integer_search_last_ms",
     "fme_pred_inter_p", "fme_pred_inter_reset", "fme_nn_param_count", "fme_load_nn_net",
     "fme_set_nn_engine", "fme_set_nn_margin_output", "fme_refine_mv", "fme_refine_mv_device",
-    "fme_refine_status", "fme_nn_copy_state_device", "fme_template_costs",
+    "fme_refine_status", "fme_nn_copy_state_device", "fme_template_costs", "fme_pred_inter_b",
 )
 
 
@@ -100,6 +100,7 @@ def load_library(path=None):
         "fme_refine_status": (I, [P]),
         "fme_nn_copy_state_device": (I, [P, P, P]),
         "fme_template_costs": (I, [P, P, P, I, P]),
+        "fme_pred_inter_b": (I, [P, P, P, I, P]),
     }
     for name, (res, args) in sig.items():
         f = getattr(lib, name)
@@ -200,6 +201,15 @@ class FmeContext:
         res = np.zeros(len(reqs), dtype=PU_RES_DTYPE)
         if len(reqs):
             _check(self.lib, self.lib.fme_pred_inter_p(self.h, _ptr(reqs), _ptr(res), len(reqs), stream))
+        return res
+
+    def pred_inter_b(self, reqs, stream=None):
+        """fme_pred_inter_b: predInterSearch on a B slice, one fme_pu_res_b per fme_pu_req_b."""
+        from .abi import PU_REQ_B_DTYPE, PU_RES_B_DTYPE
+        reqs = np.ascontiguousarray(reqs, dtype=PU_REQ_B_DTYPE)
+        res = np.zeros(len(reqs), dtype=PU_RES_B_DTYPE)
+        if len(reqs):
+            _check(self.lib, self.lib.fme_pred_inter_b(self.h, _ptr(reqs), _ptr(res), len(reqs), stream))
         return res
 
     def template_costs(self, reqs, stream=None):

@@ -507,6 +507,61 @@ def make_pu_requests(rng, width, height, org_id, ref_ids, lambda_id, max_depth=3
     return reqs
 
 
+def make_pu_requests_b(rng, width, height, org_id, l0, l1, lambda_id, max_depth=3, amp=12.0, cand_noise=24,
+                       one_cand_frac=0.1, lossless_frac=0.0, search_range=SEARCH_RANGE, bipred_range=4,
+                       fast_me_gen_b=True, clip_bipred=False):
+    """fme_pu_req_b stream of a B frame in encoder call order (as make_pu_requests).  l0 / l1: lists
+    of (picture slot, signed POC distance) per reference index; an L1 slot that is also in L0 gets
+    l1_to_l0 = its L0 index (getList1IdxToList0Idx).  Candidates of a reference lie near the
+    motion field scaled by its POC distance."""
+    from .abi import MAX_REFS, PU_CLIP_BIPRED, PU_FAST_ME_GEN_B, PU_LOSSLESS, PU_REQ_B_DTYPE
+    p = make_pu_requests(rng, width, height, org_id, [0], lambda_id, max_depth=max_depth, amp=amp,
+                         search_range=search_range)
+    n = len(p)
+    ctus_x = (width + MAX_CU - 1) // MAX_CU
+    vx, vy = motion_field(rng, ctus_x, (height + MAX_CU - 1) // MAX_CU, amp)
+    reqs = np.zeros(n, dtype=PU_REQ_B_DTYPE)
+    for f in ("x", "y", "w", "h", "cu_x", "cu_y", "part_size", "depth", "org_id", "lambda_id", "search_range"):
+        reqs[f] = p[f]
+    # part index within the CU and the CU width (the stream lists a CU's PUs consecutively)
+    key = np.stack([p["cu_x"], p["cu_y"], p["depth"], p["part_size"]], 1).astype(np.int64)
+    same = np.r_[False, (key[1:] == key[:-1]).all(1)]
+    idx = np.zeros(n, np.int64)
+    for i in range(1, n):
+        idx[i] = idx[i - 1] + 1 if same[i] else 0
+    reqs["part_idx"] = idx
+    reqs["cu_w"] = MAX_CU >> p["depth"].astype(np.int64)
+    reqs["bipred_range"] = bipred_range
+    flags = np.where(rng.random(n) < lossless_frac, PU_LOSSLESS, 0)
+    if fast_me_gen_b:
+        flags |= PU_FAST_ME_GEN_B
+    if clip_bipred:
+        flags |= PU_CLIP_BIPRED
+    reqs["flags"] = flags
+    reqs["num_refs"] = [len(l0), len(l1)]
+    reqs["l1_to_l0"] = -1
+    slots0 = [s for s, _ in l0]
+    for k, (s, _) in enumerate(l1):
+        if s in slots0:
+            reqs["l1_to_l0"][:, k] = slots0.index(s)
+    ctu = (p["cu_y"].astype(np.int64) // MAX_CU) * ctus_x + p["cu_x"].astype(np.int64) // MAX_CU
+    for l, lst in enumerate((l0, l1)):
+        assert len(lst) <= MAX_REFS
+        for k, (slot, d) in enumerate(lst):
+            reqs["ref_id"][:, l, k] = slot
+            bx = 4 * np.rint(vx.reshape(-1)[ctu] * d).astype(np.int64)
+            by = 4 * np.rint(vy.reshape(-1)[ctu] * d).astype(np.int64)
+            c0x = bx + rng.integers(-cand_noise, cand_noise + 1, n)
+            c0y = by + rng.integers(-cand_noise, cand_noise + 1, n)
+            kind = rng.integers(0, 4, n)
+            c1x = np.where(kind < 2, bx + rng.integers(-cand_noise, cand_noise + 1, n), np.where(kind == 2, c0x, 0))
+            c1y = np.where(kind < 2, by + rng.integers(-cand_noise, cand_noise + 1, n), np.where(kind == 2, c0y, 0))
+            reqs["cand"][:, l, k, 0, 0], reqs["cand"][:, l, k, 0, 1] = c0x, c0y
+            reqs["cand"][:, l, k, 1, 0], reqs["cand"][:, l, k, 1, 1] = c1x, c1y
+            reqs["n_cand"][:, l, k] = np.where(rng.random(n) < one_cand_frac, 1, 2)
+    return reqs
+
+
 def pu_requests_to_jobs(reqs, width, height):
     """The xMotionEstimation jobs of single-reference, single-candidate requests whose
     m_integerMv2Nx2N reads see the initial (0, 0): mvp = cand[0][0], xSetSearchRange(mvp, range)

@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define FME_ABI_VERSION 5
+#define FME_ABI_VERSION 6
 
 /* ---- error codes ---------------------------------------------------------------- */
 #define FME_OK            0
@@ -368,6 +368,75 @@ int fme_pred_inter_reset(fme_ctx* ctx);
  * costs[(i * FME_MAX_REFS + k) * 2 + m] (0xFFFFFFFF where there is no candidate).  Host arrays,
  * synchronous. */
 int fme_template_costs(fme_ctx* ctx, const fme_pu_req* reqs, uint32_t* costs, int n, void* stream);
+
+/* ---- predInterSearch for B slices ------------------------------------ *
+ * TEncSearch::predInterSearch on a B slice (TEncSearch.cpp:3746-4105) with the switches of the
+ * shipped random-access configuration: FEN = 1 (FASTINTERSEARCH_MODE1: one bi-pred iteration,
+ * over the list opposite the cheaper uni-pred list, 3918-3941) and MvdL1ZeroFlag = false
+ * (TEncGOP.cpp:1392-1418 sets it only when both lists hold the same pictures: lowdelay B, not
+ * supported here); FastMEForGenBLowDelayEnabled and ClipForBiPredMeEnabled per request flag.
+ * Per request, in the encoder's call order:
+ *   uiMbBits = xGetBlkBits(part_size, B slice, part_idx, uiLastMode) (4286-4333), uiLastMode being
+ *             the decision of the request before (part_idx 1 continues that request's CU);
+ *   uni-pred (3786-3865): list 0, then list 1, each reference as fme_pred_inter_p runs it
+ *             (m_integerMv2Nx2N per list); with FME_PU_FAST_ME_GEN_B an L1 reference that is also
+ *             L0 reference l1_to_l0[k] takes L0's MV, its cost re-priced with L1's predictor;
+ *   bi-pred (3868-4022) unless isBipredRestriction (TComDataCU.cpp:2758-2770: 8x8 CU, PU side
+ *             < 8): the other list's uni-pred luma prediction at its best MV (motionCompensation),
+ *             key = 2 * org - pred (removeHighFreq, TComYuv.cpp:411-455), and per reference of the
+ *             searched list xMotionEstimation(bBi) (4461-4534): xSetSearchRange around the
+ *             reference's uni MV with bipred_range, xPatternSearch (every integer position),
+ *             FracDIF on the key, NN_pred on the carried state (no EMI step), fWeight 0.5;
+ *             xCheckBestMVP; strict minimum;
+ *   decision (4041-4105): bi when uiCostBi <= uiCost[0] and <= the best L1 cost over references
+ *             not in L0 (costValidList1); else L0 when uiCost[0] <= costValidList1; else L1.
+ * Merge and the AMP merge-only test (bTestNormalMC false) stay with the caller.                 */
+#define FME_PU_FAST_ME_GEN_B 0x02u   /* FastMEForGenBLowDelayEnabled (cfg default true)          */
+#define FME_PU_CLIP_BIPRED   0x04u   /* ClipForBiPredMeEnabled: key clipped to 8 bits            */
+
+typedef struct fme_pu_req_b {
+  uint16_t x, y;              /* PU luma rectangle                                              */
+  uint8_t  w, h;
+  uint16_t cu_x, cu_y;        /* luma origin of the CU                                          */
+  uint8_t  part_size;         /* FME_PART_*                                                     */
+  uint8_t  depth;             /* CU depth                                                       */
+  uint8_t  org_id;            /* original picture slot                                          */
+  uint8_t  part_idx;          /* iPartIdx within the CU                                         */
+  uint8_t  cu_w;              /* CU width (getWidth(0), isBipredRestriction)                    */
+  uint8_t  lambda_id;
+  uint8_t  search_range;      /* m_aaiAdaptSR (0 -> 64)                                         */
+  uint8_t  bipred_range;      /* m_bipredSearchRange (0 -> 4)                                   */
+  uint8_t  flags;             /* FME_PU_*                                                       */
+  uint8_t  num_refs[2];       /* getNumRefIdx(list), 1..FME_MAX_REFS                            */
+  uint8_t  ref_id[2][FME_MAX_REFS];     /* picture slot of (list, reference index)              */
+  uint8_t  n_cand[2][FME_MAX_REFS];     /* AMVPInfo::iN (1 or 2)                                */
+  int8_t   l1_to_l0[FME_MAX_REFS];      /* TComSlice::getList1IdxToList0Idx, -1: not in L0      */
+  uint8_t  reserved[7];
+  int16_t  cand[2][FME_MAX_REFS][2][2]; /* AMVP candidates, quarter-pel (hor, ver)              */
+} fme_pu_req_b;   /* 112 bytes */
+
+typedef struct fme_pu_res_b {
+  uint8_t  inter_dir;         /* 1: L0, 2: L1, 3: bi (setInterDirSubParts)                      */
+  uint8_t  ref_idx[2];        /* decided reference index per list (0 for an unused list)        */
+  uint8_t  mvp_idx[2];        /* its AMVP index                                                 */
+  uint8_t  bi_list;           /* list searched by the bi-pred iteration; 0xFF: none             */
+  uint16_t reserved;
+  int16_t  mv[2][2];          /* decided MVs, quarter-pel (0 for an unused list)                */
+  int16_t  mvp[2][2];         /* their predictors                                               */
+  uint32_t bits, cost;        /* uiMEBits and the decided cost                                  */
+  uint32_t uni_cost[2];       /* uiCost[0], costValidList1                                      */
+  uint32_t uni_bits[2];       /* uiBits[0], bitsValidList1                                      */
+  uint32_t bi_cost, bi_bits;  /* uiCostBi, uiBits[2] (0xFFFFFFFF / 0: no bi-pred search)        */
+  uint32_t ref_cost[2][FME_MAX_REFS];   /* uni uiCostTemp per (list, reference)                 */
+  int16_t  ref_mv[2][FME_MAX_REFS][2];  /* uni cMvTemp per (list, reference)                    */
+  uint32_t bi_ref_cost[FME_MAX_REFS];   /* bi uiCostTemp per reference of bi_list               */
+  int16_t  bi_ref_mv[FME_MAX_REFS][2];  /* bi cMvTemp per reference of bi_list                  */
+  uint8_t  ref_mvp_idx[2][FME_MAX_REFS];/* uni aaiMvpIdx after xCheckBestMVP                    */
+} fme_pu_res_b;   /* 160 bytes */
+
+/* Host arrays, synchronous on `stream`; a batch with an invalid request is rejected before any
+ * work runs.  m_integerMv2Nx2N (both lists) is the state fme_pred_inter_reset forgets. */
+int fme_pred_inter_b(fme_ctx* ctx, const fme_pu_req_b* reqs, fme_pu_res_b* res, int n, void* stream);
 
 /* ---- single-PU entry points with the TEncSearch argument lists ---------------------------- *
  * xPatternSearchFracDIF(bIsLosslessCoded, pcPatternKey, piRefY, iRefStride, pcMvInt,

@@ -1025,26 +1025,129 @@ static uint32_t pi_blk_bits(int part_size) {
 /* xGetTemplateCost (TEncSearch.cpp:4397-4436): clipMv, xPredInterBlk(COMPONENT_Y, bi = false),
  * getDistPart(DF_SAD) (plain SAD, TComRdCost.cpp:187-197, 327-349), calcRdCost(bits, SAD, DF_SAD)
  * (TComRdCost.cpp:57-102, COST_STANDARD_LOSSY: SAD + bits * lambdaMotionSAD / 65536). */
-static uint32_t pi_template_cost(const orc_ctx* ctx, const fme_pu_req* q, int k, int m, int16_t* pred) {
-  const orc_picture* ref = &ctx->pics[q->ref_id[k]];
-  const orc_picture* org = &ctx->pics[q->org_id];
-  int mx = q->cand[k][m][0], my = q->cand[k][m][1];
-  mc_clip_mv(&mx, &my, ref->width, ref->height, q->cu_x, q->cu_y);
-  mc_pred_blk(ref->luma, ref->stride, ref->width, ref->height, 0, q->x, q->y, q->w, q->h, mx, my, 0, pred, q->w);
+typedef struct pi_pu {   /* the geometry and slots every xMotionEstimation of one PU shares */
+  int x, y, w, h, cu_x, cu_y, org_id, lambda_id, lossless;
+} pi_pu;
+
+/* motionCompensation's luma part for one list (xPredInterUni, bi = false): 8-bit prediction. */
+static void pi_pred_uni(const orc_ctx* ctx, const pi_pu* g, int ref_id, int mx, int my, int16_t* pred) {
+  const orc_picture* ref = &ctx->pics[ref_id];
+  mc_clip_mv(&mx, &my, ref->width, ref->height, g->cu_x, g->cu_y);
+  mc_pred_blk(ref->luma, ref->stride, ref->width, ref->height, 0, g->x, g->y, g->w, g->h, mx, my, 0, pred, g->w);
+}
+
+static uint32_t pi_tmpl(const orc_ctx* ctx, const pi_pu* g, int ref_id, int mx, int my, int m, int16_t* pred) {
+  const orc_picture* org = &ctx->pics[g->org_id];
+  pi_pred_uni(ctx, g, ref_id, mx, my, pred);
   uint32_t sad = 0;
-  for (int y = 0; y < q->h; y++)
-    for (int x = 0; x < q->w; x++) {
-      const int d = pred[y * q->w + x] - org->luma[(size_t)(q->y + y) * org->stride + q->x + x];
+  for (int y = 0; y < g->h; y++)
+    for (int x = 0; x < g->w; x++) {
+      const int d = pred[y * g->w + x] - org->luma[(size_t)(g->y + y) * org->stride + g->x + x];
       sad += (uint32_t)(d < 0 ? -d : d);
     }
-  const double ml = ctx->mlambda[q->lambda_id];
+  const double ml = ctx->mlambda[g->lambda_id];
   return (uint32_t)((double)sad + ((double)pi_mvp_idx_bits(m, 2) * ml) / 65536.0);
+}
+
+static pi_pu pi_pu_of(const fme_pu_req* q) {
+  pi_pu g = {q->x, q->y, q->w, q->h, q->cu_x, q->cu_y, q->org_id, q->lambda_id, (q->flags & FME_PU_LOSSLESS) != 0};
+  return g;
 }
 
 /* xGetTemplateCost of AMVP candidate m of reference k of one request (exported for the tests). */
 uint32_t orc_template_cost(const orc_ctx* ctx, const fme_pu_req* q, int k, int m) {
   int16_t pred[64 * 64];
-  return pi_template_cost(ctx, q, k, m, pred);
+  const pi_pu g = pi_pu_of(q);
+  return pi_tmpl(ctx, &g, q->ref_id[k], q->cand[k][m][0], q->cand[k][m][1], m, pred);
+}
+
+/* xEstimateMvPredAMVP (4186-4256): with two candidates the first with the least template cost. */
+static int pi_amvp(const orc_ctx* ctx, const pi_pu* g, int ref_id, int n_cand, const int16_t cand[2][2],
+                   int16_t* pred) {
+  int idx = 0;
+  if (n_cand > 1) {
+    uint32_t best = 0xFFFFFFFFu;
+    for (int m = 0; m < n_cand; m++) {
+      const uint32_t c = pi_tmpl(ctx, g, ref_id, cand[m][0], cand[m][1], m, pred);
+      if (best > c) {
+        best = c;
+        idx = m;
+      }
+    }
+  }
+  return idx;
+}
+
+/* The reference-index bits of uiBitsTemp (3792-3800). */
+static uint32_t pi_ref_bits(int k, int num_refs) {
+  if (num_refs <= 1) return 0;
+  return (uint32_t)k + 1u - (k == num_refs - 1 ? 1u : 0u);
+}
+
+/* xMotionEstimation (4439-4599) on one (PU, reference): xSetSearchRange around the predictor (uni)
+ * or around the start MV bc (bi), the integer search (xTZSearch with the EMI step and the
+ * m_integerMv2Nx2N start pred2n, or xPatternSearch on the bi key), FracDIF, NN_pred, the tail. */
+static int pi_me(orc_ctx* ctx, const pi_pu* g, int ref_id, int mvp_x, int mvp_y, uint32_t bits, int range,
+                 const int16_t* pred2n, const int16_t* bikey, int bc_x, int bc_y, fme_result* r) {
+  const orc_picture* org = &ctx->pics[g->org_id];
+  fme_job j;
+  memset(&j, 0, sizeof(j));
+  j.x = (uint16_t)g->x; j.y = (uint16_t)g->y; j.w = (uint8_t)g->w; j.h = (uint8_t)g->h;
+  j.org_id = (uint8_t)g->org_id; j.ref_id = (uint8_t)ref_id;
+  j.mvp_x = (int16_t)mvp_x; j.mvp_y = (int16_t)mvp_y;
+  int cx = bikey ? bc_x : mvp_x, cy = bikey ? bc_y : mvp_y;
+  tz_clip(&cx, &cy, org->width, org->height, g->cu_x, g->cu_y);
+  int lx = cx - (range << 2), ly = cy - (range << 2), rx = cx + (range << 2), ry = cy + (range << 2);
+  tz_clip(&lx, &ly, org->width, org->height, g->cu_x, g->cu_y);
+  tz_clip(&rx, &ry, org->width, org->height, g->cu_x, g->cu_y);
+  j.lt_x = (int16_t)mv_round4(lx); j.lt_y = (int16_t)mv_round4(ly);
+  j.rb_x = (int16_t)mv_round4(rx); j.rb_y = (int16_t)mv_round4(ry);
+  j.flags = (uint8_t)((bikey ? FME_JOB_BIPRED : FME_JOB_EMI) | (g->lossless ? FME_JOB_LOSSLESS : 0u));
+  j.lambda_id = (uint8_t)g->lambda_id;
+  j.bits_in = (uint16_t)bits;
+  j.key_offset = bikey ? 0 : -1;
+  fme_tz_ext e;
+  memset(&e, 0, sizeof(e));
+  e.cu_x = (uint16_t)g->cu_x; e.cu_y = (uint16_t)g->cu_y;
+  e.search_range = (uint8_t)range;
+  if (pred2n) {   /* pIntegerMv2Nx2NPred (4511-4515) */
+    e.flags = FME_TZ_PRED2NX2N;
+    e.pred2n_x = pred2n[0];
+    e.pred2n_y = pred2n[1];
+  }
+  const int16_t* keys = ctx->keys;
+  const size_t n_keys = ctx->n_keys;
+  if (bikey) {   /* m_cYuvPredTemp as this job's key block */
+    ctx->keys = bikey;
+    ctx->n_keys = (size_t)g->w * g->h;
+  }
+  int rc = orc_integer_search(ctx, &j, &e, NULL, 1);
+  if (!rc) rc = orc_refine(ctx, &j, r, 1);
+  ctx->keys = keys;
+  ctx->n_keys = n_keys;
+  return rc;
+}
+
+/* xCheckBestMVP (4344-4394), cost scale 0: move to a candidate with strictly fewer MV bits. */
+static void pi_check_best_mvp(double ml, const int16_t cand[2][2], int n_cand, int mx, int my, int* idx,
+                              uint32_t* bits, uint32_t* cost) {
+  if (n_cand < 2) return;
+  const int org_bits = (int)(mv_bits(mx, my, 0, cand[*idx][0], cand[*idx][1]) + pi_mvp_idx_bits(*idx, 2));
+  int best_bits = org_bits, best_idx = *idx;
+  for (int m = 0; m < n_cand; m++) {
+    if (m == *idx) continue;
+    const int b = (int)(mv_bits(mx, my, 0, cand[m][0], cand[m][1]) + pi_mvp_idx_bits(m, 2));
+    if (b < best_bits) {
+      best_bits = b;
+      best_idx = m;
+    }
+  }
+  if (best_idx != *idx) {
+    *idx = best_idx;
+    const uint32_t org_total = *bits;
+    *bits = org_total - (uint32_t)org_bits + (uint32_t)best_bits;
+    *cost = (*cost - orc_cost(ml, org_total)) + orc_cost(ml, *bits);
+  }
 }
 
 void orc_pred_inter_reset(orc_ctx* ctx) { memset(ctx->int_mv_2n, 0, sizeof(ctx->int_mv_2n)); }
@@ -1060,7 +1163,6 @@ int orc_pred_inter_p(orc_ctx* ctx, const fme_pu_req* reqs, fme_pu_res* res, int 
       free(pred);
       return FME_E_INVALID;
     }
-    const orc_picture* org = &ctx->pics[q->org_id];
     const double ml = ctx->mlambda[q->lambda_id];
     const int range = q->search_range ? q->search_range : 64;
     uint32_t best_cost = 0xFFFFFFFFu;   /* uiCost[0] = max */
@@ -1070,82 +1172,25 @@ int orc_pred_inter_p(orc_ctx* ctx, const fme_pu_req* reqs, fme_pu_res* res, int 
         return FME_E_INVALID;
       }
       /* uiBitsTemp = uiMbBits[0] + reference-index bits (3792-3800) */
-      uint32_t bits = pi_blk_bits(q->part_size);
-      if (q->num_refs > 1) {
-        bits += (uint32_t)k + 1;
-        if (k == q->num_refs - 1) bits--;
-      }
-      /* xEstimateMvPredAMVP (4186-4256) */
-      int idx = 0;
-      if (q->n_cand[k] > 1) {
-        uint32_t best = 0xFFFFFFFFu;
-        for (int m = 0; m < q->n_cand[k]; m++) {
-          const uint32_t c = pi_template_cost(ctx, q, k, m, pred);
-          if (best > c) {
-            best = c;
-            idx = m;
-          }
-        }
-      }
+      uint32_t bits = pi_blk_bits(q->part_size) + pi_ref_bits(k, q->num_refs);
+      const pi_pu g = pi_pu_of(q);
+      int idx = pi_amvp(ctx, &g, q->ref_id[k], q->n_cand[k], q->cand[k], pred);
       bits += pi_mvp_idx_bits(idx, 2);   /* m_auiMVPIdxCost[idx][AMVP_MAX_NUM_CANDS] (3812) */
       /* xMotionEstimation (4439-4599): xSetSearchRange, xTZSearch (+ EMI), FracDIF, NN, tail */
-      fme_job j;
-      memset(&j, 0, sizeof(j));
-      j.x = q->x; j.y = q->y; j.w = q->w; j.h = q->h;
-      j.org_id = q->org_id; j.ref_id = q->ref_id[k];
-      j.mvp_x = q->cand[k][idx][0]; j.mvp_y = q->cand[k][idx][1];
-      int cx = j.mvp_x, cy = j.mvp_y;
-      tz_clip(&cx, &cy, org->width, org->height, q->cu_x, q->cu_y);
-      int lx = cx - (range << 2), ly = cy - (range << 2), rx = cx + (range << 2), ry = cy + (range << 2);
-      tz_clip(&lx, &ly, org->width, org->height, q->cu_x, q->cu_y);
-      tz_clip(&rx, &ry, org->width, org->height, q->cu_x, q->cu_y);
-      j.lt_x = (int16_t)mv_round4(lx); j.lt_y = (int16_t)mv_round4(ly);
-      j.rb_x = (int16_t)mv_round4(rx); j.rb_y = (int16_t)mv_round4(ry);
-      j.flags = (uint8_t)(FME_JOB_EMI | ((q->flags & FME_PU_LOSSLESS) ? FME_JOB_LOSSLESS : 0u));
-      j.lambda_id = q->lambda_id;
-      j.bits_in = (uint16_t)bits;
-      j.key_offset = -1;
-      fme_tz_ext e;
-      memset(&e, 0, sizeof(e));
-      e.cu_x = q->cu_x; e.cu_y = q->cu_y;
-      e.search_range = (uint8_t)range;
-      if (!(q->part_size == FME_PART_2Nx2N && q->depth == 0)) {   /* pIntegerMv2Nx2NPred (4511-4515) */
-        e.flags = FME_TZ_PRED2NX2N;
-        e.pred2n_x = ctx->int_mv_2n[k][0];
-        e.pred2n_y = ctx->int_mv_2n[k][1];
-      }
+      const int reads2n = !(q->part_size == FME_PART_2Nx2N && q->depth == 0);
       fme_result r;
-      int rc = orc_integer_search(ctx, &j, &e, NULL, 1);
-      if (!rc) rc = orc_refine(ctx, &j, &r, 1);
+      const int rc = pi_me(ctx, &g, q->ref_id[k], q->cand[k][idx][0], q->cand[k][idx][1], bits, range,
+                           reads2n ? ctx->int_mv_2n[0][k] : NULL, NULL, 0, 0, &r);
       if (rc) {
         free(pred);
         return rc;
       }
       if (q->part_size == FME_PART_2Nx2N) {   /* m_integerMv2Nx2N = rcMv after the TZ search (4523-4526) */
-        ctx->int_mv_2n[k][0] = r.mv_int_x;
-        ctx->int_mv_2n[k][1] = r.mv_int_y;
+        ctx->int_mv_2n[0][k][0] = r.mv_int_x;
+        ctx->int_mv_2n[0][k][1] = r.mv_int_y;
       }
-      /* xCheckBestMVP (4344-4394), cost scale 0 */
       uint32_t rbits = r.bits, rcost = r.cost;
-      if (q->n_cand[k] >= 2) {
-        const int org_bits = (int)(mv_bits(r.mv_x, r.mv_y, 0, q->cand[k][idx][0], q->cand[k][idx][1]) +
-                                   pi_mvp_idx_bits(idx, 2));
-        int best_bits = org_bits, best_idx = idx;
-        for (int m = 0; m < q->n_cand[k]; m++) {
-          if (m == idx) continue;
-          const int b = (int)(mv_bits(r.mv_x, r.mv_y, 0, q->cand[k][m][0], q->cand[k][m][1]) + pi_mvp_idx_bits(m, 2));
-          if (b < best_bits) {
-            best_bits = b;
-            best_idx = m;
-          }
-        }
-        if (best_idx != idx) {
-          idx = best_idx;
-          const uint32_t org_total = rbits;
-          rbits = org_total - (uint32_t)org_bits + (uint32_t)best_bits;
-          rcost = (rcost - orc_cost(ml, org_total)) + orc_cost(ml, rbits);
-        }
-      }
+      pi_check_best_mvp(ml, q->cand[k], q->n_cand[k], r.mv_x, r.mv_y, &idx, &rbits, &rcost);
       o->ref_cost[k] = rcost;
       o->ref_bits[k] = rbits;
       o->ref_mv[k][0] = r.mv_x;
@@ -1166,4 +1211,237 @@ int orc_pred_inter_p(orc_ctx* ctx, const fme_pu_req* reqs, fme_pu_res* res, int 
   }
   free(pred);
   return FME_OK;
+}
+
+/* =====================================================================================
+ * predInterSearch for B slices, sequential: TEncSearch.cpp:3746-4105 with
+ * FEN 1/2 (one bi-pred iteration) and MvdL1ZeroFlag false.
+ * ===================================================================================== */
+
+/* xGetBlkBits (TEncSearch.cpp:4286-4333) for a B slice: uiBlkBit[0..2]. */
+static void pi_blk_bits_b(int part_size, int part_idx, int last_mode, uint32_t out[3]) {
+  static const uint32_t hor[2][3][3] = {{{0, 0, 3}, {0, 0, 0}, {0, 0, 0}}, {{5, 7, 7}, {7, 5, 7}, {6, 6, 6}}};
+  static const uint32_t ver[2][3][3] = {{{0, 2, 3}, {0, 0, 0}, {0, 0, 0}}, {{5, 7, 7}, {5, 5, 7}, {6, 6, 6}}};
+  if (part_size == FME_PART_2Nx2N || part_size == FME_PART_NxN) {
+    out[0] = 3; out[1] = 3; out[2] = 5;
+  } else {
+    const int hz = part_size == FME_PART_2NxN || part_size == FME_PART_2NxnU || part_size == FME_PART_2NxnD;
+    const uint32_t* t = hz ? hor[part_idx][last_mode] : ver[part_idx][last_mode];
+    out[0] = t[0]; out[1] = t[1]; out[2] = t[2];
+  }
+}
+
+/* xMotionEstimation(bBi)'s key (TEncSearch.cpp:4461-4471): the other list's uni-pred luma
+ * prediction (motionCompensation) at (mvx, mvy), key = 2 * org - pred (removeHighFreq, TComYuv.cpp
+ * :411-455), clipped to 8 bits with ClipForBiPredMe.  key: w*h. */
+void orc_bi_key(const orc_ctx* ctx, int org_id, int ref_id, int x, int y, int w, int h, int cu_x, int cu_y,
+                int mvx, int mvy, int clip, int16_t* key) {
+  int16_t pred[64 * 64];
+  const pi_pu g = {x, y, w, h, cu_x, cu_y, org_id, 0, 0};
+  pi_pred_uni(ctx, &g, ref_id, mvx, mvy, pred);
+  const orc_picture* org = &ctx->pics[org_id];
+  for (int r = 0; r < h; r++)
+    for (int c = 0; c < w; c++) {
+      int v = 2 * org->luma[(size_t)(y + r) * org->stride + x + c] - pred[r * w + c];
+      if (clip) v = clampi(v, 0, 255);
+      key[r * w + c] = (int16_t)v;
+    }
+}
+
+/* TComDataCU::getNumPartitions for the part_idx check. */
+static int pi_num_parts(int part_size) {
+  return part_size == FME_PART_2Nx2N ? 1 : (part_size == FME_PART_NxN ? 4 : 2);
+}
+
+int orc_pred_inter_b(orc_ctx* ctx, const fme_pu_req_b* reqs, fme_pu_res_b* res, int n) {
+  if (ctx->cfg.fast_inter_mode != 1 && ctx->cfg.fast_inter_mode != 2) return FME_E_INVALID;   /* iNumIter 1 */
+  int16_t* pred = (int16_t*)malloc(sizeof(int16_t) * 64 * 64);
+  int16_t* key = (int16_t*)malloc(sizeof(int16_t) * 64 * 64);
+  int last_mode = 0;   /* uiLastMode: 0 L0, 1 L1, 2 bi (predInterSearch local, per CU) */
+  int rc = FME_OK;
+  for (int i = 0; i < n && !rc; i++) {
+    const fme_pu_req_b* q = &reqs[i];
+    fme_pu_res_b* o = &res[i];
+    memset(o, 0, sizeof(*o));
+    if (q->org_id >= FME_MAX_PICTURES || !ctx->pics[q->org_id].luma || q->lambda_id >= FME_MAX_LAMBDAS ||
+        q->part_size > FME_PART_nRx2N || q->part_idx >= pi_num_parts(q->part_size) ||
+        (q->flags & ~(FME_PU_LOSSLESS | FME_PU_FAST_ME_GEN_B | FME_PU_CLIP_BIPRED))) {
+      rc = FME_E_INVALID;
+      break;
+    }
+    for (int l = 0; l < 2 && !rc; l++) {
+      if (q->num_refs[l] < 1 || q->num_refs[l] > FME_MAX_REFS) rc = FME_E_INVALID;
+      for (int k = 0; k < q->num_refs[l] && !rc; k++)
+        if (q->ref_id[l][k] >= FME_MAX_PICTURES || !ctx->pics[q->ref_id[l][k]].luma || q->n_cand[l][k] < 1 ||
+            q->n_cand[l][k] > 2 || (l == 1 && q->l1_to_l0[k] >= q->num_refs[0]))
+          rc = FME_E_INVALID;
+    }
+    if (!rc && q->part_size != FME_PART_2Nx2N && q->part_size != FME_PART_NxN && q->part_idx == 1 &&
+        (i == 0 || reqs[i - 1].part_idx != 0 || reqs[i - 1].part_size != q->part_size ||
+         reqs[i - 1].cu_x != q->cu_x || reqs[i - 1].cu_y != q->cu_y))
+      rc = FME_E_INVALID;   /* uiLastMode comes from the CU's first PU, the request before */
+    if (rc) break;
+    if (q->part_idx == 0) last_mode = 0;
+    const pi_pu g = {q->x, q->y, q->w, q->h, q->cu_x, q->cu_y, q->org_id, q->lambda_id, (q->flags & FME_PU_LOSSLESS) != 0};
+    const double ml = ctx->mlambda[q->lambda_id];
+    const int range = q->search_range ? q->search_range : 64;
+    const int brange = q->bipred_range ? q->bipred_range : 4;
+    uint32_t mb[3];
+    pi_blk_bits_b(q->part_size, q->part_idx, last_mode, mb);
+    uint32_t cost[2] = {0xFFFFFFFFu, 0xFFFFFFFFu}, bits[2] = {0, 0};
+    int16_t mv[2][2] = {{0, 0}, {0, 0}};
+    int ridx[2] = {0, 0};
+    uint32_t cost_l0[FME_MAX_REFS], bits_l0[FME_MAX_REFS];
+    int16_t mvt[2][FME_MAX_REFS][2];
+    int mvpi[2][FME_MAX_REFS];
+    uint32_t cost_v1 = 0xFFFFFFFFu, bits_v1 = 0xFFFFFFFFu;   /* costValidList1 / bitsValidList1 */
+    int16_t mv_v1[2] = {0, 0};
+    int ridx_v1 = 0;
+    const int reads2n = !(q->part_size == FME_PART_2Nx2N && q->depth == 0);
+    /* uni-directional prediction (3786-3865) */
+    for (int l = 0; l < 2 && !rc; l++)
+      for (int k = 0; k < q->num_refs[l] && !rc; k++) {
+        uint32_t b = mb[l] + pi_ref_bits(k, q->num_refs[l]);
+        int idx = pi_amvp(ctx, &g, q->ref_id[l][k], q->n_cand[l][k], q->cand[l][k], pred);
+        b += pi_mvp_idx_bits(idx, 2);
+        uint32_t c;
+        if ((q->flags & FME_PU_FAST_ME_GEN_B) && l == 1 && q->l1_to_l0[k] >= 0) {
+          /* 3814-3827: L0's result, its bit-rate part re-priced with L1's predictor */
+          const int k0 = q->l1_to_l0[k];
+          mvt[1][k][0] = mvt[0][k0][0];
+          mvt[1][k][1] = mvt[0][k0][1];
+          c = cost_l0[k0] - orc_cost(ml, bits_l0[k0]);
+          b += mv_bits(mvt[1][k][0], mvt[1][k][1], 0, q->cand[1][k][idx][0], q->cand[1][k][idx][1]);
+          c += orc_cost(ml, b);
+        } else {
+          fme_result r;
+          rc = pi_me(ctx, &g, q->ref_id[l][k], q->cand[l][k][idx][0], q->cand[l][k][idx][1], b, range,
+                     reads2n ? ctx->int_mv_2n[l][k] : NULL, NULL, 0, 0, &r);
+          if (rc) break;
+          if (q->part_size == FME_PART_2Nx2N) {
+            ctx->int_mv_2n[l][k][0] = r.mv_int_x;
+            ctx->int_mv_2n[l][k][1] = r.mv_int_y;
+          }
+          mvt[l][k][0] = r.mv_x;
+          mvt[l][k][1] = r.mv_y;
+          b = r.bits;
+          c = r.cost;
+        }
+        pi_check_best_mvp(ml, q->cand[l][k], q->n_cand[l][k], mvt[l][k][0], mvt[l][k][1], &idx, &b, &c);
+        mvpi[l][k] = idx;
+        o->ref_cost[l][k] = c;
+        o->ref_mv[l][k][0] = mvt[l][k][0];
+        o->ref_mv[l][k][1] = mvt[l][k][1];
+        o->ref_mvp_idx[l][k] = (uint8_t)idx;
+        if (l == 0) {
+          cost_l0[k] = c;
+          bits_l0[k] = b;
+        }
+        if (c < cost[l]) {
+          cost[l] = c;
+          bits[l] = b;
+          mv[l][0] = mvt[l][k][0];
+          mv[l][1] = mvt[l][k][1];
+          ridx[l] = k;
+        }
+        if (l == 1 && c < cost_v1 && q->l1_to_l0[k] < 0) {
+          cost_v1 = c;
+          bits_v1 = b;
+          mv_v1[0] = mvt[1][k][0];
+          mv_v1[1] = mvt[1][k][1];
+          ridx_v1 = k;
+        }
+      }
+    if (rc) break;
+    /* bi-predictive motion estimation (3868-4022), one iteration */
+    uint32_t cost_bi = 0xFFFFFFFFu, bits_bi = 0;
+    int16_t mv_bi[2][2] = {{mv[0][0], mv[0][1]}, {mv[1][0], mv[1][1]}};
+    int ridx_bi[2] = {ridx[0], ridx[1]};
+    int mvpi_bi[2][FME_MAX_REFS];
+    memcpy(mvpi_bi, mvpi, sizeof(mvpi));
+    o->bi_list = 0xFF;
+    o->bi_cost = 0xFFFFFFFFu;
+    const int restricted = q->cu_w == 8 && (q->w < 8 || q->h < 8);   /* isBipredRestriction */
+    if (!restricted) {
+      uint32_t mot[2] = {bits[0] - mb[0], bits[1] - mb[1]};
+      bits_bi = mb[2] + mot[0] + mot[1];
+      const int L = cost[0] <= cost[1] ? 1 : 0;   /* FASTINTERSEARCH_MODE1/2 (3931-3941) */
+      /* motionCompensation of the other list, removeHighFreq (TComYuv.cpp:411-455) */
+      orc_bi_key(ctx, q->org_id, q->ref_id[1 - L][ridx[1 - L]], q->x, q->y, q->w, q->h, q->cu_x, q->cu_y,
+                 mv[1 - L][0], mv[1 - L][1], (q->flags & FME_PU_CLIP_BIPRED) != 0, key);
+      o->bi_list = (uint8_t)L;
+      for (int k = 0; k < q->num_refs[L]; k++) {
+        uint32_t b = mb[2] + mot[1 - L] + pi_ref_bits(k, q->num_refs[L]) + pi_mvp_idx_bits(mvpi_bi[L][k], 2);
+        const int16_t* p = q->cand[L][k][mvpi_bi[L][k]];
+        fme_result r;
+        rc = pi_me(ctx, &g, q->ref_id[L][k], p[0], p[1], b, brange, NULL, key, mvt[L][k][0], mvt[L][k][1], &r);
+        if (rc) break;
+        uint32_t c = r.cost;
+        b = r.bits;
+        int idx = mvpi_bi[L][k];
+        pi_check_best_mvp(ml, q->cand[L][k], q->n_cand[L][k], r.mv_x, r.mv_y, &idx, &b, &c);
+        mvpi_bi[L][k] = idx;
+        o->bi_ref_cost[k] = c;
+        o->bi_ref_mv[k][0] = r.mv_x;
+        o->bi_ref_mv[k][1] = r.mv_y;
+        if (c < cost_bi) {
+          mv_bi[L][0] = r.mv_x;
+          mv_bi[L][1] = r.mv_y;
+          ridx_bi[L] = k;
+          cost_bi = c;
+          mot[L] = b - mb[2] - mot[1 - L];
+          bits_bi = b;
+        }
+      }
+      if (rc) break;
+      /* (!bChanged needs every bi cost at the Distortion maximum: not reachable with 32-bit costs
+       * below it, so its xCheckBestMVP re-run of 4008-4021 is not restated.) */
+    }
+    o->bi_cost = cost_bi;
+    o->bi_bits = restricted ? 0 : bits_bi;
+    o->uni_cost[0] = cost[0];
+    o->uni_bits[0] = bits[0];
+    o->uni_cost[1] = cost_v1;
+    o->uni_bits[1] = bits_v1;
+    /* decision (4041-4105) */
+    if (cost_bi <= cost[0] && cost_bi <= cost_v1) {
+      last_mode = 2;
+      o->inter_dir = 3;
+      o->bits = bits_bi;
+      o->cost = cost_bi;
+      for (int l = 0; l < 2; l++) {
+        o->ref_idx[l] = (uint8_t)ridx_bi[l];
+        o->mvp_idx[l] = (uint8_t)mvpi_bi[l][ridx_bi[l]];
+        o->mv[l][0] = mv_bi[l][0];
+        o->mv[l][1] = mv_bi[l][1];
+        o->mvp[l][0] = q->cand[l][ridx_bi[l]][mvpi_bi[l][ridx_bi[l]]][0];
+        o->mvp[l][1] = q->cand[l][ridx_bi[l]][mvpi_bi[l][ridx_bi[l]]][1];
+      }
+    } else if (cost[0] <= cost_v1) {
+      last_mode = 0;
+      o->inter_dir = 1;
+      o->bits = bits[0];
+      o->cost = cost[0];
+      o->ref_idx[0] = (uint8_t)ridx[0];
+      o->mvp_idx[0] = (uint8_t)mvpi[0][ridx[0]];
+      o->mv[0][0] = mv[0][0];
+      o->mv[0][1] = mv[0][1];
+      o->mvp[0][0] = q->cand[0][ridx[0]][mvpi[0][ridx[0]]][0];
+      o->mvp[0][1] = q->cand[0][ridx[0]][mvpi[0][ridx[0]]][1];
+    } else {
+      last_mode = 1;
+      o->inter_dir = 2;
+      o->bits = bits_v1;
+      o->cost = cost_v1;
+      o->ref_idx[1] = (uint8_t)ridx_v1;
+      o->mvp_idx[1] = (uint8_t)mvpi[1][ridx_v1];
+      o->mv[1][0] = mv_v1[0];
+      o->mv[1][1] = mv_v1[1];
+      o->mvp[1][0] = q->cand[1][ridx_v1][mvpi[1][ridx_v1]][0];
+      o->mvp[1][1] = q->cand[1][ridx_v1][mvpi[1][ridx_v1]][1];
+    }
+  }
+  free(pred);
+  free(key);
+  return rc;
 }

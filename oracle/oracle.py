@@ -69,6 +69,9 @@ class Oracle:
         lib.orc_pred_inter_reset.argtypes = [_P]
         lib.orc_template_cost.restype = C.c_uint32
         lib.orc_template_cost.argtypes = [_P, _P, C.c_int, C.c_int]
+        lib.orc_pred_inter_b.restype = C.c_int
+        lib.orc_pred_inter_b.argtypes = [_P, _P, _P, C.c_int]
+        lib.orc_bi_key.argtypes = [_P] + [C.c_int] * 11 + [_P]
         lib.orc_mc.restype = C.c_int
         lib.orc_mc.argtypes = [_P, _P, C.c_int, _P, C.c_int, _P, _P, C.c_int, C.c_int, C.c_int]
         lib.orc_nn_param_count.restype = C.c_int
@@ -169,6 +172,22 @@ class Oracle:
     def pred_inter_reset(self):
         self.lib.orc_pred_inter_reset(self.ctx)
 
+    def pred_inter_b(self, reqs):
+        """orc_pred_inter_b: predInterSearch on a B slice, one fme_pu_res_b per request."""
+        from nnfme.abi import PU_REQ_B_DTYPE, PU_RES_B_DTYPE
+        reqs = np.ascontiguousarray(reqs, dtype=PU_REQ_B_DTYPE)
+        res = np.zeros(len(reqs), dtype=PU_RES_B_DTYPE)
+        rc = self.lib.orc_pred_inter_b(self.ctx, _ptr(reqs), _ptr(res), len(reqs))
+        if rc != 0:
+            raise RuntimeError(f"orc_pred_inter_b failed: {rc}")
+        return res
+
+    def bi_key(self, org_id, ref_id, x, y, w, h, cu_x, cu_y, mvx, mvy, clip=False):
+        """orc_bi_key: 2 * org - the other list's uni-pred luma prediction (removeHighFreq)."""
+        key = np.zeros((h, w), np.int16)
+        self.lib.orc_bi_key(self.ctx, org_id, ref_id, x, y, w, h, cu_x, cu_y, mvx, mvy, int(bool(clip)), _ptr(key))
+        return key
+
     def template_cost(self, req, k, m):
         """orc_template_cost: xGetTemplateCost of candidate m of reference k of one fme_pu_req."""
         from nnfme.abi import PU_REQ_DTYPE
@@ -235,6 +254,8 @@ class Reference:
         lib.ref_integer_search.argtypes = [_P, _P, _P, _P, C.c_int]
         lib.ref_template_cost.restype = C.c_uint32
         lib.ref_template_cost.argtypes = [_P] + [C.c_int] * 12
+        lib.ref_bi_key.restype = C.c_int
+        lib.ref_bi_key.argtypes = [_P] + [C.c_int] * 11 + [_P]
         lib.ref_mc.restype = C.c_int
         lib.ref_mc.argtypes = [_P, _P, C.c_int, _P, C.c_int, _P, _P, C.c_int, C.c_int, C.c_int]
         self.h = lib.ref_create(use_hadamard, fast_inter_mode, nn_mode)
@@ -279,6 +300,13 @@ class Reference:
         if v == 0xFFFFFFFF:
             raise RuntimeError("ref_template_cost: unset picture or bad slot")
         return v
+
+    def bi_key(self, org_id, ref_id, x, y, w, h, cu_x, cu_y, mvx, mvy, clip=False):
+        """The reference's TComYuv::removeHighFreq on the other list's prediction (ref_bi_key)."""
+        key = np.zeros((h, w), np.int16)
+        if self.lib.ref_bi_key(self.h, org_id, ref_id, x, y, w, h, cu_x, cu_y, mvx, mvy, int(bool(clip)), _ptr(key)):
+            raise RuntimeError("ref_bi_key: unset picture or bad slot")
+        return key
 
     def set_keys(self, keys):
         keys = np.ascontiguousarray(keys, dtype=np.int16)

@@ -667,6 +667,59 @@ uint32_t ref_template_cost(void* h, int org_id, int ref_id, int x, int y, int w,
   return (UInt)c->s.rd.calcRdCost(bits, sad, DF_SAD);
 }
 
+// The bi-pred search key of xMotionEstimation(bBi) (TEncSearch.cpp:4461-4471): the other list's
+// uni-pred luma prediction (motionCompensation: clipMv, xPredInterBlk's filter order, isLast) in a
+// TComYuv, the original copied into m_cYuvPredTemp, then the reference's own
+// TComYuv::removeHighFreq (TComYuv.cpp:411-455) with or without ClipForBiPredMe.  key: w*h.
+int ref_bi_key(void* h, int org_id, int ref_id, int x, int y, int w, int hgt, int cu_x, int cu_y, int mvx, int mvy,
+               int clip, int16_t* key) {
+  RefCtx* c = static_cast<RefCtx*>(h);
+  if (org_id < 0 || org_id >= FME_MAX_PICTURES || ref_id < 0 || ref_id >= FME_MAX_PICTURES ||
+      !c->pics[org_id].set || !c->pics[ref_id].set)
+    return -1;
+  TComPicYuv& ref = c->pics[ref_id].yuv;
+  TComPicYuv& org = c->pics[org_id].yuv;
+  const int W = ref.getWidth(COMPONENT_Y), H = ref.getHeight(COMPONENT_Y);
+  {   // TComDataCU::clipMv
+    const int hmax = (W + 8 - cu_x - 1) << 2, hmin = (-64 - 8 - cu_x + 1) * 4;
+    const int vmax = (H + 8 - cu_y - 1) << 2, vmin = (-64 - 8 - cu_y + 1) * 4;
+    mvx = std::min(hmax, std::max(hmin, mvx));
+    mvy = std::min(vmax, std::max(vmin, mvy));
+  }
+  TComYuv other, temp;
+  other.create(w, hgt, CHROMA_400);
+  temp.create(w, hgt, CHROMA_400);
+  TComInterpolationFilter f;
+  const int rs = ref.getStride(COMPONENT_Y);
+  Pel* src = ref.getAddr(COMPONENT_Y) + (y + (mvy >> 2)) * rs + x + (mvx >> 2);
+  Pel* dst = other.getAddr(COMPONENT_Y);
+  const int ds = other.getStride(COMPONENT_Y);
+  const int xf = mvx & 3, yf = mvy & 3;
+  if (yf == 0) {
+    f.filterHor(COMPONENT_Y, src, rs, dst, ds, w, hgt, xf, true, CHROMA_400, 8);
+  } else if (xf == 0) {
+    f.filterVer(COMPONENT_Y, src, rs, dst, ds, w, hgt, yf, true, true, CHROMA_400, 8);
+  } else {
+    std::vector<Pel> tmp((size_t)w * (hgt + NTAPS_LUMA - 1));
+    f.filterHor(COMPONENT_Y, src - ((NTAPS_LUMA >> 1) - 1) * rs, rs, tmp.data(), w, w, hgt + NTAPS_LUMA - 1, xf, false,
+                CHROMA_400, 8);
+    f.filterVer(COMPONENT_Y, tmp.data() + ((NTAPS_LUMA >> 1) - 1) * w, w, dst, ds, w, hgt, yf, false, true, CHROMA_400,
+                8);
+  }
+  const int os = org.getStride(COMPONENT_Y), ts = temp.getStride(COMPONENT_Y);
+  const Pel* o = org.getAddr(COMPONENT_Y) + y * os + x;
+  Pel* t = temp.getAddr(COMPONENT_Y);
+  for (int r = 0; r < hgt; r++)
+    for (int q = 0; q < w; q++) t[r * ts + q] = o[r * os + q];
+  const Int bd[MAX_NUM_CHANNEL_TYPE] = {8, 8};
+  temp.removeHighFreq(&other, 0, w, hgt, bd, clip != 0);
+  for (int r = 0; r < hgt; r++)
+    for (int q = 0; q < w; q++) key[r * w + q] = (int16_t)t[r * ts + q];
+  other.destroy();
+  temp.destroy();
+  return 0;
+}
+
 }  // extern "C"
 
 // ---- integer motion estimation ----------------------------------------
