@@ -135,6 +135,7 @@ struct fme_ctx {
   DevBuf<int16_t> d_tz_emi;   // [n][2] post-EMI integer MVs (producer levels)
   DevBuf<uint32_t> d_amvp_sad;
   DevBuf<BiKeyTask> d_bikey;
+  DevBuf<int32_t> d_ch_i32;     // k_tz_level: psrc
 
   std::unique_ptr<fme_ctx> single;  // private context for the single-PU entry points
   DevBuf<uint8_t> single_pic;
@@ -231,7 +232,7 @@ int fme_destroy(fme_ctx* c) {
     if (c->chroma_owned[i]) (void)hipFree(c->chroma_owned[i]);
   c->d_mc_jobs.release(); c->d_mc_planes.release(); c->d_mc_invalid.release();
   c->d_tz_ext.release(); c->d_tz_sad.release(); c->d_tz_rst.release(); c->d_tz_rq.release();
-  c->d_amvp.release(); c->d_amvp_sad.release(); c->d_bikey.release(); c->d_tz_emi.release();
+  c->d_amvp.release(); c->d_amvp_sad.release(); c->d_bikey.release(); c->d_ch_i32.release(); c->d_tz_emi.release();
   for (auto& e : c->ev_tz)
     if (e) (void)hipEventDestroy(e);
   for (auto& e : c->ev_mc)
@@ -786,6 +787,73 @@ static int tz_run_host(fme_ctx* c, fme_job* jobs, const fme_tz_ext* ext, uint32_
   if (sad) HIP_TRY(hipMemcpyAsync(sad, c->d_tz_sad.p, (size_t)n * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
   if (emi) HIP_TRY(hipMemcpyAsync(emi, c->d_tz_emi.p, (size_t)n * 2 * sizeof(int16_t), hipMemcpyDeviceToHost, s));
   HIP_TRY(hipStreamSynchronize(s));
+  return FME_OK;
+}
+
+// The integer searches of a producer's jobs by m_integerMv2Nx2N dependency level.  jobs / ext in
+// call order (ext's pred2n already set where src[u] < 0); lvl[u]: the level of job u; src[u]: the
+// job whose post-EMI MV is u's m_integerMv2Nx2N, or -1.  One upload, one k_tz_level launch per
+// level back to back on the stream (a level reads the earlier levels' MVs from device memory), one
+// download: the chain of a 1080p frame (≈ 2,200 levels, most of a few jobs: the bottom CTU row has
+// no depth-0 CU) never waits for the host.  emi: the post-EMI integer MV of every job.
+static int tz_by_level(fme_ctx* c, std::vector<fme_job>& jobs, std::vector<fme_tz_ext>& ext,
+                       const std::vector<int>& src, const std::vector<int>& lvl, hipStream_t s,
+                       std::vector<int16_t>& emi) {
+  const int nu = (int)jobs.size();
+  emi.assign((size_t)nu * 2, 0);
+  if (nu == 0) return FME_OK;
+  int max_level = 0;
+  for (int v : lvl) max_level = std::max(max_level, v);
+  std::vector<int32_t> off((size_t)max_level + 2, 0), pos((size_t)nu), psrc((size_t)nu);
+  std::vector<int> order((size_t)nu);
+  for (int u = 0; u < nu; u++) off[lvl[u] + 1]++;
+  for (int l = 0; l <= max_level; l++) off[l + 1] += off[l];
+  {
+    std::vector<int32_t> fill(off.begin(), off.end() - 1);
+    for (int u = 0; u < nu; u++) {
+      pos[u] = fill[lvl[u]]++;
+      order[pos[u]] = u;
+    }
+  }
+  std::vector<fme_job> lj((size_t)nu);
+  std::vector<fme_tz_ext> le((size_t)nu);
+  for (int q = 0; q < nu; q++) {
+    const int u = order[q];
+    lj[q] = jobs[u];
+    le[q] = ext[u];
+    psrc[q] = ((ext[u].flags & FME_TZ_PRED2NX2N) && src[u] >= 0) ? pos[src[u]] : -1;
+  }
+  HIP_TRY(c->d_jobs.reserve(nu));
+  HIP_TRY(c->d_tz_ext.reserve(nu));
+  HIP_TRY(c->d_tz_emi.reserve((size_t)2 * nu));
+  HIP_TRY(c->d_ch_i32.reserve((size_t)nu));
+  HIP_TRY(hipMemcpyAsync(c->d_jobs.p, lj.data(), (size_t)nu * sizeof(fme_job), hipMemcpyHostToDevice, s));
+  HIP_TRY(hipMemcpyAsync(c->d_tz_ext.p, le.data(), (size_t)nu * sizeof(fme_tz_ext), hipMemcpyHostToDevice, s));
+  HIP_TRY(hipMemcpyAsync(c->d_ch_i32.p, psrc.data(), (size_t)nu * sizeof(int32_t), hipMemcpyHostToDevice, s));
+  TzArgs ta{};
+  ta.a.jobs = c->d_jobs.p;
+  ta.a.keys = c->d_keys.p;
+  ta.a.n_keys = (int64_t)c->n_keys;
+  ta.a.mlambda = c->d_mlambda.p;
+  ta.a.pics = c->d_pics.p;
+  ta.a.n = nu;
+  ta.a.use_hadamard = c->cfg.use_hadamard ? 1 : 0;
+  ta.a.fen = c->cfg.fast_inter_mode;
+  ta.jobs_out = c->d_jobs.p;
+  ta.ext = c->d_tz_ext.p;
+  ta.emi_mv = c->d_tz_emi.p;
+  const TzChain ch{c->d_ch_i32.p, max_level + 1};
+  HIP_TRY(launch_tz_levels(ta, ch, off.data(), s));
+  std::vector<int16_t> lemi((size_t)2 * nu);
+  HIP_TRY(hipMemcpyAsync(lj.data(), c->d_jobs.p, (size_t)nu * sizeof(fme_job), hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipMemcpyAsync(lemi.data(), c->d_tz_emi.p, (size_t)2 * nu * sizeof(int16_t), hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipStreamSynchronize(s));
+  for (int q = 0; q < nu; q++) {
+    const int u = order[q];
+    jobs[u] = lj[q];
+    emi[2 * u] = lemi[2 * q];
+    emi[2 * u + 1] = lemi[2 * q + 1];
+  }
   return FME_OK;
 }
 
@@ -1370,10 +1438,9 @@ int fme_pred_inter_p(fme_ctx* c, const fme_pu_req* reqs, fme_pu_res* res, int n,
       e.flags = reads ? FME_TZ_PRED2NX2N : 0;
     }
   }
-  // ---- 2. dependency levels of m_integerMv2Nx2N ----
-  std::vector<int> level((size_t)n, 0), src((size_t)nj, -1);   // src: job whose post-EMI MV is read
+  // ---- 2. integer searches by m_integerMv2Nx2N dependency level ----
+  std::vector<int> level((size_t)n, 0), src((size_t)nj, -1), lvl((size_t)nj, 0);   // src: job whose post-EMI MV is read
   int last[FME_MAX_REFS] = {-1, -1, -1, -1};
-  int max_level = 0;
   for (int i = 0; i < n; i++) {
     const fme_pu_req& q = reqs[i];
     const bool reads = !(q.part_size == FME_PART_2Nx2N && q.depth == 0);
@@ -1385,40 +1452,18 @@ int fme_pred_inter_p(fme_ctx* c, const fme_pu_req* reqs, fme_pu_res* res, int n,
         }
     if (q.part_size == FME_PART_2Nx2N)
       for (int k = 0; k < q.num_refs; k++) last[k] = i;
-    max_level = std::max(max_level, level[i]);
-  }
-  std::vector<std::vector<int>> by_level((size_t)max_level + 1);
-  for (int i = 0; i < n; i++) by_level[level[i]].push_back(i);
-  std::vector<int16_t> emi_mv((size_t)nj * 2, 0);   // post-EMI integer MV of 2Nx2N jobs
-  std::vector<fme_job> lj;
-  std::vector<fme_tz_ext> le;
-  std::vector<int> lidx;
-  std::vector<int16_t> lemi;
-  for (int L = 0; L <= max_level; L++) {
-    lj.clear(); le.clear(); lidx.clear();
-    for (int i : by_level[L])
-      for (int k = 0; k < reqs[i].num_refs; k++) {
-        const int jx = base[i] + k;
-        fme_tz_ext e = ext[jx];
-        if (e.flags & FME_TZ_PRED2NX2N) {
-          const int sj = src[jx];
-          e.pred2n_x = sj >= 0 ? emi_mv[2 * sj] : c->int_mv_2n[0][k][0];
-          e.pred2n_y = sj >= 0 ? emi_mv[2 * sj + 1] : c->int_mv_2n[0][k][1];
-        }
-        lj.push_back(jobs[jx]);
-        le.push_back(e);
-        lidx.push_back(jx);
+    for (int k = 0; k < q.num_refs; k++) {
+      lvl[base[i] + k] = level[i];
+      fme_tz_ext& e = ext[base[i] + k];
+      if ((e.flags & FME_TZ_PRED2NX2N) && src[base[i] + k] < 0) {
+        e.pred2n_x = c->int_mv_2n[0][k][0];
+        e.pred2n_y = c->int_mv_2n[0][k][1];
       }
-    lemi.resize(2 * lj.size());
-    // the integer searches of this level, with the EMI square step's result for the levels above
-    rc = tz_run_host(c, lj.data(), le.data(), nullptr, (int)lj.size(), stream, lemi.data());
-    if (rc) return rc;
-    for (size_t m = 0; m < lj.size(); m++) {
-      jobs[lidx[m]] = lj[m];
-      emi_mv[2 * lidx[m]] = lemi[2 * m];
-      emi_mv[2 * lidx[m] + 1] = lemi[2 * m + 1];
     }
   }
+  std::vector<int16_t> emi_mv;
+  rc = tz_by_level(c, jobs, ext, src, lvl, s, emi_mv);
+  if (rc) return rc;
   // ---- 3. the sub-pel path over every job in request order ----
   std::vector<fme_result> r((size_t)nj);
   rc = fme_refine(c, jobs.data(), r.data(), nj, stream);
@@ -1615,9 +1660,8 @@ int fme_pred_inter_b(fme_ctx* c, const fme_pu_req_b* reqs, fme_pu_res_b* res, in
   ubeg[n] = (int)uj.size();
   const int nu = (int)uj.size();
   {
-    std::vector<int> level((size_t)n, 0), src((size_t)nu, -1);
+    std::vector<int> level((size_t)n, 0), src((size_t)nu, -1), lvl((size_t)nu, 0);
     int last[8] = {-1, -1, -1, -1, -1, -1, -1, -1};   // last 2Nx2N writer of m_integerMv2Nx2N[l][k]
-    int max_level = 0;
     for (int i = 0; i < n; i++) {
       for (int u = ubeg[i]; u < ubeg[i + 1]; u++)
         if ((ue[u].flags & FME_TZ_PRED2NX2N) && last[ukey[u]] >= 0) {
@@ -1626,38 +1670,17 @@ int fme_pred_inter_b(fme_ctx* c, const fme_pu_req_b* reqs, fme_pu_res_b* res, in
         }
       if (reqs[i].part_size == FME_PART_2Nx2N)
         for (int u = ubeg[i]; u < ubeg[i + 1]; u++) last[ukey[u]] = i;
-      max_level = std::max(max_level, level[i]);
-    }
-    std::vector<std::vector<int>> by_level((size_t)max_level + 1);
-    for (int i = 0; i < n; i++) by_level[level[i]].push_back(i);
-    std::vector<int16_t> emi_mv((size_t)nu * 2, 0), lemi;
-    std::vector<fme_job> lj;
-    std::vector<fme_tz_ext> le;
-    std::vector<int> lidx;
-    for (int L = 0; L <= max_level; L++) {
-      lj.clear(); le.clear(); lidx.clear();
-      for (int i : by_level[L])
-        for (int u = ubeg[i]; u < ubeg[i + 1]; u++) {
-          fme_tz_ext e = ue[u];
-          if (e.flags & FME_TZ_PRED2NX2N) {
-            const int sj = src[u];
-            e.pred2n_x = sj >= 0 ? emi_mv[2 * sj] : c->int_mv_2n[ukey[u] >> 2][ukey[u] & 3][0];
-            e.pred2n_y = sj >= 0 ? emi_mv[2 * sj + 1] : c->int_mv_2n[ukey[u] >> 2][ukey[u] & 3][1];
-          }
-          lj.push_back(uj[u]);
-          le.push_back(e);
-          lidx.push_back(u);
+      for (int u = ubeg[i]; u < ubeg[i + 1]; u++) {
+        lvl[u] = level[i];
+        if ((ue[u].flags & FME_TZ_PRED2NX2N) && src[u] < 0) {
+          ue[u].pred2n_x = c->int_mv_2n[ukey[u] >> 2][ukey[u] & 3][0];
+          ue[u].pred2n_y = c->int_mv_2n[ukey[u] >> 2][ukey[u] & 3][1];
         }
-      if (lj.empty()) continue;
-      lemi.resize(2 * lj.size());
-      rc = tz_run_host(c, lj.data(), le.data(), nullptr, (int)lj.size(), stream, lemi.data());
-      if (rc) return rc;
-      for (size_t m = 0; m < lj.size(); m++) {
-        uj[lidx[m]] = lj[m];
-        emi_mv[2 * lidx[m]] = lemi[2 * m];
-        emi_mv[2 * lidx[m] + 1] = lemi[2 * m + 1];
       }
     }
+    std::vector<int16_t> emi_mv;
+    rc = tz_by_level(c, uj, ue, src, lvl, s, emi_mv);
+    if (rc) return rc;
   }
   // ---- 3. the uni-pred sub-pel path in call order ----
   uint32_t s0[12];

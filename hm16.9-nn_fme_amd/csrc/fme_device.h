@@ -154,6 +154,13 @@ struct TzSchedule {
 };
 hipError_t launch_tz(const TzArgs& ta, const TzSchedule& sc, int kid, hipStream_t s);
 hipError_t launch_tz_raster(const TzArgs& ta, const TzSchedule& sc, int kid, int nq, hipStream_t s);
+// The dependency levels of a producer's m_integerMv2Nx2N chain (fme_tz.hip k_tz_level): jobs in
+// level order, level l = jobs [lvl_off[l], lvl_off[l+1]), one launch per level, back to back.
+struct TzChain {
+  const int32_t* psrc;        // [n]: job whose post-EMI MV is m_integerMv2Nx2N, or -1
+  int32_t nlev;
+};
+hipError_t launch_tz_levels(const TzArgs& ta, const TzChain& ch, const int32_t* h_lvl_off, hipStream_t s);
 
 // Host-side launch helpers (fme_kernels.hip).
 hipError_t launch_classify(const BatchArgs& a, const WorkBufs& w, hipStream_t s);

@@ -410,9 +410,16 @@ constexpr int kTzRec = 8;   // best_sad, bx, by, pnr, RR.l, RR.r, RR.t, RR.b
 //   RASTER = true:  pass 2, one queued PU per wave: its raster points are spread over the wave's
 //                   64 / L groups (their (cost, scan index) minimum is the sequential scan's best),
 //                   then every group finishes the star refinement of the same PU in lock-step.
-template <int UW, int UH, bool RASTER>
+//   MODE 2 (chain): one job (rjid) per wave, every one of the wave's G = 64 / L groups on it: each
+//                   step takes up to G candidates the reference tests without a decision between
+//                   them (a diamond ring, the two-point pair, a stretch of the raster), group g
+//                   computes candidate g, and every lane applies xTZSearchHelp's updates in the
+//                   reference's order — the search's dependent steps shrink G-fold (k_tz_level).
+//                   pred (x, y): m_integerMv2Nx2N for a job whose ext has FME_TZ_PRED2NX2N.
+template <int UW, int UH, int MODE>
 __device__ __forceinline__ void tz_unit(const TzArgs& ta, int cls_off, int cls_cnt, int p, int u, int L, int PW,
-                                        int PH, int rjid) {
+                                        int PH, int rjid, int pred_x = 0, int pred_y = 0) {
+  constexpr bool RASTER = MODE == 1, CHAIN = MODE == 2;
   constexpr int KID = UW == 4 ? 0 : (UH == 4 ? 1 : 2);
   const BatchArgs& a = ta.a;
   const int UX = PW / UW, LR = UX * (PH / UH);
@@ -422,8 +429,8 @@ __device__ __forceinline__ void tz_unit(const TzArgs& ta, int cls_off, int cls_c
   const int uu = real ? u : 0;
   const int ux = uu % UX, uy = uu / UX;
 
-  const int jid = RASTER ? rjid : ta.perm[cls_off + p];
-  const fme_job j = RASTER ? a.jobs[jid] : ta.sjobs[cls_off + p];
+  const int jid = (RASTER || CHAIN) ? rjid : ta.perm[cls_off + p];
+  const fme_job j = (RASTER || CHAIN) ? a.jobs[jid] : ta.sjobs[cls_off + p];
   const fme_tz_ext e = ta.ext[jid];
   const PicDesc ref = a.pics[j.ref_id];
   const double ml = a.mlambda[j.lambda_id];
@@ -465,7 +472,7 @@ __device__ __forceinline__ void tz_unit(const TzArgs& ta, int cls_off, int cls_c
   s.RR = s.R;
   s.range = e.search_range ? e.search_range : 64;
   s.k = -1; s.dist = 1; s.ox = s.oy = 0; s.opnr = 0; s.ret = P_DONE;
-  const bool defer = !RASTER && ta.defer;
+  const bool defer = MODE == 0 && ta.defer;
   s.sx = s.sy = 0; s.px = s.py = 0; s.has_pred = false;
   s.rx = s.ry = 0;
   s.square = ta.emi_mv != nullptr && (j.flags & FME_JOB_EMI) && !(j.flags & FME_JOB_BIPRED);
@@ -520,7 +527,7 @@ __device__ __forceinline__ void tz_unit(const TzArgs& ta, int cls_off, int cls_c
     s.sx = round4(mx);
     s.sy = round4(my);
     s.has_pred = (e.flags & FME_TZ_PRED2NX2N) != 0;
-    int qx = e.pred2n_x * 4, qy = e.pred2n_y * 4;
+    int qx = (CHAIN ? pred_x : e.pred2n_x) * 4, qy = (CHAIN ? pred_y : e.pred2n_y) * 4;
     clip_qpel(qx, qy, ref.width, ref.height, e.cu_x, e.cu_y);
     s.px = round4(qx);
     s.py = round4(qy);
@@ -538,6 +545,71 @@ __device__ __forceinline__ void tz_unit(const TzArgs& ta, int cls_off, int cls_c
 #else
   constexpr int B = 1;
 #endif
+  if constexpr (CHAIN) {
+    // xTZSearchHelp's updates over a batch in the reference's order keep the first strict minimum of
+    // cost = distortion + MV cost below the running best: one (cost, batch index) minimum over the
+    // groups.  A diamond ring or raster stretch is enumerated directly once the state machine has
+    // entered it (next_candidate's look-ahead per point would cost more than the loads it saves).
+    const int lane = (int)threadIdx.x & 63, g = lane / L, G = 64 / L;
+    for (int step = 0; step < (1 << 16); step++) {   // bound: a search tests < 2,000 points
+      int mx = 0, my = 0, mp = 0, md = 0, nc = 0;
+      bool more = true;
+      while (nc < G && more) {
+        if (nc > 0 && (s.phase == P_FIRST || s.phase == P_STAR) && s.k >= 0) {
+          bool ok;
+          int x, y, pnr, pd;
+          while (nc < G && diamond_point(s, s.k, ok, x, y, pnr, pd)) {
+            s.k++;
+            if (ok) {
+              if (nc == g) { mx = x; my = y; mp = pnr; md = pd; }
+              nc++;
+            }
+          }
+          break;
+        }
+        if (nc > 0 && s.phase == P_RASTER) {
+          while (nc < G && s.ry <= s.RR.b) {
+            if (nc == g) { mx = s.rx; my = s.ry; mp = 0; md = 5; }
+            nc++;
+            s.rx += 5;
+            if (s.rx > s.RR.r) { s.rx = s.RR.l; s.ry += 5; }
+          }
+          break;
+        }
+        int x, y, pnr, pd;
+        bool m = false;
+        if (!next_candidate(s, ref.width, ref.height, e.cu_x, e.cu_y, x, y, pnr, pd, m, false)) break;
+        if (nc == g) { mx = x; my = y; mp = pnr; md = pd; }
+        nc++;
+        more = m;
+      }
+      if (nc == 0) break;   // wave-uniform: one job per wave
+      uint32_t part = 0;
+      if (g < nc && real) {
+        uint32_t w[UH][ND];
+        uint32_t s0;
+        load_window<UW, UH>(w, s0, ref, ox + mx, oy + my, sub);
+        part = unit_part<UW, UH>(w, s0, kk, sk2, kbuf, sad_metric, sub);
+      }
+      const uint32_t dg = group_sum(part, L);
+      uint64_t key = ~0ull;
+      if (g < nc) key = ((uint64_t)(dg + mv_cost(ml, mv_bits(mx, my, 2, j.mvp_x, j.mvp_y))) << 32) | (uint32_t)g;
+      for (int off = L; off < 64; off <<= 1) {
+        const uint64_t o = (uint64_t)__shfl_xor((unsigned long long)key, off, 64);
+        key = o < key ? o : key;
+      }
+      const uint32_t cost = (uint32_t)(key >> 32);
+      if (cost < s.best_sad) {
+        const int wl = (int)(uint32_t)key * L;
+        s.best_sad = cost;
+        s.bx = __shfl(mx, wl, 64);
+        s.by = __shfl(my, wl, 64);
+        s.bdist = __shfl(md, wl, 64);
+        s.pnr = __shfl(mp, wl, 64);
+        s.bround = 0;
+      }
+    }
+  } else
   for (int step = 0; step < (1 << 16); step++) {   // bound: a search tests < 2,000 points
     int cx[B], cy[B], cp[B], cd[B];
     int nc = 0;
@@ -584,8 +656,8 @@ __device__ __forceinline__ void tz_unit(const TzArgs& ta, int cls_off, int cls_c
       }
     }
   }
-  if (active && u == 0 && (!RASTER || ((int)threadIdx.x & 63) == 0)) {
-    if (!RASTER && s.phase == P_DEFER) {
+  if (active && u == 0 && (MODE == 0 || ((int)threadIdx.x & 63) == 0)) {
+    if (MODE == 0 && s.phase == P_DEFER) {
       uint32_t* rec = ta.rst + (size_t)jid * kTzRec;
       rec[0] = s.best_sad;
       rec[1] = (uint32_t)s.bx; rec[2] = (uint32_t)s.by; rec[3] = (uint32_t)s.pnr;
@@ -638,7 +710,7 @@ void k_tz(TzArgs ta, TzSchedule sc, int kid) {
   const int L = tz_group_lanes(PW, PH, UW, UH);
   const int gl = blk * kTzNT + (int)threadIdx.x;
   const int p = gl / L;
-  tz_unit<UW, UH, false>(ta, sc.class_off[c], sc.class_cnt[c], p, gl - p * L, L, PW, PH, 0);
+  tz_unit<UW, UH, 0>(ta, sc.class_off[c], sc.class_cnt[c], p, gl - p * L, L, PW, PH, 0);
 }
 
 // pass 2: one queued PU (job index) per wave
@@ -653,10 +725,42 @@ void k_tz_raster(TzArgs ta, TzSchedule sc, int kid, int nq) {
   const int jid = ta.rq[(size_t)kid * ta.a.n + wv];
   const int PW = ta.a.jobs[jid].w, PH = ta.a.jobs[jid].h;   // validated by k_classify
   const int L = tz_group_lanes(PW, PH, UW, UH);
-  tz_unit<UW, UH, true>(ta, 0, 1, 0, (int)(threadIdx.x & 63) & (L - 1), L, PW, PH, jid);
+  tz_unit<UW, UH, 1>(ta, 0, 1, 0, (int)(threadIdx.x & 63) & (L - 1), L, PW, PH, jid);
+}
+
+// One dependency level of a producer's m_integerMv2Nx2N chain (fme_pred_inter_p/b): one wave per
+// job in chain mode.  The host launches the levels back to back on one stream, so a level reads the
+// post-EMI MVs of earlier levels from global memory (kernel boundaries order them) and no level
+// waits for the host.  ch.psrc[q] >= 0: job q's m_integerMv2Nx2N is job psrc[q]'s result; -1: its
+// ext already holds it.
+__global__ __launch_bounds__(64) void k_tz_level(TzArgs ta, TzChain ch, int first) {
+  const int q = first + (int)blockIdx.x, lane = (int)threadIdx.x;
+  const int PW = ta.a.jobs[q].w, PH = ta.a.jobs[q].h;   // shapes checked by the host
+  const int ps = ch.psrc[q];
+  const int px = ps >= 0 ? ta.emi_mv[2 * ps] : ta.ext[q].pred2n_x;
+  const int py = ps >= 0 ? ta.emi_mv[2 * ps + 1] : ta.ext[q].pred2n_y;
+  const int kid = (PW % 8) ? 0 : ((PH % 8) ? 1 : 2);
+  if (kid == 0) {
+    const int L = tz_group_lanes(PW, PH, 4, 8);
+    tz_unit<4, 8, 2>(ta, 0, 1, 0, lane & (L - 1), L, PW, PH, q, px, py);
+  } else if (kid == 1) {
+    const int L = tz_group_lanes(PW, PH, 8, 4);
+    tz_unit<8, 4, 2>(ta, 0, 1, 0, lane & (L - 1), L, PW, PH, q, px, py);
+  } else {
+    const int L = tz_group_lanes(PW, PH, 8, 8);
+    tz_unit<8, 8, 2>(ta, 0, 1, 0, lane & (L - 1), L, PW, PH, q, px, py);
+  }
 }
 
 }  // namespace
+
+hipError_t launch_tz_levels(const TzArgs& ta, const TzChain& ch, const int32_t* h_lvl_off, hipStream_t s) {
+  for (int lv = 0; lv < ch.nlev; lv++) {
+    const int n = h_lvl_off[lv + 1] - h_lvl_off[lv];
+    if (n > 0) hipLaunchKernelGGL(k_tz_level, dim3(n), dim3(64), 0, s, ta, ch, h_lvl_off[lv]);
+  }
+  return hipGetLastError();
+}
 
 // Unit shape of a class for the integer search: 8 wide / tall where the PU allows, else 4.
 int tz_kernel_of(int cls) {

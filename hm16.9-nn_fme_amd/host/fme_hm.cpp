@@ -212,6 +212,27 @@ void InterSearchP::reset() {
   check(fme_pred_inter_reset(search_.ctx()), "fme_pred_inter_reset");
 }
 
+// ---- InterSearchB -------------------------------------------------------------------------
+
+int InterSearchB::add(const fme_pu_req_b& req) {
+  reqs_.push_back(req);
+  return (int)reqs_.size() - 1;
+}
+
+std::vector<fme_pu_res_b> InterSearchB::run() {
+  std::vector<fme_pu_res_b> res(reqs_.size());
+  std::lock_guard<std::mutex> lk(search_.mutex());
+  if (!reqs_.empty())
+    check(fme_pred_inter_b(search_.ctx(), reqs_.data(), res.data(), (int)reqs_.size(), nullptr), "fme_pred_inter_b");
+  reqs_.clear();
+  return res;
+}
+
+void InterSearchB::reset() {
+  std::lock_guard<std::mutex> lk(search_.mutex());
+  check(fme_pred_inter_reset(search_.ctx()), "fme_pred_inter_reset");
+}
+
 // ---- CtuRowBatcher -----------------------------------------------------------------------
 
 CtuRowBatcher::CtuRowBatcher(FracSearch& search, int maxRowsInFlight)

@@ -149,6 +149,23 @@ class InterSearchP {
   std::vector<fme_pu_req> reqs_;
 };
 
+// TEncSearch::predInterSearch for B slices (TEncSearch.cpp:3746-4105; FEN 1/2, MvdL1ZeroFlag
+// false): uni-pred over both lists, the one-iteration bi-pred search on the removeHighFreq key and
+// the uni / bi decision, one fme_pu_res_b per fme_pu_req_b.  A CU's second PU must be queued right
+// after its first (uiLastMode).  Same queue discipline as InterSearchP.
+class InterSearchB {
+ public:
+  explicit InterSearchB(FracSearch& search) : search_(search) {}
+  int add(const fme_pu_req_b& req);
+  int pending() const { return (int)reqs_.size(); }
+  std::vector<fme_pu_res_b> run();
+  void reset();                          // m_integerMv2Nx2N of both lists = (0, 0)
+
+ private:
+  FracSearch& search_;
+  std::vector<fme_pu_req_b> reqs_;
+};
+
 // Per-CTU-row batch producer (double-buffered: the caller fills row k+1 while row k runs).
 class CtuRowBatcher {
  public:

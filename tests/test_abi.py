@@ -92,7 +92,8 @@ def test_hm_adapter_library_exports():
     for sym in ("fme_hm::FracSearch::xPatternSearchFracDIF", "fme_hm::FracSearch::NN_pred",
                 "fme_hm::FracSearch::setPicture", "fme_hm::CtuRowBatcher::submit",
                 "fme_hm::CtuRowBatcher::wait", "fme_hm::CtuRowBatcher::addBiPred",
-                "fme_hm::loadWeights", "fme_hm::InterSearchP::run", "fme_hm::InterSearchP::reset"):
+                "fme_hm::loadWeights", "fme_hm::InterSearchP::run", "fme_hm::InterSearchP::reset",
+                "fme_hm::InterSearchB::run", "fme_hm::InterSearchB::reset"):
         assert sym in out, sym
     deps = subprocess.run(["ldd", so], capture_output=True, text=True).stdout
     assert "libfme_amd.so" in deps
