@@ -21,9 +21,9 @@ one host core (HM is single-threaded) over a bounded sample of the same job mix;
 `cpu_baseline_all_cores` runs one job stream per host core.  Both run
 before the GPU is initialised.
 
-`roofline` is for the main search phase (the lane-per-unit EMI + FracDIF kernels of the 18
-power-of-two PU shapes, ~99.4 % of the jobs, on three concurrent streams, k_search_lane88
-dominant), timed by HIP events recorded on the batch stream at the fork and after the join: the
+`roofline` is for the main search phase (k_search_lane: the lane-per-unit EMI + FracDIF kernel
+of every PU shape, one persistent launch per batch), timed by HIP events recorded on the batch
+stream around it: the
 path is integer-VALU bound, so `bound` is "valu" with the reference's integer ops (§8(d)) per
 second over the VALU peak; the HBM roof of the same phase is the `hbm` entry.
 """
@@ -256,6 +256,32 @@ def tz_cpu_rate(jobs, ext, keys, pics, seconds):
     return done / (time.perf_counter() - t0), done
 
 
+def tz_roofline(jobs, ext, pics, kernel_ms, sample=20000):
+    """Work of the frame's integer searches, from the oracle's counters on the first `sample` jobs
+    (HM order): points tested per search and distortion samples per point.  Each sample is three
+    reference integer ops (SSE: difference, square, accumulate; SAD: difference, absolute value,
+    accumulate).  The searches are bound by the latency of their dependent window loads (one per
+    tested point), not by ALU or HBM: the fractions say how far from either roof they sit."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    from oracle import Oracle
+    orc = Oracle(nn_mode=0, fast_inter_mode=1)
+    for k, v in pics.items():
+        orc.set_picture(k, v)
+    for lid, lam in enumerate(synth.LDP_LAMBDA[QP]):
+        orc.set_lambda(lid, lam)
+    m = min(sample, len(jobs))
+    orc.tz_counters(reset=True)
+    orc.integer_search(jobs[:m], ext[:m])
+    points, samples = orc.tz_counters(reset=True)
+    n = len(jobs)
+    ops = 3.0 * samples / m * n
+    achieved = ops / (kernel_ms * 1e-3) / 1e12
+    return {"bound": "latency (dependent window loads)", "achieved": achieved, "peak": VALU_PEAK_TOPS,
+            "unit": "Tops/s (int32 VALU lane-ops)", "frac": achieved / VALU_PEAK_TOPS,
+            "points_per_search": points / m, "samples_per_point": samples / points,
+            "reference_ops_per_frame": ops, "sample": f"oracle counters over the first {m} searches"}
+
+
 def tz_leg(dev, stream, reps, cpu_seconds):
     """Integer motion estimation (xTZSearch / bi-pred xPatternSearch) of one 1080p frame's jobs:
     510 CTUs x 423 calls x 4 refs in HM order, HBM-resident jobs, HIP events around the launches."""
@@ -299,6 +325,7 @@ def tz_leg(dev, stream, reps, cpu_seconds):
     t = float(np.median(ms))
     out.update({"kernel_ms": t, "pu_per_s_kernels": len(jobs) / (t / 1e3), "ms_per_frame": wall * 1e3,
                 "pu_per_s": len(jobs) / wall, "kernels": "fme::k_tz<4,8>, <8,4>, <8,8> + deferred raster pass k_tz_raster<...> (+ classify, scatter)"})
+    out["roofline"] = tz_roofline(jobs, ext, pics, t)
     if "cpu_baseline" in out:
         out["speedup_vs_cpu_1core"] = out["pu_per_s"] / out["cpu_baseline"]["value"]
     ctx.close()
@@ -350,16 +377,50 @@ def pred_inter_leg(dev, reps, cpu_seconds):
     t = float(np.median(ts))
     out.update({"ms_per_frame": t * 1e3, "requests_per_s": len(reqs) / t, "jobs_per_s": nj / t,
                 "note": "bounded by the reference's m_integerMv2Nx2N chain: the bottom CTU row (56 rows) has no "
-                        "depth-0 CU, so its 30 CTUs form one sequential chain of 2Nx2N searches (DESIGN.md section 4)"})
+                        "depth-0 CU, so its 30 CTUs form one sequential chain of ~2,200 levels of 2Nx2N searches, "
+                        "one k_tz_level launch each (DESIGN.md section 4)"})
     if "cpu_baseline" in out:
         out["speedup_vs_cpu_1core"] = out["requests_per_s"] / out["cpu_baseline"]["value"]
+    # the B-slice producer on the same frame: L0 = {t-1, t-2}, L1 = {t+1, t+2} (fme_pred_inter_b)
+    pics[5] = synth.synth_luma(W, H, 3)
+    ctx.set_picture(5, pics[5])
+    reqs_b = synth.make_pu_requests_b(np.random.default_rng(3), W, H, org_id=4, l0=[(0, 1), (1, 2)],
+                                      l1=[(5, -1), (2, -2)], lambda_id=0, max_depth=3)
+    b = {"workload": f"{W}x{H} B frame: {len(reqs_b)} PU requests, 2 + 2 references, uni-pred over both lists, "
+                     f"one bi-pred iteration (FEN 1) on device-built removeHighFreq keys, NN on"}
+    if cpu_seconds > 0:
+        orc.set_picture(5, pics[5])
+        orc.pred_inter_reset()
+        done, t0 = 0, time.perf_counter()
+        while time.perf_counter() - t0 < cpu_seconds and done < len(reqs_b):
+            e = min(done + 1000, len(reqs_b))
+            while e < len(reqs_b) and reqs_b["part_idx"][e] != 0:   # a CU's PUs stay in one call
+                e += 1
+            orc.pred_inter_b(reqs_b[done:e])
+            done = e
+        b["cpu_baseline"] = {"value": done / (time.perf_counter() - t0), "unit": "PU requests/s", "cores": 1,
+                             "kind": "port", "sample": f"first {done} requests, sequential (orc_pred_inter_b)"}
+    ctx.pred_inter_b(reqs_b[:2000])
+    ts = []
+    for _ in range(reps):
+        ctx.pred_inter_reset()
+        t0 = time.perf_counter()
+        res_b = ctx.pred_inter_b(reqs_b)
+        ts.append(time.perf_counter() - t0)
+    tb = float(np.median(ts))
+    b.update({"ms_per_frame": tb * 1e3, "requests_per_s": len(reqs_b) / tb,
+              "inter_dir_counts": {"L0": int((res_b["inter_dir"] == 1).sum()), "L1": int((res_b["inter_dir"] == 2).sum()),
+                                   "bi": int((res_b["inter_dir"] == 3).sum())}})
+    if "cpu_baseline" in b:
+        b["speedup_vs_cpu_1core"] = b["requests_per_s"] / b["cpu_baseline"]["value"]
+    out["b_slice"] = b
     ctx.close()
     return out
 
 
 def read_pmc_traffic(workload):
     """HBM bytes per main search launch from the committed rocprofv3 PMC summary of this workload
-    (profiles/pmc_traffic.json, regenerated by tools/gpu_check.sh from the current tree)."""
+    (profiles/pmc_traffic.json, regenerated by tools/gpu_profile.sh from the current tree)."""
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     if workload != "c3_qp22" or not os.path.exists(path):
         return None, None
@@ -591,8 +652,8 @@ def main():
                 "unit": "Tops/s (int32 VALU lane-ops)",
                 "frac": valu / VALU_PEAK_TOPS,
                 "traffic": traffic,
-                "kernel": "main search phase: fme::k_search_lane{48,84,88} (EMI + FracDIF) on three "
-                          "concurrent streams, fork to join; k_search_lane88 dominant",
+                "kernel": "main search phase: fme::k_search_lane (EMI + FracDIF, every PU shape, one "
+                          "persistent launch per batch)",
                 "kernel_jobs": int(len(small_jobs)),
                 "algorithmic_ops_per_launch": ops_small,
                 "algorithmic_bytes_per_launch": bytes_small,

@@ -34,14 +34,16 @@
 #define FME_XCD_SWIZZLE 1
 #endif
 // Candidates per quarter pass (2: column-phase pairs, 1: one candidate per pass — fewer live
-// registers, the first-stage column recomputed per candidate)
+// registers, the first-stage column recomputed per candidate) and half-stage vertical pairs
+// {(0,-1),(0,1)} and {(s,-1),(s,1)} in one pass (2) or one candidate per pass (1).  A/B on the
+// 1080p batch (tools/ab_bench.py, one kernel for every class): 1/1 1.185 ms, QPAIR 2 1.146,
+// HPAIR 2 1.091, both 2 1.054 — the shared first stages save more issue slots than the extra
+// live key - pred array costs at 2 waves/SIMD (FME_LANE_WAVES 3 spills: 1.480 ms).
 #ifndef FME_LANE_QPAIR
-#define FME_LANE_QPAIR 1
+#define FME_LANE_QPAIR 2
 #endif
-// Half-stage vertical pairs {(0,-1),(0,1)} and {(s,-1),(s,1)} in one pass (2) or one
-// candidate per pass (1)
 #ifndef FME_LANE_HPAIR
-#define FME_LANE_HPAIR 1
+#define FME_LANE_HPAIR 2
 #endif
 // occupancy target (waves per SIMD) that bounds the register allocation
 #ifndef FME_LANE_WAVES

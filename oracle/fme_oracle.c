@@ -763,8 +763,23 @@ typedef struct tz_state {
   int best_x, best_y, best_dist, best_round, point_nr;
 } tz_state;
 
+/* Work counters of the integer searches (bench.py's k_tz roofline): points tested and the samples
+ * their distortions read (FEN-subsampled rows counted once). */
+static uint64_t g_tz_points, g_tz_samples;
+void orc_tz_counters(uint64_t out[2], int reset) {
+  out[0] = g_tz_points;
+  out[1] = g_tz_samples;
+  if (reset) g_tz_points = g_tz_samples = 0;
+}
+static void tz_count(int w, int h, int fen) {
+  const int sub = (w == 12 || w == 24 || w == 48) && (fen == 1 || fen == 3) && h > 8;
+  g_tz_points++;
+  g_tz_samples += (uint64_t)w * (uint64_t)(sub ? h / 2 : h);
+}
+
 /* xTZSearchHelp normal branch (TEncSearch.cpp:1155-1188, save = false). */
 static void tz_help(tz_state* s, int x, int y, int point_nr, int dist) {
+  tz_count(s->w, s->h, s->fen);
   orc_pred_block(s->ref, s->x0, s->y0, s->w, s->h, 4 * x, 4 * y, s->cur);
   uint32_t d = int_dist(s->key, s->w, s->cur, s->w, s->w, s->h, s->fen);
   if (d < s->best_sad) {
@@ -986,6 +1001,7 @@ int orc_integer_search(orc_ctx* ctx, fme_job* jobs, const fme_tz_ext* ext, uint3
       s.best_sad = 0xFFFFFFFFu;
       for (int y = j->lt_y; y <= j->rb_y; y++)
         for (int x = j->lt_x; x <= j->rb_x; x++) {
+          tz_count(w, h, s.fen);
           orc_pred_block(ref, j->x, j->y, w, h, 4 * x, 4 * y, cur);
           const uint32_t d = int_dist(key, w, cur, w, w, h, s.fen) + orc_cost(s.ml, mv_bits(x, y, 2, s.mvp_x, s.mvp_y));
           if (d < s.best_sad) { s.best_sad = d; s.best_x = x; s.best_y = y; }

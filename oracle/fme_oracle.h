@@ -122,6 +122,8 @@ int orc_refine(orc_ctx* ctx, const fme_job* jobs, fme_result* res, int n);
 /* ---- integer motion estimation: xTZSearch / xPatternSearch per job;
  * writes jobs[i].mv_x/mv_y and sad[i].  Returns 0 or a negative FME_E_* code. */
 int orc_integer_search(orc_ctx* ctx, fme_job* jobs, const fme_tz_ext* ext, uint32_t* sad, int n);
+/* points tested / distortion samples read by the integer searches since the last reset */
+void orc_tz_counters(uint64_t out[2], int reset);
 
 /* ---- motion compensation ------------------------------------ */
 typedef struct orc_yuv {

@@ -69,6 +69,7 @@ class Oracle:
         lib.orc_pred_inter_reset.argtypes = [_P]
         lib.orc_template_cost.restype = C.c_uint32
         lib.orc_template_cost.argtypes = [_P, _P, C.c_int, C.c_int]
+        lib.orc_tz_counters.argtypes = [_P, C.c_int]
         lib.orc_pred_inter_b.restype = C.c_int
         lib.orc_pred_inter_b.argtypes = [_P, _P, _P, C.c_int]
         lib.orc_bi_key.argtypes = [_P] + [C.c_int] * 11 + [_P]
@@ -171,6 +172,12 @@ class Oracle:
 
     def pred_inter_reset(self):
         self.lib.orc_pred_inter_reset(self.ctx)
+
+    def tz_counters(self, reset=True):
+        """(points tested, distortion samples read) by the integer searches since the last reset."""
+        out = np.zeros(2, np.uint64)
+        self.lib.orc_tz_counters(_ptr(out), int(bool(reset)))
+        return int(out[0]), int(out[1])
 
     def pred_inter_b(self, reqs):
         """orc_pred_inter_b: predInterSearch on a B slice, one fme_pu_res_b per request."""
