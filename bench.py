@@ -194,6 +194,42 @@ def mc_algorithmic_bytes(jobs):
     return int((lists * ref + (3 * w * h) // 2 + 24).sum())
 
 
+def drop_in_leg(dev, calls=300):
+    """The TEncSearch-shaped single-PU entry points, one call per PU as a live encoder would make
+    them (fme_frac_dif_single: host key / window in, half / quarter / cost out, synchronous;
+    fme_nn_pred_single): wall microseconds per call.  Latency-bound by construction (one launch
+    and one host round trip per call); the batch path is the throughput path."""
+    from nnfme.runtime import FmeContext
+    rng = np.random.default_rng(5)
+    pic = synth.synth_luma(W, H, 1).astype(np.int16)
+    org = synth.synth_luma(W, H, 0).astype(np.int16)
+    pad = 80
+    plane = np.pad(pic, pad, mode="edge")
+    ctx = FmeContext(device=dev.index, nn_mode=1, qp=QP, fast_inter_mode=1)
+    ml = 65536.0 * np.sqrt(synth.LDP_LAMBDA[QP][0])
+    out = {}
+    for (w, h) in ((8, 8), (16, 16), (64, 64)):
+        ts = []
+        for i in range(calls // 3):
+            x = 4 * int(rng.integers(0, (W - w) // 4)) if i else 0
+            y = 4 * int(rng.integers(0, (H - h) // 4)) if i else 0
+            mv = (int(rng.integers(-8, 9)), int(rng.integers(-8, 9)))
+            t0 = time.perf_counter()
+            ctx.frac_dif_single(org[y:y + h, x:x + w], plane, (y + pad, x + pad), mv, (0, 0), ml)
+            ts.append(time.perf_counter() - t0)
+        out[f"frac_dif_{w}x{h}_us"] = float(np.median(ts[1:]) * 1e6)
+    ts = []
+    for i in range(calls):
+        e = rng.integers(0, 5000, 8).astype(np.uint32)
+        t0 = time.perf_counter()
+        ctx.nn_pred_single(e, int(rng.integers(0, 5000)), 8, 8)
+        ts.append(time.perf_counter() - t0)
+    out["nn_pred_us"] = float(np.median(ts[1:]) * 1e6)
+    out["note"] = "median wall time per synchronous call, Python ctypes caller included"
+    ctx.close()
+    return out
+
+
 def mc_leg(dev, stream, reps):
     """Motion compensation of one 1080p frame's decided PUs (TComPrediction::motionCompensation:
     luma 8-tap + 4:2:0 chroma 4-tap), device-resident jobs / pictures / planes; HIP events around
@@ -494,10 +530,11 @@ def main():
     # ---- inputs (untimed): one frame's jobs in HM order -----------------------------------------
     jobs = make_frame_jobs(1000, args.jobs, CALLS, BIPRED)
     n1 = len(jobs)
-    keys = None
-    if BIPRED > 0:   # bi-pred key blocks (2*org - pred_other), resident with the jobs
+    keys = key_reqs = None
+    if BIPRED > 0:   # bi-pred keys (removeHighFreq of the other list's prediction), resident with the jobs
         kpics = {k: synth.synth_luma(W, H, t) for k, t in zip(range(5), (7, 6, 5, 4, 0))}
-        keys = synth.make_bipred_keys_fast(np.random.default_rng(77), jobs, kpics)
+        key_reqs, key_count = synth.make_bipred_key_reqs(np.random.default_rng(77), jobs, 4, [0, 1, 2, 3])
+        keys = synth.bipred_keys(key_reqs, kpics, key_count)   # the CPU baseline's copy (same values)
 
     # ---- CPU baselines first, before anything touches the GPU (fork-safe) -------------------
     cpu = {}
@@ -544,8 +581,10 @@ def main():
     net = weights.case_net(wl["net"]) if NN == 2 else None
     ctx = FmeContext(device=dev_index, use_hadamard=1, nn_mode=NN, qp=QP, fast_inter_mode=1,
                      max_jobs=n1 * FPS, net=net, nn_engine=wl.get("engine", 0))
-    if keys is not None:
-        ctx.set_keys(keys)
+    if key_reqs is not None:   # built on the device (fme_build_bipred_keys, k_bi_key)
+        for k, v in kpics.items():
+            ctx.set_picture(k, v)
+        ctx.build_bipred_keys(key_reqs, len(keys))
 
     # synthetic frame pool (the trace's originals / reconstructions): frame g -> pool[g % 8]
     pool = np.stack([synth.synth_luma(W, H, t) for t in range(8)])
@@ -604,6 +643,7 @@ def main():
 
     mc = mc_leg(dev, torch.cuda.current_stream(dev), reps=max(5, args.steps // 2)) \
         if rank == 0 and not args.no_mc and W == 1920 and NN != 2 else None
+    single = drop_in_leg(dev) if rank == 0 and not args.no_mc and W == 1920 and NN == 1 else None
     pi = None
     if rank == 0 and not args.no_pi and W == 1920 and world == 1 and NN == 1:
         pi = pred_inter_leg(dev, reps=2, cpu_seconds=0.0 if args.no_cpu_baseline else 4.0)
@@ -681,6 +721,8 @@ def main():
             out["nn_state_fixup_jobs_rank0"] = int(fixed)
         if mc:
             out["motion_compensation"] = mc
+        if single:
+            out["drop_in_single_pu"] = single
         if tz:
             out["integer_search"] = tz
         if pi:

@@ -1321,6 +1321,35 @@ int fme_template_costs(fme_ctx* c, const fme_pu_req* reqs, uint32_t* costs, int 
   return FME_OK;
 }
 
+int fme_build_bipred_keys(fme_ctx* c, const fme_bikey_req* reqs, int n, size_t key_count, void* stream) {
+  static_assert(sizeof(fme_bikey_req) == sizeof(BiKeyTask), "fme_bikey_req is the kernel's task record");
+  if (!c || (n > 0 && !reqs)) return fail(FME_E_INVALID, "fme_build_bipred_keys: null argument");
+  if (n < 0) return fail(FME_E_INVALID, "fme_build_bipred_keys: n = %d", n);
+  HIP_TRY(hipSetDevice(c->device));
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  for (int i = 0; i < n; i++) {
+    const fme_bikey_req& q = reqs[i];
+    const PicDesc& org = c->pics[q.org_id < FME_MAX_PICTURES ? q.org_id : 0];
+    const PicDesc& ref = c->pics[q.ref_id < FME_MAX_PICTURES ? q.ref_id : 0];
+    if (!valid_pu_shape(q.w, q.h) || q.org_id >= FME_MAX_PICTURES || q.ref_id >= FME_MAX_PICTURES || !org.luma ||
+        !ref.luma || ref.width != org.width || ref.height != org.height || q.x + q.w > org.width ||
+        q.y + q.h > org.height || q.key_offset < 0 || (q.key_offset & 3) ||
+        (size_t)q.key_offset + (size_t)q.w * q.h > key_count || (q.flags & ~FME_PU_CLIP_BIPRED))
+      return fail(FME_E_INVALID, "fme_build_bipred_keys: request %d invalid", i);
+  }
+  int rc = sync_tables(c, s);
+  if (rc) return rc;
+  HIP_TRY(c->d_keys.reserve(key_count));
+  c->n_keys = key_count;
+  if (n == 0) return FME_OK;
+  HIP_TRY(c->d_bikey.reserve((size_t)n));
+  HIP_TRY(hipMemcpyAsync(c->d_bikey.p, reqs, (size_t)n * sizeof(BiKeyTask), hipMemcpyHostToDevice, s));
+  BiKeyArgs ka{c->d_bikey.p, c->d_pics.p, c->d_keys.p, (int32_t)n};
+  HIP_TRY(launch_bi_key(ka, s));
+  HIP_TRY(hipStreamSynchronize(s));
+  return FME_OK;
+}
+
 int fme_pred_inter_reset(fme_ctx* c) {
   if (!c) return fail(FME_E_INVALID, "fme_pred_inter_reset: null ctx");
   std::memset(c->int_mv_2n, 0, sizeof(c->int_mv_2n));

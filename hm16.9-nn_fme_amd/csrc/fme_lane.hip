@@ -35,15 +35,19 @@
 #endif
 // Candidates per quarter pass (2: column-phase pairs, 1: one candidate per pass — fewer live
 // registers, the first-stage column recomputed per candidate) and half-stage vertical pairs
-// {(0,-1),(0,1)} and {(s,-1),(s,1)} in one pass (2) or one candidate per pass (1).  A/B on the
-// 1080p batch (tools/ab_bench.py, one kernel for every class): 1/1 1.185 ms, QPAIR 2 1.146,
-// HPAIR 2 1.091, both 2 1.054 — the shared first stages save more issue slots than the extra
-// live key - pred array costs at 2 waves/SIMD (FME_LANE_WAVES 3 spills: 1.480 ms).
+// {(0,-1),(0,1)} and {(s,-1),(s,1)} in one pass (2) or one candidate per pass (1); the 8x4 unit
+// shape always uses 1 (lane_unit).  A/B on the 1080p batch (tools/ab_bench.py, one kernel for
+// every class, all shapes alike): 1/1 1.185 ms, QPAIR 2 1.146, HPAIR 2 1.091, both 2 1.054 — the
+// shared first stages save more issue slots than the extra live key - pred array costs at
+// 2 waves/SIMD (FME_LANE_WAVES 3 spills: 1.480 ms).
 #ifndef FME_LANE_QPAIR
 #define FME_LANE_QPAIR 2
 #endif
 #ifndef FME_LANE_HPAIR
 #define FME_LANE_HPAIR 2
+#endif
+#ifndef FME_LANE_PAIR84   // 1: the 8x4 unit shape paired too
+#define FME_LANE_PAIR84 0
 #endif
 // occupancy target (waves per SIMD) that bounds the register allocation
 #ifndef FME_LANE_WAVES
@@ -219,7 +223,7 @@ __device__ __forceinline__ void take_qtr(int i, uint32_t part, uint32_t live, do
 }
 
 // (0,0), (0,-1), (0,1)
-template <int UW, int UH, int T>
+template <int UW, int UH, int T, int HPM>
 __device__ __forceinline__ void half_center(uint32_t (&v)[UH + 8][UW / 4 + 2], const KeySrc<UW, UH / 2>& K,
                                             bool had, uint32_t (&d)[3]) {
   constexpr int RV = UH + 8, UJ = UH / 2;
@@ -270,17 +274,17 @@ __device__ __forceinline__ void half_center(uint32_t (&v)[UH + 8][UW / 4 + 2], c
     if (sel & 1) d[1] = unit_dist<UW, UH, T>(X1, had);
     if (sel & 2) d[2] = unit_dist<UW, UH, T>(X2, had);
   };
-#if FME_LANE_HPAIR == 2
-  vpass(std::integral_constant<int, 3>{});
-#else
-  vpass(std::integral_constant<int, 1>{});
-  launder(v);
-  vpass(std::integral_constant<int, 2>{});
-#endif
+  if constexpr (HPM == 2) {
+    vpass(std::integral_constant<int, 3>{});
+  } else {
+    vpass(std::integral_constant<int, 1>{});
+    launder(v);
+    vpass(std::integral_constant<int, 2>{});
+  }
 }
 
 // (s,0), (s,-1), (s,1) for s = -1 (SIDE 0: half column x) or +1 (SIDE 1: half column x+1)
-template <int UW, int UH, int T, int SIDE>
+template <int UW, int UH, int T, int SIDE, int HPM>
 __device__ __forceinline__ void half_side(uint32_t (&v)[UH + 8][UW / 4 + 2], const KeySrc<UW, UH / 2>& K,
                                           bool had, uint32_t (&d)[3]) {
   constexpr int RV = UH + 8, UJ = UH / 2;
@@ -342,39 +346,44 @@ __device__ __forceinline__ void half_side(uint32_t (&v)[UH + 8][UW / 4 + 2], con
     if (sel & 1) d[1] = unit_dist<UW, UH, T>(XB, had);
     if (sel & 2) d[2] = unit_dist<UW, UH, T>(XC, had);
   };
-#if FME_LANE_HPAIR == 2
-  dpass(std::integral_constant<int, 3>{});
-#else
-  dpass(std::integral_constant<int, 1>{});
-  dpass(std::integral_constant<int, 2>{});
-#endif
+  if constexpr (HPM == 2) {
+    dpass(std::integral_constant<int, 3>{});
+  } else {
+    dpass(std::integral_constant<int, 1>{});
+    dpass(std::integral_constant<int, 2>{});
+  }
 }
 
 // Quarter passes: pass PS covers column phase k = QP_K[PS] (dqx = k-1) and one or two row
 // phases l (dqy = l-1); candidate (k1, l1) is the half best.  A phase with fraction 0 filters
 // with {0,0,0,64,0,0,0,0}, which equals HM's copy / 1-D paths after rounding.
-#if FME_LANE_QPAIR == 2
-constexpr int kQPasses = 5;
-__host__ __device__ constexpr int qp_k(int ps) { return ps < 2 ? 0 : (ps == 2 ? 1 : 2); }
-__host__ __device__ constexpr int qp_l0(int ps) { return (ps == 1 || ps == 4) ? 2 : 0; }
-__host__ __device__ constexpr int qp_l1(int ps) { return ps == 0 ? 1 : (ps == 2 ? 2 : (ps == 3 ? 1 : -1)); }
-#else
-constexpr int kQPasses = 8;   // (k,l) for k, l in 0..2 without (1,1)
-__host__ __device__ constexpr int qp_k(int ps) { return (ps + (ps >= 4 ? 1 : 0)) / 3; }
-__host__ __device__ constexpr int qp_l0(int ps) { return (ps + (ps >= 4 ? 1 : 0)) % 3; }
-__host__ __device__ constexpr int qp_l1(int ps) { return -1; }
-#endif
+// QM 2: five passes, (k, l) = (0: 0,1) (0: 2) (1: 0,2) (2: 0,1) (2: 2); QM 1: eight, (k, l) for
+// k, l in 0..2 without (1,1).
+template <int QM> __host__ __device__ constexpr int qp_passes() { return QM == 2 ? 5 : 8; }
+template <int QM> __host__ __device__ constexpr int qp_k(int ps) {
+  return QM == 2 ? (ps < 2 ? 0 : (ps == 2 ? 1 : 2)) : (ps + (ps >= 4 ? 1 : 0)) / 3;
+}
+template <int QM> __host__ __device__ constexpr int qp_l0(int ps) {
+  return QM == 2 ? ((ps == 1 || ps == 4) ? 2 : 0) : (ps + (ps >= 4 ? 1 : 0)) % 3;
+}
+template <int QM> __host__ __device__ constexpr int qp_l1(int ps) {
+  return QM == 2 ? (ps == 0 ? 1 : (ps == 2 ? 2 : (ps == 3 ? 1 : -1))) : -1;
+}
 // Q9 index of pass ps's first / second candidate
-__host__ __device__ constexpr int qp_idx0(int ps) { return q9_index(qp_k(ps) - 1, qp_l0(ps) - 1); }
-__host__ __device__ constexpr int qp_idx1(int ps) { return qp_l1(ps) < 0 ? -1 : q9_index(qp_k(ps) - 1, qp_l1(ps) - 1); }
+template <int QM> __host__ __device__ constexpr int qp_idx0(int ps) {
+  return q9_index(qp_k<QM>(ps) - 1, qp_l0<QM>(ps) - 1);
+}
+template <int QM> __host__ __device__ constexpr int qp_idx1(int ps) {
+  return qp_l1<QM>(ps) < 0 ? -1 : q9_index(qp_k<QM>(ps) - 1, qp_l1<QM>(ps) - 1);
+}
 
-template <int UW, int UH, int T, int PS>
+template <int UW, int UH, int T, int QM, int PS>
 __device__ __forceinline__ void qtr_pass(uint32_t (&v)[UH + 8][UW / 4 + 2], const KeySrc<UW, UH / 2>& K,
                                          bool had, int hx, int hy, uint32_t (&d)[2]) {
   constexpr int RV = UH + 8, UJ = UH / 2;
-  constexpr int k = qp_k(PS);
-  constexpr int NP = qp_l1(PS) < 0 ? 1 : 2;
-  const int LS[2] = {qp_l0(PS), qp_l1(PS) < 0 ? 0 : qp_l1(PS)};
+  constexpr int k = qp_k<QM>(PS);
+  constexpr int NP = qp_l1<QM>(PS) < 0 ? 1 : 2;
+  const int LS[2] = {qp_l0<QM>(PS), qp_l1<QM>(PS) < 0 ? 0 : qp_l1<QM>(PS)};
   const int qx = 2 * hx + (k - 1);
   const int ix = qx >> 2, fx = qx & 3;
   const uint32_t dlt = (uint32_t)(1 + ix);
@@ -419,16 +428,16 @@ __device__ __forceinline__ void qtr_pass(uint32_t (&v)[UH + 8][UW / 4 + 2], cons
   d[1] = NP > 1 ? unit_dist<UW, UH, T>(XQ[NP - 1], had) : 0u;
 }
 
-template <int L, int UW, int UH, int T, int... PS>
+template <int L, int UW, int UH, int T, int QM, int... PS>
 __device__ __forceinline__ void qtr_all(uint32_t (&v)[UH + 8][UW / 4 + 2], const KeySrc<UW, UH / 2>& K,
                                         bool had, uint32_t live, int hx, int hy, double ml, int mvx, int mvy, int px,
                                         int py, uint32_t& best, int& bi, std::integer_sequence<int, PS...>) {
   auto one = [&](auto ps_c) {
     constexpr int ps = decltype(ps_c)::value;
     uint32_t d[2];
-    qtr_pass<UW, UH, T, ps>(v, K, had, hx, hy, d);
-    take_qtr<L>(qp_idx0(ps), d[0], live, ml, mvx, mvy, hx, hy, px, py, best, bi);
-    if constexpr (qp_l1(ps) >= 0) take_qtr<L>(qp_idx1(ps), d[1], live, ml, mvx, mvy, hx, hy, px, py, best, bi);
+    qtr_pass<UW, UH, T, QM, ps>(v, K, had, hx, hy, d);
+    take_qtr<L>(qp_idx0<QM>(ps), d[0], live, ml, mvx, mvy, hx, hy, px, py, best, bi);
+    if constexpr (qp_l1<QM>(ps) >= 0) take_qtr<L>(qp_idx1<QM>(ps), d[1], live, ml, mvx, mvy, hx, hy, px, py, best, bi);
   };
   (one(std::integral_constant<int, PS>{}), ...);
 }
@@ -476,6 +485,9 @@ __device__ __forceinline__ void lane_unit(const BatchArgs& a, const fme_job* __r
                                           const int32_t* __restrict__ perm, int cls_off, int cls_cnt,
                                           int wt) {
   constexpr int T = ((PW % 8) == 0 && (PH % 8) == 0) ? 8 : 4;
+  // pair modes per unit shape: the 8x4 units spill with paired passes (144 B/lane), the others not
+  constexpr bool k84 = UH == 4 && !FME_LANE_PAIR84;
+  constexpr int kQP = k84 ? 1 : FME_LANE_QPAIR, kHP = k84 ? 1 : FME_LANE_HPAIR;
   static_assert(UW % T == 0 && UH % T == 0, "unit must hold whole SATD tiles");
   static_assert(PW % UW == 0 && PH % UH == 0, "units tile the PU");
   constexpr int UX = PW / UW, LR = UX * (PH / UH);   // units of the PU
@@ -741,18 +753,18 @@ __device__ __forceinline__ void lane_unit(const BatchArgs& a, const fme_job* __r
   int hbi = 9;
   {
     uint32_t d[3] = {0u, 0u, 0u};
-    half_center<UW, UH, T>(v, K, had, d);
+    half_center<UW, UH, T, kHP>(v, K, had, d);
     take_half<L>(0, d[0], live, ml, mvx, mvy, mvp_x, mvp_y, hbest, hbi);
     take_half<L>(1, d[1], live, ml, mvx, mvy, mvp_x, mvp_y, hbest, hbi);
     take_half<L>(2, d[2], live, ml, mvx, mvy, mvp_x, mvp_y, hbest, hbi);
   }
   {
     uint32_t d[3];
-    half_side<UW, UH, T, 0>(v, K, had, d);
+    half_side<UW, UH, T, 0, kHP>(v, K, had, d);
     take_half<L>(3, d[0], live, ml, mvx, mvy, mvp_x, mvp_y, hbest, hbi);
     take_half<L>(5, d[1], live, ml, mvx, mvy, mvp_x, mvp_y, hbest, hbi);
     take_half<L>(7, d[2], live, ml, mvx, mvy, mvp_x, mvp_y, hbest, hbi);
-    half_side<UW, UH, T, 1>(v, K, had, d);
+    half_side<UW, UH, T, 1, kHP>(v, K, had, d);
     take_half<L>(4, d[0], live, ml, mvx, mvy, mvp_x, mvp_y, hbest, hbi);
     take_half<L>(6, d[1], live, ml, mvx, mvy, mvp_x, mvp_y, hbest, hbi);
     take_half<L>(8, d[2], live, ml, mvx, mvy, mvp_x, mvp_y, hbest, hbi);
@@ -762,8 +774,8 @@ __device__ __forceinline__ void lane_unit(const BatchArgs& a, const fme_job* __r
   // ---- 4. quarter-pel stage: passes over column phases (Q9 candidate 0 = the half best) -------
   uint32_t qbest = hbest;
   int qbi = 0;
-  qtr_all<L, UW, UH, T>(v, K, had, live, hx, hy, ml, mvx, mvy, mvp_x, mvp_y, qbest, qbi,
-                        std::make_integer_sequence<int, kQPasses>{});
+  qtr_all<L, UW, UH, T, kQP>(v, K, had, live, hx, hy, ml, mvx, mvy, mvp_x, mvp_y, qbest, qbi,
+                             std::make_integer_sequence<int, qp_passes<kQP>()>{});
   const int bq = qbi;
 
   // ---- results: bytes 0..15 (mv_int, mv (NN tail), half, qtr, frac_cost) ------------------------

@@ -28,10 +28,6 @@ namespace {
 
 using namespace simd;
 
-#ifndef FME_MC_PROBE
-#define FME_MC_PROBE 0
-#endif
-
 
 // TComInterpolationFilter.cpp:57-75 as int8 quads (luma: taps 0-3, 4-7; chroma: taps 0-3).
 // Fraction 0 uses the identity filter (64 at the centre tap): through the two-stage form below
@@ -123,13 +119,7 @@ struct UnitWin {
   uint32_t w[R][ND];
   uint32_t s0;
   __device__ __forceinline__ void load(const Plane& pl, bool aligned, int bx, int by) {
-#if FME_MC_PROBE == 1   // timing probe only: no reference reads
-    for (int r = 0; r < R; r++)
-      for (int k = 0; k < ND; k++) w[r][k] = (uint32_t)(bx * 7 + by * 13 + r + k);
-    s0 = (uint32_t)bx & 3;
-#else
     s0 = load_window<R, ND>(pl, bx - (N / 2 - 1), by - (N / 2 - 1), aligned, w);
-#endif
   }
   // Two stages in the (s - 128) domain, which absorbs filterCopy / filter<N, ., isFirst = true,
   // .>'s -IF_INTERNAL_OFFS: stage 1 = sum c.s - 8192; stage 2 uni (isLast): (sum + 2048 +

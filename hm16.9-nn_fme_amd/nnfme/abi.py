@@ -129,6 +129,16 @@ PU_RES_B_DTYPE = np.dtype(
     align=False,
 )
 assert PU_RES_B_DTYPE.itemsize == 160
+# fme_bikey_req (include/fme.h)
+BIKEY_REQ_DTYPE = np.dtype(
+    [
+        ("x", "<u2"), ("y", "<u2"), ("w", "u1"), ("h", "u1"), ("org_id", "u1"), ("ref_id", "u1"),
+        ("cu_x", "<u2"), ("cu_y", "<u2"), ("mv_x", "<i2"), ("mv_y", "<i2"),
+        ("key_offset", "<i4"), ("flags", "<u4"),
+    ],
+    align=False,
+)
+assert BIKEY_REQ_DTYPE.itemsize == 24
 PART_2Nx2N, PART_2NxN, PART_Nx2N, PART_NxN, PART_2NxnU, PART_2NxnD, PART_nLx2N, PART_nRx2N = range(8)
 
 MC_L0 = 0x01

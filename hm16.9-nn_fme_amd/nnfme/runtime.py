@@ -15,7 +15,7 @@ from .weights import load_weights
 PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB_PATH = os.environ.get("FME_LIB_PATH") or os.path.join(PKG_ROOT, "libfme_amd.so")
 
-ABI_VERSION = 6
+ABI_VERSION = 7
 TIMING_NAMES = ("classify", "scatter", "search", "nn_tail", "batch", "search_main", "search_aux")
 
 # Every entry point include/fme.h declares (the ABI test checks the .so exports them).
@@ -30,7 +30,7 @@ ABI_SYMBOLS = (
     "fme_integer_search", "fme_integer_search_device", "fme_integer_search_last_ms",
     "fme_pred_inter_p", "fme_pred_inter_reset", "fme_nn_param_count", "fme_load_nn_net",
     "fme_set_nn_engine", "fme_set_nn_margin_output", "fme_refine_mv", "fme_refine_mv_device",
-    "fme_refine_status", "fme_nn_copy_state_device", "fme_template_costs", "fme_pred_inter_b",
+    "fme_refine_status", "fme_nn_copy_state_device", "fme_template_costs", "fme_pred_inter_b", "fme_build_bipred_keys",
 )
 
 
@@ -101,6 +101,7 @@ def load_library(path=None):
         "fme_nn_copy_state_device": (I, [P, P, P]),
         "fme_template_costs": (I, [P, P, P, I, P]),
         "fme_pred_inter_b": (I, [P, P, P, I, P]),
+        "fme_build_bipred_keys": (I, [P, P, I, C.c_size_t, P]),
     }
     for name, (res, args) in sig.items():
         f = getattr(lib, name)
@@ -211,6 +212,13 @@ class FmeContext:
         if len(reqs):
             _check(self.lib, self.lib.fme_pred_inter_b(self.h, _ptr(reqs), _ptr(res), len(reqs), stream))
         return res
+
+    def build_bipred_keys(self, reqs, key_count, stream=None):
+        """fme_build_bipred_keys: removeHighFreq keys of the other list's prediction, on the device,
+        into the context's key buffer (key_count elements)."""
+        from .abi import BIKEY_REQ_DTYPE
+        reqs = np.ascontiguousarray(reqs, dtype=BIKEY_REQ_DTYPE)
+        _check(self.lib, self.lib.fme_build_bipred_keys(self.h, _ptr(reqs), len(reqs), int(key_count), stream))
 
     def template_costs(self, reqs, stream=None):
         """fme_template_costs: xGetTemplateCost per (request, reference, candidate) -> uint32

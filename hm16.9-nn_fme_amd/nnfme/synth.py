@@ -562,6 +562,74 @@ def make_pu_requests_b(rng, width, height, org_id, l0, l1, lambda_id, max_depth=
     return reqs
 
 
+# TComInterpolationFilter.cpp:57-63 luma taps by quarter-pel fraction
+LUMA_TAPS = np.array([[0, 0, 0, 64, 0, 0, 0, 0], [-1, 4, -10, 58, 17, -5, 1, 0],
+                      [-1, 4, -11, 40, 40, -11, 4, -1], [0, 1, -5, 17, 58, -10, 4, -1]], dtype=np.int64)
+
+
+def make_bipred_key_reqs(rng, jobs, org_id, ref_ids, mv_span=40, clip=False):
+    """fme_bikey_req per bi-pred job (key_offset == -2): the other list's reference (one of
+    ref_ids) and quarter-pel MV (U[-mv_span, mv_span]^2), CU origin = the PU's CTU; assigns
+    key_offset (cumulative w*h) in the jobs.  Returns (requests, key count)."""
+    from .abi import BIKEY_REQ_DTYPE, PU_CLIP_BIPRED
+    sel = np.flatnonzero(jobs["key_offset"] == -2)
+    sizes = jobs["w"][sel].astype(np.int64) * jobs["h"][sel].astype(np.int64)
+    offs = np.concatenate([[0], np.cumsum(sizes)])
+    reqs = np.zeros(len(sel), dtype=BIKEY_REQ_DTYPE)
+    for f in ("x", "y", "w", "h"):
+        reqs[f] = jobs[f][sel]
+    reqs["org_id"] = org_id
+    reqs["ref_id"] = rng.choice(np.asarray(ref_ids), size=len(sel))
+    reqs["cu_x"] = jobs["x"][sel].astype(np.int64) & ~(MAX_CU - 1)
+    reqs["cu_y"] = jobs["y"][sel].astype(np.int64) & ~(MAX_CU - 1)
+    reqs["mv_x"] = rng.integers(-mv_span, mv_span + 1, len(sel))
+    reqs["mv_y"] = rng.integers(-mv_span, mv_span + 1, len(sel))
+    reqs["key_offset"] = offs[:-1]
+    reqs["flags"] = PU_CLIP_BIPRED if clip else 0
+    jobs["key_offset"][sel] = offs[:-1]
+    return reqs, int(offs[-1])
+
+
+def bipred_keys(reqs, pictures, key_count):
+    """What fme_build_bipred_keys computes, vectorised per PU shape: the uni-pred luma prediction
+    of the other list (clipMv, xPredInterBlk's copy / 1-D / 2-D paths with HM's rounding) and
+    key = 2 * org - pred (removeHighFreq).  pictures: {slot: uint8 [H, W]}."""
+    keys = np.zeros(key_count, dtype=np.int16)
+    ids = sorted(pictures)
+    stack = np.stack([pictures[i] for i in ids]).astype(np.int64)
+    Hp, Wp = stack.shape[1:]
+    shapes = set(zip(reqs["w"].tolist(), reqs["h"].tolist()))
+    for (w, h) in shapes:
+        m = np.flatnonzero((reqs["w"] == w) & (reqs["h"] == h))
+        q = reqs[m]
+        x, y = q["x"].astype(np.int64), q["y"].astype(np.int64)
+        cux, cuy = q["cu_x"].astype(np.int64), q["cu_y"].astype(np.int64)
+        mvx = np.minimum((Wp + 8 - cux - 1) << 2, np.maximum((-MAX_CU - 8 - cux + 1) * 4, q["mv_x"].astype(np.int64)))
+        mvy = np.minimum((Hp + 8 - cuy - 1) << 2, np.maximum((-MAX_CU - 8 - cuy + 1) * 4, q["mv_y"].astype(np.int64)))
+        fx, fy = mvx & 3, mvy & 3
+        rows = np.clip(y[:, None] + (mvy >> 2)[:, None] + np.arange(-3, h + 4)[None, :], 0, Hp - 1)
+        cols = np.clip(x[:, None] + (mvx >> 2)[:, None] + np.arange(-3, w + 4)[None, :], 0, Wp - 1)
+        ref = np.searchsorted(ids, q["ref_id"])
+        win = stack[ref[:, None, None], rows[:, :, None], cols[:, None, :]]          # (n, h+7, w+7)
+        ch, cv = LUMA_TAPS[fx], LUMA_TAPS[fy]
+        hs = sum(ch[:, k, None, None] * win[:, :, k:k + w] for k in range(8))        # (n, h+7, w)
+        a = np.clip((hs[:, 3:3 + h, :] + 32) >> 6, 0, 255)                           # fy == 0
+        vs = sum(cv[:, k, None, None] * win[:, k:k + h, 3:3 + w] for k in range(8))  # fx == 0
+        b = np.clip((vs + 32) >> 6, 0, 255)
+        t = hs - 8192                                                                 # 2-D
+        cs = sum(cv[:, k, None, None] * t[:, k:k + h, :] for k in range(8))
+        c = np.clip((cs + 2048 + (8192 << 6)) >> 12, 0, 255)
+        pred = np.where((fy == 0)[:, None, None], a, np.where((fx == 0)[:, None, None], b, c))
+        org = stack[np.searchsorted(ids, q["org_id"])[:, None, None], (y[:, None] + np.arange(h))[:, :, None],
+                    (x[:, None] + np.arange(w))[:, None, :]]
+        key = 2 * org - pred
+        clip = (q["flags"] & 0x04) != 0
+        key = np.where(clip[:, None, None], np.clip(key, 0, 255), key)
+        idx = q["key_offset"].astype(np.int64)[:, None] + np.arange(w * h)[None, :]
+        keys[idx] = key.reshape(len(m), -1)
+    return keys
+
+
 def pu_requests_to_jobs(reqs, width, height):
     """The xMotionEstimation jobs of single-reference, single-candidate requests whose
     m_integerMv2Nx2N reads see the initial (0, 0): mvp = cand[0][0], xSetSearchRange(mvp, range)

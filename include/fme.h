@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define FME_ABI_VERSION 6
+#define FME_ABI_VERSION 7
 
 /* ---- error codes ---------------------------------------------------------------- */
 #define FME_OK            0
@@ -433,6 +433,22 @@ typedef struct fme_pu_res_b {
   int16_t  bi_ref_mv[FME_MAX_REFS][2];  /* bi cMvTemp per reference of bi_list                  */
   uint8_t  ref_mvp_idx[2][FME_MAX_REFS];/* uni aaiMvpIdx after xCheckBestMVP                    */
 } fme_pu_res_b;   /* 160 bytes */
+
+/* Bi-pred search keys on the device for callers that drive fme_refine themselves: per request
+ * the other list's uni-pred luma prediction at (mv_x, mv_y) (motionCompensation: clipMv against
+ * the CU origin, xPredInterBlk) and key = 2 * org - pred (TComYuv::removeHighFreq, TComYuv.cpp:
+ * 411-455; clipped to 8 bits with FME_PU_CLIP_BIPRED), written as the w*h block at key_offset of
+ * the context's key buffer (which becomes key_count elements, replacing fme_set_keys' content).
+ * key_offset must be a multiple of 4.  Host request array, synchronous. */
+typedef struct fme_bikey_req {
+  uint16_t x, y;
+  uint8_t  w, h, org_id, ref_id;   /* ref_id: the other list's reference picture slot           */
+  uint16_t cu_x, cu_y;
+  int16_t  mv_x, mv_y;             /* the other list's MV, quarter-pel                          */
+  int32_t  key_offset;
+  uint32_t flags;                  /* FME_PU_CLIP_BIPRED                                        */
+} fme_bikey_req;   /* 24 bytes */
+int fme_build_bipred_keys(fme_ctx* ctx, const fme_bikey_req* reqs, int n, size_t key_count, void* stream);
 
 /* Host arrays, synchronous on `stream`; a batch with an invalid request is rejected before any
  * work runs.  m_integerMv2Nx2N (both lists) is the state fme_pred_inter_reset forgets. */

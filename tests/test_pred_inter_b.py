@@ -106,6 +106,26 @@ def test_bi_key_matches_reference_harness():
     assert n == 10 * len(synth.ALL_PU_SIZES)
 
 
+def test_vectorised_bipred_keys_equal_oracle():
+    """synth.bipred_keys (what fme_build_bipred_keys computes; the bench's CPU copy of the C4 keys)
+    against the oracle's orc_bi_key: every shape, far MVs (clipMv), with and without the clip."""
+    from oracle import Oracle
+    pics = _pics()
+    rng = np.random.default_rng(9)
+    jobs = synth.make_jobs(rng, W, H, 600, 4, [0, 1, 2, 3], [0], bipred_frac=0.5)
+    reqs, kc = synth.make_bipred_key_reqs(rng, jobs, 4, [0, 1, 2, 3], mv_span=300)
+    reqs["flags"][::3] = abi.PU_CLIP_BIPRED
+    keys = synth.bipred_keys(reqs, pics, kc)
+    orc = Oracle(nn_mode=0)
+    _setup(orc, pics)
+    for q in reqs:
+        w, h, o = int(q["w"]), int(q["h"]), int(q["key_offset"])
+        want = orc.bi_key(int(q["org_id"]), int(q["ref_id"]), int(q["x"]), int(q["y"]), w, h, int(q["cu_x"]),
+                          int(q["cu_y"]), int(q["mv_x"]), int(q["mv_y"]), bool(q["flags"] & abi.PU_CLIP_BIPRED))
+        assert np.array_equal(keys[o:o + w * h].reshape(h, w), want), q
+    assert len(reqs) > 200
+
+
 def test_oracle_b_decision_rules():
     """The loop's rules on its own outputs: per-list strict minima, costValidList1 over L1
     references not in L0, the copied L1 reference's MV, isBipredRestriction, the bi-pred list
@@ -235,6 +255,40 @@ def test_pred_inter_b_matches_oracle():
     _compare(got, exp)
     assert np.array_equal(ctx.nn_get_state(), orc.nn_get_state())
     assert set(np.unique(got["inter_dir"])) == {1, 2, 3}
+
+
+@pytest.mark.gpu
+def test_device_bipred_keys_drive_refine_like_host_keys():
+    """fme_build_bipred_keys (k_bi_key) gives the keys synth.bipred_keys computes: bi-pred refine
+    jobs read them and equal the same jobs on host-uploaded keys (and the oracle)."""
+    from nnfme.runtime import FmeContext
+    from oracle import Oracle
+    pics = _pics()
+    rng = np.random.default_rng(10)
+    jobs = synth.make_jobs(rng, W, H, 800, 4, [0, 1, 2, 3], [0, 1, 2, 3], bipred_frac=0.6)
+    reqs, kc = synth.make_bipred_key_reqs(rng, jobs, 4, [0, 1, 2, 3], mv_span=200)
+    reqs["flags"][::4] = abi.PU_CLIP_BIPRED
+    keys = synth.bipred_keys(reqs, pics, kc)
+    dev_ctx, host_ctx = FmeContext(nn_mode=1, qp=22), FmeContext(nn_mode=1, qp=22)
+    for c in (dev_ctx, host_ctx):
+        _setup(c, pics)
+    dev_ctx.build_bipred_keys(reqs, kc)
+    host_ctx.set_keys(keys)
+    a, b = dev_ctx.refine(jobs), host_ctx.refine(jobs)
+    assert a.tobytes() == b.tobytes()
+    orc = Oracle(nn_mode=1, qp=22)
+    from nnfme import weights
+    orc.load_nn(weights.load_weights(22))
+    _setup(orc, pics)
+    orc.set_keys(keys)
+    want = orc.refine(jobs)
+    for f in ("mv_x", "mv_y", "cost", "bits", "frac_cost"):
+        assert np.array_equal(a[f], want[f]), f
+    bad = reqs.copy()
+    bad["key_offset"][3] += 2   # not a multiple of 4
+    from nnfme.runtime import FmeError
+    with pytest.raises(FmeError):
+        dev_ctx.build_bipred_keys(bad, kc)
 
 
 @pytest.mark.gpu
