@@ -225,6 +225,39 @@ __device__ __forceinline__ void store_outputs(fme_result* r, fme_mv_result* mv_o
   }
 }
 
+// Last-writer scan of NN_pred()'s carried globals (k_nn_tail, k_nn_deep_tail).  Job base + t of
+// the block's NW waves (t = threadIdx.x) has run[f] = its index when it writes field f (array_e
+// slot f < 8; f = 8: C and the PU size), else -1.  src[f] = the last writer at or before the job
+// (carry[f]: the last writer before `base`, or -1); tot[f] = the block's last writer (or carry).
+// Writer indices grow with the lane, so the last writer at or below a lane is the highest set bit
+// of the wave's write mask at or below it: ballots and wave-uniform reads instead of a
+// shuffle scan (each ds_bpermute step of which waited on the previous one).
+template <int NW>
+__device__ __forceinline__ void writer_scan(const int (&run)[9], const int (&carry)[9], int base,
+                                            int32_t (*wave_tot)[9], int (&src)[9], int (&tot)[9]) {
+  const int lane = (int)threadIdx.x & 63, wid = (int)threadIdx.x >> 6;
+  const int wbase = base + 64 * wid;
+  const unsigned long long below = ~0ull >> (63 - lane);
+  int incl[9];
+#pragma unroll
+  for (int f = 0; f < 9; f++) {
+    const unsigned long long mask = __ballot(run[f] >= 0);
+    const unsigned long long m = mask & below;
+    incl[f] = m ? wbase + 63 - __clzll(m) : -1;
+    if (lane == 0) wave_tot[wid][f] = mask ? wbase + 63 - __clzll(mask) : -1;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int f = 0; f < 9; f++) {
+    const int t = lane < NW ? wave_tot[lane][f] : -1;
+    const unsigned long long pm = __ballot(lane < wid && t >= 0);   // earlier waves with a writer
+    const unsigned long long am = __ballot(t >= 0);
+    const int prev = pm ? __builtin_amdgcn_readlane(t, 63 - __clzll(pm)) : carry[f];
+    src[f] = max(incl[f], prev);
+    tot[f] = am ? __builtin_amdgcn_readlane(t, 63 - __clzll(am)) : carry[f];
+  }
+}
+
 // A batch k_classify rejected: every job is marked, nothing else is written, and the NN state
 // is carried through unchanged (the host flips the state slot after every batch).
 __device__ __forceinline__ void reject_job(const BatchArgs& a, const WorkBufs& w, int i, int state_in) {

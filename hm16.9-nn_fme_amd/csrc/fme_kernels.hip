@@ -407,33 +407,25 @@ __global__ __launch_bounds__(kTailNT) void k_nn_tail(BatchArgs a, WorkBufs w,
     for (int s = 0; s < 8; s++) run[s] = (np > s) ? i : -1;
     run[8] = emi ? i : -1;
   }
-  int incl[9];
+  int carry[9], src[9], tot[9];
 #pragma unroll
-  for (int f = 0; f < 9; f++) {
-    int v = run[f];
-#pragma unroll
-    for (int off = 1; off < 64; off <<= 1) {
-      const int o = __shfl_up(v, off, 64);
-      if (lane >= off) v = max(v, o);
-    }
-    incl[f] = v;
-    if (lane == 63) wave_tot[wid][f] = v;
-  }
-  __syncthreads();
-  int src[9];
-#pragma unroll
-  for (int f = 0; f < 9; f++) {
-    int carry = w.blk_prefix[blockIdx.x * 9 + f];
-    for (int u = 0; u < wid; u++) carry = max(carry, wave_tot[u][f]);
-    src[f] = max(incl[f], carry);   // inclusive: this job's own pushes count
-  }
+  for (int f = 0; f < 9; f++) carry[f] = w.blk_prefix[blockIdx.x * 9 + f];
+  writer_scan<kTailNT / 64>(run, carry, blockIdx.x * kJobsPerScanBlock, wave_tot, src, tot);
+  (void)wid;
+  (void)lane;
   if (!valid) return;
 
   const uint32_t* st_in = w.nn_state + 12 * state_in;
   uint32_t* st_out = w.nn_state + 12 * (state_in ^ 1);
   fme_result* r = a.res + i;
   const double ml = a.mlambda[j.lambda_id];
-  const int mvx = r->mv_int_x, mvy = r->mv_int_y;
+  // the record's 64 bytes in four loads (the NN inputs are usually the job's own pushes)
+  typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+  const u32x4* rb = reinterpret_cast<const u32x4*>(r);
+  const u32x4 r0 = rb[0], r1 = rb[1], r2 = rb[2], r3 = rb[3];
+  const int mvx = (int16_t)(r0.x & 0xFFFF), mvy = (int16_t)(r0.x >> 16);
+  const uint32_t own_emi[8] = {r1.w, r2.x, r2.y, r2.z, r2.w, r3.x, r3.y, r3.z};
+  const uint32_t own_c = r1.z, own_n_emi = r3.w & 0xFF, frac_cost = r0.w;
   int offx, offy, cls = 255;
   uint16_t status = 0;
   if (a.nn_mode) {
@@ -441,7 +433,10 @@ __global__ __launch_bounds__(kTailNT) void k_nn_tail(BatchArgs a, WorkBufs w,
     uint32_t written = st_in[11];
 #pragma unroll
     for (int s = 0; s < 8; s++) {
-      if (src[s] >= 0) {
+      if (src[s] == i) {
+        e[s] = own_emi[s];
+        written |= 1u << s;
+      } else if (src[s] >= 0) {
         e[s] = a.res[src[s]].emi[s];
         written |= 1u << s;
       } else {
@@ -449,7 +444,12 @@ __global__ __launch_bounds__(kTailNT) void k_nn_tail(BatchArgs a, WorkBufs w,
       }
     }
     uint32_t c, ph, pw;
-    if (src[8] >= 0) {
+    if (src[8] == i) {
+      c = own_c;
+      ph = j.h;
+      pw = j.w;
+      written |= 0x100u;
+    } else if (src[8] >= 0) {
       c = a.res[src[8]].c;
       ph = a.jobs[src[8]].h;
       pw = a.jobs[src[8]].w;
@@ -460,7 +460,7 @@ __global__ __launch_bounds__(kTailNT) void k_nn_tail(BatchArgs a, WorkBufs w,
       pw = st_in[10];
     }
     cls = nn_forward(nnp_g, e, c, (int)ph, (int)pw);
-    if (!(j.flags & FME_JOB_EMI) || r->n_emi < 8) status |= FME_RES_NN_STALE;
+    if (!(j.flags & FME_JOB_EMI) || own_n_emi < 8) status |= FME_RES_NN_STALE;
     if ((written & 0x1FFu) != 0x1FFu) status |= FME_RES_NN_UNINIT;
     offx = cls % 7 - 3;
     offy = cls / 7 - 3;
@@ -473,14 +473,16 @@ __global__ __launch_bounds__(kTailNT) void k_nn_tail(BatchArgs a, WorkBufs w,
       st_out[11] = written;
     }
   } else {
-    offx = 2 * r->half_x + r->qtr_x;
-    offy = 2 * r->half_y + r->qtr_y;
+    const int8_t hx = (int8_t)(r0.z & 0xFF), hy = (int8_t)((r0.z >> 8) & 0xFF);
+    const int8_t qx = (int8_t)((r0.z >> 16) & 0xFF), qy = (int8_t)(r0.z >> 24);
+    offx = 2 * hx + qx;
+    offy = 2 * hy + qy;
   }
   const int fx = 4 * mvx + offx, fy = 4 * mvy + offy;
   const uint32_t mvb = mv_bits(fx, fy, 0, j.mvp_x, j.mvp_y);
   const uint32_t bits = (uint32_t)j.bits_in + mvb;
   const double fw = (j.flags & FME_JOB_BIPRED) ? 0.5 : 1.0;
-  const double val = floor(fw * ((double)r->frac_cost - (double)mv_cost(ml, mvb))) + (double)mv_cost(ml, bits);
+  const double val = floor(fw * ((double)frac_cost - (double)mv_cost(ml, mvb))) + (double)mv_cost(ml, bits);
   // gcc/x86-64 (Distortion)(double) semantics for the cost
   store_outputs(r, w.mv_out, i, fx, fy, (uint32_t)(int64_t)val, bits, (uint8_t)cls, status);
 }

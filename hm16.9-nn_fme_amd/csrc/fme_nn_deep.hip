@@ -310,29 +310,10 @@ __global__ __launch_bounds__(kRound) void k_nn_deep_tail(BatchArgs a, WorkBufs w
       for (int s = 0; s < 8; s++) run[s] = (np > s) ? i : -1;
       run[8] = emi ? i : -1;
     }
-    int src[9];
+    int src[9], tot[9];
+    writer_scan<kRound / 64>(run, carry, blockIdx.x * kJobsPerScanBlock + rnd * kRound, wave_tot, src, tot);
 #pragma unroll
-    for (int f = 0; f < 9; f++) {
-      int v = run[f];
-#pragma unroll
-      for (int off = 1; off < 64; off <<= 1) {
-        const int o = __shfl_up(v, off, 64);
-        if (lane >= off) v = max(v, o);
-      }
-      src[f] = v;
-      if (lane == 63) wave_tot[wid][f] = v;
-    }
-    __syncthreads();
-#pragma unroll
-    for (int f = 0; f < 9; f++) {
-      int c = carry[f];
-      for (int u = 0; u < wid; u++) c = max(c, wave_tot[u][f]);
-      src[f] = max(src[f], c);
-      int tot = carry[f];
-#pragma unroll
-      for (int u = 0; u < kRound / 64; u++) tot = max(tot, wave_tot[u][f]);
-      carry[f] = tot;
-    }
+    for (int f = 0; f < 9; f++) carry[f] = tot[f];
     __syncthreads();   // wave_tot is rewritten next round
 
     // the NN_pred() inputs this job sees (TEncSearch.cpp:88-113 / Backups/15:4944-5000)

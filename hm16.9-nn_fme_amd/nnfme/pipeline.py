@@ -101,7 +101,8 @@ class FrameReplay:
         self.org = torch.empty((n_steps * F, H, W), dtype=torch.uint8, device=device)
         self.states = torch.zeros((n_steps, 12), dtype=torch.int32, device=device)
         self.s_comp = torch.cuda.default_stream(device)
-        self.s_copy = torch.cuda.Stream(device)
+        self.s_copy = torch.cuda.Stream(device)   # H2D: jobs, originals, reconstructions
+        self.s_down = torch.cuda.Stream(device)   # D2H: results (the other copy direction, its own engine)
         self.uploaded = -1
         self.ev_in = [torch.cuda.Event() for _ in range(2)]
         self.ev_comp = [torch.cuda.Event() for _ in range(2)]
@@ -147,11 +148,17 @@ class FrameReplay:
             self._publish(g0 + j, src_rank)
 
     def prime(self):
-        """References of the first frames (recon -4 .. -2), before the run (untimed)."""
+        """References of the first frames (recon -4 .. -2), before the run (untimed); every
+        host result row is written once by the copy engine, so no timed step is the first DMA
+        into fresh pinned pages (on a fresh buffer some hipMemcpyAsync calls blocked the host
+        for up to 7 ms each: 2.15 ms per 1080p step against 1.32 once the rows had been used)."""
         with self.torch.cuda.stream(self.s_copy):
             for g in range(-REFS, -1):
                 self._publish(g, 0)
+        for k in range(self.steps):
+            _memcpy_async(self.h_out[k], self.d_out[k & 1], self.h_out.shape[1], D2H, self.s_down)
         self.s_copy.synchronize()
+        self.s_down.synchronize()
 
     def _bind(self, k):
         ctx, W, H, F = self.ctx, self.W, self.H, self.F
@@ -163,12 +170,14 @@ class FrameReplay:
             ctx.bind_picture_device(s, self.recon[f0 - REFS + s + REFS].data_ptr(), W, W, H)
 
     # -- one step -----------------------------------------------------------------------------
-    # Streams: the batch runs on the device's default stream, every copy on one copy stream, in
-    # the order U(0), U(1), D(0), U(2), D(1), ...: the upload of step k+1 is queued before the
-    # download of step k, so it overlaps step k's batch, and the download overlaps step k+1's.
-    # (With the library's two auxiliary streams that is four streams = the process's four hardware
-    # queues (GPU_MAX_HW_QUEUES): more streams share queues, and a copy stream's event waits then
-    # block kernels queued behind them.)
+    # Streams: the batch runs on the device's default stream, the uploads on one copy stream
+    # (U(0), U(1), U(2), ...: the upload of step k+1 is queued right after step k's batch is
+    # enqueued, so it overlaps that batch) and the downloads on another (D(k) waits for step k's
+    # batch and overlaps step k+1's).  The two directions use separate copy engines and PCIe is
+    # full duplex: on one stream the 31.7 MB up + 13.8 MB down of a 1080p step serialised
+    # (1.75 ms per step against 1.25 ms for the batch alone).  Compute + two copy streams stay
+    # within the process's four hardware queues (GPU_MAX_HW_QUEUES); more streams share queues,
+    # and a copy stream's event waits then block kernels queued behind them.
     def _upload(self, k):
         F = self.F
         b = k & 1
@@ -205,10 +214,10 @@ class FrameReplay:
         self.ev_comp[b].record(comp)
         if prefetch and k + 1 < self.steps:
             self._upload(k + 1)
-        cp = self.s_copy
-        cp.wait_event(self.ev_comp[b])
-        _memcpy_async(self.h_out[k], self.d_out[b], self.h_out.shape[1], D2H, cp)
-        self.ev_out[b].record(cp)
+        dn = self.s_down
+        dn.wait_event(self.ev_comp[b])
+        _memcpy_async(self.h_out[k], self.d_out[b], self.h_out.shape[1], D2H, dn)
+        self.ev_out[b].record(dn)
 
     def results(self, k):
         return self.h_out[k].numpy().view(MV_RESULT_DTYPE)
@@ -220,6 +229,7 @@ class FrameReplay:
         torch = self.torch
         self.s_copy.synchronize()
         self.s_comp.synchronize()
+        self.s_down.synchronize()
         if self.world == 1:
             return 0
         import torch.distributed as dist

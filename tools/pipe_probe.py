@@ -19,6 +19,9 @@ from nnfme.runtime import FmeContext  # noqa: E402
 
 def main():
     name = sys.argv[1] if len(sys.argv) > 1 else "c3_qp22"
+    if os.environ.get("PIPE_EV_TIMING"):   # A/B: the replay's ordering events with timing enabled
+        ev = torch.cuda.Event
+        torch.cuda.Event = lambda *a, **k: ev(enable_timing=True)
     wl = bench.WORKLOADS[name]
     bench.W, bench.H, bench.QP = wl["W"], wl["H"], wl["QP"]
     jobs = bench.make_frame_jobs(1000, "ctu", wl["calls"], wl["bipred"])
@@ -50,7 +53,7 @@ def main():
     print(f"{name}: device-resident {wall:.3f} ms/step ({rep.n / wall / 1e3:.1f} M PU/s)")
 
 
-if __name__ == "__main__":
+if __name__ == "__main__" and not os.environ.get("PROBE_HOST"):
     main()
 
 
@@ -87,11 +90,11 @@ def timeline():
             self.ev_comp[b].record(comp)
             if prefetch and k + 1 < self.steps:
                 self._upload(k + 1)
-            cp = self.s_copy
-            cp.wait_event(self.ev_comp[b])
-            pipeline._memcpy_async(self.h_out[k], self.d_out[b], self.h_out.shape[1], pipeline.D2H, cp)
-            self.ev_out[b].record(cp)
-            marks[k]["d"].record(cp)
+            dn = self.s_down
+            dn.wait_event(self.ev_comp[b])
+            pipeline._memcpy_async(self.h_out[k], self.d_out[b], self.h_out.shape[1], pipeline.D2H, dn)
+            self.ev_out[b].record(dn)
+            marks[k]["d"].record(dn)
 
     rep = T(ctx, jobs, pool, lambda f: bench.frame_lambda(wl, f), steps, device=torch.device("cuda", 0))
     rep.prime()
@@ -110,3 +113,54 @@ def timeline():
 
 if __name__ == "__main__" and os.environ.get("PROBE_TIMELINE"):
     timeline()
+
+
+def host_calls():
+    """Host time of every HIP call issue() makes (PROBE_HOST=1): which one blocks."""
+    import collections
+    wl = bench.WORKLOADS["c3_qp22"]
+    bench.W, bench.H, bench.QP = wl["W"], wl["H"], wl["QP"]
+    jobs = bench.make_frame_jobs(1000, "ctu", wl["calls"], wl["bipred"])
+    ctx = FmeContext(device=0, nn_mode=1, qp=22, max_jobs=len(jobs))
+    pool = np.stack([synth.synth_luma(wl["W"], wl["H"], t) for t in range(8)])
+    steps = 24
+    rec = collections.defaultdict(list)
+
+    def timed(name, fn):
+        def w(*a, **k):
+            t = time.perf_counter()
+            r = fn(*a, **k)
+            rec[name].append((time.perf_counter() - t) * 1e3)
+            return r
+        return w
+    pipeline._memcpy_async = timed("memcpy_async", pipeline._memcpy_async)
+    for m in ("refine_mv_device", "bind_picture_device", "set_lambda"):
+        setattr(ctx, m, timed(m, getattr(ctx, m)))
+    rep = pipeline.FrameReplay(ctx, jobs, pool, lambda f: bench.frame_lambda(wl, f), steps,
+                               device=torch.device("cuda", 0))
+    for ev in rep.ev_in + rep.ev_comp + rep.ev_out:
+        ev.record = timed("event_record", ev.record)
+    rep.s_comp.wait_event = timed("wait_event", rep.s_comp.wait_event)
+    rep.prime()
+    for k in range(4):
+        rep.issue(k, prefetch=k < 3)
+    rep.finish()
+    rec.clear()
+    t = time.perf_counter()
+    for k in range(4, steps):
+        h = time.perf_counter()
+        rep.issue(k)
+        rec["issue"].append((time.perf_counter() - h) * 1e3)
+    h = time.perf_counter()
+    rep.finish()
+    rec["finish"].append((time.perf_counter() - h) * 1e3)
+    wall = (time.perf_counter() - t) * 1e3 / (steps - 4)
+    print(f"host_calls: pipelined {wall:.3f} ms/step")
+    for k, v in rec.items():
+        v = np.array(v)
+        print(f"  {k:22s} n={len(v):4d} sum={v.sum():8.3f} max={v.max():7.3f} median={np.median(v):.3f} ms")
+
+
+if __name__ == "__main__" and os.environ.get("PROBE_HOST"):
+    host_calls()   # a fresh process: the first replay
+    host_calls()
