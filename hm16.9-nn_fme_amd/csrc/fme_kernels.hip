@@ -382,47 +382,17 @@ __device__ __forceinline__ int nn_forward(const float* __restrict__ Q, const uin
   return best;
 }
 
-// One lane per job, 1024 lanes per block = one 1024-job scan block (kJobsPerScanBlock).
-constexpr int kTailNT = kJobsPerScanBlock;
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
-__global__ __launch_bounds__(kTailNT) void k_nn_tail(BatchArgs a, WorkBufs w,
-                                                     const float* __restrict__ nnp_g, int state_in) {
-  __shared__ int32_t wave_tot[kTailNT / 64][9];
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int i = blockIdx.x * kJobsPerScanBlock + tid;
-  const bool valid = i < a.n;
-  if (w.sched->invalid) {
-    if (valid) reject_job(a, w, i, state_in);
-    return;
-  }
-  fme_job j{};
-  if (valid) j = a.jobs[i];
-
-  // writer indices of this job (slots it pushes, C/PU size), prefix-max across the block
-  int run[9];
-  {
-    const bool emi = valid && (j.flags & FME_JOB_EMI);
-    const int np = emi ? emi_pushes(j) : 0;
-#pragma unroll
-    for (int s = 0; s < 8; s++) run[s] = (np > s) ? i : -1;
-    run[8] = emi ? i : -1;
-  }
-  int carry[9], src[9], tot[9];
-#pragma unroll
-  for (int f = 0; f < 9; f++) carry[f] = w.blk_prefix[blockIdx.x * 9 + f];
-  writer_scan<kTailNT / 64>(run, carry, blockIdx.x * kJobsPerScanBlock, wave_tot, src, tot);
-  (void)wid;
-  (void)lane;
-  if (!valid) return;
-
+// NN_pred() on the inputs job i sees + the xMotionEstimation tail (TEncSearch.cpp:4583-4597):
+// src = the last writer of each carried field (writer_scan), r0..r3 = the job's 64-byte record.
+__device__ __forceinline__ void tail_job(const BatchArgs& a, const WorkBufs& w, const float* __restrict__ nnp_g,
+                                         int state_in, int i, const fme_job& j, const int (&src)[9], u32x4 r0,
+                                         u32x4 r1, u32x4 r2, u32x4 r3) {
   const uint32_t* st_in = w.nn_state + 12 * state_in;
   uint32_t* st_out = w.nn_state + 12 * (state_in ^ 1);
   fme_result* r = a.res + i;
   const double ml = a.mlambda[j.lambda_id];
-  // the record's 64 bytes in four loads (the NN inputs are usually the job's own pushes)
-  typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-  const u32x4* rb = reinterpret_cast<const u32x4*>(r);
-  const u32x4 r0 = rb[0], r1 = rb[1], r2 = rb[2], r3 = rb[3];
   const int mvx = (int16_t)(r0.x & 0xFFFF), mvy = (int16_t)(r0.x >> 16);
   const uint32_t own_emi[8] = {r1.w, r2.x, r2.y, r2.z, r2.w, r3.x, r3.y, r3.z};
   const uint32_t own_c = r1.z, own_n_emi = r3.w & 0xFF, frac_cost = r0.w;
@@ -485,6 +455,64 @@ __global__ __launch_bounds__(kTailNT) void k_nn_tail(BatchArgs a, WorkBufs w,
   const double val = floor(fw * ((double)frac_cost - (double)mv_cost(ml, mvb))) + (double)mv_cost(ml, bits);
   // gcc/x86-64 (Distortion)(double) semantics for the cost
   store_outputs(r, w.mv_out, i, fx, fy, (uint32_t)(int64_t)val, bits, (uint8_t)cls, status);
+}
+
+// One lane per job; a block scans one 1024-job block (kJobsPerScanBlock, the granularity of
+// k_scatter's carry-in) in rounds of kTailNT jobs, the carry passed from round to round.
+// A/B on the 1080p batch (tools/ab_bench.py, identical results): 1024 lanes at 4 waves/SIMD
+// 0.112 ms, 512 lanes x 2 rounds at 6 waves/SIMD 0.108, 256 x 4 at 6 0.121, at 5 0.119: the tail
+// is bound by its own issue (≈ 3,100 instructions per wave, 1,640 of them packed f32 multiply /
+// add in the reference's k order), not by latency; kept at one round.
+constexpr int kTailNT = kJobsPerScanBlock;
+static_assert(kJobsPerScanBlock % kTailNT == 0, "rounds tile the scan block");
+
+__global__ __launch_bounds__(kTailNT)
+void k_nn_tail(BatchArgs a, WorkBufs w, const float* __restrict__ nnp_g, int state_in) {
+  __shared__ int32_t wave_tot[kTailNT / 64][9];
+  const int tid = threadIdx.x;
+  if (w.sched->invalid) {
+    for (int rnd = 0; rnd < kJobsPerScanBlock / kTailNT; rnd++) {
+      const int i = blockIdx.x * kJobsPerScanBlock + rnd * kTailNT + tid;
+      if (i < a.n) reject_job(a, w, i, state_in);
+    }
+    return;
+  }
+  int carry[9];
+#pragma unroll
+  for (int f = 0; f < 9; f++) carry[f] = w.blk_prefix[blockIdx.x * 9 + f];
+  for (int rnd = 0; rnd < kJobsPerScanBlock / kTailNT; rnd++) {
+    const int base = blockIdx.x * kJobsPerScanBlock + rnd * kTailNT;
+    if (base >= a.n) break;   // block-uniform
+    const int i = base + tid;
+    const bool valid = i < a.n;
+    fme_job j{};
+    // the job and its 64-byte record, issued before the scan's barrier (the NN inputs are
+    // usually the job's own pushes)
+    u32x4 r0{}, r1{}, r2{}, r3{};
+    if (valid) {
+      j = a.jobs[i];
+      const u32x4* rb = reinterpret_cast<const u32x4*>(a.res + i);
+      r0 = rb[0];
+      r1 = rb[1];
+      r2 = rb[2];
+      r3 = rb[3];
+    }
+    // writer indices of this job (slots it pushes, C / PU size)
+    int run[9];
+    {
+      const bool emi = valid && (j.flags & FME_JOB_EMI);
+      const int np = emi ? emi_pushes(j) : 0;
+#pragma unroll
+      for (int s = 0; s < 8; s++) run[s] = (np > s) ? i : -1;
+      run[8] = emi ? i : -1;
+    }
+    int src[9], tot[9];
+    writer_scan<kTailNT / 64>(run, carry, base, wave_tot, src, tot);
+#pragma unroll
+    for (int f = 0; f < 9; f++) carry[f] = tot[f];
+    if (valid) tail_job(a, w, nnp_g, state_in, i, j, src, r0, r1, r2, r3);
+    if (kJobsPerScanBlock / kTailNT > 1) __syncthreads();   // wave_tot is rewritten next round
+  }
 }
 
 // NN_pred() on one explicit input (fme_nn_pred_single): e[8], C, PUHeight, PUWidth.
