@@ -596,9 +596,7 @@ def main():
 
     for s in range(args.warmup):
         rep.issue(s, prefetch=s + 1 < args.warmup)   # the first timed step uploads its own inputs
-    rep.s_copy.synchronize()
-    rep.s_comp.synchronize()
-    rep.s_down.synchronize()
+    rep.drain()
 
     # ---- timed region: H2D (jobs, originals, reconstructions + RCCL broadcast) -> refine ->
     # D2H of the 16-byte results, two steps in flight; the NN-state chain fix-up when sharded ----

@@ -157,6 +157,7 @@ struct fme_ctx {
   long long ev_tail = 0;        // sets harvested
   bool timed = false;
   hipEvent_t ev_done = nullptr; // end of the last batch (fme_refine_status)
+  hipEvent_t ev_search = nullptr; // caller's event, recorded before each search launch (fme_set_search_event)
   bool batch_issued = false;
   float last_ms[FME_NUM_TIMINGS] = {};
   double acc_ms[FME_NUM_TIMINGS] = {};
@@ -612,6 +613,7 @@ static int refine_batch(fme_ctx* c, const fme_job* d_jobs, fme_result* d_res, fm
   if (prof) HIP_TRY(hipEventRecord(ev[2], s));
   HIP_TRY(launch_scatter(a, w, s));
   if (prof) HIP_TRY(hipEventRecord(ev[3], s));
+  if (c->ev_search) HIP_TRY(hipEventRecord(c->ev_search, s));
   // the lane kernel: every PU shape, one launch on the batch stream
   HIP_TRY(launch_search_lane(a, w, s));
   if (prof) HIP_TRY(hipEventRecord(ev[4], s));
@@ -643,6 +645,12 @@ int fme_refine_mv_device(fme_ctx* c, const fme_job* d_jobs, fme_mv_result* d_out
   HIP_TRY(hipSetDevice(c->device));
   HIP_TRY(c->d_res.reserve(n));   // full records: context scratch
   return refine_batch(c, d_jobs, c->d_res.p, d_out, n, static_cast<hipStream_t>(stream));
+}
+
+int fme_set_search_event(fme_ctx* c, void* event) {
+  if (!c) return fail(FME_E_INVALID, "fme_set_search_event: null ctx");
+  c->ev_search = static_cast<hipEvent_t>(event);
+  return FME_OK;
 }
 
 int fme_refine_status(fme_ctx* c) {

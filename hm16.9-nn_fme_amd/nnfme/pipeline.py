@@ -107,6 +107,12 @@ class FrameReplay:
         self.ev_in = [torch.cuda.Event() for _ in range(2)]
         self.ev_comp = [torch.cuda.Event() for _ in range(2)]
         self.ev_out = [torch.cuda.Event() for _ in range(2)]
+        # recorded by the library right before each batch's search kernel (fme_set_search_event):
+        # step k's results are downloaded once step k+1's search runs (see issue())
+        self.ev_search = torch.cuda.Event()
+        self.ev_search.record(self.s_comp)        # creates the underlying hipEvent_t
+        ctx.set_search_event(self.ev_search)
+        self.pending = None                       # step whose download is not issued yet
         self.fixed_jobs = 0
 
     def first_frame(self, k):
@@ -171,13 +177,16 @@ class FrameReplay:
 
     # -- one step -----------------------------------------------------------------------------
     # Streams: the batch runs on the device's default stream, the uploads on one copy stream
-    # (U(0), U(1), U(2), ...: the upload of step k+1 is queued right after step k's batch is
-    # enqueued, so it overlaps that batch) and the downloads on another (D(k) waits for step k's
-    # batch and overlaps step k+1's).  The two directions use separate copy engines and PCIe is
-    # full duplex: on one stream the 31.7 MB up + 13.8 MB down of a 1080p step serialised
-    # (1.75 ms per step against 1.25 ms for the batch alone).  Compute + two copy streams stay
-    # within the process's four hardware queues (GPU_MAX_HW_QUEUES); more streams share queues,
-    # and a copy stream's event waits then block kernels queued behind them.
+    # (the upload of step k+1 is queued right after step k's batch, so it overlaps that batch) and
+    # the downloads on another: the two directions use separate copy engines, and PCIe is full
+    # duplex (on one stream the 31.7 MB up + 13.8 MB down of a 1080p step serialised: 1.75 ms per
+    # step against 1.25 ms for the batch alone).  The download of step k waits until step k+1's
+    # search kernel runs (the library records ev_search before each search launch): a
+    # device-to-host copy's posted PCIe writes hold back every read the device issues behind
+    # them, so a download that overlapped step k+1's prologue held each of its kernel launches
+    # (AQL packet fetches) until the copy had drained, ≈ 0.25 ms per step.  Compute + two copy
+    # streams stay within the process's four hardware queues (GPU_MAX_HW_QUEUES); more streams
+    # share queues, and a copy stream's event waits then block kernels queued behind them.
     def _upload(self, k):
         F = self.F
         b = k & 1
@@ -214,10 +223,24 @@ class FrameReplay:
         self.ev_comp[b].record(comp)
         if prefetch and k + 1 < self.steps:
             self._upload(k + 1)
+        if self.pending is not None:
+            self._download(self.pending, self.ev_search)   # step k's search started: k-1 is done
+        self.pending = k
+
+    def _download(self, k, after):
         dn = self.s_down
-        dn.wait_event(self.ev_comp[b])
-        _memcpy_async(self.h_out[k], self.d_out[b], self.h_out.shape[1], D2H, dn)
-        self.ev_out[b].record(dn)
+        dn.wait_event(after)
+        _memcpy_async(self.h_out[k], self.d_out[k & 1], self.h_out.shape[1], D2H, dn)
+        self.ev_out[k & 1].record(dn)
+
+    def drain(self):
+        """Issue the last step's download and wait for every stream."""
+        if self.pending is not None:
+            self._download(self.pending, self.ev_comp[self.pending & 1])
+            self.pending = None
+        self.s_copy.synchronize()
+        self.s_comp.synchronize()
+        self.s_down.synchronize()
 
     def results(self, k):
         return self.h_out[k].numpy().view(MV_RESULT_DTYPE)
@@ -227,9 +250,7 @@ class FrameReplay:
         """Wait for every step; when sharded, chain the NN states and refine each batch's
         carried-state prefix again (steps >= first_step).  Returns the number of re-run jobs."""
         torch = self.torch
-        self.s_copy.synchronize()
-        self.s_comp.synchronize()
-        self.s_down.synchronize()
+        self.drain()
         if self.world == 1:
             return 0
         import torch.distributed as dist

@@ -15,7 +15,7 @@ from .weights import load_weights
 PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB_PATH = os.environ.get("FME_LIB_PATH") or os.path.join(PKG_ROOT, "libfme_amd.so")
 
-ABI_VERSION = 7
+ABI_VERSION = 8
 TIMING_NAMES = ("classify", "scatter", "search", "nn_tail", "batch", "search_main", "search_aux")
 
 # Every entry point include/fme.h declares (the ABI test checks the .so exports them).
@@ -31,6 +31,7 @@ ABI_SYMBOLS = (
     "fme_pred_inter_p", "fme_pred_inter_reset", "fme_nn_param_count", "fme_load_nn_net",
     "fme_set_nn_engine", "fme_set_nn_margin_output", "fme_refine_mv", "fme_refine_mv_device",
     "fme_refine_status", "fme_nn_copy_state_device", "fme_template_costs", "fme_pred_inter_b", "fme_build_bipred_keys",
+    "fme_set_search_event",
 )
 
 
@@ -99,6 +100,7 @@ def load_library(path=None):
         "fme_refine_mv_device": (I, [P, P, P, I, P]),
         "fme_refine_status": (I, [P]),
         "fme_nn_copy_state_device": (I, [P, P, P]),
+        "fme_set_search_event": (I, [P, P]),
         "fme_template_costs": (I, [P, P, P, I, P]),
         "fme_pred_inter_b": (I, [P, P, P, I, P]),
         "fme_build_bipred_keys": (I, [P, P, I, C.c_size_t, P]),
@@ -335,6 +337,13 @@ class FmeContext:
     def nn_copy_state_device(self, d_ptr, stream=None):
         """Enqueue a copy of the carried NN state (12 words) to device memory at d_ptr."""
         _check(self.lib, self.lib.fme_nn_copy_state_device(self.h, C.c_void_p(d_ptr), stream))
+
+    def set_search_event(self, event):
+        """Record `event` (a torch.cuda.Event or a raw hipEvent_t, None: off) on the batch stream
+        right before each later batch's search kernel (fme_set_search_event)."""
+        if event is not None and hasattr(event, "cuda_event"):
+            event = event.cuda_event
+        _check(self.lib, self.lib.fme_set_search_event(self.h, C.c_void_p(event) if event else None))
 
     def frac_dif_single(self, key, ref_window, ref_origin, mv_int, mvp, motion_lambda, lossless=False):
         """xPatternSearchFracDIF argument list: key block (int16 HxW), a padded reference

@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define FME_ABI_VERSION 7
+#define FME_ABI_VERSION 8
 
 /* ---- error codes ---------------------------------------------------------------- */
 #define FME_OK            0
@@ -240,6 +240,15 @@ int fme_nn_set_state(fme_ctx* ctx, const uint32_t* in12);
 /* Enqueue on `stream` a device-to-device copy of the state after every batch issued so far
  * (12 words to d_out12): per-frame end states without a host round trip.                    */
 int fme_nn_copy_state_device(fme_ctx* ctx, uint32_t* d_out12, void* stream);
+
+/* Optional: a hipEvent_t that every later batch records on its stream right before the search
+ * kernel, i.e. once the batch's dispatch-heavy prologue (tables, classify, schedule, scatter) has
+ * run; NULL turns it off.  A pipeline waits on it to start the previous batch's results download
+ * only when the long search kernel is running: a device-to-host copy's posted PCIe writes hold
+ * back every read the device issues behind them (AQL packet and kernel-argument fetches), so a
+ * download overlapping a prologue delayed each of its launches by the length of the copy.   */
+int fme_set_search_event(fme_ctx* ctx, void* event);
+
 
 /* ---- the batch path --------------------------------------------------------------------- *
  * Runs EMI step -> FracDIF -> NN_pred -> xMotionEstimation tail for n jobs, in job order

@@ -19,11 +19,11 @@ def header_functions():
 def test_library_exports_header():
     lib = runtime.load_library()
     names = header_functions()
-    assert len(names) == 43
+    assert len(names) == 44
     assert set(names) == set(runtime.ABI_SYMBOLS)
     for n in names:
         assert hasattr(lib, n), n
-    assert lib.fme_abi_version() == runtime.ABI_VERSION == 7
+    assert lib.fme_abi_version() == runtime.ABI_VERSION == 8
 
 
 def test_struct_layouts():
@@ -78,6 +78,7 @@ def test_null_arguments_rejected():
     assert lib.fme_refine_mv_device(None, None, None, 1, None) == -1
     assert lib.fme_refine_status(None) == -1
     assert lib.fme_nn_copy_state_device(None, None, None) == -1
+    assert lib.fme_set_search_event(None, None) == -1
     assert lib.fme_destroy(None) == 0
 
 

@@ -57,64 +57,6 @@ if __name__ == "__main__" and not os.environ.get("PROBE_HOST"):
     main()
 
 
-def timeline():
-    """Per-step events: when each step's batch could start (its waits satisfied) and ended, when
-    its upload and download ended (ms from the first event)."""
-    wl = bench.WORKLOADS["c3_qp22"]
-    bench.W, bench.H, bench.QP = wl["W"], wl["H"], wl["QP"]
-    jobs = bench.make_frame_jobs(1000, "ctu", wl["calls"], wl["bipred"])
-    ctx = FmeContext(device=0, nn_mode=1, qp=22, max_jobs=len(jobs))
-    pool = np.stack([synth.synth_luma(wl["W"], wl["H"], t) for t in range(8)])
-    steps = 12
-    E = lambda: torch.cuda.Event(enable_timing=True)  # noqa: E731
-    marks = {k: {n: E() for n in ("u", "c0", "c1", "d")} for k in range(steps)}
-
-    class T(pipeline.FrameReplay):
-        def _upload(self, k):
-            super()._upload(k)
-            marks[k]["u"].record(self.s_copy)
-
-        def issue(self, k, prefetch=True):
-            ctx_ = self.ctx
-            b = k & 1
-            if self.uploaded < k:
-                self._upload(k)
-            comp = self.s_comp
-            comp.wait_event(self.ev_in[b])
-            if k >= 2:
-                comp.wait_event(self.ev_out[b])
-            marks[k]["c0"].record(comp)
-            self._bind(k)
-            ctx_.refine_mv_device(self.d_jobs[b].data_ptr(), self.d_out[b].data_ptr(), self.n, comp.cuda_stream)
-            marks[k]["c1"].record(comp)
-            self.ev_comp[b].record(comp)
-            if prefetch and k + 1 < self.steps:
-                self._upload(k + 1)
-            dn = self.s_down
-            dn.wait_event(self.ev_comp[b])
-            pipeline._memcpy_async(self.h_out[k], self.d_out[b], self.h_out.shape[1], pipeline.D2H, dn)
-            self.ev_out[b].record(dn)
-            marks[k]["d"].record(dn)
-
-    rep = T(ctx, jobs, pool, lambda f: bench.frame_lambda(wl, f), steps, device=torch.device("cuda", 0))
-    rep.prime()
-    base = E()
-    torch.cuda.synchronize()
-    base.record(rep.s_comp)
-    for k in range(steps):
-        rep.issue(k)
-    rep.finish()
-    torch.cuda.synchronize()
-    for k in range(steps):
-        t = {n: base.elapsed_time(e) for n, e in marks[k].items()}
-        print(f"step {k:2d}: upload end {t['u']:8.3f}  batch start {t['c0']:8.3f} end {t['c1']:8.3f} "
-              f"({t['c1'] - t['c0']:.3f})  download end {t['d']:8.3f}")
-
-
-if __name__ == "__main__" and os.environ.get("PROBE_TIMELINE"):
-    timeline()
-
-
 def host_calls():
     """Host time of every HIP call issue() makes (PROBE_HOST=1): which one blocks."""
     import collections
