@@ -515,6 +515,9 @@ def main():
     ap.add_argument("--cpu-cores", type=int, default=0,
                     help="cores for cpu_baseline_all_cores (0: all available, at most 16; -1: skip)")
     ap.add_argument("--dist-backend", default="nccl", help="torch.distributed backend for N > 1 (nccl = RCCL)")
+    ap.add_argument("--download", choices=("deferred", "immediate"), default=None,
+                    help="results download of step k: once step k+1's search runs (deferred) or right after "
+                         "step k (immediate); default: the workload's measured choice (DESIGN.md section 5)")
     args = ap.parse_args()
 
     global W, H, QP, METRIC
@@ -589,8 +592,9 @@ def main():
     # synthetic frame pool (the trace's originals / reconstructions): frame g -> pool[g % 8]
     pool = np.stack([synth.synth_luma(W, H, t) for t in range(8)])
     steps_total = args.warmup + args.steps
+    defer = (args.download or wl.get("download", "deferred")) == "deferred"
     rep = FrameReplay(ctx, jobs, pool, lambda f: frame_lambda(wl, f), steps_total, frames_per_step=FPS,
-                      world=world, rank=rank, device=dev)
+                      world=world, rank=rank, device=dev, defer_download=defer)
     n = rep.n
     rep.prime()
 

@@ -76,7 +76,7 @@ def group_jobs(base, frames):
 
 class FrameReplay:
     def __init__(self, ctx, base_jobs, pool, lambda_of, n_steps, frames_per_step=1, world=1, rank=0, device=None,
-                 group=None):
+                 group=None, defer_download=True):
         """ctx: an FmeContext on `device`; base_jobs: one frame's jobs (ref_id = reference
         distance - 1); pool: uint8 [P, H, W] host frames, frame g's pictures are pool[g % P];
         lambda_of(g): frame g's lambda."""
@@ -111,7 +111,8 @@ class FrameReplay:
         # step k's results are downloaded once step k+1's search runs (see issue())
         self.ev_search = torch.cuda.Event()
         self.ev_search.record(self.s_comp)        # creates the underlying hipEvent_t
-        ctx.set_search_event(self.ev_search)
+        self.defer_download = defer_download
+        ctx.set_search_event(self.ev_search if defer_download else None)
         self.pending = None                       # step whose download is not issued yet
         self.fixed_jobs = 0
 
@@ -223,6 +224,9 @@ class FrameReplay:
         self.ev_comp[b].record(comp)
         if prefetch and k + 1 < self.steps:
             self._upload(k + 1)
+        if not self.defer_download:
+            self._download(k, self.ev_comp[b])
+            return
         if self.pending is not None:
             self._download(self.pending, self.ev_search)   # step k's search started: k-1 is done
         self.pending = k
