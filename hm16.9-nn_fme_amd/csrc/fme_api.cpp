@@ -29,8 +29,11 @@ namespace {
 
 thread_local std::string g_last_error = "";
 
-// counts buffer: 25 class counts (+ invalid), 24 scatter cursors, 8 lane tile-queue heads
-constexpr int kCountWords = 2 * kNumClasses + 1 + 8;
+// counts buffer: 25 class counts (+ invalid), 24 scatter cursors, 8 lane tile-queue heads; zeroed per
+// batch by one
+// hipMemsetAsync, padded to 64 words (256 B) so the runtime issues one fill kernel, not two
+constexpr int kCountWords = 64;
+static_assert(2 * kNumClasses + 1 + 8 <= kCountWords, "counter block");
 
 int fail(int code, const char* fmt, ...) {
   char buf[512];
