@@ -138,6 +138,7 @@ struct fme_ctx {
   DevBuf<int16_t> d_tz_emi;   // [n][2] post-EMI integer MVs (producer levels)
   DevBuf<uint32_t> d_amvp_sad;
   DevBuf<BiKeyTask> d_bikey;
+  DevBuf<int32_t> d_key_invalid;  // invalid requests of the last fme_build_bipred_keys_device
   DevBuf<int32_t> d_ch_i32;     // k_tz_level: psrc
 
   std::unique_ptr<fme_ctx> single;  // private context for the single-PU entry points
@@ -210,6 +211,8 @@ int fme_create(int device, const fme_config* cfg, fme_ctx** out_ctx) {
   HIP_TRY(hipEventCreateWithFlags(&c->ev_done, hipEventDisableTiming));
   HIP_TRY(c->nn_state.reserve(24));
   HIP_TRY(hipMemset(c->nn_state.p, 0, 24 * sizeof(uint32_t)));
+  HIP_TRY(c->d_key_invalid.reserve(1));
+  HIP_TRY(hipMemset(c->d_key_invalid.p, 0, sizeof(int32_t)));
   HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&c->h_counts), (kNumClasses + 1) * sizeof(int32_t), hipHostMallocDefault));
   if (const char* e = getenv("FME_TZ_DEFER")) c->tz_defer = (e[0] == '1');
   if (const char* e = getenv("FME_TZ_DEFER_MIN")) c->tz_defer_min = atoi(e);
@@ -236,7 +239,7 @@ int fme_destroy(fme_ctx* c) {
     if (c->chroma_owned[i]) (void)hipFree(c->chroma_owned[i]);
   c->d_mc_jobs.release(); c->d_mc_planes.release(); c->d_mc_invalid.release();
   c->d_tz_ext.release(); c->d_tz_sad.release(); c->d_tz_rst.release(); c->d_tz_rq.release();
-  c->d_amvp.release(); c->d_amvp_sad.release(); c->d_bikey.release(); c->d_ch_i32.release(); c->d_tz_emi.release();
+  c->d_amvp.release(); c->d_amvp_sad.release(); c->d_bikey.release(); c->d_key_invalid.release(); c->d_ch_i32.release(); c->d_tz_emi.release();
   for (auto& e : c->ev_tz)
     if (e) (void)hipEventDestroy(e);
   for (auto& e : c->ev_mc)
@@ -585,6 +588,7 @@ static int refine_batch(fme_ctx* c, const fme_job* d_jobs, fme_result* d_res, fm
   a.res = d_res;
   a.keys = c->d_keys.p;
   a.n_keys = (int64_t)c->n_keys;
+  a.key_invalid = c->d_key_invalid.p;
   a.mlambda = c->d_mlambda.p;
   a.pics = c->d_pics.p;
   a.n = n;
@@ -688,6 +692,7 @@ static int tz_run(fme_ctx* c, fme_job* d_jobs, const fme_tz_ext* d_ext, uint32_t
   a.jobs = d_jobs;
   a.keys = c->d_keys.p;
   a.n_keys = (int64_t)c->n_keys;
+  a.key_invalid = c->d_key_invalid.p;
   a.mlambda = c->d_mlambda.p;
   a.pics = c->d_pics.p;
   a.n = n;
@@ -845,6 +850,7 @@ static int tz_by_level(fme_ctx* c, std::vector<fme_job>& jobs, std::vector<fme_t
   ta.a.jobs = c->d_jobs.p;
   ta.a.keys = c->d_keys.p;
   ta.a.n_keys = (int64_t)c->n_keys;
+  ta.a.key_invalid = c->d_key_invalid.p;
   ta.a.mlambda = c->d_mlambda.p;
   ta.a.pics = c->d_pics.p;
   ta.a.n = nu;
@@ -1355,9 +1361,33 @@ int fme_build_bipred_keys(fme_ctx* c, const fme_bikey_req* reqs, int n, size_t k
   if (n == 0) return FME_OK;
   HIP_TRY(c->d_bikey.reserve((size_t)n));
   HIP_TRY(hipMemcpyAsync(c->d_bikey.p, reqs, (size_t)n * sizeof(BiKeyTask), hipMemcpyHostToDevice, s));
-  BiKeyArgs ka{c->d_bikey.p, c->d_pics.p, c->d_keys.p, (int32_t)n};
+  HIP_TRY(hipMemsetAsync(c->d_key_invalid.p, 0, sizeof(int32_t), s));   // host-validated: the keys are good
+  BiKeyArgs ka{c->d_bikey.p, c->d_pics.p, c->d_keys.p, (int32_t)n, nullptr, (int64_t)key_count};
   HIP_TRY(launch_bi_key(ka, s));
   HIP_TRY(hipStreamSynchronize(s));
+  return FME_OK;
+}
+
+// The frame replay's per-frame form: requests already in device memory, everything stream-ordered
+// (no host synchronisation).  Validation runs in k_bi_key; a request that fails it is skipped and
+// counted, and every later batch whose jobs read keys is rejected until keys are built again.
+int fme_build_bipred_keys_device(fme_ctx* c, const fme_bikey_req* d_reqs, int n, size_t key_count, void* stream) {
+  if (!c || (n > 0 && !d_reqs)) return fail(FME_E_INVALID, "fme_build_bipred_keys_device: null argument");
+  if (n < 0) return fail(FME_E_INVALID, "fme_build_bipred_keys_device: n = %d", n);
+  HIP_TRY(hipSetDevice(c->device));
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  int rc = sync_tables(c, s);
+  if (rc) return rc;
+  if (key_count > c->d_keys.cap) {   // growing frees the old buffer: let queued batches finish first
+    HIP_TRY(hipStreamSynchronize(s));
+    HIP_TRY(c->d_keys.reserve(key_count));
+  }
+  c->n_keys = key_count;
+  HIP_TRY(hipMemsetAsync(c->d_key_invalid.p, 0, sizeof(int32_t), s));
+  if (n == 0) return FME_OK;
+  BiKeyArgs ka{reinterpret_cast<const BiKeyTask*>(d_reqs), c->d_pics.p, c->d_keys.p, (int32_t)n,
+               c->d_key_invalid.p, (int64_t)key_count};
+  HIP_TRY(launch_bi_key(ka, s));
   return FME_OK;
 }
 
@@ -1912,7 +1942,8 @@ int fme_pred_inter_b(fme_ctx* c, const fme_pu_req_b* reqs, fme_pu_res_b* res, in
     c->n_keys = key_total;
     HIP_TRY(c->d_bikey.reserve(keyt.size()));
     HIP_TRY(hipMemcpyAsync(c->d_bikey.p, keyt.data(), keyt.size() * sizeof(BiKeyTask), hipMemcpyHostToDevice, s));
-    BiKeyArgs ka{c->d_bikey.p, c->d_pics.p, c->d_keys.p, (int32_t)keyt.size()};
+    HIP_TRY(hipMemsetAsync(c->d_key_invalid.p, 0, sizeof(int32_t), s));
+    BiKeyArgs ka{c->d_bikey.p, c->d_pics.p, c->d_keys.p, (int32_t)keyt.size(), nullptr, (int64_t)key_total};
     HIP_TRY(launch_bi_key(ka, s));
     rc = tz_run_host(c, bj.data(), be.data(), nullptr, (int)bj.size(), stream, nullptr);
     if (rc) return rc;

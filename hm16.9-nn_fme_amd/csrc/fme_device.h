@@ -74,6 +74,8 @@ struct BiKeyArgs {
   const PicDesc* pics;
   int16_t* keys;
   int32_t n;
+  int32_t* invalid;           // device-resident requests: validated here, rejected ones counted
+  int64_t n_keys;             // (then) the key buffer's length
 };
 hipError_t launch_bi_key(const BiKeyArgs& a, hipStream_t s);
 
@@ -90,6 +92,8 @@ struct BatchArgs {
   int32_t use_hadamard;
   int32_t fen;
   int32_t nn_mode;
+  const int32_t* key_invalid; // > 0: the last device-built keys had invalid requests; batches
+                              // whose jobs read keys are rejected (k_classify)
 };
 
 struct Schedule;

@@ -107,6 +107,8 @@ __global__ __launch_bounds__(kBlock) void k_classify(BatchArgs a, WorkBufs w) {
     const int i = base + q * kBlock + tid;
     if (i < a.n) jb[q] = a.jobs[i];
   }
+  __shared__ int32_t keys_bad;
+  if (tid == 0) keys_bad = a.key_invalid ? *a.key_invalid : 0;
   lut[tid] = kClassLut.v[tid];
   if (tid < FME_MAX_PICTURES) {
     const PicDesc p = a.pics[tid];
@@ -130,7 +132,7 @@ __global__ __launch_bounds__(kBlock) void k_classify(BatchArgs a, WorkBufs w) {
       bool ok = j.ref_id < FME_MAX_PICTURES && j.lambda_id < FME_MAX_LAMBDAS && pic_w[j.ref_id] >= 0;
       if (ok) {
         if (j.key_offset >= 0) {
-          ok = (int64_t)j.key_offset + (int64_t)j.w * j.h <= a.n_keys;
+          ok = (int64_t)j.key_offset + (int64_t)j.w * j.h <= a.n_keys && keys_bad == 0;
         } else {
           ok = j.org_id < FME_MAX_PICTURES && pic_w[j.org_id] >= 0 &&
                (int)j.x + j.w <= pic_w[j.org_id] && (int)j.y + j.h <= pic_h[j.org_id];

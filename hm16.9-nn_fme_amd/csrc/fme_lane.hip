@@ -26,6 +26,8 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <type_traits>
+#include <utility>
 
 #include "fme_device.h"
 #include "fme_simd.h"
@@ -41,7 +43,7 @@
 // shared first stages save more issue slots than the extra live key - pred array costs at
 // 2 waves/SIMD (FME_LANE_WAVES 3 spills: 1.480 ms).
 #ifndef FME_LANE_QPAIR
-#define FME_LANE_QPAIR 2
+#define FME_LANE_QPAIR 1
 #endif
 #ifndef FME_LANE_HPAIR
 #define FME_LANE_HPAIR 2
@@ -49,14 +51,22 @@
 #ifndef FME_LANE_PAIR84   // 1: the 8x4 unit shape paired too
 #define FME_LANE_PAIR84 0
 #endif
+// Each PU class's search is its own function (noinline): inlined into one switch, the classes'
+// hoisted constants and live ranges merged into one allocation that spilled (1,286 VGPRs and
+// 2,098 SGPRs at 3 waves/SIMD) although every class alone fits.
+#ifndef FME_LANE_UNIT_ATTR
+#define FME_LANE_UNIT_ATTR __attribute__((noinline))
+#endif
 // occupancy target (waves per SIMD) that bounds the register allocation
 #ifndef FME_LANE_WAVES
-#define FME_LANE_WAVES 2
+#define FME_LANE_WAVES 3
 #endif
 
 namespace fme {
 namespace {
 using namespace simd;
+
+#define FME_AI __attribute__((always_inline))
 
 constexpr int kLaneNT = 256;
 
@@ -81,7 +91,15 @@ __device__ __forceinline__ uint32_t group_sum(uint32_t v) {
   return v;
 }
 
-__host__ __device__ constexpr int pow2_at_least(int v) { return v <= 1 ? 1 : 2 * pow2_at_least((v + 1) / 2); }
+template <int I, int N, class F>
+__device__ __forceinline__ void static_for(F&& f) {
+  if constexpr (I < N) {
+    f(std::integral_constant<int, I>{});
+    static_for<I + 1, N>(f);
+  }
+}
+
+__host__ __device__ __forceinline__ constexpr int pow2_at_least(int v) { return v <= 1 ? 1 : 2 * pow2_at_least((v + 1) / 2); }
 
 // low 16 bits of a and b -> one packed pair (a in the low half)
 __device__ __forceinline__ uint32_t pack2(int a, int b) { return __builtin_amdgcn_perm((uint32_t)b, (uint32_t)a, 0x05040100u); }
@@ -160,41 +178,112 @@ struct KeySrc {
 };
 
 // ---- distortion of one unit for one candidate ------------------------------------------------
-// X[c][j]: key - pred, column c, rows (2j, 2j+1) packed.  Sum over the unit's T x T tiles of
-// xCalcHADs (had) or SAD.
-template <int UW, int UH, int T>
-__device__ __forceinline__ uint32_t unit_dist(uint32_t (&X)[UW][UH / 2], bool had) {
+// How a lane's unit is scored: SATD (had) or SAD, and, for the 4x8 units of an 8x8-tiled PU, the
+// lane pair that shares each 8x8 tile (sgn: +1 / -1 per half in the even / odd lane; emask: ~0 in
+// the even lane, which reports the tile, 0 in the odd one).
+struct Metric {
+  bool had;
+  uint32_t sgn, emask;
+};
+
+// One 8x8 SATD tile split over a lane pair: the even lane holds columns 0..3, the odd lane columns
+// 4..7 (X[c][j]: this lane's column c, rows 2j, 2j+1).  xCalcHADs8x8's butterflies
+// (TComRdCost.cpp:1330-1425) with the column-distance-4 stage across the pair (DPP quad_perm
+// [1,0,3,2]); the odd lane forms b - a instead of a - b, and since every later stage is linear and
+// the transform ends in |.|, that sign never shows.  Returns this lane's sum of the last stage's
+// max terms (see satd_packed).
+__device__ __forceinline__ uint32_t satd8_pair(uint32_t (&X)[4][4], uint32_t sgn) {
+#pragma unroll
+  for (int c = 0; c < 4; c++)
+#pragma unroll
+    for (int j = 0; j < 4; j++) X[c][j] = pk(up(dpp<0xB1>(X[c][j])) * up(sgn) + up(X[c][j]));
+#pragma unroll
+  for (int d = 2; d >= 1; d >>= 1)
+#pragma unroll
+    for (int c = 0; c < 4; c++)
+      if ((c & d) == 0)
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+          const uint32_t a = X[c][j], b = X[c + d][j];
+          X[c][j] = pk_add(a, b);
+          X[c + d][j] = pk_sub(a, b);
+        }
+#pragma unroll
+  for (int d = 2; d >= 1; d >>= 1)
+#pragma unroll
+    for (int c = 0; c < 4; c++)
+#pragma unroll
+      for (int j = 0; j < 4; j++)
+        if ((j & d) == 0) {
+          const uint32_t a = X[c][j], b = X[c][j + d];
+          X[c][j] = pk_add(a, b);
+          X[c][j + d] = pk_sub(a, b);
+        }
   uint32_t s = 0;
 #pragma unroll
-  for (int ty = 0; ty < UH / T; ty++)
+  for (int c = 0; c < 4; c += 2)
 #pragma unroll
-    for (int tx = 0; tx < UW / T; tx++) {
-      uint32_t Y[T][T / 2];
-#pragma unroll
-      for (int c = 0; c < T; c++)
-#pragma unroll
-        for (int j = 0; j < T / 2; j++) Y[c][j] = X[tx * T + c][ty * (T / 2) + j];
-      if (had) {
-        s += satd_packed<T>(Y);
-      } else {
-        s += sad_packed<T>(Y);
-      }
+    for (int j = 0; j < 4; j++) {
+      const uint32_t a = pk_abs(X[c][j]), b = pk_abs(X[c + 1][j]);
+      const uint32_t los = __builtin_amdgcn_perm(b, a, 0x05040100u);
+      const uint32_t his = __builtin_amdgcn_perm(b, a, 0x07060302u);
+      const v2s m = __builtin_elementwise_max(up(los), up(his));
+      s = udot2(pk(m), 0x00010001u, s);
     }
   return s;
 }
 
+// X[c][j]: key - pred, column c, rows (2j, 2j+1) packed.  Sum over the unit's T x T tiles of
+// xCalcHADs (had) or SAD; for a unit that is half of an 8x8 tile (UW 4, T 8) the even lane
+// returns the tile's value and the odd lane 0.
+template <int UW, int UH, int T>
+__device__ __forceinline__ uint32_t unit_dist(uint32_t (&X)[UW][UH / 2], const Metric& m) {
+  if constexpr (T == 8 && UW == 4) {
+    static_assert(UH == 8, "4x8 half tiles");
+    if (m.had) {
+      uint32_t s = satd8_pair(X, m.sgn);
+      s += dpp<0xB1>(s);                 // the tile's total in both lanes
+      return ((s + 1) >> 1) & m.emask;   // (2s + 2) >> 2
+    }
+    uint32_t s = 0;
+#pragma unroll
+    for (int c = 0; c < UW; c++)
+#pragma unroll
+      for (int j = 0; j < UH / 2; j++) s = udot2(pk_abs(X[c][j]), 0x00010001u, s);
+    return s;
+  } else {
+    uint32_t s = 0;
+#pragma unroll
+    for (int ty = 0; ty < UH / T; ty++)
+#pragma unroll
+      for (int tx = 0; tx < UW / T; tx++) {
+        uint32_t Y[T][T / 2];
+#pragma unroll
+        for (int c = 0; c < T; c++)
+#pragma unroll
+          for (int j = 0; j < T / 2; j++) Y[c][j] = X[tx * T + c][ty * (T / 2) + j];
+        if (m.had) {
+          s += satd_packed<T>(Y);
+        } else {
+          s += sad_packed<T>(Y);
+        }
+      }
+    return s;
+  }
+}
+
 // Candidate offsets (xPatternRefinement tables, TEncSearch.cpp:212-236).
-__host__ __device__ constexpr int h9_dx(int i) { return (i == 3 || i == 5 || i == 7) ? -1 : ((i == 4 || i == 6 || i == 8) ? 1 : 0); }
-__host__ __device__ constexpr int h9_dy(int i) { return (i == 1 || i == 5 || i == 6) ? -1 : ((i == 2 || i == 7 || i == 8) ? 1 : 0); }
-__host__ __device__ constexpr int q9_dx(int i) { return (i == 3 || i == 5 || i == 7) ? -1 : ((i == 4 || i == 6 || i == 8) ? 1 : 0); }
-__host__ __device__ constexpr int q9_dy(int i) { return (i == 1 || i == 3 || i == 4) ? -1 : ((i == 2 || i == 7 || i == 8) ? 1 : 0); }
+__host__ __device__ __forceinline__ constexpr int h9_dx(int i) { return (i == 3 || i == 5 || i == 7) ? -1 : ((i == 4 || i == 6 || i == 8) ? 1 : 0); }
+__host__ __device__ __forceinline__ constexpr int h9_dy(int i) { return (i == 1 || i == 5 || i == 6) ? -1 : ((i == 2 || i == 7 || i == 8) ? 1 : 0); }
+__host__ __device__ __forceinline__ constexpr int q9_dx(int i) { return (i == 3 || i == 5 || i == 7) ? -1 : ((i == 4 || i == 6 || i == 8) ? 1 : 0); }
+__host__ __device__ __forceinline__ constexpr int q9_dy(int i) { return (i == 1 || i == 3 || i == 4) ? -1 : ((i == 2 || i == 7 || i == 8) ? 1 : 0); }
 // Q9 index of (dqx, dqy)
-__host__ __device__ constexpr int q9_index(int dx, int dy) {
+__host__ __device__ __forceinline__ constexpr int q9_index(int dx, int dy) {
   return dy == 0 ? (dx == 0 ? 0 : (dx < 0 ? 5 : 6)) : dy < 0 ? (dx == 0 ? 1 : (dx < 0 ? 3 : 4)) : (dx == 0 ? 2 : (dx < 0 ? 7 : 8));
 }
 // EMI positions: 0 centre, then TL, T, TR, L, R, BL, B, BR (xTZ8PointSquareSearch order)
-__host__ __device__ constexpr int emi_dx(int p) { return (p == 1 || p == 4 || p == 6) ? -1 : ((p == 3 || p == 5 || p == 8) ? 1 : 0); }
-__host__ __device__ constexpr int emi_dy(int p) { return p >= 1 && p <= 3 ? -1 : (p >= 6 ? 1 : 0); }
+__host__ __device__ __forceinline__ constexpr int emi_dx(int p) { return (p == 1 || p == 4 || p == 6) ? -1 : ((p == 3 || p == 5 || p == 8) ? 1 : 0); }
+__host__ __device__ __forceinline__ constexpr int emi_dy(int p) { return p >= 1 && p <= 3 ? -1 : (p >= 6 ? 1 : 0); }
 
 // =============================================================================================
 // Candidate passes of one unit.  v: re-centred window (rows -4..UH+3, cols -4..UW+3, s - 128
@@ -225,7 +314,7 @@ __device__ __forceinline__ void take_qtr(int i, uint32_t part, uint32_t live, do
 // (0,0), (0,-1), (0,1)
 template <int UW, int UH, int T, int HPM>
 __device__ __forceinline__ void half_center(uint32_t (&v)[UH + 8][UW / 4 + 2], const KeySrc<UW, UH / 2>& K,
-                                            bool had, uint32_t (&d)[3]) {
+                                            const Metric& had, uint32_t (&d)[3]) {
   constexpr int RV = UH + 8, UJ = UH / 2;
   uint32_t c2lo, c2hi;
   taps8(2, c2lo, c2hi);
@@ -240,7 +329,7 @@ __device__ __forceinline__ void half_center(uint32_t (&v)[UH + 8][UW / 4 + 2], c
   }
   launder(v);
   // (0,-1), (0,1): vertical half-pel on integer columns (transposed window')
-  auto vpass = [&](auto sel_c) {   // sel 1: (0,-1) only, 2: (0,1) only, 3: both
+  auto vpass = [&](auto sel_c) FME_AI {   // sel 1: (0,-1) only, 2: (0,1) only, 3: both
     constexpr int sel = decltype(sel_c)::value;
     uint32_t X1[UW][UJ], X2[UW][UJ];
 #pragma unroll
@@ -286,7 +375,7 @@ __device__ __forceinline__ void half_center(uint32_t (&v)[UH + 8][UW / 4 + 2], c
 // (s,0), (s,-1), (s,1) for s = -1 (SIDE 0: half column x) or +1 (SIDE 1: half column x+1)
 template <int UW, int UH, int T, int SIDE, int HPM>
 __device__ __forceinline__ void half_side(uint32_t (&v)[UH + 8][UW / 4 + 2], const KeySrc<UW, UH / 2>& K,
-                                          bool had, uint32_t (&d)[3]) {
+                                          const Metric& had, uint32_t (&d)[3]) {
   constexpr int RV = UH + 8, UJ = UH / 2;
   uint32_t c2lo, c2hi;
   taps8(2, c2lo, c2hi);
@@ -307,7 +396,7 @@ __device__ __forceinline__ void half_side(uint32_t (&v)[UH + 8][UW / 4 + 2], con
   }
   launder(v);
   // (s,-1), (s,1): 2-D half-pel (first stage rows -4..UH+3 of half column jc, then vertical)
-  auto dpass = [&](auto sel_c) {   // sel 1: (s,-1) only, 2: (s,1) only, 3: both
+  auto dpass = [&](auto sel_c) FME_AI {   // sel 1: (s,-1) only, 2: (s,1) only, 3: both
     constexpr int sel = decltype(sel_c)::value;
     const uint32_t c16[4] = {p16(-1, 4), p16(-11, 40), p16(40, -11), p16(4, -1)};
     const uint32_t c16o[5] = {p16(0, -1), p16(4, -11), p16(40, 40), p16(-11, 4), p16(-1, 0)};
@@ -359,27 +448,27 @@ __device__ __forceinline__ void half_side(uint32_t (&v)[UH + 8][UW / 4 + 2], con
 // with {0,0,0,64,0,0,0,0}, which equals HM's copy / 1-D paths after rounding.
 // QM 2: five passes, (k, l) = (0: 0,1) (0: 2) (1: 0,2) (2: 0,1) (2: 2); QM 1: eight, (k, l) for
 // k, l in 0..2 without (1,1).
-template <int QM> __host__ __device__ constexpr int qp_passes() { return QM == 2 ? 5 : 8; }
-template <int QM> __host__ __device__ constexpr int qp_k(int ps) {
+template <int QM> __host__ __device__ __forceinline__ constexpr int qp_passes() { return QM == 2 ? 5 : 8; }
+template <int QM> __host__ __device__ __forceinline__ constexpr int qp_k(int ps) {
   return QM == 2 ? (ps < 2 ? 0 : (ps == 2 ? 1 : 2)) : (ps + (ps >= 4 ? 1 : 0)) / 3;
 }
-template <int QM> __host__ __device__ constexpr int qp_l0(int ps) {
+template <int QM> __host__ __device__ __forceinline__ constexpr int qp_l0(int ps) {
   return QM == 2 ? ((ps == 1 || ps == 4) ? 2 : 0) : (ps + (ps >= 4 ? 1 : 0)) % 3;
 }
-template <int QM> __host__ __device__ constexpr int qp_l1(int ps) {
+template <int QM> __host__ __device__ __forceinline__ constexpr int qp_l1(int ps) {
   return QM == 2 ? (ps == 0 ? 1 : (ps == 2 ? 2 : (ps == 3 ? 1 : -1))) : -1;
 }
 // Q9 index of pass ps's first / second candidate
-template <int QM> __host__ __device__ constexpr int qp_idx0(int ps) {
+template <int QM> __host__ __device__ __forceinline__ constexpr int qp_idx0(int ps) {
   return q9_index(qp_k<QM>(ps) - 1, qp_l0<QM>(ps) - 1);
 }
-template <int QM> __host__ __device__ constexpr int qp_idx1(int ps) {
+template <int QM> __host__ __device__ __forceinline__ constexpr int qp_idx1(int ps) {
   return qp_l1<QM>(ps) < 0 ? -1 : q9_index(qp_k<QM>(ps) - 1, qp_l1<QM>(ps) - 1);
 }
 
 template <int UW, int UH, int T, int QM, int PS>
 __device__ __forceinline__ void qtr_pass(uint32_t (&v)[UH + 8][UW / 4 + 2], const KeySrc<UW, UH / 2>& K,
-                                         bool had, int hx, int hy, uint32_t (&d)[2]) {
+                                         const Metric& had, int hx, int hy, uint32_t (&d)[2]) {
   constexpr int RV = UH + 8, UJ = UH / 2;
   constexpr int k = qp_k<QM>(PS);
   constexpr int NP = qp_l1<QM>(PS) < 0 ? 1 : 2;
@@ -428,246 +517,230 @@ __device__ __forceinline__ void qtr_pass(uint32_t (&v)[UH + 8][UW / 4 + 2], cons
   d[1] = NP > 1 ? unit_dist<UW, UH, T>(XQ[NP - 1], had) : 0u;
 }
 
-template <int L, int UW, int UH, int T, int QM, int... PS>
-__device__ __forceinline__ void qtr_all(uint32_t (&v)[UH + 8][UW / 4 + 2], const KeySrc<UW, UH / 2>& K,
-                                        bool had, uint32_t live, int hx, int hy, double ml, int mvx, int mvy, int px,
-                                        int py, uint32_t& best, int& bi, std::integer_sequence<int, PS...>) {
-  auto one = [&](auto ps_c) {
-    constexpr int ps = decltype(ps_c)::value;
-    uint32_t d[2];
-    qtr_pass<UW, UH, T, QM, ps>(v, K, had, hx, hy, d);
-    take_qtr<L>(qp_idx0<QM>(ps), d[0], live, ml, mvx, mvy, hx, hy, px, py, best, bi);
-    if constexpr (qp_l1<QM>(ps) >= 0) take_qtr<L>(qp_idx1<QM>(ps), d[1], live, ml, mvx, mvy, hx, hy, px, py, best, bi);
-  };
-  (one(std::integral_constant<int, PS>{}), ...);
-}
-
 typedef uint32_t u32x4a __attribute__((ext_vector_type(4), aligned(4)));
+typedef uint32_t u32x3a __attribute__((ext_vector_type(3), aligned(4)));
 typedef uint32_t u32x2a __attribute__((ext_vector_type(2), aligned(4)));
 typedef __attribute__((address_space(1))) const u32x4a gu4;
+typedef __attribute__((address_space(1))) const u32x3a gu3;
 typedef __attribute__((address_space(1))) const u32x2a gu2;
-typedef __attribute__((address_space(1))) const uint16_t gu16;
 
-// N dwords of picture row `row` from byte xb (4-aligned); edge-replicated when not inside.
+// N dwords from byte address p, any alignment (gfx950 runs global memory in unaligned access
+// mode; tools/probes/unaligned_probe.hip checks it on the box).
 template <int N>
-__device__ __forceinline__ void load_row(const uint8_t* row, int xb, int width, bool inside, uint32_t (&out)[N]) {
-  if (inside) {
-    const uint8_t* p = row + xb;
-    int k = 0;
+__device__ __forceinline__ void ld_bytes(const void* p, uint32_t (&o)[N]) {
+  const uint8_t* q = (const uint8_t*)p;
+  constexpr int K4 = N / 4 * 4;
 #pragma unroll
-    for (; k + 4 <= N; k += 4) {
-      const u32x4a v = *(gu4*)(p + 4 * k);
-      out[k] = v.x; out[k + 1] = v.y; out[k + 2] = v.z; out[k + 3] = v.w;
-    }
-#pragma unroll
-    for (; k + 2 <= N; k += 2) {
-      const u32x2a v = *(gu2*)(p + 4 * k);
-      out[k] = v.x; out[k + 1] = v.y;
-    }
-#pragma unroll
-    for (; k < N; k++) out[k] = gld32(p + 4 * k);
-  } else {
-#pragma unroll
-    for (int k = 0; k < N; k++) {
-      uint32_t v = 0;
-#pragma unroll
-      for (int b = 0; b < 4; b++) v |= gld8(row + clamp_i(xb + 4 * k + b, 0, width - 1)) << (8 * b);
-      out[k] = v;
-    }
+  for (int k = 0; k < K4; k += 4) {
+    const u32x4a v = *(gu4*)(q + 4 * k);
+    o[k] = v.x; o[k + 1] = v.y; o[k + 2] = v.z; o[k + 3] = v.w;
+  }
+  if constexpr (N - K4 == 3) {
+    const u32x3a v = *(gu3*)(q + 4 * K4);
+    o[K4] = v.x; o[K4 + 1] = v.y; o[K4 + 2] = v.z;
+  } else if constexpr (N - K4 == 2) {
+    const u32x2a v = *(gu2*)(q + 4 * K4);
+    o[K4] = v.x; o[K4 + 1] = v.y;
+  } else if constexpr (N - K4 == 1) {
+    o[K4] = gld32(q + 4 * K4);
   }
 }
 
+// Rows y0 .. y0+R-1, 4N bytes from column x0 of a picture, as (sample - 128) bytes, with HM's
+// padded-picture semantics (TComPicYuv::extendPicBorder): rows and columns clamped to the
+// picture.  Away from the left / right edges each row is one unaligned load; near them each dword
+// is read at the clamped run xa = clamp(x, 0, W-4) and v_perm picks the replicated bytes.
+template <int R, int N>
+__device__ __forceinline__ void load_window(const PicDesc& pic, int x0, int y0, uint32_t (&v)[R][N]) {
+  // opaque origin: the row / column clamps are not shared across calls (hoisted out of a pass
+  // loop they stay live, and spill, for the whole search)
+  asm volatile("" : "+v"(x0), "+v"(y0));
+  const bool inside = x0 >= 0 && x0 + 4 * N <= pic.width;
+  if (inside) {
+#pragma unroll
+    for (int r = 0; r < R; r++) {
+      const int yy = clamp_i(y0 + r, 0, pic.height - 1);
+      ld_bytes<N>(pic.luma + (size_t)yy * pic.stride + x0, v[r]);
+      // row addresses four at a time: every load is still in flight before the first use, but
+      // the scheduler does not keep R 64-bit addresses live at once
+      if ((r & 3) == 3) __builtin_amdgcn_sched_barrier(0);
+    }
+  } else {
+    int xa[N];
+    uint32_t sel[N];
+#pragma unroll
+    for (int k = 0; k < N; k++) {
+      xa[k] = clamp_i(x0 + 4 * k, 0, pic.width - 4);
+      sel[k] = 0;
+#pragma unroll
+      for (int i = 0; i < 4; i++) sel[k] |= (uint32_t)(clamp_i(x0 + 4 * k + i, 0, pic.width - 1) - xa[k]) << (8 * i);
+    }
+#pragma unroll
+    for (int r = 0; r < R; r++) {
+      const uint8_t* row = pic.luma + (size_t)clamp_i(y0 + r, 0, pic.height - 1) * pic.stride;
+#pragma unroll
+      for (int k = 0; k < N; k++) {
+        uint32_t t[1];
+        ld_bytes<1>(row + xa[k], t);
+        v[r][k] = __builtin_amdgcn_perm(0u, t[0], sel[k]);
+      }
+      if ((r & 3) == 3) __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < R; r++)
+#pragma unroll
+    for (int k = 0; k < N; k++) v[r][k] ^= 0x80808080u;
+}
+
 // =============================================================================================
-// One lane: unit (ux, uy) of PU p of class (PW x PH), unit UW x UH.
+// One lane: unit (ux, uy) of PU p of class (PW x PH), unit UW x UH (4x8, or 8x4 for the shapes
+// whose height is not a multiple of 8).  PUs of more than 64 units (48x64, 64x48, 64x64) give a
+// lane two units, one in the top and one in the bottom half of the PU: every candidate pass then
+// runs once per half, with the other half's window and key re-loaded (L1 / L2 hits).
 // =============================================================================================
 template <int PW, int PH, int UW, int UH>
-__device__ __forceinline__ void lane_unit(const BatchArgs& a, const fme_job* __restrict__ sjobs,
+__device__ FME_LANE_UNIT_ATTR void lane_unit(const BatchArgs& a, const fme_job* __restrict__ sjobs,
                                           const int32_t* __restrict__ perm, int cls_off, int cls_cnt,
                                           int wt) {
   constexpr int T = ((PW % 8) == 0 && (PH % 8) == 0) ? 8 : 4;
-  // pair modes per unit shape: the 8x4 units spill with paired passes (144 B/lane), the others not
-  constexpr bool k84 = UH == 4 && !FME_LANE_PAIR84;
+  static_assert((T == 8 && UW == 4 && UH == 8) || (T == 4 && UW == 4 && UH == 4) || (T == 4 && UW * UH == 32),
+                "4x8 units (a lane pair per 8x8 SATD tile) or 4x4 units (one 4x4 tile per lane)");
+  constexpr bool k84 = UW == 8 && UH == 4 && !FME_LANE_PAIR84;
   constexpr int kQP = k84 ? 1 : FME_LANE_QPAIR, kHP = k84 ? 1 : FME_LANE_HPAIR;
-  static_assert(UW % T == 0 && UH % T == 0, "unit must hold whole SATD tiles");
   static_assert(PW % UW == 0 && PH % UH == 0, "units tile the PU");
-  constexpr int UX = PW / UW, LR = UX * (PH / UH);   // units of the PU
-  constexpr int L = pow2_at_least(LR);                // lanes of its group (AMP: 6 -> 8, 12 -> 16, 48 -> 64)
+  constexpr int UX = PW / UW, UY = PH / UH, NU = UX * UY;
+  constexpr int UPL = NU > 64 ? 2 : 1;                // units per lane
+  constexpr int UYH = UY / UPL, NUH = UX * UYH;       // unit rows / units per half
+  static_assert(UPL == 1 || UY % 2 == 0, "halves of whole unit rows");
+  constexpr int L = pow2_at_least(NUH);               // lanes of the PU's group (AMP: 6 -> 8, 24 -> 32, 48 -> 64)
   static_assert(L <= 64, "a PU's group fits one wave");
+  static_assert(T == 4 || UX % 2 == 0, "an 8x8 tile's two units sit in lanes 2k, 2k+1");
   // the modified setDistParam's integer metric (TComRdCost.cpp:200-230): SAD for W in {12, 24, 48},
   // with xTZSearchHelp's FEN row subsampling (TEncSearch.cpp:1158-1164); SSE otherwise
   constexpr bool kSadEmi = PW == 12 || PW == 24 || PW == 48;
-  constexpr int RW = UH + 10;                 // window rows (-5 .. UH+4)
-  constexpr int NWL = (UW + 13 + 3) / 4;      // dwords loaded per row (any start alignment)
-  constexpr int NW = (UW + 10 + 3) / 4;       // dwords per row after re-alignment
   constexpr int RV = UH + 8;                  // re-centred window rows (-4 .. UH+3)
   constexpr int NV = UW / 4 + 2;              // re-centred dwords per row (cols -4 .. UW+3)
   constexpr int UJ = UH / 2;                  // packed row pairs per column
+  constexpr int EW = (UW + 2 + 3) / 4;        // EMI window dwords per row (cols -1 .. UW)
+  constexpr int KW = UW / 2;                  // key dwords per row (bytes: UW / 4 used; int16 pairs: UW / 2)
 
-  const int gl = wt * 64 + ((int)threadIdx.x & 63);   // wave tile wt: 64 lanes = 64 / L PUs
+  const int lane = (int)threadIdx.x & 63;
+  const int gl = wt * 64 + lane;               // wave tile wt: 64 lanes = 64 / L PUs
   int p = gl / L;
   const int u = gl - p * L;
   const bool active = p < cls_cnt;
   if (!active) p = cls_cnt - 1;              // duplicate work, no stores (keeps the group whole)
-  const uint32_t live = u < LR ? ~0u : 0u;   // padding lanes repeat the last unit, summed as 0
-  const int uu = u < LR ? u : LR - 1;
+  const uint32_t live = u < NUH ? ~0u : 0u;  // padding lanes repeat the last unit, summed as 0
+  const int uu = u < NUH ? u : NUH - 1;
   const int ux = uu % UX, uy = uu / UX;
 
   const fme_job j = sjobs[cls_off + p];
   const int jid = perm[cls_off + p];
   const PicDesc ref = a.pics[j.ref_id];
   const double ml = a.mlambda[j.lambda_id];
-  const bool had = a.use_hadamard && !(j.flags & FME_JOB_LOSSLESS);
+  const Metric met = {a.use_hadamard && !(j.flags & FME_JOB_LOSSLESS), (lane & 1) ? 0xFFFFFFFFu : 0x00010001u,
+                      (lane & 1) ? 0u : ~0u};
   const bool kbuf = j.key_offset >= 0;
-  const int ox = (int)j.x + ux * UW, oy = (int)j.y + uy * UH;   // unit origin
+  const int ox = (int)j.x + ux * UW, oy = (int)j.y + uy * UH;   // unit origin (top half)
+  constexpr int kHalfRows = UYH * UH;                             // bottom half: oy + kHalfRows
   const int mvp_x = j.mvp_x, mvp_y = j.mvp_y;
 
-  // ---- 1. loads ------------------------------------------------------------------------------
-  uint32_t w[RW][NW];
-  {
-    const int px0 = ox + j.mv_x - 5, py0 = oy + j.mv_y - 5;
-    const int xb = px0 & ~3;
-    const uint32_t s0 = (uint32_t)(px0 - xb);
-    const bool inside = xb >= 0 && xb + 4 * NWL <= ref.width;
-    uint32_t raw[RW][NWL];
+  // key rows of half h, row-major: org bytes (s - 128) in kraw[r][0 .. UW/4) (uni-pred), or the
+  // job's int16 key pairs (cols 2k, 2k+1) in kraw[r][0 .. UW/2)
+  auto load_kraw = [&](int h, uint32_t (&kraw)[UH][KW]) FME_AI {
+    int ky = oy + h * kHalfRows;
+    asm volatile("" : "+v"(ky));   // not shared across calls (see load_window)
+    if (!kbuf) {
+      const PicDesc org = a.pics[j.org_id];
 #pragma unroll
-    for (int r = 0; r < RW; r++) {
-      const int yy = clamp_i(py0 + r, 0, ref.height - 1);
-      load_row<NWL>(ref.luma + (size_t)yy * ref.stride, xb, ref.width, inside, raw[r]);
-    }
+      for (int r = 0; r < UH; r++) {
+        uint32_t t[UW / 4];
+        ld_bytes<UW / 4>(org.luma + (size_t)(ky + r) * org.stride + ox, t);
 #pragma unroll
-    for (int r = 0; r < RW; r++)
+        for (int k = 0; k < UW / 4; k++) kraw[r][k] = t[k] ^ 0x80808080u;
 #pragma unroll
-      for (int k = 0; k < NW; k++) w[r][k] = __builtin_amdgcn_alignbyte(raw[r][k + 1], raw[r][k], s0) ^ 0x80808080u;
-  }
-  // key block, one register array for either form: org bytes (s - 128) in kraw[r][0 .. UW/4)
-  // (uni-pred), or the job's int16 key pairs (cols 2k, 2k+1) in kraw[r][0 .. UW/2)
-  uint32_t kraw[UH][UW / 2];
-  if (!kbuf) {
-    const PicDesc org = a.pics[j.org_id];
-#pragma unroll
-    for (int r = 0; r < UH; r++) {
-      const uint8_t* q = org.luma + (size_t)(oy + r) * org.stride + ox;
-      if constexpr (UW == 8) {
-        const u32x2a ov = *(gu2*)q;
-        kraw[r][0] = ov.x ^ 0x80808080u;
-        kraw[r][1] = ov.y ^ 0x80808080u;
-      } else {
-        kraw[r][0] = gld32(q) ^ 0x80808080u;
+        for (int k = UW / 4; k < KW; k++) kraw[r][k] = 0;
       }
+    } else {
+      const int16_t* kb = a.keys + (size_t)j.key_offset + (size_t)(ky - (int)j.y) * PW + ux * UW;
 #pragma unroll
-      for (int k = UW / 4; k < UW / 2; k++) kraw[r][k] = 0;
+      for (int r = 0; r < UH; r++) ld_bytes<KW>(kb + r * PW, kraw[r]);
     }
-  } else {
-    const int16_t* kb = a.keys + (size_t)j.key_offset + (size_t)(uy * UH) * PW + ux * UW;
-#pragma unroll
-    for (int r = 0; r < UH; r++)
-#pragma unroll
-      for (int k = 0; k < UW / 2; k++) {
-        const uint32_t lo = *(gu16*)(kb + r * PW + 2 * k), hi = *(gu16*)(kb + r * PW + 2 * k + 1);
-        kraw[r][k] = lo | (hi << 16);
-      }
-  }
+  };
 
-  // ---- 2. EMI square step -----------------------------------------------------------------------
+  // ---- 1. EMI square step -----------------------------------------------------------------------
   int mvx = j.mv_x, mvy = j.mv_y;
   int ex = 0, ey = 0, n_emi = 0;
   uint32_t cval = 0, emi[8];
 #pragma unroll
   for (int k = 0; k < 8; k++) emi[k] = 0;
   if (j.flags & FME_JOB_EMI) {
-    // Row-major: window row R (= 5 + dy + r) serves positions (dx, dy) with org row r = R-5-dy;
-    // its byte groups at dx = -1, 0, 1 are formed once.
     uint32_t e9[9];
-    if constexpr (kSadEmi) {   // SAD of the (even, with FEN) rows, doubled when subsampled
-      const bool sub = a.fen == 1 || a.fen == 3;   // and PH > 8: every 12/24/48-wide shape
 #pragma unroll
-      for (int q = 0; q < 9; q++) e9[q] = 0;
+    for (int q = 0; q < 9; q++) e9[q] = 0;
 #pragma unroll
-      for (int r = 0; r < UH; r++) {
-        if ((r & 1) && sub) continue;   // unit rows start on even PU rows
-#pragma unroll
-        for (int pos = 0; pos < 9; pos++) {
-          const int R = r + 5 + emi_dy(pos);
-#pragma unroll
-          for (int k = 0; k < UW / 4; k++) {
-            const uint32_t pv = rbytes(w[R], 5 + emi_dx(pos) + 4 * k) ^ 0x80808080u;   // samples 0..255
-            if (!kbuf) {
-              e9[pos] = __builtin_amdgcn_sad_u8(kraw[r][k] ^ 0x80808080u, pv, e9[pos]);
-            } else {   // int16 key: |key - pred| per sample
-              const int k0 = (int16_t)(kraw[r][2 * k] & 0xFFFF), k1 = (int16_t)(kraw[r][2 * k] >> 16);
-              const int k2 = (int16_t)(kraw[r][2 * k + 1] & 0xFFFF), k3 = (int16_t)(kraw[r][2 * k + 1] >> 16);
-              e9[pos] += (uint32_t)(abs(k0 - (int)(pv & 0xFF)) + abs(k1 - (int)((pv >> 8) & 0xFF)) +
-                                    abs(k2 - (int)((pv >> 16) & 0xFF)) + abs(k3 - (int)(pv >> 24)));
-            }
-          }
-        }
-        __builtin_amdgcn_sched_barrier(0);
-      }
-      if (sub) {
-#pragma unroll
-        for (int q = 0; q < 9; q++) e9[q] <<= 1;
-      }
-    } else if (!kbuf) {   // SSE = So2 - 2 Sop + Spp on the s - 128 bytes
-      int so2 = 0, sop[9], spp[3][3];   // spp[dx][dy]
-#pragma unroll
-      for (int i = 0; i < 9; i++) sop[i] = 0;
-#pragma unroll
-      for (int i = 0; i < 3; i++)
-#pragma unroll
-        for (int q = 0; q < 3; q++) spp[i][q] = 0;
+    for (int h = 0; h < UPL; h++) {
+      uint32_t kraw[UH][KW];
+      load_kraw(h, kraw);
+      // integer samples at rows -1 .. UH, cols -1 .. UW around the TZ MV (s - 128 bytes)
+      uint32_t w[UH + 2][EW];
+      load_window(ref, ox + mvx - 1, oy + h * kHalfRows + mvy - 1, w);
+      int so2 = 0;   // SSE's sum of squared key samples
 #pragma unroll
       for (int r = 0; r < UH; r++)
 #pragma unroll
         for (int k = 0; k < UW / 4; k++) so2 = dot4(kraw[r][k], kraw[r][k], so2);
+      // one position at a time, every array index a compile-time constant (a computed index
+      // sends the accumulators to scratch)
 #pragma unroll
-      for (int R = 4; R < UH + 6; R++) {
+      for (int pos = 0; pos < 9; pos++) {
+        const int dx = emi_dx(pos), dy = emi_dy(pos);
+        uint32_t e = 0;
+        if constexpr (kSadEmi) {   // SAD of the (even, with FEN) rows, doubled when subsampled
+          const bool sub = a.fen == 1 || a.fen == 3;   // and PH > 8: every 12/24/48-wide shape
 #pragma unroll
-        for (int dx = -1; dx <= 1; dx++)
+          for (int r = 0; r < UH; r++) {
+            if ((r & 1) && sub) continue;   // unit rows start on even PU rows
 #pragma unroll
-          for (int k = 0; k < UW / 4; k++) {
-            const uint32_t pv = rbytes(w[R], 5 + dx + 4 * k);
-            const int pp = dot4(pv, pv, 0);
-#pragma unroll
-            for (int dy = -1; dy <= 1; dy++) {
-              const int r = R - 5 - dy;
-              if (r < 0 || r >= UH) continue;
-              int pos = 0;
-#pragma unroll
-              for (int q = 0; q < 9; q++)
-                if (emi_dx(q) == dx && emi_dy(q) == dy) pos = q;
-              sop[pos] = dot4(kraw[r][k], pv, sop[pos]);
-              spp[dx + 1][dy + 1] += pp;
+            for (int k = 0; k < UW / 4; k++) {
+              const uint32_t pv = rbytes(w[r + 1 + dy], 1 + dx + 4 * k) ^ 0x80808080u;   // samples 0..255
+              if (!kbuf) {
+                e = __builtin_amdgcn_sad_u8(kraw[r][k] ^ 0x80808080u, pv, e);
+              } else {   // int16 key: |key - pred| per sample
+                const uint32_t d0 = pk_sub(kraw[r][2 * k], lo_pair(pv)), d1 = pk_sub(kraw[r][2 * k + 1], hi_pair(pv));
+                e = udot2(pk_abs(d1), 0x00010001u, udot2(pk_abs(d0), 0x00010001u, e));
+              }
             }
           }
-        __builtin_amdgcn_sched_barrier(0);
+        } else if (!kbuf) {   // SSE = So2 - 2 Sop + Spp on the s - 128 bytes
+          int sop = 0, spp = 0;
+#pragma unroll
+          for (int r = 0; r < UH; r++)
+#pragma unroll
+            for (int k = 0; k < UW / 4; k++) {
+              const uint32_t pv = rbytes(w[r + 1 + dy], 1 + dx + 4 * k);
+              sop = dot4(kraw[r][k], pv, sop);
+              spp = dot4(pv, pv, spp);
+            }
+          e = (uint32_t)(so2 - 2 * sop + spp);
+        } else {   // int16 key: sum of (key - pred)^2
+#pragma unroll
+          for (int r = 0; r < UH; r++)
+#pragma unroll
+            for (int k = 0; k < UW / 4; k++) {
+              const uint32_t x = rbytes(w[r + 1 + dy], 1 + dx + 4 * k) ^ 0x80808080u;   // samples 0..255
+              const uint32_t d0 = pk_sub(kraw[r][2 * k], lo_pair(x)), d1 = pk_sub(kraw[r][2 * k + 1], hi_pair(x));
+              e = (uint32_t)dot2(d1, d1, dot2(d0, d0, (int)e));
+            }
+        }
+        e9[pos] += e;
       }
+    }
+    if constexpr (kSadEmi) {
+      if (a.fen == 1 || a.fen == 3) {
 #pragma unroll
-      for (int q = 0; q < 9; q++) e9[q] = (uint32_t)(so2 - 2 * sop[q] + spp[emi_dx(q) + 1][emi_dy(q) + 1]);
-    } else {
-#pragma unroll
-      for (int q = 0; q < 9; q++) e9[q] = 0;
-#pragma unroll
-      for (int R = 4; R < UH + 6; R++) {
-#pragma unroll
-        for (int dx = -1; dx <= 1; dx++)
-#pragma unroll
-          for (int k = 0; k < UW / 4; k++) {
-            const uint32_t x = rbytes(w[R], 5 + dx + 4 * k) ^ 0x80808080u;   // samples 0..255
-            const uint32_t lo = lo_pair(x), hi = hi_pair(x);
-#pragma unroll
-            for (int dy = -1; dy <= 1; dy++) {
-              const int r = R - 5 - dy;
-              if (r < 0 || r >= UH) continue;
-              int pos = 0;
-#pragma unroll
-              for (int q = 0; q < 9; q++)
-                if (emi_dx(q) == dx && emi_dy(q) == dy) pos = q;
-              const uint32_t d0 = pk_sub(kraw[r][2 * k], lo);
-              const uint32_t d1 = pk_sub(kraw[r][2 * k + 1], hi);
-              e9[pos] = (uint32_t)dot2(d1, d1, dot2(d0, d0, (int)e9[pos]));
-            }
-          }
-        __builtin_amdgcn_sched_barrier(0);
+        for (int q = 0; q < 9; q++) e9[q] <<= 1;
       }
     }
 #pragma unroll
@@ -719,63 +792,82 @@ __device__ __forceinline__ void lane_unit(const BatchArgs& a, const fme_job* __r
     *(gw4*)(rec + 32) = q1;
     *(gw4*)(rec + 48) = q2;
   }
+  (void)ex;
+  (void)ey;
 
-  // ---- re-centre the window on mv_int': rows -4..UH+3, cols -4..UW+3 ---------------------------
+  // ---- the resident half: window rows -4..UH+3, cols -4..UW+3 around mv_int', and the key as
+  // signed int16 (key - 128) pairs K[c][j] = (row 2j, row 2j+1) of column c ----------------------
   uint32_t v[RV][NV];
-  {
-    const uint32_t sh = (uint32_t)(1 + ex);
-#pragma unroll
-    for (int r = 0; r < RV; r++) {
-      uint32_t srow[NV + 1];
-#pragma unroll
-      for (int k = 0; k <= NV; k++) srow[k] = ey < 0 ? w[r][k] : (ey == 0 ? w[r + 1][k] : w[r + 2][k]);
-#pragma unroll
-      for (int k = 0; k < NV; k++) v[r][k] = __builtin_amdgcn_alignbyte(srow[k + 1], srow[k], sh);
-    }
-  }
-
-  // ---- key as signed int16 (key - 128) pairs: K[c][j] = (row 2j, row 2j+1) of column c ------------
   KeySrc<UW, UJ> K;
+  auto load_half = [&](int h) FME_AI {
+    load_window(ref, ox + mvx - 4, oy + h * kHalfRows + mvy - 4, v);
+    uint32_t kraw[UH][KW];
+    load_kraw(h, kraw);
 #pragma unroll
-  for (int c = 0; c < UW; c++)
+    for (int c = 0; c < UW; c++)
 #pragma unroll
-    for (int jj = 0; jj < UJ; jj++) {
-      const uint32_t ko = sext_pair(kraw[2 * jj + 1][c >> 2], kraw[2 * jj][c >> 2], c & 3);
-      const uint32_t hs = (c & 1) ? 0x07060302u : 0x05040100u;   // 16-bit half c&1 of each row
-      const uint32_t kb = pk_sub(__builtin_amdgcn_perm(kraw[2 * jj + 1][c >> 1], kraw[2 * jj][c >> 1], hs), 0x00800080u);
-      K.set(c, jj, kbuf ? kb : ko);
+      for (int jj = 0; jj < UJ; jj++) {
+        const uint32_t ko = sext_pair(kraw[2 * jj + 1][c >> 2], kraw[2 * jj][c >> 2], c & 3);
+        const uint32_t hs = (c & 1) ? 0x07060302u : 0x05040100u;   // 16-bit half c&1 of each row
+        const uint32_t kb = pk_sub(__builtin_amdgcn_perm(kraw[2 * jj + 1][c >> 1], kraw[2 * jj][c >> 1], hs), 0x00800080u);
+        K.set(c, jj, kbuf ? kb : ko);
+      }
+  };
+  load_half(0);
+  int cur = 0;
+  // One candidate pass over the PU: the resident half first, then (two units per lane) the other.
+  auto over_halves = [&](auto&& pass, auto& d) FME_AI {
+    pass(d);
+    if constexpr (UPL == 2) {
+      cur ^= 1;
+      __builtin_amdgcn_sched_barrier(0);   // the other half's loads stay after this pass (one window live)
+      launder(v);
+      load_half(cur);
+      __builtin_amdgcn_sched_barrier(0);
+      std::remove_reference_t<decltype(d)> d2;
+      pass(d2);
+#pragma unroll
+      for (int m = 0; m < (int)(sizeof(d) / sizeof(d[0])); m++) d[m] += d2[m];
     }
+  };
 
-  // ---- 3. half-pel stage (H9 order: (0,0),(0,-1),(0,1),(-1,0),(1,0),(-1,-1),(1,-1),(-1,1),(1,1)) ---
+  // ---- 2. half-pel stage (H9 order: (0,0),(0,-1),(0,1),(-1,0),(1,0),(-1,-1),(1,-1),(-1,1),(1,1)) ---
   // Candidates arrive out of H9 order: keep the first strict minimum in H9 order with an index
   // tie-break (d < best, or d == best at a lower index).
   uint32_t hbest = 0xFFFFFFFFu;
   int hbi = 9;
   {
     uint32_t d[3] = {0u, 0u, 0u};
-    half_center<UW, UH, T, kHP>(v, K, had, d);
+    over_halves([&](uint32_t (&dd)[3]) FME_AI { half_center<UW, UH, T, kHP>(v, K, met, dd); }, d);
     take_half<L>(0, d[0], live, ml, mvx, mvy, mvp_x, mvp_y, hbest, hbi);
     take_half<L>(1, d[1], live, ml, mvx, mvy, mvp_x, mvp_y, hbest, hbi);
     take_half<L>(2, d[2], live, ml, mvx, mvy, mvp_x, mvp_y, hbest, hbi);
   }
   {
     uint32_t d[3];
-    half_side<UW, UH, T, 0, kHP>(v, K, had, d);
+    over_halves([&](uint32_t (&dd)[3]) FME_AI { half_side<UW, UH, T, 0, kHP>(v, K, met, dd); }, d);
     take_half<L>(3, d[0], live, ml, mvx, mvy, mvp_x, mvp_y, hbest, hbi);
     take_half<L>(5, d[1], live, ml, mvx, mvy, mvp_x, mvp_y, hbest, hbi);
     take_half<L>(7, d[2], live, ml, mvx, mvy, mvp_x, mvp_y, hbest, hbi);
-    half_side<UW, UH, T, 1, kHP>(v, K, had, d);
+    over_halves([&](uint32_t (&dd)[3]) FME_AI { half_side<UW, UH, T, 1, kHP>(v, K, met, dd); }, d);
     take_half<L>(4, d[0], live, ml, mvx, mvy, mvp_x, mvp_y, hbest, hbi);
     take_half<L>(6, d[1], live, ml, mvx, mvy, mvp_x, mvp_y, hbest, hbi);
     take_half<L>(8, d[2], live, ml, mvx, mvy, mvp_x, mvp_y, hbest, hbi);
   }
   const int hx = h9_dx(hbi), hy = h9_dy(hbi);
 
-  // ---- 4. quarter-pel stage: passes over column phases (Q9 candidate 0 = the half best) -------
+  // ---- 3. quarter-pel stage: passes over column phases (Q9 candidate 0 = the half best) -------
   uint32_t qbest = hbest;
   int qbi = 0;
-  qtr_all<L, UW, UH, T, kQP>(v, K, had, live, hx, hy, ml, mvx, mvy, mvp_x, mvp_y, qbest, qbi,
-                             std::make_integer_sequence<int, qp_passes<kQP>()>{});
+  auto qone = [&](auto ps_c) FME_AI {
+    constexpr int ps = decltype(ps_c)::value;
+    uint32_t d[2];
+    over_halves([&](uint32_t (&dd)[2]) FME_AI { qtr_pass<UW, UH, T, kQP, ps>(v, K, met, hx, hy, dd); }, d);
+    take_qtr<L>(qp_idx0<kQP>(ps), d[0], live, ml, mvx, mvy, hx, hy, mvp_x, mvp_y, qbest, qbi);
+    if constexpr (qp_l1<kQP>(ps) >= 0)
+      take_qtr<L>(qp_idx1<kQP>(ps), d[1], live, ml, mvx, mvy, hx, hy, mvp_x, mvp_y, qbest, qbi);
+  };
+  static_for<0, qp_passes<kQP>()>(qone);
   const int bq = qbi;
 
   // ---- results: bytes 0..15 (mv_int, mv (NN tail), half, qtr, frac_cost) ------------------------
@@ -803,19 +895,23 @@ __device__ __forceinline__ int xcc_id() {
 
 // (class id, PU W, PU H, unit W, unit H) — fme_device.h class table; one kernel per unit
 // shape, since a kernel's register allocation is the maximum over its cases.
-#define FME_LANE48_CLASSES(X) X(0, 4, 8, 4, 8) X(3, 4, 16, 4, 8)
-#define FME_LANE84_CLASSES(X) X(1, 8, 4, 8, 4) X(4, 16, 4, 8, 4)
+// 4x8 units for every shape whose width is a multiple of 4 and height a multiple of 8 (an 8x8
+// SATD tile is a lane pair), 4x4 units (one SATD tile each) for the 4x4-tiled shapes.
+#define FME_LANE48_CLASSES(X) X(0, 4, 8, 4, 4) X(3, 4, 16, 4, 4)
+#define FME_LANE84_CLASSES(X) X(1, 8, 4, 4, 4) X(4, 16, 4, 4, 4)
 #define FME_LANE88_CLASSES(X)                                                                        \
-  X(2, 8, 8, 8, 8) X(5, 8, 16, 8, 8) X(6, 16, 8, 8, 8) X(9, 16, 16, 8, 8) X(10, 8, 32, 8, 8)         \
-  X(11, 32, 8, 8, 8) X(12, 16, 32, 8, 8) X(13, 32, 16, 8, 8) X(16, 32, 32, 8, 8) X(17, 16, 64, 8, 8) \
-  X(18, 64, 16, 8, 8) X(19, 32, 64, 8, 8) X(20, 64, 32, 8, 8) X(23, 64, 64, 8, 8)
-// the AMP shapes whose unit count is not a power of two: 12x16 / 16x12 in 4x8 / 8x4 units (6 of 8
-// lanes), 24x32 / 32x24 in 8x8 units (12 of 16), 48x64 / 64x48 (48 of 64)
+  X(2, 8, 8, 4, 8) X(5, 8, 16, 4, 8) X(6, 16, 8, 4, 8) X(9, 16, 16, 4, 8) X(10, 8, 32, 4, 8)         \
+  X(11, 32, 8, 4, 8) X(12, 16, 32, 4, 8) X(13, 32, 16, 4, 8) X(16, 32, 32, 4, 8) X(17, 16, 64, 4, 8) \
+  X(18, 64, 16, 4, 8) X(19, 32, 64, 4, 8) X(20, 64, 32, 4, 8) X(23, 64, 64, 4, 8)
+// the AMP shapes whose unit count is not a power of two: 12x16 / 16x12 in 4x4 units (12 of 16
+// lanes), 24x32 / 32x24 (24 of 32), 48x64 / 64x48 (two halves of 48 units, 48 of 64 lanes)
 #define FME_LANE_AMP_CLASSES(X)                                                                      \
-  X(7, 12, 16, 4, 8) X(8, 16, 12, 8, 4) X(14, 24, 32, 8, 8) X(15, 32, 24, 8, 8) X(21, 48, 64, 8, 8)   \
-  X(22, 64, 48, 8, 8)
+  X(7, 12, 16, 4, 4) X(8, 16, 12, 4, 4) X(14, 24, 32, 4, 8) X(15, 32, 24, 4, 8) X(21, 48, 64, 4, 8)   \
+  X(22, 64, 48, 4, 8)
+#ifndef FME_LANE_CLASSES   // (a subset may be given on the command line for register-usage probes)
 #define FME_LANE_CLASSES(X) \
   FME_LANE48_CLASSES(X) FME_LANE84_CLASSES(X) FME_LANE88_CLASSES(X) FME_LANE_AMP_CLASSES(X)
+#endif
 
 // One kernel serves every lane class.  A workgroup claims four consecutive 64-lane wave tiles
 // (one per wave; a tile holds 64 / L PUs of one class) per atomic from its XCD's queue
@@ -876,7 +972,8 @@ void k_search_lane(BatchArgs a, WorkBufs w) {
 // Lanes per PU of a lane-kernel class, 0 for classes the cooperative kernels serve.
 int lane_lanes_per_pu(int cls) {
   switch (cls) {
-#define FME_L(ID, PW_, PH_, UW_, UH_) case ID: return pow2_at_least((PW_ / UW_) * (PH_ / UH_));
+#define FME_L(ID, PW_, PH_, UW_, UH_) \
+  case ID: return pow2_at_least((PW_ / UW_) * (PH_ / UH_) > 64 ? (PW_ / UW_) * (PH_ / UH_) / 2 : (PW_ / UW_) * (PH_ / UH_));
     FME_LANE_CLASSES(FME_L)
 #undef FME_L
     default: return 0;

@@ -352,6 +352,23 @@ __global__ __launch_bounds__(kMcBlock) void k_bi_key(BiKeyArgs a) {
   if (task >= a.n) return;   // wave-uniform
   const int lane = (int)(threadIdx.x & 63);
   const BiKeyTask t = a.tasks[task];
+  if (a.invalid) {   // device-resident requests (fme_build_bipred_keys_device): the host checks' equivalent
+    bool shape = false;
+#pragma unroll
+    for (int k = 0; k < kNumClasses; k++) shape |= kClassW[k] == t.w && kClassH[k] == t.h;
+    bool ok = shape && t.org_id < FME_MAX_PICTURES && t.ref_id < FME_MAX_PICTURES && t.key_off >= 0 &&
+              (t.key_off & 3) == 0 && (int64_t)t.key_off + (int64_t)t.w * t.h <= a.n_keys &&
+              (t.clip & ~FME_PU_CLIP_BIPRED) == 0;
+    if (ok) {
+      const PicDesc r = a.pics[t.ref_id], o = a.pics[t.org_id];
+      ok = r.luma && o.luma && r.width == o.width && r.height == o.height && t.x + t.w <= o.width &&
+           t.y + t.h <= o.height;
+    }
+    if (!ok) {
+      if (lane == 0) atomicAdd(a.invalid, 1);
+      return;   // wave-uniform
+    }
+  }
   const PicDesc ref = a.pics[t.ref_id], org = a.pics[t.org_id];
   int mx = t.mv_x, my = t.mv_y;
   clip_mv(mx, my, ref.width, ref.height, t.cu_x, t.cu_y);

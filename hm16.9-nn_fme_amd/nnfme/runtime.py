@@ -15,7 +15,7 @@ from .weights import load_weights
 PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB_PATH = os.environ.get("FME_LIB_PATH") or os.path.join(PKG_ROOT, "libfme_amd.so")
 
-ABI_VERSION = 8
+ABI_VERSION = 9
 TIMING_NAMES = ("classify", "scatter", "search", "nn_tail", "batch", "search_main", "search_aux")
 
 # Every entry point include/fme.h declares (the ABI test checks the .so exports them).
@@ -31,7 +31,7 @@ ABI_SYMBOLS = (
     "fme_pred_inter_p", "fme_pred_inter_reset", "fme_nn_param_count", "fme_load_nn_net",
     "fme_set_nn_engine", "fme_set_nn_margin_output", "fme_refine_mv", "fme_refine_mv_device",
     "fme_refine_status", "fme_nn_copy_state_device", "fme_template_costs", "fme_pred_inter_b", "fme_build_bipred_keys",
-    "fme_set_search_event",
+    "fme_set_search_event", "fme_build_bipred_keys_device",
 )
 
 
@@ -104,12 +104,17 @@ def load_library(path=None):
         "fme_template_costs": (I, [P, P, P, I, P]),
         "fme_pred_inter_b": (I, [P, P, P, I, P]),
         "fme_build_bipred_keys": (I, [P, P, I, C.c_size_t, P]),
+        "fme_build_bipred_keys_device": (I, [P, P, I, C.c_size_t, P]),
     }
+    # an explicitly named library is an A/B variant (tools/ab_bench.py): possibly an older ABI
+    strict = os.path.abspath(path) == os.path.abspath(LIB_PATH)
     for name, (res, args) in sig.items():
-        f = getattr(lib, name)
+        f = getattr(lib, name, None)
+        if f is None:   # tests/test_abi.py checks that the library exports every fme.h entry point
+            continue
         f.restype = res
         f.argtypes = args
-    if lib.fme_abi_version() != ABI_VERSION:
+    if strict and lib.fme_abi_version() != ABI_VERSION:
         raise FmeError(-1, "ABI version mismatch")
     _libs[path] = lib
     return lib
@@ -221,6 +226,13 @@ class FmeContext:
         from .abi import BIKEY_REQ_DTYPE
         reqs = np.ascontiguousarray(reqs, dtype=BIKEY_REQ_DTYPE)
         _check(self.lib, self.lib.fme_build_bipred_keys(self.h, _ptr(reqs), len(reqs), int(key_count), stream))
+
+    def build_bipred_keys_device(self, d_reqs, n, key_count, stream=None):
+        """fme_build_bipred_keys_device: the same from a device-resident request array, in stream
+        order (no host synchronisation; invalid requests make every later batch that reads
+        keys rejected, see fme.h)."""
+        _check(self.lib, self.lib.fme_build_bipred_keys_device(self.h, C.c_void_p(d_reqs), int(n), int(key_count),
+                                                                C.c_void_p(stream) if stream else None))
 
     def template_costs(self, reqs, stream=None):
         """fme_template_costs: xGetTemplateCost per (request, reference, candidate) -> uint32

@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define FME_ABI_VERSION 8
+#define FME_ABI_VERSION 9
 
 /* ---- error codes ---------------------------------------------------------------- */
 #define FME_OK            0
@@ -458,6 +458,13 @@ typedef struct fme_bikey_req {
   uint32_t flags;                  /* FME_PU_CLIP_BIPRED                                        */
 } fme_bikey_req;   /* 24 bytes */
 int fme_build_bipred_keys(fme_ctx* ctx, const fme_bikey_req* reqs, int n, size_t key_count, void* stream);
+/* The same for a device-resident request array, stream-ordered and without host synchronisation
+ * (a per-frame step of a frame pipeline: the other list's MVs are known on the device).  The
+ * requests are validated on the device; invalid ones are skipped and counted, and then every later
+ * batch with a job that reads keys is rejected (FME_RES_REJECTED, fme_refine_status) until keys
+ * are built again.  The key buffer grows (after synchronising `stream`) when key_count exceeds it. */
+int fme_build_bipred_keys_device(fme_ctx* ctx, const fme_bikey_req* d_reqs, int n, size_t key_count,
+                                 void* stream);
 
 /* Host arrays, synchronous on `stream`; a batch with an invalid request is rejected before any
  * work runs.  m_integerMv2Nx2N (both lists) is the state fme_pred_inter_reset forgets. */
