@@ -66,7 +66,8 @@ WORKLOADS = {
                     "8 frames per batch (configs[1])"),
     "c4": dict(W=2560, H=1600, QP=27, nn=1, calls=333, bipred=0.205, gop="ra", frames=1,
                desc="2560x1600 random-access QP27 B-frames, NN_pred on, 2+2 refs, ~1331 calls/CTU, 20.5 % bi-pred "
-                    "with 2*org - pred keys, RA GOP-8 lambdas (configs[3])"),
+                    "with 2*org - pred keys built per frame on the device inside the timed step, RA GOP-8 "
+                    "lambdas (configs[3])"),
     "c5": dict(W=1920, H=1080, QP=22, nn=2, net="scr3x40", engine=1, calls=423, bipred=0.0, gop="ldp", frames=1,
                desc="1920x1080 lowdelay_P QP22 with the 3-hidden-layer NN_pred (Backups/4 SCR 9-40-40-40-49, "
                     "double) as a batched MFMA GEMM (v_mfma_f64_16x16x4) (configs[4])"),
@@ -195,38 +196,22 @@ def mc_algorithmic_bytes(jobs):
 
 
 def drop_in_leg(dev, calls=300):
-    """The TEncSearch-shaped single-PU entry points, one call per PU as a live encoder would make
-    them (fme_frac_dif_single: host key / window in, half / quarter / cost out, synchronous;
-    fme_nn_pred_single): wall microseconds per call.  Latency-bound by construction (one launch
-    and one host round trip per call); the batch path is the throughput path."""
-    from nnfme.runtime import FmeContext
-    rng = np.random.default_rng(5)
-    pic = synth.synth_luma(W, H, 1).astype(np.int16)
-    org = synth.synth_luma(W, H, 0).astype(np.int16)
-    pad = 80
-    plane = np.pad(pic, pad, mode="edge")
-    ctx = FmeContext(device=dev.index, nn_mode=1, qp=QP, fast_inter_mode=1)
-    ml = 65536.0 * np.sqrt(synth.LDP_LAMBDA[QP][0])
-    out = {}
-    for (w, h) in ((8, 8), (16, 16), (64, 64)):
-        ts = []
-        for i in range(calls // 3):
-            x = 4 * int(rng.integers(0, (W - w) // 4)) if i else 0
-            y = 4 * int(rng.integers(0, (H - h) // 4)) if i else 0
-            mv = (int(rng.integers(-8, 9)), int(rng.integers(-8, 9)))
-            t0 = time.perf_counter()
-            ctx.frac_dif_single(org[y:y + h, x:x + w], plane, (y + pad, x + pad), mv, (0, 0), ml)
-            ts.append(time.perf_counter() - t0)
-        out[f"frac_dif_{w}x{h}_us"] = float(np.median(ts[1:]) * 1e6)
-    ts = []
-    for i in range(calls):
-        e = rng.integers(0, 5000, 8).astype(np.uint32)
-        t0 = time.perf_counter()
-        ctx.nn_pred_single(e, int(rng.integers(0, 5000)), 8, 8)
-        ts.append(time.perf_counter() - t0)
-    out["nn_pred_us"] = float(np.median(ts[1:]) * 1e6)
-    out["note"] = "median wall time per synchronous call, Python ctypes caller included"
-    ctx.close()
+    """The TEncSearch-shaped single-PU entry points, one call per PU as a live encoder in drop-in
+    mode would make them, timed from C++ (tests/cpp/test_hm_adapter.cpp --time-single through
+    fme_hm::FracSearch): xPatternSearchFracDIF (fme_frac_dif_single: key and window staged in
+    pinned, device-mapped host memory, one launch, one synchronisation) and NN_pred
+    (fme_nn_pred_single); median wall microseconds per call.  Latency-bound by construction; the
+    batch path is the throughput path."""
+    import subprocess
+    exe = os.path.join(ROOT, "hm16.9-nn_fme_amd", "host", "test_hm_adapter")
+    if not os.path.exists(exe):
+        return {"error": f"{exe} not built"}
+    p = subprocess.run([exe, "--time-single", str(calls)], capture_output=True, text=True, timeout=300)
+    if p.returncode != 0:
+        return {"error": (p.stdout + p.stderr)[-400:]}
+    out = json.loads(p.stdout.strip().splitlines()[-1])
+    out["note"] = ("median wall time per synchronous call from C++ (fme_hm::FracSearch), caller's copies of "
+                   "the key and the window into the staging block included")
     return out
 
 
@@ -584,17 +569,16 @@ def main():
     net = weights.case_net(wl["net"]) if NN == 2 else None
     ctx = FmeContext(device=dev_index, use_hadamard=1, nn_mode=NN, qp=QP, fast_inter_mode=1,
                      max_jobs=n1 * FPS, net=net, nn_engine=wl.get("engine", 0))
-    if key_reqs is not None:   # built on the device (fme_build_bipred_keys, k_bi_key)
-        for k, v in kpics.items():
-            ctx.set_picture(k, v)
-        ctx.build_bipred_keys(key_reqs, len(keys))
 
     # synthetic frame pool (the trace's originals / reconstructions): frame g -> pool[g % 8]
     pool = np.stack([synth.synth_luma(W, H, t) for t in range(8)])
     steps_total = args.warmup + args.steps
     defer = (args.download or wl.get("download", "deferred")) == "deferred"
+    # bi-pred keys (configs[3]): every step builds its frame's removeHighFreq keys on the device from
+    # that frame's pictures (fme_build_bipred_keys_device, k_bi_key) inside the timed step
     rep = FrameReplay(ctx, jobs, pool, lambda f: frame_lambda(wl, f), steps_total, frames_per_step=FPS,
-                      world=world, rank=rank, device=dev, defer_download=defer)
+                      world=world, rank=rank, device=dev, defer_download=defer,
+                      key_reqs=key_reqs, key_count=len(keys) if keys is not None else 0)
     n = rep.n
     rep.prime()
 
@@ -638,6 +622,9 @@ def main():
             torch.cuda.synchronize(dev)
             t1 = time.perf_counter()
             for s in range(args.steps):
+                if rep.kreqs is not None:
+                    ctx.build_bipred_keys_device(rep.d_kreqs[s & 1].data_ptr(), len(rep.kreqs), rep.key_count * FPS,
+                                                 comp.cuda_stream)
                 ctx.refine_mv_device(rep.d_jobs[s & 1].data_ptr(), rep.d_out[s & 1].data_ptr(), n, comp.cuda_stream)
             comp.synchronize()
             dt = (time.perf_counter() - t1) / args.steps

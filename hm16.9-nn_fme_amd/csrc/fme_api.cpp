@@ -75,6 +75,20 @@ struct DevBuf {
 
 }  // namespace
 
+// fme_frac_dif_single's staging block (see fme_ctx::stage).
+struct SingleStage {
+  fme_job job;
+  int32_t perm[8];
+  fme_result res;
+  fme_mv_result mv;
+  PicDesc pic;
+  double ml;
+  uint32_t nn_in[12];
+  int32_t nn_out[4];
+  int16_t key[64 * 64];
+  uint8_t win[72 * 72];
+};
+
 struct fme_ctx {
   int device = 0;
   fme_config cfg{};
@@ -142,6 +156,11 @@ struct fme_ctx {
   DevBuf<int32_t> d_ch_i32;     // k_tz_level: psrc
 
   std::unique_ptr<fme_ctx> single;  // private context for the single-PU entry points
+  // Single-PU staging in pinned, device-mapped host memory: one kernel reads the job, key and
+  // window over PCIe and writes the record back (fme_frac_dif_single / fme_nn_pred_single).
+  struct SingleStage* stage = nullptr;
+  uint8_t* stage_dev = nullptr;
+  hipStream_t single_stream = nullptr;
   DevBuf<uint8_t> single_pic;
   DevBuf<fme_job> single_job;
   DevBuf<fme_result> single_res;
@@ -250,6 +269,8 @@ int fme_destroy(fme_ctx* c) {
   c->d_sched.release();
   if (c->ev_done) (void)hipEventDestroy(c->ev_done);
   c->single_pic.release(); c->single_job.release(); c->single_res.release();
+  if (c->stage) (void)hipHostFree(c->stage);
+  if (c->single_stream) (void)hipStreamDestroy(c->single_stream);
   c->single_nn_in.release(); c->single_nn_out.release();
   if (c->h_counts) (void)hipHostFree(c->h_counts);
   for (auto& set : c->ev)
@@ -930,59 +951,84 @@ int fme_refine_mv(fme_ctx* c, const fme_job* jobs, fme_mv_result* out, int n, vo
 // xPatternSearchFracDIF for one PU: the reference window around mv_int becomes a private
 // (w+8) x (h+8) picture; the MV predictor is shifted by 4*mv_int so that every MV-cost
 // argument (xPatternRefinement's (cMvTest << scale) - pred) is unchanged.
+static int ensure_stage(fme_ctx* c) {
+  if (c->stage) return FME_OK;
+  void* p = nullptr;
+  HIP_TRY(hipHostMalloc(&p, sizeof(SingleStage), hipHostMallocMapped));
+  c->stage = static_cast<SingleStage*>(p);
+  void* d = nullptr;
+  HIP_TRY(hipHostGetDevicePointer(&d, p, 0));
+  c->stage_dev = static_cast<uint8_t*>(d);
+  HIP_TRY(hipStreamCreateWithFlags(&c->single_stream, hipStreamNonBlocking));
+  std::memset(c->stage, 0, sizeof(SingleStage));
+  return FME_OK;
+}
+
+static int class_of(int w, int h) {
+  for (int k = 0; k < kNumClasses; k++)
+    if (kClassW[k] == w && kClassH[k] == h) return k;
+  return -1;
+}
+
+// xPatternSearchFracDIF for one PU, as TEncSearch calls it: the key block (pcPatternKey, HM Pel)
+// and the reference window around the integer MV (rows -4..h+3, columns -4..w+3 of the padded
+// picture) are staged in pinned, device-mapped host memory; one launch of k_search_single (the
+// batch kernel's per-PU search, no EMI step) reads them over PCIe and writes the record back; one
+// stream synchronisation.  (Round 2: a sub-context picture upload, a key upload and a 5-launch
+// batch with its copies, 136-148 us per call.)
 int fme_frac_dif_single(fme_ctx* c, int lossless, const int16_t* key, int key_stride, int w, int h,
                         const int16_t* ref, int ref_stride, int mv_int_x, int mv_int_y, int mvp_x,
                         int mvp_y, double motion_lambda, int16_t* half_xy, int16_t* qtr_xy,
                         uint32_t* cost) {
   if (!c || !key || !ref || !half_xy || !qtr_xy || !cost) return fail(FME_E_INVALID, "fme_frac_dif_single: null argument");
-  if (w < 4 || h < 4 || w > 64 || h > 64 || (w & 3) || (h & 3)) return fail(FME_E_UNSUPPORTED, "fme_frac_dif_single: %dx%d", w, h);
+  const int cls = class_of(w, h);
+  if (cls < 0) return fail(FME_E_UNSUPPORTED, "fme_frac_dif_single: %dx%d", w, h);
+  const int px = mvp_x - 4 * mv_int_x, py = mvp_y - 4 * mv_int_y;
+  if (px < -32768 || px > 32767 || py < -32768 || py > 32767) return fail(FME_E_INVALID, "fme_frac_dif_single: predictor out of range");
   HIP_TRY(hipSetDevice(c->device));
-  if (!c->single) {
-    fme_config sc = c->cfg;
-    sc.nn_mode = 0;
-    sc.max_jobs = 1;
-    fme_ctx* sub = nullptr;
-    int rc = fme_create(c->device, &sc, &sub);
-    if (rc) return rc;
-    c->single.reset(sub);
-  }
-  fme_ctx* sub = c->single.get();
-  sub->cfg.use_hadamard = c->cfg.use_hadamard;
+  int rc = ensure_stage(c);
+  if (rc) return rc;
+  SingleStage* st = c->stage;
   const int pw = w + 8, ph = h + 8;
-  std::vector<uint8_t> win((size_t)pw * ph);
-  for (int y = 0; y < ph; y++)
-    for (int x = 0; x < pw; x++) {
-      const int v = ref[(ptrdiff_t)(mv_int_y - 4 + y) * ref_stride + (mv_int_x - 4 + x)];
-      win[(size_t)y * pw + x] = (uint8_t)std::min(255, std::max(0, v));
-    }
-  std::vector<int16_t> kb((size_t)w * h);
-  for (int y = 0; y < h; y++)
-    for (int x = 0; x < w; x++) kb[(size_t)y * w + x] = key[(ptrdiff_t)y * key_stride + x];
-  int rc = fme_set_picture(sub, 0, win.data(), pw, pw, ph, nullptr);
-  if (rc) return rc;
-  rc = fme_set_keys(sub, kb.data(), kb.size(), nullptr);
-  if (rc) return rc;
-  rc = fme_set_motion_lambda(sub, 0, motion_lambda);
-  if (rc) return rc;
+  for (int y = 0; y < ph; y++) {
+    const int16_t* src = ref + (ptrdiff_t)(mv_int_y - 4 + y) * ref_stride + (mv_int_x - 4);
+    uint8_t* dst = st->win + (size_t)y * pw;
+    for (int x = 0; x < pw; x++) dst[x] = (uint8_t)std::min(255, std::max(0, (int)src[x]));
+  }
+  for (int y = 0; y < h; y++) std::memcpy(st->key + (size_t)y * w, key + (ptrdiff_t)y * key_stride, (size_t)w * sizeof(int16_t));
   fme_job j{};
   j.x = 4;
   j.y = 4;
   j.w = (uint8_t)w;
   j.h = (uint8_t)h;
-  j.org_id = 0;
-  j.ref_id = 0;
-  j.mv_x = 0;
-  j.mv_y = 0;
-  const int px = mvp_x - 4 * mv_int_x, py = mvp_y - 4 * mv_int_y;
-  if (px < -32768 || px > 32767 || py < -32768 || py > 32767) return fail(FME_E_INVALID, "fme_frac_dif_single: predictor out of range");
   j.mvp_x = (int16_t)px;
   j.mvp_y = (int16_t)py;
   j.flags = lossless ? FME_JOB_LOSSLESS : 0;
-  j.lambda_id = 0;
   j.key_offset = 0;
-  fme_result r{};
-  rc = fme_refine(sub, &j, &r, 1, nullptr);
-  if (rc) return rc;
+  st->job = j;
+  st->perm[0] = 0;
+  st->ml = motion_lambda;
+  st->pic = PicDesc{};
+  st->pic.luma = c->stage_dev + offsetof(SingleStage, win);
+  st->pic.stride = pw;
+  st->pic.width = pw;
+  st->pic.height = ph;
+  BatchArgs a{};
+  a.jobs = reinterpret_cast<const fme_job*>(c->stage_dev + offsetof(SingleStage, job));
+  a.res = reinterpret_cast<fme_result*>(c->stage_dev + offsetof(SingleStage, res));
+  a.keys = reinterpret_cast<const int16_t*>(c->stage_dev + offsetof(SingleStage, key));
+  a.n_keys = (int64_t)w * h;
+  a.mlambda = reinterpret_cast<const double*>(c->stage_dev + offsetof(SingleStage, ml));
+  a.pics = reinterpret_cast<const PicDesc*>(c->stage_dev + offsetof(SingleStage, pic));
+  a.n = 1;
+  a.use_hadamard = c->cfg.use_hadamard ? 1 : 0;
+  a.fen = c->cfg.fast_inter_mode;
+  WorkBufs wb{};
+  wb.sjobs = const_cast<fme_job*>(a.jobs);
+  wb.perm = reinterpret_cast<int32_t*>(c->stage_dev + offsetof(SingleStage, perm));
+  HIP_TRY(launch_search_single(a, wb, cls, c->single_stream));
+  HIP_TRY(hipStreamSynchronize(c->single_stream));
+  const fme_result& r = st->res;
   half_xy[0] = r.half_x;
   half_xy[1] = r.half_y;
   qtr_xy[0] = r.qtr_x;
@@ -996,18 +1042,20 @@ int fme_nn_pred_single(fme_ctx* c, const uint32_t* e, uint32_t cc, int pu_h, int
   const bool deep = c->cfg.nn_mode == 2;
   if (deep ? !c->net_loaded : !c->nn_loaded) return fail(FME_E_STATE, "fme_nn_pred_single: no weights loaded");
   HIP_TRY(hipSetDevice(c->device));
-  HIP_TRY(c->single_nn_in.reserve(11));
-  HIP_TRY(c->single_nn_out.reserve(1));
-  uint32_t in[11];
+  int rc = ensure_stage(c);
+  if (rc) return rc;
+  // inputs and the class through the mapped staging block: one launch, one synchronisation
+  uint32_t* in = c->stage->nn_in;
   for (int s = 0; s < 8; s++) in[s] = e[s];
   in[8] = cc;
   in[9] = (uint32_t)pu_h;
   in[10] = (uint32_t)pu_w;
-  HIP_TRY(hipMemcpy(c->single_nn_in.p, in, sizeof(in), hipMemcpyHostToDevice));
-  HIP_TRY(deep ? launch_nn_deep_single(c->net, c->d_net.p, c->single_nn_in.p, c->single_nn_out.p, nullptr)
-               : launch_nn_single(c->d_nn.p, c->single_nn_in.p, c->single_nn_out.p, nullptr));
-  int32_t cls = 0;
-  HIP_TRY(hipMemcpy(&cls, c->single_nn_out.p, sizeof(cls), hipMemcpyDeviceToHost));
+  const uint32_t* d_in = reinterpret_cast<const uint32_t*>(c->stage_dev + offsetof(SingleStage, nn_in));
+  int32_t* d_out = reinterpret_cast<int32_t*>(c->stage_dev + offsetof(SingleStage, nn_out));
+  HIP_TRY(deep ? launch_nn_deep_single(c->net, c->d_net.p, d_in, d_out, c->single_stream)
+               : launch_nn_single(c->d_nn.p, d_in, d_out, c->single_stream));
+  HIP_TRY(hipStreamSynchronize(c->single_stream));
+  const int32_t cls = c->stage->nn_out[0];
   *nn_class = cls;
   if (out4) {
     // MVX_HALF, MVX_QRTER, MVY_HALF, MVY_QRTER of the switch at TEncSearch.cpp:136-193:

@@ -179,6 +179,9 @@ hipError_t launch_put_tables(PicDesc* d_pics, double* d_ml, const PicDesc* pics,
 // enough workgroups to fill the chip, each pulling tiles from its XCD's queue (then the other
 // XCDs').  `a.n` bounds the work.
 hipError_t launch_search_lane(const BatchArgs& a, const WorkBufs& w, hipStream_t s);
+// One PU of class cls whose job / key / picture / record pointers may be device-mapped host memory
+// (the single-PU entry point): one wave.
+hipError_t launch_search_single(const BatchArgs& a, const WorkBufs& w, int cls, hipStream_t s);
 int lane_lanes_per_pu(int cls);                    // lanes of a class's PU group (pow2), 0: none
 int cu_count(int device);                          // compute units (workgroup budget of a launch)
 // Packed NN layout for the tail kernel (nn_pack, fme_kernels.hip): offsets in floats, every

@@ -57,9 +57,15 @@
 #ifndef FME_LANE_UNIT_ATTR
 #define FME_LANE_UNIT_ATTR __attribute__((noinline))
 #endif
+// 1: the half stage's six side candidates from shared half columns and the quarter stage as three
+// column-phase passes of all their candidates (fewest first stages; needs 2 waves/SIMD of
+// registers); 0: the pair modes above
+#ifndef FME_LANE_SHARE
+#define FME_LANE_SHARE 1
+#endif
 // occupancy target (waves per SIMD) that bounds the register allocation
 #ifndef FME_LANE_WAVES
-#define FME_LANE_WAVES 3
+#define FME_LANE_WAVES 2
 #endif
 
 namespace fme {
@@ -100,6 +106,20 @@ __device__ __forceinline__ void static_for(F&& f) {
 }
 
 __host__ __device__ __forceinline__ constexpr int pow2_at_least(int v) { return v <= 1 ? 1 : 2 * pow2_at_least((v + 1) / 2); }
+
+// The first dot product of a chain with an inline-constant accumulator, in the VOP3P encoding:
+// the compiler picks v_dot4c / v_dot2c (accumulator tied to the destination) and materialises the
+// constant with a v_mov first (≈ 700 movs per lane-class function, 11 % of its VALU).
+__device__ __forceinline__ int dot4_k32(uint32_t a, uint32_t b) {
+  int d;
+  asm("v_dot4_i32_i8 %0, %1, %2, 32" : "=v"(d) : "v"(a), "v"(b));
+  return d;
+}
+__device__ __forceinline__ int dot2_k0(uint32_t a, uint32_t b) {
+  int d;
+  asm("v_dot2_i32_i16 %0, %1, %2, 0" : "=v"(d) : "v"(a), "v"(b));
+  return d;
+}
 
 // low 16 bits of a and b -> one packed pair (a in the low half)
 __device__ __forceinline__ uint32_t pack2(int a, int b) { return __builtin_amdgcn_perm((uint32_t)b, (uint32_t)a, 0x05040100u); }
@@ -443,6 +463,128 @@ __device__ __forceinline__ void half_side(uint32_t (&v)[UH + 8][UW / 4 + 2], con
   }
 }
 
+// All six side candidates from the UW + 1 half-pel columns x - 1/2, x = 0..UW, which both sides
+// share (side -1 takes columns 0..UW-1, side +1 columns 1..UW): in H9 numbering d = {3: (-1,0),
+// 5: (-1,-1), 7: (-1,1), 4: (1,0), 6: (1,-1), 8: (1,1)} as d[0..5] = 3, 5, 7, 4, 6, 8.  One first
+// stage per half column (rows -4..UH+3, xExtDIFUpSamplingH's filteredBlock[0][2] row) gives all
+// three vertical phases: the first-stage sums carry +32, so the integer rows' 1-D rounding is
+// (s + 32) >> 6 of the same sums, and the vertical half-pel pass, whose taps add to 64, gets its
+// 2048 rounding offset from them with a zero accumulator.
+template <int UW, int UH, int T>
+__device__ __forceinline__ void half_sides(uint32_t (&v)[UH + 8][UW / 4 + 2], const KeySrc<UW, UH / 2>& K,
+                                           const Metric& had, uint32_t (&d)[6]) {
+  constexpr int RV = UH + 8, UJ = UH / 2;
+  uint32_t c2lo, c2hi;
+  taps8(2, c2lo, c2hi);
+  const uint32_t c16[4] = {p16(-1, 4), p16(-11, 40), p16(40, -11), p16(4, -1)};
+  const uint32_t c16o[5] = {p16(0, -1), p16(4, -11), p16(40, 40), p16(-11, 4), p16(-1, 0)};
+  uint32_t XS[6][UW][UJ];
+#pragma unroll
+  for (int k = 0; k <= UW; k++) {
+    launder(v);
+    int hv[RV];
+#pragma unroll
+    for (int r = 0; r < RV; r++) hv[r] = dot4(rbytes(v[r], k + 4), c2hi, dot4_k32(rbytes(v[r], k), c2lo));
+    uint32_t HP[RV / 2];
+#pragma unroll
+    for (int r = 0; r < RV; r += 2) HP[r / 2] = pack2(hv[r], hv[r + 1]);
+    uint32_t X0[UJ], XM[UJ], XP[UJ];   // (s,0), (s,-1), (s,1) of this column
+    int v2[UH + 1];
+#pragma unroll
+    for (int i = 0; i <= UH; i++) {   // half rows between window rows i+3, i+4
+      int acc;
+      if ((i & 1) == 0) {
+        acc = dot2_k0(HP[i / 2], c16[0]);
+#pragma unroll
+        for (int t = 1; t < 4; t++) acc = dot2(HP[i / 2 + t], c16[t], acc);
+      } else {
+        acc = dot2_k0(HP[(i - 1) / 2 + 1], c16o[1]);   // pair 0 is (0, -1): row i-1 only
+        acc = dot2(HP[(i - 1) / 2], c16o[0], acc);
+#pragma unroll
+        for (int t = 2; t < 5; t++) acc = dot2(HP[(i - 1) / 2 + t], c16o[t], acc);
+      }
+      v2[i] = clamp_s8(acc >> 12);
+    }
+#pragma unroll
+    for (int jj = 0; jj < UJ; jj++) {
+      X0[jj] = pack2(clamp_s8(hv[4 + 2 * jj] >> 6), clamp_s8(hv[5 + 2 * jj] >> 6));
+      XM[jj] = pack2(v2[2 * jj], v2[2 * jj + 1]);
+      XP[jj] = pack2(v2[2 * jj + 1], v2[2 * jj + 2]);
+    }
+#pragma unroll
+    for (int jj = 0; jj < UJ; jj++) {
+      if (k < UW) {   // side -1, column k
+        XS[0][k][jj] = pk_sub(K.at(k, jj), X0[jj]);
+        XS[1][k][jj] = pk_sub(K.at(k, jj), XM[jj]);
+        XS[2][k][jj] = pk_sub(K.at(k, jj), XP[jj]);
+      }
+      if (k > 0) {    // side +1, column k - 1
+        XS[3][k - 1][jj] = pk_sub(K.at(k - 1, jj), X0[jj]);
+        XS[4][k - 1][jj] = pk_sub(K.at(k - 1, jj), XM[jj]);
+        XS[5][k - 1][jj] = pk_sub(K.at(k - 1, jj), XP[jj]);
+      }
+    }
+    __builtin_amdgcn_sched_barrier(0);   // one column at a time (register pressure)
+  }
+#pragma unroll
+  for (int m = 0; m < 6; m++) d[m] = unit_dist<UW, UH, T>(XS[m], had);
+}
+
+// Quarter pass over one column phase k (dqx = k - 1) with all its row phases l (dqy = l - 1)
+// except the half best (1,1) itself: 3, 2, 3 candidates for k = 0, 1, 2, one first stage each.
+// First-stage sums carry +32 (the vertical taps add to 64: the 2048 rounding offset), and a
+// fraction-0 phase filters with {0,0,0,64,0,0,0,0}, which equals HM's copy / 1-D paths after
+// rounding ((64 A + 2048) >> 12 == (A + 32) >> 6).
+template <int UW, int UH, int T, int k>
+__device__ __forceinline__ void qtr_col(uint32_t (&v)[UH + 8][UW / 4 + 2], const KeySrc<UW, UH / 2>& K,
+                                        const Metric& had, int hx, int hy, uint32_t (&d)[3]) {
+  constexpr int RV = UH + 8, UJ = UH / 2;
+  constexpr int NP = k == 1 ? 2 : 3;
+  const int LS[3] = {0, k == 1 ? 2 : 1, 2};
+  const int qx = 2 * hx + (k - 1);
+  const int ix = qx >> 2, fx = qx & 3;
+  const uint32_t dlt = (uint32_t)(1 + ix);
+  uint32_t clo, chi;
+  taps8_any(fx, clo, chi);
+  uint32_t cpe[NP][5], cpo[NP][5];
+#pragma unroll
+  for (int m = 0; m < NP; m++) {
+    const int qy = 2 * hy + (LS[m] - 1);
+    const int iy = qy >> 2, fy = qy & 3;
+    vpairs(fy, 1 + iy, cpe[m]);
+    vpairs(fy, 2 + iy, cpo[m]);
+  }
+  uint32_t XQ[NP][UW][UJ];
+#pragma unroll
+  for (int x = 0; x < UW; x++) {
+    launder(v);
+    uint32_t HQ[RV / 2];
+#pragma unroll
+    for (int r = 0; r < RV; r += 2) {
+      const int h0 = dot4(rbytes_d(v[r], x + 4, dlt), chi, dot4_k32(rbytes_d(v[r], x, dlt), clo));
+      const int h1 = dot4(rbytes_d(v[r + 1], x + 4, dlt), chi, dot4_k32(rbytes_d(v[r + 1], x, dlt), clo));
+      HQ[r / 2] = pack2(h0, h1);
+    }
+#pragma unroll
+    for (int m = 0; m < NP; m++) {
+      int vq[UH];
+#pragma unroll
+      for (int y = 0; y < UH; y++) {
+        const int m0 = (y & 1) ? (y - 1) / 2 : y / 2;
+        int acc = dot2_k0(HQ[m0], (y & 1) ? cpo[m][0] : cpe[m][0]);
+#pragma unroll
+        for (int t = 1; t < 5; t++) acc = dot2(HQ[m0 + t], (y & 1) ? cpo[m][t] : cpe[m][t], acc);
+        vq[y] = clamp_s8(acc >> 12);
+      }
+#pragma unroll
+      for (int jj = 0; jj < UJ; jj++) XQ[m][x][jj] = pk_sub(K.at(x, jj), pack2(vq[2 * jj], vq[2 * jj + 1]));
+    }
+    __builtin_amdgcn_sched_barrier(0);   // one column at a time (register pressure)
+  }
+#pragma unroll
+  for (int m = 0; m < NP; m++) d[m] = unit_dist<UW, UH, T>(XQ[m], had);
+}
+
 // Quarter passes: pass PS covers column phase k = QP_K[PS] (dqx = k-1) and one or two row
 // phases l (dqy = l-1); candidate (k1, l1) is the half best.  A phase with fraction 0 filters
 // with {0,0,0,64,0,0,0,0}, which equals HM's copy / 1-D paths after rounding.
@@ -593,6 +735,31 @@ __device__ __forceinline__ void load_window(const PicDesc& pic, int x0, int y0, 
     for (int k = 0; k < N; k++) v[r][k] ^= 0x80808080u;
 }
 
+// Per-workgroup copies of the batch's picture and lambda tables (k_search_lane fills them once):
+// every tile reads its PU's reference / original picture descriptor and motion lambda from LDS
+// instead of a dependent global load before its window loads.
+__shared__ PicDesc g_pics[FME_MAX_PICTURES];
+__shared__ double g_ml[FME_MAX_LAMBDAS];
+// Record staging (FME_LANE_REC_LDS): each PU's 64-byte fme_result is assembled in LDS by the PU's
+// first lane, then the wave writes the tile's records with four lanes per record, so every store
+// instruction writes whole 64-byte lines (one lane per record wrote four separate 16-byte pieces:
+// 256 bytes of WRITE_SIZE per job).
+#ifndef FME_LANE_REC_LDS
+#define FME_LANE_REC_LDS 1
+#endif
+#if FME_LANE_REC_LDS
+__shared__ uint4 g_rec[256 / 64][64][4];
+__shared__ int32_t g_rec_jid[256 / 64][64];
+#endif
+
+// Global pointers typed as such (global_load / global_store, not flat).
+typedef __attribute__((address_space(1))) const fme_job g_job;
+typedef __attribute__((address_space(1))) const int32_t g_i32;
+typedef __attribute__((address_space(1))) fme_result g_res;
+typedef __attribute__((address_space(1))) const int16_t g_i16;
+typedef __attribute__((address_space(1))) const uint8_t g_u8;
+
+
 // =============================================================================================
 // One lane: unit (ux, uy) of PU p of class (PW x PH), unit UW x UH (4x8, or 8x4 for the shapes
 // whose height is not a multiple of 8).  PUs of more than 64 units (48x64, 64x48, 64x64) give a
@@ -600,9 +767,17 @@ __device__ __forceinline__ void load_window(const PicDesc& pic, int x0, int y0, 
 // runs once per half, with the other half's window and key re-loaded (L1 / L2 hits).
 // =============================================================================================
 template <int PW, int PH, int UW, int UH>
-__device__ FME_LANE_UNIT_ATTR void lane_unit(const BatchArgs& a, const fme_job* __restrict__ sjobs,
-                                          const int32_t* __restrict__ perm, int cls_off, int cls_cnt,
-                                          int wt) {
+// (The signature matters to the register allocation of the call: with the kernel-argument
+// reference `a` the callee saves no registers; with the same values as separate scalar arguments
+// it saved and restored 114 callee-saved VGPRs per call.)
+__device__ FME_LANE_UNIT_ATTR void lane_unit(const BatchArgs& a, const fme_job* __restrict__ sjobs_,
+                                             const int32_t* __restrict__ perm_, int cls_off, int cls_cnt,
+                                             int wt) {
+  g_job* const sjobs = (g_job*)sjobs_;
+  g_i32* const perm = (g_i32*)perm_;
+  g_res* const res = (g_res*)a.res;
+  g_i16* const keys = (g_i16*)a.keys;
+  const int use_hadamard = a.use_hadamard, fen = a.fen;
   constexpr int T = ((PW % 8) == 0 && (PH % 8) == 0) ? 8 : 4;
   static_assert((T == 8 && UW == 4 && UH == 8) || (T == 4 && UW == 4 && UH == 4) || (T == 4 && UW * UH == 32),
                 "4x8 units (a lane pair per 8x8 SATD tile) or 4x4 units (one 4x4 tile per lane)");
@@ -635,11 +810,17 @@ __device__ FME_LANE_UNIT_ATTR void lane_unit(const BatchArgs& a, const fme_job* 
   const int uu = u < NUH ? u : NUH - 1;
   const int ux = uu % UX, uy = uu / UX;
 
-  const fme_job j = sjobs[cls_off + p];
+  fme_job j;
+  {   // two 16-byte global loads (a struct copy through an address-space-1 pointer does not compile
+      // in the host pass)
+    const u32x4a q0 = *(gu4*)(sjobs + cls_off + p), q1 = *(gu4*)((g_u8*)(sjobs + cls_off + p) + 16);
+    uint32_t tmp[8] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w};
+    __builtin_memcpy(&j, tmp, sizeof(j));
+  }
   const int jid = perm[cls_off + p];
-  const PicDesc ref = a.pics[j.ref_id];
-  const double ml = a.mlambda[j.lambda_id];
-  const Metric met = {a.use_hadamard && !(j.flags & FME_JOB_LOSSLESS), (lane & 1) ? 0xFFFFFFFFu : 0x00010001u,
+  const PicDesc ref = g_pics[j.ref_id];
+  const double ml = g_ml[j.lambda_id];
+  const Metric met = {use_hadamard && !(j.flags & FME_JOB_LOSSLESS), (lane & 1) ? 0xFFFFFFFFu : 0x00010001u,
                       (lane & 1) ? 0u : ~0u};
   const bool kbuf = j.key_offset >= 0;
   const int ox = (int)j.x + ux * UW, oy = (int)j.y + uy * UH;   // unit origin (top half)
@@ -652,7 +833,7 @@ __device__ FME_LANE_UNIT_ATTR void lane_unit(const BatchArgs& a, const fme_job* 
     int ky = oy + h * kHalfRows;
     asm volatile("" : "+v"(ky));   // not shared across calls (see load_window)
     if (!kbuf) {
-      const PicDesc org = a.pics[j.org_id];
+      const PicDesc org = g_pics[j.org_id];
 #pragma unroll
       for (int r = 0; r < UH; r++) {
         uint32_t t[UW / 4];
@@ -663,11 +844,15 @@ __device__ FME_LANE_UNIT_ATTR void lane_unit(const BatchArgs& a, const fme_job* 
         for (int k = UW / 4; k < KW; k++) kraw[r][k] = 0;
       }
     } else {
-      const int16_t* kb = a.keys + (size_t)j.key_offset + (size_t)(ky - (int)j.y) * PW + ux * UW;
+      g_i16* kb = keys + (size_t)j.key_offset + (size_t)(ky - (int)j.y) * PW + ux * UW;
 #pragma unroll
-      for (int r = 0; r < UH; r++) ld_bytes<KW>(kb + r * PW, kraw[r]);
+      for (int r = 0; r < UH; r++) ld_bytes<KW>((const void*)(kb + r * PW), kraw[r]);
     }
   };
+
+  // one unit per lane: its key rows are loaded once, for the EMI step and the sub-pel passes
+  uint32_t kraw0[UH][KW];
+  if constexpr (UPL == 1) load_kraw(0, kraw0);
 
   // ---- 1. EMI square step -----------------------------------------------------------------------
   int mvx = j.mv_x, mvy = j.mv_y;
@@ -682,7 +867,14 @@ __device__ FME_LANE_UNIT_ATTR void lane_unit(const BatchArgs& a, const fme_job* 
 #pragma unroll
     for (int h = 0; h < UPL; h++) {
       uint32_t kraw[UH][KW];
-      load_kraw(h, kraw);
+      if constexpr (UPL == 1) {
+#pragma unroll
+        for (int r = 0; r < UH; r++)
+#pragma unroll
+          for (int k = 0; k < KW; k++) kraw[r][k] = kraw0[r][k];
+      } else {
+        load_kraw(h, kraw);
+      }
       // integer samples at rows -1 .. UH, cols -1 .. UW around the TZ MV (s - 128 bytes)
       uint32_t w[UH + 2][EW];
       load_window(ref, ox + mvx - 1, oy + h * kHalfRows + mvy - 1, w);
@@ -698,7 +890,7 @@ __device__ FME_LANE_UNIT_ATTR void lane_unit(const BatchArgs& a, const fme_job* 
         const int dx = emi_dx(pos), dy = emi_dy(pos);
         uint32_t e = 0;
         if constexpr (kSadEmi) {   // SAD of the (even, with FEN) rows, doubled when subsampled
-          const bool sub = a.fen == 1 || a.fen == 3;   // and PH > 8: every 12/24/48-wide shape
+          const bool sub = fen == 1 || fen == 3;   // and PH > 8: every 12/24/48-wide shape
 #pragma unroll
           for (int r = 0; r < UH; r++) {
             if ((r & 1) && sub) continue;   // unit rows start on even PU rows
@@ -738,7 +930,7 @@ __device__ FME_LANE_UNIT_ATTR void lane_unit(const BatchArgs& a, const fme_job* 
       }
     }
     if constexpr (kSadEmi) {
-      if (a.fen == 1 || a.fen == 3) {
+      if (fen == 1 || fen == 3) {
 #pragma unroll
         for (int q = 0; q < 9; q++) e9[q] <<= 1;
       }
@@ -782,7 +974,16 @@ __device__ FME_LANE_UNIT_ATTR void lane_unit(const BatchArgs& a, const fme_job* 
     mvy = by;
   }
   typedef __attribute__((address_space(1))) u32x4a gw4;
-  uint8_t* const rec = reinterpret_cast<uint8_t*>(a.res + jid);
+#if FME_LANE_REC_LDS
+  const int wid = (int)threadIdx.x >> 6;
+  if (u == 0) {   // bytes 16..63 of the record: cost, bits (NN tail), c, emi[8], n_emi
+    g_rec[wid][lane][1] = make_uint4(0u, 0u, cval, emi[0]);
+    g_rec[wid][lane][2] = make_uint4(emi[1], emi[2], emi[3], emi[4]);
+    g_rec[wid][lane][3] = make_uint4(emi[5], emi[6], emi[7], (uint32_t)n_emi);
+    g_rec_jid[wid][lane] = active ? jid : -1;
+  }
+#else
+  __attribute__((address_space(1))) uint8_t* const rec = reinterpret_cast<__attribute__((address_space(1))) uint8_t*>(res + jid);
   if (active && u == 0) {   // bytes 16..63 of the record: cost, bits (NN tail), c, emi[8], n_emi
     u32x4a q0, q1, q2;
     q0.x = 0; q0.y = 0; q0.z = cval; q0.w = emi[0];
@@ -792,6 +993,7 @@ __device__ FME_LANE_UNIT_ATTR void lane_unit(const BatchArgs& a, const fme_job* 
     *(gw4*)(rec + 32) = q1;
     *(gw4*)(rec + 48) = q2;
   }
+#endif
   (void)ex;
   (void)ey;
 
@@ -802,7 +1004,14 @@ __device__ FME_LANE_UNIT_ATTR void lane_unit(const BatchArgs& a, const fme_job* 
   auto load_half = [&](int h) FME_AI {
     load_window(ref, ox + mvx - 4, oy + h * kHalfRows + mvy - 4, v);
     uint32_t kraw[UH][KW];
-    load_kraw(h, kraw);
+    if constexpr (UPL == 1) {
+#pragma unroll
+      for (int r = 0; r < UH; r++)
+#pragma unroll
+        for (int k = 0; k < KW; k++) kraw[r][k] = kraw0[r][k];
+    } else {
+      load_kraw(h, kraw);
+    }
 #pragma unroll
     for (int c = 0; c < UW; c++)
 #pragma unroll
@@ -843,7 +1052,16 @@ __device__ FME_LANE_UNIT_ATTR void lane_unit(const BatchArgs& a, const fme_job* 
     take_half<L>(1, d[1], live, ml, mvx, mvy, mvp_x, mvp_y, hbest, hbi);
     take_half<L>(2, d[2], live, ml, mvx, mvy, mvp_x, mvp_y, hbest, hbi);
   }
-  {
+  if constexpr (FME_LANE_SHARE) {
+    uint32_t d[6];
+    over_halves([&](uint32_t (&dd)[6]) FME_AI { half_sides<UW, UH, T>(v, K, met, dd); }, d);
+    take_half<L>(3, d[0], live, ml, mvx, mvy, mvp_x, mvp_y, hbest, hbi);
+    take_half<L>(5, d[1], live, ml, mvx, mvy, mvp_x, mvp_y, hbest, hbi);
+    take_half<L>(7, d[2], live, ml, mvx, mvy, mvp_x, mvp_y, hbest, hbi);
+    take_half<L>(4, d[3], live, ml, mvx, mvy, mvp_x, mvp_y, hbest, hbi);
+    take_half<L>(6, d[4], live, ml, mvx, mvy, mvp_x, mvp_y, hbest, hbi);
+    take_half<L>(8, d[5], live, ml, mvx, mvy, mvp_x, mvp_y, hbest, hbi);
+  } else {
     uint32_t d[3];
     over_halves([&](uint32_t (&dd)[3]) FME_AI { half_side<UW, UH, T, 0, kHP>(v, K, met, dd); }, d);
     take_half<L>(3, d[0], live, ml, mvx, mvy, mvp_x, mvp_y, hbest, hbi);
@@ -867,19 +1085,56 @@ __device__ FME_LANE_UNIT_ATTR void lane_unit(const BatchArgs& a, const fme_job* 
     if constexpr (qp_l1<kQP>(ps) >= 0)
       take_qtr<L>(qp_idx1<kQP>(ps), d[1], live, ml, mvx, mvy, hx, hy, mvp_x, mvp_y, qbest, qbi);
   };
-  static_for<0, qp_passes<kQP>()>(qone);
+  if constexpr (FME_LANE_SHARE) {
+    auto qcol = [&](auto k_c) FME_AI {
+      constexpr int kk = decltype(k_c)::value;
+      uint32_t d[3];
+      over_halves([&](uint32_t (&dd)[3]) FME_AI { qtr_col<UW, UH, T, kk>(v, K, met, hx, hy, dd); }, d);
+      take_qtr<L>(q9_index(kk - 1, -1), d[0], live, ml, mvx, mvy, hx, hy, mvp_x, mvp_y, qbest, qbi);
+      take_qtr<L>(q9_index(kk - 1, kk == 1 ? 1 : 0), d[1], live, ml, mvx, mvy, hx, hy, mvp_x, mvp_y, qbest, qbi);
+      if constexpr (kk != 1) take_qtr<L>(q9_index(kk - 1, 1), d[2], live, ml, mvx, mvy, hx, hy, mvp_x, mvp_y, qbest, qbi);
+    };
+    static_for<0, 3>(qcol);
+  } else {
+    static_for<0, qp_passes<kQP>()>(qone);
+  }
   const int bq = qbi;
 
   // ---- results: bytes 0..15 (mv_int, mv (NN tail), half, qtr, frac_cost) ------------------------
+  const uint32_t r_mv = (uint32_t)(uint16_t)mvx | ((uint32_t)(uint16_t)mvy << 16);
+  const uint32_t r_hq = (uint32_t)(uint8_t)hx | ((uint32_t)(uint8_t)hy << 8) | ((uint32_t)(uint8_t)q9_dx(bq) << 16) |
+                        ((uint32_t)(uint8_t)q9_dy(bq) << 24);
+#if FME_LANE_REC_LDS
+  if (u == 0) g_rec[wid][lane][0] = make_uint4(r_mv, 0u, r_hq, qbest);
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  // the tile's 64 / L records, four lanes per record (quarter = lane % 4): 16 records per store
+  constexpr int NP = 64 / L;
+#pragma unroll
+  for (int s0 = 0; s0 < (NP * 4 + 63) / 64; s0++) {
+    const int r = s0 * 16 + (lane >> 2);   // record of this lane's quarter
+    if (r < NP) {
+      const int src = r * L;              // the PU's first lane
+      const int rj = g_rec_jid[wid][src];
+      if (rj >= 0) {
+        const uint4 q = g_rec[wid][src][lane & 3];
+        u32x4a o;
+        o.x = q.x; o.y = q.y; o.z = q.z; o.w = q.w;
+        *(gw4*)(reinterpret_cast<__attribute__((address_space(1))) uint8_t*>(res + rj) + 16 * (lane & 3)) = o;
+      }
+    }
+  }
+#else
   if (active && u == 0) {
     u32x4a q;
-    q.x = (uint32_t)(uint16_t)mvx | ((uint32_t)(uint16_t)mvy << 16);
+    q.x = r_mv;
     q.y = 0;
-    q.z = (uint32_t)(uint8_t)hx | ((uint32_t)(uint8_t)hy << 8) | ((uint32_t)(uint8_t)q9_dx(bq) << 16) |
-          ((uint32_t)(uint8_t)q9_dy(bq) << 24);
+    q.z = r_hq;
     q.w = qbest;
     *(gw4*)rec = q;
   }
+#endif
 }
 
 // The XCD this wave runs on (HW_REG_XCC_ID, gfx940+: bits 3:0).
@@ -926,19 +1181,66 @@ __device__ __forceinline__ int xcc_id() {
   case ID:                                                                                           \
     lane_unit<PW_, PH_, UW_, UH_>(a, w.sjobs, w.perm, sc->class_off[ID], sc->class_cnt[ID], wt);     \
     break;
+#ifndef FME_LANE_WAVE_CLAIMS   // 1: each wave claims its own tiles (no workgroup barrier per claim)
+#define FME_LANE_WAVE_CLAIMS 0
+#endif
 __global__ __launch_bounds__(kLaneNT) __attribute__((amdgpu_waves_per_eu(FME_LANE_WAVES)))
 void k_search_lane(BatchArgs a, WorkBufs w) {
-  constexpr int kGroup = kLaneNT / 64;   // wave tiles per claim
-  __shared__ int32_t claim[2];
   const Schedule* __restrict__ sc = w.sched;
   int32_t* ctr = w.tile_ctr;
-  const int home = xcc_id(), wid = threadIdx.x >> 6;
+  __shared__ int32_t s_xq[8][kNumClasses + 1];
+  {   // the batch's tables and the XCD queues, once per workgroup
+    const uint32_t* ps = reinterpret_cast<const uint32_t*>(a.pics);
+    uint32_t* pd = reinterpret_cast<uint32_t*>(g_pics);
+    for (int i = threadIdx.x; i < (int)(sizeof(g_pics) / 4); i += kLaneNT) pd[i] = ps[i];
+    if (threadIdx.x < FME_MAX_LAMBDAS) g_ml[threadIdx.x] = a.mlambda[threadIdx.x];
+    for (int i = threadIdx.x; i < 8 * (kNumClasses + 1); i += kLaneNT) (&s_xq[0][0])[i] = (&sc->xq[0][0])[i];
+  }
+  const int home = xcc_id(), wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
+#if FME_LANE_WAVE_CLAIMS
+  __syncthreads();
+  // Each wave claims one tile at a time from its XCD's queue, the next claim issued before the
+  // current tile is searched (its latency hides behind the tile), then drains the other XCDs'.
+  // The class of tile t is the number of class starts xq[x][c] <= t, less one: a ballot over the
+  // queue's 25 boundaries held one per lane.
+  auto claim_v = [&](int xx) FME_AI {   // the claimed index in lane 0 (read after the tile)
+    int v = 0;
+    if (lane == 0) v = atomicAdd(&ctr[xx], 1);
+    return v;
+  };
+  auto claim = [&](int xx) FME_AI { return __builtin_amdgcn_readfirstlane(claim_v(xx)); };
+  int x = home, tried = 0;
+  int xql = lane <= kNumClasses ? s_xq[x][lane] : 0x7FFFFFFF;
+  int len = __builtin_amdgcn_readlane(xql, kNumClasses);
+  int t = claim(x);
+  while (true) {
+    if (t >= len) {   // queue drained: the next XCD's
+      if (++tried == 8) break;
+      x = (home + tried) & 7;
+      xql = lane <= kNumClasses ? s_xq[x][lane] : 0x7FFFFFFF;
+      len = __builtin_amdgcn_readlane(xql, kNumClasses);
+      t = claim(x);
+      continue;
+    }
+    const int nxt_v = claim_v(x);
+    const int c = __popcll(__ballot(lane < kNumClasses && xql <= t)) - 1;
+    const int nt = sc->prefix[c + 1] - sc->prefix[c];
+    const int wt = x * (nt >> 3) + min(x, nt & 7) + (t - __builtin_amdgcn_readlane(xql, c));
+    switch (c) {
+      FME_LANE_CLASSES(FME_CASE)
+      default: break;
+    }
+    t = __builtin_amdgcn_readfirstlane(nxt_v);
+  }
+#else
+  constexpr int kGroup = kLaneNT / 64;   // wave tiles per claim
+  __shared__ int32_t claim[2];
   int x = home, tried = 0, par = 0;
   if (threadIdx.x == 0) claim[0] = atomicAdd(&ctr[x], 1);
   __syncthreads();
   int t = __builtin_amdgcn_readfirstlane(claim[0]);
   while (true) {
-    const int len = sc->xq[x][kNumClasses];
+    const int len = s_xq[x][kNumClasses];
     if (kGroup * t >= len) {   // queue drained: the next XCD's
       if (++tried == 8) break;
       x = (home + tried) & 7;
@@ -953,9 +1255,9 @@ void k_search_lane(BatchArgs a, WorkBufs w) {
     const int tw = kGroup * t + wid;
     if (tw < len) {
       int c = 0;
-      while (c < kNumClasses - 1 && tw >= sc->xq[x][c + 1]) c++;
+      while (c < kNumClasses - 1 && tw >= s_xq[x][c + 1]) c++;
       const int nt = sc->prefix[c + 1] - sc->prefix[c];
-      const int wt = x * (nt >> 3) + min(x, nt & 7) + (tw - sc->xq[x][c]);
+      const int wt = x * (nt >> 3) + min(x, nt & 7) + (tw - s_xq[x][c]);
       switch (c) {
         FME_LANE_CLASSES(FME_CASE)
         default: break;
@@ -966,8 +1268,35 @@ void k_search_lane(BatchArgs a, WorkBufs w) {
     __syncthreads();
     t = __builtin_amdgcn_readfirstlane(claim[par]);
   }
+#endif
+  (void)wid;
+  (void)lane;
 }
 #undef FME_CASE
+
+// The single-PU entry point's kernel (fme_frac_dif_single): one workgroup of one wave searches one
+// PU of class `cls` whose job, key, window picture and record all live in pinned, device-mapped host
+// memory — one launch per call, no copies.
+#define FME_SCASE(ID, PW_, PH_, UW_, UH_)                                                            \
+  case ID:                                                                                           \
+    lane_unit<PW_, PH_, UW_, UH_>(a, w.sjobs, w.perm, 0, 1, 0);                                      \
+    break;
+__global__ __launch_bounds__(64) void k_search_single(BatchArgs a, WorkBufs w, int cls) {
+  if (threadIdx.x < sizeof(PicDesc) / 4)
+    reinterpret_cast<uint32_t*>(g_pics)[threadIdx.x] = reinterpret_cast<const uint32_t*>(a.pics)[threadIdx.x];
+  if (threadIdx.x == 0) g_ml[0] = a.mlambda[0];
+  __syncthreads();
+  switch (cls) {
+    FME_LANE_CLASSES(FME_SCASE)
+    default: break;
+  }
+}
+#undef FME_SCASE
+
+hipError_t launch_search_single(const BatchArgs& a, const WorkBufs& w, int cls, hipStream_t s) {
+  hipLaunchKernelGGL(k_search_single, dim3(1), dim3(64), 0, s, a, w, cls);
+  return hipGetLastError();
+}
 
 // Lanes per PU of a lane-kernel class, 0 for classes the cooperative kernels serve.
 int lane_lanes_per_pu(int cls) {

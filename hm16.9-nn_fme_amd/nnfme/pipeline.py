@@ -61,25 +61,46 @@ ORG0 = 32      # first original-picture slot
 REFS = 4       # lowdelay_P / the workloads' reference count
 
 
-def group_jobs(base, frames):
+def group_jobs(base, frames, key_count=0):
     """The job batch of a group of `frames` frames: the base frame's jobs (org_id anything,
-    ref_id = reference distance - 1 in 0..3, lambda slot 0) once per frame, slots remapped."""
+    ref_id = reference distance - 1 in 0..3, lambda slot 0) once per frame, slots remapped; frame
+    j's bi-pred key blocks follow frame j-1's (key_count elements per frame)."""
     out = []
     for j in range(frames):
         g = np.array(base, dtype=JOB_DTYPE, copy=True)
         g["org_id"] = ORG0 + j
         g["ref_id"] = j + 3 - base["ref_id"].astype(np.int64)
         g["lambda_id"] = j
+        bi = g["key_offset"] >= 0
+        g["key_offset"][bi] += j * key_count
+        out.append(g)
+    return np.concatenate(out)
+
+
+def group_key_reqs(base, frames, key_count):
+    """The bi-pred key requests (fme_bikey_req) of a group of frames, remapped like group_jobs:
+    frame j's original in slot ORG0 + j, its reference at distance ref_id + 1 in slot
+    j + 3 - ref_id, its keys at key_offset + j * key_count."""
+    from .abi import BIKEY_REQ_DTYPE
+    out = []
+    for j in range(frames):
+        g = np.array(base, dtype=BIKEY_REQ_DTYPE, copy=True)
+        g["org_id"] = ORG0 + j
+        g["ref_id"] = j + 3 - base["ref_id"].astype(np.int64)
+        g["key_offset"] += j * key_count
         out.append(g)
     return np.concatenate(out)
 
 
 class FrameReplay:
     def __init__(self, ctx, base_jobs, pool, lambda_of, n_steps, frames_per_step=1, world=1, rank=0, device=None,
-                 group=None, defer_download=True):
+                 group=None, defer_download=True, key_reqs=None, key_count=0):
         """ctx: an FmeContext on `device`; base_jobs: one frame's jobs (ref_id = reference
         distance - 1); pool: uint8 [P, H, W] host frames, frame g's pictures are pool[g % P];
-        lambda_of(g): frame g's lambda."""
+        lambda_of(g): frame g's lambda.  key_reqs (fme_bikey_req, ref_id = distance - 1) and
+        key_count: the frame's bi-pred key requests; each step uploads them with its jobs and builds
+        its frames' removeHighFreq keys on the device from that step's pictures, before its batch
+        (fme_build_bipred_keys_device), so the keys are per-frame work inside the timed step."""
         import torch
         self.torch, self.ctx = torch, ctx
         self.world, self.rank, self.group = world, rank, group
@@ -89,10 +110,16 @@ class FrameReplay:
         P, H, W = pool.shape
         self.P, self.H, self.W = P, H, W
         self.pool = torch.from_numpy(np.ascontiguousarray(pool)).pin_memory()
-        self.jobs = group_jobs(base_jobs, F)
+        self.key_count = int(key_count)
+        self.jobs = group_jobs(base_jobs, F, self.key_count)
         self.n = n = len(self.jobs)
         self.h_jobs = torch.from_numpy(self.jobs.view(np.uint8).copy()).pin_memory()
         self.d_jobs = [torch.empty(n * JOB_DTYPE.itemsize, dtype=torch.uint8, device=device) for _ in range(2)]
+        self.kreqs = None
+        if key_reqs is not None and len(key_reqs):
+            self.kreqs = group_key_reqs(key_reqs, F, self.key_count)
+            self.h_kreqs = torch.from_numpy(self.kreqs.view(np.uint8).copy()).pin_memory()
+            self.d_kreqs = [torch.empty(self.h_kreqs.numel(), dtype=torch.uint8, device=device) for _ in range(2)]
         self.d_out = [torch.empty(n * MV_RESULT_DTYPE.itemsize, dtype=torch.uint8, device=device) for _ in range(2)]
         self.h_out = torch.empty((n_steps, n * MV_RESULT_DTYPE.itemsize), dtype=torch.uint8).pin_memory()
         frames = n_steps * world * F
@@ -197,6 +224,8 @@ class FrameReplay:
             if k >= 2:
                 cp.wait_event(self.ev_comp[b])            # step k-2 is done with the slot
             _memcpy_async(self.d_jobs[b], self.h_jobs, self.h_jobs.numel(), H2D, cp)
+            if self.kreqs is not None:
+                _memcpy_async(self.d_kreqs[b], self.h_kreqs, self.h_kreqs.numel(), H2D, cp)
             self._upload_run(self.org, k * F, f0, F, cp)
             base = k * self.world * F
             for r in range(self.world):   # recon(first frame of rank r's batch - 1 + j), by rank r
@@ -216,6 +245,9 @@ class FrameReplay:
         if k >= 2:
             comp.wait_event(self.ev_out[b])                # step k-2's results have left
         self._bind(k)
+        if self.kreqs is not None:   # this step's frames' removeHighFreq keys, from this step's pictures
+            ctx.build_bipred_keys_device(self.d_kreqs[b].data_ptr(), len(self.kreqs), self.key_count * self.F,
+                                         comp.cuda_stream)
         if self.world > 1:
             ctx.nn_reset()                                 # stream-ordered: this batch starts fresh
         ctx.refine_mv_device(self.d_jobs[b].data_ptr(), self.d_out[b].data_ptr(), self.n, comp.cuda_stream)
@@ -277,6 +309,8 @@ class FrameReplay:
                 continue
             with torch.cuda.stream(comp):
                 self._bind(k)
+                if self.kreqs is not None:
+                    ctx.build_bipred_keys(self.kreqs, self.key_count * self.F, comp.cuda_stream)
                 ctx.nn_set_state(carry)
                 out[:p] = ctx.refine_mv(self.jobs[:p], comp.cuda_stream)
             fixed += p

@@ -6,8 +6,11 @@
 // oracle (oracle/fme_oracle.c, test infrastructure) run over the same job sequence.  Also
 // checks the single-PU xPatternSearchFracDIF / NN_pred entry points and the error path.
 // Exit status 0 = all equal.  Run by tests/test_gpu_parity.py::test_cpp_hm_adapter.
+#include <algorithm>
+#include <chrono>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <memory>
 #include <random>
@@ -357,8 +360,61 @@ static int run() {
   return 0;
 }
 
-int main() {
+// --time-single: wall time per synchronous single-PU call from C++ (xPatternSearchFracDIF at
+// 8x8 / 16x16 / 64x64 and NN_pred), as an HM encoder in drop-in mode would make them; one JSON
+// line on stdout (bench.py's drop_in_single_pu leg).
+int time_single(int calls) {
+  using namespace fme_hm;
+  using clk = std::chrono::steady_clock;
+  SearchConfig cfg;
+  cfg.qp = 22;
+  FracSearch search(cfg);
+  const int PW = W + 2 * PAD;
+  const std::vector<int16_t> pic = make_picture(1, 11), org = make_picture(0, 12);
+  std::vector<int16_t> padded((size_t)PW * (H + 2 * PAD));
+  for (int y = -PAD; y < H + PAD; y++)
+    for (int x = -PAD; x < W + PAD; x++)
+      padded[(size_t)(y + PAD) * PW + x + PAD] =
+          pic[(size_t)std::min(H - 1, std::max(0, y)) * W + std::min(W - 1, std::max(0, x))];
+  std::mt19937 rng(5);
+  auto R = [&](int lo, int hi) { return std::uniform_int_distribution<int>(lo, hi)(rng); };
+  search.setLambda(kLambda[0]);
+  printf("{");
+  const int shapes[3][2] = {{8, 8}, {16, 16}, {64, 64}};
+  for (const auto& sh : shapes) {
+    const int w = sh[0], h = sh[1];
+    std::vector<double> ts;
+    for (int i = 0; i < calls; i++) {
+      const int x = 4 * R(0, (W - w) / 4), y = 4 * R(0, (H - h) / 4);
+      Mv mvInt(R(-8, 8), R(-8, 8)), mh, mq;
+      search.setPredictor(Mv(R(-16, 16), R(-16, 16)));
+      Distortion cost = 0;
+      const int16_t* key = org.data() + (size_t)y * W + x;
+      const int16_t* refY = padded.data() + (size_t)(y + PAD) * PW + x + PAD;
+      const auto t0 = clk::now();
+      search.xPatternSearchFracDIF(false, key, W, w, h, refY, PW, &mvInt, mh, mq, cost);
+      ts.push_back(std::chrono::duration<double, std::micro>(clk::now() - t0).count());
+    }
+    std::sort(ts.begin() + 1, ts.end());
+    printf("\"frac_dif_%dx%d_us\": %.2f, ", w, h, ts[1 + (ts.size() - 1) / 2]);
+  }
+  std::vector<double> ts;
+  for (int i = 0; i < calls; i++) {
+    uint32_t e[8];
+    for (uint32_t& v : e) v = (uint32_t)R(0, 5000);
+    int xh, xq, yh, yq;
+    const auto t0 = clk::now();
+    search.NN_pred(e, (uint32_t)R(0, 5000), 8, 8, xh, xq, yh, yq);
+    ts.push_back(std::chrono::duration<double, std::micro>(clk::now() - t0).count());
+  }
+  std::sort(ts.begin() + 1, ts.end());
+  printf("\"nn_pred_us\": %.2f, \"calls\": %d}\n", ts[1 + (ts.size() - 1) / 2], calls);
+  return 0;
+}
+
+int main(int argc, char** argv) {
   try {
+    if (argc > 1 && !strcmp(argv[1], "--time-single")) return time_single(argc > 2 ? atoi(argv[2]) : 300);
     return run();
   } catch (const fme_hm::Error& e) {
     fprintf(stderr, "hm adapter: error %d: %s\n", e.code(), e.what());

@@ -98,3 +98,46 @@ def test_c4_frame_full_size(frame_c4):
     assert len(mism) == 0, f"{len(mism)} NN class mismatches, first {mism[:5]}"
     assert np.array_equal(a["mv_x"], 4 * a["mv_int_x"].astype(np.int32) + a["nn_class"] % 7 - 3)
     assert np.array_equal(a["mv_y"], 4 * a["mv_int_y"].astype(np.int32) + a["nn_class"] // 7 - 3)
+
+
+def test_replay_builds_keys_per_frame():
+    """FrameReplay with bi-pred key requests: each step uploads its frames' requests and builds
+    their keys on the device from that step's pictures; the replayed results (MV, cost, bits, NN
+    class, carried state across frames) equal the oracle run frame after frame with each frame's
+    own pictures and keys."""
+    import torch
+    from nnfme import pipeline
+    from nnfme.abi import MV_RESULT_DTYPE
+    from nnfme.pipeline import FrameReplay
+    from nnfme.runtime import FmeContext
+    from oracle import Oracle
+    w, h, F, steps = 416, 240, 2, 3
+    rng = np.random.default_rng(41)
+    base = synth.make_ctu_jobs(rng, w, h, 120, 4, [0, 1, 2, 3], [0], bipred_frac=0.2)
+    reqs, kc = synth.make_bipred_key_reqs(np.random.default_rng(42), base, 4, [0, 1, 2, 3])
+    pool = np.stack([synth.synth_luma(w, h, t) for t in range(8)])
+    lam = lambda f: synth.ra_lambda(QP, f % 8)   # noqa: E731
+    ctx = FmeContext(nn_mode=1, qp=QP, fast_inter_mode=1)
+    rep = FrameReplay(ctx, base, pool, lam, steps, frames_per_step=F, device=torch.device("cuda", 0),
+                      key_reqs=reqs, key_count=kc)
+    rep.prime()
+    for k in range(steps):
+        rep.issue(k)
+    rep.finish()
+    o = Oracle(nn_mode=1, qp=QP)
+    o.load_nn(weights.load_weights(QP))
+    for k in range(steps):
+        f0 = rep.first_frame(k)
+        pics = {pipeline.ORG0 + j: pool[(f0 + j) % 8] for j in range(F)}
+        pics.update({s: pool[(f0 - pipeline.REFS + s) % 8] for s in range(F + pipeline.REFS - 1)})
+        for kk, v in pics.items():
+            o.set_picture(kk, v)
+        for j in range(F):
+            o.set_lambda(j, lam(f0 + j))
+        o.set_keys(synth.bipred_keys(rep.kreqs, pics, kc * F))
+        want = o.refine(rep.jobs)
+        got = rep.results(k)
+        for f in ("mv_x", "mv_y", "cost", "bits", "nn_class"):
+            bad = np.flatnonzero(got[f] != want[f])
+            assert len(bad) == 0, f"step {k}: {f} differs at {len(bad)} jobs, first {bad[:5]}"
+    assert got.dtype == MV_RESULT_DTYPE
