@@ -607,6 +607,7 @@ def main():
             t = t.cpu()
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
+    rep.check_status(args.warmup)   # no timed step may have been rejected on the device
     nb, acc = ctx.accumulated_timings(reset=True)
     ctx.set_profiling(False)
     tm = {k: v / max(nb, 1) for k, v in acc.items()}

@@ -111,6 +111,7 @@ struct fme_ctx {
   bool net_loaded = false;
   int nn_engine = FME_NN_ENGINE_EXACT;
   float* nn_margin = nullptr;  // caller-owned device array (fme_set_nn_margin_output)
+  int nn_margin_cap = 0;       // its length
 
   DevBuf<fme_job> d_jobs;      // staging for fme_refine (host arrays)
   DevBuf<fme_result> d_res;
@@ -470,9 +471,11 @@ int fme_set_nn_engine(fme_ctx* c, int engine) {
   return FME_OK;
 }
 
-int fme_set_nn_margin_output(fme_ctx* c, float* d_margin) {
+int fme_set_nn_margin_output(fme_ctx* c, float* d_margin, int capacity) {
   if (!c) return fail(FME_E_INVALID, "fme_set_nn_margin_output: null ctx");
-  c->nn_margin = d_margin;
+  if (d_margin && capacity <= 0) return fail(FME_E_INVALID, "fme_set_nn_margin_output: capacity %d", capacity);
+  c->nn_margin = capacity > 0 ? d_margin : nullptr;
+  c->nn_margin_cap = d_margin ? capacity : 0;
   return FME_OK;
 }
 
@@ -596,6 +599,8 @@ static int refine_batch(fme_ctx* c, const fme_job* d_jobs, fme_result* d_res, fm
                         hipStream_t s) {
   if (c->cfg.nn_mode == 1 && !c->nn_loaded) return fail(FME_E_STATE, "fme_refine_device: nn_mode set but no weights loaded");
   if (c->cfg.nn_mode == 2 && !c->net_loaded) return fail(FME_E_STATE, "fme_refine_device: nn_mode 2 but no net loaded");
+  if (c->cfg.nn_mode == 2 && c->nn_margin && n > c->nn_margin_cap)
+    return fail(FME_E_INVALID, "fme_refine: %d jobs but the margin output holds %d", n, c->nn_margin_cap);
   HIP_TRY(hipSetDevice(c->device));
   int rc = ensure_work(c, n);
   if (rc) return rc;

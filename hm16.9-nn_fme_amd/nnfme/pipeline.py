@@ -259,8 +259,8 @@ class FrameReplay:
         if not self.defer_download:
             self._download(k, self.ev_comp[b])
             return
-        if self.pending is not None:
-            self._download(self.pending, self.ev_search)   # step k's search started: k-1 is done
+        if self.pending is not None:   # step k's search started: k-1 is done (its own batch event otherwise)
+            self._download(self.pending, self.ev_search if self.n > 0 else self.ev_comp[self.pending & 1])
         self.pending = k
 
     def _download(self, k, after):
@@ -270,13 +270,23 @@ class FrameReplay:
         self.ev_out[k & 1].record(dn)
 
     def drain(self):
-        """Issue the last step's download and wait for every stream."""
+        """Issue the last step's download and wait for every stream; the library no longer records
+        into this replay's search event afterwards (the context may outlive the replay)."""
         if self.pending is not None:
             self._download(self.pending, self.ev_comp[self.pending & 1])
             self.pending = None
         self.s_copy.synchronize()
         self.s_comp.synchronize()
         self.s_down.synchronize()
+        self.ctx.set_search_event(None)
+
+    def check_status(self, first_step=0):
+        """Raise if any step's batch was rejected on the device (FME_RES_REJECTED: an invalid job
+        or invalid device-built keys); the throughput of a rejected step would count nothing."""
+        from .abi import RES_REJECTED
+        for k in range(first_step, self.steps):
+            if np.any(self.results(k)["status"] & RES_REJECTED):
+                raise RuntimeError(f"frame replay: step {k}'s batch was rejected on the device")
 
     def results(self, k):
         return self.h_out[k].numpy().view(MV_RESULT_DTYPE)

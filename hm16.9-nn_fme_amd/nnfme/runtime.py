@@ -95,7 +95,7 @@ def load_library(path=None):
         "fme_nn_param_count": (I, [P]),
         "fme_load_nn_net": (I, [P, P, P, I]),
         "fme_set_nn_engine": (I, [P, I]),
-        "fme_set_nn_margin_output": (I, [P, P]),
+        "fme_set_nn_margin_output": (I, [P, P, I]),
         "fme_refine_mv": (I, [P, P, P, I, P]),
         "fme_refine_mv_device": (I, [P, P, P, I, P]),
         "fme_refine_status": (I, [P]),
@@ -300,9 +300,11 @@ class FmeContext:
         """0: exact (bit-exact to the reference's loops), 1: MFMA GEMM (k-ordered FMA chain)."""
         _check(self.lib, self.lib.fme_set_nn_engine(self.h, int(engine)))
 
-    def set_nn_margin_output(self, d_ptr):
-        """Device float[n] receiving top-1 minus top-2 of each later batch's NN outputs (0: off)."""
-        _check(self.lib, self.lib.fme_set_nn_margin_output(self.h, C.c_void_p(d_ptr) if d_ptr else None))
+    def set_nn_margin_output(self, d_ptr, capacity=0):
+        """Device float[capacity] receiving top-1 minus top-2 of each later batch's NN outputs (0: off);
+        a later batch of more than `capacity` jobs is rejected."""
+        _check(self.lib, self.lib.fme_set_nn_margin_output(self.h, C.c_void_p(d_ptr) if d_ptr else None,
+                                                           int(capacity) if d_ptr else 0))
 
     def nn_reset(self):
         _check(self.lib, self.lib.fme_nn_reset_state(self.h))

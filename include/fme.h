@@ -226,7 +226,9 @@ int fme_load_nn_net(fme_ctx* ctx, const fme_nn_net* net, const double* params, i
 int fme_set_nn_engine(fme_ctx* ctx, int engine);
 /* Optional diagnostic output of nn_mode 2: a device array of n floats that each later batch fills
  * with top-1 minus top-2 of OUT (after the output activation) per job; NULL turns it off. */
-int fme_set_nn_margin_output(fme_ctx* ctx, float* d_margin);
+int fme_set_nn_margin_output(fme_ctx* ctx, float* d_margin, int capacity);
+/* (capacity: elements of d_margin; a later nn_mode 2 batch larger than that is rejected with
+ * FME_E_INVALID instead of writing past the caller's array; d_margin null / capacity 0: off) */
 
 /* Forget the array_e/C/PUHeight/PUWidth state carried across calls (process start).  Stream-
  * ordered: it takes effect at the start of the next batch, after every batch already issued. */

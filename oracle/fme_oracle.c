@@ -47,7 +47,7 @@ uint32_t orc_cost(double mlambda, uint32_t bits) {
 
 /* getBitsOfVectorWithPredictor, TComRdCost.h:171-174. */
 static inline uint32_t mv_bits(int x, int y, int scale, int px, int py) {
-  return orc_eg_bits((x << scale) - px) + orc_eg_bits((y << scale) - py);
+  return orc_eg_bits(x * (1 << scale) - px) + orc_eg_bits(y * (1 << scale) - py);   /* x << scale (UB for x < 0 in C) */
 }
 
 /* Edge-replicated sample (TComPicYuv::extendPicBorder, TComPicYuv.cpp:229-276). */
@@ -639,7 +639,7 @@ static void mc_filter(int ntaps, const int* coef, int vert, int first, int last,
     offset += first ? 0 : 8192 << 6;
   } else {
     shift -= first ? 6 : 0;
-    offset = first ? -8192 << shift : 0;
+    offset = first ? -8192 * (1 << shift) : 0;   /* -8192 << shift (UB in C) */
   }
   for (int r = 0; r < h; r++)
     for (int c = 0; c < w; c++) {

@@ -57,10 +57,13 @@ def edge_jobs(rng, width, height, n):
     return j
 
 
-def build_case(name, seed, width, height, n_jobs, hadme, fen, nn_mode, qp, bipred=0.15, n_edge=96, net=None):
+def build_case(name, seed, width, height, n_jobs, hadme, fen, nn_mode, qp, bipred=0.15, n_edge=96, net=None, gop="ldp"):
     rng = np.random.default_rng(seed)
     pics = {i: synth.synth_luma(width, height, i, seed=seed) for i in range(5)}
-    lambdas = np.array(synth.LDP_LAMBDA[qp if qp in synth.LDP_LAMBDA else 22], dtype=np.float64)
+    if gop == "ra":   # random-access GOP-8 lambdas (TEncSlice.cpp:246-325): entries POC 8, 4, 2, 1
+        lambdas = np.array([synth.ra_lambda(qp, e) for e in range(4)], dtype=np.float64)
+    else:
+        lambdas = np.array(synth.LDP_LAMBDA[qp if qp in synth.LDP_LAMBDA else 22], dtype=np.float64)
     a = synth.make_jobs(rng, width, height, n_jobs, 4, [0, 1, 2, 3], [0, 1, 2, 3], bipred_frac=bipred)
     b = edge_jobs(rng, width, height, n_edge)
     jobs = np.concatenate([b[:8], a, b[8:]])
@@ -202,6 +205,10 @@ CASES = [
     ("fen3_qp27_nn", 13, 128, 96, 400, 1, 3, 1, 27),
     ("qp32_nn", 14, 128, 96, 400, 1, 1, 1, 32),
     ("qp37_nn", 15, 128, 96, 400, 1, 1, 1, 37),
+    # configs[1] exactly: HADME on, FEN 1, NN_pred off (the standard FracDIF MV)
+    ("hadme_fen1_nnoff_qp22", 18, 160, 96, 800, 1, 1, 0, 22),
+    # configs[3]'s random-access lambdas (GOP-8 depths 0..3) with its bi-pred share
+    ("ra_qp27_nn", 19, 160, 96, 800, 1, 1, 1, 27, 0.205, 96, None, "ra"),
 ]
 
 
@@ -217,6 +224,12 @@ DEEP_CASES = [
 
 def main():
     os.makedirs(OUT, exist_ok=True)
+    only = sys.argv[sys.argv.index("--only") + 1].split(",") if "--only" in sys.argv else None
+    if only:
+        for c in CASES + DEEP_CASES:
+            if c[0] in only:
+                build_case(*c)
+        return 0
     if "--deep-only" in sys.argv:
         for c in DEEP_CASES:
             build_case(*c)

@@ -9,7 +9,8 @@ import os
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-ORACLE_SO = os.path.join(HERE, "liboracle.so")
+# FME_ORACLE_SO: the sanitizer build (liboracle_asan.so, tests/test_sanitize.py) instead
+ORACLE_SO = os.environ.get("FME_ORACLE_SO") or os.path.join(HERE, "liboracle.so")
 REF_SO = os.path.join(HERE, "_ref", "libhmref.so")
 
 _P = C.c_void_p

@@ -63,7 +63,7 @@ std::vector<int16_t> make_picture(int t, uint32_t seed) {
 }
 
 int clip_qpel(int v, int pos, int pic) {   // TComDataCU::clipMv (TComDataCU.cpp:2778-2785)
-  const int vmax = (pic + 8 - pos - 1) << 2, vmin = (-64 - 8 - pos + 1) << 2;
+  const int vmax = (pic + 8 - pos - 1) * 4, vmin = (-64 - 8 - pos + 1) * 4;   // (HM shifts; UB on negatives here)
   return std::min(vmax, std::max(vmin, v));
 }
 int div4_round(int v) { return (v + 2) >> 2; }   // TComMv::divideByPowerOf2 with rounding

@@ -167,7 +167,7 @@ def _frame_run(pics, jobs, name, engine, margin=False):
     m = None
     if margin:
         m = torch.zeros(len(jobs), dtype=torch.float32, device="cuda")
-        ctx.set_nn_margin_output(m.data_ptr())
+        ctx.set_nn_margin_output(m.data_ptr(), len(jobs))
     res = ctx.refine(jobs)
     ctx.set_nn_margin_output(0)
     return res, (m.cpu().numpy() if m is not None else None)
