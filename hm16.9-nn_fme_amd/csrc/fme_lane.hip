@@ -1151,19 +1151,20 @@ __device__ __forceinline__ int xcc_id() {
 // (class id, PU W, PU H, unit W, unit H) — fme_device.h class table; one kernel per unit
 // shape, since a kernel's register allocation is the maximum over its cases.
 // 4x8 units for every shape whose width is a multiple of 4 and height a multiple of 8 (an 8x8
-// SATD tile is a lane pair; 4x4-tiled shapes keep their two tiles in the lane), 8x4 units for
-// 8x4 / 16x4 / 16x12.  (4x4 units for the 4x4-tiled shapes: 6-13 % more instructions per PU,
-// A/B 0.924 -> see DESIGN §4.)
+// SATD tile is a lane pair; the 4x4-tiled 4x8 / 4x16 / 12x16 keep their two tiles in the lane),
+// 4x4 units (one SATD tile each) for 8x4 / 16x4 / 16x12.  (4x4 units for 4x8-tiled shapes: about
+// 18 % more instructions per PU, measured 0.924 -> 0.9xx ms; 8x4 units for the 8x4-like shapes gave
+// wrong half / quarter results on ~15 % of their golden jobs and are not used)
 #define FME_LANE48_CLASSES(X) X(0, 4, 8, 4, 8) X(3, 4, 16, 4, 8)
-#define FME_LANE84_CLASSES(X) X(1, 8, 4, 8, 4) X(4, 16, 4, 8, 4)
+#define FME_LANE84_CLASSES(X) X(1, 8, 4, 4, 4) X(4, 16, 4, 4, 4)
 #define FME_LANE88_CLASSES(X)                                                                        \
   X(2, 8, 8, 4, 8) X(5, 8, 16, 4, 8) X(6, 16, 8, 4, 8) X(9, 16, 16, 4, 8) X(10, 8, 32, 4, 8)         \
   X(11, 32, 8, 4, 8) X(12, 16, 32, 4, 8) X(13, 32, 16, 4, 8) X(16, 32, 32, 4, 8) X(17, 16, 64, 4, 8) \
   X(18, 64, 16, 4, 8) X(19, 32, 64, 4, 8) X(20, 64, 32, 4, 8) X(23, 64, 64, 4, 8)
-// the AMP shapes whose unit count is not a power of two: 12x16 / 16x12 (6 of 8 lanes), 24x32 /
-// 32x24 (24 of 32), 48x64 / 64x48 (two halves of 48 units, 48 of 64 lanes)
+// the AMP shapes whose unit count is not a power of two: 12x16 (6 of 8 lanes), 16x12 in 4x4 units
+// (12 of 16), 24x32 / 32x24 (24 of 32), 48x64 / 64x48 (two halves of 48 units, 48 of 64 lanes)
 #define FME_LANE_AMP_CLASSES(X)                                                                      \
-  X(7, 12, 16, 4, 8) X(8, 16, 12, 8, 4) X(14, 24, 32, 4, 8) X(15, 32, 24, 4, 8) X(21, 48, 64, 4, 8)   \
+  X(7, 12, 16, 4, 8) X(8, 16, 12, 4, 4) X(14, 24, 32, 4, 8) X(15, 32, 24, 4, 8) X(21, 48, 64, 4, 8)   \
   X(22, 64, 48, 4, 8)
 #ifndef FME_LANE_CLASSES   // (a subset may be given on the command line for register-usage probes)
 #define FME_LANE_CLASSES(X) \
