@@ -68,15 +68,22 @@ WORKLOADS = {
                desc="2560x1600 random-access QP27 B-frames, NN_pred on, 2+2 refs, ~1331 calls/CTU, 20.5 % bi-pred "
                     "with 2*org - pred keys built per frame on the device inside the timed step, RA GOP-8 "
                     "lambdas (configs[3])"),
-    "c5": dict(W=1920, H=1080, QP=22, nn=2, net="scr3x40", engine=1, calls=423, bipred=0.0, gop="ldp", frames=1,
+    "c5": dict(W=1920, H=1080, QP=22, nn=2, net="scr3x40+slotreset", engine=1, calls=423, bipred=0.0, gop="ldp",
+               frames=1,
                desc="1920x1080 lowdelay_P QP22 with the 3-hidden-layer NN_pred (Backups/4 SCR 9-40-40-40-49, "
-                    "double) as a batched MFMA GEMM (v_mfma_f64_16x16x4) (configs[4])"),
-    "c5_exact": dict(W=1920, H=1080, QP=22, nn=2, net="scr3x40", engine=0, calls=423, bipred=0.0, gop="ldp",
-                     frames=1, desc="configs[4] net through the exact (scalar, reference-order) engine"),
-    "c5_b4x40": dict(W=1920, H=1080, QP=22, nn=2, net="blowing4x40+rezero", engine=1, calls=423, bipred=0.0,
+                    "double) as a batched MFMA GEMM (v_mfma_f64_16x16x4) (configs[4]); the SCR weights run on the "
+                    "master's EMI inputs (distance-1 SSE square, C = its best) with the backups' per-call "
+                    "array_e reset, not on Backups/4's own input path (every-point SAD pushes, C = min over "
+                    "the TZ points, distance-2 ring): input parity with the backup unpinned (include/fme.h)"),
+    "c5_exact": dict(W=1920, H=1080, QP=22, nn=2, net="scr3x40+slotreset", engine=0, calls=423, bipred=0.0,
                      gop="ldp", frames=1,
+                     desc="configs[4] net through the exact (scalar, reference-order) engine, master's EMI "
+                          "inputs with the per-call array_e reset"),
+    "c5_b4x40": dict(W=1920, H=1080, QP=22, nn=2, net="blowing4x40+rezero+slotreset", engine=1, calls=423,
+                     bipred=0.0, gop="ldp", frames=1,
                      desc="1920x1080 QP22 with the 4x40 blowing net (Backups/15, float, hidden layers re-zeroed) "
-                          "as a batched MFMA GEMM (v_mfma_f32_16x16x4)"),
+                          "as a batched MFMA GEMM (v_mfma_f32_16x16x4), master's EMI inputs with the per-call "
+                          "array_e reset"),
 }
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md chip table (spec)
 # int32 VALU lane-ops/s: 256 CUs x 4 SIMDs x 32 lanes/clk (a wave64 op issues over 2 clk) x
@@ -669,6 +676,9 @@ def main():
                     "NN weights, no random init)",
             "config": {"workload": WDESC,
                        "workload_id": args.workload,
+                       **({"nn_net": wl["net"], "nn_inputs": "master EMI step (distance-1 SSE square, C = its "
+                           "best SSE), per-call array_e reset; Backups/4's own input path not restated "
+                           "(input parity unpinned)"} if NN == 2 else {}),
                        "job_stream": args.jobs,
                        "frames_per_step": FPS,
                        "jobs_per_step_per_gpu": n, "parallelism": f"frame-sharded x{world}",

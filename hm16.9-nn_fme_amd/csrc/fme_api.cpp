@@ -112,6 +112,8 @@ struct fme_ctx {
   int nn_engine = FME_NN_ENGINE_EXACT;
   float* nn_margin = nullptr;  // caller-owned device array (fme_set_nn_margin_output)
   int nn_margin_cap = 0;       // its length
+  void* nn_logits = nullptr;   // caller-owned device array (fme_set_nn_logit_output), 49 per job
+  int nn_logits_cap = 0;       // its length in jobs
 
   DevBuf<fme_job> d_jobs;      // staging for fme_refine (host arrays)
   DevBuf<fme_result> d_res;
@@ -143,6 +145,7 @@ struct fme_ctx {
   DevBuf<uint32_t> d_tz_sad;
   DevBuf<uint32_t> d_tz_rst;   // raster hand-off records [n][8]
   DevBuf<int32_t> d_tz_rq;     // raster queues [3][n] + 3 lengths
+  bool tz_wave = true;                     // FME_TZ_WAVE=0: the lane-per-unit kernels (A/B)
   bool tz_defer = FME_TZ_DEFER_DEFAULT;   // FME_TZ_DEFER=0/1: raster searches in a second pass
   int tz_defer_min = 4096;                 // FME_TZ_DEFER_MIN: batches below this size run in one pass
   hipEvent_t ev_tz[2] = {nullptr, nullptr};
@@ -197,7 +200,7 @@ struct fme_ctx {
 namespace fme {
 size_t nn_deep_packed_bytes(const fme_nn_net& n);
 void nn_deep_pack(const fme_nn_net& n, const double* params, void* out);
-hipError_t launch_nn_deep_tail(const fme_nn_net& n, const void* packed, float* margin, const BatchArgs& a,
+hipError_t launch_nn_deep_tail(const fme_nn_net& n, const void* packed, float* margin, void* logits, const BatchArgs& a,
                                const WorkBufs& w, int state_in, int engine, hipStream_t s);
 hipError_t launch_nn_deep_single(const fme_nn_net& n, const void* packed, const uint32_t* in11, int32_t* out,
                                  hipStream_t s);
@@ -234,6 +237,7 @@ int fme_create(int device, const fme_config* cfg, fme_ctx** out_ctx) {
   HIP_TRY(c->d_key_invalid.reserve(1));
   HIP_TRY(hipMemset(c->d_key_invalid.p, 0, sizeof(int32_t)));
   HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&c->h_counts), (kNumClasses + 1) * sizeof(int32_t), hipHostMallocDefault));
+  if (const char* e = getenv("FME_TZ_WAVE")) c->tz_wave = (e[0] == '1');
   if (const char* e = getenv("FME_TZ_DEFER")) c->tz_defer = (e[0] == '1');
   if (const char* e = getenv("FME_TZ_DEFER_MIN")) c->tz_defer_min = atoi(e);
   if (cfg->max_jobs > 0) {
@@ -433,6 +437,8 @@ int fme_nn_param_count(const fme_nn_net* n) {
   if (n->out_act != FME_NN_OUT_LINEAR && n->out_act != FME_NN_OUT_SIGMOID)
     return fail(FME_E_INVALID, "fme_nn_param_count: out_act %d", n->out_act);
   if (n->carry_hidden >> n->n_hidden) return fail(FME_E_INVALID, "fme_nn_param_count: carry_hidden 0x%x", n->carry_hidden);
+  if (n->input_flags & ~FME_NN_IN_SLOT_RESET)
+    return fail(FME_E_INVALID, "fme_nn_param_count: input_flags 0x%x", n->input_flags);
   int count = n->embedding ? 64 : 0, fan = n->embedding ? 17 : 9;
   for (int l = 0; l < n->n_hidden; l++) {
     const int w = n->width[l];
@@ -468,6 +474,14 @@ int fme_set_nn_engine(fme_ctx* c, int engine) {
   if (!c || (engine != FME_NN_ENGINE_EXACT && engine != FME_NN_ENGINE_MFMA))
     return fail(FME_E_INVALID, "fme_set_nn_engine: bad argument");
   c->nn_engine = engine;
+  return FME_OK;
+}
+
+int fme_set_nn_logit_output(fme_ctx* c, void* d_logits, int capacity) {
+  if (!c) return fail(FME_E_INVALID, "fme_set_nn_logit_output: null ctx");
+  if (d_logits && capacity <= 0) return fail(FME_E_INVALID, "fme_set_nn_logit_output: capacity %d", capacity);
+  c->nn_logits = capacity > 0 ? d_logits : nullptr;
+  c->nn_logits_cap = d_logits ? capacity : 0;
   return FME_OK;
 }
 
@@ -601,6 +615,8 @@ static int refine_batch(fme_ctx* c, const fme_job* d_jobs, fme_result* d_res, fm
   if (c->cfg.nn_mode == 2 && !c->net_loaded) return fail(FME_E_STATE, "fme_refine_device: nn_mode 2 but no net loaded");
   if (c->cfg.nn_mode == 2 && c->nn_margin && n > c->nn_margin_cap)
     return fail(FME_E_INVALID, "fme_refine: %d jobs but the margin output holds %d", n, c->nn_margin_cap);
+  if (c->cfg.nn_mode == 2 && c->nn_logits && n > c->nn_logits_cap)
+    return fail(FME_E_INVALID, "fme_refine: %d jobs but the logit output holds %d", n, c->nn_logits_cap);
   HIP_TRY(hipSetDevice(c->device));
   int rc = ensure_work(c, n);
   if (rc) return rc;
@@ -652,7 +668,7 @@ static int refine_batch(fme_ctx* c, const fme_job* d_jobs, fme_result* d_res, fm
   if (prof) HIP_TRY(hipEventRecord(ev[4], s));
   if (prof) HIP_TRY(hipEventRecord(ev[5], s));
   HIP_TRY(c->cfg.nn_mode == 2
-              ? launch_nn_deep_tail(c->net, c->d_net.p, c->nn_margin, a, w, c->state_cur, c->nn_engine, s)
+              ? launch_nn_deep_tail(c->net, c->d_net.p, c->nn_margin, c->nn_logits, a, w, c->state_cur, c->nn_engine, s)
               : launch_nn_tail(a, w, c->d_nn.p, c->state_cur, s));
   if (prof) {
     HIP_TRY(hipEventRecord(ev[6], s));
@@ -746,7 +762,7 @@ static int tz_run(fme_ctx* c, fme_job* d_jobs, const fme_tz_ext* d_ext, uint32_t
     sc.class_off[k] = off;
     sc.class_cnt[k] = cnt;
     for (int q = 0; q < 3; q++) sc.prefix[q][k] = nb[q];
-    nb[tz_kernel_of(k)] += (int)(((long long)cnt * tz_lanes_per_pu(k) + 255) / 256);
+    nb[tz_kernel_of(k)] += c->tz_wave ? cnt : (int)(((long long)cnt * tz_lanes_per_pu(k) + 255) / 256);
     off += cnt;
   }
   for (int q = 0; q < 3; q++) sc.prefix[q][kNumClasses] = nb[q];
@@ -761,7 +777,7 @@ static int tz_run(fme_ctx* c, fme_job* d_jobs, const fme_tz_ext* d_ext, uint32_t
   ta.emi_mv = d_emi;
   // small batches (the producer's dependency levels) skip the second pass: its extra host
   // synchronisation costs more than the raster divergence it removes
-  const bool defer = c->tz_defer && n >= c->tz_defer_min;
+  const bool defer = !c->tz_wave && c->tz_defer && n >= c->tz_defer_min;
   ta.defer = defer ? 1 : 0;
   if (defer) {
     HIP_TRY(c->d_tz_rst.reserve((size_t)n * 8));
@@ -783,9 +799,9 @@ static int tz_run(fme_ctx* c, fme_job* d_jobs, const fme_tz_ext* d_ext, uint32_t
   HIP_TRY(hipEventRecord(c->ev_fork, s));
   HIP_TRY(hipStreamWaitEvent(c->aux, c->ev_fork, 0));
   HIP_TRY(hipStreamWaitEvent(c->aux2, c->ev_fork, 0));
-  HIP_TRY(launch_tz(ta, sc, 0, c->aux));
-  HIP_TRY(launch_tz(ta, sc, 1, c->aux2));
-  HIP_TRY(launch_tz(ta, sc, 2, s));
+  HIP_TRY((c->tz_wave ? launch_tz_wave : launch_tz)(ta, sc, 0, c->aux));
+  HIP_TRY((c->tz_wave ? launch_tz_wave : launch_tz)(ta, sc, 1, c->aux2));
+  HIP_TRY((c->tz_wave ? launch_tz_wave : launch_tz)(ta, sc, 2, s));
   HIP_TRY(hipEventRecord(c->ev_join, c->aux));
   HIP_TRY(hipEventRecord(c->ev_join2, c->aux2));
   HIP_TRY(hipStreamWaitEvent(s, c->ev_join, 0));

@@ -158,6 +158,7 @@ struct TzSchedule {
 };
 hipError_t launch_tz(const TzArgs& ta, const TzSchedule& sc, int kid, hipStream_t s);
 hipError_t launch_tz_raster(const TzArgs& ta, const TzSchedule& sc, int kid, int nq, hipStream_t s);
+hipError_t launch_tz_wave(const TzArgs& ta, const TzSchedule& sc, int kid, hipStream_t s);   // prefix in waves
 // The dependency levels of a producer's m_integerMv2Nx2N chain (fme_tz.hip k_tz_level): jobs in
 // level order, level l = jobs [lvl_off[l], lvl_off[l+1]), one launch per level, back to back.
 struct TzChain {

@@ -85,8 +85,10 @@ struct DeepLayout {
 struct DeepArgs {
   const void* P;          // packed parameters (float or double)
   float* margin;          // [n] or null
+  void* logits;           // [n][49] of T (OUT before the output activation) or null
   int32_t emb_mode;       // FME_NN_EMB_MASTER / FME_NN_EMB_SWAP (EMB kernels)
   int32_t out_act;        // FME_NN_OUT_*
+  uint32_t in_flags;      // FME_NN_IN_*
 };
 
 // ---- exact engine: one lane per job ----------------------------------------------------------
@@ -317,11 +319,17 @@ __global__ __launch_bounds__(kRound) void k_nn_deep_tail(BatchArgs a, WorkBufs w
     __syncthreads();   // wave_tot is rewritten next round
 
     // the NN_pred() inputs this job sees (TEncSearch.cpp:88-113 / Backups/15:4944-5000)
+    // FME_NN_IN_SLOT_RESET: the backups memset array_e on every call, so only this call's own
+    // pushes are non-zero (Backups/4:4421-4422, Backups/15:4961-4962).
+    const bool reset = (d.in_flags & FME_NN_IN_SLOT_RESET) != 0;
     uint32_t e[8];
     uint32_t written = st_in[11];
 #pragma unroll
     for (int s = 0; s < 8; s++) {
-      if (src[s] >= 0) {
+      if (reset) {
+        e[s] = (valid && src[s] == i) ? a.res[i].emi[s] : 0u;
+        written |= 1u << s;
+      } else if (src[s] >= 0) {
         e[s] = valid ? a.res[src[s]].emi[s] : 0u;
         written |= 1u << s;
       } else {
@@ -348,6 +356,11 @@ __global__ __launch_bounds__(kRound) void k_nn_deep_tail(BatchArgs a, WorkBufs w
       forward_exact<T, NH, EMB>(P, in, out);
     }
     if (!valid) continue;
+    if (d.logits) {
+      T* lg = static_cast<T*>(d.logits) + (size_t)i * 49;
+#pragma unroll
+      for (int o = 0; o < 49; o++) lg[o] = out[o];
+    }
     const int cls = nn_argmax(out, d.out_act, d.margin ? d.margin + i : nullptr);
 
     fme_result* r = a.res + i;
@@ -532,10 +545,10 @@ void nn_deep_pack(const fme_nn_net& n, const double* params, void* out) {
     pack_t<float>(n, params, static_cast<float*>(out));
 }
 
-hipError_t launch_nn_deep_tail(const fme_nn_net& n, const void* packed, float* margin, const BatchArgs& a,
+hipError_t launch_nn_deep_tail(const fme_nn_net& n, const void* packed, float* margin, void* logits, const BatchArgs& a,
                                const WorkBufs& w, int state_in, int engine, hipStream_t s) {
   if (!deep_supported(n)) return hipErrorInvalidValue;
-  const DeepArgs d{packed, margin, n.embedding, n.out_act};
+  const DeepArgs d{packed, margin, logits, n.embedding, n.out_act, n.input_flags};
   const bool emb = n.embedding != FME_NN_EMB_NONE, mfma = engine == FME_NN_ENGINE_MFMA;
   if (n.precision == FME_NN_F64)
     return (mfma ? launch_deep_double_1 : launch_deep_double_0)(n.n_hidden, emb, a, w, d, state_in, s);
@@ -545,7 +558,7 @@ hipError_t launch_nn_deep_tail(const fme_nn_net& n, const void* packed, float* m
 hipError_t launch_nn_deep_single(const fme_nn_net& n, const void* packed, const uint32_t* in11, int32_t* out,
                                  hipStream_t s) {
   if (!deep_supported(n)) return hipErrorInvalidValue;
-  const DeepArgs d{packed, nullptr, n.embedding, n.out_act};
+  const DeepArgs d{packed, nullptr, nullptr, n.embedding, n.out_act, n.input_flags};
   const bool emb = n.embedding != FME_NN_EMB_NONE;
   return n.precision == FME_NN_F64 ? single_deep_double(n.n_hidden, emb, d, in11, out, s)
                                    : single_deep_float(n.n_hidden, emb, d, in11, out, s);

@@ -30,6 +30,7 @@ namespace {
 using namespace simd;
 
 constexpr int kTzNT = 256;
+#define FME_AI __attribute__((always_inline))
 
 template <int CTRL>
 __device__ __forceinline__ uint32_t dpp(uint32_t v) {
@@ -679,6 +680,272 @@ __device__ __forceinline__ void tz_unit(const TzArgs& ta, int cls_off, int cls_c
   }
 }
 
+// ---- wave-uniform search: one wave per PU ------------------------------------------------------
+// The reference's xTZSearch is a short sequence of candidate LISTS whose points do not depend on
+// each other: the three start points, the first search's diamond rings (dist 1, 2, 4, ... around
+// one origin), the two-point pair, the raster, each star round's rings, the EMI square.  A wave
+// owns one PU; its G = 64 / L lane groups evaluate G points of a list at a time (L lanes = the
+// PU's units), and xTZSearchHelp's in-order updates become a (cost, call index) minimum: in-order
+// strict updates keep the first minimum below the running best.  The first search's stop rule
+// (3 rings without a new best) needs per-ring minima, so its rings sit in 16-slot segments and are
+// decided one by one as their chunk completes (later rings are not evaluated once it stops).
+// Every branch is wave-uniform: no lane idles while another lane's search runs on.
+//
+// Ring slot 16 r + k = point k of xTZ8PointDiamondSearch(origin, 1 << r) (diamond_point order).
+__device__ __forceinline__ uint64_t wave_min_from(uint64_t key, int L, int lim) {
+  for (int off = L; off < lim; off <<= 1) {
+    const uint64_t o = (uint64_t)__shfl_xor((unsigned long long)key, off, 64);
+    key = o < key ? o : key;
+  }
+  return key;
+}
+
+template <int UW, int UH>
+__device__ __forceinline__ void tz_wave(const TzArgs& ta, int jid, const fme_job& j, int PW, int PH, int pred_x,
+                                        int pred_y) {
+  const BatchArgs& a = ta.a;
+  const int lane = (int)threadIdx.x & 63;
+  const int UX = PW / UW, LR = UX * (PH / UH);
+  int L = 1;
+  while (L < LR) L <<= 1;
+  const int G = 64 / L, g = lane / L, u = lane - g * L;
+  const bool real = u < LR;
+  const int uu = real ? u : 0;
+  const int ux = uu % UX, uy = uu / UX;
+  const fme_tz_ext e = ta.ext[jid];
+  const PicDesc ref = a.pics[j.ref_id];
+  const double ml = a.mlambda[j.lambda_id];
+  const bool kbuf = j.key_offset >= 0;
+  const bool sad_metric = PW == 12 || PW == 24 || PW == 48;
+  const bool sub = sad_metric && (a.fen == 1 || a.fen == 3) && PH > 8;
+  const int ox = (int)j.x + ux * UW, oy = (int)j.y + uy * UH;
+  constexpr int ND = UW / 4 + 1;
+
+  uint32_t kk[UH][UW / 2];
+  int sk2 = 0;
+  if (!kbuf) {
+    const PicDesc org = a.pics[j.org_id];
+#pragma unroll
+    for (int r = 0; r < UH; r++) {
+#pragma unroll
+      for (int c = 0; c < UW / 4; c++) {
+        const uint32_t v = gld32(org.luma + (size_t)(oy + r) * org.stride + ox + 4 * c);
+        kk[r][c] = v;
+        sk2 = dot4(v ^ 0x80808080u, v ^ 0x80808080u, sk2);
+      }
+#pragma unroll
+      for (int c = UW / 4; c < UW / 2; c++) kk[r][c] = 0;
+    }
+  } else {
+    const int16_t* kb = a.keys + (size_t)j.key_offset + (size_t)(uy * UH) * PW + ux * UW;
+#pragma unroll
+    for (int r = 0; r < UH; r++)
+#pragma unroll
+      for (int c = 0; c < UW / 2; c++)
+        kk[r][c] = (uint32_t)(uint16_t)kb[r * PW + 2 * c] | ((uint32_t)(uint16_t)kb[r * PW + 2 * c + 1] << 16);
+  }
+
+  // distortion + MV cost of this group's candidate (all lanes of the group get it); ~0: not tested
+  auto cost_at = [&](int x, int y, bool v) FME_AI -> uint32_t {
+    uint32_t part = 0;
+    if (v && real) {
+      uint32_t w[UH][ND];
+      uint32_t s0;
+      load_window<UW, UH>(w, s0, ref, ox + x, oy + y, sub);
+      part = unit_part<UW, UH>(w, s0, kk, sk2, kbuf, sad_metric, sub);
+    }
+    const uint32_t d = group_sum(part, L);
+    return v ? d + mv_cost(ml, mv_bits(x, y, 2, j.mvp_x, j.mvp_y)) : 0xFFFFFFFFu;
+  };
+
+  Tz s;   // the wave-uniform IntTZSearchStruct and ranges (diamond_point / two_point read them)
+  s.best_sad = 0xFFFFFFFFu;
+  s.bx = s.by = s.bdist = s.bround = s.pnr = 0;
+  s.R = Range{j.lt_x, j.rb_x, j.lt_y, j.rb_y};
+  s.RR = s.R;
+  s.range = e.search_range ? e.search_range : 64;
+  s.k = 0; s.dist = 1; s.ox = s.oy = 0; s.opnr = 0;
+  auto take = [&](uint32_t cost, int x, int y, int pd, int pnr) FME_AI {   // xTZSearchHelp's update
+    if (cost < s.best_sad) {
+      s.best_sad = cost;
+      s.bx = x; s.by = y; s.bdist = pd; s.pnr = pnr; s.bround = 0;
+    }
+  };
+  // (cost << 32 | call index) minimum of a list of n points, G at a time; pt(i, x, y) -> tested?
+  auto list_min = [&](int n, auto&& pt) FME_AI -> uint64_t {
+    uint64_t best = ~0ull;
+    for (int base = 0; base < n; base += G) {
+      const int i = base + g;
+      int x = 0, y = 0;
+      const bool v = i < n && pt(i, x, y);
+      const uint32_t c = cost_at(x, y, v);
+      const uint64_t key = wave_min_from(((uint64_t)c << 32) | (uint32_t)i, L, 64);
+      best = key < best ? key : best;
+    }
+    return best;
+  };
+  auto ring_pt = [&](int slot, int& x, int& y, int& pnr, int& pd) FME_AI -> bool {
+    s.dist = 1 << (slot >> 4);
+    bool ok;
+    return diamond_point(s, slot & 15, ok, x, y, pnr, pd) && ok;
+  };
+  int nr = 0;
+  while ((1 << nr) <= s.range) nr++;   // dist 1, 2, 4, ... <= m_iSearchRange
+  auto two_point_search = [&]() FME_AI {   // xTZ2PointSearch around the best, opnr = its point nr
+    s.ox = s.bx; s.oy = s.by; s.opnr = s.pnr;
+    const uint64_t k = list_min(2, [&](int i, int& x, int& y) FME_AI {
+      bool ok;
+      return two_point(s, i, ok, x, y) && ok;
+    });
+    if ((uint32_t)(k >> 32) < s.best_sad) {
+      int x, y;
+      bool ok;
+      two_point(s, (int)(uint32_t)k, ok, x, y);
+      take((uint32_t)(k >> 32), x, y, 2, 0);
+    }
+  };
+
+  if (j.flags & FME_JOB_BIPRED) {
+    // xPatternSearch: every point of the range in raster order
+    const int nx = s.R.r - s.R.l + 1, ny = s.R.b - s.R.t + 1;
+    if (nx > 0 && ny > 0) {
+      const uint64_t k = list_min(nx * ny, [&](int i, int& x, int& y) FME_AI {
+        x = s.R.l + i % nx; y = s.R.t + i / nx;
+        return true;
+      });
+      const int i = (int)(uint32_t)k;
+      take((uint32_t)(k >> 32), s.R.l + i % nx, s.R.t + i / nx, 0, 0);
+    }
+  } else {
+    // ---- start points: the AMVP predictor, the zero vector, the 2Nx2N MV --------------------------
+    int mx = j.mvp_x, my = j.mvp_y;
+    clip_qpel(mx, my, ref.width, ref.height, e.cu_x, e.cu_y);
+    const int sx = round4(mx), sy = round4(my);
+    const bool has_pred = (e.flags & FME_TZ_PRED2NX2N) != 0;
+    int qx = pred_x * 4, qy = pred_y * 4;
+    clip_qpel(qx, qy, ref.width, ref.height, e.cu_x, e.cu_y);
+    const int px = round4(qx), py = round4(qy);
+    {
+      uint32_t c3[3] = {0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu};
+      for (int base = 0; base < 3; base += G) {
+        const int i = base + g;
+        const int x = i == 0 ? sx : (i == 1 ? 0 : px), y = i == 0 ? sy : (i == 1 ? 0 : py);
+        const uint32_t c = cost_at(x, y, i < 3);
+#pragma unroll
+        for (int q = 0; q < 3; q++)
+          if (q >= base && q < base + G) c3[q] = __shfl(c, (q - base) * L, 64);
+      }
+      take(c3[0], sx, sy, 0, 0);
+      if (sx != 0 || sy != 0) take(c3[1], 0, 0, 0, 0);
+      if (has_pred && (sx != px || sy != py) && (px != s.bx || py != s.by)) take(c3[2], px, py, 0, 0);
+    }
+    if (has_pred) {   // xSetSearchRange(currBest << 2, m_iSearchRange): the raster's range
+      int cx = s.bx * 4, cy = s.by * 4;
+      clip_qpel(cx, cy, ref.width, ref.height, e.cu_x, e.cu_y);
+      int lx = cx - (s.range << 2), ly = cy - (s.range << 2), rx = cx + (s.range << 2), ry = cy + (s.range << 2);
+      clip_qpel(lx, ly, ref.width, ref.height, e.cu_x, e.cu_y);
+      clip_qpel(rx, ry, ref.width, ref.height, e.cu_x, e.cu_y);
+      s.RR = Range{round4(lx), round4(rx), round4(ly), round4(ry)};
+    }
+
+    // ---- first search: rings around the start, stop 3 rings after the last new best --------------
+    {
+      s.ox = s.bx; s.oy = s.by;
+      const int nslot = 16 * nr, seg = 16 * L < 64 ? 16 * L : 64;
+      uint64_t rmin = ~0ull;   // running minimum of the ring being completed (G < 16)
+      bool stop = false;
+      for (int base = 0; base < nslot && !stop; base += G) {
+        const int i = base + g;
+        int x = 0, y = 0, pnr = 0, pd = 0;
+        const bool v = i < nslot && ring_pt(i, x, y, pnr, pd);
+        const uint32_t c = cost_at(x, y, v);
+        const uint64_t key = wave_min_from(((uint64_t)c << 32) | (uint32_t)i, L, seg);
+        // rings completed by this chunk, in order
+        const int r0 = base >> 4, r1 = (base + G) >> 4;   // rings [r0, r1) end inside this chunk
+        if (G < 16) {
+          rmin = key < rmin ? key : rmin;
+          if (((base + G) & 15) != 0) continue;
+        }
+        for (int r = r0; r < r1 && r < nr; r++) {
+          uint64_t k = G < 16 ? rmin : (uint64_t)__shfl((unsigned long long)key, ((r * 16 - base) * L) & 63, 64);
+          rmin = ~0ull;
+          s.bround += 1;
+          if ((uint32_t)(k >> 32) < s.best_sad) {
+            int xx, yy, pn, pdd;
+            ring_pt((int)(uint32_t)k, xx, yy, pn, pdd);
+            take((uint32_t)(k >> 32), xx, yy, pdd, pn);
+          }
+          if (s.bround >= 3 || 2 * (1 << r) > s.range) {
+            stop = true;
+            break;
+          }
+        }
+      }
+    }
+    if (s.bdist == 1) {
+      s.bdist = 0;
+      two_point_search();
+    }
+    // ---- raster (step 5) over the re-centred range when the best is far -------------------------
+    if (s.bdist > 5) {
+      s.bdist = 5;
+      if (s.RR.l <= s.RR.r && s.RR.t <= s.RR.b) {
+        const int nx = (s.RR.r - s.RR.l) / 5 + 1, ny = (s.RR.b - s.RR.t) / 5 + 1;
+        const uint64_t k = list_min(nx * ny, [&](int i, int& x, int& y) FME_AI {
+          x = s.RR.l + 5 * (i % nx); y = s.RR.t + 5 * (i / nx);
+          return true;
+        });
+        const int i = (int)(uint32_t)k;
+        take((uint32_t)(k >> 32), s.RR.l + 5 * (i % nx), s.RR.t + 5 * (i / nx), 5, 0);
+      }
+    }
+    // ---- star refinement: every ring around the best, until the best stays ----------------------
+    for (int guard = 0; guard < 4096 && s.bdist > 0; guard++) {
+      s.ox = s.bx; s.oy = s.by; s.bdist = 0; s.pnr = 0;
+      const uint64_t k = list_min(16 * nr, [&](int i, int& x, int& y) FME_AI {
+        int pnr, pd;
+        return ring_pt(i, x, y, pnr, pd);
+      });
+      if ((uint32_t)(k >> 32) < s.best_sad) {
+        int xx, yy, pn, pdd;
+        ring_pt((int)(uint32_t)k, xx, yy, pn, pdd);
+        take((uint32_t)(k >> 32), xx, yy, pdd, pn);
+      }
+      if (s.bdist == 1) {
+        s.bdist = 0;
+        if (s.pnr != 0) two_point_search();
+      }
+    }
+  }
+  // ---- the EMI square step (producer: m_integerMv2Nx2N is the post-square MV) ----------------------
+  const bool square = ta.emi_mv != nullptr && (j.flags & FME_JOB_EMI) && !(j.flags & FME_JOB_BIPRED);
+  const int tx = s.bx, ty = s.by;
+  const uint32_t tsad = s.best_sad;
+  if (square) {
+    s.ox = s.bx; s.oy = s.by;
+    const uint64_t k = list_min(8, [&](int i, int& x, int& y) FME_AI {
+      bool ok;
+      return square_point(s, i, ok, x, y) && ok;
+    });
+    if ((uint32_t)(k >> 32) < s.best_sad) {
+      int x, y;
+      bool ok;
+      square_point(s, (int)(uint32_t)k, ok, x, y);
+      take((uint32_t)(k >> 32), x, y, 1, (int)(uint32_t)k + 1);
+    }
+  }
+  if (lane == 0) {
+    fme_job* out = ta.jobs_out + jid;
+    out->mv_x = (int16_t)tx;
+    out->mv_y = (int16_t)ty;
+    if (ta.sad) ta.sad[jid] = tsad - mv_cost(ml, mv_bits(tx, ty, 2, j.mvp_x, j.mvp_y));
+    if (ta.emi_mv) {   // the integer MV after the square step (rcMv of xTZSearch, TEncSearch.cpp:5037-5048)
+      ta.emi_mv[2 * jid] = (int16_t)s.bx;
+      ta.emi_mv[2 * jid + 1] = (int16_t)s.by;
+    }
+  }
+}
+
 __device__ __forceinline__ int xcd_block(int r, int n) {
   const int k = r & 7;
   return k * (n >> 3) + min(k, n & 7) + (r >> 3);
@@ -728,6 +995,25 @@ void k_tz_raster(TzArgs ta, TzSchedule sc, int kid, int nq) {
   tz_unit<UW, UH, 1>(ta, 0, 1, 0, (int)(threadIdx.x & 63) & (L - 1), L, PW, PH, jid);
 }
 
+// Wave-uniform bulk search: one wave per PU of the kernel's unit shape, PUs in class order (CTU
+// order inside a class); blocks dealt to the XCDs in contiguous ranges so each L2 sees one band.
+#ifndef FME_TZW_WAVES
+#define FME_TZW_WAVES 4
+#endif
+template <int UW, int UH>
+__global__ __launch_bounds__(kTzNT) __attribute__((amdgpu_waves_per_eu(FME_TZW_WAVES)))
+void k_tz_wave(TzArgs ta, TzSchedule sc, int kid, int nblk) {
+  const int b = xcd_block((int)blockIdx.x, nblk);
+  const int wv = b * (kTzNT / 64) + (int)(threadIdx.x >> 6);
+  if (wv >= sc.prefix[kid][kNumClasses]) return;
+  int c = 0;
+  while (c < kNumClasses - 1 && wv >= sc.prefix[kid][c + 1]) c++;
+  const int q = sc.class_off[c] + wv - sc.prefix[kid][c];
+  const int jid = ta.perm[q];
+  const fme_job j = ta.sjobs[q];
+  tz_wave<UW, UH>(ta, jid, j, kTzW[c], kTzH[c], ta.ext[jid].pred2n_x, ta.ext[jid].pred2n_y);
+}
+
 // One dependency level of a producer's m_integerMv2Nx2N chain (fme_pred_inter_p/b): one wave per
 // job in chain mode.  The host launches the levels back to back on one stream, so a level reads the
 // post-EMI MVs of earlier levels from global memory (kernel boundaries order them) and no level
@@ -740,16 +1026,11 @@ __global__ __launch_bounds__(64) void k_tz_level(TzArgs ta, TzChain ch, int firs
   const int px = ps >= 0 ? ta.emi_mv[2 * ps] : ta.ext[q].pred2n_x;
   const int py = ps >= 0 ? ta.emi_mv[2 * ps + 1] : ta.ext[q].pred2n_y;
   const int kid = (PW % 8) ? 0 : ((PH % 8) ? 1 : 2);
-  if (kid == 0) {
-    const int L = tz_group_lanes(PW, PH, 4, 8);
-    tz_unit<4, 8, 2>(ta, 0, 1, 0, lane & (L - 1), L, PW, PH, q, px, py);
-  } else if (kid == 1) {
-    const int L = tz_group_lanes(PW, PH, 8, 4);
-    tz_unit<8, 4, 2>(ta, 0, 1, 0, lane & (L - 1), L, PW, PH, q, px, py);
-  } else {
-    const int L = tz_group_lanes(PW, PH, 8, 8);
-    tz_unit<8, 8, 2>(ta, 0, 1, 0, lane & (L - 1), L, PW, PH, q, px, py);
-  }
+  const fme_job j = ta.a.jobs[q];
+  (void)lane;
+  if (kid == 0) tz_wave<4, 8>(ta, q, j, PW, PH, px, py);
+  else if (kid == 1) tz_wave<8, 4>(ta, q, j, PW, PH, px, py);
+  else tz_wave<8, 8>(ta, q, j, PW, PH, px, py);
 }
 
 }  // namespace
@@ -785,6 +1066,17 @@ hipError_t launch_tz(const TzArgs& ta, const TzSchedule& sc, int kid, hipStream_
   if (kid == 0) hipLaunchKernelGGL((k_tz<4, 8>), dim3(blocks), dim3(kTzNT), 0, s, ta, sc, 0);
   else if (kid == 1) hipLaunchKernelGGL((k_tz<8, 4>), dim3(blocks), dim3(kTzNT), 0, s, ta, sc, 1);
   else hipLaunchKernelGGL((k_tz<8, 8>), dim3(blocks), dim3(kTzNT), 0, s, ta, sc, 2);
+  return hipGetLastError();
+}
+
+// Wave-uniform bulk search of kernel kid: sc.prefix in waves (one per PU).
+hipError_t launch_tz_wave(const TzArgs& ta, const TzSchedule& sc, int kid, hipStream_t s) {
+  const int waves = sc.prefix[kid][kNumClasses];
+  if (waves <= 0) return hipSuccess;
+  const int blocks = (waves + kTzNT / 64 - 1) / (kTzNT / 64);
+  if (kid == 0) hipLaunchKernelGGL((k_tz_wave<4, 8>), dim3(blocks), dim3(kTzNT), 0, s, ta, sc, 0, blocks);
+  else if (kid == 1) hipLaunchKernelGGL((k_tz_wave<8, 4>), dim3(blocks), dim3(kTzNT), 0, s, ta, sc, 1, blocks);
+  else hipLaunchKernelGGL((k_tz_wave<8, 8>), dim3(blocks), dim3(kTzNT), 0, s, ta, sc, 2, blocks);
   return hipGetLastError();
 }
 

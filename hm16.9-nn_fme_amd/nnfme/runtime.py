@@ -15,7 +15,7 @@ from .weights import load_weights
 PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB_PATH = os.environ.get("FME_LIB_PATH") or os.path.join(PKG_ROOT, "libfme_amd.so")
 
-ABI_VERSION = 9
+ABI_VERSION = 10
 TIMING_NAMES = ("classify", "scatter", "search", "nn_tail", "batch", "search_main", "search_aux")
 
 # Every entry point include/fme.h declares (the ABI test checks the .so exports them).
@@ -31,7 +31,7 @@ ABI_SYMBOLS = (
     "fme_pred_inter_p", "fme_pred_inter_reset", "fme_nn_param_count", "fme_load_nn_net",
     "fme_set_nn_engine", "fme_set_nn_margin_output", "fme_refine_mv", "fme_refine_mv_device",
     "fme_refine_status", "fme_nn_copy_state_device", "fme_template_costs", "fme_pred_inter_b", "fme_build_bipred_keys",
-    "fme_set_search_event", "fme_build_bipred_keys_device",
+    "fme_set_search_event", "fme_build_bipred_keys_device", "fme_set_nn_logit_output",
 )
 
 
@@ -96,6 +96,7 @@ def load_library(path=None):
         "fme_load_nn_net": (I, [P, P, P, I]),
         "fme_set_nn_engine": (I, [P, I]),
         "fme_set_nn_margin_output": (I, [P, P, I]),
+        "fme_set_nn_logit_output": (I, [P, P, I]),
         "fme_refine_mv": (I, [P, P, P, I, P]),
         "fme_refine_mv_device": (I, [P, P, P, I, P]),
         "fme_refine_status": (I, [P]),
@@ -305,6 +306,12 @@ class FmeContext:
         a later batch of more than `capacity` jobs is rejected."""
         _check(self.lib, self.lib.fme_set_nn_margin_output(self.h, C.c_void_p(d_ptr) if d_ptr else None,
                                                            int(capacity) if d_ptr else 0))
+
+    def set_nn_logit_output(self, d_ptr, capacity=0):
+        """Device array of capacity x 49 values in the net's precision receiving OUT before the
+        output activation for each later nn_mode 2 batch (0: off)."""
+        _check(self.lib, self.lib.fme_set_nn_logit_output(self.h, C.c_void_p(d_ptr) if d_ptr else None,
+                                                          int(capacity) if d_ptr else 0))
 
     def nn_reset(self):
         _check(self.lib, self.lib.fme_nn_reset_state(self.h))

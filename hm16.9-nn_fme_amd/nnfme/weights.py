@@ -151,6 +151,7 @@ def load_checkpoint(path, mean, stdev):
 F32, F64 = 0, 1
 EMB_NONE, EMB_MASTER, EMB_SWAP = 0, 1, 2
 OUT_LINEAR, OUT_SIGMOID = 0, 1
+SLOT_RESET = 1   # FME_NN_IN_SLOT_RESET
 NET_FILES = {"scr3x40": "nn3x40_scr.nnd", "blowing4x40": "nn4x40_qp22.nnd"}
 
 
@@ -158,12 +159,13 @@ class NnNet:
     """A generic net: the fme_nn_net descriptor fields plus float64 parameters in
     fme_load_nn_net order (include/fme.h)."""
 
-    def __init__(self, precision, widths, embedding, out_act, carry_hidden, params):
+    def __init__(self, precision, widths, embedding, out_act, carry_hidden, params, input_flags=0):
         self.precision = int(precision)
         self.widths = [int(w) for w in widths]
         self.embedding = int(embedding)
         self.out_act = int(out_act)
         self.carry_hidden = int(carry_hidden)
+        self.input_flags = int(input_flags)
         self.params = np.ascontiguousarray(params, dtype=np.float64)
         if self.params.size != param_count(self):
             raise ValueError(f"{self.params.size} parameters, descriptor needs {param_count(self)}")
@@ -176,14 +178,21 @@ class NnNet:
         from .abi import NnNetStruct
         w = (self.widths + [0] * 4)[:4]
         return NnNetStruct(self.precision, self.n_hidden, (C_INT4)(*w), self.embedding, self.out_act,
-                           self.carry_hidden, 0)
+                           self.carry_hidden, self.input_flags)
 
     def with_carry(self, carry_hidden):
-        return NnNet(self.precision, self.widths, self.embedding, self.out_act, carry_hidden, self.params)
+        return NnNet(self.precision, self.widths, self.embedding, self.out_act, carry_hidden, self.params,
+                     self.input_flags)
+
+    def with_input_flags(self, input_flags):
+        """FME_NN_IN_SLOT_RESET (1): array_e slots a call did not push read 0, as after the
+        backups' per-call memset (Backups/4:4421-4422, Backups/15:4961-4962)."""
+        return NnNet(self.precision, self.widths, self.embedding, self.out_act, self.carry_hidden, self.params,
+                     input_flags)
 
     def __repr__(self):
         return (f"NnNet({'f64' if self.precision else 'f32'}, {self.widths}, emb={self.embedding}, "
-                f"out_act={self.out_act}, carry=0b{self.carry_hidden:b})")
+                f"out_act={self.out_act}, carry=0b{self.carry_hidden:b}, in=0x{self.input_flags:x})")
 
 
 def _c_int4():
@@ -242,6 +251,13 @@ def case_net(name):
     that net with carry_hidden cleared, "master" = the shipped QP22 2-layer net, generic layout."""
     if name == "master":
         return master_net(22)
-    base, _, mod = str(name).partition("+")
+    base, *mods = str(name).split("+")
     net = load_net(base)
-    return net.with_carry(0) if mod == "rezero" else net
+    for mod in mods:
+        if mod == "rezero":
+            net = net.with_carry(0)
+        elif mod == "slotreset":
+            net = net.with_input_flags(SLOT_RESET)
+        else:
+            raise ValueError(f"unknown net modifier {mod!r} in {name!r}")
+    return net

@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define FME_ABI_VERSION 9
+#define FME_ABI_VERSION 10
 
 /* ---- error codes ---------------------------------------------------------------- */
 #define FME_OK            0
@@ -179,7 +179,18 @@ int fme_load_nn_weights(fme_ctx* ctx, const float* params, int count);
 /* ---- generic (deeper) NN_pred nets: BASELINE.json configs[4] ------------------------------- *
  * nn_mode 2 runs a net loaded with fme_load_nn_net in NN_pred()'s place, with the same inputs
  * (array_e slots, C, PUHeight, PUWidth carried across calls exactly as in nn_mode 1) and the same
- * class -> MV offset switch.  The shape follows the reference's deeper nets:
+ * class -> MV offset switch.
+ * INPUT PATH - a deliberate deviation from the backups: the inputs are the master's EMI step (the
+ * SSE square at distance 1 around the TZ MV, TEncSearch.cpp:1324-1377 with save = true; C = its
+ * best SSE).  The backups build theirs differently - every xTZSearchHelp distortion is pushed
+ * (Backups/4:659-682), C is the minimum over every point xTZSearch tested (:4343-4348), U1..U4 are
+ * array_e[index_ref..+7], and a second ring at distance 2 (xTZ8PointSquareSearch2, :4873-4878)
+ * can move the integer MV.  That input path is not restated: the backups' nets run here on the
+ * master's input distribution, and parity with the backups holds for the forward pass and the
+ * per-call slot reset only (configs[4] input parity is unpinned).
+ * input_flags FME_NN_IN_SLOT_RESET: the array_e slots a call's own EMI step did not push read 0,
+ * as after the backups' per-call memset (Backups/4:4421-4422, Backups/15:4961-4962); C and the PU
+ * size stay carried (the backups never clear them).  Without it the slots carry as in nn_mode 1.  The shape follows the reference's deeper nets:
  *   Backups/4 "SCR 3 layers" (9 -> 40 -> 40 -> 40 -> 49, double, sigmoid output,
  *     TEncSearch - SCR 3 layers - no normalization.cpp:57-299, forward :4427-4480),
  *   Backups/15 "blowing 4 lyrs qp 22" (17 -> 4 x 40 -> 49, float, H-embedding rows 12->3, 16->4,
@@ -216,8 +227,9 @@ typedef struct fme_nn_net {
   int32_t  embedding;                   /* FME_NN_EMB_*                                          */
   int32_t  out_act;                     /* FME_NN_OUT_*                                          */
   uint32_t carry_hidden;                /* bit l: hidden layer l starts from the previous call's */
-  int32_t  reserved;
+  uint32_t input_flags;                 /* FME_NN_IN_*                                           */
 } fme_nn_net;   /* 40 bytes */
+#define FME_NN_IN_SLOT_RESET 1u         /* array_e slots not pushed by this call read 0           */
 
 /* Number of parameters of `net`, or a negative FME_E_* code for an invalid descriptor. */
 int fme_nn_param_count(const fme_nn_net* net);
@@ -229,6 +241,12 @@ int fme_set_nn_engine(fme_ctx* ctx, int engine);
 int fme_set_nn_margin_output(fme_ctx* ctx, float* d_margin, int capacity);
 /* (capacity: elements of d_margin; a later nn_mode 2 batch larger than that is rejected with
  * FME_E_INVALID instead of writing past the caller's array; d_margin null / capacity 0: off) */
+/* Optional diagnostic output of nn_mode 2: OUT before the output activation, 49 values per job in
+ * the net's precision (float or double), job-major, so the exact engine can be checked against the
+ * oracle bit for bit and the MFMA engine against the exact one output by output (the sigmoid's exp
+ * is the device's, within 1 ulp of glibc's; the saturation tests pin the class at its ties).
+ * capacity in jobs; a larger batch is rejected as for the margin output.                       */
+int fme_set_nn_logit_output(fme_ctx* ctx, void* d_logits, int capacity);
 
 /* Forget the array_e/C/PUHeight/PUWidth state carried across calls (process start).  Stream-
  * ordered: it takes effect at the start of the next batch, after every batch already issued. */

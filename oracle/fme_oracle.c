@@ -364,6 +364,7 @@ int orc_nn_param_count(const fme_nn_net* d) {
   if (d->embedding < FME_NN_EMB_NONE || d->embedding > FME_NN_EMB_SWAP) return FME_E_INVALID;
   if (d->out_act != FME_NN_OUT_LINEAR && d->out_act != FME_NN_OUT_SIGMOID) return FME_E_INVALID;
   if (d->carry_hidden >> d->n_hidden) return FME_E_INVALID;
+  if (d->input_flags & ~FME_NN_IN_SLOT_RESET) return FME_E_INVALID;
   int n = d->embedding ? 64 : 0, in = d->embedding ? 17 : 9;
   for (int l = 0; l < d->n_hidden; l++) {
     const int w = d->width[l];
@@ -392,7 +393,7 @@ int orc_load_nn_net(orc_ctx* ctx, const fme_nn_net* d, const double* params, int
 #define ORC_RELU(x) ((x) > 0 ? (x) : 0)
 #define ORC_DEEP_FORWARD(NAME, T, EXPF)                                                          \
   static int NAME(const fme_nn_net* d, const T* P, T carry[][FME_NN_MAX_WIDTH], const uint32_t e[8], \
-                  uint32_t c, int pu_h, int pu_w, double* logits) {                               \
+                  uint32_t c, int pu_h, int pu_w, double* logits, double* pre) {                  \
     T in[17], xa[FME_NN_MAX_WIDTH], xb[FME_NN_MAX_WIDTH], out[49];                                \
     const T* p = P;                                                                               \
     int nin = 0;                                                                                  \
@@ -437,6 +438,7 @@ int orc_load_nn_net(orc_ctx* ctx, const fme_nn_net* d, const double* params, int
       T s = 0;                                                                                    \
       for (int k = 0; k < nin; k++) s = s + p[i * nin + k] * x[k];                                \
       s = s + p[49 * nin + i];                                                                    \
+      if (pre) pre[i] = (double)s;                                                                \
       if (d->out_act == FME_NN_OUT_SIGMOID) s = (T)1 / ((T)1 + EXPF(-s));                         \
       out[i] = s;                                                                                 \
     }                                                                                             \
@@ -450,12 +452,16 @@ int orc_load_nn_net(orc_ctx* ctx, const fme_nn_net* d, const double* params, int
 ORC_DEEP_FORWARD(deep_forward_f32, float, expf)
 ORC_DEEP_FORWARD(deep_forward_f64, double, exp)
 
-int orc_nn_net_forward(orc_ctx* ctx, const uint32_t e[8], uint32_t c, int pu_h, int pu_w,
-                       double* logits) {
+int orc_nn_net_forward_pre(orc_ctx* ctx, const uint32_t e[8], uint32_t c, int pu_h, int pu_w,
+                           double* logits, double* pre) {
   if (!ctx->net.loaded) return FME_E_STATE;
   if (ctx->net.d.precision == FME_NN_F64)
-    return deep_forward_f64(&ctx->net.d, ctx->net.pd, ctx->net.carry_d, e, c, pu_h, pu_w, logits);
-  return deep_forward_f32(&ctx->net.d, ctx->net.pf, ctx->net.carry_f, e, c, pu_h, pu_w, logits);
+    return deep_forward_f64(&ctx->net.d, ctx->net.pd, ctx->net.carry_d, e, c, pu_h, pu_w, logits, pre);
+  return deep_forward_f32(&ctx->net.d, ctx->net.pf, ctx->net.carry_f, e, c, pu_h, pu_w, logits, pre);
+}
+int orc_nn_net_forward(orc_ctx* ctx, const uint32_t e[8], uint32_t c, int pu_h, int pu_w,
+                       double* logits) {
+  return orc_nn_net_forward_pre(ctx, e, c, pu_h, pu_w, logits, NULL);
 }
 
 /* ---- context -------------------------------------------------------------------------- */
@@ -561,8 +567,17 @@ int orc_refine(orc_ctx* ctx, const fme_job* jobs, fme_result* res, int n) {
     int offx, offy;
     if (ctx->cfg.nn_mode) {
       const orc_nn_state* st = &ctx->nn_state;
+      /* FME_NN_IN_SLOT_RESET: memset(array_e) on every NN_pred call (Backups/4:4421-4422,
+       * Backups/15:4961-4962), so only this call's own pushes are non-zero. */
+      uint32_t e[8];
+      const int reset = ctx->cfg.nn_mode == 2 && (ctx->net.d.input_flags & FME_NN_IN_SLOT_RESET);
+      for (int s = 0; s < 8; s++) e[s] = !reset ? st->slot[s] : (s < n_emi ? r->emi[s] : 0u);
+      if (reset) {   /* the cleared array is the state the next call starts from */
+        for (int s = 0; s < 8; s++) ctx->nn_state.slot[s] = e[s];
+        ctx->nn_state.written |= 0xFFu;
+      }
       int cls = ctx->cfg.nn_mode == 2
-                    ? orc_nn_net_forward(ctx, st->slot, st->c, (int)st->pu_h, (int)st->pu_w, NULL)
+                    ? orc_nn_net_forward(ctx, e, st->c, (int)st->pu_h, (int)st->pu_w, NULL)
                     : orc_nn_forward(ctx->nn, st->slot, st->c, (int)st->pu_h, (int)st->pu_w, NULL);
       r->nn_class = (uint8_t)cls;
       if (n_emi < 8 || !(j->flags & FME_JOB_EMI)) r->status |= FME_RES_NN_STALE;

@@ -103,6 +103,9 @@ int orc_nn_param_count(const fme_nn_net* d);
 int orc_load_nn_net(orc_ctx* ctx, const fme_nn_net* d, const double* params, int count);
 int orc_nn_net_forward(orc_ctx* ctx, const uint32_t e[8], uint32_t c, int pu_h, int pu_w,
                        double* logits);
+/* The same with OUT before the output activation (pre, 49 values as double) as well. */
+int orc_nn_net_forward_pre(orc_ctx* ctx, const uint32_t e[8], uint32_t c, int pu_h, int pu_w,
+                           double* logits, double* pre);
 
 /* context helpers */
 void orc_init(orc_ctx* ctx, const fme_config* cfg);

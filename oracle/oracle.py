@@ -82,6 +82,8 @@ class Oracle:
         lib.orc_load_nn_net.argtypes = [_P, _P, _P, C.c_int]
         lib.orc_nn_net_forward.restype = C.c_int
         lib.orc_nn_net_forward.argtypes = [_P, _P, C.c_uint32, C.c_int, C.c_int, _P]
+        lib.orc_nn_net_forward_pre.restype = C.c_int
+        lib.orc_nn_net_forward_pre.argtypes = [_P, _P, C.c_uint32, C.c_int, C.c_int, _P, _P]
         self._buf = C.create_string_buffer(lib.orc_ctx_size())
         self.ctx = C.cast(self._buf, C.c_void_p)
         cfg = _ConfigStruct(8, use_hadamard, nn_mode, qp, fast_inter_mode, 0)
@@ -125,6 +127,16 @@ class Oracle:
         if cls < 0:
             raise RuntimeError(f"orc_nn_net_forward failed: {cls}")
         return cls, logits
+
+    def nn_net_forward_pre(self, e, c, h, w):
+        """(class, OUT[49], OUT before the output activation[49]), both as float64."""
+        e = np.ascontiguousarray(e, dtype=np.uint32)
+        logits = np.zeros(49, np.float64)
+        pre = np.zeros(49, np.float64)
+        cls = self.lib.orc_nn_net_forward_pre(self.ctx, _ptr(e), int(c), int(h), int(w), _ptr(logits), _ptr(pre))
+        if cls < 0:
+            raise RuntimeError(f"orc_nn_net_forward_pre failed: {cls}")
+        return cls, logits, pre
 
     def nn_get_state(self):
         out = np.zeros(12, np.uint32)
