@@ -22,6 +22,8 @@
 // int16) as packed pairs.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+
 #include "fme_device.h"
 #include "fme_simd.h"
 
@@ -791,6 +793,13 @@ __device__ __forceinline__ void tz_wave(const TzArgs& ta, int jid, const fme_job
   };
   int nr = 0;
   while ((1 << nr) <= s.range) nr++;   // dist 1, 2, 4, ... <= m_iSearchRange
+  // compact ring order: ring sizes 4, 8, 8, 8, 16, 16, 16 (xTZ8PointDiamondSearch), point i of the
+  // concatenation -> ring slot (call order preserved)
+  auto ring_start = [](int r) FME_AI { return r == 0 ? 0 : (r < 4 ? 4 + 8 * (r - 1) : 28 + 16 * (r - 4)); };
+  auto compact_slot = [](int i) FME_AI {
+    return i < 4 ? i : (i < 28 ? 16 * (1 + (i - 4) / 8) + ((i - 4) & 7) : 16 * (4 + (i - 28) / 16) + ((i - 28) & 15));
+  };
+  const int nring_pts = ring_start(nr);
   auto two_point_search = [&]() FME_AI {   // xTZ2PointSearch around the best, opnr = its point nr
     s.ox = s.bx; s.oy = s.by; s.opnr = s.pnr;
     const uint64_t k = list_min(2, [&](int i, int& x, int& y) FME_AI {
@@ -849,7 +858,23 @@ __device__ __forceinline__ void tz_wave(const TzArgs& ta, int jid, const fme_job
     }
 
     // ---- first search: rings around the start, stop 3 rings after the last new best --------------
-    {
+    if (G <= 16) {   // ring by ring: one candidate list per ring, later rings skipped after the stop
+      s.ox = s.bx; s.oy = s.by;
+      for (int r = 0; r < nr; r++) {
+        const int r0 = ring_start(r);
+        const uint64_t k = list_min(ring_start(r + 1) - r0, [&](int i, int& x, int& y) FME_AI {
+          int pnr, pd;
+          return ring_pt(compact_slot(r0 + i), x, y, pnr, pd);
+        });
+        s.bround += 1;
+        if ((uint32_t)(k >> 32) < s.best_sad) {
+          int xx, yy, pn, pdd;
+          ring_pt(compact_slot(r0 + (int)(uint32_t)k), xx, yy, pn, pdd);
+          take((uint32_t)(k >> 32), xx, yy, pdd, pn);
+        }
+        if (s.bround >= 3 || 2 * (1 << r) > s.range) break;
+      }
+    } else {   // G >= 32: rings in 16-slot segments, several rings per chunk
       s.ox = s.bx; s.oy = s.by;
       const int nslot = 16 * nr, seg = 16 * L < 64 ? 16 * L : 64;
       uint64_t rmin = ~0ull;   // running minimum of the ring being completed (G < 16)
@@ -902,13 +927,13 @@ __device__ __forceinline__ void tz_wave(const TzArgs& ta, int jid, const fme_job
     // ---- star refinement: every ring around the best, until the best stays ----------------------
     for (int guard = 0; guard < 4096 && s.bdist > 0; guard++) {
       s.ox = s.bx; s.oy = s.by; s.bdist = 0; s.pnr = 0;
-      const uint64_t k = list_min(16 * nr, [&](int i, int& x, int& y) FME_AI {
+      const uint64_t k = list_min(nring_pts, [&](int i, int& x, int& y) FME_AI {
         int pnr, pd;
-        return ring_pt(i, x, y, pnr, pd);
+        return ring_pt(compact_slot(i), x, y, pnr, pd);
       });
       if ((uint32_t)(k >> 32) < s.best_sad) {
         int xx, yy, pn, pdd;
-        ring_pt((int)(uint32_t)k, xx, yy, pn, pdd);
+        ring_pt(compact_slot((int)(uint32_t)k), xx, yy, pn, pdd);
         take((uint32_t)(k >> 32), xx, yy, pdd, pn);
       }
       if (s.bdist == 1) {
@@ -1000,15 +1025,28 @@ void k_tz_raster(TzArgs ta, TzSchedule sc, int kid, int nq) {
 #ifndef FME_TZW_WAVES
 #define FME_TZW_WAVES 4
 #endif
+// Work order: block b runs on XCD b % 8 (round-robin dispatch), and XCD x owns the x-th eighth of
+// every class of this kernel (a spatial band per L2), largest PU class first: the long searches
+// (a 64x64 PU's raster is hundreds of dependent candidate chunks) start at once instead of
+// forming the kernel's tail behind the small ones.
+__device__ __forceinline__ int tz_kid_of(int c) { return (kTzW[c] % 8) ? 0 : ((kTzH[c] % 8) ? 1 : 2); }
 template <int UW, int UH>
 __global__ __launch_bounds__(kTzNT) __attribute__((amdgpu_waves_per_eu(FME_TZW_WAVES)))
-void k_tz_wave(TzArgs ta, TzSchedule sc, int kid, int nblk) {
-  const int b = xcd_block((int)blockIdx.x, nblk);
-  const int wv = b * (kTzNT / 64) + (int)(threadIdx.x >> 6);
-  if (wv >= sc.prefix[kid][kNumClasses]) return;
-  int c = 0;
-  while (c < kNumClasses - 1 && wv >= sc.prefix[kid][c + 1]) c++;
-  const int q = sc.class_off[c] + wv - sc.prefix[kid][c];
+void k_tz_wave(TzArgs ta, TzSchedule sc, int kid) {
+  const int x = (int)blockIdx.x & 7;
+  int t = ((int)blockIdx.x >> 3) * (kTzNT / 64) + (int)(threadIdx.x >> 6);
+  int q = -1, c = kNumClasses - 1;
+  for (; c >= 0; c--) {
+    if (tz_kid_of(c) != kid) continue;
+    const int cnt = sc.class_cnt[c];
+    const int lo = (int)(((long long)cnt * x) >> 3), hi = (int)(((long long)cnt * (x + 1)) >> 3);
+    if (t < hi - lo) {
+      q = sc.class_off[c] + lo + t;
+      break;
+    }
+    t -= hi - lo;
+  }
+  if (q < 0) return;
   const int jid = ta.perm[q];
   const fme_job j = ta.sjobs[q];
   tz_wave<UW, UH>(ta, jid, j, kTzW[c], kTzH[c], ta.ext[jid].pred2n_x, ta.ext[jid].pred2n_y);
@@ -1071,12 +1109,19 @@ hipError_t launch_tz(const TzArgs& ta, const TzSchedule& sc, int kid, hipStream_
 
 // Wave-uniform bulk search of kernel kid: sc.prefix in waves (one per PU).
 hipError_t launch_tz_wave(const TzArgs& ta, const TzSchedule& sc, int kid, hipStream_t s) {
-  const int waves = sc.prefix[kid][kNumClasses];
-  if (waves <= 0) return hipSuccess;
-  const int blocks = (waves + kTzNT / 64 - 1) / (kTzNT / 64);
-  if (kid == 0) hipLaunchKernelGGL((k_tz_wave<4, 8>), dim3(blocks), dim3(kTzNT), 0, s, ta, sc, 0, blocks);
-  else if (kid == 1) hipLaunchKernelGGL((k_tz_wave<8, 4>), dim3(blocks), dim3(kTzNT), 0, s, ta, sc, 1, blocks);
-  else hipLaunchKernelGGL((k_tz_wave<8, 8>), dim3(blocks), dim3(kTzNT), 0, s, ta, sc, 2, blocks);
+  int share = 0;   // the largest per-XCD share of this kernel's PUs (waves)
+  for (int x = 0; x < 8; x++) {
+    int n = 0;
+    for (int c = 0; c < kNumClasses; c++)
+      if (tz_kernel_of(c) == kid)
+        n += (int)(((long long)sc.class_cnt[c] * (x + 1)) >> 3) - (int)(((long long)sc.class_cnt[c] * x) >> 3);
+    share = std::max(share, n);
+  }
+  if (share <= 0) return hipSuccess;
+  const int blocks = 8 * ((share + kTzNT / 64 - 1) / (kTzNT / 64));
+  if (kid == 0) hipLaunchKernelGGL((k_tz_wave<4, 8>), dim3(blocks), dim3(kTzNT), 0, s, ta, sc, 0);
+  else if (kid == 1) hipLaunchKernelGGL((k_tz_wave<8, 4>), dim3(blocks), dim3(kTzNT), 0, s, ta, sc, 1);
+  else hipLaunchKernelGGL((k_tz_wave<8, 8>), dim3(blocks), dim3(kTzNT), 0, s, ta, sc, 2);
   return hipGetLastError();
 }
 

@@ -19,3 +19,10 @@ for r in rows:
 for k, v in ks.items():
     print(k, len(v), [round(x) for x in v[:12]])
 PY
+$T 200 rocprofv3 --kernel-trace --stats --output-format csv -d $O/pi -o run -- python tools/pred_inter_probe.py 3 > $O/pi.log 2>&1 || { tail -20 $O/pi.log; exit 1; }
+grep pred_inter $O/pi.log
+python3 - <<'PY'
+import csv
+for r in csv.DictReader(open("gpurun_out/tzprof/pi/run_kernel_stats.csv")):
+    print(r["Name"][:70], r["Calls"], round(float(r["TotalDurationNs"]) / 1e6, 2), "ms total", round(float(r["AverageNs"]) / 1e3, 1), "us avg")
+PY

@@ -22,7 +22,7 @@ for k, d in acc.items():
     per = defaultdict(list)
     for (disp, name), vals in d.items():
         per[name].append(sum(vals))   # sum over instances (XCDs/SEs) within a dispatch
-    short = k.split("(")[0]
+    short = k.replace("(anonymous namespace)::", "").split("(")[0]
     print(short)
     for name in sorted(per):
         v = per[name]
