@@ -85,6 +85,7 @@ struct SingleStage {
   double ml;
   uint32_t nn_in[12];
   int32_t nn_out[4];
+  uint32_t flag;                // completion word of the single-PU kernels (call sequence number)
   int16_t key[64 * 64];
   uint8_t win[72 * 72];
 };
@@ -165,6 +166,8 @@ struct fme_ctx {
   struct SingleStage* stage = nullptr;
   uint8_t* stage_dev = nullptr;
   hipStream_t single_stream = nullptr;
+  uint32_t single_seq = 0;
+  DevBuf<uint8_t> single_scratch;   // device staging of the inline single-PU kernel
   DevBuf<uint8_t> single_pic;
   DevBuf<fme_job> single_job;
   DevBuf<fme_result> single_res;
@@ -202,9 +205,10 @@ size_t nn_deep_packed_bytes(const fme_nn_net& n);
 void nn_deep_pack(const fme_nn_net& n, const double* params, void* out);
 hipError_t launch_nn_deep_tail(const fme_nn_net& n, const void* packed, float* margin, void* logits, const BatchArgs& a,
                                const WorkBufs& w, int state_in, int engine, hipStream_t s);
-hipError_t launch_nn_deep_single(const fme_nn_net& n, const void* packed, const uint32_t* in11, int32_t* out,
-                                 hipStream_t s);
-hipError_t launch_nn_single(const float* nnp, const uint32_t* in, int32_t* out, hipStream_t s);
+hipError_t launch_nn_deep_single(const fme_nn_net& n, const void* packed, const NnIn11& in11, int32_t* out,
+                                 uint32_t* flag, uint32_t seq, hipStream_t s);
+hipError_t launch_nn_single(const float* nnp, const NnIn11& in, int32_t* out, uint32_t* flag, uint32_t seq,
+                            hipStream_t s);
 }
 
 extern "C" {
@@ -273,7 +277,7 @@ int fme_destroy(fme_ctx* c) {
   c->counts.release(); c->blk_agg.release(); c->blk_prefix.release(); c->nn_state.release();
   c->d_sched.release();
   if (c->ev_done) (void)hipEventDestroy(c->ev_done);
-  c->single_pic.release(); c->single_job.release(); c->single_res.release();
+  c->single_pic.release(); c->single_scratch.release(); c->single_job.release(); c->single_res.release();
   if (c->stage) (void)hipHostFree(c->stage);
   if (c->single_stream) (void)hipStreamDestroy(c->single_stream);
   c->single_nn_in.release(); c->single_nn_out.release();
@@ -867,8 +871,14 @@ static int tz_by_level(fme_ctx* c, std::vector<fme_job>& jobs, std::vector<fme_t
   for (int u = 0; u < nu; u++) off[lvl[u] + 1]++;
   for (int l = 0; l <= max_level; l++) off[l + 1] += off[l];
   {
+    // within a level, the largest PUs first: blocks dispatch in index order, so the longest
+    // searches of a wide level start at once instead of forming its tail
+    std::vector<int> byarea((size_t)nu), start(64 * 64 + 2, 0);   // counting sort, area descending
+    for (int u = 0; u < nu; u++) start[64 * 64 - (int)jobs[u].w * jobs[u].h + 1]++;
+    for (size_t a = 1; a < start.size(); a++) start[a] += start[a - 1];
+    for (int u = 0; u < nu; u++) byarea[start[64 * 64 - (int)jobs[u].w * jobs[u].h]++] = u;
     std::vector<int32_t> fill(off.begin(), off.end() - 1);
-    for (int u = 0; u < nu; u++) {
+    for (int u : byarea) {
       pos[u] = fill[lvl[u]]++;
       order[pos[u]] = u;
     }
@@ -991,6 +1001,25 @@ static int class_of(int w, int h) {
   return -1;
 }
 
+// Wait for a single-PU kernel's completion word (written after its results, system-scope release)
+// instead of synchronising the stream; the stream is queried now and then so a kernel that ended
+// without writing it (a device error) is reported, not waited on forever.
+static int single_wait(fme_ctx* c, uint32_t seq) {
+  volatile uint32_t* f = &c->stage->flag;
+  for (long it = 1; *f != seq; it++) {
+    __builtin_ia32_pause();
+    if ((it & 1023) == 0) {
+      const hipError_t q = hipStreamQuery(c->single_stream);
+      if (q != hipErrorNotReady && *f != seq) {
+        if (q != hipSuccess) return fail(FME_E_DEVICE, "single-PU kernel: %s", hipGetErrorString(q));
+        return fail(FME_E_DEVICE, "single-PU kernel ended without its completion word");
+      }
+    }
+  }
+  __atomic_thread_fence(__ATOMIC_ACQUIRE);
+  return FME_OK;
+}
+
 // xPatternSearchFracDIF for one PU, as TEncSearch calls it: the key block (pcPatternKey, HM Pel)
 // and the reference window around the integer MV (rows -4..h+3, columns -4..w+3 of the padded
 // picture) are staged in pinned, device-mapped host memory; one launch of k_search_single (the
@@ -1011,6 +1040,44 @@ int fme_frac_dif_single(fme_ctx* c, int lossless, const int16_t* key, int key_st
   if (rc) return rc;
   SingleStage* st = c->stage;
   const int pw = w + 8, ph = h + 8;
+  const uint32_t seq = ++c->single_seq;
+  if (w <= 16 && h <= 16) {   // everything in the kernel argument: no host-memory reads on the device
+    HIP_TRY(c->single_scratch.reserve(64 + kInlineBytes + 64));
+    SingleInline p{};
+    p.job.x = 4;
+    p.job.y = 4;
+    p.job.w = (uint8_t)w;
+    p.job.h = (uint8_t)h;
+    p.job.mvp_x = (int16_t)px;
+    p.job.mvp_y = (int16_t)py;
+    p.job.flags = lossless ? FME_JOB_LOSSLESS : 0;
+    p.job.key_offset = 0;
+    p.ml = motion_lambda;
+    p.res = reinterpret_cast<fme_result*>(c->stage_dev + offsetof(SingleStage, res));
+    p.flag = reinterpret_cast<uint32_t*>(c->stage_dev + offsetof(SingleStage, flag));
+    p.scratch = c->single_scratch.p;
+    p.win_stride = pw;
+    p.win_h = ph;
+    p.key_bytes = w * h * 2;
+    p.seq = (int32_t)seq;
+    int16_t* kd = reinterpret_cast<int16_t*>(p.data);
+    for (int y = 0; y < h; y++) std::memcpy(kd + y * w, key + (ptrdiff_t)y * key_stride, (size_t)w * sizeof(int16_t));
+    uint8_t* wd = reinterpret_cast<uint8_t*>(p.data) + p.key_bytes;
+    for (int y = 0; y < ph; y++) {
+      const int16_t* src = ref + (ptrdiff_t)(mv_int_y - 4 + y) * ref_stride + (mv_int_x - 4);
+      for (int x = 0; x < pw; x++) wd[y * pw + x] = (uint8_t)std::min(255, std::max(0, (int)src[x]));
+    }
+    HIP_TRY(launch_search_single_inline(p, cls, c->cfg.use_hadamard ? 1 : 0, c->cfg.fast_inter_mode, c->single_stream));
+    rc = single_wait(c, seq);
+    if (rc) return rc;
+    const fme_result& r = st->res;
+    half_xy[0] = r.half_x;
+    half_xy[1] = r.half_y;
+    qtr_xy[0] = r.qtr_x;
+    qtr_xy[1] = r.qtr_y;
+    *cost = r.frac_cost;
+    return FME_OK;
+  }
   for (int y = 0; y < ph; y++) {
     const int16_t* src = ref + (ptrdiff_t)(mv_int_y - 4 + y) * ref_stride + (mv_int_x - 4);
     uint8_t* dst = st->win + (size_t)y * pw;
@@ -1047,8 +1114,10 @@ int fme_frac_dif_single(fme_ctx* c, int lossless, const int16_t* key, int key_st
   WorkBufs wb{};
   wb.sjobs = const_cast<fme_job*>(a.jobs);
   wb.perm = reinterpret_cast<int32_t*>(c->stage_dev + offsetof(SingleStage, perm));
-  HIP_TRY(launch_search_single(a, wb, cls, c->single_stream));
-  HIP_TRY(hipStreamSynchronize(c->single_stream));
+  HIP_TRY(launch_search_single(a, wb, cls, c->single_stream,
+                               reinterpret_cast<uint32_t*>(c->stage_dev + offsetof(SingleStage, flag)), seq));
+  rc = single_wait(c, seq);
+  if (rc) return rc;
   const fme_result& r = st->res;
   half_xy[0] = r.half_x;
   half_xy[1] = r.half_y;
@@ -1065,17 +1134,20 @@ int fme_nn_pred_single(fme_ctx* c, const uint32_t* e, uint32_t cc, int pu_h, int
   HIP_TRY(hipSetDevice(c->device));
   int rc = ensure_stage(c);
   if (rc) return rc;
-  // inputs and the class through the mapped staging block: one launch, one synchronisation
-  uint32_t* in = c->stage->nn_in;
-  for (int s = 0; s < 8; s++) in[s] = e[s];
-  in[8] = cc;
-  in[9] = (uint32_t)pu_h;
-  in[10] = (uint32_t)pu_w;
-  const uint32_t* d_in = reinterpret_cast<const uint32_t*>(c->stage_dev + offsetof(SingleStage, nn_in));
+  // inputs in the kernel argument, the class and the completion word through mapped host memory:
+  // one launch, a spin on the completion word
+  NnIn11 in{};
+  for (int s = 0; s < 8; s++) in.v[s] = e[s];
+  in.v[8] = cc;
+  in.v[9] = (uint32_t)pu_h;
+  in.v[10] = (uint32_t)pu_w;
   int32_t* d_out = reinterpret_cast<int32_t*>(c->stage_dev + offsetof(SingleStage, nn_out));
-  HIP_TRY(deep ? launch_nn_deep_single(c->net, c->d_net.p, d_in, d_out, c->single_stream)
-               : launch_nn_single(c->d_nn.p, d_in, d_out, c->single_stream));
-  HIP_TRY(hipStreamSynchronize(c->single_stream));
+  uint32_t* d_flag = reinterpret_cast<uint32_t*>(c->stage_dev + offsetof(SingleStage, flag));
+  const uint32_t seq = ++c->single_seq;
+  HIP_TRY(deep ? launch_nn_deep_single(c->net, c->d_net.p, in, d_out, d_flag, seq, c->single_stream)
+               : launch_nn_single(c->d_nn.p, in, d_out, d_flag, seq, c->single_stream));
+  rc = single_wait(c, seq);
+  if (rc) return rc;
   const int32_t cls = c->stage->nn_out[0];
   *nn_class = cls;
   if (out4) {

@@ -182,7 +182,25 @@ hipError_t launch_put_tables(PicDesc* d_pics, double* d_ml, const PicDesc* pics,
 hipError_t launch_search_lane(const BatchArgs& a, const WorkBufs& w, hipStream_t s);
 // One PU of class cls whose job / key / picture / record pointers may be device-mapped host memory
 // (the single-PU entry point): one wave.
-hipError_t launch_search_single(const BatchArgs& a, const WorkBufs& w, int cls, hipStream_t s);
+hipError_t launch_search_single(const BatchArgs& a, const WorkBufs& w, int cls, hipStream_t s, uint32_t* flag,
+                                uint32_t seq);
+// fme_frac_dif_single for small PUs: the job, the window and the key travel in the kernel argument
+// (no dependent reads of host memory); the kernel stages them in a device scratch block, searches,
+// writes the record to mapped host memory, then the completion word (host spins on it).
+struct NnIn11 {   // NN_pred() inputs of a single call: array_e slots[8], C, PUHeight, PUWidth
+  uint32_t v[11];
+};
+constexpr int kInlineBytes = 24 * 24 + 16 * 16 * 2;   // a <= 16x16 PU's window + int16 key
+struct SingleInline {
+  fme_job job;
+  double ml;
+  fme_result* res;             // mapped host record
+  uint32_t* flag;              // mapped host completion word
+  uint8_t* scratch;            // device: [job 32 B][perm 32 B][key][window]
+  int32_t win_stride, win_h, key_bytes, seq;
+  uint32_t data[kInlineBytes / 4];   // key (int16, w*h) then window ((w+8)*(h+8) bytes), dword-packed
+};
+hipError_t launch_search_single_inline(const SingleInline& p, int cls, int use_hadamard, int fen, hipStream_t s);
 int lane_lanes_per_pu(int cls);                    // lanes of a class's PU group (pow2), 0: none
 int cu_count(int device);                          // compute units (workgroup budget of a launch)
 // Packed NN layout for the tail kernel (nn_pack, fme_kernels.hip): offsets in floats, every

@@ -518,16 +518,79 @@ void k_nn_tail(BatchArgs a, WorkBufs w, const float* __restrict__ nnp_g, int sta
 }
 
 // NN_pred() on one explicit input (fme_nn_pred_single): e[8], C, PUHeight, PUWidth.
-__global__ void k_nn_single(const float* __restrict__ nnp, const uint32_t* in, int32_t* out) {
-  if (threadIdx.x != 0) return;
-  uint32_t e[8];
+// fme_nn_pred_single: the 11 input words are the kernel argument; the class goes to mapped host
+// memory followed by the call's completion word (system-scope release; the host spins on it).
+// The same arithmetic as nn_forward with the rows spread over the wave (lane rp owns row pair rp of
+// each layer; every row is still summed in k order without contraction), so a single call's
+// latency is one dependent chain per layer instead of the whole net's.
+__global__ __launch_bounds__(64) void k_nn_single(const float* __restrict__ Q, NnIn11 in11, int32_t* out,
+                                                  uint32_t* flag, uint32_t seq) {
+  __shared__ float s_x1[22], s_x2[20];
+  const int rp = (int)threadIdx.x;
+  const int t = emb_row_h((int)in11.v[9]) * 8 + emb_row_w((int)in11.v[10]);
+  float in[9];
+  const uint32_t raw[9] = {in11.v[0], in11.v[1], in11.v[2], in11.v[3], in11.v[8],
+                           in11.v[4], in11.v[5], in11.v[6], in11.v[7]};
 #pragma unroll
-  for (int s = 0; s < 8; s++) e[s] = in[s];
-  out[0] = nn_forward(nnp, e, in[8], (int)in[9], (int)in[10]);
+  for (int k = 0; k < 9; k++) {
+    float v = (float)raw[k];
+    v = (v - Q[kNnPkMean + k]) / Q[kNnPkStd + k];
+    in[k] = v * Q[kNnPkGin + k];
+  }
+  if (rp < 11) {
+    const float* pfx = Q + kNnPkPfx + t * 22;
+    f2 x = {pfx[2 * rp], pfx[2 * rp + 1]};
+#pragma unroll
+    for (int k = 0; k < 9; k++) x = x + ld2(Q, kNnPkW1 + (rp * 9 + k) * 2) * (f2){in[k], in[k]};
+    x = relu2(x + ld2(Q, kNnPkB1 + 2 * rp));
+    x = x * ld2(Q, kNnPkG1 + 2 * rp) + ld2(Q, kNnPkBE1 + 2 * rp);
+    s_x1[2 * rp] = x.x;
+    s_x1[2 * rp + 1] = x.y;
+  }
+  __syncthreads();
+  if (rp < 10) {
+    f2 x = {0.0f, 0.0f};
+#pragma unroll
+    for (int k = 0; k < 22; k++) x = x + ld2(Q, kNnPkW2 + (rp * 22 + k) * 2) * (f2){s_x1[k], s_x1[k]};
+    x = relu2(x + ld2(Q, kNnPkB2 + 2 * rp));
+    x = x * ld2(Q, kNnPkG2 + 2 * rp) + ld2(Q, kNnPkBE2 + 2 * rp);
+    s_x2[2 * rp] = x.x;
+    s_x2[2 * rp + 1] = x.y;
+  }
+  __syncthreads();
+  // output row pair rp, then the first maximum over the 49 rows (strict >, rows in order)
+  float bv = -INFINITY;
+  int bi = 64;
+  if (rp < 25) {
+    f2 x = {0.0f, 0.0f};
+#pragma unroll
+    for (int k = 0; k < 20; k++) x = x + ld2(Q, kNnPkW3 + (rp * 20 + k) * 2) * (f2){s_x2[k], s_x2[k]};
+    x = x + ld2(Q, kNnPkBout + 2 * rp);
+    bv = x.x;
+    bi = 2 * rp;
+    if (rp < 24 && x.y > bv) {
+      bv = x.y;
+      bi = 2 * rp + 1;
+    }
+  }
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const float ov = __shfl_xor(bv, off, 64);
+    const int oi = __shfl_xor(bi, off, 64);
+    if (ov > bv || (ov == bv && oi < bi)) {
+      bv = ov;
+      bi = oi;
+    }
+  }
+  if (rp == 0) {
+    out[0] = bi;
+    __hip_atomic_store(flag, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
 }
 
-hipError_t launch_nn_single(const float* nnp, const uint32_t* in, int32_t* out, hipStream_t s) {
-  hipLaunchKernelGGL(k_nn_single, dim3(1), dim3(64), 0, s, nnp, in, out);
+hipError_t launch_nn_single(const float* nnp, const NnIn11& in, int32_t* out, uint32_t* flag, uint32_t seq,
+                            hipStream_t s) {
+  hipLaunchKernelGGL(k_nn_single, dim3(1), dim3(64), 0, s, nnp, in, out, flag, seq);
   return hipGetLastError();
 }
 

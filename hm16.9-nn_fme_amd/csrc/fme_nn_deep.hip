@@ -388,16 +388,64 @@ __global__ __launch_bounds__(kRound) void k_nn_deep_tail(BatchArgs a, WorkBufs w
 
 // NN_pred() of the generic net on one explicit input (fme_nn_pred_single, nn_mode 2):
 // in11 = array_e slots[8], C, PUHeight, PUWidth.
+// The exact engine's arithmetic with the rows of each layer spread over the wave (lane i owns row i;
+// every row still sums k = 0.. in order with separate roundings), activations through LDS, then
+// the first maximum by a (value, row) reduction: one dependent chain per layer per call.
 template <typename T, int NH, bool EMB>
-__global__ __launch_bounds__(64) void k_nn_deep_single(DeepArgs d, const uint32_t* in11, int32_t* out) {
-  if (threadIdx.x != 0) return;
+__global__ __launch_bounds__(64) void k_nn_deep_single(DeepArgs d, NnIn11 in11, int32_t* out, uint32_t* flag,
+                                                       uint32_t seq) {
+  using D = DeepLayout<NH, EMB>;
+  __shared__ T s_x[2][kHW];
   const T* __restrict__ P = static_cast<const T*>(d.P);
+  const int i = (int)threadIdx.x;
   uint32_t e[8];
-  for (int s = 0; s < 8; s++) e[s] = in11[s];
-  T in[17], o[49];
-  nn_inputs<T, EMB>(P, d.emb_mode, e, in11[8], in11[9], in11[10], in);
-  forward_exact<T, NH, EMB>(P, in, o);
-  out[0] = nn_argmax(o, d.out_act, nullptr);
+#pragma unroll
+  for (int q = 0; q < 8; q++) e[q] = in11.v[q];
+  T in[17];
+  nn_inputs<T, EMB>(P, d.emb_mode, e, in11.v[8], in11.v[9], in11.v[10], in);
+  if (i < kHW) {
+    T s = (T)0;
+#pragma unroll
+    for (int k = 0; k < D::K0; k++) s = s + P[D::w(0) + i * D::KP0 + k] * in[k];
+    s = s + P[D::b(0) + i];
+    s_x[0][i] = relu(s) * P[D::g(0) + i] + P[D::be(0) + i];
+  }
+  __syncthreads();
+#pragma unroll
+  for (int l = 1; l < NH; l++) {
+    if (i < kHW) {
+      T s = (T)0;
+#pragma unroll
+      for (int k = 0; k < kHW; k++) s = s + P[D::w(l) + i * kHW + k] * s_x[(l - 1) & 1][k];
+      s = s + P[D::b(l) + i];
+      s_x[l & 1][i] = relu(s) * P[D::g(l) + i] + P[D::be(l) + i];
+    }
+    __syncthreads();
+  }
+  T bv = (T)0;
+  int bi = 64;
+  if (i < 49) {
+    T s = (T)0;
+#pragma unroll
+    for (int k = 0; k < kHW; k++) s = s + P[D::kWout + i * kHW + k] * s_x[(NH - 1) & 1][k];
+    s = s + P[D::kBout + i];
+    if (d.out_act == FME_NN_OUT_SIGMOID) s = (T)1 / ((T)1 + nn_exp(-s));
+    bv = s;
+    bi = i;
+  }
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const T ov = __shfl_xor(bv, off, 64);
+    const int oi = __shfl_xor(bi, off, 64);
+    if (oi < 64 && (bi == 64 || ov > bv || (ov == bv && oi < bi))) {
+      bv = ov;
+      bi = oi;
+    }
+  }
+  if (i == 0) {
+    out[0] = bi;
+    __hip_atomic_store(flag, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
 }
 
 // ---------------------------------------------------------------------------------------
@@ -473,21 +521,22 @@ hipError_t FME_CAT(launch_deep_, FME_DEEP_SUFFIX, )(int nh, bool emb, const Batc
 
 #if !FME_DEEP_MFMA
 template <int NH, bool EMB>
-static hipError_t single_one(const DeepArgs& d, const uint32_t* in11, int32_t* out, hipStream_t s) {
-  hipLaunchKernelGGL((k_nn_deep_single<FME_DEEP_T, NH, EMB>), dim3(1), dim3(64), 0, s, d, in11, out);
+static hipError_t single_one(const DeepArgs& d, const NnIn11& in11, int32_t* out, uint32_t* flag, uint32_t seq,
+                             hipStream_t s) {
+  hipLaunchKernelGGL((k_nn_deep_single<FME_DEEP_T, NH, EMB>), dim3(1), dim3(64), 0, s, d, in11, out, flag, seq);
   return hipGetLastError();
 }
-hipError_t FME_CAT(single_deep_, FME_DEEP_T, )(int nh, bool emb, const DeepArgs& d, const uint32_t* in11,
-                                               int32_t* out, hipStream_t s) {
+hipError_t FME_CAT(single_deep_, FME_DEEP_T, )(int nh, bool emb, const DeepArgs& d, const NnIn11& in11,
+                                               int32_t* out, uint32_t* flag, uint32_t seq, hipStream_t s) {
   switch (nh * 2 + (emb ? 1 : 0)) {
-    case 2: return single_one<1, false>(d, in11, out, s);
-    case 3: return single_one<1, true>(d, in11, out, s);
-    case 4: return single_one<2, false>(d, in11, out, s);
-    case 5: return single_one<2, true>(d, in11, out, s);
-    case 6: return single_one<3, false>(d, in11, out, s);
-    case 7: return single_one<3, true>(d, in11, out, s);
-    case 8: return single_one<4, false>(d, in11, out, s);
-    case 9: return single_one<4, true>(d, in11, out, s);
+    case 2: return single_one<1, false>(d, in11, out, flag, seq, s);
+    case 3: return single_one<1, true>(d, in11, out, flag, seq, s);
+    case 4: return single_one<2, false>(d, in11, out, flag, seq, s);
+    case 5: return single_one<2, true>(d, in11, out, flag, seq, s);
+    case 6: return single_one<3, false>(d, in11, out, flag, seq, s);
+    case 7: return single_one<3, true>(d, in11, out, flag, seq, s);
+    case 8: return single_one<4, false>(d, in11, out, flag, seq, s);
+    case 9: return single_one<4, true>(d, in11, out, flag, seq, s);
     default: return hipErrorInvalidValue;
   }
 }
@@ -499,8 +548,8 @@ hipError_t launch_deep_float_0(int, bool, const BatchArgs&, const WorkBufs&, con
 hipError_t launch_deep_float_1(int, bool, const BatchArgs&, const WorkBufs&, const DeepArgs&, int, hipStream_t);
 hipError_t launch_deep_double_0(int, bool, const BatchArgs&, const WorkBufs&, const DeepArgs&, int, hipStream_t);
 hipError_t launch_deep_double_1(int, bool, const BatchArgs&, const WorkBufs&, const DeepArgs&, int, hipStream_t);
-hipError_t single_deep_float(int, bool, const DeepArgs&, const uint32_t*, int32_t*, hipStream_t);
-hipError_t single_deep_double(int, bool, const DeepArgs&, const uint32_t*, int32_t*, hipStream_t);
+hipError_t single_deep_float(int, bool, const DeepArgs&, const NnIn11&, int32_t*, uint32_t*, uint32_t, hipStream_t);
+hipError_t single_deep_double(int, bool, const DeepArgs&, const NnIn11&, int32_t*, uint32_t*, uint32_t, hipStream_t);
 
 static bool deep_supported(const fme_nn_net& n) {
   if (n.n_hidden < 1 || n.n_hidden > FME_NN_MAX_HIDDEN) return false;
@@ -555,13 +604,13 @@ hipError_t launch_nn_deep_tail(const fme_nn_net& n, const void* packed, float* m
   return (mfma ? launch_deep_float_1 : launch_deep_float_0)(n.n_hidden, emb, a, w, d, state_in, s);
 }
 
-hipError_t launch_nn_deep_single(const fme_nn_net& n, const void* packed, const uint32_t* in11, int32_t* out,
-                                 hipStream_t s) {
+hipError_t launch_nn_deep_single(const fme_nn_net& n, const void* packed, const NnIn11& in11, int32_t* out,
+                                 uint32_t* flag, uint32_t seq, hipStream_t s) {
   if (!deep_supported(n)) return hipErrorInvalidValue;
   const DeepArgs d{packed, nullptr, nullptr, n.embedding, n.out_act, n.input_flags};
   const bool emb = n.embedding != FME_NN_EMB_NONE;
-  return n.precision == FME_NN_F64 ? single_deep_double(n.n_hidden, emb, d, in11, out, s)
-                                   : single_deep_float(n.n_hidden, emb, d, in11, out, s);
+  return n.precision == FME_NN_F64 ? single_deep_double(n.n_hidden, emb, d, in11, out, flag, seq, s)
+                                   : single_deep_float(n.n_hidden, emb, d, in11, out, flag, seq, s);
 }
 #endif
 

@@ -694,23 +694,68 @@ __device__ __forceinline__ void tz_unit(const TzArgs& ta, int cls_off, int cls_c
 // Every branch is wave-uniform: no lane idles while another lane's search runs on.
 //
 // Ring slot 16 r + k = point k of xTZ8PointDiamondSearch(origin, 1 << r) (diamond_point order).
+// Minimum over lanes l ^ off for off = L, 2L, .. < lim (lanes of one group hold the same key): DPP
+// row permutations up to 8, the swizzle for 16, a bpermute only for 32 (a chain of six 64-bit
+// bpermutes cost ~0.3 us per candidate chunk of a lone chain wave).
+template <int CTRL>
+__device__ __forceinline__ uint64_t dpp64(uint64_t v) {
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_mov_dpp((int)(uint32_t)v, CTRL, 0xF, 0xF, true);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_mov_dpp((int)(uint32_t)(v >> 32), CTRL, 0xF, 0xF, true);
+  return ((uint64_t)hi << 32) | lo;
+}
 __device__ __forceinline__ uint64_t wave_min_from(uint64_t key, int L, int lim) {
-  for (int off = L; off < lim; off <<= 1) {
-    const uint64_t o = (uint64_t)__shfl_xor((unsigned long long)key, off, 64);
-    key = o < key ? o : key;
+  auto mn = [](uint64_t a, uint64_t b) { return b < a ? b : a; };
+  if (L <= 1 && 1 < lim) key = mn(key, dpp64<0xB1>(key));    // quad_perm [1,0,3,2]
+  if (L <= 2 && 2 < lim) key = mn(key, dpp64<0x4E>(key));    // quad_perm [2,3,0,1]
+  if (L <= 4 && 4 < lim) key = mn(key, dpp64<0x141>(key));   // row_half_mirror
+  if (L <= 8 && 8 < lim) key = mn(key, dpp64<0x140>(key));   // row_mirror
+  if (L <= 16 && 16 < lim) {
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_ds_swizzle((int)(uint32_t)key, 0x401F);   // lane ^ 16
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_ds_swizzle((int)(uint32_t)(key >> 32), 0x401F);
+    key = mn(key, ((uint64_t)hi << 32) | lo);
   }
+  if (L <= 32 && 32 < lim) key = mn(key, (uint64_t)__shfl_xor((unsigned long long)key, 32, 64));
   return key;
 }
 
-template <int UW, int UH>
+// NW waves of one workgroup on one PU (the producer's chain levels: few jobs, latency-bound): the
+// groups of all waves share each list; wave minima meet in LDS.
+template <int NW>
+__device__ __forceinline__ uint64_t block_min(uint64_t key) {
+  if constexpr (NW == 1) {
+    return key;
+  } else {
+    __shared__ uint64_t s_key[NW];
+    if ((threadIdx.x & 63) == 0) s_key[threadIdx.x >> 6] = key;
+    __syncthreads();
+    uint64_t m = s_key[0];
+#pragma unroll
+    for (int w = 1; w < NW; w++) m = s_key[w] < m ? s_key[w] : m;
+    __syncthreads();
+    return m;
+  }
+}
+
+// The producer chain's staged search area: the reference rows / columns every point of the job's
+// search range can touch, copied once into LDS (edge-replicated like the global path), so the
+// chain's dependent candidate chunks read LDS instead of L2 / HBM.  Points outside it (the zero
+// vector, a raster re-centred past the range) fall back to global loads.
+struct TzStage {
+  const uint32_t* lds;   // null: no staging (bulk kernel)
+  int x0, y0;            // picture position of lds[0] (x0 a multiple of 16)
+  int sw4, sh;           // dwords per row, rows
+};
+constexpr int kTzStageDwords = 12288;   // 48 KB: a 64x64 PU's +-64 area is 208 x 192 bytes
+
+template <int UW, int UH, int NW = 1>
 __device__ __forceinline__ void tz_wave(const TzArgs& ta, int jid, const fme_job& j, int PW, int PH, int pred_x,
-                                        int pred_y) {
+                                        int pred_y, TzStage st = TzStage{nullptr, 0, 0, 0, 0}) {
   const BatchArgs& a = ta.a;
-  const int lane = (int)threadIdx.x & 63;
+  const int lane = (int)threadIdx.x & 63, wid = NW == 1 ? 0 : (int)threadIdx.x >> 6;
   const int UX = PW / UW, LR = UX * (PH / UH);
   int L = 1;
   while (L < LR) L <<= 1;
-  const int G = 64 / L, g = lane / L, u = lane - g * L;
+  const int G = NW * (64 / L), g = wid * (64 / L) + lane / L, u = lane % L;
   const bool real = u < LR;
   const int uu = real ? u : 0;
   const int ux = uu % UX, uy = uu / UX;
@@ -753,7 +798,19 @@ __device__ __forceinline__ void tz_wave(const TzArgs& ta, int jid, const fme_job
     if (v && real) {
       uint32_t w[UH][ND];
       uint32_t s0;
-      load_window<UW, UH>(w, s0, ref, ox + x, oy + y, sub);
+      const int bx = ox + x, by = oy + y, xa = bx & ~3;
+      const int c4 = (xa - st.x0) >> 2, r0 = by - st.y0;
+      if (st.lds && xa >= st.x0 && c4 + ND <= st.sw4 && r0 >= 0 && r0 + UH <= st.sh) {
+        s0 = (uint32_t)(bx - xa);
+#pragma unroll
+        for (int r = 0; r < UH; r++) {
+          if (sub && (r & 1)) continue;
+#pragma unroll
+          for (int q = 0; q < ND; q++) w[r][q] = st.lds[(r0 + r) * st.sw4 + c4 + q];
+        }
+      } else {
+        load_window<UW, UH>(w, s0, ref, bx, by, sub);
+      }
       part = unit_part<UW, UH>(w, s0, kk, sk2, kbuf, sad_metric, sub);
     }
     const uint32_t d = group_sum(part, L);
@@ -781,7 +838,7 @@ __device__ __forceinline__ void tz_wave(const TzArgs& ta, int jid, const fme_job
       int x = 0, y = 0;
       const bool v = i < n && pt(i, x, y);
       const uint32_t c = cost_at(x, y, v);
-      const uint64_t key = wave_min_from(((uint64_t)c << 32) | (uint32_t)i, L, 64);
+      const uint64_t key = block_min<NW>(wave_min_from(((uint64_t)c << 32) | (uint32_t)i, L, 64));
       best = key < best ? key : best;
     }
     return best;
@@ -840,9 +897,18 @@ __device__ __forceinline__ void tz_wave(const TzArgs& ta, int jid, const fme_job
         const int i = base + g;
         const int x = i == 0 ? sx : (i == 1 ? 0 : px), y = i == 0 ? sy : (i == 1 ? 0 : py);
         const uint32_t c = cost_at(x, y, i < 3);
+        if constexpr (NW == 1) {
 #pragma unroll
-        for (int q = 0; q < 3; q++)
-          if (q >= base && q < base + G) c3[q] = __shfl(c, (q - base) * L, 64);
+          for (int q = 0; q < 3; q++)
+            if (q >= base && q < base + G) c3[q] = __shfl(c, (q - base) * L, 64);
+        } else {   // G >= 3 with several waves: the three costs through LDS
+          __shared__ uint32_t s_c3[3];
+          if (i < 3 && u == 0) s_c3[i] = c;
+          __syncthreads();
+#pragma unroll
+          for (int q = 0; q < 3; q++) c3[q] = s_c3[q];
+          __syncthreads();
+        }
       }
       take(c3[0], sx, sy, 0, 0);
       if (sx != 0 || sy != 0) take(c3[1], 0, 0, 0, 0);
@@ -858,7 +924,7 @@ __device__ __forceinline__ void tz_wave(const TzArgs& ta, int jid, const fme_job
     }
 
     // ---- first search: rings around the start, stop 3 rings after the last new best --------------
-    if (G <= 16) {   // ring by ring: one candidate list per ring, later rings skipped after the stop
+    if (G <= 16 || NW > 1) {   // ring by ring: one candidate list per ring, later rings skipped after the stop
       s.ox = s.bx; s.oy = s.by;
       for (int r = 0; r < nr; r++) {
         const int r0 = ring_start(r);
@@ -959,7 +1025,7 @@ __device__ __forceinline__ void tz_wave(const TzArgs& ta, int jid, const fme_job
       take((uint32_t)(k >> 32), x, y, 1, (int)(uint32_t)k + 1);
     }
   }
-  if (lane == 0) {
+  if ((NW == 1 ? lane : (int)threadIdx.x) == 0) {   // one writer per PU (NW = 1: per wave)
     fme_job* out = ta.jobs_out + jid;
     out->mv_x = (int16_t)tx;
     out->mv_y = (int16_t)ty;
@@ -1057,7 +1123,10 @@ void k_tz_wave(TzArgs ta, TzSchedule sc, int kid) {
 // post-EMI MVs of earlier levels from global memory (kernel boundaries order them) and no level
 // waits for the host.  ch.psrc[q] >= 0: job q's m_integerMv2Nx2N is job psrc[q]'s result; -1: its
 // ext already holds it.
-__global__ __launch_bounds__(64) void k_tz_level(TzArgs ta, TzChain ch, int first) {
+#ifndef FME_TZL_WAVES
+#define FME_TZL_WAVES 1   // waves per chain job (A/B: 8 waves 276 ms per P frame, spilling; 1 wave 198 ms)
+#endif
+__global__ __launch_bounds__(64 * FME_TZL_WAVES) void k_tz_level(TzArgs ta, TzChain ch, int first) {
   const int q = first + (int)blockIdx.x, lane = (int)threadIdx.x;
   const int PW = ta.a.jobs[q].w, PH = ta.a.jobs[q].h;   // shapes checked by the host
   const int ps = ch.psrc[q];
@@ -1065,10 +1134,46 @@ __global__ __launch_bounds__(64) void k_tz_level(TzArgs ta, TzChain ch, int firs
   const int py = ps >= 0 ? ta.emi_mv[2 * ps + 1] : ta.ext[q].pred2n_y;
   const int kid = (PW % 8) ? 0 : ((PH % 8) ? 1 : 2);
   const fme_job j = ta.a.jobs[q];
-  (void)lane;
-  if (kid == 0) tz_wave<4, 8>(ta, q, j, PW, PH, px, py);
-  else if (kid == 1) tz_wave<8, 4>(ta, q, j, PW, PH, px, py);
-  else tz_wave<8, 8>(ta, q, j, PW, PH, px, py);
+  // stage the search area [R.l, R.r + PW) x [R.t, R.b + PH) around the PU (+ alignment slack)
+  __shared__ uint4 s_win[kTzStageDwords / 4];
+  TzStage st{reinterpret_cast<const uint32_t*>(s_win), 0, 0, 0, 0};
+  {
+    const PicDesc ref = ta.a.pics[j.ref_id];
+    st.x0 = ((int)j.x + j.lt_x) & ~15;
+    st.y0 = (int)j.y + j.lt_y;
+    const int x1 = (int)j.x + j.rb_x + PW + 4;
+    st.sw4 = ((x1 - st.x0 + 15) & ~15) >> 2;
+    st.sh = j.rb_y - j.lt_y + PH;
+    if (st.sh <= 0 || st.sw4 <= 0 || st.sw4 * st.sh > kTzStageDwords) {
+      st.lds = nullptr;   // (a range too large for the stage: global loads)
+    } else {
+      const int n16 = (st.sw4 >> 2) * st.sh;
+      const bool vec = (ref.stride & 15) == 0 && ((uintptr_t)ref.luma & 15) == 0;
+      for (int i = lane; i < n16; i += 64 * FME_TZL_WAVES) {
+        const int r = i / (st.sw4 >> 2), c = st.x0 + 16 * (i - r * (st.sw4 >> 2));
+        const uint8_t* row = ref.luma + (size_t)clamp_i(st.y0 + r, 0, ref.height - 1) * ref.stride;
+        uint4 v;
+        if (vec && c >= 0 && c + 16 <= ref.width) {
+          v = *reinterpret_cast<const uint4*>(row + c);
+        } else {
+          uint32_t d[4];
+#pragma unroll
+          for (int k = 0; k < 4; k++) {
+            uint32_t b = 0;
+#pragma unroll
+            for (int e = 0; e < 4; e++) b |= (uint32_t)gld8(row + clamp_i(c + 4 * k + e, 0, ref.width - 1)) << (8 * e);
+            d[k] = b;
+          }
+          v = make_uint4(d[0], d[1], d[2], d[3]);
+        }
+        s_win[i] = v;
+      }
+    }
+    __syncthreads();
+  }
+  if (kid == 0) tz_wave<4, 8, FME_TZL_WAVES>(ta, q, j, PW, PH, px, py, st);
+  else if (kid == 1) tz_wave<8, 4, FME_TZL_WAVES>(ta, q, j, PW, PH, px, py, st);
+  else tz_wave<8, 8, FME_TZL_WAVES>(ta, q, j, PW, PH, px, py, st);
 }
 
 }  // namespace
@@ -1076,7 +1181,7 @@ __global__ __launch_bounds__(64) void k_tz_level(TzArgs ta, TzChain ch, int firs
 hipError_t launch_tz_levels(const TzArgs& ta, const TzChain& ch, const int32_t* h_lvl_off, hipStream_t s) {
   for (int lv = 0; lv < ch.nlev; lv++) {
     const int n = h_lvl_off[lv + 1] - h_lvl_off[lv];
-    if (n > 0) hipLaunchKernelGGL(k_tz_level, dim3(n), dim3(64), 0, s, ta, ch, h_lvl_off[lv]);
+    if (n > 0) hipLaunchKernelGGL(k_tz_level, dim3(n), dim3(64 * FME_TZL_WAVES), 0, s, ta, ch, h_lvl_off[lv]);
   }
   return hipGetLastError();
 }
