@@ -147,8 +147,6 @@ struct fme_ctx {
   DevBuf<uint32_t> d_tz_rst;   // raster hand-off records [n][8]
   DevBuf<int32_t> d_tz_rq;     // raster queues [3][n] + 3 lengths
   bool tz_wave = true;                     // FME_TZ_WAVE=0: the lane-per-unit kernels (A/B)
-  bool tz_flow = false;                    // FME_TZ_FLOW=1: the producer chain as one dataflow launch (k_tz_flow)
-  DevBuf<int32_t> d_flow;                  // [counter, fail, pad..64), done[n], mv[n] of k_tz_flow
   bool tz_defer = FME_TZ_DEFER_DEFAULT;   // FME_TZ_DEFER=0/1: raster searches in a second pass
   int tz_defer_min = 4096;                 // FME_TZ_DEFER_MIN: batches below this size run in one pass
   hipEvent_t ev_tz[2] = {nullptr, nullptr};
@@ -244,7 +242,6 @@ int fme_create(int device, const fme_config* cfg, fme_ctx** out_ctx) {
   HIP_TRY(hipMemset(c->d_key_invalid.p, 0, sizeof(int32_t)));
   HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&c->h_counts), (kNumClasses + 1) * sizeof(int32_t), hipHostMallocDefault));
   if (const char* e = getenv("FME_TZ_WAVE")) c->tz_wave = (e[0] == '1');
-  if (const char* e = getenv("FME_TZ_FLOW")) c->tz_flow = (e[0] == '1');
   if (const char* e = getenv("FME_TZ_DEFER")) c->tz_defer = (e[0] == '1');
   if (const char* e = getenv("FME_TZ_DEFER_MIN")) c->tz_defer_min = atoi(e);
   if (cfg->max_jobs > 0) {
@@ -270,7 +267,7 @@ int fme_destroy(fme_ctx* c) {
     if (c->chroma_owned[i]) (void)hipFree(c->chroma_owned[i]);
   c->d_mc_jobs.release(); c->d_mc_planes.release(); c->d_mc_invalid.release();
   c->d_tz_ext.release(); c->d_tz_sad.release(); c->d_tz_rst.release(); c->d_tz_rq.release();
-  c->d_amvp.release(); c->d_amvp_sad.release(); c->d_bikey.release(); c->d_key_invalid.release(); c->d_ch_i32.release(); c->d_flow.release(); c->d_tz_emi.release();
+  c->d_amvp.release(); c->d_amvp_sad.release(); c->d_bikey.release(); c->d_key_invalid.release(); c->d_ch_i32.release(); c->d_tz_emi.release();
   for (auto& e : c->ev_tz)
     if (e) (void)hipEventDestroy(e);
   for (auto& e : c->ev_mc)
@@ -915,22 +912,11 @@ static int tz_by_level(fme_ctx* c, std::vector<fme_job>& jobs, std::vector<fme_t
   ta.ext = c->d_tz_ext.p;
   ta.emi_mv = c->d_tz_emi.p;
   const TzChain ch{c->d_ch_i32.p, max_level + 1};
-  if (c->tz_flow) {   // one dataflow launch (FME_TZ_FLOW=1; default: one kernel per level)
-    HIP_TRY(c->d_flow.reserve((size_t)2 * nu + 64));
-    HIP_TRY(hipMemsetAsync(c->d_flow.p, 0, ((size_t)nu + 64) * sizeof(int32_t), s));
-    static int cus = 0;
-    if (!cus) cus = cu_count(c->device);
-    HIP_TRY(launch_tz_flow(ta, ch, nu, cus * 8, c->d_flow.p, c->d_flow.p + 64, c->d_flow.p + 1, s));
-    HIP_TRY(hipMemcpyAsync(c->h_counts, c->d_flow.p + 1, sizeof(int32_t), hipMemcpyDeviceToHost, s));
-  } else {
-    HIP_TRY(launch_tz_levels(ta, ch, off.data(), s));
-  }
+  HIP_TRY(launch_tz_levels(ta, ch, off.data(), s));
   std::vector<int16_t> lemi((size_t)2 * nu);
   HIP_TRY(hipMemcpyAsync(lj.data(), c->d_jobs.p, (size_t)nu * sizeof(fme_job), hipMemcpyDeviceToHost, s));
   HIP_TRY(hipMemcpyAsync(lemi.data(), c->d_tz_emi.p, (size_t)2 * nu * sizeof(int16_t), hipMemcpyDeviceToHost, s));
   HIP_TRY(hipStreamSynchronize(s));
-  if (c->tz_flow && c->h_counts[0])
-    return fail(FME_E_DEVICE, "integer search chain: a dependency wait exceeded its bound");
   for (int q = 0; q < nu; q++) {
     const int u = order[q];
     jobs[u] = lj[q];

@@ -166,10 +166,6 @@ struct TzChain {
   int32_t nlev;
 };
 hipError_t launch_tz_levels(const TzArgs& ta, const TzChain& ch, const int32_t* h_lvl_off, hipStream_t s);
-// The chain as one dataflow launch (k_tz_flow): jobs in level order, counter / done zeroed by the
-// caller, fail[0] set if a dependency wait exceeded its bound.
-hipError_t launch_tz_flow(const TzArgs& ta, const TzChain& ch, int n, int waves, int* counter, int* done, int* fail,
-                          hipStream_t s);
 
 // Host-side launch helpers (fme_kernels.hip).
 hipError_t launch_classify(const BatchArgs& a, const WorkBufs& w, hipStream_t s);

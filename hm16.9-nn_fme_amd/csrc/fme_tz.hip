@@ -1178,67 +1178,7 @@ __global__ __launch_bounds__(64 * FME_TZL_WAVES) void k_tz_level(TzArgs ta, TzCh
   else tz_wave<8, 8, FME_TZL_WAVES>(ta, q, j, PW, PH, px, py, st);
 }
 
-// The whole chain in one launch (dataflow): persistent waves take jobs in level order from an
-// atomic counter and a job whose m_integerMv2Nx2N comes from job psrc[q] waits for that job's
-// completion word.  psrc[q] < q and every index below the counter's value has been taken by a
-// running wave, so the oldest unfinished job never waits: no deadlock whatever the dispatch order,
-// and every wave exits once the counter passes n.  Replaces one launch per level (a 1080p P frame
-// has ~4,400 levels of ~20 us each): independent chains (per reference, per CTU row) overlap, and
-// a level-wide barrier becomes a per-job dependency.  A wait that exceeds its bound sets fail[0]
-// and lets the wave go on (the host reports FME_E_DEVICE) rather than hanging the device.
-__global__ __launch_bounds__(64) void k_tz_flow(TzArgs ta, TzChain ch, int n, int* counter, int* done, int* fail) {
-  // done[q]: completion word of job q; done[n + q]: its post-EMI MV (x | y << 16).  Both are
-  // written and polled with device-scope read-modify-write atomics, coherent across the XCDs'
-  // L2s like the job counter.
-  const int lane = (int)threadIdx.x;
-  for (;;) {
-    int q = 0;
-    if (lane == 0) q = atomicAdd(counter, 1);
-    q = __shfl(q, 0, 64);
-    if (q >= n) break;
-    const int ps = ch.psrc[q];
-    int px = ta.ext[q].pred2n_x, py = ta.ext[q].pred2n_y;
-    if (ps >= 0) {
-      int v = 0;
-      if (lane == 0) {
-        bool ok = false;
-        for (int it = 0; it < (1 << 18); it++) {   // ~0.4 s: far above a chain's whole duration
-          if (atomicAdd(done + ps, 0)) {
-            ok = true;
-            break;
-          }
-          __builtin_amdgcn_s_sleep(2);
-        }
-        if (!ok) atomicExch(fail, 1);
-        v = atomicAdd(done + n + ps, 0);
-      }
-      v = __shfl(v, 0, 64);
-      px = (int)(int16_t)(v & 0xFFFF);
-      py = (int)(int16_t)((uint32_t)v >> 16);
-    }
-    const int PW = ta.a.jobs[q].w, PH = ta.a.jobs[q].h;
-    const int kid = (PW % 8) ? 0 : ((PH % 8) ? 1 : 2);
-    const fme_job j = ta.a.jobs[q];
-    if (kid == 0) tz_wave<4, 8>(ta, q, j, PW, PH, px, py);
-    else if (kid == 1) tz_wave<8, 4>(ta, q, j, PW, PH, px, py);
-    else tz_wave<8, 8>(ta, q, j, PW, PH, px, py);
-    if (lane == 0) {   // (lane 0 wrote emi_mv[q] inside tz_wave)
-      const int v = (int)((uint32_t)(uint16_t)ta.emi_mv[2 * q] | ((uint32_t)(uint16_t)ta.emi_mv[2 * q + 1] << 16));
-      atomicExch(done + n + q, v);
-      __threadfence();
-      atomicExch(done + q, 1);
-    }
-  }
-}
-
 }  // namespace
-
-hipError_t launch_tz_flow(const TzArgs& ta, const TzChain& ch, int n, int waves, int* counter, int* done, int* fail,
-                          hipStream_t s) {
-  if (n <= 0) return hipSuccess;
-  hipLaunchKernelGGL(k_tz_flow, dim3(std::min(n, waves)), dim3(64), 0, s, ta, ch, n, counter, done, fail);
-  return hipGetLastError();
-}
 
 hipError_t launch_tz_levels(const TzArgs& ta, const TzChain& ch, const int32_t* h_lvl_off, hipStream_t s) {
   for (int lv = 0; lv < ch.nlev; lv++) {
