@@ -236,30 +236,41 @@ __device__ __forceinline__ void forward_mfma(const T* __restrict__ P, T* act, in
 template <int KS, int KSTR, int NB>
 __device__ __forceinline__ void hidden_t(const double* __restrict__ W, const double* __restrict__ bias,
                                          const double* __restrict__ g, const double* __restrict__ be,
-                                         double (&b)[NB], int c16, int q) {
+                                         double (&b)[4][NB], int c16, int q) {
+  // all four 16-job tiles at once: 12 independent accumulator chains keep the MFMA pipe full
   using M = Mfma<double>;
-  typename M::acc_t acc[3];
+  typename M::acc_t acc[3][4];
 #pragma unroll
-  for (int mt = 0; mt < 3; mt++) acc[mt] = typename M::acc_t{0, 0, 0, 0};
+  for (int mt = 0; mt < 3; mt++)
+#pragma unroll
+    for (int nt = 0; nt < 4; nt++) acc[mt][nt] = typename M::acc_t{0, 0, 0, 0};
 #pragma unroll
   for (int kk = 0; kk < KS; kk++)
 #pragma unroll
-    for (int mt = 0; mt < 3; mt++) acc[mt] = M::mma(W[(mt * 16 + c16) * KSTR + kk * 4 + q], b[kk], acc[mt]);
+    for (int mt = 0; mt < 3; mt++) {
+      const double a = W[(mt * 16 + c16) * KSTR + kk * 4 + q];
 #pragma unroll
-  for (int mt = 0; mt < 3; mt++) asm volatile("s_nop 15\n\ts_nop 15" : "+a"(acc[mt]));   // (see layer_mfma)
+      for (int nt = 0; nt < 4; nt++) acc[mt][nt] = M::mma(a, b[nt][kk], acc[mt][nt]);
+    }
+#pragma unroll
+  for (int mt = 0; mt < 3; mt++)
+#pragma unroll
+    for (int nt = 0; nt < 4; nt++) asm volatile("s_nop 15\n\ts_nop 15" : "+a"(acc[mt][nt]));   // (see layer_mfma)
 #pragma unroll
   for (int mt = 0; mt < 3; mt++)
 #pragma unroll
     for (int r = 0; r < 4; r++) {
       if (4 * mt + r >= NB) continue;
       const int u = mt * 16 + q + 4 * r;
-      b[4 * mt + r] = relu(acc[mt][r] + bias[u]) * g[u] + be[u];
+      const double bb = bias[u], gg = g[u], ee = be[u];
+#pragma unroll
+      for (int nt = 0; nt < 4; nt++) b[nt][4 * mt + r] = relu(acc[mt][nt][r] + bb) * gg + ee;
     }
 }
 
 template <int NH, bool EMB, int L>
-struct ChainT {   // hidden layers L..NH-1 of one 16-job tile, in registers
-  static __device__ __forceinline__ void run(const double* __restrict__ P, double (&b)[kHW / 4], int c16, int q) {
+struct ChainT {   // hidden layers L..NH-1, in registers
+  static __device__ __forceinline__ void run(const double* __restrict__ P, double (&b)[4][kHW / 4], int c16, int q) {
     using D = DeepLayout<NH, EMB>;
     hidden_t<kHW / 4, kHW, kHW / 4>(P + D::w(L), P + D::b(L), P + D::g(L), P + D::be(L), b, c16, q);
     ChainT<NH, EMB, L + 1>::run(P, b, c16, q);
@@ -267,7 +278,7 @@ struct ChainT {   // hidden layers L..NH-1 of one 16-job tile, in registers
 };
 template <int NH, bool EMB>
 struct ChainT<NH, EMB, NH> {
-  static __device__ __forceinline__ void run(const double* __restrict__, double (&)[kHW / 4], int, int) {}
+  static __device__ __forceinline__ void run(const double* __restrict__, double (&)[4][kHW / 4], int, int) {}
 };
 
 template <int NH, bool EMB>
@@ -275,30 +286,32 @@ __device__ __forceinline__ void forward_mfma_t(const double* __restrict__ P, dou
   using D = DeepLayout<NH, EMB>;
   using M = Mfma<double>;
   const int c16 = lane & 15, q = lane >> 4;
+  double b[4][kHW / 4];
+#pragma unroll
+  for (int nt = 0; nt < 4; nt++)
+#pragma unroll
+    for (int kk = 0; kk < kHW / 4; kk++) b[nt][kk] = kk < D::KP0 / 4 ? act[(nt * 16 + c16) * kAS + kk * 4 + q] : 0.0;
+  hidden_t<D::KP0 / 4, D::KP0, kHW / 4>(P + D::w(0), P + D::b(0), P + D::g(0), P + D::be(0), b, c16, q);
+  ChainT<NH, EMB, 1>::run(P, b, c16, q);
 #pragma unroll 1
-  for (int nt = 0; nt < 4; nt++) {
-    double* row = act + (nt * 16 + c16) * kAS;
-    double b[kHW / 4];
+  for (int mt = 0; mt < kOP / 16; mt++) {   // output tiles one at a time (4 job tiles each)
+    typename M::acc_t acc[4];
 #pragma unroll
-    for (int kk = 0; kk < kHW / 4; kk++) b[kk] = kk < D::KP0 / 4 ? row[kk * 4 + q] : 0.0;
-    hidden_t<D::KP0 / 4, D::KP0, kHW / 4>(P + D::w(0), P + D::b(0), P + D::g(0), P + D::be(0), b, c16, q);
-    ChainT<NH, EMB, 1>::run(P, b, c16, q);
-    typename M::acc_t acc[kOP / 16];
+    for (int nt = 0; nt < 4; nt++) acc[nt] = typename M::acc_t{0, 0, 0, 0};
 #pragma unroll
-    for (int mt = 0; mt < kOP / 16; mt++) acc[mt] = typename M::acc_t{0, 0, 0, 0};
+    for (int kk = 0; kk < kHW / 4; kk++) {
+      const double a = P[D::kWout + (mt * 16 + c16) * kHW + kk * 4 + q];
 #pragma unroll
-    for (int kk = 0; kk < kHW / 4; kk++)
+      for (int nt = 0; nt < 4; nt++) acc[nt] = M::mma(a, b[nt][kk], acc[nt]);
+    }
 #pragma unroll
-      for (int mt = 0; mt < kOP / 16; mt++)
-        acc[mt] = M::mma(P[D::kWout + (mt * 16 + c16) * kHW + kk * 4 + q], b[kk], acc[mt]);
+    for (int nt = 0; nt < 4; nt++) asm volatile("s_nop 15\n\ts_nop 15" : "+a"(acc[nt]));
 #pragma unroll
-    for (int mt = 0; mt < kOP / 16; mt++) asm volatile("s_nop 15\n\ts_nop 15" : "+a"(acc[mt]));
-#pragma unroll
-    for (int mt = 0; mt < kOP / 16; mt++)
+    for (int nt = 0; nt < 4; nt++)
 #pragma unroll
       for (int r = 0; r < 4; r++) {
         const int u = mt * 16 + q + 4 * r;
-        if (u < 49) row[u] = acc[mt][r] + P[D::kBout + u];
+        if (u < 49) act[(nt * 16 + c16) * kAS + u] = acc[nt][r] + P[D::kBout + u];
       }
   }
 }
