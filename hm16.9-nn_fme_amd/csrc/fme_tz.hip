@@ -738,20 +738,9 @@ __device__ __forceinline__ uint64_t block_min(uint64_t key) {
   }
 }
 
-// The producer chain's staged search area: the reference rows / columns every point of the job's
-// search range can touch, copied once into LDS (edge-replicated like the global path), so the
-// chain's dependent candidate chunks read LDS instead of L2 / HBM.  Points outside it (the zero
-// vector, a raster re-centred past the range) fall back to global loads.
-struct TzStage {
-  const uint32_t* lds;   // null: no staging (bulk kernel)
-  int x0, y0;            // picture position of lds[0] (x0 a multiple of 16)
-  int sw4, sh;           // dwords per row, rows
-};
-constexpr int kTzStageDwords = 12288;   // 48 KB: a 64x64 PU's +-64 area is 208 x 192 bytes
-
 template <int UW, int UH, int NW = 1>
 __device__ __forceinline__ void tz_wave(const TzArgs& ta, int jid, const fme_job& j, int PW, int PH, int pred_x,
-                                        int pred_y, TzStage st = TzStage{nullptr, 0, 0, 0, 0}) {
+                                        int pred_y) {
   const BatchArgs& a = ta.a;
   const int lane = (int)threadIdx.x & 63, wid = NW == 1 ? 0 : (int)threadIdx.x >> 6;
   const int UX = PW / UW, LR = UX * (PH / UH);
@@ -800,19 +789,7 @@ __device__ __forceinline__ void tz_wave(const TzArgs& ta, int jid, const fme_job
     if (v && real) {
       uint32_t w[UH][ND];
       uint32_t s0;
-      const int bx = ox + x, by = oy + y, xa = bx & ~3;
-      const int c4 = (xa - st.x0) >> 2, r0 = by - st.y0;
-      if (st.lds && xa >= st.x0 && c4 + ND <= st.sw4 && r0 >= 0 && r0 + UH <= st.sh) {
-        s0 = (uint32_t)(bx - xa);
-#pragma unroll
-        for (int r = 0; r < UH; r++) {
-          if (sub && (r & 1)) continue;
-#pragma unroll
-          for (int q = 0; q < ND; q++) w[r][q] = st.lds[(r0 + r) * st.sw4 + c4 + q];
-        }
-      } else {
-        load_window<UW, UH>(w, s0, ref, bx, by, sub);
-      }
+      load_window<UW, UH>(w, s0, ref, ox + x, oy + y, sub);
       part = unit_part<UW, UH>(w, s0, kk, sk2, kbuf, sad_metric, sub);
     }
     const uint32_t d = group_sum(part, L);
@@ -1136,46 +1113,9 @@ __global__ __launch_bounds__(64 * FME_TZL_WAVES) void k_tz_level(TzArgs ta, TzCh
   const int py = ps >= 0 ? ta.emi_mv[2 * ps + 1] : ta.ext[q].pred2n_y;
   const int kid = (PW % 8) ? 0 : ((PH % 8) ? 1 : 2);
   const fme_job j = ta.a.jobs[q];
-  // stage the search area [R.l, R.r + PW) x [R.t, R.b + PH) around the PU (+ alignment slack)
-  __shared__ uint4 s_win[kTzStageDwords / 4];
-  TzStage st{reinterpret_cast<const uint32_t*>(s_win), 0, 0, 0, 0};
-  {
-    const PicDesc ref = ta.a.pics[j.ref_id];
-    st.x0 = ((int)j.x + j.lt_x) & ~15;
-    st.y0 = (int)j.y + j.lt_y;
-    const int x1 = (int)j.x + j.rb_x + PW + 4;
-    st.sw4 = ((x1 - st.x0 + 15) & ~15) >> 2;
-    st.sh = j.rb_y - j.lt_y + PH;
-    if (st.sh <= 0 || st.sw4 <= 0 || st.sw4 * st.sh > kTzStageDwords) {
-      st.lds = nullptr;   // (a range too large for the stage: global loads)
-    } else {
-      const int n16 = (st.sw4 >> 2) * st.sh;
-      const bool vec = (ref.stride & 15) == 0 && ((uintptr_t)ref.luma & 15) == 0;
-      for (int i = lane; i < n16; i += 64 * FME_TZL_WAVES) {
-        const int r = i / (st.sw4 >> 2), c = st.x0 + 16 * (i - r * (st.sw4 >> 2));
-        const uint8_t* row = ref.luma + (size_t)clamp_i(st.y0 + r, 0, ref.height - 1) * ref.stride;
-        uint4 v;
-        if (vec && c >= 0 && c + 16 <= ref.width) {
-          v = *reinterpret_cast<const uint4*>(row + c);
-        } else {
-          uint32_t d[4];
-#pragma unroll
-          for (int k = 0; k < 4; k++) {
-            uint32_t b = 0;
-#pragma unroll
-            for (int e = 0; e < 4; e++) b |= (uint32_t)gld8(row + clamp_i(c + 4 * k + e, 0, ref.width - 1)) << (8 * e);
-            d[k] = b;
-          }
-          v = make_uint4(d[0], d[1], d[2], d[3]);
-        }
-        s_win[i] = v;
-      }
-    }
-    __syncthreads();
-  }
-  if (kid == 0) tz_wave<4, 8, FME_TZL_WAVES>(ta, q, j, PW, PH, px, py, st);
-  else if (kid == 1) tz_wave<8, 4, FME_TZL_WAVES>(ta, q, j, PW, PH, px, py, st);
-  else tz_wave<8, 8, FME_TZL_WAVES>(ta, q, j, PW, PH, px, py, st);
+  if (kid == 0) tz_wave<4, 8, FME_TZL_WAVES>(ta, q, j, PW, PH, px, py);
+  else if (kid == 1) tz_wave<8, 4, FME_TZL_WAVES>(ta, q, j, PW, PH, px, py);
+  else tz_wave<8, 8, FME_TZL_WAVES>(ta, q, j, PW, PH, px, py);
 }
 
 }  // namespace
