@@ -352,7 +352,7 @@ def tz_leg(dev, stream, reps, cpu_seconds):
     wall = (time.perf_counter() - t0) / reps
     t = float(np.median(ms))
     out.update({"kernel_ms": t, "pu_per_s_kernels": len(jobs) / (t / 1e3), "ms_per_frame": wall * 1e3,
-                "pu_per_s": len(jobs) / wall, "kernels": "fme::k_tz<4,8>, <8,4>, <8,8> + deferred raster pass k_tz_raster<...> (+ classify, scatter)"})
+                "pu_per_s": len(jobs) / wall, "kernels": "fme::k_tz_wave<4,8>, <8,4>, <8,8>: one wave per PU, three concurrent launches (+ classify, scatter)"})
     out["roofline"] = tz_roofline(jobs, ext, pics, t)
     if "cpu_baseline" in out:
         out["speedup_vs_cpu_1core"] = out["pu_per_s"] / out["cpu_baseline"]["value"]

@@ -19,10 +19,6 @@
 
 #include "fme_device.h"
 
-#ifndef FME_TZ_DEFER_DEFAULT
-#define FME_TZ_DEFER_DEFAULT 1
-#endif
-
 using namespace fme;
 
 namespace {
@@ -115,6 +111,8 @@ struct fme_ctx {
   int nn_margin_cap = 0;       // its length
   void* nn_logits = nullptr;   // caller-owned device array (fme_set_nn_logit_output), 49 per job
   int nn_logits_cap = 0;       // its length in jobs
+  const uint32_t* nn_in = nullptr;   // caller-owned NN input rows of FME_JOB_NN_IN jobs (fme_set_nn_inputs)
+  int nn_in_cap = 0;                 // its length in rows
 
   DevBuf<fme_job> d_jobs;      // staging for fme_refine (host arrays)
   DevBuf<fme_result> d_res;
@@ -144,11 +142,7 @@ struct fme_ctx {
   // integer search: staging for the host entry point, timing events
   DevBuf<fme_tz_ext> d_tz_ext;
   DevBuf<uint32_t> d_tz_sad;
-  DevBuf<uint32_t> d_tz_rst;   // raster hand-off records [n][8]
-  DevBuf<int32_t> d_tz_rq;     // raster queues [3][n] + 3 lengths
-  bool tz_wave = true;                     // FME_TZ_WAVE=0: the lane-per-unit kernels (A/B)
-  bool tz_defer = FME_TZ_DEFER_DEFAULT;   // FME_TZ_DEFER=0/1: raster searches in a second pass
-  int tz_defer_min = 4096;                 // FME_TZ_DEFER_MIN: batches below this size run in one pass
+  DevBuf<uint32_t> d_tz_nn_in;   // staging of fme_integer_search_ring's NN input rows
   hipEvent_t ev_tz[2] = {nullptr, nullptr};
   bool tz_timed = false;
   // predInterSearch producer: m_integerMv2Nx2N[REF_PIC_LIST_0][k] (TEncSearch.h:118), AMVP staging
@@ -241,9 +235,6 @@ int fme_create(int device, const fme_config* cfg, fme_ctx** out_ctx) {
   HIP_TRY(c->d_key_invalid.reserve(1));
   HIP_TRY(hipMemset(c->d_key_invalid.p, 0, sizeof(int32_t)));
   HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&c->h_counts), (kNumClasses + 1) * sizeof(int32_t), hipHostMallocDefault));
-  if (const char* e = getenv("FME_TZ_WAVE")) c->tz_wave = (e[0] == '1');
-  if (const char* e = getenv("FME_TZ_DEFER")) c->tz_defer = (e[0] == '1');
-  if (const char* e = getenv("FME_TZ_DEFER_MIN")) c->tz_defer_min = atoi(e);
   if (cfg->max_jobs > 0) {
     const size_t n = (size_t)cfg->max_jobs;
     const size_t nb = (n + kJobsPerScanBlock - 1) / kJobsPerScanBlock;
@@ -266,7 +257,7 @@ int fme_destroy(fme_ctx* c) {
   for (int i = 0; i < FME_MAX_PICTURES; i++)
     if (c->chroma_owned[i]) (void)hipFree(c->chroma_owned[i]);
   c->d_mc_jobs.release(); c->d_mc_planes.release(); c->d_mc_invalid.release();
-  c->d_tz_ext.release(); c->d_tz_sad.release(); c->d_tz_rst.release(); c->d_tz_rq.release();
+  c->d_tz_ext.release(); c->d_tz_sad.release(); c->d_tz_nn_in.release();
   c->d_amvp.release(); c->d_amvp_sad.release(); c->d_bikey.release(); c->d_key_invalid.release(); c->d_ch_i32.release(); c->d_tz_emi.release();
   for (auto& e : c->ev_tz)
     if (e) (void)hipEventDestroy(e);
@@ -410,11 +401,12 @@ int fme_set_keys(fme_ctx* c, const int16_t* keys, size_t count, void* stream) {
   if (!c || (!keys && count)) return fail(FME_E_INVALID, "fme_set_keys: null argument");
   HIP_TRY(hipSetDevice(c->device));
   HIP_TRY(c->d_keys.reserve(count));
-  if (count) {
-    hipStream_t s = static_cast<hipStream_t>(stream);
-    HIP_TRY(hipMemcpyAsync(c->d_keys.p, keys, count * sizeof(int16_t), hipMemcpyHostToDevice, s));
-    HIP_TRY(hipStreamSynchronize(s));
-  }
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  if (count) HIP_TRY(hipMemcpyAsync(c->d_keys.p, keys, count * sizeof(int16_t), hipMemcpyHostToDevice, s));
+  // fresh host keys: a rejection left by an earlier device build no longer applies (fme.h: rejected
+  // "until keys are built again"), in stream order with the upload
+  HIP_TRY(hipMemsetAsync(c->d_key_invalid.p, 0, sizeof(int32_t), s));
+  HIP_TRY(hipStreamSynchronize(s));
   c->n_keys = count;
   return FME_OK;
 }
@@ -441,8 +433,10 @@ int fme_nn_param_count(const fme_nn_net* n) {
   if (n->out_act != FME_NN_OUT_LINEAR && n->out_act != FME_NN_OUT_SIGMOID)
     return fail(FME_E_INVALID, "fme_nn_param_count: out_act %d", n->out_act);
   if (n->carry_hidden >> n->n_hidden) return fail(FME_E_INVALID, "fme_nn_param_count: carry_hidden 0x%x", n->carry_hidden);
-  if (n->input_flags & ~FME_NN_IN_SLOT_RESET)
+  if (n->input_flags & ~(FME_NN_IN_SLOT_RESET | FME_NN_IN_TZ_RING))
     return fail(FME_E_INVALID, "fme_nn_param_count: input_flags 0x%x", n->input_flags);
+  if ((n->input_flags & FME_NN_IN_TZ_RING) && ((n->input_flags & FME_NN_IN_SLOT_RESET) || n->carry_hidden))
+    return fail(FME_E_INVALID, "fme_nn_param_count: FME_NN_IN_TZ_RING with FME_NN_IN_SLOT_RESET or carry_hidden");
   int count = n->embedding ? 64 : 0, fan = n->embedding ? 17 : 9;
   for (int l = 0; l < n->n_hidden; l++) {
     const int w = n->width[l];
@@ -486,6 +480,14 @@ int fme_set_nn_logit_output(fme_ctx* c, void* d_logits, int capacity) {
   if (d_logits && capacity <= 0) return fail(FME_E_INVALID, "fme_set_nn_logit_output: capacity %d", capacity);
   c->nn_logits = capacity > 0 ? d_logits : nullptr;
   c->nn_logits_cap = d_logits ? capacity : 0;
+  return FME_OK;
+}
+
+int fme_set_nn_inputs(fme_ctx* c, const uint32_t* d_rows, int capacity) {
+  if (!c) return fail(FME_E_INVALID, "fme_set_nn_inputs: null ctx");
+  if (d_rows && capacity <= 0) return fail(FME_E_INVALID, "fme_set_nn_inputs: capacity %d", capacity);
+  c->nn_in = capacity > 0 ? d_rows : nullptr;
+  c->nn_in_cap = d_rows ? capacity : 0;
   return FME_OK;
 }
 
@@ -641,6 +643,8 @@ static int refine_batch(fme_ctx* c, const fme_job* d_jobs, fme_result* d_res, fm
   a.use_hadamard = c->cfg.use_hadamard ? 1 : 0;
   a.fen = c->cfg.fast_inter_mode;
   a.nn_mode = c->cfg.nn_mode ? 1 : 0;
+  a.nn_in = c->nn_in;
+  a.nn_in_cap = c->nn_in_cap;
   WorkBufs w = work_bufs(c);
   w.mv_out = d_mv;
 
@@ -723,8 +727,9 @@ int fme_refine_status(fme_ctx* c) {
 
 // d_emi (may be null): also run the EMI square step of uni-pred EMI jobs and write the resulting
 // integer MV there (the producer's m_integerMv2Nx2N), leaving jobs' mv_x / mv_y at the TZ best.
+// d_nn_in (may be null): FME_TZ_RING jobs run the backups' square + ring and write their NN inputs.
 static int tz_run(fme_ctx* c, fme_job* d_jobs, const fme_tz_ext* d_ext, uint32_t* d_sad, int n, void* stream,
-                  int16_t* d_emi) {
+                  int16_t* d_emi, uint32_t* d_nn_in = nullptr) {
   if (!c || (n > 0 && (!d_jobs || !d_ext))) return fail(FME_E_INVALID, "fme_integer_search_device: null argument");
   if (n < 0) return fail(FME_E_INVALID, "fme_integer_search_device: n = %d", n);
   if (n == 0) return FME_OK;
@@ -766,7 +771,7 @@ static int tz_run(fme_ctx* c, fme_job* d_jobs, const fme_tz_ext* d_ext, uint32_t
     sc.class_off[k] = off;
     sc.class_cnt[k] = cnt;
     for (int q = 0; q < 3; q++) sc.prefix[q][k] = nb[q];
-    nb[tz_kernel_of(k)] += c->tz_wave ? cnt : (int)(((long long)cnt * tz_lanes_per_pu(k) + 255) / 256);
+    nb[tz_kernel_of(k)] += cnt;
     off += cnt;
   }
   for (int q = 0; q < 3; q++) sc.prefix[q][kNumClasses] = nb[q];
@@ -779,18 +784,7 @@ static int tz_run(fme_ctx* c, fme_job* d_jobs, const fme_tz_ext* d_ext, uint32_t
   ta.ext = d_ext;
   ta.sad = d_sad;
   ta.emi_mv = d_emi;
-  // small batches (the producer's dependency levels) skip the second pass: its extra host
-  // synchronisation costs more than the raster divergence it removes
-  const bool defer = !c->tz_wave && c->tz_defer && n >= c->tz_defer_min;
-  ta.defer = defer ? 1 : 0;
-  if (defer) {
-    HIP_TRY(c->d_tz_rst.reserve((size_t)n * 8));
-    HIP_TRY(c->d_tz_rq.reserve((size_t)3 * n + 4));
-    ta.rst = c->d_tz_rst.p;
-    ta.rq = c->d_tz_rq.p;
-    ta.rqn = c->d_tz_rq.p + (size_t)3 * n;
-    HIP_TRY(hipMemsetAsync(ta.rqn, 0, 4 * sizeof(int32_t), s));
-  }
+  ta.nn_in = d_nn_in;
   if (c->profiling) HIP_TRY(hipEventRecord(c->ev_tz[0], s));
   // the three unit-shape kernels are latency-bound and independent: 4x8 and 8x4 units on the two
   // auxiliary streams, 8x8 units on the caller's stream, joined before returning
@@ -803,36 +797,20 @@ static int tz_run(fme_ctx* c, fme_job* d_jobs, const fme_tz_ext* d_ext, uint32_t
   HIP_TRY(hipEventRecord(c->ev_fork, s));
   HIP_TRY(hipStreamWaitEvent(c->aux, c->ev_fork, 0));
   HIP_TRY(hipStreamWaitEvent(c->aux2, c->ev_fork, 0));
-  HIP_TRY((c->tz_wave ? launch_tz_wave : launch_tz)(ta, sc, 0, c->aux));
-  HIP_TRY((c->tz_wave ? launch_tz_wave : launch_tz)(ta, sc, 1, c->aux2));
-  HIP_TRY((c->tz_wave ? launch_tz_wave : launch_tz)(ta, sc, 2, s));
+  HIP_TRY(launch_tz_wave(ta, sc, 0, c->aux));
+  HIP_TRY(launch_tz_wave(ta, sc, 1, c->aux2));
+  HIP_TRY(launch_tz_wave(ta, sc, 2, s));
   HIP_TRY(hipEventRecord(c->ev_join, c->aux));
   HIP_TRY(hipEventRecord(c->ev_join2, c->aux2));
   HIP_TRY(hipStreamWaitEvent(s, c->ev_join, 0));
   HIP_TRY(hipStreamWaitEvent(s, c->ev_join2, 0));
-  if (defer) {
-    // pass 2: the queued raster searches, one PU per wave (queue lengths read back: one sync)
-    HIP_TRY(hipMemcpyAsync(c->h_counts, ta.rqn, 3 * sizeof(int32_t), hipMemcpyDeviceToHost, s));
-    HIP_TRY(hipStreamSynchronize(s));
-    const int nq[3] = {c->h_counts[0], c->h_counts[1], c->h_counts[2]};
-    HIP_TRY(hipEventRecord(c->ev_fork, s));
-    HIP_TRY(hipStreamWaitEvent(c->aux, c->ev_fork, 0));
-    HIP_TRY(hipStreamWaitEvent(c->aux2, c->ev_fork, 0));
-    HIP_TRY(launch_tz_raster(ta, sc, 0, nq[0], c->aux));
-    HIP_TRY(launch_tz_raster(ta, sc, 1, nq[1], c->aux2));
-    HIP_TRY(launch_tz_raster(ta, sc, 2, nq[2], s));
-    HIP_TRY(hipEventRecord(c->ev_join, c->aux));
-    HIP_TRY(hipEventRecord(c->ev_join2, c->aux2));
-    HIP_TRY(hipStreamWaitEvent(s, c->ev_join, 0));
-    HIP_TRY(hipStreamWaitEvent(s, c->ev_join2, 0));
-  }
   if (c->profiling) HIP_TRY(hipEventRecord(c->ev_tz[1], s));
   c->tz_timed = c->profiling;
   return FME_OK;
 }
 
 static int tz_run_host(fme_ctx* c, fme_job* jobs, const fme_tz_ext* ext, uint32_t* sad, int n, void* stream,
-                       int16_t* emi) {
+                       int16_t* emi, uint32_t* nn_in = nullptr) {
   if (!c || (n > 0 && (!jobs || !ext))) return fail(FME_E_INVALID, "fme_integer_search: null argument");
   if (n <= 0) return n == 0 ? FME_OK : fail(FME_E_INVALID, "fme_integer_search: n = %d", n);
   HIP_TRY(hipSetDevice(c->device));
@@ -841,13 +819,18 @@ static int tz_run_host(fme_ctx* c, fme_job* jobs, const fme_tz_ext* ext, uint32_
   HIP_TRY(c->d_tz_ext.reserve(n));
   HIP_TRY(c->d_tz_sad.reserve(n));
   if (emi) HIP_TRY(c->d_tz_emi.reserve((size_t)2 * n));
+  if (nn_in) HIP_TRY(c->d_tz_nn_in.reserve((size_t)9 * n));
   HIP_TRY(hipMemcpyAsync(c->d_jobs.p, jobs, (size_t)n * sizeof(fme_job), hipMemcpyHostToDevice, s));
   HIP_TRY(hipMemcpyAsync(c->d_tz_ext.p, ext, (size_t)n * sizeof(fme_tz_ext), hipMemcpyHostToDevice, s));
-  int rc = tz_run(c, c->d_jobs.p, c->d_tz_ext.p, c->d_tz_sad.p, n, stream, emi ? c->d_tz_emi.p : nullptr);
+  // rows of jobs without FME_TZ_RING are left untouched: start from the caller's values
+  if (nn_in) HIP_TRY(hipMemcpyAsync(c->d_tz_nn_in.p, nn_in, (size_t)9 * n * sizeof(uint32_t), hipMemcpyHostToDevice, s));
+  int rc = tz_run(c, c->d_jobs.p, c->d_tz_ext.p, c->d_tz_sad.p, n, stream, emi ? c->d_tz_emi.p : nullptr,
+                  nn_in ? c->d_tz_nn_in.p : nullptr);
   if (rc) return rc;
   HIP_TRY(hipMemcpyAsync(jobs, c->d_jobs.p, (size_t)n * sizeof(fme_job), hipMemcpyDeviceToHost, s));
   if (sad) HIP_TRY(hipMemcpyAsync(sad, c->d_tz_sad.p, (size_t)n * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
   if (emi) HIP_TRY(hipMemcpyAsync(emi, c->d_tz_emi.p, (size_t)n * 2 * sizeof(int16_t), hipMemcpyDeviceToHost, s));
+  if (nn_in) HIP_TRY(hipMemcpyAsync(nn_in, c->d_tz_nn_in.p, (size_t)9 * n * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
   HIP_TRY(hipStreamSynchronize(s));
   return FME_OK;
 }
@@ -935,6 +918,18 @@ int fme_integer_search_device(fme_ctx* c, fme_job* d_jobs, const fme_tz_ext* d_e
 
 int fme_integer_search(fme_ctx* c, fme_job* jobs, const fme_tz_ext* ext, uint32_t* sad, int n, void* stream) {
   return tz_run_host(c, jobs, ext, sad, n, stream, nullptr);
+}
+
+int fme_integer_search_ring_device(fme_ctx* c, fme_job* d_jobs, const fme_tz_ext* d_ext, uint32_t* d_sad,
+                                   uint32_t* d_nn_in, int n, void* stream) {
+  if (!d_nn_in && n > 0) return fail(FME_E_INVALID, "fme_integer_search_ring_device: null nn_in");
+  return tz_run(c, d_jobs, d_ext, d_sad, n, stream, nullptr, d_nn_in);
+}
+
+int fme_integer_search_ring(fme_ctx* c, fme_job* jobs, const fme_tz_ext* ext, uint32_t* sad, uint32_t* nn_in,
+                            int n, void* stream) {
+  if (!nn_in && n > 0) return fail(FME_E_INVALID, "fme_integer_search_ring: null nn_in");
+  return tz_run_host(c, jobs, ext, sad, n, stream, nullptr, nn_in);
 }
 
 int fme_integer_search_last_ms(fme_ctx* c, float* ms) {
@@ -1499,10 +1494,10 @@ int fme_build_bipred_keys(fme_ctx* c, const fme_bikey_req* reqs, int n, size_t k
   if (rc) return rc;
   HIP_TRY(c->d_keys.reserve(key_count));
   c->n_keys = key_count;
-  if (n == 0) return FME_OK;
+  HIP_TRY(hipMemsetAsync(c->d_key_invalid.p, 0, sizeof(int32_t), s));   // host-validated: the keys are good
+  if (n == 0) return hipStreamSynchronize(s) == hipSuccess ? FME_OK : fail(FME_E_DEVICE, "fme_build_bipred_keys: sync");
   HIP_TRY(c->d_bikey.reserve((size_t)n));
   HIP_TRY(hipMemcpyAsync(c->d_bikey.p, reqs, (size_t)n * sizeof(BiKeyTask), hipMemcpyHostToDevice, s));
-  HIP_TRY(hipMemsetAsync(c->d_key_invalid.p, 0, sizeof(int32_t), s));   // host-validated: the keys are good
   BiKeyArgs ka{c->d_bikey.p, c->d_pics.p, c->d_keys.p, (int32_t)n, nullptr, (int64_t)key_count};
   HIP_TRY(launch_bi_key(ka, s));
   HIP_TRY(hipStreamSynchronize(s));

@@ -94,6 +94,8 @@ struct BatchArgs {
   int32_t nn_mode;
   const int32_t* key_invalid; // > 0: the last device-built keys had invalid requests; batches
                               // whose jobs read keys are rejected (k_classify)
+  const uint32_t* nn_in;      // NN input rows of FME_JOB_NN_IN jobs ([nn_in_cap][9]) or null
+  int32_t nn_in_cap;
 };
 
 struct Schedule;
@@ -142,11 +144,8 @@ struct TzArgs {
   fme_job* jobs_out;          // mv_x / mv_y written per job
   const fme_tz_ext* ext;
   uint32_t* sad;              // may be null
-  int32_t defer;              // 1: pass 1 queues raster searches for pass 2 (k_tz_raster)
-  uint32_t* rst;              // [n][8] raster hand-off records, by job index
-  int32_t* rq;                // [3][n] queued job indices per kernel
-  int32_t* rqn;               // [3] queue lengths
   int16_t* emi_mv;            // [n][2] or null: the MV after the EMI square step (uni-pred EMI jobs)
+  uint32_t* nn_in;            // [n][9] or null: FME_TZ_RING jobs' NN inputs (array_e[index_ref..+7], C)
 };
 int tz_kernel_of(int cls);    // 0: 4x8 units, 1: 8x4, 2: 8x8
 int tz_lanes_per_pu(int cls);
@@ -156,8 +155,6 @@ struct TzSchedule {
   int32_t class_off[kNumClasses];
   int32_t class_cnt[kNumClasses];
 };
-hipError_t launch_tz(const TzArgs& ta, const TzSchedule& sc, int kid, hipStream_t s);
-hipError_t launch_tz_raster(const TzArgs& ta, const TzSchedule& sc, int kid, int nq, hipStream_t s);
 hipError_t launch_tz_wave(const TzArgs& ta, const TzSchedule& sc, int kid, hipStream_t s);   // prefix in waves
 // The dependency levels of a producer's m_integerMv2Nx2N chain (fme_tz.hip k_tz_level): jobs in
 // level order, level l = jobs [lvl_off[l], lvl_off[l+1]), one launch per level, back to back.
@@ -229,6 +226,19 @@ hipError_t launch_nn_tail(const BatchArgs& a, const WorkBufs& w, const float* nn
 
 // The tail kernels' output: xMotionEstimation's MV / cost / bits with the NN class and status,
 // into the full record or, for fme_refine_mv*, the compact one alone.
+// The carried array_e slots a job writes (slots 0 .. n-1) and whether it writes C / PU size:
+// FME_JOB_EMI: the EMI square step's pushes (its count by geometry, TEncSearch.cpp:1341-1376);
+// FME_JOB_NN_IN: a whole input row (the backups' path: all 8 slots, unpushed ones 0, and C).
+__device__ __forceinline__ int nn_pushes(const fme_job& j) {
+  if (j.flags & FME_JOB_NN_IN) return 8;
+  if (!(j.flags & FME_JOB_EMI)) return 0;
+  const bool top = j.mv_y - 1 >= j.lt_y, bot = j.mv_y + 1 <= j.rb_y;
+  const bool left = j.mv_x - 1 >= j.lt_x, right = j.mv_x + 1 <= j.rb_x;
+  const int cols = 1 + (left ? 1 : 0) + (right ? 1 : 0);
+  return (top ? cols : 0) + (left ? 1 : 0) + (right ? 1 : 0) + (bot ? cols : 0);
+}
+__device__ __forceinline__ bool nn_writes_c(const fme_job& j) { return (j.flags & (FME_JOB_EMI | FME_JOB_NN_IN)) != 0; }
+
 __device__ __forceinline__ void store_outputs(fme_result* r, fme_mv_result* mv_out, int i, int fx, int fy,
                                               uint32_t cost, uint32_t bits, uint8_t cls, uint16_t status) {
   if (mv_out) {

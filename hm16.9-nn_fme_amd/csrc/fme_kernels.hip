@@ -70,14 +70,6 @@ __host__ __device__ __forceinline__ int class_of(int w, int h) {
   return 255;
 }
 
-// Push count of the EMI square step by geometry alone (TEncSearch.cpp:1341-1376).
-__device__ __forceinline__ int emi_pushes(const fme_job& j) {
-  const bool top = j.mv_y - 1 >= j.lt_y, bot = j.mv_y + 1 <= j.rb_y;
-  const bool left = j.mv_x - 1 >= j.lt_x, right = j.mv_x + 1 <= j.rb_x;
-  const int cols = 1 + (left ? 1 : 0) + (right ? 1 : 0);
-  return (top ? cols : 0) + (left ? 1 : 0) + (right ? 1 : 0) + (bot ? cols : 0);
-}
-
 // ---------------------------------------------------------------------------------------
 // classify: class histogram + first pass of the NN writer prefix-max
 // ---------------------------------------------------------------------------------------
@@ -138,11 +130,13 @@ __global__ __launch_bounds__(kBlock) void k_classify(BatchArgs a, WorkBufs w) {
                (int)j.x + j.w <= pic_w[j.org_id] && (int)j.y + j.h <= pic_h[j.org_id];
         }
       }
+      // FME_JOB_NN_IN: its input row must be bound (fme_set_nn_inputs)
+      if ((j.flags & FME_JOB_NN_IN) && (!a.nn_in || i >= a.nn_in_cap)) ok = false;
       if (!ok) c = 255;
       w.cls[i] = (uint8_t)c;
       atomicAdd(&hist[c == 255 ? kNumClasses : c], 1);
-      if (j.flags & FME_JOB_EMI) {
-        const int np = emi_pushes(j);
+      if (nn_writes_c(j)) {
+        const int np = nn_pushes(j);
 #pragma unroll
         for (int s = 0; s < 8; s++)
           if (np > s) mx[s] = max(mx[s], i);
@@ -432,7 +426,7 @@ __device__ __forceinline__ void tail_job(const BatchArgs& a, const WorkBufs& w, 
       pw = st_in[10];
     }
     cls = nn_forward(nnp_g, e, c, (int)ph, (int)pw);
-    if (!(j.flags & FME_JOB_EMI) || own_n_emi < 8) status |= FME_RES_NN_STALE;
+    if (!nn_writes_c(j) || own_n_emi < 8) status |= FME_RES_NN_STALE;
     if ((written & 0x1FFu) != 0x1FFu) status |= FME_RES_NN_UNINIT;
     offx = cls % 7 - 3;
     offy = cls / 7 - 3;
@@ -502,11 +496,11 @@ void k_nn_tail(BatchArgs a, WorkBufs w, const float* __restrict__ nnp_g, int sta
     // writer indices of this job (slots it pushes, C / PU size)
     int run[9];
     {
-      const bool emi = valid && (j.flags & FME_JOB_EMI);
-      const int np = emi ? emi_pushes(j) : 0;
+      const bool wr = valid && nn_writes_c(j);
+      const int np = wr ? nn_pushes(j) : 0;
 #pragma unroll
       for (int s = 0; s < 8; s++) run[s] = (np > s) ? i : -1;
-      run[8] = emi ? i : -1;
+      run[8] = wr ? i : -1;
     }
     int src[9], tot[9];
     writer_scan<kTailNT / 64>(run, carry, base, wave_tot, src, tot);

@@ -758,6 +758,7 @@ typedef __attribute__((address_space(1))) const int32_t g_i32;
 typedef __attribute__((address_space(1))) fme_result g_res;
 typedef __attribute__((address_space(1))) const int16_t g_i16;
 typedef __attribute__((address_space(1))) const uint8_t g_u8;
+typedef __attribute__((address_space(1))) const uint32_t g_u32;
 
 
 // =============================================================================================
@@ -972,6 +973,14 @@ __device__ FME_LANE_UNIT_ATTR void lane_unit(const BatchArgs& a, const fme_job* 
     ey = by - sy;
     mvx = bx;
     mvy = by;
+  } else if (j.flags & FME_JOB_NN_IN) {
+    // the backups' input path: the integer search's square + ring already moved mv and pushed
+    // the inputs (FME_TZ_RING); the job's row holds array_e[index_ref .. +7] and C
+    g_u32* const row = (g_u32*)(a.nn_in + (size_t)9 * jid);
+#pragma unroll
+    for (int k = 0; k < 8; k++) emi[k] = row[k];
+    cval = row[8];
+    n_emi = 8;
   }
   typedef __attribute__((address_space(1))) u32x4a gw4;
 #if FME_LANE_REC_LDS

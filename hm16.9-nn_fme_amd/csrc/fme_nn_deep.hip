@@ -44,12 +44,6 @@ constexpr int kOP = 64;                           // output rows padded to 4 MFM
 constexpr int kAS = 65;                           // LDS activation row stride (elements)
 
 
-__device__ __forceinline__ int emi_pushes_d(const fme_job& j) {   // TEncSearch.cpp:1341-1376
-  const bool top = j.mv_y - 1 >= j.lt_y, bot = j.mv_y + 1 <= j.rb_y;
-  const bool left = j.mv_x - 1 >= j.lt_x, right = j.mv_x + 1 <= j.rb_x;
-  const int cols = 1 + (left ? 1 : 0) + (right ? 1 : 0);
-  return (top ? cols : 0) + (left ? 1 : 0) + (right ? 1 : 0) + (bot ? cols : 0);
-}
 // Embedding rows: W (and Backups/15's H) 4,8,12,16,24,32,64 -> 1..7; the master's H swaps 12/16.
 __device__ __forceinline__ int row_w(int v) {
   return v == 4 ? 1 : v == 8 ? 2 : v == 12 ? 3 : v == 16 ? 4 : v == 24 ? 5 : v == 32 ? 6 : v == 64 ? 7 : 0;
@@ -92,7 +86,6 @@ struct DeepArgs {
   int32_t emb_mode;       // FME_NN_EMB_MASTER / FME_NN_EMB_SWAP (EMB kernels)
   int32_t out_act;        // FME_NN_OUT_*
   uint32_t in_flags;      // FME_NN_IN_*
-  int32_t tmode;          // double nets on the MFMA engine: 1 = forward_mfma_t (FME_DEEP_TRANSPOSED=1)
 };
 
 // ---- exact engine: one lane per job ----------------------------------------------------------
@@ -226,95 +219,6 @@ __device__ __forceinline__ void forward_mfma(const T* __restrict__ P, T* act, in
   layer_mfma<T, kHW, kOP, false>(act, P + D::kWout, P + D::kBout, nullptr, nullptr, lane);
 }
 
-// Double nets without the per-layer LDS round trips: the layers are computed transposed,
-// OUT^T[unit][job] = W[unit][k] * X^T[k][job], with the weights as the A operand and 16 jobs as
-// the N dimension.  v_mfma_f64_16x16x4_f64 leaves lane (job c16, q) holding units q + 4r of each
-// 16-unit tile, which is exactly the B operand the next layer's K-step 4 mt + r needs from that
-// lane (unit 4 kk + q), so hidden activations stay in registers from layer to layer; only the
-// input rows and the output rows pass through this wave's LDS rows.  Same products in the same k
-// order as forward_mfma.
-template <int KS, int KSTR, int NB>
-__device__ __forceinline__ void hidden_t(const double* __restrict__ W, const double* __restrict__ bias,
-                                         const double* __restrict__ g, const double* __restrict__ be,
-                                         double (&b)[4][NB], int c16, int q) {
-  // all four 16-job tiles at once: 12 independent accumulator chains keep the MFMA pipe full
-  using M = Mfma<double>;
-  typename M::acc_t acc[3][4];
-#pragma unroll
-  for (int mt = 0; mt < 3; mt++)
-#pragma unroll
-    for (int nt = 0; nt < 4; nt++) acc[mt][nt] = typename M::acc_t{0, 0, 0, 0};
-#pragma unroll
-  for (int kk = 0; kk < KS; kk++)
-#pragma unroll
-    for (int mt = 0; mt < 3; mt++) {
-      const double a = W[(mt * 16 + c16) * KSTR + kk * 4 + q];
-#pragma unroll
-      for (int nt = 0; nt < 4; nt++) acc[mt][nt] = M::mma(a, b[nt][kk], acc[mt][nt]);
-    }
-#pragma unroll
-  for (int mt = 0; mt < 3; mt++)
-#pragma unroll
-    for (int nt = 0; nt < 4; nt++) asm volatile("s_nop 15\n\ts_nop 15" : "+a"(acc[mt][nt]));   // (see layer_mfma)
-#pragma unroll
-  for (int mt = 0; mt < 3; mt++)
-#pragma unroll
-    for (int r = 0; r < 4; r++) {
-      if (4 * mt + r >= NB) continue;
-      const int u = mt * 16 + q + 4 * r;
-      const double bb = bias[u], gg = g[u], ee = be[u];
-#pragma unroll
-      for (int nt = 0; nt < 4; nt++) b[nt][4 * mt + r] = relu(acc[mt][nt][r] + bb) * gg + ee;
-    }
-}
-
-template <int NH, bool EMB, int L>
-struct ChainT {   // hidden layers L..NH-1, in registers
-  static __device__ __forceinline__ void run(const double* __restrict__ P, double (&b)[4][kHW / 4], int c16, int q) {
-    using D = DeepLayout<NH, EMB>;
-    hidden_t<kHW / 4, kHW, kHW / 4>(P + D::w(L), P + D::b(L), P + D::g(L), P + D::be(L), b, c16, q);
-    ChainT<NH, EMB, L + 1>::run(P, b, c16, q);
-  }
-};
-template <int NH, bool EMB>
-struct ChainT<NH, EMB, NH> {
-  static __device__ __forceinline__ void run(const double* __restrict__, double (&)[4][kHW / 4], int, int) {}
-};
-
-template <int NH, bool EMB>
-__device__ __forceinline__ void forward_mfma_t(const double* __restrict__ P, double* act, int lane) {
-  using D = DeepLayout<NH, EMB>;
-  using M = Mfma<double>;
-  const int c16 = lane & 15, q = lane >> 4;
-  double b[4][kHW / 4];
-#pragma unroll
-  for (int nt = 0; nt < 4; nt++)
-#pragma unroll
-    for (int kk = 0; kk < kHW / 4; kk++) b[nt][kk] = kk < D::KP0 / 4 ? act[(nt * 16 + c16) * kAS + kk * 4 + q] : 0.0;
-  hidden_t<D::KP0 / 4, D::KP0, kHW / 4>(P + D::w(0), P + D::b(0), P + D::g(0), P + D::be(0), b, c16, q);
-  ChainT<NH, EMB, 1>::run(P, b, c16, q);
-#pragma unroll 1
-  for (int mt = 0; mt < kOP / 16; mt++) {   // output tiles one at a time (4 job tiles each)
-    typename M::acc_t acc[4];
-#pragma unroll
-    for (int nt = 0; nt < 4; nt++) acc[nt] = typename M::acc_t{0, 0, 0, 0};
-#pragma unroll
-    for (int kk = 0; kk < kHW / 4; kk++) {
-      const double a = P[D::kWout + (mt * 16 + c16) * kHW + kk * 4 + q];
-#pragma unroll
-      for (int nt = 0; nt < 4; nt++) acc[nt] = M::mma(a, b[nt][kk], acc[nt]);
-    }
-#pragma unroll
-    for (int nt = 0; nt < 4; nt++) asm volatile("s_nop 15\n\ts_nop 15" : "+a"(acc[nt]));
-#pragma unroll
-    for (int nt = 0; nt < 4; nt++)
-#pragma unroll
-      for (int r = 0; r < 4; r++) {
-        const int u = mt * 16 + q + 4 * r;
-        if (u < 49) act[(nt * 16 + c16) * kAS + u] = acc[nt][r] + P[D::kBout + u];
-      }
-  }
-}
 
 // x = ((T)raw - mean) / stdev * gamma_in for raw = e0..e3, C, e4..e7, after the two embedding rows
 // (TEncSearch.cpp:88-113, Backups/4:4427-4441, Backups/15:4966-5005).
@@ -400,11 +304,11 @@ __global__ __launch_bounds__(kRound) void k_nn_deep_tail(BatchArgs a, WorkBufs w
     // writer indices of this job, prefix-max over the round (carry from earlier rounds/blocks)
     int run[9];
     {
-      const bool emi = valid && (j.flags & FME_JOB_EMI);
-      const int np = emi ? emi_pushes_d(j) : 0;
+      const bool wr = valid && nn_writes_c(j);
+      const int np = wr ? nn_pushes(j) : 0;
 #pragma unroll
       for (int s = 0; s < 8; s++) run[s] = (np > s) ? i : -1;
-      run[8] = emi ? i : -1;
+      run[8] = wr ? i : -1;
     }
     int src[9], tot[9];
     writer_scan<kRound / 64>(run, carry, blockIdx.x * kJobsPerScanBlock + rnd * kRound, wave_tot, src, tot);
@@ -443,14 +347,7 @@ __global__ __launch_bounds__(kRound) void k_nn_deep_tail(BatchArgs a, WorkBufs w
     if (MFMA) {
 #pragma unroll
       for (int k = 0; k < L::KP0; k++) act[lane * kAS + k] = k < L::K0 ? in[k] : (T)0;
-      if constexpr (sizeof(T) == 8) {
-        if (d.tmode)
-          forward_mfma_t<NH, EMB>(reinterpret_cast<const double*>(P), reinterpret_cast<double*>(act), lane);
-        else
-          forward_mfma<T, NH, EMB>(P, act, lane);
-      } else {
-        forward_mfma<T, NH, EMB>(P, act, lane);
-      }
+      forward_mfma<T, NH, EMB>(P, act, lane);
 #pragma unroll
       for (int o = 0; o < 49; o++) out[o] = act[lane * kAS + o];
     } else {
@@ -466,7 +363,7 @@ __global__ __launch_bounds__(kRound) void k_nn_deep_tail(BatchArgs a, WorkBufs w
 
     fme_result* r = a.res + i;
     uint16_t status = 0;
-    if (!(j.flags & FME_JOB_EMI) || r->n_emi < 8) status |= FME_RES_NN_STALE;
+    if (!nn_writes_c(j) || r->n_emi < 8) status |= FME_RES_NN_STALE;
     if ((written & 0x1FFu) != 0x1FFu) status |= FME_RES_NN_UNINIT;
     if (i == a.n - 1) {
 #pragma unroll
@@ -698,11 +595,7 @@ void nn_deep_pack(const fme_nn_net& n, const double* params, void* out) {
 hipError_t launch_nn_deep_tail(const fme_nn_net& n, const void* packed, float* margin, void* logits, const BatchArgs& a,
                                const WorkBufs& w, int state_in, int engine, hipStream_t s) {
   if (!deep_supported(n)) return hipErrorInvalidValue;
-  static const int tmode = [] {
-    const char* e = getenv("FME_DEEP_TRANSPOSED");
-    return e ? atoi(e) : 0;
-  }();
-  const DeepArgs d{packed, margin, logits, n.embedding, n.out_act, n.input_flags, tmode};
+  const DeepArgs d{packed, margin, logits, n.embedding, n.out_act, n.input_flags};
   const bool emb = n.embedding != FME_NN_EMB_NONE, mfma = engine == FME_NN_ENGINE_MFMA;
   if (n.precision == FME_NN_F64)
     return (mfma ? launch_deep_double_1 : launch_deep_double_0)(n.n_hidden, emb, a, w, d, state_in, s);
@@ -712,7 +605,7 @@ hipError_t launch_nn_deep_tail(const fme_nn_net& n, const void* packed, float* m
 hipError_t launch_nn_deep_single(const fme_nn_net& n, const void* packed, const NnIn11& in11, int32_t* out,
                                  uint32_t* flag, uint32_t seq, hipStream_t s) {
   if (!deep_supported(n)) return hipErrorInvalidValue;
-  const DeepArgs d{packed, nullptr, nullptr, n.embedding, n.out_act, n.input_flags, 0};
+  const DeepArgs d{packed, nullptr, nullptr, n.embedding, n.out_act, n.input_flags};
   const bool emb = n.embedding != FME_NN_EMB_NONE;
   return n.precision == FME_NN_F64 ? single_deep_double(n.n_hidden, emb, d, in11, out, flag, seq, s)
                                    : single_deep_float(n.n_hidden, emb, d, in11, out, flag, seq, s);

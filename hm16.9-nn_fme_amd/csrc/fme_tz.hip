@@ -10,12 +10,9 @@
 // xTZ2PointSearch (1191-1322), xSetSearchRange (4602-4624), TComDataCU::clipMv
 // (TComDataCU.cpp:2773-2786), TComMv::divideByPowerOf2 (TComMv.h:122-130).
 //
-// Mapping: one lane per unit of a PU (8x8, 8x4 or 4x8; a PU of W x H has (W/UW)(H/UH) units,
-// the group padded to a power of two), as in fme_lane.hip.  The search is a state machine every
-// lane of a group steps in lock-step: it yields the next candidate the reference would test (range
-// checks and phase changes without a test are folded into the step), the group sums its units'
-// distortions with DPP, and every lane applies xTZSearchHelp's update.  Groups of one wave advance
-// together; a finished group idles until the wave's last group is done.
+// Mapping: one wave per PU (k_tz_wave; tz_wave below): the PU's units (8x8, 8x4 or 4x8; the group
+// of L lanes padded to a power of two) sit in consecutive lanes, and the wave's 64 / L groups
+// evaluate the candidates of one reference list (a diamond ring, the raster, ...) together.
 // Metric (the NN_FME integer-ME setDistParam, TComRdCost.cpp:200-230): SSE for widths 4..64, SAD
 // for 12/24/48 with the FEN even-row subsampling when H > 8; uni-pred keys as (s - 128) bytes
 // (SSE = Sk2 - 2 Sks + Sss with v_dot4_i32_i8, SAD with v_sad_u8), bi-pred keys (2 org - pred,
@@ -60,28 +57,15 @@ struct Range {
   int l, r, t, b;
 };
 
-enum Phase {
-  P_START, P_ZERO, P_PRED, P_RANGE, P_FIRST, P_TWO1, P_TWO, P_RASTER_CHK, P_RASTER, P_STAR_CHK, P_STAR,
-  P_STAR_END, P_FULL, P_DONE, P_DEFER, P_SQUARE
-};
 
 struct Tz {
   // IntTZSearchStruct
   uint32_t best_sad;
   int bx, by, bdist, bround, pnr;
-  // state machine
-  int phase, ret;
-  int sx, sy;           // rounded start (the AMVP predictor)
-  int px, py;           // 2Nx2N integer MV
-  bool has_pred;
-  int ox, oy;           // origin of the running diamond / two-point search
+  int ox, oy;           // origin of the running diamond / two-point / square search
   int dist, k, opnr;
-  int rx, ry;           // raster iterators
   Range R, RR;          // search range, raster range
   int range;            // m_iSearchRange
-  bool square;          // run the EMI square step after the search (ta.emi_mv)
-  int tx, ty;           // the TZ best before the square step
-  uint32_t tsad;
 };
 
 // xTZ8PointSquareSearch (TEncSearch.cpp:1324-1377) at distance 1: point k of (1 2 3 / 4 . 5 / 6 7 8) in
@@ -95,6 +79,28 @@ __device__ __forceinline__ bool square_point(const Tz& s, int k, bool& ok, int& 
   ok = (dy < 0 ? y >= s.R.t : true) && (dy > 0 ? y <= s.R.b : true) && (dx < 0 ? x >= s.R.l : true) &&
        (dx > 0 ? x <= s.R.r : true);
   return true;
+}
+
+// Point i of the backups' final pair of squares around (ox, oy): i < 8: xTZ8PointSquareSearch at
+// distance 1 (square_point); i = 8..23: xTZ8PointSquareSearch2 at distance 2 (Backups/4:876-965),
+// 16 points in its call order with its range checks, which test the x -/+ 1 points of the top and
+// bottom rows against the left / right bound of distance 2.
+__device__ __forceinline__ void ring_square_point(const Tz& s, int i, bool& ok, int& x, int& y) {
+  if (i < 8) {
+    square_point(s, i, ok, x, y);
+    return;
+  }
+  // per ring point: dx, dy in -2..2 (stored +2), and which bounds it checks: bit 0 top, 1 bottom,
+  // 2 left (x - 2 >= l), 3 right (x + 2 <= r)
+  const int k = i - 8;
+  // 4-bit fields per point k (dx + 2, dy + 2, checks), packed so a runtime k needs no table in memory
+  const uint64_t kDx = 0x4321040404043210ull, kDy = 0x4444433221100000ull, kChk = 0xaa26684848499155ull;
+  const int dxk = (int)((kDx >> (4 * k)) & 15), dyk = (int)((kDy >> (4 * k)) & 15);
+  x = s.ox + dxk - 2;
+  y = s.oy + dyk - 2;
+  const int c = (int)((kChk >> (4 * k)) & 15);
+  ok = (!(c & 1) || s.oy - 2 >= s.R.t) && (!(c & 2) || s.oy + 2 <= s.R.b) && (!(c & 4) || s.ox - 2 >= s.R.l) &&
+       (!(c & 8) || s.ox + 2 <= s.R.r);
 }
 
 // Point k of xTZ8PointDiamondSearch(origin, dist) in call order, with the range check the
@@ -177,166 +183,6 @@ __device__ __forceinline__ bool two_point_has_more(const Tz& s) {
   return false;
 }
 
-// Next candidate of the search (x, y, point number, distance for xTZSearchHelp); false = done.
-// `more`: the following call continues the same list (diamond, two-point, raster, full search)
-// without a decision that depends on this candidate's result, so the two can be evaluated together.
-// `defer` (wave-uniform): stop at the raster (P_DEFER) and leave it to the second pass.
-__device__ __forceinline__ bool next_candidate(Tz& s, int pw, int ph, int cu_x, int cu_y, int& x, int& y, int& pnr,
-                                               int& pd, bool& more, bool defer) {
-  more = false;
-  for (int guard = 0; guard < 64; guard++) {   // phase changes between two tests are bounded
-    switch (s.phase) {
-      case P_START:
-        s.phase = P_ZERO;
-        x = s.sx; y = s.sy; pnr = 0; pd = 0;
-        return true;
-      case P_ZERO:
-        s.phase = P_PRED;
-        if ((s.sx != 0 || s.sy != 0) && (s.bx != 0 || s.by != 0)) {
-          x = 0; y = 0; pnr = 0; pd = 0;
-          return true;
-        }
-        break;
-      case P_PRED:
-        s.phase = P_RANGE;
-        if (s.has_pred && (s.sx != s.px || s.sy != s.py) && (s.px != s.bx || s.py != s.by)) {
-          x = s.px; y = s.py; pnr = 0; pd = 0;
-          return true;
-        }
-        break;
-      case P_RANGE:
-        s.RR = s.R;
-        if (s.has_pred) {   // xSetSearchRange(currBest << 2, m_iSearchRange): raster range only
-          int cx = s.bx * 4, cy = s.by * 4;
-          clip_qpel(cx, cy, pw, ph, cu_x, cu_y);
-          int lx = cx - (s.range << 2), ly = cy - (s.range << 2), rx = cx + (s.range << 2), ry = cy + (s.range << 2);
-          clip_qpel(lx, ly, pw, ph, cu_x, cu_y);
-          clip_qpel(rx, ry, pw, ph, cu_x, cu_y);
-          s.RR = Range{round4(lx), round4(rx), round4(ly), round4(ry)};
-        }
-        s.phase = P_FIRST;
-        s.ox = s.bx; s.oy = s.by; s.dist = 1; s.k = -1;
-        break;
-      case P_FIRST:
-      case P_STAR: {
-        if (s.k < 0) {
-          s.bround += 1;
-          s.k = 0;
-        }
-        bool ok;
-        while (diamond_point(s, s.k, ok, x, y, pnr, pd)) {
-          s.k++;
-          if (ok) {
-            more = diamond_has_more(s);
-            return true;
-          }
-        }
-        if (s.phase == P_FIRST) {
-          if (s.bround >= 3 || 2 * s.dist > s.range) s.phase = P_TWO1;
-          else { s.dist *= 2; s.k = -1; }
-        } else {
-          if (2 * s.dist > s.range) s.phase = P_STAR_END;
-          else { s.dist *= 2; s.k = -1; }
-        }
-        break;
-      }
-      case P_TWO1:
-        s.phase = P_RASTER_CHK;
-        if (s.bdist == 1) {
-          s.bdist = 0;
-          s.ox = s.bx; s.oy = s.by; s.opnr = s.pnr; s.k = 0;
-          s.ret = P_RASTER_CHK;
-          s.phase = P_TWO;
-        }
-        break;
-      case P_TWO: {
-        bool ok;
-        while (two_point(s, s.k, ok, x, y)) {
-          s.k++;
-          if (ok) {
-            pnr = 0; pd = 2;
-            more = two_point_has_more(s);
-            return true;
-          }
-        }
-        s.phase = s.ret;
-        break;
-      }
-      case P_RASTER_CHK:
-        s.phase = P_STAR_CHK;
-        if (s.bdist > 5) {
-          s.bdist = 5;
-          if (s.RR.l <= s.RR.r && s.RR.t <= s.RR.b) {
-            s.rx = s.RR.l; s.ry = s.RR.t;
-            s.phase = defer ? P_DEFER : P_RASTER;
-          }
-        }
-        break;
-      case P_RASTER:
-        if (s.ry > s.RR.b) {
-          s.phase = P_STAR_CHK;
-          break;
-        }
-        x = s.rx; y = s.ry; pnr = 0; pd = 5;
-        s.rx += 5;
-        if (s.rx > s.RR.r) { s.rx = s.RR.l; s.ry += 5; }
-        more = s.ry <= s.RR.b;
-        return true;
-      case P_STAR_CHK:
-        if (s.bdist > 0) {
-          s.ox = s.bx; s.oy = s.by; s.bdist = 0; s.pnr = 0; s.dist = 1; s.k = -1;
-          s.phase = P_STAR;
-        } else if (s.square) {
-          s.tx = s.bx; s.ty = s.by; s.tsad = s.best_sad;
-          s.ox = s.bx; s.oy = s.by; s.k = 0;
-          s.phase = P_SQUARE;
-        } else {
-          s.phase = P_DONE;
-        }
-        break;
-      case P_SQUARE: {
-        bool ok;
-        while (square_point(s, s.k, ok, x, y)) {
-          s.k++;
-          if (ok) {
-            pnr = s.k; pd = 1;
-            bool o2;
-            int x2, y2;
-            more = false;
-            for (int j = s.k; square_point(s, j, o2, x2, y2); j++)
-              if (o2) { more = true; break; }
-            return true;
-          }
-        }
-        s.phase = P_DONE;
-        break;
-      }
-      case P_STAR_END:
-        s.phase = P_STAR_CHK;
-        if (s.bdist == 1) {
-          s.bdist = 0;
-          if (s.pnr != 0) {
-            s.ox = s.bx; s.oy = s.by; s.opnr = s.pnr; s.k = 0;
-            s.ret = P_STAR_CHK;
-            s.phase = P_TWO;
-          }
-        }
-        break;
-      case P_FULL:   // xPatternSearch: raster order over the whole range
-        if (s.ry > s.R.b || s.R.l > s.R.r) {
-          s.phase = P_DONE;
-          break;
-        }
-        x = s.rx; y = s.ry; pnr = 0; pd = 0;
-        if (++s.rx > s.R.r) { s.rx = s.R.l; s.ry++; }
-        more = s.ry <= s.R.b;
-        return true;
-      default:
-        return false;
-    }
-  }
-  return false;
-}
 
 // Reference window of one unit at displacement (bx, by) from its origin: UH rows (FEN: even rows
 // only) of ND dwords from the aligned column, and the byte shift s0 of the first sample.
@@ -403,285 +249,6 @@ __device__ __forceinline__ uint32_t unit_part(const uint32_t (&w)[UH][UW / 4 + 1
   uint32_t part = (!kbuf && !sad_metric) ? (uint32_t)(sk2 - 2 * sop + spp) : acc;
   if (sub) part <<= 1;
   return part;
-}
-
-// Raster hand-off record (pass 1 -> pass 2), by job index: the search state when
-// xTZSearch reaches its raster (bdist is 5 from there on, the round count is no longer read).
-constexpr int kTzRec = 8;   // best_sad, bx, by, pnr, RR.l, RR.r, RR.t, RR.b
-
-// One lane: unit u of a PU of class geometry (PW x PH, units UW x UH).
-//   RASTER = false: pass 1, groups of L lanes per PU (p = the group's PU in the class).  With
-//                   ta.defer a search that reaches its raster stops there and is queued.
-//   RASTER = true:  pass 2, one queued PU per wave: its raster points are spread over the wave's
-//                   64 / L groups (their (cost, scan index) minimum is the sequential scan's best),
-//                   then every group finishes the star refinement of the same PU in lock-step.
-//   MODE 2 (chain): one job (rjid) per wave, every one of the wave's G = 64 / L groups on it: each
-//                   step takes up to G candidates the reference tests without a decision between
-//                   them (a diamond ring, the two-point pair, a stretch of the raster), group g
-//                   computes candidate g, and every lane applies xTZSearchHelp's updates in the
-//                   reference's order — the search's dependent steps shrink G-fold (k_tz_level).
-//                   pred (x, y): m_integerMv2Nx2N for a job whose ext has FME_TZ_PRED2NX2N.
-template <int UW, int UH, int MODE>
-__device__ __forceinline__ void tz_unit(const TzArgs& ta, int cls_off, int cls_cnt, int p, int u, int L, int PW,
-                                        int PH, int rjid, int pred_x = 0, int pred_y = 0) {
-  constexpr bool RASTER = MODE == 1, CHAIN = MODE == 2;
-  constexpr int KID = UW == 4 ? 0 : (UH == 4 ? 1 : 2);
-  const BatchArgs& a = ta.a;
-  const int UX = PW / UW, LR = UX * (PH / UH);
-  const bool active = p < cls_cnt;
-  if (!active) p = cls_cnt - 1;
-  const bool real = u < LR;                 // padding lanes contribute 0
-  const int uu = real ? u : 0;
-  const int ux = uu % UX, uy = uu / UX;
-
-  const int jid = (RASTER || CHAIN) ? rjid : ta.perm[cls_off + p];
-  const fme_job j = (RASTER || CHAIN) ? a.jobs[jid] : ta.sjobs[cls_off + p];
-  const fme_tz_ext e = ta.ext[jid];
-  const PicDesc ref = a.pics[j.ref_id];
-  const double ml = a.mlambda[j.lambda_id];
-  const bool kbuf = j.key_offset >= 0;
-  const bool sad_metric = PW == 12 || PW == 24 || PW == 48;
-  const bool sub = sad_metric && (a.fen == 1 || a.fen == 3) && PH > 8;
-  const int ox = (int)j.x + ux * UW, oy = (int)j.y + uy * UH;
-
-  // key of this unit in one register array: uni-pred org bytes in kk[r][0 .. UW/4) (raw; the SSE
-  // path flips them to s - 128), bi-pred int16 key pairs in kk[r][0 .. UW/2)
-  uint32_t kk[UH][UW / 2];
-  int sk2 = 0;
-  if (!kbuf) {
-    const PicDesc org = a.pics[j.org_id];
-#pragma unroll
-    for (int r = 0; r < UH; r++) {
-#pragma unroll
-      for (int c = 0; c < UW / 4; c++) {
-        const uint32_t v = gld32(org.luma + (size_t)(oy + r) * org.stride + ox + 4 * c);
-        kk[r][c] = v;
-        sk2 = dot4(v ^ 0x80808080u, v ^ 0x80808080u, sk2);
-      }
-#pragma unroll
-      for (int c = UW / 4; c < UW / 2; c++) kk[r][c] = 0;
-    }
-  } else {
-    const int16_t* kb = a.keys + (size_t)j.key_offset + (size_t)(uy * UH) * PW + ux * UW;
-#pragma unroll
-    for (int r = 0; r < UH; r++)
-#pragma unroll
-      for (int c = 0; c < UW / 2; c++)
-        kk[r][c] = (uint32_t)(uint16_t)kb[r * PW + 2 * c] | ((uint32_t)(uint16_t)kb[r * PW + 2 * c + 1] << 16);
-  }
-
-  Tz s;
-  s.best_sad = 0xFFFFFFFFu;
-  s.bx = s.by = s.bdist = s.bround = s.pnr = 0;
-  s.R = Range{j.lt_x, j.rb_x, j.lt_y, j.rb_y};
-  s.RR = s.R;
-  s.range = e.search_range ? e.search_range : 64;
-  s.k = -1; s.dist = 1; s.ox = s.oy = 0; s.opnr = 0; s.ret = P_DONE;
-  const bool defer = MODE == 0 && ta.defer;
-  s.sx = s.sy = 0; s.px = s.py = 0; s.has_pred = false;
-  s.rx = s.ry = 0;
-  s.square = ta.emi_mv != nullptr && (j.flags & FME_JOB_EMI) && !(j.flags & FME_JOB_BIPRED);
-  s.tx = s.ty = 0; s.tsad = 0;
-  constexpr int ND = UW / 4 + 1;
-  if (RASTER) {
-    const uint32_t* rec = ta.rst + (size_t)jid * kTzRec;
-    s.best_sad = rec[0];
-    s.bx = (int)rec[1]; s.by = (int)rec[2]; s.pnr = (int)rec[3];
-    s.RR = Range{(int)rec[4], (int)rec[5], (int)rec[6], (int)rec[7]};
-    s.bdist = 5;
-    s.phase = P_STAR_CHK;
-    // the raster: point i of the scan is (RR.l + 5 (i % nx), RR.t + 5 (i / nx))
-    const int nx = (s.RR.r - s.RR.l) / 5 + 1, npts = nx * ((s.RR.b - s.RR.t) / 5 + 1);
-    const int g = ((int)threadIdx.x & 63) / L, G = 64 / L;
-    uint64_t best = ~0ull;
-    for (int base = 0; base < npts; base += G) {
-      const int i = base + g;
-      const bool valid = i < npts;
-      const int iy = valid ? i / nx : 0;
-      const int cx = s.RR.l + 5 * (valid ? i - iy * nx : 0), cy = s.RR.t + 5 * iy;
-      uint32_t part = 0;
-      if (valid && real) {
-        uint32_t w[UH][ND];
-        uint32_t s0;
-        load_window<UW, UH>(w, s0, ref, ox + cx, oy + cy, sub);
-        part = unit_part<UW, UH>(w, s0, kk, sk2, kbuf, sad_metric, sub);
-      }
-      const uint32_t d = group_sum(part, L);
-      const uint32_t cost = valid ? d + mv_cost(ml, mv_bits(cx, cy, 2, j.mvp_x, j.mvp_y)) : 0xFFFFFFFFu;
-      uint64_t key = ((uint64_t)cost << 32) | (uint32_t)i;
-      for (int off = L; off < 64; off <<= 1) {
-        const uint64_t o = (uint64_t)__shfl_xor((unsigned long long)key, off, 64);
-        key = o < key ? o : key;
-      }
-      best = key < best ? key : best;
-    }
-    if (npts > 0 && (uint32_t)(best >> 32) < s.best_sad) {
-      const int bi = (int)(uint32_t)best, iy = bi / nx;
-      s.best_sad = (uint32_t)(best >> 32);
-      s.bx = s.RR.l + 5 * (bi - iy * nx);
-      s.by = s.RR.t + 5 * iy;
-      s.bround = 0;
-      s.pnr = 0;
-    }
-  } else if (j.flags & FME_JOB_BIPRED) {
-    s.phase = P_FULL;
-    s.rx = j.lt_x; s.ry = j.lt_y;
-  } else {
-    int mx = j.mvp_x, my = j.mvp_y;
-    clip_qpel(mx, my, ref.width, ref.height, e.cu_x, e.cu_y);
-    s.sx = round4(mx);
-    s.sy = round4(my);
-    s.has_pred = (e.flags & FME_TZ_PRED2NX2N) != 0;
-    int qx = (CHAIN ? pred_x : e.pred2n_x) * 4, qy = (CHAIN ? pred_y : e.pred2n_y) * 4;
-    clip_qpel(qx, qy, ref.width, ref.height, e.cu_x, e.cu_y);
-    s.px = round4(qx);
-    s.py = round4(qy);
-    s.phase = P_START;
-  }
-
-  // Up to B candidates per step: consecutive points of one list (a diamond, the two-point pair,
-  // the raster) do not depend on each other's results, so their windows are loaded together
-  // (one memory latency per batch instead of per point) and xTZSearchHelp's updates are then
-  // applied in the reference's order.
-  // Measured on the 1080p frame (tools/tz_probe.py): B = 1 at 3 waves/SIMD 20.6 ms, B = 2 29.7 ms,
-  // B = 4/6 65.9 ms — the batch's windows cost more occupancy than the saved latency is worth.
-#ifdef FME_TZ_BATCH
-  constexpr int B = FME_TZ_BATCH;
-#else
-  constexpr int B = 1;
-#endif
-  if constexpr (CHAIN) {
-    // xTZSearchHelp's updates over a batch in the reference's order keep the first strict minimum of
-    // cost = distortion + MV cost below the running best: one (cost, batch index) minimum over the
-    // groups.  A diamond ring or raster stretch is enumerated directly once the state machine has
-    // entered it (next_candidate's look-ahead per point would cost more than the loads it saves).
-    const int lane = (int)threadIdx.x & 63, g = lane / L, G = 64 / L;
-    for (int step = 0; step < (1 << 16); step++) {   // bound: a search tests < 2,000 points
-      int mx = 0, my = 0, mp = 0, md = 0, nc = 0;
-      bool more = true;
-      while (nc < G && more) {
-        if (nc > 0 && (s.phase == P_FIRST || s.phase == P_STAR) && s.k >= 0) {
-          bool ok;
-          int x, y, pnr, pd;
-          while (nc < G && diamond_point(s, s.k, ok, x, y, pnr, pd)) {
-            s.k++;
-            if (ok) {
-              if (nc == g) { mx = x; my = y; mp = pnr; md = pd; }
-              nc++;
-            }
-          }
-          break;
-        }
-        if (nc > 0 && s.phase == P_RASTER) {
-          while (nc < G && s.ry <= s.RR.b) {
-            if (nc == g) { mx = s.rx; my = s.ry; mp = 0; md = 5; }
-            nc++;
-            s.rx += 5;
-            if (s.rx > s.RR.r) { s.rx = s.RR.l; s.ry += 5; }
-          }
-          break;
-        }
-        int x, y, pnr, pd;
-        bool m = false;
-        if (!next_candidate(s, ref.width, ref.height, e.cu_x, e.cu_y, x, y, pnr, pd, m, false)) break;
-        if (nc == g) { mx = x; my = y; mp = pnr; md = pd; }
-        nc++;
-        more = m;
-      }
-      if (nc == 0) break;   // wave-uniform: one job per wave
-      uint32_t part = 0;
-      if (g < nc && real) {
-        uint32_t w[UH][ND];
-        uint32_t s0;
-        load_window<UW, UH>(w, s0, ref, ox + mx, oy + my, sub);
-        part = unit_part<UW, UH>(w, s0, kk, sk2, kbuf, sad_metric, sub);
-      }
-      const uint32_t dg = group_sum(part, L);
-      uint64_t key = ~0ull;
-      if (g < nc) key = ((uint64_t)(dg + mv_cost(ml, mv_bits(mx, my, 2, j.mvp_x, j.mvp_y))) << 32) | (uint32_t)g;
-      for (int off = L; off < 64; off <<= 1) {
-        const uint64_t o = (uint64_t)__shfl_xor((unsigned long long)key, off, 64);
-        key = o < key ? o : key;
-      }
-      const uint32_t cost = (uint32_t)(key >> 32);
-      if (cost < s.best_sad) {
-        const int wl = (int)(uint32_t)key * L;
-        s.best_sad = cost;
-        s.bx = __shfl(mx, wl, 64);
-        s.by = __shfl(my, wl, 64);
-        s.bdist = __shfl(md, wl, 64);
-        s.pnr = __shfl(mp, wl, 64);
-        s.bround = 0;
-      }
-    }
-  } else
-  for (int step = 0; step < (1 << 16); step++) {   // bound: a search tests < 2,000 points
-    int cx[B], cy[B], cp[B], cd[B];
-    int nc = 0;
-    bool more = true;
-#pragma unroll
-    for (int b = 0; b < B; b++) {
-      cx[b] = cy[b] = cp[b] = cd[b] = 0;
-      if (more) {
-        bool m = false;
-        if (next_candidate(s, ref.width, ref.height, e.cu_x, e.cu_y, cx[b], cy[b], cp[b], cd[b], m, defer)) {
-          nc = b + 1;
-          more = m;
-        } else {
-          more = false;
-        }
-      }
-    }
-    if (!__any(nc > 0 ? 1 : 0)) break;
-    if (nc == 0) continue;   // this group is done; the wave's other groups still search
-    // ---- windows of this unit at the batch's displacements: all loads in flight ----------------
-    uint32_t w[B][UH][ND];
-    uint32_t s0[B];
-#pragma unroll
-    for (int b = 0; b < B; b++) {
-      s0[b] = 0;
-      if (b < nc && real) load_window<UW, UH>(w[b], s0[b], ref, ox + cx[b], oy + cy[b], sub);
-    }
-    // ---- distortions, then xTZSearchHelp's updates in order --------------------------------------
-#pragma unroll
-    for (int b = 0; b < B; b++) {
-      if (b >= nc) break;
-      const uint32_t part = real ? unit_part<UW, UH>(w[b], s0[b], kk, sk2, kbuf, sad_metric, sub) : 0u;
-      uint32_t d = group_sum(part, L);
-      if (d < s.best_sad) {
-        d += mv_cost(ml, mv_bits(cx[b], cy[b], 2, j.mvp_x, j.mvp_y));
-        if (d < s.best_sad) {
-          s.best_sad = d;
-          s.bx = cx[b];
-          s.by = cy[b];
-          s.bdist = cd[b];
-          s.bround = 0;
-          s.pnr = cp[b];
-        }
-      }
-    }
-  }
-  if (active && u == 0 && (MODE == 0 || ((int)threadIdx.x & 63) == 0)) {
-    if (MODE == 0 && s.phase == P_DEFER) {
-      uint32_t* rec = ta.rst + (size_t)jid * kTzRec;
-      rec[0] = s.best_sad;
-      rec[1] = (uint32_t)s.bx; rec[2] = (uint32_t)s.by; rec[3] = (uint32_t)s.pnr;
-      rec[4] = (uint32_t)s.RR.l; rec[5] = (uint32_t)s.RR.r; rec[6] = (uint32_t)s.RR.t; rec[7] = (uint32_t)s.RR.b;
-      const int slot = atomicAdd(ta.rqn + KID, 1);
-      ta.rq[(size_t)KID * ta.a.n + slot] = jid;
-      return;
-    }
-    fme_job* out = ta.jobs_out + jid;
-    const int bx = s.square ? s.tx : s.bx, by = s.square ? s.ty : s.by;
-    const uint32_t bsad = s.square ? s.tsad : s.best_sad;
-    out->mv_x = (int16_t)bx;
-    out->mv_y = (int16_t)by;
-    if (ta.sad) ta.sad[jid] = bsad - mv_cost(ml, mv_bits(bx, by, 2, j.mvp_x, j.mvp_y));
-    if (ta.emi_mv) {   // the integer MV after the square step (rcMv of xTZSearch, TEncSearch.cpp:5037-5048)
-      ta.emi_mv[2 * jid] = (int16_t)s.bx;
-      ta.emi_mv[2 * jid + 1] = (int16_t)s.by;
-    }
-  }
 }
 
 // ---- wave-uniform search: one wave per PU ------------------------------------------------------
@@ -783,8 +350,16 @@ __device__ __forceinline__ void tz_wave(const TzArgs& ta, int jid, const fme_job
         kk[r][c] = (uint32_t)(uint16_t)kb[r * PW + 2 * c] | ((uint32_t)(uint16_t)kb[r * PW + 2 * c + 1] << 16);
   }
 
-  // distortion + MV cost of this group's candidate (all lanes of the group get it); ~0: not tested
-  auto cost_at = [&](int x, int y, bool v) FME_AI -> uint32_t {
+  // The backups' input path (FME_TZ_RING, Backups/4 and Backups/15 xTZSearch): every distortion
+  // xTZSearchHelp computes is pushed into array_e (Backups/4:659, 677); C = the least of the pushes
+  // before the final square (:4343-4348), and the square + ring pushes after it are the NN inputs.
+  // The bulk kernel only (one wave per PU: the slots are gathered with in-wave shuffles).
+  const bool ring = NW == 1 && ta.nn_in != nullptr && (e.flags & FME_TZ_RING) && !(j.flags & FME_JOB_BIPRED);
+  uint32_t cmin = 0xFFFFFFFFu;   // least distortion pushed so far (wave-uniform)
+
+  // distortion + MV cost of this group's candidate (all lanes of the group get it); ~0: not tested.
+  // dist: the distortion alone (~0 when not tested).
+  auto cost_at = [&](int x, int y, bool v, uint32_t& dist) FME_AI -> uint32_t {
     uint32_t part = 0;
     if (v && real) {
       uint32_t w[UH][ND];
@@ -793,7 +368,15 @@ __device__ __forceinline__ void tz_wave(const TzArgs& ta, int jid, const fme_job
       part = unit_part<UW, UH>(w, s0, kk, sk2, kbuf, sad_metric, sub);
     }
     const uint32_t d = group_sum(part, L);
+    dist = v ? d : 0xFFFFFFFFu;
     return v ? d + mv_cost(ml, mv_bits(x, y, 2, j.mvp_x, j.mvp_y)) : 0xFFFFFFFFu;
+  };
+  // the least tested distortion of a chunk into cmin (ring mode)
+  auto push_min = [&](uint32_t dist, int lim) FME_AI {
+    if (ring) {
+      const uint32_t m = (uint32_t)(wave_min_from((uint64_t)dist << 32, L, lim) >> 32);
+      cmin = m < cmin ? m : cmin;
+    }
   };
 
   Tz s;   // the wave-uniform IntTZSearchStruct and ranges (diamond_point / two_point read them)
@@ -816,9 +399,11 @@ __device__ __forceinline__ void tz_wave(const TzArgs& ta, int jid, const fme_job
       const int i = base + g;
       int x = 0, y = 0;
       const bool v = i < n && pt(i, x, y);
-      const uint32_t c = cost_at(x, y, v);
+      uint32_t dist;
+      const uint32_t c = cost_at(x, y, v, dist);
       const uint64_t key = block_min<NW>(wave_min_from(((uint64_t)c << 32) | (uint32_t)i, L, 64));
       best = key < best ? key : best;
+      push_min(dist, 64);
     }
     return best;
   };
@@ -871,15 +456,19 @@ __device__ __forceinline__ void tz_wave(const TzArgs& ta, int jid, const fme_job
     clip_qpel(qx, qy, ref.width, ref.height, e.cu_x, e.cu_y);
     const int px = round4(qx), py = round4(qy);
     {
-      uint32_t c3[3] = {0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu};
+      uint32_t c3[3] = {0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu}, d3[3] = {0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu};
       for (int base = 0; base < 3; base += G) {
         const int i = base + g;
         const int x = i == 0 ? sx : (i == 1 ? 0 : px), y = i == 0 ? sy : (i == 1 ? 0 : py);
-        const uint32_t c = cost_at(x, y, i < 3);
+        uint32_t dist;
+        const uint32_t c = cost_at(x, y, i < 3, dist);
         if constexpr (NW == 1) {
 #pragma unroll
           for (int q = 0; q < 3; q++)
-            if (q >= base && q < base + G) c3[q] = __shfl(c, (q - base) * L, 64);
+            if (q >= base && q < base + G) {
+              c3[q] = __shfl(c, (q - base) * L, 64);
+              d3[q] = __shfl(dist, (q - base) * L, 64);
+            }
         } else {   // G >= 3 with several waves: the three costs through LDS
           __shared__ uint32_t s_c3[3];
           if (i < 3 && u == 0) s_c3[i] = c;
@@ -887,11 +476,19 @@ __device__ __forceinline__ void tz_wave(const TzArgs& ta, int jid, const fme_job
 #pragma unroll
           for (int q = 0; q < 3; q++) c3[q] = s_c3[q];
           __syncthreads();
+          (void)dist;
         }
       }
       take(c3[0], sx, sy, 0, 0);
-      if (sx != 0 || sy != 0) take(c3[1], 0, 0, 0, 0);
-      if (has_pred && (sx != px || sy != py) && (px != s.bx || py != s.by)) take(c3[2], px, py, 0, 0);
+      cmin = d3[0];
+      if (sx != 0 || sy != 0) {
+        take(c3[1], 0, 0, 0, 0);
+        cmin = d3[1] < cmin ? d3[1] : cmin;
+      }
+      if (has_pred && (sx != px || sy != py) && (px != s.bx || py != s.by)) {
+        take(c3[2], px, py, 0, 0);
+        cmin = d3[2] < cmin ? d3[2] : cmin;
+      }
     }
     if (has_pred) {   // xSetSearchRange(currBest << 2, m_iSearchRange): the raster's range
       int cx = s.bx * 4, cy = s.by * 4;
@@ -923,22 +520,33 @@ __device__ __forceinline__ void tz_wave(const TzArgs& ta, int jid, const fme_job
       s.ox = s.bx; s.oy = s.by;
       const int nslot = 16 * nr, seg = 16 * L < 64 ? 16 * L : 64;
       uint64_t rmin = ~0ull;   // running minimum of the ring being completed (G < 16)
+      uint32_t rdmin = 0xFFFFFFFFu;   // its least distortion (ring mode)
       bool stop = false;
       for (int base = 0; base < nslot && !stop; base += G) {
         const int i = base + g;
         int x = 0, y = 0, pnr = 0, pd = 0;
         const bool v = i < nslot && ring_pt(i, x, y, pnr, pd);
-        const uint32_t c = cost_at(x, y, v);
+        uint32_t dist;
+        const uint32_t c = cost_at(x, y, v, dist);
         const uint64_t key = wave_min_from(((uint64_t)c << 32) | (uint32_t)i, L, seg);
+        // per-ring least distortion (rings after the stop are evaluated here but not tested by the
+        // reference, so they must not reach C)
+        const uint32_t dseg = ring ? (uint32_t)(wave_min_from((uint64_t)dist << 32, L, seg) >> 32) : 0u;
         // rings completed by this chunk, in order
         const int r0 = base >> 4, r1 = (base + G) >> 4;   // rings [r0, r1) end inside this chunk
         if (G < 16) {
           rmin = key < rmin ? key : rmin;
+          rdmin = dseg < rdmin ? dseg : rdmin;
           if (((base + G) & 15) != 0) continue;
         }
         for (int r = r0; r < r1 && r < nr; r++) {
           uint64_t k = G < 16 ? rmin : (uint64_t)__shfl((unsigned long long)key, ((r * 16 - base) * L) & 63, 64);
+          if (ring) {
+            const uint32_t dr = G < 16 ? rdmin : (uint32_t)__shfl(dseg, ((r * 16 - base) * L) & 63, 64);
+            cmin = dr < cmin ? dr : cmin;
+          }
           rmin = ~0ull;
+          rdmin = 0xFFFFFFFFu;
           s.bround += 1;
           if ((uint32_t)(k >> 32) < s.best_sad) {
             int xx, yy, pn, pdd;
@@ -991,6 +599,7 @@ __device__ __forceinline__ void tz_wave(const TzArgs& ta, int jid, const fme_job
   const bool square = ta.emi_mv != nullptr && (j.flags & FME_JOB_EMI) && !(j.flags & FME_JOB_BIPRED);
   const int tx = s.bx, ty = s.by;
   const uint32_t tsad = s.best_sad;
+  const uint32_t c_tz = cmin;   // C: the pushes before index_ref
   if (square) {
     s.ox = s.bx; s.oy = s.by;
     const uint64_t k = list_min(8, [&](int i, int& x, int& y) FME_AI {
@@ -1004,66 +613,71 @@ __device__ __forceinline__ void tz_wave(const TzArgs& ta, int jid, const fme_job
       take((uint32_t)(k >> 32), x, y, 1, (int)(uint32_t)k + 1);
     }
   }
+  // ---- the backups' tail (FME_TZ_RING): xTZ8PointSquareSearch at distance 1 and
+  // xTZ8PointSquareSearch2 at distance 2 around the star best (Backups/4:4868-4878, 818-873,
+  // 876-965), every distortion pushed; rcMv moves with their xTZSearchHelp updates ---------------
+  uint32_t eslot[8] = {0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u};   // array_e[index_ref + k] (0: never pushed)
+  if (ring) {
+    s.ox = s.bx; s.oy = s.by;
+    // the 24 points in call order; bit i of `okm`: point i passes the reference's range checks
+    uint32_t okm = 0;
+#pragma unroll
+    for (int i = 0; i < 24; i++) {
+      bool ok;
+      int x, y;
+      ring_square_point(s, i, ok, x, y);
+      okm |= ok ? (1u << i) : 0u;
+    }
+    uint64_t best = ~0ull;
+    for (int base = 0; base < 24; base += G) {
+      const int i = base + g;
+      int x = 0, y = 0;
+      bool ok = false;
+      if (i < 24) ring_square_point(s, i, ok, x, y);
+      uint32_t dist;
+      const uint32_t c = cost_at(x, y, ok, dist);
+      const uint64_t key = wave_min_from(((uint64_t)c << 32) | (uint32_t)i, L, 64);
+      best = key < best ? key : best;
+      // slot k = the k-th pushed point: its group's distortion
+      uint32_t m = okm;
+#pragma unroll
+      for (int k = 0; k < 8; k++) {
+        const int idx = m ? __builtin_ctz(m) : 32;
+        m &= m ? m - 1 : 0u;
+        if (idx >= base && idx < base + G) eslot[k] = (uint32_t)__shfl((int)dist, ((idx - base) * L) & 63, 64);
+      }
+    }
+    if ((uint32_t)(best >> 32) < s.best_sad) {
+      int x, y;
+      bool ok;
+      ring_square_point(s, (int)(uint32_t)best, ok, x, y);
+      take((uint32_t)(best >> 32), x, y, 0, 0);
+    }
+  }
   if ((NW == 1 ? lane : (int)threadIdx.x) == 0) {   // one writer per PU (NW = 1: per wave)
     fme_job* out = ta.jobs_out + jid;
-    out->mv_x = (int16_t)tx;
-    out->mv_y = (int16_t)ty;
-    if (ta.sad) ta.sad[jid] = tsad - mv_cost(ml, mv_bits(tx, ty, 2, j.mvp_x, j.mvp_y));
+    // ring mode: rcMv after the ring (Backups/4:4881-4882); otherwise the TZ best before the square
+    const int bx = ring ? s.bx : tx, by = ring ? s.by : ty;
+    const uint32_t bsad = ring ? s.best_sad : tsad;
+    out->mv_x = (int16_t)bx;
+    out->mv_y = (int16_t)by;
+    if (ta.sad) ta.sad[jid] = bsad - mv_cost(ml, mv_bits(bx, by, 2, j.mvp_x, j.mvp_y));
     if (ta.emi_mv) {   // the integer MV after the square step (rcMv of xTZSearch, TEncSearch.cpp:5037-5048)
       ta.emi_mv[2 * jid] = (int16_t)s.bx;
       ta.emi_mv[2 * jid + 1] = (int16_t)s.by;
     }
+    if (ring) {   // U1 V1 U2 H1 H2 U3 V2 U4 = array_e[index_ref .. +7], then C (Backups/4:4343-4359)
+      uint32_t* o = ta.nn_in + (size_t)9 * jid;
+#pragma unroll
+      for (int k = 0; k < 8; k++) o[k] = eslot[k];
+      o[8] = c_tz;
+    }
   }
 }
 
-__device__ __forceinline__ int xcd_block(int r, int n) {
-  const int k = r & 7;
-  return k * (n >> 3) + min(k, n & 7) + (r >> 3);
-}
-
-#ifndef FME_TZ_WAVES
-#define FME_TZ_WAVES 3   // occupancy target: 3 waves/SIMD (<= 168 VGPRs) measured best (1: 23.5, 4: 26.3 ms)
-#endif
 __constant__ int kTzW[kNumClasses] = {4, 8, 8, 4, 16, 8, 16, 12, 16, 16, 8, 32, 16, 32, 24, 32, 32, 16, 64, 32, 64, 48, 64, 64};
 __constant__ int kTzH[kNumClasses] = {8, 4, 8, 16, 4, 16, 8, 16, 12, 16, 32, 8, 32, 16, 32, 24, 32, 64, 16, 64, 32, 64, 48, 64};
 
-__device__ __forceinline__ int tz_group_lanes(int PW, int PH, int UW, int UH) {
-  const int LR = (PW / UW) * (PH / UH);
-  int L = 1;
-  while (L < LR) L <<= 1;
-  return L;
-}
-
-// pass 1: the class's PUs in groups of L lanes, blocks dealt to the XCDs in contiguous ranges
-template <int UW, int UH>
-__global__ __launch_bounds__(kTzNT) __attribute__((amdgpu_waves_per_eu(FME_TZ_WAVES)))
-void k_tz(TzArgs ta, TzSchedule sc, int kid) {
-  const int b = blockIdx.x;
-  int c = 0;
-  while (c < kNumClasses - 1 && b >= sc.prefix[kid][c + 1]) c++;
-  const int nblk = sc.prefix[kid][c + 1] - sc.prefix[kid][c];
-  const int blk = xcd_block(b - sc.prefix[kid][c], nblk);
-  const int PW = kTzW[c], PH = kTzH[c];
-  const int L = tz_group_lanes(PW, PH, UW, UH);
-  const int gl = blk * kTzNT + (int)threadIdx.x;
-  const int p = gl / L;
-  tz_unit<UW, UH, 0>(ta, sc.class_off[c], sc.class_cnt[c], p, gl - p * L, L, PW, PH, 0);
-}
-
-// pass 2: one queued PU (job index) per wave
-#ifndef FME_TZR_WAVES
-#define FME_TZR_WAVES FME_TZ_WAVES
-#endif
-template <int UW, int UH>
-__global__ __launch_bounds__(kTzNT) __attribute__((amdgpu_waves_per_eu(FME_TZR_WAVES)))
-void k_tz_raster(TzArgs ta, TzSchedule sc, int kid, int nq) {
-  const int wv = (int)(blockIdx.x * (kTzNT / 64) + (threadIdx.x >> 6));
-  if (wv >= nq) return;
-  const int jid = ta.rq[(size_t)kid * ta.a.n + wv];
-  const int PW = ta.a.jobs[jid].w, PH = ta.a.jobs[jid].h;   // validated by k_classify
-  const int L = tz_group_lanes(PW, PH, UW, UH);
-  tz_unit<UW, UH, 1>(ta, 0, 1, 0, (int)(threadIdx.x & 63) & (L - 1), L, PW, PH, jid);
-}
 
 // Wave-uniform bulk search: one wave per PU of the kernel's unit shape, PUs in class order (CTU
 // order inside a class); blocks dealt to the XCDs in contiguous ranges so each L2 sees one band.
@@ -1106,7 +720,7 @@ void k_tz_wave(TzArgs ta, TzSchedule sc, int kid) {
 #define FME_TZL_WAVES 1   // waves per chain job (A/B: 8 waves 276 ms per P frame, spilling; 1 wave 198 ms)
 #endif
 __global__ __launch_bounds__(64 * FME_TZL_WAVES) void k_tz_level(TzArgs ta, TzChain ch, int first) {
-  const int q = first + (int)blockIdx.x, lane = (int)threadIdx.x;
+  const int q = first + (int)blockIdx.x;
   const int PW = ta.a.jobs[q].w, PH = ta.a.jobs[q].h;   // shapes checked by the host
   const int ps = ch.psrc[q];
   const int px = ps >= 0 ? ta.emi_mv[2 * ps] : ta.ext[q].pred2n_x;
@@ -1143,17 +757,6 @@ int tz_lanes_per_pu(int cls) {
   return l;
 }
 
-// One unit-shape kernel (kid 0: 4x8 units, 1: 8x4, 2: 8x8); the three are independent and the
-// runtime runs them on separate streams.
-hipError_t launch_tz(const TzArgs& ta, const TzSchedule& sc, int kid, hipStream_t s) {
-  const int blocks = sc.prefix[kid][kNumClasses];
-  if (blocks <= 0) return hipSuccess;
-  if (kid == 0) hipLaunchKernelGGL((k_tz<4, 8>), dim3(blocks), dim3(kTzNT), 0, s, ta, sc, 0);
-  else if (kid == 1) hipLaunchKernelGGL((k_tz<8, 4>), dim3(blocks), dim3(kTzNT), 0, s, ta, sc, 1);
-  else hipLaunchKernelGGL((k_tz<8, 8>), dim3(blocks), dim3(kTzNT), 0, s, ta, sc, 2);
-  return hipGetLastError();
-}
-
 // Wave-uniform bulk search of kernel kid: sc.prefix in waves (one per PU).
 hipError_t launch_tz_wave(const TzArgs& ta, const TzSchedule& sc, int kid, hipStream_t s) {
   int share = 0;   // the largest per-XCD share of this kernel's PUs (waves)
@@ -1172,14 +775,5 @@ hipError_t launch_tz_wave(const TzArgs& ta, const TzSchedule& sc, int kid, hipSt
   return hipGetLastError();
 }
 
-// The raster searches pass 1 queued for kernel kid (nq of them, read back by the host).
-hipError_t launch_tz_raster(const TzArgs& ta, const TzSchedule& sc, int kid, int nq, hipStream_t s) {
-  if (nq <= 0) return hipSuccess;
-  const int blocks = (nq + kTzNT / 64 - 1) / (kTzNT / 64);
-  if (kid == 0) hipLaunchKernelGGL((k_tz_raster<4, 8>), dim3(blocks), dim3(kTzNT), 0, s, ta, sc, 0, nq);
-  else if (kid == 1) hipLaunchKernelGGL((k_tz_raster<8, 4>), dim3(blocks), dim3(kTzNT), 0, s, ta, sc, 1, nq);
-  else hipLaunchKernelGGL((k_tz_raster<8, 8>), dim3(blocks), dim3(kTzNT), 0, s, ta, sc, 2, nq);
-  return hipGetLastError();
-}
 
 }  // namespace fme

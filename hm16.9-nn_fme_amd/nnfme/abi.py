@@ -68,6 +68,7 @@ TZ_EXT_DTYPE = np.dtype(
 )
 assert TZ_EXT_DTYPE.itemsize == 12
 TZ_PRED2NX2N = 0x01
+TZ_RING = 0x02          # the backups' xTZSearch tail (fme_integer_search_ring)
 
 # fme_pu_req (64 B) / fme_pu_res (80 B): predInterSearch's P-slice PU / reference loop (include/fme.h)
 MAX_REFS = 4
@@ -149,6 +150,7 @@ CONFIG_FIELDS = ("bit_depth", "use_hadamard", "nn_mode", "qp", "fast_inter_mode"
 JOB_EMI = 0x01
 JOB_BIPRED = 0x02
 JOB_LOSSLESS = 0x04
+JOB_NN_IN = 0x08        # NN inputs from the bound row (the backups' input path)
 
 RES_NN_STALE = 0x01
 RES_NN_UNINIT = 0x02

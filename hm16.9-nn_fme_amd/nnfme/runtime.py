@@ -15,7 +15,7 @@ from .weights import load_weights
 PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB_PATH = os.environ.get("FME_LIB_PATH") or os.path.join(PKG_ROOT, "libfme_amd.so")
 
-ABI_VERSION = 10
+ABI_VERSION = 11
 TIMING_NAMES = ("classify", "scatter", "search", "nn_tail", "batch", "search_main", "search_aux")
 
 # Every entry point include/fme.h declares (the ABI test checks the .so exports them).
@@ -32,6 +32,7 @@ ABI_SYMBOLS = (
     "fme_set_nn_engine", "fme_set_nn_margin_output", "fme_refine_mv", "fme_refine_mv_device",
     "fme_refine_status", "fme_nn_copy_state_device", "fme_template_costs", "fme_pred_inter_b", "fme_build_bipred_keys",
     "fme_set_search_event", "fme_build_bipred_keys_device", "fme_set_nn_logit_output",
+    "fme_set_nn_inputs", "fme_integer_search_ring", "fme_integer_search_ring_device",
 )
 
 
@@ -106,6 +107,9 @@ def load_library(path=None):
         "fme_pred_inter_b": (I, [P, P, P, I, P]),
         "fme_build_bipred_keys": (I, [P, P, I, C.c_size_t, P]),
         "fme_build_bipred_keys_device": (I, [P, P, I, C.c_size_t, P]),
+        "fme_set_nn_inputs": (I, [P, P, I]),
+        "fme_integer_search_ring": (I, [P, P, P, P, P, I, P]),
+        "fme_integer_search_ring_device": (I, [P, P, P, P, P, I, P]),
     }
     # an explicitly named library is an A/B variant (tools/ab_bench.py): possibly an older ABI
     strict = os.path.abspath(path) == os.path.abspath(LIB_PATH)
@@ -115,8 +119,13 @@ def load_library(path=None):
             continue
         f.restype = res
         f.argtypes = args
-    if strict and lib.fme_abi_version() != ABI_VERSION:
+    abi = lib.fme_abi_version()
+    if strict and abi != ABI_VERSION:
         raise FmeError(-1, "ABI version mismatch")
+    if abi != ABI_VERSION:   # an A/B variant: say so, and FmeContext refuses what it cannot honour
+        import warnings
+        warnings.warn(f"{path}: ABI {abi}, this binding is ABI {ABI_VERSION}")
+    lib.fme_abi = abi
     _libs[path] = lib
     return lib
 
@@ -192,6 +201,28 @@ class FmeContext:
         sad = np.zeros(len(jobs), np.uint32)
         _check(self.lib, self.lib.fme_integer_search(self.h, _ptr(jobs), _ptr(ext), _ptr(sad), len(jobs), stream))
         return jobs, sad
+
+    def integer_search_ring(self, jobs, ext, stream=None):
+        """fme_integer_search_ring: FME_TZ_RING jobs run the backups' xTZSearch tail (square + ring,
+        every distortion pushed); returns (jobs, sad, nn_in[n][9] = array_e[index_ref..+7], C)."""
+        from .abi import TZ_EXT_DTYPE
+        jobs = np.array(jobs, dtype=JOB_DTYPE, copy=True)
+        ext = np.ascontiguousarray(ext, dtype=TZ_EXT_DTYPE)
+        sad = np.zeros(len(jobs), np.uint32)
+        nn_in = np.zeros((len(jobs), 9), np.uint32)
+        _check(self.lib, self.lib.fme_integer_search_ring(self.h, _ptr(jobs), _ptr(ext), _ptr(sad), _ptr(nn_in),
+                                                          len(jobs), stream))
+        return jobs, sad, nn_in
+
+    def integer_search_ring_device(self, d_jobs, d_ext, d_sad, d_nn_in, n, stream=None):
+        _check(self.lib, self.lib.fme_integer_search_ring_device(self.h, C.c_void_p(d_jobs), C.c_void_p(d_ext),
+                                                                 C.c_void_p(d_sad), C.c_void_p(d_nn_in), n, stream))
+
+    def set_nn_inputs(self, d_ptr, capacity=0):
+        """Bind the device rows (uint32 [capacity][9]) FME_JOB_NN_IN jobs read their NN inputs from
+        (fme_set_nn_inputs); 0 / None unbinds."""
+        _check(self.lib, self.lib.fme_set_nn_inputs(self.h, C.c_void_p(d_ptr) if d_ptr else None,
+                                                    int(capacity) if d_ptr else 0))
 
     def integer_search_device(self, d_jobs, d_ext, d_sad, n, stream=None):
         _check(self.lib, self.lib.fme_integer_search_device(self.h, C.c_void_p(d_jobs), C.c_void_p(d_ext),
@@ -293,6 +324,12 @@ class FmeContext:
 
     def load_nn_net(self, net):
         """A generic NN_pred net (nnfme.weights.NnNet) for nn_mode 2 (fme_load_nn_net)."""
+        # input flags need ABI 10 (FME_NN_IN_SLOT_RESET) / 11 (FME_NN_IN_TZ_RING): an older A/B
+        # variant would ignore them and run a different input path without a word
+        need = 11 if net.input_flags & 2 else (10 if net.input_flags else 0)
+        if getattr(self.lib, "fme_abi", ABI_VERSION) < need:
+            raise FmeError(-1, f"net input flags 0x{net.input_flags:x} need ABI {need}, library has "
+                               f"{self.lib.fme_abi}")
         d = net.desc_struct()
         p = np.ascontiguousarray(net.params, dtype=np.float64)
         _check(self.lib, self.lib.fme_load_nn_net(self.h, C.byref(d), _ptr(p), p.size))

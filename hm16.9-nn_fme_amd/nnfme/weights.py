@@ -152,6 +152,7 @@ F32, F64 = 0, 1
 EMB_NONE, EMB_MASTER, EMB_SWAP = 0, 1, 2
 OUT_LINEAR, OUT_SIGMOID = 0, 1
 SLOT_RESET = 1   # FME_NN_IN_SLOT_RESET
+TZ_RING = 2      # FME_NN_IN_TZ_RING: the backups' own input path (FME_JOB_NN_IN rows)
 NET_FILES = {"scr3x40": "nn3x40_scr.nnd", "blowing4x40": "nn4x40_qp22.nnd"}
 
 
@@ -248,7 +249,8 @@ def master_net(qp=22):
 
 def case_net(name):
     """Nets named by fixtures and bench workloads: an .nnd blob (NET_FILES key), "<name>+rezero" =
-    that net with carry_hidden cleared, "master" = the shipped QP22 2-layer net, generic layout."""
+    that net with carry_hidden cleared, "+slotreset" / "+tzring" = with FME_NN_IN_SLOT_RESET /
+    FME_NN_IN_TZ_RING, "master" = the shipped QP22 2-layer net, generic layout."""
     if name == "master":
         return master_net(22)
     base, *mods = str(name).split("+")
@@ -258,6 +260,8 @@ def case_net(name):
             net = net.with_carry(0)
         elif mod == "slotreset":
             net = net.with_input_flags(SLOT_RESET)
+        elif mod == "tzring":
+            net = net.with_input_flags(TZ_RING)
         else:
             raise ValueError(f"unknown net modifier {mod!r} in {name!r}")
     return net

@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define FME_ABI_VERSION 10
+#define FME_ABI_VERSION 11
 
 /* ---- error codes ---------------------------------------------------------------- */
 #define FME_OK            0
@@ -77,6 +77,10 @@ typedef struct fme_config {
 #define FME_JOB_EMI       0x01u  /* run the EMI square step (uni-pred TZ path)           */
 #define FME_JOB_BIPRED    0x02u  /* bi-pred iteration: weight 0.5 in the cost tail        */
 #define FME_JOB_LOSSLESS  0x04u  /* CU transquant bypass: SAD instead of SATD            */
+#define FME_JOB_NN_IN     0x08u  /* the backups' input path (nn_mode 2, FME_NN_IN_TZ_RING):
+                                    no EMI step here - mv is the integer search's final MV
+                                    (after its square + ring, FME_TZ_RING) and the NN inputs
+                                    are row i of the array bound with fme_set_nn_inputs     */
 
 typedef struct fme_job {
   uint16_t x, y;
@@ -180,22 +184,25 @@ int fme_load_nn_weights(fme_ctx* ctx, const float* params, int count);
  * nn_mode 2 runs a net loaded with fme_load_nn_net in NN_pred()'s place, with the same inputs
  * (array_e slots, C, PUHeight, PUWidth carried across calls exactly as in nn_mode 1) and the same
  * class -> MV offset switch.
- * INPUT PATH - a deliberate deviation from the backups: the inputs are the master's EMI step (the
- * SSE square at distance 1 around the TZ MV, TEncSearch.cpp:1324-1377 with save = true; C = its
- * best SSE).  The backups build theirs differently - every xTZSearchHelp distortion is pushed
- * (Backups/4:659-682), C is the minimum over every point xTZSearch tested (:4343-4348), U1..U4 are
- * array_e[index_ref..+7], and a second ring at distance 2 (xTZ8PointSquareSearch2, :4873-4878)
- * can move the integer MV.  That input path is not restated: the backups' nets run here on the
- * master's input distribution, and parity with the backups holds for the forward pass and the
- * per-call slot reset only (configs[4] input parity is unpinned).
- * input_flags FME_NN_IN_SLOT_RESET: the array_e slots a call's own EMI step did not push read 0,
- * as after the backups' per-call memset (Backups/4:4421-4422, Backups/15:4961-4962); C and the PU
- * size stay carried (the backups never clear them).  Without it the slots carry as in nn_mode 1.  The shape follows the reference's deeper nets:
- *   Backups/4 "SCR 3 layers" (9 -> 40 -> 40 -> 40 -> 49, double, sigmoid output,
- *     TEncSearch - SCR 3 layers - no normalization.cpp:57-299, forward :4427-4480),
- *   Backups/15 "blowing 4 lyrs qp 22" (17 -> 4 x 40 -> 49, float, H-embedding rows 12->3, 16->4,
- *     TEncSearch - blowing - 4 lyrs qp 22.cpp:57-75, 849-1160, forward :4954-5052),
- *   and the master net itself (17 -> 22 -> 20 -> 49, float).
+ * INPUT PATHS.  Without input flags a deeper net sees the master's EMI step (the SSE square at
+ * distance 1 around the TZ MV, TEncSearch.cpp:1324-1377 with save = true; C = its best SSE) with
+ * the slots carried as in nn_mode 1.
+ * input_flags FME_NN_IN_TZ_RING: the backups' own input path.  Both backups push EVERY
+ * xTZSearchHelp distortion into array_e (Backups/4:659, Backups/15:1257), end xTZSearch with
+ * xTZ8PointSquareSearch at distance 1 and xTZ8PointSquareSearch2 at distance 2 around the star best
+ * (Backups/4:4868-4878, 818-965; their updates move rcMv), and build NN_pred's inputs in
+ * xPatternSearchFast (Backups/4:4343-4359, Backups/15:4935-4951): C = the least distortion pushed
+ * before the square (index_ref), U1 V1 U2 H1 H2 U3 V2 U4 = array_e[index_ref .. index_ref + 7], then
+ * memset(array_e) (Backups/4:4421-4422, Backups/15:4961-4962).  Here fme_integer_search_ring
+ * (FME_TZ_RING jobs) runs that xTZSearch and writes the nine inputs per job; fme_refine takes them
+ * for FME_JOB_NN_IN jobs from the array bound with fme_set_nn_inputs.  Bi-pred calls never run
+ * xPatternSearchFast in the backups, so they reuse the last uni-pred call's class (MVX_HALF ..
+ * MVY_QRTER are globals): a job without FME_JOB_NN_IN reads the carried inputs of the last
+ * FME_JOB_NN_IN job (its whole row: all 8 slots, C, PU size), which gives that class.  Not
+ * combinable with FME_NN_IN_SLOT_RESET or carry_hidden (FME_E_INVALID).
+ * input_flags FME_NN_IN_SLOT_RESET (master inputs): the array_e slots a call's own EMI step did not
+ * push read 0, as after the backups' per-call memset; C and the PU size stay carried.  The shape
+ * follows the reference's deeper nets:
  * Per call: x = ((double|float)raw - mean) / stdev * gamma_in for raw = e0,e1,e2,e3,C,e4,e5,e6,e7;
  * IN = [emb0[rowH] | emb1[rowW] | x] (embedding != NONE) or x; per hidden layer
  * X[i] = relu(sum_k W[i][k] * IN[k] + b[i]) * gamma[i] + beta[i], summed k = 0.. in order with a
@@ -230,6 +237,13 @@ typedef struct fme_nn_net {
   uint32_t input_flags;                 /* FME_NN_IN_*                                           */
 } fme_nn_net;   /* 40 bytes */
 #define FME_NN_IN_SLOT_RESET 1u         /* array_e slots not pushed by this call read 0           */
+#define FME_NN_IN_TZ_RING    2u         /* the backups' input path (FME_JOB_NN_IN rows)           */
+
+/* The NN input rows of FME_JOB_NN_IN jobs: a device array of `capacity` rows of 9 uint32 (array_e
+ * slots 0..7, C), row i for job i of a batch; written by fme_integer_search_ring(_device) for its
+ * FME_TZ_RING jobs.  A batch with an FME_JOB_NN_IN job beyond the capacity, or with none bound, is
+ * rejected (FME_E_INVALID on the host path, FME_RES_REJECTED on the device path).  NULL unbinds.  */
+int fme_set_nn_inputs(fme_ctx* ctx, const uint32_t* d_rows, int capacity);
 
 /* Number of parameters of `net`, or a negative FME_E_* code for an invalid descriptor. */
 int fme_nn_param_count(const fme_nn_net* net);
@@ -310,6 +324,10 @@ int fme_refine_status(fme_ctx* ctx);
  * subsampling) plus the MV cost at cost scale 2.  On return job.mv_x/mv_y hold the integer MV
  * (ready for fme_refine) and sad[i] = ruiSAD (distortion at that MV).                             */
 #define FME_TZ_PRED2NX2N 0x01u
+#define FME_TZ_RING      0x02u   /* the backups' xTZSearch tail: square (distance 1) + ring (distance 2),
+                                    every distortion pushed (fme_integer_search_ring; see
+                                    FME_NN_IN_TZ_RING): job.mv_x/mv_y and sad[i] are then the MV
+                                    after the ring, and its nine NN inputs are written            */
 
 typedef struct fme_tz_ext {
   uint16_t cu_x, cu_y;          /* luma origin of the PU's CU (TComDataCU::clipMv)              */
@@ -323,6 +341,13 @@ int fme_integer_search(fme_ctx* ctx, fme_job* jobs, const fme_tz_ext* ext, uint3
                        void* stream);
 int fme_integer_search_device(fme_ctx* ctx, fme_job* d_jobs, const fme_tz_ext* d_ext, uint32_t* d_sad,
                               int n, void* stream);
+/* The same searches with the NN inputs of their FME_TZ_RING jobs: nn_in[9 i .. 9 i + 8] =
+ * array_e[index_ref .. index_ref + 7] (0 where fewer were pushed), C (host arrays / device arrays;
+ * rows of other jobs are left untouched).  Uni-pred bulk searches only (not the producers).       */
+int fme_integer_search_ring(fme_ctx* ctx, fme_job* jobs, const fme_tz_ext* ext, uint32_t* sad,
+                            uint32_t* nn_in, int n, void* stream);
+int fme_integer_search_ring_device(fme_ctx* ctx, fme_job* d_jobs, const fme_tz_ext* d_ext,
+                                   uint32_t* d_sad, uint32_t* d_nn_in, int n, void* stream);
 /* With profiling on: device milliseconds of the last integer-search launches; waits for them. */
 int fme_integer_search_last_ms(fme_ctx* ctx, float* ms);
 

@@ -364,7 +364,9 @@ int orc_nn_param_count(const fme_nn_net* d) {
   if (d->embedding < FME_NN_EMB_NONE || d->embedding > FME_NN_EMB_SWAP) return FME_E_INVALID;
   if (d->out_act != FME_NN_OUT_LINEAR && d->out_act != FME_NN_OUT_SIGMOID) return FME_E_INVALID;
   if (d->carry_hidden >> d->n_hidden) return FME_E_INVALID;
-  if (d->input_flags & ~FME_NN_IN_SLOT_RESET) return FME_E_INVALID;
+  if (d->input_flags & ~(FME_NN_IN_SLOT_RESET | FME_NN_IN_TZ_RING)) return FME_E_INVALID;
+  if ((d->input_flags & FME_NN_IN_TZ_RING) && ((d->input_flags & FME_NN_IN_SLOT_RESET) || d->carry_hidden))
+    return FME_E_INVALID;
   int n = d->embedding ? 64 : 0, in = d->embedding ? 17 : 9;
   for (int l = 0; l < d->n_hidden; l++) {
     const int w = d->width[l];
@@ -483,6 +485,10 @@ void orc_set_lambda(orc_ctx* ctx, int id, double lambda) {
   ctx->mlambda[id] = 65536.0 * sq + 0;
 }
 void orc_set_motion_lambda(orc_ctx* ctx, int id, double ml) { ctx->mlambda[id] = ml; }
+void orc_set_nn_inputs(orc_ctx* ctx, const uint32_t* rows, int n) {
+  ctx->nn_in = rows;
+  ctx->nn_in_n = rows ? n : 0;
+}
 void orc_set_keys(orc_ctx* ctx, const int16_t* keys, size_t n) {
   ctx->keys = keys;
   ctx->n_keys = n;
@@ -546,7 +552,20 @@ int orc_refine(orc_ctx* ctx, const fme_job* jobs, fme_result* res, int n) {
     int mvx = j->mv_x, mvy = j->mv_y;
     uint32_t c = 0;
     int n_emi = 0;
-    if (j->flags & FME_JOB_EMI) {
+    if (j->flags & FME_JOB_NN_IN) {
+      /* the backups' input path: the row the integer search wrote (FME_TZ_RING), array_e's
+       * slots after the per-call memset (Backups/4:4343-4359, 4421-4422) */
+      if (!ctx->nn_in || i >= ctx->nn_in_n) { free(key); return FME_E_INVALID; }
+      const uint32_t* row = ctx->nn_in + (size_t)9 * i;
+      n_emi = 8;
+      for (int s = 0; s < 8; s++) r->emi[s] = row[s];
+      c = row[8];
+      for (int s = 0; s < 8; s++) ctx->nn_state.slot[s] = r->emi[s];
+      ctx->nn_state.c = c;
+      ctx->nn_state.pu_h = (uint32_t)h;
+      ctx->nn_state.pu_w = (uint32_t)w;
+      ctx->nn_state.written |= 0x1FFu;
+    } else if (j->flags & FME_JOB_EMI) {
       n_emi = orc_emi(ref, key, w, j->x, j->y, w, h, j->mv_x, j->mv_y, j->mvp_x, j->mvp_y,
                       j->lt_x, j->lt_y, j->rb_x, j->rb_y, ml, ctx->cfg.fast_inter_mode, r->emi,
                       &mvx, &mvy, &c);
@@ -580,7 +599,7 @@ int orc_refine(orc_ctx* ctx, const fme_job* jobs, fme_result* res, int n) {
                     ? orc_nn_net_forward(ctx, e, st->c, (int)st->pu_h, (int)st->pu_w, NULL)
                     : orc_nn_forward(ctx->nn, st->slot, st->c, (int)st->pu_h, (int)st->pu_w, NULL);
       r->nn_class = (uint8_t)cls;
-      if (n_emi < 8 || !(j->flags & FME_JOB_EMI)) r->status |= FME_RES_NN_STALE;
+      if (n_emi < 8 || !(j->flags & (FME_JOB_EMI | FME_JOB_NN_IN))) r->status |= FME_RES_NN_STALE;
       if ((st->written & 0x1FFu) != 0x1FFu) r->status |= FME_RES_NN_UNINIT;
       /* class -> (MVX_HALF<<1)+MVX_QRTER, (MVY_HALF<<1)+MVY_QRTER: (cls%7-3, cls/7-3),
        * the switch of TEncSearch.cpp:136-193. */
@@ -776,6 +795,10 @@ typedef struct tz_state {
   int16_t* cur;
   uint32_t best_sad;
   int best_x, best_y, best_dist, best_round, point_nr;
+  /* the backups' array_e (FME_TZ_RING): pushes before index_ref feed C (their minimum), the first
+   * eight after it are the NN inputs */
+  int ring, after, npush;
+  uint32_t cmin, e[8];
 } tz_state;
 
 /* Work counters of the integer searches (bench.py's k_tz roofline): points tested and the samples
@@ -797,6 +820,10 @@ static void tz_help(tz_state* s, int x, int y, int point_nr, int dist) {
   tz_count(s->w, s->h, s->fen);
   orc_pred_block(s->ref, s->x0, s->y0, s->w, s->h, 4 * x, 4 * y, s->cur);
   uint32_t d = int_dist(s->key, s->w, s->cur, s->w, s->w, s->h, s->fen);
+  if (s->ring) { /* array_e[counter_i] = uiSad (Backups/4:659) */
+    if (!s->after) s->cmin = d < s->cmin ? d : s->cmin;
+    else if (s->npush < 8) s->e[s->npush++] = d;
+  }
   if (d < s->best_sad) {
     d += orc_cost(s->ml, mv_bits(x, y, 2, s->mvp_x, s->mvp_y));
     if (d < s->best_sad) {
@@ -982,9 +1009,47 @@ static void tz_search(tz_state* s, const fme_job* j, const fme_tz_ext* e, int pw
       if (s->point_nr != 0) tz_two_point(s, &R);
     }
   }
+  if (s->ring) {
+    /* the backups' tail (Backups/4:4868-4878): index_ref = counter_i, then xTZ8PointSquareSearch at
+     * distance 1 and xTZ8PointSquareSearch2 at distance 2, both around the star best */
+    s->after = 1;
+    const int sx = s->best_x, sy = s->best_y;
+    int pts[8][2];
+    const int np = square_points(sx, sy, R.l, R.t, R.r, R.b, pts);   /* TEncSearch.cpp:1324-1377 */
+    for (int i = 0; i < np; i++) tz_help(s, pts[i][0], pts[i][1], 0, 1);
+    /* xTZ8PointSquareSearch2 (Backups/4:876-965): the x -/+ 1 points of the top and bottom rows
+     * are checked against the left / right bound of distance 2 */
+    const int top = sy - 2, bot = sy + 2, left = sx - 2, right = sx + 2;
+    const int okt = top >= R.t, okb = bot <= R.b, okl = left >= R.l, okr = right <= R.r;
+    if (okt) {
+      if (okl) tz_help(s, left, top, 9, 2);
+      if (okl) tz_help(s, sx - 1, top, 10, 2);
+      tz_help(s, sx, top, 11, 2);
+      if (okr) tz_help(s, sx + 1, top, 12, 2);
+      if (okr) tz_help(s, right, top, 13, 2);
+    }
+    if (okl) tz_help(s, left, sy - 1, 14, 2);
+    if (okr) tz_help(s, right, sy - 1, 15, 2);
+    if (okl) tz_help(s, left, sy, 16, 2);
+    if (okr) tz_help(s, right, sy, 17, 2);
+    if (okl) tz_help(s, left, sy + 1, 18, 2);
+    if (okr) tz_help(s, right, sy + 1, 19, 2);
+    if (okb) {
+      if (okl) tz_help(s, left, bot, 20, 2);
+      if (okl) tz_help(s, sx - 1, bot, 21, 2);
+      tz_help(s, sx, bot, 22, 2);
+      if (okr) tz_help(s, sx + 1, bot, 23, 2);
+      if (okr) tz_help(s, right, bot, 24, 2);
+    }
+  }
 }
 
 int orc_integer_search(orc_ctx* ctx, fme_job* jobs, const fme_tz_ext* ext, uint32_t* sad, int n) {
+  return orc_integer_search_ring(ctx, jobs, ext, sad, NULL, n);
+}
+
+int orc_integer_search_ring(orc_ctx* ctx, fme_job* jobs, const fme_tz_ext* ext, uint32_t* sad, uint32_t* nn_in,
+                            int n) {
   int16_t* key = (int16_t*)malloc(sizeof(int16_t) * 64 * 64);
   int16_t* cur = (int16_t*)malloc(sizeof(int16_t) * 64 * 64);
   for (int i = 0; i < n; i++) {
@@ -1011,6 +1076,8 @@ int orc_integer_search(orc_ctx* ctx, fme_job* jobs, const fme_tz_ext* ext, uint3
     s.ref = ref; s.key = key; s.x0 = j->x; s.y0 = j->y; s.w = w; s.h = h;
     s.fen = ctx->cfg.fast_inter_mode; s.mvp_x = j->mvp_x; s.mvp_y = j->mvp_y;
     s.ml = ctx->mlambda[j->lambda_id]; s.cur = cur;
+    s.ring = nn_in != NULL && (ext[i].flags & FME_TZ_RING) && !(j->flags & FME_JOB_BIPRED);
+    s.cmin = 0xFFFFFFFFu;
     if (j->flags & FME_JOB_BIPRED) {
       /* xPatternSearch (TEncSearch.cpp:4627-4680): raster order, strict minimum */
       s.best_sad = 0xFFFFFFFFu;
@@ -1027,6 +1094,10 @@ int orc_integer_search(orc_ctx* ctx, fme_job* jobs, const fme_tz_ext* ext, uint3
     j->mv_x = (int16_t)s.best_x;
     j->mv_y = (int16_t)s.best_y;
     if (sad) sad[i] = s.best_sad - orc_cost(s.ml, mv_bits(s.best_x, s.best_y, 2, s.mvp_x, s.mvp_y));
+    if (s.ring) { /* U1 V1 U2 H1 H2 U3 V2 U4, C (Backups/4:4343-4359); unpushed slots read 0 */
+      for (int k = 0; k < 8; k++) nn_in[(size_t)9 * i + k] = k < s.npush ? s.e[k] : 0u;
+      nn_in[(size_t)9 * i + 8] = s.cmin;
+    }
   }
   free(key);
   free(cur);

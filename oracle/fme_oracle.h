@@ -62,6 +62,8 @@ typedef struct orc_ctx {
   orc_nn_state nn_state;
   orc_nn_net net;
   int16_t int_mv_2n[2][FME_MAX_REFS][2];   /* m_integerMv2Nx2N[list][ref] (TEncSearch.h:118) */
+  const uint32_t* nn_in;                   /* FME_JOB_NN_IN input rows (orc_set_nn_inputs)     */
+  int nn_in_n;
 } orc_ctx;
 
 /* primitives (exported for unit tests) */
@@ -125,6 +127,10 @@ int orc_refine(orc_ctx* ctx, const fme_job* jobs, fme_result* res, int n);
 /* ---- integer motion estimation: xTZSearch / xPatternSearch per job;
  * writes jobs[i].mv_x/mv_y and sad[i].  Returns 0 or a negative FME_E_* code. */
 int orc_integer_search(orc_ctx* ctx, fme_job* jobs, const fme_tz_ext* ext, uint32_t* sad, int n);
+/* the same with the backups' tail for FME_TZ_RING jobs: nn_in[9 i ..] = array_e[index_ref .. +7], C */
+int orc_integer_search_ring(orc_ctx* ctx, fme_job* jobs, const fme_tz_ext* ext, uint32_t* sad,
+                            uint32_t* nn_in, int n);
+void orc_set_nn_inputs(orc_ctx* ctx, const uint32_t* rows, int n);
 /* points tested / distortion samples read by the integer searches since the last reset */
 void orc_tz_counters(uint64_t out[2], int reset);
 

@@ -20,7 +20,7 @@ sys.path[:0] = [HERE, os.path.join(ROOT, "hm16.9-nn_fme_amd")]
 
 from oracle import Oracle, Reference  # noqa: E402
 from nnfme import synth, weights  # noqa: E402
-from nnfme.abi import JOB_BIPRED, JOB_EMI, JOB_LOSSLESS, compare_results  # noqa: E402
+from nnfme.abi import JOB_BIPRED, JOB_EMI, JOB_LOSSLESS, JOB_NN_IN, TZ_RING, compare_results  # noqa: E402
 
 OUT = os.path.join(ROOT, "tests", "golden")
 
@@ -184,6 +184,62 @@ def build_tz_case(name, seed, width, height, calls, fen, search_range, bipred, m
           f"{int((ext['flags'] != 0).sum())} with a 2Nx2N start, {int((far > 4 * 20).sum())} ending > 20 px from the predictor")
 
 
+def build_ring_case(name, seed, width, height, calls, fen, search_range, bipred, mvp_noise, net, qp=22):
+    """The backups' own NN input path (configs[4]): xTZSearch with the final square + ring, every
+    distortion pushed (FME_TZ_RING: mv, sad and the nine NN inputs per job), then the sub-pel path
+    with the deeper net on those inputs (FME_JOB_NN_IN; bi-pred jobs reuse the last uni-pred call's
+    inputs).  Both stages from _ref; the oracle must agree on every output."""
+    rng = np.random.default_rng(seed)
+    pics = {i: synth.synth_luma(width, height, i, seed=seed) for i in range(5)}
+    lambdas = np.array(synth.LDP_LAMBDA[qp], dtype=np.float64)
+    jobs, ext = synth.make_tz_jobs(rng, width, height, calls, 4, [0, 1, 2, 3], [0, 1, 2, 3], bipred_frac=bipred,
+                                   search_range=search_range, mvp_noise=mvp_noise)
+    ext["flags"] |= TZ_RING
+    keys = synth.make_bipred_keys(rng, jobs, pics)
+    ref = Reference(use_hadamard=1, nn_mode=2, fast_inter_mode=fen)
+    orc = Oracle(use_hadamard=1, nn_mode=2, qp=qp, fast_inter_mode=fen)
+    nnet = weights.case_net(net)
+    for eng in (ref, orc):
+        for k, v in pics.items():
+            eng.set_picture(k, v)
+        for lid, lam in enumerate(lambdas):
+            eng.set_lambda(lid, float(lam))
+        eng.set_keys(keys if keys.size else np.zeros(1, np.int16))
+        eng.load_nn_net(nnet)
+    out_r, sad_r, nn_r = ref.integer_search_ring(jobs, ext)
+    out_o, sad_o, nn_o = orc.integer_search_ring(jobs, ext)
+    bad = (out_r["mv_x"] != out_o["mv_x"]) | (out_r["mv_y"] != out_o["mv_y"]) | (sad_r != sad_o) | \
+        (nn_r != nn_o).any(axis=1)
+    if bad.any():
+        raise SystemExit(f"{name}: oracle disagrees with _ref's integer search on {int(bad.sum())} jobs")
+    uni = (jobs["flags"] & JOB_BIPRED) == 0
+    rjobs = out_r.copy()
+    rjobs["flags"] = np.where(uni, JOB_NN_IN, rjobs["flags"]).astype(np.uint8)
+    for eng in (ref, orc):
+        eng.set_nn_inputs(nn_r)
+    r_ref = ref.refine(rjobs)
+    r_orc = orc.refine(rjobs)
+    bad, first, counts = compare_results(r_ref, r_orc)
+    if bad:
+        raise SystemExit(f"{name}: oracle disagrees with _ref on {bad} refinements (first {first}): {counts}")
+    path = os.path.join(OUT, f"{name}.npz")
+    np.savez_compressed(path, pictures=np.stack([pics[i] for i in range(5)]), lambdas=lambdas, keys=keys,
+                        jobs=jobs, ext=ext, mv_x=out_r["mv_x"], mv_y=out_r["mv_y"], sad=sad_r, nn_in=nn_r,
+                        refine_jobs=rjobs, results=r_ref, net=np.array(net),
+                        config=np.array([1, fen, 2, qp, search_range], dtype=np.int32))
+    moved = ((out_r["mv_x"] != orc.integer_search(jobs, ext)[0]["mv_x"]) & uni).sum()
+    print(f"{path}: {len(jobs)} jobs, {int((~uni).sum())} bi-pred, {int(moved)} moved by the square + ring, "
+          f"{int((nn_r[uni, :8] == 0).any(axis=1).sum())} with < 8 pushes, classes {len(set(r_ref['nn_class']))}")
+
+
+RING_CASES = [
+    # name, seed, W, H, calls/CTU/ref, FEN, SearchRange, bi-pred share, predictor noise, net
+    ("ring_scr3x40_fen1", 41, 160, 96, 40, 1, 64, 0.15, 24, "scr3x40+tzring"),
+    ("ring_b4x40_sr8_fen3", 42, 128, 96, 40, 3, 8, 0.1, 60, "blowing4x40+rezero+tzring"),
+    # SearchRange 2: the square and the ring mostly clipped by the range (fewer than 8 pushes)
+    ("ring_scr3x40_sr2_fen0", 43, 128, 96, 30, 0, 2, 0.1, 24, "scr3x40+tzring"),
+]
+
 TZ_CASES = [
     # name, seed, W, H, calls/CTU/ref, FEN, SearchRange, bi-pred share, predictor noise (qpel)
     ("tz_ldp_fen1", 31, 160, 96, 40, 1, 64, 0.15, 24),
@@ -234,6 +290,12 @@ def main():
         for c in DEEP_CASES:
             build_case(*c)
         return 0
+    if "--ring-only" in sys.argv:
+        for c in RING_CASES:
+            build_ring_case(*c)
+        return 0
+    for c in RING_CASES:
+        build_ring_case(*c)
     for c in DEEP_CASES:
         build_case(*c)
     if "--mc-only" not in sys.argv and "--tz-only" not in sys.argv:

@@ -65,6 +65,9 @@ class Oracle:
         lib.orc_refine.argtypes = [_P, _P, _P, C.c_int]
         lib.orc_integer_search.restype = C.c_int
         lib.orc_integer_search.argtypes = [_P, _P, _P, _P, C.c_int]
+        lib.orc_integer_search_ring.restype = C.c_int
+        lib.orc_integer_search_ring.argtypes = [_P, _P, _P, _P, _P, C.c_int]
+        lib.orc_set_nn_inputs.argtypes = [_P, _P, C.c_int]
         lib.orc_pred_inter_p.restype = C.c_int
         lib.orc_pred_inter_p.argtypes = [_P, _P, _P, C.c_int]
         lib.orc_pred_inter_reset.argtypes = [_P]
@@ -173,6 +176,27 @@ class Oracle:
             raise RuntimeError(f"orc_integer_search failed: {rc}")
         return jobs, sad
 
+    def integer_search_ring(self, jobs, ext):
+        """orc_integer_search_ring: (jobs, sad, nn_in[n][9]); FME_TZ_RING jobs run the backups' tail."""
+        jobs = np.array(jobs, copy=True)
+        ext = np.ascontiguousarray(ext)
+        sad = np.zeros(len(jobs), np.uint32)
+        nn_in = np.zeros((len(jobs), 9), np.uint32)
+        rc = self.lib.orc_integer_search_ring(self.ctx, _ptr(jobs), _ptr(ext), _ptr(sad), _ptr(nn_in), len(jobs))
+        if rc != 0:
+            raise RuntimeError(f"orc_integer_search_ring failed: {rc}")
+        return jobs, sad, nn_in
+
+    def set_nn_inputs(self, rows):
+        """The FME_JOB_NN_IN input rows of the next refine calls ([n][9] uint32; None unbinds)."""
+        if rows is None:
+            self._keep.pop("nn_in", None)
+            self.lib.orc_set_nn_inputs(self.ctx, None, 0)
+            return
+        rows = np.ascontiguousarray(rows, dtype=np.uint32).reshape(-1, 9)
+        self._keep["nn_in"] = rows
+        self.lib.orc_set_nn_inputs(self.ctx, _ptr(rows), len(rows))
+
     def pred_inter_p(self, reqs):
         """orc_pred_inter_p: predInterSearch's P-slice PU / reference loop, one fme_pu_res per request."""
         from nnfme.abi import PU_REQ_DTYPE, PU_RES_DTYPE
@@ -272,6 +296,9 @@ class Reference:
         lib.ref_set_picture_yuv.argtypes = [_P, C.c_int, _P, C.c_int, _P, _P, C.c_int, C.c_int, C.c_int]
         lib.ref_integer_search.restype = C.c_int
         lib.ref_integer_search.argtypes = [_P, _P, _P, _P, C.c_int]
+        lib.ref_integer_search_ring.restype = C.c_int
+        lib.ref_integer_search_ring.argtypes = [_P, _P, _P, _P, _P, C.c_int]
+        lib.ref_set_nn_inputs.argtypes = [_P, _P, C.c_int]
         lib.ref_template_cost.restype = C.c_uint32
         lib.ref_template_cost.argtypes = [_P] + [C.c_int] * 12
         lib.ref_bi_key.restype = C.c_int
@@ -303,6 +330,23 @@ class Reference:
         if rc != 0:
             raise RuntimeError(f"ref_integer_search failed: {rc}")
         return jobs, sad
+
+    def integer_search_ring(self, jobs, ext):
+        jobs = np.array(jobs, copy=True)
+        ext = np.ascontiguousarray(ext)
+        sad = np.zeros(len(jobs), np.uint32)
+        nn_in = np.zeros((len(jobs), 9), np.uint32)
+        rc = self.lib.ref_integer_search_ring(self.h, _ptr(jobs), _ptr(ext), _ptr(sad), _ptr(nn_in), len(jobs))
+        if rc != 0:
+            raise RuntimeError(f"ref_integer_search_ring failed: {rc}")
+        return jobs, sad, nn_in
+
+    def set_nn_inputs(self, rows):
+        if rows is None:
+            self.lib.ref_set_nn_inputs(self.h, None, 0)
+            return
+        rows = np.ascontiguousarray(rows, dtype=np.uint32).reshape(-1, 9)
+        self.lib.ref_set_nn_inputs(self.h, _ptr(rows), len(rows))
 
     def mc(self, mc_jobs, y, cb, cr):
         jobs = np.ascontiguousarray(mc_jobs)

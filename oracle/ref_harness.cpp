@@ -289,6 +289,7 @@ struct RefCtx {
   // NN_pred global state (TEncSearch.cpp:55-57): array_e storage, C, PUHeight, PUWidth.
   uint32_t slot[8] = {0};
   uint32_t C = 0, puh = 0, puw = 0;
+  std::vector<uint32_t> nn_in;   // FME_JOB_NN_IN rows (ref_set_nn_inputs), 9 per job
 };
 
 int nnClass(const float* P, const uint32_t* e, uint32_t c, int H, int W) {
@@ -373,6 +374,12 @@ void ref_set_keys(void* h, const int16_t* k, size_t n) {
 void ref_load_nn(void* h, const float* p) {
   RefCtx* c = static_cast<RefCtx*>(h);
   c->nn.assign(p, p + FME_NN_PARAMS);
+}
+
+void ref_set_nn_inputs(void* h, const uint32_t* rows, int n) {
+  RefCtx* c = static_cast<RefCtx*>(h);
+  if (rows) c->nn_in.assign(rows, rows + (size_t)9 * n);
+  else c->nn_in.clear();
 }
 
 void ref_nn_reset(void* h) {
@@ -463,7 +470,19 @@ int ref_refine(void* h, const fme_job* jobs, fme_result* res, int n) {
     int ix = j.mv_x, iy = j.mv_y;
     uint32_t C = 0;
     int npush = 0;
-    if (j.flags & FME_JOB_EMI) {
+    if (j.flags & FME_JOB_NN_IN) {   // the backups' inputs, as xPatternSearchFast read them
+      if ((size_t)9 * (i + 1) > c->nn_in.size()) return FME_E_INVALID;
+      const uint32_t* row = c->nn_in.data() + (size_t)9 * i;
+      npush = 8;
+      for (int k = 0; k < 8; k++) {
+        r.emi[k] = row[k];
+        c->slot[k] = row[k];
+      }
+      C = row[8];
+      c->C = C;
+      c->puh = hh;
+      c->puw = w;
+    } else if (j.flags & FME_JOB_EMI) {
       s.rd.setCostScale(2);
       RefSearch::Best b;
       b.x = j.mv_x;
@@ -741,6 +760,7 @@ struct Tz {
   Pel* refY;
   int stride;
   int lt_x, lt_y, rb_x, rb_y;
+  std::vector<long>* array_e;   // the backups' every-point pushes (Backups/4:659), or null
   void clipMv(TComMv& mv, int pw, int ph, int cux, int cuy) {
     const int hmax = (pw + 8 - cux - 1) << 2, hmin = (-64 - 8 - cux + 1) << 2;
     const int vmax = (ph + 8 - cuy - 1) << 2, vmin = (-64 - 8 - cuy + 1) << 2;
@@ -749,6 +769,7 @@ struct Tz {
   }
   void help(TzStruct& t, int x, int y, int pnr, unsigned dist) {   // xTZSearchHelp, normal branch
     Distortion d = s.intDist(key, refY, stride, x, y);
+    if (array_e) array_e->push_back((long)d);   // array_e[counter_i] = uiSad; counter_i++
     if (d < t.uiBestSad) {
       d += s.rd.getCostOfVectorWithPredictor(x, y);
       if (d < t.uiBestSad) {
@@ -831,14 +852,60 @@ struct Tz {
       }
     }
   }
+  // xTZ8PointSquareSearch (TEncSearch.cpp:1324-1377 = Backups/4:818-873)
+  void square(TzStruct& t, int sx, int sy, int iDist) {
+    const int iTop = sy - iDist, iBottom = sy + iDist, iLeft = sx - iDist, iRight = sx + iDist;
+    t.uiBestRound += 1;
+    if (iTop >= lt_y) {
+      if (iLeft >= lt_x) help(t, iLeft, iTop, 1, iDist);
+      help(t, sx, iTop, 2, iDist);
+      if (iRight <= rb_x) help(t, iRight, iTop, 3, iDist);
+    }
+    if (iLeft >= lt_x) help(t, iLeft, sy, 4, iDist);
+    if (iRight <= rb_x) help(t, iRight, sy, 5, iDist);
+    if (iBottom <= rb_y) {
+      if (iLeft >= lt_x) help(t, iLeft, iBottom, 6, iDist);
+      help(t, sx, iBottom, 7, iDist);
+      if (iRight <= rb_x) help(t, iRight, iBottom, 8, iDist);
+    }
+  }
+  // xTZ8PointSquareSearch2 (Backups/4:876-965): 16 points at distance iDist, in its call order
+  // and with its checks (the x -/+ 1 points of the top / bottom rows test iLeft / iRight)
+  void square2(TzStruct& t, int sx, int sy, int iDist) {
+    const int iTop = sy - iDist, iBottom = sy + iDist, iLeft = sx - iDist, iRight = sx + iDist;
+    t.uiBestRound += 1;
+    if (iTop >= lt_y) {
+      if (iLeft >= lt_x) help(t, iLeft, iTop, 9, iDist);
+      if (iLeft >= lt_x) help(t, sx - 1, iTop, 10, iDist);
+      help(t, sx, iTop, 11, iDist);
+      if (iRight <= rb_x) help(t, sx + 1, iTop, 12, iDist);
+      if (iRight <= rb_x) help(t, iRight, iTop, 13, iDist);
+    }
+    if (iLeft >= lt_x) help(t, iLeft, sy - 1, 14, iDist);
+    if (iRight <= rb_x) help(t, iRight, sy - 1, 15, iDist);
+    if (iLeft >= lt_x) help(t, iLeft, sy, 16, iDist);
+    if (iRight <= rb_x) help(t, iRight, sy, 17, iDist);
+    if (iLeft >= lt_x) help(t, iLeft, sy + 1, 18, iDist);
+    if (iRight <= rb_x) help(t, iRight, sy + 1, 19, iDist);
+    if (iBottom <= rb_y) {
+      if (iLeft >= lt_x) help(t, iLeft, iBottom, 20, iDist);
+      if (iLeft >= lt_x) help(t, sx - 1, iBottom, 21, iDist);
+      help(t, sx, iBottom, 22, iDist);
+      if (iRight <= rb_x) help(t, sx + 1, iBottom, 23, iDist);
+      if (iRight <= rb_x) help(t, iRight, iBottom, 24, iDist);
+    }
+  }
   void twoPoint(TzStruct& t) {   // xTZ2PointSearch: the two neighbours not yet tested
     const int sx = t.iBestX, sy = t.iBestY;
     static const int kPts[9][2][2] = {{{0, 0}, {0, 0}},   {{-1, 0}, {0, -1}}, {{-1, -1}, {1, -1}},
                                       {{0, -1}, {1, 0}},  {{-1, 1}, {-1, -1}}, {{1, -1}, {1, 1}},
                                       {{-1, 0}, {0, 1}},  {{-1, 1}, {1, 1}},   {{1, 0}, {0, 1}}};
-    if (t.ucPointNr < 1 || t.ucPointNr > 8) return;
+    // the reference switches on ucPointNr once, at entry (TEncSearch.cpp:1203): the first point's
+    // xTZSearchHelp may set it to 0 before the second is tested
+    const int pnr = t.ucPointNr;
+    if (pnr < 1 || pnr > 8) return;
     for (int k = 0; k < 2; k++) {
-      const int dx = kPts[t.ucPointNr][k][0], dy = kPts[t.ucPointNr][k][1];
+      const int dx = kPts[pnr][k][0], dy = kPts[pnr][k][1];
       const int x = sx + dx, y = sy + dy;
       if (dx < 0 && x < lt_x) continue;
       if (dx > 0 && x > rb_x) continue;
@@ -850,7 +917,16 @@ struct Tz {
 };
 }  // namespace
 
+extern "C" int ref_integer_search_ring(void* h, fme_job* jobs, const fme_tz_ext* ext, uint32_t* sad,
+                                       uint32_t* nn_in, int n);
 extern "C" int ref_integer_search(void* h, fme_job* jobs, const fme_tz_ext* ext, uint32_t* sad, int n) {
+  return ref_integer_search_ring(h, jobs, ext, sad, nullptr, n);
+}
+
+// nn_in != null: FME_TZ_RING jobs run the backups' xTZSearch tail (Backups/4:4868-4878) and get the
+// inputs xPatternSearchFast builds from array_e (:4343-4359).
+extern "C" int ref_integer_search_ring(void* h, fme_job* jobs, const fme_tz_ext* ext, uint32_t* sad,
+                                       uint32_t* nn_in, int n) {
   RefCtx* c = static_cast<RefCtx*>(h);
   RefSearch& s = c->s;
   std::vector<Pel> keybuf(64 * 64);
@@ -876,7 +952,9 @@ extern "C" int ref_integer_search(void* h, fme_job* jobs, const fme_tz_ext* ext,
     TComMv pred(j.mvp_x, j.mvp_y);
     s.rd.setPredictor(pred);
     s.rd.setCostScale(2);
-    Tz tz{s, &key, refY, rs, j.lt_x, j.lt_y, j.rb_x, j.rb_y};
+    std::vector<long> array_e;   // counter_i = 0 at the call's start (the previous call's memset)
+    const bool ring = nn_in && (ext[i].flags & FME_TZ_RING) && !(j.flags & FME_JOB_BIPRED);
+    Tz tz{s, &key, refY, rs, j.lt_x, j.lt_y, j.rb_x, j.rb_y, ring ? &array_e : nullptr};
     TzStruct t{std::numeric_limits<Distortion>::max(), 0, 0, 0, 0, 0};
     const int pw = ref.getWidth(COMPONENT_Y), ph = ref.getHeight(COMPONENT_Y);
     if (j.flags & FME_JOB_BIPRED) {   // xPatternSearch
@@ -936,6 +1014,19 @@ extern "C" int ref_integer_search(void* h, fme_job* jobs, const fme_tz_ext* ext,
           t.uiBestDistance = 0;
           if (t.ucPointNr != 0) tz.twoPoint(t);
         }
+      }
+      if (ring) {   // Backups/4:4868-4878, then xPatternSearchFast's reads (4343-4359)
+        iStartX = t.iBestX;
+        iStartY = t.iBestY;
+        const size_t index_ref = array_e.size();
+        tz.square(t, iStartX, iStartY, 1);
+        tz.square2(t, iStartX, iStartY, 2);
+        long C = array_e[0];
+        for (size_t k = 1; k <= index_ref - 1; k++)
+          if (array_e[k] < C) C = array_e[k];
+        for (int k = 0; k < 8; k++)
+          nn_in[(size_t)9 * i + k] = index_ref + k < array_e.size() ? (uint32_t)array_e[index_ref + k] : 0u;
+        nn_in[(size_t)9 * i + 8] = (uint32_t)C;
       }
     }
     j.mv_x = (int16_t)t.iBestX;

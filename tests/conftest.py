@@ -34,7 +34,14 @@ def pytest_collection_modifyitems(config, items):
 
 def golden_cases():
     """Sub-pel refinement fixtures (fme_job -> fme_result)."""
-    return sorted(f[:-4] for f in os.listdir(GOLDEN) if f.endswith(".npz") and not f.startswith(("mc_", "tz_")))
+    return sorted(f[:-4] for f in os.listdir(GOLDEN)
+                  if f.endswith(".npz") and not f.startswith(("mc_", "tz_", "ring_")))
+
+
+def ring_golden_cases():
+    """The backups' NN input path (configs[4]): integer search with the final square + ring
+    (fme_job + fme_tz_ext -> MV, ruiSAD, nine NN inputs), then FME_JOB_NN_IN refinements."""
+    return sorted(f[:-4] for f in os.listdir(GOLDEN) if f.endswith(".npz") and f.startswith("ring_"))
 
 
 def tz_golden_cases():
