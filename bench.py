@@ -10,7 +10,8 @@ the jobs (32 B each), the frame's original and one reconstructed reference pictu
 from pinned host memory, and the 16-byte fme_mv_result per job comes back (nnfme.pipeline.
 FrameReplay: two steps in flight on separate copy / compute streams, no host synchronisation
 inside a batch).  With N ranks (torchrun, one GPU each) rank r replays frames r, r+N, ... (weak
-scaling); each reconstruction is uploaded by one rank and RCCL-broadcast to all, and the NN
+scaling); each reconstruction is uploaded by one rank and sent (RCCL point-to-point) to the
+ranks whose frames reference it, and the NN
 carried state is chained across ranks at the end (all_gather of 12 words per frame + prefix
 re-run), all inside the timed region.  `device_resident` reports the same batches with inputs
 and outputs already in HBM.
@@ -682,8 +683,12 @@ def main():
                        "job_stream": args.jobs,
                        "frames_per_step": FPS,
                        "jobs_per_step_per_gpu": n, "parallelism": f"frame-sharded x{world}",
+                       # what torch.distributed actually ran (None: one process, no process group)
+                       "dist_backend": dist.get_backend() if dist.is_initialized() else None,
+                       "pg_world_size": dist.get_world_size() if dist.is_initialized() else 1,
                        "timed": "per step: H2D of the jobs (32 B each), of the frames' originals and of one "
-                                "reconstructed reference per frame (RCCL broadcast when sharded), refine, D2H of "
+                                "reconstructed reference per frame (when sharded: RCCL point-to-point sends to the "
+                                "<= 3 other ranks whose frames reference it), refine, D2H of "
                                 "the 16-byte fme_mv_result per job; two steps in flight on separate copy / "
                                 "compute streams" + ("; NN-state chain fix-up included" if world > 1 else "")},
             "roofline": {

@@ -4,15 +4,16 @@ Per step (one batch of xMotionEstimation jobs = one frame, or a group of F small
 a launch fills the chip):
   * H2D of the batch's job descriptors, of the frames' original pictures and of one
     reconstructed reference picture per frame (trace replay: frame f's references are the
-    reconstructions of f-1..f-4; each is uploaded once, by the rank that publishes it, and
-    broadcast to every rank over RCCL/xGMI when the run is sharded);
+    reconstructions of f-1..f-4; each is uploaded once, by the rank that publishes it, and sent
+    over RCCL/xGMI point-to-point to the ranks whose frames reference it - at most three other
+    ranks, whatever the world size - when the run is sharded);
   * fme_refine_mv_device (EMI step -> FracDIF -> NN_pred -> cost tail, no host synchronisation);
   * D2H of the 16-byte fme_mv_result per job.
 Two steps are in flight: the uploads of step k+1 and the download of step k-1 run on their own
 streams while step k computes (events order the double-buffered job / output slots).
 
 Sharding (world > 1): rank r replays batches r, r + world, ... (weak scaling; no collective on
-the data path besides the picture broadcasts).  NN_pred's carried state crosses frames in the
+the data path besides the reconstructions' point-to-point sends).  NN_pred's carried state crosses frames in the
 reference, so every batch starts from a reset state, each batch's end state is copied on the
 device (fme_nn_copy_state_device), and after the run the states are all-gathered (12 words per
 batch), chained in encode order (nnfme.dist.chain_states) and the jobs up to each batch's last
@@ -149,7 +150,8 @@ class FrameReplay:
 
     # -- pictures ---------------------------------------------------------------------------
     def _publish(self, g, src_rank):
-        """Reconstruction of frame g: uploaded by src_rank, broadcast to every rank."""
+        """Reconstruction of frame g (before the run: frames -4 .. -2): uploaded by src_rank,
+        broadcast to every rank."""
         dst = self.recon[g + REFS]
         if self.rank == src_rank:
             _memcpy_async(dst, self.pool[g % self.P], self.H * self.W, H2D, torch_current_stream(dst))
@@ -162,6 +164,56 @@ class FrameReplay:
             else:
                 dist.broadcast(dst, src=src_rank, group=self.group)
 
+    def rank_of_frame(self, g):
+        return (g // self.F) % self.world
+
+    def readers(self, h):
+        """Ranks (other than the publisher) whose frames reference reconstruction h: frames h+1 ..
+        h+REFS of the run."""
+        frames = self.steps * self.world * self.F
+        out = []
+        for d in range(1, REFS + 1):
+            f = h + d
+            if 0 <= f < frames:
+                r = self.rank_of_frame(f)
+                if r not in out:
+                    out.append(r)
+        return out
+
+    def _exchange(self, k, stream):
+        """Step k's reconstructions (frame base + r F - 1 + j, uploaded by rank r) go point-to-point
+        to the ranks that reference them (self.readers): every rank runs the same op list, sends of
+        its own frames and receives of the frames it needs, in one batch_isend_irecv (one RCCL group
+        on the copy stream).  Pictures stay resident for the run, so each is sent once."""
+        import torch.distributed as dist
+        F, W = self.F, self.world
+        base = k * W * F
+        gloo = dist.get_backend(self.group) == "gloo"
+        ops, fixups = [], []
+        for r in range(W):
+            for j in range(F):
+                h = base + r * F - 1 + j
+                dsts = [d for d in self.readers(h) if d != r]
+                if self.rank == r:
+                    buf = self.recon[h + REFS]
+                    if gloo:   # CPU rehearsal: gloo sends host tensors
+                        stream.synchronize()
+                        buf = buf.cpu()
+                    for d in dsts:
+                        ops.append(dist.P2POp(dist.isend, buf, d, group=self.group))
+                elif self.rank in dsts:
+                    buf = self.recon[h + REFS]
+                    if gloo:
+                        tmp = self.torch.empty_like(buf, device="cpu")
+                        fixups.append((buf, tmp))
+                        buf = tmp
+                    ops.append(dist.P2POp(dist.irecv, buf, r, group=self.group))
+        if ops:
+            for w in dist.batch_isend_irecv(ops):
+                w.wait()
+        for dst, tmp in fixups:
+            dst.copy_(tmp, non_blocking=False)
+
     def _upload_run(self, dst, d0, g0, count, stream):
         """Planes of frames g0 .. g0+count-1 into dst[d0 ..]: one copy per run of frames that is
         contiguous in the pool (a small-frame batch is a few large copies, not many small ones)."""
@@ -173,13 +225,10 @@ class FrameReplay:
             i += run
 
     def _publish_run(self, g0, count, src_rank, stream):
-        """Reconstructions of frames g0 .. g0+count-1, uploaded by src_rank (one copy per pool
-        run), broadcast to every rank."""
-        if self.world == 1:
+        """Reconstructions of frames g0 .. g0+count-1 that src_rank uploads (one copy per pool
+        run); when sharded, _exchange then sends them to their readers."""
+        if self.rank == src_rank:
             self._upload_run(self.recon, g0 + REFS, g0, count, stream)
-            return
-        for j in range(count):
-            self._publish(g0 + j, src_rank)
 
     def prime(self):
         """References of the first frames (recon -4 .. -2), before the run (untimed); every
@@ -228,8 +277,10 @@ class FrameReplay:
                 _memcpy_async(self.d_kreqs[b], self.h_kreqs, self.h_kreqs.numel(), H2D, cp)
             self._upload_run(self.org, k * F, f0, F, cp)
             base = k * self.world * F
-            for r in range(self.world):   # recon(first frame of rank r's batch - 1 + j), by rank r
-                self._publish_run(base + r * F - 1, F, r, cp)
+            # recon(first frame of rank r's batch - 1 + j) is uploaded by rank r ...
+            self._publish_run(base + self.rank * F - 1, F, self.rank, cp)
+            if self.world > 1:   # ... and sent to the ranks whose frames reference it
+                self._exchange(k, cp)
             self.ev_in[b].record(cp)
         self.uploaded = k
 

@@ -175,3 +175,60 @@ def test_gloo_two_rank_frame_sharding(tmp_path):
         r = got[str(f)].view(RESULT_DTYPE)
         n_bad, first, counts = compare_results(r, want[f])
         assert n_bad == 0, f"frame {f}: first bad job {first}, {counts}"
+
+
+# ---- FrameReplay's reconstruction exchange (nnfme.pipeline), CPU rehearsal over gloo ------------
+class _Stream:
+    def synchronize(self):
+        pass
+
+
+def _exchange_rank(rank, world, port, F, steps, out_path):
+    import torch
+    import torch.distributed as dist
+    from nnfme.pipeline import REFS, FrameReplay
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    rep = FrameReplay.__new__(FrameReplay)   # the exchange only: no device, no context
+    rep.torch, rep.world, rep.rank, rep.group, rep.F, rep.steps = torch, world, rank, None, F, steps
+    frames = steps * world * F
+    rep.recon = torch.zeros((frames + REFS, 4, 4), dtype=torch.uint8)
+    sends = 0
+    for k in range(steps):
+        base = k * world * F
+        for j in range(F):   # this rank's uploads: frames base + rank F - 1 + j, marked with their number
+            h = base + rank * F - 1 + j
+            rep.recon[h + REFS].fill_((h + 7) % 251)
+            sends += len([d for d in rep.readers(h) if d != rank])
+        rep._exchange(k, _Stream())
+    have = [int(rep.recon[h + REFS, 0, 0]) for h in range(-REFS, frames)]
+    np.save(out_path % rank, np.array(have + [sends], np.int64))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,F", [(4, 1), (8, 1), (3, 2)])
+def test_frame_replay_exchange_sends_each_reconstruction_to_its_readers(tmp_path, world, F):
+    """Every rank ends up holding exactly the reconstructions its frames reference (frames g-1 ..
+    g-4 of each of its frames g) - the ones it uploads itself plus what the others sent - and no
+    rank sends to more than three others (LDP references the previous four frames)."""
+    import torch.multiprocessing as mp
+    from nnfme.pipeline import REFS
+    steps = 3
+    out = str(tmp_path / "have_%d.npy")
+    mp.spawn(_exchange_rank, args=(world, _free_port(), F, steps, out), nprocs=world, join=True)
+    frames = steps * world * F
+    for r in range(world):
+        got = np.load(out % r)
+        have, sends = got[:-1], int(got[-1])
+        mine = [g for g in range(frames) if (g // F) % world == r]
+        need = {g - d for g in mine for d in range(1, REFS + 1) if g - d >= -1}
+        own = {k * world * F + r * F - 1 + j for k in range(steps) for j in range(F)}
+        for h in range(-1, frames):
+            v = int(have[h + REFS])
+            if h in need or h in own:
+                assert v == (h + 7) % 251, (r, h, v)
+            else:
+                assert v == 0, (r, h, v)   # not sent where nobody reads it
+        assert sends <= 3 * steps * F
