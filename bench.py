@@ -41,7 +41,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "hm16.9-nn_fme_amd"))
 
 from nnfme import synth  # noqa: E402
-from nnfme.abi import JOB_DTYPE, RESULT_DTYPE  # noqa: E402
+from nnfme.abi import JOB_BIPRED, JOB_DTYPE, JOB_NN_IN, RESULT_DTYPE, TZ_RING  # noqa: E402
 
 W, H, QP = 1920, 1080, 22
 METRIC = "sub-pel PU refinements/sec @ 1080p lowdelay_P QP22; bit-exact MV/SATD vs HM"
@@ -69,22 +69,22 @@ WORKLOADS = {
                desc="2560x1600 random-access QP27 B-frames, NN_pred on, 2+2 refs, ~1331 calls/CTU, 20.5 % bi-pred "
                     "with 2*org - pred keys built per frame on the device inside the timed step, RA GOP-8 "
                     "lambdas (configs[3])"),
-    "c5": dict(W=1920, H=1080, QP=22, nn=2, net="scr3x40+slotreset", engine=1, calls=423, bipred=0.0, gop="ldp",
-               frames=1,
+    "c5": dict(W=1920, H=1080, QP=22, nn=2, net="scr3x40+tzring", engine=1, calls=423, bipred=0.0, gop="ldp",
+               frames=1, inputs="ring",
                desc="1920x1080 lowdelay_P QP22 with the 3-hidden-layer NN_pred (Backups/4 SCR 9-40-40-40-49, "
-                    "double) as a batched MFMA GEMM (v_mfma_f64_16x16x4) (configs[4]); the SCR weights run on the "
-                    "master's EMI inputs (distance-1 SSE square, C = its best) with the backups' per-call "
-                    "array_e reset, not on Backups/4's own input path (every-point SAD pushes, C = min over "
-                    "the TZ points, distance-2 ring): input parity with the backup unpinned (include/fme.h)"),
-    "c5_exact": dict(W=1920, H=1080, QP=22, nn=2, net="scr3x40+slotreset", engine=0, calls=423, bipred=0.0,
-                     gop="ldp", frames=1,
-                     desc="configs[4] net through the exact (scalar, reference-order) engine, master's EMI "
-                          "inputs with the per-call array_e reset"),
-    "c5_b4x40": dict(W=1920, H=1080, QP=22, nn=2, net="blowing4x40+rezero+slotreset", engine=1, calls=423,
-                     bipred=0.0, gop="ldp", frames=1,
+                    "double) as a batched MFMA GEMM (v_mfma_f64_16x16x4) (configs[4]) on Backups/4's own input path: "
+                    "every xTZSearchHelp distortion pushed, the final square + distance-2 ring (which may move the "
+                    "integer MV), C = the least push before the square (fme_integer_search_ring -> FME_JOB_NN_IN "
+                    "jobs, 36 B of NN inputs per job uploaded with the job)"),
+    "c5_exact": dict(W=1920, H=1080, QP=22, nn=2, net="scr3x40+tzring", engine=0, calls=423, bipred=0.0,
+                     gop="ldp", frames=1, inputs="ring",
+                     desc="configs[4] net through the exact (scalar, reference-order) engine on Backups/4's own input "
+                          "path"),
+    "c5_b4x40": dict(W=1920, H=1080, QP=22, nn=2, net="blowing4x40+rezero+tzring", engine=1, calls=423,
+                     bipred=0.0, gop="ldp", frames=1, inputs="ring",
                      desc="1920x1080 QP22 with the 4x40 blowing net (Backups/15, float, hidden layers re-zeroed) "
-                          "as a batched MFMA GEMM (v_mfma_f32_16x16x4), master's EMI inputs with the per-call "
-                          "array_e reset"),
+                          "as a batched MFMA GEMM (v_mfma_f32_16x16x4) on Backups/15's own input path (the same "
+                          "integer-search tail as Backups/4)"),
 }
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md chip table (spec)
 # int32 VALU lane-ops/s: 256 CUs x 4 SIMDs x 32 lanes/clk (a wave64 op issues over 2 clk) x
@@ -146,6 +146,41 @@ def _cpu_reference():
     if _CPU.get("keys") is not None:
         ref.set_keys(_CPU["keys"])
     return ref
+
+
+def ring_inputs_cpu(jobs, ext, pics, m):
+    """The backups' input path for the CPU baseline: the oracle's integer search with the square +
+    ring (orc_integer_search_ring) on the first m jobs -> (refine jobs with FME_JOB_NN_IN, rows)."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    from oracle import Oracle
+    from nnfme.abi import JOB_BIPRED, JOB_NN_IN
+    orc = Oracle(fast_inter_mode=1)
+    for k, v in pics.items():
+        orc.set_picture(k, v)
+    orc.set_lambda(0, synth.LDP_LAMBDA[QP][1])
+    out, _, rows = orc.integer_search_ring(jobs[:m], ext[:m])
+    out["flags"] = np.where((out["flags"] & JOB_BIPRED) == 0, JOB_NN_IN, out["flags"]).astype(np.uint8)
+    return out, rows
+
+
+def cpu_baseline_ring(jobs, rows, net_name, pics, seconds):
+    """oracle/_ref's sub-pel path with the deeper net on the backups' inputs (FME_JOB_NN_IN rows), one
+    core, whole passes over the sample until `seconds` have elapsed."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    from oracle import Reference
+    from nnfme import weights
+    ref = Reference(use_hadamard=1, nn_mode=2, fast_inter_mode=1)
+    for k, v in pics.items():
+        ref.set_picture(k, v)
+    ref.set_lambda(0, synth.LDP_LAMBDA[QP][1])
+    ref.load_nn_net(weights.case_net(net_name))
+    ref.set_nn_inputs(rows)
+    ref.refine(jobs[:1000])
+    done, t0 = 0, time.perf_counter()
+    while time.perf_counter() - t0 < seconds:
+        ref.refine(jobs)
+        done += len(jobs)
+    return done / (time.perf_counter() - t0), time.perf_counter() - t0, done
 
 
 def cpu_baseline(jobs, pics, seconds):
@@ -524,7 +559,12 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
 
     # ---- inputs (untimed): one frame's jobs in HM order -----------------------------------------
-    jobs = make_frame_jobs(1000, args.jobs, CALLS, BIPRED)
+    RING = wl.get("inputs") == "ring"
+    if RING:   # configs[4] on the backups' input path: the frame's integer searches come first
+        jobs, tz_ext = synth.make_tz_jobs(np.random.default_rng(1000), W, H, CALLS, 4, [0, 1, 2, 3], [0])
+        tz_ext["flags"] |= TZ_RING
+    else:
+        jobs = make_frame_jobs(1000, args.jobs, CALLS, BIPRED)
     n1 = len(jobs)
     keys = key_reqs = None
     if BIPRED > 0:   # bi-pred keys (removeHighFreq of the other list's prediction), resident with the jobs
@@ -535,7 +575,18 @@ def main():
     # ---- CPU baselines first, before anything touches the GPU (fork-safe) -------------------
     cpu = {}
     _CPU["nn"], _CPU["keys"] = min(NN, 1), keys
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and RING:
+        pics = {k: synth.synth_luma(W, H, t) for k, t in zip(range(5), (7, 6, 5, 4, 0))}
+        rjobs, rrows = ring_inputs_cpu(jobs, tz_ext, pics, 20000)
+        rate, dt, done = cpu_baseline_ring(rjobs, rrows, wl["net"], pics, args.cpu_seconds)
+        cpu["cpu_baseline"] = {
+            "value": rate, "unit": "PU/s", "cores": 1, "kind": "reference",
+            "sample": f"{done} jobs ({done // len(rjobs)} passes over the first {len(rjobs)} jobs of the frame, HM "
+                      f"order) on one host core, {dt:.1f} s; oracle/_ref = the reference's TLibCommon -O2 in "
+                      f"TEncSearch order with the backup's net restated scalar (double / float, its loop order) on "
+                      f"the backup's NN inputs (their integer searches by the oracle, untimed)",
+        }
+    elif rank == 0 and world == 1 and not args.no_cpu_baseline:
         pics = {k: synth.synth_luma(W, H, t) for k, t in zip(range(5), (7, 6, 5, 4, 0))}
         rate, dt, done = cpu_baseline(jobs, pics, args.cpu_seconds)
         cpu["cpu_baseline"] = {
@@ -578,6 +629,14 @@ def main():
     ctx = FmeContext(device=dev_index, use_hadamard=1, nn_mode=NN, qp=QP, fast_inter_mode=1,
                      max_jobs=n1 * FPS, net=net, nn_engine=wl.get("engine", 0))
 
+    nn_rows = None
+    if RING:   # untimed: the frame's integer searches on the GPU, with the backups' square + ring
+        for k, t in zip(range(5), (7, 6, 5, 4, 0)):
+            ctx.set_picture(k, synth.synth_luma(W, H, t))
+        ctx.set_lambda(0, frame_lambda(wl, 0))
+        jobs, _, nn_rows = ctx.integer_search_ring(jobs, tz_ext)
+        jobs["flags"] = np.where((jobs["flags"] & JOB_BIPRED) == 0, JOB_NN_IN, jobs["flags"]).astype(np.uint8)
+
     # synthetic frame pool (the trace's originals / reconstructions): frame g -> pool[g % 8]
     pool = np.stack([synth.synth_luma(W, H, t) for t in range(8)])
     steps_total = args.warmup + args.steps
@@ -586,7 +645,7 @@ def main():
     # that frame's pictures (fme_build_bipred_keys_device, k_bi_key) inside the timed step
     rep = FrameReplay(ctx, jobs, pool, lambda f: frame_lambda(wl, f), steps_total, frames_per_step=FPS,
                       world=world, rank=rank, device=dev, defer_download=defer,
-                      key_reqs=key_reqs, key_count=len(keys) if keys is not None else 0)
+                      key_reqs=key_reqs, key_count=len(keys) if keys is not None else 0, nn_rows=nn_rows)
     n = rep.n
     rep.prime()
 
@@ -631,6 +690,7 @@ def main():
             torch.cuda.synchronize(dev)
             t1 = time.perf_counter()
             for s in range(args.steps):
+                rep.bind_rows(s & 1)
                 if rep.kreqs is not None:
                     ctx.build_bipred_keys_device(rep.d_kreqs[s & 1].data_ptr(), len(rep.kreqs), rep.key_count * FPS,
                                                  comp.cuda_stream)
@@ -677,9 +737,12 @@ def main():
                     "NN weights, no random init)",
             "config": {"workload": WDESC,
                        "workload_id": args.workload,
-                       **({"nn_net": wl["net"], "nn_inputs": "master EMI step (distance-1 SSE square, C = its "
-                           "best SSE), per-call array_e reset; Backups/4's own input path not restated "
-                           "(input parity unpinned)"} if NN == 2 else {}),
+                       **({"nn_net": wl["net"], "nn_inputs": "the backups' own input path (Backups/4:659, "
+                           "4343-4359, 4868-4878; Backups/15:1257, 4935-4962, 5440-5445): every xTZSearchHelp "
+                           "distortion pushed, final square + distance-2 ring, C = least push before the square, "
+                           "U1..U4/V/H = the next 8 pushes, per-call memset; jobs and rows from "
+                           "fme_integer_search_ring on the first frame's pictures (untimed), replayed every step "
+                           "with their 36-byte input rows uploaded per step"} if NN == 2 else {}),
                        "job_stream": args.jobs,
                        "frames_per_step": FPS,
                        "jobs_per_step_per_gpu": n, "parallelism": f"frame-sharded x{world}",

@@ -95,13 +95,15 @@ def group_key_reqs(base, frames, key_count):
 
 class FrameReplay:
     def __init__(self, ctx, base_jobs, pool, lambda_of, n_steps, frames_per_step=1, world=1, rank=0, device=None,
-                 group=None, defer_download=True, key_reqs=None, key_count=0):
+                 group=None, defer_download=True, key_reqs=None, key_count=0, nn_rows=None):
         """ctx: an FmeContext on `device`; base_jobs: one frame's jobs (ref_id = reference
         distance - 1); pool: uint8 [P, H, W] host frames, frame g's pictures are pool[g % P];
         lambda_of(g): frame g's lambda.  key_reqs (fme_bikey_req, ref_id = distance - 1) and
         key_count: the frame's bi-pred key requests; each step uploads them with its jobs and builds
         its frames' removeHighFreq keys on the device from that step's pictures, before its batch
-        (fme_build_bipred_keys_device), so the keys are per-frame work inside the timed step."""
+        (fme_build_bipred_keys_device), so the keys are per-frame work inside the timed step.
+        nn_rows (uint32 [n][9]): the NN input rows of the frame's FME_JOB_NN_IN jobs (the backups'
+        input path); each step uploads them with its jobs and binds them (fme_set_nn_inputs)."""
         import torch
         self.torch, self.ctx = torch, ctx
         self.world, self.rank, self.group = world, rank, group
@@ -121,6 +123,12 @@ class FrameReplay:
             self.kreqs = group_key_reqs(key_reqs, F, self.key_count)
             self.h_kreqs = torch.from_numpy(self.kreqs.view(np.uint8).copy()).pin_memory()
             self.d_kreqs = [torch.empty(self.h_kreqs.numel(), dtype=torch.uint8, device=device) for _ in range(2)]
+        self.rows = None
+        if nn_rows is not None:
+            self.rows = np.tile(np.ascontiguousarray(nn_rows, dtype=np.uint32).reshape(-1, 9), (F, 1))
+            assert len(self.rows) == n
+            self.h_rows = torch.from_numpy(self.rows.view(np.uint8).copy()).pin_memory()
+            self.d_rows = [torch.empty(self.h_rows.numel(), dtype=torch.uint8, device=device) for _ in range(2)]
         self.d_out = [torch.empty(n * MV_RESULT_DTYPE.itemsize, dtype=torch.uint8, device=device) for _ in range(2)]
         self.h_out = torch.empty((n_steps, n * MV_RESULT_DTYPE.itemsize), dtype=torch.uint8).pin_memory()
         frames = n_steps * world * F
@@ -243,8 +251,14 @@ class FrameReplay:
         self.s_copy.synchronize()
         self.s_down.synchronize()
 
+    def bind_rows(self, b):
+        """Bind slot b's NN input rows for the next batches (no-op without rows)."""
+        if self.rows is not None:
+            self.ctx.set_nn_inputs(self.d_rows[b].data_ptr(), self.n)
+
     def _bind(self, k):
         ctx, W, H, F = self.ctx, self.W, self.H, self.F
+        self.bind_rows(k & 1)
         f0 = self.first_frame(k)
         for j in range(F):
             ctx.bind_picture_device(ORG0 + j, self.org[k * F + j].data_ptr(), W, W, H)
@@ -273,6 +287,8 @@ class FrameReplay:
             if k >= 2:
                 cp.wait_event(self.ev_comp[b])            # step k-2 is done with the slot
             _memcpy_async(self.d_jobs[b], self.h_jobs, self.h_jobs.numel(), H2D, cp)
+            if self.rows is not None:
+                _memcpy_async(self.d_rows[b], self.h_rows, self.h_rows.numel(), H2D, cp)
             if self.kreqs is not None:
                 _memcpy_async(self.d_kreqs[b], self.h_kreqs, self.h_kreqs.numel(), H2D, cp)
             self._upload_run(self.org, k * F, f0, F, cp)
