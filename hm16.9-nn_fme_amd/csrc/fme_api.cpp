@@ -21,6 +21,12 @@
 
 using namespace fme;
 
+// 1: the search hands its records to the tail in class order (contiguous per tile, read back
+// through k_scatter's ipos); 0: in call order, straight into the caller's results (A/B).
+#ifndef FME_SORTED_RECS
+#define FME_SORTED_RECS 1
+#endif
+
 namespace {
 
 thread_local std::string g_last_error = "";
@@ -119,6 +125,8 @@ struct fme_ctx {
   DevBuf<fme_mv_result> d_mv;   // staging for fme_refine_mv
   DevBuf<uint8_t> cls;
   DevBuf<int32_t> perm;
+  DevBuf<int32_t> ipos;        // job -> position in perm (class-order record hand-off)
+  DevBuf<fme_result> srec;     // the search's records in class order
   DevBuf<fme_job> sjobs;
   DevBuf<int32_t> counts;      // 25 counts, 24 cursors, 24 tile-queue heads: one memset
   DevBuf<int32_t> blk_agg;
@@ -266,6 +274,7 @@ int fme_destroy(fme_ctx* c) {
   c->d_pics.release(); c->d_mlambda.release(); c->d_keys.release(); c->d_nn.release(); c->d_net.release();
   c->d_jobs.release(); c->d_res.release(); c->d_mv.release(); c->cls.release(); c->perm.release(); c->sjobs.release();
   c->counts.release(); c->blk_agg.release(); c->blk_prefix.release(); c->nn_state.release();
+  c->ipos.release(); c->srec.release();
   c->d_sched.release();
   if (c->ev_done) (void)hipEventDestroy(c->ev_done);
   c->single_pic.release(); c->single_scratch.release(); c->single_job.release(); c->single_res.release();
@@ -544,6 +553,10 @@ static int ensure_work(fme_ctx* c, int n) {
   HIP_TRY(c->sjobs.reserve(n));
   HIP_TRY(c->blk_agg.reserve(nb * 9));
   HIP_TRY(c->blk_prefix.reserve(nb * 9));
+  if (FME_SORTED_RECS) {
+    HIP_TRY(c->ipos.reserve(n));
+    HIP_TRY(c->srec.reserve(n));
+  }
   return FME_OK;
 }
 
@@ -560,6 +573,7 @@ static WorkBufs work_bufs(fme_ctx* c) {
   w.nn_state = c->nn_state.p;
   w.sched = c->d_sched.p;
   w.mv_out = nullptr;
+  w.ipos = c->ipos.p;
   return w;
 }
 
@@ -645,6 +659,7 @@ static int refine_batch(fme_ctx* c, const fme_job* d_jobs, fme_result* d_res, fm
   a.nn_mode = c->cfg.nn_mode ? 1 : 0;
   a.nn_in = c->nn_in;
   a.nn_in_cap = c->nn_in_cap;
+  a.srec = FME_SORTED_RECS ? c->srec.p : nullptr;
   WorkBufs w = work_bufs(c);
   w.mv_out = d_mv;
 
@@ -1413,11 +1428,20 @@ struct BPu {
   uint32_t cost_v1, bits_v1;
   int16_t mv_v1[2];
   int ridx_v1;
-  int L;            // list of the bi-pred search
+  int L;            // list of the current bi-pred iteration
   uint32_t mot[2];  // uiMotBits
   int bi0;          // first bi job of this request in the round's list
-  int stage;        // 0 waiting, 1 bi-pred search issued, 2 decided
+  int stage;        // 0 waiting, 1 bi-pred iteration issued, 2 decided, 3 next iteration due
   int last_mode;    // uiLastMode after this request's decision
+  // bi-pred iteration state (3871-4022)
+  int it, niter;
+  int16_t mvbi[2][2];
+  int ridxbi[2];
+  int mvpibi[2][FME_MAX_REFS];
+  uint32_t cost_bi, bits_bi;
+  int ps_ref[2];          // m_acYuvPred[l]: the reference and MV list l's stored prediction used
+  int16_t ps_mv[2][2];
+  int bip_ref, bip_mvp;   // bestBiPRefIdxL1, bestBiPMvpL1 (MvdL1ZeroFlag)
 };
 
 int two_part(int part_size) { return part_size != FME_PART_2Nx2N && part_size != FME_PART_NxN; }
@@ -1740,18 +1764,19 @@ int fme_pred_inter_p(fme_ctx* c, const fme_pu_req* reqs, fme_pu_res* res, int n,
 //      which depends on the previous PU's decision (uiLastMode); the searches never read bits_in,
 //      so the host re-prices each tail exactly (tail_cost);
 //   4. rounds: every request whose uiLastMode is known gets its uni-pred outcome on the host, then
-//      its bi-pred key (k_bi_key), its bi-pred integer searches (xPatternSearch jobs) and one
+//      its next bi-pred iteration's key (k_bi_key), integer searches (xPatternSearch jobs) and one
 //      fme_refine over the uni jobs plus the round's bi jobs in call order: bi jobs read the carried
 //      NN state and write none, so the uni jobs repeat their results and each bi job sees the state
-//      of its position.  The round's decisions give the next requests their uiLastMode (two rounds
-//      at most: only the second PU of a two-PU CU waits).
+//      of its position (a request's iterations all see the state after its own uni jobs).  FEN 1/2
+//      and MvdL1ZeroFlag run one iteration, FEN 0/3 up to four (each on the key of the other list's
+//      current bi-pred best); a request whose iteration changed nothing stops.  The round's
+//      decisions give the next requests their uiLastMode (only the second PU of a two-PU CU waits,
+//      so at most 2 x 4 rounds).
 
 int fme_pred_inter_b(fme_ctx* c, const fme_pu_req_b* reqs, fme_pu_res_b* res, int n, void* stream) {
   if (!c || (n > 0 && (!reqs || !res))) return fail(FME_E_INVALID, "fme_pred_inter_b: null argument");
   if (n <= 0) return n == 0 ? FME_OK : fail(FME_E_INVALID, "fme_pred_inter_b: n = %d", n);
-  if (c->cfg.fast_inter_mode != 1 && c->cfg.fast_inter_mode != 2)
-    return fail(FME_E_UNSUPPORTED, "fme_pred_inter_b: FEN %d (only FEN 1/2: one bi-pred iteration)",
-                c->cfg.fast_inter_mode);
+  const int fen = c->cfg.fast_inter_mode;
   HIP_TRY(hipSetDevice(c->device));
   hipStream_t s = static_cast<hipStream_t>(stream);
   // ---- validation (nothing runs on a bad batch) ----
@@ -1761,7 +1786,7 @@ int fme_pred_inter_b(fme_ctx* c, const fme_pu_req_b* reqs, fme_pu_res_b* res, in
     if (!valid_pu_shape(q.w, q.h) || q.part_size > FME_PART_nRx2N || q.part_idx >= num_parts(q.part_size) ||
         q.org_id >= FME_MAX_PICTURES || !org.luma || q.x + q.w > org.width || q.y + q.h > org.height ||
         q.lambda_id >= FME_MAX_LAMBDAS || !c->lambda_set[q.lambda_id] ||
-        (q.flags & ~(FME_PU_LOSSLESS | FME_PU_FAST_ME_GEN_B | FME_PU_CLIP_BIPRED)))
+        (q.flags & ~(FME_PU_LOSSLESS | FME_PU_FAST_ME_GEN_B | FME_PU_CLIP_BIPRED | FME_PU_MVD_L1_ZERO)))
       return fail(FME_E_INVALID, "fme_pred_inter_b: request %d invalid (shape %dx%d, part %d/%d)", i, q.w, q.h,
                   q.part_size, q.part_idx);
     if (two_part(q.part_size) && q.part_idx == 1 &&
@@ -1787,16 +1812,20 @@ int fme_pred_inter_b(fme_ctx* c, const fme_pu_req_b* reqs, fme_pu_res_b* res, in
   };
   // ---- 1. xEstimateMvPredAMVP template costs over every (request, list, reference) ----
   std::vector<int> amvp((size_t)n * 8, 0);   // chosen AMVP index of (i, l, k) = [i * 8 + l * 4 + k]
+  // *puiDistBiP of list-1 references under MvdL1ZeroFlag (one candidate: its template cost, 4214-4217)
+  std::vector<uint32_t> bipd((size_t)n * 8, 0xFFFFFFFFu);
   {
     std::vector<AmvpTask> tasks;
-    std::vector<int> slot;
+    std::vector<int> slot, nc;
     for (int i = 0; i < n; i++) {
       const fme_pu_req_b& q = reqs[i];
       for (int l = 0; l < 2; l++)
         for (int k = 0; k < q.num_refs[l]; k++) {
-          if (q.n_cand[l][k] < 2) continue;
+          const int m_n = q.n_cand[l][k] >= 2 ? 2 : ((q.flags & FME_PU_MVD_L1_ZERO) && l == 1 ? 1 : 0);
+          if (!m_n) continue;
           slot.push_back(i * 8 + l * 4 + k);
-          for (int m = 0; m < 2; m++)
+          nc.push_back(m_n);
+          for (int m = 0; m < m_n; m++)
             tasks.push_back(AmvpTask{q.x, q.y, q.w, q.h, q.org_id, q.ref_id[l][k], q.cu_x, q.cu_y,
                                      q.cand[l][k][m][0], q.cand[l][k][m][1]});
         }
@@ -1810,16 +1839,17 @@ int fme_pred_inter_b(fme_ctx* c, const fme_pu_req_b* reqs, fme_pu_res_b* res, in
       HIP_TRY(launch_amvp_sad(aa, s));
       HIP_TRY(hipMemcpyAsync(tsad.data(), c->d_amvp_sad.p, tasks.size() * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
       HIP_TRY(hipStreamSynchronize(s));
-      for (size_t t = 0; t < slot.size(); t++) {
+      for (size_t t = 0, base = 0; t < slot.size(); base += nc[t], t++) {
         const double ml = c->mlambda[reqs[slot[t] / 8].lambda_id];
         uint32_t best = 0xFFFFFFFFu;
-        for (int m = 0; m < 2; m++) {   // uiBestCost > uiTmpCost: the first least cost wins
-          const uint32_t cost = (uint32_t)((double)tsad[2 * t + m] + ((double)mvp_idx_bits(m, 2) * ml) / 65536.0);
+        for (int m = 0; m < nc[t]; m++) {   // uiBestCost > uiTmpCost: the first least cost wins
+          const uint32_t cost = (uint32_t)((double)tsad[base + m] + ((double)mvp_idx_bits(m, 2) * ml) / 65536.0);
           if (best > cost) {
             best = cost;
             amvp[slot[t]] = m;
           }
         }
+        bipd[slot[t]] = best;
       }
     }
   }
@@ -1913,10 +1943,17 @@ int fme_pred_inter_b(fme_ctx* c, const fme_pu_req_b* reqs, fme_pu_res_b* res, in
     p.bits_v1 = 0xFFFFFFFFu;
     p.mv_v1[0] = p.mv_v1[1] = 0;
     p.ridx_v1 = 0;
+    p.bip_ref = p.bip_mvp = 0;
     uint32_t cost_l0[FME_MAX_REFS] = {}, bits_l0[FME_MAX_REFS] = {};
+    uint32_t best_bip = 0xFFFFFFFFu;   // bestBiPDist (3805-3810)
     for (int l = 0; l < 2; l++)
       for (int k = 0; k < q.num_refs[l]; k++) {
         int idx = amvp[i * 8 + l * 4 + k];
+        if ((q.flags & FME_PU_MVD_L1_ZERO) && l == 1 && bipd[i * 8 + 4 + k] < best_bip) {
+          best_bip = bipd[i * 8 + 4 + k];
+          p.bip_ref = k;
+          p.bip_mvp = idx;
+        }
         uint32_t b = p.mb[l] + ref_bits(k, q.num_refs[l]) + mvp_idx_bits(idx, 2), cst;
         if (copied(q, l, k)) {   // TEncSearch.cpp:3814-3827
           const int k0 = q.l1_to_l0[k];
@@ -2016,12 +2053,94 @@ int fme_pred_inter_b(fme_ctx* c, const fme_pu_req_b* reqs, fme_pu_res_b* res, in
   std::vector<BiKeyTask> keyt;
   std::vector<int> issued;
   std::vector<fme_result> rs;
+  size_t key_total = 0;
+  // bi-pred setup (3871-3916): uiMotBits, and under MvdL1ZeroFlag list 1 at its best predictor
+  auto bi_setup = [&](int i) {
+    const fme_pu_req_b& q = reqs[i];
+    BPu& p = st[i];
+    std::memcpy(p.mvbi, p.mv, sizeof(p.mvbi));
+    p.ridxbi[0] = p.ridx[0];
+    p.ridxbi[1] = p.ridx[1];
+    std::memcpy(p.mvpibi, p.mvpi, sizeof(p.mvpibi));
+    p.ps_ref[0] = p.ridx[0];
+    p.ps_ref[1] = p.ridx[1];
+    std::memcpy(p.ps_mv, p.mv, sizeof(p.ps_mv));
+    p.cost_bi = 0xFFFFFFFFu;
+    p.mot[0] = p.bits[0] - p.mb[0];
+    if (q.flags & FME_PU_MVD_L1_ZERO) {
+      const int kb = p.bip_ref;
+      p.mvpibi[1][kb] = p.bip_mvp;
+      p.mvbi[1][0] = p.ps_mv[1][0] = p.mvt[1][kb][0] = q.cand[1][kb][p.bip_mvp][0];
+      p.mvbi[1][1] = p.ps_mv[1][1] = p.mvt[1][kb][1] = q.cand[1][kb][p.bip_mvp][1];
+      p.ridxbi[1] = p.ps_ref[1] = kb;
+      p.mot[1] = p.mb[1] + ref_bits(kb, q.num_refs[1]) + mvp_idx_bits(p.bip_mvp, 2);
+    } else {
+      p.mot[1] = p.bits[1] - p.mb[1];
+    }
+    p.bits_bi = p.mb[2] + p.mot[0] + p.mot[1];
+    p.it = 0;
+    p.niter = (fen == 1 || fen == 2 || (q.flags & FME_PU_MVD_L1_ZERO)) ? 1 : 4;
+  };
+  // one iteration's key (the other list's stored prediction, 3946-3952 and 4461-4471) and searches
+  auto bi_issue = [&](int i) {
+    const fme_pu_req_b& q = reqs[i];
+    BPu& p = st[i];
+    const bool l1z = (q.flags & FME_PU_MVD_L1_ZERO) != 0;
+    int L = p.it % 2;
+    if (fen == 1 || fen == 2) L = p.cost[0] <= p.cost[1] ? 1 : 0;   // FASTINTERSEARCH_MODE1/2 (3931-3941)
+    else if (p.it == 0) L = 0;
+    if (p.it == 0 && !l1z) {
+      p.ps_ref[1 - L] = p.ridx[1 - L];
+      p.ps_mv[1 - L][0] = p.mv[1 - L][0];
+      p.ps_mv[1 - L][1] = p.mv[1 - L][1];
+    }
+    if (l1z) L = 0;
+    p.L = L;
+    const int key_off = (int)key_total;
+    key_total += (size_t)q.w * q.h;
+    keyt.push_back(BiKeyTask{q.x, q.y, q.w, q.h, q.org_id, q.ref_id[1 - L][p.ps_ref[1 - L]], q.cu_x, q.cu_y,
+                             p.ps_mv[1 - L][0], p.ps_mv[1 - L][1], key_off,
+                             (q.flags & FME_PU_CLIP_BIPRED) ? 1u : 0u});
+    const PicDesc& org = c->pics[q.org_id];
+    const int brange = q.bipred_range ? q.bipred_range : 4;
+    p.bi0 = (int)bj.size();
+    for (int k = 0; k < q.num_refs[L]; k++) {
+      const int m = p.mvpibi[L][k];
+      // xSetSearchRange around cMvTemp[L][k], the last ME result of (L, k) (4486-4490)
+      int cx = p.mvt[L][k][0], cy = p.mvt[L][k][1];
+      clip_qpel(cx, cy, org.width, org.height, q.cu_x, q.cu_y);
+      int lx = cx - (brange << 2), ly = cy - (brange << 2), rx = cx + (brange << 2), ry = cy + (brange << 2);
+      clip_qpel(lx, ly, org.width, org.height, q.cu_x, q.cu_y);
+      clip_qpel(rx, ry, org.width, org.height, q.cu_x, q.cu_y);
+      fme_job j{};
+      j.x = q.x; j.y = q.y; j.w = q.w; j.h = q.h;
+      j.org_id = q.org_id; j.ref_id = q.ref_id[L][k];
+      j.mvp_x = q.cand[L][k][m][0]; j.mvp_y = q.cand[L][k][m][1];
+      j.lt_x = (int16_t)round4(lx); j.lt_y = (int16_t)round4(ly);
+      j.rb_x = (int16_t)round4(rx); j.rb_y = (int16_t)round4(ry);
+      j.flags = (uint8_t)(FME_JOB_BIPRED | ((q.flags & FME_PU_LOSSLESS) ? FME_JOB_LOSSLESS : 0u));
+      j.lambda_id = q.lambda_id;
+      j.bits_in = (uint16_t)(p.mb[2] + p.mot[1 - L] + ref_bits(k, q.num_refs[L]) + mvp_idx_bits(m, 2));
+      j.key_offset = key_off;
+      fme_tz_ext e{};
+      e.cu_x = q.cu_x; e.cu_y = q.cu_y;
+      e.search_range = (uint8_t)brange;
+      bj.push_back(j);
+      be.push_back(e);
+    }
+    p.stage = 1;
+    issued.push_back(i);
+  };
   for (;;) {
     bj.clear(); be.clear(); keyt.clear(); issued.clear();
-    size_t key_total = 0;
+    key_total = 0;
     for (int i = 0; i < n; i++) {
       const fme_pu_req_b& q = reqs[i];
       BPu& p = st[i];
+      if (p.stage == 3) {
+        bi_issue(i);
+        continue;
+      }
       if (p.stage != 0) continue;
       const bool dep = two_part(q.part_size) && q.part_idx == 1;
       if (dep && st[i - 1].stage != 2) continue;   // uiLastMode not known yet
@@ -2032,45 +2151,8 @@ int fme_pred_inter_b(fme_ctx* c, const fme_pu_req_b* reqs, fme_pu_res_b* res, in
         decide(i, mvbi, p.ridx, p.mvpi);
         continue;
       }
-      // bi-pred setup (3871-3916) and the other list's prediction -> key (3946-3952, 4461-4471)
-      p.mot[0] = p.bits[0] - p.mb[0];
-      p.mot[1] = p.bits[1] - p.mb[1];
-      const int L = p.cost[0] <= p.cost[1] ? 1 : 0;   // FASTINTERSEARCH_MODE1/2 (3931-3941)
-      p.L = L;
-      const int key_off = (int)key_total;
-      key_total += (size_t)q.w * q.h;
-      keyt.push_back(BiKeyTask{q.x, q.y, q.w, q.h, q.org_id, q.ref_id[1 - L][p.ridx[1 - L]], q.cu_x, q.cu_y,
-                               p.mv[1 - L][0], p.mv[1 - L][1], key_off,
-                               (q.flags & FME_PU_CLIP_BIPRED) ? 1u : 0u});
-      const PicDesc& org = c->pics[q.org_id];
-      const int brange = q.bipred_range ? q.bipred_range : 4;
-      p.bi0 = (int)bj.size();
-      for (int k = 0; k < q.num_refs[L]; k++) {
-        const int m = p.mvpi[L][k];
-        // xSetSearchRange around the reference's uni-pred MV (4486-4490)
-        int cx = p.mvt[L][k][0], cy = p.mvt[L][k][1];
-        clip_qpel(cx, cy, org.width, org.height, q.cu_x, q.cu_y);
-        int lx = cx - (brange << 2), ly = cy - (brange << 2), rx = cx + (brange << 2), ry = cy + (brange << 2);
-        clip_qpel(lx, ly, org.width, org.height, q.cu_x, q.cu_y);
-        clip_qpel(rx, ry, org.width, org.height, q.cu_x, q.cu_y);
-        fme_job j{};
-        j.x = q.x; j.y = q.y; j.w = q.w; j.h = q.h;
-        j.org_id = q.org_id; j.ref_id = q.ref_id[L][k];
-        j.mvp_x = q.cand[L][k][m][0]; j.mvp_y = q.cand[L][k][m][1];
-        j.lt_x = (int16_t)round4(lx); j.lt_y = (int16_t)round4(ly);
-        j.rb_x = (int16_t)round4(rx); j.rb_y = (int16_t)round4(ry);
-        j.flags = (uint8_t)(FME_JOB_BIPRED | ((q.flags & FME_PU_LOSSLESS) ? FME_JOB_LOSSLESS : 0u));
-        j.lambda_id = q.lambda_id;
-        j.bits_in = (uint16_t)(p.mb[2] + p.mot[1 - L] + ref_bits(k, q.num_refs[L]) + mvp_idx_bits(m, 2));
-        j.key_offset = key_off;
-        fme_tz_ext e{};
-        e.cu_x = q.cu_x; e.cu_y = q.cu_y;
-        e.search_range = (uint8_t)brange;
-        bj.push_back(j);
-        be.push_back(e);
-      }
-      p.stage = 1;
-      issued.push_back(i);
+      bi_setup(i);
+      bi_issue(i);
     }
     if (issued.empty()) break;
     // keys, bi-pred integer searches, then the sub-pel path over uni + bi jobs in call order
@@ -2108,33 +2190,52 @@ int fme_pred_inter_b(fme_ctx* c, const fme_pu_req_b* reqs, fme_pu_res_b* res, in
       fme_pu_res_b& o = res[i];
       const double ml = c->mlambda[q.lambda_id];
       const int L = p.L;
-      int16_t mvbi[2][2] = {{p.mv[0][0], p.mv[0][1]}, {p.mv[1][0], p.mv[1][1]}};
-      int ridxbi[2] = {p.ridx[0], p.ridx[1]};
-      int mvpibi[2][FME_MAX_REFS];
-      std::memcpy(mvpibi, p.mvpi, sizeof(mvpibi));
-      uint32_t cost_bi = 0xFFFFFFFFu, bits_bi = p.mb[2] + p.mot[0] + p.mot[1];
+      bool changed = false;
+      std::memset(o.bi_ref_cost, 0, sizeof(o.bi_ref_cost));
+      std::memset(o.bi_ref_mv, 0, sizeof(o.bi_ref_mv));
       for (int k = 0; k < q.num_refs[L]; k++) {
         const fme_result& r = rs[pos[t2] + k];
+        p.mvt[L][k][0] = r.mv_x;
+        p.mvt[L][k][1] = r.mv_y;
         uint32_t b = r.bits, cst = r.cost;
-        int idx = mvpibi[L][k];
+        int idx = p.mvpibi[L][k];
         check_best_mvp(ml, q.cand[L][k], q.n_cand[L][k], r.mv_x, r.mv_y, idx, b, cst);
-        mvpibi[L][k] = idx;
+        p.mvpibi[L][k] = idx;
         o.bi_ref_cost[k] = cst;
         o.bi_ref_mv[k][0] = r.mv_x;
         o.bi_ref_mv[k][1] = r.mv_y;
-        if (cst < cost_bi) {   // 3985-3995
-          mvbi[L][0] = r.mv_x;
-          mvbi[L][1] = r.mv_y;
-          ridxbi[L] = k;
-          cost_bi = cst;
+        if (cst < p.cost_bi) {   // 3985-4005
+          changed = true;
+          p.mvbi[L][0] = r.mv_x;
+          p.mvbi[L][1] = r.mv_y;
+          p.ridxbi[L] = k;
+          p.cost_bi = cst;
           p.mot[L] = b - p.mb[2] - p.mot[1 - L];
-          bits_bi = b;
+          p.bits_bi = b;
+          if (p.niter != 1) {   // setAllMv + motionCompensation of list L
+            p.ps_ref[L] = k;
+            p.ps_mv[L][0] = r.mv_x;
+            p.ps_mv[L][1] = r.mv_y;
+          }
         }
       }
       o.bi_list = (uint8_t)L;
-      o.bi_cost = cost_bi;
-      o.bi_bits = bits_bi;
-      decide(i, mvbi, ridxbi, mvpibi);
+      o.bi_iters = (uint8_t)(p.it + 1);
+      if (changed && p.it + 1 < p.niter) {
+        p.it++;
+        p.stage = 3;
+        continue;
+      }
+      if (!changed && p.cost_bi <= p.cost[0] && p.cost_bi <= p.cost[1]) {   // 4008-4021
+        for (int l = 0; l < ((q.flags & FME_PU_MVD_L1_ZERO) ? 1 : 2); l++) {
+          const int k = p.ridxbi[l];
+          check_best_mvp(ml, q.cand[l][k], q.n_cand[l][k], p.mvbi[l][0], p.mvbi[l][1], p.mvpibi[l][k], p.bits_bi,
+                         p.cost_bi);
+        }
+      }
+      o.bi_cost = p.cost_bi;
+      o.bi_bits = p.bits_bi;
+      decide(i, p.mvbi, p.ridxbi, p.mvpibi);
     }
   }
   // ---- m_integerMv2Nx2N: the last 2Nx2N request's post-EMI integer MV per (list, reference) ----

@@ -96,6 +96,11 @@ struct BatchArgs {
                               // whose jobs read keys are rejected (k_classify)
   const uint32_t* nn_in;      // NN input rows of FME_JOB_NN_IN jobs ([nn_in_cap][9]) or null
   int32_t nn_in_cap;
+  // The search -> tail hand-off: the search writes each tile's records contiguously in class
+  // order (srec[q], q = the job's position in perm) and the tails read them through
+  // WorkBufs::ipos (job -> q), so no record leaves as scattered half lines.  Null: the records go
+  // to res in call order (the single-PU kernels).
+  fme_result* srec;
 };
 
 struct Schedule;
@@ -113,7 +118,12 @@ struct WorkBufs {
   Schedule* sched;       // built on the device by k_schedule from counts
   int32_t* tile_ctr;     // [8] lane-kernel tile queue heads (zeroed with counts)
   fme_mv_result* mv_out; // compact per-job output (fme_refine_mv*), or null
+  int32_t* ipos;         // [n] position of job i in perm (written by k_scatter; BatchArgs::srec)
 };
+// The search record of job i (class order through ipos, or call order).
+__device__ __forceinline__ const fme_result* search_rec(const BatchArgs& a, const WorkBufs& w, int i) {
+  return a.srec ? a.srec + w.ipos[i] : a.res + i;
+}
 
 // Schedule of the search kernel (k_schedule builds it on the device): class c's jobs are
 // sjobs/perm[class_off[c] .. + class_cnt[c]) and its 64-lane wave tiles [prefix[c], prefix[c+1]).
@@ -239,8 +249,11 @@ __device__ __forceinline__ int nn_pushes(const fme_job& j) {
 }
 __device__ __forceinline__ bool nn_writes_c(const fme_job& j) { return (j.flags & (FME_JOB_EMI | FME_JOB_NN_IN)) != 0; }
 
-__device__ __forceinline__ void store_outputs(fme_result* r, fme_mv_result* mv_out, int i, int fx, int fy,
-                                              uint32_t cost, uint32_t bits, uint8_t cls, uint16_t status) {
+// r: the job's record in call order (full-record output); src: its search record (== r when the
+// search wrote in call order): with a class-order hand-off the whole record is written here.
+__device__ __forceinline__ void store_outputs(fme_result* r, const fme_result* src, fme_mv_result* mv_out, int i,
+                                              int fx, int fy, uint32_t cost, uint32_t bits, uint8_t cls,
+                                              uint16_t status) {
   if (mv_out) {
     fme_mv_result o;
     o.mv_x = (int16_t)fx;
@@ -252,6 +265,7 @@ __device__ __forceinline__ void store_outputs(fme_result* r, fme_mv_result* mv_o
     o.status = status;
     mv_out[i] = o;
   } else {
+    if (src != r) *r = *src;
     r->mv_x = (int16_t)fx;
     r->mv_y = (int16_t)fy;
     r->cost = cost;

@@ -224,6 +224,7 @@ __global__ __launch_bounds__(kBlock) void k_scatter(BatchArgs a, WorkBufs w) {
       const int dst = sc->class_off[cls[q]] + basep[cls[q]] + rank[q];
       w.perm[dst] = i;
       w.sjobs[dst] = jb[q];
+      if (a.srec) w.ipos[i] = dst;
     }
   }
   // Exclusive prefix-max of the NN-writer aggregates over the blocks before this one: k_nn_tail's
@@ -388,6 +389,7 @@ __device__ __forceinline__ void tail_job(const BatchArgs& a, const WorkBufs& w, 
   const uint32_t* st_in = w.nn_state + 12 * state_in;
   uint32_t* st_out = w.nn_state + 12 * (state_in ^ 1);
   fme_result* r = a.res + i;
+  const fme_result* sr = search_rec(a, w, i);
   const double ml = a.mlambda[j.lambda_id];
   const int mvx = (int16_t)(r0.x & 0xFFFF), mvy = (int16_t)(r0.x >> 16);
   const uint32_t own_emi[8] = {r1.w, r2.x, r2.y, r2.z, r2.w, r3.x, r3.y, r3.z};
@@ -403,7 +405,7 @@ __device__ __forceinline__ void tail_job(const BatchArgs& a, const WorkBufs& w, 
         e[s] = own_emi[s];
         written |= 1u << s;
       } else if (src[s] >= 0) {
-        e[s] = a.res[src[s]].emi[s];
+        e[s] = search_rec(a, w, src[s])->emi[s];
         written |= 1u << s;
       } else {
         e[s] = st_in[s];
@@ -416,7 +418,7 @@ __device__ __forceinline__ void tail_job(const BatchArgs& a, const WorkBufs& w, 
       pw = j.w;
       written |= 0x100u;
     } else if (src[8] >= 0) {
-      c = a.res[src[8]].c;
+      c = search_rec(a, w, src[8])->c;
       ph = a.jobs[src[8]].h;
       pw = a.jobs[src[8]].w;
       written |= 0x100u;
@@ -450,7 +452,7 @@ __device__ __forceinline__ void tail_job(const BatchArgs& a, const WorkBufs& w, 
   const double fw = (j.flags & FME_JOB_BIPRED) ? 0.5 : 1.0;
   const double val = floor(fw * ((double)frac_cost - (double)mv_cost(ml, mvb))) + (double)mv_cost(ml, bits);
   // gcc/x86-64 (Distortion)(double) semantics for the cost
-  store_outputs(r, w.mv_out, i, fx, fy, (uint32_t)(int64_t)val, bits, (uint8_t)cls, status);
+  store_outputs(r, sr, w.mv_out, i, fx, fy, (uint32_t)(int64_t)val, bits, (uint8_t)cls, status);
 }
 
 // One lane per job; a block scans one 1024-job block (kJobsPerScanBlock, the granularity of
@@ -487,7 +489,7 @@ void k_nn_tail(BatchArgs a, WorkBufs w, const float* __restrict__ nnp_g, int sta
     u32x4 r0{}, r1{}, r2{}, r3{};
     if (valid) {
       j = a.jobs[i];
-      const u32x4* rb = reinterpret_cast<const u32x4*>(a.res + i);
+      const u32x4* rb = reinterpret_cast<const u32x4*>(search_rec(a, w, i));
       r0 = rb[0];
       r1 = rb[1];
       r2 = rb[2];
@@ -560,6 +562,9 @@ __global__ __launch_bounds__(64) void k_nn_single(const float* __restrict__ Q, N
 #pragma unroll
     for (int k = 0; k < 20; k++) x = x + ld2(Q, kNnPkW3 + (rp * 20 + k) * 2) * (f2){s_x2[k], s_x2[k]};
     x = x + ld2(Q, kNnPkBout + 2 * rp);
+    // the batch rule's NaNs (row 0 taken first, then strict >): a NaN row 0 wins, a later NaN never
+    if (x.x != x.x) x.x = rp == 0 ? INFINITY : -INFINITY;
+    if (x.y != x.y) x.y = -INFINITY;
     bv = x.x;
     bi = 2 * rp;
     if (rp < 24 && x.y > bv) {

@@ -67,6 +67,12 @@
 #ifndef FME_LANE_WAVES
 #define FME_LANE_WAVES 2
 #endif
+// 1: one unit per lane loads ONE window, rows -5..UH+4 and cols -5..UW+4 around the TZ MV, for both
+// the EMI step and the sub-pel passes (re-centred on the EMI best in registers: a row select and a
+// byte shift per dword); 0: the EMI window, then a second, dependent load around mv_int'.
+#ifndef FME_LANE_BIGWIN
+#define FME_LANE_BIGWIN 1
+#endif
 
 namespace fme {
 namespace {
@@ -740,17 +746,13 @@ __device__ __forceinline__ void load_window(const PicDesc& pic, int x0, int y0, 
 // instead of a dependent global load before its window loads.
 __shared__ PicDesc g_pics[FME_MAX_PICTURES];
 __shared__ double g_ml[FME_MAX_LAMBDAS];
-// Record staging (FME_LANE_REC_LDS): each PU's 64-byte fme_result is assembled in LDS by the PU's
-// first lane, then the wave writes the tile's records with four lanes per record, so every store
-// instruction writes whole 64-byte lines (one lane per record wrote four separate 16-byte pieces:
-// 256 bytes of WRITE_SIZE per job).
-#ifndef FME_LANE_REC_LDS
-#define FME_LANE_REC_LDS 1
-#endif
-#if FME_LANE_REC_LDS
+// Record staging: each PU's 64-byte fme_result is assembled in LDS by the PU's first lane, then
+// the wave writes the tile's records with four lanes per record, so every store instruction writes
+// whole 64-byte lines (one lane per record wrote four separate 16-byte pieces: 256 bytes of
+// WRITE_SIZE per job); in class order (BatchArgs::srec) a tile's records are also contiguous.
 __shared__ uint4 g_rec[256 / 64][64][4];
 __shared__ int32_t g_rec_jid[256 / 64][64];
-#endif
+
 
 // Global pointers typed as such (global_load / global_store, not flat).
 typedef __attribute__((address_space(1))) const fme_job g_job;
@@ -776,7 +778,7 @@ __device__ FME_LANE_UNIT_ATTR void lane_unit(const BatchArgs& a, const fme_job* 
                                              int wt) {
   g_job* const sjobs = (g_job*)sjobs_;
   g_i32* const perm = (g_i32*)perm_;
-  g_res* const res = (g_res*)a.res;
+  g_res* const outp = (g_res*)(a.srec ? a.srec : a.res);   // where this kernel's records go
   g_i16* const keys = (g_i16*)a.keys;
   const int use_hadamard = a.use_hadamard, fen = a.fen;
   constexpr int T = ((PW % 8) == 0 && (PH % 8) == 0) ? 8 : 4;
@@ -854,6 +856,11 @@ __device__ FME_LANE_UNIT_ATTR void lane_unit(const BatchArgs& a, const fme_job* 
   // one unit per lane: its key rows are loaded once, for the EMI step and the sub-pel passes
   uint32_t kraw0[UH][KW];
   if constexpr (UPL == 1) load_kraw(0, kraw0);
+  // FME_LANE_BIGWIN: the whole neighbourhood the EMI step can move to, loaded with the key
+  constexpr bool kBig = FME_LANE_BIGWIN && UPL == 1;
+  constexpr int BR = kBig ? UH + 10 : 1;   // rows -5 .. UH+4
+  uint32_t bw[BR][4];                       // cols -5 .. UW+4 (14 of 16 bytes)
+  if constexpr (kBig) load_window(ref, ox + (int)j.mv_x - 5, oy + (int)j.mv_y - 5, bw);
 
   // ---- 1. EMI square step -----------------------------------------------------------------------
   int mvx = j.mv_x, mvy = j.mv_y;
@@ -876,9 +883,15 @@ __device__ FME_LANE_UNIT_ATTR void lane_unit(const BatchArgs& a, const fme_job* 
       } else {
         load_kraw(h, kraw);
       }
-      // integer samples at rows -1 .. UH, cols -1 .. UW around the TZ MV (s - 128 bytes)
-      uint32_t w[UH + 2][EW];
-      load_window(ref, ox + mvx - 1, oy + h * kHalfRows + mvy - 1, w);
+      // integer samples at rows -1 .. UH, cols -1 .. UW around the TZ MV (s - 128 bytes); with the
+      // big window: its rows 4 .. UH+5, bytes 4 .. (EMI offset e -> bytes 4 + e of bw)
+      constexpr int EO = kBig ? 4 : 0;   // window offset of row / column -1
+      uint32_t w[kBig ? 1 : UH + 2][kBig ? 4 : EW];
+      if constexpr (!kBig) load_window(ref, ox + mvx - 1, oy + h * kHalfRows + mvy - 1, w);
+      auto wrow = [&](int r) FME_AI -> const auto& {
+        if constexpr (kBig) return bw[r + EO];
+        else return w[r];
+      };
       int so2 = 0;   // SSE's sum of squared key samples
 #pragma unroll
       for (int r = 0; r < UH; r++)
@@ -897,7 +910,7 @@ __device__ FME_LANE_UNIT_ATTR void lane_unit(const BatchArgs& a, const fme_job* 
             if ((r & 1) && sub) continue;   // unit rows start on even PU rows
 #pragma unroll
             for (int k = 0; k < UW / 4; k++) {
-              const uint32_t pv = rbytes(w[r + 1 + dy], 1 + dx + 4 * k) ^ 0x80808080u;   // samples 0..255
+              const uint32_t pv = rbytes(wrow(r + 1 + dy), EO + 1 + dx + 4 * k) ^ 0x80808080u;   // samples 0..255
               if (!kbuf) {
                 e = __builtin_amdgcn_sad_u8(kraw[r][k] ^ 0x80808080u, pv, e);
               } else {   // int16 key: |key - pred| per sample
@@ -912,7 +925,7 @@ __device__ FME_LANE_UNIT_ATTR void lane_unit(const BatchArgs& a, const fme_job* 
           for (int r = 0; r < UH; r++)
 #pragma unroll
             for (int k = 0; k < UW / 4; k++) {
-              const uint32_t pv = rbytes(w[r + 1 + dy], 1 + dx + 4 * k);
+              const uint32_t pv = rbytes(wrow(r + 1 + dy), EO + 1 + dx + 4 * k);
               sop = dot4(kraw[r][k], pv, sop);
               spp = dot4(pv, pv, spp);
             }
@@ -922,7 +935,7 @@ __device__ FME_LANE_UNIT_ATTR void lane_unit(const BatchArgs& a, const fme_job* 
           for (int r = 0; r < UH; r++)
 #pragma unroll
             for (int k = 0; k < UW / 4; k++) {
-              const uint32_t x = rbytes(w[r + 1 + dy], 1 + dx + 4 * k) ^ 0x80808080u;   // samples 0..255
+              const uint32_t x = rbytes(wrow(r + 1 + dy), EO + 1 + dx + 4 * k) ^ 0x80808080u;   // samples 0..255
               const uint32_t d0 = pk_sub(kraw[r][2 * k], lo_pair(x)), d1 = pk_sub(kraw[r][2 * k + 1], hi_pair(x));
               e = (uint32_t)dot2(d1, d1, dot2(d0, d0, (int)e));
             }
@@ -983,35 +996,34 @@ __device__ FME_LANE_UNIT_ATTR void lane_unit(const BatchArgs& a, const fme_job* 
     n_emi = 8;
   }
   typedef __attribute__((address_space(1))) u32x4a gw4;
-#if FME_LANE_REC_LDS
   const int wid = (int)threadIdx.x >> 6;
   if (u == 0) {   // bytes 16..63 of the record: cost, bits (NN tail), c, emi[8], n_emi
     g_rec[wid][lane][1] = make_uint4(0u, 0u, cval, emi[0]);
     g_rec[wid][lane][2] = make_uint4(emi[1], emi[2], emi[3], emi[4]);
     g_rec[wid][lane][3] = make_uint4(emi[5], emi[6], emi[7], (uint32_t)n_emi);
-    g_rec_jid[wid][lane] = active ? jid : -1;
+    // destination record: class order (the tile's records contiguous) or call order
+    g_rec_jid[wid][lane] = !active ? -1 : (a.srec ? cls_off + p : jid);
   }
-#else
-  __attribute__((address_space(1))) uint8_t* const rec = reinterpret_cast<__attribute__((address_space(1))) uint8_t*>(res + jid);
-  if (active && u == 0) {   // bytes 16..63 of the record: cost, bits (NN tail), c, emi[8], n_emi
-    u32x4a q0, q1, q2;
-    q0.x = 0; q0.y = 0; q0.z = cval; q0.w = emi[0];
-    q1.x = emi[1]; q1.y = emi[2]; q1.z = emi[3]; q1.w = emi[4];
-    q2.x = emi[5]; q2.y = emi[6]; q2.z = emi[7]; q2.w = (uint32_t)n_emi;
-    *(gw4*)(rec + 16) = q0;
-    *(gw4*)(rec + 32) = q1;
-    *(gw4*)(rec + 48) = q2;
-  }
-#endif
-  (void)ex;
-  (void)ey;
+
 
   // ---- the resident half: window rows -4..UH+3, cols -4..UW+3 around mv_int', and the key as
   // signed int16 (key - 128) pairs K[c][j] = (row 2j, row 2j+1) of column c ----------------------
   uint32_t v[RV][NV];
   KeySrc<UW, UJ> K;
   auto load_half = [&](int h) FME_AI {
-    load_window(ref, ox + mvx - 4, oy + h * kHalfRows + mvy - 4, v);
+    if constexpr (kBig) {   // re-centre the big window on mv_int' = TZ MV + (ex, ey)
+      const uint32_t sh = (uint32_t)(1 + ex);
+#pragma unroll
+      for (int r = 0; r < RV; r++) {
+        uint32_t row[4];
+#pragma unroll
+        for (int k = 0; k < 4; k++) row[k] = ey < 0 ? bw[r][k] : (ey == 0 ? bw[r + 1][k] : bw[r + 2][k]);
+#pragma unroll
+        for (int k = 0; k < NV; k++) v[r][k] = __builtin_amdgcn_alignbyte(row[k + 1], row[k], sh);
+      }
+    } else {
+      load_window(ref, ox + mvx - 4, oy + h * kHalfRows + mvy - 4, v);
+    }
     uint32_t kraw[UH][KW];
     if constexpr (UPL == 1) {
 #pragma unroll
@@ -1113,7 +1125,6 @@ __device__ FME_LANE_UNIT_ATTR void lane_unit(const BatchArgs& a, const fme_job* 
   const uint32_t r_mv = (uint32_t)(uint16_t)mvx | ((uint32_t)(uint16_t)mvy << 16);
   const uint32_t r_hq = (uint32_t)(uint8_t)hx | ((uint32_t)(uint8_t)hy << 8) | ((uint32_t)(uint8_t)q9_dx(bq) << 16) |
                         ((uint32_t)(uint8_t)q9_dy(bq) << 24);
-#if FME_LANE_REC_LDS
   if (u == 0) g_rec[wid][lane][0] = make_uint4(r_mv, 0u, r_hq, qbest);
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
@@ -1130,20 +1141,11 @@ __device__ FME_LANE_UNIT_ATTR void lane_unit(const BatchArgs& a, const fme_job* 
         const uint4 q = g_rec[wid][src][lane & 3];
         u32x4a o;
         o.x = q.x; o.y = q.y; o.z = q.z; o.w = q.w;
-        *(gw4*)(reinterpret_cast<__attribute__((address_space(1))) uint8_t*>(res + rj) + 16 * (lane & 3)) = o;
+        *(gw4*)(reinterpret_cast<__attribute__((address_space(1))) uint8_t*>(outp + rj) + 16 * (lane & 3)) = o;
       }
     }
   }
-#else
-  if (active && u == 0) {
-    u32x4a q;
-    q.x = r_mv;
-    q.y = 0;
-    q.z = r_hq;
-    q.w = qbest;
-    *(gw4*)rec = q;
-  }
-#endif
+
 }
 
 // The XCD this wave runs on (HW_REG_XCC_ID, gfx940+: bits 3:0).

@@ -325,10 +325,10 @@ __global__ __launch_bounds__(kRound) void k_nn_deep_tail(BatchArgs a, WorkBufs w
 #pragma unroll
     for (int s = 0; s < 8; s++) {
       if (reset) {
-        e[s] = (valid && src[s] == i) ? a.res[i].emi[s] : 0u;
+        e[s] = (valid && src[s] == i) ? search_rec(a, w, i)->emi[s] : 0u;
         written |= 1u << s;
       } else if (src[s] >= 0) {
-        e[s] = valid ? a.res[src[s]].emi[s] : 0u;
+        e[s] = valid ? search_rec(a, w, src[s])->emi[s] : 0u;
         written |= 1u << s;
       } else {
         e[s] = st_in[s];
@@ -336,7 +336,7 @@ __global__ __launch_bounds__(kRound) void k_nn_deep_tail(BatchArgs a, WorkBufs w
     }
     uint32_t c = st_in[8], ph = st_in[9], pw = st_in[10];
     if (src[8] >= 0 && valid) {
-      c = a.res[src[8]].c;
+      c = search_rec(a, w, src[8])->c;
       ph = a.jobs[src[8]].h;
       pw = a.jobs[src[8]].w;
       written |= 0x100u;
@@ -362,8 +362,9 @@ __global__ __launch_bounds__(kRound) void k_nn_deep_tail(BatchArgs a, WorkBufs w
     const int cls = nn_argmax(out, d.out_act, d.margin ? d.margin + i : nullptr);
 
     fme_result* r = a.res + i;
+    const fme_result* sr = search_rec(a, w, i);
     uint16_t status = 0;
-    if (!nn_writes_c(j) || r->n_emi < 8) status |= FME_RES_NN_STALE;
+    if (!nn_writes_c(j) || sr->n_emi < 8) status |= FME_RES_NN_STALE;
     if ((written & 0x1FFu) != 0x1FFu) status |= FME_RES_NN_UNINIT;
     if (i == a.n - 1) {
 #pragma unroll
@@ -373,14 +374,14 @@ __global__ __launch_bounds__(kRound) void k_nn_deep_tail(BatchArgs a, WorkBufs w
       st_out[10] = pw;
       st_out[11] = written;
     }
-    const int fx = 4 * r->mv_int_x + cls % 7 - 3, fy = 4 * r->mv_int_y + cls / 7 - 3;
+    const int fx = 4 * sr->mv_int_x + cls % 7 - 3, fy = 4 * sr->mv_int_y + cls / 7 - 3;
     const double ml = a.mlambda[j.lambda_id];
     const uint32_t mvb = mv_bits(fx, fy, 0, j.mvp_x, j.mvp_y);
     const uint32_t bits = (uint32_t)j.bits_in + mvb;
     const double fw = (j.flags & FME_JOB_BIPRED) ? 0.5 : 1.0;
-    const double val = floor(fw * ((double)r->frac_cost - (double)mv_cost(ml, mvb))) + (double)mv_cost(ml, bits);
+    const double val = floor(fw * ((double)sr->frac_cost - (double)mv_cost(ml, mvb))) + (double)mv_cost(ml, bits);
     // gcc/x86-64 (Distortion)(double) semantics for the cost
-    store_outputs(r, w.mv_out, i, fx, fy, (uint32_t)(int64_t)val, bits, (uint8_t)cls, status);
+    store_outputs(r, sr, w.mv_out, i, fx, fy, (uint32_t)(int64_t)val, bits, (uint8_t)cls, status);
   }
 }
 
@@ -428,6 +429,8 @@ __global__ __launch_bounds__(64) void k_nn_deep_single(DeepArgs d, NnIn11 in11, 
     for (int k = 0; k < kHW; k++) s = s + P[D::kWout + i * kHW + k] * s_x[(NH - 1) & 1][k];
     s = s + P[D::kBout + i];
     if (d.out_act == FME_NN_OUT_SIGMOID) s = (T)1 / ((T)1 + nn_exp(-s));
+    // the serial rule's NaNs (cls = 0, then `best < out[o]`): a NaN row 0 wins, a later NaN never
+    if (s != s) s = i == 0 ? (T)INFINITY : (T)-INFINITY;
     bv = s;
     bi = i;
   }

@@ -100,6 +100,7 @@ assert PU_RES_DTYPE.itemsize == 80
 PU_LOSSLESS = 0x01
 PU_FAST_ME_GEN_B = 0x02
 PU_CLIP_BIPRED = 0x04
+PU_MVD_L1_ZERO = 0x08
 # fme_pu_req_b / fme_pu_res_b (include/fme.h): predInterSearch on a B slice
 PU_REQ_B_DTYPE = np.dtype(
     [
@@ -118,7 +119,7 @@ assert PU_REQ_B_DTYPE.itemsize == 112
 PU_RES_B_DTYPE = np.dtype(
     [
         ("inter_dir", "u1"), ("ref_idx", "u1", (2,)), ("mvp_idx", "u1", (2,)), ("bi_list", "u1"),
-        ("reserved", "<u2"),
+        ("bi_iters", "u1"), ("reserved", "u1"),
         ("mv", "<i2", (2, 2)), ("mvp", "<i2", (2, 2)),
         ("bits", "<u4"), ("cost", "<u4"),
         ("uni_cost", "<u4", (2,)), ("uni_bits", "<u4", (2,)),

@@ -15,7 +15,7 @@ from .weights import load_weights
 PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB_PATH = os.environ.get("FME_LIB_PATH") or os.path.join(PKG_ROOT, "libfme_amd.so")
 
-ABI_VERSION = 11
+ABI_VERSION = 12
 TIMING_NAMES = ("classify", "scatter", "search", "nn_tail", "batch", "search_main", "search_aux")
 
 # Every entry point include/fme.h declares (the ABI test checks the .so exports them).

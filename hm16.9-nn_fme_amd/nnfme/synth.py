@@ -509,12 +509,12 @@ def make_pu_requests(rng, width, height, org_id, ref_ids, lambda_id, max_depth=3
 
 def make_pu_requests_b(rng, width, height, org_id, l0, l1, lambda_id, max_depth=3, amp=12.0, cand_noise=24,
                        one_cand_frac=0.1, lossless_frac=0.0, search_range=SEARCH_RANGE, bipred_range=4,
-                       fast_me_gen_b=True, clip_bipred=False):
+                       fast_me_gen_b=True, clip_bipred=False, mvd_l1_zero=False):
     """fme_pu_req_b stream of a B frame in encoder call order (as make_pu_requests).  l0 / l1: lists
     of (picture slot, signed POC distance) per reference index; an L1 slot that is also in L0 gets
     l1_to_l0 = its L0 index (getList1IdxToList0Idx).  Candidates of a reference lie near the
     motion field scaled by its POC distance."""
-    from .abi import MAX_REFS, PU_CLIP_BIPRED, PU_FAST_ME_GEN_B, PU_LOSSLESS, PU_REQ_B_DTYPE
+    from .abi import MAX_REFS, PU_CLIP_BIPRED, PU_FAST_ME_GEN_B, PU_LOSSLESS, PU_MVD_L1_ZERO, PU_REQ_B_DTYPE
     p = make_pu_requests(rng, width, height, org_id, [0], lambda_id, max_depth=max_depth, amp=amp,
                          search_range=search_range)
     n = len(p)
@@ -537,6 +537,8 @@ def make_pu_requests_b(rng, width, height, org_id, l0, l1, lambda_id, max_depth=
         flags |= PU_FAST_ME_GEN_B
     if clip_bipred:
         flags |= PU_CLIP_BIPRED
+    if mvd_l1_zero:   # a slice-level switch: every request of the frame
+        flags |= PU_MVD_L1_ZERO
     reqs["flags"] = flags
     reqs["num_refs"] = [len(l0), len(l1)]
     reqs["l1_to_l0"] = -1

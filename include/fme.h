@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define FME_ABI_VERSION 11
+#define FME_ABI_VERSION 12
 
 /* ---- error codes ---------------------------------------------------------------- */
 #define FME_OK            0
@@ -424,11 +424,15 @@ int fme_pred_inter_reset(fme_ctx* ctx);
 int fme_template_costs(fme_ctx* ctx, const fme_pu_req* reqs, uint32_t* costs, int n, void* stream);
 
 /* ---- predInterSearch for B slices ------------------------------------ *
- * TEncSearch::predInterSearch on a B slice (TEncSearch.cpp:3746-4105) with the switches of the
- * shipped random-access configuration: FEN = 1 (FASTINTERSEARCH_MODE1: one bi-pred iteration,
- * over the list opposite the cheaper uni-pred list, 3918-3941) and MvdL1ZeroFlag = false
- * (TEncGOP.cpp:1392-1418 sets it only when both lists hold the same pictures: lowdelay B, not
- * supported here); FastMEForGenBLowDelayEnabled and ClipForBiPredMeEnabled per request flag.
+ * TEncSearch::predInterSearch on a B slice (TEncSearch.cpp:3746-4105), every FEN
+ * (fme_config.fast_inter_mode): FEN 1/2 (FASTINTERSEARCH_MODE1/2) run one bi-pred iteration over
+ * the list opposite the cheaper uni-pred list (3918-3941); FEN 0/3 run up to four, alternating
+ * L0, L1, L0, L1, each on the key of the other list's current bi-pred best, stopping at the first
+ * iteration that improves nothing (then xCheckBestMVP on the bi MVs, 4008-4021).  MvdL1ZeroFlag
+ * (TEncGOP.cpp:1392-1418: lowdelay B, both lists holding the same pictures) is a request flag:
+ * list 1 fixed at the AMVP predictor of least template cost over its references (3805-3810,
+ * 3878-3909), one L0 iteration.  FastMEForGenBLowDelayEnabled and ClipForBiPredMeEnabled per
+ * request flag.
  * Per request, in the encoder's call order:
  *   uiMbBits = xGetBlkBits(part_size, B slice, part_idx, uiLastMode) (4286-4333), uiLastMode being
  *             the decision of the request before (part_idx 1 continues that request's CU);
@@ -439,7 +443,7 @@ int fme_template_costs(fme_ctx* ctx, const fme_pu_req* reqs, uint32_t* costs, in
  *             < 8): the other list's uni-pred luma prediction at its best MV (motionCompensation),
  *             key = 2 * org - pred (removeHighFreq, TComYuv.cpp:411-455), and per reference of the
  *             searched list xMotionEstimation(bBi) (4461-4534): xSetSearchRange around the
- *             reference's uni MV with bipred_range, xPatternSearch (every integer position),
+ *             reference's last MV with bipred_range, xPatternSearch (every integer position),
  *             FracDIF on the key, NN_pred on the carried state (no EMI step), fWeight 0.5;
  *             xCheckBestMVP; strict minimum;
  *   decision (4041-4105): bi when uiCostBi <= uiCost[0] and <= the best L1 cost over references
@@ -447,6 +451,9 @@ int fme_template_costs(fme_ctx* ctx, const fme_pu_req* reqs, uint32_t* costs, in
  * Merge and the AMP merge-only test (bTestNormalMC false) stay with the caller.                 */
 #define FME_PU_FAST_ME_GEN_B 0x02u   /* FastMEForGenBLowDelayEnabled (cfg default true)          */
 #define FME_PU_CLIP_BIPRED   0x04u   /* ClipForBiPredMeEnabled: key clipped to 8 bits            */
+#define FME_PU_MVD_L1_ZERO   0x08u   /* TComSlice::getMvdL1ZeroFlag (GPB slices of lowdelay B,
+                                        TEncGOP.cpp:1410-1418): list 1 at its best template-cost
+                                        AMVP predictor with zero MVD, one list-0 bi iteration   */
 
 typedef struct fme_pu_req_b {
   uint16_t x, y;              /* PU luma rectangle                                              */
@@ -473,8 +480,9 @@ typedef struct fme_pu_res_b {
   uint8_t  inter_dir;         /* 1: L0, 2: L1, 3: bi (setInterDirSubParts)                      */
   uint8_t  ref_idx[2];        /* decided reference index per list (0 for an unused list)        */
   uint8_t  mvp_idx[2];        /* its AMVP index                                                 */
-  uint8_t  bi_list;           /* list searched by the bi-pred iteration; 0xFF: none             */
-  uint16_t reserved;
+  uint8_t  bi_list;           /* list searched by the last bi-pred iteration; 0xFF: none        */
+  uint8_t  bi_iters;          /* bi-pred iterations run (FEN 0/3: up to 4)                      */
+  uint8_t  reserved;
   int16_t  mv[2][2];          /* decided MVs, quarter-pel (0 for an unused list)                */
   int16_t  mvp[2][2];         /* their predictors                                               */
   uint32_t bits, cost;        /* uiMEBits and the decided cost                                  */
@@ -483,8 +491,8 @@ typedef struct fme_pu_res_b {
   uint32_t bi_cost, bi_bits;  /* uiCostBi, uiBits[2] (0xFFFFFFFF / 0: no bi-pred search)        */
   uint32_t ref_cost[2][FME_MAX_REFS];   /* uni uiCostTemp per (list, reference)                 */
   int16_t  ref_mv[2][FME_MAX_REFS][2];  /* uni cMvTemp per (list, reference)                    */
-  uint32_t bi_ref_cost[FME_MAX_REFS];   /* bi uiCostTemp per reference of bi_list               */
-  int16_t  bi_ref_mv[FME_MAX_REFS][2];  /* bi cMvTemp per reference of bi_list                  */
+  uint32_t bi_ref_cost[FME_MAX_REFS];   /* bi uiCostTemp per reference of bi_list (last iteration) */
+  int16_t  bi_ref_mv[FME_MAX_REFS][2];  /* bi cMvTemp per reference of bi_list (last iteration)    */
   uint8_t  ref_mvp_idx[2][FME_MAX_REFS];/* uni aaiMvpIdx after xCheckBestMVP                    */
 } fme_pu_res_b;   /* 160 bytes */
 

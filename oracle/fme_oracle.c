@@ -1163,9 +1163,11 @@ uint32_t orc_template_cost(const orc_ctx* ctx, const fme_pu_req* q, int k, int m
   return pi_tmpl(ctx, &g, q->ref_id[k], q->cand[k][m][0], q->cand[k][m][1], m, pred);
 }
 
-/* xEstimateMvPredAMVP (4186-4256): with two candidates the first with the least template cost. */
-static int pi_amvp(const orc_ctx* ctx, const pi_pu* g, int ref_id, int n_cand, const int16_t cand[2][2],
-                   int16_t* pred) {
+/* xEstimateMvPredAMVP (4186-4256): with two candidates the first with the least template cost.
+ * dist_bip (may be null): *puiDistBiP, the chosen candidate's template cost; with one candidate it
+ * is computed only when one_cand_dist is set (MvdL1ZeroFlag and list 1, 4214-4217). */
+static int pi_amvp2(const orc_ctx* ctx, const pi_pu* g, int ref_id, int n_cand, const int16_t cand[2][2],
+                    int16_t* pred, uint32_t* dist_bip, int one_cand_dist) {
   int idx = 0;
   if (n_cand > 1) {
     uint32_t best = 0xFFFFFFFFu;
@@ -1174,10 +1176,17 @@ static int pi_amvp(const orc_ctx* ctx, const pi_pu* g, int ref_id, int n_cand, c
       if (best > c) {
         best = c;
         idx = m;
+        if (dist_bip) *dist_bip = c;
       }
     }
+  } else if (one_cand_dist && dist_bip) {
+    *dist_bip = pi_tmpl(ctx, g, ref_id, cand[0][0], cand[0][1], 0, pred);
   }
   return idx;
+}
+static int pi_amvp(const orc_ctx* ctx, const pi_pu* g, int ref_id, int n_cand, const int16_t cand[2][2],
+                   int16_t* pred) {
+  return pi_amvp2(ctx, g, ref_id, n_cand, cand, pred, NULL, 0);
 }
 
 /* The reference-index bits of uiBitsTemp (3792-3800). */
@@ -1316,8 +1325,10 @@ int orc_pred_inter_p(orc_ctx* ctx, const fme_pu_req* reqs, fme_pu_res* res, int 
 }
 
 /* =====================================================================================
- * predInterSearch for B slices, sequential: TEncSearch.cpp:3746-4105 with
- * FEN 1/2 (one bi-pred iteration) and MvdL1ZeroFlag false.
+ * predInterSearch for B slices, sequential: TEncSearch.cpp:3746-4105 —
+ * FEN 1/2 (one bi-pred iteration over the list opposite the cheaper uni list), FEN 0/3 (up to four
+ * alternating iterations, each on the key of the other list's current best), and MvdL1ZeroFlag
+ * (FME_PU_MVD_L1_ZERO, lowdelay B: list 1 fixed at its best AMVP predictor, one L0 iteration).
  * ===================================================================================== */
 
 /* xGetBlkBits (TEncSearch.cpp:4286-4333) for a B slice: uiBlkBit[0..2]. */
@@ -1356,7 +1367,8 @@ static int pi_num_parts(int part_size) {
 }
 
 int orc_pred_inter_b(orc_ctx* ctx, const fme_pu_req_b* reqs, fme_pu_res_b* res, int n) {
-  if (ctx->cfg.fast_inter_mode != 1 && ctx->cfg.fast_inter_mode != 2) return FME_E_INVALID;   /* iNumIter 1 */
+  const int fen = ctx->cfg.fast_inter_mode;
+  if (fen < 0 || fen > 3) return FME_E_INVALID;
   int16_t* pred = (int16_t*)malloc(sizeof(int16_t) * 64 * 64);
   int16_t* key = (int16_t*)malloc(sizeof(int16_t) * 64 * 64);
   int last_mode = 0;   /* uiLastMode: 0 L0, 1 L1, 2 bi (predInterSearch local, per CU) */
@@ -1367,7 +1379,7 @@ int orc_pred_inter_b(orc_ctx* ctx, const fme_pu_req_b* reqs, fme_pu_res_b* res, 
     memset(o, 0, sizeof(*o));
     if (q->org_id >= FME_MAX_PICTURES || !ctx->pics[q->org_id].luma || q->lambda_id >= FME_MAX_LAMBDAS ||
         q->part_size > FME_PART_nRx2N || q->part_idx >= pi_num_parts(q->part_size) ||
-        (q->flags & ~(FME_PU_LOSSLESS | FME_PU_FAST_ME_GEN_B | FME_PU_CLIP_BIPRED))) {
+        (q->flags & ~(FME_PU_LOSSLESS | FME_PU_FAST_ME_GEN_B | FME_PU_CLIP_BIPRED | FME_PU_MVD_L1_ZERO))) {
       rc = FME_E_INVALID;
       break;
     }
@@ -1400,11 +1412,20 @@ int orc_pred_inter_b(orc_ctx* ctx, const fme_pu_req_b* reqs, fme_pu_res_b* res, 
     int16_t mv_v1[2] = {0, 0};
     int ridx_v1 = 0;
     const int reads2n = !(q->part_size == FME_PART_2Nx2N && q->depth == 0);
+    const int mvdl1z = (q->flags & FME_PU_MVD_L1_ZERO) != 0;
+    uint32_t best_bip_dist = 0xFFFFFFFFu, bip_dist = 0xFFFFFFFFu;   /* bestBiPDist, biPDistTemp */
+    int best_bip_mvp = 0, best_bip_ref = 0;                          /* bestBiPMvpL1, bestBiPRefIdxL1 */
     /* uni-directional prediction (3786-3865) */
     for (int l = 0; l < 2 && !rc; l++)
       for (int k = 0; k < q->num_refs[l] && !rc; k++) {
         uint32_t b = mb[l] + pi_ref_bits(k, q->num_refs[l]);
-        int idx = pi_amvp(ctx, &g, q->ref_id[l][k], q->n_cand[l][k], q->cand[l][k], pred);
+        int idx = pi_amvp2(ctx, &g, q->ref_id[l][k], q->n_cand[l][k], q->cand[l][k], pred, &bip_dist,
+                           mvdl1z && l == 1);
+        if (mvdl1z && l == 1 && bip_dist < best_bip_dist) {   /* 3805-3810 */
+          best_bip_dist = bip_dist;
+          best_bip_mvp = idx;
+          best_bip_ref = k;
+        }
         b += pi_mvp_idx_bits(idx, 2);
         uint32_t c;
         if ((q->flags & FME_PU_FAST_ME_GEN_B) && l == 1 && q->l1_to_l0[k] >= 0) {
@@ -1455,7 +1476,7 @@ int orc_pred_inter_b(orc_ctx* ctx, const fme_pu_req_b* reqs, fme_pu_res_b* res, 
         }
       }
     if (rc) break;
-    /* bi-predictive motion estimation (3868-4022), one iteration */
+    /* bi-predictive motion estimation (3868-4022) */
     uint32_t cost_bi = 0xFFFFFFFFu, bits_bi = 0;
     int16_t mv_bi[2][2] = {{mv[0][0], mv[0][1]}, {mv[1][0], mv[1][1]}};
     int ridx_bi[2] = {ridx[0], ridx[1]};
@@ -1463,41 +1484,102 @@ int orc_pred_inter_b(orc_ctx* ctx, const fme_pu_req_b* reqs, fme_pu_res_b* res, 
     memcpy(mvpi_bi, mvpi, sizeof(mvpi));
     o->bi_list = 0xFF;
     o->bi_cost = 0xFFFFFFFFu;
+    o->bi_iters = 0;
     const int restricted = q->cu_w == 8 && (q->w < 8 || q->h < 8);   /* isBipredRestriction */
     if (!restricted) {
-      uint32_t mot[2] = {bits[0] - mb[0], bits[1] - mb[1]};
-      bits_bi = mb[2] + mot[0] + mot[1];
-      const int L = cost[0] <= cost[1] ? 1 : 0;   /* FASTINTERSEARCH_MODE1/2 (3931-3941) */
-      /* motionCompensation of the other list, removeHighFreq (TComYuv.cpp:411-455) */
-      orc_bi_key(ctx, q->org_id, q->ref_id[1 - L][ridx[1 - L]], q->x, q->y, q->w, q->h, q->cu_x, q->cu_y,
-                 mv[1 - L][0], mv[1 - L][1], (q->flags & FME_PU_CLIP_BIPRED) != 0, key);
-      o->bi_list = (uint8_t)L;
-      for (int k = 0; k < q->num_refs[L]; k++) {
-        uint32_t b = mb[2] + mot[1 - L] + pi_ref_bits(k, q->num_refs[L]) + pi_mvp_idx_bits(mvpi_bi[L][k], 2);
-        const int16_t* p = q->cand[L][k][mvpi_bi[L][k]];
-        fme_result r;
-        rc = pi_me(ctx, &g, q->ref_id[L][k], p[0], p[1], b, brange, NULL, key, mvt[L][k][0], mvt[L][k][1], &r);
+      uint32_t mot[2];
+      /* m_acYuvPred[l]: the (reference, MV) each list's stored prediction was made with */
+      int ps_ref[2] = {ridx[0], ridx[1]};
+      int16_t ps_mv[2][2] = {{mv[0][0], mv[0][1]}, {mv[1][0], mv[1][1]}};
+      if (mvdl1z) {   /* 3876-3909: list 1 at its best template-cost AMVP predictor, MVD zero */
+        const int kb = best_bip_ref;
+        mvpi_bi[1][kb] = best_bip_mvp;
+        mv_bi[1][0] = q->cand[1][kb][best_bip_mvp][0];
+        mv_bi[1][1] = q->cand[1][kb][best_bip_mvp][1];
+        ridx_bi[1] = kb;
+        ps_ref[1] = kb;
+        ps_mv[1][0] = mv_bi[1][0];
+        ps_mv[1][1] = mv_bi[1][1];
+        mot[0] = bits[0] - mb[0];
+        mot[1] = mb[1] + pi_ref_bits(kb, q->num_refs[1]) + pi_mvp_idx_bits(mvpi_bi[1][kb], 2);
+        bits_bi = mb[2] + mot[0] + mot[1];
+        mvt[1][kb][0] = mv_bi[1][0];
+        mvt[1][kb][1] = mv_bi[1][1];
+      } else {
+        mot[0] = bits[0] - mb[0];
+        mot[1] = bits[1] - mb[1];
+        bits_bi = mb[2] + mot[0] + mot[1];
+      }
+      /* 4 iterations; FASTINTERSEARCH_MODE1/2 or MvdL1ZeroFlag: one (3919-3925) */
+      const int niter = (fen == 1 || fen == 2 || mvdl1z) ? 1 : 4;
+      for (int it = 0; it < niter && !rc; it++) {
+        int L = it % 2;
+        if (fen == 1 || fen == 2) L = cost[0] <= cost[1] ? 1 : 0;   /* 3931-3941 */
+        else if (it == 0) L = 0;
+        if (it == 0 && !mvdl1z) {   /* motionCompensation of the other list at its uni best (3946-3952) */
+          ps_ref[1 - L] = ridx[1 - L];
+          ps_mv[1 - L][0] = mv[1 - L][0];
+          ps_mv[1 - L][1] = mv[1 - L][1];
+        }
+        if (mvdl1z) L = 0;   /* 3956-3960 */
+        /* xMotionEstimation(bBi)'s key: removeHighFreq of the other list's stored prediction */
+        orc_bi_key(ctx, q->org_id, q->ref_id[1 - L][ps_ref[1 - L]], q->x, q->y, q->w, q->h, q->cu_x, q->cu_y,
+                   ps_mv[1 - L][0], ps_mv[1 - L][1], (q->flags & FME_PU_CLIP_BIPRED) != 0, key);
+        o->bi_list = (uint8_t)L;
+        o->bi_iters = (uint8_t)(it + 1);
+        memset(o->bi_ref_cost, 0, sizeof(o->bi_ref_cost));
+        memset(o->bi_ref_mv, 0, sizeof(o->bi_ref_mv));
+        int changed = 0;
+        for (int k = 0; k < q->num_refs[L]; k++) {
+          uint32_t b = mb[2] + mot[1 - L] + pi_ref_bits(k, q->num_refs[L]) + pi_mvp_idx_bits(mvpi_bi[L][k], 2);
+          const int16_t* p = q->cand[L][k][mvpi_bi[L][k]];
+          fme_result r;
+          /* ±BipredSearchRange around cMvTemp[L][k], the last ME result of (L, k) (4486-4490) */
+          rc = pi_me(ctx, &g, q->ref_id[L][k], p[0], p[1], b, brange, NULL, key, mvt[L][k][0], mvt[L][k][1], &r);
+          if (rc) break;
+          mvt[L][k][0] = r.mv_x;
+          mvt[L][k][1] = r.mv_y;
+          uint32_t c = r.cost;
+          b = r.bits;
+          int idx = mvpi_bi[L][k];
+          pi_check_best_mvp(ml, q->cand[L][k], q->n_cand[L][k], r.mv_x, r.mv_y, &idx, &b, &c);
+          mvpi_bi[L][k] = idx;
+          o->bi_ref_cost[k] = c;
+          o->bi_ref_mv[k][0] = r.mv_x;
+          o->bi_ref_mv[k][1] = r.mv_y;
+          if (c < cost_bi) {   /* 3985-4005 */
+            changed = 1;
+            mv_bi[L][0] = r.mv_x;
+            mv_bi[L][1] = r.mv_y;
+            ridx_bi[L] = k;
+            cost_bi = c;
+            mot[L] = b - mb[2] - mot[1 - L];
+            bits_bi = b;
+            if (niter != 1) {   /* set motion + motionCompensation of list L */
+              ps_ref[L] = k;
+              ps_mv[L][0] = r.mv_x;
+              ps_mv[L][1] = r.mv_y;
+            }
+          }
+        }
         if (rc) break;
-        uint32_t c = r.cost;
-        b = r.bits;
-        int idx = mvpi_bi[L][k];
-        pi_check_best_mvp(ml, q->cand[L][k], q->n_cand[L][k], r.mv_x, r.mv_y, &idx, &b, &c);
-        mvpi_bi[L][k] = idx;
-        o->bi_ref_cost[k] = c;
-        o->bi_ref_mv[k][0] = r.mv_x;
-        o->bi_ref_mv[k][1] = r.mv_y;
-        if (c < cost_bi) {
-          mv_bi[L][0] = r.mv_x;
-          mv_bi[L][1] = r.mv_y;
-          ridx_bi[L] = k;
-          cost_bi = c;
-          mot[L] = b - mb[2] - mot[1 - L];
-          bits_bi = b;
+        if (!changed) {   /* 4008-4021 */
+          if (cost_bi <= cost[0] && cost_bi <= cost[1]) {
+            int i0 = mvpi_bi[0][ridx_bi[0]];
+            pi_check_best_mvp(ml, q->cand[0][ridx_bi[0]], q->n_cand[0][ridx_bi[0]], mv_bi[0][0], mv_bi[0][1], &i0,
+                              &bits_bi, &cost_bi);
+            mvpi_bi[0][ridx_bi[0]] = i0;
+            if (!mvdl1z) {
+              int i1 = mvpi_bi[1][ridx_bi[1]];
+              pi_check_best_mvp(ml, q->cand[1][ridx_bi[1]], q->n_cand[1][ridx_bi[1]], mv_bi[1][0], mv_bi[1][1],
+                                &i1, &bits_bi, &cost_bi);
+              mvpi_bi[1][ridx_bi[1]] = i1;
+            }
+          }
+          break;
         }
       }
       if (rc) break;
-      /* (!bChanged needs every bi cost at the Distortion maximum: not reachable with 32-bit costs
-       * below it, so its xCheckBestMVP re-run of 4008-4021 is not restated.) */
     }
     o->bi_cost = cost_bi;
     o->bi_bits = restricted ? 0 : bits_bi;

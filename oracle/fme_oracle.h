@@ -153,8 +153,8 @@ int orc_mc(const orc_yuv* pics, const fme_mc_job* jobs, int n, uint8_t* y, int y
 int orc_pred_inter_p(orc_ctx* ctx, const fme_pu_req* reqs, fme_pu_res* res, int n);
 void orc_pred_inter_reset(orc_ctx* ctx);
 uint32_t orc_template_cost(const orc_ctx* ctx, const fme_pu_req* q, int k, int m);   /* TEncSearch.cpp:4397-4436 */
-/* predInterSearch for B slices (TEncSearch.cpp:3746-4105, FEN 1/2, MvdL1ZeroFlag false): uni loop
- * over both lists, the one-iteration bi-pred search on the removeHighFreq key, the decision. */
+/* predInterSearch for B slices (TEncSearch.cpp:3746-4105, FEN 0-3, MvdL1ZeroFlag per request): uni loop
+ * over both lists, the bi-pred iterations on the removeHighFreq key, the decision. */
 int orc_pred_inter_b(orc_ctx* ctx, const fme_pu_req_b* reqs, fme_pu_res_b* res, int n);
 void orc_bi_key(const orc_ctx* ctx, int org_id, int ref_id, int x, int y, int w, int h, int cu_x, int cu_y,
                 int mvx, int mvy, int clip, int16_t* key);   /* TEncSearch.cpp:4461-4471 */

@@ -23,7 +23,7 @@ def test_library_exports_header():
     assert set(names) == set(runtime.ABI_SYMBOLS)
     for n in names:
         assert hasattr(lib, n), n
-    assert lib.fme_abi_version() == runtime.ABI_VERSION == 11
+    assert lib.fme_abi_version() == runtime.ABI_VERSION == 12
 
 
 def test_struct_layouts():

@@ -208,17 +208,102 @@ def test_oracle_b_rejects_unsupported():
     from oracle import Oracle
     pics = _pics()
     reqs = _reqs(4, max_depth=1)
-    for fen in (0, 3):   # iNumIter 4: not restated
-        orc = Oracle(nn_mode=0, fast_inter_mode=fen)
-        _setup(orc, pics)
-        with pytest.raises(RuntimeError):
-            orc.pred_inter_b(reqs[:4])
     orc = Oracle(nn_mode=0, fast_inter_mode=2)
     _setup(orc, pics)
     bad = reqs[:8].copy()
     bad["num_refs"][3] = [1, 0]
     with pytest.raises(RuntimeError):
         orc.pred_inter_b(bad)
+    bad = reqs[:8].copy()
+    bad["flags"][2] |= 0x10   # no such request flag
+    with pytest.raises(RuntimeError):
+        orc.pred_inter_b(bad)
+
+
+def test_oracle_b_fen0_iterations():
+    """FEN 0/3 (iNumIter 4, TEncSearch.cpp:3918-4022): iteration 0 searches L0 on the key of the L1
+    uni best and always improves on MAX, so a non-restricted PU runs 2..4 iterations, alternating
+    lists (the last one searched is (iters - 1) % 2); its bi cost never exceeds the FEN-2 search of
+    L0 with the same key when FEN 2 also picks L0 (FEN 0 and 2 share the full-row metric; on a
+    CU's first PU uiMbBits does not depend on an earlier decision).  FEN 3 is FEN 0's loop with
+    the even-row metric of FEN 1.  With bi chosen, each list's MV is a searched MV of that list (or the uni MV of the
+    list never searched)."""
+    from oracle import Oracle
+    pics = _pics()
+    reqs = _reqs(5, max_depth=2)
+    res = {}
+    for fen in (0, 2, 3):
+        o = Oracle(nn_mode=0, fast_inter_mode=fen)
+        _setup(o, pics)
+        res[fen] = o.pred_inter_b(reqs)
+    restricted = (reqs["cu_w"] == 8) & ((reqs["w"] < 8) | (reqs["h"] < 8))
+    for fen in (0, 3):
+        r = res[fen]
+        it = r["bi_iters"].astype(int)
+        assert (it[restricted] == 0).all() and (r["bi_list"][restricted] == 0xFF).all()
+        assert it[~restricted].min() >= 2 and it.max() <= 4
+        assert (r["bi_list"][~restricted] == (it[~restricted] - 1) % 2).all()
+        assert len(set(it[~restricted])) == 3, np.bincount(it)   # 2, 3 and 4 all occur
+    r0, r1 = res[0], res[2]
+    first = reqs["part_idx"] == 0
+    assert np.array_equal(r0["ref_cost"][first], r1["ref_cost"][first])
+    assert np.array_equal(r0["uni_cost"][first], r1["uni_cost"][first])
+    same_first = ~restricted & first & (r1["bi_list"] == 0)
+    assert same_first.sum() > 20
+    assert (r0["bi_cost"][same_first] <= r1["bi_cost"][same_first]).all()
+    assert (r0["bi_cost"][~restricted] < 0xFFFFFFFF).all()
+    assert (r0["inter_dir"] == 3).sum() > 50
+
+
+def test_oracle_b_mvd_l1_zero():
+    """MvdL1ZeroFlag (lowdelay B, both lists the same pictures; TEncSearch.cpp:3805-3810, 3876-3925):
+    list 1 at the AMVP predictor of least template cost over its references (zero MVD), one L0
+    iteration; L0 uni-pred and the L1 uni searches as without the flag."""
+    from oracle import Oracle
+    pics = _pics()
+    l = [(0, 1), (1, 2)]
+    rng = np.random.default_rng(6)
+    reqs = synth.make_pu_requests_b(rng, W, H, org_id=4, l0=l, l1=l, lambda_id=0, max_depth=2, mvd_l1_zero=True)
+    plain = reqs.copy()
+    plain["flags"] &= np.uint8(0xFF ^ abi.PU_MVD_L1_ZERO)
+    o, p = Oracle(nn_mode=0, fast_inter_mode=0), Oracle(nn_mode=0, fast_inter_mode=0)
+    _setup(o, pics)
+    _setup(p, pics)
+    r, rp = o.pred_inter_b(reqs), p.pred_inter_b(plain)
+    first = reqs["part_idx"] == 0   # (a second PU's uiMbBits follows its CU's first decision)
+    assert np.array_equal(r["ref_cost"][first], rp["ref_cost"][first])
+    assert np.array_equal(r["uni_cost"][first], rp["uni_cost"][first])
+    restricted = (reqs["cu_w"] == 8) & ((reqs["w"] < 8) | (reqs["h"] < 8))
+    assert (r["bi_iters"][~restricted] == 1).all() and (r["bi_list"][~restricted] == 0).all()
+    bi = np.flatnonzero(r["inter_dir"] == 3)
+    assert len(bi) > 20
+    for i in bi:
+        assert tuple(r["mv"][i][1]) == tuple(r["mvp"][i][1])   # zero MVD in list 1
+        k = int(r["ref_idx"][i][1])
+        assert tuple(r["mvp"][i][1]) == tuple(reqs["cand"][i][1][k][int(r["mvp_idx"][i][1])])
+    # the template costs decide list 1 (xGetTemplateCost with the candidate's index bits)
+    p1 = _as_p(reqs, 1)
+    for i in bi[:100]:
+        q = reqs[i]
+        best, kb, mb = None, 0, 0
+        for k in range(int(q["num_refs"][1])):
+            c = [o.template_cost(p1[i], k, m) for m in range(int(q["n_cand"][1][k]))]
+            m = int(np.argmin(c))
+            if best is None or c[m] < best:
+                best, kb, mb = c[m], k, m
+        assert (int(r["ref_idx"][i][1]), int(r["mvp_idx"][i][1])) == (kb, mb), i
+
+
+def _as_p(reqs, l):
+    """The list-l view of B requests as fme_pu_req (the P-slice request layout)."""
+    p = np.zeros(len(reqs), dtype=abi.PU_REQ_DTYPE)
+    for f in ("x", "y", "w", "h", "cu_x", "cu_y", "part_size", "depth", "org_id", "lambda_id", "search_range"):
+        p[f] = reqs[f]
+    p["num_refs"] = reqs["num_refs"][:, l]
+    p["ref_id"] = reqs["ref_id"][:, l]
+    p["n_cand"] = reqs["n_cand"][:, l]
+    p["cand"] = reqs["cand"][:, l]
+    return p
 
 
 # ---- GPU parity (through the C ABI) ---------------------------------------------------------------
@@ -311,8 +396,53 @@ def test_pred_inter_b_clip_no_fast_me_and_rejection():
     second = int(np.flatnonzero(reqs["part_idx"] == 1)[0])
     with pytest.raises(FmeError):   # a second PU without its CU's first PU before it
         ctx.pred_inter_b(reqs[second:])
-    ctx0 = FmeContext(nn_mode=0, fast_inter_mode=0)
-    _setup(ctx0, pics)
+    bad = reqs.copy()
+    bad["flags"][5] |= 0x10   # no such request flag
     with pytest.raises(FmeError):
-        ctx0.pred_inter_b(reqs[:4])
+        ctx.pred_inter_b(bad)
     assert len(ctx.pred_inter_b(reqs[:0])) == 0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("fen,nn", [(0, 1), (3, 0)])
+def test_pred_inter_b_fen_iterations_match_oracle(fen, nn):
+    """FEN 0 / 3: up to four bi-pred iterations per PU, run by the host in rounds (one fme_refine
+    per round), against the oracle's sequential loop; NN on for FEN 0 (the carried state across
+    the rounds' repeated uni jobs)."""
+    from nnfme import weights
+    from nnfme.runtime import FmeContext
+    from oracle import Oracle
+    pics = _pics()
+    reqs = _reqs(23, max_depth=2, lossless_frac=0.03)
+    kw = dict(nn_mode=nn, qp=22, fast_inter_mode=fen)
+    ctx, orc = FmeContext(**kw), Oracle(**kw)
+    if nn:
+        orc.load_nn(weights.load_weights(22))
+    _setup(ctx, pics)
+    _setup(orc, pics)
+    got, exp = ctx.pred_inter_b(reqs), orc.pred_inter_b(reqs)
+    _compare(got, exp)
+    assert set(np.unique(got["bi_iters"])) >= {2, 3, 4}
+    if nn:
+        assert np.array_equal(ctx.nn_get_state(), orc.nn_get_state())
+
+
+@pytest.mark.gpu
+def test_pred_inter_b_mvd_l1_zero_matches_oracle():
+    """MvdL1ZeroFlag on a lowdelay-B stream (both lists the same two pictures, FEN 1, NN on):
+    list 1 at its best template-cost predictor, one L0 iteration."""
+    from nnfme import weights
+    from nnfme.runtime import FmeContext
+    from oracle import Oracle
+    pics = _pics()
+    l = [(0, 1), (1, 2)]
+    rng = np.random.default_rng(24)
+    reqs = synth.make_pu_requests_b(rng, W, H, org_id=4, l0=l, l1=l, lambda_id=0, max_depth=2, mvd_l1_zero=True)
+    ctx = FmeContext(nn_mode=1, qp=22, fast_inter_mode=1)
+    orc = Oracle(nn_mode=1, qp=22, fast_inter_mode=1)
+    orc.load_nn(weights.load_weights(22))
+    _setup(ctx, pics)
+    _setup(orc, pics)
+    got, exp = ctx.pred_inter_b(reqs), orc.pred_inter_b(reqs)
+    _compare(got, exp)
+    assert (got["inter_dir"] == 3).sum() > 20
