@@ -77,19 +77,10 @@ struct DevBuf {
 
 }  // namespace
 
-// fme_frac_dif_single's staging block (see fme_ctx::stage).
+// The deeper nets' single NN_pred call (k_nn_deep_single): class and completion word.
 struct SingleStage {
-  fme_job job;
-  int32_t perm[8];
-  fme_result res;
-  fme_mv_result mv;
-  PicDesc pic;
-  double ml;
-  uint32_t nn_in[12];
   int32_t nn_out[4];
-  uint32_t flag;                // completion word of the single-PU kernels (call sequence number)
-  int16_t key[64 * 64];
-  uint8_t win[72 * 72];
+  uint32_t flag;                // completion word (call sequence number)
 };
 
 struct fme_ctx {
@@ -151,6 +142,7 @@ struct fme_ctx {
   DevBuf<fme_tz_ext> d_tz_ext;
   DevBuf<uint32_t> d_tz_sad;
   DevBuf<uint32_t> d_tz_nn_in;   // staging of fme_integer_search_ring's NN input rows
+  DevBuf<int32_t> d_tz_ctr;      // the bulk search's per-XCD queue heads
   hipEvent_t ev_tz[2] = {nullptr, nullptr};
   bool tz_timed = false;
   // predInterSearch producer: m_integerMv2Nx2N[REF_PIC_LIST_0][k] (TEncSearch.h:118), AMVP staging
@@ -162,19 +154,23 @@ struct fme_ctx {
   DevBuf<int32_t> d_key_invalid;  // invalid requests of the last fme_build_bipred_keys_device
   DevBuf<int32_t> d_ch_i32;     // k_tz_level: psrc
 
-  std::unique_ptr<fme_ctx> single;  // private context for the single-PU entry points
-  // Single-PU staging in pinned, device-mapped host memory: one kernel reads the job, key and
-  // window over PCIe and writes the record back (fme_frac_dif_single / fme_nn_pred_single).
+  // The deeper nets' single NN_pred: inputs in the kernel argument, class and completion word in
+  // pinned, device-mapped host memory.
   struct SingleStage* stage = nullptr;
   uint8_t* stage_dev = nullptr;
   hipStream_t single_stream = nullptr;
   uint32_t single_seq = 0;
-  DevBuf<uint8_t> single_scratch;   // device staging of the inline single-PU kernel
-  DevBuf<uint8_t> single_pic;
-  DevBuf<fme_job> single_job;
-  DevBuf<fme_result> single_res;
-  DevBuf<uint32_t> single_nn_in;
-  DevBuf<int32_t> single_nn_out;
+  // The single-call server (fme_server.hip) behind fme_frac_dif_single and the master net's
+  // fme_nn_pred_single: its mailbox in pinned, device-mapped host memory, its own stream.
+  SrvBox* box = nullptr;
+  SrvBox* box_dev = nullptr;
+  hipStream_t srv_stream = nullptr;
+  bool srv_running = false;
+  uint32_t srv_epoch = 0;       // of the instance launched last
+  uint32_t srv_done = 0;        // sequence number of the last completed call
+  uint32_t srv_nn_gen = 0;      // weight generation the running instance copied to LDS
+  uint32_t nn_gen = 0;          // bumped by fme_load_nn_weights
+  uint64_t srv_khz = 100000;    // wall-clock rate (s_memrealtime)
 
   // Profiling: a ring of event sets, one per profiled batch, read once the batch has finished
   // (harvest_events), so profiling a run of batches adds no synchronisation.  Per set: 0 start,
@@ -209,8 +205,6 @@ hipError_t launch_nn_deep_tail(const fme_nn_net& n, const void* packed, float* m
                                const WorkBufs& w, int state_in, int engine, hipStream_t s);
 hipError_t launch_nn_deep_single(const fme_nn_net& n, const void* packed, const NnIn11& in11, int32_t* out,
                                  uint32_t* flag, uint32_t seq, hipStream_t s);
-hipError_t launch_nn_single(const float* nnp, const NnIn11& in, int32_t* out, uint32_t* flag, uint32_t seq,
-                            hipStream_t s);
 }
 
 extern "C" {
@@ -256,9 +250,13 @@ int fme_create(int device, const fme_config* cfg, fme_ctx** out_ctx) {
   return FME_OK;
 }
 
+}  // extern "C"
+static int srv_stop(fme_ctx* c);
+extern "C" {
 int fme_destroy(fme_ctx* c) {
   if (!c) return FME_OK;
   (void)hipSetDevice(c->device);
+  (void)srv_stop(c);
   (void)hipDeviceSynchronize();
   for (int i = 0; i < FME_MAX_PICTURES; i++)
     if (c->pic_owned[i] && c->pics[i].luma) (void)hipFree(const_cast<uint8_t*>(c->pics[i].luma));
@@ -274,13 +272,13 @@ int fme_destroy(fme_ctx* c) {
   c->d_pics.release(); c->d_mlambda.release(); c->d_keys.release(); c->d_nn.release(); c->d_net.release();
   c->d_jobs.release(); c->d_res.release(); c->d_mv.release(); c->cls.release(); c->perm.release(); c->sjobs.release();
   c->counts.release(); c->blk_agg.release(); c->blk_prefix.release(); c->nn_state.release();
-  c->ipos.release(); c->srec.release();
+  c->ipos.release(); c->srec.release(); c->d_tz_ctr.release();
   c->d_sched.release();
   if (c->ev_done) (void)hipEventDestroy(c->ev_done);
-  c->single_pic.release(); c->single_scratch.release(); c->single_job.release(); c->single_res.release();
   if (c->stage) (void)hipHostFree(c->stage);
   if (c->single_stream) (void)hipStreamDestroy(c->single_stream);
-  c->single_nn_in.release(); c->single_nn_out.release();
+  if (c->box) (void)hipHostFree(c->box);
+  if (c->srv_stream) (void)hipStreamDestroy(c->srv_stream);
   if (c->h_counts) (void)hipHostFree(c->h_counts);
   for (auto& set : c->ev)
     for (auto& e : set)
@@ -290,7 +288,6 @@ int fme_destroy(fme_ctx* c) {
   if (c->aux2) (void)hipStreamDestroy(c->aux2);
   if (c->ev_join) (void)hipEventDestroy(c->ev_join);
   if (c->aux) (void)hipStreamDestroy(c->aux);
-  if (c->single) fme_destroy(c->single.release());
   delete c;
   return FME_OK;
 }
@@ -428,6 +425,7 @@ int fme_load_nn_weights(fme_ctx* c, const float* params, int count) {
   nn_pack(params, packed.data());
   HIP_TRY(hipMemcpy(c->d_nn.p, packed.data(), kNnPkFloats * sizeof(float), hipMemcpyHostToDevice));
   c->nn_loaded = true;
+  c->nn_gen++;   // a running server instance holds the old weights in LDS: it is restarted
   return FME_OK;
 }
 
@@ -581,6 +579,10 @@ static WorkBufs work_bufs(fme_ctx* c) {
 // kernel: rebinding pictures for the next frame never waits for the batch in flight, and the
 // batch stream holds no copy-engine transfer (which would queue behind bulk uploads).
 static int sync_tables(fme_ctx* c, hipStream_t s) {
+  // a resident server could hold up this work on a hardware queue its stream shares: stop it
+  // (a few microseconds; the next single call relaunches it)
+  int rc = srv_stop(c);
+  if (rc) return rc;
   if (!c->tables_dirty) return FME_OK;
   HIP_TRY(launch_put_tables(c->d_pics.p, c->d_mlambda.p, c->pics, c->mlambda, s));
   c->tables_dirty = false;
@@ -800,6 +802,9 @@ static int tz_run(fme_ctx* c, fme_job* d_jobs, const fme_tz_ext* d_ext, uint32_t
   ta.sad = d_sad;
   ta.emi_mv = d_emi;
   ta.nn_in = d_nn_in;
+  HIP_TRY(c->d_tz_ctr.reserve(24));
+  ta.ctr = c->d_tz_ctr.p;
+  HIP_TRY(hipMemsetAsync(ta.ctr, 0, 24 * sizeof(int32_t), s));
   if (c->profiling) HIP_TRY(hipEventRecord(c->ev_tz[0], s));
   // the three unit-shape kernels are latency-bound and independent: 4x8 and 8x4 units on the two
   // auxiliary streams, 8x8 units on the caller's stream, joined before returning
@@ -989,9 +994,7 @@ int fme_refine_mv(fme_ctx* c, const fme_job* jobs, fme_mv_result* out, int n, vo
   return refine_host(c, jobs, nullptr, out, n, stream, "fme_refine_mv");
 }
 
-// xPatternSearchFracDIF for one PU: the reference window around mv_int becomes a private
-// (w+8) x (h+8) picture; the MV predictor is shifted by 4*mv_int so that every MV-cost
-// argument (xPatternRefinement's (cMvTest << scale) - pred) is unchanged.
+// The deeper nets' single NN_pred call: its completion word in pinned, device-mapped host memory.
 static int ensure_stage(fme_ctx* c) {
   if (c->stage) return FME_OK;
   void* p = nullptr;
@@ -1030,12 +1033,100 @@ static int single_wait(fme_ctx* c, uint32_t seq) {
   return FME_OK;
 }
 
+// ---- the single-call server (fme_server.hip) ----------------------------------------------------
+// One resident workgroup serves fme_frac_dif_single and the master net's fme_nn_pred_single: the
+// host writes the request into the mailbox (pinned, device-mapped), releases req_seq and spins on
+// done_seq.  An instance exits after kSrvIdleUs without a call or kSrvLifeMs of life (or on `stop`)
+// and writes its epoch to `stopped`; a call that finds its instance gone relaunches one, which
+// serves the pending request.
+constexpr uint64_t kSrvIdleUs = 2000;
+constexpr uint64_t kSrvLifeMs = 100;
+
+static int srv_open(fme_ctx* c) {
+  if (c->box) return FME_OK;
+  void* p = nullptr;
+  HIP_TRY(hipHostMalloc(&p, sizeof(SrvBox), hipHostMallocMapped));
+  std::memset(p, 0, sizeof(SrvBox));
+  c->box = static_cast<SrvBox*>(p);
+  void* d = nullptr;
+  HIP_TRY(hipHostGetDevicePointer(&d, p, 0));
+  c->box_dev = static_cast<SrvBox*>(d);
+  HIP_TRY(hipStreamCreateWithFlags(&c->srv_stream, hipStreamNonBlocking));
+  int khz = 0;
+  if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, c->device) == hipSuccess && khz > 0)
+    c->srv_khz = (uint64_t)khz;
+  return FME_OK;
+}
+
+static int srv_launch(fme_ctx* c) {
+  __atomic_store_n(&c->box->stop, 0u, __ATOMIC_RELEASE);
+  const uint32_t epoch = ++c->srv_epoch;
+  c->srv_nn_gen = c->nn_gen;
+  HIP_TRY(launch_server(c->box_dev, c->nn_loaded ? c->d_nn.p : nullptr, c->srv_done, epoch,
+                        kSrvIdleUs * c->srv_khz / 1000, kSrvLifeMs * c->srv_khz, c->srv_stream));
+  c->srv_running = true;
+  return FME_OK;
+}
+
+// The running instance's end: its `stopped` word (or a device error on its stream).
+static int srv_join(fme_ctx* c) {
+  volatile uint32_t* st = &c->box->stopped;
+  for (long it = 1; *st != c->srv_epoch; it++) {
+    __builtin_ia32_pause();
+    if ((it & 1023) == 0) {
+      const hipError_t q = hipStreamQuery(c->srv_stream);
+      if (q != hipErrorNotReady && *st != c->srv_epoch) {
+        c->srv_running = false;
+        if (q != hipSuccess) return fail(FME_E_DEVICE, "single-call server: %s", hipGetErrorString(q));
+        return fail(FME_E_DEVICE, "single-call server ended without its stop word");
+      }
+    }
+  }
+  c->srv_running = false;
+  HIP_TRY(hipStreamSynchronize(c->srv_stream));
+  return FME_OK;
+}
+
+static int srv_stop(fme_ctx* c) {
+  if (!c->srv_running) return FME_OK;
+  __atomic_store_n(&c->box->stop, 1u, __ATOMIC_RELEASE);
+  return srv_join(c);
+}
+
+// One call: the request fields and payload are in c->box already.
+static int srv_call(fme_ctx* c, bool uses_nn) {
+  int rc = FME_OK;
+  if (c->srv_running && uses_nn && c->srv_nn_gen != c->nn_gen) rc = srv_stop(c);
+  if (!rc && !c->srv_running) rc = srv_launch(c);
+  if (rc) return rc;
+  const uint32_t seq = c->srv_done + 1;
+  __atomic_store_n(&c->box->req_seq, seq, __ATOMIC_RELEASE);
+  volatile uint32_t* done = &c->box->done_seq;
+  volatile uint32_t* st = &c->box->stopped;
+  for (long it = 1; *done != seq; it++) {
+    __builtin_ia32_pause();
+    if (*st == c->srv_epoch && *done != seq) {   // the instance left before it saw the call
+      c->srv_running = false;
+      HIP_TRY(hipStreamSynchronize(c->srv_stream));
+      rc = srv_launch(c);
+      if (rc) return rc;
+    } else if ((it & 4095) == 0) {
+      const hipError_t q = hipStreamQuery(c->srv_stream);
+      if (q != hipErrorNotReady && q != hipSuccess) {
+        c->srv_running = false;
+        return fail(FME_E_DEVICE, "single-call server: %s", hipGetErrorString(q));
+      }
+    }
+  }
+  __atomic_thread_fence(__ATOMIC_ACQUIRE);
+  c->srv_done = seq;
+  return FME_OK;
+}
+
 // xPatternSearchFracDIF for one PU, as TEncSearch calls it: the key block (pcPatternKey, HM Pel)
 // and the reference window around the integer MV (rows -4..h+3, columns -4..w+3 of the padded
-// picture) are staged in pinned, device-mapped host memory; one launch of k_search_single (the
-// batch kernel's per-PU search, no EMI step) reads them over PCIe and writes the record back; one
-// stream synchronisation.  (Round 2: a sub-context picture upload, a key upload and a 5-launch
-// batch with its copies, 136-148 us per call.)
+// picture) go into the server's mailbox; the MV predictor is shifted by 4*mv_int so that every
+// MV-cost argument (xPatternRefinement's (cMvTest << scale) - pred) is unchanged.
 int fme_frac_dif_single(fme_ctx* c, int lossless, const int16_t* key, int key_stride, int w, int h,
                         const int16_t* ref, int ref_stride, int mv_int_x, int mv_int_y, int mvp_x,
                         int mvp_y, double motion_lambda, int16_t* half_xy, int16_t* qtr_xy,
@@ -1046,94 +1137,30 @@ int fme_frac_dif_single(fme_ctx* c, int lossless, const int16_t* key, int key_st
   const int px = mvp_x - 4 * mv_int_x, py = mvp_y - 4 * mv_int_y;
   if (px < -32768 || px > 32767 || py < -32768 || py > 32767) return fail(FME_E_INVALID, "fme_frac_dif_single: predictor out of range");
   HIP_TRY(hipSetDevice(c->device));
-  int rc = ensure_stage(c);
+  int rc = srv_open(c);
   if (rc) return rc;
-  SingleStage* st = c->stage;
+  SrvBox* b = c->box;
   const int pw = w + 8, ph = h + 8;
-  const uint32_t seq = ++c->single_seq;
-  if (w <= 16 && h <= 16) {   // everything in the kernel argument: no host-memory reads on the device
-    HIP_TRY(c->single_scratch.reserve(64 + kInlineBytes + 64));
-    SingleInline p{};
-    p.job.x = 4;
-    p.job.y = 4;
-    p.job.w = (uint8_t)w;
-    p.job.h = (uint8_t)h;
-    p.job.mvp_x = (int16_t)px;
-    p.job.mvp_y = (int16_t)py;
-    p.job.flags = lossless ? FME_JOB_LOSSLESS : 0;
-    p.job.key_offset = 0;
-    p.ml = motion_lambda;
-    p.res = reinterpret_cast<fme_result*>(c->stage_dev + offsetof(SingleStage, res));
-    p.flag = reinterpret_cast<uint32_t*>(c->stage_dev + offsetof(SingleStage, flag));
-    p.scratch = c->single_scratch.p;
-    p.win_stride = pw;
-    p.win_h = ph;
-    p.key_bytes = w * h * 2;
-    p.seq = (int32_t)seq;
-    int16_t* kd = reinterpret_cast<int16_t*>(p.data);
-    for (int y = 0; y < h; y++) std::memcpy(kd + y * w, key + (ptrdiff_t)y * key_stride, (size_t)w * sizeof(int16_t));
-    uint8_t* wd = reinterpret_cast<uint8_t*>(p.data) + p.key_bytes;
-    for (int y = 0; y < ph; y++) {
-      const int16_t* src = ref + (ptrdiff_t)(mv_int_y - 4 + y) * ref_stride + (mv_int_x - 4);
-      for (int x = 0; x < pw; x++) wd[y * pw + x] = (uint8_t)std::min(255, std::max(0, (int)src[x]));
-    }
-    HIP_TRY(launch_search_single_inline(p, cls, c->cfg.use_hadamard ? 1 : 0, c->cfg.fast_inter_mode, c->single_stream));
-    rc = single_wait(c, seq);
-    if (rc) return rc;
-    const fme_result& r = st->res;
-    half_xy[0] = r.half_x;
-    half_xy[1] = r.half_y;
-    qtr_xy[0] = r.qtr_x;
-    qtr_xy[1] = r.qtr_y;
-    *cost = r.frac_cost;
-    return FME_OK;
-  }
+  for (int y = 0; y < h; y++) std::memcpy(b->key + y * w, key + (ptrdiff_t)y * key_stride, (size_t)w * sizeof(int16_t));
   for (int y = 0; y < ph; y++) {
     const int16_t* src = ref + (ptrdiff_t)(mv_int_y - 4 + y) * ref_stride + (mv_int_x - 4);
-    uint8_t* dst = st->win + (size_t)y * pw;
+    uint8_t* dst = b->win + y * pw;
     for (int x = 0; x < pw; x++) dst[x] = (uint8_t)std::min(255, std::max(0, (int)src[x]));
   }
-  for (int y = 0; y < h; y++) std::memcpy(st->key + (size_t)y * w, key + (ptrdiff_t)y * key_stride, (size_t)w * sizeof(int16_t));
-  fme_job j{};
-  j.x = 4;
-  j.y = 4;
-  j.w = (uint8_t)w;
-  j.h = (uint8_t)h;
-  j.mvp_x = (int16_t)px;
-  j.mvp_y = (int16_t)py;
-  j.flags = lossless ? FME_JOB_LOSSLESS : 0;
-  j.key_offset = 0;
-  st->job = j;
-  st->perm[0] = 0;
-  st->ml = motion_lambda;
-  st->pic = PicDesc{};
-  st->pic.luma = c->stage_dev + offsetof(SingleStage, win);
-  st->pic.stride = pw;
-  st->pic.width = pw;
-  st->pic.height = ph;
-  BatchArgs a{};
-  a.jobs = reinterpret_cast<const fme_job*>(c->stage_dev + offsetof(SingleStage, job));
-  a.res = reinterpret_cast<fme_result*>(c->stage_dev + offsetof(SingleStage, res));
-  a.keys = reinterpret_cast<const int16_t*>(c->stage_dev + offsetof(SingleStage, key));
-  a.n_keys = (int64_t)w * h;
-  a.mlambda = reinterpret_cast<const double*>(c->stage_dev + offsetof(SingleStage, ml));
-  a.pics = reinterpret_cast<const PicDesc*>(c->stage_dev + offsetof(SingleStage, pic));
-  a.n = 1;
-  a.use_hadamard = c->cfg.use_hadamard ? 1 : 0;
-  a.fen = c->cfg.fast_inter_mode;
-  WorkBufs wb{};
-  wb.sjobs = const_cast<fme_job*>(a.jobs);
-  wb.perm = reinterpret_cast<int32_t*>(c->stage_dev + offsetof(SingleStage, perm));
-  HIP_TRY(launch_search_single(a, wb, cls, c->single_stream,
-                               reinterpret_cast<uint32_t*>(c->stage_dev + offsetof(SingleStage, flag)), seq));
-  rc = single_wait(c, seq);
+  b->kind = kSrvFrac;
+  b->w = w;
+  b->h = h;
+  b->mvp_x = px;
+  b->mvp_y = py;
+  b->sad = (lossless || !c->cfg.use_hadamard) ? 1 : 0;
+  b->ml = motion_lambda;
+  rc = srv_call(c, false);
   if (rc) return rc;
-  const fme_result& r = st->res;
-  half_xy[0] = r.half_x;
-  half_xy[1] = r.half_y;
-  qtr_xy[0] = r.qtr_x;
-  qtr_xy[1] = r.qtr_y;
-  *cost = r.frac_cost;
+  half_xy[0] = (int16_t)b->out[0];
+  half_xy[1] = (int16_t)b->out[1];
+  qtr_xy[0] = (int16_t)b->out[2];
+  qtr_xy[1] = (int16_t)b->out[3];
+  *cost = (uint32_t)b->out[4];
   return FME_OK;
 }
 
@@ -1142,7 +1169,20 @@ int fme_nn_pred_single(fme_ctx* c, const uint32_t* e, uint32_t cc, int pu_h, int
   const bool deep = c->cfg.nn_mode == 2;
   if (deep ? !c->net_loaded : !c->nn_loaded) return fail(FME_E_STATE, "fme_nn_pred_single: no weights loaded");
   HIP_TRY(hipSetDevice(c->device));
-  int rc = ensure_stage(c);
+  int rc;
+  if (!deep) {   // the master net: the server, weights in its LDS
+    rc = srv_open(c);
+    if (rc) return rc;
+    for (int s = 0; s < 8; s++) c->box->nn_in[s] = e[s];
+    c->box->nn_in[8] = cc;
+    c->box->nn_in[9] = (uint32_t)pu_h;
+    c->box->nn_in[10] = (uint32_t)pu_w;
+    c->box->kind = kSrvNn;
+    rc = srv_call(c, true);
+    if (rc) return rc;
+    *nn_class = c->box->out[0];
+  } else {
+  rc = ensure_stage(c);
   if (rc) return rc;
   // inputs in the kernel argument, the class and the completion word through mapped host memory:
   // one launch, a spin on the completion word
@@ -1154,12 +1194,12 @@ int fme_nn_pred_single(fme_ctx* c, const uint32_t* e, uint32_t cc, int pu_h, int
   int32_t* d_out = reinterpret_cast<int32_t*>(c->stage_dev + offsetof(SingleStage, nn_out));
   uint32_t* d_flag = reinterpret_cast<uint32_t*>(c->stage_dev + offsetof(SingleStage, flag));
   const uint32_t seq = ++c->single_seq;
-  HIP_TRY(deep ? launch_nn_deep_single(c->net, c->d_net.p, in, d_out, d_flag, seq, c->single_stream)
-               : launch_nn_single(c->d_nn.p, in, d_out, d_flag, seq, c->single_stream));
+  HIP_TRY(launch_nn_deep_single(c->net, c->d_net.p, in, d_out, d_flag, seq, c->single_stream));
   rc = single_wait(c, seq);
   if (rc) return rc;
-  const int32_t cls = c->stage->nn_out[0];
-  *nn_class = cls;
+  *nn_class = c->stage->nn_out[0];
+  }
+  const int cls = *nn_class;
   if (out4) {
     // MVX_HALF, MVX_QRTER, MVY_HALF, MVY_QRTER of the switch at TEncSearch.cpp:136-193:
     // the half/quarter split of the offset (cls % 7 - 3, cls / 7 - 3) with the quarter part

@@ -156,6 +156,7 @@ struct TzArgs {
   uint32_t* sad;              // may be null
   int16_t* emi_mv;            // [n][2] or null: the MV after the EMI square step (uni-pred EMI jobs)
   uint32_t* nn_in;            // [n][9] or null: FME_TZ_RING jobs' NN inputs (array_e[index_ref..+7], C)
+  int32_t* ctr;               // [3][8] per-kernel, per-XCD queue heads of the bulk search (zeroed per run)
 };
 int tz_kernel_of(int cls);    // 0: 4x8 units, 1: 8x4, 2: 8x8
 int tz_lanes_per_pu(int cls);
@@ -187,27 +188,30 @@ hipError_t launch_put_tables(PicDesc* d_pics, double* d_ml, const PicDesc* pics,
 // enough workgroups to fill the chip, each pulling tiles from its XCD's queue (then the other
 // XCDs').  `a.n` bounds the work.
 hipError_t launch_search_lane(const BatchArgs& a, const WorkBufs& w, hipStream_t s);
-// One PU of class cls whose job / key / picture / record pointers may be device-mapped host memory
-// (the single-PU entry point): one wave.
-hipError_t launch_search_single(const BatchArgs& a, const WorkBufs& w, int cls, hipStream_t s, uint32_t* flag,
-                                uint32_t seq);
-// fme_frac_dif_single for small PUs: the job, the window and the key travel in the kernel argument
-// (no dependent reads of host memory); the kernel stages them in a device scratch block, searches,
-// writes the record to mapped host memory, then the completion word (host spins on it).
 struct NnIn11 {   // NN_pred() inputs of a single call: array_e slots[8], C, PUHeight, PUWidth
   uint32_t v[11];
 };
-constexpr int kInlineBytes = 24 * 24 + 16 * 16 * 2;   // a <= 16x16 PU's window + int16 key
-struct SingleInline {
-  fme_job job;
-  double ml;
-  fme_result* res;             // mapped host record
-  uint32_t* flag;              // mapped host completion word
-  uint8_t* scratch;            // device: [job 32 B][perm 32 B][key][window]
-  int32_t win_stride, win_h, key_bytes, seq;
-  uint32_t data[kInlineBytes / 4];   // key (int16, w*h) then window ((w+8)*(h+8) bytes), dword-packed
+// The single-call server (fme_server.hip): one resident workgroup polls `req_seq` in this block of
+// pinned, device-mapped host memory, serves the call and releases `done_seq`; `stopped` = the
+// epoch of an instance that exited (idle, lifetime or `stop`).  Request fields share the first
+// lines, the answer has its own, the payload follows.
+enum { kSrvNn = 1, kSrvFrac = 2 };
+struct SrvBox {
+  uint32_t req_seq;            // host -> device, written last
+  uint32_t kind;               // kSrvNn / kSrvFrac
+  uint32_t stop;
+  int32_t w, h, mvp_x, mvp_y;  // FracDIF: PU size, predictor - 4 * integer MV (quarter-pel)
+  int32_t sad;                 // 1: SAD (lossless or HADME off), 0: SATD
+  double ml;                   // motion lambda (TComRdCost::m_motionLambda)
+  uint32_t nn_in[12];          // NN_pred: array_e[8], C, PUHeight, PUWidth
+  alignas(64) uint32_t done_seq;   // device -> host
+  uint32_t stopped;
+  int32_t out[6];              // FracDIF: half x, y, quarter x, y, cost; NN: class
+  alignas(64) int16_t key[64 * 64];
+  uint8_t win[72 * 72];        // (w + 8) x (h + 8) window around the integer MV, stride w + 8
 };
-hipError_t launch_search_single_inline(const SingleInline& p, int cls, int use_hadamard, int fen, hipStream_t s);
+hipError_t launch_server(SrvBox* box, const float* nn, uint32_t served, uint32_t epoch, uint64_t idle_ticks,
+                         uint64_t life_ticks, hipStream_t s);
 int lane_lanes_per_pu(int cls);                    // lanes of a class's PU group (pow2), 0: none
 int cu_count(int device);                          // compute units (workgroup budget of a launch)
 // Packed NN layout for the tail kernel (nn_pack, fme_kernels.hip): offsets in floats, every
@@ -231,6 +235,20 @@ static_assert(kNnPkW1 % 2 == 0 && kNnPkW2 % 2 == 0 && kNnPkW3 % 2 == 0 && kNnPkB
               kNnPkG1 % 2 == 0 && kNnPkBE1 % 2 == 0 && kNnPkB2 % 2 == 0 && kNnPkG2 % 2 == 0 &&
               kNnPkBE2 % 2 == 0 && kNnPkBout % 2 == 0, "pair regions must be 8-byte aligned");
 void nn_pack(const float* params, float* packed);   // FME_NN_PARAMS floats -> kNnPkFloats
+// NN_pred()'s embedding rows of PUHeight / PUWidth (the switches of TEncSearch.cpp:93-113)
+__device__ __forceinline__ int emb_row_h(int h) {
+  return h == 4 ? 1 : h == 8 ? 2 : h == 16 ? 3 : h == 12 ? 4 : h == 24 ? 5 : h == 32 ? 6 : h == 64 ? 7 : 0;
+}
+__device__ __forceinline__ int emb_row_w(int w) {
+  return w == 4 ? 1 : w == 8 ? 2 : w == 12 ? 3 : w == 16 ? 4 : w == 24 ? 5 : w == 32 ? 6 : w == 64 ? 7 : 0;
+}
+typedef float f2 __attribute__((ext_vector_type(2)));   // a row pair of the packed layout
+__device__ __forceinline__ f2 ld2(const float* __restrict__ Q, int o) { return *(const f2*)(Q + o); }
+__device__ __forceinline__ f2 relu2(f2 s) {
+  s.x = s.x < 0.0f ? 0.0f : s.x;
+  s.y = s.y < 0.0f ? 0.0f : s.y;
+  return s;
+}
 hipError_t launch_nn_tail(const BatchArgs& a, const WorkBufs& w, const float* nn_params,
                           int state_in, hipStream_t s);
 

@@ -265,19 +265,11 @@ enum {
   P_MEAN = 2042, P_STD = 2051
 };
 
-__device__ __forceinline__ int emb_row_h(int h) {
-  return h == 4 ? 1 : h == 8 ? 2 : h == 16 ? 3 : h == 12 ? 4 : h == 24 ? 5 : h == 32 ? 6 : h == 64 ? 7 : 0;
-}
-__device__ __forceinline__ int emb_row_w(int w) {
-  return w == 4 ? 1 : w == 8 ? 2 : w == 12 ? 3 : w == 16 ? 4 : w == 24 ? 5 : w == 32 ? 6 : w == 64 ? 7 : 0;
-}
 
 // Device layout of the net for the tail (built once per weight load by nn_pack, fme_device.h
 // kNnPk*): rows paired for packed f32 math (row r in .x, row r+1 in .y, so both halves run
 // the reference's sequential k order), and the 8 embedding terms of layer 1 folded into a
 // per-PU-shape prefix: the partial sums after k = 0..7 depend only on (PUHeight, PUWidth).
-typedef float f2 __attribute__((ext_vector_type(2)));
-
 void nn_pack(const float* P, float* Q) {
   for (int i = 0; i < kNnPkFloats; i++) Q[i] = 0.0f;
   for (int rh = 0; rh < 8; rh++)
@@ -312,12 +304,6 @@ void nn_pack(const float* P, float* Q) {
   }
 }
 
-__device__ __forceinline__ f2 ld2(const float* __restrict__ Q, int o) { return *(const f2*)(Q + o); }
-__device__ __forceinline__ f2 relu2(f2 s) {
-  s.x = s.x < 0.0f ? 0.0f : s.x;
-  s.y = s.y < 0.0f ? 0.0f : s.y;
-  return s;
-}
 
 // NN_pred() (TEncSearch.cpp:85-134) on the packed layout: float32, every dot product summed in
 // k order without contraction (the sequential-k contract), BN as x*g + b.  The
@@ -513,85 +499,6 @@ void k_nn_tail(BatchArgs a, WorkBufs w, const float* __restrict__ nnp_g, int sta
   }
 }
 
-// NN_pred() on one explicit input (fme_nn_pred_single): e[8], C, PUHeight, PUWidth.
-// fme_nn_pred_single: the 11 input words are the kernel argument; the class goes to mapped host
-// memory followed by the call's completion word (system-scope release; the host spins on it).
-// The same arithmetic as nn_forward with the rows spread over the wave (lane rp owns row pair rp of
-// each layer; every row is still summed in k order without contraction), so a single call's
-// latency is one dependent chain per layer instead of the whole net's.
-__global__ __launch_bounds__(64) void k_nn_single(const float* __restrict__ Q, NnIn11 in11, int32_t* out,
-                                                  uint32_t* flag, uint32_t seq) {
-  __shared__ float s_x1[22], s_x2[20];
-  const int rp = (int)threadIdx.x;
-  const int t = emb_row_h((int)in11.v[9]) * 8 + emb_row_w((int)in11.v[10]);
-  float in[9];
-  const uint32_t raw[9] = {in11.v[0], in11.v[1], in11.v[2], in11.v[3], in11.v[8],
-                           in11.v[4], in11.v[5], in11.v[6], in11.v[7]};
-#pragma unroll
-  for (int k = 0; k < 9; k++) {
-    float v = (float)raw[k];
-    v = (v - Q[kNnPkMean + k]) / Q[kNnPkStd + k];
-    in[k] = v * Q[kNnPkGin + k];
-  }
-  if (rp < 11) {
-    const float* pfx = Q + kNnPkPfx + t * 22;
-    f2 x = {pfx[2 * rp], pfx[2 * rp + 1]};
-#pragma unroll
-    for (int k = 0; k < 9; k++) x = x + ld2(Q, kNnPkW1 + (rp * 9 + k) * 2) * (f2){in[k], in[k]};
-    x = relu2(x + ld2(Q, kNnPkB1 + 2 * rp));
-    x = x * ld2(Q, kNnPkG1 + 2 * rp) + ld2(Q, kNnPkBE1 + 2 * rp);
-    s_x1[2 * rp] = x.x;
-    s_x1[2 * rp + 1] = x.y;
-  }
-  __syncthreads();
-  if (rp < 10) {
-    f2 x = {0.0f, 0.0f};
-#pragma unroll
-    for (int k = 0; k < 22; k++) x = x + ld2(Q, kNnPkW2 + (rp * 22 + k) * 2) * (f2){s_x1[k], s_x1[k]};
-    x = relu2(x + ld2(Q, kNnPkB2 + 2 * rp));
-    x = x * ld2(Q, kNnPkG2 + 2 * rp) + ld2(Q, kNnPkBE2 + 2 * rp);
-    s_x2[2 * rp] = x.x;
-    s_x2[2 * rp + 1] = x.y;
-  }
-  __syncthreads();
-  // output row pair rp, then the first maximum over the 49 rows (strict >, rows in order)
-  float bv = -INFINITY;
-  int bi = 64;
-  if (rp < 25) {
-    f2 x = {0.0f, 0.0f};
-#pragma unroll
-    for (int k = 0; k < 20; k++) x = x + ld2(Q, kNnPkW3 + (rp * 20 + k) * 2) * (f2){s_x2[k], s_x2[k]};
-    x = x + ld2(Q, kNnPkBout + 2 * rp);
-    // the batch rule's NaNs (row 0 taken first, then strict >): a NaN row 0 wins, a later NaN never
-    if (x.x != x.x) x.x = rp == 0 ? INFINITY : -INFINITY;
-    if (x.y != x.y) x.y = -INFINITY;
-    bv = x.x;
-    bi = 2 * rp;
-    if (rp < 24 && x.y > bv) {
-      bv = x.y;
-      bi = 2 * rp + 1;
-    }
-  }
-#pragma unroll
-  for (int off = 1; off < 64; off <<= 1) {
-    const float ov = __shfl_xor(bv, off, 64);
-    const int oi = __shfl_xor(bi, off, 64);
-    if (ov > bv || (ov == bv && oi < bi)) {
-      bv = ov;
-      bi = oi;
-    }
-  }
-  if (rp == 0) {
-    out[0] = bi;
-    __hip_atomic_store(flag, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-  }
-}
-
-hipError_t launch_nn_single(const float* nnp, const NnIn11& in, int32_t* out, uint32_t* flag, uint32_t seq,
-                            hipStream_t s) {
-  hipLaunchKernelGGL(k_nn_single, dim3(1), dim3(64), 0, s, nnp, in, out, flag, seq);
-  return hipGetLastError();
-}
 
 // ---------------------------------------------------------------------------------------
 // host launch helpers

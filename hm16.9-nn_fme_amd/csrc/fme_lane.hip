@@ -1288,85 +1288,6 @@ void k_search_lane(BatchArgs a, WorkBufs w) {
 }
 #undef FME_CASE
 
-// The single-PU entry point's kernel (fme_frac_dif_single): one workgroup of one wave searches one
-// PU of class `cls` whose job, key, window picture and record all live in pinned, device-mapped host
-// memory — one launch per call, no copies.
-#define FME_SCASE(ID, PW_, PH_, UW_, UH_)                                                            \
-  case ID:                                                                                           \
-    lane_unit<PW_, PH_, UW_, UH_>(a, w.sjobs, w.perm, 0, 1, 0);                                      \
-    break;
-// Completion: every record store of the wave is done (barrier), then one system-scope release of
-// the call's sequence number into mapped host memory (the host spins on it instead of a stream
-// synchronisation: launch_latency probe, 6.3 vs 10.3 us round trip).
-__device__ __forceinline__ void single_done(uint32_t* flag, uint32_t seq) {
-  __syncthreads();
-  if (threadIdx.x == 0 && flag) __hip_atomic_store(flag, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-}
-__global__ __launch_bounds__(64) void k_search_single(BatchArgs a, WorkBufs w, int cls, uint32_t* flag, uint32_t seq) {
-  if (threadIdx.x < sizeof(PicDesc) / 4)
-    reinterpret_cast<uint32_t*>(g_pics)[threadIdx.x] = reinterpret_cast<const uint32_t*>(a.pics)[threadIdx.x];
-  if (threadIdx.x == 0) g_ml[0] = a.mlambda[0];
-  __syncthreads();
-  switch (cls) {
-    FME_LANE_CLASSES(FME_SCASE)
-    default: break;
-  }
-  single_done(flag, seq);
-}
-
-hipError_t launch_search_single(const BatchArgs& a, const WorkBufs& w, int cls, hipStream_t s, uint32_t* flag,
-                                uint32_t seq) {
-  hipLaunchKernelGGL(k_search_single, dim3(1), dim3(64), 0, s, a, w, cls, flag, seq);
-  return hipGetLastError();
-}
-
-// Small PUs: the call's whole input is the kernel argument.  The wave copies the key and window
-// from the kernarg segment into its device scratch block (read back by the same workgroup after
-// the barrier), then runs the batch kernel's per-PU search on it.
-__global__ __launch_bounds__(64) void k_search_single_inline(SingleInline p, int cls, int use_hadamard, int fen) {
-  const uint32_t* kd = p.data;   // read from the kernarg segment
-  uint32_t* sc = reinterpret_cast<uint32_t*>(p.scratch);
-  const int nd = (p.key_bytes + p.win_stride * p.win_h + 3) >> 2;
-  for (int i = (int)threadIdx.x; i < nd; i += 64) sc[16 + i] = kd[i];
-  if (threadIdx.x < 8) sc[threadIdx.x] = reinterpret_cast<const uint32_t*>(&p.job)[threadIdx.x];
-  if (threadIdx.x == 8) sc[8] = 0;   // perm[0]
-  if (threadIdx.x == 0) {
-    PicDesc pd{};
-    pd.luma = p.scratch + 64 + p.key_bytes;
-    pd.stride = pd.width = p.win_stride;
-    pd.height = p.win_h;
-    g_pics[0] = pd;
-    g_ml[0] = p.ml;
-  }
-  __syncthreads();
-  BatchArgs a{};
-  a.jobs = reinterpret_cast<const fme_job*>(p.scratch);
-  a.res = p.res;
-  a.keys = reinterpret_cast<const int16_t*>(p.scratch + 64);
-  a.n_keys = p.key_bytes / 2;
-  a.n = 1;
-  a.use_hadamard = use_hadamard;
-  a.fen = fen;
-  const fme_job* sj = reinterpret_cast<const fme_job*>(p.scratch);
-  const int32_t* perm = reinterpret_cast<const int32_t*>(p.scratch + 32);
-  switch (cls) {
-#define FME_ICASE(ID, PW_, PH_, UW_, UH_)                                                            \
-  case ID:                                                                                           \
-    if constexpr (PW_ <= 16 && PH_ <= 16) lane_unit<PW_, PH_, UW_, UH_>(a, sj, perm, 0, 1, 0);        \
-    break;
-    FME_LANE_CLASSES(FME_ICASE)
-#undef FME_ICASE
-    default: break;
-  }
-  single_done(p.flag, (uint32_t)p.seq);
-}
-#undef FME_SCASE
-
-hipError_t launch_search_single_inline(const SingleInline& p, int cls, int use_hadamard, int fen, hipStream_t s) {
-  hipLaunchKernelGGL(k_search_single_inline, dim3(1), dim3(64), 0, s, p, cls, use_hadamard, fen);
-  return hipGetLastError();
-}
-
 // Lanes per PU of a lane-kernel class, 0 for classes the cooperative kernels serve.
 int lane_lanes_per_pu(int cls) {
   switch (cls) {

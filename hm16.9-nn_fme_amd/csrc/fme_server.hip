@@ -1,0 +1,352 @@
+// fme_server.hip — the single-call server behind fme_frac_dif_single and fme_nn_pred_single.
+//
+// TEncSearch calls xPatternSearchFracDIF (TEncSearch.cpp:5232-5269) and NN_pred (85-204) once per
+// PU, so the drop-in entry points are latency-bound: a kernel launch plus its completion costs
+// more than the work.  Instead one workgroup stays resident while calls keep coming: it polls a
+// request word in pinned, device-mapped host memory (SrvBox, fme_device.h), serves the call with
+// all 16 of its waves, writes the answer back to host memory and releases a completion word the
+// host spins on.  It exits after kSrv idle time without a request, after its lifetime, or when
+// the host sets `stop`, and says so in `stopped` (the instance's epoch); the host relaunches it on
+// the next call (fme_api.cpp srv_call), so no wave outlives its process by more than the idle
+// limit and a batch queued behind it on a shared hardware queue waits at most that long.
+//
+// FracDIF is restated latency-first: a lane per pixel of an 8x8 block (or of four 4x4 blocks), a
+// wave per (candidate, block), the separable filter's first stage for the three fractional phases
+// computed once into LDS, SATD butterflies across lanes.  Same arithmetic as the batch kernel and
+// the oracle (orc_frac_dif): bit-exact.
+#include "fme_device.h"
+
+namespace fme {
+namespace {
+
+constexpr int kSrvThreads = 1024;
+
+// TComInterpolationFilter::m_lumaFilter (TComInterpolationFilter.cpp:57-63)
+__constant__ int8_t kSrvLuma[4][8] = {{0, 0, 0, 64, 0, 0, 0, 0},
+                                      {-1, 4, -10, 58, 17, -5, 1, 0},
+                                      {-1, 4, -11, 40, 40, -11, 4, -1},
+                                      {0, 1, -5, 17, 58, -10, 4, -1}};
+// xPatternRefinement's candidate orders (TEncSearch.cpp:1591-1645 over s_acMvRefineH / Q)
+__constant__ int8_t kSrvRefH[9][2] = {{0, 0}, {0, -1}, {0, 1}, {-1, 0}, {1, 0}, {-1, -1}, {1, -1}, {-1, 1}, {1, 1}};
+__constant__ int8_t kSrvRefQ[9][2] = {{0, 0}, {0, -1}, {0, 1}, {-1, -1}, {1, -1}, {-1, 0}, {1, 0}, {-1, 1}, {1, 1}};
+
+__device__ __forceinline__ uint32_t sys_load(const uint32_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ void sys_store_release(uint32_t* p, uint32_t v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// TComRdCost::xGetExpGolombNumberOfBits (TComRdCost.cpp:172-185): 2 * floor(log2 t) + 1
+__device__ __forceinline__ uint32_t eg_bits_d(int v) {
+  const uint32_t t = v <= 0 ? ((uint32_t)(-v) << 1) + 1u : (uint32_t)v << 1;
+  return 2u * (31u - (uint32_t)__clz((int)t)) + 1u;
+}
+
+struct SrvLds {
+  float nn[kNnPkFloats];
+  float x1[22], x2[20];
+  int16_t key[64 * 64];
+  int16_t hp[3][72 * 65];       // first filter stage, fractional phase 1..3, columns -1 .. w-1
+  uint8_t win[72 * 72];
+  uint32_t cost[16];
+  int32_t ctl[8];               // stop, seq, kind, w, h, mvp_x, mvp_y, sad
+  uint32_t nn_in[12];
+  double ml;
+  int32_t sel[2];               // half-stage best (hx, hy)
+};
+
+// First-stage sample at window row wy, PU column x (window column x + 4), phase fx: the 14-bit
+// value m_filteredBlockTmp holds (filterHor isLast = false; filterCopy isFirst for fx = 0).
+__device__ __forceinline__ int h_stage(const SrvLds& L, int w, int fx, int x, int wy) {
+  return fx ? (int)L.hp[fx - 1][wy * (w + 1) + x + 1] : ((int)L.win[wy * (w + 8) + x + 4] << 6) - 8192;
+}
+
+// The 9 candidates of one xPatternRefinement stage: distortion per candidate into L.cost.
+// (ox, oy) of candidate k = base + 2 * ref (half) or base + ref (quarter), quarter-pel offsets from
+// the integer MV.  Work item (candidate, block) per wave; lanes are the block's pixels.
+__device__ void stage_dist(SrvLds& L, int w, int h, bool sad, bool half, int bx0, int by0) {
+  const int lane = (int)threadIdx.x & 63, wid = (int)threadIdx.x >> 6;
+  const bool b8 = !sad && (w & 7) == 0 && (h & 7) == 0;   // xGetHADs: 8x8 when both dims allow
+  const int nb4 = (w >> 2) * (h >> 2);
+  const int nb = b8 ? (w >> 3) * (h >> 3) : (nb4 + 3) >> 2;
+  for (int item = wid; item < 9 * nb; item += kSrvThreads / 64) {
+    const int k = item / nb, b = item - k * nb;
+    const int ox = bx0 + (half ? 2 * kSrvRefH[k][0] : kSrvRefQ[k][0]);
+    const int oy = by0 + (half ? 2 * kSrvRefH[k][1] : kSrvRefQ[k][1]);
+    int c, r;
+    bool valid = true;
+    if (b8) {
+      const int bw = w >> 3;
+      c = (b % bw) * 8 + (lane & 7);
+      r = (b / bw) * 8 + (lane >> 3);
+    } else {
+      int blk = b * 4 + (lane >> 4);
+      valid = blk < nb4;
+      blk = valid ? blk : 0;
+      const int bw = w >> 2;
+      c = (blk % bw) * 4 + (lane & 3);
+      r = (blk / bw) * 4 + ((lane >> 2) & 3);
+    }
+    const int ix = ox >> 2, fx = ox & 3, iy = oy >> 2, fy = oy & 3;
+    const int x = c + ix, wy0 = r + iy + 4;
+    int v;
+    if (fy == 0) {
+      v = (h_stage(L, w, fx, x, wy0) + 8192 + 32) >> 6;   // filterCopy, !isFirst isLast
+    } else {
+      int s = 0;
+#pragma unroll
+      for (int t = 0; t < 8; t++) s += (int)kSrvLuma[fy][t] * h_stage(L, w, fx, x, wy0 + t - 3);
+      v = (s + 2048 + (8192 << 6)) >> 12;                  // filter<8, true, false, true>
+    }
+    v = min(255, max(0, v));
+    int d = valid ? (int)L.key[r * w + c] - v : 0;
+    uint32_t add;
+    if (sad) {
+      uint32_t a = (uint32_t)abs(d);
+#pragma unroll
+      for (int m = 1; m < 64; m <<= 1) a += (uint32_t)__shfl_xor((int)a, m, 64);
+      add = a;
+    } else if (b8) {   // 8x8 Walsh-Hadamard across the lanes, sum |coef|, (s + 2) >> 2 (xCalcHADs8x8)
+#pragma unroll
+      for (int m = 1; m < 64; m <<= 1) {
+        const int p = __shfl_xor(d, m, 64);
+        d = (lane & m) ? p - d : d + p;
+      }
+      uint32_t a = (uint32_t)abs(d);
+#pragma unroll
+      for (int m = 1; m < 64; m <<= 1) a += (uint32_t)__shfl_xor((int)a, m, 64);
+      add = (a + 2) >> 2;
+    } else {           // four 4x4 blocks per wave, each (s + 1) >> 1 (xCalcHADs4x4)
+#pragma unroll
+      for (int m = 1; m < 16; m <<= 1) {
+        const int p = __shfl_xor(d, m, 64);
+        d = (lane & m) ? p - d : d + p;
+      }
+      uint32_t a = (uint32_t)abs(d);
+#pragma unroll
+      for (int m = 1; m < 16; m <<= 1) a += (uint32_t)__shfl_xor((int)a, m, 64);
+      a = valid ? (a + 1) >> 1 : 0u;
+      add = (uint32_t)__shfl((int)a, 0, 64) + (uint32_t)__shfl((int)a, 16, 64) + (uint32_t)__shfl((int)a, 32, 64) +
+            (uint32_t)__shfl((int)a, 48, 64);
+    }
+    if (lane == 0) atomicAdd(&L.cost[k], add);
+  }
+}
+
+// Wave 0: distortion + MV cost per candidate (lane k), the first strict minimum in candidate order.
+__device__ void stage_pick(const SrvLds& L, bool half, int hx, int hy, int& best_k, uint32_t& best) {
+  const int lane = (int)threadIdx.x & 63;
+  const int px = L.ctl[5], py = L.ctl[6];
+  uint32_t tot = 0xFFFFFFFFu;
+  if (lane < 9) {
+    // getCostOfVectorWithPredictor at cost scale 1 (half) / 0 (quarter), MV relative to the
+    // integer MV (the predictor came shifted by 4 * mv_int)
+    const int mx = half ? 2 * kSrvRefH[lane][0] : 2 * hx + kSrvRefQ[lane][0];
+    const int my = half ? 2 * kSrvRefH[lane][1] : 2 * hy + kSrvRefQ[lane][1];
+    const uint32_t bits = eg_bits_d(mx - px) + eg_bits_d(my - py);
+    tot = L.cost[lane] + (uint32_t)((L.ml * (double)bits) / 65536.0);
+  }
+  int k = lane < 9 ? lane : 64;
+#pragma unroll
+  for (int m = 1; m < 16; m <<= 1) {
+    const uint32_t ot = (uint32_t)__shfl_xor((int)tot, m, 64);
+    const int ok = __shfl_xor(k, m, 64);
+    if (ot < tot || (ot == tot && ok < k)) {
+      tot = ot;
+      k = ok;
+    }
+  }
+  best_k = k;
+  best = tot;
+}
+
+__device__ void serve_frac(SrvLds& L, SrvBox* box) {
+  const int tid = (int)threadIdx.x;
+  const int w = L.ctl[3], h = L.ctl[4];
+  const bool sad = L.ctl[7] != 0;
+  const int pw = w + 8, ph = h + 8;
+  // the call's window and key (host memory, read once, in parallel)
+  {
+    const uint32_t* wsrc = reinterpret_cast<const uint32_t*>(box->win);
+    uint32_t* wdst = reinterpret_cast<uint32_t*>(L.win);
+    for (int i = tid; i < (pw * ph + 3) >> 2; i += kSrvThreads) wdst[i] = wsrc[i];
+    const uint32_t* ksrc = reinterpret_cast<const uint32_t*>(box->key);
+    uint32_t* kdst = reinterpret_cast<uint32_t*>(L.key);
+    for (int i = tid; i < (w * h) >> 1; i += kSrvThreads) kdst[i] = ksrc[i];
+    if (tid < 16) L.cost[tid] = 0;
+  }
+  __syncthreads();
+  // first filter stage of phases 1..3 over window rows 0 .. h+7, PU columns -1 .. w-1
+  {
+    const int cols = w + 1, plane = ph * cols;
+    for (int i = tid; i < 3 * plane; i += kSrvThreads) {
+      const int f = i / plane, rem = i - f * plane, wy = rem / cols, x = rem - wy * cols - 1;
+      const uint8_t* row = L.win + wy * pw + x + 1;   // taps at window columns x + 4 - 3 ...
+      int s = 0;
+#pragma unroll
+      for (int t = 0; t < 8; t++) s += (int)kSrvLuma[f + 1][t] * (int)row[t];
+      L.hp[f][rem] = (int16_t)(s - 8192);
+    }
+  }
+  __syncthreads();
+  stage_dist(L, w, h, sad, true, 0, 0);
+  __syncthreads();
+  if (tid < 64) {
+    int k;
+    uint32_t best;
+    stage_pick(L, true, 0, 0, k, best);
+    if (tid == 0) {
+      L.sel[0] = kSrvRefH[k][0];
+      L.sel[1] = kSrvRefH[k][1];
+    }
+  }
+  __syncthreads();
+  const int hx = L.sel[0], hy = L.sel[1];
+  if (tid < 16) L.cost[tid] = 0;
+  __syncthreads();
+  stage_dist(L, w, h, sad, false, 2 * hx, 2 * hy);
+  __syncthreads();
+  if (tid < 64) {
+    int k;
+    uint32_t best;
+    stage_pick(L, false, hx, hy, k, best);
+    if (tid == 0) {
+      box->out[0] = hx;
+      box->out[1] = hy;
+      box->out[2] = kSrvRefQ[k][0];
+      box->out[3] = kSrvRefQ[k][1];
+      box->out[4] = (int32_t)best;
+    }
+  }
+}
+
+// NN_pred (TEncSearch.cpp:85-134) on the packed layout in LDS: lane rp owns row pair rp of each
+// layer, every row summed in k order without contraction (the batch tail's arithmetic).
+__device__ void serve_nn(SrvLds& L, SrvBox* box) {
+  const int rp = (int)threadIdx.x;
+  const float* Q = L.nn;
+  const uint32_t* v = L.nn_in;   // copied by the polling lane with the request
+  const int t = emb_row_h((int)v[9]) * 8 + emb_row_w((int)v[10]);
+  float in[9];
+  const uint32_t raw[9] = {v[0], v[1], v[2], v[3], v[8], v[4], v[5], v[6], v[7]};
+#pragma unroll
+  for (int k = 0; k < 9; k++) {
+    float x = (float)raw[k];
+    x = (x - Q[kNnPkMean + k]) / Q[kNnPkStd + k];
+    in[k] = x * Q[kNnPkGin + k];
+  }
+  if (rp < 11) {
+    const float* pfx = Q + kNnPkPfx + t * 22;
+    f2 x = {pfx[2 * rp], pfx[2 * rp + 1]};
+#pragma unroll
+    for (int k = 0; k < 9; k++) x = x + ld2(Q, kNnPkW1 + (rp * 9 + k) * 2) * (f2){in[k], in[k]};
+    x = relu2(x + ld2(Q, kNnPkB1 + 2 * rp));
+    x = x * ld2(Q, kNnPkG1 + 2 * rp) + ld2(Q, kNnPkBE1 + 2 * rp);
+    L.x1[2 * rp] = x.x;
+    L.x1[2 * rp + 1] = x.y;
+  }
+  __syncthreads();
+  if (rp < 10) {
+    f2 x = {0.0f, 0.0f};
+#pragma unroll
+    for (int k = 0; k < 22; k++) x = x + ld2(Q, kNnPkW2 + (rp * 22 + k) * 2) * (f2){L.x1[k], L.x1[k]};
+    x = relu2(x + ld2(Q, kNnPkB2 + 2 * rp));
+    x = x * ld2(Q, kNnPkG2 + 2 * rp) + ld2(Q, kNnPkBE2 + 2 * rp);
+    L.x2[2 * rp] = x.x;
+    L.x2[2 * rp + 1] = x.y;
+  }
+  __syncthreads();
+  if (rp < 64) {
+    // output row pair rp, then the first maximum over the 49 rows (strict >, rows in order)
+    float bv = -INFINITY;
+    int bi = 64;
+    if (rp < 25) {
+      f2 x = {0.0f, 0.0f};
+#pragma unroll
+      for (int k = 0; k < 20; k++) x = x + ld2(Q, kNnPkW3 + (rp * 20 + k) * 2) * (f2){L.x2[k], L.x2[k]};
+      x = x + ld2(Q, kNnPkBout + 2 * rp);
+      // the batch rule's NaNs (row 0 taken first, then strict >): a NaN row 0 wins, a later NaN never
+      if (x.x != x.x) x.x = rp == 0 ? INFINITY : -INFINITY;
+      if (x.y != x.y) x.y = -INFINITY;
+      bv = x.x;
+      bi = 2 * rp;
+      if (rp < 24 && x.y > bv) {
+        bv = x.y;
+        bi = 2 * rp + 1;
+      }
+    }
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+      const float ov = __shfl_xor(bv, off, 64);
+      const int oi = __shfl_xor(bi, off, 64);
+      if (ov > bv || (ov == bv && oi < bi)) {
+        bv = ov;
+        bi = oi;
+      }
+    }
+    if (rp == 0) box->out[0] = bi;
+  }
+}
+
+__global__ __launch_bounds__(kSrvThreads) void k_server(SrvBox* box, const float* nn, uint32_t served, uint32_t epoch,
+                                                        uint64_t idle_ticks, uint64_t life_ticks) {
+  __shared__ SrvLds L;
+  const int tid = (int)threadIdx.x;
+  if (nn)
+    for (int i = tid; i < kNnPkFloats; i += kSrvThreads) L.nn[i] = nn[i];
+  const uint64_t t0 = wall_clock64();
+  uint64_t last = t0;
+  for (;;) {
+    if (tid == 0) {
+      uint32_t seq = served, stop = 0;
+      for (;;) {
+        seq = sys_load(&box->req_seq);
+        stop = sys_load(&box->stop);
+        if (seq != served || stop) break;
+        const uint64_t now = wall_clock64();
+        if (now - last > idle_ticks || now - t0 > life_ticks) {
+          stop = 1;
+          break;
+        }
+        __builtin_amdgcn_s_sleep(2);
+      }
+      L.ctl[0] = (int32_t)stop;
+      L.ctl[1] = (int32_t)seq;
+      if (!stop) {
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");   // the request's payload after its word
+        L.ctl[2] = (int32_t)box->kind;
+        L.ctl[3] = box->w;
+        L.ctl[4] = box->h;
+        L.ctl[5] = box->mvp_x;
+        L.ctl[6] = box->mvp_y;
+        L.ctl[7] = box->sad;
+        L.ml = box->ml;
+        for (int k = 0; k < 11; k++) L.nn_in[k] = box->nn_in[k];
+      }
+    }
+    __syncthreads();
+    if (L.ctl[0]) break;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+    const uint32_t seq = (uint32_t)L.ctl[1];
+    if (L.ctl[2] == kSrvFrac)
+      serve_frac(L, box);
+    else
+      serve_nn(L, box);
+    __syncthreads();
+    if (tid == 0) sys_store_release(&box->done_seq, seq);   // after the answer's stores
+    served = seq;
+    last = wall_clock64();
+  }
+  if (tid == 0) sys_store_release(&box->stopped, epoch);
+}
+
+}  // namespace
+
+hipError_t launch_server(SrvBox* box, const float* nn, uint32_t served, uint32_t epoch, uint64_t idle_ticks,
+                         uint64_t life_ticks, hipStream_t s) {
+  hipLaunchKernelGGL(k_server, dim3(1), dim3(kSrvThreads), 0, s, box, nn, served, epoch, idle_ticks, life_ticks);
+  return hipGetLastError();
+}
+
+}  // namespace fme

@@ -104,32 +104,76 @@ def test_invalid_jobs_rejected():
     _assert_same(ctx.refine(g["jobs"][:40]), g["results"][:40], "after rejection")
 
 
-def test_frac_dif_single_matches_batch():
-    """The TEncSearch-shaped single-PU entry point equals the batch path's FracDIF fields."""
-    g = load_golden("ldp_qp22_hadme_fen1_nn")
-    ctx = _ctx(g)
+def _frac_single_check(ctx, g, idx):
     jobs, ref = g["jobs"], g["results"]
     pics = g["pictures"]
     pad = 80
-    checked = 0
-    for i in range(0, len(jobs), 37):
+    planes = {}
+    for i in idx:
         j, r = jobs[i], ref[i]
         w, h, x, y = int(j["w"]), int(j["h"]), int(j["x"]), int(j["y"])
-        plane = np.pad(pics[int(j["ref_id"])].astype(np.int16), pad, mode="edge")
+        rid = int(j["ref_id"])
+        if rid not in planes:
+            planes[rid] = np.pad(pics[rid].astype(np.int16), pad, mode="edge")
         if int(j["key_offset"]) >= 0:
             key = g["keys"][int(j["key_offset"]):int(j["key_offset"]) + w * h].reshape(h, w)
         else:
             key = pics[int(j["org_id"])][y:y + h, x:x + w]
         ml = 65536.0 * np.sqrt(float(g["lambdas"][int(j["lambda_id"])]))
-        half, qtr, cost = ctx.frac_dif_single(key, plane, (y + pad, x + pad),
+        half, qtr, cost = ctx.frac_dif_single(key, planes[rid], (y + pad, x + pad),
                                               (int(r["mv_int_x"]), int(r["mv_int_y"])),
                                               (int(j["mvp_x"]), int(j["mvp_y"])), ml,
                                               lossless=bool(j["flags"] & 4))
-        assert half == (int(r["half_x"]), int(r["half_y"])), i
-        assert qtr == (int(r["qtr_x"]), int(r["qtr_y"])), i
-        assert cost == int(r["frac_cost"]), i
-        checked += 1
-    assert checked > 20
+        assert (half, qtr, cost) == ((int(r["half_x"]), int(r["half_y"])), (int(r["qtr_x"]), int(r["qtr_y"])),
+                                     int(r["frac_cost"])), (i, w, h)
+
+
+def test_frac_dif_single_matches_batch():
+    """The TEncSearch-shaped single-PU entry point (the resident server, fme_server.hip) equals the
+    batch path's FracDIF fields."""
+    g = load_golden("ldp_qp22_hadme_fen1_nn")
+    _frac_single_check(_ctx(g), g, range(0, len(g["jobs"]), 37))
+
+
+@pytest.mark.parametrize("case", golden_cases())
+def test_frac_dif_single_every_shape(case):
+    """Every PU shape of every golden case (SATD 8x8 / 4x4 tilings, SAD with HADME off and for
+    lossless jobs, bi-pred keys outside 0..255), up to 6 jobs per shape."""
+    g = load_golden(case)
+    jobs = g["jobs"]
+    idx = []
+    for (w, h) in synth.ALL_PU_SIZES:
+        sel = np.flatnonzero((jobs["w"] == w) & (jobs["h"] == h))
+        idx += list(sel[:: max(1, len(sel) // 6)][:6])
+    lossless = np.flatnonzero(jobs["flags"] & 4)
+    idx += list(lossless[:8])
+    _frac_single_check(_ctx(g), g, idx)
+
+
+def test_single_call_server_lifecycle():
+    """The server instance idles out and is relaunched by the next call, is stopped by batch work
+    and by a weight reload (its LDS copy of the net), and answers the same across all of it."""
+    import time
+    from oracle import Oracle
+    g = load_golden("ldp_qp22_hadme_fen1_nn")
+    ctx = _ctx(g)
+    idx = list(range(0, 400, 40))
+    _frac_single_check(ctx, g, idx)
+    time.sleep(0.02)                                     # > the idle limit: the instance has left
+    _frac_single_check(ctx, g, idx)
+    _assert_same(ctx.refine(g["jobs"][:64]), g["results"][:64], "batch between single calls")
+    _frac_single_check(ctx, g, idx)
+    o = Oracle()
+    e, c = np.arange(1000, 9000, 1000, dtype=np.uint32), 4321
+    for qp in (22, 27, 22):                              # the resident copy follows each reload
+        ctx.load_nn(weights.load_weights(qp))
+        cls, _ = ctx.nn_pred_single(e, c, 16, 8)
+        assert cls == o.nn_class(weights.load_weights(qp), e, c, 16, 8)[0]
+    t0 = time.perf_counter()
+    for _ in range(300):
+        ctx.nn_pred_single(e, c, 16, 8)
+    per_call = (time.perf_counter() - t0) / 300
+    assert per_call < 200e-6, per_call
 
 
 @pytest.mark.parametrize("qp", [22, 27, 32, 37])
