@@ -142,7 +142,6 @@ struct fme_ctx {
   DevBuf<fme_tz_ext> d_tz_ext;
   DevBuf<uint32_t> d_tz_sad;
   DevBuf<uint32_t> d_tz_nn_in;   // staging of fme_integer_search_ring's NN input rows
-  DevBuf<int32_t> d_tz_ctr;      // the bulk search's per-XCD queue heads
   hipEvent_t ev_tz[2] = {nullptr, nullptr};
   bool tz_timed = false;
   // predInterSearch producer: m_integerMv2Nx2N[REF_PIC_LIST_0][k] (TEncSearch.h:118), AMVP staging
@@ -272,7 +271,7 @@ int fme_destroy(fme_ctx* c) {
   c->d_pics.release(); c->d_mlambda.release(); c->d_keys.release(); c->d_nn.release(); c->d_net.release();
   c->d_jobs.release(); c->d_res.release(); c->d_mv.release(); c->cls.release(); c->perm.release(); c->sjobs.release();
   c->counts.release(); c->blk_agg.release(); c->blk_prefix.release(); c->nn_state.release();
-  c->ipos.release(); c->srec.release(); c->d_tz_ctr.release();
+  c->ipos.release(); c->srec.release();
   c->d_sched.release();
   if (c->ev_done) (void)hipEventDestroy(c->ev_done);
   if (c->stage) (void)hipHostFree(c->stage);
@@ -802,9 +801,6 @@ static int tz_run(fme_ctx* c, fme_job* d_jobs, const fme_tz_ext* d_ext, uint32_t
   ta.sad = d_sad;
   ta.emi_mv = d_emi;
   ta.nn_in = d_nn_in;
-  HIP_TRY(c->d_tz_ctr.reserve(24));
-  ta.ctr = c->d_tz_ctr.p;
-  HIP_TRY(hipMemsetAsync(ta.ctr, 0, 24 * sizeof(int32_t), s));
   if (c->profiling) HIP_TRY(hipEventRecord(c->ev_tz[0], s));
   // the three unit-shape kernels are latency-bound and independent: 4x8 and 8x4 units on the two
   // auxiliary streams, 8x8 units on the caller's stream, joined before returning

@@ -156,7 +156,6 @@ struct TzArgs {
   uint32_t* sad;              // may be null
   int16_t* emi_mv;            // [n][2] or null: the MV after the EMI square step (uni-pred EMI jobs)
   uint32_t* nn_in;            // [n][9] or null: FME_TZ_RING jobs' NN inputs (array_e[index_ref..+7], C)
-  int32_t* ctr;               // [3][8] per-kernel, per-XCD queue heads of the bulk search (zeroed per run)
 };
 int tz_kernel_of(int cls);    // 0: 4x8 units, 1: 8x4, 2: 8x8
 int tz_lanes_per_pu(int cls);

@@ -67,12 +67,6 @@
 #ifndef FME_LANE_WAVES
 #define FME_LANE_WAVES 2
 #endif
-// 1: one unit per lane loads ONE window, rows -5..UH+4 and cols -5..UW+4 around the TZ MV, for both
-// the EMI step and the sub-pel passes (re-centred on the EMI best in registers: a row select and a
-// byte shift per dword); 0: the EMI window, then a second, dependent load around mv_int'.
-#ifndef FME_LANE_BIGWIN
-#define FME_LANE_BIGWIN 1
-#endif
 
 namespace fme {
 namespace {
@@ -856,15 +850,10 @@ __device__ FME_LANE_UNIT_ATTR void lane_unit(const BatchArgs& a, const fme_job* 
   // one unit per lane: its key rows are loaded once, for the EMI step and the sub-pel passes
   uint32_t kraw0[UH][KW];
   if constexpr (UPL == 1) load_kraw(0, kraw0);
-  // FME_LANE_BIGWIN: the whole neighbourhood the EMI step can move to, loaded with the key
-  constexpr bool kBig = FME_LANE_BIGWIN && UPL == 1;
-  constexpr int BR = kBig ? UH + 10 : 1;   // rows -5 .. UH+4
-  uint32_t bw[BR][4];                       // cols -5 .. UW+4 (14 of 16 bytes)
-  if constexpr (kBig) load_window(ref, ox + (int)j.mv_x - 5, oy + (int)j.mv_y - 5, bw);
 
   // ---- 1. EMI square step -----------------------------------------------------------------------
   int mvx = j.mv_x, mvy = j.mv_y;
-  int ex = 0, ey = 0, n_emi = 0;
+  int n_emi = 0;
   uint32_t cval = 0, emi[8];
 #pragma unroll
   for (int k = 0; k < 8; k++) emi[k] = 0;
@@ -883,15 +872,9 @@ __device__ FME_LANE_UNIT_ATTR void lane_unit(const BatchArgs& a, const fme_job* 
       } else {
         load_kraw(h, kraw);
       }
-      // integer samples at rows -1 .. UH, cols -1 .. UW around the TZ MV (s - 128 bytes); with the
-      // big window: its rows 4 .. UH+5, bytes 4 .. (EMI offset e -> bytes 4 + e of bw)
-      constexpr int EO = kBig ? 4 : 0;   // window offset of row / column -1
-      uint32_t w[kBig ? 1 : UH + 2][kBig ? 4 : EW];
-      if constexpr (!kBig) load_window(ref, ox + mvx - 1, oy + h * kHalfRows + mvy - 1, w);
-      auto wrow = [&](int r) FME_AI -> const auto& {
-        if constexpr (kBig) return bw[r + EO];
-        else return w[r];
-      };
+      // integer samples at rows -1 .. UH, cols -1 .. UW around the TZ MV (s - 128 bytes)
+      uint32_t w[UH + 2][EW];
+      load_window(ref, ox + mvx - 1, oy + h * kHalfRows + mvy - 1, w);
       int so2 = 0;   // SSE's sum of squared key samples
 #pragma unroll
       for (int r = 0; r < UH; r++)
@@ -910,7 +893,7 @@ __device__ FME_LANE_UNIT_ATTR void lane_unit(const BatchArgs& a, const fme_job* 
             if ((r & 1) && sub) continue;   // unit rows start on even PU rows
 #pragma unroll
             for (int k = 0; k < UW / 4; k++) {
-              const uint32_t pv = rbytes(wrow(r + 1 + dy), EO + 1 + dx + 4 * k) ^ 0x80808080u;   // samples 0..255
+              const uint32_t pv = rbytes(w[r + 1 + dy], 1 + dx + 4 * k) ^ 0x80808080u;   // samples 0..255
               if (!kbuf) {
                 e = __builtin_amdgcn_sad_u8(kraw[r][k] ^ 0x80808080u, pv, e);
               } else {   // int16 key: |key - pred| per sample
@@ -925,7 +908,7 @@ __device__ FME_LANE_UNIT_ATTR void lane_unit(const BatchArgs& a, const fme_job* 
           for (int r = 0; r < UH; r++)
 #pragma unroll
             for (int k = 0; k < UW / 4; k++) {
-              const uint32_t pv = rbytes(wrow(r + 1 + dy), EO + 1 + dx + 4 * k);
+              const uint32_t pv = rbytes(w[r + 1 + dy], 1 + dx + 4 * k);
               sop = dot4(kraw[r][k], pv, sop);
               spp = dot4(pv, pv, spp);
             }
@@ -935,7 +918,7 @@ __device__ FME_LANE_UNIT_ATTR void lane_unit(const BatchArgs& a, const fme_job* 
           for (int r = 0; r < UH; r++)
 #pragma unroll
             for (int k = 0; k < UW / 4; k++) {
-              const uint32_t x = rbytes(wrow(r + 1 + dy), EO + 1 + dx + 4 * k) ^ 0x80808080u;   // samples 0..255
+              const uint32_t x = rbytes(w[r + 1 + dy], 1 + dx + 4 * k) ^ 0x80808080u;   // samples 0..255
               const uint32_t d0 = pk_sub(kraw[r][2 * k], lo_pair(x)), d1 = pk_sub(kraw[r][2 * k + 1], hi_pair(x));
               e = (uint32_t)dot2(d1, d1, dot2(d0, d0, (int)e));
             }
@@ -982,8 +965,6 @@ __device__ FME_LANE_UNIT_ATTR void lane_unit(const BatchArgs& a, const fme_job* 
       }
     }
     cval = best - best_cost;
-    ex = bx - sx;
-    ey = by - sy;
     mvx = bx;
     mvy = by;
   } else if (j.flags & FME_JOB_NN_IN) {
@@ -1011,19 +992,7 @@ __device__ FME_LANE_UNIT_ATTR void lane_unit(const BatchArgs& a, const fme_job* 
   uint32_t v[RV][NV];
   KeySrc<UW, UJ> K;
   auto load_half = [&](int h) FME_AI {
-    if constexpr (kBig) {   // re-centre the big window on mv_int' = TZ MV + (ex, ey)
-      const uint32_t sh = (uint32_t)(1 + ex);
-#pragma unroll
-      for (int r = 0; r < RV; r++) {
-        uint32_t row[4];
-#pragma unroll
-        for (int k = 0; k < 4; k++) row[k] = ey < 0 ? bw[r][k] : (ey == 0 ? bw[r + 1][k] : bw[r + 2][k]);
-#pragma unroll
-        for (int k = 0; k < NV; k++) v[r][k] = __builtin_amdgcn_alignbyte(row[k + 1], row[k], sh);
-      }
-    } else {
-      load_window(ref, ox + mvx - 4, oy + h * kHalfRows + mvy - 4, v);
-    }
+    load_window(ref, ox + mvx - 4, oy + h * kHalfRows + mvy - 4, v);
     uint32_t kraw[UH][KW];
     if constexpr (UPL == 1) {
 #pragma unroll

@@ -705,45 +705,9 @@ __device__ __forceinline__ int tz_entry(const TzSchedule& sc, int kid, int x, in
   return -1;
 }
 
-#ifndef FME_TZ_PERSIST   // 1: persistent waves claiming PUs from per-XCD queues; 0: one wave per PU
-#define FME_TZ_PERSIST 1
-#endif
-// The XCD this wave runs on (HW_REG_XCC_ID, gfx940+: bits 3:0).
-__device__ __forceinline__ int tz_xcc_id() { return __builtin_amdgcn_s_getreg((20) | (0 << 6) | ((4 - 1) << 11)) & 7; }
-
 template <int UW, int UH>
 __global__ __launch_bounds__(kTzNT) __attribute__((amdgpu_waves_per_eu(FME_TZW_WAVES)))
 void k_tz_wave(TzArgs ta, TzSchedule sc, int kid) {
-#if FME_TZ_PERSIST
-  // Persistent: a one-wave-per-PU grid of ~860 K short waves is bound by wave dispatch (measured
-  // residency 1.6 of 4 waves / SIMD).  Each wave claims its next PU from its XCD's queue (an atomic
-  // per PU, issued before the current search so its latency hides behind it), then drains the
-  // other XCDs' queues.
-  const int lane = (int)threadIdx.x & 63, home = tz_xcc_id();
-  int32_t* ctr = ta.ctr + 8 * kid;
-  auto claim_v = [&](int xx) FME_AI {
-    int v = 0;
-    if (lane == 0) v = atomicAdd(&ctr[xx], 1);
-    return v;
-  };
-  int x = home, tried = 0;
-  int t = __builtin_amdgcn_readfirstlane(claim_v(x));
-  for (;;) {
-    int c;
-    const int q = tz_entry(sc, kid, x, t, c);
-    if (q < 0) {   // queue drained: the next XCD's
-      if (++tried == 8) break;
-      x = (home + tried) & 7;
-      t = __builtin_amdgcn_readfirstlane(claim_v(x));
-      continue;
-    }
-    const int nxt = claim_v(x);
-    const int jid = ta.perm[q];
-    const fme_job j = ta.sjobs[q];
-    tz_wave<UW, UH>(ta, jid, j, kTzW[c], kTzH[c], ta.ext[jid].pred2n_x, ta.ext[jid].pred2n_y);
-    t = __builtin_amdgcn_readfirstlane(nxt);
-  }
-#else
   const int x = (int)blockIdx.x & 7;
   const int t = ((int)blockIdx.x >> 3) * (kTzNT / 64) + (int)(threadIdx.x >> 6);
   int c;
@@ -752,7 +716,6 @@ void k_tz_wave(TzArgs ta, TzSchedule sc, int kid) {
   const int jid = ta.perm[q];
   const fme_job j = ta.sjobs[q];
   tz_wave<UW, UH>(ta, jid, j, kTzW[c], kTzH[c], ta.ext[jid].pred2n_x, ta.ext[jid].pred2n_y);
-#endif
 }
 
 // One dependency level of a producer's m_integerMv2Nx2N chain (fme_pred_inter_p/b): one wave per
@@ -812,18 +775,7 @@ hipError_t launch_tz_wave(const TzArgs& ta, const TzSchedule& sc, int kid, hipSt
     share = std::max(share, n);
   }
   if (share <= 0) return hipSuccess;
-  int blocks = 8 * ((share + kTzNT / 64 - 1) / (kTzNT / 64));
-#if FME_TZ_PERSIST
-  {   // enough waves to fill the chip at the kernel's occupancy, no more than the PUs need
-    static int cus = 0;
-    if (!cus) {
-      int dev = 0;
-      (void)hipGetDevice(&dev);
-      cus = cu_count(dev);
-    }
-    blocks = std::min(blocks, cus * 4 * FME_TZW_WAVES / (kTzNT / 64));
-  }
-#endif
+  const int blocks = 8 * ((share + kTzNT / 64 - 1) / (kTzNT / 64));
   if (kid == 0) hipLaunchKernelGGL((k_tz_wave<4, 8>), dim3(blocks), dim3(kTzNT), 0, s, ta, sc, 0);
   else if (kid == 1) hipLaunchKernelGGL((k_tz_wave<8, 4>), dim3(blocks), dim3(kTzNT), 0, s, ta, sc, 1);
   else hipLaunchKernelGGL((k_tz_wave<8, 8>), dim3(blocks), dim3(kTzNT), 0, s, ta, sc, 2);
