@@ -21,12 +21,6 @@
 
 using namespace fme;
 
-// 1: the search hands its records to the tail in class order (contiguous per tile, read back
-// through k_scatter's ipos); 0: in call order, straight into the caller's results (A/B).
-#ifndef FME_SORTED_RECS
-#define FME_SORTED_RECS 1
-#endif
-
 namespace {
 
 thread_local std::string g_last_error = "";
@@ -116,8 +110,6 @@ struct fme_ctx {
   DevBuf<fme_mv_result> d_mv;   // staging for fme_refine_mv
   DevBuf<uint8_t> cls;
   DevBuf<int32_t> perm;
-  DevBuf<int32_t> ipos;        // job -> position in perm (class-order record hand-off)
-  DevBuf<fme_result> srec;     // the search's records in class order
   DevBuf<fme_job> sjobs;
   DevBuf<int32_t> counts;      // 25 counts, 24 cursors, 24 tile-queue heads: one memset
   DevBuf<int32_t> blk_agg;
@@ -271,7 +263,6 @@ int fme_destroy(fme_ctx* c) {
   c->d_pics.release(); c->d_mlambda.release(); c->d_keys.release(); c->d_nn.release(); c->d_net.release();
   c->d_jobs.release(); c->d_res.release(); c->d_mv.release(); c->cls.release(); c->perm.release(); c->sjobs.release();
   c->counts.release(); c->blk_agg.release(); c->blk_prefix.release(); c->nn_state.release();
-  c->ipos.release(); c->srec.release();
   c->d_sched.release();
   if (c->ev_done) (void)hipEventDestroy(c->ev_done);
   if (c->stage) (void)hipHostFree(c->stage);
@@ -550,10 +541,6 @@ static int ensure_work(fme_ctx* c, int n) {
   HIP_TRY(c->sjobs.reserve(n));
   HIP_TRY(c->blk_agg.reserve(nb * 9));
   HIP_TRY(c->blk_prefix.reserve(nb * 9));
-  if (FME_SORTED_RECS) {
-    HIP_TRY(c->ipos.reserve(n));
-    HIP_TRY(c->srec.reserve(n));
-  }
   return FME_OK;
 }
 
@@ -570,7 +557,6 @@ static WorkBufs work_bufs(fme_ctx* c) {
   w.nn_state = c->nn_state.p;
   w.sched = c->d_sched.p;
   w.mv_out = nullptr;
-  w.ipos = c->ipos.p;
   return w;
 }
 
@@ -660,7 +646,6 @@ static int refine_batch(fme_ctx* c, const fme_job* d_jobs, fme_result* d_res, fm
   a.nn_mode = c->cfg.nn_mode ? 1 : 0;
   a.nn_in = c->nn_in;
   a.nn_in_cap = c->nn_in_cap;
-  a.srec = FME_SORTED_RECS ? c->srec.p : nullptr;
   WorkBufs w = work_bufs(c);
   w.mv_out = d_mv;
 
@@ -1055,7 +1040,7 @@ static int srv_open(fme_ctx* c) {
 }
 
 static int srv_launch(fme_ctx* c) {
-  __atomic_store_n(&c->box->stop, 0u, __ATOMIC_RELEASE);
+  __atomic_store_n(&c->box->req[0][3], 0u, __ATOMIC_RELEASE);
   const uint32_t epoch = ++c->srv_epoch;
   c->srv_nn_gen = c->nn_gen;
   HIP_TRY(launch_server(c->box_dev, c->nn_loaded ? c->d_nn.p : nullptr, c->srv_done, epoch,
@@ -1085,7 +1070,7 @@ static int srv_join(fme_ctx* c) {
 
 static int srv_stop(fme_ctx* c) {
   if (!c->srv_running) return FME_OK;
-  __atomic_store_n(&c->box->stop, 1u, __ATOMIC_RELEASE);
+  __atomic_store_n(&c->box->req[0][3], 1u, __ATOMIC_RELEASE);
   return srv_join(c);
 }
 
@@ -1096,7 +1081,7 @@ static int srv_call(fme_ctx* c, bool uses_nn) {
   if (!rc && !c->srv_running) rc = srv_launch(c);
   if (rc) return rc;
   const uint32_t seq = c->srv_done + 1;
-  __atomic_store_n(&c->box->req_seq, seq, __ATOMIC_RELEASE);
+  __atomic_store_n(&c->box->req[0][0], seq, __ATOMIC_RELEASE);
   volatile uint32_t* done = &c->box->done_seq;
   volatile uint32_t* st = &c->box->stopped;
   for (long it = 1; *done != seq; it++) {
@@ -1143,13 +1128,10 @@ int fme_frac_dif_single(fme_ctx* c, int lossless, const int16_t* key, int key_st
     uint8_t* dst = b->win + y * pw;
     for (int x = 0; x < pw; x++) dst[x] = (uint8_t)std::min(255, std::max(0, (int)src[x]));
   }
-  b->kind = kSrvFrac;
-  b->w = w;
-  b->h = h;
-  b->mvp_x = px;
-  b->mvp_y = py;
-  b->sad = (lossless || !c->cfg.use_hadamard) ? 1 : 0;
   b->ml = motion_lambda;
+  b->req[0][1] = (uint32_t)kSrvFrac | ((lossless || !c->cfg.use_hadamard) ? 4u : 0u) | ((uint32_t)(w - 1) << 8) |
+                 ((uint32_t)(h - 1) << 16);
+  b->req[0][2] = (uint32_t)(uint16_t)px | ((uint32_t)(uint16_t)py << 16);
   rc = srv_call(c, false);
   if (rc) return rc;
   half_xy[0] = (int16_t)b->out[0];
@@ -1169,11 +1151,13 @@ int fme_nn_pred_single(fme_ctx* c, const uint32_t* e, uint32_t cc, int pu_h, int
   if (!deep) {   // the master net: the server, weights in its LDS
     rc = srv_open(c);
     if (rc) return rc;
-    for (int s = 0; s < 8; s++) c->box->nn_in[s] = e[s];
-    c->box->nn_in[8] = cc;
-    c->box->nn_in[9] = (uint32_t)pu_h;
-    c->box->nn_in[10] = (uint32_t)pu_w;
-    c->box->kind = kSrvNn;
+    const uint32_t in[12] = {e[0], e[1], e[2], e[3], e[4], e[5], e[6], e[7], cc, (uint32_t)pu_h, (uint32_t)pu_w, 0u};
+    const uint32_t seq = c->srv_done + 1;   // the call's sequence number (srv_call)
+    for (int b = 1; b < 5; b++) {   // each block's inputs, then its sequence word
+      for (int k = 0; k < 3; k++) c->box->req[b][1 + k] = in[3 * (b - 1) + k];
+      __atomic_store_n(&c->box->req[b][0], seq, __ATOMIC_RELEASE);
+    }
+    c->box->req[0][1] = kSrvNn;
     rc = srv_call(c, true);
     if (rc) return rc;
     *nn_class = c->box->out[0];

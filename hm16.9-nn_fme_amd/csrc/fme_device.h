@@ -96,11 +96,6 @@ struct BatchArgs {
                               // whose jobs read keys are rejected (k_classify)
   const uint32_t* nn_in;      // NN input rows of FME_JOB_NN_IN jobs ([nn_in_cap][9]) or null
   int32_t nn_in_cap;
-  // The search -> tail hand-off: the search writes each tile's records contiguously in class
-  // order (srec[q], q = the job's position in perm) and the tails read them through
-  // WorkBufs::ipos (job -> q), so no record leaves as scattered half lines.  Null: the records go
-  // to res in call order (the single-PU kernels).
-  fme_result* srec;
 };
 
 struct Schedule;
@@ -118,12 +113,9 @@ struct WorkBufs {
   Schedule* sched;       // built on the device by k_schedule from counts
   int32_t* tile_ctr;     // [8] lane-kernel tile queue heads (zeroed with counts)
   fme_mv_result* mv_out; // compact per-job output (fme_refine_mv*), or null
-  int32_t* ipos;         // [n] position of job i in perm (written by k_scatter; BatchArgs::srec)
 };
-// The search record of job i (class order through ipos, or call order).
-__device__ __forceinline__ const fme_result* search_rec(const BatchArgs& a, const WorkBufs& w, int i) {
-  return a.srec ? a.srec + w.ipos[i] : a.res + i;
-}
+// The search record of job i (the search writes its records in call order; the tail completes them).
+__device__ __forceinline__ const fme_result* search_rec(const BatchArgs& a, const WorkBufs&, int i) { return a.res + i; }
 
 // Schedule of the search kernel (k_schedule builds it on the device): class c's jobs are
 // sjobs/perm[class_off[c] .. + class_cnt[c]) and its 64-lane wave tiles [prefix[c], prefix[c+1]).
@@ -196,13 +188,14 @@ struct NnIn11 {   // NN_pred() inputs of a single call: array_e slots[8], C, PUH
 // lines, the answer has its own, the payload follows.
 enum { kSrvNn = 1, kSrvFrac = 2 };
 struct SrvBox {
-  uint32_t req_seq;            // host -> device, written last
-  uint32_t kind;               // kSrvNn / kSrvFrac
-  uint32_t stop;
-  int32_t w, h, mvp_x, mvp_y;  // FracDIF: PU size, predictor - 4 * integer MV (quarter-pel)
-  int32_t sad;                 // 1: SAD (lossless or HADME off), 0: SATD
+  // host -> device, in 16-byte blocks that the server reads with one load each, so a block's fields
+  // are those written before its sequence word.  req[0]: seq (written last), shape = kind (bits
+  // 0-1) | SAD (bit 2: lossless or HADME off) | w - 1 (bits 8-15) | h - 1 (bits 16-23), the FracDIF
+  // predictor - 4 * integer MV (x low 16 bits, y high 16, quarter-pel), stop (set by the host to end
+  // the instance); req[1..4]: seq and three NN_pred inputs each (array_e[8], C, PUHeight, PUWidth),
+  // taken only when all four carry the seq.
+  alignas(64) uint32_t req[5][4];
   double ml;                   // motion lambda (TComRdCost::m_motionLambda)
-  uint32_t nn_in[12];          // NN_pred: array_e[8], C, PUHeight, PUWidth
   alignas(64) uint32_t done_seq;   // device -> host
   uint32_t stopped;
   int32_t out[6];              // FracDIF: half x, y, quarter x, y, cost; NN: class
@@ -266,8 +259,8 @@ __device__ __forceinline__ int nn_pushes(const fme_job& j) {
 }
 __device__ __forceinline__ bool nn_writes_c(const fme_job& j) { return (j.flags & (FME_JOB_EMI | FME_JOB_NN_IN)) != 0; }
 
-// r: the job's record in call order (full-record output); src: its search record (== r when the
-// search wrote in call order): with a class-order hand-off the whole record is written here.
+// r: the job's record in call order (full-record output); src: its search record (the search
+// writes its fields into r itself, so src == r and only the tail's fields are written here).
 __device__ __forceinline__ void store_outputs(fme_result* r, const fme_result* src, fme_mv_result* mv_out, int i,
                                               int fx, int fy, uint32_t cost, uint32_t bits, uint8_t cls,
                                               uint16_t status) {

@@ -224,7 +224,6 @@ __global__ __launch_bounds__(kBlock) void k_scatter(BatchArgs a, WorkBufs w) {
       const int dst = sc->class_off[cls[q]] + basep[cls[q]] + rank[q];
       w.perm[dst] = i;
       w.sjobs[dst] = jb[q];
-      if (a.srec) w.ipos[i] = dst;
     }
   }
   // Exclusive prefix-max of the NN-writer aggregates over the blocks before this one: k_nn_tail's

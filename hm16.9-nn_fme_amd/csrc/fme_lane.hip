@@ -311,8 +311,11 @@ __host__ __device__ __forceinline__ constexpr int emi_dy(int p) { return p >= 1 
 // =============================================================================================
 // `live`: ~0 on the lanes of a PU's units, 0 on the idle lanes that pad a group of 6 / 12 / 48
 // units (AMP shapes) to a power of two, so they add nothing to the group's sum.
+// The MV cost from the workgroup's table: g_cost[lambda][bits] = (UInt)(mlambda * bits / 65536.0)
+// (TComRdCost.h:165), computed once per launch by the same double arithmetic.
+__device__ __forceinline__ uint32_t mv_cost(const uint32_t* ml, uint32_t bits) { return ml[bits]; }
 template <int L>
-__device__ __forceinline__ void take_half(int i, uint32_t part, uint32_t live, double ml, int mvx, int mvy, int px,
+__device__ __forceinline__ void take_half(int i, uint32_t part, uint32_t live, const uint32_t* ml, int mvx, int mvy, int px,
                                           int py, uint32_t& best, int& bi) {
   const uint32_t d = group_sum<L>(part & live) + mv_cost(ml, mv_bits(2 * mvx + h9_dx(i), 2 * mvy + h9_dy(i), 1, px, py));
   if (d < best || (d == best && i < bi)) {
@@ -321,7 +324,7 @@ __device__ __forceinline__ void take_half(int i, uint32_t part, uint32_t live, d
   }
 }
 template <int L>
-__device__ __forceinline__ void take_qtr(int i, uint32_t part, uint32_t live, double ml, int mvx, int mvy, int hx,
+__device__ __forceinline__ void take_qtr(int i, uint32_t part, uint32_t live, const uint32_t* ml, int mvx, int mvy, int hx,
                                          int hy, int px, int py, uint32_t& best, int& bi) {
   const int qx = 2 * hx + q9_dx(i), qy = 2 * hy + q9_dy(i);
   const uint32_t d = group_sum<L>(part & live) + mv_cost(ml, mv_bits(4 * mvx + qx, 4 * mvy + qy, 0, px, py));
@@ -739,11 +742,14 @@ __device__ __forceinline__ void load_window(const PicDesc& pic, int x0, int y0, 
 // every tile reads its PU's reference / original picture descriptor and motion lambda from LDS
 // instead of a dependent global load before its window loads.
 __shared__ PicDesc g_pics[FME_MAX_PICTURES];
-__shared__ double g_ml[FME_MAX_LAMBDAS];
+// MV bits of one candidate: two exp-Golomb lengths of values below 2^18 (int16 MVs and predictors,
+// cost scale <= 2), each at most 37.
+constexpr int kCostBits = 80;
+__shared__ uint32_t g_cost[FME_MAX_LAMBDAS][kCostBits];
 // Record staging: each PU's 64-byte fme_result is assembled in LDS by the PU's first lane, then
 // the wave writes the tile's records with four lanes per record, so every store instruction writes
 // whole 64-byte lines (one lane per record wrote four separate 16-byte pieces: 256 bytes of
-// WRITE_SIZE per job); in class order (BatchArgs::srec) a tile's records are also contiguous.
+// WRITE_SIZE per job).
 __shared__ uint4 g_rec[256 / 64][64][4];
 __shared__ int32_t g_rec_jid[256 / 64][64];
 
@@ -772,7 +778,7 @@ __device__ FME_LANE_UNIT_ATTR void lane_unit(const BatchArgs& a, const fme_job* 
                                              int wt) {
   g_job* const sjobs = (g_job*)sjobs_;
   g_i32* const perm = (g_i32*)perm_;
-  g_res* const outp = (g_res*)(a.srec ? a.srec : a.res);   // where this kernel's records go
+  g_res* const outp = (g_res*)a.res;
   g_i16* const keys = (g_i16*)a.keys;
   const int use_hadamard = a.use_hadamard, fen = a.fen;
   constexpr int T = ((PW % 8) == 0 && (PH % 8) == 0) ? 8 : 4;
@@ -816,7 +822,7 @@ __device__ FME_LANE_UNIT_ATTR void lane_unit(const BatchArgs& a, const fme_job* 
   }
   const int jid = perm[cls_off + p];
   const PicDesc ref = g_pics[j.ref_id];
-  const double ml = g_ml[j.lambda_id];
+  const uint32_t* const ml = g_cost[j.lambda_id];
   const Metric met = {use_hadamard && !(j.flags & FME_JOB_LOSSLESS), (lane & 1) ? 0xFFFFFFFFu : 0x00010001u,
                       (lane & 1) ? 0u : ~0u};
   const bool kbuf = j.key_offset >= 0;
@@ -982,8 +988,7 @@ __device__ FME_LANE_UNIT_ATTR void lane_unit(const BatchArgs& a, const fme_job* 
     g_rec[wid][lane][1] = make_uint4(0u, 0u, cval, emi[0]);
     g_rec[wid][lane][2] = make_uint4(emi[1], emi[2], emi[3], emi[4]);
     g_rec[wid][lane][3] = make_uint4(emi[5], emi[6], emi[7], (uint32_t)n_emi);
-    // destination record: class order (the tile's records contiguous) or call order
-    g_rec_jid[wid][lane] = !active ? -1 : (a.srec ? cls_off + p : jid);
+    g_rec_jid[wid][lane] = !active ? -1 : jid;   // destination record (call order)
   }
 
 
@@ -1176,7 +1181,8 @@ void k_search_lane(BatchArgs a, WorkBufs w) {
     const uint32_t* ps = reinterpret_cast<const uint32_t*>(a.pics);
     uint32_t* pd = reinterpret_cast<uint32_t*>(g_pics);
     for (int i = threadIdx.x; i < (int)(sizeof(g_pics) / 4); i += kLaneNT) pd[i] = ps[i];
-    if (threadIdx.x < FME_MAX_LAMBDAS) g_ml[threadIdx.x] = a.mlambda[threadIdx.x];
+    for (int i = threadIdx.x; i < FME_MAX_LAMBDAS * kCostBits; i += kLaneNT)
+      g_cost[i / kCostBits][i % kCostBits] = simd::mv_cost(a.mlambda[i / kCostBits], (uint32_t)(i % kCostBits));
     for (int i = threadIdx.x; i < 8 * (kNumClasses + 1); i += kLaneNT) (&s_xq[0][0])[i] = (&sc->xq[0][0])[i];
   }
   const int home = xcc_id(), wid = threadIdx.x >> 6, lane = threadIdx.x & 63;

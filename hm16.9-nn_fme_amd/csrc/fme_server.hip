@@ -30,12 +30,48 @@ __constant__ int8_t kSrvLuma[4][8] = {{0, 0, 0, 64, 0, 0, 0, 0},
 __constant__ int8_t kSrvRefH[9][2] = {{0, 0}, {0, -1}, {0, 1}, {-1, 0}, {1, 0}, {-1, -1}, {1, -1}, {-1, 1}, {1, 1}};
 __constant__ int8_t kSrvRefQ[9][2] = {{0, 0}, {0, -1}, {0, 1}, {-1, -1}, {1, -1}, {-1, 0}, {1, 0}, {-1, 1}, {1, 1}};
 
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+// 16 bytes of host memory in one request, past the caches
+__device__ __forceinline__ u32x4 load_block(const uint32_t* p) {
+  u32x4 v;
+  asm volatile("global_load_dwordx4 %0, %1, off sc0 sc1\n\ts_waitcnt vmcnt(0)" : "=v"(v) : "v"(p) : "memory");
+  return v;
+}
 __device__ __forceinline__ uint32_t sys_load(const uint32_t* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 __device__ __forceinline__ void sys_store_release(uint32_t* p, uint32_t v) {
   __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
+
+// The value of lane ^ m (m a power of two below 64) without the LDS pipe: DPP within a row of 16
+// lanes, v_permlane16/32_swap across rows.
+template <int CTRL>
+__device__ __forceinline__ int dpp_i(int v) { return __builtin_amdgcn_update_dpp(0, v, CTRL, 0xF, 0xF, false); }
+template <int M>
+__device__ __forceinline__ int xor_lane(int v, int lane) {
+  if constexpr (M == 1) return dpp_i<0xB1>(v);          // quad_perm [1, 0, 3, 2]
+  else if constexpr (M == 2) return dpp_i<0x4E>(v);     // quad_perm [2, 3, 0, 1]
+  else if constexpr (M == 4) {                          // row_shl:4 / row_shr:4
+    const int up = dpp_i<0x104>(v), dn = dpp_i<0x114>(v);
+    return (lane & 4) ? dn : up;
+  } else if constexpr (M == 8) return dpp_i<0x128>(v);  // row_ror:8
+  else if constexpr (M == 16) {
+    const auto p = __builtin_amdgcn_permlane16_swap(v, v, false, false);
+    return (lane & 16) ? (int)p[0] : (int)p[1];
+  } else {
+    const auto p = __builtin_amdgcn_permlane32_swap(v, v, false, false);
+    return (lane & 32) ? (int)p[0] : (int)p[1];
+  }
+}
+// Butterfly stage over lane bit M: (a + b, a - b) with a the lower lane's value.
+template <int M>
+__device__ __forceinline__ int bfly(int d, int lane) {
+  const int p = xor_lane<M>(d, lane);
+  return (lane & M) ? p - d : d + p;
+}
+template <int M>
+__device__ __forceinline__ uint32_t xsum(uint32_t a, int lane) { return a + (uint32_t)xor_lane<M>((int)a, lane); }
 
 // TComRdCost::xGetExpGolombNumberOfBits (TComRdCost.cpp:172-185): 2 * floor(log2 t) + 1
 __device__ __forceinline__ uint32_t eg_bits_d(int v) {
@@ -49,7 +85,7 @@ struct SrvLds {
   int16_t key[64 * 64];
   int16_t hp[3][72 * 65];       // first filter stage, fractional phase 1..3, columns -1 .. w-1
   uint8_t win[72 * 72];
-  uint32_t cost[16];
+  uint32_t cost[2][16];           // per candidate: half stage, quarter stage
   int32_t ctl[8];               // stop, seq, kind, w, h, mvp_x, mvp_y, sad
   uint32_t nn_in[12];
   double ml;
@@ -70,8 +106,20 @@ __device__ void stage_dist(SrvLds& L, int w, int h, bool sad, bool half, int bx0
   const bool b8 = !sad && (w & 7) == 0 && (h & 7) == 0;   // xGetHADs: 8x8 when both dims allow
   const int nb4 = (w >> 2) * (h >> 2);
   const int nb = b8 ? (w >> 3) * (h >> 3) : (nb4 + 3) >> 2;
-  for (int item = wid; item < 9 * nb; item += kSrvThreads / 64) {
+  // each wave takes a contiguous run of the (candidate-major) items and adds its partial sums to
+  // L.cost once per candidate it touched (a run spans at most two candidates once nb >= 16)
+  constexpr int NWV = kSrvThreads / 64;
+  const int n_items = 9 * nb, per = (n_items + NWV - 1) / NWV;
+  const int i0 = wid * per, i1 = min(n_items, i0 + per);
+  uint32_t acc = 0;
+  int kcur = i0 < i1 ? i0 / nb : 0;
+  for (int item = i0; item < i1; item++) {
     const int k = item / nb, b = item - k * nb;
+    if (k != kcur) {
+      if (lane == 0) atomicAdd(&L.cost[half ? 0 : 1][kcur], acc);
+      acc = 0;
+      kcur = k;
+    }
     const int ox = bx0 + (half ? 2 * kSrvRefH[k][0] : kSrvRefQ[k][0]);
     const int oy = by0 + (half ? 2 * kSrvRefH[k][1] : kSrvRefQ[k][1]);
     int c, r;
@@ -104,34 +152,23 @@ __device__ void stage_dist(SrvLds& L, int w, int h, bool sad, bool half, int bx0
     uint32_t add;
     if (sad) {
       uint32_t a = (uint32_t)abs(d);
-#pragma unroll
-      for (int m = 1; m < 64; m <<= 1) a += (uint32_t)__shfl_xor((int)a, m, 64);
+      a = xsum<32>(xsum<16>(xsum<8>(xsum<4>(xsum<2>(xsum<1>(a, lane), lane), lane), lane), lane), lane);
       add = a;
     } else if (b8) {   // 8x8 Walsh-Hadamard across the lanes, sum |coef|, (s + 2) >> 2 (xCalcHADs8x8)
-#pragma unroll
-      for (int m = 1; m < 64; m <<= 1) {
-        const int p = __shfl_xor(d, m, 64);
-        d = (lane & m) ? p - d : d + p;
-      }
+      d = bfly<32>(bfly<16>(bfly<8>(bfly<4>(bfly<2>(bfly<1>(d, lane), lane), lane), lane), lane), lane);
       uint32_t a = (uint32_t)abs(d);
-#pragma unroll
-      for (int m = 1; m < 64; m <<= 1) a += (uint32_t)__shfl_xor((int)a, m, 64);
+      a = xsum<32>(xsum<16>(xsum<8>(xsum<4>(xsum<2>(xsum<1>(a, lane), lane), lane), lane), lane), lane);
       add = (a + 2) >> 2;
     } else {           // four 4x4 blocks per wave, each (s + 1) >> 1 (xCalcHADs4x4)
-#pragma unroll
-      for (int m = 1; m < 16; m <<= 1) {
-        const int p = __shfl_xor(d, m, 64);
-        d = (lane & m) ? p - d : d + p;
-      }
+      d = bfly<8>(bfly<4>(bfly<2>(bfly<1>(d, lane), lane), lane), lane);
       uint32_t a = (uint32_t)abs(d);
-#pragma unroll
-      for (int m = 1; m < 16; m <<= 1) a += (uint32_t)__shfl_xor((int)a, m, 64);
+      a = xsum<8>(xsum<4>(xsum<2>(xsum<1>(a, lane), lane), lane), lane);
       a = valid ? (a + 1) >> 1 : 0u;
-      add = (uint32_t)__shfl((int)a, 0, 64) + (uint32_t)__shfl((int)a, 16, 64) + (uint32_t)__shfl((int)a, 32, 64) +
-            (uint32_t)__shfl((int)a, 48, 64);
+      add = xsum<32>(xsum<16>(a, lane), lane);   // the four blocks' (rounded) sums
     }
-    if (lane == 0) atomicAdd(&L.cost[k], add);
+    acc += add;
   }
+  if (i0 < i1 && lane == 0) atomicAdd(&L.cost[half ? 0 : 1][kcur], acc);
 }
 
 // Wave 0: distortion + MV cost per candidate (lane k), the first strict minimum in candidate order.
@@ -145,7 +182,7 @@ __device__ void stage_pick(const SrvLds& L, bool half, int hx, int hy, int& best
     const int mx = half ? 2 * kSrvRefH[lane][0] : 2 * hx + kSrvRefQ[lane][0];
     const int my = half ? 2 * kSrvRefH[lane][1] : 2 * hy + kSrvRefQ[lane][1];
     const uint32_t bits = eg_bits_d(mx - px) + eg_bits_d(my - py);
-    tot = L.cost[lane] + (uint32_t)((L.ml * (double)bits) / 65536.0);
+    tot = L.cost[half ? 0 : 1][lane] + (uint32_t)((L.ml * (double)bits) / 65536.0);
   }
   int k = lane < 9 ? lane : 64;
 #pragma unroll
@@ -166,17 +203,6 @@ __device__ void serve_frac(SrvLds& L, SrvBox* box) {
   const int w = L.ctl[3], h = L.ctl[4];
   const bool sad = L.ctl[7] != 0;
   const int pw = w + 8, ph = h + 8;
-  // the call's window and key (host memory, read once, in parallel)
-  {
-    const uint32_t* wsrc = reinterpret_cast<const uint32_t*>(box->win);
-    uint32_t* wdst = reinterpret_cast<uint32_t*>(L.win);
-    for (int i = tid; i < (pw * ph + 3) >> 2; i += kSrvThreads) wdst[i] = wsrc[i];
-    const uint32_t* ksrc = reinterpret_cast<const uint32_t*>(box->key);
-    uint32_t* kdst = reinterpret_cast<uint32_t*>(L.key);
-    for (int i = tid; i < (w * h) >> 1; i += kSrvThreads) kdst[i] = ksrc[i];
-    if (tid < 16) L.cost[tid] = 0;
-  }
-  __syncthreads();
   // first filter stage of phases 1..3 over window rows 0 .. h+7, PU columns -1 .. w-1
   {
     const int cols = w + 1, plane = ph * cols;
@@ -203,8 +229,6 @@ __device__ void serve_frac(SrvLds& L, SrvBox* box) {
   }
   __syncthreads();
   const int hx = L.sel[0], hy = L.sel[1];
-  if (tid < 16) L.cost[tid] = 0;
-  __syncthreads();
   stage_dist(L, w, h, sad, false, 2 * hx, 2 * hy);
   __syncthreads();
   if (tid < 64) {
@@ -298,36 +322,58 @@ __global__ __launch_bounds__(kSrvThreads) void k_server(SrvBox* box, const float
   const uint64_t t0 = wall_clock64();
   uint64_t last = t0;
   for (;;) {
-    if (tid == 0) {
+    if (tid < 64) {   // wave 0 polls: lanes 0..4 read the five request blocks
+      const int lane = tid;
       uint32_t seq = served, stop = 0;
+      u32x4 hd = {0u, 0u, 0u, 0u};
       for (;;) {
-        seq = sys_load(&box->req_seq);
-        stop = sys_load(&box->stop);
-        if (seq != served || stop) break;
+        if (lane < 5) hd = load_block(box->req[lane]);
+        seq = (uint32_t)__builtin_amdgcn_readfirstlane((int)hd.x);
+        if (seq != served) {
+          const uint32_t kind = (uint32_t)__builtin_amdgcn_readfirstlane((int)hd.y) & 3u;
+          // an NN call's inputs ride in blocks 1..4: all of them must be this call's
+          if (kind != kSrvNn || __ballot(lane >= 1 && lane < 5 && hd.x != seq) == 0) break;
+          continue;
+        }
+        stop = (uint32_t)__builtin_amdgcn_readfirstlane((int)hd.w);   // the host's stop word rides in req[0]
+        if (stop) break;
         const uint64_t now = wall_clock64();
         if (now - last > idle_ticks || now - t0 > life_ticks) {
           stop = 1;
           break;
         }
-        __builtin_amdgcn_s_sleep(2);
+        __builtin_amdgcn_s_sleep(1);
       }
-      L.ctl[0] = (int32_t)stop;
-      L.ctl[1] = (int32_t)seq;
-      if (!stop) {
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");   // the request's payload after its word
-        L.ctl[2] = (int32_t)box->kind;
-        L.ctl[3] = box->w;
-        L.ctl[4] = box->h;
-        L.ctl[5] = box->mvp_x;
-        L.ctl[6] = box->mvp_y;
-        L.ctl[7] = box->sad;
-        L.ml = box->ml;
-        for (int k = 0; k < 11; k++) L.nn_in[k] = box->nn_in[k];
+      if (lane == 0) {
+        L.ctl[0] = (int32_t)stop;
+        L.ctl[1] = (int32_t)seq;
+        L.ctl[2] = (int32_t)(hd.y & 3u);                 // kind
+        L.ctl[7] = (int32_t)((hd.y >> 2) & 1u);          // sad
+        L.ctl[3] = (int32_t)((hd.y >> 8) & 0xFFu) + 1;   // w
+        L.ctl[4] = (int32_t)((hd.y >> 16) & 0xFFu) + 1;  // h
+        L.ctl[5] = (int32_t)(int16_t)(hd.z & 0xFFFFu);   // mvp_x - 4 * mv_int_x
+        L.ctl[6] = (int32_t)(int16_t)(hd.z >> 16);
+      } else if (lane < 5) {
+        L.nn_in[3 * (lane - 1)] = hd.y;
+        L.nn_in[3 * (lane - 1) + 1] = hd.z;
+        L.nn_in[3 * (lane - 1) + 2] = hd.w;
       }
     }
     __syncthreads();
     if (L.ctl[0]) break;
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");   // the payload after its request word
+    if (L.ctl[2] == kSrvFrac) {   // the window and key, every thread at once (one round trip)
+      const int w = L.ctl[3], h = L.ctl[4];
+      const uint32_t* wsrc = reinterpret_cast<const uint32_t*>(box->win);
+      uint32_t* wdst = reinterpret_cast<uint32_t*>(L.win);
+      for (int i = tid; i < ((w + 8) * (h + 8) + 3) >> 2; i += kSrvThreads) wdst[i] = wsrc[i];
+      const uint32_t* ksrc = reinterpret_cast<const uint32_t*>(box->key);
+      uint32_t* kdst = reinterpret_cast<uint32_t*>(L.key);
+      for (int i = tid; i < (w * h) >> 1; i += kSrvThreads) kdst[i] = ksrc[i];
+      if (tid < 32) (&L.cost[0][0])[tid] = 0;
+      if (tid == 64) L.ml = box->ml;
+      __syncthreads();
+    }
     const uint32_t seq = (uint32_t)L.ctl[1];
     if (L.ctl[2] == kSrvFrac)
       serve_frac(L, box);
