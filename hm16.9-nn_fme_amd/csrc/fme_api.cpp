@@ -1017,7 +1017,7 @@ static int single_wait(fme_ctx* c, uint32_t seq) {
 // ---- the single-call server (fme_server.hip) ----------------------------------------------------
 // One resident workgroup serves fme_frac_dif_single and the master net's fme_nn_pred_single: the
 // host writes the request into the mailbox (pinned, device-mapped), releases req_seq and spins on
-// done_seq.  An instance exits after kSrvIdleUs without a call or kSrvLifeMs of life (or on `stop`)
+// the answer block res.  An instance exits after kSrvIdleUs without a call or kSrvLifeMs of life (or on `stop`)
 // and writes its epoch to `stopped`; a call that finds its instance gone relaunches one, which
 // serves the pending request.
 constexpr uint64_t kSrvIdleUs = 2000;
@@ -1082,7 +1082,7 @@ static int srv_call(fme_ctx* c, bool uses_nn) {
   if (rc) return rc;
   const uint32_t seq = c->srv_done + 1;
   __atomic_store_n(&c->box->req[0][0], seq, __ATOMIC_RELEASE);
-  volatile uint32_t* done = &c->box->done_seq;
+  volatile uint32_t* done = &c->box->res[0];
   volatile uint32_t* st = &c->box->stopped;
   for (long it = 1; *done != seq; it++) {
     __builtin_ia32_pause();
@@ -1134,11 +1134,12 @@ int fme_frac_dif_single(fme_ctx* c, int lossless, const int16_t* key, int key_st
   b->req[0][2] = (uint32_t)(uint16_t)px | ((uint32_t)(uint16_t)py << 16);
   rc = srv_call(c, false);
   if (rc) return rc;
-  half_xy[0] = (int16_t)b->out[0];
-  half_xy[1] = (int16_t)b->out[1];
-  qtr_xy[0] = (int16_t)b->out[2];
-  qtr_xy[1] = (int16_t)b->out[3];
-  *cost = (uint32_t)b->out[4];
+  const uint32_t hq = b->res[2];
+  half_xy[0] = (int16_t)(int8_t)(hq & 0xFF);
+  half_xy[1] = (int16_t)(int8_t)((hq >> 8) & 0xFF);
+  qtr_xy[0] = (int16_t)(int8_t)((hq >> 16) & 0xFF);
+  qtr_xy[1] = (int16_t)(int8_t)(hq >> 24);
+  *cost = b->res[1];
   return FME_OK;
 }
 
@@ -1160,7 +1161,7 @@ int fme_nn_pred_single(fme_ctx* c, const uint32_t* e, uint32_t cc, int pu_h, int
     c->box->req[0][1] = kSrvNn;
     rc = srv_call(c, true);
     if (rc) return rc;
-    *nn_class = c->box->out[0];
+    *nn_class = (int)c->box->res[1];
   } else {
   rc = ensure_stage(c);
   if (rc) return rc;
@@ -1193,6 +1194,12 @@ int fme_nn_pred_single(fme_ctx* c, const uint32_t* e, uint32_t cc, int pu_h, int
     split(ox, out4[0], out4[1]);
     split(oy, out4[2], out4[3]);
   }
+  return FME_OK;
+}
+
+int fme_single_last_device_us(fme_ctx* c, float* us) {
+  if (!c || !us) return fail(FME_E_INVALID, "fme_single_last_device_us: null argument");
+  *us = c->box ? (float)((double)c->box->res[3] * 1000.0 / (double)c->srv_khz) : 0.0f;
   return FME_OK;
 }
 

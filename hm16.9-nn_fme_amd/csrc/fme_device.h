@@ -183,7 +183,7 @@ struct NnIn11 {   // NN_pred() inputs of a single call: array_e slots[8], C, PUH
   uint32_t v[11];
 };
 // The single-call server (fme_server.hip): one resident workgroup polls `req_seq` in this block of
-// pinned, device-mapped host memory, serves the call and releases `done_seq`; `stopped` = the
+// pinned, device-mapped host memory, serves the call and stores the answer block `res`; `stopped` = the
 // epoch of an instance that exited (idle, lifetime or `stop`).  Request fields share the first
 // lines, the answer has its own, the payload follows.
 enum { kSrvNn = 1, kSrvFrac = 2 };
@@ -196,9 +196,10 @@ struct SrvBox {
   // taken only when all four carry the seq.
   alignas(64) uint32_t req[5][4];
   double ml;                   // motion lambda (TComRdCost::m_motionLambda)
-  alignas(64) uint32_t done_seq;   // device -> host
+  // device -> host, one 16-byte store: seq, FracDIF cost / NN class, FracDIF half x, y and quarter
+  // x, y as int8 (bytes 0..3), the call's device ticks (request read to answer)
+  alignas(64) uint32_t res[4];
   uint32_t stopped;
-  int32_t out[6];              // FracDIF: half x, y, quarter x, y, cost; NN: class
   alignas(64) int16_t key[64 * 64];
   uint8_t win[72 * 72];        // (w + 8) x (h + 8) window around the integer MV, stride w + 8
 };

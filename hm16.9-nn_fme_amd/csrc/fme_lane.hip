@@ -773,9 +773,11 @@ template <int PW, int PH, int UW, int UH>
 // (The signature matters to the register allocation of the call: with the kernel-argument
 // reference `a` the callee saves no registers; with the same values as separate scalar arguments
 // it saved and restored 114 callee-saved VGPRs per call.)
+// (The lane comes from mbcnt and the wave index is an argument: a callee that reads no work-item
+// id needs none passed, so the caller keeps no VGPR of it alive, and reloads none, around the call.)
 __device__ FME_LANE_UNIT_ATTR void lane_unit(const BatchArgs& a, const fme_job* __restrict__ sjobs_,
                                              const int32_t* __restrict__ perm_, int cls_off, int cls_cnt,
-                                             int wt) {
+                                             int wt, int wid) {
   g_job* const sjobs = (g_job*)sjobs_;
   g_i32* const perm = (g_i32*)perm_;
   g_res* const outp = (g_res*)a.res;
@@ -803,7 +805,7 @@ __device__ FME_LANE_UNIT_ATTR void lane_unit(const BatchArgs& a, const fme_job* 
   constexpr int EW = (UW + 2 + 3) / 4;        // EMI window dwords per row (cols -1 .. UW)
   constexpr int KW = UW / 2;                  // key dwords per row (bytes: UW / 4 used; int16 pairs: UW / 2)
 
-  const int lane = (int)threadIdx.x & 63;
+  const int lane = (int)__lane_id();
   const int gl = wt * 64 + lane;               // wave tile wt: 64 lanes = 64 / L PUs
   int p = gl / L;
   const int u = gl - p * L;
@@ -821,7 +823,13 @@ __device__ FME_LANE_UNIT_ATTR void lane_unit(const BatchArgs& a, const fme_job* 
     __builtin_memcpy(&j, tmp, sizeof(j));
   }
   const int jid = perm[cls_off + p];
-  const PicDesc ref = g_pics[j.ref_id];
+  // The reference's descriptor is read from LDS where a window is loaded (an opaque index keeps
+  // the compiler from holding the 40-byte copy in registers, or scratch, across the passes).
+  auto ref_pic = [&]() FME_AI -> PicDesc {
+    int rid = j.ref_id;
+    asm volatile("" : "+v"(rid));
+    return g_pics[rid];
+  };
   const uint32_t* const ml = g_cost[j.lambda_id];
   const Metric met = {use_hadamard && !(j.flags & FME_JOB_LOSSLESS), (lane & 1) ? 0xFFFFFFFFu : 0x00010001u,
                       (lane & 1) ? 0u : ~0u};
@@ -880,7 +888,7 @@ __device__ FME_LANE_UNIT_ATTR void lane_unit(const BatchArgs& a, const fme_job* 
       }
       // integer samples at rows -1 .. UH, cols -1 .. UW around the TZ MV (s - 128 bytes)
       uint32_t w[UH + 2][EW];
-      load_window(ref, ox + mvx - 1, oy + h * kHalfRows + mvy - 1, w);
+      load_window(ref_pic(), ox + mvx - 1, oy + h * kHalfRows + mvy - 1, w);
       int so2 = 0;   // SSE's sum of squared key samples
 #pragma unroll
       for (int r = 0; r < UH; r++)
@@ -983,7 +991,6 @@ __device__ FME_LANE_UNIT_ATTR void lane_unit(const BatchArgs& a, const fme_job* 
     n_emi = 8;
   }
   typedef __attribute__((address_space(1))) u32x4a gw4;
-  const int wid = (int)threadIdx.x >> 6;
   if (u == 0) {   // bytes 16..63 of the record: cost, bits (NN tail), c, emi[8], n_emi
     g_rec[wid][lane][1] = make_uint4(0u, 0u, cval, emi[0]);
     g_rec[wid][lane][2] = make_uint4(emi[1], emi[2], emi[3], emi[4]);
@@ -997,7 +1004,7 @@ __device__ FME_LANE_UNIT_ATTR void lane_unit(const BatchArgs& a, const fme_job* 
   uint32_t v[RV][NV];
   KeySrc<UW, UJ> K;
   auto load_half = [&](int h) FME_AI {
-    load_window(ref, ox + mvx - 4, oy + h * kHalfRows + mvy - 4, v);
+    load_window(ref_pic(), ox + mvx - 4, oy + h * kHalfRows + mvy - 4, v);
     uint32_t kraw[UH][KW];
     if constexpr (UPL == 1) {
 #pragma unroll
@@ -1167,8 +1174,11 @@ __device__ __forceinline__ int xcc_id() {
 // 1.21 ms, eight 1.24, sixteen 1.29; without the XCD queues 1.25.
 #define FME_CASE(ID, PW_, PH_, UW_, UH_)                                                             \
   case ID:                                                                                           \
-    lane_unit<PW_, PH_, UW_, UH_>(a, w.sjobs, w.perm, sc->class_off[ID], sc->class_cnt[ID], wt);     \
+    lane_unit<PW_, PH_, UW_, UH_>(a, w.sjobs, w.perm, sc->class_off[ID], sc->class_cnt[ID], wt, wid); \
     break;
+#ifndef FME_LANE_CLAIM_LDS
+#define FME_LANE_CLAIM_LDS 0
+#endif
 #ifndef FME_LANE_WAVE_CLAIMS   // 1: each wave claims its own tiles (no workgroup barrier per claim)
 #define FME_LANE_WAVE_CLAIMS 0
 #endif
@@ -1185,7 +1195,7 @@ void k_search_lane(BatchArgs a, WorkBufs w) {
       g_cost[i / kCostBits][i % kCostBits] = simd::mv_cost(a.mlambda[i / kCostBits], (uint32_t)(i % kCostBits));
     for (int i = threadIdx.x; i < 8 * (kNumClasses + 1); i += kLaneNT) (&s_xq[0][0])[i] = (&sc->xq[0][0])[i];
   }
-  const int home = xcc_id(), wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int home = xcc_id(), wid = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6), lane = __lane_id();
 #if FME_LANE_WAVE_CLAIMS
   __syncthreads();
   // Each wave claims one tile at a time from its XCD's queue, the next claim issued before the
@@ -1240,20 +1250,28 @@ void k_search_lane(BatchArgs a, WorkBufs w) {
       continue;
     }
     int nxt = 0;
+#if FME_LANE_CLAIM_LDS   // the next claim lands in LDS before the tile (its latency is not hidden)
+    par ^= 1;
+    if (threadIdx.x == 0) claim[par] = atomicAdd(&ctr[x], 1);
+#else
     if (threadIdx.x == 0) nxt = atomicAdd(&ctr[x], 1);
+#endif
     const int tw = kGroup * t + wid;
     if (tw < len) {
       int c = 0;
       while (c < kNumClasses - 1 && tw >= s_xq[x][c + 1]) c++;
       const int nt = sc->prefix[c + 1] - sc->prefix[c];
-      const int wt = x * (nt >> 3) + min(x, nt & 7) + (tw - s_xq[x][c]);
+      // wave-uniform: kept in an SGPR, so no VGPR of it lives (and is spilled) across the call
+      const int wt = __builtin_amdgcn_readfirstlane(x * (nt >> 3) + min(x, nt & 7) + (tw - s_xq[x][c]));
       switch (c) {
         FME_LANE_CLASSES(FME_CASE)
         default: break;
       }
     }
+#if !FME_LANE_CLAIM_LDS
     par ^= 1;   // claim[par] is rewritten only after every wave has passed the barrier below
     if (threadIdx.x == 0) claim[par] = nxt;
+#endif
     __syncthreads();
     t = __builtin_amdgcn_readfirstlane(claim[par]);
   }

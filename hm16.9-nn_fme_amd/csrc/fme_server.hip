@@ -21,11 +21,15 @@ namespace {
 
 constexpr int kSrvThreads = 1024;
 
-// TComInterpolationFilter::m_lumaFilter (TComInterpolationFilter.cpp:57-63)
-__constant__ int8_t kSrvLuma[4][8] = {{0, 0, 0, 64, 0, 0, 0, 0},
-                                      {-1, 4, -10, 58, 17, -5, 1, 0},
-                                      {-1, 4, -11, 40, 40, -11, 4, -1},
-                                      {0, 1, -5, 17, 58, -10, 4, -1}};
+// TComInterpolationFilter::m_lumaFilter (TComInterpolationFilter.cpp:57-63): tap t (a constant
+// after unrolling) of fraction f, as selects of immediates (no memory load in the filter loops).
+__device__ __forceinline__ int luma_tap(int f, int t) {
+  constexpr int8_t T[4][8] = {{0, 0, 0, 64, 0, 0, 0, 0},
+                              {-1, 4, -10, 58, 17, -5, 1, 0},
+                              {-1, 4, -11, 40, 40, -11, 4, -1},
+                              {0, 1, -5, 17, 58, -10, 4, -1}};
+  return f == 0 ? T[0][t] : (f == 1 ? T[1][t] : (f == 2 ? T[2][t] : T[3][t]));
+}
 // xPatternRefinement's candidate orders (TEncSearch.cpp:1591-1645 over s_acMvRefineH / Q)
 __constant__ int8_t kSrvRefH[9][2] = {{0, 0}, {0, -1}, {0, 1}, {-1, 0}, {1, 0}, {-1, -1}, {1, -1}, {-1, 1}, {1, 1}};
 __constant__ int8_t kSrvRefQ[9][2] = {{0, 0}, {0, -1}, {0, 1}, {-1, -1}, {1, -1}, {-1, 0}, {1, 0}, {-1, 1}, {1, 1}};
@@ -36,6 +40,9 @@ __device__ __forceinline__ u32x4 load_block(const uint32_t* p) {
   u32x4 v;
   asm volatile("global_load_dwordx4 %0, %1, off sc0 sc1\n\ts_waitcnt vmcnt(0)" : "=v"(v) : "v"(p) : "memory");
   return v;
+}
+__device__ __forceinline__ void store_block(uint32_t* p, u32x4 v) {
+  asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1" : : "v"(p), "v"(v) : "memory");
 }
 __device__ __forceinline__ uint32_t sys_load(const uint32_t* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -81,7 +88,6 @@ __device__ __forceinline__ uint32_t eg_bits_d(int v) {
 
 struct SrvLds {
   float nn[kNnPkFloats];
-  float x1[22], x2[20];
   int16_t key[64 * 64];
   int16_t hp[3][72 * 65];       // first filter stage, fractional phase 1..3, columns -1 .. w-1
   uint8_t win[72 * 72];
@@ -90,19 +96,14 @@ struct SrvLds {
   uint32_t nn_in[12];
   double ml;
   int32_t sel[2];               // half-stage best (hx, hy)
+  uint32_t ans[2];              // the answer (SrvBox::res[1..2])
 };
-
-// First-stage sample at window row wy, PU column x (window column x + 4), phase fx: the 14-bit
-// value m_filteredBlockTmp holds (filterHor isLast = false; filterCopy isFirst for fx = 0).
-__device__ __forceinline__ int h_stage(const SrvLds& L, int w, int fx, int x, int wy) {
-  return fx ? (int)L.hp[fx - 1][wy * (w + 1) + x + 1] : ((int)L.win[wy * (w + 8) + x + 4] << 6) - 8192;
-}
 
 // The 9 candidates of one xPatternRefinement stage: distortion per candidate into L.cost.
 // (ox, oy) of candidate k = base + 2 * ref (half) or base + ref (quarter), quarter-pel offsets from
 // the integer MV.  Work item (candidate, block) per wave; lanes are the block's pixels.
 __device__ void stage_dist(SrvLds& L, int w, int h, bool sad, bool half, int bx0, int by0) {
-  const int lane = (int)threadIdx.x & 63, wid = (int)threadIdx.x >> 6;
+  const int lane = (int)threadIdx.x & 63, wid = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
   const bool b8 = !sad && (w & 7) == 0 && (h & 7) == 0;   // xGetHADs: 8x8 when both dims allow
   const int nb4 = (w >> 2) * (h >> 2);
   const int nb = b8 ? (w >> 3) * (h >> 3) : (nb4 + 3) >> 2;
@@ -112,9 +113,14 @@ __device__ void stage_dist(SrvLds& L, int w, int h, bool sad, bool half, int bx0
   const int n_items = 9 * nb, per = (n_items + NWV - 1) / NWV;
   const int i0 = wid * per, i1 = min(n_items, i0 + per);
   uint32_t acc = 0;
-  int kcur = i0 < i1 ? i0 / nb : 0;
-  for (int item = i0; item < i1; item++) {
-    const int k = item / nb, b = item - k * nb;
+  const int bw8 = w >> 3, bw4 = w >> 2;
+  int k = i0 < i1 ? i0 / nb : 0, b = i0 - k * nb;   // (candidate, block) of the run's first item
+  int kcur = k;
+  for (int item = i0; item < i1; item++, b++) {
+    if (b == nb) {
+      b = 0;
+      k++;
+    }
     if (k != kcur) {
       if (lane == 0) atomicAdd(&L.cost[half ? 0 : 1][kcur], acc);
       acc = 0;
@@ -125,26 +131,39 @@ __device__ void stage_dist(SrvLds& L, int w, int h, bool sad, bool half, int bx0
     int c, r;
     bool valid = true;
     if (b8) {
-      const int bw = w >> 3;
-      c = (b % bw) * 8 + (lane & 7);
-      r = (b / bw) * 8 + (lane >> 3);
+      const int by = b / bw8;
+      c = (b - by * bw8) * 8 + (lane & 7);
+      r = by * 8 + (lane >> 3);
     } else {
       int blk = b * 4 + (lane >> 4);
       valid = blk < nb4;
       blk = valid ? blk : 0;
-      const int bw = w >> 2;
-      c = (blk % bw) * 4 + (lane & 3);
-      r = (blk / bw) * 4 + ((lane >> 2) & 3);
+      const int by = blk / bw4;
+      c = (blk - by * bw4) * 4 + (lane & 3);
+      r = by * 4 + ((lane >> 2) & 3);
     }
-    const int ix = ox >> 2, fx = ox & 3, iy = oy >> 2, fy = oy & 3;
+    // the candidate's phases are wave-uniform: scalar branches, taps as immediates
+    const int ix = __builtin_amdgcn_readfirstlane(ox >> 2), fx = __builtin_amdgcn_readfirstlane(ox & 3);
+    const int iy = __builtin_amdgcn_readfirstlane(oy >> 2), fy = __builtin_amdgcn_readfirstlane(oy & 3);
     const int x = c + ix, wy0 = r + iy + 4;
+    // first-stage samples at window rows wy0 - 3 .. wy0 + 4: the 14-bit values m_filteredBlockTmp
+    // holds (filterHor with isLast false; filterCopy's isFirst branch for fraction 0)
+    int hs[8];
+    if (fx == 0) {
+#pragma unroll
+      for (int t = 0; t < 8; t++) hs[t] = ((int)L.win[(wy0 + t - 3) * (w + 8) + x + 4] << 6) - 8192;
+    } else {
+      const int16_t* hp = L.hp[fx - 1] + x + 1;
+#pragma unroll
+      for (int t = 0; t < 8; t++) hs[t] = hp[(wy0 + t - 3) * (w + 1)];
+    }
     int v;
     if (fy == 0) {
-      v = (h_stage(L, w, fx, x, wy0) + 8192 + 32) >> 6;   // filterCopy, !isFirst isLast
+      v = (hs[3] + 8192 + 32) >> 6;                        // filterCopy, !isFirst isLast
     } else {
       int s = 0;
 #pragma unroll
-      for (int t = 0; t < 8; t++) s += (int)kSrvLuma[fy][t] * h_stage(L, w, fx, x, wy0 + t - 3);
+      for (int t = 0; t < 8; t++) s += luma_tap(fy, t) * hs[t];
       v = (s + 2048 + (8192 << 6)) >> 12;                  // filter<8, true, false, true>
     }
     v = min(255, max(0, v));
@@ -204,16 +223,17 @@ __device__ void serve_frac(SrvLds& L, SrvBox* box) {
   const bool sad = L.ctl[7] != 0;
   const int pw = w + 8, ph = h + 8;
   // first filter stage of phases 1..3 over window rows 0 .. h+7, PU columns -1 .. w-1
-  {
-    const int cols = w + 1, plane = ph * cols;
-    for (int i = tid; i < 3 * plane; i += kSrvThreads) {
-      const int f = i / plane, rem = i - f * plane, wy = rem / cols, x = rem - wy * cols - 1;
-      const uint8_t* row = L.win + wy * pw + x + 1;   // taps at window columns x + 4 - 3 ...
-      int s = 0;
+  {   // thread (xr, rr): column xr - 1 of rows rr, rr + 8, ... of the three phases' planes
+    const int cols = w + 1, xr = tid & 127;
+    if (xr < cols)
+      for (int R = tid >> 7; R < 3 * ph; R += kSrvThreads >> 7) {
+        const int f = R >= 2 * ph ? 2 : (R >= ph ? 1 : 0), wy = R - f * ph;
+        const uint8_t* row = L.win + wy * pw + xr;   // taps at window columns x + 4 - 3 ...
+        int s = 0;
 #pragma unroll
-      for (int t = 0; t < 8; t++) s += (int)kSrvLuma[f + 1][t] * (int)row[t];
-      L.hp[f][rem] = (int16_t)(s - 8192);
-    }
+        for (int t = 0; t < 8; t++) s += luma_tap(f + 1, t) * (int)row[t];
+        L.hp[f][wy * cols + xr] = (int16_t)(s - 8192);
+      }
   }
   __syncthreads();
   stage_dist(L, w, h, sad, true, 0, 0);
@@ -236,21 +256,25 @@ __device__ void serve_frac(SrvLds& L, SrvBox* box) {
     uint32_t best;
     stage_pick(L, false, hx, hy, k, best);
     if (tid == 0) {
-      box->out[0] = hx;
-      box->out[1] = hy;
-      box->out[2] = kSrvRefQ[k][0];
-      box->out[3] = kSrvRefQ[k][1];
-      box->out[4] = (int32_t)best;
+      L.ans[0] = best;
+      L.ans[1] = (uint32_t)(uint8_t)hx | ((uint32_t)(uint8_t)hy << 8) | ((uint32_t)(uint8_t)kSrvRefQ[k][0] << 16) |
+                 ((uint32_t)(uint8_t)kSrvRefQ[k][1] << 24);
     }
   }
 }
 
-// NN_pred (TEncSearch.cpp:85-134) on the packed layout in LDS: lane rp owns row pair rp of each
-// layer, every row summed in k order without contraction (the batch tail's arithmetic).
+// NN_pred (TEncSearch.cpp:85-134) on the packed layout in LDS, in wave 0 alone: lane rp owns row
+// pair rp of each layer, every row summed in k order without contraction (the batch tail's
+// arithmetic), and a layer's outputs reach every lane as scalars (readlane) instead of through
+// LDS and a workgroup barrier.
+__device__ __forceinline__ float lane_f(float v, int l) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), l));
+}
 __device__ void serve_nn(SrvLds& L, SrvBox* box) {
   const int rp = (int)threadIdx.x;
+  if (rp >= 64) return;
   const float* Q = L.nn;
-  const uint32_t* v = L.nn_in;   // copied by the polling lane with the request
+  const uint32_t* v = L.nn_in;   // copied by the polling lanes with the request
   const int t = emb_row_h((int)v[9]) * 8 + emb_row_w((int)v[10]);
   float in[9];
   const uint32_t raw[9] = {v[0], v[1], v[2], v[3], v[8], v[4], v[5], v[6], v[7]};
@@ -260,56 +284,57 @@ __device__ void serve_nn(SrvLds& L, SrvBox* box) {
     x = (x - Q[kNnPkMean + k]) / Q[kNnPkStd + k];
     in[k] = x * Q[kNnPkGin + k];
   }
-  if (rp < 11) {
+  const int r1 = rp < 11 ? rp : 10, r2 = rp < 10 ? rp : 9, r3 = rp < 25 ? rp : 24;
+  f2 x1;
+  {
     const float* pfx = Q + kNnPkPfx + t * 22;
-    f2 x = {pfx[2 * rp], pfx[2 * rp + 1]};
+    x1 = (f2){pfx[2 * r1], pfx[2 * r1 + 1]};
 #pragma unroll
-    for (int k = 0; k < 9; k++) x = x + ld2(Q, kNnPkW1 + (rp * 9 + k) * 2) * (f2){in[k], in[k]};
-    x = relu2(x + ld2(Q, kNnPkB1 + 2 * rp));
-    x = x * ld2(Q, kNnPkG1 + 2 * rp) + ld2(Q, kNnPkBE1 + 2 * rp);
-    L.x1[2 * rp] = x.x;
-    L.x1[2 * rp + 1] = x.y;
+    for (int k = 0; k < 9; k++) x1 = x1 + ld2(Q, kNnPkW1 + (r1 * 9 + k) * 2) * (f2){in[k], in[k]};
+    x1 = relu2(x1 + ld2(Q, kNnPkB1 + 2 * r1));
+    x1 = x1 * ld2(Q, kNnPkG1 + 2 * r1) + ld2(Q, kNnPkBE1 + 2 * r1);
   }
-  __syncthreads();
-  if (rp < 10) {
-    f2 x = {0.0f, 0.0f};
+  f2 x2 = {0.0f, 0.0f};
 #pragma unroll
-    for (int k = 0; k < 22; k++) x = x + ld2(Q, kNnPkW2 + (rp * 22 + k) * 2) * (f2){L.x1[k], L.x1[k]};
-    x = relu2(x + ld2(Q, kNnPkB2 + 2 * rp));
-    x = x * ld2(Q, kNnPkG2 + 2 * rp) + ld2(Q, kNnPkBE2 + 2 * rp);
-    L.x2[2 * rp] = x.x;
-    L.x2[2 * rp + 1] = x.y;
+  for (int k = 0; k < 22; k++) {
+    const float a = lane_f((k & 1) ? x1.y : x1.x, k >> 1);
+    x2 = x2 + ld2(Q, kNnPkW2 + (r2 * 22 + k) * 2) * (f2){a, a};
   }
-  __syncthreads();
-  if (rp < 64) {
-    // output row pair rp, then the first maximum over the 49 rows (strict >, rows in order)
-    float bv = -INFINITY;
-    int bi = 64;
-    if (rp < 25) {
-      f2 x = {0.0f, 0.0f};
+  x2 = relu2(x2 + ld2(Q, kNnPkB2 + 2 * r2));
+  x2 = x2 * ld2(Q, kNnPkG2 + 2 * r2) + ld2(Q, kNnPkBE2 + 2 * r2);
+  f2 x3 = {0.0f, 0.0f};
 #pragma unroll
-      for (int k = 0; k < 20; k++) x = x + ld2(Q, kNnPkW3 + (rp * 20 + k) * 2) * (f2){L.x2[k], L.x2[k]};
-      x = x + ld2(Q, kNnPkBout + 2 * rp);
-      // the batch rule's NaNs (row 0 taken first, then strict >): a NaN row 0 wins, a later NaN never
-      if (x.x != x.x) x.x = rp == 0 ? INFINITY : -INFINITY;
-      if (x.y != x.y) x.y = -INFINITY;
-      bv = x.x;
-      bi = 2 * rp;
-      if (rp < 24 && x.y > bv) {
-        bv = x.y;
-        bi = 2 * rp + 1;
-      }
+  for (int k = 0; k < 20; k++) {
+    const float a = lane_f((k & 1) ? x2.y : x2.x, k >> 1);
+    x3 = x3 + ld2(Q, kNnPkW3 + (r3 * 20 + k) * 2) * (f2){a, a};
+  }
+  x3 = x3 + ld2(Q, kNnPkBout + 2 * r3);
+  // output row pair rp, then the first maximum over the 49 rows (strict >, rows in order)
+  float bv = -INFINITY;
+  int bi = 64;
+  if (rp < 25) {
+    // the batch rule's NaNs (row 0 taken first, then strict >): a NaN row 0 wins, a later NaN never
+    if (x3.x != x3.x) x3.x = rp == 0 ? INFINITY : -INFINITY;
+    if (x3.y != x3.y) x3.y = -INFINITY;
+    bv = x3.x;
+    bi = 2 * rp;
+    if (rp < 24 && x3.y > bv) {
+      bv = x3.y;
+      bi = 2 * rp + 1;
     }
+  }
 #pragma unroll
-    for (int off = 1; off < 64; off <<= 1) {
-      const float ov = __shfl_xor(bv, off, 64);
-      const int oi = __shfl_xor(bi, off, 64);
-      if (ov > bv || (ov == bv && oi < bi)) {
-        bv = ov;
-        bi = oi;
-      }
+  for (int off = 1; off < 64; off <<= 1) {
+    const float ov = __shfl_xor(bv, off, 64);
+    const int oi = __shfl_xor(bi, off, 64);
+    if (ov > bv || (ov == bv && oi < bi)) {
+      bv = ov;
+      bi = oi;
     }
-    if (rp == 0) box->out[0] = bi;
+  }
+  if (rp == 0) {
+    L.ans[0] = (uint32_t)bi;
+    L.ans[1] = 0;
   }
 }
 
@@ -361,17 +386,22 @@ __global__ __launch_bounds__(kSrvThreads) void k_server(SrvBox* box, const float
     }
     __syncthreads();
     if (L.ctl[0]) break;
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");   // the payload after its request word
+    const uint64_t t_req = wall_clock64();
     if (L.ctl[2] == kSrvFrac) {   // the window and key, every thread at once (one round trip)
       const int w = L.ctl[3], h = L.ctl[4];
+      // system-scope loads: straight from host memory, no cache to invalidate first
       const uint32_t* wsrc = reinterpret_cast<const uint32_t*>(box->win);
       uint32_t* wdst = reinterpret_cast<uint32_t*>(L.win);
-      for (int i = tid; i < ((w + 8) * (h + 8) + 3) >> 2; i += kSrvThreads) wdst[i] = wsrc[i];
+      for (int i = tid; i < ((w + 8) * (h + 8) + 3) >> 2; i += kSrvThreads) wdst[i] = sys_load(wsrc + i);
       const uint32_t* ksrc = reinterpret_cast<const uint32_t*>(box->key);
       uint32_t* kdst = reinterpret_cast<uint32_t*>(L.key);
-      for (int i = tid; i < (w * h) >> 1; i += kSrvThreads) kdst[i] = ksrc[i];
+      for (int i = tid; i < (w * h) >> 1; i += kSrvThreads) kdst[i] = sys_load(ksrc + i);
       if (tid < 32) (&L.cost[0][0])[tid] = 0;
-      if (tid == 64) L.ml = box->ml;
+      if (tid == 64) {
+        const uint32_t* m = reinterpret_cast<const uint32_t*>(&box->ml);
+        const uint64_t lo = sys_load(m), hi = sys_load(m + 1);
+        L.ml = __builtin_bit_cast(double, lo | (hi << 32));
+      }
       __syncthreads();
     }
     const uint32_t seq = (uint32_t)L.ctl[1];
@@ -380,7 +410,10 @@ __global__ __launch_bounds__(kSrvThreads) void k_server(SrvBox* box, const float
     else
       serve_nn(L, box);
     __syncthreads();
-    if (tid == 0) sys_store_release(&box->done_seq, seq);   // after the answer's stores
+    if (tid == 0) {   // the answer and its sequence word in one 16-byte store, past the caches
+      const u32x4 r = {seq, L.ans[0], L.ans[1], (uint32_t)(wall_clock64() - t_req)};
+      store_block(box->res, r);
+    }
     served = seq;
     last = wall_clock64();
   }

@@ -24,7 +24,7 @@ ABI_SYMBOLS = (
     "fme_bind_picture_device", "fme_set_lambda", "fme_set_motion_lambda", "fme_set_keys",
     "fme_load_nn_weights", "fme_nn_reset_state", "fme_nn_get_state", "fme_nn_set_state", "fme_refine", "fme_refine_device",
     "fme_frac_dif_single", "fme_nn_pred_single", "fme_set_profiling", "fme_last_timings",
-    "fme_accumulated_timings", "fme_search_kernel_of_shape",
+    "fme_accumulated_timings", "fme_single_last_device_us", "fme_search_kernel_of_shape",
     "fme_set_picture_chroma", "fme_bind_picture_chroma_device", "fme_motion_compensate",
     "fme_motion_compensate_device", "fme_mc_invalid_count", "fme_mc_last_ms",
     "fme_integer_search", "fme_integer_search_device", "fme_integer_search_last_ms",
@@ -81,6 +81,7 @@ def load_library(path=None):
         "fme_set_profiling": (I, [P, I]),
         "fme_last_timings": (I, [P, P, I]),
         "fme_accumulated_timings": (I, [P, P, I, I]),
+        "fme_single_last_device_us": (I, [P, P]),
         "fme_search_kernel_of_shape": (I, [I, I]),
         "fme_set_picture_chroma": (I, [P, I, P, P, I, P]),
         "fme_bind_picture_chroma_device": (I, [P, I, P, P, I]),
@@ -432,6 +433,13 @@ class FmeContext:
         ms = np.zeros(len(TIMING_NAMES), np.float32)
         _check(self.lib, self.lib.fme_last_timings(self.h, _ptr(ms), ms.size))
         return dict(zip(TIMING_NAMES, ms.tolist()))
+
+    def single_last_device_us(self):
+        """Device microseconds of the last single-PU call (the server's read of the request to its
+        answer)."""
+        us = np.zeros(1, np.float32)
+        _check(self.lib, self.lib.fme_single_last_device_us(self.h, _ptr(us)))
+        return float(us[0])
 
     def accumulated_timings(self, reset=True):
         """(batches, {name: summed device ms}) over the profiled batches since the last reset."""

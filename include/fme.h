@@ -605,6 +605,10 @@ int fme_set_profiling(fme_ctx* ctx, int enable);
 int fme_search_kernel_of_shape(int width, int height);
 int fme_last_timings(fme_ctx* ctx, float* ms, int count);
 int fme_accumulated_timings(fme_ctx* ctx, double* ms, int count, int reset);
+/* The last fme_frac_dif_single / fme_nn_pred_single call as the resident server saw it: device
+ * microseconds from reading the request to releasing the answer (the rest of the call's wall time
+ * is the host, PCIe and polling). */
+int fme_single_last_device_us(fme_ctx* ctx, float* us);
 
 #ifdef __cplusplus
 }

@@ -19,7 +19,7 @@ def header_functions():
 def test_library_exports_header():
     lib = runtime.load_library()
     names = header_functions()
-    assert len(names) == 49
+    assert len(names) == 50
     assert set(names) == set(runtime.ABI_SYMBOLS)
     for n in names:
         assert hasattr(lib, n), n
