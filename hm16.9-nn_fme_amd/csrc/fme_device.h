@@ -165,6 +165,9 @@ struct TzChain {
   int32_t nlev;
 };
 hipError_t launch_tz_levels(const TzArgs& ta, const TzChain& ch, const int32_t* h_lvl_off, hipStream_t s);
+// The same chain in one persistent launch; done[n] zeroed by the caller, abort_w[0] too (> 0 after
+// the launch: a wait timed out and the results are incomplete).
+hipError_t launch_tz_flow(const TzArgs& ta, const TzChain& ch, int32_t* done, int32_t* abort_w, int n, hipStream_t s);
 
 // Host-side launch helpers (fme_kernels.hip).
 hipError_t launch_classify(const BatchArgs& a, const WorkBufs& w, hipStream_t s);
@@ -199,6 +202,7 @@ struct SrvBox {
   // device -> host, one 16-byte store: seq, FracDIF cost / NN class, FracDIF half x, y and quarter
   // x, y as int8 (bytes 0..3), the call's device ticks (request read to answer)
   alignas(64) uint32_t res[4];
+  uint32_t marks[4];           // FracDIF checkpoints of the call (fme_single_last_device_us)
   uint32_t stopped;
   alignas(64) int16_t key[64 * 64];
   uint8_t win[72 * 72];        // (w + 8) x (h + 8) window around the integer MV, stride w + 8

@@ -1176,9 +1176,6 @@ __device__ __forceinline__ int xcc_id() {
   case ID:                                                                                           \
     lane_unit<PW_, PH_, UW_, UH_>(a, w.sjobs, w.perm, sc->class_off[ID], sc->class_cnt[ID], wt, wid); \
     break;
-#ifndef FME_LANE_CLAIM_LDS
-#define FME_LANE_CLAIM_LDS 0
-#endif
 #ifndef FME_LANE_WAVE_CLAIMS   // 1: each wave claims its own tiles (no workgroup barrier per claim)
 #define FME_LANE_WAVE_CLAIMS 0
 #endif
@@ -1250,12 +1247,7 @@ void k_search_lane(BatchArgs a, WorkBufs w) {
       continue;
     }
     int nxt = 0;
-#if FME_LANE_CLAIM_LDS   // the next claim lands in LDS before the tile (its latency is not hidden)
-    par ^= 1;
-    if (threadIdx.x == 0) claim[par] = atomicAdd(&ctr[x], 1);
-#else
     if (threadIdx.x == 0) nxt = atomicAdd(&ctr[x], 1);
-#endif
     const int tw = kGroup * t + wid;
     if (tw < len) {
       int c = 0;
@@ -1268,10 +1260,8 @@ void k_search_lane(BatchArgs a, WorkBufs w) {
         default: break;
       }
     }
-#if !FME_LANE_CLAIM_LDS
     par ^= 1;   // claim[par] is rewritten only after every wave has passed the barrier below
     if (threadIdx.x == 0) claim[par] = nxt;
-#endif
     __syncthreads();
     t = __builtin_amdgcn_readfirstlane(claim[par]);
   }

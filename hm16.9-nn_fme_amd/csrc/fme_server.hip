@@ -97,6 +97,8 @@ struct SrvLds {
   double ml;
   int32_t sel[2];               // half-stage best (hx, hy)
   uint32_t ans[2];              // the answer (SrvBox::res[1..2])
+  uint32_t mark[4];             // FracDIF checkpoints (ticks since the request read): first stage, half
+                                // distortions, half pick, quarter distortions
 };
 
 // The 9 candidates of one xPatternRefinement stage: distortion per candidate into L.cost.
@@ -217,8 +219,11 @@ __device__ void stage_pick(const SrvLds& L, bool half, int hx, int hy, int& best
   best = tot;
 }
 
-__device__ void serve_frac(SrvLds& L, SrvBox* box) {
+__device__ void serve_frac(SrvLds& L, SrvBox* box, uint64_t t_req) {
   const int tid = (int)threadIdx.x;
+  auto mark = [&](int m) {
+    if (tid == 0) L.mark[m] = (uint32_t)(wall_clock64() - t_req);
+  };
   const int w = L.ctl[3], h = L.ctl[4];
   const bool sad = L.ctl[7] != 0;
   const int pw = w + 8, ph = h + 8;
@@ -236,8 +241,10 @@ __device__ void serve_frac(SrvLds& L, SrvBox* box) {
       }
   }
   __syncthreads();
+  mark(0);
   stage_dist(L, w, h, sad, true, 0, 0);
   __syncthreads();
+  mark(1);
   if (tid < 64) {
     int k;
     uint32_t best;
@@ -248,9 +255,11 @@ __device__ void serve_frac(SrvLds& L, SrvBox* box) {
     }
   }
   __syncthreads();
+  mark(2);
   const int hx = L.sel[0], hy = L.sel[1];
   stage_dist(L, w, h, sad, false, 2 * hx, 2 * hy);
   __syncthreads();
+  mark(3);
   if (tid < 64) {
     int k;
     uint32_t best;
@@ -406,11 +415,13 @@ __global__ __launch_bounds__(kSrvThreads) void k_server(SrvBox* box, const float
     }
     const uint32_t seq = (uint32_t)L.ctl[1];
     if (L.ctl[2] == kSrvFrac)
-      serve_frac(L, box);
+      serve_frac(L, box, t_req);
     else
       serve_nn(L, box);
     __syncthreads();
     if (tid == 0) {   // the answer and its sequence word in one 16-byte store, past the caches
+      const u32x4 m = {L.mark[0], L.mark[1], L.mark[2], L.mark[3]};
+      store_block(box->marks, m);
       const u32x4 r = {seq, L.ans[0], L.ans[1], (uint32_t)(wall_clock64() - t_req)};
       store_block(box->res, r);
     }

@@ -81,7 +81,7 @@ def load_library(path=None):
         "fme_set_profiling": (I, [P, I]),
         "fme_last_timings": (I, [P, P, I]),
         "fme_accumulated_timings": (I, [P, P, I, I]),
-        "fme_single_last_device_us": (I, [P, P]),
+        "fme_single_last_device_us": (I, [P, P, I]),
         "fme_search_kernel_of_shape": (I, [I, I]),
         "fme_set_picture_chroma": (I, [P, I, P, P, I, P]),
         "fme_bind_picture_chroma_device": (I, [P, I, P, P, I]),
@@ -434,12 +434,13 @@ class FmeContext:
         _check(self.lib, self.lib.fme_last_timings(self.h, _ptr(ms), ms.size))
         return dict(zip(TIMING_NAMES, ms.tolist()))
 
-    def single_last_device_us(self):
+    def single_last_device_us(self, phases=False):
         """Device microseconds of the last single-PU call (the server's read of the request to its
-        answer)."""
-        us = np.zeros(1, np.float32)
-        _check(self.lib, self.lib.fme_single_last_device_us(self.h, _ptr(us)))
-        return float(us[0])
+        answer); phases=True: also the FracDIF checkpoints (first stage, half distortions, half
+        pick, quarter distortions)."""
+        us = np.zeros(5, np.float32)
+        _check(self.lib, self.lib.fme_single_last_device_us(self.h, _ptr(us), 5))
+        return us.tolist() if phases else float(us[0])
 
     def accumulated_timings(self, reset=True):
         """(batches, {name: summed device ms}) over the profiled batches since the last reset."""

@@ -605,10 +605,11 @@ int fme_set_profiling(fme_ctx* ctx, int enable);
 int fme_search_kernel_of_shape(int width, int height);
 int fme_last_timings(fme_ctx* ctx, float* ms, int count);
 int fme_accumulated_timings(fme_ctx* ctx, double* ms, int count, int reset);
-/* The last fme_frac_dif_single / fme_nn_pred_single call as the resident server saw it: device
- * microseconds from reading the request to releasing the answer (the rest of the call's wall time
- * is the host, PCIe and polling). */
-int fme_single_last_device_us(fme_ctx* ctx, float* us);
+/* The last fme_frac_dif_single / fme_nn_pred_single call as the resident server saw it, device
+ * microseconds since it read the request: us[0] to the answer (the rest of the call's wall time
+ * is the host, PCIe and polling); FracDIF only, us[1..4] to the first filter stage, the half
+ * stage's distortions, its pick, the quarter stage's distortions.  count <= 5 values. */
+int fme_single_last_device_us(fme_ctx* ctx, float* us, int count);
 
 #ifdef __cplusplus
 }

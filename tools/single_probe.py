@@ -26,7 +26,7 @@ def main():
     rng = np.random.default_rng(3)
     ml = 65536.0 * np.sqrt(synth.LDP_LAMBDA[22][0])
     for (w, h) in ((8, 8), (16, 16), (64, 64)):
-        wall, dev = [], []
+        wall, dev, ph = [], [], []
         for i in range(calls):
             x, y = 4 * int(rng.integers(0, (W - w) // 4)), 4 * int(rng.integers(0, (H - h) // 4))
             key = org[y:y + h, x:x + w]
@@ -35,8 +35,12 @@ def main():
             t0 = time.perf_counter()
             ctx.frac_dif_single(key, pic, (y + pad, x + pad), mv, mvp, ml)
             wall.append(time.perf_counter() - t0)
-            dev.append(ctx.single_last_device_us())
-        print(f"frac_dif {w}x{h}: wall {np.median(wall[1:]) * 1e6:.2f} us, device {np.median(dev[1:]):.2f} us", flush=True)
+            p = ctx.single_last_device_us(phases=True)
+            dev.append(p[0])
+            ph.append(p[1:])
+        m = np.median(np.array(ph[1:]), axis=0)
+        print(f"frac_dif {w}x{h}: wall {np.median(wall[1:]) * 1e6:.2f} us, device {np.median(dev[1:]):.2f} us "
+              f"(first stage {m[0]:.2f}, half dist {m[1]:.2f}, half pick {m[2]:.2f}, quarter dist {m[3]:.2f})", flush=True)
     wall, dev = [], []
     for i in range(calls):
         e = rng.integers(0, 5000, 8).astype(np.uint32)
