@@ -21,12 +21,6 @@
 
 using namespace fme;
 
-// 1: the producers' m_integerMv2Nx2N chain as one persistent launch (k_tz_flow); 0: one launch
-// per dependency level (k_tz_level)
-#ifndef FME_TZ_FLOW
-#define FME_TZ_FLOW 1
-#endif
-
 namespace {
 
 thread_local std::string g_last_error = "";
@@ -150,7 +144,6 @@ struct fme_ctx {
   DevBuf<BiKeyTask> d_bikey;
   DevBuf<int32_t> d_key_invalid;  // invalid requests of the last fme_build_bipred_keys_device
   DevBuf<int32_t> d_ch_i32;     // k_tz_level: psrc
-  DevBuf<int32_t> d_flow;       // k_tz_flow: abort count, then a completion word per chain job
 
   // The deeper nets' single NN_pred: inputs in the kernel argument, class and completion word in
   // pinned, device-mapped host memory.
@@ -262,7 +255,7 @@ int fme_destroy(fme_ctx* c) {
     if (c->chroma_owned[i]) (void)hipFree(c->chroma_owned[i]);
   c->d_mc_jobs.release(); c->d_mc_planes.release(); c->d_mc_invalid.release();
   c->d_tz_ext.release(); c->d_tz_sad.release(); c->d_tz_nn_in.release();
-  c->d_amvp.release(); c->d_amvp_sad.release(); c->d_bikey.release(); c->d_key_invalid.release(); c->d_ch_i32.release(); c->d_tz_emi.release(); c->d_flow.release();
+  c->d_amvp.release(); c->d_amvp_sad.release(); c->d_bikey.release(); c->d_key_invalid.release(); c->d_ch_i32.release(); c->d_tz_emi.release();
   for (auto& e : c->ev_tz)
     if (e) (void)hipEventDestroy(e);
   for (auto& e : c->ev_mc)
@@ -903,22 +896,11 @@ static int tz_by_level(fme_ctx* c, std::vector<fme_job>& jobs, std::vector<fme_t
   ta.ext = c->d_tz_ext.p;
   ta.emi_mv = c->d_tz_emi.p;
   const TzChain ch{c->d_ch_i32.p, max_level + 1};
-#if FME_TZ_FLOW
-  HIP_TRY(c->d_flow.reserve((size_t)nu + 1));
-  HIP_TRY(hipMemsetAsync(c->d_flow.p, 0, ((size_t)nu + 1) * sizeof(int32_t), s));
-  HIP_TRY(launch_tz_flow(ta, ch, c->d_flow.p + 1, c->d_flow.p, nu, s));
-  int32_t aborted = 0;
-  HIP_TRY(hipMemcpyAsync(&aborted, c->d_flow.p, sizeof(int32_t), hipMemcpyDeviceToHost, s));
-#else
   HIP_TRY(launch_tz_levels(ta, ch, off.data(), s));
-#endif
   std::vector<int16_t> lemi((size_t)2 * nu);
   HIP_TRY(hipMemcpyAsync(lj.data(), c->d_jobs.p, (size_t)nu * sizeof(fme_job), hipMemcpyDeviceToHost, s));
   HIP_TRY(hipMemcpyAsync(lemi.data(), c->d_tz_emi.p, (size_t)2 * nu * sizeof(int16_t), hipMemcpyDeviceToHost, s));
   HIP_TRY(hipStreamSynchronize(s));
-#if FME_TZ_FLOW
-  if (aborted) return fail(FME_E_DEVICE, "integer-search chain: %d wait(s) timed out", aborted);
-#endif
   for (int q = 0; q < nu; q++) {
     const int u = order[q];
     jobs[u] = lj[q];

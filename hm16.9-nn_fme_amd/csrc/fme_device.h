@@ -165,9 +165,6 @@ struct TzChain {
   int32_t nlev;
 };
 hipError_t launch_tz_levels(const TzArgs& ta, const TzChain& ch, const int32_t* h_lvl_off, hipStream_t s);
-// The same chain in one persistent launch; done[n] zeroed by the caller, abort_w[0] too (> 0 after
-// the launch: a wait timed out and the results are incomplete).
-hipError_t launch_tz_flow(const TzArgs& ta, const TzChain& ch, int32_t* done, int32_t* abort_w, int n, hipStream_t s);
 
 // Host-side launch helpers (fme_kernels.hip).
 hipError_t launch_classify(const BatchArgs& a, const WorkBufs& w, hipStream_t s);
@@ -204,8 +201,8 @@ struct SrvBox {
   alignas(64) uint32_t res[4];
   uint32_t marks[4];           // FracDIF checkpoints of the call (fme_single_last_device_us)
   uint32_t stopped;
-  alignas(64) int16_t key[64 * 64];
-  uint8_t win[72 * 72];        // (w + 8) x (h + 8) window around the integer MV, stride w + 8
+  alignas(64) int16_t key[64 * 64];   // w * h (a multiple of 16 bytes for every PU shape)
+  alignas(16) uint8_t win[72 * 72 + 16];   // (w + 8) x (h + 8) window around the integer MV, stride w + 8
 };
 hipError_t launch_server(SrvBox* box, const float* nn, uint32_t served, uint32_t epoch, uint64_t idle_ticks,
                          uint64_t life_ticks, hipStream_t s);

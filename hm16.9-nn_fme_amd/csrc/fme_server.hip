@@ -88,9 +88,9 @@ __device__ __forceinline__ uint32_t eg_bits_d(int v) {
 
 struct SrvLds {
   float nn[kNnPkFloats];
-  int16_t key[64 * 64];
+  alignas(16) int16_t key[64 * 64];
   int16_t hp[3][72 * 65];       // first filter stage, fractional phase 1..3, columns -1 .. w-1
-  uint8_t win[72 * 72];
+  alignas(16) uint8_t win[72 * 72 + 16];
   uint32_t cost[2][16];           // per candidate: half stage, quarter stage
   int32_t ctl[8];               // stop, seq, kind, w, h, mvp_x, mvp_y, sad
   uint32_t nn_in[12];
@@ -398,13 +398,14 @@ __global__ __launch_bounds__(kSrvThreads) void k_server(SrvBox* box, const float
     const uint64_t t_req = wall_clock64();
     if (L.ctl[2] == kSrvFrac) {   // the window and key, every thread at once (one round trip)
       const int w = L.ctl[3], h = L.ctl[4];
-      // system-scope loads: straight from host memory, no cache to invalidate first
+      // 16-byte system-coherent loads: straight from host memory, no cache to invalidate first,
+      // one request per block (the window's last block may read into the padding after it)
       const uint32_t* wsrc = reinterpret_cast<const uint32_t*>(box->win);
-      uint32_t* wdst = reinterpret_cast<uint32_t*>(L.win);
-      for (int i = tid; i < ((w + 8) * (h + 8) + 3) >> 2; i += kSrvThreads) wdst[i] = sys_load(wsrc + i);
+      u32x4* wdst = reinterpret_cast<u32x4*>(L.win);
+      for (int i = tid; i < ((w + 8) * (h + 8) + 15) >> 4; i += kSrvThreads) wdst[i] = load_block(wsrc + 4 * i);
       const uint32_t* ksrc = reinterpret_cast<const uint32_t*>(box->key);
-      uint32_t* kdst = reinterpret_cast<uint32_t*>(L.key);
-      for (int i = tid; i < (w * h) >> 1; i += kSrvThreads) kdst[i] = sys_load(ksrc + i);
+      u32x4* kdst = reinterpret_cast<u32x4*>(L.key);
+      for (int i = tid; i < (w * h) >> 3; i += kSrvThreads) kdst[i] = load_block(ksrc + 4 * i);
       if (tid < 32) (&L.cost[0][0])[tid] = 0;
       if (tid == 64) {
         const uint32_t* m = reinterpret_cast<const uint32_t*>(&box->ml);

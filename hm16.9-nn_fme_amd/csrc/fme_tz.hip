@@ -666,9 +666,7 @@ __device__ __forceinline__ void tz_wave(const TzArgs& ta, int jid, const fme_job
     out->mv_y = (int16_t)by;
     if (ta.sad) ta.sad[jid] = bsad - mv_cost(ml, mv_bits(bx, by, 2, j.mvp_x, j.mvp_y));
     if (ta.emi_mv) {   // the integer MV after the square step (rcMv of xTZSearch, TEncSearch.cpp:5037-5048)
-      // one agent-coherent 32-bit store: the chain launch (k_tz_flow) reads it on other XCDs
-      const uint32_t mv = (uint32_t)(uint16_t)s.bx | ((uint32_t)(uint16_t)s.by << 16);
-      __hip_atomic_store(reinterpret_cast<uint32_t*>(ta.emi_mv) + jid, mv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      reinterpret_cast<uint32_t*>(ta.emi_mv)[jid] = (uint32_t)(uint16_t)s.bx | ((uint32_t)(uint16_t)s.by << 16);
     }
     if (ring) {   // U1 V1 U2 H1 H2 U3 V2 U4 = array_e[index_ref .. +7], then C (Backups/4:4343-4359)
       uint32_t* o = ta.nn_in + (size_t)9 * jid;
@@ -744,73 +742,7 @@ __global__ __launch_bounds__(64 * FME_TZL_WAVES) void k_tz_level(TzArgs ta, TzCh
   else tz_wave<8, 8, FME_TZL_WAVES>(ta, q, j, PW, PH, px, py);
 }
 
-// The chain as one persistent launch (FME_TZ_FLOW): wave w searches jobs w, w + W, w + 2W, ... of
-// the level-ordered list, and a job whose m_integerMv2Nx2N comes from job ps first waits for ps's
-// completion word.  Progress: ps < q always, every wave takes its jobs in increasing order, and all
-// W waves are resident at once (W is sized to the chip at one wave per SIMD slot), so the smallest
-// unfinished job never waits.  Waits poll with relaxed agent-scope loads (no read-modify-write, so
-// no atomic traffic on the polled lines) and back off; a wait longer than `bound` ticks (seconds)
-// counts itself in abort[0] and every wave leaves, so a lost completion cannot hang the launch.
-__global__ __launch_bounds__(64) void k_tz_flow(TzArgs ta, TzChain ch, int32_t* done, int32_t* abort_w, int n, int W,
-                                                uint64_t bound) {
-  const int lane = (int)threadIdx.x;
-  for (int q = (int)blockIdx.x; q < n; q += W) {
-    const int ps = ch.psrc[q];
-    if (ps >= 0) {
-      const uint64_t t0 = wall_clock64();
-      int spins = 0;
-      while (__hip_atomic_load(done + ps, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) {
-        if ((++spins & 63) == 0) {
-          if (__hip_atomic_load(abort_w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) return;
-          if (wall_clock64() - t0 > bound) {
-            if (lane == 0) atomicAdd(abort_w, 1);
-            return;
-          }
-        }
-        __builtin_amdgcn_s_sleep(1);
-      }
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    }
-    const int PW = ta.a.jobs[q].w, PH = ta.a.jobs[q].h;   // shapes checked by the host
-    int px = ta.ext[q].pred2n_x, py = ta.ext[q].pred2n_y;
-    if (ps >= 0) {
-      const uint32_t mv =
-          __hip_atomic_load(reinterpret_cast<const uint32_t*>(ta.emi_mv) + ps, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      px = (int)(int16_t)(mv & 0xFFFFu);
-      py = (int)(int16_t)(mv >> 16);
-    }
-    const int kid = (PW % 8) ? 0 : ((PH % 8) ? 1 : 2);
-    const fme_job j = ta.a.jobs[q];
-    if (kid == 0) tz_wave<4, 8, 1>(ta, q, j, PW, PH, px, py);
-    else if (kid == 1) tz_wave<8, 4, 1>(ta, q, j, PW, PH, px, py);
-    else tz_wave<8, 8, 1>(ta, q, j, PW, PH, px, py);
-    // lane 0 wrote the job's post-square MV: its completion word after it (agent-scope release)
-    if (lane == 0) __hip_atomic_store(done + q, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-  }
-}
-
 }  // namespace
-
-hipError_t launch_tz_flow(const TzArgs& ta, const TzChain& ch, int32_t* done, int32_t* abort_w, int n, hipStream_t s) {
-  static int cus = 0;
-  if (!cus) {
-    int dev = 0;
-    (void)hipGetDevice(&dev);
-    cus = cu_count(dev);
-  }
-  // one-wave workgroups, 4 per CU (one per SIMD): all resident at once whatever the register use
-  const int W = std::min(n, 4 * cus);
-  int rate = 100000;   // kHz of s_memrealtime
-  {
-    int dev = 0;
-    (void)hipGetDevice(&dev);
-    int khz = 0;
-    if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev) == hipSuccess && khz > 0) rate = khz;
-  }
-  const uint64_t bound = (uint64_t)rate * 1000u * 4u;   // 4 s
-  hipLaunchKernelGGL(k_tz_flow, dim3(W), dim3(64), 0, s, ta, ch, done, abort_w, n, W, bound);
-  return hipGetLastError();
-}
 
 hipError_t launch_tz_levels(const TzArgs& ta, const TzChain& ch, const int32_t* h_lvl_off, hipStream_t s) {
   for (int lv = 0; lv < ch.nlev; lv++) {
