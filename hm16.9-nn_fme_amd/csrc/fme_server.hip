@@ -97,8 +97,8 @@ struct SrvLds {
   double ml;
   int32_t sel[2];               // half-stage best (hx, hy)
   uint32_t ans[2];              // the answer (SrvBox::res[1..2])
-  uint32_t mark[4];             // FracDIF checkpoints (ticks since the request read): first stage, half
-                                // distortions, half pick, quarter distortions
+  uint32_t mark[4];             // FracDIF checkpoints (ticks since the request read): payload in LDS,
+                                // first stage, half distortions, quarter distortions
 };
 
 // The 9 candidates of one xPatternRefinement stage: distortion per candidate into L.cost.
@@ -241,10 +241,10 @@ __device__ void serve_frac(SrvLds& L, SrvBox* box, uint64_t t_req) {
       }
   }
   __syncthreads();
-  mark(0);
+  mark(1);
   stage_dist(L, w, h, sad, true, 0, 0);
   __syncthreads();
-  mark(1);
+  mark(2);
   if (tid < 64) {
     int k;
     uint32_t best;
@@ -255,7 +255,6 @@ __device__ void serve_frac(SrvLds& L, SrvBox* box, uint64_t t_req) {
     }
   }
   __syncthreads();
-  mark(2);
   const int hx = L.sel[0], hy = L.sel[1];
   stage_dist(L, w, h, sad, false, 2 * hx, 2 * hy);
   __syncthreads();
@@ -413,6 +412,7 @@ __global__ __launch_bounds__(kSrvThreads) void k_server(SrvBox* box, const float
         L.ml = __builtin_bit_cast(double, lo | (hi << 32));
       }
       __syncthreads();
+      if (tid == 0) L.mark[0] = (uint32_t)(wall_clock64() - t_req);
     }
     const uint32_t seq = (uint32_t)L.ctl[1];
     if (L.ctl[2] == kSrvFrac)

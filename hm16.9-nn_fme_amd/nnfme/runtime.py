@@ -436,8 +436,8 @@ class FmeContext:
 
     def single_last_device_us(self, phases=False):
         """Device microseconds of the last single-PU call (the server's read of the request to its
-        answer); phases=True: also the FracDIF checkpoints (first stage, half distortions, half
-        pick, quarter distortions)."""
+        answer); phases=True: also the FracDIF checkpoints (payload in LDS, first stage, half
+        distortions, quarter distortions)."""
         us = np.zeros(5, np.float32)
         _check(self.lib, self.lib.fme_single_last_device_us(self.h, _ptr(us), 5))
         return us.tolist() if phases else float(us[0])

@@ -607,8 +607,9 @@ int fme_last_timings(fme_ctx* ctx, float* ms, int count);
 int fme_accumulated_timings(fme_ctx* ctx, double* ms, int count, int reset);
 /* The last fme_frac_dif_single / fme_nn_pred_single call as the resident server saw it, device
  * microseconds since it read the request: us[0] to the answer (the rest of the call's wall time
- * is the host, PCIe and polling); FracDIF only, us[1..4] to the first filter stage, the half
- * stage's distortions, its pick, the quarter stage's distortions.  count <= 5 values. */
+ * is the host, PCIe and polling); FracDIF only, us[1..4] to the payload (key and window) in LDS,
+ * the first filter stage, the half stage's distortions, the quarter stage's distortions.  count <= 5
+ * values. */
 int fme_single_last_device_us(fme_ctx* ctx, float* us, int count);
 
 #ifdef __cplusplus

@@ -40,7 +40,7 @@ def main():
             ph.append(p[1:])
         m = np.median(np.array(ph[1:]), axis=0)
         print(f"frac_dif {w}x{h}: wall {np.median(wall[1:]) * 1e6:.2f} us, device {np.median(dev[1:]):.2f} us "
-              f"(first stage {m[0]:.2f}, half dist {m[1]:.2f}, half pick {m[2]:.2f}, quarter dist {m[3]:.2f})", flush=True)
+              f"(payload {m[0]:.2f}, first stage {m[1]:.2f}, half dist {m[2]:.2f}, quarter dist {m[3]:.2f})", flush=True)
     wall, dev = [], []
     for i in range(calls):
         e = rng.integers(0, 5000, 8).astype(np.uint32)
