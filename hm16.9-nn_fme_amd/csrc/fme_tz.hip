@@ -308,7 +308,7 @@ __device__ __forceinline__ uint64_t block_min(uint64_t key) {
   }
 }
 
-template <int UW, int UH, int NW = 1, bool PF = false>
+template <int UW, int UH, int NW = 1>
 __device__ __forceinline__ void tz_wave(const TzArgs& ta, int jid, const fme_job& j, int PW, int PH, int pred_x,
                                         int pred_y) {
   const BatchArgs& a = ta.a;
@@ -396,50 +396,17 @@ __device__ __forceinline__ void tz_wave(const TzArgs& ta, int jid, const fme_job
     }
   };
   // (cost << 32 | call index) minimum of a list of n points, G at a time; pt(i, x, y) -> tested?
-  // PF (the chain levels, one job per wave on the critical path): the next chunk's point and
-  // window are loaded before the current chunk's distortion and minimum, so the load latency of
-  // a multi-chunk list overlaps the compute.  (pt may set list state from i, e.g. a ring's dist:
-  // the caller recomputes the winner's point after the list.)
   auto list_min = [&](int n, auto&& pt) FME_AI -> uint64_t {
     uint64_t best = ~0ull;
-    if constexpr (!PF) {
-      for (int base = 0; base < n; base += G) {
-        const int i = base + g;
-        int x = 0, y = 0;
-        const bool v = i < n && pt(i, x, y);
-        uint32_t dist;
-        const uint32_t c = cost_at(x, y, v, dist);
-        const uint64_t key = block_min<NW>(wave_min_from(((uint64_t)c << 32) | (uint32_t)i, L, 64));
-        best = key < best ? key : best;
-        push_min(dist, 64);
-      }
-    } else {
+    for (int base = 0; base < n; base += G) {
+      const int i = base + g;
       int x = 0, y = 0;
-      bool v = g < n && pt(g, x, y);
-      uint32_t w[UH][ND], s0 = 0;
-      if (v && real) load_window<UW, UH>(w, s0, ref, ox + x, oy + y, sub);
-      for (int base = 0; base < n; base += G) {
-        const int i = base + g;
-        int xn = 0, yn = 0;
-        bool vn = false;
-        uint32_t wn[UH][ND], s0n = 0;
-        if (base + G < n) {
-          vn = i + G < n && pt(i + G, xn, yn);
-          if (vn && real) load_window<UW, UH>(wn, s0n, ref, ox + xn, oy + yn, sub);
-        }
-        const uint32_t part = (v && real) ? unit_part<UW, UH>(w, s0, kk, sk2, kbuf, sad_metric, sub) : 0u;
-        const uint32_t d = group_sum(part, L);
-        const uint32_t dist = v ? d : 0xFFFFFFFFu;
-        const uint32_t c = v ? d + mv_cost(ml, mv_bits(x, y, 2, j.mvp_x, j.mvp_y)) : 0xFFFFFFFFu;
-        const uint64_t key = block_min<NW>(wave_min_from(((uint64_t)c << 32) | (uint32_t)i, L, 64));
-        best = key < best ? key : best;
-        push_min(dist, 64);
-        x = xn; y = yn; v = vn; s0 = s0n;
-#pragma unroll
-        for (int r = 0; r < UH; r++)
-#pragma unroll
-          for (int q = 0; q < ND; q++) w[r][q] = wn[r][q];
-      }
+      const bool v = i < n && pt(i, x, y);
+      uint32_t dist;
+      const uint32_t c = cost_at(x, y, v, dist);
+      const uint64_t key = block_min<NW>(wave_min_from(((uint64_t)c << 32) | (uint32_t)i, L, 64));
+      best = key < best ? key : best;
+      push_min(dist, 64);
     }
     return best;
   };
@@ -719,9 +686,6 @@ __constant__ int kTzH[kNumClasses] = {8, 4, 8, 16, 4, 16, 8, 16, 12, 16, 32, 8, 
 #ifndef FME_TZW_WAVES
 #define FME_TZW_WAVES 4
 #endif
-#ifndef FME_TZW_PREFETCH   // 1: the bulk search pipelines its candidate lists too (see list_min)
-#define FME_TZW_PREFETCH 0
-#endif
 // Work order: block b runs on XCD b % 8 (round-robin dispatch), and XCD x owns the x-th eighth of
 // every class of this kernel (a spatial band per L2), largest PU class first: the long searches
 // (a 64x64 PU's raster is hundreds of dependent candidate chunks) start at once instead of
@@ -750,7 +714,7 @@ void k_tz_wave(TzArgs ta, TzSchedule sc, int kid) {
   if (q < 0) return;
   const int jid = ta.perm[q];
   const fme_job j = ta.sjobs[q];
-  tz_wave<UW, UH, 1, FME_TZW_PREFETCH>(ta, jid, j, kTzW[c], kTzH[c], ta.ext[jid].pred2n_x, ta.ext[jid].pred2n_y);
+  tz_wave<UW, UH>(ta, jid, j, kTzW[c], kTzH[c], ta.ext[jid].pred2n_x, ta.ext[jid].pred2n_y);
 }
 
 // One dependency level of a producer's m_integerMv2Nx2N chain (fme_pred_inter_p/b): one wave per
@@ -758,9 +722,6 @@ void k_tz_wave(TzArgs ta, TzSchedule sc, int kid) {
 // post-EMI MVs of earlier levels from global memory (kernel boundaries order them) and no level
 // waits for the host.  ch.psrc[q] >= 0: job q's m_integerMv2Nx2N is job psrc[q]'s result; -1: its
 // ext already holds it.
-#ifndef FME_TZL_PREFETCH   // the chain levels pipeline their candidate lists (list_min)
-#define FME_TZL_PREFETCH 1
-#endif
 #ifndef FME_TZL_WAVES
 #define FME_TZL_WAVES 1   // waves per chain job (A/B: 8 waves 276 ms per P frame, spilling; 1 wave 198 ms)
 #endif
@@ -776,9 +737,9 @@ __global__ __launch_bounds__(64 * FME_TZL_WAVES) void k_tz_level(TzArgs ta, TzCh
   }
   const int kid = (PW % 8) ? 0 : ((PH % 8) ? 1 : 2);
   const fme_job j = ta.a.jobs[q];
-  if (kid == 0) tz_wave<4, 8, FME_TZL_WAVES, FME_TZL_PREFETCH>(ta, q, j, PW, PH, px, py);
-  else if (kid == 1) tz_wave<8, 4, FME_TZL_WAVES, FME_TZL_PREFETCH>(ta, q, j, PW, PH, px, py);
-  else tz_wave<8, 8, FME_TZL_WAVES, FME_TZL_PREFETCH>(ta, q, j, PW, PH, px, py);
+  if (kid == 0) tz_wave<4, 8, FME_TZL_WAVES>(ta, q, j, PW, PH, px, py);
+  else if (kid == 1) tz_wave<8, 4, FME_TZL_WAVES>(ta, q, j, PW, PH, px, py);
+  else tz_wave<8, 8, FME_TZL_WAVES>(ta, q, j, PW, PH, px, py);
 }
 
 }  // namespace
