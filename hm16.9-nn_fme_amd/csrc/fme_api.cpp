@@ -1121,16 +1121,31 @@ int fme_frac_dif_single(fme_ctx* c, int lossless, const int16_t* key, int key_st
   int rc = srv_open(c);
   if (rc) return rc;
   SrvBox* b = c->box;
-  const int pw = w + 8, ph = h + 8;
-  for (int y = 0; y < h; y++) std::memcpy(b->key + y * w, key + (ptrdiff_t)y * key_stride, (size_t)w * sizeof(int16_t));
+  const uint32_t seq = c->srv_done + 1;   // the call's sequence number (srv_call)
+  const int pw = w + 8, ph = h + 8, win_bytes = pw * ph, bytes = win_bytes + 2 * w * h;
+  // small PUs: window and key ride in the request blocks (kSrvTagged), 12 bytes per block
+  const bool tagged = bytes <= kSrvTagBytes;
+  alignas(16) uint8_t stream[kSrvTagBytes + 12];
+  uint8_t* wdst = tagged ? stream : b->win;
+  int16_t* kdst = tagged ? reinterpret_cast<int16_t*>(stream + win_bytes) : b->key;
+  for (int y = 0; y < h; y++) std::memcpy(kdst + y * w, key + (ptrdiff_t)y * key_stride, (size_t)w * sizeof(int16_t));
   for (int y = 0; y < ph; y++) {
     const int16_t* src = ref + (ptrdiff_t)(mv_int_y - 4 + y) * ref_stride + (mv_int_x - 4);
-    uint8_t* dst = b->win + y * pw;
+    uint8_t* dst = wdst + y * pw;
     for (int x = 0; x < pw; x++) dst[x] = (uint8_t)std::min(255, std::max(0, (int)src[x]));
   }
-  b->ml = motion_lambda;
-  b->req[0][1] = (uint32_t)kSrvFrac | ((lossless || !c->cfg.use_hadamard) ? 4u : 0u) | ((uint32_t)(w - 1) << 8) |
-                 ((uint32_t)(h - 1) << 16);
+  if (tagged)
+    for (int p = 0; 12 * p < bytes; p++) {
+      std::memcpy(&b->req[2 + p][1], stream + 12 * p, 12);
+      __atomic_store_n(&b->req[2 + p][0], seq, __ATOMIC_RELEASE);
+    }
+  uint32_t mlw[2];
+  std::memcpy(mlw, &motion_lambda, sizeof(mlw));
+  b->req[1][1] = mlw[0];
+  b->req[1][2] = mlw[1];
+  __atomic_store_n(&b->req[1][0], seq, __ATOMIC_RELEASE);
+  b->req[0][1] = (uint32_t)kSrvFrac | ((lossless || !c->cfg.use_hadamard) ? (uint32_t)kSrvSad : 0u) |
+                 (tagged ? (uint32_t)kSrvTagged : 0u) | ((uint32_t)(w - 1) << 8) | ((uint32_t)(h - 1) << 16);
   b->req[0][2] = (uint32_t)(uint16_t)px | ((uint32_t)(uint16_t)py << 16);
   rc = srv_call(c, false);
   if (rc) return rc;

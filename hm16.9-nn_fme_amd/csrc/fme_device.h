@@ -186,16 +186,22 @@ struct NnIn11 {   // NN_pred() inputs of a single call: array_e slots[8], C, PUH
 // pinned, device-mapped host memory, serves the call and stores the answer block `res`; `stopped` = the
 // epoch of an instance that exited (idle, lifetime or `stop`).  Request fields share the first
 // lines, the answer has its own, the payload follows.
-enum { kSrvNn = 1, kSrvFrac = 2 };
+enum { kSrvNn = 1, kSrvFrac = 2, kSrvSad = 4, kSrvTagged = 8 };
+constexpr int kSrvBlocks = 128;                       // request blocks, all read by every poll
+constexpr int kSrvTagBytes = 12 * (kSrvBlocks - 2);   // FracDIF payload that rides in the blocks
 struct SrvBox {
-  // host -> device, in 16-byte blocks that the server reads with one load each, so a block's fields
-  // are those written before its sequence word.  req[0]: seq (written last), shape = kind (bits
-  // 0-1) | SAD (bit 2: lossless or HADME off) | w - 1 (bits 8-15) | h - 1 (bits 16-23), the FracDIF
-  // predictor - 4 * integer MV (x low 16 bits, y high 16, quarter-pel), stop (set by the host to end
-  // the instance); req[1..4]: seq and three NN_pred inputs each (array_e[8], C, PUHeight, PUWidth),
-  // taken only when all four carry the seq.
-  alignas(64) uint32_t req[5][4];
-  double ml;                   // motion lambda (TComRdCost::m_motionLambda)
+  // host -> device, in 16-byte blocks that the polling wave reads all at once (two per lane, one
+  // load each), so a block's fields are those written before its sequence word.  req[0]: seq,
+  // shape = kind (bits 0-1) | kSrvSad (lossless or HADME off) | kSrvTagged | w - 1 (bits 8-15) |
+  // h - 1 (bits 16-23), the FracDIF predictor - 4 * integer MV (x low 16 bits, y high 16,
+  // quarter-pel), stop (set by the host to end the instance).  The rest carry this call's seq in
+  // word 0 and are taken only when every one the call uses does:
+  //   NN_pred: req[1..4], three inputs each (array_e[8], C, PUHeight, PUWidth);
+  //   FracDIF: req[1] = the motion lambda (TComRdCost::m_motionLambda, a double in words 1-2);
+  //   kSrvTagged: req[2..] = the window then the key, 12 bytes per block, when they fit in
+  //   kSrvTagBytes (the payload arrives with the request: no second round trip); otherwise they are
+  //   in key / win below, read after the request.
+  alignas(64) uint32_t req[kSrvBlocks][4];
   // device -> host, one 16-byte store: seq, FracDIF cost / NN class, FracDIF half x, y and quarter
   // x, y as int8 (bytes 0..3), the call's device ticks (request read to answer)
   alignas(64) uint32_t res[4];

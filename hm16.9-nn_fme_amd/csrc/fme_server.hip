@@ -31,8 +31,18 @@ __device__ __forceinline__ int luma_tap(int f, int t) {
   return f == 0 ? T[0][t] : (f == 1 ? T[1][t] : (f == 2 ? T[2][t] : T[3][t]));
 }
 // xPatternRefinement's candidate orders (TEncSearch.cpp:1591-1645 over s_acMvRefineH / Q)
-__constant__ int8_t kSrvRefH[9][2] = {{0, 0}, {0, -1}, {0, 1}, {-1, 0}, {1, 0}, {-1, -1}, {1, -1}, {-1, 1}, {1, 1}};
-__constant__ int8_t kSrvRefQ[9][2] = {{0, 0}, {0, -1}, {0, 1}, {-1, -1}, {1, -1}, {-1, 0}, {1, 0}, {-1, 1}, {1, 1}};
+// packed as 2-bit (offset + 1) fields so that candidate k's offset is a shift of an immediate,
+// not a constant-memory load in the candidate loop
+constexpr int8_t kSrvRefH[9][2] = {{0, 0}, {0, -1}, {0, 1}, {-1, 0}, {1, 0}, {-1, -1}, {1, -1}, {-1, 1}, {1, 1}};
+constexpr int8_t kSrvRefQ[9][2] = {{0, 0}, {0, -1}, {0, 1}, {-1, -1}, {1, -1}, {-1, 0}, {1, 0}, {-1, 1}, {1, 1}};
+constexpr uint32_t pack_ref(const int8_t (&t)[9][2], int c) {
+  uint32_t v = 0;
+  for (int k = 0; k < 9; k++) v |= (uint32_t)(t[k][c] + 1) << (2 * k);
+  return v;
+}
+constexpr uint32_t kRefHx = pack_ref(kSrvRefH, 0), kRefHy = pack_ref(kSrvRefH, 1);
+constexpr uint32_t kRefQx = pack_ref(kSrvRefQ, 0), kRefQy = pack_ref(kSrvRefQ, 1);
+__device__ __forceinline__ int ref_of(uint32_t packed, int k) { return (int)((packed >> (2 * k)) & 3u) - 1; }
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 // 16 bytes of host memory in one request, past the caches
@@ -41,11 +51,13 @@ __device__ __forceinline__ u32x4 load_block(const uint32_t* p) {
   asm volatile("global_load_dwordx4 %0, %1, off sc0 sc1\n\ts_waitcnt vmcnt(0)" : "=v"(v) : "v"(p) : "memory");
   return v;
 }
+// two such blocks, both requests in flight before the wait
+__device__ __forceinline__ void load_pair(const uint32_t* p, const uint32_t* q, u32x4& a, u32x4& b) {
+  asm volatile("global_load_dwordx4 %0, %2, off sc0 sc1\n\tglobal_load_dwordx4 %1, %3, off sc0 sc1\n\ts_waitcnt vmcnt(0)"
+               : "=&v"(a), "=&v"(b) : "v"(p), "v"(q) : "memory");
+}
 __device__ __forceinline__ void store_block(uint32_t* p, u32x4 v) {
   asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1" : : "v"(p), "v"(v) : "memory");
-}
-__device__ __forceinline__ uint32_t sys_load(const uint32_t* p) {
-  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 __device__ __forceinline__ void sys_store_release(uint32_t* p, uint32_t v) {
   __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -92,7 +104,7 @@ struct SrvLds {
   int16_t hp[3][72 * 65];       // first filter stage, fractional phase 1..3, columns -1 .. w-1
   alignas(16) uint8_t win[72 * 72 + 16];
   uint32_t cost[2][16];           // per candidate: half stage, quarter stage
-  int32_t ctl[8];               // stop, seq, kind, w, h, mvp_x, mvp_y, sad
+  int32_t ctl[9];               // stop, seq, kind, w, h, mvp_x, mvp_y, sad, tagged
   uint32_t nn_in[12];
   double ml;
   int32_t sel[2];               // half-stage best (hx, hy)
@@ -101,12 +113,84 @@ struct SrvLds {
                                 // first stage, half distortions, quarter distortions
 };
 
+// Distortion of block group b of the PU at quarter-pel offset (ox, oy) from the integer MV (wave-
+// uniform), lanes = the group's pixels: 8x8 SATD, four 4x4 SATDs or SAD, summed over the wave.
+template <bool SAD, bool B8>
+__device__ __forceinline__ uint32_t item_dist(const SrvLds& L, int w, int nb4, int b, int ox, int oy, int lane) {
+  const int bw8 = w >> 3, bw4 = w >> 2;
+  int c, r;
+  bool valid = true;
+  if constexpr (B8) {
+    const int by = b / bw8;
+    c = (b - by * bw8) * 8 + (lane & 7);
+    r = by * 8 + (lane >> 3);
+  } else {
+    int blk = b * 4 + (lane >> 4);
+    valid = blk < nb4;
+    blk = valid ? blk : 0;
+    const int by = blk / bw4;
+    c = (blk - by * bw4) * 4 + (lane & 3);
+    r = by * 4 + ((lane >> 2) & 3);
+  }
+  // the candidate's phases are wave-uniform: scalar branches, taps as immediates
+  const int ix = __builtin_amdgcn_readfirstlane(ox >> 2), fx = __builtin_amdgcn_readfirstlane(ox & 3);
+  const int iy = __builtin_amdgcn_readfirstlane(oy >> 2), fy = __builtin_amdgcn_readfirstlane(oy & 3);
+  const int x = c + ix, wy0 = r + iy + 4;
+  // first-stage samples at window rows wy0 - 3 .. wy0 + 4: the 14-bit values m_filteredBlockTmp
+  // holds (filterHor with isLast false; filterCopy's isFirst branch for fraction 0)
+  int hs[8];
+  if (fx == 0) {
+#pragma unroll
+    for (int t = 0; t < 8; t++) hs[t] = ((int)L.win[(wy0 + t - 3) * (w + 8) + x + 4] << 6) - 8192;
+  } else {
+    const int16_t* hp = L.hp[fx - 1] + x + 1;
+#pragma unroll
+    for (int t = 0; t < 8; t++) hs[t] = hp[(wy0 + t - 3) * (w + 1)];
+  }
+  int v;
+  if (fy == 0) {
+    v = (hs[3] + 8192 + 32) >> 6;                        // filterCopy, !isFirst isLast
+  } else {
+    int s = 0;
+#pragma unroll
+    for (int t = 0; t < 8; t++) s += luma_tap(fy, t) * hs[t];
+    v = (s + 2048 + (8192 << 6)) >> 12;                  // filter<8, true, false, true>
+  }
+  v = min(255, max(0, v));
+  int d = valid ? (int)L.key[r * w + c] - v : 0;
+  uint32_t add;
+  if constexpr (SAD) {
+    uint32_t a = (uint32_t)abs(d);
+    a = xsum<32>(xsum<16>(xsum<8>(xsum<4>(xsum<2>(xsum<1>(a, lane), lane), lane), lane), lane), lane);
+    add = a;
+  } else if constexpr (B8) {   // 8x8 Walsh-Hadamard across the lanes, sum |coef|, (s + 2) >> 2 (xCalcHADs8x8)
+    d = bfly<32>(bfly<16>(bfly<8>(bfly<4>(bfly<2>(bfly<1>(d, lane), lane), lane), lane), lane), lane);
+    uint32_t a = (uint32_t)abs(d);
+    a = xsum<32>(xsum<16>(xsum<8>(xsum<4>(xsum<2>(xsum<1>(a, lane), lane), lane), lane), lane), lane);
+    add = (a + 2) >> 2;
+  } else {           // four 4x4 blocks per wave, each (s + 1) >> 1 (xCalcHADs4x4)
+    d = bfly<8>(bfly<4>(bfly<2>(bfly<1>(d, lane), lane), lane), lane);
+    uint32_t a = (uint32_t)abs(d);
+    a = xsum<8>(xsum<4>(xsum<2>(xsum<1>(a, lane), lane), lane), lane);
+    a = valid ? (a + 1) >> 1 : 0u;
+    add = xsum<32>(xsum<16>(a, lane), lane);   // the four blocks' (rounded) sums
+  }
+  return add;
+}
+
 // The 9 candidates of one xPatternRefinement stage: distortion per candidate into L.cost.
 // (ox, oy) of candidate k = base + 2 * ref (half) or base + ref (quarter), quarter-pel offsets from
 // the integer MV.  Work item (candidate, block) per wave; lanes are the block's pixels.
-__device__ void stage_dist(SrvLds& L, int w, int h, bool sad, bool half, int bx0, int by0) {
+// SAD: lossless or HADME off; B8: xGetHADs' 8x8 transform (both dimensions multiples of 8).
+template <bool SAD, bool B8>
+#ifdef FME_SRV_NOINL
+__device__ __noinline__
+#else
+__device__
+#endif
+void stage_dist(SrvLds& L, int w, int h, bool half, int bx0, int by0) {
   const int lane = (int)threadIdx.x & 63, wid = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
-  const bool b8 = !sad && (w & 7) == 0 && (h & 7) == 0;   // xGetHADs: 8x8 when both dims allow
+  constexpr bool b8 = B8;
   const int nb4 = (w >> 2) * (h >> 2);
   const int nb = b8 ? (w >> 3) * (h >> 3) : (nb4 + 3) >> 2;
   // each wave takes a contiguous run of the (candidate-major) items and adds its partial sums to
@@ -115,7 +199,6 @@ __device__ void stage_dist(SrvLds& L, int w, int h, bool sad, bool half, int bx0
   const int n_items = 9 * nb, per = (n_items + NWV - 1) / NWV;
   const int i0 = wid * per, i1 = min(n_items, i0 + per);
   uint32_t acc = 0;
-  const int bw8 = w >> 3, bw4 = w >> 2;
   int k = i0 < i1 ? i0 / nb : 0, b = i0 - k * nb;   // (candidate, block) of the run's first item
   int kcur = k;
   for (int item = i0; item < i1; item++, b++) {
@@ -128,66 +211,9 @@ __device__ void stage_dist(SrvLds& L, int w, int h, bool sad, bool half, int bx0
       acc = 0;
       kcur = k;
     }
-    const int ox = bx0 + (half ? 2 * kSrvRefH[k][0] : kSrvRefQ[k][0]);
-    const int oy = by0 + (half ? 2 * kSrvRefH[k][1] : kSrvRefQ[k][1]);
-    int c, r;
-    bool valid = true;
-    if (b8) {
-      const int by = b / bw8;
-      c = (b - by * bw8) * 8 + (lane & 7);
-      r = by * 8 + (lane >> 3);
-    } else {
-      int blk = b * 4 + (lane >> 4);
-      valid = blk < nb4;
-      blk = valid ? blk : 0;
-      const int by = blk / bw4;
-      c = (blk - by * bw4) * 4 + (lane & 3);
-      r = by * 4 + ((lane >> 2) & 3);
-    }
-    // the candidate's phases are wave-uniform: scalar branches, taps as immediates
-    const int ix = __builtin_amdgcn_readfirstlane(ox >> 2), fx = __builtin_amdgcn_readfirstlane(ox & 3);
-    const int iy = __builtin_amdgcn_readfirstlane(oy >> 2), fy = __builtin_amdgcn_readfirstlane(oy & 3);
-    const int x = c + ix, wy0 = r + iy + 4;
-    // first-stage samples at window rows wy0 - 3 .. wy0 + 4: the 14-bit values m_filteredBlockTmp
-    // holds (filterHor with isLast false; filterCopy's isFirst branch for fraction 0)
-    int hs[8];
-    if (fx == 0) {
-#pragma unroll
-      for (int t = 0; t < 8; t++) hs[t] = ((int)L.win[(wy0 + t - 3) * (w + 8) + x + 4] << 6) - 8192;
-    } else {
-      const int16_t* hp = L.hp[fx - 1] + x + 1;
-#pragma unroll
-      for (int t = 0; t < 8; t++) hs[t] = hp[(wy0 + t - 3) * (w + 1)];
-    }
-    int v;
-    if (fy == 0) {
-      v = (hs[3] + 8192 + 32) >> 6;                        // filterCopy, !isFirst isLast
-    } else {
-      int s = 0;
-#pragma unroll
-      for (int t = 0; t < 8; t++) s += luma_tap(fy, t) * hs[t];
-      v = (s + 2048 + (8192 << 6)) >> 12;                  // filter<8, true, false, true>
-    }
-    v = min(255, max(0, v));
-    int d = valid ? (int)L.key[r * w + c] - v : 0;
-    uint32_t add;
-    if (sad) {
-      uint32_t a = (uint32_t)abs(d);
-      a = xsum<32>(xsum<16>(xsum<8>(xsum<4>(xsum<2>(xsum<1>(a, lane), lane), lane), lane), lane), lane);
-      add = a;
-    } else if (b8) {   // 8x8 Walsh-Hadamard across the lanes, sum |coef|, (s + 2) >> 2 (xCalcHADs8x8)
-      d = bfly<32>(bfly<16>(bfly<8>(bfly<4>(bfly<2>(bfly<1>(d, lane), lane), lane), lane), lane), lane);
-      uint32_t a = (uint32_t)abs(d);
-      a = xsum<32>(xsum<16>(xsum<8>(xsum<4>(xsum<2>(xsum<1>(a, lane), lane), lane), lane), lane), lane);
-      add = (a + 2) >> 2;
-    } else {           // four 4x4 blocks per wave, each (s + 1) >> 1 (xCalcHADs4x4)
-      d = bfly<8>(bfly<4>(bfly<2>(bfly<1>(d, lane), lane), lane), lane);
-      uint32_t a = (uint32_t)abs(d);
-      a = xsum<8>(xsum<4>(xsum<2>(xsum<1>(a, lane), lane), lane), lane);
-      a = valid ? (a + 1) >> 1 : 0u;
-      add = xsum<32>(xsum<16>(a, lane), lane);   // the four blocks' (rounded) sums
-    }
-    acc += add;
+    const int ox = bx0 + (half ? 2 * ref_of(kRefHx, k) : ref_of(kRefQx, k));
+    const int oy = by0 + (half ? 2 * ref_of(kRefHy, k) : ref_of(kRefQy, k));
+    acc += item_dist<SAD, B8>(L, w, nb4, b, ox, oy, lane);
   }
   if (i0 < i1 && lane == 0) atomicAdd(&L.cost[half ? 0 : 1][kcur], acc);
 }
@@ -200,21 +226,22 @@ __device__ void stage_pick(const SrvLds& L, bool half, int hx, int hy, int& best
   if (lane < 9) {
     // getCostOfVectorWithPredictor at cost scale 1 (half) / 0 (quarter), MV relative to the
     // integer MV (the predictor came shifted by 4 * mv_int)
-    const int mx = half ? 2 * kSrvRefH[lane][0] : 2 * hx + kSrvRefQ[lane][0];
-    const int my = half ? 2 * kSrvRefH[lane][1] : 2 * hy + kSrvRefQ[lane][1];
+    const int mx = half ? 2 * ref_of(kRefHx, lane) : 2 * hx + ref_of(kRefQx, lane);
+    const int my = half ? 2 * ref_of(kRefHy, lane) : 2 * hy + ref_of(kRefQy, lane);
     const uint32_t bits = eg_bits_d(mx - px) + eg_bits_d(my - py);
     tot = L.cost[half ? 0 : 1][lane] + (uint32_t)((L.ml * (double)bits) / 65536.0);
   }
   int k = lane < 9 ? lane : 64;
-#pragma unroll
-  for (int m = 1; m < 16; m <<= 1) {
-    const uint32_t ot = (uint32_t)__shfl_xor((int)tot, m, 64);
-    const int ok = __shfl_xor(k, m, 64);
+  auto step = [&](uint32_t ot, int ok) {
     if (ot < tot || (ot == tot && ok < k)) {
       tot = ot;
       k = ok;
     }
-  }
+  };
+  step((uint32_t)xor_lane<1>((int)tot, lane), xor_lane<1>(k, lane));
+  step((uint32_t)xor_lane<2>((int)tot, lane), xor_lane<2>(k, lane));
+  step((uint32_t)xor_lane<4>((int)tot, lane), xor_lane<4>(k, lane));
+  step((uint32_t)xor_lane<8>((int)tot, lane), xor_lane<8>(k, lane));
   best_k = k;
   best = tot;
 }
@@ -222,18 +249,35 @@ __device__ void stage_pick(const SrvLds& L, bool half, int hx, int hy, int& best
 __device__ void serve_frac(SrvLds& L, SrvBox* box, uint64_t t_req) {
   const int tid = (int)threadIdx.x;
   auto mark = [&](int m) {
+#ifndef FME_SRV_NOMARKS
     if (tid == 0) L.mark[m] = (uint32_t)(wall_clock64() - t_req);
+#endif
   };
   const int w = L.ctl[3], h = L.ctl[4];
   const bool sad = L.ctl[7] != 0;
   const int pw = w + 8, ph = h + 8;
   // first filter stage of phases 1..3 over window rows 0 .. h+7, PU columns -1 .. w-1
-  {   // thread (xr, rr): column xr - 1 of rows rr, rr + 8, ... of the three phases' planes
-    const int cols = w + 1, xr = tid & 127;
+  const int cols = w + 1, plane = ph * cols, span = (plane + 63) & ~63;
+  if (3 * span <= 4 * kSrvThreads) {
+    // up to 32x32: one output per work item, each phase's plane starting on a wave boundary (the
+    // phase is uniform)
+    for (int i = tid; i < 3 * span; i += kSrvThreads) {
+      const int f = __builtin_amdgcn_readfirstlane(i) / span, j = i - f * span;
+      if (j < plane) {
+        const int wy = j / cols, xr = j - wy * cols;
+        const uint8_t* row = L.win + wy * pw + xr;   // taps at window columns x + 4 - 3 ...
+        int s = 0;
+#pragma unroll
+        for (int t = 0; t < 8; t++) s += luma_tap(f + 1, t) * (int)row[t];
+        L.hp[f][j] = (int16_t)(s - 8192);
+      }
+    }
+  } else {   // thread (xr, rr): column xr - 1 of rows rr, rr + 8, ... of the three phases' planes
+    const int xr = tid & 127;
     if (xr < cols)
       for (int R = tid >> 7; R < 3 * ph; R += kSrvThreads >> 7) {
         const int f = R >= 2 * ph ? 2 : (R >= ph ? 1 : 0), wy = R - f * ph;
-        const uint8_t* row = L.win + wy * pw + xr;   // taps at window columns x + 4 - 3 ...
+        const uint8_t* row = L.win + wy * pw + xr;
         int s = 0;
 #pragma unroll
         for (int t = 0; t < 8; t++) s += luma_tap(f + 1, t) * (int)row[t];
@@ -242,7 +286,16 @@ __device__ void serve_frac(SrvLds& L, SrvBox* box, uint64_t t_req) {
   }
   __syncthreads();
   mark(1);
-  stage_dist(L, w, h, sad, true, 0, 0);
+  // one stage's distortions, specialised on the transform
+  auto dist = [&](bool half, int bx0, int by0) {
+    if (sad)
+      stage_dist<true, false>(L, w, h, half, bx0, by0);
+    else if ((w & 7) == 0 && (h & 7) == 0)
+      stage_dist<false, true>(L, w, h, half, bx0, by0);
+    else
+      stage_dist<false, false>(L, w, h, half, bx0, by0);
+  };
+  dist(true, 0, 0);
   __syncthreads();
   mark(2);
   if (tid < 64) {
@@ -250,13 +303,13 @@ __device__ void serve_frac(SrvLds& L, SrvBox* box, uint64_t t_req) {
     uint32_t best;
     stage_pick(L, true, 0, 0, k, best);
     if (tid == 0) {
-      L.sel[0] = kSrvRefH[k][0];
-      L.sel[1] = kSrvRefH[k][1];
+      L.sel[0] = ref_of(kRefHx, k);
+      L.sel[1] = ref_of(kRefHy, k);
     }
   }
   __syncthreads();
   const int hx = L.sel[0], hy = L.sel[1];
-  stage_dist(L, w, h, sad, false, 2 * hx, 2 * hy);
+  dist(false, 2 * hx, 2 * hy);
   __syncthreads();
   mark(3);
   if (tid < 64) {
@@ -265,8 +318,8 @@ __device__ void serve_frac(SrvLds& L, SrvBox* box, uint64_t t_req) {
     stage_pick(L, false, hx, hy, k, best);
     if (tid == 0) {
       L.ans[0] = best;
-      L.ans[1] = (uint32_t)(uint8_t)hx | ((uint32_t)(uint8_t)hy << 8) | ((uint32_t)(uint8_t)kSrvRefQ[k][0] << 16) |
-                 ((uint32_t)(uint8_t)kSrvRefQ[k][1] << 24);
+      L.ans[1] = (uint32_t)(uint8_t)hx | ((uint32_t)(uint8_t)hy << 8) | ((uint32_t)(uint8_t)ref_of(kRefQx, k) << 16) |
+                 ((uint32_t)(uint8_t)ref_of(kRefQy, k) << 24);
     }
   }
 }
@@ -331,15 +384,19 @@ __device__ void serve_nn(SrvLds& L, SrvBox* box) {
       bi = 2 * rp + 1;
     }
   }
-#pragma unroll
-  for (int off = 1; off < 64; off <<= 1) {
-    const float ov = __shfl_xor(bv, off, 64);
-    const int oi = __shfl_xor(bi, off, 64);
+  // rows live in lanes 0..24: an xor reduction over 32 lanes (DPP and permlane16, no LDS pipe)
+  auto step = [&](float ov, int oi) {
     if (ov > bv || (ov == bv && oi < bi)) {
       bv = ov;
       bi = oi;
     }
-  }
+  };
+  auto xf = [&](auto m, float v) { return __builtin_bit_cast(float, xor_lane<decltype(m)::value>(__builtin_bit_cast(int, v), rp)); };
+  step(xf(std::integral_constant<int, 1>{}, bv), xor_lane<1>(bi, rp));
+  step(xf(std::integral_constant<int, 2>{}, bv), xor_lane<2>(bi, rp));
+  step(xf(std::integral_constant<int, 4>{}, bv), xor_lane<4>(bi, rp));
+  step(xf(std::integral_constant<int, 8>{}, bv), xor_lane<8>(bi, rp));
+  step(xf(std::integral_constant<int, 16>{}, bv), xor_lane<16>(bi, rp));
   if (rp == 0) {
     L.ans[0] = (uint32_t)bi;
     L.ans[1] = 0;
@@ -355,17 +412,22 @@ __global__ __launch_bounds__(kSrvThreads) void k_server(SrvBox* box, const float
   const uint64_t t0 = wall_clock64();
   uint64_t last = t0;
   for (;;) {
-    if (tid < 64) {   // wave 0 polls: lanes 0..4 read the five request blocks
+    if (tid < 64) {   // wave 0 polls: lane l reads request blocks l and l + 64
       const int lane = tid;
-      uint32_t seq = served, stop = 0;
-      u32x4 hd = {0u, 0u, 0u, 0u};
+      uint32_t seq = served, stop = 0, shape = 0;
+      int need = 0;
+      u32x4 hd, hb;
       for (;;) {
-        if (lane < 5) hd = load_block(box->req[lane]);
+        load_pair(box->req[lane], box->req[lane + 64], hd, hb);
         seq = (uint32_t)__builtin_amdgcn_readfirstlane((int)hd.x);
         if (seq != served) {
-          const uint32_t kind = (uint32_t)__builtin_amdgcn_readfirstlane((int)hd.y) & 3u;
-          // an NN call's inputs ride in blocks 1..4: all of them must be this call's
-          if (kind != kSrvNn || __ballot(lane >= 1 && lane < 5 && hd.x != seq) == 0) break;
+          shape = (uint32_t)__builtin_amdgcn_readfirstlane((int)hd.y);
+          need = 4;   // blocks 1..need must all be this call's
+          if ((shape & 3u) == kSrvFrac) {
+            const int w = (int)((shape >> 8) & 0xFFu) + 1, h = (int)((shape >> 16) & 0xFFu) + 1;
+            need = (shape & kSrvTagged) ? 1 + ((w + 8) * (h + 8) + 2 * w * h + 11) / 12 : 1;
+          }
+          if (__ballot((lane >= 1 && lane <= need && hd.x != seq) || (lane + 64 <= need && hb.x != seq)) == 0) break;
           continue;
         }
         stop = (uint32_t)__builtin_amdgcn_readfirstlane((int)hd.w);   // the host's stop word rides in req[0]
@@ -380,45 +442,73 @@ __global__ __launch_bounds__(kSrvThreads) void k_server(SrvBox* box, const float
       if (lane == 0) {
         L.ctl[0] = (int32_t)stop;
         L.ctl[1] = (int32_t)seq;
-        L.ctl[2] = (int32_t)(hd.y & 3u);                 // kind
-        L.ctl[7] = (int32_t)((hd.y >> 2) & 1u);          // sad
-        L.ctl[3] = (int32_t)((hd.y >> 8) & 0xFFu) + 1;   // w
-        L.ctl[4] = (int32_t)((hd.y >> 16) & 0xFFu) + 1;  // h
-        L.ctl[5] = (int32_t)(int16_t)(hd.z & 0xFFFFu);   // mvp_x - 4 * mv_int_x
+        L.ctl[2] = (int32_t)(shape & 3u);                 // kind
+        L.ctl[7] = (shape & kSrvSad) ? 1 : 0;
+        L.ctl[8] = (shape & kSrvTagged) ? 1 : 0;
+        L.ctl[3] = (int32_t)((shape >> 8) & 0xFFu) + 1;   // w
+        L.ctl[4] = (int32_t)((shape >> 16) & 0xFFu) + 1;  // h
+        L.ctl[5] = (int32_t)(int16_t)(hd.z & 0xFFFFu);    // mvp_x - 4 * mv_int_x
         L.ctl[6] = (int32_t)(int16_t)(hd.z >> 16);
-      } else if (lane < 5) {
-        L.nn_in[3 * (lane - 1)] = hd.y;
-        L.nn_in[3 * (lane - 1) + 1] = hd.z;
-        L.nn_in[3 * (lane - 1) + 2] = hd.w;
+      }
+      if (!stop && (shape & 3u) == kSrvNn) {
+        if (lane >= 1 && lane < 5) {
+          L.nn_in[3 * (lane - 1)] = hd.y;
+          L.nn_in[3 * (lane - 1) + 1] = hd.z;
+          L.nn_in[3 * (lane - 1) + 2] = hd.w;
+        }
+      } else if (!stop) {
+        if (lane < 32) (&L.cost[0][0])[lane] = 0;
+        if (lane == 1) L.ml = __builtin_bit_cast(double, (uint64_t)hd.y | ((uint64_t)hd.z << 32));
+        if (shape & kSrvTagged) {   // the payload words of blocks 2..need: window, then key
+          const int w = (int)((shape >> 8) & 0xFFu) + 1, h = (int)((shape >> 16) & 0xFFu) + 1;
+          const int winw = (w + 8) * (h + 8) / 4, totw = winw + w * h / 2;
+          uint32_t* wd = reinterpret_cast<uint32_t*>(L.win);
+          uint32_t* kd = reinterpret_cast<uint32_t*>(L.key);
+          auto put = [&](int blk, const u32x4& v) {
+            if (blk < 2 || blk > need) return;
+            const uint32_t x[3] = {v.y, v.z, v.w};
+#pragma unroll
+            for (int k = 0; k < 3; k++) {
+              const int q = 3 * (blk - 2) + k;
+              if (q < winw) wd[q] = x[k];
+              else if (q < totw) kd[q - winw] = x[k];
+            }
+          };
+          put(lane, hd);
+          put(lane + 64, hb);
+        }
       }
     }
     __syncthreads();
     if (L.ctl[0]) break;
     const uint64_t t_req = wall_clock64();
-    if (L.ctl[2] == kSrvFrac) {   // the window and key, every thread at once (one round trip)
+    if (L.ctl[2] == kSrvFrac) {
       const int w = L.ctl[3], h = L.ctl[4];
-      // 16-byte system-coherent loads: straight from host memory, no cache to invalidate first,
-      // one request per block (the window's last block may read into the padding after it)
-      const uint32_t* wsrc = reinterpret_cast<const uint32_t*>(box->win);
-      u32x4* wdst = reinterpret_cast<u32x4*>(L.win);
-      for (int i = tid; i < ((w + 8) * (h + 8) + 15) >> 4; i += kSrvThreads) wdst[i] = load_block(wsrc + 4 * i);
-      const uint32_t* ksrc = reinterpret_cast<const uint32_t*>(box->key);
-      u32x4* kdst = reinterpret_cast<u32x4*>(L.key);
-      for (int i = tid; i < (w * h) >> 3; i += kSrvThreads) kdst[i] = load_block(ksrc + 4 * i);
-      if (tid < 32) (&L.cost[0][0])[tid] = 0;
-      if (tid == 64) {
-        const uint32_t* m = reinterpret_cast<const uint32_t*>(&box->ml);
-        const uint64_t lo = sys_load(m), hi = sys_load(m + 1);
-        L.ml = __builtin_bit_cast(double, lo | (hi << 32));
+      if (L.ctl[8] == 0) {   // not tagged: the window and key, every thread at once (one round trip)
+        // 16-byte system-coherent loads: straight from host memory, no cache to invalidate first,
+        // one request per block (the window's last block may read into the padding after it)
+        const uint32_t* wsrc = reinterpret_cast<const uint32_t*>(box->win);
+        u32x4* wdst = reinterpret_cast<u32x4*>(L.win);
+        for (int i = tid; i < ((w + 8) * (h + 8) + 15) >> 4; i += kSrvThreads) wdst[i] = load_block(wsrc + 4 * i);
+        const uint32_t* ksrc = reinterpret_cast<const uint32_t*>(box->key);
+        u32x4* kdst = reinterpret_cast<u32x4*>(L.key);
+        for (int i = tid; i < (w * h) >> 3; i += kSrvThreads) kdst[i] = load_block(ksrc + 4 * i);
+        __syncthreads();
       }
-      __syncthreads();
       if (tid == 0) L.mark[0] = (uint32_t)(wall_clock64() - t_req);
     }
     const uint32_t seq = (uint32_t)L.ctl[1];
-    if (L.ctl[2] == kSrvFrac)
+    if (L.ctl[2] == kSrvFrac) {
       serve_frac(L, box, t_req);
-    else
+    } else {   // marks: shader-clock cycles and wall ticks of the net itself
+      const uint64_t c0 = clock64(), w0 = wall_clock64();
       serve_nn(L, box);
+      if (tid == 0) {
+        L.mark[0] = (uint32_t)(clock64() - c0);
+        L.mark[1] = (uint32_t)(wall_clock64() - w0);
+        L.mark[2] = L.mark[3] = 0;
+      }
+    }
     __syncthreads();
     if (tid == 0) {   // the answer and its sequence word in one 16-byte store, past the caches
       const u32x4 m = {L.mark[0], L.mark[1], L.mark[2], L.mark[3]};

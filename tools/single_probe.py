@@ -41,14 +41,20 @@ def main():
         m = np.median(np.array(ph[1:]), axis=0)
         print(f"frac_dif {w}x{h}: wall {np.median(wall[1:]) * 1e6:.2f} us, device {np.median(dev[1:]):.2f} us "
               f"(payload {m[0]:.2f}, first stage {m[1]:.2f}, half dist {m[2]:.2f}, quarter dist {m[3]:.2f})", flush=True)
-    wall, dev = [], []
+    wall, dev, net = [], [], []
     for i in range(calls):
         e = rng.integers(0, 5000, 8).astype(np.uint32)
         t0 = time.perf_counter()
         ctx.nn_pred_single(e, int(rng.integers(0, 5000)), 8, 8)
         wall.append(time.perf_counter() - t0)
-        dev.append(ctx.single_last_device_us())
-    print(f"nn_pred: wall {np.median(wall[1:]) * 1e6:.2f} us, device {np.median(dev[1:]):.2f} us", flush=True)
+        p = ctx.single_last_device_us(phases=True)
+        dev.append(p[0])
+        net.append(p[1:3])
+    # the NN marks: shader-clock cycles of the net (reported through the 100 MHz wall scale) and
+    # its wall time, so their ratio is the shader clock while the server runs
+    cyc, nus = np.median(np.array(net[1:]), axis=0)
+    print(f"nn_pred: wall {np.median(wall[1:]) * 1e6:.2f} us, device {np.median(dev[1:]):.2f} us, "
+          f"net {nus:.2f} us = {cyc * 100:.0f} shader cycles ({cyc * 100 / max(nus, 1e-3):.0f} MHz)", flush=True)
 
 
 if __name__ == "__main__":
