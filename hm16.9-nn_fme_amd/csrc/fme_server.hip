@@ -324,80 +324,81 @@ __device__ void serve_frac(SrvLds& L, SrvBox* box, uint64_t t_req) {
   }
 }
 
-// NN_pred (TEncSearch.cpp:85-134) on the packed layout in LDS, in wave 0 alone: lane rp owns row
-// pair rp of each layer, every row summed in k order without contraction (the batch tail's
-// arithmetic), and a layer's outputs reach every lane as scalars (readlane) instead of through
-// LDS and a workgroup barrier.
+// NN_pred (TEncSearch.cpp:85-134) on the packed layout in LDS, in wave 0 alone: lane r owns row r
+// of each layer (22, 20 and 49 rows), every row summed in k order without contraction (the batch
+// tail's arithmetic, one row at a time instead of row pairs), and a layer's outputs reach every lane
+// as scalars (readlane) instead of through LDS and a workgroup barrier.  Every weight a lane needs is
+// read from LDS before the first layer starts, so the dependent chains never wait on LDS, and the
+// nine input normalisations (a float division each) run once, one per lane, then broadcast.
 __device__ __forceinline__ float lane_f(float v, int l) {
   return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), l));
 }
+// element (row r, k) of a packed [row pairs][K][2] matrix
+__device__ __forceinline__ int pk_at(int base, int K, int r, int k) { return base + ((r >> 1) * K + k) * 2 + (r & 1); }
+__device__ __forceinline__ float relu1(float s) { return s < 0.0f ? 0.0f : s; }
 __device__ void serve_nn(SrvLds& L, SrvBox* box) {
-  const int rp = (int)threadIdx.x;
-  if (rp >= 64) return;
+  const int r = (int)threadIdx.x;
+  if (r >= 64) return;
   const float* Q = L.nn;
   const uint32_t* v = L.nn_in;   // copied by the polling lanes with the request
   const int t = emb_row_h((int)v[9]) * 8 + emb_row_w((int)v[10]);
-  float in[9];
-  const uint32_t raw[9] = {v[0], v[1], v[2], v[3], v[8], v[4], v[5], v[6], v[7]};
+  const int r1 = r < 22 ? r : 21, r2 = r < 20 ? r : 19, r3 = r < 49 ? r : 48;
+  float w1[9], w2[22], w3[20];
 #pragma unroll
-  for (int k = 0; k < 9; k++) {
-    float x = (float)raw[k];
-    x = (x - Q[kNnPkMean + k]) / Q[kNnPkStd + k];
-    in[k] = x * Q[kNnPkGin + k];
-  }
-  const int r1 = rp < 11 ? rp : 10, r2 = rp < 10 ? rp : 9, r3 = rp < 25 ? rp : 24;
-  f2 x1;
+  for (int k = 0; k < 9; k++) w1[k] = Q[pk_at(kNnPkW1, 9, r1, k)];
+#pragma unroll
+  for (int k = 0; k < 22; k++) w2[k] = Q[pk_at(kNnPkW2, 22, r2, k)];
+#pragma unroll
+  for (int k = 0; k < 20; k++) w3[k] = Q[pk_at(kNnPkW3, 20, r3, k)];
+  const float p1 = Q[kNnPkPfx + t * 22 + r1], b1 = Q[kNnPkB1 + r1], g1 = Q[kNnPkG1 + r1], be1 = Q[kNnPkBE1 + r1];
+  const float b2 = Q[kNnPkB2 + r2], g2 = Q[kNnPkG2 + r2], be2 = Q[kNnPkBE2 + r2], bo = Q[kNnPkBout + r3];
+  // input k in lane k: raw order e0..e3, C, e4..e7
+  float xin;
   {
-    const float* pfx = Q + kNnPkPfx + t * 22;
-    x1 = (f2){pfx[2 * r1], pfx[2 * r1 + 1]};
-#pragma unroll
-    for (int k = 0; k < 9; k++) x1 = x1 + ld2(Q, kNnPkW1 + (r1 * 9 + k) * 2) * (f2){in[k], in[k]};
-    x1 = relu2(x1 + ld2(Q, kNnPkB1 + 2 * r1));
-    x1 = x1 * ld2(Q, kNnPkG1 + 2 * r1) + ld2(Q, kNnPkBE1 + 2 * r1);
+    const int k = r < 9 ? r : 8;
+    const int src = k < 4 ? k : (k == 4 ? 8 : k - 1);
+    xin = (float)v[src];
+    xin = (xin - Q[kNnPkMean + k]) / Q[kNnPkStd + k];
+    xin = xin * Q[kNnPkGin + k];
   }
-  f2 x2 = {0.0f, 0.0f};
+  float x1 = p1;
 #pragma unroll
-  for (int k = 0; k < 22; k++) {
-    const float a = lane_f((k & 1) ? x1.y : x1.x, k >> 1);
-    x2 = x2 + ld2(Q, kNnPkW2 + (r2 * 22 + k) * 2) * (f2){a, a};
-  }
-  x2 = relu2(x2 + ld2(Q, kNnPkB2 + 2 * r2));
-  x2 = x2 * ld2(Q, kNnPkG2 + 2 * r2) + ld2(Q, kNnPkBE2 + 2 * r2);
-  f2 x3 = {0.0f, 0.0f};
+  for (int k = 0; k < 9; k++) x1 = x1 + w1[k] * lane_f(xin, k);
+  x1 = relu1(x1 + b1);
+  x1 = x1 * g1 + be1;
+  float x2 = 0.0f;
 #pragma unroll
-  for (int k = 0; k < 20; k++) {
-    const float a = lane_f((k & 1) ? x2.y : x2.x, k >> 1);
-    x3 = x3 + ld2(Q, kNnPkW3 + (r3 * 20 + k) * 2) * (f2){a, a};
-  }
-  x3 = x3 + ld2(Q, kNnPkBout + 2 * r3);
-  // output row pair rp, then the first maximum over the 49 rows (strict >, rows in order)
+  for (int k = 0; k < 22; k++) x2 = x2 + w2[k] * lane_f(x1, k);
+  x2 = relu1(x2 + b2);
+  x2 = x2 * g2 + be2;
+  float x3 = 0.0f;
+#pragma unroll
+  for (int k = 0; k < 20; k++) x3 = x3 + w3[k] * lane_f(x2, k);
+  x3 = x3 + bo;
+  // the first maximum over the 49 rows (strict >, rows in order) with the batch rule's NaNs (row 0
+  // taken first, then strict >): a NaN row 0 wins, a later NaN never
   float bv = -INFINITY;
   int bi = 64;
-  if (rp < 25) {
-    // the batch rule's NaNs (row 0 taken first, then strict >): a NaN row 0 wins, a later NaN never
-    if (x3.x != x3.x) x3.x = rp == 0 ? INFINITY : -INFINITY;
-    if (x3.y != x3.y) x3.y = -INFINITY;
-    bv = x3.x;
-    bi = 2 * rp;
-    if (rp < 24 && x3.y > bv) {
-      bv = x3.y;
-      bi = 2 * rp + 1;
-    }
+  if (r < 49) {
+    if (x3 != x3) x3 = r == 0 ? INFINITY : -INFINITY;
+    bv = x3;
+    bi = r;
   }
-  // rows live in lanes 0..24: an xor reduction over 32 lanes (DPP and permlane16, no LDS pipe)
+  // an xor reduction over the 64 lanes (DPP and permlanes, no LDS pipe), ties to the lower row
   auto step = [&](float ov, int oi) {
     if (ov > bv || (ov == bv && oi < bi)) {
       bv = ov;
       bi = oi;
     }
   };
-  auto xf = [&](auto m, float v) { return __builtin_bit_cast(float, xor_lane<decltype(m)::value>(__builtin_bit_cast(int, v), rp)); };
-  step(xf(std::integral_constant<int, 1>{}, bv), xor_lane<1>(bi, rp));
-  step(xf(std::integral_constant<int, 2>{}, bv), xor_lane<2>(bi, rp));
-  step(xf(std::integral_constant<int, 4>{}, bv), xor_lane<4>(bi, rp));
-  step(xf(std::integral_constant<int, 8>{}, bv), xor_lane<8>(bi, rp));
-  step(xf(std::integral_constant<int, 16>{}, bv), xor_lane<16>(bi, rp));
-  if (rp == 0) {
+  auto xf = [&](auto m, float x) { return __builtin_bit_cast(float, xor_lane<decltype(m)::value>(__builtin_bit_cast(int, x), r)); };
+  step(xf(std::integral_constant<int, 1>{}, bv), xor_lane<1>(bi, r));
+  step(xf(std::integral_constant<int, 2>{}, bv), xor_lane<2>(bi, r));
+  step(xf(std::integral_constant<int, 4>{}, bv), xor_lane<4>(bi, r));
+  step(xf(std::integral_constant<int, 8>{}, bv), xor_lane<8>(bi, r));
+  step(xf(std::integral_constant<int, 16>{}, bv), xor_lane<16>(bi, r));
+  step(xf(std::integral_constant<int, 32>{}, bv), xor_lane<32>(bi, r));
+  if (r == 0) {
     L.ans[0] = (uint32_t)bi;
     L.ans[1] = 0;
   }
