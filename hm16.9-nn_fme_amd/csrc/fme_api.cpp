@@ -162,6 +162,7 @@ struct fme_ctx {
   uint32_t srv_nn_gen = 0;      // weight generation the running instance copied to LDS
   uint32_t nn_gen = 0;          // bumped by fme_load_nn_weights
   uint64_t srv_khz = 100000;    // wall-clock rate (s_memrealtime)
+  bool srv_marks = false;       // the server records its phase checkpoints (fme_single_last_device_us)
 
   // Profiling: a ring of event sets, one per profiled batch, read once the batch has finished
   // (harvest_events), so profiling a run of batches adds no synchronisation.  Per set: 0 start,
@@ -1145,7 +1146,8 @@ int fme_frac_dif_single(fme_ctx* c, int lossless, const int16_t* key, int key_st
   b->req[1][2] = mlw[1];
   __atomic_store_n(&b->req[1][0], seq, __ATOMIC_RELEASE);
   b->req[0][1] = (uint32_t)kSrvFrac | ((lossless || !c->cfg.use_hadamard) ? (uint32_t)kSrvSad : 0u) |
-                 (tagged ? (uint32_t)kSrvTagged : 0u) | ((uint32_t)(w - 1) << 8) | ((uint32_t)(h - 1) << 16);
+                 (tagged ? (uint32_t)kSrvTagged : 0u) | (c->srv_marks ? (uint32_t)kSrvMarks : 0u) |
+                 ((uint32_t)(w - 1) << 8) | ((uint32_t)(h - 1) << 16);
   b->req[0][2] = (uint32_t)(uint16_t)px | ((uint32_t)(uint16_t)py << 16);
   rc = srv_call(c, false);
   if (rc) return rc;
@@ -1173,7 +1175,7 @@ int fme_nn_pred_single(fme_ctx* c, const uint32_t* e, uint32_t cc, int pu_h, int
       for (int k = 0; k < 3; k++) c->box->req[b][1 + k] = in[3 * (b - 1) + k];
       __atomic_store_n(&c->box->req[b][0], seq, __ATOMIC_RELEASE);
     }
-    c->box->req[0][1] = kSrvNn;
+    c->box->req[0][1] = kSrvNn | (c->srv_marks ? (uint32_t)kSrvMarks : 0u);
     rc = srv_call(c, true);
     if (rc) return rc;
     *nn_class = (int)c->box->res[1];
@@ -1215,6 +1217,7 @@ int fme_nn_pred_single(fme_ctx* c, const uint32_t* e, uint32_t cc, int pu_h, int
 int fme_single_last_device_us(fme_ctx* c, float* us, int count) {
   if (!c || (count > 0 && !us)) return fail(FME_E_INVALID, "fme_single_last_device_us: null argument");
   const double k = 1000.0 / (double)c->srv_khz;
+  if (count > 1) c->srv_marks = true;   // checkpoints cost wall-clock reads: recorded once asked for
   for (int i = 0; i < count && i < 5; i++)
     us[i] = !c->box ? 0.0f : (float)((double)(i == 0 ? c->box->res[3] : c->box->marks[i - 1]) * k);
   return FME_OK;

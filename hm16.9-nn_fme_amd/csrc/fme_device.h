@@ -186,13 +186,14 @@ struct NnIn11 {   // NN_pred() inputs of a single call: array_e slots[8], C, PUH
 // pinned, device-mapped host memory, serves the call and stores the answer block `res`; `stopped` = the
 // epoch of an instance that exited (idle, lifetime or `stop`).  Request fields share the first
 // lines, the answer has its own, the payload follows.
-enum { kSrvNn = 1, kSrvFrac = 2, kSrvSad = 4, kSrvTagged = 8 };
+enum { kSrvNn = 1, kSrvFrac = 2, kSrvSad = 4, kSrvTagged = 8, kSrvMarks = 16 };
 constexpr int kSrvBlocks = 128;                       // request blocks, all read by every poll
 constexpr int kSrvTagBytes = 12 * (kSrvBlocks - 2);   // FracDIF payload that rides in the blocks
 struct SrvBox {
   // host -> device, in 16-byte blocks that the polling wave reads all at once (two per lane, one
   // load each), so a block's fields are those written before its sequence word.  req[0]: seq,
-  // shape = kind (bits 0-1) | kSrvSad (lossless or HADME off) | kSrvTagged | w - 1 (bits 8-15) |
+  // shape = kind (bits 0-1) | kSrvSad (lossless or HADME off) | kSrvTagged | kSrvMarks (record the
+  // phase checkpoints in `marks`) | w - 1 (bits 8-15) |
   // h - 1 (bits 16-23), the FracDIF predictor - 4 * integer MV (x low 16 bits, y high 16,
   // quarter-pel), stop (set by the host to end the instance).  The rest carry this call's seq in
   // word 0 and are taken only when every one the call uses does:

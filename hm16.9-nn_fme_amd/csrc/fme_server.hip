@@ -104,7 +104,7 @@ struct SrvLds {
   int16_t hp[3][72 * 65];       // first filter stage, fractional phase 1..3, columns -1 .. w-1
   alignas(16) uint8_t win[72 * 72 + 16];
   uint32_t cost[2][16];           // per candidate: half stage, quarter stage
-  int32_t ctl[9];               // stop, seq, kind, w, h, mvp_x, mvp_y, sad, tagged
+  int32_t ctl[10];              // stop, seq, kind, w, h, mvp_x, mvp_y, sad, tagged, marks
   uint32_t nn_in[12];
   double ml;
   int32_t sel[2];               // half-stage best (hx, hy)
@@ -248,10 +248,9 @@ __device__ void stage_pick(const SrvLds& L, bool half, int hx, int hy, int& best
 
 __device__ void serve_frac(SrvLds& L, SrvBox* box, uint64_t t_req) {
   const int tid = (int)threadIdx.x;
+  const bool marks = L.ctl[9] != 0;   // checkpoints only when asked for (each is a wall-clock read)
   auto mark = [&](int m) {
-#ifndef FME_SRV_NOMARKS
-    if (tid == 0) L.mark[m] = (uint32_t)(wall_clock64() - t_req);
-#endif
+    if (marks && tid == 0) L.mark[m] = (uint32_t)(wall_clock64() - t_req);
   };
   const int w = L.ctl[3], h = L.ctl[4];
   const bool sad = L.ctl[7] != 0;
@@ -446,6 +445,7 @@ __global__ __launch_bounds__(kSrvThreads) void k_server(SrvBox* box, const float
         L.ctl[2] = (int32_t)(shape & 3u);                 // kind
         L.ctl[7] = (shape & kSrvSad) ? 1 : 0;
         L.ctl[8] = (shape & kSrvTagged) ? 1 : 0;
+        L.ctl[9] = (shape & kSrvMarks) ? 1 : 0;
         L.ctl[3] = (int32_t)((shape >> 8) & 0xFFu) + 1;   // w
         L.ctl[4] = (int32_t)((shape >> 16) & 0xFFu) + 1;  // h
         L.ctl[5] = (int32_t)(int16_t)(hd.z & 0xFFFFu);    // mvp_x - 4 * mv_int_x
@@ -496,12 +496,12 @@ __global__ __launch_bounds__(kSrvThreads) void k_server(SrvBox* box, const float
         for (int i = tid; i < (w * h) >> 3; i += kSrvThreads) kdst[i] = load_block(ksrc + 4 * i);
         __syncthreads();
       }
-      if (tid == 0) L.mark[0] = (uint32_t)(wall_clock64() - t_req);
+      if (L.ctl[9] && tid == 0) L.mark[0] = (uint32_t)(wall_clock64() - t_req);
     }
     const uint32_t seq = (uint32_t)L.ctl[1];
     if (L.ctl[2] == kSrvFrac) {
       serve_frac(L, box, t_req);
-    } else {   // marks: shader-clock cycles and wall ticks of the net itself
+    } else if (L.ctl[9]) {   // marks: shader-clock cycles and wall ticks of the net itself
       const uint64_t c0 = clock64(), w0 = wall_clock64();
       serve_nn(L, box);
       if (tid == 0) {
@@ -509,11 +509,15 @@ __global__ __launch_bounds__(kSrvThreads) void k_server(SrvBox* box, const float
         L.mark[1] = (uint32_t)(wall_clock64() - w0);
         L.mark[2] = L.mark[3] = 0;
       }
+    } else {
+      serve_nn(L, box);
     }
     __syncthreads();
     if (tid == 0) {   // the answer and its sequence word in one 16-byte store, past the caches
-      const u32x4 m = {L.mark[0], L.mark[1], L.mark[2], L.mark[3]};
-      store_block(box->marks, m);
+      if (L.ctl[9]) {
+        const u32x4 m = {L.mark[0], L.mark[1], L.mark[2], L.mark[3]};
+        store_block(box->marks, m);
+      }
       const u32x4 r = {seq, L.ans[0], L.ans[1], (uint32_t)(wall_clock64() - t_req)};
       store_block(box->res, r);
     }

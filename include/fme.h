@@ -608,8 +608,10 @@ int fme_accumulated_timings(fme_ctx* ctx, double* ms, int count, int reset);
 /* The last fme_frac_dif_single / fme_nn_pred_single call as the resident server saw it, device
  * microseconds since it read the request: us[0] to the answer (the rest of the call's wall time
  * is the host, PCIe and polling); FracDIF only, us[1..4] to the payload (key and window) in LDS,
- * the first filter stage, the half stage's distortions, the quarter stage's distortions.  count <= 5
- * values. */
+ * the first filter stage, the half stage's distortions, the quarter stage's distortions (NN_pred:
+ * us[1] shader cycles / 100 and us[2] the net's own microseconds).  count <= 5 values.  The
+ * checkpoints cost the server wall-clock reads, so it records them only once a caller has asked
+ * for them (count > 1): from the next call on; until then us[1..4] are zero. */
 int fme_single_last_device_us(fme_ctx* ctx, float* us, int count);
 
 #ifdef __cplusplus
