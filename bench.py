@@ -224,6 +224,68 @@ def cpu_baseline_all_cores(jobs, pics, rate1, seconds, cores):
     return total / wall, wall, total
 
 
+def parity_leg(rep, wl, net, step, state, seconds, max_jobs=0):
+    """The exact job stream of one timed step against oracle/_ref (the reference's TLibCommon driven
+    in TEncSearch order, TEncSearch.cpp:4529-4597) after the timed region: the step's jobs with its
+    picture binding (FrameReplay._bind: originals, the four reconstructions, lambdas by POC) and the
+    NN state the GPU had before the step (fme_nn_get_state), every xMotionEstimation output of the
+    16-byte record (rcMv, ruiBits, ruiCost, NN class) compared, in job order, one host core, until
+    `seconds` have passed (whole 20k-job chunks; the whole step when it fits)."""
+    from nnfme import weights
+    from nnfme.pipeline import ORG0, REFS
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    from oracle import Reference
+    if rep.kreqs is not None:
+        return {"skipped": "bi-pred keys are built on the device per step; the key parity is "
+                           "tests/test_gpu_c4.py's"}
+    nn = wl["nn"]
+    ref = Reference(use_hadamard=1, nn_mode=nn, fast_inter_mode=1)
+    if nn == 1:
+        ref.load_nn(weights.load_weights(wl["QP"]))
+    elif nn == 2:
+        ref.load_nn_net(net)
+    F, P = rep.F, rep.P
+    f0 = rep.first_frame(step)
+    pool = rep.pool.numpy()
+    for j in range(F):
+        ref.set_picture(ORG0 + j, pool[(f0 + j) % P])
+        ref.set_lambda(j, rep.lambda_of(f0 + j))
+    for slot in range(F + REFS - 1):
+        ref.set_picture(slot, pool[(f0 - REFS + slot) % P])
+    ref.nn_set_state(state)
+    if rep.rows is not None:
+        ref.set_nn_inputs(rep.rows)
+    jobs, gpu = rep.jobs, rep.results(step)
+    n = len(jobs) if max_jobs <= 0 else min(max_jobs, len(jobs))
+    fields = ("mv_x", "mv_y", "bits", "cost") + (("nn_class",) if nn else ())
+    bad = {f: 0 for f in fields}
+    mism = 0
+    first = None
+    done, t0 = 0, time.perf_counter()
+    while done < n and time.perf_counter() - t0 < seconds:
+        e = min(done + 20000, n)
+        r = ref.refine(jobs[done:e])
+        g = gpu[done:e]
+        m = np.zeros(e - done, bool)
+        for f in fields:
+            d = g[f] != r[f]
+            bad[f] += int(d.sum())
+            m |= d
+        if first is None and m.any():
+            first = done + int(np.flatnonzero(m)[0])
+        mism += int(m.sum())
+        done = e
+    out = {"jobs_checked": done, "mismatches": mism, "step": step, "of_step_jobs": len(jobs),
+           "fields": list(fields), "per_field": bad, "first_mismatch": first,
+           "reference": "oracle/_ref (the reference's TLibCommon -O2, TEncSearch order restated; NN "
+                        "restated scalar) with the step's pictures, lambdas and carried NN state",
+           "seconds": round(time.perf_counter() - t0, 2)}
+    if nn == 2 and wl.get("engine"):
+        out["note"] = ("MFMA engine: FMA-chain rounding, not bit-exact by construction (DESIGN.md §3); "
+                       "a mismatch is a near-tie class")
+    return out
+
+
 def mc_algorithmic_bytes(jobs):
     """Motion compensation, per PU and list: the luma 8-tap footprint (w+7)(h+7) and the two
     chroma 4-tap footprints (w/2+3)(h/2+3); per PU: the predicted samples (1.5 w h, written) and
@@ -543,6 +605,12 @@ def main():
     ap.add_argument("--cpu-cores", type=int, default=0,
                     help="cores for cpu_baseline_all_cores (0: all available, at most 16; -1: skip)")
     ap.add_argument("--dist-backend", default="nccl", help="torch.distributed backend for N > 1 (nccl = RCCL)")
+    ap.add_argument("--parity-seconds", type=float, default=30.0,
+                    help="bound of the after-run check of one timed step against oracle/_ref (0: skip)")
+    ap.add_argument("--download-engine", choices=("kernel", "blit"), default="kernel",
+                    help="results download: the library's few-workgroup copy kernel (fme_download_device) "
+                         "or hipMemcpyAsync (a blit kernel of hundreds of workgroups)")
+    ap.add_argument("--download-wgs", type=int, default=8, help="workgroups of the download kernel")
     ap.add_argument("--download", choices=("deferred", "immediate"), default=None,
                     help="results download of step k: once step k+1's search runs (deferred) or right after "
                          "step k (immediate); default: the workload's measured choice (DESIGN.md section 5)")
@@ -645,13 +713,16 @@ def main():
     # that frame's pictures (fme_build_bipred_keys_device, k_bi_key) inside the timed step
     rep = FrameReplay(ctx, jobs, pool, lambda f: frame_lambda(wl, f), steps_total, frames_per_step=FPS,
                       world=world, rank=rank, device=dev, defer_download=defer,
-                      key_reqs=key_reqs, key_count=len(keys) if keys is not None else 0, nn_rows=nn_rows)
+                      key_reqs=key_reqs, key_count=len(keys) if keys is not None else 0, nn_rows=nn_rows,
+                      download_engine=args.download_engine, download_wgs=args.download_wgs)
     n = rep.n
     rep.prime()
 
     for s in range(args.warmup):
         rep.issue(s, prefetch=s + 1 < args.warmup)   # the first timed step uploads its own inputs
     rep.drain()
+    # the NN_pred state the first timed step starts from (untimed), for the after-run parity check
+    state0 = ctx.nn_get_state() if world == 1 else None
 
     # ---- timed region: H2D (jobs, originals, reconstructions + RCCL broadcast) -> refine ->
     # D2H of the 16-byte results, two steps in flight; the NN-state chain fix-up when sharded ----
@@ -699,6 +770,10 @@ def main():
             dt = (time.perf_counter() - t1) / args.steps
         dres = {"value": n / dt, "unit": "PU/s", "ms_per_step": dt * 1e3,
                 "note": "jobs, pictures and results HBM-resident, one GPU, batches back to back"}
+
+    parity = None
+    if rank == 0 and world == 1 and args.parity_seconds > 0:
+        parity = parity_leg(rep, wl, net, args.warmup, state0, args.parity_seconds)
 
     mc = mc_leg(dev, torch.cuda.current_stream(dev), reps=max(5, args.steps // 2)) \
         if rank == 0 and not args.no_mc and W == 1920 and NN != 2 else None
@@ -753,7 +828,10 @@ def main():
                                 "reconstructed reference per frame (when sharded: RCCL point-to-point sends to the "
                                 "<= 3 other ranks whose frames reference it), refine, D2H of "
                                 "the 16-byte fme_mv_result per job; two steps in flight on separate copy / "
-                                "compute streams" + ("; NN-state chain fix-up included" if world > 1 else "")},
+                                "compute streams" + ("; NN-state chain fix-up included" if world > 1 else ""),
+                       "download": (f"fme_download_device ({args.download_wgs} one-wave workgroups, system-scope "
+                                    f"stores into the pinned rows)" if args.download_engine == "kernel"
+                                    else "hipMemcpyAsync (ROCclr blit kernel)")},
             "roofline": {
                 "bound": "valu",
                 "achieved": valu,
@@ -786,6 +864,8 @@ def main():
             out["speedup_vs_cpu_all_cores"] = value / cpu["cpu_baseline_all_cores"]["value"]
         if dres:
             out["device_resident"] = dres
+        if parity:
+            out["parity"] = parity
         if world > 1:
             out["nn_state_fixup_jobs_rank0"] = int(fixed)
         if mc:

@@ -8,6 +8,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cmath>
 #include <cstdlib>
 #include <cstdarg>
@@ -244,6 +245,15 @@ int fme_create(int device, const fme_config* cfg, fme_ctx** out_ctx) {
 
 }  // extern "C"
 static int srv_stop(fme_ctx* c);
+// Grows the bi-pred key buffer to n elements.  Growing frees the old buffer, which batches queued on
+// any stream (the caller's, the integer search's auxiliary streams, another caller stream) may still
+// read: every stream of the device is drained first, and only when the buffer really grows.
+static int grow_keys(fme_ctx* c, size_t n) {
+  if (n <= c->d_keys.cap) return FME_OK;
+  HIP_TRY(hipDeviceSynchronize());
+  HIP_TRY(c->d_keys.reserve(n));
+  return FME_OK;
+}
 extern "C" {
 int fme_destroy(fme_ctx* c) {
   if (!c) return FME_OK;
@@ -397,7 +407,12 @@ int fme_set_motion_lambda(fme_ctx* c, int id, double ml) {
 int fme_set_keys(fme_ctx* c, const int16_t* keys, size_t count, void* stream) {
   if (!c || (!keys && count)) return fail(FME_E_INVALID, "fme_set_keys: null argument");
   HIP_TRY(hipSetDevice(c->device));
-  HIP_TRY(c->d_keys.reserve(count));
+  // the upload and the memset below are GPU work: a resident single-call server could hold them up
+  // on a hardware queue its stream shares (sync_tables does the same for batches)
+  int rc = srv_stop(c);
+  if (rc) return rc;
+  rc = grow_keys(c, count);
+  if (rc) return rc;
   hipStream_t s = static_cast<hipStream_t>(stream);
   if (count) HIP_TRY(hipMemcpyAsync(c->d_keys.p, keys, count * sizeof(int16_t), hipMemcpyHostToDevice, s));
   // fresh host keys: a rejection left by an earlier device build no longer applies (fme.h: rejected
@@ -709,6 +724,22 @@ int fme_refine_mv_device(fme_ctx* c, const fme_job* d_jobs, fme_mv_result* d_out
 int fme_set_search_event(fme_ctx* c, void* event) {
   if (!c) return fail(FME_E_INVALID, "fme_set_search_event: null ctx");
   c->ev_search = static_cast<hipEvent_t>(event);
+  return FME_OK;
+}
+
+int fme_download_device(fme_ctx* c, const void* d_src, void* h_dst, size_t bytes, int workgroups, void* stream) {
+  if (!c || (bytes && (!d_src || !h_dst))) return fail(FME_E_INVALID, "fme_download_device: null argument");
+  if ((bytes & 15) || (reinterpret_cast<uintptr_t>(d_src) & 15) || (reinterpret_cast<uintptr_t>(h_dst) & 15))
+    return fail(FME_E_INVALID, "fme_download_device: pointers and size must be 16-byte multiples");
+  if (workgroups < 0 || workgroups > 1024) return fail(FME_E_INVALID, "fme_download_device: %d workgroups", workgroups);
+  if (!bytes) return FME_OK;
+  HIP_TRY(hipSetDevice(c->device));
+  void* dst = nullptr;   // the device's address of the pinned host rows
+  if (hipHostGetDevicePointer(&dst, h_dst, 0) != hipSuccess || !dst) {
+    (void)hipGetLastError();
+    return fail(FME_E_INVALID, "fme_download_device: h_dst is not pinned host memory");
+  }
+  HIP_TRY(launch_download(d_src, dst, bytes / 16, workgroups ? workgroups : 8, static_cast<hipStream_t>(stream)));
   return FME_OK;
 }
 
@@ -1051,8 +1082,16 @@ static int srv_launch(fme_ctx* c) {
 }
 
 // The running instance's end: its `stopped` word (or a device error on its stream).
+// Host-side bound of a wait on the server (a call, or its stop): far above any call's work (a 64x64
+// FracDIF takes ~0.1 ms, an instance lives 100 ms), so only a server that never answers reaches it.
+constexpr double kSrvWaitLimitS = 2.0;
+static bool srv_waited_too_long(std::chrono::steady_clock::time_point t0) {
+  return std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > kSrvWaitLimitS;
+}
+
 static int srv_join(fme_ctx* c) {
   volatile uint32_t* st = &c->box->stopped;
+  const auto t0 = std::chrono::steady_clock::now();
   for (long it = 1; *st != c->srv_epoch; it++) {
     __builtin_ia32_pause();
     if ((it & 1023) == 0) {
@@ -1061,6 +1100,10 @@ static int srv_join(fme_ctx* c) {
         c->srv_running = false;
         if (q != hipSuccess) return fail(FME_E_DEVICE, "single-call server: %s", hipGetErrorString(q));
         return fail(FME_E_DEVICE, "single-call server ended without its stop word");
+      }
+      if (srv_waited_too_long(t0)) {
+        c->srv_running = false;
+        return fail(FME_E_DEVICE, "single-call server: no stop word after %.1f s", kSrvWaitLimitS);
       }
     }
   }
@@ -1085,11 +1128,14 @@ static int srv_call(fme_ctx* c, bool uses_nn) {
   __atomic_store_n(&c->box->req[0][0], seq, __ATOMIC_RELEASE);
   volatile uint32_t* done = &c->box->res[0];
   volatile uint32_t* st = &c->box->stopped;
+  const auto t0 = std::chrono::steady_clock::now();
   for (long it = 1; *done != seq; it++) {
     __builtin_ia32_pause();
     if (*st == c->srv_epoch && *done != seq) {   // the instance left before it saw the call
       c->srv_running = false;
       HIP_TRY(hipStreamSynchronize(c->srv_stream));
+      if (srv_waited_too_long(t0))
+        return fail(FME_E_DEVICE, "single-call server: call %u unanswered after %.1f s", seq, kSrvWaitLimitS);
       rc = srv_launch(c);
       if (rc) return rc;
     } else if ((it & 4095) == 0) {
@@ -1097,6 +1143,12 @@ static int srv_call(fme_ctx* c, bool uses_nn) {
       if (q != hipErrorNotReady && q != hipSuccess) {
         c->srv_running = false;
         return fail(FME_E_DEVICE, "single-call server: %s", hipGetErrorString(q));
+      }
+      if (srv_waited_too_long(t0)) {   // stop the instance (it exits within its lifetime) and give up
+        __atomic_store_n(&c->box->req[0][3], 1u, __ATOMIC_RELEASE);
+        (void)srv_join(c);
+        c->srv_running = false;
+        return fail(FME_E_DEVICE, "single-call server: call %u unanswered after %.1f s", seq, kSrvWaitLimitS);
       }
     }
   }
@@ -1180,7 +1232,10 @@ int fme_nn_pred_single(fme_ctx* c, const uint32_t* e, uint32_t cc, int pu_h, int
     if (rc) return rc;
     *nn_class = (int)c->box->res[1];
   } else {
-  rc = ensure_stage(c);
+  // a resident server (a FracDIF call just before) would hold this launch up on a hardware queue
+  // its stream shares until its idle exit: stop it first, as the batch entry points do
+  rc = srv_stop(c);
+  if (!rc) rc = ensure_stage(c);
   if (rc) return rc;
   // inputs in the kernel argument, the class and the completion word through mapped host memory:
   // one launch, a spin on the completion word
@@ -1562,8 +1617,8 @@ int fme_build_bipred_keys(fme_ctx* c, const fme_bikey_req* reqs, int n, size_t k
       return fail(FME_E_INVALID, "fme_build_bipred_keys: request %d invalid", i);
   }
   int rc = sync_tables(c, s);
+  if (!rc) rc = grow_keys(c, key_count);
   if (rc) return rc;
-  HIP_TRY(c->d_keys.reserve(key_count));
   c->n_keys = key_count;
   HIP_TRY(hipMemsetAsync(c->d_key_invalid.p, 0, sizeof(int32_t), s));   // host-validated: the keys are good
   if (n == 0) return hipStreamSynchronize(s) == hipSuccess ? FME_OK : fail(FME_E_DEVICE, "fme_build_bipred_keys: sync");
@@ -1585,10 +1640,8 @@ int fme_build_bipred_keys_device(fme_ctx* c, const fme_bikey_req* d_reqs, int n,
   hipStream_t s = static_cast<hipStream_t>(stream);
   int rc = sync_tables(c, s);
   if (rc) return rc;
-  if (key_count > c->d_keys.cap) {   // growing frees the old buffer: let queued batches finish first
-    HIP_TRY(hipStreamSynchronize(s));
-    HIP_TRY(c->d_keys.reserve(key_count));
-  }
+  rc = grow_keys(c, key_count);   // growing frees the old buffer: every queued batch finishes first
+  if (rc) return rc;
   c->n_keys = key_count;
   HIP_TRY(hipMemsetAsync(c->d_key_invalid.p, 0, sizeof(int32_t), s));
   if (n == 0) return FME_OK;
@@ -2203,7 +2256,8 @@ int fme_pred_inter_b(fme_ctx* c, const fme_pu_req_b* reqs, fme_pu_res_b* res, in
     }
     if (issued.empty()) break;
     // keys, bi-pred integer searches, then the sub-pel path over uni + bi jobs in call order
-    HIP_TRY(c->d_keys.reserve(key_total));
+    rc = grow_keys(c, key_total);
+    if (rc) return rc;
     c->n_keys = key_total;
     HIP_TRY(c->d_bikey.reserve(keyt.size()));
     HIP_TRY(hipMemcpyAsync(c->d_bikey.p, keyt.data(), keyt.size() * sizeof(BiKeyTask), hipMemcpyHostToDevice, s));

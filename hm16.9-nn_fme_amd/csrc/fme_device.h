@@ -250,6 +250,8 @@ __device__ __forceinline__ f2 relu2(f2 s) {
   s.y = s.y < 0.0f ? 0.0f : s.y;
   return s;
 }
+// Results download into pinned host memory (fme_download_device): `wgs` workgroups of 64 lanes.
+hipError_t launch_download(const void* src, void* dst, size_t n16, int wgs, hipStream_t s);
 hipError_t launch_nn_tail(const BatchArgs& a, const WorkBufs& w, const float* nn_params,
                           int state_in, hipStream_t s);
 

@@ -15,6 +15,8 @@
 // (this file is compiled with -ffp-contract=off) and sequential-k sums.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+
 #include "fme_device.h"
 
 namespace fme {
@@ -566,6 +568,36 @@ int cu_count(int device) {
   int v = 0;
   if (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || v <= 0) v = 256;
   return v;
+}
+
+// ---------------------------------------------------------------------------------------
+// results download: device rows -> pinned host memory, few workgroups.  Each lane keeps four
+// 16-byte loads in flight, then stores them with system-scope (sc0 sc1) write-through stores:
+// the rows go straight to the PCIe write path, no cache line of host memory stays in L2.
+// ---------------------------------------------------------------------------------------
+constexpr int kDlThreads = 64;
+__device__ __forceinline__ void dl_store(u32x4* p, u32x4 v) {
+  asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1" : : "v"(p), "v"(v) : "memory");
+}
+__global__ __launch_bounds__(kDlThreads) void k_download(const u32x4* __restrict__ src, u32x4* dst, long n16) {
+  const long stride = (long)gridDim.x * kDlThreads;
+  long i = (long)blockIdx.x * kDlThreads + threadIdx.x;
+  for (; i + 3 * stride < n16; i += 4 * stride) {
+    const u32x4 a = src[i], b = src[i + stride], c = src[i + 2 * stride], d = src[i + 3 * stride];
+    dl_store(dst + i, a);
+    dl_store(dst + i + stride, b);
+    dl_store(dst + i + 2 * stride, c);
+    dl_store(dst + i + 3 * stride, d);
+  }
+  for (; i < n16; i += stride) dl_store(dst + i, src[i]);
+}
+
+hipError_t launch_download(const void* src, void* dst, size_t n16, int wgs, hipStream_t s) {
+  const long need = (long)((n16 + kDlThreads - 1) / kDlThreads);
+  const int g = (int)std::min<long>(wgs, std::max<long>(need, 1));
+  hipLaunchKernelGGL(k_download, dim3(g), dim3(kDlThreads), 0, s, static_cast<const u32x4*>(src),
+                     static_cast<u32x4*>(dst), (long)n16);
+  return hipGetLastError();
 }
 
 hipError_t launch_nn_tail(const BatchArgs& a, const WorkBufs& w, const float* nn_params,

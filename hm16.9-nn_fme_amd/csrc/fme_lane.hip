@@ -871,7 +871,17 @@ __device__ FME_LANE_UNIT_ATTR void lane_unit(const BatchArgs& a, const fme_job* 
   uint32_t cval = 0, emi[8];
 #pragma unroll
   for (int k = 0; k < 8; k++) emi[k] = 0;
-  if (j.flags & FME_JOB_EMI) {
+  // FME_JOB_NN_IN takes precedence over FME_JOB_EMI (fme.h: NN_IN means no EMI step), as in the
+  // oracle (fme_oracle.c orc_refine), the harness and nn_pushes()
+  if (j.flags & FME_JOB_NN_IN) {
+    // the backups' input path: the integer search's square + ring already moved mv and pushed
+    // the inputs (FME_TZ_RING); the job's row holds array_e[index_ref .. +7] and C
+    g_u32* const row = (g_u32*)(a.nn_in + (size_t)9 * jid);
+#pragma unroll
+    for (int k = 0; k < 8; k++) emi[k] = row[k];
+    cval = row[8];
+    n_emi = 8;
+  } else if (j.flags & FME_JOB_EMI) {
     uint32_t e9[9];
 #pragma unroll
     for (int q = 0; q < 9; q++) e9[q] = 0;
@@ -981,14 +991,6 @@ __device__ FME_LANE_UNIT_ATTR void lane_unit(const BatchArgs& a, const fme_job* 
     cval = best - best_cost;
     mvx = bx;
     mvy = by;
-  } else if (j.flags & FME_JOB_NN_IN) {
-    // the backups' input path: the integer search's square + ring already moved mv and pushed
-    // the inputs (FME_TZ_RING); the job's row holds array_e[index_ref .. +7] and C
-    g_u32* const row = (g_u32*)(a.nn_in + (size_t)9 * jid);
-#pragma unroll
-    for (int k = 0; k < 8; k++) emi[k] = row[k];
-    cval = row[8];
-    n_emi = 8;
   }
   typedef __attribute__((address_space(1))) u32x4a gw4;
   if (u == 0) {   // bytes 16..63 of the record: cost, bits (NN tail), c, emi[8], n_emi

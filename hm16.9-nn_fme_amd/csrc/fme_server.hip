@@ -428,7 +428,8 @@ __global__ __launch_bounds__(kSrvThreads) void k_server(SrvBox* box, const float
             need = (shape & kSrvTagged) ? 1 + ((w + 8) * (h + 8) + 2 * w * h + 11) / 12 : 1;
           }
           if (__ballot((lane >= 1 && lane <= need && hd.x != seq) || (lane + 64 <= need && hb.x != seq)) == 0) break;
-          continue;
+          // a block still carries an older call's sequence word: poll again, but the stop word and the
+          // lifetime still end the instance (the host relaunches, or gives up after its own bound)
         }
         stop = (uint32_t)__builtin_amdgcn_readfirstlane((int)hd.w);   // the host's stop word rides in req[0]
         if (stop) break;

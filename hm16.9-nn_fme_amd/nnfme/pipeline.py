@@ -95,7 +95,8 @@ def group_key_reqs(base, frames, key_count):
 
 class FrameReplay:
     def __init__(self, ctx, base_jobs, pool, lambda_of, n_steps, frames_per_step=1, world=1, rank=0, device=None,
-                 group=None, defer_download=True, key_reqs=None, key_count=0, nn_rows=None):
+                 group=None, defer_download=True, key_reqs=None, key_count=0, nn_rows=None,
+                 download_engine="kernel", download_wgs=8):
         """ctx: an FmeContext on `device`; base_jobs: one frame's jobs (ref_id = reference
         distance - 1); pool: uint8 [P, H, W] host frames, frame g's pictures are pool[g % P];
         lambda_of(g): frame g's lambda.  key_reqs (fme_bikey_req, ref_id = distance - 1) and
@@ -103,7 +104,11 @@ class FrameReplay:
         its frames' removeHighFreq keys on the device from that step's pictures, before its batch
         (fme_build_bipred_keys_device), so the keys are per-frame work inside the timed step.
         nn_rows (uint32 [n][9]): the NN input rows of the frame's FME_JOB_NN_IN jobs (the backups'
-        input path); each step uploads them with its jobs and binds them (fme_set_nn_inputs)."""
+        input path); each step uploads them with its jobs and binds them (fme_set_nn_inputs).
+        download_engine: "kernel" (fme_download_device: the library's copy kernel of
+        download_wgs one-wave workgroups, which holds a few wave slots beside the next step's
+        search) or "blit" (hipMemcpyAsync, which this ROCm runs as a blit kernel of hundreds of
+        workgroups that take the search kernel's CUs)."""
         import torch
         self.torch, self.ctx = torch, ctx
         self.world, self.rank, self.group = world, rank, group
@@ -148,6 +153,9 @@ class FrameReplay:
         self.ev_search = torch.cuda.Event()
         self.ev_search.record(self.s_comp)        # creates the underlying hipEvent_t
         self.defer_download = defer_download
+        if download_engine not in ("kernel", "blit"):
+            raise ValueError(f"download_engine {download_engine!r}")
+        self.download_engine, self.download_wgs = download_engine, int(download_wgs)
         ctx.set_search_event(self.ev_search if defer_download else None)
         self.pending = None                       # step whose download is not issued yet
         self.fixed_jobs = 0
@@ -333,7 +341,11 @@ class FrameReplay:
     def _download(self, k, after):
         dn = self.s_down
         dn.wait_event(after)
-        _memcpy_async(self.h_out[k], self.d_out[k & 1], self.h_out.shape[1], D2H, dn)
+        if self.download_engine == "kernel":
+            self.ctx.download_device(self.d_out[k & 1].data_ptr(), self.h_out[k].data_ptr(), self.h_out.shape[1],
+                                     self.download_wgs, dn.cuda_stream)
+        else:
+            _memcpy_async(self.h_out[k], self.d_out[k & 1], self.h_out.shape[1], D2H, dn)
         self.ev_out[k & 1].record(dn)
 
     def drain(self):

@@ -15,7 +15,7 @@ from .weights import load_weights
 PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB_PATH = os.environ.get("FME_LIB_PATH") or os.path.join(PKG_ROOT, "libfme_amd.so")
 
-ABI_VERSION = 12
+ABI_VERSION = 13
 TIMING_NAMES = ("classify", "scatter", "search", "nn_tail", "batch", "search_main", "search_aux")
 
 # Every entry point include/fme.h declares (the ABI test checks the .so exports them).
@@ -33,6 +33,7 @@ ABI_SYMBOLS = (
     "fme_refine_status", "fme_nn_copy_state_device", "fme_template_costs", "fme_pred_inter_b", "fme_build_bipred_keys",
     "fme_set_search_event", "fme_build_bipred_keys_device", "fme_set_nn_logit_output",
     "fme_set_nn_inputs", "fme_integer_search_ring", "fme_integer_search_ring_device",
+    "fme_download_device",
 )
 
 
@@ -111,6 +112,7 @@ def load_library(path=None):
         "fme_set_nn_inputs": (I, [P, P, I]),
         "fme_integer_search_ring": (I, [P, P, P, P, P, I, P]),
         "fme_integer_search_ring_device": (I, [P, P, P, P, P, I, P]),
+        "fme_download_device": (I, [P, P, P, C.c_size_t, I, P]),
     }
     # an explicitly named library is an A/B variant (tools/ab_bench.py): possibly an older ABI
     strict = os.path.abspath(path) == os.path.abspath(LIB_PATH)
@@ -396,6 +398,12 @@ class FmeContext:
     def nn_copy_state_device(self, d_ptr, stream=None):
         """Enqueue a copy of the carried NN state (12 words) to device memory at d_ptr."""
         _check(self.lib, self.lib.fme_nn_copy_state_device(self.h, C.c_void_p(d_ptr), stream))
+
+    def download_device(self, d_src_ptr, h_dst_ptr, nbytes, workgroups=0, stream=None):
+        """Copy nbytes of device rows into pinned host memory with the library's few-workgroup copy
+        kernel (fme_download_device), asynchronous on `stream`."""
+        _check(self.lib, self.lib.fme_download_device(self.h, C.c_void_p(d_src_ptr), C.c_void_p(h_dst_ptr),
+                                                      nbytes, workgroups, stream))
 
     def set_search_event(self, event):
         """Record `event` (a torch.cuda.Event or a raw hipEvent_t, None: off) on the batch stream

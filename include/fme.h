@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define FME_ABI_VERSION 12
+#define FME_ABI_VERSION 13
 
 /* ---- error codes ---------------------------------------------------------------- */
 #define FME_OK            0
@@ -282,6 +282,18 @@ int fme_nn_copy_state_device(fme_ctx* ctx, uint32_t* d_out12, void* stream);
  * back every read the device issues behind them (AQL packet and kernel-argument fetches), so a
  * download overlapping a prologue delayed each of its launches by the length of the copy.   */
 int fme_set_search_event(fme_ctx* ctx, void* event);
+
+/* Download of device records (fme_mv_result / fme_result rows, any 16-byte-multiple span) into
+ * pinned host memory (hipHostMalloc, hipHostRegister or a torch pin_memory() tensor) by the
+ * library's own copy kernel of at most `workgroups` workgroups of 64 lanes (0: the default, 8),
+ * each lane storing 16-byte blocks with system-scope (write-through) stores, asynchronous on
+ * `stream`.  A hipMemcpyAsync device-to-host copy runs on this ROCm as a blit kernel of hundreds
+ * of workgroups, which, queued beside a running batch, took the CUs of the search kernel
+ * (23.6 % of GPU time in the round-4 profile); this one holds a few wave slots.  No replacement
+ * of a reference interface: the reference keeps its results in host memory.
+ * d_src and h_dst must be 16-byte aligned and `bytes` a multiple of 16.                       */
+int fme_download_device(fme_ctx* ctx, const void* d_src, void* h_dst, size_t bytes, int workgroups,
+                        void* stream);
 
 
 /* ---- the batch path --------------------------------------------------------------------- *

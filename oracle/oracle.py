@@ -281,6 +281,7 @@ class Reference:
         lib.ref_set_keys.argtypes = [_P, _P, C.c_size_t]
         lib.ref_load_nn.argtypes = [_P, _P]
         lib.ref_nn_reset.argtypes = [_P]
+        lib.ref_nn_set_state.argtypes = [_P, _P]
         lib.ref_nn_class.restype = C.c_int
         lib.ref_nn_class.argtypes = [_P, _P, C.c_uint32, C.c_int, C.c_int]
         lib.ref_pred_block.restype = C.c_int
@@ -382,6 +383,12 @@ class Reference:
 
     def nn_reset(self):
         self.lib.ref_nn_reset(self.h)
+
+    def nn_set_state(self, st):
+        """NN_pred's carried globals from a 12-word state (fme_nn_get_state's layout)."""
+        st = np.ascontiguousarray(st, dtype=np.uint32)
+        assert st.size >= 11
+        self.lib.ref_nn_set_state(self.h, _ptr(st))
 
     def load_nn_net(self, net):
         d = net.desc_struct()

@@ -389,6 +389,16 @@ void ref_nn_reset(void* h) {
   c->net.reset();
 }
 
+// NN_pred()'s carried globals from a 12-word state (fme_nn_get_state layout: array_e slots 0..7, C,
+// PUHeight, PUWidth, written mask): the state a run of jobs in the middle of a stream starts from.
+void ref_nn_set_state(void* h, const uint32_t* st) {
+  RefCtx* c = static_cast<RefCtx*>(h);
+  for (int k = 0; k < 8; k++) c->slot[k] = st[k];
+  c->C = st[8];
+  c->puh = st[9];
+  c->puw = st[10];
+}
+
 void ref_load_nn_net(void* h, const fme_nn_net* d, const double* p, int count) {
   RefCtx* c = static_cast<RefCtx*>(h);
   c->net.d = *d;

@@ -139,3 +139,77 @@ def test_profiled_back_to_back_batches():
     ctx.set_profiling(False)
     assert nb == 40
     assert acc["batch"] > 0 and acc["search"] > 0
+
+
+def test_download_device_into_pinned_rows():
+    """fme_download_device (the frame replay's results download): device rows land in pinned host
+    memory byte for byte for any workgroup count, also at an offset into the pinned buffer; unaligned
+    sizes and pageable host memory are refused."""
+    import torch
+    from nnfme.runtime import FmeError
+    g = load_golden("qp32_nn")
+    ctx = _ctx(g)
+    rng = np.random.default_rng(5)
+    n = (1 << 20) + 16 * 37
+    src = torch.from_numpy(rng.integers(0, 256, n, dtype=np.uint8)).cuda()
+    dst = torch.zeros(n + 4096, dtype=torch.uint8).pin_memory()
+    s = torch.cuda.current_stream()
+    for wgs in (0, 1, 3, 8, 64):
+        dst.zero_()
+        ctx.download_device(src.data_ptr(), dst.data_ptr(), n, wgs, s.cuda_stream)
+        s.synchronize()
+        assert torch.equal(dst[:n], src.cpu()), wgs
+        assert not dst[n:].any()
+    dst.zero_()
+    ctx.download_device(src.data_ptr() + 64, dst.data_ptr() + 4096, n - 64, 8, s.cuda_stream)
+    s.synchronize()
+    assert torch.equal(dst[4096:4096 + n - 64], src[64:].cpu())
+    with pytest.raises(FmeError):
+        ctx.download_device(src.data_ptr(), dst.data_ptr(), 100, 8, s.cuda_stream)
+    pageable = np.zeros(4096, np.uint8)
+    with pytest.raises(FmeError):
+        ctx.download_device(src.data_ptr(), pageable.ctypes.data, 4096, 8, s.cuda_stream)
+
+
+def test_device_built_keys_rejection_cycle():
+    """fme_build_bipred_keys_device with one invalid request (a key block beyond the buffer): a later
+    batch whose jobs read keys is rejected on the device; a batch of uni-pred jobs is not; a clean
+    rebuild clears the rejection (fme.h, 'rejected until keys are built again')."""
+    import torch
+    from nnfme import synth
+    from nnfme.abi import BIKEY_REQ_DTYPE, JOB_BIPRED, MV_RESULT_DTYPE
+    W, H = 416, 240
+    rng = np.random.default_rng(41)
+    pics = {k: synth.synth_luma(W, H, t) for k, t in zip(range(5), (7, 6, 5, 4, 0))}
+    jobs = synth.make_ctu_jobs(rng, W, H, 64, 4, [0, 1, 2, 3], [0], bipred_frac=0.3)
+    reqs, key_count = synth.make_bipred_key_reqs(np.random.default_rng(7), jobs, 4, [0, 1, 2, 3])
+    from nnfme.runtime import FmeContext
+    ctx = FmeContext(nn_mode=1, qp=22, max_jobs=len(jobs))
+    for k, v in pics.items():
+        ctx.set_picture(k, v)
+    ctx.set_lambda(0, synth.LDP_LAMBDA[22][1])
+    dev = torch.device("cuda", 0)
+    s = torch.cuda.current_stream(dev)
+    bad = np.array(reqs, dtype=BIKEY_REQ_DTYPE, copy=True)
+    bad["key_offset"][len(bad) // 2] = key_count          # block beyond the key buffer
+    bi = (jobs["flags"] & JOB_BIPRED) != 0
+    assert bi.any() and (~bi).any()
+    uni = np.ascontiguousarray(jobs[~bi])
+
+    def run(js):
+        dj = torch.from_numpy(np.ascontiguousarray(js).view(np.uint8).copy()).to(dev)
+        out = torch.zeros(len(js) * MV_RESULT_DTYPE.itemsize, dtype=torch.uint8, device=dev)
+        ctx.refine_mv_device(dj.data_ptr(), out.data_ptr(), len(js), s.cuda_stream)
+        st = ctx.refine_status()
+        return st, out.cpu().numpy().view(MV_RESULT_DTYPE)
+
+    d_bad = torch.from_numpy(bad.view(np.uint8).copy()).to(dev)
+    ctx.build_bipred_keys_device(d_bad.data_ptr(), len(bad), key_count, s.cuda_stream)
+    st, out = run(jobs)
+    assert st > 0 and np.all(out["status"] & RES_REJECTED), "key batch not rejected"
+    st, out = run(uni)
+    assert st == 0 and not np.any(out["status"] & RES_REJECTED), "uni-pred batch rejected"
+    d_good = torch.from_numpy(np.ascontiguousarray(reqs).view(np.uint8).copy()).to(dev)
+    ctx.build_bipred_keys_device(d_good.data_ptr(), len(reqs), key_count, s.cuda_stream)
+    st, out = run(jobs)
+    assert st == 0 and not np.any(out["status"] & RES_REJECTED), "rejection not cleared by a clean rebuild"

@@ -321,3 +321,64 @@ def test_cpp_hm_adapter():
     p = subprocess.run([exe], capture_output=True, text=True, timeout=300)
     assert p.returncode == 0, p.stdout + p.stderr
     assert "hm adapter ok" in p.stdout
+
+
+def test_emi_and_nn_in_flags_together():
+    """A job flagged both FME_JOB_EMI and FME_JOB_NN_IN takes its NN inputs from its row and runs no
+    EMI step (fme.h), in the lane kernel as in the oracle and the reference harness."""
+    import torch
+    from oracle import Oracle
+    from nnfme.abi import JOB_NN_IN
+    g = load_golden("ldp_qp22_hadme_fen1_nn")
+    jobs = np.ascontiguousarray(g["jobs"][:400]).copy()
+    emi = np.flatnonzero(jobs["flags"] & JOB_EMI)
+    assert len(emi) > 50
+    jobs["flags"][emi[::3]] |= JOB_NN_IN
+    rng = np.random.default_rng(17)
+    rows = rng.integers(0, 200000, (len(jobs), 9)).astype(np.uint32)
+    ctx = _ctx(g)
+    d_rows = torch.from_numpy(rows.view(np.uint8).copy()).cuda()
+    ctx.set_nn_inputs(d_rows.data_ptr(), len(jobs))
+    try:
+        res = ctx.refine(jobs)
+    finally:
+        ctx.set_nn_inputs(None)
+    hadme, fen, nn_mode, qp = (int(v) for v in g["config"])
+    o = Oracle(use_hadamard=hadme, nn_mode=nn_mode, qp=qp, fast_inter_mode=fen)
+    o.load_nn(weights.load_weights(qp))
+    for i, p in enumerate(g["pictures"]):
+        o.set_picture(i, p)
+    for i, lam in enumerate(g["lambdas"]):
+        o.set_lambda(i, float(lam))
+    o.set_nn_inputs(rows)
+    want = o.refine(jobs)
+    _assert_same(res, want, "EMI | NN_IN")
+    both = emi[::3]
+    assert np.all(res["n_emi"][both] == 8) and np.array_equal(res["c"][both], rows[both, 8])
+
+
+def test_1080p_ctu_stream_every_job_against_reference():
+    """The job stream the bench times (synth.make_ctu_jobs: HM's CTU order, a smooth motion field,
+    the SURVEY §8(d) PU mix; one 1080p LDP QP22 frame, NN on) through the HIP batch path, every job's
+    every field - integer MV after EMI, half / quarter offsets, FracDIF cost, C, the EMI pushes, the
+    NN class, the final MV, bits and cost - against oracle/_ref (the reference's TLibCommon) run over
+    the whole frame in job order from a fresh NN state."""
+    from oracle import Reference
+    W, H = 1920, 1080
+    rng = np.random.default_rng(1000)
+    pics = {k: synth.synth_luma(W, H, t) for k, t in zip(range(5), (7, 6, 5, 4, 0))}
+    jobs = synth.make_ctu_jobs(rng, W, H, 423, 4, [0, 1, 2, 3], [0])
+    assert len(jobs) == 862920
+    ctx = _frame_ctx(pics)
+    ctx.set_lambda(0, synth.LDP_LAMBDA[22][1])
+    a = ctx.refine(jobs)
+    ref = Reference(use_hadamard=1, nn_mode=1, fast_inter_mode=1)
+    for k, v in pics.items():
+        ref.set_picture(k, v)
+    ref.set_lambda(0, synth.LDP_LAMBDA[22][1])
+    ref.load_nn(weights.load_weights(22))
+    want = np.concatenate([ref.refine(jobs[i:i + 50000]) for i in range(0, len(jobs), 50000)])
+    fields = ("mv_int_x", "mv_int_y", "half_x", "half_y", "qtr_x", "qtr_y", "frac_cost", "c", "n_emi",
+              "nn_class", "mv_x", "mv_y", "bits", "cost")
+    bad, first, counts = compare_results(a, want, fields)
+    assert bad == 0, f"1080p CTU stream: {bad} of {len(jobs)} jobs differ, first {first}: {counts}"
