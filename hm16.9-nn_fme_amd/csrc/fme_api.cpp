@@ -42,6 +42,15 @@ int fail(int code, const char* fmt, ...) {
   return code;
 }
 
+// The main10 path (cfg.bit_depth 10) covers the sub-pel refinement batch (fme_refine*, the pixel
+// kernel of fme_px.hip) and NN_pred; the 8-bit-only kernels refuse a 10-bit context.
+#define NEED_8BIT(c, fn)                                                                          \
+  do {                                                                                            \
+    if ((c)->cfg.bit_depth != 8)                                                                  \
+      return fail(FME_E_UNSUPPORTED, "%s: bit_depth %d (the 10-bit path covers fme_refine* and "  \
+                  "fme_nn_pred_single)", fn, (c)->cfg.bit_depth);                                 \
+  } while (0)
+
 #define HIP_TRY(expr)                                                                       \
   do {                                                                                      \
     hipError_t _e = (expr);                                                                 \
@@ -209,7 +218,8 @@ const char* fme_last_error(void) { return g_last_error.c_str(); }
 int fme_create(int device, const fme_config* cfg, fme_ctx** out_ctx) {
   if (!cfg || !out_ctx) return fail(FME_E_INVALID, "fme_create: null argument");
   *out_ctx = nullptr;
-  if (cfg->bit_depth != 8) return fail(FME_E_UNSUPPORTED, "fme_create: bit_depth %d (only 8)", cfg->bit_depth);
+  if (cfg->bit_depth != 8 && cfg->bit_depth != 10)
+    return fail(FME_E_UNSUPPORTED, "fme_create: bit_depth %d (8, or 10 for the main10 configurations)", cfg->bit_depth);
   if (cfg->nn_mode < 0 || cfg->nn_mode > 2) return fail(FME_E_INVALID, "fme_create: nn_mode %d", cfg->nn_mode);
   int ndev = 0;
   HIP_TRY(hipGetDeviceCount(&ndev));
@@ -310,7 +320,8 @@ int fme_set_picture(fme_ctx* c, int id, const uint8_t* luma, int stride, int wid
   if (width <= 0 || height <= 0 || stride < width || width > 65535 || height > 65535)
     return fail(FME_E_INVALID, "fme_set_picture: %dx%d stride %d", width, height, stride);
   HIP_TRY(hipSetDevice(c->device));
-  const size_t bytes = (size_t)width * height;
+  const size_t bps = c->cfg.bit_depth > 8 ? 2 : 1;   // bytes per sample (10-bit: uint16 samples)
+  const size_t bytes = (size_t)width * height * bps;
   uint8_t* dst = c->pic_owned[id] ? const_cast<uint8_t*>(c->pics[id].luma) : nullptr;
   if (!dst || c->pic_bytes[id] < bytes) {
     if (dst) HIP_TRY(hipFree(dst));
@@ -319,7 +330,7 @@ int fme_set_picture(fme_ctx* c, int id, const uint8_t* luma, int stride, int wid
     c->pic_bytes[id] = bytes;
   }
   hipStream_t s = static_cast<hipStream_t>(stream);
-  HIP_TRY(hipMemcpy2DAsync(dst, width, luma, stride, width, height, hipMemcpyHostToDevice, s));
+  HIP_TRY(hipMemcpy2DAsync(dst, width * bps, luma, stride * bps, width * bps, height, hipMemcpyHostToDevice, s));
   HIP_TRY(hipStreamSynchronize(s));  // the caller may free its host plane on return
   keep_chroma(c, id, width, height);
   c->pics[id] = PicDesc{dst, width, width, height, c->pics[id].cb, c->pics[id].cr, c->pics[id].cstride, 0};
@@ -344,6 +355,7 @@ int fme_bind_picture_device(fme_ctx* c, int id, const uint8_t* d_luma, int strid
 
 int fme_set_picture_chroma(fme_ctx* c, int id, const uint8_t* cb, const uint8_t* cr, int stride, void* stream) {
   if (!c || !cb || !cr) return fail(FME_E_INVALID, "fme_set_picture_chroma: null argument");
+  NEED_8BIT(c, "fme_set_picture_chroma");
   if (id < 0 || id >= FME_MAX_PICTURES) return fail(FME_E_INVALID, "fme_set_picture_chroma: id %d", id);
   if (!c->pics[id].luma) return fail(FME_E_STATE, "fme_set_picture_chroma: picture %d has no luma plane", id);
   const int cw = c->pics[id].width >> 1, ch = c->pics[id].height >> 1;
@@ -371,6 +383,7 @@ int fme_set_picture_chroma(fme_ctx* c, int id, const uint8_t* cb, const uint8_t*
 
 int fme_bind_picture_chroma_device(fme_ctx* c, int id, const uint8_t* d_cb, const uint8_t* d_cr, int stride) {
   if (!c || !d_cb || !d_cr) return fail(FME_E_INVALID, "fme_bind_picture_chroma_device: null argument");
+  NEED_8BIT(c, "fme_bind_picture_chroma_device");
   if (id < 0 || id >= FME_MAX_PICTURES) return fail(FME_E_INVALID, "fme_bind_picture_chroma_device: id %d", id);
   if (!c->pics[id].luma) return fail(FME_E_STATE, "fme_bind_picture_chroma_device: picture %d has no luma plane", id);
   if (stride < (c->pics[id].width >> 1)) return fail(FME_E_INVALID, "fme_bind_picture_chroma_device: stride %d", stride);
@@ -688,8 +701,9 @@ static int refine_batch(fme_ctx* c, const fme_job* d_jobs, fme_result* d_res, fm
   HIP_TRY(launch_scatter(a, w, s));
   if (prof) HIP_TRY(hipEventRecord(ev[3], s));
   if (c->ev_search) HIP_TRY(hipEventRecord(c->ev_search, s));
-  // the lane kernel: every PU shape, one launch on the batch stream
-  HIP_TRY(launch_search_lane(a, w, s));
+  // the lane kernel: every PU shape, one launch on the batch stream (8-bit); the pixel kernel at
+  // bit depth 10 (fme_px.hip)
+  HIP_TRY(c->cfg.bit_depth > 8 ? launch_search_px(a, w, c->cfg.bit_depth, s) : launch_search_lane(a, w, s));
   if (prof) HIP_TRY(hipEventRecord(ev[4], s));
   if (prof) HIP_TRY(hipEventRecord(ev[5], s));
   HIP_TRY(c->cfg.nn_mode == 2
@@ -764,6 +778,7 @@ int fme_refine_status(fme_ctx* c) {
 static int tz_run(fme_ctx* c, fme_job* d_jobs, const fme_tz_ext* d_ext, uint32_t* d_sad, int n, void* stream,
                   int16_t* d_emi, uint32_t* d_nn_in = nullptr) {
   if (!c || (n > 0 && (!d_jobs || !d_ext))) return fail(FME_E_INVALID, "fme_integer_search_device: null argument");
+  NEED_8BIT(c, "fme_integer_search");
   if (n < 0) return fail(FME_E_INVALID, "fme_integer_search_device: n = %d", n);
   if (n == 0) return FME_OK;
   HIP_TRY(hipSetDevice(c->device));
@@ -845,6 +860,7 @@ static int tz_run(fme_ctx* c, fme_job* d_jobs, const fme_tz_ext* d_ext, uint32_t
 static int tz_run_host(fme_ctx* c, fme_job* jobs, const fme_tz_ext* ext, uint32_t* sad, int n, void* stream,
                        int16_t* emi, uint32_t* nn_in = nullptr) {
   if (!c || (n > 0 && (!jobs || !ext))) return fail(FME_E_INVALID, "fme_integer_search: null argument");
+  NEED_8BIT(c, "fme_integer_search");
   if (n <= 0) return n == 0 ? FME_OK : fail(FME_E_INVALID, "fme_integer_search: n = %d", n);
   HIP_TRY(hipSetDevice(c->device));
   hipStream_t s = static_cast<hipStream_t>(stream);
@@ -1166,6 +1182,7 @@ int fme_frac_dif_single(fme_ctx* c, int lossless, const int16_t* key, int key_st
                         int mvp_y, double motion_lambda, int16_t* half_xy, int16_t* qtr_xy,
                         uint32_t* cost) {
   if (!c || !key || !ref || !half_xy || !qtr_xy || !cost) return fail(FME_E_INVALID, "fme_frac_dif_single: null argument");
+  NEED_8BIT(c, "fme_frac_dif_single");
   const int cls = class_of(w, h);
   if (cls < 0) return fail(FME_E_UNSUPPORTED, "fme_frac_dif_single: %dx%d", w, h);
   const int px = mvp_x - 4 * mv_int_x, py = mvp_y - 4 * mv_int_y;
@@ -1303,6 +1320,7 @@ static const char* mc_job_problem(const fme_ctx* c, const fme_mc_job& j, int wid
 
 static int mc_launch(fme_ctx* c, const fme_mc_job* d_jobs, int n, uint8_t* y, int ys, uint8_t* cb, uint8_t* cr,
                      int cs, int width, int height, hipStream_t s) {
+  NEED_8BIT(c, "fme_motion_compensate");
   HIP_TRY(c->d_mc_invalid.reserve(1));
   HIP_TRY(hipMemsetAsync(c->d_mc_invalid.p, 0, sizeof(int32_t), s));
   if (int e = sync_tables(c, s)) return e;
@@ -1556,6 +1574,7 @@ extern "C" {
 // costs[(i * FME_MAX_REFS + k) * 2 + m]; 0xFFFFFFFF for k >= num_refs or m >= n_cand[k].
 int fme_template_costs(fme_ctx* c, const fme_pu_req* reqs, uint32_t* costs, int n, void* stream) {
   if (!c || (n > 0 && (!reqs || !costs))) return fail(FME_E_INVALID, "fme_template_costs: null argument");
+  NEED_8BIT(c, "fme_template_costs");
   if (n <= 0) return n == 0 ? FME_OK : fail(FME_E_INVALID, "fme_template_costs: n = %d", n);
   HIP_TRY(hipSetDevice(c->device));
   hipStream_t s = static_cast<hipStream_t>(stream);
@@ -1603,6 +1622,7 @@ int fme_template_costs(fme_ctx* c, const fme_pu_req* reqs, uint32_t* costs, int 
 int fme_build_bipred_keys(fme_ctx* c, const fme_bikey_req* reqs, int n, size_t key_count, void* stream) {
   static_assert(sizeof(fme_bikey_req) == sizeof(BiKeyTask), "fme_bikey_req is the kernel's task record");
   if (!c || (n > 0 && !reqs)) return fail(FME_E_INVALID, "fme_build_bipred_keys: null argument");
+  NEED_8BIT(c, "fme_build_bipred_keys");
   if (n < 0) return fail(FME_E_INVALID, "fme_build_bipred_keys: n = %d", n);
   HIP_TRY(hipSetDevice(c->device));
   hipStream_t s = static_cast<hipStream_t>(stream);
@@ -1635,6 +1655,7 @@ int fme_build_bipred_keys(fme_ctx* c, const fme_bikey_req* reqs, int n, size_t k
 // counted, and every later batch whose jobs read keys is rejected until keys are built again.
 int fme_build_bipred_keys_device(fme_ctx* c, const fme_bikey_req* d_reqs, int n, size_t key_count, void* stream) {
   if (!c || (n > 0 && !d_reqs)) return fail(FME_E_INVALID, "fme_build_bipred_keys_device: null argument");
+  NEED_8BIT(c, "fme_build_bipred_keys_device");
   if (n < 0) return fail(FME_E_INVALID, "fme_build_bipred_keys_device: n = %d", n);
   HIP_TRY(hipSetDevice(c->device));
   hipStream_t s = static_cast<hipStream_t>(stream);
@@ -1667,6 +1688,7 @@ int fme_pred_inter_reset(fme_ctx* c) {
 //   4. xCheckBestMVP and the reference choice on the host.
 int fme_pred_inter_p(fme_ctx* c, const fme_pu_req* reqs, fme_pu_res* res, int n, void* stream) {
   if (!c || (n > 0 && (!reqs || !res))) return fail(FME_E_INVALID, "fme_pred_inter_p: null argument");
+  NEED_8BIT(c, "fme_pred_inter_p");
   if (n <= 0) return n == 0 ? FME_OK : fail(FME_E_INVALID, "fme_pred_inter_p: n = %d", n);
   HIP_TRY(hipSetDevice(c->device));
   hipStream_t s = static_cast<hipStream_t>(stream);
@@ -1875,6 +1897,7 @@ int fme_pred_inter_p(fme_ctx* c, const fme_pu_req* reqs, fme_pu_res* res, int n,
 
 int fme_pred_inter_b(fme_ctx* c, const fme_pu_req_b* reqs, fme_pu_res_b* res, int n, void* stream) {
   if (!c || (n > 0 && (!reqs || !res))) return fail(FME_E_INVALID, "fme_pred_inter_b: null argument");
+  NEED_8BIT(c, "fme_pred_inter_b");
   if (n <= 0) return n == 0 ? FME_OK : fail(FME_E_INVALID, "fme_pred_inter_b: n = %d", n);
   const int fen = c->cfg.fast_inter_mode;
   HIP_TRY(hipSetDevice(c->device));

@@ -179,6 +179,9 @@ hipError_t launch_put_tables(PicDesc* d_pics, double* d_ml, const PicDesc* pics,
 // enough workgroups to fill the chip, each pulling tiles from its XCD's queue (then the other
 // XCDs').  `a.n` bounds the work.
 hipError_t launch_search_lane(const BatchArgs& a, const WorkBufs& w, hipStream_t s);
+// Bit depth 10 (main10): the pixel-per-lane search (fme_px.hip), same records as the lane kernel;
+// pictures hold uint16 samples (PicDesc::luma reinterpreted, stride in samples).
+hipError_t launch_search_px(const BatchArgs& a, const WorkBufs& w, int bit_depth, hipStream_t s);
 struct NnIn11 {   // NN_pred() inputs of a single call: array_e slots[8], C, PUHeight, PUWidth
   uint32_t v[11];
 };

@@ -15,6 +15,7 @@
 // computed once into LDS, SATD butterflies across lanes.  Same arithmetic as the batch kernel and
 // the oracle (orc_frac_dif): bit-exact.
 #include "fme_device.h"
+#include "fme_xlane.h"
 
 namespace fme {
 namespace {
@@ -63,34 +64,7 @@ __device__ __forceinline__ void sys_store_release(uint32_t* p, uint32_t v) {
   __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
-// The value of lane ^ m (m a power of two below 64) without the LDS pipe: DPP within a row of 16
-// lanes, v_permlane16/32_swap across rows.
-template <int CTRL>
-__device__ __forceinline__ int dpp_i(int v) { return __builtin_amdgcn_update_dpp(0, v, CTRL, 0xF, 0xF, false); }
-template <int M>
-__device__ __forceinline__ int xor_lane(int v, int lane) {
-  if constexpr (M == 1) return dpp_i<0xB1>(v);          // quad_perm [1, 0, 3, 2]
-  else if constexpr (M == 2) return dpp_i<0x4E>(v);     // quad_perm [2, 3, 0, 1]
-  else if constexpr (M == 4) {                          // row_shl:4 / row_shr:4
-    const int up = dpp_i<0x104>(v), dn = dpp_i<0x114>(v);
-    return (lane & 4) ? dn : up;
-  } else if constexpr (M == 8) return dpp_i<0x128>(v);  // row_ror:8
-  else if constexpr (M == 16) {
-    const auto p = __builtin_amdgcn_permlane16_swap(v, v, false, false);
-    return (lane & 16) ? (int)p[0] : (int)p[1];
-  } else {
-    const auto p = __builtin_amdgcn_permlane32_swap(v, v, false, false);
-    return (lane & 32) ? (int)p[0] : (int)p[1];
-  }
-}
-// Butterfly stage over lane bit M: (a + b, a - b) with a the lower lane's value.
-template <int M>
-__device__ __forceinline__ int bfly(int d, int lane) {
-  const int p = xor_lane<M>(d, lane);
-  return (lane & M) ? p - d : d + p;
-}
-template <int M>
-__device__ __forceinline__ uint32_t xsum(uint32_t a, int lane) { return a + (uint32_t)xor_lane<M>((int)a, lane); }
+using namespace xlane;   // xor_lane, bfly, xsum (fme_xlane.h)
 
 // TComRdCost::xGetExpGolombNumberOfBits (TComRdCost.cpp:172-185): 2 * floor(log2 t) + 1
 __device__ __forceinline__ uint32_t eg_bits_d(int v) {

@@ -146,9 +146,13 @@ class FmeContext:
     """One device context: pictures, lambdas, keys, NN weights and the carried NN state."""
 
     def __init__(self, device=0, use_hadamard=1, nn_mode=1, qp=22, fast_inter_mode=1, max_jobs=0,
-                 load_nn=True, lib_path=None, net=None, nn_engine=0):
+                 load_nn=True, lib_path=None, net=None, nn_engine=0, bit_depth=8):
+        """bit_depth 10 (the main10 configurations): pictures are uint16 sample planes and the
+        refinement batches run the pixel kernel (fme_px.hip); the other 8-bit-only entry points
+        refuse such a context (FME_E_UNSUPPORTED)."""
         self.lib = load_library(lib_path)
-        self.cfg = FmeConfig(8, use_hadamard, nn_mode, qp, fast_inter_mode, max_jobs)
+        self.bit_depth = int(bit_depth)
+        self.cfg = FmeConfig(self.bit_depth, use_hadamard, nn_mode, qp, fast_inter_mode, max_jobs)
         h = C.c_void_p()
         _check(self.lib, self.lib.fme_create(device, C.byref(self.cfg), C.byref(h)))
         self.h = h
@@ -173,11 +177,12 @@ class FmeContext:
 
     # -- state --------------------------------------------------------------------------
     def set_picture(self, pid, luma, stream=None):
-        luma = np.ascontiguousarray(luma, dtype=np.uint8)
+        luma = np.ascontiguousarray(luma, dtype=np.uint16 if self.bit_depth > 8 else np.uint8)
         h, w = luma.shape
         _check(self.lib, self.lib.fme_set_picture(self.h, pid, _ptr(luma), w, w, h, stream))
 
     def bind_picture_device(self, pid, data_ptr, stride, width, height):
+        """A caller-owned device plane (8-bit samples, or uint16 at bit depth 10; stride in samples)."""
         _check(self.lib, self.lib.fme_bind_picture_device(self.h, pid, C.c_void_p(data_ptr), stride, width, height))
 
     def set_picture_chroma(self, pid, cb, cr, stream=None):

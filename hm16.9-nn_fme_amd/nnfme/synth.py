@@ -56,6 +56,27 @@ def synth_luma(width, height, t, seed=None):
     return np.clip(np.rint(acc), 0, 255).astype(np.uint8)
 
 
+def synth_luma_hbd(width, height, t, bit_depth=10, seed=None):
+    """The same synthetic frame at a higher bit depth (uint16[height, width], main10): the 8-bit
+    frame's field at (bit_depth - 8) more bits of precision plus its own noise, clipped to the range."""
+    if seed is None:
+        seed = SEEDS.get((width, height), 7)
+    rng = np.random.default_rng(seed)
+    a = rng.uniform(10, 40, 12)
+    fx = rng.uniform(0.01, 0.2, 12)
+    fy = rng.uniform(0.01, 0.2, 12)
+    phi = rng.uniform(0, 2 * np.pi, 12)
+    noise = np.random.default_rng(seed * 1000 + t + 1).normal(0, 2, (height, width))
+    x = np.arange(width, dtype=np.float64)[None, :]
+    y = np.arange(height, dtype=np.float64)[:, None]
+    acc = np.full((height, width), 128.0)
+    for i in range(12):
+        acc += a[i] * np.sin(fx[i] * (x + 0.37 * t) + fy[i] * (y + 0.21 * t) + phi[i])
+    acc += noise
+    scale = float(1 << (bit_depth - 8))
+    return np.clip(np.rint(acc * scale), 0, (1 << bit_depth) - 1).astype(np.uint16)
+
+
 def _clip_mv_qpel(v, pos, pic, size_max=MAX_CU):
     """TComDataCU::clipMv on quarter-pel values, with the PU position standing in for the
     CU position (TComDataCU.cpp:2778-2785)."""

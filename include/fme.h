@@ -46,7 +46,12 @@ extern "C" {
 
 /* ---- configuration (TAppEncCfg.cpp options the path depends on) ------------------- */
 typedef struct fme_config {
-  int32_t bit_depth;        /* internal luma bit depth; only 8 is supported              */
+  int32_t bit_depth;        /* internal luma bit depth: 8, or 10 for the main10
+                               configurations (cfg/encoder_*_main10.cfg InternalBitDepth 10):
+                               pictures are then uint16 sample planes (strides in samples) and
+                               the refinement batches (fme_refine*) run the pixel kernel;
+                               integer search, MC, producers, bi-pred key builds and
+                               fme_frac_dif_single return FME_E_UNSUPPORTED at 10 bits       */
   int32_t use_hadamard;     /* HadamardME (TAppEncCfg.cpp:760): SATD vs SAD in FracDIF   */
   int32_t nn_mode;          /* 0: standard FracDIF MV (TEncSearch.cpp:4587-4588 variant)
                                1: NN_pred() MV (shipped behaviour, TEncSearch.cpp:4590-4591)
@@ -147,7 +152,8 @@ int         fme_destroy(fme_ctx* ctx);
 const char* fme_last_error(void);
 
 /* ---- pictures ----------------------------------------------------------------------- *
- * 8-bit luma planes, unpadded (width x height, row stride in bytes).  The path reads
+ * 8-bit luma planes, unpadded (width x height, row stride in bytes; at bit_depth 10 `luma`
+ * points to uint16_t samples and the stride counts samples).  The path reads
  * outside the picture with edge replication, which equals HM's padded TComPicYuv
  * (extendPicBorder, TComPicYuv.cpp:229-276) for every MV TComDataCU::clipMv admits.  */
 int fme_set_picture(fme_ctx* ctx, int id, const uint8_t* luma, int stride, int width, int height,

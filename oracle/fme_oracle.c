@@ -54,33 +54,43 @@ static inline uint32_t mv_bits(int x, int y, int scale, int px, int py) {
 static inline int ref_px(const orc_picture* p, int x, int y) {
   x = clampi(x, 0, p->width - 1);
   y = clampi(y, 0, p->height - 1);
-  return p->luma[(size_t)y * p->stride + x];
+  return p->luma16 ? p->luma16[(size_t)y * p->stride + x] : p->luma[(size_t)y * p->stride + x];
 }
+static inline int pic_bd(const orc_picture* p) { return p->bd > 8 ? p->bd : 8; }
+/* headRoom = max(2, IF_INTERNAL_PREC - bitDepth): filterCopy's shift and the filters' headroom
+ * (TComInterpolationFilter.cpp:113, 129, 201) - 6 at 8 bits, 4 at 10 */
+static inline int if_headroom(int bd) { return 14 - bd < 2 ? 2 : 14 - bd; }
 
 /* First (horizontal) stage output at integer row y: the 14-bit value the reference stores
  * in m_filteredBlockTmp[fx] (filterHor with isLast=false: filterCopy isFirst branch for
- * fx==0, TComInterpolationFilter.cpp:111-124; filter<8,false,true,false> otherwise,
- * :196-252 with shift 0 and offset -8192). */
+ * fx==0, TComInterpolationFilter.cpp:111-124, (s << headRoom) - 8192; filter<8,false,true,false>
+ * otherwise, :196-252 with shift 6 - headRoom and offset -8192 << shift: shift 0 at 8 bits, 2 at
+ * 10).  Stored as Pel (int16). */
 static inline int hor_stage(const orc_picture* p, int x, int y, int fx) {
-  if (fx == 0) return (ref_px(p, x, y) << 6) - 8192;
+  const int hr = if_headroom(pic_bd(p));
+  if (fx == 0) return (ref_px(p, x, y) << hr) - 8192;
+  const int sh = 6 - hr;
   int s = 0;
   for (int k = 0; k < 8; k++) s += kLuma[fx][k] * ref_px(p, x + k - 3, y);
-  return (int)(int16_t)(s - 8192);
+  return (int)(int16_t)((s - 8192 * (1 << sh)) >> sh);
 }
 
 /* Second (vertical, isLast) stage: filterCopy !isFirst branch for fy==0
- * (TComInterpolationFilter.cpp:126-150) and filter<8,true,false,true> otherwise
- * (shift 12, offset 2048 + (8192 << 6), clip to [0,255]). */
+ * (TComInterpolationFilter.cpp:126-150: (v + 8192 + (1 << (headRoom-1))) >> headRoom) and
+ * filter<8,true,false,true> otherwise (shift 6 + headRoom, offset (1 << (shift-1)) + (8192 << 6):
+ * 12 / 2048 at 8 bits, 10 / 512 at 10), clipped to [0, (1 << bitDepth) - 1]. */
 int orc_pred_sample(const orc_picture* p, int x, int y, int fx, int fy) {
+  const int bd = pic_bd(p), hr = if_headroom(bd);
   int v;
   if (fy == 0) {
-    v = (hor_stage(p, x, y, fx) + 8192 + 32) >> 6;
+    v = (hor_stage(p, x, y, fx) + 8192 + (1 << (hr - 1))) >> hr;
   } else {
+    const int sh = 6 + hr;
     int s = 0;
     for (int k = 0; k < 8; k++) s += kLuma[fy][k] * hor_stage(p, x, y + k - 3, fx);
-    v = (s + 2048 + (8192 << 6)) >> 12;
+    v = (s + (1 << (sh - 1)) + (8192 << 6)) >> sh;
   }
-  return clampi(v, 0, 255);
+  return clampi(v, 0, (1 << bd) - 1);
 }
 
 /* Prediction block of a PU at (x0,y0) displaced by quarter-pel (qx,qy). */
@@ -176,14 +186,23 @@ uint32_t orc_sse(const int16_t* org, int os, const int16_t* cur, int cs, int w, 
 
 /* Integer-ME metric selected by the modified setDistParam (TComRdCost.cpp:200-230):
  * SSE for W in {4,8,16,32,64}; SAD for 12/24/48 with the FEN even-row subsampling of
- * xTZSearchHelp (TEncSearch.cpp:1158-1164). */
+ * xTZSearchHelp (TEncSearch.cpp:1158-1164).  Above 8 bits DISTORTION_PRECISION_ADJUSTMENT
+ * (TypeDef.h:140-143, FULL_NBIT 0) drops bits: SAD >> (bd - 8) over the block (TComRdCost.cpp:
+ * 370-536), SSE (d * d) >> 2 (bd - 8) per sample (:875-1130). */
 static uint32_t int_dist(const int16_t* key, int ks, const int16_t* cur, int cs, int w, int h,
-                         int fen) {
+                         int fen, int bd) {
   if (w == 12 || w == 24 || w == 48) {
     int sub = ((fen == 1 || fen == 3) && h > 8) ? 1 : 0;
-    return orc_sad(key, ks, cur, cs, w, h, sub);
+    return orc_sad(key, ks, cur, cs, w, h, sub) >> (bd - 8);
   }
-  return orc_sse(key, ks, cur, cs, w, h);
+  if (bd == 8) return orc_sse(key, ks, cur, cs, w, h);
+  uint32_t s = 0;
+  for (int y = 0; y < h; y++)
+    for (int x = 0; x < w; x++) {
+      const int d = key[y * ks + x] - cur[y * cs + x];
+      s += (uint32_t)(d * d) >> (2 * (bd - 8));
+    }
+  return s;
 }
 
 /* xPatternSearchFracDIF (TEncSearch.cpp:5232-5269) with xPatternRefinement (1591-1645):
@@ -193,12 +212,13 @@ void orc_frac_dif(const orc_picture* p, const int16_t* key, int ks, int x0, int 
                   int mv_x, int mv_y, int mvp_x, int mvp_y, double mlambda, int use_hadamard,
                   int8_t half[2], int8_t qtr[2], uint32_t* cost) {
   int16_t* pred = (int16_t*)malloc(sizeof(int16_t) * (size_t)w * h);
+  const int dsh = pic_bd(p) - 8;   /* xGetHADs / xGetSAD: uiSum >> (bitDepth - 8) */
   uint32_t best = 0xFFFFFFFFu;
   int bi = 0;
   for (int i = 0; i < 9; i++) {
     const int dx = kRefineH[i][0], dy = kRefineH[i][1];
     orc_pred_block(p, x0, y0, w, h, 4 * mv_x + 2 * dx, 4 * mv_y + 2 * dy, pred);
-    uint32_t d = use_hadamard ? orc_satd(key, ks, pred, w, w, h) : orc_sad(key, ks, pred, w, w, h, 0);
+    uint32_t d = (use_hadamard ? orc_satd(key, ks, pred, w, w, h) : orc_sad(key, ks, pred, w, w, h, 0)) >> dsh;
     d += orc_cost(mlambda, mv_bits(2 * mv_x + dx, 2 * mv_y + dy, 1, mvp_x, mvp_y));
     if (d < best) {
       best = d;
@@ -212,7 +232,7 @@ void orc_frac_dif(const orc_picture* p, const int16_t* key, int ks, int x0, int 
     const int dx = kRefineQ[i][0], dy = kRefineQ[i][1];
     const int qx = 4 * mv_x + 2 * hx + dx, qy = 4 * mv_y + 2 * hy + dy;
     orc_pred_block(p, x0, y0, w, h, qx, qy, pred);
-    uint32_t d = use_hadamard ? orc_satd(key, ks, pred, w, w, h) : orc_sad(key, ks, pred, w, w, h, 0);
+    uint32_t d = (use_hadamard ? orc_satd(key, ks, pred, w, w, h) : orc_sad(key, ks, pred, w, w, h, 0)) >> dsh;
     d += orc_cost(mlambda, mv_bits(qx, qy, 0, mvp_x, mvp_y));
     if (d < best) {
       best = d;
@@ -261,14 +281,14 @@ int orc_emi(const orc_picture* p, const int16_t* key, int ks, int x0, int y0, in
             double mlambda, int fen, uint32_t emi[8], int* best_x, int* best_y, uint32_t* c) {
   int16_t* cur = (int16_t*)malloc(sizeof(int16_t) * (size_t)w * h);
   orc_pred_block(p, x0, y0, w, h, 4 * sx, 4 * sy, cur);
-  uint32_t best_sad = int_dist(key, ks, cur, w, w, h, fen) +
+  uint32_t best_sad = int_dist(key, ks, cur, w, w, h, fen, pic_bd(p)) +
                       orc_cost(mlambda, mv_bits(sx, sy, 2, mvp_x, mvp_y));
   int bx = sx, by = sy;
   int pts[8][2];
   const int n = square_points(sx, sy, lt_x, lt_y, rb_x, rb_y, pts);
   for (int i = 0; i < n; i++) {
     orc_pred_block(p, x0, y0, w, h, 4 * pts[i][0], 4 * pts[i][1], cur);
-    uint32_t d = int_dist(key, ks, cur, w, w, h, fen);
+    uint32_t d = int_dist(key, ks, cur, w, w, h, fen, pic_bd(p));
     emi[i] = d;
     if (d < best_sad) {
       d += orc_cost(mlambda, mv_bits(pts[i][0], pts[i][1], 2, mvp_x, mvp_y));
@@ -475,6 +495,16 @@ void orc_init(orc_ctx* ctx, const fme_config* cfg) {
 }
 void orc_set_picture(orc_ctx* ctx, int id, const uint8_t* luma, int stride, int w, int h) {
   ctx->pics[id].luma = luma;
+  ctx->pics[id].luma16 = NULL;
+  ctx->pics[id].bd = 8;
+  ctx->pics[id].stride = stride;
+  ctx->pics[id].width = w;
+  ctx->pics[id].height = h;
+}
+void orc_set_picture16(orc_ctx* ctx, int id, const uint16_t* luma, int stride, int w, int h) {
+  ctx->pics[id].luma = NULL;
+  ctx->pics[id].luma16 = luma;
+  ctx->pics[id].bd = ctx->cfg.bit_depth;
   ctx->pics[id].stride = stride;
   ctx->pics[id].width = w;
   ctx->pics[id].height = h;
@@ -538,15 +568,15 @@ int orc_refine(orc_ctx* ctx, const fme_job* jobs, fme_result* res, int n) {
     }
     const orc_picture* ref = &ctx->pics[j->ref_id];
     const orc_picture* org = &ctx->pics[j->org_id];
-    if (!ref->luma) { free(key); return FME_E_STATE; }
+    if (!ref->luma && !ref->luma16) { free(key); return FME_E_STATE; }
     const int w = j->w, h = j->h;
     if (j->key_offset >= 0) {
       if ((size_t)j->key_offset + (size_t)w * h > ctx->n_keys) { free(key); return FME_E_INVALID; }
       memcpy(key, ctx->keys + j->key_offset, sizeof(int16_t) * w * h);
     } else {
-      if (!org->luma) { free(key); return FME_E_STATE; }
+      if (!org->luma && !org->luma16) { free(key); return FME_E_STATE; }
       for (int y = 0; y < h; y++)
-        for (int x = 0; x < w; x++) key[y * w + x] = org->luma[(size_t)(j->y + y) * org->stride + j->x + x];
+        for (int x = 0; x < w; x++) key[y * w + x] = (int16_t)ref_px(org, j->x + x, j->y + y);
     }
     const double ml = ctx->mlambda[j->lambda_id];
     int mvx = j->mv_x, mvy = j->mv_y;
@@ -819,7 +849,7 @@ static void tz_count(int w, int h, int fen) {
 static void tz_help(tz_state* s, int x, int y, int point_nr, int dist) {
   tz_count(s->w, s->h, s->fen);
   orc_pred_block(s->ref, s->x0, s->y0, s->w, s->h, 4 * x, 4 * y, s->cur);
-  uint32_t d = int_dist(s->key, s->w, s->cur, s->w, s->w, s->h, s->fen);
+  uint32_t d = int_dist(s->key, s->w, s->cur, s->w, s->w, s->h, s->fen, pic_bd(s->ref));
   if (s->ring) { /* array_e[counter_i] = uiSad (Backups/4:659) */
     if (!s->after) s->cmin = d < s->cmin ? d : s->cmin;
     else if (s->npush < 8) s->e[s->npush++] = d;
@@ -1061,15 +1091,15 @@ int orc_integer_search_ring(orc_ctx* ctx, fme_job* jobs, const fme_tz_ext* ext, 
     }
     const orc_picture* ref = &ctx->pics[j->ref_id];
     const orc_picture* org = &ctx->pics[j->org_id];
-    if (!ref->luma) { free(key); free(cur); return FME_E_STATE; }
+    if (!ref->luma && !ref->luma16) { free(key); free(cur); return FME_E_STATE; }
     const int w = j->w, h = j->h;
     if (j->key_offset >= 0) {
       if ((size_t)j->key_offset + (size_t)w * h > ctx->n_keys) { free(key); free(cur); return FME_E_INVALID; }
       memcpy(key, ctx->keys + j->key_offset, sizeof(int16_t) * w * h);
     } else {
-      if (!org->luma) { free(key); free(cur); return FME_E_STATE; }
+      if (!org->luma && !org->luma16) { free(key); free(cur); return FME_E_STATE; }
       for (int y = 0; y < h; y++)
-        for (int x = 0; x < w; x++) key[y * w + x] = org->luma[(size_t)(j->y + y) * org->stride + j->x + x];
+        for (int x = 0; x < w; x++) key[y * w + x] = (int16_t)ref_px(org, j->x + x, j->y + y);
     }
     tz_state s;
     memset(&s, 0, sizeof(s));
@@ -1085,7 +1115,7 @@ int orc_integer_search_ring(orc_ctx* ctx, fme_job* jobs, const fme_tz_ext* ext, 
         for (int x = j->lt_x; x <= j->rb_x; x++) {
           tz_count(w, h, s.fen);
           orc_pred_block(ref, j->x, j->y, w, h, 4 * x, 4 * y, cur);
-          const uint32_t d = int_dist(key, w, cur, w, w, h, s.fen) + orc_cost(s.ml, mv_bits(x, y, 2, s.mvp_x, s.mvp_y));
+          const uint32_t d = int_dist(key, w, cur, w, w, h, s.fen, pic_bd(ref)) + orc_cost(s.ml, mv_bits(x, y, 2, s.mvp_x, s.mvp_y));
           if (d < s.best_sad) { s.best_sad = d; s.best_x = x; s.best_y = y; }
         }
     } else {

@@ -27,8 +27,10 @@ extern "C" {
 #endif
 
 typedef struct orc_picture {
-  const uint8_t* luma;
+  const uint8_t* luma;     /* 8-bit samples, or NULL when luma16 is set                        */
   int stride, width, height;
+  const uint16_t* luma16;  /* bit depths 9..12 (main10): 16-bit samples, stride in samples      */
+  int bd;                  /* the picture's bit depth (8 with luma)                              */
 } orc_picture;
 
 /* Carried NN_pred() global state: array_e storage, C, PUHeight, PUWidth (TEncSearch.cpp:55-57). */
@@ -112,6 +114,8 @@ int orc_nn_net_forward_pre(orc_ctx* ctx, const uint32_t e[8], uint32_t c, int pu
 /* context helpers */
 void orc_init(orc_ctx* ctx, const fme_config* cfg);
 void orc_set_picture(orc_ctx* ctx, int id, const uint8_t* luma, int stride, int w, int h);
+/* cfg.bit_depth 9..12 (main10 = 10): 16-bit samples, stride in samples */
+void orc_set_picture16(orc_ctx* ctx, int id, const uint16_t* luma, int stride, int w, int h);
 void orc_set_lambda(orc_ctx* ctx, int id, double lambda);
 void orc_set_motion_lambda(orc_ctx* ctx, int id, double mlambda);
 void orc_set_keys(orc_ctx* ctx, const int16_t* keys, size_t n);

@@ -57,9 +57,17 @@ def edge_jobs(rng, width, height, n):
     return j
 
 
-def build_case(name, seed, width, height, n_jobs, hadme, fen, nn_mode, qp, bipred=0.15, n_edge=96, net=None, gop="ldp"):
+def build_case(name, seed, width, height, n_jobs, hadme, fen, nn_mode, qp, bipred=0.15, n_edge=96, net=None, gop="ldp",
+               bit_depth=8):
+    """bit_depth 10: the main10 configurations (cfg/encoder_lowdelay_P_main10.cfg:58): 16-bit
+    pictures, _ref's TComInterpolationFilter / TComRdCost run with bitDepth 10.  The lambdas are the
+    8-bit ones: HM scales the QP by 6 * (bitDepth - 8 - DISTORTION_PRECISION_ADJUSTMENT(bitDepth - 8))
+    = 0 in the shipped build (TypeDef.h:140-143, FULL_NBIT 0), so lambda does not change."""
     rng = np.random.default_rng(seed)
-    pics = {i: synth.synth_luma(width, height, i, seed=seed) for i in range(5)}
+    if bit_depth > 8:
+        pics = {i: synth.synth_luma_hbd(width, height, i, bit_depth, seed=seed) for i in range(5)}
+    else:
+        pics = {i: synth.synth_luma(width, height, i, seed=seed) for i in range(5)}
     if gop == "ra":   # random-access GOP-8 lambdas (TEncSlice.cpp:246-325): entries POC 8, 4, 2, 1
         lambdas = np.array([synth.ra_lambda(qp, e) for e in range(4)], dtype=np.float64)
     else:
@@ -70,8 +78,8 @@ def build_case(name, seed, width, height, n_jobs, hadme, fen, nn_mode, qp, bipre
     # recompute the bi-pred keys over the final order
     jobs["key_offset"][(jobs["flags"] & JOB_BIPRED) != 0] = -2
     keys = synth.make_bipred_keys(rng, jobs, pics)
-    ref = Reference(use_hadamard=hadme, nn_mode=nn_mode, fast_inter_mode=fen)
-    orc = Oracle(use_hadamard=hadme, nn_mode=nn_mode, qp=qp, fast_inter_mode=fen)
+    ref = Reference(use_hadamard=hadme, nn_mode=nn_mode, fast_inter_mode=fen, bit_depth=bit_depth)
+    orc = Oracle(use_hadamard=hadme, nn_mode=nn_mode, qp=qp, fast_inter_mode=fen, bit_depth=bit_depth)
     wts = weights.load_weights(qp)
     for eng in (ref, orc):
         for k, v in pics.items():
@@ -97,6 +105,7 @@ def build_case(name, seed, width, height, n_jobs, hadme, fen, nn_mode, qp, bipre
         results=r_ref,
         config=np.array([hadme, fen, nn_mode, qp], dtype=np.int32),
         **({"net": np.array(net)} if net is not None else {}),
+        **({"bit_depth": np.array([bit_depth], np.int32)} if bit_depth != 8 else {}),
     )
     print(f"{path}: {len(jobs)} jobs, {int((jobs['flags'] & JOB_BIPRED != 0).sum())} bi-pred, "
           f"{int((r_ref['n_emi'] < 8).sum())} with < 8 EMI pushes")
@@ -268,6 +277,17 @@ CASES = [
 ]
 
 
+# main10 (InternalBitDepth 10, cfg/encoder_lowdelay_P_main10.cfg:58 and the RA / LD main10 cfgs):
+# the sub-pel path with 16-bit pictures; every PU shape, edges, lossless jobs, bi-pred keys
+MAIN10_CASES = [
+    # name, seed, W, H, jobs, HADME, FEN, nn_mode, QP, bi-pred, edge jobs, net, gop, bit depth
+    ("main10_ldp_qp22_hadme_fen1_nn", 51, 160, 96, 1200, 1, 1, 1, 22, 0.15, 96, None, "ldp", 10),
+    ("main10_sad_fen0_nnoff", 52, 160, 96, 600, 0, 0, 0, 22, 0.15, 96, None, "ldp", 10),
+    ("main10_fen3_qp27_nn", 53, 128, 96, 500, 1, 3, 1, 27, 0.15, 96, None, "ldp", 10),
+    ("main10_ra_qp37_nn", 54, 128, 96, 500, 1, 1, 1, 37, 0.205, 96, None, "ra", 10),
+]
+
+
 # nn_mode 2: the reference's deeper nets (BASELINE.json configs[4]) and the master net through the
 # generic path.  nn4x40 runs with its X3/X4 carry cleared ("+rezero"): the batch engines do not run
 # carried hidden layers (fme_load_nn_net rejects carry_hidden); the oracle and _ref cover both.
@@ -290,6 +310,10 @@ def main():
         for c in DEEP_CASES:
             build_case(*c)
         return 0
+    if "--main10-only" in sys.argv:
+        for c in MAIN10_CASES:
+            build_case(*c)
+        return 0
     if "--ring-only" in sys.argv:
         for c in RING_CASES:
             build_ring_case(*c)
@@ -299,7 +323,7 @@ def main():
     for c in DEEP_CASES:
         build_case(*c)
     if "--mc-only" not in sys.argv and "--tz-only" not in sys.argv:
-        for c in CASES:
+        for c in CASES + MAIN10_CASES:
             build_case(*c)
     if "--tz-only" not in sys.argv:
         for c in MC_CASES:

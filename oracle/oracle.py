@@ -34,8 +34,9 @@ def _load(path):
 class Oracle:
     """Plain-C restatement (fme_oracle.c)."""
 
-    def __init__(self, use_hadamard=1, nn_mode=1, qp=22, fast_inter_mode=1):
+    def __init__(self, use_hadamard=1, nn_mode=1, qp=22, fast_inter_mode=1, bit_depth=8):
         self.lib = lib = _load(ORACLE_SO)
+        self.bit_depth = bit_depth
         lib.orc_ctx_size.restype = C.c_size_t
         lib.orc_eg_bits.restype = C.c_uint32
         lib.orc_eg_bits.argtypes = [C.c_int]
@@ -54,6 +55,7 @@ class Oracle:
         lib.orc_emi_push_count.argtypes = [C.c_int] * 6
         lib.orc_init.argtypes = [_P, _P]
         lib.orc_set_picture.argtypes = [_P, C.c_int, _P, C.c_int, C.c_int, C.c_int]
+        lib.orc_set_picture16.argtypes = [_P, C.c_int, _P, C.c_int, C.c_int, C.c_int]
         lib.orc_set_lambda.argtypes = [_P, C.c_int, C.c_double]
         lib.orc_set_motion_lambda.argtypes = [_P, C.c_int, C.c_double]
         lib.orc_set_keys.argtypes = [_P, _P, C.c_size_t]
@@ -89,11 +91,17 @@ class Oracle:
         lib.orc_nn_net_forward_pre.argtypes = [_P, _P, C.c_uint32, C.c_int, C.c_int, _P, _P]
         self._buf = C.create_string_buffer(lib.orc_ctx_size())
         self.ctx = C.cast(self._buf, C.c_void_p)
-        cfg = _ConfigStruct(8, use_hadamard, nn_mode, qp, fast_inter_mode, 0)
+        cfg = _ConfigStruct(bit_depth, use_hadamard, nn_mode, qp, fast_inter_mode, 0)
         lib.orc_init(self.ctx, C.byref(cfg))
         self._keep = {}
 
     def set_picture(self, pid, luma):
+        """8-bit planes (uint8), or 16-bit samples (uint16) of the context's bit depth (main10)."""
+        if self.bit_depth > 8:
+            luma = np.ascontiguousarray(luma, dtype=np.uint16)
+            self._keep[("pic", pid)] = luma
+            self.lib.orc_set_picture16(self.ctx, pid, _ptr(luma), luma.shape[1], luma.shape[1], luma.shape[0])
+            return
         luma = np.ascontiguousarray(luma, dtype=np.uint8)
         self._keep[("pic", pid)] = luma
         self.lib.orc_set_picture(self.ctx, pid, _ptr(luma), luma.shape[1], luma.shape[1], luma.shape[0])
@@ -262,8 +270,9 @@ class Oracle:
         out = np.zeros((h, w), dtype=np.int16)
         # build an orc_picture on the fly: {const uint8_t*, int stride, width, height}
         class Pic(C.Structure):
-            _fields_ = [("luma", C.c_void_p), ("stride", C.c_int), ("width", C.c_int), ("height", C.c_int)]
-        p = Pic(luma.ctypes.data, luma.shape[1], luma.shape[1], luma.shape[0])
+            _fields_ = [("luma", C.c_void_p), ("stride", C.c_int), ("width", C.c_int), ("height", C.c_int),
+                        ("luma16", C.c_void_p), ("bd", C.c_int)]
+        p = Pic(luma.ctypes.data, luma.shape[1], luma.shape[1], luma.shape[0], None, 8)
         self.lib.orc_pred_block(C.byref(p), x0, y0, w, h, qx, qy, _ptr(out))
         return out
 
@@ -271,12 +280,15 @@ class Oracle:
 class Reference:
     """The reference's own TLibCommon primitives driven in TEncSearch order (_ref)."""
 
-    def __init__(self, use_hadamard=1, nn_mode=1, fast_inter_mode=1):
+    def __init__(self, use_hadamard=1, nn_mode=1, fast_inter_mode=1, bit_depth=8):
         self.lib = lib = _load(REF_SO)
+        self.bit_depth = bit_depth
         lib.ref_create.restype = C.c_void_p
         lib.ref_create.argtypes = [C.c_int, C.c_int, C.c_int]
         lib.ref_destroy.argtypes = [_P]
         lib.ref_set_picture.argtypes = [_P, C.c_int, _P, C.c_int, C.c_int, C.c_int]
+        lib.ref_set_picture16.argtypes = [_P, C.c_int, _P, C.c_int, C.c_int, C.c_int]
+        lib.ref_set_bit_depth.argtypes = [_P, C.c_int]
         lib.ref_set_lambda.argtypes = [_P, C.c_int, C.c_double]
         lib.ref_set_keys.argtypes = [_P, _P, C.c_size_t]
         lib.ref_load_nn.argtypes = [_P, _P]
@@ -307,6 +319,8 @@ class Reference:
         lib.ref_mc.restype = C.c_int
         lib.ref_mc.argtypes = [_P, _P, C.c_int, _P, C.c_int, _P, _P, C.c_int, C.c_int, C.c_int]
         self.h = lib.ref_create(use_hadamard, fast_inter_mode, nn_mode)
+        if bit_depth != 8:
+            lib.ref_set_bit_depth(self.h, bit_depth)
 
     def __del__(self):
         try:
@@ -315,6 +329,11 @@ class Reference:
             pass
 
     def set_picture(self, pid, luma):
+        """8-bit planes, or 16-bit samples at the harness's bit depth (main10)."""
+        if self.bit_depth > 8:
+            luma = np.ascontiguousarray(luma, dtype=np.uint16)
+            self.lib.ref_set_picture16(self.h, pid, _ptr(luma), luma.shape[1], luma.shape[1], luma.shape[0])
+            return
         luma = np.ascontiguousarray(luma, dtype=np.uint8)
         self.lib.ref_set_picture(self.h, pid, _ptr(luma), luma.shape[1], luma.shape[1], luma.shape[0])
 

@@ -45,6 +45,7 @@ class RefSearch : public TComPrediction {
   DistParam dp;
   bool hadme = true;
   int fen = 0;
+  int bd = 8;   // the sequence's luma bit depth (m_cDistParam.bitDepth, TEncSearch.cpp:1090, 1630)
 
   RefSearch() {
     initTempBuff(CHROMA_400);
@@ -52,10 +53,10 @@ class RefSearch : public TComPrediction {
   }
 
   void setLambda(double lambda) {
-    BitDepths bd;
-    bd.recon[CHANNEL_TYPE_LUMA] = 8;
-    bd.recon[CHANNEL_TYPE_CHROMA] = 8;
-    rd.setLambda(lambda, bd);
+    BitDepths bds;
+    bds.recon[CHANNEL_TYPE_LUMA] = bd;
+    bds.recon[CHANNEL_TYPE_CHROMA] = bd;
+    rd.setLambda(lambda, bds);
     rd.selectMotionLambda(true, 0, false);
   }
 
@@ -64,14 +65,14 @@ class RefSearch : public TComPrediction {
     const int ts = m_filteredBlockTmp[0].getStride(COMPONENT_Y);
     const int ds = m_filteredBlock[0][0].getStride(COMPONENT_Y);
     Pel* src = roi - 4 * stride - 1;  // half filter size rows up, one column left
-    m_if.filterHor(COMPONENT_Y, src, stride, m_filteredBlockTmp[0].getAddr(COMPONENT_Y), ts, w + 1, h + 8, 0, false, CHROMA_400, 8);
-    m_if.filterHor(COMPONENT_Y, src, stride, m_filteredBlockTmp[2].getAddr(COMPONENT_Y), ts, w + 1, h + 8, 2, false, CHROMA_400, 8);
+    m_if.filterHor(COMPONENT_Y, src, stride, m_filteredBlockTmp[0].getAddr(COMPONENT_Y), ts, w + 1, h + 8, 0, false, CHROMA_400, bd);
+    m_if.filterHor(COMPONENT_Y, src, stride, m_filteredBlockTmp[2].getAddr(COMPONENT_Y), ts, w + 1, h + 8, 2, false, CHROMA_400, bd);
     Pel* t0 = m_filteredBlockTmp[0].getAddr(COMPONENT_Y);
     Pel* t2 = m_filteredBlockTmp[2].getAddr(COMPONENT_Y);
-    m_if.filterVer(COMPONENT_Y, t0 + 4 * ts + 1, ts, m_filteredBlock[0][0].getAddr(COMPONENT_Y), ds, w, h, 0, false, true, CHROMA_400, 8);
-    m_if.filterVer(COMPONENT_Y, t0 + 3 * ts + 1, ts, m_filteredBlock[2][0].getAddr(COMPONENT_Y), ds, w, h + 1, 2, false, true, CHROMA_400, 8);
-    m_if.filterVer(COMPONENT_Y, t2 + 4 * ts, ts, m_filteredBlock[0][2].getAddr(COMPONENT_Y), ds, w + 1, h, 0, false, true, CHROMA_400, 8);
-    m_if.filterVer(COMPONENT_Y, t2 + 3 * ts, ts, m_filteredBlock[2][2].getAddr(COMPONENT_Y), ds, w + 1, h + 1, 2, false, true, CHROMA_400, 8);
+    m_if.filterVer(COMPONENT_Y, t0 + 4 * ts + 1, ts, m_filteredBlock[0][0].getAddr(COMPONENT_Y), ds, w, h, 0, false, true, CHROMA_400, bd);
+    m_if.filterVer(COMPONENT_Y, t0 + 3 * ts + 1, ts, m_filteredBlock[2][0].getAddr(COMPONENT_Y), ds, w, h + 1, 2, false, true, CHROMA_400, bd);
+    m_if.filterVer(COMPONENT_Y, t2 + 4 * ts, ts, m_filteredBlock[0][2].getAddr(COMPONENT_Y), ds, w + 1, h, 0, false, true, CHROMA_400, bd);
+    m_if.filterVer(COMPONENT_Y, t2 + 3 * ts, ts, m_filteredBlock[2][2].getAddr(COMPONENT_Y), ds, w + 1, h + 1, 2, false, true, CHROMA_400, bd);
   }
 
   // --- quarter-pel planes around the best half position (xExtDIFUpSamplingQ) ---------
@@ -86,10 +87,10 @@ class RefSearch : public TComPrediction {
     Pel* t1 = m_filteredBlockTmp[1].getAddr(COMPONENT_Y);
     Pel* t2 = m_filteredBlockTmp[2].getAddr(COMPONENT_Y);
     Pel* t3 = m_filteredBlockTmp[3].getAddr(COMPONENT_Y);
-    m_if.filterHor(COMPONENT_Y, s1, stride, t1, ts, w, extH, 1, false, CHROMA_400, 8);
-    m_if.filterHor(COMPONENT_Y, s3, stride, t3, ts, w, extH, 3, false, CHROMA_400, 8);
+    m_if.filterHor(COMPONENT_Y, s1, stride, t1, ts, w, extH, 1, false, CHROMA_400, bd);
+    m_if.filterHor(COMPONENT_Y, s3, stride, t3, ts, w, extH, 3, false, CHROMA_400, bd);
     auto ver = [&](Pel* src, int fy, int dy, int dx) {
-      m_if.filterVer(COMPONENT_Y, src, ts, m_filteredBlock[dy][dx].getAddr(COMPONENT_Y), ds, w, h, fy, false, true, CHROMA_400, 8);
+      m_if.filterVer(COMPONENT_Y, src, ts, m_filteredBlock[dy][dx].getAddr(COMPONENT_Y), ds, w, h, fy, false, true, CHROMA_400, bd);
     };
     const int rowTop = 3 * ts;      // (halfFilterSize - 1) rows
     const int rowZero = hy == 0 ? ts : 0;
@@ -128,7 +129,7 @@ class RefSearch : public TComPrediction {
       if (hv == 2 && (vv & 1) == 0) p += 1;
       if ((hv & 1) == 0 && vv == 2) p += rs;
       dp.pCur = p;
-      dp.bitDepth = 8;
+      dp.bitDepth = bd;
       Distortion d = dp.DistFunc(&dp);
       d += rd.getCostOfVectorWithPredictor(tab[i][0] + mvx, tab[i][1] + mvy);
       if (d < best) {
@@ -168,7 +169,7 @@ class RefSearch : public TComPrediction {
   };
   Distortion intDist(TComPattern* key, Pel* refY, int stride, int x, int y) {
     rd.setDistParam(key, refY + y * stride + x, stride, dp);
-    dp.bitDepth = 8;
+    dp.bitDepth = bd;
     if ((fen == 1 || fen == 3) && dp.iRows > 8) dp.iSubShift = 1;
     return dp.DistFunc(&dp);
   }
@@ -364,6 +365,22 @@ int ref_set_picture(void* h, int id, const uint8_t* luma, int stride, int w, int
   return 0;
 }
 
+// main10: the luma bit depth of the sub-pel path (ref_refine) and 16-bit sample planes
+void ref_set_bit_depth(void* h, int bd) { static_cast<RefCtx*>(h)->s.bd = bd; }
+
+int ref_set_picture16(void* h, int id, const uint16_t* luma, int stride, int w, int hgt) {
+  RefCtx* c = static_cast<RefCtx*>(h);
+  Pic& p = c->pics[id];
+  p.yuv.createWithoutCUInfo(w, hgt, CHROMA_400, true, 64, 64);  // 80-sample margin
+  Pel* dst = p.yuv.getAddr(COMPONENT_Y);
+  const int ds = p.yuv.getStride(COMPONENT_Y);
+  for (int y = 0; y < hgt; y++)
+    for (int x = 0; x < w; x++) dst[y * ds + x] = (Pel)luma[(size_t)y * stride + x];
+  p.yuv.extendPicBorder();
+  p.set = true;
+  return 0;
+}
+
 void ref_set_lambda(void* h, int id, double lambda) { static_cast<RefCtx*>(h)->lambda[id] = lambda; }
 
 void ref_set_keys(void* h, const int16_t* k, size_t n) {
@@ -472,7 +489,7 @@ int ref_refine(void* h, const fme_job* jobs, fme_result* res, int n) {
         for (int x = 0; x < w; x++) keybuf[y * w + x] = o[y * os + x];
     }
     TComPattern key;
-    key.initPattern(keybuf.data(), w, hh, w, 8);
+    key.initPattern(keybuf.data(), w, hh, w, s.bd);
     s.setLambda(c->lambda[j.lambda_id]);
     TComMv pred(j.mvp_x, j.mvp_y);
     s.rd.setPredictor(pred);
@@ -957,7 +974,7 @@ extern "C" int ref_integer_search_ring(void* h, fme_job* jobs, const fme_tz_ext*
         for (int x = 0; x < w; x++) keybuf[y * w + x] = o[y * os + x];
     }
     TComPattern key;
-    key.initPattern(keybuf.data(), w, hh, w, 8);
+    key.initPattern(keybuf.data(), w, hh, w, s.bd);
     s.setLambda(c->lambda[j.lambda_id]);
     TComMv pred(j.mvp_x, j.mvp_y);
     s.rd.setPredictor(pred);

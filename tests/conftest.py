@@ -35,7 +35,12 @@ def pytest_collection_modifyitems(config, items):
 def golden_cases():
     """Sub-pel refinement fixtures (fme_job -> fme_result)."""
     return sorted(f[:-4] for f in os.listdir(GOLDEN)
-                  if f.endswith(".npz") and not f.startswith(("mc_", "tz_", "ring_")))
+                  if f.endswith(".npz") and not f.startswith(("mc_", "tz_", "ring_", "main10_")))
+
+
+def main10_golden_cases():
+    """Sub-pel refinement fixtures at bit depth 10 (the main10 configurations)."""
+    return sorted(f[:-4] for f in os.listdir(GOLDEN) if f.endswith(".npz") and f.startswith("main10_"))
 
 
 def ring_golden_cases():

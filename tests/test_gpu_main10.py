@@ -1,0 +1,94 @@
+"""Bit depth 10 (the main10 configurations: cfg/encoder_lowdelay_P_main10.cfg:58,
+encoder_randomaccess_main10.cfg:60, encoder_lowdelay_main10.cfg:56 InternalBitDepth 10) through
+the HIP path: 16-bit pictures, the pixel-per-lane search kernel (csrc/fme_px.hip), the same NN tail.
+
+Bit-exact against the main10 goldens (oracle/_ref's TComInterpolationFilter / TComRdCost at
+bitDepth 10, the C oracle agreeing) and, over a whole 416x240 frame in HM's CTU order, every field
+of every job against oracle/_ref run live."""
+import numpy as np
+import pytest
+
+from conftest import load_golden, main10_golden_cases
+from nnfme import synth, weights
+from nnfme.abi import JOB_DTYPE, MV_FIELDS, MV_RESULT_DTYPE, RESULT_DTYPE, compare_results
+from test_gpu_parity import _assert_same, _ctx
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("case", main10_golden_cases())
+def test_main10_golden(case):
+    g = load_golden(case)
+    assert int(g["bit_depth"][0]) == 10
+    _assert_same(_ctx(g).refine(g["jobs"]), g["results"], case)
+
+
+@pytest.mark.parametrize("case", main10_golden_cases())
+def test_main10_golden_split_batches_and_device_path(case):
+    """Batches split anywhere carry the NN state; the device-resident compact-record path gives
+    the same outputs."""
+    import torch
+    g = load_golden(case)
+    ctx = _ctx(g)
+    j = g["jobs"]
+    cuts = [0, 1, 9, 250, len(j) - 3, len(j)]
+    parts = [ctx.refine(j[a:b]) for a, b in zip(cuts[:-1], cuts[1:]) if b > a]
+    _assert_same(np.concatenate(parts), g["results"], case + " split")
+    ctx2 = _ctx(g)
+    dj = torch.from_numpy(np.ascontiguousarray(j).view(np.uint8).copy()).cuda()
+    out = torch.zeros(len(j) * MV_RESULT_DTYPE.itemsize, dtype=torch.uint8, device="cuda")
+    s = torch.cuda.current_stream()
+    ctx2.refine_mv_device(dj.data_ptr(), out.data_ptr(), len(j), s.cuda_stream)
+    assert ctx2.refine_status() == 0
+    got = out.cpu().numpy().view(MV_RESULT_DTYPE)
+    for f in ("mv_x", "mv_y", "cost", "bits", "nn_class"):
+        assert np.array_equal(got[f], g["results"][f]), f
+
+
+def test_main10_entry_points_outside_the_path_refuse():
+    """A 10-bit context refuses the 8-bit-only kernels with FME_E_UNSUPPORTED (-4) instead of
+    reading 16-bit planes as bytes; 12 bits is refused at creation."""
+    from nnfme.runtime import FmeContext, FmeError
+    from nnfme.abi import TZ_EXT_DTYPE
+    g = load_golden(main10_golden_cases()[0])
+    ctx = _ctx(g)
+    jobs = g["jobs"][:4]
+    ext = np.zeros(4, TZ_EXT_DTYPE)
+    with pytest.raises(FmeError) as e:
+        ctx.integer_search(jobs, ext)
+    assert e.value.code == -4
+    with pytest.raises(FmeError) as e:
+        key = np.zeros((8, 8), np.int16)
+        ctx.frac_dif_single(key, np.zeros((40, 40), np.int16), (16, 16), (0, 0), (0, 0), 100.0)
+    assert e.value.code == -4
+    with pytest.raises(FmeError) as e:
+        FmeContext(bit_depth=12)
+    assert e.value.code == -4
+    # the NN_pred single call is bit-depth independent
+    cls, _ = ctx.nn_pred_single(np.arange(1, 9, dtype=np.uint32) * 1000, 777, 8, 8)
+    assert 0 <= cls < 49
+
+
+def test_main10_frame_every_job_against_reference():
+    """One 416x240 main10 frame (HM's CTU order, the §8(d) PU mix, 4 references, NN on, FEN 1):
+    every field of every job against oracle/_ref run live from a fresh NN state."""
+    from oracle import Reference
+    from nnfme.runtime import FmeContext
+    W, H = 416, 240
+    pics = {k: synth.synth_luma_hbd(W, H, t, 10) for k, t in zip(range(5), (7, 6, 5, 4, 0))}
+    jobs = synth.make_ctu_jobs(np.random.default_rng(10), W, H, 331, 4, [0, 1, 2, 3], [0])
+    lam = synth.LDP_LAMBDA[22][1]
+    ctx = FmeContext(nn_mode=1, qp=22, fast_inter_mode=1, max_jobs=len(jobs), bit_depth=10)
+    ref = Reference(use_hadamard=1, nn_mode=1, fast_inter_mode=1, bit_depth=10)
+    for e in (ctx, ref):
+        for k, v in pics.items():
+            e.set_picture(k, v)
+        e.set_lambda(0, lam)
+    ref.load_nn(weights.load_weights(22))
+    a = ctx.refine(jobs)
+    want = ref.refine(jobs)
+    fields = ("mv_int_x", "mv_int_y", "half_x", "half_y", "qtr_x", "qtr_y", "frac_cost", "c", "n_emi",
+              "nn_class", "mv_x", "mv_y", "bits", "cost")
+    bad, first, counts = compare_results(a, want, fields)
+    assert bad == 0, f"main10 frame: {bad} of {len(jobs)} jobs differ, first {first}: {counts}"
+    assert JOB_DTYPE.itemsize == 32 and RESULT_DTYPE.itemsize == 64 and MV_FIELDS

@@ -21,7 +21,8 @@ pytestmark = pytest.mark.gpu
 def _ctx(g, **over):
     from nnfme.runtime import FmeContext
     hadme, fen, nn_mode, qp = (int(v) for v in g["config"])
-    kw = dict(use_hadamard=hadme, nn_mode=nn_mode, qp=qp, fast_inter_mode=fen)
+    kw = dict(use_hadamard=hadme, nn_mode=nn_mode, qp=qp, fast_inter_mode=fen,
+              bit_depth=int(g["bit_depth"][0]) if "bit_depth" in g else 8)
     if "net" in g:
         kw["net"] = weights.case_net(str(g["net"]))
     kw.update(over)

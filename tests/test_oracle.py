@@ -5,7 +5,7 @@ import os
 import numpy as np
 import pytest
 
-from conftest import tz_golden_cases, mc_golden_cases, mc_inputs, golden_cases, load_golden
+from conftest import tz_golden_cases, mc_golden_cases, mc_inputs, golden_cases, load_golden, main10_golden_cases
 from nnfme import synth, weights
 from nnfme.abi import PARITY_FIELDS, compare_results
 from oracle import REF_SO, Oracle, Reference
@@ -15,7 +15,8 @@ HAVE_REF = os.path.exists(REF_SO)
 
 def _engine(cls, g):
     hadme, fen, nn_mode, qp = (int(v) for v in g["config"])
-    kw = dict(use_hadamard=hadme, nn_mode=nn_mode, fast_inter_mode=fen)
+    kw = dict(use_hadamard=hadme, nn_mode=nn_mode, fast_inter_mode=fen,
+              bit_depth=int(g["bit_depth"][0]) if "bit_depth" in g else 8)
     if cls is Oracle:
         kw["qp"] = qp
     e = cls(**kw)
@@ -45,6 +46,37 @@ def test_reference_harness_matches_golden(case):
     res = _engine(Reference, g).refine(g["jobs"])
     bad, first, counts = compare_results(res, g["results"])
     assert bad == 0, f"{case}: {bad} mismatching jobs, first {first}: {counts}"
+
+
+@pytest.mark.parametrize("case", main10_golden_cases())
+def test_main10_oracle_matches_golden(case):
+    """Bit depth 10 (main10): the plain-C restatement's interpolation (headRoom 4: first-stage shift
+    2, second-stage shift 10, clip to 1023) and distortions (>> 2, SSE (d * d) >> 4 per sample)
+    against _ref's TComInterpolationFilter / TComRdCost run at bitDepth 10."""
+    g = load_golden(case)
+    assert int(g["bit_depth"][0]) == 10 and g["pictures"].dtype == np.uint16 and g["pictures"].max() > 255
+    res = _engine(Oracle, g).refine(g["jobs"])
+    bad, first, counts = compare_results(res, g["results"])
+    assert bad == 0, f"{case}: {bad} mismatching jobs, first {first}: {counts}"
+
+
+@pytest.mark.skipif(not HAVE_REF, reason="oracle/_ref not built (needs /root/reference)")
+@pytest.mark.parametrize("case", main10_golden_cases())
+def test_main10_reference_harness_matches_golden(case):
+    g = load_golden(case)
+    res = _engine(Reference, g).refine(g["jobs"])
+    bad, first, counts = compare_results(res, g["results"])
+    assert bad == 0, f"{case}: {bad} mismatching jobs, first {first}: {counts}"
+
+
+def test_main10_goldens_cover_every_pu_shape():
+    seen, flags = set(), 0
+    for case in main10_golden_cases():
+        j = load_golden(case)["jobs"]
+        seen |= set(zip(j["w"].tolist(), j["h"].tolist()))
+        flags |= int(np.bitwise_or.reduce(j["flags"]))
+    assert set(synth.ALL_PU_SIZES) <= seen
+    assert flags == 0x7
 
 
 def test_golden_covers_every_pu_shape_and_flag():
