@@ -146,6 +146,8 @@ struct fme_ctx {
   DevBuf<uint32_t> d_tz_nn_in;   // staging of fme_integer_search_ring's NN input rows
   hipEvent_t ev_tz[2] = {nullptr, nullptr};
   bool tz_timed = false;
+  // phase wall times of the last producer call (fme_pred_inter_phases)
+  double pi_ms[FME_PI_PHASES] = {};
   // predInterSearch producer: m_integerMv2Nx2N[REF_PIC_LIST_0][k] (TEncSearch.h:118), AMVP staging
   int16_t int_mv_2n[2][FME_MAX_REFS][2] = {};   // m_integerMv2Nx2N[list][ref]
   DevBuf<AmvpTask> d_amvp;
@@ -890,9 +892,11 @@ static int tz_run_host(fme_ctx* c, fme_job* jobs, const fme_tz_ext* ext, uint32_
 // level back to back on the stream (a level reads the earlier levels' MVs from device memory), one
 // download: the chain of a 1080p frame (≈ 2,200 levels, most of a few jobs: the bottom CTU row has
 // no depth-0 CU) never waits for the host.  emi: the post-EMI integer MV of every job.
+struct PiClock;
+static void pi_lap(PiClock* clk, int k);
 static int tz_by_level(fme_ctx* c, std::vector<fme_job>& jobs, std::vector<fme_tz_ext>& ext,
                        const std::vector<int>& src, const std::vector<int>& lvl, hipStream_t s,
-                       std::vector<int16_t>& emi) {
+                       std::vector<int16_t>& emi, PiClock* clk = nullptr) {
   const int nu = (int)jobs.size();
   emi.assign((size_t)nu * 2, 0);
   if (nu == 0) return FME_OK;
@@ -923,6 +927,7 @@ static int tz_by_level(fme_ctx* c, std::vector<fme_job>& jobs, std::vector<fme_t
     le[q] = ext[u];
     psrc[q] = ((ext[u].flags & FME_TZ_PRED2NX2N) && src[u] >= 0) ? pos[src[u]] : -1;
   }
+  pi_lap(clk, 2);   // the level ordering is host setup; the chain starts with its upload
   HIP_TRY(c->d_jobs.reserve(nu));
   HIP_TRY(c->d_tz_ext.reserve(nu));
   HIP_TRY(c->d_tz_emi.reserve((size_t)2 * nu));
@@ -1672,6 +1677,32 @@ int fme_build_bipred_keys_device(fme_ctx* c, const fme_bikey_req* d_reqs, int n,
   return FME_OK;
 }
 
+// Phase clock of the producers (fme_pred_inter_phases): lap(k) adds the time since the last lap to
+// phase k.
+struct PiClock {
+  fme_ctx* c;
+  std::chrono::steady_clock::time_point t0, t;
+  explicit PiClock(fme_ctx* cc) : c(cc), t0(std::chrono::steady_clock::now()), t(t0) {
+    for (double& v : c->pi_ms) v = 0.0;
+  }
+  void lap(int k) {
+    const auto now = std::chrono::steady_clock::now();
+    c->pi_ms[k] += std::chrono::duration<double, std::milli>(now - t).count();
+    t = now;
+  }
+  ~PiClock() { c->pi_ms[7] = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count(); }
+};
+
+static void pi_lap(PiClock* clk, int k) {
+  if (clk) clk->lap(k);
+}
+
+int fme_pred_inter_phases(fme_ctx* c, double* ms, int count) {
+  if (!c || (count > 0 && !ms)) return fail(FME_E_INVALID, "fme_pred_inter_phases: null argument");
+  for (int i = 0; i < count && i < FME_PI_PHASES; i++) ms[i] = c->pi_ms[i];
+  return FME_OK;
+}
+
 int fme_pred_inter_reset(fme_ctx* c) {
   if (!c) return fail(FME_E_INVALID, "fme_pred_inter_reset: null ctx");
   std::memset(c->int_mv_2n, 0, sizeof(c->int_mv_2n));
@@ -1692,6 +1723,7 @@ int fme_pred_inter_p(fme_ctx* c, const fme_pu_req* reqs, fme_pu_res* res, int n,
   if (n <= 0) return n == 0 ? FME_OK : fail(FME_E_INVALID, "fme_pred_inter_p: n = %d", n);
   HIP_TRY(hipSetDevice(c->device));
   hipStream_t s = static_cast<hipStream_t>(stream);
+  PiClock clk(c);
   // ---- validation (nothing runs on a bad batch) ----
   for (int i = 0; i < n; i++) {
     const fme_pu_req& q = reqs[i];
@@ -1728,6 +1760,7 @@ int fme_pred_inter_p(fme_ctx* c, const fme_pu_req* reqs, fme_pu_res* res, int n,
     }
   }
   std::vector<uint32_t> tsad(tasks.size());
+  clk.lap(0);
   if (!tasks.empty()) {
     HIP_TRY(c->d_amvp.reserve(tasks.size()));
     HIP_TRY(c->d_amvp_sad.reserve(tasks.size()));
@@ -1737,6 +1770,7 @@ int fme_pred_inter_p(fme_ctx* c, const fme_pu_req* reqs, fme_pu_res* res, int n,
     HIP_TRY(hipMemcpyAsync(tsad.data(), c->d_amvp_sad.p, tasks.size() * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
     HIP_TRY(hipStreamSynchronize(s));
   }
+  clk.lap(1);
   // ---- jobs: one xMotionEstimation per (request, reference) ----
   std::vector<fme_job> jobs((size_t)nj);
   std::vector<fme_tz_ext> ext((size_t)nj);
@@ -1814,12 +1848,15 @@ int fme_pred_inter_p(fme_ctx* c, const fme_pu_req* reqs, fme_pu_res* res, int n,
     }
   }
   std::vector<int16_t> emi_mv;
-  rc = tz_by_level(c, jobs, ext, src, lvl, s, emi_mv);
+  clk.lap(2);
+  rc = tz_by_level(c, jobs, ext, src, lvl, s, emi_mv, &clk);
   if (rc) return rc;
+  clk.lap(3);
   // ---- 3. the sub-pel path over every job in request order ----
   std::vector<fme_result> r((size_t)nj);
   rc = fme_refine(c, jobs.data(), r.data(), nj, stream);
   if (rc) return rc;
+  clk.lap(4);
   // ---- 4. xCheckBestMVP, reference choice, m_integerMv2Nx2N ----
   for (int i = 0; i < n; i++) {
     const fme_pu_req& q = reqs[i];
@@ -1875,6 +1912,7 @@ int fme_pred_inter_p(fme_ctx* c, const fme_pu_req* reqs, fme_pu_res* res, int n,
         c->int_mv_2n[0][k][1] = r[base[i] + k].mv_int_y;
       }
   }
+  clk.lap(5);
   return FME_OK;
 }
 
@@ -1902,6 +1940,7 @@ int fme_pred_inter_b(fme_ctx* c, const fme_pu_req_b* reqs, fme_pu_res_b* res, in
   const int fen = c->cfg.fast_inter_mode;
   HIP_TRY(hipSetDevice(c->device));
   hipStream_t s = static_cast<hipStream_t>(stream);
+  PiClock clk(c);
   // ---- validation (nothing runs on a bad batch) ----
   for (int i = 0; i < n; i++) {
     const fme_pu_req_b& q = reqs[i];
@@ -1953,6 +1992,7 @@ int fme_pred_inter_b(fme_ctx* c, const fme_pu_req_b* reqs, fme_pu_res_b* res, in
                                      q.cand[l][k][m][0], q.cand[l][k][m][1]});
         }
     }
+    clk.lap(0);
     if (!tasks.empty()) {
       std::vector<uint32_t> tsad(tasks.size());
       HIP_TRY(c->d_amvp.reserve(tasks.size()));
@@ -1976,6 +2016,7 @@ int fme_pred_inter_b(fme_ctx* c, const fme_pu_req_b* reqs, fme_pu_res_b* res, in
       }
     }
   }
+  clk.lap(1);
   // ---- 2. uni-pred jobs in call order, integer searches by m_integerMv2Nx2N level ----
   std::vector<int> ujob((size_t)n * 8, -1), ubeg(n + 1, 0);
   std::vector<fme_job> uj;
@@ -2038,9 +2079,11 @@ int fme_pred_inter_b(fme_ctx* c, const fme_pu_req_b* reqs, fme_pu_res_b* res, in
       }
     }
     std::vector<int16_t> emi_mv;
-    rc = tz_by_level(c, uj, ue, src, lvl, s, emi_mv);
+    clk.lap(2);
+    rc = tz_by_level(c, uj, ue, src, lvl, s, emi_mv, &clk);
     if (rc) return rc;
   }
+  clk.lap(3);
   // ---- 3. the uni-pred sub-pel path in call order ----
   uint32_t s0[12];
   rc = fme_nn_get_state(c, s0);
@@ -2048,6 +2091,7 @@ int fme_pred_inter_b(fme_ctx* c, const fme_pu_req_b* reqs, fme_pu_res_b* res, in
   std::vector<fme_result> ru((size_t)nu);
   rc = fme_refine(c, uj.data(), ru.data(), nu, stream);
   if (rc) return rc;
+  clk.lap(4);
   // ---- 4. rounds of host decisions and bi-pred searches ----
   std::vector<BPu> st((size_t)n);
   for (int i = 0; i < n; i++) st[i].stage = 0;
@@ -2362,6 +2406,7 @@ int fme_pred_inter_b(fme_ctx* c, const fme_pu_req_b* reqs, fme_pu_res_b* res, in
       decide(i, p.mvbi, p.ridxbi, p.mvpibi);
     }
   }
+  clk.lap(6);
   // ---- m_integerMv2Nx2N: the last 2Nx2N request's post-EMI integer MV per (list, reference) ----
   for (int i = 0; i < n; i++)
     if (reqs[i].part_size == FME_PART_2Nx2N)

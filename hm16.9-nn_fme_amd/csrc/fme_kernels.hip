@@ -572,13 +572,13 @@ int cu_count(int device) {
 
 // ---------------------------------------------------------------------------------------
 // results download: device rows -> pinned host memory, few workgroups.  Each lane keeps four
-// 16-byte loads in flight, then stores them with system-scope (sc0 sc1) write-through stores:
-// the rows go straight to the PCIe write path, no cache line of host memory stays in L2.
+// 16-byte loads in flight, then stores them non-temporally: the rows go to the PCIe write path
+// without allocating in L2.  tools/probes/d2h_kernel_probe.hip (profiles/r05_ab.log): PCIe write
+// bound at ~54 GB/s from 8 workgroups of 256 lanes with nt stores (0.264 ms per 13.8 MB), where
+// system-scope sc0 sc1 stores need 64 workgroups and one-wave groups 128.
 // ---------------------------------------------------------------------------------------
-constexpr int kDlThreads = 64;
-__device__ __forceinline__ void dl_store(u32x4* p, u32x4 v) {
-  asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1" : : "v"(p), "v"(v) : "memory");
-}
+constexpr int kDlThreads = 256;
+__device__ __forceinline__ void dl_store(u32x4* p, u32x4 v) { __builtin_nontemporal_store(v, p); }
 __global__ __launch_bounds__(kDlThreads) void k_download(const u32x4* __restrict__ src, u32x4* dst, long n16) {
   const long stride = (long)gridDim.x * kDlThreads;
   long i = (long)blockIdx.x * kDlThreads + threadIdx.x;

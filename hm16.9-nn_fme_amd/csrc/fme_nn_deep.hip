@@ -42,6 +42,9 @@ constexpr int kHW = FME_NN_MAX_WIDTH;             // hidden width (padded)
 constexpr int kHP = 48;                           // hidden rows padded to 3 MFMA tiles
 constexpr int kOP = 64;                           // output rows padded to 4 MFMA tiles
 constexpr int kAS = 65;                           // LDS activation row stride (elements)
+#ifndef FME_DEEP_BHOIST
+#define FME_DEEP_BHOIST 1
+#endif
 
 
 // Embedding rows: W (and Backups/15's H) 4,8,12,16,24,32,64 -> 1..7; the master's H swaps 12/16.
@@ -158,6 +161,19 @@ __device__ __forceinline__ void layer_mfma(T* act, const T* __restrict__ W, cons
   using M = Mfma<T>;
   constexpr int NT = NP / 16;
   const int c16 = lane & 15, k4 = lane >> 4;
+  // HOIST: the layer's B fragments (B[k][unit] = W[unit][k]) loaded once per wave, all in flight
+  // before the first MFMA and reused by the four 16-job tiles, instead of a load per (tile, k-step,
+  // unit tile) that kept each MFMA behind a global-load latency.  The double nets run at one wave
+  // per SIMD anyway (33 KB of LDS activations per wave); the float ones would lose their second
+  // wave to the registers (FME_DEEP_BHOIST: 1 double only, 2 both, 0 neither).
+  constexpr bool HOIST = FME_DEEP_BHOIST >= 2 || (FME_DEEP_BHOIST == 1 && sizeof(T) == 8);
+  T bw[HOIST ? K / 4 : 1][NT];
+  if constexpr (HOIST) {
+#pragma unroll
+    for (int kk = 0; kk < K / 4; kk++)
+#pragma unroll
+      for (int nt = 0; nt < NT; nt++) bw[kk][nt] = W[(nt * 16 + c16) * K + kk * 4 + k4];
+  }
 #pragma unroll
   for (int mt = 0; mt < 4; mt++) {
     typename M::acc_t acc[NT];
@@ -168,8 +184,8 @@ __device__ __forceinline__ void layer_mfma(T* act, const T* __restrict__ W, cons
       const T a = act[(mt * 16 + c16) * kAS + kk * 4 + k4];         // A[job][k]
 #pragma unroll
       for (int nt = 0; nt < NT; nt++) {
-        const T bw = W[(nt * 16 + c16) * K + kk * 4 + k4];          // B[k][unit] = W[unit][k]
-        acc[nt] = M::mma(a, bw, acc[nt]);
+        const T b = HOIST ? bw[HOIST ? kk : 0][nt] : W[(nt * 16 + c16) * K + kk * 4 + k4];
+        acc[nt] = M::mma(a, b, acc[nt]);
       }
     }
     if constexpr (sizeof(T) == 8) {

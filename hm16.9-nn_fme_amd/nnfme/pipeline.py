@@ -106,7 +106,7 @@ class FrameReplay:
         nn_rows (uint32 [n][9]): the NN input rows of the frame's FME_JOB_NN_IN jobs (the backups'
         input path); each step uploads them with its jobs and binds them (fme_set_nn_inputs).
         download_engine: "kernel" (fme_download_device: the library's copy kernel of
-        download_wgs one-wave workgroups, which holds a few wave slots beside the next step's
+        download_wgs workgroups of 256 lanes, which hold a few wave slots beside the next step's
         search) or "blit" (hipMemcpyAsync, which this ROCm runs as a blit kernel of hundreds of
         workgroups that take the search kernel's CUs)."""
         import torch

@@ -15,7 +15,7 @@ from .weights import load_weights
 PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB_PATH = os.environ.get("FME_LIB_PATH") or os.path.join(PKG_ROOT, "libfme_amd.so")
 
-ABI_VERSION = 13
+ABI_VERSION = 14
 TIMING_NAMES = ("classify", "scatter", "search", "nn_tail", "batch", "search_main", "search_aux")
 
 # Every entry point include/fme.h declares (the ABI test checks the .so exports them).
@@ -33,7 +33,7 @@ ABI_SYMBOLS = (
     "fme_refine_status", "fme_nn_copy_state_device", "fme_template_costs", "fme_pred_inter_b", "fme_build_bipred_keys",
     "fme_set_search_event", "fme_build_bipred_keys_device", "fme_set_nn_logit_output",
     "fme_set_nn_inputs", "fme_integer_search_ring", "fme_integer_search_ring_device",
-    "fme_download_device",
+    "fme_download_device", "fme_pred_inter_phases",
 )
 
 
@@ -113,6 +113,7 @@ def load_library(path=None):
         "fme_integer_search_ring": (I, [P, P, P, P, P, I, P]),
         "fme_integer_search_ring_device": (I, [P, P, P, P, P, I, P]),
         "fme_download_device": (I, [P, P, P, C.c_size_t, I, P]),
+        "fme_pred_inter_phases": (I, [P, P, I]),
     }
     # an explicitly named library is an A/B variant (tools/ab_bench.py): possibly an older ABI
     strict = os.path.abspath(path) == os.path.abspath(LIB_PATH)
@@ -409,6 +410,14 @@ class FmeContext:
         kernel (fme_download_device), asynchronous on `stream`."""
         _check(self.lib, self.lib.fme_download_device(self.h, C.c_void_p(d_src_ptr), C.c_void_p(h_dst_ptr),
                                                       nbytes, workgroups, stream))
+
+    PI_PHASES = ("expand", "amvp", "setup", "level_chain", "refine", "decide", "bi_rounds", "total")
+
+    def pred_inter_phases(self):
+        """{phase: ms} of the last fme_pred_inter_p / _b call (fme_pred_inter_phases)."""
+        out = np.zeros(8, np.float64)
+        _check(self.lib, self.lib.fme_pred_inter_phases(self.h, _ptr(out), 8))
+        return dict(zip(self.PI_PHASES, out.tolist()))
 
     def set_search_event(self, event):
         """Record `event` (a torch.cuda.Event or a raw hipEvent_t, None: off) on the batch stream

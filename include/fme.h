@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define FME_ABI_VERSION 13
+#define FME_ABI_VERSION 14
 
 /* ---- error codes ---------------------------------------------------------------- */
 #define FME_OK            0
@@ -291,8 +291,9 @@ int fme_set_search_event(fme_ctx* ctx, void* event);
 
 /* Download of device records (fme_mv_result / fme_result rows, any 16-byte-multiple span) into
  * pinned host memory (hipHostMalloc, hipHostRegister or a torch pin_memory() tensor) by the
- * library's own copy kernel of at most `workgroups` workgroups of 64 lanes (0: the default, 8),
- * each lane storing 16-byte blocks with system-scope (write-through) stores, asynchronous on
+ * library's own copy kernel of at most `workgroups` workgroups of 256 lanes (0: the default, 8),
+ * each lane storing 16-byte blocks with non-temporal stores (PCIe-write bound, ~54 GB/s from 8
+ * workgroups: tools/probes/d2h_kernel_probe.hip), asynchronous on
  * `stream`.  A hipMemcpyAsync device-to-host copy runs on this ROCm as a blit kernel of hundreds
  * of workgroups, which, queued beside a running batch, took the CUs of the search kernel
  * (23.6 % of GPU time in the round-4 profile); this one holds a few wave slots.  No replacement
@@ -540,6 +541,16 @@ int fme_build_bipred_keys_device(fme_ctx* ctx, const fme_bikey_req* d_reqs, int 
 /* Host arrays, synchronous on `stream`; a batch with an invalid request is rejected before any
  * work runs.  m_integerMv2Nx2N (both lists) is the state fme_pred_inter_reset forgets. */
 int fme_pred_inter_b(fme_ctx* ctx, const fme_pu_req_b* reqs, fme_pu_res_b* res, int n, void* stream);
+
+/* Wall-clock milliseconds of the last fme_pred_inter_p / fme_pred_inter_b call by phase (host clock
+ * around each phase, the device work of a phase included in it, ms[FME_PI_PHASES]):
+ *   0 validation and request expansion (host)      1 AMVP template costs (k_amvp_sad round trip)
+ *   2 job setup and level ordering (host)           3 the m_integerMv2Nx2N level chain (k_tz_level)
+ *   4 the sub-pel refinement (fme_refine)           5 xCheckBestMVP / reference choice (host)
+ *   6 B slices: the bi-pred rounds (keys, xPatternSearch, refine, decisions)   7 total
+ * No replacement of a reference interface (measurement of the producers). */
+#define FME_PI_PHASES 8
+int fme_pred_inter_phases(fme_ctx* ctx, double* ms, int count);
 
 /* ---- single-PU entry points with the TEncSearch argument lists ---------------------------- *
  * xPatternSearchFracDIF(bIsLosslessCoded, pcPatternKey, piRefY, iRefStride, pcMvInt,

@@ -351,6 +351,7 @@ def test_emi_and_nn_in_flags_together():
         o.set_picture(i, p)
     for i, lam in enumerate(g["lambdas"]):
         o.set_lambda(i, float(lam))
+    o.set_keys(g["keys"] if g["keys"].size else np.zeros(1, np.int16))
     o.set_nn_inputs(rows)
     want = o.refine(jobs)
     _assert_same(res, want, "EMI | NN_IN")

@@ -1,0 +1,56 @@
+// Device -> pinned host copy by a kernel: bandwidth by workgroup count, workgroup size and store
+// flavour (plain / nt / sc0 sc1), against hipMemcpyAsync's own copy, 13.8 MB (one 1080p frame's
+// fme_mv_result rows).  Standalone (nothing else runs).
+#include <hip/hip_runtime.h>
+#include <cstdio>
+#include <cstdint>
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+template <int MODE>
+__global__ void k_dl(const u32x4* __restrict__ src, u32x4* dst, long n16) {
+  const long stride = (long)gridDim.x * blockDim.x;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n16; i += stride) {
+    const u32x4 v = src[i];
+    if (MODE == 0) dst[i] = v;
+    else if (MODE == 1) __builtin_nontemporal_store(v, dst + i);
+    else asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1" : : "v"(dst + i), "v"(v) : "memory");
+  }
+}
+
+int main() {
+  const size_t bytes = 13806720;
+  const long n16 = bytes / 16;
+  void *d, *h;
+  if (hipMalloc(&d, bytes) != hipSuccess || hipHostMalloc(&h, bytes, 0) != hipSuccess) return 1;
+  (void)hipMemset(d, 1, bytes);
+  hipEvent_t e0, e1;
+  (void)hipEventCreate(&e0);
+  (void)hipEventCreate(&e1);
+  auto timeit = [&](auto&& f) {
+    f();
+    (void)hipDeviceSynchronize();
+    (void)hipEventRecord(e0, 0);
+    for (int r = 0; r < 10; r++) f();
+    (void)hipEventRecord(e1, 0);
+    (void)hipEventSynchronize(e1);
+    float ms = 0;
+    (void)hipEventElapsedTime(&ms, e0, e1);
+    return ms / 10;
+  };
+  float ms = timeit([&] { (void)hipMemcpyAsync(h, d, bytes, hipMemcpyDeviceToHost, 0); });
+  printf("hipMemcpyAsync D2H: %.3f ms (%.1f GB/s)\n", ms, bytes / ms / 1e6);
+  const int wgs[] = {8, 16, 32, 64, 128, 256, 512, 1024};
+  const int thr[] = {64, 256};
+  const char* names[] = {"plain", "nt", "sc0sc1"};
+  for (int mode = 0; mode < 3; mode++)
+    for (int t : thr)
+      for (int g : wgs) {
+        float m = timeit([&] {
+          if (mode == 0) hipLaunchKernelGGL(k_dl<0>, dim3(g), dim3(t), 0, 0, (const u32x4*)d, (u32x4*)h, n16);
+          else if (mode == 1) hipLaunchKernelGGL(k_dl<1>, dim3(g), dim3(t), 0, 0, (const u32x4*)d, (u32x4*)h, n16);
+          else hipLaunchKernelGGL(k_dl<2>, dim3(g), dim3(t), 0, 0, (const u32x4*)d, (u32x4*)h, n16);
+        });
+        printf("kernel %-7s %4d WG x %3d: %.3f ms (%.1f GB/s)\n", names[mode], g, t, m, bytes / m / 1e6);
+      }
+  return 0;
+}
