@@ -57,6 +57,10 @@ WORKLOADS = {
                     desc="1920x1080 lowdelay_P QP27, NN_pred on, 4 refs (configs[2] at QP27)"),
     "c3_qp32": dict(W=1920, H=1080, QP=32, nn=1, calls=423, bipred=0.0, gop="ldp", frames=1,
                     desc="1920x1080 lowdelay_P QP32, NN_pred on, 4 refs (configs[2] at QP32)"),
+    "c3_qp22_main10": dict(W=1920, H=1080, QP=22, nn=1, calls=423, bipred=0.0, gop="ldp", frames=1, bit_depth=10,
+                           desc="1920x1080 lowdelay_P main10 (InternalBitDepth 10, cfg/encoder_lowdelay_P_main10.cfg:58) "
+                                "QP22, NN_pred on, 4 refs (configs[2] at 10 bit: 16-bit samples, the pixel-per-lane "
+                                "kernel k_search_px)"),
     "c3_qp37": dict(W=1920, H=1080, QP=37, nn=1, calls=423, bipred=0.0, gop="ldp", frames=1,
                     desc="1920x1080 lowdelay_P QP37, NN_pred on, 4 refs (configs[2] at QP37)"),
     "c1": dict(W=416, H=240, QP=22, nn=1, calls=331, bipred=0.0, gop="ldp", frames=8,
@@ -95,11 +99,12 @@ HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md chip table (spec)
 VALU_PEAK_TOPS = 256 * 4 * 32 * 2.4e9 / 1e12
 
 
-def algorithmic_bytes(jobs):
-    """W*H (org) + (W+8)(H+8) (reference footprint) + 48 (descriptor + result)."""
+def algorithmic_bytes(jobs, bps=1):
+    """W*H (org) + (W+8)(H+8) (reference footprint) samples of bps bytes (2 at
+    main10) + 48 (descriptor + result)."""
     w = jobs["w"].astype(np.int64)
     h = jobs["h"].astype(np.int64)
-    return int((w * h + (w + 8) * (h + 8) + 48).sum())
+    return int((bps * (w * h + (w + 8) * (h + 8)) + 48).sum())
 
 
 def main_kernel_mask(ctx, jobs):
@@ -141,7 +146,7 @@ def _cpu_reference():
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     from oracle import Reference
     from nnfme import weights
-    ref = Reference(use_hadamard=1, nn_mode=_CPU.get("nn", 1), fast_inter_mode=1)
+    ref = Reference(use_hadamard=1, nn_mode=_CPU.get("nn", 1), fast_inter_mode=1, bit_depth=_CPU.get("bd", 8))
     for k, v in _CPU["pics"].items():
         ref.set_picture(k, v)
     ref.set_lambda(0, synth.LDP_LAMBDA[QP][1])
@@ -242,7 +247,7 @@ def parity_leg(rep, wl, net, step, state, seconds, max_jobs=0):
         return {"skipped": "bi-pred keys are built on the device per step; the key parity is "
                            "tests/test_gpu_c4.py's"}
     nn = wl["nn"]
-    ref = Reference(use_hadamard=1, nn_mode=nn, fast_inter_mode=1)
+    ref = Reference(use_hadamard=1, nn_mode=nn, fast_inter_mode=1, bit_depth=wl.get("bit_depth", 8))
     if nn == 1:
         ref.load_nn(weights.load_weights(wl["QP"]))
     elif nn == 2:
@@ -263,7 +268,7 @@ def parity_leg(rep, wl, net, step, state, seconds, max_jobs=0):
     fields = ("mv_x", "mv_y", "bits", "cost") + (("nn_class",) if nn else ())
     bad = {f: 0 for f in fields}
     mism = 0
-    first = None
+    first = detail = None
     done, t0 = 0, time.perf_counter()
     while done < n and time.perf_counter() - t0 < seconds:
         e = min(done + 20000, n)
@@ -275,11 +280,14 @@ def parity_leg(rep, wl, net, step, state, seconds, max_jobs=0):
             bad[f] += int(d.sum())
             m |= d
         if first is None and m.any():
-            first = done + int(np.flatnonzero(m)[0])
+            i0 = int(np.flatnonzero(m)[0])
+            first = done + i0
+            detail = {"gpu": {f: int(g[f][i0]) for f in fields}, "ref": {f: int(r[f][i0]) for f in fields}}
         mism += int(m.sum())
         done = e
     out = {"jobs_checked": done, "mismatches": mism, "step": step, "of_step_jobs": len(jobs),
            "fields": list(fields), "per_field": bad, "first_mismatch": first,
+           **({"first_mismatch_detail": detail} if detail else {}),
            "reference": "oracle/_ref (the reference's TLibCommon -O2, TEncSearch order restated; NN "
                         "restated scalar) with the step's pictures, lambdas and carried NN state",
            "seconds": round(time.perf_counter() - t0, 2)}
@@ -287,6 +295,32 @@ def parity_leg(rep, wl, net, step, state, seconds, max_jobs=0):
         out["note"] = ("MFMA engine: FMA-chain rounding, not bit-exact by construction (DESIGN.md §3); "
                        "a mismatch is a near-tie class")
     return out
+
+
+def host_path_check(ctx, rep, wl, step, state, net, bd, m=2000):
+    """A fresh context on the same device with the step's bindings (host pictures, lambdas) and
+    state, refining the step's first m jobs through the host path: which of the replay and the
+    reference it agrees with."""
+    from nnfme.abi import MV_FIELDS
+    from nnfme.pipeline import ORG0, REFS
+    from nnfme.runtime import FmeContext
+    c2 = FmeContext(device=ctx.device, use_hadamard=1, nn_mode=wl["nn"], qp=wl["QP"], fast_inter_mode=1,
+                    max_jobs=m, net=net, nn_engine=wl.get("engine", 0), bit_depth=bd)
+    pool = rep.pool.numpy()
+    f0 = rep.first_frame(step)
+    for j in range(rep.F):
+        c2.set_picture(ORG0 + j, pool[(f0 + j) % rep.P])
+        c2.set_lambda(j, rep.lambda_of(f0 + j))
+    for slot in range(rep.F + REFS - 1):
+        c2.set_picture(slot, pool[(f0 - REFS + slot) % rep.P])
+    c2.nn_set_state(state)
+    b = c2.refine_mv(rep.jobs[:m])
+    g = rep.results(step)[:m]
+    c2.close()
+    return {"jobs": m, "host_vs_replay": {f: int((b[f] != g[f]).sum()) for f in MV_FIELDS},
+            "job0": {"job": [int(v) for v in rep.jobs[0].tolist()], "replay": [int(v) for v in g[0].tolist()],
+                     "host": [int(v) for v in b[0].tolist()]},
+            "lambda": rep.lambda_of(f0), "first_frame": f0}
 
 
 def mc_algorithmic_bytes(jobs):
@@ -612,9 +646,11 @@ def main():
     ap.add_argument("--dist-backend", default="nccl", help="torch.distributed backend for N > 1 (nccl = RCCL)")
     ap.add_argument("--parity-seconds", type=float, default=30.0,
                     help="bound of the after-run check of one timed step against oracle/_ref (0: skip)")
-    ap.add_argument("--download-engine", choices=("kernel", "blit"), default="kernel",
+    ap.add_argument("--download-engine", choices=("kernel", "blit"), default="blit",
                     help="results download: the library's few-workgroup copy kernel (fme_download_device) "
-                         "or hipMemcpyAsync (a blit kernel of hundreds of workgroups)")
+                         "or hipMemcpyAsync (a blit kernel of hundreds of workgroups; the default: in the "
+                         "pipeline the copy kernel's workgroups wait for the persistent search's slots, "
+                         "1.39 against 1.22 ms per step, profiles/r05_ab.log)")
     ap.add_argument("--download-wgs", type=int, default=8, help="workgroups of the download kernel")
     ap.add_argument("--download", choices=("deferred", "immediate"), default=None,
                     help="results download of step k: once step k+1's search runs (deferred) or right after "
@@ -625,6 +661,10 @@ def main():
     wl = WORKLOADS[args.workload]
     W, H, QP = wl["W"], wl["H"], wl["QP"]
     NN, CALLS, BIPRED, WDESC, FPS = wl["nn"], wl["calls"], wl["bipred"], wl["desc"], wl["frames"]
+    BD = wl.get("bit_depth", 8)
+
+    def picture(t):   # one synthetic luma plane (uint16 main10 samples at bit depth 10)
+        return synth.synth_luma(W, H, t) if BD == 8 else synth.synth_luma_hbd(W, H, t, bit_depth=BD)
     if args.workload != "c3_qp22":
         METRIC = f"sub-pel PU refinements/sec @ {args.workload}: {WDESC.split(',')[0]}; bit-exact MV/SATD vs HM"
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -647,7 +687,7 @@ def main():
 
     # ---- CPU baselines first, before anything touches the GPU (fork-safe) -------------------
     cpu = {}
-    _CPU["nn"], _CPU["keys"] = min(NN, 1), keys
+    _CPU["nn"], _CPU["keys"], _CPU["bd"] = min(NN, 1), keys, BD
     if rank == 0 and world == 1 and not args.no_cpu_baseline and RING:
         pics = {k: synth.synth_luma(W, H, t) for k, t in zip(range(5), (7, 6, 5, 4, 0))}
         rjobs, rrows = ring_inputs_cpu(jobs, tz_ext, pics, 20000)
@@ -660,7 +700,7 @@ def main():
                       f"the backup's NN inputs (their integer searches by the oracle, untimed)",
         }
     elif rank == 0 and world == 1 and not args.no_cpu_baseline:
-        pics = {k: synth.synth_luma(W, H, t) for k, t in zip(range(5), (7, 6, 5, 4, 0))}
+        pics = {k: picture(t) for k, t in zip(range(5), (7, 6, 5, 4, 0))}
         rate, dt, done = cpu_baseline(jobs, pics, args.cpu_seconds)
         cpu["cpu_baseline"] = {
             "value": rate, "unit": "PU/s", "cores": 1, "kind": "reference",
@@ -700,7 +740,7 @@ def main():
 
     net = weights.case_net(wl["net"]) if NN == 2 else None
     ctx = FmeContext(device=dev_index, use_hadamard=1, nn_mode=NN, qp=QP, fast_inter_mode=1,
-                     max_jobs=n1 * FPS, net=net, nn_engine=wl.get("engine", 0))
+                     max_jobs=n1 * FPS, net=net, nn_engine=wl.get("engine", 0), bit_depth=BD)
 
     nn_rows = None
     if RING:   # untimed: the frame's integer searches on the GPU, with the backups' square + ring
@@ -711,7 +751,7 @@ def main():
         jobs["flags"] = np.where((jobs["flags"] & JOB_BIPRED) == 0, JOB_NN_IN, jobs["flags"]).astype(np.uint8)
 
     # synthetic frame pool (the trace's originals / reconstructions): frame g -> pool[g % 8]
-    pool = np.stack([synth.synth_luma(W, H, t) for t in range(8)])
+    pool = np.stack([picture(t) for t in range(8)])
     steps_total = args.warmup + args.steps
     defer = (args.download or wl.get("download", "deferred")) == "deferred"
     # bi-pred keys (configs[3]): every step builds its frame's removeHighFreq keys on the device from
@@ -751,10 +791,19 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     rep.check_status(args.warmup)   # no timed step may have been rejected on the device
+    snap = rep.results(args.warmup).copy() if args.parity_seconds > 0 else None
     nb, acc = ctx.accumulated_timings(reset=True)
     ctx.set_profiling(False)
     tm = {k: v / max(nb, 1) for k, v in acc.items()}
     value = world * n * args.steps / elapsed
+
+    parity = None
+    if rank == 0 and world == 1 and args.parity_seconds > 0:
+        parity = parity_leg(rep, wl, net, args.warmup, state0, args.parity_seconds)
+        if parity.get("mismatches"):   # localise: the library's host path on the same bindings
+            parity["host_path_check"] = host_path_check(ctx, rep, wl, args.warmup, state0, net, BD)
+            now = rep.results(args.warmup)
+            parity["rows_changed_since_timed_region"] = int((now != snap).sum())
 
     # ---- device-resident rate (extra key): the same batches with jobs, pictures and results
     # already in HBM, back to back on one stream (no PCIe in the loop) ---------------------------
@@ -776,25 +825,22 @@ def main():
         dres = {"value": n / dt, "unit": "PU/s", "ms_per_step": dt * 1e3,
                 "note": "jobs, pictures and results HBM-resident, one GPU, batches back to back"}
 
-    parity = None
-    if rank == 0 and world == 1 and args.parity_seconds > 0:
-        parity = parity_leg(rep, wl, net, args.warmup, state0, args.parity_seconds)
 
     mc = mc_leg(dev, torch.cuda.current_stream(dev), reps=max(5, args.steps // 2)) \
-        if rank == 0 and not args.no_mc and W == 1920 and NN != 2 else None
-    single = drop_in_leg(dev) if rank == 0 and not args.no_mc and W == 1920 and NN == 1 else None
+        if rank == 0 and not args.no_mc and W == 1920 and NN != 2 and BD == 8 else None
+    single = drop_in_leg(dev) if rank == 0 and not args.no_mc and W == 1920 and NN == 1 and BD == 8 else None
     pi = None
-    if rank == 0 and not args.no_pi and W == 1920 and world == 1 and NN == 1:
+    if rank == 0 and not args.no_pi and W == 1920 and world == 1 and NN == 1 and BD == 8:
         pi = pred_inter_leg(dev, reps=2, cpu_seconds=0.0 if args.no_cpu_baseline else 4.0)
     tz = None
-    if rank == 0 and not args.no_tz and W == 1920 and world == 1 and NN == 1:
+    if rank == 0 and not args.no_tz and W == 1920 and world == 1 and NN == 1 and BD == 8:
         tz = tz_leg(dev, torch.cuda.current_stream(dev), reps=max(3, args.steps // 4),
                     cpu_seconds=0.0 if args.no_cpu_baseline else 6.0)
 
     if rank == 0:
         gj = rep.jobs
         small_jobs = gj[main_kernel_mask(ctx, gj)]
-        bytes_small = algorithmic_bytes(small_jobs)
+        bytes_small = algorithmic_bytes(small_jobs, 2 if BD > 8 else 1)
         small_s = tm["search_main"] / 1e3
         ops_small = algorithmic_ops(small_jobs)
         valu = ops_small / small_s / 1e12
@@ -811,6 +857,7 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
+            "bit_depth": BD,
             "dtype": "int16/int32 (NN f32)" if NN != 2 else
                      "int16/int32 (NN %s)" % ("f64" if net.precision == weights.F64 else "f32"),
             "data": "synthetic (SURVEY.md §8(d) YUV generator + PU-size mix; reference per-QP "
@@ -846,7 +893,9 @@ def main():
                 "frac": valu / VALU_PEAK_TOPS,
                 "traffic": traffic,
                 "kernel": "main search phase: fme::k_search_lane (EMI + FracDIF, every PU shape, one "
-                          "persistent launch per batch)",
+                          "persistent launch per batch)" if BD == 8 else
+                          "main search phase at bit depth 10: fme::k_search_px<10> (EMI + FracDIF, pixel per lane, "
+                          "one job per workgroup iteration, every PU shape)",
                 "kernel_jobs": int(len(small_jobs)),
                 "algorithmic_ops_per_launch": ops_small,
                 "algorithmic_bytes_per_launch": bytes_small,

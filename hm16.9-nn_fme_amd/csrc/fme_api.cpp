@@ -16,6 +16,7 @@
 #include <cstring>
 #include <memory>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "fme_device.h"
@@ -78,6 +79,47 @@ struct DevBuf {
     cap = 0;
   }
 };
+
+// Pinned host memory, grown on demand: the producers' transfer buffers (full-rate DMA, and no page
+// faults on the buffers of the next call).
+template <typename T>
+struct HostBuf {
+  T* p = nullptr;
+  size_t cap = 0;
+  hipError_t reserve(size_t n) {
+    if (n <= cap) return hipSuccess;
+    if (p) (void)hipHostFree(p);
+    p = nullptr;
+    cap = 0;
+    const size_t want = std::max<size_t>(n + n / 4, 1);   // headroom: fewer regrowths
+    hipError_t e = hipHostMalloc(reinterpret_cast<void**>(&p), want * sizeof(T), hipHostMallocDefault);
+    if (e == hipSuccess) cap = want;
+    return e;
+  }
+  void release() {
+    if (p) (void)hipHostFree(p);
+    p = nullptr;
+    cap = 0;
+  }
+};
+
+// f(lo, hi) over [0, n) in up to 8 host threads (the producers' per-request loops; the caller's
+// thread takes the first slice).
+template <typename F>
+void par_for(int n, F&& f) {
+  const unsigned hc = std::thread::hardware_concurrency();
+  const int nt = n < 32768 ? 1 : (int)std::min<unsigned>(8u, hc ? hc : 1u);
+  if (nt <= 1) {
+    f(0, n);
+    return;
+  }
+  std::vector<std::thread> th;
+  th.reserve((size_t)nt - 1);
+  for (int t = 1; t < nt; t++)
+    th.emplace_back([&f, n, nt, t] { f((int)((long long)n * t / nt), (int)((long long)n * (t + 1) / nt)); });
+  f(0, (int)((long long)n / nt));
+  for (auto& x : th) x.join();
+}
 
 }  // namespace
 
@@ -156,6 +198,22 @@ struct fme_ctx {
   DevBuf<BiKeyTask> d_bikey;
   DevBuf<int32_t> d_key_invalid;  // invalid requests of the last fme_build_bipred_keys_device
   DevBuf<int32_t> d_ch_i32;     // k_tz_level: psrc
+  // fme_pred_inter_p scratch, kept across calls: pinned transfer buffers, host arrays, the
+  // level-ordered device copies of the jobs
+  HostBuf<AmvpTask> h_pi_tasks;
+  HostBuf<uint32_t> h_pi_tsad;
+  HostBuf<fme_job> h_pi_jobs;
+  HostBuf<fme_tz_ext> h_pi_ext;
+  HostBuf<int32_t> h_pi_idx;      // [2 nj]: level order, then its inverse
+  HostBuf<int32_t> h_pi_psrc;
+  HostBuf<fme_mv_result> h_pi_mv;
+  HostBuf<fme_result> h_pi_last;  // the full records of the last 2Nx2N request
+  std::vector<int> pi_base, pi_task, pi_level, pi_src, pi_lvl, pi_start;
+  std::vector<int32_t> pi_off, pi_fill;
+  std::vector<uint8_t> pi_amvp_idx;
+  DevBuf<fme_job> d_pi_jobs;      // level order
+  DevBuf<fme_tz_ext> d_pi_ext;
+  DevBuf<int32_t> d_pi_idx;
 
   // The deeper nets' single NN_pred: inputs in the kernel argument, class and completion word in
   // pinned, device-mapped host memory.
@@ -247,7 +305,7 @@ int fme_create(int device, const fme_config* cfg, fme_ctx** out_ctx) {
     const size_t nb = (n + kJobsPerScanBlock - 1) / kJobsPerScanBlock;
     HIP_TRY(c->cls.reserve(n));
     HIP_TRY(c->perm.reserve(n));
-    HIP_TRY(c->sjobs.reserve(n));
+    if (FME_SJOBS) HIP_TRY(c->sjobs.reserve(n));
     HIP_TRY(c->blk_agg.reserve(nb * 9));
     HIP_TRY(c->blk_prefix.reserve(nb * 9));
   }
@@ -279,6 +337,9 @@ int fme_destroy(fme_ctx* c) {
   c->d_mc_jobs.release(); c->d_mc_planes.release(); c->d_mc_invalid.release();
   c->d_tz_ext.release(); c->d_tz_sad.release(); c->d_tz_nn_in.release();
   c->d_amvp.release(); c->d_amvp_sad.release(); c->d_bikey.release(); c->d_key_invalid.release(); c->d_ch_i32.release(); c->d_tz_emi.release();
+  c->h_pi_tasks.release(); c->h_pi_tsad.release(); c->h_pi_jobs.release(); c->h_pi_ext.release();
+  c->h_pi_idx.release(); c->h_pi_psrc.release(); c->h_pi_mv.release(); c->h_pi_last.release();
+  c->d_pi_jobs.release(); c->d_pi_ext.release(); c->d_pi_idx.release();
   for (auto& e : c->ev_tz)
     if (e) (void)hipEventDestroy(e);
   for (auto& e : c->ev_mc)
@@ -569,7 +630,7 @@ static int ensure_work(fme_ctx* c, int n) {
   const size_t nb = ((size_t)n + kJobsPerScanBlock - 1) / kJobsPerScanBlock;
   HIP_TRY(c->cls.reserve(n));
   HIP_TRY(c->perm.reserve(n));
-  HIP_TRY(c->sjobs.reserve(n));
+  if (FME_SJOBS) HIP_TRY(c->sjobs.reserve(n));
   HIP_TRY(c->blk_agg.reserve(nb * 9));
   HIP_TRY(c->blk_prefix.reserve(nb * 9));
   return FME_OK;
@@ -1743,90 +1804,116 @@ int fme_pred_inter_p(fme_ctx* c, const fme_pu_req* reqs, fme_pu_res* res, int n,
   }
   int rc = sync_tables(c, s);
   if (rc) return rc;
-  // ---- 1. xEstimateMvPredAMVP template costs ----
-  std::vector<int> base(n + 1, 0);
+  // ---- 1. xEstimateMvPredAMVP template costs: two tasks per (request, reference) with two
+  // candidates, built into pinned memory by the host threads ----
+  std::vector<int>& base = c->pi_base;
+  std::vector<int>& task_of = c->pi_task;
+  base.resize((size_t)n + 1);
+  base[0] = 0;
   for (int i = 0; i < n; i++) base[i + 1] = base[i] + reqs[i].num_refs;
   const int nj = base[n];
-  std::vector<AmvpTask> tasks;
-  std::vector<int> task_of((size_t)nj, -1);
-  for (int i = 0; i < n; i++) {
-    const fme_pu_req& q = reqs[i];
-    for (int k = 0; k < q.num_refs; k++) {
-      if (q.n_cand[k] < 2) continue;
-      task_of[base[i] + k] = (int)tasks.size();
-      for (int m = 0; m < 2; m++)
-        tasks.push_back(AmvpTask{q.x, q.y, q.w, q.h, q.org_id, q.ref_id[k], q.cu_x, q.cu_y, q.cand[k][m][0],
-                                 q.cand[k][m][1]});
+  task_of.resize((size_t)nj);
+  int ntasks = 0;
+  for (int i = 0; i < n; i++)
+    for (int k = 0; k < reqs[i].num_refs; k++) {
+      const bool two = reqs[i].n_cand[k] >= 2;
+      task_of[base[i] + k] = two ? ntasks : -1;
+      ntasks += two ? 2 : 0;
     }
-  }
-  std::vector<uint32_t> tsad(tasks.size());
+  HIP_TRY(c->h_pi_tasks.reserve((size_t)ntasks));
+  HIP_TRY(c->h_pi_tsad.reserve((size_t)ntasks));
+  AmvpTask* const tasks = c->h_pi_tasks.p;
+  const uint32_t* const tsad = c->h_pi_tsad.p;
+  par_for(n, [&](int lo, int hi) {
+    for (int i = lo; i < hi; i++) {
+      const fme_pu_req& q = reqs[i];
+      for (int k = 0; k < q.num_refs; k++) {
+        const int t = task_of[base[i] + k];
+        if (t < 0) continue;
+        for (int m = 0; m < 2; m++)
+          tasks[t + m] = AmvpTask{q.x, q.y, q.w, q.h, q.org_id, q.ref_id[k], q.cu_x, q.cu_y, q.cand[k][m][0],
+                                  q.cand[k][m][1]};
+      }
+    }
+  });
   clk.lap(0);
-  if (!tasks.empty()) {
-    HIP_TRY(c->d_amvp.reserve(tasks.size()));
-    HIP_TRY(c->d_amvp_sad.reserve(tasks.size()));
-    HIP_TRY(hipMemcpyAsync(c->d_amvp.p, tasks.data(), tasks.size() * sizeof(AmvpTask), hipMemcpyHostToDevice, s));
-    AmvpArgs aa{c->d_amvp.p, c->d_pics.p, c->d_amvp_sad.p, (int32_t)tasks.size()};
+  if (ntasks > 0) {
+    HIP_TRY(c->d_amvp.reserve((size_t)ntasks));
+    HIP_TRY(c->d_amvp_sad.reserve((size_t)ntasks));
+    HIP_TRY(hipMemcpyAsync(c->d_amvp.p, tasks, (size_t)ntasks * sizeof(AmvpTask), hipMemcpyHostToDevice, s));
+    AmvpArgs aa{c->d_amvp.p, c->d_pics.p, c->d_amvp_sad.p, (int32_t)ntasks};
     HIP_TRY(launch_amvp_sad(aa, s));
-    HIP_TRY(hipMemcpyAsync(tsad.data(), c->d_amvp_sad.p, tasks.size() * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipMemcpyAsync(c->h_pi_tsad.p, c->d_amvp_sad.p, (size_t)ntasks * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
     HIP_TRY(hipStreamSynchronize(s));
   }
   clk.lap(1);
-  // ---- jobs: one xMotionEstimation per (request, reference) ----
-  std::vector<fme_job> jobs((size_t)nj);
-  std::vector<fme_tz_ext> ext((size_t)nj);
-  std::vector<uint8_t> amvp_idx((size_t)nj, 0);
-  for (int i = 0; i < n; i++) {
-    const fme_pu_req& q = reqs[i];
-    const PicDesc& org = c->pics[q.org_id];
-    const double ml = c->mlambda[q.lambda_id];
-    const int range = q.search_range ? q.search_range : 64;
-    for (int k = 0; k < q.num_refs; k++) {
-      const int jx = base[i] + k;
-      int idx = 0;
-      if (task_of[jx] >= 0) {   // uiBestCost > uiTmpCost: the first least cost wins
-        uint32_t best = 0xFFFFFFFFu;
-        for (int m = 0; m < 2; m++) {
-          const uint32_t cost =
-              (uint32_t)((double)tsad[task_of[jx] + m] + ((double)mvp_idx_bits(m, 2) * ml) / 65536.0);
-          if (best > cost) {
-            best = cost;
-            idx = m;
+  // ---- jobs: one xMotionEstimation per (request, reference), in request order ----
+  HIP_TRY(c->h_pi_jobs.reserve((size_t)nj));
+  HIP_TRY(c->h_pi_ext.reserve((size_t)nj));
+  fme_job* const jobs = c->h_pi_jobs.p;
+  fme_tz_ext* const ext = c->h_pi_ext.p;
+  std::vector<uint8_t>& amvp_idx = c->pi_amvp_idx;
+  amvp_idx.resize((size_t)nj);
+  par_for(n, [&](int lo, int hi) {
+    for (int i = lo; i < hi; i++) {
+      const fme_pu_req& q = reqs[i];
+      const PicDesc& org = c->pics[q.org_id];
+      const double ml = c->mlambda[q.lambda_id];
+      const int range = q.search_range ? q.search_range : 64;
+      for (int k = 0; k < q.num_refs; k++) {
+        const int jx = base[i] + k;
+        int idx = 0;
+        if (task_of[jx] >= 0) {   // uiBestCost > uiTmpCost: the first least cost wins
+          uint32_t best = 0xFFFFFFFFu;
+          for (int m = 0; m < 2; m++) {
+            const uint32_t cost =
+                (uint32_t)((double)tsad[task_of[jx] + m] + ((double)mvp_idx_bits(m, 2) * ml) / 65536.0);
+            if (best > cost) {
+              best = cost;
+              idx = m;
+            }
           }
         }
+        amvp_idx[jx] = (uint8_t)idx;
+        uint32_t bits = blk_bits_p(q.part_size);
+        if (q.num_refs > 1) bits += (uint32_t)k + 1u - (k == q.num_refs - 1 ? 1u : 0u);
+        bits += mvp_idx_bits(idx, 2);
+        const int px = q.cand[k][idx][0], py = q.cand[k][idx][1];
+        // xSetSearchRange (TEncSearch.cpp:4602-4624)
+        int cx = px, cy = py;
+        clip_qpel(cx, cy, org.width, org.height, q.cu_x, q.cu_y);
+        int lx = cx - (range << 2), ly = cy - (range << 2), rx = cx + (range << 2), ry = cy + (range << 2);
+        clip_qpel(lx, ly, org.width, org.height, q.cu_x, q.cu_y);
+        clip_qpel(rx, ry, org.width, org.height, q.cu_x, q.cu_y);
+        fme_job& j = jobs[jx];
+        j = fme_job{};
+        j.x = q.x; j.y = q.y; j.w = q.w; j.h = q.h;
+        j.org_id = q.org_id; j.ref_id = q.ref_id[k];
+        j.mvp_x = (int16_t)px; j.mvp_y = (int16_t)py;
+        j.lt_x = (int16_t)round4(lx); j.lt_y = (int16_t)round4(ly);
+        j.rb_x = (int16_t)round4(rx); j.rb_y = (int16_t)round4(ry);
+        j.flags = (uint8_t)(FME_JOB_EMI | ((q.flags & FME_PU_LOSSLESS) ? FME_JOB_LOSSLESS : 0u));
+        j.lambda_id = q.lambda_id;
+        j.bits_in = (uint16_t)bits;
+        j.key_offset = -1;
+        fme_tz_ext& e = ext[jx];
+        e = fme_tz_ext{};
+        e.cu_x = q.cu_x; e.cu_y = q.cu_y;
+        e.search_range = (uint8_t)range;
+        const bool reads = !(q.part_size == FME_PART_2Nx2N && q.depth == 0);
+        e.flags = reads ? FME_TZ_PRED2NX2N : 0;
       }
-      amvp_idx[jx] = (uint8_t)idx;
-      uint32_t bits = blk_bits_p(q.part_size);
-      if (q.num_refs > 1) bits += (uint32_t)k + 1u - (k == q.num_refs - 1 ? 1u : 0u);
-      bits += mvp_idx_bits(idx, 2);
-      const int px = q.cand[k][idx][0], py = q.cand[k][idx][1];
-      // xSetSearchRange (TEncSearch.cpp:4602-4624)
-      int cx = px, cy = py;
-      clip_qpel(cx, cy, org.width, org.height, q.cu_x, q.cu_y);
-      int lx = cx - (range << 2), ly = cy - (range << 2), rx = cx + (range << 2), ry = cy + (range << 2);
-      clip_qpel(lx, ly, org.width, org.height, q.cu_x, q.cu_y);
-      clip_qpel(rx, ry, org.width, org.height, q.cu_x, q.cu_y);
-      fme_job& j = jobs[jx];
-      j = fme_job{};
-      j.x = q.x; j.y = q.y; j.w = q.w; j.h = q.h;
-      j.org_id = q.org_id; j.ref_id = q.ref_id[k];
-      j.mvp_x = (int16_t)px; j.mvp_y = (int16_t)py;
-      j.lt_x = (int16_t)round4(lx); j.lt_y = (int16_t)round4(ly);
-      j.rb_x = (int16_t)round4(rx); j.rb_y = (int16_t)round4(ry);
-      j.flags = (uint8_t)(FME_JOB_EMI | ((q.flags & FME_PU_LOSSLESS) ? FME_JOB_LOSSLESS : 0u));
-      j.lambda_id = q.lambda_id;
-      j.bits_in = (uint16_t)bits;
-      j.key_offset = -1;
-      fme_tz_ext& e = ext[jx];
-      e = fme_tz_ext{};
-      e.cu_x = q.cu_x; e.cu_y = q.cu_y;
-      e.search_range = (uint8_t)range;
-      const bool reads = !(q.part_size == FME_PART_2Nx2N && q.depth == 0);
-      e.flags = reads ? FME_TZ_PRED2NX2N : 0;
     }
-  }
+  });
   // ---- 2. integer searches by m_integerMv2Nx2N dependency level ----
-  std::vector<int> level((size_t)n, 0), src((size_t)nj, -1), lvl((size_t)nj, 0);   // src: job whose post-EMI MV is read
+  std::vector<int>& level = c->pi_level;
+  std::vector<int>& src = c->pi_src;   // job whose post-EMI MV is read
+  std::vector<int>& lvl = c->pi_lvl;
+  level.assign((size_t)n, 0);
+  src.assign((size_t)nj, -1);
+  lvl.resize((size_t)nj);
   int last[FME_MAX_REFS] = {-1, -1, -1, -1};
+  int max_level = 0;
   for (int i = 0; i < n; i++) {
     const fme_pu_req& q = reqs[i];
     const bool reads = !(q.part_size == FME_PART_2Nx2N && q.depth == 0);
@@ -1838,6 +1925,7 @@ int fme_pred_inter_p(fme_ctx* c, const fme_pu_req* reqs, fme_pu_res* res, int n,
         }
     if (q.part_size == FME_PART_2Nx2N)
       for (int k = 0; k < q.num_refs; k++) last[k] = i;
+    max_level = std::max(max_level, level[i]);
     for (int k = 0; k < q.num_refs; k++) {
       lvl[base[i] + k] = level[i];
       fme_tz_ext& e = ext[base[i] + k];
@@ -1847,71 +1935,148 @@ int fme_pred_inter_p(fme_ctx* c, const fme_pu_req* reqs, fme_pu_res* res, int n,
       }
     }
   }
-  std::vector<int16_t> emi_mv;
+  // level order: by level, within a level the largest PUs first (blocks dispatch in index order, so
+  // the longest searches of a wide level start at once instead of forming its tail)
+  std::vector<int32_t>& off = c->pi_off;
+  std::vector<int32_t>& fill = c->pi_fill;
+  std::vector<int>& start = c->pi_start;
+  off.assign((size_t)max_level + 2, 0);
+  for (int u = 0; u < nj; u++) off[lvl[u] + 1]++;
+  for (int l = 0; l <= max_level; l++) off[l + 1] += off[l];
+  fill.assign(off.begin(), off.end() - 1);
+  start.assign(64 * 64 + 2, 0);   // counting sort by area, descending
+  for (int u = 0; u < nj; u++) start[64 * 64 - (int)jobs[u].w * jobs[u].h + 1]++;
+  for (size_t a = 1; a < start.size(); a++) start[a] += start[a - 1];
+  HIP_TRY(c->h_pi_idx.reserve((size_t)2 * nj));
+  HIP_TRY(c->h_pi_psrc.reserve((size_t)nj));
+  int32_t* const order = c->h_pi_idx.p;        // level position -> job
+  int32_t* const pos = c->h_pi_idx.p + nj;     // job -> level position
+  {
+    std::vector<int>& byarea = c->pi_level;   // request levels are no longer needed
+    byarea.resize((size_t)nj);
+    for (int u = 0; u < nj; u++) byarea[start[64 * 64 - (int)jobs[u].w * jobs[u].h]++] = u;
+    for (int u : byarea) {
+      pos[u] = fill[lvl[u]]++;
+      order[pos[u]] = u;
+    }
+  }
+  int32_t* const psrc = c->h_pi_psrc.p;
+  par_for(nj, [&](int lo, int hi) {
+    for (int q = lo; q < hi; q++) {
+      const int u = order[q];
+      psrc[q] = ((ext[u].flags & FME_TZ_PRED2NX2N) && src[u] >= 0) ? pos[src[u]] : -1;
+    }
+  });
   clk.lap(2);
-  rc = tz_by_level(c, jobs, ext, src, lvl, s, emi_mv, &clk);
-  if (rc) return rc;
+  HIP_TRY(c->d_jobs.reserve(nj));
+  HIP_TRY(c->d_tz_ext.reserve(nj));
+  HIP_TRY(c->d_pi_jobs.reserve(nj));
+  HIP_TRY(c->d_pi_ext.reserve(nj));
+  HIP_TRY(c->d_pi_idx.reserve((size_t)2 * nj));
+  HIP_TRY(c->d_ch_i32.reserve(nj));
+  HIP_TRY(c->d_tz_emi.reserve((size_t)2 * nj));
+  HIP_TRY(hipMemcpyAsync(c->d_jobs.p, jobs, (size_t)nj * sizeof(fme_job), hipMemcpyHostToDevice, s));
+  HIP_TRY(hipMemcpyAsync(c->d_tz_ext.p, ext, (size_t)nj * sizeof(fme_tz_ext), hipMemcpyHostToDevice, s));
+  HIP_TRY(hipMemcpyAsync(c->d_pi_idx.p, order, (size_t)2 * nj * sizeof(int32_t), hipMemcpyHostToDevice, s));
+  HIP_TRY(hipMemcpyAsync(c->d_ch_i32.p, psrc, (size_t)nj * sizeof(int32_t), hipMemcpyHostToDevice, s));
+  HIP_TRY(launch_gather_jobs(c->d_jobs.p, c->d_tz_ext.p, c->d_pi_idx.p, c->d_pi_jobs.p, c->d_pi_ext.p, nj, s));
+  {
+    TzArgs ta{};
+    ta.a.jobs = c->d_pi_jobs.p;
+    ta.a.keys = c->d_keys.p;
+    ta.a.n_keys = (int64_t)c->n_keys;
+    ta.a.key_invalid = c->d_key_invalid.p;
+    ta.a.mlambda = c->d_mlambda.p;
+    ta.a.pics = c->d_pics.p;
+    ta.a.n = nj;
+    ta.a.use_hadamard = c->cfg.use_hadamard ? 1 : 0;
+    ta.a.fen = c->cfg.fast_inter_mode;
+    ta.jobs_out = c->d_pi_jobs.p;
+    ta.ext = c->d_pi_ext.p;
+    ta.emi_mv = c->d_tz_emi.p;
+    const TzChain ch{c->d_ch_i32.p, max_level + 1};
+    HIP_TRY(launch_tz_levels(ta, ch, off.data(), s));
+  }
+  // the searched jobs back in request order for the sub-pel pass, on the device
+  HIP_TRY(launch_gather_jobs(c->d_pi_jobs.p, nullptr, c->d_pi_idx.p + nj, c->d_jobs.p, nullptr, nj, s));
+  HIP_TRY(hipStreamSynchronize(s));   // phase boundary (fme_pred_inter_phases)
   clk.lap(3);
-  // ---- 3. the sub-pel path over every job in request order ----
-  std::vector<fme_result> r((size_t)nj);
-  rc = fme_refine(c, jobs.data(), r.data(), nj, stream);
+  // ---- 3. the sub-pel path over every job in request order (compact results to the host) ----
+  HIP_TRY(c->d_res.reserve(nj));
+  HIP_TRY(c->d_mv.reserve(nj));
+  HIP_TRY(c->h_pi_mv.reserve((size_t)nj));
+  HIP_TRY(c->h_pi_last.reserve(FME_MAX_REFS));
+  rc = refine_batch(c, c->d_jobs.p, c->d_res.p, c->d_mv.p, nj, s);
   if (rc) return rc;
+  const fme_mv_result* const r = c->h_pi_mv.p;
+  HIP_TRY(hipMemcpyAsync(c->h_pi_mv.p, c->d_mv.p, (size_t)nj * sizeof(fme_mv_result), hipMemcpyDeviceToHost, s));
+  // m_integerMv2Nx2N[k] after this call: mv_int of the last 2Nx2N request with a reference k
+  for (int k = 0; k < FME_MAX_REFS; k++)
+    if (last[k] >= 0)
+      HIP_TRY(hipMemcpyAsync(c->h_pi_last.p + k, c->d_res.p + base[last[k]] + k, sizeof(fme_result),
+                             hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipMemcpyAsync(c->h_counts, &c->d_sched.p->invalid, sizeof(int32_t), hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipStreamSynchronize(s));
+  if (c->h_counts[0] > 0)
+    return fail(FME_E_INVALID, "fme_pred_inter_p: %d job(s) rejected by the refinement batch", c->h_counts[0]);
   clk.lap(4);
-  // ---- 4. xCheckBestMVP, reference choice, m_integerMv2Nx2N ----
-  for (int i = 0; i < n; i++) {
-    const fme_pu_req& q = reqs[i];
-    const double ml = c->mlambda[q.lambda_id];
-    fme_pu_res& o = res[i];
-    o = fme_pu_res{};
-    uint32_t best = 0xFFFFFFFFu;
-    for (int k = 0; k < q.num_refs; k++) {
-      const int jx = base[i] + k;
-      const fme_result& rr = r[jx];
-      const int mx = rr.mv_x, my = rr.mv_y;
-      int idx = amvp_idx[jx];
-      uint32_t bits = rr.bits, cost = rr.cost;
-      if (q.n_cand[k] >= 2) {
-        const int org_bits = (int)(eg_bits(mx - q.cand[k][idx][0]) + eg_bits(my - q.cand[k][idx][1]) +
-                                   mvp_idx_bits(idx, 2));
-        int best_bits = org_bits, best_idx = idx;
-        for (int m = 0; m < q.n_cand[k]; m++) {
-          if (m == idx) continue;
-          const int b = (int)(eg_bits(mx - q.cand[k][m][0]) + eg_bits(my - q.cand[k][m][1]) + mvp_idx_bits(m, 2));
-          if (b < best_bits) {
-            best_bits = b;
-            best_idx = m;
+  // ---- 4. xCheckBestMVP and the reference choice, per request ----
+  par_for(n, [&](int lo, int hi) {
+    for (int i = lo; i < hi; i++) {
+      const fme_pu_req& q = reqs[i];
+      const double ml = c->mlambda[q.lambda_id];
+      fme_pu_res& o = res[i];
+      o = fme_pu_res{};
+      uint32_t best = 0xFFFFFFFFu;
+      for (int k = 0; k < q.num_refs; k++) {
+        const int jx = base[i] + k;
+        const fme_mv_result& rr = r[jx];
+        const int mx = rr.mv_x, my = rr.mv_y;
+        int idx = amvp_idx[jx];
+        uint32_t bits = rr.bits, cost = rr.cost;
+        if (q.n_cand[k] >= 2) {
+          const int org_bits = (int)(eg_bits(mx - q.cand[k][idx][0]) + eg_bits(my - q.cand[k][idx][1]) +
+                                     mvp_idx_bits(idx, 2));
+          int best_bits = org_bits, best_idx = idx;
+          for (int m = 0; m < q.n_cand[k]; m++) {
+            if (m == idx) continue;
+            const int b = (int)(eg_bits(mx - q.cand[k][m][0]) + eg_bits(my - q.cand[k][m][1]) + mvp_idx_bits(m, 2));
+            if (b < best_bits) {
+              best_bits = b;
+              best_idx = m;
+            }
+          }
+          if (best_idx != idx) {
+            idx = best_idx;
+            const uint32_t org_total = bits;
+            bits = org_total - (uint32_t)org_bits + (uint32_t)best_bits;
+            cost = (cost - rd_cost(ml, org_total)) + rd_cost(ml, bits);
           }
         }
-        if (best_idx != idx) {
-          idx = best_idx;
-          const uint32_t org_total = bits;
-          bits = org_total - (uint32_t)org_bits + (uint32_t)best_bits;
-          cost = (cost - rd_cost(ml, org_total)) + rd_cost(ml, bits);
+        o.ref_cost[k] = cost;
+        o.ref_bits[k] = bits;
+        o.ref_mv[k][0] = (int16_t)mx;
+        o.ref_mv[k][1] = (int16_t)my;
+        o.ref_mvp_idx[k] = (uint8_t)idx;
+        if (cost < best) {
+          best = cost;
+          o.cost = cost;
+          o.bits = bits;
+          o.mv_x = (int16_t)mx;
+          o.mv_y = (int16_t)my;
+          o.ref_idx = (uint8_t)k;
+          o.mvp_idx = (uint8_t)idx;
+          o.mvp_x = q.cand[k][idx][0];
+          o.mvp_y = q.cand[k][idx][1];
         }
       }
-      o.ref_cost[k] = cost;
-      o.ref_bits[k] = bits;
-      o.ref_mv[k][0] = (int16_t)mx;
-      o.ref_mv[k][1] = (int16_t)my;
-      o.ref_mvp_idx[k] = (uint8_t)idx;
-      if (cost < best) {
-        best = cost;
-        o.cost = cost;
-        o.bits = bits;
-        o.mv_x = (int16_t)mx;
-        o.mv_y = (int16_t)my;
-        o.ref_idx = (uint8_t)k;
-        o.mvp_idx = (uint8_t)idx;
-        o.mvp_x = q.cand[k][idx][0];
-        o.mvp_y = q.cand[k][idx][1];
-      }
     }
-    if (q.part_size == FME_PART_2Nx2N)
-      for (int k = 0; k < q.num_refs; k++) {
-        c->int_mv_2n[0][k][0] = r[base[i] + k].mv_int_x;
-        c->int_mv_2n[0][k][1] = r[base[i] + k].mv_int_y;
-      }
-  }
+  });
+  for (int k = 0; k < FME_MAX_REFS; k++)
+    if (last[k] >= 0) {
+      c->int_mv_2n[0][k][0] = c->h_pi_last.p[k].mv_int_x;
+      c->int_mv_2n[0][k][1] = c->h_pi_last.p[k].mv_int_y;
+    }
   clk.lap(5);
   return FME_OK;
 }

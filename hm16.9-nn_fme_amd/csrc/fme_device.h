@@ -7,6 +7,14 @@
 
 #include "../../include/fme.h"
 
+// 0 (default): k_scatter writes only the permutation and the searches gather jobs[perm[i]];
+// 1: k_scatter also copies each job into class order (sjobs) for contiguous reads.  Same search
+// time on the 1080p frame (0.901 against 0.896 ms, profiles/r05_ab.log) for 27.6 MB less written
+// and read per batch.  A build variant for that A/B, not a second path.
+#ifndef FME_SJOBS
+#define FME_SJOBS 0
+#endif
+
 namespace fme {
 
 constexpr int kNumClasses = 24;      // HEVC inter PU shapes 4x8 .. 64x64 incl. AMP
@@ -104,7 +112,8 @@ struct Schedule;
 struct WorkBufs {
   uint8_t* cls;          // [n] class id, 255 = invalid
   int32_t* perm;         // [n] jobs grouped by class (original index)
-  fme_job* sjobs;        // [n] copies of the jobs in class order (search reads them contiguously)
+  fme_job* sjobs;        // [n] copies of the jobs in class order (FME_SJOBS 1: the searches read
+                         // them contiguously; 0: they read jobs[perm[i]] and k_scatter writes none)
   int32_t* counts;       // [kNumClasses + 1]: per-class count, [24] = invalid jobs
   int32_t* cursor;       // [kNumClasses]
   int32_t* blk_agg;      // [nblk * 9] per-block max of the NN writer indices
@@ -255,6 +264,10 @@ __device__ __forceinline__ f2 relu2(f2 s) {
 }
 // Results download into pinned host memory (fme_download_device): `wgs` workgroups of 64 lanes.
 hipError_t launch_download(const void* src, void* dst, size_t n16, int wgs, hipStream_t s);
+// dst[q] = src[idx[q]] for q < n (jobs, and the integer-search extensions when both ext pointers are
+// set): the producers' request order <-> dependency-level order on the device
+hipError_t launch_gather_jobs(const fme_job* src, const fme_tz_ext* src_ext, const int32_t* idx, fme_job* dst,
+                              fme_tz_ext* dst_ext, int n, hipStream_t s);
 hipError_t launch_nn_tail(const BatchArgs& a, const WorkBufs& w, const float* nn_params,
                           int state_in, hipStream_t s);
 

@@ -210,7 +210,7 @@ __global__ __launch_bounds__(kBlock) void k_scatter(BatchArgs a, WorkBufs w) {
     cls[q] = 255;
     if (i < a.n) {
       cls[q] = w.cls[i];
-      jb[q] = a.jobs[i];
+      if (FME_SJOBS) jb[q] = a.jobs[i];
     }
   }
 #pragma unroll
@@ -225,7 +225,7 @@ __global__ __launch_bounds__(kBlock) void k_scatter(BatchArgs a, WorkBufs w) {
     if (cls[q] < kNumClasses) {
       const int dst = sc->class_off[cls[q]] + basep[cls[q]] + rank[q];
       w.perm[dst] = i;
-      w.sjobs[dst] = jb[q];
+      if (FME_SJOBS) w.sjobs[dst] = jb[q];
     }
   }
   // Exclusive prefix-max of the NN-writer aggregates over the blocks before this one: k_nn_tail's
@@ -590,6 +590,25 @@ __global__ __launch_bounds__(kDlThreads) void k_download(const u32x4* __restrict
     dl_store(dst + i + 3 * stride, d);
   }
   for (; i < n16; i += stride) dl_store(dst + i, src[i]);
+}
+
+__global__ __launch_bounds__(kBlock) void k_gather_jobs(const fme_job* __restrict__ src,
+                                                       const fme_tz_ext* __restrict__ src_ext,
+                                                       const int32_t* __restrict__ idx, fme_job* __restrict__ dst,
+                                                       fme_tz_ext* __restrict__ dst_ext, int n) {
+  const int q = blockIdx.x * kBlock + threadIdx.x;
+  if (q >= n) return;
+  const int u = idx[q];
+  dst[q] = src[u];
+  if (dst_ext) dst_ext[q] = src_ext[u];
+}
+
+hipError_t launch_gather_jobs(const fme_job* src, const fme_tz_ext* src_ext, const int32_t* idx, fme_job* dst,
+                              fme_tz_ext* dst_ext, int n, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_gather_jobs, dim3((n + kBlock - 1) / kBlock), dim3(kBlock), 0, s, src, src_ext, idx, dst,
+                     dst_ext, n);
+  return hipGetLastError();
 }
 
 hipError_t launch_download(const void* src, void* dst, size_t n16, int wgs, hipStream_t s) {

@@ -815,14 +815,15 @@ __device__ FME_LANE_UNIT_ATTR void lane_unit(const BatchArgs& a, const fme_job* 
   const int uu = u < NUH ? u : NUH - 1;
   const int ux = uu % UX, uy = uu / UX;
 
+  const int jid = perm[cls_off + p];
   fme_job j;
   {   // two 16-byte global loads (a struct copy through an address-space-1 pointer does not compile
-      // in the host pass)
-    const u32x4a q0 = *(gu4*)(sjobs + cls_off + p), q1 = *(gu4*)((g_u8*)(sjobs + cls_off + p) + 16);
+      // in the host pass): the class-ordered copy, or (FME_SJOBS 0) the caller's job by its index
+    g_job* const src = FME_SJOBS ? sjobs + cls_off + p : (g_job*)a.jobs + jid;
+    const u32x4a q0 = *(gu4*)src, q1 = *(gu4*)((g_u8*)src + 16);
     uint32_t tmp[8] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w};
     __builtin_memcpy(&j, tmp, sizeof(j));
   }
-  const int jid = perm[cls_off + p];
   // The reference's descriptor is read from LDS where a window is loaded (an opaque index keeps
   // the compiler from holding the 40-byte copy in registers, or scratch, across the passes).
   auto ref_pic = [&]() FME_AI -> PicDesc {

@@ -42,6 +42,9 @@ constexpr int kHW = FME_NN_MAX_WIDTH;             // hidden width (padded)
 constexpr int kHP = 48;                           // hidden rows padded to 3 MFMA tiles
 constexpr int kOP = 64;                           // output rows padded to 4 MFMA tiles
 constexpr int kAS = 65;                           // LDS activation row stride (elements)
+#ifndef FME_DEEP_MALL
+#define FME_DEEP_MALL 1
+#endif
 #ifndef FME_DEEP_BHOIST
 #define FME_DEEP_BHOIST 1
 #endif
@@ -174,18 +177,27 @@ __device__ __forceinline__ void layer_mfma(T* act, const T* __restrict__ W, cons
 #pragma unroll
       for (int nt = 0; nt < NT; nt++) bw[kk][nt] = W[(nt * 16 + c16) * K + kk * 4 + k4];
   }
+  // ALL (FME_DEEP_MALL): the four 16-job tiles' accumulators in flight together, k outermost, so
+  // 4 * NT independent MFMA chains hide the f64 MFMA latency at one wave per SIMD (the tile-by-tile
+  // order had NT = 3 or 4 chains); each accumulator still sums k in the same order (same bits).
+  constexpr int MG = FME_DEEP_MALL ? 4 : 1;   // tiles per pass
 #pragma unroll
-  for (int mt = 0; mt < 4; mt++) {
-    typename M::acc_t acc[NT];
+  for (int m0 = 0; m0 < 4; m0 += MG) {
+    typename M::acc_t acc[MG][NT];
 #pragma unroll
-    for (int nt = 0; nt < NT; nt++) acc[nt] = typename M::acc_t{0, 0, 0, 0};
+    for (int mi = 0; mi < MG; mi++)
+#pragma unroll
+      for (int nt = 0; nt < NT; nt++) acc[mi][nt] = typename M::acc_t{0, 0, 0, 0};
 #pragma unroll
     for (int kk = 0; kk < K / 4; kk++) {
-      const T a = act[(mt * 16 + c16) * kAS + kk * 4 + k4];         // A[job][k]
 #pragma unroll
-      for (int nt = 0; nt < NT; nt++) {
-        const T b = HOIST ? bw[HOIST ? kk : 0][nt] : W[(nt * 16 + c16) * K + kk * 4 + k4];
-        acc[nt] = M::mma(a, b, acc[nt]);
+      for (int mi = 0; mi < MG; mi++) {
+        const T a = act[((m0 + mi) * 16 + c16) * kAS + kk * 4 + k4];   // A[job][k]
+#pragma unroll
+        for (int nt = 0; nt < NT; nt++) {
+          const T b = HOIST ? bw[HOIST ? kk : 0][nt] : W[(nt * 16 + c16) * K + kk * 4 + k4];
+          acc[mi][nt] = M::mma(a, b, acc[mi][nt]);
+        }
       }
     }
     if constexpr (sizeof(T) == 8) {
@@ -194,7 +206,9 @@ __device__ __forceinline__ void layer_mfma(T* act, const T* __restrict__ W, cons
       // rows were read stale in every tile but the last (tools/deep_probe.py).  Pad explicitly:
       // the accumulators are operands of the pad, so no read of them is placed before it.
 #pragma unroll
-      for (int nt = 0; nt < NT; nt++) asm volatile("s_nop 15\n\ts_nop 15" : "+a"(acc[nt]));
+      for (int mi = 0; mi < MG; mi++)
+#pragma unroll
+        for (int nt = 0; nt < NT; nt++) asm volatile("s_nop 15\n\ts_nop 15" : "+a"(acc[mi][nt]));
     }
 #pragma unroll
     for (int nt = 0; nt < NT; nt++) {
@@ -205,11 +219,13 @@ __device__ __forceinline__ void layer_mfma(T* act, const T* __restrict__ W, cons
         bbe = be[col];
       }
 #pragma unroll
-      for (int r = 0; r < 4; r++) {
-        T s = acc[nt][r] + bb;
-        if (HIDDEN) s = relu(s) * gg + bbe;
-        act[(mt * 16 + M::row(lane, r)) * kAS + col] = s;
-      }
+      for (int mi = 0; mi < MG; mi++)
+#pragma unroll
+        for (int r = 0; r < 4; r++) {
+          T s = acc[mi][nt][r] + bb;
+          if (HIDDEN) s = relu(s) * gg + bbe;
+          act[((m0 + mi) * 16 + M::row(lane, r)) * kAS + col] = s;
+        }
     }
   }
 }
@@ -319,23 +335,32 @@ __global__ __launch_bounds__(kRound) void k_nn_deep_tail(BatchArgs a, WorkBufs w
     if (valid) j = a.jobs[i];
     // writer indices of this job, prefix-max over the round (carry from earlier rounds/blocks)
     int run[9];
+    const bool wr = valid && nn_writes_c(j);
     {
-      const bool wr = valid && nn_writes_c(j);
       const int np = wr ? nn_pushes(j) : 0;
 #pragma unroll
       for (int s = 0; s < 8; s++) run[s] = (np > s) ? i : -1;
       run[8] = wr ? i : -1;
     }
-    int src[9], tot[9];
-    writer_scan<kRound / 64>(run, carry, blockIdx.x * kJobsPerScanBlock + rnd * kRound, wave_tot, src, tot);
+    // FME_NN_IN_SLOT_RESET: the backups memset array_e on every call, so only this call's own
+    // pushes are non-zero (Backups/4:4421-4422, Backups/15:4961-4962) and only C / PU size carry.
+    // A round whose every job writes them (the backups' input path: every uni-pred job) needs no
+    // scan at all: each job is its own last writer, and the carry is the round's last job.
+    const bool reset = (d.in_flags & FME_NN_IN_SLOT_RESET) != 0;
+    int src[9];
+    if (reset && __syncthreads_and(!valid || wr)) {
 #pragma unroll
-    for (int f = 0; f < 9; f++) carry[f] = tot[f];
-    __syncthreads();   // wave_tot is rewritten next round
+      for (int f = 0; f < 9; f++) src[f] = run[f];
+      carry[8] = min(a.n, blockIdx.x * kJobsPerScanBlock + (rnd + 1) * kRound) - 1;
+    } else {
+      int tot[9];
+      writer_scan<kRound / 64>(run, carry, blockIdx.x * kJobsPerScanBlock + rnd * kRound, wave_tot, src, tot);
+#pragma unroll
+      for (int f = 0; f < 9; f++) carry[f] = tot[f];
+      __syncthreads();   // wave_tot is rewritten next round
+    }
 
     // the NN_pred() inputs this job sees (TEncSearch.cpp:88-113 / Backups/15:4944-5000)
-    // FME_NN_IN_SLOT_RESET: the backups memset array_e on every call, so only this call's own
-    // pushes are non-zero (Backups/4:4421-4422, Backups/15:4961-4962).
-    const bool reset = (d.in_flags & FME_NN_IN_SLOT_RESET) != 0;
     uint32_t e[8];
     uint32_t written = st_in[11];
 #pragma unroll

@@ -69,6 +69,9 @@ __device__ __forceinline__ uint32_t px_cost(double ml, uint32_t bits) {   // TCo
   return (uint32_t)((ml * (double)bits) / 65536.0);
 }
 
+// Classes 0 .. kPxSmallClasses-1 (fme_device.h kClassW / kClassH: 4x8 .. 16x16) are at most 16
+// wide and tall: one wave per job (k_search_px_wave); the larger shapes one workgroup per job.
+constexpr int kPxSmallClasses = 10;
 constexpr int kPxMaxWin = (64 + 10) * (64 + 10);
 constexpr int kPxMaxPlane = (64 + 8) * (64 + 1);
 struct PxLds {
@@ -84,8 +87,8 @@ struct PxLds {
 // One (candidate, block group) item: lanes = the group's pixels; quarter-pel offset (ox, oy) from
 // the re-centred integer MV (wave-uniform).  Returns the group's summed per-tile transform (8x8:
 // (s + 2) >> 2 per tile; 4x4: (s + 1) >> 1 per tile) or SAD, on every lane.
-template <int BD, bool SAD, bool B8>
-__device__ __forceinline__ uint32_t px_item(const PxLds& L, int w, int ws, int ex, int ey, int nb4, int b, int ox,
+template <int BD, bool SAD, bool B8, class LT>
+__device__ __forceinline__ uint32_t px_item(const LT& L, int w, int ws, int ex, int ey, int nb4, int b, int ox,
                                             int oy, int lane) {
   constexpr int HR = 14 - BD < 2 ? 2 : 14 - BD, SH2 = 6 + HR, MAXV = (1 << BD) - 1;
   const int bw8 = w >> 3, bw4 = w >> 2;
@@ -164,7 +167,7 @@ __device__ void px_stage(PxLds& L, int w, int h, int ws, int ex, int ey, int st,
     }
     const int ox = bx0 + (st == 0 ? 2 * px_ref(kPxHx, k) : px_ref(kPxQx, k));
     const int oy = by0 + (st == 0 ? 2 * px_ref(kPxHy, k) : px_ref(kPxQy, k));
-    acc += px_item<BD, SAD, B8>(L, w, ws, ex, ey, nb4, b, ox, oy, lane);
+    acc += px_item<BD, SAD, B8, PxLds>(L, w, ws, ex, ey, nb4, b, ox, oy, lane);
   }
   if (i0 < i1 && lane == 0) atomicAdd(&L.cost[st][kcur], acc);
 }
@@ -204,7 +207,9 @@ __global__ __launch_bounds__(kPxNT) void k_search_px(BatchArgs a, WorkBufs wb) {
   if (wb.sched->invalid) return;   // rejected batch: the tail marks every record
   constexpr int HR = 14 - BD < 2 ? 2 : 14 - BD, SH1 = 6 - HR, DSH = BD - 8;
   const int tid = (int)threadIdx.x, lane = tid & 63;
-  for (int i = blockIdx.x; i < a.n; i += gridDim.x) {
+  // the PUs wider or taller than 16 (class order from k_scatter; k_search_px_wave takes the rest)
+  for (int q = wb.sched->class_off[kPxSmallClasses] + (int)blockIdx.x; q < a.n; q += gridDim.x) {
+    const int i = wb.perm[q];
     const fme_job j = a.jobs[i];
     const int w = j.w, h = j.h, ws = w + 10, wh = h + 10;
     // ---- 1. window and key -------------------------------------------------------------------
@@ -373,6 +378,212 @@ __global__ __launch_bounds__(kPxNT) void k_search_px(BatchArgs a, WorkBufs wb) {
   }
 }
 
+// ---- one wave per job: the PUs of at most 16 x 16 -------------------------------------------------
+// The same five steps as k_search_px with the wave's own LDS slice and no workgroup barrier: the
+// 4x8 / 8x4 / 8x8 majority of a frame's PUs kept a 256-lane workgroup and eight barriers busy per
+// job (17 us of workgroup time per job on the 1080p main10 frame).  Sums are wave reductions
+// (every lane holds every total), so the EMI decision and the candidate picks run on all lanes.
+constexpr int kPxSW = 16;                                   // largest side of the wave kernel's PUs
+struct PxSmall {
+  int16_t win[(kPxSW + 10) * (kPxSW + 10)];
+  alignas(16) int16_t key[kPxSW * kPxSW];
+  int16_t hp[3][(kPxSW + 8) * (kPxSW + 1)];
+};
+__device__ __forceinline__ void px_wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+template <int BD, bool SAD, bool B8>
+__device__ __forceinline__ void px_wave_costs(const PxSmall& L, int w, int h, int ws, int ex, int ey, int st, int bx0,
+                                              int by0, int lane, uint32_t (&cost)[9]) {
+  const int nb4 = (w >> 2) * (h >> 2);
+  const int nb = B8 ? (w >> 3) * (h >> 3) : (nb4 + 3) >> 2;
+#pragma unroll
+  for (int k = 0; k < 9; k++) {
+    const int ox = bx0 + (st == 0 ? 2 * px_ref(kPxHx, k) : px_ref(kPxQx, k));
+    const int oy = by0 + (st == 0 ? 2 * px_ref(kPxHy, k) : px_ref(kPxQy, k));
+    uint32_t acc = 0;
+    for (int b = 0; b < nb; b++) acc += px_item<BD, SAD, B8, PxSmall>(L, w, ws, ex, ey, nb4, b, ox, oy, lane);
+    cost[k] = acc;
+  }
+}
+
+template <int BD>
+__global__ __launch_bounds__(kPxNT) void k_search_px_wave(BatchArgs a, WorkBufs wb) {
+  __shared__ PxSmall Ls[kPxWaves];
+  if (wb.sched->invalid) return;
+  constexpr int HR = 14 - BD < 2 ? 2 : 14 - BD, SH1 = 6 - HR, DSH = BD - 8;
+  const int lane = (int)threadIdx.x & 63, wid = (int)threadIdx.x >> 6;
+  PxSmall& L = Ls[wid];
+  const int n_small = wb.sched->class_off[kPxSmallClasses];
+  for (int q = (int)blockIdx.x * kPxWaves + wid; q < n_small; q += (int)gridDim.x * kPxWaves) {
+    const int i = __builtin_amdgcn_readfirstlane(wb.perm[q]);
+    const fme_job j = a.jobs[i];
+    const int w = j.w, h = j.h, ws = w + 10, wh = h + 10;
+    // ---- 1. window and key (rows of the window per pass: 64 / ws) ----
+    {
+      const PicDesc ref = a.pics[j.ref_id];
+      const uint16_t* rl = reinterpret_cast<const uint16_t*>(ref.luma);
+      const int x0 = (int)j.x + j.mv_x - 5, y0 = (int)j.y + j.mv_y - 5;
+      const int rpp = 64 / ws, lr = lane / ws, lc = lane - lr * ws;
+      const int xx = min(max(x0 + lc, 0), ref.width - 1);
+      if (lr < rpp)
+        for (int r = lr; r < wh; r += rpp) {
+          const int yy = min(max(y0 + r, 0), ref.height - 1);
+          L.win[r * ws + lc] = (int16_t)rl[(size_t)yy * ref.stride + xx];
+        }
+      const int kr = lane / w, kc = lane - kr * w, krp = 64 / w;
+      if (j.key_offset >= 0) {
+        const int16_t* kb = a.keys + j.key_offset;
+        for (int e = lane; e < w * h; e += 64) L.key[e] = kb[e];
+      } else {
+        const PicDesc org = a.pics[j.org_id];
+        const uint16_t* ol = reinterpret_cast<const uint16_t*>(org.luma);
+        if (kr < krp)
+          for (int r = kr; r < h; r += krp) L.key[r * w + kc] = (int16_t)ol[(size_t)(j.y + r) * org.stride + j.x + kc];
+      }
+    }
+    px_wave_sync();
+    const double ml = a.mlambda[j.lambda_id];
+    // ---- 2. EMI square step (or the backups' NN input row) ----
+    int ex = 0, ey = 0, n_emi = 0;
+    uint32_t cval = 0, emi[8];
+#pragma unroll
+    for (int p = 0; p < 8; p++) emi[p] = 0;
+    if (j.flags & FME_JOB_NN_IN) {   // takes precedence over FME_JOB_EMI (fme.h)
+      const uint32_t* row = a.nn_in + (size_t)9 * i;
+#pragma unroll
+      for (int p = 0; p < 8; p++) emi[p] = row[p];
+      cval = row[8];
+      n_emi = 8;
+    } else if (j.flags & FME_JOB_EMI) {
+      const bool sad = w == 12 || w == 24 || w == 48;
+      const int sub = (sad && (a.fen == 1 || a.fen == 3) && h > 8) ? 1 : 0;
+      uint32_t e9[9];
+#pragma unroll
+      for (int p = 0; p < 9; p++) e9[p] = 0;
+      for (int e = lane; e < w * h; e += 64) {
+        const int r = e / w, cc = e - r * w;
+        if (sub && (r & 1)) continue;
+        const int kv = L.key[e];
+#pragma unroll
+        for (int p = 0; p < 9; p++) {
+          const int d = kv - (int)L.win[(r + 5 + px_emi_dy(p)) * ws + cc + 5 + px_emi_dx(p)];
+          e9[p] += sad ? (uint32_t)abs(d) : ((uint32_t)(d * d) >> (2 * DSH));
+        }
+      }
+#pragma unroll
+      for (int p = 0; p < 9; p++) {
+        const uint32_t v = wave_sum(e9[p], lane);
+        e9[p] = sad ? ((v << sub) >> DSH) : v;
+      }
+      const int sx = j.mv_x, sy = j.mv_y;
+      auto cost_at = [&](int x, int y) {   // cost scale 2 (full-pel MV against the quarter-pel predictor)
+        return px_cost(ml, px_eg_bits((x << 2) - j.mvp_x) + px_eg_bits((y << 2) - j.mvp_y));
+      };
+      uint32_t best = e9[0] + cost_at(sx, sy), best_cost = best - e9[0];
+      int bx = sx, by = sy;
+      const bool top = sy - 1 >= j.lt_y, bot = sy + 1 <= j.rb_y, left = sx - 1 >= j.lt_x, right = sx + 1 <= j.rb_x;
+#pragma unroll
+      for (int p = 1; p <= 8; p++) {
+        const int dx = px_emi_dx(p), dy = px_emi_dy(p);
+        const bool ok = (dy == -1 ? top : (dy == 1 ? bot : true)) && (dx == -1 ? left : (dx == 1 ? right : true));
+        if (!ok) continue;
+        const uint32_t d = e9[p];
+#pragma unroll
+        for (int s = 0; s < 8; s++)   // emi[n_emi++] = d with static register indices
+          if (s == n_emi) emi[s] = d;
+        n_emi++;
+        if (d < best) {
+          const uint32_t cst = cost_at(sx + dx, sy + dy);
+          if (d + cst < best) {
+            best = d + cst;
+            best_cost = cst;
+            bx = sx + dx;
+            by = sy + dy;
+          }
+        }
+      }
+      ex = bx - sx;
+      ey = by - sy;
+      cval = best - best_cost;
+    }
+    const int mvx = j.mv_x + ex, mvy = j.mv_y + ey;
+    // ---- 3. first filter stage of phases 1..3, row by row ----
+    {
+      const int cols = w + 1, rows = h + 8, rpp = 64 / cols, lr = lane / cols, lc = lane - lr * cols;
+      if (lr < rpp)
+        for (int f = 0; f < 3; f++)
+          for (int wy = lr; wy < rows; wy += rpp) {
+            const int16_t* row = L.win + (wy + 1 + ey) * ws + lc + 1 + ex;
+            int s = 0;
+#pragma unroll
+            for (int t = 0; t < 8; t++) s += px_tap(f + 1, t) * (int)row[t];
+            L.hp[f][wy * cols + lc] = (int16_t)((s - 8192 * (1 << SH1)) >> SH1);
+          }
+    }
+    px_wave_sync();
+    // ---- 4. half and quarter stages, the first strict minimum in xPatternRefinement's order ----
+    const bool use_sad = !a.use_hadamard || (j.flags & FME_JOB_LOSSLESS);
+    const bool b8 = (w & 7) == 0 && (h & 7) == 0;
+    uint32_t cost[9];
+    auto stage = [&](int st, int bx0, int by0) {
+      if (use_sad)
+        px_wave_costs<BD, true, false>(L, w, h, ws, ex, ey, st, bx0, by0, lane, cost);
+      else if (b8)
+        px_wave_costs<BD, false, true>(L, w, h, ws, ex, ey, st, bx0, by0, lane, cost);
+      else
+        px_wave_costs<BD, false, false>(L, w, h, ws, ex, ey, st, bx0, by0, lane, cost);
+    };
+    auto pick = [&](int st, int hx, int hy, uint32_t& best) -> int {
+      int bk = 0;
+      best = 0xFFFFFFFFu;
+#pragma unroll
+      for (int k = 0; k < 9; k++) {
+        uint32_t bits;
+        if (st == 0)   // cost scale 1 around 2 * mv_int
+          bits = px_eg_bits(((2 * mvx + px_ref(kPxHx, k)) << 1) - j.mvp_x) +
+                 px_eg_bits(((2 * mvy + px_ref(kPxHy, k)) << 1) - j.mvp_y);
+        else           // cost scale 0 around 4 * mv_int + 2 * half
+          bits = px_eg_bits(4 * mvx + 2 * hx + px_ref(kPxQx, k) - j.mvp_x) +
+                 px_eg_bits(4 * mvy + 2 * hy + px_ref(kPxQy, k) - j.mvp_y);
+        const uint32_t tot = (cost[k] >> DSH) + px_cost(ml, bits);
+        if (tot < best) {
+          best = tot;
+          bk = k;
+        }
+      }
+      return bk;
+    };
+    uint32_t hbest, qbest;
+    stage(0, 0, 0);
+    const int hk = pick(0, 0, 0, hbest);
+    const int hx = px_ref(kPxHx, hk), hy = px_ref(kPxHy, hk);
+    stage(1, 2 * hx, 2 * hy);
+    const int qk = pick(1, hx, hy, qbest);
+    (void)hbest;
+    // ---- 5. the record (fme_result bytes 0..63; the tail adds mv, cost, bits, class, status) ----
+    if (lane < 4) {
+      uint4 o;
+      if (lane == 0)
+        o = make_uint4((uint32_t)(uint16_t)mvx | ((uint32_t)(uint16_t)mvy << 16), 0u,
+                       (uint32_t)(uint8_t)hx | ((uint32_t)(uint8_t)hy << 8) | ((uint32_t)(uint8_t)px_ref(kPxQx, qk) << 16) |
+                           ((uint32_t)(uint8_t)px_ref(kPxQy, qk) << 24),
+                       qbest);
+      else if (lane == 1)
+        o = make_uint4(0u, 0u, cval, emi[0]);
+      else if (lane == 2)
+        o = make_uint4(emi[1], emi[2], emi[3], emi[4]);
+      else
+        o = make_uint4(emi[5], emi[6], emi[7], (uint32_t)n_emi);
+      reinterpret_cast<uint4*>(a.res + i)[lane] = o;
+    }
+    px_wave_sync();   // the next job rewrites this wave's LDS
+  }
+}
+
 }  // namespace
 
 // Workgroups of the pixel kernel: three fit a CU (47 KB of LDS each), persistent over the jobs.
@@ -383,9 +594,12 @@ hipError_t launch_search_px(const BatchArgs& a, const WorkBufs& w, int bit_depth
     (void)hipGetDevice(&dev);
     cus = cu_count(dev);
   }
-  const int blocks = (int)std::min<long long>(a.n, 3LL * cus);
-  if (blocks <= 0) return hipSuccess;
+  if (a.n <= 0) return hipSuccess;
   if (bit_depth != 10) return hipErrorInvalidValue;
+  // the small PUs, a wave each (17 KB of LDS per workgroup), then the larger ones, a workgroup each
+  const int wave_blocks = (int)std::min<long long>((a.n + kPxWaves - 1) / kPxWaves, 8LL * cus);
+  hipLaunchKernelGGL(k_search_px_wave<10>, dim3(wave_blocks), dim3(kPxNT), 0, s, a, w);
+  const int blocks = (int)std::min<long long>(a.n, 3LL * cus);
   hipLaunchKernelGGL(k_search_px<10>, dim3(blocks), dim3(kPxNT), 0, s, a, w);
   return hipGetLastError();
 }

@@ -713,7 +713,7 @@ void k_tz_wave(TzArgs ta, TzSchedule sc, int kid) {
   const int q = tz_entry(sc, kid, x, t, c);
   if (q < 0) return;
   const int jid = ta.perm[q];
-  const fme_job j = ta.sjobs[q];
+  const fme_job j = FME_SJOBS ? ta.sjobs[q] : ta.a.jobs[jid];
   tz_wave<UW, UH>(ta, jid, j, kTzW[c], kTzH[c], ta.ext[jid].pred2n_x, ta.ext[jid].pred2n_y);
 }
 

@@ -96,10 +96,11 @@ def group_key_reqs(base, frames, key_count):
 class FrameReplay:
     def __init__(self, ctx, base_jobs, pool, lambda_of, n_steps, frames_per_step=1, world=1, rank=0, device=None,
                  group=None, defer_download=True, key_reqs=None, key_count=0, nn_rows=None,
-                 download_engine="kernel", download_wgs=8):
+                 download_engine="blit", download_wgs=8):
         """ctx: an FmeContext on `device`; base_jobs: one frame's jobs (ref_id = reference
         distance - 1); pool: uint8 [P, H, W] host frames, frame g's pictures are pool[g % P];
-        lambda_of(g): frame g's lambda.  key_reqs (fme_bikey_req, ref_id = distance - 1) and
+        lambda_of(g): frame g's lambda (pool uint16: main10 samples for a bit-depth-10 context,
+        the pictures bound with the stride in samples).  key_reqs (fme_bikey_req, ref_id = distance - 1) and
         key_count: the frame's bi-pred key requests; each step uploads them with its jobs and builds
         its frames' removeHighFreq keys on the device from that step's pictures, before its batch
         (fme_build_bipred_keys_device), so the keys are per-frame work inside the timed step.
@@ -117,7 +118,12 @@ class FrameReplay:
         self.steps = n_steps
         P, H, W = pool.shape
         self.P, self.H, self.W = P, H, W
-        self.pool = torch.from_numpy(np.ascontiguousarray(pool)).pin_memory()
+        if pool.dtype not in (np.uint8, np.uint16):
+            raise ValueError(f"frame pool dtype {pool.dtype}: uint8 or uint16 (main10) samples")
+        self.bps = pool.dtype.itemsize                  # bytes per sample
+        pdt = torch.uint8 if self.bps == 1 else torch.int16   # 10-bit samples fit int16
+        host = np.ascontiguousarray(pool).view(np.uint8 if self.bps == 1 else np.int16)
+        self.pool = torch.from_numpy(host).pin_memory()
         self.key_count = int(key_count)
         self.jobs = group_jobs(base_jobs, F, self.key_count)
         self.n = n = len(self.jobs)
@@ -138,8 +144,8 @@ class FrameReplay:
         self.h_out = torch.empty((n_steps, n * MV_RESULT_DTYPE.itemsize), dtype=torch.uint8).pin_memory()
         frames = n_steps * world * F
         # every reconstructed picture of the run (frames -4 .. frames - 1) and this rank's originals
-        self.recon = torch.empty((frames + REFS, H, W), dtype=torch.uint8, device=device)
-        self.org = torch.empty((n_steps * F, H, W), dtype=torch.uint8, device=device)
+        self.recon = torch.empty((frames + REFS, H, W), dtype=pdt, device=device)
+        self.org = torch.empty((n_steps * F, H, W), dtype=pdt, device=device)
         self.states = torch.zeros((n_steps, 12), dtype=torch.int32, device=device)
         self.s_comp = torch.cuda.default_stream(device)
         self.s_copy = torch.cuda.Stream(device)   # H2D: jobs, originals, reconstructions
@@ -170,7 +176,7 @@ class FrameReplay:
         broadcast to every rank."""
         dst = self.recon[g + REFS]
         if self.rank == src_rank:
-            _memcpy_async(dst, self.pool[g % self.P], self.H * self.W, H2D, torch_current_stream(dst))
+            _memcpy_async(dst, self.pool[g % self.P], self.H * self.W * self.bps, H2D, torch_current_stream(dst))
         if self.world > 1:
             import torch.distributed as dist
             if dist.get_backend(self.group) == "gloo":   # CPU rehearsal of the sharded path
@@ -237,7 +243,7 @@ class FrameReplay:
         while i < count:
             s = (g0 + i) % self.P
             run = min(count - i, self.P - s)
-            _memcpy_async(dst[d0 + i], self.pool[s], run * self.H * self.W, H2D, stream)
+            _memcpy_async(dst[d0 + i], self.pool[s], run * self.H * self.W * self.bps, H2D, stream)
             i += run
 
     def _publish_run(self, g0, count, src_rank, stream):

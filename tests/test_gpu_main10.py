@@ -92,3 +92,40 @@ def test_main10_frame_every_job_against_reference():
     bad, first, counts = compare_results(a, want, fields)
     assert bad == 0, f"main10 frame: {bad} of {len(jobs)} jobs differ, first {first}: {counts}"
     assert JOB_DTYPE.itemsize == 32 and RESULT_DTYPE.itemsize == 64 and MV_FIELDS
+
+
+def test_main10_frame_replay_against_reference():
+    """The bench's replay (FrameReplay: per-step uploads of 16-bit originals and reconstructions,
+    pictures bound with the stride in samples, the results downloaded by the library's kernel) at
+    bit depth 10, two frames per step over three steps: every step's results equal oracle/_ref run
+    frame after frame with that step's pictures, lambdas and the NN state carried across steps."""
+    import torch
+    from nnfme import pipeline
+    from nnfme.pipeline import FrameReplay
+    from nnfme.runtime import FmeContext
+    from oracle import Reference
+    w, h, F, steps = 416, 240, 2, 3
+    base = synth.make_ctu_jobs(np.random.default_rng(43), w, h, 200, 4, [0, 1, 2, 3], [0])
+    pool = np.stack([synth.synth_luma_hbd(w, h, t, 10) for t in range(8)])
+    assert pool.dtype == np.uint16 and int(pool.max()) > 255
+    lam = lambda f: synth.LDP_LAMBDA[22][(f + 1) % 4]   # noqa: E731
+    ctx = FmeContext(nn_mode=1, qp=22, fast_inter_mode=1, bit_depth=10)
+    rep = FrameReplay(ctx, base, pool, lam, steps, frames_per_step=F, device=torch.device("cuda", 0))
+    rep.prime()
+    for k in range(steps):
+        rep.issue(k)
+    rep.finish()
+    ref = Reference(use_hadamard=1, nn_mode=1, fast_inter_mode=1, bit_depth=10)
+    ref.load_nn(weights.load_weights(22))
+    for k in range(steps):
+        f0 = rep.first_frame(k)
+        for j in range(F):
+            ref.set_picture(pipeline.ORG0 + j, pool[(f0 + j) % 8])
+            ref.set_lambda(j, lam(f0 + j))
+        for s in range(F + pipeline.REFS - 1):
+            ref.set_picture(s, pool[(f0 - pipeline.REFS + s) % 8])
+        want = ref.refine(rep.jobs)
+        got = rep.results(k)
+        for f in ("mv_x", "mv_y", "cost", "bits", "nn_class"):
+            bad = np.flatnonzero(got[f] != want[f])
+            assert len(bad) == 0, f"step {k}: {f} differs at {len(bad)} jobs, first {bad[:5]}"

@@ -28,7 +28,7 @@ if [ "${PROF:-1}" = 1 ]; then
 fi
 if [ "${WORKLOADS:-1}" = 1 ]; then
   run bench_c1 300 python bench.py --workload c1 --no-pi --no-tz --no-mc --cpu-seconds 12 --cpu-cores -1
-  for w in c2 c3_qp27 c3_qp32 c3_qp37 c4 c5 c5_exact c5_b4x40; do
+  for w in c2 c3_qp27 c3_qp32 c3_qp37 c3_qp22_main10 c4 c5 c5_exact c5_b4x40; do
     run bench_$w 300 $B --workload $w
   done
 fi

@@ -22,14 +22,26 @@ for step in "$@"; do
     benchfull) run benchfull 600 python -u bench.py ;;
     prof) run prof 400 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run -- python3 bench.py --no-cpu-baseline --no-pi --no-tz --no-mc --parity-seconds 0 ;;
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
-    pdebug) run pdebug 300 python -u tools/parity_debug.py ;;
+    pdebug) run pdebug 300 python -u tools/parity_debug.py 20 3 8 && run pdebug10 300 python -u tools/parity_debug.py 3 3 10 ;;
+    pprobe) CPU=0 run pprobe 300 python -u tools/pred_inter_probe.py 3 ;;
+    m10prof) run m10prof 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/m10prof -o run -- python3 bench.py --workload c3_qp22_main10 --no-cpu-baseline --parity-seconds 0 --steps 5 ;;
     d2h) run d2h 200 ./tools/probes/d2h_kernel_probe ;;
     deepab) run deep_hoist 400 python -u bench.py --workload c5 --no-cpu-baseline --parity-seconds 0 --steps 20 && \
             FME_LIB_PATH=$PWD/hm16.9-nn_fme_amd/variants/deep_nohoist/libfme_amd.so run deep_nohoist 400 python -u bench.py --workload c5 --no-cpu-baseline --parity-seconds 0 --steps 20 ;;
-    pbench) run pb3 300 python -u bench.py --no-pi --no-tz --no-mc --cpu-seconds 2 --steps 3 --parity-seconds 4 && \
-            run pb20 300 python -u bench.py --no-pi --no-tz --no-mc --no-cpu-baseline --steps 20 --parity-seconds 4 && \
-            run pb20blit 300 python -u bench.py --no-pi --no-tz --no-mc --no-cpu-baseline --steps 20 --parity-seconds 4 --download-engine blit ;;
-    occab) run occab 400 python -u tools/ab_bench.py hm16.9-nn_fme_amd hm16.9-nn_fme_amd/variants/s0 hm16.9-nn_fme_amd/variants/w3s0 --rounds 4 ;;
+    pbench) run pbA 300 python -u bench.py --no-pi --no-tz --no-mc --no-cpu-baseline --steps 20 --parity-seconds 3 && \
+            run pbB 300 python -u bench.py --no-pi --no-tz --no-mc --cpu-seconds 2 --steps 3 --parity-seconds 3 && \
+            run pbC 300 python -u bench.py --workload c3_qp22_main10 --no-cpu-baseline --steps 3 --parity-seconds 3 && \
+            run pbD 300 python -u bench.py --workload c3_qp22_main10 --cpu-seconds 2 --steps 3 --parity-seconds 3 ;;
+    resab) run res_blit 300 python -u bench.py --no-pi --no-tz --no-mc --no-cpu-baseline --parity-seconds 0 && \
+           FME_LIB_PATH=$PWD/hm16.9-nn_fme_amd/variants/res16/libfme_amd.so run res16_k8 300 python -u bench.py --no-pi --no-tz --no-mc --no-cpu-baseline --parity-seconds 0 --download-engine kernel --download-wgs 8 && \
+           FME_LIB_PATH=$PWD/hm16.9-nn_fme_amd/variants/res16/libfme_amd.so run res16_k16 300 python -u bench.py --no-pi --no-tz --no-mc --no-cpu-baseline --parity-seconds 0 --download-engine kernel --download-wgs 16 && \
+           FME_LIB_PATH=$PWD/hm16.9-nn_fme_amd/variants/res16/libfme_amd.so run res16_blit 300 python -u bench.py --no-pi --no-tz --no-mc --no-cpu-baseline --parity-seconds 0 ;;
+    occab) run occab 400 python -u tools/ab_bench.py . variants/s0 variants/w3s0 variants/nosj --rounds 4 ;;
+    main10) run main10_test 300 python -u -m pytest tests/test_gpu_main10.py -m gpu -x -q -p no:cacheprovider --timeout 200 --timeout-method thread && \
+            run main10_bench 400 python -u bench.py --workload c3_qp22_main10 --cpu-seconds 6 --parity-seconds 15 ;;
+    deepab2) run deeptests 400 python -u -m pytest tests/test_deep_nn.py tests/test_ring.py -m gpu -x -q -p no:cacheprovider --timeout 300 --timeout-method thread && \
+             run deep_mall 300 python -u bench.py --workload c5 --no-cpu-baseline --parity-seconds 0 --steps 20 && \
+             FME_LIB_PATH=$PWD/hm16.9-nn_fme_amd/variants/deep_mall0/libfme_amd.so run deep_mall0 300 python -u bench.py --workload c5 --no-cpu-baseline --parity-seconds 0 --steps 20 ;;
     tzprof) run tzprof 700 bash tools/gpu_tz_prof.sh ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac

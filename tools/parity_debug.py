@@ -1,6 +1,8 @@
-"""Debug of the bench's after-run parity leg: the replay's results of one step against (A) oracle/_ref
-with the parity leg's bindings, (B) the HIP host path with the same bindings, (C) the replay's own
-download engines."""
+"""Debug of the bench's after-run parity leg: every step of a FrameReplay (the bench's 1080p job
+stream) against the library's host path with that step's bindings, NN off so that no carried state
+enters: a mismatch is a binding (pictures, lambdas, jobs) or ordering problem of the replay.
+
+usage: python tools/parity_debug.py [steps] [warmup] [bit_depth]"""
 import os
 import sys
 
@@ -12,51 +14,67 @@ sys.path[:0] = [os.path.join(ROOT, "hm16.9-nn_fme_amd"), ROOT, os.path.join(ROOT
 import torch  # noqa: E402
 
 import bench  # noqa: E402
-from nnfme import synth, weights  # noqa: E402
+from nnfme import synth  # noqa: E402
 from nnfme.abi import MV_FIELDS  # noqa: E402
 from nnfme.pipeline import ORG0, REFS, FrameReplay  # noqa: E402
 from nnfme.runtime import FmeContext  # noqa: E402
 
 
 def main():
+    steps = int(sys.argv[1]) if len(sys.argv) > 1 else 20
+    warm = int(sys.argv[2]) if len(sys.argv) > 2 else 3
+    bd = int(sys.argv[3]) if len(sys.argv) > 3 else 8
     wl = bench.WORKLOADS["c3_qp22"]
-    bench.W, bench.H, bench.QP = wl["W"], wl["H"], wl["QP"]
     jobs = bench.make_frame_jobs(1000, "ctu", wl["calls"], wl["bipred"])
-    ctx = FmeContext(device=0, nn_mode=1, qp=22, fast_inter_mode=1, max_jobs=len(jobs))
-    pool = np.stack([synth.synth_luma(bench.W, bench.H, t) for t in range(8)])
-    m = 20000
-    for engine in ("blit", "kernel"):
-        ctx.nn_reset()
-        rep = FrameReplay(ctx, jobs, pool, lambda f: bench.frame_lambda(wl, f), 6, device=torch.device("cuda", 0),
-                          download_engine=engine)
-        rep.prime()
-        for s in range(3):
-            rep.issue(s, prefetch=s < 2)
-        rep.drain()
-        st = ctx.nn_get_state()
-        for s in range(3, 6):
-            rep.issue(s)
-        rep.finish()
-        g = rep.results(3)[:m]
-        a = bench.parity_leg(rep, wl, None, 3, st, 60.0, max_jobs=m)
-        print(engine, "parity leg:", {k: a[k] for k in ("jobs_checked", "mismatches", "per_field", "first_mismatch")},
-              flush=True)
-        # (B) the host path with the same bindings and state
-        c2 = FmeContext(device=0, nn_mode=1, qp=22, fast_inter_mode=1, max_jobs=m)
-        f0 = rep.first_frame(3)
+    m = 4000
+    pic = (lambda t: synth.synth_luma(1920, 1080, t)) if bd == 8 else \
+        (lambda t: synth.synth_luma_hbd(1920, 1080, t, bit_depth=bd))
+    pool = np.stack([pic(t) for t in range(8)])
+    ctx = FmeContext(device=0, nn_mode=0, qp=22, fast_inter_mode=1, max_jobs=len(jobs), bit_depth=bd)
+    lam = lambda f: bench.frame_lambda(wl, f)   # noqa: E731
+    rep = FrameReplay(ctx, jobs, pool, lam, warm + steps, device=torch.device("cuda", 0))
+    rep.prime()
+    for s in range(warm):
+        rep.issue(s, prefetch=s + 1 < warm)
+    rep.drain()
+    ctx.set_profiling(True)
+    for s in range(warm, warm + steps):
+        rep.issue(s)
+    rep.finish(first_step=warm)
+    torch.cuda.synchronize()
+    c2 = FmeContext(device=0, nn_mode=0, qp=22, fast_inter_mode=1, max_jobs=m, bit_depth=bd)
+    for k in range(warm + steps):
+        f0 = rep.first_frame(k)
         c2.set_picture(ORG0, pool[f0 % 8])
-        c2.set_lambda(0, bench.frame_lambda(wl, f0))
+        c2.set_lambda(0, lam(f0))
         for slot in range(REFS):
             c2.set_picture(slot, pool[(f0 - REFS + slot) % 8])
-        c2.nn_set_state(st)
         b = c2.refine_mv(rep.jobs[:m])
-        for f in MV_FIELDS:
-            d = int((b[f] != g[f]).sum())
-            if d:
-                print(engine, "host path vs replay: field", f, d, "first", int(np.flatnonzero(b[f] != g[f])[0]))
-        print(engine, "host path vs replay checked", flush=True)
-        print("job0", rep.jobs[0], "gpu", g[0], "host", b[0])
-        del rep
+        g = rep.results(k)[:m]
+        bad = {f: int((b[f] != g[f]).sum()) for f in MV_FIELDS if f != "status"}
+        # which frame's bindings do the replay's results match?
+        match = None
+        if any(bad.values()):
+            for d in (-2, -1, 1, 2):
+                f1 = f0 + d
+                c2.set_picture(ORG0, pool[f1 % 8])
+                c2.set_lambda(0, lam(f1))
+                for slot in range(REFS):
+                    c2.set_picture(slot, pool[(f1 - REFS + slot) % 8])
+                b2 = c2.refine_mv(rep.jobs[:m])
+                if all(int((b2[f] != g[f]).sum()) == 0 for f in ("mv_x", "mv_y", "cost")):
+                    match = d
+                    break
+            for dl in (-1, 1, 2):   # only the lambda of another frame
+                c2.set_picture(ORG0, pool[f0 % 8])
+                for slot in range(REFS):
+                    c2.set_picture(slot, pool[(f0 - REFS + slot) % 8])
+                c2.set_lambda(0, lam(f0 + dl))
+                b2 = c2.refine_mv(rep.jobs[:m])
+                if all(int((b2[f] != g[f]).sum()) == 0 for f in ("mv_x", "mv_y", "cost")):
+                    match = f"lambda{dl:+d}"
+                    break
+        print(f"step {k}: frame {f0} lambda {lam(f0)} mismatches {bad} matches frame offset {match}", flush=True)
 
 
 if __name__ == "__main__":

@@ -38,6 +38,8 @@ def main():
     print(f"pred_inter_p {W}x{H} depth {depth}: {len(reqs)} PU requests ({nj} xMotionEstimation jobs) in {t * 1e3:.1f} ms "
           f"-> {len(reqs) / t / 1e6:.2f} M requests/s, {nj / t / 1e6:.2f} M jobs/s; ref_idx histogram "
           f"{np.bincount(res['ref_idx'], minlength=4).tolist()}", flush=True)
+    print("pred_inter phases (ms, last frame):",
+          {k: round(v, 2) for k, v in ctx.pred_inter_phases().items()}, flush=True)
     # CPU: the oracle's sequential restatement on a bounded sample (first CTU rows)
     if os.environ.get("CPU", "1") == "1":
         from oracle import Oracle
