@@ -652,6 +652,8 @@ def main():
                          "pipeline the copy kernel's workgroups wait for the persistent search's slots, "
                          "1.39 against 1.22 ms per step, profiles/r05_ab.log)")
     ap.add_argument("--download-wgs", type=int, default=8, help="workgroups of the download kernel")
+    ap.add_argument("--search-reserve", type=int, default=0,
+                    help="resident search workgroups left free for the download kernel (fme_set_search_reserve)")
     ap.add_argument("--download", choices=("deferred", "immediate"), default=None,
                     help="results download of step k: once step k+1's search runs (deferred) or right after "
                          "step k (immediate); default: the workload's measured choice (DESIGN.md section 5)")
@@ -759,7 +761,8 @@ def main():
     rep = FrameReplay(ctx, jobs, pool, lambda f: frame_lambda(wl, f), steps_total, frames_per_step=FPS,
                       world=world, rank=rank, device=dev, defer_download=defer,
                       key_reqs=key_reqs, key_count=len(keys) if keys is not None else 0, nn_rows=nn_rows,
-                      download_engine=args.download_engine, download_wgs=args.download_wgs)
+                      download_engine=args.download_engine, download_wgs=args.download_wgs,
+                      search_reserve=args.search_reserve)
     n = rep.n
     rep.prime()
 

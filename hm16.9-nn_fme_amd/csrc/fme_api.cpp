@@ -141,6 +141,14 @@ struct fme_ctx {
 
   DevBuf<PicDesc> d_pics;
   DevBuf<double> d_mlambda;
+  // the tables' upload ring (sync_tables): pinned, device-mapped slots, each guarded by the event of
+  // the launch that reads it
+  static constexpr int kTabSlots = 16;
+  TablesSlot* h_tab = nullptr;
+  TablesSlot* h_tab_dev = nullptr;
+  hipEvent_t tab_ev[kTabSlots] = {};
+  bool tab_used[kTabSlots] = {};
+  int tab_next = 0;
   DevBuf<int16_t> d_keys;
   size_t n_keys = 0;
   DevBuf<float> d_nn;         // packed layout (nn_pack, kNnPkFloats)
@@ -208,7 +216,10 @@ struct fme_ctx {
   HostBuf<int32_t> h_pi_psrc;
   HostBuf<fme_mv_result> h_pi_mv;
   HostBuf<fme_result> h_pi_last;  // the full records of the last 2Nx2N request
-  std::vector<int> pi_base, pi_task, pi_level, pi_src, pi_lvl, pi_start;
+  HostBuf<fme_result> h_pi_ures;  // fme_pred_inter_b: the uni-pred jobs' records
+  HostBuf<fme_job> h_pi_seq;      // fme_pred_inter_b: one round's jobs in call order
+  HostBuf<fme_mv_result> h_pi_rs; // fme_pred_inter_b: their results
+  std::vector<int> pi_base, pi_task, pi_level, pi_src, pi_lvl, pi_start, pi_byarea;
   std::vector<int32_t> pi_off, pi_fill;
   std::vector<uint8_t> pi_amvp_idx;
   DevBuf<fme_job> d_pi_jobs;      // level order
@@ -248,6 +259,7 @@ struct fme_ctx {
   bool timed = false;
   hipEvent_t ev_done = nullptr; // end of the last batch (fme_refine_status)
   hipEvent_t ev_search = nullptr; // caller's event, recorded before each search launch (fme_set_search_event)
+  int search_reserve = 0;         // resident search workgroups left free (fme_set_search_reserve)
   bool batch_issued = false;
   float last_ms[FME_NUM_TIMINGS] = {};
   double acc_ms[FME_NUM_TIMINGS] = {};
@@ -299,7 +311,7 @@ int fme_create(int device, const fme_config* cfg, fme_ctx** out_ctx) {
   HIP_TRY(hipMemset(c->nn_state.p, 0, 24 * sizeof(uint32_t)));
   HIP_TRY(c->d_key_invalid.reserve(1));
   HIP_TRY(hipMemset(c->d_key_invalid.p, 0, sizeof(int32_t)));
-  HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&c->h_counts), (kNumClasses + 1) * sizeof(int32_t), hipHostMallocDefault));
+  HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&c->h_counts), kCountWords * sizeof(int32_t), hipHostMallocDefault));
   if (cfg->max_jobs > 0) {
     const size_t n = (size_t)cfg->max_jobs;
     const size_t nb = (n + kJobsPerScanBlock - 1) / kJobsPerScanBlock;
@@ -339,6 +351,7 @@ int fme_destroy(fme_ctx* c) {
   c->d_amvp.release(); c->d_amvp_sad.release(); c->d_bikey.release(); c->d_key_invalid.release(); c->d_ch_i32.release(); c->d_tz_emi.release();
   c->h_pi_tasks.release(); c->h_pi_tsad.release(); c->h_pi_jobs.release(); c->h_pi_ext.release();
   c->h_pi_idx.release(); c->h_pi_psrc.release(); c->h_pi_mv.release(); c->h_pi_last.release();
+  c->h_pi_ures.release(); c->h_pi_seq.release(); c->h_pi_rs.release();
   c->d_pi_jobs.release(); c->d_pi_ext.release(); c->d_pi_idx.release();
   for (auto& e : c->ev_tz)
     if (e) (void)hipEventDestroy(e);
@@ -354,6 +367,9 @@ int fme_destroy(fme_ctx* c) {
   if (c->box) (void)hipHostFree(c->box);
   if (c->srv_stream) (void)hipStreamDestroy(c->srv_stream);
   if (c->h_counts) (void)hipHostFree(c->h_counts);
+  if (c->h_tab) (void)hipHostFree(c->h_tab);
+  for (auto& e : c->tab_ev)
+    if (e) (void)hipEventDestroy(e);
   for (auto& set : c->ev)
     for (auto& e : set)
       if (e) (void)hipEventDestroy(e);
@@ -661,7 +677,23 @@ static int sync_tables(fme_ctx* c, hipStream_t s) {
   int rc = srv_stop(c);
   if (rc) return rc;
   if (!c->tables_dirty) return FME_OK;
-  HIP_TRY(launch_put_tables(c->d_pics.p, c->d_mlambda.p, c->pics, c->mlambda, s));
+  if (!c->h_tab) {
+    void* p = nullptr;
+    HIP_TRY(hipHostMalloc(&p, fme_ctx::kTabSlots * sizeof(TablesSlot), hipHostMallocMapped));
+    c->h_tab = static_cast<TablesSlot*>(p);
+    void* d = nullptr;
+    HIP_TRY(hipHostGetDevicePointer(&d, p, 0));
+    c->h_tab_dev = static_cast<TablesSlot*>(d);
+    for (auto& e : c->tab_ev) HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  }
+  const int k = c->tab_next;
+  c->tab_next = (k + 1) % fme_ctx::kTabSlots;
+  if (c->tab_used[k]) HIP_TRY(hipEventSynchronize(c->tab_ev[k]));   // its last launch has run
+  std::memcpy(c->h_tab[k].pics, c->pics, sizeof(c->pics));
+  std::memcpy(c->h_tab[k].ml, c->mlambda, sizeof(c->mlambda));
+  HIP_TRY(launch_put_tables(c->d_pics.p, c->d_mlambda.p, c->h_tab_dev + k, s));
+  HIP_TRY(hipEventRecord(c->tab_ev[k], s));
+  c->tab_used[k] = true;
   c->tables_dirty = false;
   return FME_OK;
 }
@@ -766,7 +798,7 @@ static int refine_batch(fme_ctx* c, const fme_job* d_jobs, fme_result* d_res, fm
   if (c->ev_search) HIP_TRY(hipEventRecord(c->ev_search, s));
   // the lane kernel: every PU shape, one launch on the batch stream (8-bit); the pixel kernel at
   // bit depth 10 (fme_px.hip)
-  HIP_TRY(c->cfg.bit_depth > 8 ? launch_search_px(a, w, c->cfg.bit_depth, s) : launch_search_lane(a, w, s));
+  HIP_TRY(c->cfg.bit_depth > 8 ? launch_search_px(a, w, c->cfg.bit_depth, s) : launch_search_lane(a, w, c->search_reserve, s));
   if (prof) HIP_TRY(hipEventRecord(ev[4], s));
   if (prof) HIP_TRY(hipEventRecord(ev[5], s));
   HIP_TRY(c->cfg.nn_mode == 2
@@ -801,6 +833,12 @@ int fme_refine_mv_device(fme_ctx* c, const fme_job* d_jobs, fme_mv_result* d_out
 int fme_set_search_event(fme_ctx* c, void* event) {
   if (!c) return fail(FME_E_INVALID, "fme_set_search_event: null ctx");
   c->ev_search = static_cast<hipEvent_t>(event);
+  return FME_OK;
+}
+
+int fme_set_search_reserve(fme_ctx* c, int workgroups) {
+  if (!c || workgroups < 0 || workgroups > 4096) return fail(FME_E_INVALID, "fme_set_search_reserve: bad argument");
+  c->search_reserve = workgroups;
   return FME_OK;
 }
 
@@ -870,11 +908,12 @@ static int tz_run(fme_ctx* c, fme_job* d_jobs, const fme_tz_ext* d_ext, uint32_t
   HIP_TRY(hipMemsetAsync(c->counts.p, 0, kCountWords * sizeof(int32_t), s));
   HIP_TRY(launch_classify(a, w, s));
   HIP_TRY(launch_schedule(w, c->sched_p, s));   // class offsets for the scatter
-  HIP_TRY(hipMemcpyAsync(c->h_counts, c->counts.p, (kNumClasses + 1) * sizeof(int32_t), hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipMemcpyAsync(c->h_counts, c->counts.p, kCountWords * sizeof(int32_t), hipMemcpyDeviceToHost, s));
   HIP_TRY(hipStreamSynchronize(s));
   if (c->h_counts[kNumClasses] > 0)
     return fail(FME_E_INVALID, "fme_integer_search_device: %d job(s) with an unsupported PU size or unset picture/lambda/key",
                 c->h_counts[kNumClasses]);
+  const bool keyed = c->h_counts[kKeyedWord] > 0;
   TzSchedule sc{};
   int off = 0, nb[3] = {0, 0, 0};
   for (int k = 0; k < kNumClasses; k++) {
@@ -908,9 +947,9 @@ static int tz_run(fme_ctx* c, fme_job* d_jobs, const fme_tz_ext* d_ext, uint32_t
   HIP_TRY(hipEventRecord(c->ev_fork, s));
   HIP_TRY(hipStreamWaitEvent(c->aux, c->ev_fork, 0));
   HIP_TRY(hipStreamWaitEvent(c->aux2, c->ev_fork, 0));
-  HIP_TRY(launch_tz_wave(ta, sc, 0, c->aux));
-  HIP_TRY(launch_tz_wave(ta, sc, 1, c->aux2));
-  HIP_TRY(launch_tz_wave(ta, sc, 2, s));
+  HIP_TRY(launch_tz_wave(ta, sc, 0, keyed, c->aux));
+  HIP_TRY(launch_tz_wave(ta, sc, 1, keyed, c->aux2));
+  HIP_TRY(launch_tz_wave(ta, sc, 2, keyed, s));
   HIP_TRY(hipEventRecord(c->ev_join, c->aux));
   HIP_TRY(hipEventRecord(c->ev_join2, c->aux2));
   HIP_TRY(hipStreamWaitEvent(s, c->ev_join, 0));
@@ -1738,6 +1777,79 @@ int fme_build_bipred_keys_device(fme_ctx* c, const fme_bikey_req* d_reqs, int n,
   return FME_OK;
 }
 
+// The producers' integer searches by m_integerMv2Nx2N dependency level.  jobs / ext: pinned host
+// arrays in request order; src[u]: the job whose post-EMI MV job u reads (-1: none); lvl[u] its
+// level.  The jobs go to the device once, are reordered there by level (within a level the largest
+// PUs first) for k_tz_level's launches, and come back in request order in c->d_jobs for the sub-pel
+// pass; nothing returns to the host.
+static int tz_levels_device(fme_ctx* c, const fme_job* jobs, const fme_tz_ext* ext, const std::vector<int>& src,
+                            const std::vector<int>& lvl, int nj, int max_level, hipStream_t s) {
+  if (nj <= 0) return FME_OK;
+  // level order: blocks dispatch in index order, so the longest searches of a wide level start at once
+  std::vector<int32_t>& off = c->pi_off;
+  std::vector<int32_t>& fill = c->pi_fill;
+  std::vector<int>& start = c->pi_start;
+  off.assign((size_t)max_level + 2, 0);
+  for (int u = 0; u < nj; u++) off[lvl[u] + 1]++;
+  for (int l = 0; l <= max_level; l++) off[l + 1] += off[l];
+  fill.assign(off.begin(), off.end() - 1);
+  start.assign(64 * 64 + 2, 0);   // counting sort by area, descending
+  for (int u = 0; u < nj; u++) start[64 * 64 - (int)jobs[u].w * jobs[u].h + 1]++;
+  for (size_t a = 1; a < start.size(); a++) start[a] += start[a - 1];
+  HIP_TRY(c->h_pi_idx.reserve((size_t)2 * nj));
+  HIP_TRY(c->h_pi_psrc.reserve((size_t)nj));
+  int32_t* const order = c->h_pi_idx.p;        // level position -> job
+  int32_t* const pos = c->h_pi_idx.p + nj;     // job -> level position
+  {
+    std::vector<int>& byarea = c->pi_byarea;
+    byarea.resize((size_t)nj);
+    for (int u = 0; u < nj; u++) byarea[start[64 * 64 - (int)jobs[u].w * jobs[u].h]++] = u;
+    for (int u : byarea) {
+      pos[u] = fill[lvl[u]]++;
+      order[pos[u]] = u;
+    }
+  }
+  int32_t* const psrc = c->h_pi_psrc.p;
+  par_for(nj, [&](int lo, int hi) {
+    for (int q = lo; q < hi; q++) {
+      const int u = order[q];
+      psrc[q] = ((ext[u].flags & FME_TZ_PRED2NX2N) && src[u] >= 0) ? pos[src[u]] : -1;
+    }
+  });
+  HIP_TRY(c->d_jobs.reserve(nj));
+  HIP_TRY(c->d_tz_ext.reserve(nj));
+  HIP_TRY(c->d_pi_jobs.reserve(nj));
+  HIP_TRY(c->d_pi_ext.reserve(nj));
+  HIP_TRY(c->d_pi_idx.reserve((size_t)2 * nj));
+  HIP_TRY(c->d_ch_i32.reserve(nj));
+  HIP_TRY(c->d_tz_emi.reserve((size_t)2 * nj));
+  HIP_TRY(hipMemcpyAsync(c->d_jobs.p, jobs, (size_t)nj * sizeof(fme_job), hipMemcpyHostToDevice, s));
+  HIP_TRY(hipMemcpyAsync(c->d_tz_ext.p, ext, (size_t)nj * sizeof(fme_tz_ext), hipMemcpyHostToDevice, s));
+  HIP_TRY(hipMemcpyAsync(c->d_pi_idx.p, order, (size_t)2 * nj * sizeof(int32_t), hipMemcpyHostToDevice, s));
+  HIP_TRY(hipMemcpyAsync(c->d_ch_i32.p, psrc, (size_t)nj * sizeof(int32_t), hipMemcpyHostToDevice, s));
+  HIP_TRY(launch_gather_jobs(c->d_jobs.p, c->d_tz_ext.p, c->d_pi_idx.p, c->d_pi_jobs.p, c->d_pi_ext.p, nj, s));
+  {
+    TzArgs ta{};
+    ta.a.jobs = c->d_pi_jobs.p;
+    ta.a.keys = c->d_keys.p;
+    ta.a.n_keys = (int64_t)c->n_keys;
+    ta.a.key_invalid = c->d_key_invalid.p;
+    ta.a.mlambda = c->d_mlambda.p;
+    ta.a.pics = c->d_pics.p;
+    ta.a.n = nj;
+    ta.a.use_hadamard = c->cfg.use_hadamard ? 1 : 0;
+    ta.a.fen = c->cfg.fast_inter_mode;
+    ta.jobs_out = c->d_pi_jobs.p;
+    ta.ext = c->d_pi_ext.p;
+    ta.emi_mv = c->d_tz_emi.p;
+    const TzChain ch{c->d_ch_i32.p, max_level + 1};
+    HIP_TRY(launch_tz_levels(ta, ch, off.data(), s));
+  }
+  // the searched jobs back in request order for the sub-pel pass, on the device
+  HIP_TRY(launch_gather_jobs(c->d_pi_jobs.p, nullptr, c->d_pi_idx.p + nj, c->d_jobs.p, nullptr, nj, s));
+  return FME_OK;
+}
+
 // Phase clock of the producers (fme_pred_inter_phases): lap(k) adds the time since the last lap to
 // phase k.
 struct PiClock {
@@ -1935,70 +2047,9 @@ int fme_pred_inter_p(fme_ctx* c, const fme_pu_req* reqs, fme_pu_res* res, int n,
       }
     }
   }
-  // level order: by level, within a level the largest PUs first (blocks dispatch in index order, so
-  // the longest searches of a wide level start at once instead of forming its tail)
-  std::vector<int32_t>& off = c->pi_off;
-  std::vector<int32_t>& fill = c->pi_fill;
-  std::vector<int>& start = c->pi_start;
-  off.assign((size_t)max_level + 2, 0);
-  for (int u = 0; u < nj; u++) off[lvl[u] + 1]++;
-  for (int l = 0; l <= max_level; l++) off[l + 1] += off[l];
-  fill.assign(off.begin(), off.end() - 1);
-  start.assign(64 * 64 + 2, 0);   // counting sort by area, descending
-  for (int u = 0; u < nj; u++) start[64 * 64 - (int)jobs[u].w * jobs[u].h + 1]++;
-  for (size_t a = 1; a < start.size(); a++) start[a] += start[a - 1];
-  HIP_TRY(c->h_pi_idx.reserve((size_t)2 * nj));
-  HIP_TRY(c->h_pi_psrc.reserve((size_t)nj));
-  int32_t* const order = c->h_pi_idx.p;        // level position -> job
-  int32_t* const pos = c->h_pi_idx.p + nj;     // job -> level position
-  {
-    std::vector<int>& byarea = c->pi_level;   // request levels are no longer needed
-    byarea.resize((size_t)nj);
-    for (int u = 0; u < nj; u++) byarea[start[64 * 64 - (int)jobs[u].w * jobs[u].h]++] = u;
-    for (int u : byarea) {
-      pos[u] = fill[lvl[u]]++;
-      order[pos[u]] = u;
-    }
-  }
-  int32_t* const psrc = c->h_pi_psrc.p;
-  par_for(nj, [&](int lo, int hi) {
-    for (int q = lo; q < hi; q++) {
-      const int u = order[q];
-      psrc[q] = ((ext[u].flags & FME_TZ_PRED2NX2N) && src[u] >= 0) ? pos[src[u]] : -1;
-    }
-  });
   clk.lap(2);
-  HIP_TRY(c->d_jobs.reserve(nj));
-  HIP_TRY(c->d_tz_ext.reserve(nj));
-  HIP_TRY(c->d_pi_jobs.reserve(nj));
-  HIP_TRY(c->d_pi_ext.reserve(nj));
-  HIP_TRY(c->d_pi_idx.reserve((size_t)2 * nj));
-  HIP_TRY(c->d_ch_i32.reserve(nj));
-  HIP_TRY(c->d_tz_emi.reserve((size_t)2 * nj));
-  HIP_TRY(hipMemcpyAsync(c->d_jobs.p, jobs, (size_t)nj * sizeof(fme_job), hipMemcpyHostToDevice, s));
-  HIP_TRY(hipMemcpyAsync(c->d_tz_ext.p, ext, (size_t)nj * sizeof(fme_tz_ext), hipMemcpyHostToDevice, s));
-  HIP_TRY(hipMemcpyAsync(c->d_pi_idx.p, order, (size_t)2 * nj * sizeof(int32_t), hipMemcpyHostToDevice, s));
-  HIP_TRY(hipMemcpyAsync(c->d_ch_i32.p, psrc, (size_t)nj * sizeof(int32_t), hipMemcpyHostToDevice, s));
-  HIP_TRY(launch_gather_jobs(c->d_jobs.p, c->d_tz_ext.p, c->d_pi_idx.p, c->d_pi_jobs.p, c->d_pi_ext.p, nj, s));
-  {
-    TzArgs ta{};
-    ta.a.jobs = c->d_pi_jobs.p;
-    ta.a.keys = c->d_keys.p;
-    ta.a.n_keys = (int64_t)c->n_keys;
-    ta.a.key_invalid = c->d_key_invalid.p;
-    ta.a.mlambda = c->d_mlambda.p;
-    ta.a.pics = c->d_pics.p;
-    ta.a.n = nj;
-    ta.a.use_hadamard = c->cfg.use_hadamard ? 1 : 0;
-    ta.a.fen = c->cfg.fast_inter_mode;
-    ta.jobs_out = c->d_pi_jobs.p;
-    ta.ext = c->d_pi_ext.p;
-    ta.emi_mv = c->d_tz_emi.p;
-    const TzChain ch{c->d_ch_i32.p, max_level + 1};
-    HIP_TRY(launch_tz_levels(ta, ch, off.data(), s));
-  }
-  // the searched jobs back in request order for the sub-pel pass, on the device
-  HIP_TRY(launch_gather_jobs(c->d_pi_jobs.p, nullptr, c->d_pi_idx.p + nj, c->d_jobs.p, nullptr, nj, s));
+  rc = tz_levels_device(c, jobs, ext, src, lvl, nj, max_level, s);
+  if (rc) return rc;
   HIP_TRY(hipStreamSynchronize(s));   // phase boundary (fme_pred_inter_phases)
   clk.lap(3);
   // ---- 3. the sub-pel path over every job in request order (compact results to the host) ----
@@ -2142,8 +2193,8 @@ int fme_pred_inter_b(fme_ctx* c, const fme_pu_req_b* reqs, fme_pu_res_b* res, in
   // *puiDistBiP of list-1 references under MvdL1ZeroFlag (one candidate: its template cost, 4214-4217)
   std::vector<uint32_t> bipd((size_t)n * 8, 0xFFFFFFFFu);
   {
-    std::vector<AmvpTask> tasks;
     std::vector<int> slot, nc;
+    size_t ntasks = 0;
     for (int i = 0; i < n; i++) {
       const fme_pu_req_b& q = reqs[i];
       for (int l = 0; l < 2; l++)
@@ -2152,20 +2203,28 @@ int fme_pred_inter_b(fme_ctx* c, const fme_pu_req_b* reqs, fme_pu_res_b* res, in
           if (!m_n) continue;
           slot.push_back(i * 8 + l * 4 + k);
           nc.push_back(m_n);
-          for (int m = 0; m < m_n; m++)
-            tasks.push_back(AmvpTask{q.x, q.y, q.w, q.h, q.org_id, q.ref_id[l][k], q.cu_x, q.cu_y,
-                                     q.cand[l][k][m][0], q.cand[l][k][m][1]});
+          ntasks += (size_t)m_n;
         }
     }
+    HIP_TRY(c->h_pi_tasks.reserve(ntasks));
+    HIP_TRY(c->h_pi_tsad.reserve(ntasks));
+    AmvpTask* const tasks = c->h_pi_tasks.p;
+    for (size_t t = 0, base = 0; t < slot.size(); base += nc[t], t++) {
+      const fme_pu_req_b& q = reqs[slot[t] / 8];
+      const int l = (slot[t] >> 2) & 1, k = slot[t] & 3;
+      for (int m = 0; m < nc[t]; m++)
+        tasks[base + m] = AmvpTask{q.x, q.y, q.w, q.h, q.org_id, q.ref_id[l][k], q.cu_x, q.cu_y, q.cand[l][k][m][0],
+                                   q.cand[l][k][m][1]};
+    }
     clk.lap(0);
-    if (!tasks.empty()) {
-      std::vector<uint32_t> tsad(tasks.size());
-      HIP_TRY(c->d_amvp.reserve(tasks.size()));
-      HIP_TRY(c->d_amvp_sad.reserve(tasks.size()));
-      HIP_TRY(hipMemcpyAsync(c->d_amvp.p, tasks.data(), tasks.size() * sizeof(AmvpTask), hipMemcpyHostToDevice, s));
-      AmvpArgs aa{c->d_amvp.p, c->d_pics.p, c->d_amvp_sad.p, (int32_t)tasks.size()};
+    if (ntasks > 0) {
+      const uint32_t* const tsad = c->h_pi_tsad.p;
+      HIP_TRY(c->d_amvp.reserve(ntasks));
+      HIP_TRY(c->d_amvp_sad.reserve(ntasks));
+      HIP_TRY(hipMemcpyAsync(c->d_amvp.p, tasks, ntasks * sizeof(AmvpTask), hipMemcpyHostToDevice, s));
+      AmvpArgs aa{c->d_amvp.p, c->d_pics.p, c->d_amvp_sad.p, (int32_t)ntasks};
       HIP_TRY(launch_amvp_sad(aa, s));
-      HIP_TRY(hipMemcpyAsync(tsad.data(), c->d_amvp_sad.p, tasks.size() * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+      HIP_TRY(hipMemcpyAsync(c->h_pi_tsad.p, c->d_amvp_sad.p, ntasks * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
       HIP_TRY(hipStreamSynchronize(s));
       for (size_t t = 0, base = 0; t < slot.size(); base += nc[t], t++) {
         const double ml = c->mlambda[reqs[slot[t] / 8].lambda_id];
@@ -2182,50 +2241,65 @@ int fme_pred_inter_b(fme_ctx* c, const fme_pu_req_b* reqs, fme_pu_res_b* res, in
     }
   }
   clk.lap(1);
-  // ---- 2. uni-pred jobs in call order, integer searches by m_integerMv2Nx2N level ----
+  // ---- 2. uni-pred jobs in call order (pinned), integer searches by m_integerMv2Nx2N level ----
   std::vector<int> ujob((size_t)n * 8, -1), ubeg(n + 1, 0);
-  std::vector<fme_job> uj;
-  std::vector<fme_tz_ext> ue;
-  std::vector<int> ukey;   // (list, reference) of each uni job
+  int nu = 0;
   for (int i = 0; i < n; i++) {
-    const fme_pu_req_b& q = reqs[i];
-    const PicDesc& org = c->pics[q.org_id];
-    const int range = q.search_range ? q.search_range : 64;
-    ubeg[i] = (int)uj.size();
+    ubeg[i] = nu;
     for (int l = 0; l < 2; l++)
-      for (int k = 0; k < q.num_refs[l]; k++) {
-        if (copied(q, l, k)) continue;
-        const int idx = amvp[i * 8 + l * 4 + k];
-        const int px = q.cand[l][k][idx][0], py = q.cand[l][k][idx][1];
-        int cx = px, cy = py;
-        clip_qpel(cx, cy, org.width, org.height, q.cu_x, q.cu_y);
-        int lx = cx - (range << 2), ly = cy - (range << 2), rx = cx + (range << 2), ry = cy + (range << 2);
-        clip_qpel(lx, ly, org.width, org.height, q.cu_x, q.cu_y);
-        clip_qpel(rx, ry, org.width, org.height, q.cu_x, q.cu_y);
-        fme_job j{};
-        j.x = q.x; j.y = q.y; j.w = q.w; j.h = q.h;
-        j.org_id = q.org_id; j.ref_id = q.ref_id[l][k];
-        j.mvp_x = (int16_t)px; j.mvp_y = (int16_t)py;
-        j.lt_x = (int16_t)round4(lx); j.lt_y = (int16_t)round4(ly);
-        j.rb_x = (int16_t)round4(rx); j.rb_y = (int16_t)round4(ry);
-        j.flags = (uint8_t)(FME_JOB_EMI | ((q.flags & FME_PU_LOSSLESS) ? FME_JOB_LOSSLESS : 0u));
-        j.lambda_id = q.lambda_id;
-        j.bits_in = (uint16_t)(ref_bits(k, q.num_refs[l]) + mvp_idx_bits(idx, 2));   // + uiMbBits[l] later
-        j.key_offset = -1;
-        fme_tz_ext e{};
-        e.cu_x = q.cu_x; e.cu_y = q.cu_y;
-        e.search_range = (uint8_t)range;
-        e.flags = (q.part_size == FME_PART_2Nx2N && q.depth == 0) ? 0 : FME_TZ_PRED2NX2N;
-        ujob[i * 8 + l * 4 + k] = (int)uj.size();
-        uj.push_back(j);
-        ue.push_back(e);
-        ukey.push_back(l * 4 + k);
-      }
+      for (int k = 0; k < reqs[i].num_refs[l]; k++)
+        if (!copied(reqs[i], l, k)) ujob[i * 8 + l * 4 + k] = nu++;
   }
-  ubeg[n] = (int)uj.size();
-  const int nu = (int)uj.size();
+  ubeg[n] = nu;
+  HIP_TRY(c->h_pi_jobs.reserve((size_t)nu));
+  HIP_TRY(c->h_pi_ext.reserve((size_t)nu));
+  fme_job* const uj = c->h_pi_jobs.p;
+  fme_tz_ext* const ue = c->h_pi_ext.p;
+  std::vector<int> ukey((size_t)nu);   // (list, reference) of each uni job
+  par_for(n, [&](int lo, int hi) {
+    for (int i = lo; i < hi; i++) {
+      const fme_pu_req_b& q = reqs[i];
+      const PicDesc& org = c->pics[q.org_id];
+      const int range = q.search_range ? q.search_range : 64;
+      for (int l = 0; l < 2; l++)
+        for (int k = 0; k < q.num_refs[l]; k++) {
+          const int u = ujob[i * 8 + l * 4 + k];
+          if (u < 0) continue;
+          const int idx = amvp[i * 8 + l * 4 + k];
+          const int px = q.cand[l][k][idx][0], py = q.cand[l][k][idx][1];
+          int cx = px, cy = py;
+          clip_qpel(cx, cy, org.width, org.height, q.cu_x, q.cu_y);
+          int lx = cx - (range << 2), ly = cy - (range << 2), rx = cx + (range << 2), ry = cy + (range << 2);
+          clip_qpel(lx, ly, org.width, org.height, q.cu_x, q.cu_y);
+          clip_qpel(rx, ry, org.width, org.height, q.cu_x, q.cu_y);
+          fme_job& j = uj[u];
+          j = fme_job{};
+          j.x = q.x; j.y = q.y; j.w = q.w; j.h = q.h;
+          j.org_id = q.org_id; j.ref_id = q.ref_id[l][k];
+          j.mvp_x = (int16_t)px; j.mvp_y = (int16_t)py;
+          j.lt_x = (int16_t)round4(lx); j.lt_y = (int16_t)round4(ly);
+          j.rb_x = (int16_t)round4(rx); j.rb_y = (int16_t)round4(ry);
+          j.flags = (uint8_t)(FME_JOB_EMI | ((q.flags & FME_PU_LOSSLESS) ? FME_JOB_LOSSLESS : 0u));
+          j.lambda_id = q.lambda_id;
+          j.bits_in = (uint16_t)(ref_bits(k, q.num_refs[l]) + mvp_idx_bits(idx, 2));   // + uiMbBits[l] later
+          j.key_offset = -1;
+          fme_tz_ext& e = ue[u];
+          e = fme_tz_ext{};
+          e.cu_x = q.cu_x; e.cu_y = q.cu_y;
+          e.search_range = (uint8_t)range;
+          e.flags = (q.part_size == FME_PART_2Nx2N && q.depth == 0) ? 0 : FME_TZ_PRED2NX2N;
+          ukey[u] = l * 4 + k;
+        }
+    }
+  });
   {
-    std::vector<int> level((size_t)n, 0), src((size_t)nu, -1), lvl((size_t)nu, 0);
+    std::vector<int>& src = c->pi_src;
+    std::vector<int>& lvl = c->pi_lvl;
+    std::vector<int>& level = c->pi_level;
+    level.assign((size_t)n, 0);
+    src.assign((size_t)nu, -1);
+    lvl.resize((size_t)nu);
+    int max_level = 0;
     int last[8] = {-1, -1, -1, -1, -1, -1, -1, -1};   // last 2Nx2N writer of m_integerMv2Nx2N[l][k]
     for (int i = 0; i < n; i++) {
       for (int u = ubeg[i]; u < ubeg[i + 1]; u++)
@@ -2235,6 +2309,7 @@ int fme_pred_inter_b(fme_ctx* c, const fme_pu_req_b* reqs, fme_pu_res_b* res, in
         }
       if (reqs[i].part_size == FME_PART_2Nx2N)
         for (int u = ubeg[i]; u < ubeg[i + 1]; u++) last[ukey[u]] = i;
+      max_level = std::max(max_level, level[i]);
       for (int u = ubeg[i]; u < ubeg[i + 1]; u++) {
         lvl[u] = level[i];
         if ((ue[u].flags & FME_TZ_PRED2NX2N) && src[u] < 0) {
@@ -2243,19 +2318,28 @@ int fme_pred_inter_b(fme_ctx* c, const fme_pu_req_b* reqs, fme_pu_res_b* res, in
         }
       }
     }
-    std::vector<int16_t> emi_mv;
     clk.lap(2);
-    rc = tz_by_level(c, uj, ue, src, lvl, s, emi_mv, &clk);
+    rc = tz_levels_device(c, uj, ue, src, lvl, nu, max_level, s);
     if (rc) return rc;
+    HIP_TRY(hipStreamSynchronize(s));   // phase boundary (fme_pred_inter_phases)
   }
   clk.lap(3);
-  // ---- 3. the uni-pred sub-pel path in call order ----
+  // ---- 3. the uni-pred sub-pel path in call order (full records: the tails are re-priced) ----
   uint32_t s0[12];
   rc = fme_nn_get_state(c, s0);
   if (rc) return rc;
-  std::vector<fme_result> ru((size_t)nu);
-  rc = fme_refine(c, uj.data(), ru.data(), nu, stream);
+  HIP_TRY(c->d_res.reserve(nu));
+  HIP_TRY(c->h_pi_ures.reserve((size_t)nu));
+  rc = refine_batch(c, c->d_jobs.p, c->d_res.p, nullptr, nu, s);
   if (rc) return rc;
+  // the searched uni jobs (the rounds replay them) and their records
+  HIP_TRY(hipMemcpyAsync(uj, c->d_jobs.p, (size_t)nu * sizeof(fme_job), hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipMemcpyAsync(c->h_pi_ures.p, c->d_res.p, (size_t)nu * sizeof(fme_result), hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipMemcpyAsync(c->h_counts, &c->d_sched.p->invalid, sizeof(int32_t), hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipStreamSynchronize(s));
+  if (c->h_counts[0] > 0)
+    return fail(FME_E_INVALID, "fme_pred_inter_b: %d job(s) rejected by the refinement batch", c->h_counts[0]);
+  const fme_result* const ru = c->h_pi_ures.p;
   clk.lap(4);
   // ---- 4. rounds of host decisions and bi-pred searches ----
   std::vector<BPu> st((size_t)n);
@@ -2380,11 +2464,10 @@ int fme_pred_inter_b(fme_ctx* c, const fme_pu_req_b* reqs, fme_pu_res_b* res, in
     }
     p.stage = 2;
   };
-  std::vector<fme_job> bj, seq;
+  std::vector<fme_job> bj;
   std::vector<fme_tz_ext> be;
   std::vector<BiKeyTask> keyt;
   std::vector<int> issued;
-  std::vector<fme_result> rs;
   size_t key_total = 0;
   // bi-pred setup (3871-3916): uiMotBits, and under MvdL1ZeroFlag list 1 at its best predictor
   auto bi_setup = [&](int i) {
@@ -2498,24 +2581,38 @@ int fme_pred_inter_b(fme_ctx* c, const fme_pu_req_b* reqs, fme_pu_res_b* res, in
     HIP_TRY(launch_bi_key(ka, s));
     rc = tz_run_host(c, bj.data(), be.data(), nullptr, (int)bj.size(), stream, nullptr);
     if (rc) return rc;
-    seq.clear();
+    // the round's jobs in call order (pinned): every uni job, each issued request's bi jobs after its own
     std::vector<int> pos(issued.size());
-    size_t t = 0;
+    const size_t nseq = (size_t)nu + bj.size();
+    HIP_TRY(c->h_pi_seq.reserve(nseq));
+    HIP_TRY(c->h_pi_rs.reserve(nseq));
+    fme_job* const seq = c->h_pi_seq.p;
+    size_t t = 0, ns = 0;
     for (int i = 0; i < n; i++) {
-      seq.insert(seq.end(), uj.begin() + ubeg[i], uj.begin() + ubeg[i + 1]);
+      std::memcpy(seq + ns, uj + ubeg[i], (size_t)(ubeg[i + 1] - ubeg[i]) * sizeof(fme_job));
+      ns += (size_t)(ubeg[i + 1] - ubeg[i]);
       if (t < issued.size() && issued[t] == i) {
-        pos[t] = (int)seq.size();
+        pos[t] = (int)ns;
         const int nb = reqs[i].num_refs[st[i].L];
-        seq.insert(seq.end(), bj.begin() + st[i].bi0, bj.begin() + st[i].bi0 + nb);
+        std::memcpy(seq + ns, bj.data() + st[i].bi0, (size_t)nb * sizeof(fme_job));
+        ns += (size_t)nb;
         t++;
       }
     }
     rc = fme_nn_set_state(c, s0);
-    if (!rc) {
-      rs.resize(seq.size());
-      rc = fme_refine(c, seq.data(), rs.data(), (int)seq.size(), stream);
-    }
     if (rc) return rc;
+    HIP_TRY(c->d_jobs.reserve(ns));
+    HIP_TRY(c->d_res.reserve(ns));
+    HIP_TRY(c->d_mv.reserve(ns));
+    HIP_TRY(hipMemcpyAsync(c->d_jobs.p, seq, ns * sizeof(fme_job), hipMemcpyHostToDevice, s));
+    rc = refine_batch(c, c->d_jobs.p, c->d_res.p, c->d_mv.p, (int)ns, s);
+    if (rc) return rc;
+    HIP_TRY(hipMemcpyAsync(c->h_pi_rs.p, c->d_mv.p, ns * sizeof(fme_mv_result), hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipMemcpyAsync(c->h_counts, &c->d_sched.p->invalid, sizeof(int32_t), hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    if (c->h_counts[0] > 0)
+      return fail(FME_E_INVALID, "fme_pred_inter_b: %d job(s) rejected by a bi-pred round", c->h_counts[0]);
+    const fme_mv_result* const rs = c->h_pi_rs.p;
     for (size_t t2 = 0; t2 < issued.size(); t2++) {
       const int i = issued[t2];
       const fme_pu_req_b& q = reqs[i];
@@ -2527,7 +2624,7 @@ int fme_pred_inter_b(fme_ctx* c, const fme_pu_req_b* reqs, fme_pu_res_b* res, in
       std::memset(o.bi_ref_cost, 0, sizeof(o.bi_ref_cost));
       std::memset(o.bi_ref_mv, 0, sizeof(o.bi_ref_mv));
       for (int k = 0; k < q.num_refs[L]; k++) {
-        const fme_result& r = rs[pos[t2] + k];
+        const fme_mv_result& r = rs[pos[t2] + k];
         p.mvt[L][k][0] = r.mv_x;
         p.mvt[L][k][1] = r.mv_y;
         uint32_t b = r.bits, cst = r.cost;

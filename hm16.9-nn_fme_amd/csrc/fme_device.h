@@ -20,6 +20,7 @@ namespace fme {
 constexpr int kNumClasses = 24;      // HEVC inter PU shapes 4x8 .. 64x64 incl. AMP
 constexpr int kBlock = 256;          // threads per workgroup (4 wavefronts)
 constexpr int kJobsPerScanBlock = 1024;  // classify / NN kernels: 4 jobs per thread
+constexpr int kKeyedWord = 60;           // counts[]: jobs that read a key block (k_classify)
 
 // PU shape of each class (W, H).  Order: by area, then width.
 constexpr int kClassW[kNumClasses] = {4, 8, 8, 4, 16, 8, 16, 12, 16, 16, 8, 32,
@@ -166,7 +167,9 @@ struct TzSchedule {
   int32_t class_off[kNumClasses];
   int32_t class_cnt[kNumClasses];
 };
-hipError_t launch_tz_wave(const TzArgs& ta, const TzSchedule& sc, int kid, hipStream_t s);   // prefix in waves
+// keyed: some job of the batch reads a key block (bi-pred): the kernels that hold int16 keys;
+// otherwise the uni-pred form, whose key rows take half the registers
+hipError_t launch_tz_wave(const TzArgs& ta, const TzSchedule& sc, int kid, bool keyed, hipStream_t s);   // prefix in waves
 // The dependency levels of a producer's m_integerMv2Nx2N chain (fme_tz.hip k_tz_level): jobs in
 // level order, level l = jobs [lvl_off[l], lvl_off[l+1]), one launch per level, back to back.
 struct TzChain {
@@ -183,11 +186,17 @@ hipError_t launch_scatter(const BatchArgs& a, const WorkBufs& w, hipStream_t s);
 // 12 words of NN state written to dst in stream order (reset / set_state)
 hipError_t launch_put_state(uint32_t* dst, const uint32_t* v12, hipStream_t s);
 // the picture / lambda tables written in stream order from kernel arguments
-hipError_t launch_put_tables(PicDesc* d_pics, double* d_ml, const PicDesc* pics, const double* ml, hipStream_t s);
+// One batch's picture / lambda tables (a pinned, device-mapped host slot; k_put_tables copies it).
+struct TablesSlot {
+  PicDesc pics[FME_MAX_PICTURES];
+  double ml[FME_MAX_LAMBDAS];
+};
+hipError_t launch_put_tables(PicDesc* d_pics, double* d_ml, const TablesSlot* t_dev, hipStream_t s);
 // The search kernel reads its schedule from *w.sched (no host round trip); it is launched with
 // enough workgroups to fill the chip, each pulling tiles from its XCD's queue (then the other
 // XCDs').  `a.n` bounds the work.
-hipError_t launch_search_lane(const BatchArgs& a, const WorkBufs& w, hipStream_t s);
+// reserve > 0: the grid is the resident workgroups (FME_LANE_WAVES per CU) less `reserve`
+hipError_t launch_search_lane(const BatchArgs& a, const WorkBufs& w, int reserve, hipStream_t s);
 // Bit depth 10 (main10): the pixel-per-lane search (fme_px.hip), same records as the lane kernel;
 // pictures hold uint16 samples (PicDesc::luma reinterpreted, stride in samples).
 hipError_t launch_search_px(const BatchArgs& a, const WorkBufs& w, int bit_depth, hipStream_t s);

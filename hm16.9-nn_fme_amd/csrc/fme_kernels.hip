@@ -101,8 +101,11 @@ __global__ __launch_bounds__(kBlock) void k_classify(BatchArgs a, WorkBufs w) {
     const int i = base + q * kBlock + tid;
     if (i < a.n) jb[q] = a.jobs[i];
   }
-  __shared__ int32_t keys_bad;
-  if (tid == 0) keys_bad = a.key_invalid ? *a.key_invalid : 0;
+  __shared__ int32_t keys_bad, keyed;
+  if (tid == 0) {
+    keys_bad = a.key_invalid ? *a.key_invalid : 0;
+    keyed = 0;
+  }
   lut[tid] = kClassLut.v[tid];
   if (tid < FME_MAX_PICTURES) {
     const PicDesc p = a.pics[tid];
@@ -137,6 +140,7 @@ __global__ __launch_bounds__(kBlock) void k_classify(BatchArgs a, WorkBufs w) {
       if (!ok) c = 255;
       w.cls[i] = (uint8_t)c;
       atomicAdd(&hist[c == 255 ? kNumClasses : c], 1);
+      if (j.key_offset >= 0) atomicAdd(&keyed, 1);
       if (nn_writes_c(j)) {
         const int np = nn_pushes(j);
 #pragma unroll
@@ -151,6 +155,7 @@ __global__ __launch_bounds__(kBlock) void k_classify(BatchArgs a, WorkBufs w) {
     if (mx[f] >= 0) atomicMax(&agg[f], mx[f]);
   __syncthreads();
   if (tid < kNumClasses + 1 && hist[tid]) atomicAdd(&w.counts[tid], hist[tid]);
+  if (tid == 0 && keyed) atomicAdd(&w.counts[kKeyedWord], keyed);
   if (tid < 9) w.blk_agg[blockIdx.x * 9 + tid] = agg[tid];
 }
 
@@ -520,24 +525,19 @@ __global__ void k_put_state(uint32_t* dst, State12 st) {
   if (threadIdx.x < 12) dst[threadIdx.x] = st.v[threadIdx.x];
 }
 
-// The picture / lambda tables of a batch, likewise as a kernel argument (3 KB < the 4 KB limit):
-// no copy-engine transfer on the batch stream, which would queue behind bulk uploads.
-struct TablesArg {
-  PicDesc pics[FME_MAX_PICTURES];
-  double ml[FME_MAX_LAMBDAS];
-};
-static_assert(sizeof(TablesArg) <= 3584, "tables must fit the kernel-argument segment");
-__global__ __launch_bounds__(256) void k_put_tables(PicDesc* __restrict__ pics, double* __restrict__ ml, TablesArg t) {
+// The picture / lambda tables of a batch from a pinned, device-mapped host slot (fme_api.cpp
+// sync_tables: a ring of slots, each reused only once its launch has run).  (They were a 3.5 KB
+// kernel argument: with batches queued two deep, a launch then read the arguments of the batch two
+// before or after it, i.e. another frame's pictures and lambdas; tools/parity_debug.py.)
+__global__ __launch_bounds__(256) void k_put_tables(PicDesc* __restrict__ pics, double* __restrict__ ml,
+                                                    const TablesSlot* __restrict__ t) {
   const int i = threadIdx.x;
-  if (i < FME_MAX_PICTURES) pics[i] = t.pics[i];
-  if (i < FME_MAX_LAMBDAS) ml[i] = t.ml[i];
+  if (i < FME_MAX_PICTURES) pics[i] = t->pics[i];
+  if (i < FME_MAX_LAMBDAS) ml[i] = t->ml[i];
 }
 
-hipError_t launch_put_tables(PicDesc* d_pics, double* d_ml, const PicDesc* pics, const double* ml, hipStream_t s) {
-  TablesArg t;
-  for (int i = 0; i < FME_MAX_PICTURES; i++) t.pics[i] = pics[i];
-  for (int i = 0; i < FME_MAX_LAMBDAS; i++) t.ml[i] = ml[i];
-  hipLaunchKernelGGL(k_put_tables, dim3(1), dim3(256), 0, s, d_pics, d_ml, t);
+hipError_t launch_put_tables(PicDesc* d_pics, double* d_ml, const TablesSlot* t_dev, hipStream_t s) {
+  hipLaunchKernelGGL(k_put_tables, dim3(1), dim3(256), 0, s, d_pics, d_ml, t_dev);
   return hipGetLastError();
 }
 

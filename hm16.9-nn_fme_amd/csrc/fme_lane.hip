@@ -1288,7 +1288,7 @@ int lane_lanes_per_pu(int cls) {
 // Workgroups of the lane-kernel launch: at most the wave tiles n jobs could need (4 per
 // workgroup), at most 4 per CU (the kernel holds 2; spare workgroups find the queues drained
 // and exit).
-static int lane_grid(int n) {
+static int lane_grid(int n, int reserve) {
   static int cus = 0;
   if (!cus) {
     int dev = 0;
@@ -1302,11 +1302,14 @@ static int lane_grid(int n) {
       classes++;
     }
   const long long waves = ((long long)n * max_l + 63) / 64 + classes;
-  return (int)std::min<long long>((waves + kLaneNT / 64 - 1) / (kLaneNT / 64), 4LL * cus);
+  // reserve > 0: exactly the resident workgroups less `reserve` (spare workgroups beyond the
+  // resident ones would take the slots left free as soon as they open)
+  const long long cap = reserve > 0 ? std::max(1LL, (long long)FME_LANE_WAVES * cus - reserve) : 4LL * cus;
+  return (int)std::min<long long>((waves + kLaneNT / 64 - 1) / (kLaneNT / 64), cap);
 }
 
-hipError_t launch_search_lane(const BatchArgs& a, const WorkBufs& w, hipStream_t s) {
-  const int blocks = lane_grid(a.n);
+hipError_t launch_search_lane(const BatchArgs& a, const WorkBufs& w, int reserve, hipStream_t s) {
+  const int blocks = lane_grid(a.n, reserve);
   if (blocks <= 0) return hipSuccess;
   hipLaunchKernelGGL(k_search_lane, dim3(blocks), dim3(kLaneNT), 0, s, a, w);
   return hipGetLastError();

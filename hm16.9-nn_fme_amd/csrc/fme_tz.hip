@@ -218,9 +218,9 @@ __device__ __forceinline__ void load_window(uint32_t (&w)[UH][UW / 4 + 1], uint3
 }
 
 // One unit's share of the distortion (TComRdCost metric of the integer search) for a window.
-template <int UW, int UH>
+template <int UW, int UH, int KW>
 __device__ __forceinline__ uint32_t unit_part(const uint32_t (&w)[UH][UW / 4 + 1], uint32_t s0,
-                                              const uint32_t (&kk)[UH][UW / 2], int sk2, bool kbuf,
+                                              const uint32_t (&kk)[UH][KW], int sk2, bool kbuf,
                                               bool sad_metric, bool sub) {
   int sop = 0, spp = 0;
   uint32_t acc = 0;
@@ -238,7 +238,7 @@ __device__ __forceinline__ uint32_t unit_part(const uint32_t (&w)[UH][UW / 4 + 1
           sop = dot4(kk[r][c] ^ 0x80808080u, ps, sop);
           spp = dot4(ps, ps, spp);
         }
-      } else {
+      } else if constexpr (KW == UW / 2) {
         const uint32_t d0 = pk_sub(kk[r][2 * c], lo_pair(pv));
         const uint32_t d1 = pk_sub(kk[r][2 * c + 1], hi_pair(pv));
         if (sad_metric) {
@@ -308,7 +308,9 @@ __device__ __forceinline__ uint64_t block_min(uint64_t key) {
   }
 }
 
-template <int UW, int UH, int NW = 1>
+// KB: -1 any job; 0 the uni-pred form (no job of the launch reads a key block: the key rows are
+// UW / 4 dwords of bytes, half the registers of the int16 form)
+template <int UW, int UH, int NW = 1, int KB = -1>
 __device__ __forceinline__ void tz_wave(const TzArgs& ta, int jid, const fme_job& j, int PW, int PH, int pred_x,
                                         int pred_y) {
   const BatchArgs& a = ta.a;
@@ -323,13 +325,14 @@ __device__ __forceinline__ void tz_wave(const TzArgs& ta, int jid, const fme_job
   const fme_tz_ext e = ta.ext[jid];
   const PicDesc ref = a.pics[j.ref_id];
   const double ml = a.mlambda[j.lambda_id];
-  const bool kbuf = j.key_offset >= 0;
+  const bool kbuf = KB != 0 && j.key_offset >= 0;
   const bool sad_metric = PW == 12 || PW == 24 || PW == 48;
   const bool sub = sad_metric && (a.fen == 1 || a.fen == 3) && PH > 8;
   const int ox = (int)j.x + ux * UW, oy = (int)j.y + uy * UH;
   constexpr int ND = UW / 4 + 1;
 
-  uint32_t kk[UH][UW / 2];
+  constexpr int KW = KB == 0 ? UW / 4 : UW / 2;   // key dwords per row
+  uint32_t kk[UH][KW];
   int sk2 = 0;
   if (!kbuf) {
     const PicDesc org = a.pics[j.org_id];
@@ -342,9 +345,9 @@ __device__ __forceinline__ void tz_wave(const TzArgs& ta, int jid, const fme_job
         sk2 = dot4(v ^ 0x80808080u, v ^ 0x80808080u, sk2);
       }
 #pragma unroll
-      for (int c = UW / 4; c < UW / 2; c++) kk[r][c] = 0;
+      for (int c = UW / 4; c < KW; c++) kk[r][c] = 0;
     }
-  } else {
+  } else if constexpr (KW == UW / 2) {
     const int16_t* kb = a.keys + (size_t)j.key_offset + (size_t)(uy * UH) * PW + ux * UW;
 #pragma unroll
     for (int r = 0; r < UH; r++)
@@ -368,7 +371,7 @@ __device__ __forceinline__ void tz_wave(const TzArgs& ta, int jid, const fme_job
       uint32_t w[UH][ND];
       uint32_t s0;
       load_window<UW, UH>(w, s0, ref, ox + x, oy + y, sub);
-      part = unit_part<UW, UH>(w, s0, kk, sk2, kbuf, sad_metric, sub);
+      part = unit_part<UW, UH, KW>(w, s0, kk, sk2, kbuf, sad_metric, sub);
     }
     const uint32_t d = group_sum(part, L);
     dist = v ? d : 0xFFFFFFFFu;
@@ -683,8 +686,8 @@ __constant__ int kTzH[kNumClasses] = {8, 4, 8, 16, 4, 16, 8, 16, 12, 16, 32, 8, 
 
 // Wave-uniform bulk search: one wave per PU of the kernel's unit shape, PUs in class order (CTU
 // order inside a class); blocks dealt to the XCDs in contiguous ranges so each L2 sees one band.
-#ifndef FME_TZW_WAVES
-#define FME_TZW_WAVES 4
+#ifndef FME_TZW_WAVES   // waves per SIMD (1080p frame, tools/tz_probe.py: 4 -> 6.17 ms, 5 -> 5.84 ms)
+#define FME_TZW_WAVES 5
 #endif
 // Work order: block b runs on XCD b % 8 (round-robin dispatch), and XCD x owns the x-th eighth of
 // every class of this kernel (a spatial band per L2), largest PU class first: the long searches
@@ -704,7 +707,7 @@ __device__ __forceinline__ int tz_entry(const TzSchedule& sc, int kid, int x, in
   return -1;
 }
 
-template <int UW, int UH>
+template <int UW, int UH, int KB>
 __global__ __launch_bounds__(kTzNT) __attribute__((amdgpu_waves_per_eu(FME_TZW_WAVES)))
 void k_tz_wave(TzArgs ta, TzSchedule sc, int kid) {
   const int x = (int)blockIdx.x & 7;
@@ -714,7 +717,7 @@ void k_tz_wave(TzArgs ta, TzSchedule sc, int kid) {
   if (q < 0) return;
   const int jid = ta.perm[q];
   const fme_job j = FME_SJOBS ? ta.sjobs[q] : ta.a.jobs[jid];
-  tz_wave<UW, UH>(ta, jid, j, kTzW[c], kTzH[c], ta.ext[jid].pred2n_x, ta.ext[jid].pred2n_y);
+  tz_wave<UW, UH, 1, KB>(ta, jid, j, kTzW[c], kTzH[c], ta.ext[jid].pred2n_x, ta.ext[jid].pred2n_y);
 }
 
 // One dependency level of a producer's m_integerMv2Nx2N chain (fme_pred_inter_p/b): one wave per
@@ -768,7 +771,7 @@ int tz_lanes_per_pu(int cls) {
 }
 
 // Wave-uniform bulk search of kernel kid: sc.prefix in waves (one per PU).
-hipError_t launch_tz_wave(const TzArgs& ta, const TzSchedule& sc, int kid, hipStream_t s) {
+hipError_t launch_tz_wave(const TzArgs& ta, const TzSchedule& sc, int kid, bool keyed, hipStream_t s) {
   int share = 0;   // the largest per-XCD share of this kernel's PUs (waves)
   for (int x = 0; x < 8; x++) {
     int n = 0;
@@ -779,9 +782,15 @@ hipError_t launch_tz_wave(const TzArgs& ta, const TzSchedule& sc, int kid, hipSt
   }
   if (share <= 0) return hipSuccess;
   const int blocks = 8 * ((share + kTzNT / 64 - 1) / (kTzNT / 64));
-  if (kid == 0) hipLaunchKernelGGL((k_tz_wave<4, 8>), dim3(blocks), dim3(kTzNT), 0, s, ta, sc, 0);
-  else if (kid == 1) hipLaunchKernelGGL((k_tz_wave<8, 4>), dim3(blocks), dim3(kTzNT), 0, s, ta, sc, 1);
-  else hipLaunchKernelGGL((k_tz_wave<8, 8>), dim3(blocks), dim3(kTzNT), 0, s, ta, sc, 2);
+  if (keyed) {
+    if (kid == 0) hipLaunchKernelGGL((k_tz_wave<4, 8, -1>), dim3(blocks), dim3(kTzNT), 0, s, ta, sc, 0);
+    else if (kid == 1) hipLaunchKernelGGL((k_tz_wave<8, 4, -1>), dim3(blocks), dim3(kTzNT), 0, s, ta, sc, 1);
+    else hipLaunchKernelGGL((k_tz_wave<8, 8, -1>), dim3(blocks), dim3(kTzNT), 0, s, ta, sc, 2);
+  } else {
+    if (kid == 0) hipLaunchKernelGGL((k_tz_wave<4, 8, 0>), dim3(blocks), dim3(kTzNT), 0, s, ta, sc, 0);
+    else if (kid == 1) hipLaunchKernelGGL((k_tz_wave<8, 4, 0>), dim3(blocks), dim3(kTzNT), 0, s, ta, sc, 1);
+    else hipLaunchKernelGGL((k_tz_wave<8, 8, 0>), dim3(blocks), dim3(kTzNT), 0, s, ta, sc, 2);
+  }
   return hipGetLastError();
 }
 

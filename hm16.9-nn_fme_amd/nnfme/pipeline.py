@@ -35,19 +35,51 @@ from .abi import JOB_DTYPE, MV_RESULT_DTYPE
 _hip = None
 
 
+def _hip_lib():
+    global _hip
+    if _hip is None:
+        h = ctypes.CDLL("libamdhip64.so.7")   # by SONAME: the runtime torch and libfme_amd.so share
+        h.hipMemcpyAsync.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_void_p]
+        h.hipMemcpyAsync.restype = ctypes.c_int
+        h.hipEventCreateWithFlags.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_uint]
+        h.hipEventCreateWithFlags.restype = ctypes.c_int
+        h.hipEventDestroy.argtypes = [ctypes.c_void_p]
+        h.hipEventDestroy.restype = ctypes.c_int
+        h.hipStreamWaitEvent.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint]
+        h.hipStreamWaitEvent.restype = ctypes.c_int
+        _hip = h
+    return _hip
+
+
 def _memcpy_async(dst, src, nbytes, kind, stream):
     """hipMemcpyAsync between pinned host and device memory on `stream` (a torch stream): the
     copy engines (SDMA) carry it.  (A torch D2H copy_ runs as a blit kernel on the CUs, which
     then waits for the search kernels' workgroups.)"""
-    global _hip
-    if _hip is None:
-        _hip = ctypes.CDLL("libamdhip64.so.7")   # by SONAME: the runtime torch and libfme_amd.so share
-        _hip.hipMemcpyAsync.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int,
-                                        ctypes.c_void_p]
-        _hip.hipMemcpyAsync.restype = ctypes.c_int
-    rc = _hip.hipMemcpyAsync(dst.data_ptr(), src.data_ptr(), nbytes, kind, stream.cuda_stream)
+    rc = _hip_lib().hipMemcpyAsync(dst.data_ptr(), src.data_ptr(), nbytes, kind, stream.cuda_stream)
     if rc != 0:
         raise RuntimeError(f"hipMemcpyAsync failed ({rc})")
+
+
+class _RawEvent:
+    """A hipEvent_t the library records (fme_set_search_event) and a stream waits on: created
+    unrecorded, so its only record is the library's."""
+
+    def __init__(self):
+        ev = ctypes.c_void_p()
+        if _hip_lib().hipEventCreateWithFlags(ctypes.byref(ev), 2) != 0:   # hipEventDisableTiming
+            raise RuntimeError("hipEventCreateWithFlags failed")
+        self.cuda_event = ev.value
+
+    def wait(self, stream):
+        if _hip_lib().hipStreamWaitEvent(stream.cuda_stream, self.cuda_event, 0) != 0:
+            raise RuntimeError("hipStreamWaitEvent failed")
+
+    def __del__(self):
+        try:
+            if self.cuda_event and _hip is not None:
+                _hip.hipEventDestroy(self.cuda_event)
+        except Exception:
+            pass
 
 
 H2D, D2H = 1, 2
@@ -96,7 +128,7 @@ def group_key_reqs(base, frames, key_count):
 class FrameReplay:
     def __init__(self, ctx, base_jobs, pool, lambda_of, n_steps, frames_per_step=1, world=1, rank=0, device=None,
                  group=None, defer_download=True, key_reqs=None, key_count=0, nn_rows=None,
-                 download_engine="blit", download_wgs=8):
+                 download_engine="blit", download_wgs=8, search_reserve=0):
         """ctx: an FmeContext on `device`; base_jobs: one frame's jobs (ref_id = reference
         distance - 1); pool: uint8 [P, H, W] host frames, frame g's pictures are pool[g % P];
         lambda_of(g): frame g's lambda (pool uint16: main10 samples for a bit-depth-10 context,
@@ -109,7 +141,8 @@ class FrameReplay:
         download_engine: "kernel" (fme_download_device: the library's copy kernel of
         download_wgs workgroups of 256 lanes, which hold a few wave slots beside the next step's
         search) or "blit" (hipMemcpyAsync, which this ROCm runs as a blit kernel of hundreds of
-        workgroups that take the search kernel's CUs)."""
+        workgroups that take the search kernel's CUs).  search_reserve: resident search workgroups
+        left free (fme_set_search_reserve), so the download kernel runs beside the search."""
         import torch
         self.torch, self.ctx = torch, ctx
         self.world, self.rank, self.group = world, rank, group
@@ -151,18 +184,22 @@ class FrameReplay:
         self.s_copy = torch.cuda.Stream(device)   # H2D: jobs, originals, reconstructions
         self.s_down = torch.cuda.Stream(device)   # D2H: results (the other copy direction, its own engine)
         self.uploaded = -1
-        self.ev_in = [torch.cuda.Event() for _ in range(2)]
-        self.ev_comp = [torch.cuda.Event() for _ in range(2)]
-        self.ev_out = [torch.cuda.Event() for _ in range(2)]
+        # one event of each kind per step, each recorded once: a stream wait on an event that is
+        # recorded again while earlier waits on it are still queued did not always wait for the
+        # record it was issued after here (step k's download then read the buffer before step k's
+        # batch had written it, or after step k+2's had: tools/parity_debug.py)
+        self.ev_in = [torch.cuda.Event() for _ in range(n_steps)]
+        self.ev_comp = [torch.cuda.Event() for _ in range(n_steps)]
+        self.ev_out = [torch.cuda.Event() for _ in range(n_steps)]
         # recorded by the library right before each batch's search kernel (fme_set_search_event):
         # step k's results are downloaded once step k+1's search runs (see issue())
-        self.ev_search = torch.cuda.Event()
-        self.ev_search.record(self.s_comp)        # creates the underlying hipEvent_t
+        self.ev_search = [_RawEvent() for _ in range(n_steps)]
         self.defer_download = defer_download
         if download_engine not in ("kernel", "blit"):
             raise ValueError(f"download_engine {download_engine!r}")
         self.download_engine, self.download_wgs = download_engine, int(download_wgs)
-        ctx.set_search_event(self.ev_search if defer_download else None)
+        ctx.set_search_reserve(int(search_reserve))   # slots the search leaves to the download kernel
+        ctx.set_search_event(None)                # set per step in issue()
         self.pending = None                       # step whose download is not issued yet
         self.fixed_jobs = 0
 
@@ -299,7 +336,7 @@ class FrameReplay:
         cp = self.s_copy
         with self.torch.cuda.stream(cp):
             if k >= 2:
-                cp.wait_event(self.ev_comp[b])            # step k-2 is done with the slot
+                cp.wait_event(self.ev_comp[k - 2])        # step k-2 is done with the slot
             _memcpy_async(self.d_jobs[b], self.h_jobs, self.h_jobs.numel(), H2D, cp)
             if self.rows is not None:
                 _memcpy_async(self.d_rows[b], self.h_rows, self.h_rows.numel(), H2D, cp)
@@ -311,7 +348,7 @@ class FrameReplay:
             self._publish_run(base + self.rank * F - 1, F, self.rank, cp)
             if self.world > 1:   # ... and sent to the ranks whose frames reference it
                 self._exchange(k, cp)
-            self.ev_in[b].record(cp)
+            self.ev_in[k].record(cp)
         self.uploaded = k
 
     def issue(self, k, prefetch=True):
@@ -322,43 +359,48 @@ class FrameReplay:
         if self.uploaded < k:
             self._upload(k)
         comp = self.s_comp
-        comp.wait_event(self.ev_in[b])
+        comp.wait_event(self.ev_in[k])
         if k >= 2:
-            comp.wait_event(self.ev_out[b])                # step k-2's results have left
+            comp.wait_event(self.ev_out[k - 2])            # step k-2's results have left
         self._bind(k)
         if self.kreqs is not None:   # this step's frames' removeHighFreq keys, from this step's pictures
             ctx.build_bipred_keys_device(self.d_kreqs[b].data_ptr(), len(self.kreqs), self.key_count * self.F,
                                          comp.cuda_stream)
         if self.world > 1:
             ctx.nn_reset()                                 # stream-ordered: this batch starts fresh
+        if self.defer_download:
+            ctx.set_search_event(self.ev_search[k])        # recorded right before this batch's search
         ctx.refine_mv_device(self.d_jobs[b].data_ptr(), self.d_out[b].data_ptr(), self.n, comp.cuda_stream)
         if self.world > 1:
             ctx.nn_copy_state_device(self.states[k].data_ptr(), comp.cuda_stream)
-        self.ev_comp[b].record(comp)
+        self.ev_comp[k].record(comp)
         if prefetch and k + 1 < self.steps:
             self._upload(k + 1)
         if not self.defer_download:
-            self._download(k, self.ev_comp[b])
+            self._download(k, self.ev_comp[k])
             return
         if self.pending is not None:   # step k's search started: k-1 is done (its own batch event otherwise)
-            self._download(self.pending, self.ev_search if self.n > 0 else self.ev_comp[self.pending & 1])
+            self._download(self.pending, self.ev_search[k] if self.n > 0 else self.ev_comp[self.pending])
         self.pending = k
 
     def _download(self, k, after):
         dn = self.s_down
-        dn.wait_event(after)
+        if isinstance(after, _RawEvent):
+            after.wait(dn)
+        else:
+            dn.wait_event(after)
         if self.download_engine == "kernel":
             self.ctx.download_device(self.d_out[k & 1].data_ptr(), self.h_out[k].data_ptr(), self.h_out.shape[1],
                                      self.download_wgs, dn.cuda_stream)
         else:
             _memcpy_async(self.h_out[k], self.d_out[k & 1], self.h_out.shape[1], D2H, dn)
-        self.ev_out[k & 1].record(dn)
+        self.ev_out[k].record(dn)
 
     def drain(self):
         """Issue the last step's download and wait for every stream; the library no longer records
         into this replay's search event afterwards (the context may outlive the replay)."""
         if self.pending is not None:
-            self._download(self.pending, self.ev_comp[self.pending & 1])
+            self._download(self.pending, self.ev_comp[self.pending])
             self.pending = None
         self.s_copy.synchronize()
         self.s_comp.synchronize()

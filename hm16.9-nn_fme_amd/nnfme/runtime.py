@@ -15,7 +15,7 @@ from .weights import load_weights
 PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB_PATH = os.environ.get("FME_LIB_PATH") or os.path.join(PKG_ROOT, "libfme_amd.so")
 
-ABI_VERSION = 14
+ABI_VERSION = 15
 TIMING_NAMES = ("classify", "scatter", "search", "nn_tail", "batch", "search_main", "search_aux")
 
 # Every entry point include/fme.h declares (the ABI test checks the .so exports them).
@@ -33,7 +33,7 @@ ABI_SYMBOLS = (
     "fme_refine_status", "fme_nn_copy_state_device", "fme_template_costs", "fme_pred_inter_b", "fme_build_bipred_keys",
     "fme_set_search_event", "fme_build_bipred_keys_device", "fme_set_nn_logit_output",
     "fme_set_nn_inputs", "fme_integer_search_ring", "fme_integer_search_ring_device",
-    "fme_download_device", "fme_pred_inter_phases",
+    "fme_download_device", "fme_pred_inter_phases", "fme_set_search_reserve",
 )
 
 
@@ -114,6 +114,7 @@ def load_library(path=None):
         "fme_integer_search_ring_device": (I, [P, P, P, P, P, I, P]),
         "fme_download_device": (I, [P, P, P, C.c_size_t, I, P]),
         "fme_pred_inter_phases": (I, [P, P, I]),
+        "fme_set_search_reserve": (I, [P, I]),
     }
     # an explicitly named library is an A/B variant (tools/ab_bench.py): possibly an older ABI
     strict = os.path.abspath(path) == os.path.abspath(LIB_PATH)
@@ -425,6 +426,10 @@ class FmeContext:
         if event is not None and hasattr(event, "cuda_event"):
             event = event.cuda_event
         _check(self.lib, self.lib.fme_set_search_event(self.h, C.c_void_p(event) if event else None))
+
+    def set_search_reserve(self, workgroups):
+        """Resident search workgroups left free for a few-workgroup kernel beside it (fme_set_search_reserve)."""
+        _check(self.lib, self.lib.fme_set_search_reserve(self.h, int(workgroups)))
 
     def frac_dif_single(self, key, ref_window, ref_origin, mv_int, mvp, motion_lambda, lossless=False):
         """xPatternSearchFracDIF argument list: key block (int16 HxW), a padded reference

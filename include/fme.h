@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define FME_ABI_VERSION 14
+#define FME_ABI_VERSION 15
 
 /* ---- error codes ---------------------------------------------------------------- */
 #define FME_OK            0
@@ -288,6 +288,13 @@ int fme_nn_copy_state_device(fme_ctx* ctx, uint32_t* d_out12, void* stream);
  * back every read the device issues behind them (AQL packet and kernel-argument fetches), so a
  * download overlapping a prologue delayed each of its launches by the length of the copy.   */
 int fme_set_search_event(fme_ctx* ctx, void* event);
+
+/* Workgroup slots the search kernel leaves free for a few-workgroup kernel on another stream (the
+ * results download of fme_download_device, queued beside the next batch's search): 0 (default)
+ * sizes the persistent search grid to fill the chip; n > 0 launches n fewer workgroups than fit
+ * resident, so such a kernel starts at once instead of after the search.  No replacement of a
+ * reference interface (pipeline tuning).                                                      */
+int fme_set_search_reserve(fme_ctx* ctx, int workgroups);
 
 /* Download of device records (fme_mv_result / fme_result rows, any 16-byte-multiple span) into
  * pinned host memory (hipHostMalloc, hipHostRegister or a torch pin_memory() tensor) by the

@@ -23,6 +23,25 @@ for step in "$@"; do
     prof) run prof 400 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run -- python3 bench.py --no-cpu-baseline --no-pi --no-tz --no-mc --parity-seconds 0 ;;
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     pdebug) run pdebug 300 python -u tools/parity_debug.py 20 3 8 && run pdebug10 300 python -u tools/parity_debug.py 3 3 10 ;;
+    verify) run pm_base 200 python -u tools/parity_debug.py 20 3 8 base && run pm_base10 200 python -u tools/parity_debug.py 6 3 10 base && \
+            run pb20 300 python -u bench.py --no-pi --no-tz --no-mc --no-cpu-baseline --steps 20 --parity-seconds 10 && \
+            run vtests 500 python -u -m pytest tests/test_gpu_c4.py tests/test_gpu_main10.py tests/test_gpu_dist.py tests/test_gpu_parity.py tests/test_gpu_async.py -m gpu -x -q -p no:cacheprovider --timeout 300 --timeout-method thread && \
+            run tz_new 200 python -u tools/tz_probe.py gpurun_out/tz_new.npz && \
+            run tztests 400 python -u -m pytest tests -m gpu -k "tz or ring or integer or pred_inter" -x -q -p no:cacheprovider --timeout 300 --timeout-method thread && \
+            CPU=0 run pprobe 300 python -u tools/pred_inter_probe.py 3 ;;
+    dlab2) B="python -u bench.py --no-pi --no-tz --no-mc --no-cpu-baseline --parity-seconds 0 --steps 20"
+           run d_blit_def 200 $B && run d_blit_imm 200 $B --download immediate && \
+           run d_k_def_r0 200 $B --download-engine kernel && \
+           run d_k_def_r8 200 $B --download-engine kernel --search-reserve 8 && \
+           run d_k_def_r16 200 $B --download-engine kernel --search-reserve 16 && \
+           run d_k_def_r32w16 200 $B --download-engine kernel --search-reserve 32 --download-wgs 16 && \
+           run d_k_imm_r16 200 $B --download-engine kernel --search-reserve 16 --download immediate && \
+           run d_blit_def_r16 200 $B --search-reserve 16 ;;
+    pmodes) run pm_base 200 python -u tools/parity_debug.py 20 3 8 base && run pm_base10 200 python -u tools/parity_debug.py 6 3 10 base && \
+            run pi_tests 400 python -u -m pytest tests -m gpu -k "pred_inter" -x -q -p no:cacheprovider --timeout 300 --timeout-method thread && \
+            run pb20 300 python -u bench.py --no-pi --no-tz --no-mc --no-cpu-baseline --steps 20 --parity-seconds 10 && \
+            CPU=0 run pprobe 300 python -u tools/pred_inter_probe.py 3 && \
+            bash tools/gpu_r5.sh tzab tests ;;
     pprobe) CPU=0 run pprobe 300 python -u tools/pred_inter_probe.py 3 ;;
     m10prof) run m10prof 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/m10prof -o run -- python3 bench.py --workload c3_qp22_main10 --no-cpu-baseline --parity-seconds 0 --steps 5 ;;
     d2h) run d2h 200 ./tools/probes/d2h_kernel_probe ;;
@@ -42,6 +61,10 @@ for step in "$@"; do
     deepab2) run deeptests 400 python -u -m pytest tests/test_deep_nn.py tests/test_ring.py -m gpu -x -q -p no:cacheprovider --timeout 300 --timeout-method thread && \
              run deep_mall 300 python -u bench.py --workload c5 --no-cpu-baseline --parity-seconds 0 --steps 20 && \
              FME_LIB_PATH=$PWD/hm16.9-nn_fme_amd/variants/deep_mall0/libfme_amd.so run deep_mall0 300 python -u bench.py --workload c5 --no-cpu-baseline --parity-seconds 0 --steps 20 ;;
+    tzab) run tz_in 200 python -u tools/tz_probe.py gpurun_out/tz_in.npz && \
+          FME_LIB_PATH=$PWD/hm16.9-nn_fme_amd/variants/tz5/libfme_amd.so run tz_5 200 python -u tools/tz_probe.py gpurun_out/tz_5.npz && \
+          run tz_in2 200 python -u tools/tz_probe.py gpurun_out/tz_in2.npz && \
+          python3 -c "import numpy as np; a=np.load('gpurun_out/tz_in.npz'); b=np.load('gpurun_out/tz_5.npz'); print('identical', all((a[k]==b[k]).all() for k in a.files))" ;;
     tzprof) run tzprof 700 bash tools/gpu_tz_prof.sh ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac

@@ -2,7 +2,9 @@
 stream) against the library's host path with that step's bindings, NN off so that no carried state
 enters: a mismatch is a binding (pictures, lambdas, jobs) or ordering problem of the replay.
 
-usage: python tools/parity_debug.py [steps] [warmup] [bit_depth]"""
+usage: python tools/parity_debug.py [steps] [warmup] [bit_depth] [mode]
+mode: base | nodefer (downloads right after each batch) | noprefetch | serial (synchronize after
+every step) | noprof (profiling off)"""
 import os
 import sys
 
@@ -24,6 +26,7 @@ def main():
     steps = int(sys.argv[1]) if len(sys.argv) > 1 else 20
     warm = int(sys.argv[2]) if len(sys.argv) > 2 else 3
     bd = int(sys.argv[3]) if len(sys.argv) > 3 else 8
+    mode = sys.argv[4] if len(sys.argv) > 4 else "base"
     wl = bench.WORKLOADS["c3_qp22"]
     jobs = bench.make_frame_jobs(1000, "ctu", wl["calls"], wl["bipred"])
     m = 4000
@@ -32,14 +35,17 @@ def main():
     pool = np.stack([pic(t) for t in range(8)])
     ctx = FmeContext(device=0, nn_mode=0, qp=22, fast_inter_mode=1, max_jobs=len(jobs), bit_depth=bd)
     lam = lambda f: bench.frame_lambda(wl, f)   # noqa: E731
-    rep = FrameReplay(ctx, jobs, pool, lam, warm + steps, device=torch.device("cuda", 0))
+    rep = FrameReplay(ctx, jobs, pool, lam, warm + steps, device=torch.device("cuda", 0),
+                      defer_download=mode != "nodefer")
     rep.prime()
     for s in range(warm):
         rep.issue(s, prefetch=s + 1 < warm)
     rep.drain()
-    ctx.set_profiling(True)
+    ctx.set_profiling(mode != "noprof")
     for s in range(warm, warm + steps):
-        rep.issue(s)
+        rep.issue(s, prefetch=mode != "noprefetch")
+        if mode == "serial":
+            torch.cuda.synchronize()
     rep.finish(first_step=warm)
     torch.cuda.synchronize()
     c2 = FmeContext(device=0, nn_mode=0, qp=22, fast_inter_mode=1, max_jobs=m, bit_depth=bd)
@@ -74,7 +80,7 @@ def main():
                 if all(int((b2[f] != g[f]).sum()) == 0 for f in ("mv_x", "mv_y", "cost")):
                     match = f"lambda{dl:+d}"
                     break
-        print(f"step {k}: frame {f0} lambda {lam(f0)} mismatches {bad} matches frame offset {match}", flush=True)
+        print(f"[{mode}] step {k}: frame {f0} lambda {lam(f0)} mismatches {bad} matches frame offset {match}", flush=True)
 
 
 if __name__ == "__main__":

@@ -40,6 +40,19 @@ def main():
           f"{np.bincount(res['ref_idx'], minlength=4).tolist()}", flush=True)
     print("pred_inter phases (ms, last frame):",
           {k: round(v, 2) for k, v in ctx.pred_inter_phases().items()}, flush=True)
+    # the B slice of bench.py's producer leg: L0 = {t-1, t-2}, L1 = {t+1, t+2}, FEN 1
+    ctx.set_picture(5, synth.synth_luma(W, H, 3))
+    reqs_b = synth.make_pu_requests_b(np.random.default_rng(3), W, H, org_id=4, l0=[(0, 1), (1, 2)],
+                                      l1=[(5, -1), (2, -2)], lambda_id=0, max_depth=depth)
+    ctx.pred_inter_b(reqs_b)   # warm-up
+    ts = []
+    for _ in range(3):
+        ctx.pred_inter_reset()
+        t0 = time.perf_counter()
+        ctx.pred_inter_b(reqs_b)
+        ts.append(time.perf_counter() - t0)
+    print(f"pred_inter_b {W}x{H} depth {depth}: {len(reqs_b)} PU requests in {np.median(ts) * 1e3:.1f} ms; phases (ms):",
+          {k: round(v, 2) for k, v in ctx.pred_inter_phases().items()}, flush=True)
     # CPU: the oracle's sequential restatement on a bounded sample (first CTU rows)
     if os.environ.get("CPU", "1") == "1":
         from oracle import Oracle
