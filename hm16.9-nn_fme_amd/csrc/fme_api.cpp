@@ -219,6 +219,7 @@ struct fme_ctx {
   HostBuf<fme_result> h_pi_ures;  // fme_pred_inter_b: the uni-pred jobs' records
   HostBuf<fme_job> h_pi_seq;      // fme_pred_inter_b: one round's jobs in call order
   HostBuf<fme_mv_result> h_pi_rs; // fme_pred_inter_b: their results
+  HostBuf<uint32_t> h_pi_rows;    // fme_pred_inter_b: the bi jobs' NN input rows
   std::vector<int> pi_base, pi_task, pi_level, pi_src, pi_lvl, pi_start, pi_byarea;
   std::vector<int32_t> pi_off, pi_fill;
   std::vector<uint8_t> pi_amvp_idx;
@@ -351,7 +352,7 @@ int fme_destroy(fme_ctx* c) {
   c->d_amvp.release(); c->d_amvp_sad.release(); c->d_bikey.release(); c->d_key_invalid.release(); c->d_ch_i32.release(); c->d_tz_emi.release();
   c->h_pi_tasks.release(); c->h_pi_tsad.release(); c->h_pi_jobs.release(); c->h_pi_ext.release();
   c->h_pi_idx.release(); c->h_pi_psrc.release(); c->h_pi_mv.release(); c->h_pi_last.release();
-  c->h_pi_ures.release(); c->h_pi_seq.release(); c->h_pi_rs.release();
+  c->h_pi_ures.release(); c->h_pi_seq.release(); c->h_pi_rs.release(); c->h_pi_rows.release();
   c->d_pi_jobs.release(); c->d_pi_ext.release(); c->d_pi_idx.release();
   for (auto& e : c->ev_tz)
     if (e) (void)hipEventDestroy(e);
@@ -2340,6 +2341,27 @@ int fme_pred_inter_b(fme_ctx* c, const fme_pu_req_b* reqs, fme_pu_res_b* res, in
   if (c->h_counts[0] > 0)
     return fail(FME_E_INVALID, "fme_pred_inter_b: %d job(s) rejected by the refinement batch", c->h_counts[0]);
   const fme_result* const ru = c->h_pi_ures.p;
+  uint32_t s_end[12];   // the carried state after the uni jobs (what a bi round must leave)
+  rc = fme_nn_get_state(c, s_end);
+  if (rc) return rc;
+  // rowst[i]: NN_pred's carried array_e slots and C after request i's uni jobs (their EMI pushes over
+  // the state before them), the inputs its bi jobs read
+  std::vector<uint32_t> rowst((size_t)n * 9);
+  {
+    uint32_t cur[9];
+    for (int k = 0; k < 9; k++) cur[k] = s0[k];
+    for (int i = 0; i < n; i++) {
+      for (int u = ubeg[i]; u < ubeg[i + 1]; u++)
+        if (uj[u].flags & FME_JOB_EMI) {
+          for (int k = 0; k < (int)ru[u].n_emi && k < 8; k++) cur[k] = ru[u].emi[k];
+          cur[8] = ru[u].c;
+        }
+      std::memcpy(&rowst[(size_t)9 * i], cur, sizeof(cur));
+      // a per-call array_e reset (FME_NN_IN_SLOT_RESET nets): a bi call has no pushes of its own
+      if (c->cfg.nn_mode == 2 && (c->net.input_flags & FME_NN_IN_SLOT_RESET))
+        std::memset(&rowst[(size_t)9 * i], 0, 8 * sizeof(uint32_t));
+    }
+  }
   clk.lap(4);
   // ---- 4. rounds of host decisions and bi-pred searches ----
   std::vector<BPu> st((size_t)n);
@@ -2581,37 +2603,46 @@ int fme_pred_inter_b(fme_ctx* c, const fme_pu_req_b* reqs, fme_pu_res_b* res, in
     HIP_TRY(launch_bi_key(ka, s));
     rc = tz_run_host(c, bj.data(), be.data(), nullptr, (int)bj.size(), stream, nullptr);
     if (rc) return rc;
-    // the round's jobs in call order (pinned): every uni job, each issued request's bi jobs after its own
-    std::vector<int> pos(issued.size());
-    const size_t nseq = (size_t)nu + bj.size();
-    HIP_TRY(c->h_pi_seq.reserve(nseq));
-    HIP_TRY(c->h_pi_rs.reserve(nseq));
+    // the round's bi jobs alone: in call order each sits right after its request's uni jobs, reads
+    // the carried NN state there and writes none (TEncSearch.cpp:88-134), so each is refined as an
+    // FME_JOB_NN_IN job whose row is that state (rowst, computed once from the uni records) instead
+    // of refining every uni job again around them
+    const int nbj = (int)bj.size();
+    HIP_TRY(c->h_pi_seq.reserve((size_t)nbj));
+    HIP_TRY(c->h_pi_rs.reserve((size_t)nbj));
+    HIP_TRY(c->h_pi_rows.reserve((size_t)nbj * 9));
     fme_job* const seq = c->h_pi_seq.p;
-    size_t t = 0, ns = 0;
-    for (int i = 0; i < n; i++) {
-      std::memcpy(seq + ns, uj + ubeg[i], (size_t)(ubeg[i + 1] - ubeg[i]) * sizeof(fme_job));
-      ns += (size_t)(ubeg[i + 1] - ubeg[i]);
-      if (t < issued.size() && issued[t] == i) {
-        pos[t] = (int)ns;
-        const int nb = reqs[i].num_refs[st[i].L];
-        std::memcpy(seq + ns, bj.data() + st[i].bi0, (size_t)nb * sizeof(fme_job));
-        ns += (size_t)nb;
-        t++;
+    uint32_t* const rows = c->h_pi_rows.p;
+    for (int i : issued) {
+      const int nb = reqs[i].num_refs[st[i].L];
+      for (int k = 0; k < nb; k++) {
+        const int q = st[i].bi0 + k;
+        seq[q] = bj[q];
+        seq[q].flags = (uint8_t)(seq[q].flags | FME_JOB_NN_IN);
+        std::memcpy(rows + (size_t)9 * q, &rowst[(size_t)9 * i], 9 * sizeof(uint32_t));
       }
     }
-    rc = fme_nn_set_state(c, s0);
+    HIP_TRY(c->d_jobs.reserve(nbj));
+    HIP_TRY(c->d_res.reserve(nbj));
+    HIP_TRY(c->d_mv.reserve(nbj));
+    HIP_TRY(c->d_tz_nn_in.reserve((size_t)nbj * 9));
+    HIP_TRY(hipMemcpyAsync(c->d_jobs.p, seq, (size_t)nbj * sizeof(fme_job), hipMemcpyHostToDevice, s));
+    HIP_TRY(hipMemcpyAsync(c->d_tz_nn_in.p, rows, (size_t)nbj * 9 * sizeof(uint32_t), hipMemcpyHostToDevice, s));
+    const uint32_t* const keep_in = c->nn_in;
+    const int keep_cap = c->nn_in_cap;
+    c->nn_in = c->d_tz_nn_in.p;
+    c->nn_in_cap = nbj;
+    rc = refine_batch(c, c->d_jobs.p, c->d_res.p, c->d_mv.p, nbj, s);
+    c->nn_in = keep_in;
+    c->nn_in_cap = keep_cap;
     if (rc) return rc;
-    HIP_TRY(c->d_jobs.reserve(ns));
-    HIP_TRY(c->d_res.reserve(ns));
-    HIP_TRY(c->d_mv.reserve(ns));
-    HIP_TRY(hipMemcpyAsync(c->d_jobs.p, seq, ns * sizeof(fme_job), hipMemcpyHostToDevice, s));
-    rc = refine_batch(c, c->d_jobs.p, c->d_res.p, c->d_mv.p, (int)ns, s);
-    if (rc) return rc;
-    HIP_TRY(hipMemcpyAsync(c->h_pi_rs.p, c->d_mv.p, ns * sizeof(fme_mv_result), hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipMemcpyAsync(c->h_pi_rs.p, c->d_mv.p, (size_t)nbj * sizeof(fme_mv_result), hipMemcpyDeviceToHost, s));
     HIP_TRY(hipMemcpyAsync(c->h_counts, &c->d_sched.p->invalid, sizeof(int32_t), hipMemcpyDeviceToHost, s));
     HIP_TRY(hipStreamSynchronize(s));
     if (c->h_counts[0] > 0)
       return fail(FME_E_INVALID, "fme_pred_inter_b: %d job(s) rejected by a bi-pred round", c->h_counts[0]);
+    rc = fme_nn_set_state(c, s_end);   // the bi rows wrote the carried state: back to after the uni jobs
+    if (rc) return rc;
     const fme_mv_result* const rs = c->h_pi_rs.p;
     for (size_t t2 = 0; t2 < issued.size(); t2++) {
       const int i = issued[t2];
@@ -2624,7 +2655,7 @@ int fme_pred_inter_b(fme_ctx* c, const fme_pu_req_b* reqs, fme_pu_res_b* res, in
       std::memset(o.bi_ref_cost, 0, sizeof(o.bi_ref_cost));
       std::memset(o.bi_ref_mv, 0, sizeof(o.bi_ref_mv));
       for (int k = 0; k < q.num_refs[L]; k++) {
-        const fme_mv_result& r = rs[pos[t2] + k];
+        const fme_mv_result& r = rs[p.bi0 + k];
         p.mvt[L][k][0] = r.mv_x;
         p.mvt[L][k][1] = r.mv_y;
         uint32_t b = r.bits, cst = r.cost;

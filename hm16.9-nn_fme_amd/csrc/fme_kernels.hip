@@ -526,9 +526,8 @@ __global__ void k_put_state(uint32_t* dst, State12 st) {
 }
 
 // The picture / lambda tables of a batch from a pinned, device-mapped host slot (fme_api.cpp
-// sync_tables: a ring of slots, each reused only once its launch has run).  (They were a 3.5 KB
-// kernel argument: with batches queued two deep, a launch then read the arguments of the batch two
-// before or after it, i.e. another frame's pictures and lambdas; tools/parity_debug.py.)
+// sync_tables: a ring of slots, each reused only once its launch has run), instead of a 3.5 KB
+// kernel argument at the edge of the argument segment.
 __global__ __launch_bounds__(256) void k_put_tables(PicDesc* __restrict__ pics, double* __restrict__ ml,
                                                     const TablesSlot* __restrict__ t) {
   const int i = threadIdx.x;

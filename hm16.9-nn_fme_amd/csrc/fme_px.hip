@@ -384,6 +384,9 @@ __global__ __launch_bounds__(kPxNT) void k_search_px(BatchArgs a, WorkBufs wb) {
 // job (17 us of workgroup time per job on the 1080p main10 frame).  Sums are wave reductions
 // (every lane holds every total), so the EMI decision and the candidate picks run on all lanes.
 constexpr int kPxSW = 16;                                   // largest side of the wave kernel's PUs
+#ifndef FME_PXW_WAVES   // waves per SIMD of the wave kernel (latency-bound: more waves hide more)
+#define FME_PXW_WAVES 4
+#endif
 struct PxSmall {
   int16_t win[(kPxSW + 10) * (kPxSW + 10)];
   alignas(16) int16_t key[kPxSW * kPxSW];
@@ -411,7 +414,7 @@ __device__ __forceinline__ void px_wave_costs(const PxSmall& L, int w, int h, in
 }
 
 template <int BD>
-__global__ __launch_bounds__(kPxNT) void k_search_px_wave(BatchArgs a, WorkBufs wb) {
+__global__ __launch_bounds__(kPxNT) __attribute__((amdgpu_waves_per_eu(FME_PXW_WAVES))) void k_search_px_wave(BatchArgs a, WorkBufs wb) {
   __shared__ PxSmall Ls[kPxWaves];
   if (wb.sched->invalid) return;
   constexpr int HR = 14 - BD < 2 ? 2 : 14 - BD, SH1 = 6 - HR, DSH = BD - 8;

@@ -37,6 +37,16 @@ for step in "$@"; do
            run d_k_def_r32w16 200 $B --download-engine kernel --search-reserve 32 --download-wgs 16 && \
            run d_k_imm_r16 200 $B --download-engine kernel --search-reserve 16 --download immediate && \
            run d_blit_def_r16 200 $B --search-reserve 16 ;;
+    dlab3) B="python -u bench.py --no-pi --no-tz --no-mc --no-cpu-baseline --parity-seconds 0 --steps 20"
+           run e_r16 200 $B --search-reserve 16 && run e_r32 200 $B --search-reserve 32 && run e_r64 200 $B --search-reserve 64 && \
+           DEBUG_CLR_LIMIT_BLIT_WG=16 run e_lim16 200 $B && DEBUG_CLR_LIMIT_BLIT_WG=64 run e_lim64 200 $B && \
+           DEBUG_CLR_LIMIT_BLIT_WG=16 run e_lim16_r16 200 $B --search-reserve 16 && \
+           GPU_BLIT_ENGINE_TYPE=1 run e_bet1 200 $B && GPU_BLIT_ENGINE_TYPE=2 run e_bet2 200 $B ;;
+    timeline) run tl 300 rocprofv3 --kernel-trace --memory-copy-trace --output-format csv -d gpurun_out/tl -o run -- python3 bench.py --no-pi --no-tz --no-mc --no-cpu-baseline --parity-seconds 0 --steps 10 --search-reserve 16 ;;
+    pxab) run px4 300 python -u bench.py --workload c3_qp22_main10 --no-cpu-baseline --parity-seconds 0 --steps 10 && \
+          FME_LIB_PATH=$PWD/hm16.9-nn_fme_amd/variants/px6/libfme_amd.so run px6 300 python -u bench.py --workload c3_qp22_main10 --no-cpu-baseline --parity-seconds 0 --steps 10 && \
+          FME_LIB_PATH=$PWD/hm16.9-nn_fme_amd/variants/tz6/libfme_amd.so run tz6 200 python -u tools/tz_probe.py gpurun_out/tz6.npz && \
+          run tz5b 200 python -u tools/tz_probe.py gpurun_out/tz5b.npz ;;
     pmodes) run pm_base 200 python -u tools/parity_debug.py 20 3 8 base && run pm_base10 200 python -u tools/parity_debug.py 6 3 10 base && \
             run pi_tests 400 python -u -m pytest tests -m gpu -k "pred_inter" -x -q -p no:cacheprovider --timeout 300 --timeout-method thread && \
             run pb20 300 python -u bench.py --no-pi --no-tz --no-mc --no-cpu-baseline --steps 20 --parity-seconds 10 && \
