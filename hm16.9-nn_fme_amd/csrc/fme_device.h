@@ -11,6 +11,9 @@
 // 1: k_scatter also copies each job into class order (sjobs) for contiguous reads.  Same search
 // time on the 1080p frame (0.901 against 0.896 ms, profiles/r05_ab.log) for 27.6 MB less written
 // and read per batch.  A build variant for that A/B, not a second path.
+#ifndef FME_LANE_BIGFIRST   // search-kernel tile queues largest class first (k_schedule / k_search_lane)
+#define FME_LANE_BIGFIRST 0
+#endif
 #ifndef FME_SJOBS
 #define FME_SJOBS 0
 #endif

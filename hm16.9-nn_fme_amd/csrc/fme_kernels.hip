@@ -189,9 +189,13 @@ __global__ __launch_bounds__(64) void k_schedule(WorkBufs w, SchedParams p) {
     const int ex = wave_excl_scan(nb);
     if (c <= kNumClasses) sc->prefix[c] = ex;     // [kNumClasses] = the total
   }
+  // FME_LANE_BIGFIRST: each XCD queue lists the classes largest first (queue position l holds
+  // class kNumClasses - 1 - l), so the long tiles start early instead of forming the launch's tail
+  const int nbs = __shfl(nb, c < kNumClasses ? kNumClasses - 1 - c : c);   // every lane takes part
+  const int nbq = FME_LANE_BIGFIRST ? (c < kNumClasses ? nbs : 0) : nb;
 #pragma unroll
   for (int x = 0; x < 8; x++) {
-    const int mine = (nb >> 3) + (x < (nb & 7) ? 1 : 0);
+    const int mine = (nbq >> 3) + (x < (nbq & 7) ? 1 : 0);
     const int ex = wave_excl_scan(mine);
     if (c <= kNumClasses) sc->xq[x][c] = ex;
   }

@@ -1222,9 +1222,10 @@ void k_search_lane(BatchArgs a, WorkBufs w) {
       continue;
     }
     const int nxt_v = claim_v(x);
-    const int c = __popcll(__ballot(lane < kNumClasses && xql <= t)) - 1;
+    const int pos = __popcll(__ballot(lane < kNumClasses && xql <= t)) - 1;   // queue position
+    const int c = FME_LANE_BIGFIRST ? kNumClasses - 1 - pos : pos;
     const int nt = sc->prefix[c + 1] - sc->prefix[c];
-    const int wt = x * (nt >> 3) + min(x, nt & 7) + (t - __builtin_amdgcn_readlane(xql, c));
+    const int wt = x * (nt >> 3) + min(x, nt & 7) + (t - __builtin_amdgcn_readlane(xql, pos));
     switch (c) {
       FME_LANE_CLASSES(FME_CASE)
       default: break;
@@ -1253,11 +1254,12 @@ void k_search_lane(BatchArgs a, WorkBufs w) {
     if (threadIdx.x == 0) nxt = atomicAdd(&ctr[x], 1);
     const int tw = kGroup * t + wid;
     if (tw < len) {
-      int c = 0;
-      while (c < kNumClasses - 1 && tw >= s_xq[x][c + 1]) c++;
+      int pos = 0;   // position in the XCD queue (FME_LANE_BIGFIRST: largest class first)
+      while (pos < kNumClasses - 1 && tw >= s_xq[x][pos + 1]) pos++;
+      const int c = FME_LANE_BIGFIRST ? kNumClasses - 1 - pos : pos;
       const int nt = sc->prefix[c + 1] - sc->prefix[c];
       // wave-uniform: kept in an SGPR, so no VGPR of it lives (and is spilled) across the call
-      const int wt = __builtin_amdgcn_readfirstlane(x * (nt >> 3) + min(x, nt & 7) + (tw - s_xq[x][c]));
+      const int wt = __builtin_amdgcn_readfirstlane(x * (nt >> 3) + min(x, nt & 7) + (tw - s_xq[x][pos]));
       switch (c) {
         FME_LANE_CLASSES(FME_CASE)
         default: break;

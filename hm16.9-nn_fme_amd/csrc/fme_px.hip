@@ -217,21 +217,45 @@ __global__ __launch_bounds__(kPxNT) void k_search_px(BatchArgs a, WorkBufs wb) {
       const PicDesc ref = a.pics[j.ref_id];
       const uint16_t* rl = reinterpret_cast<const uint16_t*>(ref.luma);
       const int x0 = (int)j.x + j.mv_x - 5, y0 = (int)j.y + j.mv_y - 5;
-      for (int e = tid; e < ws * wh; e += kPxNT) {
-        const int r = e / ws, cc = e - r * ws;
-        const int yy = min(max(y0 + r, 0), ref.height - 1), xx = min(max(x0 + cc, 0), ref.width - 1);
-        L.win[e] = (int16_t)rl[(size_t)yy * ref.stride + xx];
+      // every load of a thread issued before the first store (a load-store loop waits out one
+      // memory latency per element); (row, col) stepped by kPxNT elements without divisions
+      constexpr int kWinPer = (kPxMaxWin + kPxNT - 1) / kPxNT, kKeyPer = 64 * 64 / kPxNT;
+      {
+        const int dr = kPxNT / ws, dc = kPxNT - dr * ws;
+        int r = tid / ws, cc = tid - r * ws;
+        int16_t v[kWinPer];
+#pragma unroll
+        for (int t = 0; t < kWinPer; t++) {
+          if (r < wh) {
+            const int yy = min(max(y0 + r, 0), ref.height - 1), xx = min(max(x0 + cc, 0), ref.width - 1);
+            v[t] = (int16_t)rl[(size_t)yy * ref.stride + xx];
+          }
+          cc += dc;
+          r += dr + (cc >= ws ? 1 : 0);
+          cc -= cc >= ws ? ws : 0;
+        }
+#pragma unroll
+        for (int t = 0; t < kWinPer; t++)
+          if (tid + t * kPxNT < ws * wh) L.win[tid + t * kPxNT] = v[t];
       }
-      if (j.key_offset >= 0) {
-        const int16_t* kb = a.keys + j.key_offset;
-        for (int e = tid; e < w * h; e += kPxNT) L.key[e] = kb[e];
-      } else {
+      {
         const PicDesc org = a.pics[j.org_id];
         const uint16_t* ol = reinterpret_cast<const uint16_t*>(org.luma);
-        for (int e = tid; e < w * h; e += kPxNT) {
-          const int r = e / w, cc = e - r * w;
-          L.key[e] = (int16_t)ol[(size_t)(j.y + r) * org.stride + j.x + cc];
+        const int16_t* kb = a.keys + (j.key_offset >= 0 ? j.key_offset : 0);
+        const int dr = kPxNT / w, dc = kPxNT - dr * w;
+        int r = tid / w, cc = tid - r * w;
+        int16_t v[kKeyPer];
+#pragma unroll
+        for (int t = 0; t < kKeyPer; t++) {
+          if (r < h)
+            v[t] = j.key_offset >= 0 ? kb[tid + t * kPxNT] : (int16_t)ol[(size_t)(j.y + r) * org.stride + j.x + cc];
+          cc += dc;
+          r += dr + (cc >= w ? 1 : 0);
+          cc -= cc >= w ? w : 0;
         }
+#pragma unroll
+        for (int t = 0; t < kKeyPer; t++)
+          if (tid + t * kPxNT < w * h) L.key[tid + t * kPxNT] = v[t];
       }
       if (tid < 9) L.e9[tid] = 0;
       if (tid < 18) (&L.cost[0][0])[tid] = 0;
@@ -430,22 +454,37 @@ __global__ __launch_bounds__(kPxNT) __attribute__((amdgpu_waves_per_eu(FME_PXW_W
       const PicDesc ref = a.pics[j.ref_id];
       const uint16_t* rl = reinterpret_cast<const uint16_t*>(ref.luma);
       const int x0 = (int)j.x + j.mv_x - 5, y0 = (int)j.y + j.mv_y - 5;
+      // all of a lane's loads issued before its first store (one memory latency per job, not one
+      // per row): window rows lr, lr + rpp, ... (at most 13), key rows kr, kr + krp, ... (at most 4)
       const int rpp = 64 / ws, lr = lane / ws, lc = lane - lr * ws;
       const int xx = min(max(x0 + lc, 0), ref.width - 1);
-      if (lr < rpp)
-        for (int r = lr; r < wh; r += rpp) {
-          const int yy = min(max(y0 + r, 0), ref.height - 1);
-          L.win[r * ws + lc] = (int16_t)rl[(size_t)yy * ref.stride + xx];
-        }
+      constexpr int kWinRows = (kPxSW + 10 + 1) / 2;   // ws >= 14 -> rpp <= 4; ws = 26 -> rpp = 2
+      int16_t wv[kWinRows];
+#pragma unroll
+      for (int t = 0; t < kWinRows; t++) {
+        const int r = lr + t * rpp;
+        if (lr < rpp && r < wh) wv[t] = (int16_t)rl[(size_t)min(max(y0 + r, 0), ref.height - 1) * ref.stride + xx];
+      }
       const int kr = lane / w, kc = lane - kr * w, krp = 64 / w;
-      if (j.key_offset >= 0) {
-        const int16_t* kb = a.keys + j.key_offset;
-        for (int e = lane; e < w * h; e += 64) L.key[e] = kb[e];
-      } else {
-        const PicDesc org = a.pics[j.org_id];
-        const uint16_t* ol = reinterpret_cast<const uint16_t*>(org.luma);
-        if (kr < krp)
-          for (int r = kr; r < h; r += krp) L.key[r * w + kc] = (int16_t)ol[(size_t)(j.y + r) * org.stride + j.x + kc];
+      const PicDesc org = a.pics[j.org_id];
+      const uint16_t* ol = reinterpret_cast<const uint16_t*>(org.luma);
+      const int16_t* kb = a.keys + (j.key_offset >= 0 ? j.key_offset : 0);
+      int16_t kv4[4];
+#pragma unroll
+      for (int t = 0; t < 4; t++) {
+        const int r = kr + t * krp;
+        if (kr < krp && r < h)
+          kv4[t] = j.key_offset >= 0 ? kb[r * w + kc] : (int16_t)ol[(size_t)(j.y + r) * org.stride + j.x + kc];
+      }
+#pragma unroll
+      for (int t = 0; t < kWinRows; t++) {
+        const int r = lr + t * rpp;
+        if (lr < rpp && r < wh) L.win[r * ws + lc] = wv[t];
+      }
+#pragma unroll
+      for (int t = 0; t < 4; t++) {
+        const int r = kr + t * krp;
+        if (kr < krp && r < h) L.key[r * w + kc] = kv4[t];
       }
     }
     px_wave_sync();

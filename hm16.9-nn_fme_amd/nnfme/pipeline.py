@@ -26,6 +26,7 @@ frame G*F - 4 + s in slot s (s < F + 3), original of frame G*F + j in slot ORG0 
 reference at distance d (the base job's ref_id = d - 1) is slot j + 4 - d, its lambda slot j.
 """
 import ctypes
+import sys
 
 import numpy as np
 
@@ -75,14 +76,18 @@ class _RawEvent:
             raise RuntimeError("hipStreamWaitEvent failed")
 
     def __del__(self):
+        # not at interpreter exit: the HIP runtime may already be torn down (a profiler's exit
+        # handlers run first), and the process frees its events anyway
+        if sys.is_finalizing() or not self.cuda_event or _hip is None:
+            return
         try:
-            if self.cuda_event and _hip is not None:
-                _hip.hipEventDestroy(self.cuda_event)
+            _hip.hipEventDestroy(self.cuda_event)
         except Exception:
             pass
 
 
 H2D, D2H = 1, 2
+D2D_NOCU = 1024   # hipMemcpyDeviceToDeviceNoCU: the runtime's copy engines instead of a blit kernel
 
 
 def torch_current_stream(t):
@@ -138,7 +143,8 @@ class FrameReplay:
         (fme_build_bipred_keys_device), so the keys are per-frame work inside the timed step.
         nn_rows (uint32 [n][9]): the NN input rows of the frame's FME_JOB_NN_IN jobs (the backups'
         input path); each step uploads them with its jobs and binds them (fme_set_nn_inputs).
-        download_engine: "kernel" (fme_download_device: the library's copy kernel of
+        download_engine: "sdma" (hipMemcpyDeviceToDeviceNoCU into the pinned rows: a copy engine),
+        "kernel" (fme_download_device: the library's copy kernel of
         download_wgs workgroups of 256 lanes, which hold a few wave slots beside the next step's
         search) or "blit" (hipMemcpyAsync, which this ROCm runs as a blit kernel of hundreds of
         workgroups that take the search kernel's CUs).  search_reserve: resident search workgroups
@@ -195,13 +201,15 @@ class FrameReplay:
         # step k's results are downloaded once step k+1's search runs (see issue())
         self.ev_search = [_RawEvent() for _ in range(n_steps)]
         self.defer_download = defer_download
-        if download_engine not in ("kernel", "blit"):
+        if download_engine not in ("kernel", "blit", "sdma"):
             raise ValueError(f"download_engine {download_engine!r}")
         self.download_engine, self.download_wgs = download_engine, int(download_wgs)
         ctx.set_search_reserve(int(search_reserve))   # slots the search leaves to the download kernel
         ctx.set_search_event(None)                # set per step in issue()
         self.pending = None                       # step whose download is not issued yet
         self.fixed_jobs = 0
+        self.last_prefix = 0                      # longest carried-state prefix finish() re-ran
+        self.r_out = {}
 
     def first_frame(self, k):
         """First frame of this rank's step k."""
@@ -392,6 +400,8 @@ class FrameReplay:
         if self.download_engine == "kernel":
             self.ctx.download_device(self.d_out[k & 1].data_ptr(), self.h_out[k].data_ptr(), self.h_out.shape[1],
                                      self.download_wgs, dn.cuda_stream)
+        elif self.download_engine == "sdma":   # hipMemcpyDeviceToDeviceNoCU: a copy engine, no CUs
+            _memcpy_async(self.h_out[k], self.d_out[k & 1], self.h_out.shape[1], D2D_NOCU, dn)
         else:
             _memcpy_async(self.h_out[k], self.d_out[k & 1], self.h_out.shape[1], D2H, dn)
         self.ev_out[k].record(dn)
@@ -418,6 +428,63 @@ class FrameReplay:
     def results(self, k):
         return self.h_out[k].numpy().view(MV_RESULT_DTYPE)
 
+    # -- the HBM-resident run (bench.py's `value`) -------------------------------------------------
+    # Steps replayed with every input already in HBM (the pipelined pass uploaded and, when
+    # sharded, exchanged them into per-step buffers) and the results left there: one device
+    # buffer per step, since a sharded run re-runs each step's carried-state prefix at the end.
+    def resident_outputs(self, k0, k1):
+        torch = self.torch
+        dev = self.d_out[0].device
+        self.r_out = {k: torch.empty(self.n * MV_RESULT_DTYPE.itemsize, dtype=torch.uint8, device=dev)
+                      for k in range(k0, k1)}
+
+    def _resident_batch(self, k, n):
+        ctx, comp = self.ctx, self.s_comp
+        b = k & 1
+        self._bind(k)
+        if self.kreqs is not None:   # this step's keys, built on the device from its pictures
+            ctx.build_bipred_keys_device(self.d_kreqs[b].data_ptr(), len(self.kreqs), self.key_count * self.F,
+                                         comp.cuda_stream)
+        ctx.refine_mv_device(self.d_jobs[b].data_ptr(), self.r_out[k].data_ptr(), n, comp.cuda_stream)
+
+    def issue_resident(self, k):
+        """Step k from HBM-resident inputs into r_out[k] (no copy, no host wait)."""
+        ctx, comp = self.ctx, self.s_comp
+        ctx.set_search_event(None)
+        if self.world > 1:
+            ctx.nn_reset()                                 # stream-ordered: this batch starts fresh
+        self._resident_batch(k, self.n)
+        if self.world > 1:
+            ctx.nn_copy_state_device(self.states[k].data_ptr(), comp.cuda_stream)
+
+    def finish_resident(self, k0, k1, prefix):
+        """Sharded: all-gather the steps' end states, chain them in encode order and re-run each
+        step's carried-state prefix (`prefix` jobs, the same for every step of a replay: see
+        finish()) with its true carry-in, on the device.  Returns the number of re-run jobs."""
+        if self.world == 1 or prefix <= 0:
+            return 0
+        import torch.distributed as dist
+        torch = self.torch
+        self.s_comp.synchronize()
+        st = self.states if dist.get_backend(self.group) != "gloo" else self.states.cpu()
+        gathered = [torch.zeros_like(st) for _ in range(self.world)]
+        dist.all_gather(gathered, st, group=self.group)
+        bs = np.zeros((self.steps * self.world, 12), np.uint32)
+        for r in range(self.world):
+            g = gathered[r].cpu().numpy().view(np.uint32)
+            for k in range(self.steps):
+                bs[k * self.world + r] = g[k]
+        carries, _ = fdist.chain_states(bs)
+        fixed = 0
+        for k in range(k0, k1):
+            carry = carries[k * self.world + self.rank]
+            if not int(carry[11]):
+                continue
+            self.ctx.nn_set_state(carry)
+            self._resident_batch(k, prefix)
+            fixed += prefix
+        return fixed
+
     # -- end of the run -----------------------------------------------------------------------
     def finish(self, first_step=0):
         """Wait for every step; when sharded, chain the NN states and refine each batch's
@@ -441,6 +508,7 @@ class FrameReplay:
         for k in range(first_step, self.steps):
             out = self.results(k)
             p = fdist.uninit_prefix(out)
+            self.last_prefix = max(self.last_prefix, p)
             carry = carries[k * self.world + self.rank]
             if p == 0 or not int(carry[11]):
                 continue

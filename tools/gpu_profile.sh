@@ -17,13 +17,14 @@ run() {  # name, timeout, command...
   if [ $rc -ne 0 ]; then echo "== $name FAILED rc=$rc"; tail -30 "$O/$name.log"; exit $rc; fi
 }
 B="python bench.py --no-cpu-baseline --no-pi --no-tz --no-mc"
+P="python3 bench.py --no-cpu-baseline --no-pi --no-tz --no-mc --no-pcie --parity-seconds 0"   # profiled: kernels alone
 if [ "${PROF:-1}" = 1 ]; then
-  run trace 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/trace -o run -- $B --steps 10 --warmup 2
-  run pmc_fetch 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/pmc/fetch -o run -- $B --steps 2 --warmup 1
-  run pmc_write 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/pmc/write -o run -- $B --steps 2 --warmup 1
+  run trace 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/trace -o run -- $P --steps 10 --warmup 2
+  run pmc_fetch 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/pmc/fetch -o run -- $P --steps 2 --warmup 1
+  run pmc_write 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/pmc/write -o run -- $P --steps 2 --warmup 1
   python3 tools/pmc_traffic.py $O/pmc $O/pmc_traffic.json > /dev/null
-  run sq_n 150 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_LDS SQ_WAVES GRBM_GUI_ACTIVE --output-format csv -d $O/sq/n -o run -- $B --steps 2 --warmup 1
-  run sq_o 150 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_VMEM --output-format csv -d $O/sq/o -o run -- $B --steps 2 --warmup 1
+  run sq_n 150 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_LDS SQ_WAVES GRBM_GUI_ACTIVE --output-format csv -d $O/sq/n -o run -- $P --steps 2 --warmup 1
+  run sq_o 150 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_VMEM --output-format csv -d $O/sq/o -o run -- $P --steps 2 --warmup 1
   python3 tools/pmc_summary.py $O/sq > $O/sq_summary.txt
 fi
 if [ "${WORKLOADS:-1}" = 1 ]; then

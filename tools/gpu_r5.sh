@@ -42,11 +42,22 @@ for step in "$@"; do
            DEBUG_CLR_LIMIT_BLIT_WG=16 run e_lim16 200 $B && DEBUG_CLR_LIMIT_BLIT_WG=64 run e_lim64 200 $B && \
            DEBUG_CLR_LIMIT_BLIT_WG=16 run e_lim16_r16 200 $B --search-reserve 16 && \
            GPU_BLIT_ENGINE_TYPE=1 run e_bet1 200 $B && GPU_BLIT_ENGINE_TYPE=2 run e_bet2 200 $B ;;
-    timeline) run tl 300 rocprofv3 --kernel-trace --memory-copy-trace --output-format csv -d gpurun_out/tl -o run -- python3 bench.py --no-pi --no-tz --no-mc --no-cpu-baseline --parity-seconds 0 --steps 10 --search-reserve 16 ;;
-    pxab) run px4 300 python -u bench.py --workload c3_qp22_main10 --no-cpu-baseline --parity-seconds 0 --steps 10 && \
+    timeline) run tl 300 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/tl -o run -- python3 bench.py --no-pi --no-tz --no-mc --no-cpu-baseline --parity-seconds 0 --steps 10 --search-reserve 16 && \
+              bash tools/gpu_r5.sh dlab4 deepsq ;;
+    pxab) run m10t 300 python -u -m pytest tests/test_gpu_main10.py -m gpu -x -q -p no:cacheprovider --timeout 200 --timeout-method thread && \
+          run px4 300 python -u bench.py --workload c3_qp22_main10 --no-cpu-baseline --parity-seconds 0 --steps 10 && \
           FME_LIB_PATH=$PWD/hm16.9-nn_fme_amd/variants/px6/libfme_amd.so run px6 300 python -u bench.py --workload c3_qp22_main10 --no-cpu-baseline --parity-seconds 0 --steps 10 && \
           FME_LIB_PATH=$PWD/hm16.9-nn_fme_amd/variants/tz6/libfme_amd.so run tz6 200 python -u tools/tz_probe.py gpurun_out/tz6.npz && \
           run tz5b 200 python -u tools/tz_probe.py gpurun_out/tz5b.npz ;;
+    deepsq) run deepsq 200 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_VALU SQ_INSTS_LDS SQ_WAIT_ANY SQ_WAVE_CYCLES SQ_ACTIVE_INST_ANY SQ_WAVES GRBM_GUI_ACTIVE --output-format csv -d gpurun_out/deepsq -o run -- python3 bench.py --workload c5 --no-cpu-baseline --parity-seconds 0 --steps 3 --warmup 1 && \
+            python3 tools/pmc_summary.py gpurun_out/deepsq > gpurun_out/deepsq_summary.txt && grep -A9 "deep_tail" gpurun_out/deepsq_summary.txt ;;
+    dlab4) B="python -u bench.py --no-pi --no-tz --no-mc --no-cpu-baseline --steps 20"
+           run s_sdma 200 $B --download-engine sdma --parity-seconds 5 && run s_sdma_r16 200 $B --download-engine sdma --search-reserve 16 --parity-seconds 0 && \
+           run s_blit 200 $B --parity-seconds 0 && run s_blit_r16 200 $B --search-reserve 16 --parity-seconds 0 && \
+           run s_sdma_imm 200 $B --download-engine sdma --download immediate --parity-seconds 0 ;;
+    bigab) run bigab 400 python -u tools/ab_bench.py . variants/big --rounds 4 && bash tools/gpu_r5.sh bench1 bench2 ;;
+    bench1) run bench1 300 python -u bench.py --no-pi --no-tz --no-mc --cpu-seconds 3 --parity-seconds 10 ;;
+    bench2) run bench2 300 python -u -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --steps 6 --warmup 2 --no-pi --no-tz --no-mc --no-cpu-baseline --parity-seconds 0 --dist-backend gloo ;;
     pmodes) run pm_base 200 python -u tools/parity_debug.py 20 3 8 base && run pm_base10 200 python -u tools/parity_debug.py 6 3 10 base && \
             run pi_tests 400 python -u -m pytest tests -m gpu -k "pred_inter" -x -q -p no:cacheprovider --timeout 300 --timeout-method thread && \
             run pb20 300 python -u bench.py --no-pi --no-tz --no-mc --no-cpu-baseline --steps 20 --parity-seconds 10 && \

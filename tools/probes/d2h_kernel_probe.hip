@@ -3,6 +3,7 @@
 // fme_mv_result rows).  Standalone (nothing else runs).
 #include <hip/hip_runtime.h>
 #include <cstdio>
+#include <cstring>
 #include <cstdint>
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
@@ -39,6 +40,34 @@ int main() {
   };
   float ms = timeit([&] { (void)hipMemcpyAsync(h, d, bytes, hipMemcpyDeviceToHost, 0); });
   printf("hipMemcpyAsync D2H: %.3f ms (%.1f GB/s)\n", ms, bytes / ms / 1e6);
+  {   // host -> device, the replay's per-step upload size (jobs + two pictures)
+    const size_t ub = 31700000 / 16 * 16;
+    void *du, *hu;
+    if (hipMalloc(&du, ub) != hipSuccess || hipHostMalloc(&hu, ub, 0) != hipSuccess) return 1;
+    memset(hu, 3, ub);
+    float mu = timeit([&] { (void)hipMemcpyAsync(du, hu, ub, hipMemcpyHostToDevice, 0); });
+    printf("hipMemcpyAsync H2D %.1f MB: %.3f ms (%.1f GB/s)\n", ub / 1e6, mu, ub / mu / 1e6);
+    hipStream_t s2;
+    (void)hipStreamCreate(&s2);
+    hipEvent_t a0, a1, b0, b1;
+    (void)hipEventCreate(&a0); (void)hipEventCreate(&a1); (void)hipEventCreate(&b0); (void)hipEventCreate(&b1);
+    (void)hipDeviceSynchronize();
+    (void)hipEventRecord(a0, 0);
+    (void)hipEventRecord(b0, s2);
+    for (int r = 0; r < 10; r++) {
+      (void)hipMemcpyAsync(du, hu, ub, hipMemcpyHostToDevice, 0);
+      (void)hipMemcpyAsync(h, d, bytes, hipMemcpyDeviceToHost, s2);
+    }
+    (void)hipEventRecord(a1, 0);
+    (void)hipEventRecord(b1, s2);
+    (void)hipDeviceSynchronize();
+    float ma = 0, mb = 0;
+    (void)hipEventElapsedTime(&ma, a0, a1);
+    (void)hipEventElapsedTime(&mb, b0, b1);
+    printf("concurrent H2D %.1f MB + D2H %.1f MB on two streams: %.3f / %.3f ms per pair\n", ub / 1e6, bytes / 1e6, ma / 10, mb / 10);
+    (void)hipFree(du);
+    (void)hipHostFree(hu);
+  }
   const int wgs[] = {8, 16, 32, 64, 128, 256, 512, 1024};
   const int thr[] = {64, 256};
   const char* names[] = {"plain", "nt", "sc0sc1"};
