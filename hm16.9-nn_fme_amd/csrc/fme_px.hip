@@ -409,7 +409,7 @@ __global__ __launch_bounds__(kPxNT) void k_search_px(BatchArgs a, WorkBufs wb) {
 // (every lane holds every total), so the EMI decision and the candidate picks run on all lanes.
 constexpr int kPxSW = 16;                                   // largest side of the wave kernel's PUs
 #ifndef FME_PXW_WAVES   // waves per SIMD of the wave kernel (latency-bound: more waves hide more)
-#define FME_PXW_WAVES 4
+#define FME_PXW_WAVES 6
 #endif
 struct PxSmall {
   int16_t win[(kPxSW + 10) * (kPxSW + 10)];

@@ -55,6 +55,9 @@ for step in "$@"; do
            run s_sdma 200 $B --download-engine sdma --parity-seconds 5 && run s_sdma_r16 200 $B --download-engine sdma --search-reserve 16 --parity-seconds 0 && \
            run s_blit 200 $B --parity-seconds 0 && run s_blit_r16 200 $B --search-reserve 16 --parity-seconds 0 && \
            run s_sdma_imm 200 $B --download-engine sdma --download immediate --parity-seconds 0 ;;
+    pxab2) B="python -u bench.py --workload c3_qp22_main10 --no-cpu-baseline --parity-seconds 0 --steps 10"
+           run px6d 300 $B && FME_LIB_PATH=$PWD/hm16.9-nn_fme_amd/variants/px5/libfme_amd.so run px5 300 $B && \
+           FME_LIB_PATH=$PWD/hm16.9-nn_fme_amd/variants/px8/libfme_amd.so run px8 300 $B && run px6p 300 $B --parity-seconds 10 ;;
     bigab) run bigab 400 python -u tools/ab_bench.py . variants/big --rounds 4 && bash tools/gpu_r5.sh bench1 bench2 ;;
     bench1) run bench1 300 python -u bench.py --no-pi --no-tz --no-mc --cpu-seconds 3 --parity-seconds 10 ;;
     bench2) run bench2 300 python -u -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --steps 6 --warmup 2 --no-pi --no-tz --no-mc --no-cpu-baseline --parity-seconds 0 --dist-backend gloo ;;

@@ -47,24 +47,29 @@ int main() {
     memset(hu, 3, ub);
     float mu = timeit([&] { (void)hipMemcpyAsync(du, hu, ub, hipMemcpyHostToDevice, 0); });
     printf("hipMemcpyAsync H2D %.1f MB: %.3f ms (%.1f GB/s)\n", ub / 1e6, mu, ub / mu / 1e6);
-    hipStream_t s2;
-    (void)hipStreamCreate(&s2);
+    hipStream_t s1, s2;
+    (void)hipStreamCreateWithFlags(&s1, hipStreamNonBlocking);
+    (void)hipStreamCreateWithFlags(&s2, hipStreamNonBlocking);
     hipEvent_t a0, a1, b0, b1;
     (void)hipEventCreate(&a0); (void)hipEventCreate(&a1); (void)hipEventCreate(&b0); (void)hipEventCreate(&b1);
-    (void)hipDeviceSynchronize();
-    (void)hipEventRecord(a0, 0);
-    (void)hipEventRecord(b0, s2);
-    for (int r = 0; r < 10; r++) {
-      (void)hipMemcpyAsync(du, hu, ub, hipMemcpyHostToDevice, 0);
-      (void)hipMemcpyAsync(h, d, bytes, hipMemcpyDeviceToHost, s2);
+    for (int mode = 0; mode < 2; mode++) {   // 0: both directions on one stream (serial), 1: two streams
+      hipStream_t sd = mode ? s2 : s1;
+      (void)hipDeviceSynchronize();
+      (void)hipEventRecord(a0, s1);
+      (void)hipEventRecord(b0, sd);
+      for (int r = 0; r < 10; r++) {
+        (void)hipMemcpyAsync(du, hu, ub, hipMemcpyHostToDevice, s1);
+        (void)hipMemcpyAsync(h, d, bytes, hipMemcpyDeviceToHost, sd);
+      }
+      (void)hipEventRecord(a1, s1);
+      (void)hipEventRecord(b1, sd);
+      (void)hipDeviceSynchronize();
+      float ma = 0, mb = 0;
+      (void)hipEventElapsedTime(&ma, a0, a1);
+      (void)hipEventElapsedTime(&mb, b0, b1);
+      printf("%s H2D %.1f MB + D2H %.1f MB: %.3f / %.3f ms per pair\n", mode ? "two non-blocking streams" : "one stream, serial",
+             ub / 1e6, bytes / 1e6, ma / 10, mb / 10);
     }
-    (void)hipEventRecord(a1, 0);
-    (void)hipEventRecord(b1, s2);
-    (void)hipDeviceSynchronize();
-    float ma = 0, mb = 0;
-    (void)hipEventElapsedTime(&ma, a0, a1);
-    (void)hipEventElapsedTime(&mb, b0, b1);
-    printf("concurrent H2D %.1f MB + D2H %.1f MB on two streams: %.3f / %.3f ms per pair\n", ub / 1e6, bytes / 1e6, ma / 10, mb / 10);
     (void)hipFree(du);
     (void)hipHostFree(hu);
   }
