@@ -295,6 +295,8 @@ def parity_leg(rep, wl, net, step, state, seconds, max_jobs=0):
     if nn == 2 and wl.get("engine"):
         out["note"] = ("MFMA engine: FMA-chain rounding, not bit-exact by construction (DESIGN.md §3); "
                        "a mismatch is a near-tie class")
+        out["agreement"] = 1.0 - mism / max(done, 1)
+        out["tolerance"] = ">= 0.995 of jobs equal (tests/test_deep_nn.py)"
     return out
 
 
@@ -815,7 +817,8 @@ def main():
     parity = None
     if rank == 0 and world == 1 and args.parity_seconds > 0 and not args.no_pcie:
         parity = parity_leg(rep, wl, net, args.warmup, state0, args.parity_seconds)
-        if parity.get("mismatches"):   # localise: the library's host path on the same bindings
+        mfma = wl["nn"] == 2 and bool(wl.get("engine"))
+        if parity.get("mismatches") and not mfma and rep.rows is None:   # localise: the host path, same bindings
             parity["host_path_check"] = host_path_check(ctx, rep, wl, args.warmup, state0, net, BD)
             now = rep.results(args.warmup)
             parity["rows_changed_since_timed_region"] = int((now != snap).sum())

@@ -206,6 +206,8 @@ struct fme_ctx {
   DevBuf<BiKeyTask> d_bikey;
   DevBuf<int32_t> d_key_invalid;  // invalid requests of the last fme_build_bipred_keys_device
   DevBuf<int32_t> d_ch_i32;     // k_tz_level: psrc
+  DevBuf<int32_t> d_tzp;        // staged integer search: 8 counters, then cnt / cursor / off / seg (TzPairs)
+  DevBuf<int32_t> d_tzp_perm;   // [n] jobs grouped by (kernel, reference, CTU)
   // fme_pred_inter_p scratch, kept across calls: pinned transfer buffers, host arrays, the
   // level-ordered device copies of the jobs
   HostBuf<AmvpTask> h_pi_tasks;
@@ -945,12 +947,51 @@ static int tz_run(fme_ctx* c, fme_job* d_jobs, const fme_tz_ext* d_ext, uint32_t
   if (!c->ev_fork) HIP_TRY(hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming));
   if (!c->ev_join) HIP_TRY(hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming));
   if (!c->ev_join2) HIP_TRY(hipEventCreateWithFlags(&c->ev_join2, hipEventDisableTiming));
-  HIP_TRY(hipEventRecord(c->ev_fork, s));
-  HIP_TRY(hipStreamWaitEvent(c->aux, c->ev_fork, 0));
-  HIP_TRY(hipStreamWaitEvent(c->aux2, c->ev_fork, 0));
-  HIP_TRY(launch_tz_wave(ta, sc, 0, keyed, c->aux));
-  HIP_TRY(launch_tz_wave(ta, sc, 1, keyed, c->aux2));
-  HIP_TRY(launch_tz_wave(ta, sc, 2, keyed, s));
+  // the staged form (FME_TZ_STAGE): PUs grouped by (kernel, reference, CTU) on the device, each
+  // group's search area read into LDS once (fme_tz.hip k_tz_staged)
+  int cw = 0, ch = 0;
+  for (const PicDesc& p : c->pics)
+    if (p.luma) {
+      cw = std::max(cw, (p.width + 63) / 64);
+      ch = std::max(ch, (p.height + 63) / 64);
+    }
+  const long long np = (long long)FME_MAX_PICTURES * cw * ch;
+  if (FME_TZ_STAGE && np > 0 && np <= (1LL << 20)) {
+    const size_t words = 8 + 12 * (size_t)np;
+    if (c->d_tzp.cap < words || c->d_tzp_perm.cap < (size_t)n) {
+      HIP_TRY(hipDeviceSynchronize());   // no launch of an earlier call still reads the old buffers
+      HIP_TRY(c->d_tzp.reserve(words));
+      HIP_TRY(c->d_tzp_perm.reserve(n));
+    }
+    TzPairs tp{};
+    int32_t* b = c->d_tzp.p;
+    tp.nseg = b;
+    tp.claim = b + 3;
+    tp.cnt = b + 8;
+    tp.cursor = tp.cnt + 3 * np;
+    tp.off = tp.cursor + 3 * np;
+    tp.seg = tp.off + 3 * np;
+    tp.perm = c->d_tzp_perm.p;
+    tp.np = (int32_t)np;
+    tp.cw = cw;
+    tp.ch = ch;
+    HIP_TRY(hipMemsetAsync(b, 0, (8 + 3 * (size_t)np) * sizeof(int32_t), s));
+    HIP_TRY(launch_tz_pairs(ta, tp, w.cls, n, s));
+    HIP_TRY(hipEventRecord(c->ev_fork, s));
+    HIP_TRY(hipStreamWaitEvent(c->aux, c->ev_fork, 0));
+    HIP_TRY(hipStreamWaitEvent(c->aux2, c->ev_fork, 0));
+    const int wgs = 3 * cu_count(c->device);   // persistent: three tiles' LDS per CU
+    HIP_TRY(launch_tz_staged(ta, tp, 0, keyed, wgs, c->aux));
+    HIP_TRY(launch_tz_staged(ta, tp, 1, keyed, wgs, c->aux2));
+    HIP_TRY(launch_tz_staged(ta, tp, 2, keyed, wgs, s));
+  } else {
+    HIP_TRY(hipEventRecord(c->ev_fork, s));
+    HIP_TRY(hipStreamWaitEvent(c->aux, c->ev_fork, 0));
+    HIP_TRY(hipStreamWaitEvent(c->aux2, c->ev_fork, 0));
+    HIP_TRY(launch_tz_wave(ta, sc, 0, keyed, c->aux));
+    HIP_TRY(launch_tz_wave(ta, sc, 1, keyed, c->aux2));
+    HIP_TRY(launch_tz_wave(ta, sc, 2, keyed, s));
+  }
   HIP_TRY(hipEventRecord(c->ev_join, c->aux));
   HIP_TRY(hipEventRecord(c->ev_join2, c->aux2));
   HIP_TRY(hipStreamWaitEvent(s, c->ev_join, 0));

@@ -11,11 +11,20 @@
 // 1: k_scatter also copies each job into class order (sjobs) for contiguous reads.  Same search
 // time on the 1080p frame (0.901 against 0.896 ms, profiles/r05_ab.log) for 27.6 MB less written
 // and read per batch.  A build variant for that A/B, not a second path.
-#ifndef FME_LANE_BIGFIRST   // search-kernel tile queues largest class first (k_schedule / k_search_lane)
-#define FME_LANE_BIGFIRST 0
-#endif
 #ifndef FME_SJOBS
 #define FME_SJOBS 0
+#endif
+// 1: the bulk integer search stages each (kernel, reference, CTU) group's search area in LDS
+// (fme_tz.hip k_tz_staged); 0: one wave per PU straight from the class order (k_tz_wave)
+#ifndef FME_TZ_STAGE
+#define FME_TZ_STAGE 1
+#endif
+// Sub-bands per XCD queue of the search kernel (Schedule::xq): the XCD searches its spatial band
+// of the frame in this many consecutive strips, every class of a strip before the next strip, so
+// the jobs' lines and the reference windows a strip's PU classes share stay in the XCD's L2.
+// 1 = the round-4 order (each XCD's band class by class).
+#ifndef FME_LANE_SUBBANDS
+#define FME_LANE_SUBBANDS 8
 #endif
 
 namespace fme {
@@ -136,10 +145,12 @@ struct Schedule {
   int32_t prefix[kNumClasses + 1];
   int32_t class_off[kNumClasses];
   int32_t class_cnt[kNumClasses];
-  // The lane kernel's per-XCD tile queues: XCD x owns the x-th contiguous eighth of every
-  // class's wave tiles; its queue lists them class by class, xq[x][c] = its tiles before class c
-  // (xq[x][kNumClasses] = queue length).
-  int32_t xq[8][kNumClasses + 1];
+  // The lane kernel's per-XCD tile queues.  Every class's wave tiles are split into 8 S
+  // contiguous bands (S = FME_LANE_SUBBANDS; band B holds tiles [nt B / 8S, nt (B+1) / 8S) of a
+  // class with nt tiles), XCD x owns bands x S .. x S + S - 1, and its queue lists them band by
+  // band, class by class inside a band: xq[x][s][c] = the queue's tiles before (band x S + s,
+  // class c); xq[x][s][kNumClasses] = before band s + 1 (xq[x][S-1][kNumClasses] = its length).
+  int32_t xq[8][FME_LANE_SUBBANDS][kNumClasses + 1];
   int32_t invalid;            // jobs rejected by k_classify (the whole batch is then skipped)
   int32_t pad_[3];
 };
@@ -173,6 +184,20 @@ struct TzSchedule {
 // keyed: some job of the batch reads a key block (bi-pred): the kernels that hold int16 keys;
 // otherwise the uni-pred form, whose key rows take half the registers
 hipError_t launch_tz_wave(const TzArgs& ta, const TzSchedule& sc, int kid, bool keyed, hipStream_t s);   // prefix in waves
+// The staged bulk search's groups (fme_tz.hip k_tz_staged): PUs by (unit-shape kernel kid,
+// reference picture, CTU), np = FME_MAX_PICTURES * cw * ch groups per kernel.
+struct TzPairs {
+  int32_t* cnt;      // [3 np] PUs per group (zeroed before launch_tz_pairs)
+  int32_t* cursor;   // [3 np]
+  int32_t* off;      // [3 np] first position of each group in perm
+  int32_t* seg;      // [3][np] non-empty groups of each kernel
+  int32_t* nseg;     // [3] their counts (zeroed)
+  int32_t* claim;    // [3] group claim counters (zeroed)
+  int32_t* perm;     // [n] jobs grouped
+  int32_t np, cw, ch;
+};
+hipError_t launch_tz_pairs(const TzArgs& ta, const TzPairs& tp, const uint8_t* cls, int n, hipStream_t s);
+hipError_t launch_tz_staged(const TzArgs& ta, const TzPairs& tp, int kid, bool keyed, int workgroups, hipStream_t s);
 // The dependency levels of a producer's m_integerMv2Nx2N chain (fme_tz.hip k_tz_level): jobs in
 // level order, level l = jobs [lvl_off[l], lvl_off[l+1]), one launch per level, back to back.
 struct TzChain {

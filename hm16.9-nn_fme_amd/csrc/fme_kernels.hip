@@ -189,15 +189,20 @@ __global__ __launch_bounds__(64) void k_schedule(WorkBufs w, SchedParams p) {
     const int ex = wave_excl_scan(nb);
     if (c <= kNumClasses) sc->prefix[c] = ex;     // [kNumClasses] = the total
   }
-  // FME_LANE_BIGFIRST: each XCD queue lists the classes largest first (queue position l holds
-  // class kNumClasses - 1 - l), so the long tiles start early instead of forming the launch's tail
-  const int nbs = __shfl(nb, c < kNumClasses ? kNumClasses - 1 - c : c);   // every lane takes part
-  const int nbq = FME_LANE_BIGFIRST ? (c < kNumClasses ? nbs : 0) : nb;
-#pragma unroll
+  // per-XCD queues of bands (Schedule::xq): band B of class c = its tiles [nb B / 8S, nb (B+1) / 8S)
+  constexpr int S = FME_LANE_SUBBANDS;
+  auto band_lo = [&](int B) { return (int)(((long long)nb * B) / (8 * S)); };
+#pragma unroll 1
   for (int x = 0; x < 8; x++) {
-    const int mine = (nbq >> 3) + (x < (nbq & 7) ? 1 : 0);
-    const int ex = wave_excl_scan(mine);
-    if (c <= kNumClasses) sc->xq[x][c] = ex;
+    int run = 0;
+#pragma unroll 1
+    for (int q = 0; q < S; q++) {
+      const int B = x * S + q;
+      const int mine = c < kNumClasses ? band_lo(B + 1) - band_lo(B) : 0;
+      const int ex = run + wave_excl_scan(mine);
+      if (c <= kNumClasses) sc->xq[x][q][c] = ex;
+      run = __shfl(ex, kNumClasses);
+    }
   }
   if (c == 0) sc->invalid = inv;
 }

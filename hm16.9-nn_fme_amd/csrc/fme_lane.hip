@@ -1169,70 +1169,33 @@ __device__ __forceinline__ int xcc_id() {
 // One kernel serves every lane class.  A workgroup claims four consecutive 64-lane wave tiles
 // (one per wave; a tile holds 64 / L PUs of one class) per atomic from its XCD's queue
 // (Schedule::xq: the XCD's contiguous eighth of every class's tiles = one spatial band of the
-// CTU-ordered job stream, so each L2 sees one band, and the four waves of a CU search neighbouring
-// PUs whose reference windows share L1 lines), then from the other XCDs' queues.  The next claim
-// is issued before the current tiles are searched.  The grid is sized to fill the chip, not to
-// the (device-computed) tile count, so the host never waits for the class histogram.
+// CTU-ordered job stream, so each L2 sees one band, searched strip by strip with every class of a
+// strip together, and the four waves of a CU search neighbouring PUs whose reference windows share
+// L1 lines), then from the other XCDs' queues.  The next claim is issued before the current tiles
+// are searched.  The grid is sized to fill the chip, not to the (device-computed) tile count, so
+// the host never waits for the class histogram.
 // Measured (1080p frame, tools/ab_bench.py): per-wave claims 1.48 ms, four tiles per workgroup
-// 1.21 ms, eight 1.24, sixteen 1.29; without the XCD queues 1.25.
+// 1.21 ms, eight 1.24, sixteen 1.29; without the XCD queues 1.25 (the per-wave claim form was
+// kept as a build option until round 5 and removed unused).
 #define FME_CASE(ID, PW_, PH_, UW_, UH_)                                                             \
   case ID:                                                                                           \
     lane_unit<PW_, PH_, UW_, UH_>(a, w.sjobs, w.perm, sc->class_off[ID], sc->class_cnt[ID], wt, wid); \
     break;
-#ifndef FME_LANE_WAVE_CLAIMS   // 1: each wave claims its own tiles (no workgroup barrier per claim)
-#define FME_LANE_WAVE_CLAIMS 0
-#endif
 __global__ __launch_bounds__(kLaneNT) __attribute__((amdgpu_waves_per_eu(FME_LANE_WAVES)))
 void k_search_lane(BatchArgs a, WorkBufs w) {
+  constexpr int S = FME_LANE_SUBBANDS;
   const Schedule* __restrict__ sc = w.sched;
   int32_t* ctr = w.tile_ctr;
-  __shared__ int32_t s_xq[8][kNumClasses + 1];
+  __shared__ int32_t s_xq[8][S][kNumClasses + 1];
   {   // the batch's tables and the XCD queues, once per workgroup
     const uint32_t* ps = reinterpret_cast<const uint32_t*>(a.pics);
     uint32_t* pd = reinterpret_cast<uint32_t*>(g_pics);
     for (int i = threadIdx.x; i < (int)(sizeof(g_pics) / 4); i += kLaneNT) pd[i] = ps[i];
     for (int i = threadIdx.x; i < FME_MAX_LAMBDAS * kCostBits; i += kLaneNT)
       g_cost[i / kCostBits][i % kCostBits] = simd::mv_cost(a.mlambda[i / kCostBits], (uint32_t)(i % kCostBits));
-    for (int i = threadIdx.x; i < 8 * (kNumClasses + 1); i += kLaneNT) (&s_xq[0][0])[i] = (&sc->xq[0][0])[i];
+    for (int i = threadIdx.x; i < 8 * S * (kNumClasses + 1); i += kLaneNT) (&s_xq[0][0][0])[i] = (&sc->xq[0][0][0])[i];
   }
-  const int home = xcc_id(), wid = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6), lane = __lane_id();
-#if FME_LANE_WAVE_CLAIMS
-  __syncthreads();
-  // Each wave claims one tile at a time from its XCD's queue, the next claim issued before the
-  // current tile is searched (its latency hides behind the tile), then drains the other XCDs'.
-  // The class of tile t is the number of class starts xq[x][c] <= t, less one: a ballot over the
-  // queue's 25 boundaries held one per lane.
-  auto claim_v = [&](int xx) FME_AI {   // the claimed index in lane 0 (read after the tile)
-    int v = 0;
-    if (lane == 0) v = atomicAdd(&ctr[xx], 1);
-    return v;
-  };
-  auto claim = [&](int xx) FME_AI { return __builtin_amdgcn_readfirstlane(claim_v(xx)); };
-  int x = home, tried = 0;
-  int xql = lane <= kNumClasses ? s_xq[x][lane] : 0x7FFFFFFF;
-  int len = __builtin_amdgcn_readlane(xql, kNumClasses);
-  int t = claim(x);
-  while (true) {
-    if (t >= len) {   // queue drained: the next XCD's
-      if (++tried == 8) break;
-      x = (home + tried) & 7;
-      xql = lane <= kNumClasses ? s_xq[x][lane] : 0x7FFFFFFF;
-      len = __builtin_amdgcn_readlane(xql, kNumClasses);
-      t = claim(x);
-      continue;
-    }
-    const int nxt_v = claim_v(x);
-    const int pos = __popcll(__ballot(lane < kNumClasses && xql <= t)) - 1;   // queue position
-    const int c = FME_LANE_BIGFIRST ? kNumClasses - 1 - pos : pos;
-    const int nt = sc->prefix[c + 1] - sc->prefix[c];
-    const int wt = x * (nt >> 3) + min(x, nt & 7) + (t - __builtin_amdgcn_readlane(xql, pos));
-    switch (c) {
-      FME_LANE_CLASSES(FME_CASE)
-      default: break;
-    }
-    t = __builtin_amdgcn_readfirstlane(nxt_v);
-  }
-#else
+  const int home = xcc_id(), wid = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
   constexpr int kGroup = kLaneNT / 64;   // wave tiles per claim
   __shared__ int32_t claim[2];
   int x = home, tried = 0, par = 0;
@@ -1240,7 +1203,7 @@ void k_search_lane(BatchArgs a, WorkBufs w) {
   __syncthreads();
   int t = __builtin_amdgcn_readfirstlane(claim[0]);
   while (true) {
-    const int len = s_xq[x][kNumClasses];
+    const int len = s_xq[x][S - 1][kNumClasses];
     if (kGroup * t >= len) {   // queue drained: the next XCD's
       if (++tried == 8) break;
       x = (home + tried) & 7;
@@ -1254,12 +1217,13 @@ void k_search_lane(BatchArgs a, WorkBufs w) {
     if (threadIdx.x == 0) nxt = atomicAdd(&ctr[x], 1);
     const int tw = kGroup * t + wid;
     if (tw < len) {
-      int pos = 0;   // position in the XCD queue (FME_LANE_BIGFIRST: largest class first)
-      while (pos < kNumClasses - 1 && tw >= s_xq[x][pos + 1]) pos++;
-      const int c = FME_LANE_BIGFIRST ? kNumClasses - 1 - pos : pos;
+      int q = 0, c = 0;   // band x S + q of the queue, class c inside it
+      while (q < S - 1 && tw >= s_xq[x][q][kNumClasses]) q++;
+      while (c < kNumClasses - 1 && tw >= s_xq[x][q][c + 1]) c++;
       const int nt = sc->prefix[c + 1] - sc->prefix[c];
+      const int lo = (int)(((long long)nt * (x * S + q)) / (8 * S));   // the band's first tile of class c
       // wave-uniform: kept in an SGPR, so no VGPR of it lives (and is spilled) across the call
-      const int wt = __builtin_amdgcn_readfirstlane(x * (nt >> 3) + min(x, nt & 7) + (tw - s_xq[x][pos]));
+      const int wt = __builtin_amdgcn_readfirstlane(lo + (tw - s_xq[x][q][c]));
       switch (c) {
         FME_LANE_CLASSES(FME_CASE)
         default: break;
@@ -1270,9 +1234,7 @@ void k_search_lane(BatchArgs a, WorkBufs w) {
     __syncthreads();
     t = __builtin_amdgcn_readfirstlane(claim[par]);
   }
-#endif
   (void)wid;
-  (void)lane;
 }
 #undef FME_CASE
 

@@ -187,14 +187,39 @@ __device__ __forceinline__ bool two_point_has_more(const Tz& s) {
 }
 
 
+// The staged bulk search (k_tz_staged): a workgroup takes the PUs of one (unit-shape kernel,
+// reference picture, CTU) group and first copies the reference area their searches read into LDS:
+// kTileH rows of kTileWD dwords around the CTU displaced by the first PU's start MV, kTileM samples
+// of margin on each side (the search range, 64, plus slack for the other PUs' predictors), with the
+// padded-picture semantics of the global loads (rows and columns clamped).  A candidate window that
+// lies inside the tile is read from LDS, any other from global memory, so the results do not
+// depend on the staging.
+constexpr int kTileM = 72;
+constexpr int kTileWD = (64 + 2 * kTileM + 3 + 8 + 3) / 4;   // dwords per row (x0 aligned down to 4)
+constexpr int kTileH = 64 + 2 * kTileM;
+struct TileRef {
+  const uint32_t* lds;   // null: no staged tile
+  int x0, y0;            // picture coordinates of tile dword 0 of row 0 (x0 a multiple of 4)
+};
+
 // Reference window of one unit at displacement (bx, by) from its origin: UH rows (FEN: even rows
 // only) of ND dwords from the aligned column, and the byte shift s0 of the first sample.
 template <int UW, int UH>
 __device__ __forceinline__ void load_window(uint32_t (&w)[UH][UW / 4 + 1], uint32_t& s0, const PicDesc& ref, int bx,
-                                            int by, bool sub) {
+                                            int by, bool sub, const TileRef& t) {
   constexpr int ND = UW / 4 + 1;
   const int xa = bx & ~3;
   s0 = (uint32_t)(bx - xa);
+  if (t.lds && xa >= t.x0 && xa + 4 * ND <= t.x0 + 4 * kTileWD && by >= t.y0 && by + UH <= t.y0 + kTileH) {
+    const uint32_t* p = t.lds + (by - t.y0) * kTileWD + ((xa - t.x0) >> 2);
+#pragma unroll
+    for (int r = 0; r < UH; r++) {
+      if (sub && (r & 1)) continue;
+#pragma unroll
+      for (int q = 0; q < ND; q++) w[r][q] = p[r * kTileWD + q];
+    }
+    return;
+  }
   const bool inside = xa >= 0 && xa + 4 * ND <= ref.width;
 #pragma unroll
   for (int r = 0; r < UH; r++) {
@@ -312,7 +337,7 @@ __device__ __forceinline__ uint64_t block_min(uint64_t key) {
 // UW / 4 dwords of bytes, half the registers of the int16 form)
 template <int UW, int UH, int NW = 1, int KB = -1>
 __device__ __forceinline__ void tz_wave(const TzArgs& ta, int jid, const fme_job& j, int PW, int PH, int pred_x,
-                                        int pred_y) {
+                                        int pred_y, const TileRef& tile = TileRef{nullptr, 0, 0}) {
   const BatchArgs& a = ta.a;
   const int lane = (int)threadIdx.x & 63, wid = NW == 1 ? 0 : (int)threadIdx.x >> 6;
   const int UX = PW / UW, LR = UX * (PH / UH);
@@ -370,7 +395,7 @@ __device__ __forceinline__ void tz_wave(const TzArgs& ta, int jid, const fme_job
     if (v && real) {
       uint32_t w[UH][ND];
       uint32_t s0;
-      load_window<UW, UH>(w, s0, ref, ox + x, oy + y, sub);
+      load_window<UW, UH>(w, s0, ref, ox + x, oy + y, sub, tile);
       part = unit_part<UW, UH, KW>(w, s0, kk, sk2, kbuf, sad_metric, sub);
     }
     const uint32_t d = group_sum(part, L);
@@ -720,6 +745,124 @@ void k_tz_wave(TzArgs ta, TzSchedule sc, int kid) {
   tz_wave<UW, UH, 1, KB>(ta, jid, j, kTzW[c], kTzH[c], ta.ext[jid].pred2n_x, ta.ext[jid].pred2n_y);
 }
 
+// ---- staged bulk search: PUs grouped by (kernel, reference picture, CTU), a group's search area
+// in LDS (TileRef).  k_tz_pair_count / k_tz_pair_scan / k_tz_pair_scatter build the groups on the
+// device from the class bytes; k_tz_staged runs persistent workgroups that claim a group, stage its
+// tile and search its PUs one wave per PU (claimed from the group in order: the scatter visits the
+// class order backwards, so the large PUs tend to come first).
+__device__ __forceinline__ int tz_pair_key(const TzPairs& tp, const fme_job& j, int kid) {
+  const int cx = min((int)j.x >> 6, tp.cw - 1), cy = min((int)j.y >> 6, tp.ch - 1);
+  return kid * tp.np + ((int)j.ref_id * tp.ch + cy) * tp.cw + cx;
+}
+
+__global__ __launch_bounds__(256) void k_tz_pair_count(TzArgs ta, TzPairs tp, const uint8_t* __restrict__ cls, int n) {
+  const int i = (int)(blockIdx.x * 256 + threadIdx.x);
+  if (i >= n) return;
+  const int c = cls[i];
+  if (c >= kNumClasses) return;
+  atomicAdd(&tp.cnt[tz_pair_key(tp, ta.a.jobs[i], tz_kid_of(c))], 1);
+}
+
+// One workgroup: exclusive prefix of the 3 np group counts, the cursors, and each kernel's list of
+// non-empty groups.
+__global__ __launch_bounds__(1024) void k_tz_pair_scan(TzPairs tp) {
+  __shared__ int32_t part[1024];
+  const int tot = 3 * tp.np, per = (tot + 1023) / 1024, t = (int)threadIdx.x;
+  const int b = min(tot, t * per), e = min(tot, b + per);
+  int sum = 0;
+  for (int k = b; k < e; k++) sum += tp.cnt[k];
+  part[t] = sum;
+  __syncthreads();
+  for (int d = 1; d < 1024; d <<= 1) {   // inclusive scan (Hillis-Steele)
+    const int v = t >= d ? part[t - d] : 0;
+    __syncthreads();
+    part[t] += v;
+    __syncthreads();
+  }
+  int run = part[t] - sum;
+  for (int k = b; k < e; k++) {
+    const int c = tp.cnt[k];
+    tp.off[k] = run;
+    tp.cursor[k] = run;
+    if (c > 0) {
+      const int kid = k / tp.np;
+      tp.seg[kid * tp.np + atomicAdd(&tp.nseg[kid], 1)] = k;
+    }
+    run += c;
+  }
+}
+
+// Jobs into their groups, visiting the class order (perm) from the largest class down.
+__global__ __launch_bounds__(256) void k_tz_pair_scatter(TzArgs ta, TzPairs tp, const uint8_t* __restrict__ cls, int n) {
+  const int i = (int)(blockIdx.x * 256 + threadIdx.x);
+  if (i >= n) return;
+  const int jid = ta.perm[n - 1 - i];
+  const int c = cls[jid];
+  if (c >= kNumClasses) return;
+  const int key = tz_pair_key(tp, ta.a.jobs[jid], tz_kid_of(c));
+  tp.perm[atomicAdd(&tp.cursor[key], 1)] = jid;
+}
+
+#ifndef FME_TZS_NT   // threads per workgroup of the staged search (3 workgroups of tiles fit a CU's LDS)
+#define FME_TZS_NT 384
+#endif
+#ifndef FME_TZS_WAVES   // waves per SIMD the staged kernel's registers are sized for
+#define FME_TZS_WAVES FME_TZW_WAVES
+#endif
+template <int UW, int UH, int KB>
+__global__ __launch_bounds__(FME_TZS_NT) __attribute__((amdgpu_waves_per_eu(FME_TZS_WAVES)))
+void k_tz_staged(TzArgs ta, TzPairs tp, int kid) {
+  __shared__ uint32_t tile[kTileH * kTileWD];
+  __shared__ int32_t s_key, s_next;
+  const int lane = (int)threadIdx.x & 63;
+  while (true) {
+    if (threadIdx.x == 0) {
+      const int k = atomicAdd(&tp.claim[kid], 1);
+      s_key = k < tp.nseg[kid] ? tp.seg[kid * tp.np + k] : -1;
+      s_next = 0;
+    }
+    __syncthreads();
+    const int key = s_key;
+    if (key < 0) break;
+    const int start = tp.off[key], cnt = tp.cnt[key];
+    // the tile: the group's CTU displaced by its first PU's start MV (round4 of the clipped AMVP)
+    const int j0 = tp.perm[start];
+    const fme_job jb = ta.a.jobs[j0];
+    const fme_tz_ext e0 = ta.ext[j0];
+    const PicDesc ref = ta.a.pics[jb.ref_id];
+    int mx = jb.mvp_x, my = jb.mvp_y;
+    clip_qpel(mx, my, ref.width, ref.height, e0.cu_x, e0.cu_y);
+    const int x0 = (((int)jb.x & ~63) + round4(mx) - kTileM) & ~3;
+    const int y0 = ((int)jb.y & ~63) + round4(my) - kTileM;
+    for (int i = (int)threadIdx.x; i < kTileH * kTileWD; i += FME_TZS_NT) {
+      const int r = i / kTileWD, q = i - r * kTileWD;
+      const uint8_t* row = ref.luma + (size_t)clamp_i(y0 + r, 0, ref.height - 1) * ref.stride;
+      const int x = x0 + 4 * q;
+      uint32_t v;
+      if (x >= 0 && x + 4 <= ref.width) {
+        v = gld32(row + x);
+      } else {
+        v = 0;
+#pragma unroll
+        for (int k = 0; k < 4; k++) v |= gld8(row + clamp_i(x + k, 0, ref.width - 1)) << (8 * k);
+      }
+      tile[i] = v;
+    }
+    __syncthreads();
+    const TileRef tr{tile, x0, y0};
+    while (true) {   // one wave per PU of the group
+      int p = 0;
+      if (lane == 0) p = atomicAdd(&s_next, 1);
+      p = __builtin_amdgcn_readfirstlane(__shfl(p, 0, 64));
+      if (p >= cnt) break;
+      const int jid = tp.perm[start + p];
+      const fme_job j = ta.a.jobs[jid];
+      tz_wave<UW, UH, 1, KB>(ta, jid, j, j.w, j.h, ta.ext[jid].pred2n_x, ta.ext[jid].pred2n_y, tr);
+    }
+    __syncthreads();   // every wave is done with the tile before the next group's
+  }
+}
+
 // One dependency level of a producer's m_integerMv2Nx2N chain (fme_pred_inter_p/b): one wave per
 // job in chain mode.  The host launches the levels back to back on one stream, so a level reads the
 // post-EMI MVs of earlier levels from global memory (kernel boundaries order them) and no level
@@ -768,6 +911,28 @@ int tz_lanes_per_pu(int cls) {
   int l = 1;
   while (l < lr) l <<= 1;
   return l;
+}
+
+hipError_t launch_tz_pairs(const TzArgs& ta, const TzPairs& tp, const uint8_t* cls, int n, hipStream_t s) {
+  const int nb = (n + 255) / 256;
+  hipLaunchKernelGGL(k_tz_pair_count, dim3(nb), dim3(256), 0, s, ta, tp, cls, n);
+  hipLaunchKernelGGL(k_tz_pair_scan, dim3(1), dim3(1024), 0, s, tp);
+  hipLaunchKernelGGL(k_tz_pair_scatter, dim3(nb), dim3(256), 0, s, ta, tp, cls, n);
+  return hipGetLastError();
+}
+
+hipError_t launch_tz_staged(const TzArgs& ta, const TzPairs& tp, int kid, bool keyed, int workgroups, hipStream_t s) {
+  const dim3 g(workgroups), b(FME_TZS_NT);
+  if (keyed) {
+    if (kid == 0) hipLaunchKernelGGL((k_tz_staged<4, 8, -1>), g, b, 0, s, ta, tp, 0);
+    else if (kid == 1) hipLaunchKernelGGL((k_tz_staged<8, 4, -1>), g, b, 0, s, ta, tp, 1);
+    else hipLaunchKernelGGL((k_tz_staged<8, 8, -1>), g, b, 0, s, ta, tp, 2);
+  } else {
+    if (kid == 0) hipLaunchKernelGGL((k_tz_staged<4, 8, 0>), g, b, 0, s, ta, tp, 0);
+    else if (kid == 1) hipLaunchKernelGGL((k_tz_staged<8, 4, 0>), g, b, 0, s, ta, tp, 1);
+    else hipLaunchKernelGGL((k_tz_staged<8, 8, 0>), g, b, 0, s, ta, tp, 2);
+  }
+  return hipGetLastError();
 }
 
 // Wave-uniform bulk search of kernel kid: sc.prefix in waves (one per PU).

@@ -58,6 +58,26 @@ for step in "$@"; do
     pxab2) B="python -u bench.py --workload c3_qp22_main10 --no-cpu-baseline --parity-seconds 0 --steps 10"
            run px6d 300 $B && FME_LIB_PATH=$PWD/hm16.9-nn_fme_amd/variants/px5/libfme_amd.so run px5 300 $B && \
            FME_LIB_PATH=$PWD/hm16.9-nn_fme_amd/variants/px8/libfme_amd.so run px8 300 $B && run px6p 300 $B --parity-seconds 10 ;;
+    sbab) run sbab 500 python -u tools/ab_bench.py . variants/sb1 variants/sb16 --rounds 4 && \
+          P="python3 bench.py --no-cpu-baseline --no-pi --no-tz --no-mc --no-pcie --parity-seconds 0 --steps 2 --warmup 1" && \
+          run sb8_fetch 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/sbpmc/sb8/fetch -o run -- $P && \
+          run sb8_write 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/sbpmc/sb8/write -o run -- $P && \
+          FME_LIB_PATH=$PWD/hm16.9-nn_fme_amd/variants/sb1/libfme_amd.so run sb1_fetch 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/sbpmc/sb1/fetch -o run -- $P && \
+          FME_LIB_PATH=$PWD/hm16.9-nn_fme_amd/variants/sb16/libfme_amd.so run sb16_fetch 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/sbpmc/sb16/fetch -o run -- $P ;;
+    c5w) B="python -u bench.py --no-cpu-baseline --no-pi --no-tz --no-mc"
+         run bench_c5 300 $B --workload c5 && run bench_c5_exact 300 $B --workload c5_exact && run bench_c5_b4x40 300 $B --workload c5_b4x40 ;;
+    icache) P="python3 bench.py --no-cpu-baseline --no-pi --no-tz --no-mc --no-pcie --parity-seconds 0 --steps 2 --warmup 1"
+            run icache 150 rocprofv3 --pmc SQC_ICACHE_REQ SQC_ICACHE_HITS SQC_ICACHE_MISSES SQC_ICACHE_MISSES_DUPLICATE SQ_IFETCH SQ_WAIT_INST_ANY SQ_WAVE_CYCLES SQ_BUSY_CYCLES --output-format csv -d gpurun_out/icache -o run -- $P && \
+            python3 tools/pmc_summary.py gpurun_out/icache > gpurun_out/icache_summary.txt && \
+            run icache_tz 200 rocprofv3 --pmc SQC_ICACHE_REQ SQC_ICACHE_HITS SQC_ICACHE_MISSES SQC_ICACHE_MISSES_DUPLICATE SQ_IFETCH SQ_WAIT_INST_ANY SQ_WAVE_CYCLES SQ_BUSY_CYCLES --output-format csv -d gpurun_out/icache_tz -o run -- python3 tools/tz_probe.py gpurun_out/tz_ic.npz && \
+            python3 tools/pmc_summary.py gpurun_out/icache_tz > gpurun_out/icache_tz_summary.txt ;;
+    tlc1) run tlc1 200 rocprofv3 --kernel-trace --memory-copy-trace --output-format csv -d gpurun_out/tlc1 -o run -- python3 bench.py --workload c1 --no-cpu-baseline --no-pi --no-tz --no-mc --parity-seconds 0 --steps 10 && \
+          python3 tools/timeline.py gpurun_out/tlc1 3 8 > gpurun_out/tlc1_timeline.txt ;;
+    tzs) run tzs_tests 400 python -u -m pytest tests -m gpu -k "tz or ring or integer or pred_inter" -x -q -p no:cacheprovider --timeout 300 --timeout-method thread && \
+         run tzs_def 200 python -u tools/tz_probe.py gpurun_out/tzs_def.npz && \
+         FME_LIB_PATH=$PWD/hm16.9-nn_fme_amd/variants/tzs0/libfme_amd.so run tzs_0 200 python -u tools/tz_probe.py gpurun_out/tzs_0.npz && \
+         FME_LIB_PATH=$PWD/hm16.9-nn_fme_amd/variants/tzs4/libfme_amd.so run tzs_4 200 python -u tools/tz_probe.py gpurun_out/tzs_4.npz && \
+         python3 -c "import numpy as np; a=np.load('gpurun_out/tzs_def.npz'); b=np.load('gpurun_out/tzs_0.npz'); c=np.load('gpurun_out/tzs_4.npz'); print('identical', all((a[k]==b[k]).all() and (a[k]==c[k]).all() for k in a.files))" ;;
     bigab) run bigab 400 python -u tools/ab_bench.py . variants/big --rounds 4 && bash tools/gpu_r5.sh bench1 bench2 ;;
     bench1) run bench1 300 python -u bench.py --no-pi --no-tz --no-mc --cpu-seconds 3 --parity-seconds 10 ;;
     bench2) run bench2 300 python -u -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --steps 6 --warmup 2 --no-pi --no-tz --no-mc --no-cpu-baseline --parity-seconds 0 --dist-backend gloo ;;
