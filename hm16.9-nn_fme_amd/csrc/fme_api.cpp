@@ -206,7 +206,7 @@ struct fme_ctx {
   DevBuf<BiKeyTask> d_bikey;
   DevBuf<int32_t> d_key_invalid;  // invalid requests of the last fme_build_bipred_keys_device
   DevBuf<int32_t> d_ch_i32;     // k_tz_level: psrc
-  DevBuf<int32_t> d_tzp;        // staged integer search: 8 counters, then cnt / cursor / off / seg (TzPairs)
+  DevBuf<int32_t> d_tzp;        // staged integer search: 8 words (nseg), then cnt / cursor / off / seg (TzPairs)
   DevBuf<int32_t> d_tzp_perm;   // [n] jobs grouped by (kernel, reference, CTU)
   // fme_pred_inter_p scratch, kept across calls: pinned transfer buffers, host arrays, the
   // level-ordered device copies of the jobs
@@ -949,13 +949,14 @@ static int tz_run(fme_ctx* c, fme_job* d_jobs, const fme_tz_ext* d_ext, uint32_t
   if (!c->ev_join2) HIP_TRY(hipEventCreateWithFlags(&c->ev_join2, hipEventDisableTiming));
   // the staged form (FME_TZ_STAGE): PUs grouped by (kernel, reference, CTU) on the device, each
   // group's search area read into LDS once (fme_tz.hip k_tz_staged)
-  int cw = 0, ch = 0;
-  for (const PicDesc& p : c->pics)
-    if (p.luma) {
-      cw = std::max(cw, (p.width + 63) / 64);
-      ch = std::max(ch, (p.height + 63) / 64);
+  int cw = 0, ch = 0, npic = 0;   // CTU grid of the largest bound picture; reference ids < npic
+  for (int i = 0; i < FME_MAX_PICTURES; i++)
+    if (c->pics[i].luma) {
+      cw = std::max(cw, (c->pics[i].width + 63) / 64);
+      ch = std::max(ch, (c->pics[i].height + 63) / 64);
+      npic = i + 1;
     }
-  const long long np = (long long)FME_MAX_PICTURES * cw * ch;
+  const long long np = (long long)npic * cw * ch;
   if (FME_TZ_STAGE && np > 0 && np <= (1LL << 20)) {
     const size_t words = 8 + 12 * (size_t)np;
     if (c->d_tzp.cap < words || c->d_tzp_perm.cap < (size_t)n) {
@@ -966,7 +967,6 @@ static int tz_run(fme_ctx* c, fme_job* d_jobs, const fme_tz_ext* d_ext, uint32_t
     TzPairs tp{};
     int32_t* b = c->d_tzp.p;
     tp.nseg = b;
-    tp.claim = b + 3;
     tp.cnt = b + 8;
     tp.cursor = tp.cnt + 3 * np;
     tp.off = tp.cursor + 3 * np;
@@ -980,10 +980,9 @@ static int tz_run(fme_ctx* c, fme_job* d_jobs, const fme_tz_ext* d_ext, uint32_t
     HIP_TRY(hipEventRecord(c->ev_fork, s));
     HIP_TRY(hipStreamWaitEvent(c->aux, c->ev_fork, 0));
     HIP_TRY(hipStreamWaitEvent(c->aux2, c->ev_fork, 0));
-    const int wgs = 3 * cu_count(c->device);   // persistent: three tiles' LDS per CU
-    HIP_TRY(launch_tz_staged(ta, tp, 0, keyed, wgs, c->aux));
-    HIP_TRY(launch_tz_staged(ta, tp, 1, keyed, wgs, c->aux2));
-    HIP_TRY(launch_tz_staged(ta, tp, 2, keyed, wgs, s));
+    HIP_TRY(launch_tz_staged(ta, tp, 0, keyed, c->aux));
+    HIP_TRY(launch_tz_staged(ta, tp, 1, keyed, c->aux2));
+    HIP_TRY(launch_tz_staged(ta, tp, 2, keyed, s));
   } else {
     HIP_TRY(hipEventRecord(c->ev_fork, s));
     HIP_TRY(hipStreamWaitEvent(c->aux, c->ev_fork, 0));

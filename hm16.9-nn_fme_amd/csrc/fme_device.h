@@ -22,9 +22,10 @@
 // Sub-bands per XCD queue of the search kernel (Schedule::xq): the XCD searches its spatial band
 // of the frame in this many consecutive strips, every class of a strip before the next strip, so
 // the jobs' lines and the reference windows a strip's PU classes share stay in the XCD's L2.
-// 1 = the round-4 order (each XCD's band class by class).
+// 1 = the round-4 order (each XCD's band class by class), the default: 8 strips cut the search's
+// fetch by 7 % and cost 6 % of its time (0.955 against 0.899 ms; 16: 0.969 ms, profiles/r05_ab.log).
 #ifndef FME_LANE_SUBBANDS
-#define FME_LANE_SUBBANDS 8
+#define FME_LANE_SUBBANDS 1
 #endif
 
 namespace fme {
@@ -185,19 +186,18 @@ struct TzSchedule {
 // otherwise the uni-pred form, whose key rows take half the registers
 hipError_t launch_tz_wave(const TzArgs& ta, const TzSchedule& sc, int kid, bool keyed, hipStream_t s);   // prefix in waves
 // The staged bulk search's groups (fme_tz.hip k_tz_staged): PUs by (unit-shape kernel kid,
-// reference picture, CTU), np = FME_MAX_PICTURES * cw * ch groups per kernel.
+// reference picture, CTU), np = (bound picture ids) * cw * ch groups per kernel.
 struct TzPairs {
   int32_t* cnt;      // [3 np] PUs per group (zeroed before launch_tz_pairs)
   int32_t* cursor;   // [3 np]
   int32_t* off;      // [3 np] first position of each group in perm
-  int32_t* seg;      // [3][np] non-empty groups of each kernel
-  int32_t* nseg;     // [3] their counts (zeroed)
-  int32_t* claim;    // [3] group claim counters (zeroed)
+  int32_t* seg;      // non-empty groups, kernel-major
+  int32_t* nseg;     // [0..3): non-empty groups per kernel, [3..6): each kernel's first in seg
   int32_t* perm;     // [n] jobs grouped
   int32_t np, cw, ch;
 };
 hipError_t launch_tz_pairs(const TzArgs& ta, const TzPairs& tp, const uint8_t* cls, int n, hipStream_t s);
-hipError_t launch_tz_staged(const TzArgs& ta, const TzPairs& tp, int kid, bool keyed, int workgroups, hipStream_t s);
+hipError_t launch_tz_staged(const TzArgs& ta, const TzPairs& tp, int kid, bool keyed, hipStream_t s);
 // The dependency levels of a producer's m_integerMv2Nx2N chain (fme_tz.hip k_tz_level): jobs in
 // level order, level l = jobs [lvl_off[l], lvl_off[l+1]), one launch per level, back to back.
 struct TzChain {

@@ -20,6 +20,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdio>
 
 #include "fme_device.h"
 #include "fme_simd.h"
@@ -747,119 +748,145 @@ void k_tz_wave(TzArgs ta, TzSchedule sc, int kid) {
 
 // ---- staged bulk search: PUs grouped by (kernel, reference picture, CTU), a group's search area
 // in LDS (TileRef).  k_tz_pair_count / k_tz_pair_scan / k_tz_pair_scatter build the groups on the
-// device from the class bytes; k_tz_staged runs persistent workgroups that claim a group, stage its
-// tile and search its PUs one wave per PU (claimed from the group in order: the scatter visits the
-// class order backwards, so the large PUs tend to come first).
+// device from the class bytes; k_tz_staged runs one workgroup per group, which stages the group's
+// tile and searches its PUs one wave per PU (claimed from the group in order: the scatter visits
+// the class order backwards, so the large PUs tend to come first).
 __device__ __forceinline__ int tz_pair_key(const TzPairs& tp, const fme_job& j, int kid) {
   const int cx = min((int)j.x >> 6, tp.cw - 1), cy = min((int)j.y >> 6, tp.ch - 1);
   return kid * tp.np + ((int)j.ref_id * tp.ch + cy) * tp.cw + cx;
 }
 
-__global__ __launch_bounds__(256) void k_tz_pair_count(TzArgs ta, TzPairs tp, const uint8_t* __restrict__ cls, int n) {
-  const int i = (int)(blockIdx.x * 256 + threadIdx.x);
-  if (i >= n) return;
-  const int c = cls[i];
-  if (c >= kNumClasses) return;
-  atomicAdd(&tp.cnt[tz_pair_key(tp, ta.a.jobs[i], tz_kid_of(c))], 1);
+// Per-wave aggregation of the group atomics: the CTU-ordered stream gives a wave few distinct
+// groups (<= 12 in a CTU: 4 references x 3 kernels), so each distinct key costs one atomic per wave
+// (one per job serialised on the hot counters: 115 us for a 1080p frame).  Returns this lane's
+// position among the wave's lanes with its key; *base gets the atomic's old value (scatter).
+__device__ __forceinline__ int wave_agg_add(int32_t* ctr, int key, bool valid, int* base) {
+  const int lane = (int)threadIdx.x & 63;
+  uint64_t todo = __ballot(valid);
+  int rank = 0, b = 0;
+  while (todo) {
+    const int leader = __builtin_ctzll(todo);
+    const int k = __builtin_amdgcn_readlane(key, leader);
+    const uint64_t m = __ballot(valid && key == k);
+    int old = 0;
+    if (lane == leader) old = atomicAdd(&ctr[k], __popcll(m));
+    old = __builtin_amdgcn_readlane(old, leader);
+    if (valid && key == k) {
+      rank = __popcll(m & ((1ull << lane) - 1));
+      b = old;
+    }
+    todo &= ~m;
+  }
+  if (base) *base = b;
+  return rank;
 }
 
-// One workgroup: exclusive prefix of the 3 np group counts, the cursors, and each kernel's list of
-// non-empty groups.
+__global__ __launch_bounds__(256) void k_tz_pair_count(TzArgs ta, TzPairs tp, const uint8_t* __restrict__ cls, int n) {
+  const int i = (int)(blockIdx.x * 256 + threadIdx.x);
+  const int c = i < n ? cls[i] : 255;
+  const bool valid = c < kNumClasses;
+  const int key = valid ? tz_pair_key(tp, ta.a.jobs[i], tz_kid_of(c)) : 0;
+  (void)wave_agg_add(tp.cnt, key, valid, nullptr);
+}
+
+// One workgroup: exclusive prefix of the 3 np group counts (the cursors), and the list of non-empty
+// groups, kernel-major (a prefix of the non-empty flags): kernel kid's groups are
+// seg[nseg[3 + kid] ..) and there are nseg[kid] of them.
 __global__ __launch_bounds__(1024) void k_tz_pair_scan(TzPairs tp) {
-  __shared__ int32_t part[1024];
+  __shared__ int32_t part[1024], nz[1024], first[3];
   const int tot = 3 * tp.np, per = (tot + 1023) / 1024, t = (int)threadIdx.x;
   const int b = min(tot, t * per), e = min(tot, b + per);
-  int sum = 0;
-  for (int k = b; k < e; k++) sum += tp.cnt[k];
+  int sum = 0, nnz = 0;
+  for (int k = b; k < e; k++) {
+    const int c = tp.cnt[k];
+    sum += c;
+    nnz += c > 0;
+  }
   part[t] = sum;
+  nz[t] = nnz;
   __syncthreads();
-  for (int d = 1; d < 1024; d <<= 1) {   // inclusive scan (Hillis-Steele)
-    const int v = t >= d ? part[t - d] : 0;
+  for (int d = 1; d < 1024; d <<= 1) {   // inclusive scans (Hillis-Steele)
+    const int v = t >= d ? part[t - d] : 0, w = t >= d ? nz[t - d] : 0;
     __syncthreads();
     part[t] += v;
+    nz[t] += w;
     __syncthreads();
   }
-  int run = part[t] - sum;
+  int run = part[t] - sum, r = nz[t] - nnz;
   for (int k = b; k < e; k++) {
     const int c = tp.cnt[k];
     tp.off[k] = run;
     tp.cursor[k] = run;
-    if (c > 0) {
-      const int kid = k / tp.np;
-      tp.seg[kid * tp.np + atomicAdd(&tp.nseg[kid], 1)] = k;
-    }
+    if (k % tp.np == 0) first[k / tp.np] = r;   // the kernel's first group in seg
+    if (c > 0) tp.seg[r++] = k;
     run += c;
+  }
+  __syncthreads();
+  if (t < 3) {
+    tp.nseg[3 + t] = first[t];
+    tp.nseg[t] = (t < 2 ? first[t + 1] : nz[1023]) - first[t];
   }
 }
 
 // Jobs into their groups, visiting the class order (perm) from the largest class down.
 __global__ __launch_bounds__(256) void k_tz_pair_scatter(TzArgs ta, TzPairs tp, const uint8_t* __restrict__ cls, int n) {
   const int i = (int)(blockIdx.x * 256 + threadIdx.x);
-  if (i >= n) return;
-  const int jid = ta.perm[n - 1 - i];
-  const int c = cls[jid];
-  if (c >= kNumClasses) return;
-  const int key = tz_pair_key(tp, ta.a.jobs[jid], tz_kid_of(c));
-  tp.perm[atomicAdd(&tp.cursor[key], 1)] = jid;
+  const int jid = i < n ? ta.perm[n - 1 - i] : 0;
+  const int c = i < n ? cls[jid] : 255;
+  const bool valid = c < kNumClasses;
+  const int key = valid ? tz_pair_key(tp, ta.a.jobs[jid], tz_kid_of(c)) : 0;
+  int base;
+  const int rank = wave_agg_add(tp.cursor, key, valid, &base);
+  if (valid) tp.perm[base + rank] = jid;
 }
 
-#ifndef FME_TZS_NT   // threads per workgroup of the staged search (3 workgroups of tiles fit a CU's LDS)
-#define FME_TZS_NT 384
+#ifndef FME_TZS_NT   // threads per workgroup of the staged search (1080p frame, tools/tz_probe.py: 6 waves
+#define FME_TZS_NT 512   // 5.69 ms, 8 waves 4.83 ms; two 45.7 KB tiles per CU at 5 waves/SIMD of registers)
 #endif
 #ifndef FME_TZS_WAVES   // waves per SIMD the staged kernel's registers are sized for
 #define FME_TZS_WAVES FME_TZW_WAVES
 #endif
+// One launch per unit-shape kernel, one workgroup per group (the grid an upper bound): stage the
+// group's tile, then search its PUs, one wave per PU.  (The three kernels' searches in one launch,
+// behind a switch, spilled 282 VGPRs: the allocation is the maximum over the three.)
 template <int UW, int UH, int KB>
 __global__ __launch_bounds__(FME_TZS_NT) __attribute__((amdgpu_waves_per_eu(FME_TZS_WAVES)))
 void k_tz_staged(TzArgs ta, TzPairs tp, int kid) {
   __shared__ uint32_t tile[kTileH * kTileWD];
-  __shared__ int32_t s_key, s_next;
-  const int lane = (int)threadIdx.x & 63;
-  while (true) {
-    if (threadIdx.x == 0) {
-      const int k = atomicAdd(&tp.claim[kid], 1);
-      s_key = k < tp.nseg[kid] ? tp.seg[kid * tp.np + k] : -1;
-      s_next = 0;
-    }
-    __syncthreads();
-    const int key = s_key;
-    if (key < 0) break;
-    const int start = tp.off[key], cnt = tp.cnt[key];
-    // the tile: the group's CTU displaced by its first PU's start MV (round4 of the clipped AMVP)
-    const int j0 = tp.perm[start];
-    const fme_job jb = ta.a.jobs[j0];
-    const fme_tz_ext e0 = ta.ext[j0];
-    const PicDesc ref = ta.a.pics[jb.ref_id];
-    int mx = jb.mvp_x, my = jb.mvp_y;
-    clip_qpel(mx, my, ref.width, ref.height, e0.cu_x, e0.cu_y);
-    const int x0 = (((int)jb.x & ~63) + round4(mx) - kTileM) & ~3;
-    const int y0 = ((int)jb.y & ~63) + round4(my) - kTileM;
-    for (int i = (int)threadIdx.x; i < kTileH * kTileWD; i += FME_TZS_NT) {
-      const int r = i / kTileWD, q = i - r * kTileWD;
-      const uint8_t* row = ref.luma + (size_t)clamp_i(y0 + r, 0, ref.height - 1) * ref.stride;
-      const int x = x0 + 4 * q;
-      uint32_t v;
-      if (x >= 0 && x + 4 <= ref.width) {
-        v = gld32(row + x);
-      } else {
-        v = 0;
+  if ((int)blockIdx.x >= tp.nseg[kid]) return;
+  const int key = tp.seg[tp.nseg[3 + kid] + (int)blockIdx.x];
+  const int start = tp.off[key], cnt = tp.cnt[key];
+  // the tile: the group's CTU displaced by its first PU's start MV (round4 of the clipped AMVP)
+  const int j0 = tp.perm[start];
+  const fme_job jb = ta.a.jobs[j0];
+  const fme_tz_ext e0 = ta.ext[j0];
+  const PicDesc ref = ta.a.pics[jb.ref_id];
+  int mx = jb.mvp_x, my = jb.mvp_y;
+  clip_qpel(mx, my, ref.width, ref.height, e0.cu_x, e0.cu_y);
+  const int x0 = (((int)jb.x & ~63) + round4(mx) - kTileM) & ~3;
+  const int y0 = ((int)jb.y & ~63) + round4(my) - kTileM;
+  for (int i = (int)threadIdx.x; i < kTileH * kTileWD; i += FME_TZS_NT) {
+    const int r = i / kTileWD, q = i - r * kTileWD;
+    const uint8_t* row = ref.luma + (size_t)clamp_i(y0 + r, 0, ref.height - 1) * ref.stride;
+    const int x = x0 + 4 * q;
+    uint32_t v;
+    if (x >= 0 && x + 4 <= ref.width) {
+      v = gld32(row + x);
+    } else {
+      v = 0;
 #pragma unroll
-        for (int k = 0; k < 4; k++) v |= gld8(row + clamp_i(x + k, 0, ref.width - 1)) << (8 * k);
-      }
-      tile[i] = v;
+      for (int k = 0; k < 4; k++) v |= gld8(row + clamp_i(x + k, 0, ref.width - 1)) << (8 * k);
     }
-    __syncthreads();
-    const TileRef tr{tile, x0, y0};
-    while (true) {   // one wave per PU of the group
-      int p = 0;
-      if (lane == 0) p = atomicAdd(&s_next, 1);
-      p = __builtin_amdgcn_readfirstlane(__shfl(p, 0, 64));
-      if (p >= cnt) break;
-      const int jid = tp.perm[start + p];
-      const fme_job j = ta.a.jobs[jid];
-      tz_wave<UW, UH, 1, KB>(ta, jid, j, j.w, j.h, ta.ext[jid].pred2n_x, ta.ext[jid].pred2n_y, tr);
-    }
-    __syncthreads();   // every wave is done with the tile before the next group's
+    tile[i] = v;
+  }
+  __syncthreads();
+  const TileRef tr{tile, x0, y0};
+  // wave w takes PUs w, w + NW, ... of the group (largest first).  (Claiming them from an LDS
+  // counter with ds_add_rtn instead never finished on the box, round 5.)
+  for (int p = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6); p < cnt; p += FME_TZS_NT / 64) {
+    const int jid = tp.perm[start + p];
+    const fme_job j = ta.a.jobs[jid];
+    tz_wave<UW, UH, 1, KB>(ta, jid, j, j.w, j.h, ta.ext[jid].pred2n_x, ta.ext[jid].pred2n_y, tr);
   }
 }
 
@@ -921,8 +948,8 @@ hipError_t launch_tz_pairs(const TzArgs& ta, const TzPairs& tp, const uint8_t* c
   return hipGetLastError();
 }
 
-hipError_t launch_tz_staged(const TzArgs& ta, const TzPairs& tp, int kid, bool keyed, int workgroups, hipStream_t s) {
-  const dim3 g(workgroups), b(FME_TZS_NT);
+hipError_t launch_tz_staged(const TzArgs& ta, const TzPairs& tp, int kid, bool keyed, hipStream_t s) {
+  const dim3 g(tp.np), b(FME_TZS_NT);
   if (keyed) {
     if (kid == 0) hipLaunchKernelGGL((k_tz_staged<4, 8, -1>), g, b, 0, s, ta, tp, 0);
     else if (kid == 1) hipLaunchKernelGGL((k_tz_staged<8, 4, -1>), g, b, 0, s, ta, tp, 1);

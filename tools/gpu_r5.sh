@@ -73,11 +73,27 @@ for step in "$@"; do
             python3 tools/pmc_summary.py gpurun_out/icache_tz > gpurun_out/icache_tz_summary.txt ;;
     tlc1) run tlc1 200 rocprofv3 --kernel-trace --memory-copy-trace --output-format csv -d gpurun_out/tlc1 -o run -- python3 bench.py --workload c1 --no-cpu-baseline --no-pi --no-tz --no-mc --parity-seconds 0 --steps 10 && \
           python3 tools/timeline.py gpurun_out/tlc1 3 8 > gpurun_out/tlc1_timeline.txt ;;
-    tzs) run tzs_tests 400 python -u -m pytest tests -m gpu -k "tz or ring or integer or pred_inter" -x -q -p no:cacheprovider --timeout 300 --timeout-method thread && \
+    tzs) run tzs_tests 400 python -u -m pytest tests -m gpu -k "tz or ring or integer or pred_inter" -x -v -p no:cacheprovider --timeout 120 --timeout-method thread && \
          run tzs_def 200 python -u tools/tz_probe.py gpurun_out/tzs_def.npz && \
          FME_LIB_PATH=$PWD/hm16.9-nn_fme_amd/variants/tzs0/libfme_amd.so run tzs_0 200 python -u tools/tz_probe.py gpurun_out/tzs_0.npz && \
-         FME_LIB_PATH=$PWD/hm16.9-nn_fme_amd/variants/tzs4/libfme_amd.so run tzs_4 200 python -u tools/tz_probe.py gpurun_out/tzs_4.npz && \
-         python3 -c "import numpy as np; a=np.load('gpurun_out/tzs_def.npz'); b=np.load('gpurun_out/tzs_0.npz'); c=np.load('gpurun_out/tzs_4.npz'); print('identical', all((a[k]==b[k]).all() and (a[k]==c[k]).all() for k in a.files))" ;;
+         python3 -c "import numpy as np; a=np.load('gpurun_out/tzs_def.npz'); b=np.load('gpurun_out/tzs_0.npz'); print('identical', all((a[k]==b[k]).all() for k in a.files))" ;;
+    warm) run warm 200 python -u -c "import torch; print(torch.__version__, torch.cuda.is_available())" ;;
+    tzdbg) FME_LIB_PATH=$PWD/hm16.9-nn_fme_amd/variants/tzs0/libfme_amd.so true && \
+           FME_LIB_PATH=$PWD/hm16.9-nn_fme_amd/variants/tzdbg/libfme_amd.so run tzg_dbg 60 python -u tools/tz_golden_probe.py tz_far_fen0_sr32 ;;
+    tzab3) FME_LIB_PATH=$PWD/hm16.9-nn_fme_amd/variants/tzC/libfme_amd.so run tzC 50 python -u tools/tz_golden_probe.py tz_far_fen0_sr32 && \
+           FME_LIB_PATH=$PWD/hm16.9-nn_fme_amd/variants/tzB/libfme_amd.so run tzB 50 python -u tools/tz_golden_probe.py tz_far_fen0_sr32 && \
+           FME_LIB_PATH=$PWD/hm16.9-nn_fme_amd/variants/tzA/libfme_amd.so run tzA 50 python -u tools/tz_golden_probe.py tz_far_fen0_sr32 ;;
+    tzs2) run tzs_tests 400 python -u -m pytest tests -m gpu -k "tz or ring or integer or pred_inter" -x -v -p no:cacheprovider --timeout 120 --timeout-method thread && \
+          run tzs_def 200 python -u tools/tz_probe.py gpurun_out/tzs_def.npz && \
+          FME_LIB_PATH=$PWD/hm16.9-nn_fme_amd/variants/tzs0/libfme_amd.so run tzs_0 200 python -u tools/tz_probe.py gpurun_out/tzs_0.npz && \
+          FME_LIB_PATH=$PWD/hm16.9-nn_fme_amd/variants/tzn8/libfme_amd.so run tzs_n8 200 python -u tools/tz_probe.py gpurun_out/tzs_n8.npz && \
+          python3 -c "import numpy as np; a=np.load('gpurun_out/tzs_def.npz'); b=np.load('gpurun_out/tzs_0.npz'); c=np.load('gpurun_out/tzs_n8.npz'); print('identical', all((a[k]==b[k]).all() and (a[k]==c[k]).all() for k in a.files))" && \
+          run tzs_trace 200 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/tzs_trace -o run -- python3 tools/tz_probe.py gpurun_out/tzs_t.npz ;;
+    tzs3) run tzs_tests 400 python -u -m pytest tests -m gpu -k "tz or ring or integer or pred_inter" -x -v -p no:cacheprovider --timeout 120 --timeout-method thread && \
+          run tzs_def 200 python -u tools/tz_probe.py gpurun_out/tzs_def.npz && \
+          FME_LIB_PATH=$PWD/hm16.9-nn_fme_amd/variants/tzs0/libfme_amd.so run tzs_0 200 python -u tools/tz_probe.py gpurun_out/tzs_0.npz && \
+          python3 -c "import numpy as np; a=np.load('gpurun_out/tzs_def.npz'); b=np.load('gpurun_out/tzs_0.npz'); print('identical', all((a[k]==b[k]).all() for k in a.files))" && \
+          run tzs_trace 200 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/tzs_trace -o run -- python3 tools/tz_probe.py gpurun_out/tzs_t.npz ;;
     bigab) run bigab 400 python -u tools/ab_bench.py . variants/big --rounds 4 && bash tools/gpu_r5.sh bench1 bench2 ;;
     bench1) run bench1 300 python -u bench.py --no-pi --no-tz --no-mc --cpu-seconds 3 --parity-seconds 10 ;;
     bench2) run bench2 300 python -u -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --steps 6 --warmup 2 --no-pi --no-tz --no-mc --no-cpu-baseline --parity-seconds 0 --dist-backend gloo ;;
