@@ -262,8 +262,6 @@ def parity_leg(rep, wl, net, step, state, seconds, max_jobs=0):
     for slot in range(F + REFS - 1):
         ref.set_picture(slot, pool[(f0 - REFS + slot) % P])
     ref.nn_set_state(state)
-    if rep.rows is not None:
-        ref.set_nn_inputs(rep.rows)
     jobs, gpu = rep.jobs, rep.results(step)
     n = len(jobs) if max_jobs <= 0 else min(max_jobs, len(jobs))
     fields = ("mv_x", "mv_y", "bits", "cost") + (("nn_class",) if nn else ())
@@ -273,6 +271,8 @@ def parity_leg(rep, wl, net, step, state, seconds, max_jobs=0):
     done, t0 = 0, time.perf_counter()
     while done < n and time.perf_counter() - t0 < seconds:
         e = min(done + 20000, n)
+        if rep.rows is not None:   # row i of a refine call belongs to its job i
+            ref.set_nn_inputs(rep.rows[done:e])
         r = ref.refine(jobs[done:e])
         g = gpu[done:e]
         m = np.zeros(e - done, bool)

@@ -366,6 +366,7 @@ class Reference:
             self.lib.ref_set_nn_inputs(self.h, None, 0)
             return
         rows = np.ascontiguousarray(rows, dtype=np.uint32).reshape(-1, 9)
+        self._rows = rows   # the library keeps the pointer: keep the array alive
         self.lib.ref_set_nn_inputs(self.h, _ptr(rows), len(rows))
 
     def mc(self, mc_jobs, y, cb, cr):
