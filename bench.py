@@ -503,7 +503,9 @@ def tz_leg(dev, stream, reps, cpu_seconds):
     wall = (time.perf_counter() - t0) / reps
     t = float(np.median(ms))
     out.update({"kernel_ms": t, "pu_per_s_kernels": len(jobs) / (t / 1e3), "ms_per_frame": wall * 1e3,
-                "pu_per_s": len(jobs) / wall, "kernels": "fme::k_tz_wave<4,8>, <8,4>, <8,8>: one wave per PU, three concurrent launches (+ classify, scatter)"})
+                "pu_per_s": len(jobs) / wall, "kernels": "fme::k_tz_staged<4,8>, <8,4>, <8,8>: a workgroup per (kernel, reference, CTU) group with "
+                             "its search area in LDS, one wave per PU, three concurrent launches (+ classify, scatter, "
+                             "k_tz_pair_count / _scan / _scatter)"})
     out["roofline"] = tz_roofline(jobs, ext, pics, t)
     if "cpu_baseline" in out:
         out["speedup_vs_cpu_1core"] = out["pu_per_s"] / out["cpu_baseline"]["value"]
