@@ -901,6 +901,8 @@ static int tz_run(fme_ctx* c, fme_job* d_jobs, const fme_tz_ext* d_ext, uint32_t
   a.n = n;
   a.use_hadamard = c->cfg.use_hadamard ? 1 : 0;
   a.fen = c->cfg.fast_inter_mode;
+  a.nn_in = c->nn_in;   // FME_JOB_NN_IN jobs (the B producer's bi rounds) pass k_classify with their rows
+  a.nn_in_cap = c->nn_in_cap;
   WorkBufs w = work_bufs(c);
   if (c->profiling) {
     if (!c->ev_tz[0]) {
@@ -2641,12 +2643,11 @@ int fme_pred_inter_b(fme_ctx* c, const fme_pu_req_b* reqs, fme_pu_res_b* res, in
     HIP_TRY(hipMemsetAsync(c->d_key_invalid.p, 0, sizeof(int32_t), s));
     BiKeyArgs ka{c->d_bikey.p, c->d_pics.p, c->d_keys.p, (int32_t)keyt.size(), nullptr, (int64_t)key_total};
     HIP_TRY(launch_bi_key(ka, s));
-    rc = tz_run_host(c, bj.data(), be.data(), nullptr, (int)bj.size(), stream, nullptr);
-    if (rc) return rc;
     // the round's bi jobs alone: in call order each sits right after its request's uni jobs, reads
     // the carried NN state there and writes none (TEncSearch.cpp:88-134), so each is refined as an
     // FME_JOB_NN_IN job whose row is that state (rowst, computed once from the uni records) instead
-    // of refining every uni job again around them
+    // of refining every uni job again around them.  The jobs go up once: the bi-pred integer search
+    // (xPatternSearch) writes their MVs in place and the refinement reads them there.
     const int nbj = (int)bj.size();
     HIP_TRY(c->h_pi_seq.reserve((size_t)nbj));
     HIP_TRY(c->h_pi_rs.reserve((size_t)nbj));
@@ -2665,14 +2666,18 @@ int fme_pred_inter_b(fme_ctx* c, const fme_pu_req_b* reqs, fme_pu_res_b* res, in
     HIP_TRY(c->d_jobs.reserve(nbj));
     HIP_TRY(c->d_res.reserve(nbj));
     HIP_TRY(c->d_mv.reserve(nbj));
+    HIP_TRY(c->d_tz_ext.reserve(nbj));
+    HIP_TRY(c->d_tz_sad.reserve(nbj));
     HIP_TRY(c->d_tz_nn_in.reserve((size_t)nbj * 9));
     HIP_TRY(hipMemcpyAsync(c->d_jobs.p, seq, (size_t)nbj * sizeof(fme_job), hipMemcpyHostToDevice, s));
+    HIP_TRY(hipMemcpyAsync(c->d_tz_ext.p, be.data(), (size_t)nbj * sizeof(fme_tz_ext), hipMemcpyHostToDevice, s));
     HIP_TRY(hipMemcpyAsync(c->d_tz_nn_in.p, rows, (size_t)nbj * 9 * sizeof(uint32_t), hipMemcpyHostToDevice, s));
     const uint32_t* const keep_in = c->nn_in;
     const int keep_cap = c->nn_in_cap;
     c->nn_in = c->d_tz_nn_in.p;
     c->nn_in_cap = nbj;
-    rc = refine_batch(c, c->d_jobs.p, c->d_res.p, c->d_mv.p, nbj, s);
+    rc = tz_run(c, c->d_jobs.p, c->d_tz_ext.p, c->d_tz_sad.p, nbj, stream, nullptr);
+    if (!rc) rc = refine_batch(c, c->d_jobs.p, c->d_res.p, c->d_mv.p, nbj, s);
     c->nn_in = keep_in;
     c->nn_in_cap = keep_cap;
     if (rc) return rc;
