@@ -195,7 +195,10 @@ __device__ __forceinline__ bool two_point_has_more(const Tz& s) {
 // padded-picture semantics of the global loads (rows and columns clamped).  A candidate window that
 // lies inside the tile is read from LDS, any other from global memory, so the results do not
 // depend on the staging.
-constexpr int kTileM = 72;
+#ifndef FME_TZS_MARGIN
+#define FME_TZS_MARGIN 72
+#endif
+constexpr int kTileM = FME_TZS_MARGIN;
 constexpr int kTileWD = (64 + 2 * kTileM + 3 + 8 + 3) / 4;   // dwords per row (x0 aligned down to 4)
 constexpr int kTileH = 64 + 2 * kTileM;
 struct TileRef {
