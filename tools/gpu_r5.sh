@@ -112,6 +112,8 @@ for step in "$@"; do
          run tzo_def2 200 python -u tools/tz_probe.py gpurun_out/tzo_def2.npz && \
          FME_LIB_PATH=$PWD/hm16.9-nn_fme_amd/variants/ord/libfme_amd.so run tzo_ord2 200 python -u tools/tz_probe.py gpurun_out/tzo_ord2.npz && \
          python3 -c "import numpy as np; a=np.load('gpurun_out/tzo_def.npz'); b=np.load('gpurun_out/tzo_ord.npz'); print('identical', all((a[k]==b[k]).all() for k in a.files))" ;;
+    tlc1k) run tlc1k 200 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/tlc1k -o run -- python3 bench.py --workload c1 --no-cpu-baseline --no-pi --no-tz --no-mc --parity-seconds 0 --steps 10 && \
+           python3 tools/timeline.py gpurun_out/tlc1k 3 8 > gpurun_out/tlc1k_timeline.txt ;;
     bigab) run bigab 400 python -u tools/ab_bench.py . variants/big --rounds 4 && bash tools/gpu_r5.sh bench1 bench2 ;;
     bench1) run bench1 300 python -u bench.py --no-pi --no-tz --no-mc --cpu-seconds 3 --parity-seconds 10 ;;
     bench2) run bench2 300 python -u -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --steps 6 --warmup 2 --no-pi --no-tz --no-mc --no-cpu-baseline --parity-seconds 0 --dist-backend gloo ;;
