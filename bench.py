@@ -664,14 +664,22 @@ def main():
     ap.add_argument("--dist-backend", default="nccl", help="torch.distributed backend for N > 1 (nccl = RCCL)")
     ap.add_argument("--parity-seconds", type=float, default=30.0,
                     help="bound of the after-run check of one timed step against oracle/_ref (0: skip)")
-    ap.add_argument("--download-engine", choices=("kernel", "blit", "sdma"), default="blit",
-                    help="results download: the library's few-workgroup copy kernel (fme_download_device) "
-                         "or hipMemcpyAsync (a blit kernel of hundreds of workgroups; the default: in the "
-                         "pipeline the copy kernel's workgroups wait for the persistent search's slots, "
-                         "1.39 against 1.22 ms per step, profiles/r05_ab.log)")
+    ap.add_argument("--download-engine", choices=("kernel", "blit", "sdma"), default="sdma",
+                    help="results download: a copy engine (hipMemcpyDeviceToDeviceNoCU into the pinned rows, the "
+                         "default: no CUs), the library's few-workgroup copy kernel (fme_download_device) or "
+                         "hipMemcpyAsync (a ROCclr blit kernel of hundreds of workgroups beside the search)")
     ap.add_argument("--download-wgs", type=int, default=8, help="workgroups of the download kernel")
+    ap.add_argument("--copy-streams", type=int, choices=(1, 2), default=1,
+                    help="1: uploads and downloads in series on one copy stream (default); 2: downloads on their "
+                         "own stream (round 5's layout)")
+    ap.add_argument("--slots", type=int, default=3, help="job / result buffer ring depth of the replay")
+    ap.add_argument("--max-ahead", type=int, default=4,
+                    help="steps the host may queue ahead of the device (0: unbounded)")
+    ap.add_argument("--no-packed", action="store_true",
+                    help="upload 32-byte fme_job rows instead of 16-byte fme_job_packed rows")
     ap.add_argument("--no-pcie", action="store_true",
-                    help="skip the PCIe-inclusive pass (profiling runs: its copies would overlap the kernels)")
+                    help="profiling runs: skip the PCIe-inclusive pass (its copies would overlap the kernels); "
+                         "`value` is then the HBM-resident rate and says so")
     ap.add_argument("--search-reserve", type=int, default=0,
                     help="resident search workgroups left free for the download kernel (fme_set_search_reserve)")
     ap.add_argument("--download", choices=("deferred", "immediate"), default=None,
@@ -776,25 +784,34 @@ def main():
     pool = np.stack([picture(t) for t in range(8)])
     steps_total = args.warmup + args.steps
     defer = (args.download or wl.get("download", "deferred")) == "deferred"
+    if args.no_pcie and world > 1:
+        # the sharded resident pass re-runs each step's carried-state prefix, whose length the PCIe
+        # pass measures (FrameReplay.finish)
+        raise SystemExit("--no-pcie needs one rank (the NN-state fix-up length comes from the PCIe pass)")
     # bi-pred keys (configs[3]): every step builds its frame's removeHighFreq keys on the device from
     # that frame's pictures (fme_build_bipred_keys_device, k_bi_key) inside the timed step
     rep = FrameReplay(ctx, jobs, pool, lambda f: frame_lambda(wl, f), steps_total, frames_per_step=FPS,
                       world=world, rank=rank, device=dev, defer_download=defer,
                       key_reqs=key_reqs, key_count=len(keys) if keys is not None else 0, nn_rows=nn_rows,
                       download_engine=args.download_engine, download_wgs=args.download_wgs,
-                      search_reserve=args.search_reserve)
+                      search_reserve=args.search_reserve, packed=not args.no_packed,
+                      copy_streams=args.copy_streams, slots=args.slots, max_ahead=args.max_ahead)
     n = rep.n
     rep.prime()
 
     for s in range(args.warmup):
         rep.issue(s, prefetch=s + 1 < args.warmup)   # the first timed step uploads its own inputs
     rep.drain()
-    # the NN_pred state the first timed step starts from (untimed), for the after-run parity check
+    # the NN_pred state the first timed step starts from (untimed), for the after-run checks
     state0 = ctx.nn_get_state() if world == 1 else None
 
-    # ---- PCIe-inclusive pass (the `pcie_inclusive` key and the parity leg's step): H2D (jobs,
-    # originals, reconstructions + RCCL point-to-point) -> refine -> D2H of the 16-byte results, two
-    # steps in flight on separate copy / compute streams; the NN-state chain fix-up when sharded ----
+    # ---- `value`: SURVEY.md §8(d)'s timing, from the first H2D of job descriptors to the last D2H
+    # of results.  Per step: H2D of the jobs (16-byte packed rows + one key base per 64 jobs), the
+    # frames' originals and one reconstructed reference per frame (RCCL point-to-point to the ranks
+    # that reference it when sharded), refine, D2H of the 16-byte fme_mv_result per job; all copies
+    # in series on one copy stream beside the batch stream; the NN-state chain fix-up when sharded.
+    # The interpreter's garbage collector is off inside the timed loops (a C++ host has none). ----
+    import gc
     fixed_pcie, value_pcie, elapsed_pcie, snap = 0, None, None, None
     if args.no_pcie:   # (profiling runs) the timed steps' inputs staged into HBM untimed instead
         for s in range(args.warmup, steps_total):
@@ -803,6 +820,9 @@ def main():
     else:
         if world > 1:
             dist.barrier()
+        gc.collect()
+        gc.disable()
+        rep.host_ms, rep.host_seg = [], []
         torch.cuda.synchronize(dev)
         t0 = time.perf_counter()
         for s in range(args.warmup, steps_total):
@@ -812,9 +832,11 @@ def main():
         if world > 1:
             dist.barrier()
         elapsed_pcie = max_over_ranks(time.perf_counter() - t0, dev, world, args.dist_backend)
+        gc.enable()
         rep.check_status(args.warmup)   # no timed step may have been rejected on the device
         snap = rep.results(args.warmup).copy() if args.parity_seconds > 0 else None
         value_pcie = world * n * args.steps / elapsed_pcie
+    host_ms = np.asarray(rep.host_ms, dtype=np.float64)
 
     parity = None
     if rank == 0 and world == 1 and args.parity_seconds > 0 and not args.no_pcie:
@@ -825,19 +847,24 @@ def main():
             now = rep.results(args.warmup)
             parity["rows_changed_since_timed_region"] = int((now != snap).sum())
 
-    # ---- timed region (`value`): the same steps with every input already resident in HBM (the
-    # pass above uploaded and exchanged each step's pictures, jobs, keys requests and NN rows into
-    # per-step buffers) and the results left in HBM; per step: bind, device-built keys (configs[3]),
-    # refine; the NN-state chain fix-up on the device when sharded ----
+    # ---- `resident`: the same steps with every input already resident in HBM (the pass above
+    # uploaded and exchanged each step's pictures, jobs, key requests and NN rows) and the results
+    # left there; per step: bind, device-built keys (configs[3]), refine; the NN-state chain fix-up
+    # on the device when sharded.  At one rank its timed steps start from the PCIe pass's first NN
+    # state, so every step's results must equal the PCIe pass's bit for bit (checked below). ----
     rep.resident_outputs(0, steps_total)
     prefix = rep.last_prefix if world > 1 else 0
     for s in range(args.warmup):
         rep.issue_resident(s)
+    if state0 is not None:
+        ctx.nn_set_state(state0)   # stream-ordered: applied before the first timed batch
     torch.cuda.synchronize(dev)
     ctx.set_profiling(True)
     ctx.accumulated_timings(reset=True)
     if world > 1:
         dist.barrier()
+    gc.collect()
+    gc.disable()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     for s in range(args.warmup, steps_total):
@@ -847,33 +874,67 @@ def main():
     if world > 1:
         dist.barrier()
     elapsed = max_over_ranks(time.perf_counter() - t0, dev, world, args.dist_backend)
+    gc.enable()
     nb, acc = ctx.accumulated_timings(reset=True)
     ctx.set_profiling(False)
     tm = {k: v / max(nb, 1) for k, v in acc.items()}
-    value = world * n * args.steps / elapsed
+    value_res = world * n * args.steps / elapsed
     from nnfme.abi import RES_REJECTED
-    last = rep.r_out[steps_total - 1].cpu().numpy().view(MV_RESULT_DTYPE)
-    if np.any(last["status"] & RES_REJECTED):
-        raise RuntimeError("a resident step's batch was rejected on the device")
-    pcie = None if args.no_pcie else {"value": value_pcie, "unit": "PU/s", "ms_per_step": elapsed_pcie / args.steps * 1e3,
-            "timed": "per step: H2D of the jobs (32 B each), of the frames' originals and of one "
-                     "reconstructed reference per frame (when sharded: RCCL point-to-point sends to the "
-                     "<= 3 other ranks whose frames reference it), refine, D2H of the 16-byte fme_mv_result "
-                     "per job; two steps in flight on separate copy / compute streams"
-                     + ("; NN-state chain fix-up included" if world > 1 else ""),
-            "download": (f"fme_download_device ({args.download_wgs} workgroups of 256 lanes, non-temporal "
-                         f"16-byte stores into the pinned rows)" if args.download_engine == "kernel"
-                         else "hipMemcpyAsync DeviceToDeviceNoCU into the pinned rows (copy engine)"
-                         if args.download_engine == "sdma" else "hipMemcpyAsync (ROCclr blit kernel)"),
-            "search_reserve": args.search_reserve,
-            "of_resident": value_pcie / value,
-            "note": "45.5 MB over PCIe per 1080p step bound it (DESIGN.md §5)"}
+    res_vs_pcie = None
+    if not args.no_pcie:
+        diff_steps = []
+        for s in range(args.warmup, steps_total):
+            got = rep.r_out[s].cpu().numpy().view(MV_RESULT_DTYPE)
+            if not np.array_equal(got, rep.results(s)):
+                diff_steps.append(s)
+        res_vs_pcie = {"steps_compared": args.steps, "steps_differing": diff_steps,
+                       "equal": not diff_steps, "rank": rank,
+                       "how": "every timed step's 16-byte records of the resident pass against the PCIe pass's "
+                              "downloaded rows, same NN start state" + (" (after the carried-state fix-up)"
+                                                                         if world > 1 else "")}
+        if diff_steps:
+            raise RuntimeError(f"resident pass differs from the PCIe pass on steps {diff_steps}")
+    else:
+        last = rep.r_out[steps_total - 1].cpu().numpy().view(MV_RESULT_DTYPE)
+        if np.any(last["status"] & RES_REJECTED):
+            raise RuntimeError("a resident step's batch was rejected on the device")
+    if args.no_pcie:
+        value, ms_step, value_kind = value_res, elapsed / args.steps * 1e3, "resident (--no-pcie profiling run)"
+    else:
+        value, ms_step, value_kind = value_pcie, elapsed_pcie / args.steps * 1e3, "pcie_inclusive (SURVEY.md §8(d))"
+    resident = {"value": value_res, "unit": "PU/s", "ms_per_step": elapsed / args.steps * 1e3,
+                "timed": "per step, inputs resident in HBM: bind the step's pictures and lambdas, build its bi-pred "
+                         "keys on the device (configs[3]), refine the frame's jobs into a device result buffer"
+                         + ("; NN-state chain fix-up on the device included" if world > 1 else ""),
+                **({"of_resident_pcie": value_pcie / value_res} if value_pcie else {}),
+                **({"equals_pcie_pass": res_vs_pcie} if res_vs_pcie else {})}
+    d2h = n * MV_RESULT_DTYPE.itemsize
+    pcie = None if args.no_pcie else {
+        "timed": "from the first H2D of job descriptors to the last D2H of results (SURVEY.md §8(d)): per step H2D "
+                 "of the jobs, the frames' originals and one reconstructed reference per frame (when sharded: "
+                 "RCCL point-to-point sends to the <= 3 other ranks whose frames reference it), refine, D2H of "
+                 "the 16-byte fme_mv_result per job" + ("; NN-state chain fix-up included" if world > 1 else ""),
+        "jobs_upload": ("fme_job_packed (16 B per job + 4 B per 64 jobs), unpacked on the device by "
+                        "fme_refine_mv_packed_device" if rep.packed else
+                        "fme_job (32 B per job)" + (f"; packing refused: {rep.packed_reason}"
+                                                    if rep.packed_reason else "")),
+        "h2d_bytes_per_step": rep.h2d_bytes_per_step(), "d2h_bytes_per_step": d2h,
+        "copies": (f"one copy stream, in series: H2D(k+1) then D2H(k-1) once step k's search runs; ring of "
+                   f"{rep.R} job / result slots" if args.copy_streams == 1 else
+                   "uploads and downloads on separate copy streams"),
+        "download": (f"fme_download_device ({args.download_wgs} workgroups of 256 lanes, non-temporal "
+                     f"16-byte stores into the pinned rows)" if args.download_engine == "kernel"
+                     else "hipMemcpyAsync DeviceToDeviceNoCU into the pinned rows (copy engine, no CUs)"
+                     if args.download_engine == "sdma" else "hipMemcpyAsync (ROCclr blit kernel)"),
+        "search_reserve": args.search_reserve,
+        "max_ahead": args.max_ahead,
+        "host_issue_ms": {"median": float(np.median(host_ms)), "max": float(host_ms.max()),
+                          "sum": float(host_ms.sum()), "per_step": [round(float(v), 3) for v in host_ms],
+                          "slowest_step_parts": dict(zip(rep.host_seg_names, rep.host_seg[int(host_ms.argmax())]))}
+        if host_ms.size else None,
+        "gc": "off inside the timed loops"}
     if world > 1 and pcie:
         pcie["nn_state_fixup_jobs_rank0"] = int(fixed_pcie)
-        # sharded steps start from a reset state and are fixed up with their true carry-in, so the
-        # resident pass must reproduce the PCIe pass's (host) results bit for bit
-        got = rep.r_out[args.warmup].cpu().numpy().view(MV_RESULT_DTYPE)
-        pcie["resident_equals_pcie_rank0"] = bool(np.array_equal(got, rep.results(args.warmup)))
 
     mc = mc_leg(dev, torch.cuda.current_stream(dev), reps=max(5, args.steps // 2)) \
         if rank == 0 and not args.no_mc and W == 1920 and NN != 2 and BD == 8 else None
@@ -899,10 +960,11 @@ def main():
             "metric": METRIC,
             "value": value,
             "unit": "PU/s",
+            "value_kind": value_kind,
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
-            "ms_per_step": elapsed / args.steps * 1e3,
+            "ms_per_step": ms_step,
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
@@ -926,10 +988,7 @@ def main():
                        # what torch.distributed actually ran (None: one process, no process group)
                        "dist_backend": dist.get_backend() if dist.is_initialized() else None,
                        "pg_world_size": dist.get_world_size() if dist.is_initialized() else 1,
-                       "timed": "per step, inputs resident in HBM: bind the step's pictures and lambdas, build "
-                                "its bi-pred keys on the device (configs[3]), refine the frame's jobs into a "
-                                "device result buffer" + ("; NN-state chain fix-up on the device included"
-                                                          if world > 1 else "")},
+                       "timed": (pcie or resident)["timed"]},
             "roofline": {
                 "bound": "valu",
                 "achieved": valu,
@@ -964,6 +1023,7 @@ def main():
             out["speedup_vs_cpu_all_cores"] = value / cpu["cpu_baseline_all_cores"]["value"]
         if pcie:
             out["pcie_inclusive"] = pcie
+        out["resident"] = resident
         if parity:
             out["parity"] = parity
         if world > 1:
@@ -978,7 +1038,12 @@ def main():
             out["pred_inter_search"] = pi
         print(json.dumps(out), flush=True)
 
+    # every HIP resource of the run released here, before interpreter exit (no finaliser of ours
+    # runs after the HIP runtime or a profiler's exit handlers)
+    rep.close()
+    del rep
     ctx.close()
+    torch.cuda.synchronize(dev)
     if world > 1:
         dist.destroy_process_group()
     return 0

@@ -168,6 +168,7 @@ struct fme_ctx {
   DevBuf<fme_job> d_jobs;      // staging for fme_refine (host arrays)
   DevBuf<fme_result> d_res;
   DevBuf<fme_mv_result> d_mv;   // staging for fme_refine_mv
+  DevBuf<fme_job> d_pk_jobs;    // fme_refine*_packed_device: the unpacked batch
   DevBuf<uint8_t> cls;
   DevBuf<int32_t> perm;
   DevBuf<fme_job> sjobs;
@@ -361,7 +362,7 @@ int fme_destroy(fme_ctx* c) {
   for (auto& e : c->ev_mc)
     if (e) (void)hipEventDestroy(e);
   c->d_pics.release(); c->d_mlambda.release(); c->d_keys.release(); c->d_nn.release(); c->d_net.release();
-  c->d_jobs.release(); c->d_res.release(); c->d_mv.release(); c->cls.release(); c->perm.release(); c->sjobs.release();
+  c->d_jobs.release(); c->d_res.release(); c->d_mv.release(); c->d_pk_jobs.release(); c->cls.release(); c->perm.release(); c->sjobs.release();
   c->counts.release(); c->blk_agg.release(); c->blk_prefix.release(); c->nn_state.release();
   c->d_sched.release();
   if (c->ev_done) (void)hipEventDestroy(c->ev_done);
@@ -801,7 +802,14 @@ static int refine_batch(fme_ctx* c, const fme_job* d_jobs, fme_result* d_res, fm
   if (c->ev_search) HIP_TRY(hipEventRecord(c->ev_search, s));
   // the lane kernel: every PU shape, one launch on the batch stream (8-bit); the pixel kernel at
   // bit depth 10 (fme_px.hip)
-  HIP_TRY(c->cfg.bit_depth > 8 ? launch_search_px(a, w, c->cfg.bit_depth, s) : launch_search_lane(a, w, c->search_reserve, s));
+  if (c->cfg.bit_depth > 8) {
+    // the small- and large-PU pixel kernels one after the other: side by side on two streams they
+    // took 11.5 ms per 1080p frame against 10.5 in series (profiles/r06_ab.log: their LDS and
+    // wave slots compete)
+    HIP_TRY(launch_search_px(a, w, c->cfg.bit_depth, s, nullptr));
+  } else {
+    HIP_TRY(launch_search_lane(a, w, c->search_reserve, s));
+  }
   if (prof) HIP_TRY(hipEventRecord(ev[4], s));
   if (prof) HIP_TRY(hipEventRecord(ev[5], s));
   HIP_TRY(c->cfg.nn_mode == 2
@@ -831,6 +839,115 @@ int fme_refine_mv_device(fme_ctx* c, const fme_job* d_jobs, fme_mv_result* d_out
   HIP_TRY(hipSetDevice(c->device));
   HIP_TRY(c->d_res.reserve(n));   // full records: context scratch
   return refine_batch(c, d_jobs, c->d_res.p, d_out, n, static_cast<hipStream_t>(stream));
+}
+
+// ---- packed jobs (include/fme.h fme_job_packed) -----------------------------------------------
+int fme_pack_jobs(const fme_job* jobs, int n, fme_job_packed* out, int32_t* key_base) {
+  if (n < 0 || (n > 0 && (!jobs || !out || !key_base))) return fail(FME_E_INVALID, "fme_pack_jobs: bad argument");
+  const int waves = (n + FME_PACK_WAVE - 1) / FME_PACK_WAVE;
+  for (int wv = 0; wv < waves; wv++) {
+    int64_t next = -1;   // where the wave's next keyed block must start (-1: no keyed job yet)
+    key_base[wv] = -1;
+    const int e = std::min(n, (wv + 1) * FME_PACK_WAVE);
+    for (int i = wv * FME_PACK_WAVE; i < e; i++) {
+      const fme_job& j = jobs[i];
+      const char* why = nullptr;
+      if ((j.x & 3) || (j.y & 3) || (j.w & 3) || (j.h & 3) || j.w < 4 || j.w > 64 || j.h < 4 || j.h > 64)
+        why = "PU off the 4x4 grid or not 4..64";
+      else if (j.x >= 8192 || j.y >= 8192) why = "x or y >= 8192";
+      else if (j.org_id >= 64 || j.ref_id >= 64 || j.lambda_id >= 32) why = "slot id >= 64 or lambda_id >= 32";
+      else if (j.flags & ~15u) why = "unknown flags";
+      else if (j.bits_in >= 64) why = "bits_in >= 64";
+      else if (j.mv_x <= -32767 || j.mv_x >= 32766 || j.mv_y <= -32767 || j.mv_y >= 32766) why = "int16-extreme mv";
+      else if (j.key_offset >= 0) {
+        if (next < 0) key_base[wv] = j.key_offset;
+        else if ((int64_t)j.key_offset != next) why = "key block not dense in job order within its wave";
+        next = (int64_t)j.key_offset + (int64_t)j.w * j.h;
+      }
+      if (why) return fail(FME_E_UNSUPPORTED, "fme_pack_jobs: job %d: %s (use fme_job)", i, why);
+      uint32_t rg = 0;
+      if (j.mv_y - 1 >= j.lt_y) rg |= FME_PK_RANGE_TOP;
+      if (j.mv_y + 1 <= j.rb_y) rg |= FME_PK_RANGE_BOTTOM;
+      if (j.mv_x - 1 >= j.lt_x) rg |= FME_PK_RANGE_LEFT;
+      if (j.mv_x + 1 <= j.rb_x) rg |= FME_PK_RANGE_RIGHT;
+      fme_job_packed p;
+      p.pu = (uint32_t)(j.x >> 2) | ((uint32_t)(j.y >> 2) << 11) | ((uint32_t)((j.w >> 2) - 1) << 22) |
+             ((uint32_t)((j.h >> 2) - 1) << 26);
+      p.ctl = (uint32_t)j.org_id | ((uint32_t)j.ref_id << 6) | ((uint32_t)j.lambda_id << 12) |
+              ((uint32_t)j.flags << 17) | ((uint32_t)(j.key_offset >= 0) << 21) | (rg << 22) |
+              ((uint32_t)j.bits_in << 26);
+      p.mv_x = j.mv_x;
+      p.mv_y = j.mv_y;
+      p.mvp_x = j.mvp_x;
+      p.mvp_y = j.mvp_y;
+      out[i] = p;
+    }
+  }
+  return FME_OK;
+}
+
+int fme_unpack_jobs(const fme_job_packed* packed, const int32_t* key_base, int n, fme_job* out) {
+  if (n < 0 || (n > 0 && (!packed || !key_base || !out))) return fail(FME_E_INVALID, "fme_unpack_jobs: bad argument");
+  int64_t next = 0;
+  for (int i = 0; i < n; i++) {
+    const fme_job_packed& p = packed[i];
+    if (i % FME_PACK_WAVE == 0) next = key_base[i / FME_PACK_WAVE];
+    fme_job j;
+    j.x = (uint16_t)((p.pu & 2047u) * 4u);
+    j.y = (uint16_t)(((p.pu >> 11) & 2047u) * 4u);
+    j.w = (uint8_t)((((p.pu >> 22) & 15u) + 1u) * 4u);
+    j.h = (uint8_t)((((p.pu >> 26) & 15u) + 1u) * 4u);
+    j.org_id = (uint8_t)(p.ctl & 63u);
+    j.ref_id = (uint8_t)((p.ctl >> 6) & 63u);
+    j.lambda_id = (uint8_t)((p.ctl >> 12) & 31u);
+    j.flags = (uint8_t)((p.ctl >> 17) & 15u);
+    const uint32_t rg = (p.ctl >> 22) & 15u;
+    j.bits_in = (uint16_t)(p.ctl >> 26);
+    j.mv_x = p.mv_x;
+    j.mv_y = p.mv_y;
+    j.mvp_x = p.mvp_x;
+    j.mvp_y = p.mvp_y;
+    j.lt_x = (int16_t)(p.mv_x - ((rg & FME_PK_RANGE_LEFT) ? 1 : 0));
+    j.rb_x = (int16_t)(p.mv_x + ((rg & FME_PK_RANGE_RIGHT) ? 1 : 0));
+    j.lt_y = (int16_t)(p.mv_y - ((rg & FME_PK_RANGE_TOP) ? 1 : 0));
+    j.rb_y = (int16_t)(p.mv_y + ((rg & FME_PK_RANGE_BOTTOM) ? 1 : 0));
+    if ((p.ctl >> 21) & 1u) {
+      j.key_offset = (int32_t)next;
+      next += (int64_t)j.w * j.h;
+    } else {
+      j.key_offset = -1;
+    }
+    out[i] = j;
+  }
+  return FME_OK;
+}
+
+static int refine_packed(fme_ctx* c, const fme_job_packed* d_jobs, const int32_t* d_key_base, fme_result* d_res,
+                         fme_mv_result* d_mv, int n, void* stream, const char* fn) {
+  if (!c || (n > 0 && (!d_jobs || !d_key_base || !(d_res || d_mv)))) return fail(FME_E_INVALID, "%s: null argument", fn);
+  if (n < 0) return fail(FME_E_INVALID, "%s: n = %d", fn, n);
+  if (n == 0) return FME_OK;
+  HIP_TRY(hipSetDevice(c->device));
+  HIP_TRY(c->d_pk_jobs.reserve(n));
+  if (!d_res) {
+    HIP_TRY(c->d_res.reserve(n));   // full records: context scratch
+    d_res = c->d_res.p;
+  }
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  HIP_TRY(launch_unpack_jobs(d_jobs, d_key_base, c->d_pk_jobs.p, n, s));
+  return refine_batch(c, c->d_pk_jobs.p, d_res, d_mv, n, s);
+}
+
+int fme_refine_packed_device(fme_ctx* c, const fme_job_packed* d_jobs, const int32_t* d_key_base, fme_result* d_res,
+                             int n, void* stream) {
+  if (c && n > 0 && !d_res) return fail(FME_E_INVALID, "fme_refine_packed_device: null argument");
+  return refine_packed(c, d_jobs, d_key_base, d_res, nullptr, n, stream, "fme_refine_packed_device");
+}
+
+int fme_refine_mv_packed_device(fme_ctx* c, const fme_job_packed* d_jobs, const int32_t* d_key_base,
+                                fme_mv_result* d_out, int n, void* stream) {
+  if (c && n > 0 && !d_out) return fail(FME_E_INVALID, "fme_refine_mv_packed_device: null argument");
+  return refine_packed(c, d_jobs, d_key_base, nullptr, d_out, n, stream, "fme_refine_mv_packed_device");
 }
 
 int fme_set_search_event(fme_ctx* c, void* event) {
@@ -880,7 +997,7 @@ int fme_refine_status(fme_ctx* c) {
 // integer MV there (the producer's m_integerMv2Nx2N), leaving jobs' mv_x / mv_y at the TZ best.
 // d_nn_in (may be null): FME_TZ_RING jobs run the backups' square + ring and write their NN inputs.
 static int tz_run(fme_ctx* c, fme_job* d_jobs, const fme_tz_ext* d_ext, uint32_t* d_sad, int n, void* stream,
-                  int16_t* d_emi, uint32_t* d_nn_in = nullptr) {
+                  int16_t* d_emi, uint32_t* d_nn_in = nullptr, int ext_stride = (int)sizeof(fme_tz_ext)) {
   if (!c || (n > 0 && (!d_jobs || !d_ext))) return fail(FME_E_INVALID, "fme_integer_search_device: null argument");
   NEED_8BIT(c, "fme_integer_search");
   if (n < 0) return fail(FME_E_INVALID, "fme_integer_search_device: n = %d", n);
@@ -937,6 +1054,7 @@ static int tz_run(fme_ctx* c, fme_job* d_jobs, const fme_tz_ext* d_ext, uint32_t
   ta.perm = c->perm.p;
   ta.jobs_out = d_jobs;
   ta.ext = d_ext;
+  ta.ext_stride = ext_stride;
   ta.sad = d_sad;
   ta.emi_mv = d_emi;
   ta.nn_in = d_nn_in;
@@ -1003,23 +1121,23 @@ static int tz_run(fme_ctx* c, fme_job* d_jobs, const fme_tz_ext* d_ext, uint32_t
 }
 
 static int tz_run_host(fme_ctx* c, fme_job* jobs, const fme_tz_ext* ext, uint32_t* sad, int n, void* stream,
-                       int16_t* emi, uint32_t* nn_in = nullptr) {
+                       int16_t* emi, uint32_t* nn_in = nullptr, int ext_stride = (int)sizeof(fme_tz_ext)) {
   if (!c || (n > 0 && (!jobs || !ext))) return fail(FME_E_INVALID, "fme_integer_search: null argument");
   NEED_8BIT(c, "fme_integer_search");
   if (n <= 0) return n == 0 ? FME_OK : fail(FME_E_INVALID, "fme_integer_search: n = %d", n);
   HIP_TRY(hipSetDevice(c->device));
   hipStream_t s = static_cast<hipStream_t>(stream);
   HIP_TRY(c->d_jobs.reserve(n));
-  HIP_TRY(c->d_tz_ext.reserve(n));
+  HIP_TRY(c->d_tz_ext.reserve(((size_t)n * ext_stride + sizeof(fme_tz_ext) - 1) / sizeof(fme_tz_ext)));
   HIP_TRY(c->d_tz_sad.reserve(n));
   if (emi) HIP_TRY(c->d_tz_emi.reserve((size_t)2 * n));
   if (nn_in) HIP_TRY(c->d_tz_nn_in.reserve((size_t)9 * n));
   HIP_TRY(hipMemcpyAsync(c->d_jobs.p, jobs, (size_t)n * sizeof(fme_job), hipMemcpyHostToDevice, s));
-  HIP_TRY(hipMemcpyAsync(c->d_tz_ext.p, ext, (size_t)n * sizeof(fme_tz_ext), hipMemcpyHostToDevice, s));
+  HIP_TRY(hipMemcpyAsync(c->d_tz_ext.p, ext, (size_t)n * ext_stride, hipMemcpyHostToDevice, s));
   // rows of jobs without FME_TZ_RING are left untouched: start from the caller's values
   if (nn_in) HIP_TRY(hipMemcpyAsync(c->d_tz_nn_in.p, nn_in, (size_t)9 * n * sizeof(uint32_t), hipMemcpyHostToDevice, s));
   int rc = tz_run(c, c->d_jobs.p, c->d_tz_ext.p, c->d_tz_sad.p, n, stream, emi ? c->d_tz_emi.p : nullptr,
-                  nn_in ? c->d_tz_nn_in.p : nullptr);
+                  nn_in ? c->d_tz_nn_in.p : nullptr, ext_stride);
   if (rc) return rc;
   HIP_TRY(hipMemcpyAsync(jobs, c->d_jobs.p, (size_t)n * sizeof(fme_job), hipMemcpyDeviceToHost, s));
   if (sad) HIP_TRY(hipMemcpyAsync(sad, c->d_tz_sad.p, (size_t)n * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
@@ -1090,6 +1208,7 @@ static int tz_by_level(fme_ctx* c, std::vector<fme_job>& jobs, std::vector<fme_t
   ta.a.fen = c->cfg.fast_inter_mode;
   ta.jobs_out = c->d_jobs.p;
   ta.ext = c->d_tz_ext.p;
+  ta.ext_stride = (int)sizeof(fme_tz_ext);
   ta.emi_mv = c->d_tz_emi.p;
   const TzChain ch{c->d_ch_i32.p, max_level + 1};
   HIP_TRY(launch_tz_levels(ta, ch, off.data(), s));
@@ -1115,6 +1234,17 @@ int fme_integer_search_device(fme_ctx* c, fme_job* d_jobs, const fme_tz_ext* d_e
 
 int fme_integer_search(fme_ctx* c, fme_job* jobs, const fme_tz_ext* ext, uint32_t* sad, int n, void* stream) {
   return tz_run_host(c, jobs, ext, sad, n, stream, nullptr);
+}
+
+int fme_integer_search2_device(fme_ctx* c, fme_job* d_jobs, const fme_tz_ext2* d_ext, uint32_t* d_sad, int n,
+                               void* stream) {
+  return tz_run(c, d_jobs, reinterpret_cast<const fme_tz_ext*>(d_ext), d_sad, n, stream, nullptr, nullptr,
+                (int)sizeof(fme_tz_ext2));
+}
+
+int fme_integer_search2(fme_ctx* c, fme_job* jobs, const fme_tz_ext2* ext, uint32_t* sad, int n, void* stream) {
+  return tz_run_host(c, jobs, reinterpret_cast<const fme_tz_ext*>(ext), sad, n, stream, nullptr, nullptr,
+                     (int)sizeof(fme_tz_ext2));
 }
 
 int fme_integer_search_ring_device(fme_ctx* c, fme_job* d_jobs, const fme_tz_ext* d_ext, uint32_t* d_sad,
@@ -1884,6 +2014,7 @@ static int tz_levels_device(fme_ctx* c, const fme_job* jobs, const fme_tz_ext* e
     ta.a.fen = c->cfg.fast_inter_mode;
     ta.jobs_out = c->d_pi_jobs.p;
     ta.ext = c->d_pi_ext.p;
+    ta.ext_stride = (int)sizeof(fme_tz_ext);
     ta.emi_mv = c->d_tz_emi.p;
     const TzChain ch{c->d_ch_i32.p, max_level + 1};
     HIP_TRY(launch_tz_levels(ta, ch, off.data(), s));

@@ -173,7 +173,21 @@ struct TzArgs {
   uint32_t* sad;              // may be null
   int16_t* emi_mv;            // [n][2] or null: the MV after the EMI square step (uni-pred EMI jobs)
   uint32_t* nn_in;            // [n][9] or null: FME_TZ_RING jobs' NN inputs (array_e[index_ref..+7], C)
+  int32_t ext_stride;         // bytes per ext record: sizeof(fme_tz_ext), or sizeof(fme_tz_ext2) (predictors)
 };
+// Integer-search ext record i (either layout) and, for fme_tz_ext2 records, neighbour predictor k.
+__device__ __forceinline__ fme_tz_ext tz_ext_at(const TzArgs& ta, int i) {
+  return *reinterpret_cast<const fme_tz_ext*>(reinterpret_cast<const uint8_t*>(ta.ext) + (size_t)ta.ext_stride * i);
+}
+__device__ __forceinline__ void tz_pred_at(const TzArgs& ta, int i, int k, int& x, int& y) {
+  if (ta.ext_stride < (int)sizeof(fme_tz_ext2)) {
+    x = y = 0;
+    return;
+  }
+  const fme_tz_ext2* e = reinterpret_cast<const fme_tz_ext2*>(reinterpret_cast<const uint8_t*>(ta.ext) + (size_t)ta.ext_stride * i);
+  x = e->preds[k][0];
+  y = e->preds[k][1];
+}
 int tz_kernel_of(int cls);    // 0: 4x8 units, 1: 8x4, 2: 8x8
 int tz_lanes_per_pu(int cls);
 // Host-built schedule of the integer-search kernels (passed by value).
@@ -227,7 +241,8 @@ hipError_t launch_put_tables(PicDesc* d_pics, double* d_ml, const TablesSlot* t_
 hipError_t launch_search_lane(const BatchArgs& a, const WorkBufs& w, int reserve, hipStream_t s);
 // Bit depth 10 (main10): the pixel-per-lane search (fme_px.hip), same records as the lane kernel;
 // pictures hold uint16 samples (PicDesc::luma reinterpreted, stride in samples).
-hipError_t launch_search_px(const BatchArgs& a, const WorkBufs& w, int bit_depth, hipStream_t s);
+// s_big (may be null: s): the stream of the large-PU kernel, run beside the small-PU one
+hipError_t launch_search_px(const BatchArgs& a, const WorkBufs& w, int bit_depth, hipStream_t s, hipStream_t s_big);
 struct NnIn11 {   // NN_pred() inputs of a single call: array_e slots[8], C, PUHeight, PUWidth
   uint32_t v[11];
 };
@@ -307,6 +322,10 @@ hipError_t launch_gather_jobs(const fme_job* src, const fme_tz_ext* src_ext, con
                               fme_tz_ext* dst_ext, int n, hipStream_t s);
 hipError_t launch_nn_tail(const BatchArgs& a, const WorkBufs& w, const float* nn_params,
                           int state_in, hipStream_t s);
+// fme_job_packed -> fme_job (fme_refine*_packed_device): one lane per job, key offsets by a
+// per-wave scan from key_base[i / 64]
+hipError_t launch_unpack_jobs(const fme_job_packed* src, const int32_t* key_base, fme_job* dst, int n,
+                              hipStream_t s);
 
 // The tail kernels' output: xMotionEstimation's MV / cost / bits with the NN class and status,
 // into the full record or, for fme_refine_mv*, the compact one alone.

@@ -627,6 +627,61 @@ hipError_t launch_download(const void* src, void* dst, size_t n16, int wgs, hipS
   return hipGetLastError();
 }
 
+// ---------------------------------------------------------------------------------------
+// packed jobs (fme_job_packed, include/fme.h) -> fme_job.  Lane i unpacks job i; a wave is 64
+// consecutive jobs, whose keyed blocks follow key_base[wave] densely in job order, so each lane's
+// key offset is the base plus the exclusive sum of w*h over the wave's earlier keyed jobs.  The
+// range words are the canonical mv -/+ range bit, which gives the EMI step's four tests
+// (xTZ8PointSquareSearch, TEncSearch.cpp:1341-1376) the packed answers.
+// ---------------------------------------------------------------------------------------
+__global__ __launch_bounds__(kBlock) void k_unpack_jobs(const fme_job_packed* __restrict__ src,
+                                                       const int32_t* __restrict__ key_base,
+                                                       fme_job* __restrict__ dst, int n) {
+  const int i = blockIdx.x * kBlock + threadIdx.x;
+  fme_job_packed p{};
+  if (i < n) p = src[i];
+  const uint32_t pu = p.pu, ctl = p.ctl;
+  const int w = (int)(((pu >> 22) & 15u) + 1u) * 4, h = (int)(((pu >> 26) & 15u) + 1u) * 4;
+  const bool keyed = i < n && ((ctl >> 21) & 1u);
+  const int lane = (int)(threadIdx.x & 63);
+  int s = keyed ? w * h : 0;   // inclusive scan over the wave
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const int o = __shfl_up(s, off, 64);
+    if (lane >= off) s += o;
+  }
+  if (i >= n) return;
+  const int base = key_base[i >> 6];
+  fme_job j;
+  j.x = (uint16_t)((pu & 2047u) * 4u);
+  j.y = (uint16_t)(((pu >> 11) & 2047u) * 4u);
+  j.w = (uint8_t)w;
+  j.h = (uint8_t)h;
+  j.org_id = (uint8_t)(ctl & 63u);
+  j.ref_id = (uint8_t)((ctl >> 6) & 63u);
+  j.lambda_id = (uint8_t)((ctl >> 12) & 31u);
+  j.flags = (uint8_t)((ctl >> 17) & 15u);
+  const uint32_t rg = (ctl >> 22) & 15u;
+  j.bits_in = (uint16_t)(ctl >> 26);
+  j.mv_x = p.mv_x;
+  j.mv_y = p.mv_y;
+  j.mvp_x = p.mvp_x;
+  j.mvp_y = p.mvp_y;
+  j.lt_x = (int16_t)(p.mv_x - ((rg & FME_PK_RANGE_LEFT) ? 1 : 0));
+  j.rb_x = (int16_t)(p.mv_x + ((rg & FME_PK_RANGE_RIGHT) ? 1 : 0));
+  j.lt_y = (int16_t)(p.mv_y - ((rg & FME_PK_RANGE_TOP) ? 1 : 0));
+  j.rb_y = (int16_t)(p.mv_y + ((rg & FME_PK_RANGE_BOTTOM) ? 1 : 0));
+  j.key_offset = keyed ? base + s - w * h : -1;
+  dst[i] = j;
+}
+
+hipError_t launch_unpack_jobs(const fme_job_packed* src, const int32_t* key_base, fme_job* dst, int n,
+                              hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_unpack_jobs, dim3((n + kBlock - 1) / kBlock), dim3(kBlock), 0, s, src, key_base, dst, n);
+  return hipGetLastError();
+}
+
 hipError_t launch_nn_tail(const BatchArgs& a, const WorkBufs& w, const float* nn_params,
                           int state_in, hipStream_t s) {
   const int nb = nblocks(a.n);

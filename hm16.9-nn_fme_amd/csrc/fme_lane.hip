@@ -63,16 +63,51 @@
 #ifndef FME_LANE_SHARE
 #define FME_LANE_SHARE 1
 #endif
+// 1: the 2-D passes' second stage with taps scaled by 16, so a pair of outputs is packed by one
+// v_perm of the two sums' high halves ((16 s) >> 16 == s >> 12) and clipped as a packed pair
+// (v_pk_max_i16 / v_pk_min_i16), and the 1-D horizontal rows of the half stage shifted and clipped
+// as the packed pairs the vertical pass already holds: 3 instructions per output pair instead of 5
+// (two shifts, two med3, one perm).  0: per-output shift and clamp.
+#ifndef FME_LANE_PK16
+#define FME_LANE_PK16 0
+#endif
 // occupancy target (waves per SIMD) that bounds the register allocation
 #ifndef FME_LANE_WAVES
 #define FME_LANE_WAVES 2
 #endif
 
+// 1: a diagnostic build (make variant NAME=stamps DEFS=-DFME_LANE_STAMPS=1, tools/lane_stamps.py):
+// s_memtime stamps at the phase boundaries of every lane_unit call, summed per (class, phase) into
+// a debug buffer of their own (g_lane_stamps, read by fme_debug_lane_stamps); each boundary first
+// waits for the wave's outstanding loads, so a phase's share includes the memory latency it
+// exposes.  Never the product build: the waits forbid overlaps the real kernel has.
+#ifndef FME_LANE_STAMPS
+#define FME_LANE_STAMPS 0
+#endif
+
 namespace fme {
+#if FME_LANE_STAMPS
+// [class][phase]: 0 job + key loads, 1 EMI step, 2 sub-pel window + key, 3 half-pel stage,
+// 4 quarter-pel stage, 5 record stores, 6 calls (wave tiles), 7 unused
+__device__ unsigned long long g_lane_stamps[kNumClasses][8];
+#endif
 namespace {
 using namespace simd;
 
 #define FME_AI __attribute__((always_inline))
+
+#if FME_LANE_STAMPS
+__device__ __forceinline__ unsigned long long lane_stamp() {
+  unsigned long long t;
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t) :: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+  return t;
+}
+#define FME_STAMP(k) const unsigned long long stamp_##k = lane_stamp()
+#else
+#define FME_STAMP(k) (void)0
+#endif
 
 constexpr int kLaneNT = 256;
 
@@ -183,10 +218,26 @@ __device__ __forceinline__ int tap(int f, int k) {
   return f == 0 ? t0 : (f == 1 ? t1 : (f == 2 ? t2 : t3));
 }
 // Coefficient pairs for a vertical 8-tap filter of fraction f whose taps start `o` rows into
-// a span of 10 rows read as 5 packed row pairs: pair t = (tap(2t - o), tap(2t + 1 - o)).
+// a span of 10 rows read as 5 packed row pairs: pair t = (tap(2t - o), tap(2t + 1 - o)), scaled by
+// kVS (FME_LANE_PK16: 16).
+constexpr int kVS = FME_LANE_PK16 ? 16 : 1;
 __device__ __forceinline__ void vpairs(int f, int o, uint32_t (&c)[5]) {
 #pragma unroll
-  for (int t = 0; t < 5; t++) c[t] = p16(tap(f, 2 * t - o), tap(f, 2 * t + 1 - o));
+  for (int t = 0; t < 5; t++) c[t] = p16(kVS * tap(f, 2 * t - o), kVS * tap(f, 2 * t + 1 - o));
+}
+// (s0 >> 12, s1 >> 12) clipped to the s - 128 range, packed, from second-stage sums scaled by kVS.
+__device__ __forceinline__ uint32_t pk_round2d(int s0, int s1) {
+  if constexpr (FME_LANE_PK16) {
+    const v2s m = up(__builtin_amdgcn_perm((uint32_t)s1, (uint32_t)s0, 0x07060302u));   // high halves
+    return pk(__builtin_elementwise_min(__builtin_elementwise_max(m, v2s{-128, -128}), v2s{127, 127}));
+  } else {
+    return pack2(clamp_s8(s0 >> 12), clamp_s8(s1 >> 12));
+  }
+}
+// (h0 >> 6, h1 >> 6) clipped, from the packed pair (h0, h1) of 1-D sums (+32 carried)
+__device__ __forceinline__ uint32_t pk_round1d(uint32_t hp) {
+  const v2s m = up(hp) >> v2s{6, 6};
+  return pk(__builtin_elementwise_min(__builtin_elementwise_max(m, v2s{-128, -128}), v2s{127, 127}));
 }
 
 // ---- the key block (key - 128 as packed int16 row pairs): K(x, j) = rows (2j, 2j+1) of column x --
@@ -479,8 +530,9 @@ __device__ __forceinline__ void half_sides(uint32_t (&v)[UH + 8][UW / 4 + 2], co
   constexpr int RV = UH + 8, UJ = UH / 2;
   uint32_t c2lo, c2hi;
   taps8(2, c2lo, c2hi);
-  const uint32_t c16[4] = {p16(-1, 4), p16(-11, 40), p16(40, -11), p16(4, -1)};
-  const uint32_t c16o[5] = {p16(0, -1), p16(4, -11), p16(40, 40), p16(-11, 4), p16(-1, 0)};
+  const uint32_t c16[4] = {p16(-kVS, 4 * kVS), p16(-11 * kVS, 40 * kVS), p16(40 * kVS, -11 * kVS), p16(4 * kVS, -kVS)};
+  const uint32_t c16o[5] = {p16(0, -kVS), p16(4 * kVS, -11 * kVS), p16(40 * kVS, 40 * kVS), p16(-11 * kVS, 4 * kVS),
+                            p16(-kVS, 0)};
   uint32_t XS[6][UW][UJ];
 #pragma unroll
   for (int k = 0; k <= UW; k++) {
@@ -492,7 +544,7 @@ __device__ __forceinline__ void half_sides(uint32_t (&v)[UH + 8][UW / 4 + 2], co
 #pragma unroll
     for (int r = 0; r < RV; r += 2) HP[r / 2] = pack2(hv[r], hv[r + 1]);
     uint32_t X0[UJ], XM[UJ], XP[UJ];   // (s,0), (s,-1), (s,1) of this column
-    int v2[UH + 1];
+    int v2[UH + 1];   // second-stage sums (FME_LANE_PK16: x 16), rounded below
 #pragma unroll
     for (int i = 0; i <= UH; i++) {   // half rows between window rows i+3, i+4
       int acc;
@@ -506,13 +558,19 @@ __device__ __forceinline__ void half_sides(uint32_t (&v)[UH + 8][UW / 4 + 2], co
 #pragma unroll
         for (int t = 2; t < 5; t++) acc = dot2(HP[(i - 1) / 2 + t], c16o[t], acc);
       }
-      v2[i] = clamp_s8(acc >> 12);
+      v2[i] = FME_LANE_PK16 ? acc : clamp_s8(acc >> 12);
     }
 #pragma unroll
     for (int jj = 0; jj < UJ; jj++) {
-      X0[jj] = pack2(clamp_s8(hv[4 + 2 * jj] >> 6), clamp_s8(hv[5 + 2 * jj] >> 6));
-      XM[jj] = pack2(v2[2 * jj], v2[2 * jj + 1]);
-      XP[jj] = pack2(v2[2 * jj + 1], v2[2 * jj + 2]);
+      if constexpr (FME_LANE_PK16) {
+        X0[jj] = pk_round1d(HP[2 + jj]);   // rows 4 + 2 jj, 5 + 2 jj of the first stage
+        XM[jj] = pk_round2d(v2[2 * jj], v2[2 * jj + 1]);
+        XP[jj] = pk_round2d(v2[2 * jj + 1], v2[2 * jj + 2]);
+      } else {
+        X0[jj] = pack2(clamp_s8(hv[4 + 2 * jj] >> 6), clamp_s8(hv[5 + 2 * jj] >> 6));
+        XM[jj] = pack2(v2[2 * jj], v2[2 * jj + 1]);
+        XP[jj] = pack2(v2[2 * jj + 1], v2[2 * jj + 2]);
+      }
     }
 #pragma unroll
     for (int jj = 0; jj < UJ; jj++) {
@@ -570,17 +628,17 @@ __device__ __forceinline__ void qtr_col(uint32_t (&v)[UH + 8][UW / 4 + 2], const
     }
 #pragma unroll
     for (int m = 0; m < NP; m++) {
-      int vq[UH];
+      int vq[UH];   // second-stage sums (taps scaled by kVS)
 #pragma unroll
       for (int y = 0; y < UH; y++) {
         const int m0 = (y & 1) ? (y - 1) / 2 : y / 2;
         int acc = dot2_k0(HQ[m0], (y & 1) ? cpo[m][0] : cpe[m][0]);
 #pragma unroll
         for (int t = 1; t < 5; t++) acc = dot2(HQ[m0 + t], (y & 1) ? cpo[m][t] : cpe[m][t], acc);
-        vq[y] = clamp_s8(acc >> 12);
+        vq[y] = acc;
       }
 #pragma unroll
-      for (int jj = 0; jj < UJ; jj++) XQ[m][x][jj] = pk_sub(K.at(x, jj), pack2(vq[2 * jj], vq[2 * jj + 1]));
+      for (int jj = 0; jj < UJ; jj++) XQ[m][x][jj] = pk_sub(K.at(x, jj), pk_round2d(vq[2 * jj], vq[2 * jj + 1]));
     }
     __builtin_amdgcn_sched_barrier(0);   // one column at a time (register pressure)
   }
@@ -648,13 +706,13 @@ __device__ __forceinline__ void qtr_pass(uint32_t (&v)[UH + 8][UW / 4 + 2], cons
 #pragma unroll
       for (int y = 0; y < UH; y++) {
         const int m0 = (y & 1) ? (y - 1) / 2 : y / 2;
-        int acc = 2048;
+        int acc = 2048 * kVS;
 #pragma unroll
         for (int t = 0; t < 5; t++) acc = dot2(HQ[m0 + t], (y & 1) ? cpo[m][t] : cpe[m][t], acc);
-        vq[y] = clamp_s8(acc >> 12);
+        vq[y] = acc;
       }
 #pragma unroll
-      for (int jj = 0; jj < UJ; jj++) XQ[m][x][jj] = pk_sub(K.at(x, jj), pack2(vq[2 * jj], vq[2 * jj + 1]));
+      for (int jj = 0; jj < UJ; jj++) XQ[m][x][jj] = pk_sub(K.at(x, jj), pk_round2d(vq[2 * jj], vq[2 * jj + 1]));
     }
     __builtin_amdgcn_sched_barrier(0);   // one column at a time (register pressure)
   }
@@ -815,6 +873,7 @@ __device__ FME_LANE_UNIT_ATTR void lane_unit(const BatchArgs& a, const fme_job* 
   const int uu = u < NUH ? u : NUH - 1;
   const int ux = uu % UX, uy = uu / UX;
 
+  FME_STAMP(0);
   const int jid = perm[cls_off + p];
   fme_job j;
   {   // two 16-byte global loads (a struct copy through an address-space-1 pointer does not compile
@@ -865,6 +924,7 @@ __device__ FME_LANE_UNIT_ATTR void lane_unit(const BatchArgs& a, const fme_job* 
   // one unit per lane: its key rows are loaded once, for the EMI step and the sub-pel passes
   uint32_t kraw0[UH][KW];
   if constexpr (UPL == 1) load_kraw(0, kraw0);
+  FME_STAMP(1);
 
   // ---- 1. EMI square step -----------------------------------------------------------------------
   int mvx = j.mv_x, mvy = j.mv_y;
@@ -993,6 +1053,7 @@ __device__ FME_LANE_UNIT_ATTR void lane_unit(const BatchArgs& a, const fme_job* 
     mvx = bx;
     mvy = by;
   }
+  FME_STAMP(2);
   typedef __attribute__((address_space(1))) u32x4a gw4;
   if (u == 0) {   // bytes 16..63 of the record: cost, bits (NN tail), c, emi[8], n_emi
     g_rec[wid][lane][1] = make_uint4(0u, 0u, cval, emi[0]);
@@ -1028,6 +1089,7 @@ __device__ FME_LANE_UNIT_ATTR void lane_unit(const BatchArgs& a, const fme_job* 
       }
   };
   load_half(0);
+  FME_STAMP(3);
   int cur = 0;
   // One candidate pass over the PU: the resident half first, then (two units per lane) the other.
   auto over_halves = [&](auto&& pass, auto& d) FME_AI {
@@ -1078,6 +1140,7 @@ __device__ FME_LANE_UNIT_ATTR void lane_unit(const BatchArgs& a, const fme_job* 
     take_half<L>(8, d[2], live, ml, mvx, mvy, mvp_x, mvp_y, hbest, hbi);
   }
   const int hx = h9_dx(hbi), hy = h9_dy(hbi);
+  FME_STAMP(4);
 
   // ---- 3. quarter-pel stage: passes over column phases (Q9 candidate 0 = the half best) -------
   uint32_t qbest = hbest;
@@ -1104,6 +1167,7 @@ __device__ FME_LANE_UNIT_ATTR void lane_unit(const BatchArgs& a, const fme_job* 
     static_for<0, qp_passes<kQP>()>(qone);
   }
   const int bq = qbi;
+  FME_STAMP(5);
 
   // ---- results: bytes 0..15 (mv_int, mv (NN tail), half, qtr, frac_cost) ------------------------
   const uint32_t r_mv = (uint32_t)(uint16_t)mvx | ((uint32_t)(uint16_t)mvy << 16);
@@ -1129,7 +1193,24 @@ __device__ FME_LANE_UNIT_ATTR void lane_unit(const BatchArgs& a, const fme_job* 
       }
     }
   }
-
+#if FME_LANE_STAMPS
+  FME_STAMP(6);
+  if (lane == 0) {   // vector atomics into the debug buffer, one lane per wave
+    constexpr int C = []() constexpr {
+      for (int c = 0; c < kNumClasses; c++)
+        if (kClassW[c] == PW && kClassH[c] == PH) return c;
+      return 0;
+    }();
+    unsigned long long* d = g_lane_stamps[C];
+    atomicAdd(d + 0, stamp_1 - stamp_0);
+    atomicAdd(d + 1, stamp_2 - stamp_1);
+    atomicAdd(d + 2, stamp_3 - stamp_2);
+    atomicAdd(d + 3, stamp_4 - stamp_3);
+    atomicAdd(d + 4, stamp_5 - stamp_4);
+    atomicAdd(d + 5, stamp_6 - stamp_5);
+    atomicAdd(d + 6, 1ull);
+  }
+#endif
 }
 
 // The XCD this wave runs on (HW_REG_XCC_ID, gfx940+: bits 3:0).
@@ -1271,6 +1352,18 @@ static int lane_grid(int n, int reserve) {
   const long long cap = reserve > 0 ? std::max(1LL, (long long)FME_LANE_WAVES * cus - reserve) : 4LL * cus;
   return (int)std::min<long long>((waves + kLaneNT / 64 - 1) / (kLaneNT / 64), cap);
 }
+
+#if FME_LANE_STAMPS
+// The diagnostic build's per-(class, phase) cycle sums (kNumClasses x 8 words); reset clears them.
+extern "C" int fme_debug_lane_stamps(unsigned long long* out, int reset) {
+  if (out && hipMemcpyFromSymbol(out, HIP_SYMBOL(g_lane_stamps), sizeof(g_lane_stamps)) != hipSuccess) return -2;
+  if (reset) {
+    static const unsigned long long zero[kNumClasses][8] = {};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_lane_stamps), zero, sizeof(zero)) != hipSuccess) return -2;
+  }
+  return 0;
+}
+#endif
 
 hipError_t launch_search_lane(const BatchArgs& a, const WorkBufs& w, int reserve, hipStream_t s) {
   const int blocks = lane_grid(a.n, reserve);

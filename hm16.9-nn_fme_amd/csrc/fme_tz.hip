@@ -70,6 +70,7 @@ struct Tz {
   int dist, k, opnr;
   Range R, RR;          // search range, raster range
   int range;            // m_iSearchRange
+  bool corners;         // bCheckCornersAtDist1 of the running diamond (FastSearch 3: first search, star)
 };
 
 // xTZ8PointSquareSearch (TEncSearch.cpp:1324-1377) at distance 1: point k of (1 2 3 / 4 . 5 / 6 7 8) in
@@ -114,6 +115,11 @@ __device__ __forceinline__ bool diamond_point(const Tz& s, int k, bool& ok, int&
   const int d = s.dist, ox = s.ox, oy = s.oy;
   const Range& R = s.R;
   if (d == 1) {
+    if (s.corners) {   // bCheckCornersAtDist1 (TEncSearch.cpp:1404-1451): the square's 8 points, its checks
+      pd = 1;
+      pnr = k + 1;
+      return square_point(s, k, ok, x, y);
+    }
     if (k >= 4) return false;
     const int dx = k == 1 ? -1 : (k == 2 ? 1 : 0), dy = k == 0 ? -1 : (k == 3 ? 1 : 0);
     x = ox + dx;
@@ -351,7 +357,7 @@ __device__ __forceinline__ void tz_wave(const TzArgs& ta, int jid, const fme_job
   const bool real = u < LR;
   const int uu = real ? u : 0;
   const int ux = uu % UX, uy = uu / UX;
-  const fme_tz_ext e = ta.ext[jid];
+  const fme_tz_ext e = tz_ext_at(ta, jid);
   const PicDesc ref = a.pics[j.ref_id];
   const double ml = a.mlambda[j.lambda_id];
   const bool kbuf = KB != 0 && j.key_offset >= 0;
@@ -421,6 +427,12 @@ __device__ __forceinline__ void tz_wave(const TzArgs& ta, int jid, const fme_job
   s.RR = s.R;
   s.range = e.search_range ? e.search_range : 64;
   s.k = 0; s.dist = 1; s.ox = s.oy = 0; s.opnr = 0;
+  // FastSearch 0 (FME_TZ_FULL: xPatternSearch for every job, TEncSearch.cpp:4504-4507) and 3
+  // (FME_TZ_ENHANCED: xTZSearch with bExtendedSettings, 4726-4727, 4749-4768)
+  // (FME_TZ_RING, the backups' FastSearch 1 path, takes precedence over both)
+  const bool full = !ring && (e.flags & FME_TZ_FULL) != 0;
+  const bool enh = !full && !ring && (e.flags & FME_TZ_ENHANCED) != 0;
+  s.corners = enh;   // bFirstCornersForDiamondDist1, bStarRefinementCornersForDiamondDist1
   auto take = [&](uint32_t cost, int x, int y, int pd, int pnr) FME_AI {   // xTZSearchHelp's update
     if (cost < s.best_sad) {
       s.best_sad = cost;
@@ -449,13 +461,14 @@ __device__ __forceinline__ void tz_wave(const TzArgs& ta, int jid, const fme_job
   };
   int nr = 0;
   while ((1 << nr) <= s.range) nr++;   // dist 1, 2, 4, ... <= m_iSearchRange
-  // compact ring order: ring sizes 4, 8, 8, 8, 16, 16, 16 (xTZ8PointDiamondSearch), point i of the
-  // concatenation -> ring slot (call order preserved)
-  auto ring_start = [](int r) FME_AI { return r == 0 ? 0 : (r < 4 ? 4 + 8 * (r - 1) : 28 + 16 * (r - 4)); };
-  auto compact_slot = [](int i) FME_AI {
-    return i < 4 ? i : (i < 28 ? 16 * (1 + (i - 4) / 8) + ((i - 4) & 7) : 16 * (4 + (i - 28) / 16) + ((i - 28) & 15));
+  // compact ring order: ring sizes c0, 8, 8, 8, 16, 16, 16 (xTZ8PointDiamondSearch; c0 = 4, or 8
+  // with the distance-1 corners), point i of the concatenation -> ring slot (call order preserved)
+  auto ring_start = [](int r, int c0) FME_AI { return r == 0 ? 0 : (r < 4 ? c0 + 8 * (r - 1) : c0 + 24 + 16 * (r - 4)); };
+  auto compact_slot = [](int i, int c0) FME_AI {
+    return i < c0 ? i : (i < c0 + 24 ? 16 * (1 + (i - c0) / 8) + ((i - c0) & 7) : 16 * (4 + (i - c0 - 24) / 16) + ((i - c0 - 24) & 15));
   };
-  const int nring_pts = ring_start(nr);
+  const int c0 = s.corners ? 8 : 4;
+  const int nring_pts = ring_start(nr, c0);
   auto two_point_search = [&]() FME_AI {   // xTZ2PointSearch around the best, opnr = its point nr
     s.ox = s.bx; s.oy = s.by; s.opnr = s.pnr;
     const uint64_t k = list_min(2, [&](int i, int& x, int& y) FME_AI {
@@ -470,7 +483,7 @@ __device__ __forceinline__ void tz_wave(const TzArgs& ta, int jid, const fme_job
     }
   };
 
-  if (j.flags & FME_JOB_BIPRED) {
+  if ((j.flags & FME_JOB_BIPRED) || full) {
     // xPatternSearch: every point of the range in raster order
     const int nx = s.R.r - s.R.l + 1, ny = s.R.b - s.R.t + 1;
     if (nx > 0 && ny > 0) {
@@ -482,7 +495,8 @@ __device__ __forceinline__ void tz_wave(const TzArgs& ta, int jid, const fme_job
       take((uint32_t)(k >> 32), s.R.l + i % nx, s.R.t + i / nx, 0, 0);
     }
   } else {
-    // ---- start points: the AMVP predictor, the zero vector, the 2Nx2N MV --------------------------
+    // ---- start points: 0 the AMVP predictor, 1..3 the neighbours' MVs (FastSearch 3,
+    // m_acMvPredictors), 4 the zero vector, 5 the 2Nx2N MV; costs together, tests in call order ---
     int mx = j.mvp_x, my = j.mvp_y;
     clip_qpel(mx, my, ref.width, ref.height, e.cu_x, e.cu_y);
     const int sx = round4(mx), sy = round4(my);
@@ -490,39 +504,61 @@ __device__ __forceinline__ void tz_wave(const TzArgs& ta, int jid, const fme_job
     int qx = pred_x * 4, qy = pred_y * 4;
     clip_qpel(qx, qy, ref.width, ref.height, e.cu_x, e.cu_y);
     const int px = round4(qx), py = round4(qy);
+    int nbx[3] = {0, 0, 0}, nby[3] = {0, 0, 0};
+    if (enh) {
+#pragma unroll
+      for (int k = 0; k < 3; k++) {
+        int ax, ay;
+        tz_pred_at(ta, jid, k, ax, ay);
+        clip_qpel(ax, ay, ref.width, ref.height, e.cu_x, e.cu_y);
+        nbx[k] = round4(ax);
+        nby[k] = round4(ay);
+      }
+    }
     {
-      uint32_t c3[3] = {0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu}, d3[3] = {0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu};
-      for (int base = 0; base < 3; base += G) {
+      constexpr int NS = 6;
+      uint32_t cs[NS], ds[NS];
+#pragma unroll
+      for (int q = 0; q < NS; q++) cs[q] = ds[q] = 0xFFFFFFFFu;
+      for (int base = 0; base < NS; base += G) {
         const int i = base + g;
-        const int x = i == 0 ? sx : (i == 1 ? 0 : px), y = i == 0 ? sy : (i == 1 ? 0 : py);
+        const int x = i == 0 ? sx : (i == 1 ? nbx[0] : (i == 2 ? nbx[1] : (i == 3 ? nbx[2] : (i == 4 ? 0 : px))));
+        const int y = i == 0 ? sy : (i == 1 ? nby[0] : (i == 2 ? nby[1] : (i == 3 ? nby[2] : (i == 4 ? 0 : py))));
+        const bool v = i < NS && (i == 0 || i == 4 || (i == 5 && has_pred) || (i <= 3 && enh));
         uint32_t dist;
-        const uint32_t c = cost_at(x, y, i < 3, dist);
+        const uint32_t c = cost_at(x, y, v, dist);
         if constexpr (NW == 1) {
 #pragma unroll
-          for (int q = 0; q < 3; q++)
+          for (int q = 0; q < NS; q++)
             if (q >= base && q < base + G) {
-              c3[q] = __shfl(c, (q - base) * L, 64);
-              d3[q] = __shfl(dist, (q - base) * L, 64);
+              cs[q] = __shfl(c, (q - base) * L, 64);
+              ds[q] = __shfl(dist, (q - base) * L, 64);
             }
-        } else {   // G >= 3 with several waves: the three costs through LDS
-          __shared__ uint32_t s_c3[3];
-          if (i < 3 && u == 0) s_c3[i] = c;
+        } else {   // several waves: the costs through LDS
+          __shared__ uint32_t s_cs[NS];
+          if (i < NS && u == 0) s_cs[i] = c;
           __syncthreads();
 #pragma unroll
-          for (int q = 0; q < 3; q++) c3[q] = s_c3[q];
+          for (int q = 0; q < NS; q++)
+            if (q >= base && q < base + G) cs[q] = s_cs[q];
           __syncthreads();
           (void)dist;
         }
       }
-      take(c3[0], sx, sy, 0, 0);
-      cmin = d3[0];
-      if (sx != 0 || sy != 0) {
-        take(c3[1], 0, 0, 0, 0);
-        cmin = d3[1] < cmin ? d3[1] : cmin;
+      take(cs[0], sx, sy, 0, 0);
+      cmin = ds[0];
+      if (enh) {   // bTestOtherPredictedMV (4787-4805): "only test cMv if not obviously previously tested"
+#pragma unroll
+        for (int k = 0; k < 3; k++)
+          if ((nbx[k] != sx || nby[k] != sy) && (nbx[k] != s.bx && nby[k] != s.by)) take(cs[1 + k], nbx[k], nby[k], 0, 0);
+      }
+      if ((sx != 0 || sy != 0) && (s.bx != 0 || s.by != 0)) {
+        take(cs[4], 0, 0, 0, 0);
+        cmin = ds[4] < cmin ? ds[4] : cmin;
       }
       if (has_pred && (sx != px || sy != py) && (px != s.bx || py != s.by)) {
-        take(c3[2], px, py, 0, 0);
-        cmin = d3[2] < cmin ? d3[2] : cmin;
+        take(cs[5], px, py, 0, 0);
+        cmin = ds[5] < cmin ? ds[5] : cmin;
       }
     }
     if (has_pred) {   // xSetSearchRange(currBest << 2, m_iSearchRange): the raster's range
@@ -533,20 +569,21 @@ __device__ __forceinline__ void tz_wave(const TzArgs& ta, int jid, const fme_job
       clip_qpel(rx, ry, ref.width, ref.height, e.cu_x, e.cu_y);
       s.RR = Range{round4(lx), round4(rx), round4(ly), round4(ry)};
     }
+    const bool best_zero = s.bx == 0 && s.by == 0;   // bBestCandidateZero (4857)
 
     // ---- first search: rings around the start, stop 3 rings after the last new best --------------
     if (G <= 16 || NW > 1) {   // ring by ring: one candidate list per ring, later rings skipped after the stop
       s.ox = s.bx; s.oy = s.by;
       for (int r = 0; r < nr; r++) {
-        const int r0 = ring_start(r);
-        const uint64_t k = list_min(ring_start(r + 1) - r0, [&](int i, int& x, int& y) FME_AI {
+        const int r0 = ring_start(r, c0);
+        const uint64_t k = list_min(ring_start(r + 1, c0) - r0, [&](int i, int& x, int& y) FME_AI {
           int pnr, pd;
-          return ring_pt(compact_slot(r0 + i), x, y, pnr, pd);
+          return ring_pt(compact_slot(r0 + i, c0), x, y, pnr, pd);
         });
         s.bround += 1;
         if ((uint32_t)(k >> 32) < s.best_sad) {
           int xx, yy, pn, pdd;
-          ring_pt(compact_slot(r0 + (int)(uint32_t)k), xx, yy, pn, pdd);
+          ring_pt(compact_slot(r0 + (int)(uint32_t)k, c0), xx, yy, pn, pdd);
           take((uint32_t)(k >> 32), xx, yy, pdd, pn);
         }
         if (s.bround >= 3 || 2 * (1 << r) > s.range) break;
@@ -595,21 +632,46 @@ __device__ __forceinline__ void tz_wave(const TzArgs& ta, int jid, const fme_job
         }
       }
     }
+    // ---- FastSearch 3: the zero vector's neighbourhood at half the range (bNewZeroNeighbourhoodTest,
+    // bTestZeroVectorStart, 4900-4917), diamonds without corners around (0, 0), every ring ------------
+    if (enh && !best_zero) {
+      int nz = 0;
+      while ((1 << nz) <= (s.range >> 1)) nz++;
+      s.ox = s.oy = 0;
+      s.corners = false;
+      const uint64_t k = list_min(ring_start(nz, 4), [&](int i, int& x, int& y) FME_AI {
+        int pnr, pd;
+        return ring_pt(compact_slot(i, 4), x, y, pnr, pd);
+      });
+      if ((uint32_t)(k >> 32) < s.best_sad) {
+        int xx, yy, pn, pdd;
+        ring_pt(compact_slot((int)(uint32_t)k, 4), xx, yy, pn, pdd);
+        take((uint32_t)(k >> 32), xx, yy, pdd, pn);
+      }
+      s.corners = true;
+    }
     if (s.bdist == 1) {
       s.bdist = 0;
       two_point_search();
     }
-    // ---- raster (step 5) over the re-centred range when the best is far -------------------------
-    if (s.bdist > 5) {
-      s.bdist = 5;
-      if (s.RR.l <= s.RR.r && s.RR.t <= s.RR.b) {
-        const int nx = (s.RR.r - s.RR.l) / 5 + 1, ny = (s.RR.b - s.RR.t) / 5 + 1;
+    // ---- raster: step 5 over the re-centred range when the best is far; FastSearch 3's adaptive
+    // raster (4926-4951) always runs: step 5, or step 6 over the halved range when the best is near --
+    if (enh || s.bdist > 5) {
+      int win = 5;
+      Range rr = s.RR;
+      if (enh && !(s.bdist > 5)) {
+        win = 6;
+        rr.l /= 2; rr.r /= 2; rr.t /= 2; rr.b /= 2;   // C++ division: towards zero
+      }
+      s.bdist = win;
+      if (rr.l <= rr.r && rr.t <= rr.b) {
+        const int nx = (rr.r - rr.l) / win + 1, ny = (rr.b - rr.t) / win + 1;
         const uint64_t k = list_min(nx * ny, [&](int i, int& x, int& y) FME_AI {
-          x = s.RR.l + 5 * (i % nx); y = s.RR.t + 5 * (i / nx);
+          x = rr.l + win * (i % nx); y = rr.t + win * (i / nx);
           return true;
         });
         const int i = (int)(uint32_t)k;
-        take((uint32_t)(k >> 32), s.RR.l + 5 * (i % nx), s.RR.t + 5 * (i / nx), 5, 0);
+        take((uint32_t)(k >> 32), rr.l + win * (i % nx), rr.t + win * (i / nx), win, 0);
       }
     }
     // ---- star refinement: every ring around the best, until the best stays ----------------------
@@ -617,11 +679,11 @@ __device__ __forceinline__ void tz_wave(const TzArgs& ta, int jid, const fme_job
       s.ox = s.bx; s.oy = s.by; s.bdist = 0; s.pnr = 0;
       const uint64_t k = list_min(nring_pts, [&](int i, int& x, int& y) FME_AI {
         int pnr, pd;
-        return ring_pt(compact_slot(i), x, y, pnr, pd);
+        return ring_pt(compact_slot(i, c0), x, y, pnr, pd);
       });
       if ((uint32_t)(k >> 32) < s.best_sad) {
         int xx, yy, pn, pdd;
-        ring_pt(compact_slot((int)(uint32_t)k), xx, yy, pn, pdd);
+        ring_pt(compact_slot((int)(uint32_t)k, c0), xx, yy, pn, pdd);
         take((uint32_t)(k >> 32), xx, yy, pdd, pn);
       }
       if (s.bdist == 1) {
@@ -746,7 +808,7 @@ void k_tz_wave(TzArgs ta, TzSchedule sc, int kid) {
   if (q < 0) return;
   const int jid = ta.perm[q];
   const fme_job j = FME_SJOBS ? ta.sjobs[q] : ta.a.jobs[jid];
-  tz_wave<UW, UH, 1, KB>(ta, jid, j, kTzW[c], kTzH[c], ta.ext[jid].pred2n_x, ta.ext[jid].pred2n_y);
+  tz_wave<UW, UH, 1, KB>(ta, jid, j, kTzW[c], kTzH[c], tz_ext_at(ta, jid).pred2n_x, tz_ext_at(ta, jid).pred2n_y);
 }
 
 // ---- staged bulk search: PUs grouped by (kernel, reference picture, CTU), a group's search area
@@ -862,7 +924,7 @@ void k_tz_staged(TzArgs ta, TzPairs tp, int kid) {
   // the tile: the group's CTU displaced by its first PU's start MV (round4 of the clipped AMVP)
   const int j0 = tp.perm[start];
   const fme_job jb = ta.a.jobs[j0];
-  const fme_tz_ext e0 = ta.ext[j0];
+  const fme_tz_ext e0 = tz_ext_at(ta, j0);
   const PicDesc ref = ta.a.pics[jb.ref_id];
   int mx = jb.mvp_x, my = jb.mvp_y;
   clip_qpel(mx, my, ref.width, ref.height, e0.cu_x, e0.cu_y);
@@ -889,7 +951,7 @@ void k_tz_staged(TzArgs ta, TzPairs tp, int kid) {
   for (int p = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6); p < cnt; p += FME_TZS_NT / 64) {
     const int jid = tp.perm[start + p];
     const fme_job j = ta.a.jobs[jid];
-    tz_wave<UW, UH, 1, KB>(ta, jid, j, j.w, j.h, ta.ext[jid].pred2n_x, ta.ext[jid].pred2n_y, tr);
+    tz_wave<UW, UH, 1, KB>(ta, jid, j, j.w, j.h, tz_ext_at(ta, jid).pred2n_x, tz_ext_at(ta, jid).pred2n_y, tr);
   }
 }
 
@@ -905,7 +967,7 @@ __global__ __launch_bounds__(64 * FME_TZL_WAVES) void k_tz_level(TzArgs ta, TzCh
   const int q = first + (int)blockIdx.x;
   const int PW = ta.a.jobs[q].w, PH = ta.a.jobs[q].h;   // shapes checked by the host
   const int ps = ch.psrc[q];
-  int px = ta.ext[q].pred2n_x, py = ta.ext[q].pred2n_y;
+  int px = tz_ext_at(ta, q).pred2n_x, py = tz_ext_at(ta, q).pred2n_y;
   if (ps >= 0) {
     const uint32_t mv = reinterpret_cast<const uint32_t*>(ta.emi_mv)[ps];
     px = (int)(int16_t)(mv & 0xFFFFu);

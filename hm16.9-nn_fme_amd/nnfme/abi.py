@@ -34,6 +34,12 @@ RESULT_DTYPE = np.dtype(
 assert RESULT_DTYPE.itemsize == 64
 
 # fme_mv_result (16 B): xMotionEstimation's outputs alone (fme_refine_mv*)
+# fme_job_packed (16 B): the upload form of fme_job (include/fme.h)
+JOB_PACKED_DTYPE = np.dtype([("pu", "<u4"), ("ctl", "<u4"), ("mv_x", "<i2"), ("mv_y", "<i2"),
+                             ("mvp_x", "<i2"), ("mvp_y", "<i2")], align=False)
+assert JOB_PACKED_DTYPE.itemsize == 16
+PACK_WAVE = 64
+
 MV_RESULT_DTYPE = np.dtype(
     [("mv_x", "<i2"), ("mv_y", "<i2"), ("cost", "<u4"), ("bits", "<u4"),
      ("nn_class", "u1"), ("reserved", "u1"), ("status", "<u2")],
@@ -69,6 +75,11 @@ TZ_EXT_DTYPE = np.dtype(
 assert TZ_EXT_DTYPE.itemsize == 12
 TZ_PRED2NX2N = 0x01
 TZ_RING = 0x02          # the backups' xTZSearch tail (fme_integer_search_ring)
+TZ_FULL = 0x04          # FastSearch 0: xPatternSearch over lt..rb (uni-pred too)
+TZ_ENHANCED = 0x08      # FastSearch 3: xTZSearch with bExtendedSettings (fme_tz_ext2 predictors)
+# fme_tz_ext2 (24 B): fme_tz_ext + m_acMvPredictors[left, above, above-right] (quarter-pel)
+TZ_EXT2_DTYPE = np.dtype([("base", TZ_EXT_DTYPE), ("preds", "<i2", (3, 2))], align=False)
+assert TZ_EXT2_DTYPE.itemsize == 24
 
 # fme_pu_req (64 B) / fme_pu_res (80 B): predInterSearch's P-slice PU / reference loop (include/fme.h)
 MAX_REFS = 4

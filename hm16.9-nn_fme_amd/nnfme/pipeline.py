@@ -27,6 +27,7 @@ reference at distance d (the base job's ref_id = d - 1) is slot j + 4 - d, its l
 """
 import ctypes
 import sys
+import time
 
 import numpy as np
 
@@ -74,6 +75,12 @@ class _RawEvent:
     def wait(self, stream):
         if _hip_lib().hipStreamWaitEvent(stream.cuda_stream, self.cuda_event, 0) != 0:
             raise RuntimeError("hipStreamWaitEvent failed")
+
+    def destroy(self):
+        """Explicit release (FrameReplay.close): before interpreter exit, not in a finaliser."""
+        if self.cuda_event and _hip is not None:
+            _hip.hipEventDestroy(self.cuda_event)
+        self.cuda_event = None
 
     def __del__(self):
         # not at interpreter exit: the HIP runtime may already be torn down (a profiler's exit
@@ -133,7 +140,8 @@ def group_key_reqs(base, frames, key_count):
 class FrameReplay:
     def __init__(self, ctx, base_jobs, pool, lambda_of, n_steps, frames_per_step=1, world=1, rank=0, device=None,
                  group=None, defer_download=True, key_reqs=None, key_count=0, nn_rows=None,
-                 download_engine="blit", download_wgs=8, search_reserve=0):
+                 download_engine="sdma", download_wgs=8, search_reserve=0, packed=True, copy_streams=1, slots=3,
+                 max_ahead=4):
         """ctx: an FmeContext on `device`; base_jobs: one frame's jobs (ref_id = reference
         distance - 1); pool: uint8 [P, H, W] host frames, frame g's pictures are pool[g % P];
         lambda_of(g): frame g's lambda (pool uint16: main10 samples for a bit-depth-10 context,
@@ -143,16 +151,31 @@ class FrameReplay:
         (fme_build_bipred_keys_device), so the keys are per-frame work inside the timed step.
         nn_rows (uint32 [n][9]): the NN input rows of the frame's FME_JOB_NN_IN jobs (the backups'
         input path); each step uploads them with its jobs and binds them (fme_set_nn_inputs).
-        download_engine: "sdma" (hipMemcpyDeviceToDeviceNoCU into the pinned rows: a copy engine),
-        "kernel" (fme_download_device: the library's copy kernel of
-        download_wgs workgroups of 256 lanes, which hold a few wave slots beside the next step's
-        search) or "blit" (hipMemcpyAsync, which this ROCm runs as a blit kernel of hundreds of
+        packed: upload the jobs as 16-byte fme_job_packed rows (fme_pack_jobs, unpacked on the device
+        by fme_refine_mv_packed_device) instead of 32-byte fme_job rows; a batch outside the packed
+        form falls back to fme_job (self.packed_reason says why).
+        copy_streams: 1 (default) carries every copy of a step - H2D of step k+1, D2H of step k-1 -
+        in series on one copy stream; 2 gives the downloads their own stream (round 5's layout: an
+        H2D and a D2H in flight together took 2.57 ms where the two in series take 0.93 ms,
+        gpurun_out/d2h.log).  slots: depth of the job / result buffer rings (3: the upload of step
+        k+1 never waits for the download of step k-2).  max_ahead: issue(k) first waits for step
+        k - max_ahead's batch (0: never): a host left to run ahead blocked inside one
+        hipMemcpyAsync for 7-27 ms, until the device had drained nearly every queued step (the
+        runtime's copy queue full: profiles/r06_ab.log), which then restarted the pipeline empty.
+        download_engine: "sdma" (hipMemcpyDeviceToDeviceNoCU into the pinned rows: a copy engine,
+        no CUs), "kernel" (fme_download_device: the library's copy kernel of download_wgs workgroups
+        of 256 lanes) or "blit" (hipMemcpyAsync, which this ROCm runs as a blit kernel of hundreds of
         workgroups that take the search kernel's CUs).  search_reserve: resident search workgroups
         left free (fme_set_search_reserve), so the download kernel runs beside the search."""
         import torch
+        from .abi import JOB_PACKED_DTYPE
+        from .runtime import FmeError, pack_jobs
         self.torch, self.ctx = torch, ctx
         self.world, self.rank, self.group = world, rank, group
         self.F = F = frames_per_step
+        self.R = R = int(slots)
+        if R < 2:
+            raise ValueError("slots >= 2")
         self.lambda_of = lambda_of
         self.steps = n_steps
         P, H, W = pool.shape
@@ -166,20 +189,33 @@ class FrameReplay:
         self.key_count = int(key_count)
         self.jobs = group_jobs(base_jobs, F, self.key_count)
         self.n = n = len(self.jobs)
-        self.h_jobs = torch.from_numpy(self.jobs.view(np.uint8).copy()).pin_memory()
-        self.d_jobs = [torch.empty(n * JOB_DTYPE.itemsize, dtype=torch.uint8, device=device) for _ in range(2)]
+        self.packed, self.packed_reason = bool(packed), None
+        if self.packed:
+            try:
+                pk, kb = pack_jobs(self.jobs)
+            except FmeError as e:   # outside the packed form: the 32-byte rows
+                self.packed, self.packed_reason = False, str(e)
+        if self.packed:
+            self.h_jobs = torch.from_numpy(pk.view(np.uint8).copy()).pin_memory()
+            self.h_kb = torch.from_numpy(kb.view(np.uint8).copy()).pin_memory()
+            self.d_kb = [torch.empty(self.h_kb.numel(), dtype=torch.uint8, device=device) for _ in range(R)]
+            assert self.h_jobs.numel() == n * JOB_PACKED_DTYPE.itemsize
+        else:
+            self.h_jobs = torch.from_numpy(self.jobs.view(np.uint8).copy()).pin_memory()
+        self.job_bytes = self.h_jobs.numel() + (self.h_kb.numel() if self.packed else 0)
+        self.d_jobs = [torch.empty(self.h_jobs.numel(), dtype=torch.uint8, device=device) for _ in range(R)]
         self.kreqs = None
         if key_reqs is not None and len(key_reqs):
             self.kreqs = group_key_reqs(key_reqs, F, self.key_count)
             self.h_kreqs = torch.from_numpy(self.kreqs.view(np.uint8).copy()).pin_memory()
-            self.d_kreqs = [torch.empty(self.h_kreqs.numel(), dtype=torch.uint8, device=device) for _ in range(2)]
+            self.d_kreqs = [torch.empty(self.h_kreqs.numel(), dtype=torch.uint8, device=device) for _ in range(R)]
         self.rows = None
         if nn_rows is not None:
             self.rows = np.tile(np.ascontiguousarray(nn_rows, dtype=np.uint32).reshape(-1, 9), (F, 1))
             assert len(self.rows) == n
             self.h_rows = torch.from_numpy(self.rows.view(np.uint8).copy()).pin_memory()
-            self.d_rows = [torch.empty(self.h_rows.numel(), dtype=torch.uint8, device=device) for _ in range(2)]
-        self.d_out = [torch.empty(n * MV_RESULT_DTYPE.itemsize, dtype=torch.uint8, device=device) for _ in range(2)]
+            self.d_rows = [torch.empty(self.h_rows.numel(), dtype=torch.uint8, device=device) for _ in range(R)]
+        self.d_out = [torch.empty(n * MV_RESULT_DTYPE.itemsize, dtype=torch.uint8, device=device) for _ in range(R)]
         self.h_out = torch.empty((n_steps, n * MV_RESULT_DTYPE.itemsize), dtype=torch.uint8).pin_memory()
         frames = n_steps * world * F
         # every reconstructed picture of the run (frames -4 .. frames - 1) and this rank's originals
@@ -187,8 +223,11 @@ class FrameReplay:
         self.org = torch.empty((n_steps * F, H, W), dtype=pdt, device=device)
         self.states = torch.zeros((n_steps, 12), dtype=torch.int32, device=device)
         self.s_comp = torch.cuda.default_stream(device)
-        self.s_copy = torch.cuda.Stream(device)   # H2D: jobs, originals, reconstructions
-        self.s_down = torch.cuda.Stream(device)   # D2H: results (the other copy direction, its own engine)
+        self.s_copy = torch.cuda.Stream(device)   # H2D: jobs, originals, reconstructions (+ D2H: copy_streams 1)
+        if copy_streams not in (1, 2):
+            raise ValueError("copy_streams 1 or 2")
+        self.copy_streams = copy_streams
+        self.s_down = self.s_copy if copy_streams == 1 else torch.cuda.Stream(device)
         self.uploaded = -1
         # one event of each kind per step, each recorded once: a stream wait on an event that is
         # recorded again while earlier waits on it are still queued did not always wait for the
@@ -210,6 +249,32 @@ class FrameReplay:
         self.fixed_jobs = 0
         self.last_prefix = 0                      # longest carried-state prefix finish() re-ran
         self.r_out = {}
+        self.max_ahead = int(max_ahead)
+        self.host_ms = []                         # host wall time of each issue() call (stall hunting)
+        self.host_seg = []                        # its parts: upload, waits, bind, refine, prefetch, download
+        self.host_seg_names = ("upload", "waits", "bind", "refine", "prefetch", "download")
+
+    def h2d_bytes_per_step(self):
+        """Bytes this rank uploads per step: jobs (+ key bases), key requests, NN rows, its frames'
+        originals and the reconstructions it publishes (one per frame)."""
+        b = self.job_bytes + 2 * self.F * self.H * self.W * self.bps
+        if self.kreqs is not None:
+            b += self.h_kreqs.numel()
+        if self.rows is not None:
+            b += self.h_rows.numel()
+        return b
+
+    def close(self):
+        """Release the replay's HIP resources (events, the library's search-event hook) before the
+        interpreter exits: nothing of it is left to a destructor that may run after the HIP runtime
+        (or a profiler's exit handlers) has torn down."""
+        try:
+            self.ctx.set_search_event(None)
+        except Exception:
+            pass
+        for e in self.ev_search:
+            e.destroy()
+        self.ev_search = []
 
     def first_frame(self, k):
         """First frame of this rank's step k."""
@@ -306,9 +371,18 @@ class FrameReplay:
             for g in range(-REFS, -1):
                 self._publish(g, 0)
         for k in range(self.steps):
-            _memcpy_async(self.h_out[k], self.d_out[k & 1], self.h_out.shape[1], D2H, self.s_down)
+            self._copy_down(k, self.s_down)
         self.s_copy.synchronize()
         self.s_down.synchronize()
+
+    def _refine(self, k, out_ptr, n, stream):
+        """Step k's batch (its slot's jobs, first n of them) into out_ptr on `stream`."""
+        b = k % self.R
+        if self.packed:
+            self.ctx.refine_mv_packed_device(self.d_jobs[b].data_ptr(), self.d_kb[b].data_ptr(), out_ptr, n,
+                                             stream.cuda_stream)
+        else:
+            self.ctx.refine_mv_device(self.d_jobs[b].data_ptr(), out_ptr, n, stream.cuda_stream)
 
     def bind_rows(self, b):
         """Bind slot b's NN input rows for the next batches (no-op without rows)."""
@@ -317,7 +391,7 @@ class FrameReplay:
 
     def _bind(self, k):
         ctx, W, H, F = self.ctx, self.W, self.H, self.F
-        self.bind_rows(k & 1)
+        self.bind_rows(k % self.R)
         f0 = self.first_frame(k)
         for j in range(F):
             ctx.bind_picture_device(ORG0 + j, self.org[k * F + j].data_ptr(), W, W, H)
@@ -326,26 +400,29 @@ class FrameReplay:
             ctx.bind_picture_device(s, self.recon[f0 - REFS + s + REFS].data_ptr(), W, W, H)
 
     # -- one step -----------------------------------------------------------------------------
-    # Streams: the batch runs on the device's default stream, the uploads on one copy stream
-    # (the upload of step k+1 is queued right after step k's batch, so it overlaps that batch) and
-    # the downloads on another: the two directions use separate copy engines, and PCIe is full
-    # duplex (on one stream the 31.7 MB up + 13.8 MB down of a 1080p step serialised: 1.75 ms per
-    # step against 1.25 ms for the batch alone).  The download of step k waits until step k+1's
-    # search kernel runs (the library records ev_search before each search launch): a
-    # device-to-host copy's posted PCIe writes hold back every read the device issues behind
-    # them, so a download that overlapped step k+1's prologue held each of its kernel launches
-    # (AQL packet fetches) until the copy had drained, ≈ 0.25 ms per step.  Compute + two copy
-    # streams stay within the process's four hardware queues (GPU_MAX_HW_QUEUES); more streams
-    # share queues, and a copy stream's event waits then block kernels queued behind them.
+    # Streams: the batch runs on the device's default stream; every copy runs on one copy stream,
+    # in series, as issue(k) queues them: the H2D of step k+1 (jobs, key bases, originals, the
+    # published reconstruction; its slot was last read by step k+1-R), then the D2H of step k-1's
+    # results, which waits until step k's search kernel runs (the library records ev_search right
+    # before each search launch).  In series the two directions take 0.93 ms per 1080p step with
+    # 32-byte jobs (H2D 0.68 + D2H 0.25 ms, gpurun_out/d2h.log), less than the batch; in flight
+    # together on two streams they took 2.57 ms, which is what bound round 5's pipeline.  The
+    # download starting only once the search runs keeps a device-to-host copy's posted PCIe writes
+    # off the batch prologue's launches (each held back by the copy's length, ≈ 0.25 ms per step).
+    # The "sdma" engine (hipMemcpyDeviceToDeviceNoCU into the pinned rows) moves the download off
+    # the CUs: the ROCclr blit kernel shared them with the search (0.92 -> 1.11 ms).  Compute and
+    # copy streams stay within the process's four hardware queues (GPU_MAX_HW_QUEUES).
     def _upload(self, k):
-        F = self.F
-        b = k & 1
+        F, R = self.F, self.R
+        b = k % R
         f0 = self.first_frame(k)
         cp = self.s_copy
         with self.torch.cuda.stream(cp):
-            if k >= 2:
-                cp.wait_event(self.ev_comp[k - 2])        # step k-2 is done with the slot
+            if k >= R:
+                cp.wait_event(self.ev_comp[k - R])        # step k-R is done with the slot
             _memcpy_async(self.d_jobs[b], self.h_jobs, self.h_jobs.numel(), H2D, cp)
+            if self.packed:
+                _memcpy_async(self.d_kb[b], self.h_kb, self.h_kb.numel(), H2D, cp)
             if self.rows is not None:
                 _memcpy_async(self.d_rows[b], self.h_rows, self.h_rows.numel(), H2D, cp)
             if self.kreqs is not None:
@@ -361,15 +438,22 @@ class FrameReplay:
 
     def issue(self, k, prefetch=True):
         """Enqueue step k (and, with prefetch, the upload of step k+1); returns without waiting
-        for the device."""
+        for the device.  self.host_ms / self.host_seg record the host time of each call and of its
+        parts (stall hunting: which runtime call blocks)."""
+        pc = time.perf_counter
+        t = [pc()]
         ctx = self.ctx
-        b = k & 1
+        b = k % self.R
+        if self.max_ahead > 0 and k >= self.max_ahead:
+            self.ev_comp[k - self.max_ahead].synchronize()   # at most max_ahead steps queued
         if self.uploaded < k:
             self._upload(k)
+        t.append(pc())
         comp = self.s_comp
         comp.wait_event(self.ev_in[k])
-        if k >= 2:
-            comp.wait_event(self.ev_out[k - 2])            # step k-2's results have left
+        if k >= self.R:
+            comp.wait_event(self.ev_out[k - self.R])       # step k-R's results have left the slot
+        t.append(pc())
         self._bind(k)
         if self.kreqs is not None:   # this step's frames' removeHighFreq keys, from this step's pictures
             ctx.build_bipred_keys_device(self.d_kreqs[b].data_ptr(), len(self.kreqs), self.key_count * self.F,
@@ -378,18 +462,34 @@ class FrameReplay:
             ctx.nn_reset()                                 # stream-ordered: this batch starts fresh
         if self.defer_download:
             ctx.set_search_event(self.ev_search[k])        # recorded right before this batch's search
-        ctx.refine_mv_device(self.d_jobs[b].data_ptr(), self.d_out[b].data_ptr(), self.n, comp.cuda_stream)
+        t.append(pc())
+        self._refine(k, self.d_out[b].data_ptr(), self.n, comp)
         if self.world > 1:
             ctx.nn_copy_state_device(self.states[k].data_ptr(), comp.cuda_stream)
         self.ev_comp[k].record(comp)
+        t.append(pc())
         if prefetch and k + 1 < self.steps:
             self._upload(k + 1)
+        t.append(pc())
         if not self.defer_download:
             self._download(k, self.ev_comp[k])
-            return
-        if self.pending is not None:   # step k's search started: k-1 is done (its own batch event otherwise)
-            self._download(self.pending, self.ev_search[k] if self.n > 0 else self.ev_comp[self.pending])
-        self.pending = k
+        else:
+            if self.pending is not None:   # step k's search started: k-1 is done (its own batch event otherwise)
+                self._download(self.pending, self.ev_search[k] if self.n > 0 else self.ev_comp[self.pending])
+            self.pending = k
+        t.append(pc())
+        self.host_ms.append((t[-1] - t[0]) * 1e3)
+        self.host_seg.append([round((t[i + 1] - t[i]) * 1e3, 3) for i in range(len(t) - 1)])
+
+    def _copy_down(self, k, dn):
+        b = k % self.R
+        if self.download_engine == "kernel":
+            self.ctx.download_device(self.d_out[b].data_ptr(), self.h_out[k].data_ptr(), self.h_out.shape[1],
+                                     self.download_wgs, dn.cuda_stream)
+        elif self.download_engine == "sdma":   # hipMemcpyDeviceToDeviceNoCU: a copy engine, no CUs
+            _memcpy_async(self.h_out[k], self.d_out[b], self.h_out.shape[1], D2D_NOCU, dn)
+        else:
+            _memcpy_async(self.h_out[k], self.d_out[b], self.h_out.shape[1], D2H, dn)
 
     def _download(self, k, after):
         dn = self.s_down
@@ -397,13 +497,7 @@ class FrameReplay:
             after.wait(dn)
         else:
             dn.wait_event(after)
-        if self.download_engine == "kernel":
-            self.ctx.download_device(self.d_out[k & 1].data_ptr(), self.h_out[k].data_ptr(), self.h_out.shape[1],
-                                     self.download_wgs, dn.cuda_stream)
-        elif self.download_engine == "sdma":   # hipMemcpyDeviceToDeviceNoCU: a copy engine, no CUs
-            _memcpy_async(self.h_out[k], self.d_out[k & 1], self.h_out.shape[1], D2D_NOCU, dn)
-        else:
-            _memcpy_async(self.h_out[k], self.d_out[k & 1], self.h_out.shape[1], D2H, dn)
+        self._copy_down(k, dn)
         self.ev_out[k].record(dn)
 
     def drain(self):
@@ -440,12 +534,12 @@ class FrameReplay:
 
     def _resident_batch(self, k, n):
         ctx, comp = self.ctx, self.s_comp
-        b = k & 1
+        b = k % self.R
         self._bind(k)
         if self.kreqs is not None:   # this step's keys, built on the device from its pictures
             ctx.build_bipred_keys_device(self.d_kreqs[b].data_ptr(), len(self.kreqs), self.key_count * self.F,
                                          comp.cuda_stream)
-        ctx.refine_mv_device(self.d_jobs[b].data_ptr(), self.r_out[k].data_ptr(), n, comp.cuda_stream)
+        self._refine(k, self.r_out[k].data_ptr(), n, comp)
 
     def issue_resident(self, k):
         """Step k from HBM-resident inputs into r_out[k] (no copy, no host wait)."""

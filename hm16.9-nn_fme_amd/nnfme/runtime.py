@@ -6,6 +6,7 @@ context, and every failing C call raises FmeError with fme_last_error()'s text.
 """
 import ctypes as C
 import os
+import sys
 
 import numpy as np
 
@@ -15,7 +16,7 @@ from .weights import load_weights
 PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB_PATH = os.environ.get("FME_LIB_PATH") or os.path.join(PKG_ROOT, "libfme_amd.so")
 
-ABI_VERSION = 15
+ABI_VERSION = 16
 TIMING_NAMES = ("classify", "scatter", "search", "nn_tail", "batch", "search_main", "search_aux")
 
 # Every entry point include/fme.h declares (the ABI test checks the .so exports them).
@@ -34,6 +35,8 @@ ABI_SYMBOLS = (
     "fme_set_search_event", "fme_build_bipred_keys_device", "fme_set_nn_logit_output",
     "fme_set_nn_inputs", "fme_integer_search_ring", "fme_integer_search_ring_device",
     "fme_download_device", "fme_pred_inter_phases", "fme_set_search_reserve",
+    "fme_pack_jobs", "fme_unpack_jobs", "fme_refine_packed_device", "fme_refine_mv_packed_device",
+    "fme_integer_search2", "fme_integer_search2_device",
 )
 
 
@@ -115,6 +118,12 @@ def load_library(path=None):
         "fme_download_device": (I, [P, P, P, C.c_size_t, I, P]),
         "fme_pred_inter_phases": (I, [P, P, I]),
         "fme_set_search_reserve": (I, [P, I]),
+        "fme_pack_jobs": (I, [P, I, P, P]),
+        "fme_unpack_jobs": (I, [P, P, I, P]),
+        "fme_refine_packed_device": (I, [P, P, P, P, I, P]),
+        "fme_refine_mv_packed_device": (I, [P, P, P, P, I, P]),
+        "fme_integer_search2": (I, [P, P, P, P, I, P]),
+        "fme_integer_search2_device": (I, [P, P, P, P, I, P]),
     }
     # an explicitly named library is an A/B variant (tools/ab_bench.py): possibly an older ABI
     strict = os.path.abspath(path) == os.path.abspath(LIB_PATH)
@@ -172,6 +181,10 @@ class FmeContext:
             self.h = None
 
     def __del__(self):
+        # not at interpreter exit: the HIP runtime (and a profiler's hooks) may be torn down by
+        # then; callers close() explicitly (bench.py does, in a finally block)
+        if sys.is_finalizing():
+            return
         try:
             self.close()
         except Exception:
@@ -204,8 +217,15 @@ class FmeContext:
     # -- integer motion estimation ------------------------------------------------------------
     def integer_search(self, jobs, ext, stream=None):
         """xTZSearch / xPatternSearch per job (fme_integer_search): returns (jobs with mv_x/mv_y
-        = the integer MV, ruiSAD per job)."""
-        from .abi import TZ_EXT_DTYPE
+        = the integer MV, ruiSAD per job).  fme_tz_ext2 records (TZ_EXT2_DTYPE: FastSearch 0 / 3 with
+        the neighbour predictors) go to fme_integer_search2."""
+        from .abi import TZ_EXT_DTYPE, TZ_EXT2_DTYPE
+        if np.asarray(ext).dtype.itemsize == TZ_EXT2_DTYPE.itemsize:
+            jobs = np.array(jobs, dtype=JOB_DTYPE, copy=True)
+            ext = np.ascontiguousarray(ext, dtype=TZ_EXT2_DTYPE)
+            sad = np.zeros(len(jobs), np.uint32)
+            _check(self.lib, self.lib.fme_integer_search2(self.h, _ptr(jobs), _ptr(ext), _ptr(sad), len(jobs), stream))
+            return jobs, sad
         jobs = np.array(jobs, dtype=JOB_DTYPE, copy=True)
         ext = np.ascontiguousarray(ext, dtype=TZ_EXT_DTYPE)
         sad = np.zeros(len(jobs), np.uint32)
@@ -237,6 +257,11 @@ class FmeContext:
     def integer_search_device(self, d_jobs, d_ext, d_sad, n, stream=None):
         _check(self.lib, self.lib.fme_integer_search_device(self.h, C.c_void_p(d_jobs), C.c_void_p(d_ext),
                                                             C.c_void_p(d_sad), n, stream))
+
+    def integer_search2_device(self, d_jobs, d_ext2, d_sad, n, stream=None):
+        """fme_integer_search2_device: device jobs and fme_tz_ext2 records (FastSearch 0 / 3)."""
+        _check(self.lib, self.lib.fme_integer_search2_device(self.h, C.c_void_p(d_jobs), C.c_void_p(d_ext2),
+                                                             C.c_void_p(d_sad), n, stream))
 
     def integer_search_last_ms(self):
         ms = C.c_float()
@@ -395,6 +420,16 @@ class FmeContext:
     def refine_mv_device(self, jobs_ptr, out_ptr, n, stream=None):
         _check(self.lib, self.lib.fme_refine_mv_device(self.h, C.c_void_p(jobs_ptr), C.c_void_p(out_ptr), n, stream))
 
+    def refine_packed_device(self, pk_ptr, key_base_ptr, res_ptr, n, stream=None):
+        """fme_refine_packed_device: device-resident packed jobs (pack_jobs) -> full records."""
+        _check(self.lib, self.lib.fme_refine_packed_device(self.h, C.c_void_p(pk_ptr), C.c_void_p(key_base_ptr),
+                                                           C.c_void_p(res_ptr), n, stream))
+
+    def refine_mv_packed_device(self, pk_ptr, key_base_ptr, out_ptr, n, stream=None):
+        """fme_refine_mv_packed_device: device-resident packed jobs -> 16-byte fme_mv_result rows."""
+        _check(self.lib, self.lib.fme_refine_mv_packed_device(self.h, C.c_void_p(pk_ptr), C.c_void_p(key_base_ptr),
+                                                              C.c_void_p(out_ptr), n, stream))
+
     def refine_status(self):
         """Waits for the last batch: the number of jobs that made the device reject it (0: ran)."""
         rc = self.lib.fme_refine_status(self.h)
@@ -483,3 +518,26 @@ class FmeContext:
         out4 = np.zeros(4, np.int16)
         _check(self.lib, self.lib.fme_nn_pred_single(self.h, _ptr(e), int(c), int(pu_h), int(pu_w), C.byref(cls), _ptr(out4)))
         return cls.value, tuple(int(v) for v in out4)
+
+
+def pack_jobs(jobs, lib=None):
+    """fme_pack_jobs: fme_job rows -> (JOB_PACKED_DTYPE rows, int32 key_base per 64 jobs).  Raises
+    FmeError (FME_E_UNSUPPORTED) for a batch outside the packed form (include/fme.h)."""
+    from .abi import JOB_PACKED_DTYPE, PACK_WAVE
+    lib = lib or load_library()
+    jobs = np.ascontiguousarray(jobs, dtype=JOB_DTYPE)
+    out = np.zeros(len(jobs), dtype=JOB_PACKED_DTYPE)
+    base = np.zeros((len(jobs) + PACK_WAVE - 1) // PACK_WAVE, dtype=np.int32)
+    _check(lib, lib.fme_pack_jobs(_ptr(jobs), len(jobs), _ptr(out), _ptr(base)))
+    return out, base
+
+
+def unpack_jobs(packed, key_base, lib=None):
+    """fme_unpack_jobs: the canonical fme_job rows of packed jobs (what the device unpacks)."""
+    from .abi import JOB_PACKED_DTYPE
+    lib = lib or load_library()
+    packed = np.ascontiguousarray(packed, dtype=JOB_PACKED_DTYPE)
+    key_base = np.ascontiguousarray(key_base, dtype=np.int32)
+    out = np.zeros(len(packed), dtype=JOB_DTYPE)
+    _check(lib, lib.fme_unpack_jobs(_ptr(packed), _ptr(key_base), len(packed), _ptr(out)))
+    return out

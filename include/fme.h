@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define FME_ABI_VERSION 15
+#define FME_ABI_VERSION 16
 
 /* ---- error codes ---------------------------------------------------------------- */
 #define FME_OK            0
@@ -142,6 +142,35 @@ typedef struct fme_mv_result {
   uint8_t  reserved;
   uint16_t status;            /* FME_RES_*                                                     */
 } fme_mv_result;
+
+/* ---- the packed upload form of fme_job (16 bytes) ----------------------------------------- *
+ * What crosses PCIe per job when a caller hands a frame's jobs to the device (SURVEY.md §8(d)
+ * times the jobs' H2D): half of fme_job.  Nothing of xMotionEstimation's inputs is dropped:
+ *   pu   x/4 [0,11) | y/4 [11,22) | w/4-1 [22,26) | h/4-1 [26,30)   (HEVC PUs sit on the 4x4 grid)
+ *   ctl  org_id [0,6) | ref_id [6,12) | lambda_id [12,17) | FME_JOB_* flags [17,21) |
+ *        keyed [21] (key_offset >= 0) | EMI range bits [22,26) | bits_in [26,32)
+ *   mv, mvp as in fme_job.
+ * The search range enters the sub-pel path only through the EMI square step's four range tests
+ * around the TZ best (xTZ8PointSquareSearch, TEncSearch.cpp:1334-1376: mv.y-1 >= top,
+ * mv.y+1 <= bottom, mv.x-1 >= left, mv.x+1 <= right), so the packed job carries those four bits
+ * (FME_PK_RANGE_*) instead of the four range words.  Key blocks: key_base[w] (one int32 per 64
+ * jobs) is the key_offset of wave w's first keyed job (-1: none); the wave's later keyed jobs
+ * follow it densely in job order (offset of the previous keyed job + its w*h), which is how the
+ * producers and fme_build_bipred_keys lay keys out.  fme_pack_jobs refuses (FME_E_UNSUPPORTED,
+ * the first such job named in fme_last_error) a job outside this form: off the 4x4 grid, x or y
+ * >= 8192, a slot id >= 64 or lambda_id >= 32, bits_in >= 64, an int16-extreme mv, or a key
+ * offset that does not follow the wave's previous keyed block; such batches use fme_job.      */
+#define FME_PACK_WAVE        64
+#define FME_PK_RANGE_TOP     0x1u
+#define FME_PK_RANGE_BOTTOM  0x2u
+#define FME_PK_RANGE_LEFT    0x4u
+#define FME_PK_RANGE_RIGHT   0x8u
+typedef struct fme_job_packed {
+  uint32_t pu;
+  uint32_t ctl;
+  int16_t  mv_x, mv_y;
+  int16_t  mvp_x, mvp_y;
+} fme_job_packed;
 
 typedef struct fme_ctx fme_ctx;
 
@@ -331,6 +360,18 @@ int fme_refine_device(fme_ctx* ctx, const fme_job* d_jobs, fme_result* d_results
 int fme_refine_mv(fme_ctx* ctx, const fme_job* jobs, fme_mv_result* out, int n, void* stream);
 int fme_refine_mv_device(fme_ctx* ctx, const fme_job* d_jobs, fme_mv_result* d_out, int n,
                          void* stream);
+/* Packed jobs (fme_job_packed).  fme_pack_jobs: host, n jobs -> out[n] and key_base[ceil(n/64)]
+ * (pure host code, no context).  fme_unpack_jobs: the inverse, giving each job's canonical
+ * fme_job (range words mv -/+ the range bits, key_offset -1 for unkeyed jobs); the device path
+ * unpacks the same way.  fme_refine_packed_device / fme_refine_mv_packed_device: the device
+ * batch of fme_refine_device / fme_refine_mv_device over device-resident packed jobs (a 16-byte
+ * read and a 32-byte write per job in HBM before classify), identical results.               */
+int fme_pack_jobs(const fme_job* jobs, int n, fme_job_packed* out, int32_t* key_base);
+int fme_unpack_jobs(const fme_job_packed* packed, const int32_t* key_base, int n, fme_job* out);
+int fme_refine_packed_device(fme_ctx* ctx, const fme_job_packed* d_jobs, const int32_t* d_key_base,
+                             fme_result* d_results, int n, void* stream);
+int fme_refine_mv_packed_device(fme_ctx* ctx, const fme_job_packed* d_jobs, const int32_t* d_key_base,
+                                fme_mv_result* d_out, int n, void* stream);
 /* Waits for the last refinement batch; returns the number of jobs k_classify rejected in it
  * (0: the batch ran), or a negative FME_E_* code. */
 int fme_refine_status(fme_ctx* ctx);
@@ -354,6 +395,27 @@ int fme_refine_status(fme_ctx* ctx);
                                     every distortion pushed (fme_integer_search_ring; see
                                     FME_NN_IN_TZ_RING): job.mv_x/mv_y and sad[i] are then the MV
                                     after the ring, and its nine NN inputs are written            */
+/* The other FastSearch settings of TAppEncCfg.cpp:752 ("0:Full search 1:Diamond 2:Selective
+ * 3:Enhanced Diamond"; the default and every shipped cfg use 1), per uni-pred job:
+ *   FME_TZ_FULL      FastSearch 0, MESEARCH_FULL: xPatternSearch over the job's lt..rb
+ *                    (TEncSearch.cpp:4504-4507, 4627-4695), a strict minimum in raster order, as
+ *                    for bi-pred jobs.  The reference runs no EMI square step on this path, so its
+ *                    refinement jobs carry no FME_JOB_EMI (NN_pred then reads the carried inputs).
+ *   FME_TZ_ENHANCED  FastSearch 3, MESEARCH_DIAMOND_ENHANCED: xTZSearch(..., bExtendedSettings =
+ *                    true) (4726-4727, 4749-4768): the left / above / above-right neighbours' MVs
+ *                    tested as start points (m_acMvPredictors, xPatternSearchFast 4708-4713; from
+ *                    fme_tz_ext2.preds, zero through the 12-byte entry points), diamonds with the
+ *                    distance-1 corners, a half-range diamond search around the zero vector when
+ *                    the start is not zero, the adaptive raster (step 5, or step 6 over the halved
+ *                    range when the best is near), then the star refinement with corners.
+ * FastSearch 2 (xTZSearchSelective, 5054-5229) is not provided: with RestrictMESampling off (the
+ * default, TAppEncCfg.cpp:756) its xTZSearchHelp (1097-1150) moves pOrg / pCur by stride <<
+ * isubShift rows and calls the width's distortion function for iRows rows, and the SSE functions
+ * this path's setDistParam selects for widths 4..64 (TComRdCost.cpp:893-1205) ignore iSubShift, so
+ * the reference reads up to 8 rows past the PU in the CU-sized original buffer (past the buffer's
+ * end for a PU on the CU's bottom row): its result is not a function of the inputs.            */
+#define FME_TZ_FULL      0x04u
+#define FME_TZ_ENHANCED  0x08u
 
 typedef struct fme_tz_ext {
   uint16_t cu_x, cu_y;          /* luma origin of the PU's CU (TComDataCU::clipMv)              */
@@ -363,8 +425,20 @@ typedef struct fme_tz_ext {
   uint16_t reserved;
 } fme_tz_ext;   /* 12 bytes */
 
+/* fme_tz_ext plus xPatternSearchFast's neighbour predictors (FME_TZ_ENHANCED jobs). */
+typedef struct fme_tz_ext2 {
+  fme_tz_ext base;
+  int16_t    preds[3][2];       /* m_acMvPredictors[MD_LEFT, MD_ABOVE, MD_ABOVE_RIGHT] (getMvPredLeft /
+                                   Above / AboveRight, TEncSearch.cpp:4708-4713), quarter-pel     */
+} fme_tz_ext2;   /* 24 bytes */
+
 int fme_integer_search(fme_ctx* ctx, fme_job* jobs, const fme_tz_ext* ext, uint32_t* sad, int n,
                        void* stream);
+/* The same with fme_tz_ext2 records (host arrays / device arrays). */
+int fme_integer_search2(fme_ctx* ctx, fme_job* jobs, const fme_tz_ext2* ext, uint32_t* sad, int n,
+                        void* stream);
+int fme_integer_search2_device(fme_ctx* ctx, fme_job* d_jobs, const fme_tz_ext2* d_ext, uint32_t* d_sad,
+                               int n, void* stream);
 int fme_integer_search_device(fme_ctx* ctx, fme_job* d_jobs, const fme_tz_ext* d_ext, uint32_t* d_sad,
                               int n, void* stream);
 /* The same searches with the NN inputs of their FME_TZ_RING jobs: nn_in[9 i .. 9 i + 8] =

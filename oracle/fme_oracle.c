@@ -869,15 +869,23 @@ static void tz_help(tz_state* s, int x, int y, int point_nr, int dist) {
 
 typedef struct tz_range { int l, r, t, b; } tz_range;
 
-/* xTZ8PointDiamondSearch (TEncSearch.cpp:1379-1589), bCheckCornersAtDist1 = false. */
-static void tz_diamond(tz_state* s, const tz_range* R, int sx, int sy, int dist) {
+/* xTZ8PointDiamondSearch (TEncSearch.cpp:1379-1589); corners: bCheckCornersAtDist1 (1402-1451). */
+static void tz_diamond(tz_state* s, const tz_range* R, int sx, int sy, int dist, int corners) {
   const int top = sy - dist, bot = sy + dist, left = sx - dist, right = sx + dist;
   s->best_round += 1;
   if (dist == 1) {
-    if (top >= R->t) tz_help(s, sx, top, 2, dist);
+    if (top >= R->t) {
+      if (corners && left >= R->l) tz_help(s, left, top, 1, dist);
+      tz_help(s, sx, top, 2, dist);
+      if (corners && right <= R->r) tz_help(s, right, top, 3, dist);
+    }
     if (left >= R->l) tz_help(s, left, sy, 4, dist);
     if (right <= R->r) tz_help(s, right, sy, 5, dist);
-    if (bot <= R->b) tz_help(s, sx, bot, 7, dist);
+    if (bot <= R->b) {
+      if (corners && left >= R->l) tz_help(s, left, bot, 6, dist);
+      tz_help(s, sx, bot, 7, dist);
+      if (corners && right <= R->r) tz_help(s, right, bot, 8, dist);
+    }
   } else if (dist <= 8) {
     const int t2 = sy - (dist >> 1), b2 = sy + (dist >> 1), l2 = sx - (dist >> 1), r2 = sx + (dist >> 1);
     if (top >= R->t && left >= R->l && right <= R->r && bot <= R->b) {
@@ -986,8 +994,11 @@ static void tz_two_point(tz_state* s, const tz_range* R) {
   }
 }
 
-/* xTZSearch (TEncSearch.cpp:4737-5036) up to the EMI square step. */
-static void tz_search(tz_state* s, const fme_job* j, const fme_tz_ext* e, int pw, int ph) {
+/* xTZSearch (TEncSearch.cpp:4737-5036) up to the EMI square step; e->flags FME_TZ_ENHANCED:
+ * bExtendedSettings = true (FastSearch 3, 4726-4727) with the neighbour predictors preds[3]
+ * (m_acMvPredictors, TEncSearch.cpp:4708-4713, quarter-pel; NULL = zero). */
+static void tz_search(tz_state* s, const fme_job* j, const fme_tz_ext* e, const int16_t (*preds)[2], int pw, int ph) {
+  const int ext = (e->flags & FME_TZ_ENHANCED) && !(e->flags & FME_TZ_FULL) && !s->ring;
   const int range = e->search_range ? e->search_range : 64;
   int sx = j->mvp_x, sy = j->mvp_y;
   tz_clip(&sx, &sy, pw, ph, e->cu_x, e->cu_y);
@@ -995,6 +1006,15 @@ static void tz_search(tz_state* s, const fme_job* j, const fme_tz_ext* e, int pw
   sy = mv_round4(sy);
   s->best_sad = 0xFFFFFFFFu;
   tz_help(s, sx, sy, 0, 0);
+  if (ext) {   /* bTestOtherPredictedMV (4787-4805): "only test cMv if not obviously previously tested" */
+    for (int k = 0; k < 3; k++) {
+      int px = preds ? preds[k][0] : 0, py = preds ? preds[k][1] : 0;
+      tz_clip(&px, &py, pw, ph, e->cu_x, e->cu_y);
+      px = mv_round4(px);
+      py = mv_round4(py);
+      if ((px != sx || py != sy) && (px != s->best_x && py != s->best_y)) tz_help(s, px, py, 0, 0);
+    }
+  }
   if ((sx != 0 || sy != 0) && (s->best_x != 0 || s->best_y != 0)) tz_help(s, 0, 0, 0, 0);
   const tz_range R = {j->lt_x, j->rb_x, j->lt_y, j->rb_y};
   tz_range raster = R;
@@ -1015,25 +1035,39 @@ static void tz_search(tz_state* s, const fme_job* j, const fme_tz_ext* e, int pw
     raster.r = mv_round4(rx);
     raster.b = mv_round4(ry);
   }
+  const int best_zero = s->best_x == 0 && s->best_y == 0;   /* bBestCandidateZero (4857) */
   const int startx = s->best_x, starty = s->best_y;
   for (int d = 1; d <= range; d *= 2) {   /* first search, stops 3 rounds after the best */
-    tz_diamond(s, &R, startx, starty, d);
+    tz_diamond(s, &R, startx, starty, d, ext);
     if (s->best_round >= 3) break;
+  }
+  if (ext && !best_zero) {   /* bNewZeroNeighbourhoodTest (4900-4917): half the range around zero */
+    for (int d = 1; d <= (range >> 1); d *= 2) tz_diamond(s, &R, 0, 0, d, 0);
   }
   if (s->best_dist == 1) {
     s->best_dist = 0;
     tz_two_point(s, &R);
   }
-  if (s->best_dist > 5) {   /* raster search, iRaster = 5 */
+  if (ext) {   /* bUseAdaptiveRaster (4926-4951): step 5, or 6 over the halved range when near */
+    int win = 5;
+    tz_range rr = raster;
+    if (!(s->best_dist > 5)) {
+      win = 6;
+      rr.l /= 2; rr.r /= 2; rr.t /= 2; rr.b /= 2;   /* C++ division: towards zero */
+    }
+    s->best_dist = win;
+    for (int y = rr.t; y <= rr.b; y += win)
+      for (int x = rr.l; x <= rr.r; x += win) tz_help(s, x, y, 0, win);
+  } else if (s->best_dist > 5) {   /* raster search, iRaster = 5 */
     s->best_dist = 5;
     for (int y = raster.t; y <= raster.b; y += 5)
       for (int x = raster.l; x <= raster.r; x += 5) tz_help(s, x, y, 0, 5);
   }
-  while (s->best_dist > 0) {   /* star refinement */
+  while (s->best_dist > 0) {   /* star refinement (corners at distance 1 when extended) */
     const int bx = s->best_x, by = s->best_y;
     s->best_dist = 0;
     s->point_nr = 0;
-    for (int d = 1; d < range + 1; d *= 2) tz_diamond(s, &R, bx, by, d);
+    for (int d = 1; d < range + 1; d *= 2) tz_diamond(s, &R, bx, by, d, ext);
     if (s->best_dist == 1) {
       s->best_dist = 0;
       if (s->point_nr != 0) tz_two_point(s, &R);
@@ -1074,12 +1108,25 @@ static void tz_search(tz_state* s, const fme_job* j, const fme_tz_ext* e, int pw
   }
 }
 
+/* ext records of `stride` bytes (fme_tz_ext, or fme_tz_ext2 with the predictors after it) */
+static int tz_run_jobs(orc_ctx* ctx, fme_job* jobs, const void* ext0, size_t stride, uint32_t* sad, uint32_t* nn_in,
+                       int n);
+
 int orc_integer_search(orc_ctx* ctx, fme_job* jobs, const fme_tz_ext* ext, uint32_t* sad, int n) {
-  return orc_integer_search_ring(ctx, jobs, ext, sad, NULL, n);
+  return tz_run_jobs(ctx, jobs, ext, sizeof(fme_tz_ext), sad, NULL, n);
+}
+
+int orc_integer_search2(orc_ctx* ctx, fme_job* jobs, const fme_tz_ext2* ext, uint32_t* sad, int n) {
+  return tz_run_jobs(ctx, jobs, ext, sizeof(fme_tz_ext2), sad, NULL, n);
 }
 
 int orc_integer_search_ring(orc_ctx* ctx, fme_job* jobs, const fme_tz_ext* ext, uint32_t* sad, uint32_t* nn_in,
                             int n) {
+  return tz_run_jobs(ctx, jobs, ext, sizeof(fme_tz_ext), sad, nn_in, n);
+}
+
+static int tz_run_jobs(orc_ctx* ctx, fme_job* jobs, const void* ext0, size_t stride, uint32_t* sad, uint32_t* nn_in,
+                       int n) {
   int16_t* key = (int16_t*)malloc(sizeof(int16_t) * 64 * 64);
   int16_t* cur = (int16_t*)malloc(sizeof(int16_t) * 64 * 64);
   for (int i = 0; i < n; i++) {
@@ -1106,10 +1153,13 @@ int orc_integer_search_ring(orc_ctx* ctx, fme_job* jobs, const fme_tz_ext* ext, 
     s.ref = ref; s.key = key; s.x0 = j->x; s.y0 = j->y; s.w = w; s.h = h;
     s.fen = ctx->cfg.fast_inter_mode; s.mvp_x = j->mvp_x; s.mvp_y = j->mvp_y;
     s.ml = ctx->mlambda[j->lambda_id]; s.cur = cur;
-    s.ring = nn_in != NULL && (ext[i].flags & FME_TZ_RING) && !(j->flags & FME_JOB_BIPRED);
+    const fme_tz_ext* e = (const fme_tz_ext*)((const char*)ext0 + stride * (size_t)i);
+    const int16_t (*preds)[2] = stride >= sizeof(fme_tz_ext2) ? ((const fme_tz_ext2*)e)->preds : NULL;
+    s.ring = nn_in != NULL && (e->flags & FME_TZ_RING) && !(j->flags & FME_JOB_BIPRED);
     s.cmin = 0xFFFFFFFFu;
-    if (j->flags & FME_JOB_BIPRED) {
-      /* xPatternSearch (TEncSearch.cpp:4627-4680): raster order, strict minimum */
+    if ((j->flags & FME_JOB_BIPRED) || ((e->flags & FME_TZ_FULL) && !s.ring)) {
+      /* xPatternSearch (TEncSearch.cpp:4627-4680): raster order, strict minimum (bi-pred jobs, and
+       * every job at FastSearch 0, 4504-4507) */
       s.best_sad = 0xFFFFFFFFu;
       for (int y = j->lt_y; y <= j->rb_y; y++)
         for (int x = j->lt_x; x <= j->rb_x; x++) {
@@ -1119,7 +1169,7 @@ int orc_integer_search_ring(orc_ctx* ctx, fme_job* jobs, const fme_tz_ext* ext, 
           if (d < s.best_sad) { s.best_sad = d; s.best_x = x; s.best_y = y; }
         }
     } else {
-      tz_search(&s, j, &ext[i], ref->width, ref->height);
+      tz_search(&s, j, e, preds, ref->width, ref->height);
     }
     j->mv_x = (int16_t)s.best_x;
     j->mv_y = (int16_t)s.best_y;

@@ -131,6 +131,8 @@ int orc_refine(orc_ctx* ctx, const fme_job* jobs, fme_result* res, int n);
 /* ---- integer motion estimation: xTZSearch / xPatternSearch per job;
  * writes jobs[i].mv_x/mv_y and sad[i].  Returns 0 or a negative FME_E_* code. */
 int orc_integer_search(orc_ctx* ctx, fme_job* jobs, const fme_tz_ext* ext, uint32_t* sad, int n);
+/* fme_tz_ext2 records: FME_TZ_FULL / FME_TZ_ENHANCED with the neighbour predictors (fme.h) */
+int orc_integer_search2(orc_ctx* ctx, fme_job* jobs, const fme_tz_ext2* ext, uint32_t* sad, int n);
 /* the same with the backups' tail for FME_TZ_RING jobs: nn_in[9 i ..] = array_e[index_ref .. +7], C */
 int orc_integer_search_ring(orc_ctx* ctx, fme_job* jobs, const fme_tz_ext* ext, uint32_t* sad,
                             uint32_t* nn_in, int n);

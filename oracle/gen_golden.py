@@ -193,6 +193,54 @@ def build_tz_case(name, seed, width, height, calls, fen, search_range, bipred, m
           f"{int((ext['flags'] != 0).sum())} with a 2Nx2N start, {int((far > 4 * 20).sum())} ending > 20 px from the predictor")
 
 
+def build_tz2_case(name, seed, width, height, calls, fen, search_range, bipred, mvp_noise, mode):
+    """The other FastSearch settings (fme_tz_ext2): FastSearch 0 (FME_TZ_FULL, xPatternSearch for every
+    job) or 3 (FME_TZ_ENHANCED, xTZSearch with bExtendedSettings and the neighbour predictors
+    m_acMvPredictors) from _ref; the oracle must agree.  The predictors: near the AMVP predictor, some
+    equal to it, some zero, some far (the start-point tests' "not obviously previously tested"
+    conditions both ways)."""
+    from nnfme.abi import TZ_EXT2_DTYPE
+    rng = np.random.default_rng(seed)
+    pics = {i: synth.synth_luma(width, height, i, seed=seed) for i in range(5)}
+    lambdas = np.array(synth.LDP_LAMBDA[22], dtype=np.float64)
+    jobs, ext = synth.make_tz_jobs(rng, width, height, calls, 4, [0, 1, 2, 3], [0, 1, 2, 3], bipred_frac=bipred,
+                                   search_range=search_range, mvp_noise=mvp_noise)
+    keys = synth.make_bipred_keys(rng, jobs, pics)
+    n = len(jobs)
+    ext2 = np.zeros(n, dtype=TZ_EXT2_DTYPE)
+    ext2["base"] = ext
+    uni = (jobs["flags"] & JOB_BIPRED) == 0
+    ext2["base"]["flags"] = np.where(uni, ext["flags"] | mode, ext["flags"])
+    kind = rng.integers(0, 4, (n, 3))
+    for c, comp in ((0, "mvp_x"), (1, "mvp_y")):
+        base = jobs[comp].astype(np.int64)[:, None]
+        near = base + rng.integers(-12, 13, (n, 3))
+        far = rng.integers(-4 * 3 * search_range, 4 * 3 * search_range + 1, (n, 3))
+        v = np.where(kind == 0, base, np.where(kind == 1, 0, np.where(kind == 2, near, far)))
+        ext2["preds"][:, :, c] = np.clip(v, -32768, 32767)
+    ref = Reference(fast_inter_mode=fen)
+    orc = Oracle(fast_inter_mode=fen)
+    for eng in (ref, orc):
+        for k, v in pics.items():
+            eng.set_picture(k, v)
+        for lid, lam in enumerate(lambdas):
+            eng.set_lambda(lid, float(lam))
+        eng.set_keys(keys if keys.size else np.zeros(1, np.int16))
+    out_r, sad_r = ref.integer_search2(jobs, ext2)
+    out_o, sad_o = orc.integer_search2(jobs, ext2)
+    bad = (out_r["mv_x"] != out_o["mv_x"]) | (out_r["mv_y"] != out_o["mv_y"]) | (sad_r != sad_o)
+    if bad.any():
+        raise SystemExit(f"{name}: oracle disagrees with _ref on {int(bad.sum())} jobs")
+    # against the shipped FastSearch 1 on the same jobs: the setting changes results
+    base_r, _ = ref.integer_search(jobs, ext)
+    differ = int(((base_r["mv_x"] != out_r["mv_x"]) | (base_r["mv_y"] != out_r["mv_y"])).sum())
+    path = os.path.join(OUT, f"{name}.npz")
+    np.savez_compressed(path, pictures=np.stack([pics[i] for i in range(5)]), lambdas=lambdas, keys=keys,
+                        jobs=jobs, ext=ext2, mv_x=out_r["mv_x"], mv_y=out_r["mv_y"], sad=sad_r,
+                        config=np.array([fen, search_range], dtype=np.int32))
+    print(f"{path}: {n} jobs, {int((~uni).sum())} bi-pred, mode 0x{mode:x}, {differ} MVs differ from FastSearch 1")
+
+
 def build_ring_case(name, seed, width, height, calls, fen, search_range, bipred, mvp_noise, net, qp=22):
     """The backups' own NN input path (configs[4]): xTZSearch with the final square + ring, every
     distortion pushed (FME_TZ_RING: mv, sad and the nine NN inputs per job), then the sub-pel path
@@ -255,6 +303,13 @@ TZ_CASES = [
     ("tz_far_fen0_sr32", 32, 160, 96, 40, 0, 32, 0.1, 200),
 ]
 
+TZ2_CASES = [
+    # name, seed, W, H, calls/CTU/ref, FEN, SearchRange, bi-pred share, predictor noise (qpel), mode
+    ("tz_full_sr8_fen1", 33, 128, 96, 10, 1, 8, 0.1, 24, 0x04),
+    ("tz_enhanced_fen1", 34, 160, 96, 30, 1, 64, 0.1, 24, 0x08),
+    ("tz_enhanced_far_fen0_sr32", 35, 160, 96, 30, 0, 32, 0.1, 200, 0x08),
+]
+
 MC_CASES = [
     # name, seed, W, H, bi_frac, mv_amp (pel), identical_frac, keep_frac, fill
     ("mc_ldp_uni", 21, 160, 104, 0.0, 40, 0.0, 1.0, 0),
@@ -314,6 +369,10 @@ def main():
         for c in MAIN10_CASES:
             build_case(*c)
         return 0
+    if "--tz2-only" in sys.argv:
+        for c in TZ2_CASES:
+            build_tz2_case(*c)
+        return 0
     if "--ring-only" in sys.argv:
         for c in RING_CASES:
             build_ring_case(*c)
@@ -330,6 +389,8 @@ def main():
             build_mc_case(*c)
     for c in TZ_CASES:
         build_tz_case(*c)
+    for c in TZ2_CASES:
+        build_tz2_case(*c)
     return 0
 
 

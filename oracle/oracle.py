@@ -69,6 +69,8 @@ class Oracle:
         lib.orc_integer_search.argtypes = [_P, _P, _P, _P, C.c_int]
         lib.orc_integer_search_ring.restype = C.c_int
         lib.orc_integer_search_ring.argtypes = [_P, _P, _P, _P, _P, C.c_int]
+        lib.orc_integer_search2.restype = C.c_int
+        lib.orc_integer_search2.argtypes = [_P, _P, _P, _P, C.c_int]
         lib.orc_set_nn_inputs.argtypes = [_P, _P, C.c_int]
         lib.orc_pred_inter_p.restype = C.c_int
         lib.orc_pred_inter_p.argtypes = [_P, _P, _P, C.c_int]
@@ -175,13 +177,27 @@ class Oracle:
         return cls, logits
 
     def integer_search(self, jobs, ext):
-        """orc_integer_search: returns (jobs with mv_x/mv_y = the integer MV, sad)."""
+        """orc_integer_search: returns (jobs with mv_x/mv_y = the integer MV, sad); fme_tz_ext2
+        records (24 bytes) go to orc_integer_search2."""
+        if np.asarray(ext).dtype.itemsize == 24:
+            return self.integer_search2(jobs, ext)
         jobs = np.array(jobs, copy=True)
         ext = np.ascontiguousarray(ext)
         sad = np.zeros(len(jobs), np.uint32)
         rc = self.lib.orc_integer_search(self.ctx, _ptr(jobs), _ptr(ext), _ptr(sad), len(jobs))
         if rc != 0:
             raise RuntimeError(f"orc_integer_search failed: {rc}")
+        return jobs, sad
+
+    def integer_search2(self, jobs, ext2):
+        """orc_integer_search2: fme_tz_ext2 records (FastSearch 0 / 3 flags, neighbour predictors)."""
+        jobs = np.array(jobs, copy=True)
+        ext2 = np.ascontiguousarray(ext2)
+        assert ext2.dtype.itemsize == 24
+        sad = np.zeros(len(jobs), np.uint32)
+        rc = self.lib.orc_integer_search2(self.ctx, _ptr(jobs), _ptr(ext2), _ptr(sad), len(jobs))
+        if rc != 0:
+            raise RuntimeError(f"orc_integer_search2 failed: {rc}")
         return jobs, sad
 
     def integer_search_ring(self, jobs, ext):
@@ -311,6 +327,8 @@ class Reference:
         lib.ref_integer_search.argtypes = [_P, _P, _P, _P, C.c_int]
         lib.ref_integer_search_ring.restype = C.c_int
         lib.ref_integer_search_ring.argtypes = [_P, _P, _P, _P, _P, C.c_int]
+        lib.ref_integer_search2.restype = C.c_int
+        lib.ref_integer_search2.argtypes = [_P, _P, _P, _P, C.c_int]
         lib.ref_set_nn_inputs.argtypes = [_P, _P, C.c_int]
         lib.ref_template_cost.restype = C.c_uint32
         lib.ref_template_cost.argtypes = [_P] + [C.c_int] * 12
@@ -343,12 +361,24 @@ class Reference:
                                      y.shape[0])
 
     def integer_search(self, jobs, ext):
+        if np.asarray(ext).dtype.itemsize == 24:   # fme_tz_ext2
+            return self.integer_search2(jobs, ext)
         jobs = np.array(jobs, copy=True)
         ext = np.ascontiguousarray(ext)
         sad = np.zeros(len(jobs), np.uint32)
         rc = self.lib.ref_integer_search(self.h, _ptr(jobs), _ptr(ext), _ptr(sad), len(jobs))
         if rc != 0:
             raise RuntimeError(f"ref_integer_search failed: {rc}")
+        return jobs, sad
+
+    def integer_search2(self, jobs, ext2):
+        jobs = np.array(jobs, copy=True)
+        ext2 = np.ascontiguousarray(ext2)
+        assert ext2.dtype.itemsize == 24
+        sad = np.zeros(len(jobs), np.uint32)
+        rc = self.lib.ref_integer_search2(self.h, _ptr(jobs), _ptr(ext2), _ptr(sad), len(jobs))
+        if rc != 0:
+            raise RuntimeError(f"ref_integer_search2 failed: {rc}")
         return jobs, sad
 
     def integer_search_ring(self, jobs, ext):

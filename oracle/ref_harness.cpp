@@ -809,14 +809,31 @@ struct Tz {
       }
     }
   }
-  void diamond(TzStruct& t, int sx, int sy, int iDist) {   // xTZ8PointDiamondSearch, corners off
+  // xTZ8PointDiamondSearch (TEncSearch.cpp:1379-1589), bCheckCornersAtDist1 = corners
+  void diamond(TzStruct& t, int sx, int sy, int iDist, bool corners = false) {
     const int iTop = sy - iDist, iBottom = sy + iDist, iLeft = sx - iDist, iRight = sx + iDist;
     t.uiBestRound += 1;
     if (iDist == 1) {
-      if (iTop >= lt_y) help(t, sx, iTop, 2, iDist);
+      if (iTop >= lt_y) {
+        if (corners) {
+          if (iLeft >= lt_x) help(t, iLeft, iTop, 1, iDist);
+          help(t, sx, iTop, 2, iDist);
+          if (iRight <= rb_x) help(t, iRight, iTop, 3, iDist);
+        } else {
+          help(t, sx, iTop, 2, iDist);
+        }
+      }
       if (iLeft >= lt_x) help(t, iLeft, sy, 4, iDist);
       if (iRight <= rb_x) help(t, iRight, sy, 5, iDist);
-      if (iBottom <= rb_y) help(t, sx, iBottom, 7, iDist);
+      if (iBottom <= rb_y) {
+        if (corners) {
+          if (iLeft >= lt_x) help(t, iLeft, iBottom, 6, iDist);
+          help(t, sx, iBottom, 7, iDist);
+          if (iRight <= rb_x) help(t, iRight, iBottom, 8, iDist);
+        } else {
+          help(t, sx, iBottom, 7, iDist);
+        }
+      }
       return;
     }
     if (iDist <= 8) {
@@ -944,16 +961,25 @@ struct Tz {
 };
 }  // namespace
 
+static int ref_tz_run(void* h, fme_job* jobs, const void* ext0, size_t stride, uint32_t* sad, uint32_t* nn_in,
+                      int n);
 extern "C" int ref_integer_search_ring(void* h, fme_job* jobs, const fme_tz_ext* ext, uint32_t* sad,
-                                       uint32_t* nn_in, int n);
+                                       uint32_t* nn_in, int n) {
+  return ref_tz_run(h, jobs, ext, sizeof(fme_tz_ext), sad, nn_in, n);
+}
 extern "C" int ref_integer_search(void* h, fme_job* jobs, const fme_tz_ext* ext, uint32_t* sad, int n) {
-  return ref_integer_search_ring(h, jobs, ext, sad, nullptr, n);
+  return ref_tz_run(h, jobs, ext, sizeof(fme_tz_ext), sad, nullptr, n);
+}
+// FastSearch 0 (FME_TZ_FULL: xPatternSearch, TEncSearch.cpp:4504-4507) and 3 (FME_TZ_ENHANCED:
+// xTZSearch with bExtendedSettings, 4726-4727) with the neighbour predictors of fme_tz_ext2
+extern "C" int ref_integer_search2(void* h, fme_job* jobs, const fme_tz_ext2* ext, uint32_t* sad, int n) {
+  return ref_tz_run(h, jobs, ext, sizeof(fme_tz_ext2), sad, nullptr, n);
 }
 
 // nn_in != null: FME_TZ_RING jobs run the backups' xTZSearch tail (Backups/4:4868-4878) and get the
 // inputs xPatternSearchFast builds from array_e (:4343-4359).
-extern "C" int ref_integer_search_ring(void* h, fme_job* jobs, const fme_tz_ext* ext, uint32_t* sad,
-                                       uint32_t* nn_in, int n) {
+static int ref_tz_run(void* h, fme_job* jobs, const void* ext0, size_t stride, uint32_t* sad, uint32_t* nn_in,
+                      int n) {
   RefCtx* c = static_cast<RefCtx*>(h);
   RefSearch& s = c->s;
   std::vector<Pel> keybuf(64 * 64);
@@ -980,23 +1006,34 @@ extern "C" int ref_integer_search_ring(void* h, fme_job* jobs, const fme_tz_ext*
     s.rd.setPredictor(pred);
     s.rd.setCostScale(2);
     std::vector<long> array_e;   // counter_i = 0 at the call's start (the previous call's memset)
-    const bool ring = nn_in && (ext[i].flags & FME_TZ_RING) && !(j.flags & FME_JOB_BIPRED);
+    const fme_tz_ext& e = *reinterpret_cast<const fme_tz_ext*>(static_cast<const char*>(ext0) + stride * (size_t)i);
+    const int16_t(*preds)[2] = stride >= sizeof(fme_tz_ext2) ? reinterpret_cast<const fme_tz_ext2*>(&e)->preds : nullptr;
+    const bool ring = nn_in && (e.flags & FME_TZ_RING) && !(j.flags & FME_JOB_BIPRED);
     Tz tz{s, &key, refY, rs, j.lt_x, j.lt_y, j.rb_x, j.rb_y, ring ? &array_e : nullptr};
     TzStruct t{std::numeric_limits<Distortion>::max(), 0, 0, 0, 0, 0};
     const int pw = ref.getWidth(COMPONENT_Y), ph = ref.getHeight(COMPONENT_Y);
-    if (j.flags & FME_JOB_BIPRED) {   // xPatternSearch
+    // (FME_TZ_RING, the backups' FastSearch 1 path, takes precedence over FastSearch 0 / 3)
+    if ((j.flags & FME_JOB_BIPRED) || ((e.flags & FME_TZ_FULL) && !ring)) {   // xPatternSearch (bi-pred; FastSearch 0)
       for (int y = j.lt_y; y <= j.rb_y; y++)
         for (int x = j.lt_x; x <= j.rb_x; x++) {
           Distortion d = s.intDist(&key, refY, rs, x, y) + s.rd.getCostOfVectorWithPredictor(x, y);
           if (d < t.uiBestSad) { t.uiBestSad = d; t.iBestX = x; t.iBestY = y; }
         }
     } else {
-      const fme_tz_ext& e = ext[i];
+      const bool bExt = (e.flags & FME_TZ_ENHANCED) && !(e.flags & FME_TZ_FULL) && !ring;   // bExtendedSettings (TEncSearch.cpp:4749-4768)
       const int uiSearchRange = e.search_range ? e.search_range : 64;
       TComMv rcMv(j.mvp_x, j.mvp_y);
       tz.clipMv(rcMv, pw, ph, e.cu_x, e.cu_y);
       rcMv.divideByPowerOf2(2);
       tz.help(t, rcMv.getHor(), rcMv.getVer(), 0, 0);
+      if (bExt) {   // bTestOtherPredictedMV (4787-4805)
+        for (int index = 0; index < 3; index++) {
+          TComMv cMv(preds ? preds[index][0] : 0, preds ? preds[index][1] : 0);
+          tz.clipMv(cMv, pw, ph, e.cu_x, e.cu_y);
+          cMv.divideByPowerOf2(2);
+          if (cMv != rcMv && (cMv.getHor() != t.iBestX && cMv.getVer() != t.iBestY)) tz.help(t, cMv.getHor(), cMv.getVer(), 0, 0);
+        }
+      }
       if ((rcMv.getHor() != 0 || rcMv.getVer() != 0) && (0 != t.iBestX || 0 != t.iBestY)) tz.help(t, 0, 0, 0, 0);
       int rL = j.lt_x, rR = j.rb_x, rT = j.lt_y, rB = j.rb_y;
       if (e.flags & FME_TZ_PRED2NX2N) {
@@ -1017,16 +1054,29 @@ extern "C" int ref_integer_search_ring(void* h, fme_job* jobs, const fme_tz_ext*
         rb.divideByPowerOf2(2);
         rL = lt.getHor(); rR = rb.getHor(); rT = lt.getVer(); rB = rb.getVer();
       }
+      const bool bBestCandidateZero = t.iBestX == 0 && t.iBestY == 0;   // 4857
       int iStartX = t.iBestX, iStartY = t.iBestY;
       for (int iDist = 1; iDist <= uiSearchRange; iDist *= 2) {
-        tz.diamond(t, iStartX, iStartY, iDist);
+        tz.diamond(t, iStartX, iStartY, iDist, bExt);   // bFirstCornersForDiamondDist1
         if (t.uiBestRound >= 3) break;
       }
+      if (bExt && !bBestCandidateZero)   // bNewZeroNeighbourhoodTest, bTestZeroVectorStart (4900-4917)
+        for (int iDist = 1; iDist <= (uiSearchRange >> 1); iDist *= 2) tz.diamond(t, 0, 0, iDist, false);
       if (t.uiBestDistance == 1) {
         t.uiBestDistance = 0;
         tz.twoPoint(t);
       }
-      if ((int)t.uiBestDistance > 5) {
+      if (bExt) {   // bUseAdaptiveRaster (4926-4951)
+        int iWindowSize = 5;
+        int L = rL, R = rR, T = rT, B = rB;
+        if (!((int)t.uiBestDistance > 5)) {
+          iWindowSize++;
+          L /= 2; R /= 2; T /= 2; B /= 2;
+        }
+        t.uiBestDistance = iWindowSize;
+        for (iStartY = T; iStartY <= B; iStartY += iWindowSize)
+          for (iStartX = L; iStartX <= R; iStartX += iWindowSize) tz.help(t, iStartX, iStartY, 0, iWindowSize);
+      } else if ((int)t.uiBestDistance > 5) {
         t.uiBestDistance = 5;
         for (iStartY = rT; iStartY <= rB; iStartY += 5)
           for (iStartX = rL; iStartX <= rR; iStartX += 5) tz.help(t, iStartX, iStartY, 0, 5);
@@ -1036,7 +1086,7 @@ extern "C" int ref_integer_search_ring(void* h, fme_job* jobs, const fme_tz_ext*
         iStartY = t.iBestY;
         t.uiBestDistance = 0;
         t.ucPointNr = 0;
-        for (int iDist = 1; iDist < uiSearchRange + 1; iDist *= 2) tz.diamond(t, iStartX, iStartY, iDist);
+        for (int iDist = 1; iDist < uiSearchRange + 1; iDist *= 2) tz.diamond(t, iStartX, iStartY, iDist, bExt);
         if (t.uiBestDistance == 1) {
           t.uiBestDistance = 0;
           if (t.ucPointNr != 0) tz.twoPoint(t);

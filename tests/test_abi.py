@@ -13,17 +13,17 @@ from nnfme import abi, runtime
 def header_functions():
     txt = open(os.path.join(ROOT, "include", "fme.h")).read()
     txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
-    return sorted(set(re.findall(r"\b(fme_[a-z_]+)\s*\(", txt)))
+    return sorted(set(re.findall(r"\b(fme_[a-z0-9_]+)\s*\(", txt)))
 
 
 def test_library_exports_header():
     lib = runtime.load_library()
     names = header_functions()
-    assert len(names) == 53
+    assert len(names) == 59
     assert set(names) == set(runtime.ABI_SYMBOLS)
     for n in names:
         assert hasattr(lib, n), n
-    assert lib.fme_abi_version() == runtime.ABI_VERSION == 15
+    assert lib.fme_abi_version() == runtime.ABI_VERSION == 16
 
 
 def test_struct_layouts():
@@ -76,6 +76,9 @@ def test_null_arguments_rejected():
     assert lib.fme_refine(None, None, None, 1, None) == -1
     assert lib.fme_refine_mv(None, None, None, 1, None) == -1
     assert lib.fme_refine_mv_device(None, None, None, 1, None) == -1
+    assert lib.fme_refine_mv_packed_device(None, None, None, None, 1, None) == -1
+    assert lib.fme_refine_packed_device(None, None, None, None, 1, None) == -1
+    assert lib.fme_pack_jobs(None, 1, None, None) == -1
     assert lib.fme_refine_status(None) == -1
     assert lib.fme_nn_copy_state_device(None, None, None) == -1
     assert lib.fme_set_search_event(None, None) == -1
@@ -98,3 +101,74 @@ def test_hm_adapter_library_exports():
         assert sym in out, sym
     deps = subprocess.run(["ldd", so], capture_output=True, text=True).stdout
     assert "libfme_amd.so" in deps
+
+
+# ---- fme_job_packed (ABI 16): host packing, pure host code -----------------------------------
+def _frame_jobs(bipred=0.0, W=416, H=240):
+    from nnfme import synth
+    rng = np.random.default_rng(11)
+    jobs = synth.make_ctu_jobs(rng, W, H, 331, 4, [0, 1, 2, 3], [0], bipred_frac=bipred)
+    if bipred:
+        synth.make_bipred_key_reqs(np.random.default_rng(12), jobs, 4, [0, 1, 2, 3])
+    return jobs
+
+
+def _same_refinement_inputs(u, jobs):
+    """What the sub-pel path reads of a job: every field, except that the range words enter only
+    through the EMI step's four tests (TEncSearch.cpp:1341-1376) and a negative key offset only as
+    'unkeyed'."""
+    for f in abi.JOB_DTYPE.names:
+        if f in ("lt_x", "lt_y", "rb_x", "rb_y", "key_offset"):
+            continue
+        assert np.array_equal(u[f], jobs[f]), f
+    mx, my = jobs["mv_x"].astype(int), jobs["mv_y"].astype(int)
+    assert np.array_equal(my - 1 >= u["lt_y"], my - 1 >= jobs["lt_y"])
+    assert np.array_equal(my + 1 <= u["rb_y"], my + 1 <= jobs["rb_y"])
+    assert np.array_equal(mx - 1 >= u["lt_x"], mx - 1 >= jobs["lt_x"])
+    assert np.array_equal(mx + 1 <= u["rb_x"], mx + 1 <= jobs["rb_x"])
+    assert np.array_equal(u["key_offset"], np.where(jobs["key_offset"] >= 0, jobs["key_offset"], -1))
+
+
+def test_pack_jobs_round_trip():
+    assert abi.JOB_PACKED_DTYPE.itemsize == 16
+    for bipred in (0.0, 0.3):
+        jobs = _frame_jobs(bipred)
+        pk, kb = runtime.pack_jobs(jobs)
+        assert len(kb) == (len(jobs) + 63) // 64
+        _same_refinement_inputs(runtime.unpack_jobs(pk, kb), jobs)
+        if bipred:
+            assert (kb >= 0).any() and (jobs["key_offset"] >= 0).sum() > 1000
+
+
+def test_pack_jobs_edges_and_refusals():
+    jobs = _frame_jobs()[:300].copy()
+    # range edges: every combination of the four EMI tests survives the packing
+    jobs["lt_x"] = jobs["mv_x"] - (np.arange(300) & 1)
+    jobs["rb_x"] = jobs["mv_x"] + ((np.arange(300) >> 1) & 1)
+    jobs["lt_y"] = jobs["mv_y"] - ((np.arange(300) >> 2) & 1) * 7
+    jobs["rb_y"] = jobs["mv_y"] + ((np.arange(300) >> 3) & 1) * 64
+    jobs["bits_in"] = np.arange(300) % 64
+    jobs["lambda_id"] = np.arange(300) % 32
+    pk, kb = runtime.pack_jobs(jobs)
+    _same_refinement_inputs(runtime.unpack_jobs(pk, kb), jobs)
+    lib = runtime.load_library()
+    for field, value in (("x", 6), ("w", 6), ("bits_in", 64), ("lambda_id", 32), ("ref_id", 64),
+                         ("flags", 16), ("mv_x", 32767)):
+        bad = jobs.copy()
+        bad[field][5] = value
+        with pytest.raises(runtime.FmeError) as e:
+            runtime.pack_jobs(bad)
+        assert e.value.code == -4 and b"job 5" in lib.fme_last_error()
+    # keyed blocks must follow each other within a wave
+    bad = jobs.copy()
+    bad["key_offset"][3] = 0
+    bad["key_offset"][4] = 100   # a 4x? block of w*h != 100 before it
+    bad["w"][3], bad["h"][3] = 8, 8
+    with pytest.raises(runtime.FmeError):
+        runtime.pack_jobs(bad)
+    ok = jobs.copy()
+    ok["key_offset"][64] = 5000   # a new wave may start anywhere
+    ok["key_offset"][65] = 5000 + int(ok["w"][64]) * int(ok["h"][64])
+    pk, kb = runtime.pack_jobs(ok)
+    assert kb[1] == 5000 and kb[0] == -1
+    _same_refinement_inputs(runtime.unpack_jobs(pk, kb), ok)

@@ -71,6 +71,29 @@ def test_refine_device_resident():
     _assert_same(res, g["results"], "device-resident")
 
 
+@pytest.mark.parametrize("case", golden_cases())
+def test_golden_packed_device(case):
+    """The 16-byte upload form (fme_pack_jobs -> fme_refine_packed_device, unpacked on the device)
+    gives the golden records; a case outside the packed form is refused at pack time."""
+    import torch
+    from nnfme.runtime import FmeError, pack_jobs
+    g = load_golden(case)
+    try:
+        pk, kb = pack_jobs(g["jobs"])
+    except FmeError as e:
+        assert e.code == -4, e
+        pytest.skip(f"outside the packed form: {e}")
+    ctx = _ctx(g)
+    dpk = torch.from_numpy(pk.view(np.uint8).copy()).cuda()
+    dkb = torch.from_numpy(kb.view(np.uint8).copy()).cuda()
+    n = len(pk)
+    dr = torch.zeros(n * RESULT_DTYPE.itemsize, dtype=torch.uint8, device="cuda")
+    s = torch.cuda.current_stream()
+    ctx.refine_packed_device(dpk.data_ptr(), dkb.data_ptr(), dr.data_ptr(), n, s.cuda_stream)
+    s.synchronize()
+    _assert_same(dr.cpu().numpy().view(RESULT_DTYPE), g["results"], case + " packed")
+
+
 def test_nn_reset_restores_initial_state():
     g = load_golden("qp32_nn")
     ctx = _ctx(g)

@@ -112,3 +112,45 @@ def test_tz_device_and_timing():
     with pytest.raises(FmeError):
         ctx.integer_search(bad, g["ext"])
     assert TZ_EXT_DTYPE.itemsize == 12
+
+
+@pytest.mark.parametrize("case", ["tz_enhanced_fen1", "tz_full_sr8_fen1"])
+def test_tz2_device_and_mode_flags(case):
+    """FastSearch 0 / 3 (fme_tz_ext2) through the device entry point; the same jobs through the
+    12-byte records search with zero neighbour predictors, as the oracle does."""
+    import torch
+    sys_path_oracle()
+    from oracle import Oracle
+    from nnfme.abi import JOB_DTYPE
+    g = load_golden(case)
+    ctx = _ctx(g)
+    dev = torch.device("cuda", 0)
+    dj = torch.from_numpy(g["jobs"].view(np.uint8).copy()).to(dev)
+    de = torch.from_numpy(np.ascontiguousarray(g["ext"]).view(np.uint8).copy()).to(dev)
+    ds = torch.zeros(len(g["jobs"]), dtype=torch.int32, device=dev)
+    ctx.integer_search2_device(dj.data_ptr(), de.data_ptr(), ds.data_ptr(), len(g["jobs"]),
+                               torch.cuda.current_stream(dev).cuda_stream)
+    torch.cuda.synchronize()
+    out = dj.cpu().numpy().view(JOB_DTYPE)
+    assert np.array_equal(out["mv_x"], g["mv_x"]) and np.array_equal(out["mv_y"], g["mv_y"])
+    assert np.array_equal(ds.cpu().numpy().view(np.uint32), g["sad"])
+    base = np.ascontiguousarray(g["ext"]["base"])
+    jobs, sad = ctx.integer_search(g["jobs"], base)
+    orc = Oracle(fast_inter_mode=int(g["config"][0]))
+    for i, p in enumerate(g["pictures"]):
+        orc.set_picture(i, p)
+    for i, lam in enumerate(g["lambdas"]):
+        orc.set_lambda(i, float(lam))
+    orc.set_keys(g["keys"] if g["keys"].size else np.zeros(1, np.int16))
+    ref_jobs, ref_sad = orc.integer_search(g["jobs"], base)
+    assert np.array_equal(jobs["mv_x"], ref_jobs["mv_x"]) and np.array_equal(jobs["mv_y"], ref_jobs["mv_y"])
+    assert np.array_equal(sad, ref_sad)
+
+
+def sys_path_oracle():
+    import os
+    import sys
+    from conftest import ROOT
+    p = os.path.join(ROOT, "oracle")
+    if p not in sys.path:
+        sys.path.insert(0, p)

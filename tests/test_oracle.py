@@ -168,17 +168,23 @@ def test_tz_reference_harness_matches_golden(case):
 
 
 def test_tz_golden_covers_cases():
-    from nnfme.abi import JOB_BIPRED, TZ_PRED2NX2N
-    shapes, bi, pred, far, sr = set(), 0, 0, 0, set()
+    from nnfme.abi import JOB_BIPRED, TZ_ENHANCED, TZ_FULL, TZ_PRED2NX2N
+    shapes, bi, pred, far, sr, modes = set(), 0, 0, 0, set(), {0: 0, TZ_FULL: 0, TZ_ENHANCED: 0}
     for case in tz_golden_cases():
         g = load_golden(case)
         j = g["jobs"]
+        e = g["ext"]["base"] if g["ext"].dtype.names[0] == "base" else g["ext"]
         shapes |= set(zip(j["w"].tolist(), j["h"].tolist()))
         bi += int(((j["flags"] & JOB_BIPRED) != 0).sum())
-        pred += int(((g["ext"]["flags"] & TZ_PRED2NX2N) != 0).sum())
+        pred += int(((e["flags"] & TZ_PRED2NX2N) != 0).sum())
         far += int((np.abs(g["mv_x"] * 4 - j["mvp_x"]) > 4 * 32).sum())   # raster-search territory
         sr.add(int(g["config"][1]))
-    assert len(shapes) >= 18 and bi > 100 and pred > 300 and far > 50 and sr == {32, 64}
+        uni = (j["flags"] & JOB_BIPRED) == 0
+        for m in modes:
+            modes[m] += int((uni & ((e["flags"] & (TZ_FULL | TZ_ENHANCED)) == m)).sum())
+    assert len(shapes) >= 18 and bi > 100 and pred > 300 and far > 50 and {32, 64} <= sr
+    # FastSearch 1 (diamond), 0 (full) and 3 (enhanced diamond) each on > 100 uni-pred jobs
+    assert min(modes.values()) > 100, modes
 
 
 def test_exp_golomb_bits():

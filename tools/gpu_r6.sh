@@ -1,0 +1,42 @@
+#!/bin/bash
+# Round-6 GPU pass: steps named on the command line, each under its own time limit, the first
+# failure ends the call (no retries).  Output under gpurun_out/<name>.log.
+set -o pipefail
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+run() {  # name, timeout, command...
+  local name=$1 t=$2; shift 2
+  echo "== $name"
+  timeout -k 10 "$t" "$@" > "gpurun_out/$name.log" 2>&1
+  local rc=$?
+  tail -3 "gpurun_out/$name.log" | cut -c1-300
+  if [ $rc -ne 0 ]; then echo "== $name FAILED rc=$rc"; tail -40 "gpurun_out/$name.log" | cut -c1-300; exit $rc; fi
+}
+B="python -u bench.py --no-pi --no-tz --no-mc --no-cpu-baseline"
+for step in "$@"; do
+  case $step in
+    tests) run pytest_gpu 600 python -u -m pytest tests -m gpu -x -q -p no:cacheprovider --timeout 300 --timeout-method thread ;;
+    replaytests) run replaytests 400 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_dist.py tests/test_gpu_c4.py tests/test_gpu_main10.py -m gpu -x -q -p no:cacheprovider --timeout 200 --timeout-method thread ;;
+    pipeab) run p_default 200 $B --steps 20 --parity-seconds 10 && \
+            run p_2streams 200 $B --steps 20 --parity-seconds 0 --copy-streams 2 && \
+            run p_unpacked 200 $B --steps 20 --parity-seconds 0 --no-packed && \
+            run p_blit 200 $B --steps 20 --parity-seconds 0 --download-engine blit && \
+            run p_c1 200 $B --steps 20 --parity-seconds 5 --workload c1 ;;
+    m10) run m10tests 300 python -u -m pytest tests/test_gpu_main10.py -m gpu -x -q -p no:cacheprovider --timeout 200 --timeout-method thread && \
+         run m10bench 300 $B --workload c3_qp22_main10 --steps 10 --parity-seconds 10 ;;
+    stall) run s_c3 200 $B --steps 20 --parity-seconds 0 && run s_c1 200 $B --steps 20 --parity-seconds 0 --workload c1 ;;
+    tztests) run tztests 400 python -u -m pytest tests/test_gpu_tz.py tests/test_ring.py tests/test_gpu_parity.py -m gpu -x -q -p no:cacheprovider --timeout 300 --timeout-method thread ;;
+    stamps) run lane_stamps 200 python -u tools/lane_stamps.py 5 ;;
+    pkab) run pkab 300 python -u tools/ab_bench.py . variants/pk16 --rounds 4 ;;
+    pipe2) run q_c3 200 $B --steps 20 --parity-seconds 10 && run q_c3_ma0 200 $B --steps 20 --parity-seconds 0 --max-ahead 0 && \
+           run q_c3_ma2 200 $B --steps 20 --parity-seconds 0 --max-ahead 2 && run q_c3_blit 200 $B --steps 20 --parity-seconds 0 --download-engine blit && \
+           run q_c1 200 $B --workload c1 --steps 20 --parity-seconds 5 && run q_c1_blit 200 $B --workload c1 --steps 20 --parity-seconds 0 --download-engine blit ;;
+    bench) run bench 400 python -u bench.py --no-pi --no-tz --no-mc ;;
+    benchfull) run benchfull 600 python -u bench.py ;;
+    smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    copytl) run copytl 300 rocprofv3 --kernel-trace --memory-copy-trace --output-format csv -d gpurun_out/copytl -o run -- python3 bench.py --no-pi --no-tz --no-mc --no-cpu-baseline --parity-seconds 0 --steps 10 ;;
+    copytl_c1) run copytl_c1 300 rocprofv3 --kernel-trace --memory-copy-trace --output-format csv -d gpurun_out/copytl_c1 -o run -- python3 bench.py --workload c1 --no-cpu-baseline --no-pi --no-tz --no-mc --parity-seconds 0 --steps 10 ;;
+    prof) run prof 400 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run -- python3 bench.py --no-cpu-baseline --no-pi --no-tz --no-mc --parity-seconds 0 --no-pcie ;;
+    *) echo "unknown step $step"; exit 2 ;;
+  esac
+done
