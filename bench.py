@@ -675,6 +675,8 @@ def main():
     ap.add_argument("--slots", type=int, default=3, help="job / result buffer ring depth of the replay")
     ap.add_argument("--max-ahead", type=int, default=4,
                     help="steps the host may queue ahead of the device (0: unbounded)")
+    ap.add_argument("--lazy-events", action="store_true",
+                    help="let torch create each step's events at their first record inside the timed region")
     ap.add_argument("--no-packed", action="store_true",
                     help="upload 32-byte fme_job rows instead of 16-byte fme_job_packed rows")
     ap.add_argument("--no-pcie", action="store_true",
@@ -795,7 +797,8 @@ def main():
                       key_reqs=key_reqs, key_count=len(keys) if keys is not None else 0, nn_rows=nn_rows,
                       download_engine=args.download_engine, download_wgs=args.download_wgs,
                       search_reserve=args.search_reserve, packed=not args.no_packed,
-                      copy_streams=args.copy_streams, slots=args.slots, max_ahead=args.max_ahead)
+                      copy_streams=args.copy_streams, slots=args.slots, max_ahead=args.max_ahead,
+                      precreate_events=not args.lazy_events)
     n = rep.n
     rep.prime()
 
@@ -812,6 +815,7 @@ def main():
     # in series on one copy stream beside the batch stream; the NN-state chain fix-up when sharded.
     # The interpreter's garbage collector is off inside the timed loops (a C++ host has none). ----
     import gc
+    from nnfme import pipeline as fpipe
     fixed_pcie, value_pcie, elapsed_pcie, snap = 0, None, None, None
     if args.no_pcie:   # (profiling runs) the timed steps' inputs staged into HBM untimed instead
         for s in range(args.warmup, steps_total):
@@ -823,6 +827,7 @@ def main():
         gc.collect()
         gc.disable()
         rep.host_ms, rep.host_seg = [], []
+        fpipe.SLOW_CALLS.clear()
         torch.cuda.synchronize(dev)
         t0 = time.perf_counter()
         for s in range(args.warmup, steps_total):
@@ -932,6 +937,7 @@ def main():
                           "sum": float(host_ms.sum()), "per_step": [round(float(v), 3) for v in host_ms],
                           "slowest_step_parts": dict(zip(rep.host_seg_names, rep.host_seg[int(host_ms.argmax())]))}
         if host_ms.size else None,
+        "slow_host_calls": list(fpipe.SLOW_CALLS)[:40],
         "gc": "off inside the timed loops"}
     if world > 1 and pcie:
         pcie["nn_state_fixup_jobs_rank0"] = int(fixed_pcie)
@@ -1044,6 +1050,13 @@ def main():
     del rep
     ctx.close()
     torch.cuda.synchronize(dev)
+    # pinned host blocks go back now, not from a static destructor after the HIP runtime (or a
+    # profiler's exit handlers) has gone: the exit-time SIGSEGV in __cxa_finalize under
+    # rocprofv3 --memory-copy-trace (round 5's gpurun_out/tlc1.log)
+    import gc as _gc
+    _gc.collect()
+    torch.cuda.empty_cache()
+    torch._C._host_emptyCache()
     if world > 1:
         dist.destroy_process_group()
     return 0

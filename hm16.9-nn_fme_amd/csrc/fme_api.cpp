@@ -242,6 +242,13 @@ struct fme_ctx {
   SrvBox* box_dev = nullptr;
   hipStream_t srv_stream = nullptr;
   bool srv_running = false;
+  bool srv_orphan = false;      // a wait on the instance timed out: it may still run on srv_stream
+  // the streams this context's batches were issued on (note_stream): a buffer that a queued launch
+  // may still read is regrown only after those streams have drained, not the whole device
+  static constexpr int kMaxStreams = 8;
+  hipStream_t used_streams[kMaxStreams] = {};
+  int n_used_streams = 0;
+  bool used_overflow = false;   // more streams than tracked: fall back to a device synchronisation
   uint32_t srv_epoch = 0;       // of the instance launched last
   uint32_t srv_done = 0;        // sequence number of the last completed call
   uint32_t srv_nn_gen = 0;      // weight generation the running instance copied to LDS
@@ -334,9 +341,27 @@ static int srv_stop(fme_ctx* c);
 // Grows the bi-pred key buffer to n elements.  Growing frees the old buffer, which batches queued on
 // any stream (the caller's, the integer search's auxiliary streams, another caller stream) may still
 // read: every stream of the device is drained first, and only when the buffer really grows.
+// Remember a stream this context issued work on (reads of its buffers may be queued there).
+static void note_stream(fme_ctx* c, hipStream_t s) {
+  for (int i = 0; i < c->n_used_streams; i++)
+    if (c->used_streams[i] == s) return;
+  if (c->n_used_streams < fme_ctx::kMaxStreams) c->used_streams[c->n_used_streams++] = s;
+  else c->used_overflow = true;
+}
+// Wait for every launch of this context (its tracked streams; the device only if it used more),
+// leaving other contexts' work alone.
+static int drain_ctx(fme_ctx* c) {
+  if (c->used_overflow) {
+    HIP_TRY(hipDeviceSynchronize());
+  } else {
+    for (int i = 0; i < c->n_used_streams; i++) HIP_TRY(hipStreamSynchronize(c->used_streams[i]));
+  }
+  return FME_OK;
+}
 static int grow_keys(fme_ctx* c, size_t n) {
   if (n <= c->d_keys.cap) return FME_OK;
-  HIP_TRY(hipDeviceSynchronize());
+  int rc = drain_ctx(c);   // no queued launch of this context still reads the old key buffer
+  if (rc) return rc;
   HIP_TRY(c->d_keys.reserve(n));
   return FME_OK;
 }
@@ -676,6 +701,7 @@ static WorkBufs work_bufs(fme_ctx* c) {
 // kernel: rebinding pictures for the next frame never waits for the batch in flight, and the
 // batch stream holds no copy-engine transfer (which would queue behind bulk uploads).
 static int sync_tables(fme_ctx* c, hipStream_t s) {
+  note_stream(c, s);   // every batch entry point passes here with its stream
   // a resident server could hold up this work on a hardware queue its stream shares: stop it
   // (a few microseconds; the next single call relaunches it)
   int rc = srv_stop(c);
@@ -1080,7 +1106,8 @@ static int tz_run(fme_ctx* c, fme_job* d_jobs, const fme_tz_ext* d_ext, uint32_t
   if (FME_TZ_STAGE && np > 0 && np <= (1LL << 20)) {
     const size_t words = 8 + 12 * (size_t)np;
     if (c->d_tzp.cap < words || c->d_tzp_perm.cap < (size_t)n) {
-      HIP_TRY(hipDeviceSynchronize());   // no launch of an earlier call still reads the old buffers
+      rc = drain_ctx(c);   // no launch of an earlier call still reads the old buffers
+      if (rc) return rc;
       HIP_TRY(c->d_tzp.reserve(words));
       HIP_TRY(c->d_tzp_perm.reserve(n));
     }
@@ -1366,6 +1393,13 @@ static int srv_open(fme_ctx* c) {
 }
 
 static int srv_launch(fme_ctx* c) {
+  if (c->srv_orphan) {   // never two instances on one mailbox: relaunch only once the old one has left
+    const hipError_t q = hipStreamQuery(c->srv_stream);
+    if (q == hipErrorNotReady)
+      return fail(FME_E_DEVICE, "single-call server: the instance that timed out is still running");
+    (void)hipGetLastError();
+    c->srv_orphan = false;
+  }
   __atomic_store_n(&c->box->req[0][3], 0u, __ATOMIC_RELEASE);
   const uint32_t epoch = ++c->srv_epoch;
   c->srv_nn_gen = c->nn_gen;
@@ -1397,6 +1431,7 @@ static int srv_join(fme_ctx* c) {
       }
       if (srv_waited_too_long(t0)) {
         c->srv_running = false;
+        c->srv_orphan = true;   // srv_launch waits for it to leave srv_stream before a relaunch
         return fail(FME_E_DEVICE, "single-call server: no stop word after %.1f s", kSrvWaitLimitS);
       }
     }
@@ -1440,7 +1475,7 @@ static int srv_call(fme_ctx* c, bool uses_nn) {
       }
       if (srv_waited_too_long(t0)) {   // stop the instance (it exits within its lifetime) and give up
         __atomic_store_n(&c->box->req[0][3], 1u, __ATOMIC_RELEASE);
-        (void)srv_join(c);
+        if (srv_join(c) != FME_OK) c->srv_orphan = true;
         c->srv_running = false;
         return fail(FME_E_DEVICE, "single-call server: call %u unanswered after %.1f s", seq, kSrvWaitLimitS);
       }

@@ -67,9 +67,11 @@
 // v_perm of the two sums' high halves ((16 s) >> 16 == s >> 12) and clipped as a packed pair
 // (v_pk_max_i16 / v_pk_min_i16), and the 1-D horizontal rows of the half stage shifted and clipped
 // as the packed pairs the vertical pass already holds: 3 instructions per output pair instead of 5
-// (two shifts, two med3, one perm).  0: per-output shift and clamp.
+// (two shifts, two med3, one perm).  0: per-output shift and clamp.  A/B on the 1080p batch
+// (tools/ab_bench.py, identical results): search 0.904 -> 0.871 ms, batch 1.087 -> 1.055 ms
+// (profiles/r06_ab.log).
 #ifndef FME_LANE_PK16
-#define FME_LANE_PK16 0
+#define FME_LANE_PK16 1
 #endif
 // occupancy target (waves per SIMD) that bounds the register allocation
 #ifndef FME_LANE_WAVES

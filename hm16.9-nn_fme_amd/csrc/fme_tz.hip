@@ -25,7 +25,17 @@
 #include "fme_device.h"
 #include "fme_simd.h"
 
+// 1: a diagnostic build (make variant NAME=tzcount DEFS=-DFME_TZ_COUNT=1, tools/tz_counts.py) that
+// counts, per unit-shape kernel, the candidate windows read from the staged LDS tile and from global
+// memory (g_tz_count, read by fme_debug_tz_counts).  Never the product build.
+#ifndef FME_TZ_COUNT
+#define FME_TZ_COUNT 0
+#endif
+
 namespace fme {
+#if FME_TZ_COUNT
+__device__ unsigned long long g_tz_count[3][2];   // [kernel 4x8 / 8x4 / 8x8 units][LDS tile, global]
+#endif
 namespace {
 using namespace simd;
 
@@ -220,7 +230,18 @@ __device__ __forceinline__ void load_window(uint32_t (&w)[UH][UW / 4 + 1], uint3
   constexpr int ND = UW / 4 + 1;
   const int xa = bx & ~3;
   s0 = (uint32_t)(bx - xa);
-  if (t.lds && xa >= t.x0 && xa + 4 * ND <= t.x0 + 4 * kTileWD && by >= t.y0 && by + UH <= t.y0 + kTileH) {
+  const bool in_tile = t.lds && xa >= t.x0 && xa + 4 * ND <= t.x0 + 4 * kTileWD && by >= t.y0 && by + UH <= t.y0 + kTileH;
+#if FME_TZ_COUNT
+  if (t.lds) {   // this call's lanes, by where their window comes from (one atomic per wave and kind)
+    const uint64_t in = __ballot(in_tile), all = __ballot(1);
+    if ((threadIdx.x & 63) == (uint32_t)__builtin_ctzll(all)) {
+      constexpr int kid = UW == 4 ? 0 : (UH == 4 ? 1 : 2);
+      atomicAdd(&g_tz_count[kid][0], (unsigned long long)__builtin_popcountll(in));
+      atomicAdd(&g_tz_count[kid][1], (unsigned long long)__builtin_popcountll(all & ~in));
+    }
+  }
+#endif
+  if (in_tile) {
     const uint32_t* p = t.lds + (by - t.y0) * kTileWD + ((xa - t.x0) >> 2);
 #pragma unroll
     for (int r = 0; r < UH; r++) {
@@ -981,6 +1002,17 @@ __global__ __launch_bounds__(64 * FME_TZL_WAVES) void k_tz_level(TzArgs ta, TzCh
 }
 
 }  // namespace
+
+#if FME_TZ_COUNT
+extern "C" int fme_debug_tz_counts(unsigned long long* out6, int reset) {
+  if (out6 && hipMemcpyFromSymbol(out6, HIP_SYMBOL(g_tz_count), sizeof(g_tz_count)) != hipSuccess) return -2;
+  if (reset) {
+    static const unsigned long long zero[3][2] = {};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_tz_count), zero, sizeof(zero)) != hipSuccess) return -2;
+  }
+  return 0;
+}
+#endif
 
 hipError_t launch_tz_levels(const TzArgs& ta, const TzChain& ch, const int32_t* h_lvl_off, hipStream_t s) {
   for (int lv = 0; lv < ch.nlev; lv++) {

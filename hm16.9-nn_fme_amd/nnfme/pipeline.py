@@ -53,13 +53,30 @@ def _hip_lib():
     return _hip
 
 
+# host calls that blocked for more than 1 ms: (what, bytes, ms) (stall hunting, bench.py reports them)
+SLOW_CALLS = []
+
+
 def _memcpy_async(dst, src, nbytes, kind, stream):
     """hipMemcpyAsync between pinned host and device memory on `stream` (a torch stream): the
     copy engines (SDMA) carry it.  (A torch D2H copy_ runs as a blit kernel on the CUs, which
     then waits for the search kernels' workgroups.)"""
+    t0 = time.perf_counter()
     rc = _hip_lib().hipMemcpyAsync(dst.data_ptr(), src.data_ptr(), nbytes, kind, stream.cuda_stream)
+    dt = (time.perf_counter() - t0) * 1e3
+    if dt > 1.0:
+        SLOW_CALLS.append(("hipMemcpyAsync kind %d" % kind, int(nbytes), round(dt, 3)))
     if rc != 0:
         raise RuntimeError(f"hipMemcpyAsync failed ({rc})")
+
+
+def _timed(what, f):
+    """f() and, if it blocked the host for more than 1 ms, a SLOW_CALLS entry."""
+    t0 = time.perf_counter()
+    f()
+    dt = (time.perf_counter() - t0) * 1e3
+    if dt > 1.0:
+        SLOW_CALLS.append((what, 0, round(dt, 3)))
 
 
 class _RawEvent:
@@ -141,7 +158,7 @@ class FrameReplay:
     def __init__(self, ctx, base_jobs, pool, lambda_of, n_steps, frames_per_step=1, world=1, rank=0, device=None,
                  group=None, defer_download=True, key_reqs=None, key_count=0, nn_rows=None,
                  download_engine="sdma", download_wgs=8, search_reserve=0, packed=True, copy_streams=1, slots=3,
-                 max_ahead=4):
+                 max_ahead=4, precreate_events=True):
         """ctx: an FmeContext on `device`; base_jobs: one frame's jobs (ref_id = reference
         distance - 1); pool: uint8 [P, H, W] host frames, frame g's pictures are pool[g % P];
         lambda_of(g): frame g's lambda (pool uint16: main10 samples for a bit-depth-10 context,
@@ -239,6 +256,13 @@ class FrameReplay:
         # recorded by the library right before each batch's search kernel (fme_set_search_event):
         # step k's results are downloaded once step k+1's search runs (see issue())
         self.ev_search = [_RawEvent() for _ in range(n_steps)]
+        if precreate_events:
+            # torch creates an event's hipEvent_t at its first record: do that for every step's
+            # events here, before anything waits on them (a record while no wait on the event is
+            # queued), so the timed steps create none
+            for e in self.ev_in + self.ev_comp + self.ev_out:
+                e.record(self.s_copy)
+            self.s_copy.synchronize()
         self.defer_download = defer_download
         if download_engine not in ("kernel", "blit", "sdma"):
             raise ValueError(f"download_engine {download_engine!r}")
@@ -419,7 +443,7 @@ class FrameReplay:
         cp = self.s_copy
         with self.torch.cuda.stream(cp):
             if k >= R:
-                cp.wait_event(self.ev_comp[k - R])        # step k-R is done with the slot
+                _timed("copy stream wait_event", lambda: cp.wait_event(self.ev_comp[k - R]))   # step k-R is done with the slot
             _memcpy_async(self.d_jobs[b], self.h_jobs, self.h_jobs.numel(), H2D, cp)
             if self.packed:
                 _memcpy_async(self.d_kb[b], self.h_kb, self.h_kb.numel(), H2D, cp)
@@ -433,7 +457,7 @@ class FrameReplay:
             self._publish_run(base + self.rank * F - 1, F, self.rank, cp)
             if self.world > 1:   # ... and sent to the ranks whose frames reference it
                 self._exchange(k, cp)
-            self.ev_in[k].record(cp)
+            _timed("ev_in record", lambda: self.ev_in[k].record(cp))
         self.uploaded = k
 
     def issue(self, k, prefetch=True):

@@ -154,3 +154,39 @@ def sys_path_oracle():
     p = os.path.join(ROOT, "oracle")
     if p not in sys.path:
         sys.path.insert(0, p)
+
+
+def test_tz_staged_uneven_groups():
+    """k_tz_staged runs one workgroup of 8 waves per (unit-shape kernel, reference, CTU) group, wave w
+    taking the group's PUs w, w + 8, ...: groups of 1, 2, 7, 8, 9, 15, 16, 17 and 40 PUs (waves with
+    no PU, with one, with several) all give the oracle's MVs and SADs.  (The static wave-to-PU order
+    keeps each wave's PU index wave-uniform by construction: a readfirstlane of the wave index plus
+    a constant stride; tz_wave's candidate lists and minima assume a wave-uniform job.)"""
+    sys_path_oracle()
+    from oracle import Oracle
+    W, H = 448, 192   # 7 x 3 CTUs
+    rng = np.random.default_rng(77)
+    pics = {i: synth.synth_luma(W, H, i, seed=77) for i in range(5)}
+    jobs, ext = synth.make_tz_jobs(rng, W, H, 60, 4, [0, 1, 2, 3], [0, 1, 2, 3], bipred_frac=0.0)
+    ctu = (jobs["y"].astype(int) // 64) * 7 + jobs["x"].astype(int) // 64
+    kid = np.where(jobs["w"] % 8 != 0, 0, np.where(jobs["h"] % 8 != 0, 1, 2))
+    sizes = [1, 2, 7, 8, 9, 15, 16, 17, 40]
+    keep = np.zeros(len(jobs), bool)
+    for c in range(21):
+        for r in range(4):
+            for k in range(3):
+                idx = np.flatnonzero((ctu == c) & (jobs["ref_id"] == r) & (kid == k))
+                want = sizes[(c * 12 + r * 3 + k) % len(sizes)]
+                keep[idx[:want]] = True
+    jobs, ext = jobs[keep], ext[keep]
+    orc = Oracle(fast_inter_mode=1)
+    ctx = _ctx(fen=1)
+    for eng in (orc, ctx):
+        for k, v in pics.items():
+            eng.set_picture(k, v)
+        for lid, lam in enumerate(synth.LDP_LAMBDA[22]):
+            eng.set_lambda(lid, lam)
+    ref_jobs, ref_sad = orc.integer_search(jobs, ext)
+    got, sad = ctx.integer_search(jobs, ext)
+    bad = (got["mv_x"] != ref_jobs["mv_x"]) | (got["mv_y"] != ref_jobs["mv_y"]) | (sad != ref_sad)
+    assert not bad.any(), f"{int(bad.sum())} of {len(jobs)} jobs differ"

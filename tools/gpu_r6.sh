@@ -31,6 +31,10 @@ for step in "$@"; do
     pipe2) run q_c3 200 $B --steps 20 --parity-seconds 10 && run q_c3_ma0 200 $B --steps 20 --parity-seconds 0 --max-ahead 0 && \
            run q_c3_ma2 200 $B --steps 20 --parity-seconds 0 --max-ahead 2 && run q_c3_blit 200 $B --steps 20 --parity-seconds 0 --download-engine blit && \
            run q_c1 200 $B --workload c1 --steps 20 --parity-seconds 5 && run q_c1_blit 200 $B --workload c1 --steps 20 --parity-seconds 0 --download-engine blit ;;
+    pipe3) run r_c3 200 $B --steps 20 --parity-seconds 5 && run r_c3_ma0 200 $B --steps 20 --parity-seconds 0 --max-ahead 0 && \
+           run r_c3_lazy 200 $B --steps 20 --parity-seconds 0 --lazy-events && \
+           run r_c1 200 $B --workload c1 --steps 20 --parity-seconds 5 && run r_c1_ma0 200 $B --workload c1 --steps 20 --parity-seconds 0 --max-ahead 0 ;;
+    tzc) run tz_counts 200 python -u tools/tz_counts.py ;;
     bench) run bench 400 python -u bench.py --no-pi --no-tz --no-mc ;;
     benchfull) run benchfull 600 python -u bench.py ;;
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
