@@ -1233,8 +1233,16 @@ __device__ __forceinline__ int xcc_id() {
 // 4x4 units (one SATD tile each) for 8x4 / 16x4 / 16x12.  (4x4 units for 4x8-tiled shapes: about
 // 18 % more instructions per PU, measured 0.924 -> 0.9xx ms; 8x4 units for the 8x4-like shapes gave
 // wrong half / quarter results on ~15 % of their golden jobs and are not used)
+#ifndef FME_LANE_4X8_UNITS44   // 4x8 PUs as two 4x4 units (a lane pair) instead of one lane each
+#define FME_LANE_4X8_UNITS44 0
+#endif
+#if FME_LANE_4X8_UNITS44
+#define FME_LANE48_CLASSES(X) X(3, 4, 16, 4, 8)
+#define FME_LANE84_CLASSES(X) X(0, 4, 8, 4, 4) X(1, 8, 4, 4, 4) X(4, 16, 4, 4, 4)
+#else
 #define FME_LANE48_CLASSES(X) X(0, 4, 8, 4, 8) X(3, 4, 16, 4, 8)
 #define FME_LANE84_CLASSES(X) X(1, 8, 4, 4, 4) X(4, 16, 4, 4, 4)
+#endif
 #define FME_LANE88_CLASSES(X)                                                                        \
   X(2, 8, 8, 4, 8) X(5, 8, 16, 4, 8) X(6, 16, 8, 4, 8) X(9, 16, 16, 4, 8) X(10, 8, 32, 4, 8)         \
   X(11, 32, 8, 4, 8) X(12, 16, 32, 4, 8) X(13, 32, 16, 4, 8) X(16, 32, 32, 4, 8) X(17, 16, 64, 4, 8) \

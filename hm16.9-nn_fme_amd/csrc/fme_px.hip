@@ -143,6 +143,52 @@ __device__ __forceinline__ uint32_t px_item(const LT& L, int w, int ws, int ex, 
   }
 }
 
+// Two candidates of a 32-pixel PU (8x4 / 4x8: two 4x4 tiles) in one wave: lanes 0..31 score
+// candidate offset (ox0, oy0), lanes 32..63 (ox1, oy1), each half a lane per pixel (px_item runs one
+// candidate per wave and leaves half the lanes idle for these shapes, 60 % of a frame's PUs).
+// Returns the half's summed 4x4 transforms (or SAD) on every lane of the half.
+template <int BD, bool SAD, class LT>
+__device__ __forceinline__ uint32_t px_item_pair(const LT& L, int w, int ws, int ex, int ey, int ox0, int oy0, int ox1,
+                                                 int oy1, int lane) {
+  constexpr int HR = 14 - BD < 2 ? 2 : 14 - BD, SH2 = 6 + HR, MAXV = (1 << BD) - 1;
+  const int half = lane >> 5, blk = (lane >> 4) & 1;
+  const int bw4 = w >> 2;
+  const int by = blk / bw4;
+  const int c = (blk - by * bw4) * 4 + (lane & 3);
+  const int r = by * 4 + ((lane >> 2) & 3);
+  const int ox = half ? ox1 : ox0, oy = half ? oy1 : oy0;
+  const int ix = ox >> 2, fx = ox & 3, iy = oy >> 2, fy = oy & 3;   // per half
+  const int x = c + ix, wy0 = r + iy + 4;
+  int hs[8];
+  if (fx == 0) {   // filterCopy, isFirst: (s << headRoom) - 8192
+#pragma unroll
+    for (int t = 0; t < 8; t++) hs[t] = ((int)L.win[(wy0 + t - 3 + 1 + ey) * ws + x + 5 + ex] << HR) - 8192;
+  } else {
+    const int16_t* hp = L.hp[fx - 1] + x + 1;
+#pragma unroll
+    for (int t = 0; t < 8; t++) hs[t] = hp[(wy0 + t - 3) * (w + 1)];
+  }
+  int v;
+  if (fy == 0) {
+    v = (hs[3] + 8192 + (1 << (HR - 1))) >> HR;
+  } else {
+    int sum = 0;
+#pragma unroll
+    for (int t = 0; t < 8; t++) sum += px_tap(fy, t) * hs[t];
+    v = (sum + (1 << (SH2 - 1)) + (8192 << 6)) >> SH2;
+  }
+  v = min(MAXV, max(0, v));
+  int d = (int)L.key[r * w + c] - v;
+  if constexpr (SAD) {
+    return xsum<16>(xsum<8>(xsum<4>(xsum<2>(xsum<1>((uint32_t)abs(d), lane), lane), lane), lane), lane);
+  } else {   // xCalcHADs4x4 per 16 lanes, the half's two tiles summed
+    d = bfly<8>(bfly<4>(bfly<2>(bfly<1>(d, lane), lane), lane), lane);
+    uint32_t a = (uint32_t)abs(d);
+    a = xsum<8>(xsum<4>(xsum<2>(xsum<1>(a, lane), lane), lane), lane);
+    return xsum<16>((a + 1) >> 1, lane);
+  }
+}
+
 // One xPatternRefinement stage: every candidate's distortion into L.cost[st] (work items
 // (candidate, block group), a contiguous run per wave, one LDS add per candidate touched).
 template <int BD, bool SAD, bool B8>
@@ -425,6 +471,22 @@ __device__ __forceinline__ void px_wave_sync() {
 template <int BD, bool SAD, bool B8>
 __device__ __forceinline__ void px_wave_costs(const PxSmall& L, int w, int h, int ws, int ex, int ey, int st, int bx0,
                                               int by0, int lane, uint32_t (&cost)[9]) {
+  if constexpr (!B8) {
+    if (w * h == 32) {   // 8x4 / 4x8: candidates two at a time, one per half-wave
+#pragma unroll
+      for (int k = 0; k < 9; k += 2) {
+        const int k1 = k + 1 < 9 ? k + 1 : k;
+        const int ox0 = bx0 + (st == 0 ? 2 * px_ref(kPxHx, k) : px_ref(kPxQx, k));
+        const int oy0 = by0 + (st == 0 ? 2 * px_ref(kPxHy, k) : px_ref(kPxQy, k));
+        const int ox1 = bx0 + (st == 0 ? 2 * px_ref(kPxHx, k1) : px_ref(kPxQx, k1));
+        const int oy1 = by0 + (st == 0 ? 2 * px_ref(kPxHy, k1) : px_ref(kPxQy, k1));
+        const uint32_t sum = px_item_pair<BD, SAD, PxSmall>(L, w, ws, ex, ey, ox0, oy0, ox1, oy1, lane);
+        cost[k] = (uint32_t)__builtin_amdgcn_readlane((int)sum, 0);
+        if (k + 1 < 9) cost[k + 1] = (uint32_t)__builtin_amdgcn_readlane((int)sum, 32);
+      }
+      return;
+    }
+  }
   const int nb4 = (w >> 2) * (h >> 2);
   const int nb = B8 ? (w >> 3) * (h >> 3) : (nb4 + 3) >> 2;
 #pragma unroll

@@ -28,13 +28,24 @@ for step in "$@"; do
     tztests) run tztests 400 python -u -m pytest tests/test_gpu_tz.py tests/test_ring.py tests/test_gpu_parity.py -m gpu -x -q -p no:cacheprovider --timeout 300 --timeout-method thread ;;
     stamps) run lane_stamps 200 python -u tools/lane_stamps.py 5 ;;
     pkab) run pkab 300 python -u tools/ab_bench.py . variants/pk16 --rounds 4 ;;
+    u44ab) run u44ab 300 python -u tools/ab_bench.py . variants/u44 --rounds 4 ;;
     pipe2) run q_c3 200 $B --steps 20 --parity-seconds 10 && run q_c3_ma0 200 $B --steps 20 --parity-seconds 0 --max-ahead 0 && \
            run q_c3_ma2 200 $B --steps 20 --parity-seconds 0 --max-ahead 2 && run q_c3_blit 200 $B --steps 20 --parity-seconds 0 --download-engine blit && \
            run q_c1 200 $B --workload c1 --steps 20 --parity-seconds 5 && run q_c1_blit 200 $B --workload c1 --steps 20 --parity-seconds 0 --download-engine blit ;;
     pipe3) run r_c3 200 $B --steps 20 --parity-seconds 5 && run r_c3_ma0 200 $B --steps 20 --parity-seconds 0 --max-ahead 0 && \
            run r_c3_lazy 200 $B --steps 20 --parity-seconds 0 --lazy-events && \
            run r_c1 200 $B --workload c1 --steps 20 --parity-seconds 5 && run r_c1_ma0 200 $B --workload c1 --steps 20 --parity-seconds 0 --max-ahead 0 ;;
+    envab) for e in "NONE=1" "ROC_SIGNAL_POOL_SIZE=1024" "DEBUG_CLR_BATCH_CPU_SYNC_SIZE=100000" "DEBUG_CLR_MAX_BATCH_SIZE=100000" \
+                    "GPU_MAX_COMMAND_BUFFERS=64" "GPU_NUM_MEM_DEPENDENCY=4096" "ROC_ACTIVE_WAIT_TIMEOUT=1000"; do
+             run "env_${e%%=*}" 200 env "$e" $B --steps 30 --parity-seconds 0 || exit 1
+           done
+           run env_logwait 200 env AMD_LOG_LEVEL=4 AMD_LOG_MASK=4 $B --steps 30 --parity-seconds 0 ;;
     tzc) run tz_counts 200 python -u tools/tz_counts.py ;;
+    icache) A="python tools/ab_bench.py . --rounds 2 --reps 2"
+            run ic_a 90 rocprofv3 --pmc SQC_ICACHE_REQ SQC_ICACHE_HITS --output-format csv -d gpurun_out/ic/a -o run -- $A && \
+            run ic_b 90 rocprofv3 --pmc SQC_ICACHE_MISSES SQC_ICACHE_MISSES_DUPLICATE --output-format csv -d gpurun_out/ic/b -o run -- $A && \
+            run ic_c 90 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_IFETCH SQ_IFETCH_LEVEL SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_ANY --output-format csv -d gpurun_out/ic/c -o run -- $A && \
+            python3 tools/pmc_summary.py gpurun_out/ic > gpurun_out/icache.txt ;;
     bench) run bench 400 python -u bench.py --no-pi --no-tz --no-mc ;;
     benchfull) run benchfull 600 python -u bench.py ;;
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
