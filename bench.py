@@ -688,6 +688,12 @@ def main():
                     help="results download of step k: once step k+1's search runs (deferred) or right after "
                          "step k (immediate); default: the workload's measured choice (DESIGN.md section 5)")
     args = ap.parse_args()
+    crash = None
+    if os.environ.get("FME_CRASH_TRACE"):   # diagnostic: native stack of a fault (tools/probes/crash_trace.c)
+        import ctypes
+        import faulthandler
+        faulthandler.enable()
+        crash = ctypes.CDLL(os.path.join(ROOT, "tools", "probes", "libcrash_trace.so"))
 
     global W, H, QP, METRIC
     wl = WORKLOADS[args.workload]
@@ -1059,6 +1065,8 @@ def main():
     torch._C._host_emptyCache()
     if world > 1:
         dist.destroy_process_group()
+    if crash is not None:
+        crash.crash_trace_install()   # ahead of any handler a profiler installed since start-up
     return 0
 
 

@@ -35,11 +35,12 @@ for step in "$@"; do
     pipe3) run r_c3 200 $B --steps 20 --parity-seconds 5 && run r_c3_ma0 200 $B --steps 20 --parity-seconds 0 --max-ahead 0 && \
            run r_c3_lazy 200 $B --steps 20 --parity-seconds 0 --lazy-events && \
            run r_c1 200 $B --workload c1 --steps 20 --parity-seconds 5 && run r_c1_ma0 200 $B --workload c1 --steps 20 --parity-seconds 0 --max-ahead 0 ;;
-    envab) for e in "NONE=1" "ROC_SIGNAL_POOL_SIZE=1024" "DEBUG_CLR_BATCH_CPU_SYNC_SIZE=100000" "DEBUG_CLR_MAX_BATCH_SIZE=100000" \
-                    "GPU_MAX_COMMAND_BUFFERS=64" "GPU_NUM_MEM_DEPENDENCY=4096" "ROC_ACTIVE_WAIT_TIMEOUT=1000"; do
+    envab) for e in "NONE=1" "ROC_SIGNAL_POOL_SIZE=4096" "ROC_AQL_QUEUE_SIZE=65536" "AMD_DIRECT_DISPATCH=0" \
+                    "HSA_KERNARG_POOL_SIZE=67108864" "GPU_MAX_HW_QUEUES=8" "HSA_ENABLE_SDMA=0" "ROC_CPU_WAIT_FOR_SIGNAL=0" \
+                    "DEBUG_CLR_MAX_BATCH_SIZE=100000" "GPU_NUM_MEM_DEPENDENCY=4096"; do
              run "env_${e%%=*}" 200 env "$e" $B --steps 30 --parity-seconds 0 || exit 1
-           done
-           run env_logwait 200 env AMD_LOG_LEVEL=4 AMD_LOG_MASK=4 $B --steps 30 --parity-seconds 0 ;;
+           done ;;
+    logwait) run env_logwait 200 env AMD_LOG_LEVEL=4 AMD_LOG_MASK=294 $B --steps 12 --parity-seconds 0 ;;
     tzc) run tz_counts 200 python -u tools/tz_counts.py ;;
     icache) A="python tools/ab_bench.py . --rounds 2 --reps 2"
             run ic_a 90 rocprofv3 --pmc SQC_ICACHE_REQ SQC_ICACHE_HITS --output-format csv -d gpurun_out/ic/a -o run -- $A && \
