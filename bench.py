@@ -675,6 +675,8 @@ def main():
     ap.add_argument("--slots", type=int, default=3, help="job / result buffer ring depth of the replay")
     ap.add_argument("--max-ahead", type=int, default=4,
                     help="steps the host may queue ahead of the device (0: unbounded)")
+    ap.add_argument("--no-warm-engines", action="store_true",
+                    help="skip the SDMA engine warm-up before the pipeline (fme_warm_copy_engines; A/B)")
     ap.add_argument("--lazy-events", action="store_true",
                     help="let torch create each step's events at their first record inside the timed region")
     ap.add_argument("--no-packed", action="store_true",
@@ -804,7 +806,7 @@ def main():
                       download_engine=args.download_engine, download_wgs=args.download_wgs,
                       search_reserve=args.search_reserve, packed=not args.no_packed,
                       copy_streams=args.copy_streams, slots=args.slots, max_ahead=args.max_ahead,
-                      precreate_events=not args.lazy_events)
+                      precreate_events=not args.lazy_events, warm_engines=not args.no_warm_engines)
     n = rep.n
     rep.prime()
 
@@ -939,6 +941,7 @@ def main():
                      if args.download_engine == "sdma" else "hipMemcpyAsync (ROCclr blit kernel)"),
         "search_reserve": args.search_reserve,
         "max_ahead": args.max_ahead,
+        "copy_engines_warmed": rep.engines_warmed,
         "host_issue_ms": {"median": float(np.median(host_ms)), "max": float(host_ms.max()),
                           "sum": float(host_ms.sum()), "per_step": [round(float(v), 3) for v in host_ms],
                           "slowest_step_parts": dict(zip(rep.host_seg_names, rep.host_seg[int(host_ms.argmax())]))}

@@ -5,7 +5,10 @@
 // TEncSearch.cpp:55-57) and the per-batch work buffers.  A batch is
 //   classify -> [one 100-byte D2H: class histogram] -> scatter -> search -> scan -> nn_tail
 // on the caller's stream.  Errors are returned as FME_E_* codes; the text is kept per thread.
+#include <dlfcn.h>
 #include <hip/hip_runtime.h>
+#include <hsa/hsa.h>
+#include <hsa/hsa_ext_amd.h>
 
 #include <algorithm>
 #include <chrono>
@@ -1001,6 +1004,118 @@ int fme_download_device(fme_ctx* c, const void* d_src, void* h_dst, size_t bytes
     return fail(FME_E_INVALID, "fme_download_device: h_dst is not pinned host memory");
   }
   HIP_TRY(launch_download(d_src, dst, bytes / 16, workgroups ? workgroups : 8, static_cast<hipStream_t>(stream)));
+  return FME_OK;
+}
+
+// ---- copy-engine warm-up (fme_warm_copy_engines) ---------------------------------------------
+// ROCclr submits each hipMemcpyAsync between host and device memory to one SDMA engine of the
+// device; when a stream's previous engine is still busy it asks the HSA runtime for a free one
+// (hsa_amd_memory_copy_engine_status), and the HSA runtime creates an engine's queue at its first
+// use.  That creation blocked the submitting host thread for 5.6-7.5 ms each time a pipelined copy
+// landed on an engine not used before (gpurun_out/r06a/env_logwait.log: "Query copy engine status
+// ... free_engine_mask 0xfffe" -> copy_engine=0x2 -> a 6.7 ms host gap), and the device drained
+// meanwhile.  Here every engine gets one small copy in each direction up front, through the HSA
+// runtime HIP already initialised (its symbols resolved from the loaded library, no link
+// dependency).
+namespace {
+struct HsaCopyApi {
+  hsa_status_t (*iterate_agents)(hsa_status_t (*)(hsa_agent_t, void*), void*);
+  hsa_status_t (*agent_get_info)(hsa_agent_t, hsa_agent_info_t, void*);
+  hsa_status_t (*signal_create)(hsa_signal_value_t, uint32_t, const hsa_agent_t*, hsa_signal_t*);
+  hsa_status_t (*signal_destroy)(hsa_signal_t);
+  hsa_signal_value_t (*signal_wait)(hsa_signal_t, hsa_signal_condition_t, hsa_signal_value_t, uint64_t,
+                                    hsa_wait_state_t);
+  hsa_status_t (*copy_on_engine)(void*, hsa_agent_t, const void*, hsa_agent_t, size_t, uint32_t,
+                                 const hsa_signal_t*, hsa_signal_t, hsa_amd_sdma_engine_id_t, bool);
+};
+bool hsa_copy_api(HsaCopyApi& a) {
+  void* h = dlopen("libhsa-runtime64.so.1", RTLD_LAZY | RTLD_NOLOAD);
+  if (!h) h = dlopen("libhsa-runtime64.so.1", RTLD_LAZY);
+  if (!h) return false;
+  a.iterate_agents = reinterpret_cast<decltype(a.iterate_agents)>(dlsym(h, "hsa_iterate_agents"));
+  a.agent_get_info = reinterpret_cast<decltype(a.agent_get_info)>(dlsym(h, "hsa_agent_get_info"));
+  a.signal_create = reinterpret_cast<decltype(a.signal_create)>(dlsym(h, "hsa_signal_create"));
+  a.signal_destroy = reinterpret_cast<decltype(a.signal_destroy)>(dlsym(h, "hsa_signal_destroy"));
+  a.signal_wait = reinterpret_cast<decltype(a.signal_wait)>(dlsym(h, "hsa_signal_wait_scacquire"));
+  a.copy_on_engine = reinterpret_cast<decltype(a.copy_on_engine)>(dlsym(h, "hsa_amd_memory_async_copy_on_engine"));
+  return a.iterate_agents && a.agent_get_info && a.signal_create && a.signal_destroy && a.signal_wait &&
+         a.copy_on_engine;
+}
+struct AgentPick {
+  const HsaCopyApi* api;
+  uint32_t bdf, domain;
+  bool have_gpu = false, have_cpu = false;
+  hsa_agent_t gpu{}, cpu{};
+};
+hsa_status_t pick_agent(hsa_agent_t ag, void* data) {
+  AgentPick* p = static_cast<AgentPick*>(data);
+  hsa_device_type_t t;
+  if (p->api->agent_get_info(ag, HSA_AGENT_INFO_DEVICE, &t) != HSA_STATUS_SUCCESS) return HSA_STATUS_SUCCESS;
+  if (t == HSA_DEVICE_TYPE_CPU && !p->have_cpu) {
+    p->cpu = ag;
+    p->have_cpu = true;
+  } else if (t == HSA_DEVICE_TYPE_GPU && !p->have_gpu) {
+    uint32_t bdf = 0, dom = 0;
+    p->api->agent_get_info(ag, static_cast<hsa_agent_info_t>(HSA_AMD_AGENT_INFO_BDFID), &bdf);
+    p->api->agent_get_info(ag, static_cast<hsa_agent_info_t>(HSA_AMD_AGENT_INFO_DOMAIN), &dom);
+    if (bdf == p->bdf && dom == p->domain) {
+      p->gpu = ag;
+      p->have_gpu = true;
+    }
+  }
+  return HSA_STATUS_SUCCESS;
+}
+}  // namespace
+
+int fme_warm_copy_engines(fme_ctx* c, int* engines) {
+  if (!c) return fail(FME_E_INVALID, "fme_warm_copy_engines: null ctx");
+  if (engines) *engines = 0;
+  HIP_TRY(hipSetDevice(c->device));
+  HsaCopyApi api{};
+  if (!hsa_copy_api(api)) return fail(FME_E_DEVICE, "fme_warm_copy_engines: HSA runtime symbols not found");
+  int bus = 0, dev = 0, dom = 0;
+  HIP_TRY(hipDeviceGetAttribute(&bus, hipDeviceAttributePciBusId, c->device));
+  HIP_TRY(hipDeviceGetAttribute(&dev, hipDeviceAttributePciDeviceId, c->device));
+  HIP_TRY(hipDeviceGetAttribute(&dom, hipDeviceAttributePciDomainID, c->device));
+  AgentPick pk{&api, (uint32_t)((bus << 8) | (dev << 3)), (uint32_t)dom};
+  api.iterate_agents(pick_agent, &pk);
+  if (!pk.have_gpu || !pk.have_cpu) return fail(FME_E_DEVICE, "fme_warm_copy_engines: HSA agents not found");
+  uint32_t n_sdma = 0, n_xgmi = 0;
+  api.agent_get_info(pk.gpu, static_cast<hsa_agent_info_t>(HSA_AMD_AGENT_INFO_NUM_SDMA_ENG), &n_sdma);
+  api.agent_get_info(pk.gpu, static_cast<hsa_agent_info_t>(HSA_AMD_AGENT_INFO_NUM_SDMA_XGMI_ENG), &n_xgmi);
+  const int n_eng = std::min(16, (int)(n_sdma + n_xgmi));
+  constexpr size_t kBytes = 4096;
+  void* d = nullptr;
+  void* h = nullptr;
+  HIP_TRY(hipMalloc(&d, kBytes));
+  if (hipHostMalloc(&h, kBytes, hipHostMallocDefault) != hipSuccess) {
+    (void)hipFree(d);
+    return fail(FME_E_NOMEM, "fme_warm_copy_engines: host buffer");
+  }
+  std::memset(h, 0, kBytes);
+  int warmed = 0;
+  for (int e = 0; e < n_eng; e++) {
+    bool ok = true;
+    for (int dir = 0; dir < 2 && ok; dir++) {   // host -> device, device -> host
+      hsa_signal_t sig;
+      if (api.signal_create(1, 0, nullptr, &sig) != HSA_STATUS_SUCCESS) {
+        ok = false;
+        break;
+      }
+      const auto eid = static_cast<hsa_amd_sdma_engine_id_t>(1u << e);
+      const hsa_status_t st = dir == 0 ? api.copy_on_engine(d, pk.gpu, h, pk.cpu, kBytes, 0, nullptr, sig, eid, true)
+                                       : api.copy_on_engine(h, pk.cpu, d, pk.gpu, kBytes, 0, nullptr, sig, eid, true);
+      if (st == HSA_STATUS_SUCCESS)
+        api.signal_wait(sig, HSA_SIGNAL_CONDITION_LT, 1, UINT64_MAX, HSA_WAIT_STATE_BLOCKED);
+      else
+        ok = false;
+      api.signal_destroy(sig);
+    }
+    warmed += ok ? 1 : 0;
+  }
+  (void)hipHostFree(h);
+  (void)hipFree(d);
+  if (engines) *engines = warmed;
   return FME_OK;
 }
 

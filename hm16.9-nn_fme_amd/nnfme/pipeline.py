@@ -158,7 +158,7 @@ class FrameReplay:
     def __init__(self, ctx, base_jobs, pool, lambda_of, n_steps, frames_per_step=1, world=1, rank=0, device=None,
                  group=None, defer_download=True, key_reqs=None, key_count=0, nn_rows=None,
                  download_engine="sdma", download_wgs=8, search_reserve=0, packed=True, copy_streams=1, slots=3,
-                 max_ahead=4, precreate_events=True):
+                 max_ahead=4, precreate_events=True, warm_engines=True):
         """ctx: an FmeContext on `device`; base_jobs: one frame's jobs (ref_id = reference
         distance - 1); pool: uint8 [P, H, W] host frames, frame g's pictures are pool[g % P];
         lambda_of(g): frame g's lambda (pool uint16: main10 samples for a bit-depth-10 context,
@@ -277,6 +277,8 @@ class FrameReplay:
         self.host_ms = []                         # host wall time of each issue() call (stall hunting)
         self.host_seg = []                        # its parts: upload, waits, bind, refine, prefetch, download
         self.host_seg_names = ("upload", "waits", "bind", "refine", "prefetch", "download")
+        self.warm_engines = bool(warm_engines)
+        self.engines_warmed = None
 
     def h2d_bytes_per_step(self):
         """Bytes this rank uploads per step: jobs (+ key bases), key requests, NN rows, its frames'
@@ -391,6 +393,8 @@ class FrameReplay:
         host result row is written once by the copy engine, so no timed step is the first DMA
         into fresh pinned pages (on a fresh buffer some hipMemcpyAsync calls blocked the host
         for up to 7 ms each: 2.15 ms per 1080p step against 1.32 once the rows had been used)."""
+        if self.warm_engines:   # every SDMA engine's queue created now, not mid-pipeline (fme_warm_copy_engines)
+            self.engines_warmed = self.ctx.warm_copy_engines()
         with self.torch.cuda.stream(self.s_copy):
             for g in range(-REFS, -1):
                 self._publish(g, 0)

@@ -16,7 +16,7 @@ from .weights import load_weights
 PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB_PATH = os.environ.get("FME_LIB_PATH") or os.path.join(PKG_ROOT, "libfme_amd.so")
 
-ABI_VERSION = 16
+ABI_VERSION = 17
 TIMING_NAMES = ("classify", "scatter", "search", "nn_tail", "batch", "search_main", "search_aux")
 
 # Every entry point include/fme.h declares (the ABI test checks the .so exports them).
@@ -36,7 +36,7 @@ ABI_SYMBOLS = (
     "fme_set_nn_inputs", "fme_integer_search_ring", "fme_integer_search_ring_device",
     "fme_download_device", "fme_pred_inter_phases", "fme_set_search_reserve",
     "fme_pack_jobs", "fme_unpack_jobs", "fme_refine_packed_device", "fme_refine_mv_packed_device",
-    "fme_integer_search2", "fme_integer_search2_device",
+    "fme_integer_search2", "fme_integer_search2_device", "fme_warm_copy_engines",
 )
 
 
@@ -118,6 +118,7 @@ def load_library(path=None):
         "fme_download_device": (I, [P, P, P, C.c_size_t, I, P]),
         "fme_pred_inter_phases": (I, [P, P, I]),
         "fme_set_search_reserve": (I, [P, I]),
+        "fme_warm_copy_engines": (I, [P, P]),
         "fme_pack_jobs": (I, [P, I, P, P]),
         "fme_unpack_jobs": (I, [P, P, I, P]),
         "fme_refine_packed_device": (I, [P, P, P, P, I, P]),
@@ -461,6 +462,13 @@ class FmeContext:
         if event is not None and hasattr(event, "cuda_event"):
             event = event.cuda_event
         _check(self.lib, self.lib.fme_set_search_event(self.h, C.c_void_p(event) if event else None))
+
+    def warm_copy_engines(self):
+        """One small copy per SDMA engine and direction before a copy pipeline (fme_warm_copy_engines);
+        returns the number of engines warmed."""
+        n = C.c_int(0)
+        _check(self.lib, self.lib.fme_warm_copy_engines(self.h, C.byref(n)))
+        return n.value
 
     def set_search_reserve(self, workgroups):
         """Resident search workgroups left free for a few-workgroup kernel beside it (fme_set_search_reserve)."""

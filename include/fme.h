@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define FME_ABI_VERSION 16
+#define FME_ABI_VERSION 17
 
 /* ---- error codes ---------------------------------------------------------------- */
 #define FME_OK            0
@@ -337,6 +337,16 @@ int fme_set_search_reserve(fme_ctx* ctx, int workgroups);
  * d_src and h_dst must be 16-byte aligned and `bytes` a multiple of 16.                       */
 int fme_download_device(fme_ctx* ctx, const void* d_src, void* h_dst, size_t bytes, int workgroups,
                         void* stream);
+
+/* One small host <-> device copy on every SDMA engine of the context's device, both directions,
+ * through the HSA runtime the HIP runtime runs on (hsa_amd_memory_async_copy_on_engine), waited
+ * for; *engines (may be null) = engines that took both copies.  The HSA runtime creates an
+ * engine's queue at its first copy, and the HIP runtime moves a stream's copies to another free
+ * engine whenever its previous one is busy: the first copy on each new engine then blocked the
+ * submitting thread for 5.6-7.5 ms in the middle of a copy pipeline (profiles/r06_ab.log).  Call
+ * once before a copy pipeline's timed part.  Synchronous; no replacement of a reference
+ * interface (pipeline set-up).                                                                  */
+int fme_warm_copy_engines(fme_ctx* ctx, int* engines);
 
 
 /* ---- the batch path --------------------------------------------------------------------- *

@@ -19,11 +19,11 @@ def header_functions():
 def test_library_exports_header():
     lib = runtime.load_library()
     names = header_functions()
-    assert len(names) == 59
+    assert len(names) == 60
     assert set(names) == set(runtime.ABI_SYMBOLS)
     for n in names:
         assert hasattr(lib, n), n
-    assert lib.fme_abi_version() == runtime.ABI_VERSION == 16
+    assert lib.fme_abi_version() == runtime.ABI_VERSION == 17
 
 
 def test_struct_layouts():

@@ -40,6 +40,17 @@ for step in "$@"; do
                     "DEBUG_CLR_MAX_BATCH_SIZE=100000" "GPU_NUM_MEM_DEPENDENCY=4096"; do
              run "env_${e%%=*}" 200 env "$e" $B --steps 30 --parity-seconds 0 || exit 1
            done ;;
+    pipe4) run t_2str 200 $B --steps 30 --parity-seconds 0 --copy-streams 2 && \
+           run t_blit 200 $B --steps 30 --parity-seconds 0 --download-engine blit && \
+           run t_kern 200 $B --steps 30 --parity-seconds 0 --download-engine kernel && \
+           run t_dd0_c1 200 env AMD_DIRECT_DISPATCH=0 $B --workload c1 --steps 30 --parity-seconds 5 && \
+           run t_c1 200 $B --workload c1 --steps 30 --parity-seconds 0 ;;
+    warm) run w_c3 200 $B --steps 30 --parity-seconds 5 && \
+          run w_c3_nowarm 200 $B --steps 30 --parity-seconds 0 --no-warm-engines && \
+          run w_c3_ma0 200 $B --steps 30 --parity-seconds 0 --max-ahead 0 && \
+          run w_c3_ma8 200 $B --steps 30 --parity-seconds 0 --max-ahead 8 && \
+          run w_c1 200 $B --workload c1 --steps 30 --parity-seconds 5 && \
+          run w_c3_100 200 $B --steps 100 --parity-seconds 0 ;;
     logwait) run env_logwait 200 env AMD_LOG_LEVEL=4 AMD_LOG_MASK=294 $B --steps 12 --parity-seconds 0 ;;
     tzc) run tz_counts 200 python -u tools/tz_counts.py ;;
     icache) A="python tools/ab_bench.py . --rounds 2 --reps 2"
@@ -50,8 +61,8 @@ for step in "$@"; do
     bench) run bench 400 python -u bench.py --no-pi --no-tz --no-mc ;;
     benchfull) run benchfull 600 python -u bench.py ;;
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
-    copytl) run copytl 300 rocprofv3 --kernel-trace --memory-copy-trace --output-format csv -d gpurun_out/copytl -o run -- python3 bench.py --no-pi --no-tz --no-mc --no-cpu-baseline --parity-seconds 0 --steps 10 ;;
-    copytl_c1) run copytl_c1 300 rocprofv3 --kernel-trace --memory-copy-trace --output-format csv -d gpurun_out/copytl_c1 -o run -- python3 bench.py --workload c1 --no-cpu-baseline --no-pi --no-tz --no-mc --parity-seconds 0 --steps 10 ;;
+    copytl) run copytl 300 env FME_CRASH_TRACE=1 rocprofv3 --kernel-trace --memory-copy-trace --output-format csv -d gpurun_out/copytl -o run -- python3 bench.py --no-pi --no-tz --no-mc --no-cpu-baseline --parity-seconds 0 --steps 10 ;;
+    copytl_c1) run copytl_c1 300 env FME_CRASH_TRACE=1 rocprofv3 --kernel-trace --memory-copy-trace --output-format csv -d gpurun_out/copytl_c1 -o run -- python3 bench.py --workload c1 --no-cpu-baseline --no-pi --no-tz --no-mc --parity-seconds 0 --steps 10 ;;
     prof) run prof 400 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run -- python3 bench.py --no-cpu-baseline --no-pi --no-tz --no-mc --parity-seconds 0 --no-pcie ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
