@@ -614,6 +614,31 @@ def read_pmc_traffic(workload):
         return None, None
 
 
+def write_timeline(path, rep, k0, k1, elapsed_s):
+    """The PCIe pass's timeline (FrameReplay timeline=True): per step, ms from the timed region's
+    start to the start / end of its H2D uploads (copy stream), its batch (compute stream) and its
+    results download (copy stream), then the per-step spans and the overlap of copies with batches."""
+    rows = rep.timeline_rows(k0, k1)
+    with open(path, "w") as f:
+        f.write("# FrameReplay PCIe pass, HIP timing events on the copy and compute streams (ms from the first "
+                "timed issue); wall %.3f ms for %d steps\n" % (elapsed_s * 1e3, k1 - k0))
+        f.write("# step    up0      up1  | b0       b1   |  d0       d1   | up_ms  batch_ms  down_ms  batch_gap_ms\n")
+        prev_b1 = None
+        for r in rows:
+            gap = (r["b0"] - prev_b1) if prev_b1 is not None else 0.0
+            f.write("%5d %8.3f %8.3f | %8.3f %8.3f | %8.3f %8.3f | %6.3f %8.3f %8.3f %8.3f\n" % (
+                r["step"], r["up0"], r["up1"], r["b0"], r["b1"], r["d0"], r["d1"], r["up1"] - r["up0"],
+                r["b1"] - r["b0"], r["d1"] - r["d0"], gap))
+            prev_b1 = r["b1"]
+        span = rows[-1]["d1"] - rows[0]["up0"]
+        busy = sum(r["b1"] - r["b0"] for r in rows)
+        f.write("# first upload start -> last download end %.3f ms; batches busy %.3f ms (%.1f %%); "
+                "mean batch %.3f ms, mean upload %.3f ms, mean download %.3f ms\n" % (
+                    span, busy, 100 * busy / span, busy / len(rows),
+                    sum(r["up1"] - r["up0"] for r in rows) / len(rows),
+                    sum(r["d1"] - r["d0"] for r in rows) / len(rows)))
+
+
 def frame_lambda(wl, f):
     """Lambda of frame f: lowdelay_P by POC % 4 (cfg Frame1-4), random access by GOP-8 entry."""
     if wl["gop"] == "ra":
@@ -675,6 +700,8 @@ def main():
     ap.add_argument("--slots", type=int, default=3, help="job / result buffer ring depth of the replay")
     ap.add_argument("--max-ahead", type=int, default=4,
                     help="steps the host may queue ahead of the device (0: unbounded)")
+    ap.add_argument("--timeline", default=None,
+                    help="write the PCIe pass's per-step copy / batch timeline (HIP timing events) to this file")
     ap.add_argument("--no-warm-engines", action="store_true",
                     help="skip the SDMA engine warm-up before the pipeline (fme_warm_copy_engines; A/B)")
     ap.add_argument("--lazy-events", action="store_true",
@@ -806,7 +833,8 @@ def main():
                       download_engine=args.download_engine, download_wgs=args.download_wgs,
                       search_reserve=args.search_reserve, packed=not args.no_packed,
                       copy_streams=args.copy_streams, slots=args.slots, max_ahead=args.max_ahead,
-                      precreate_events=not args.lazy_events, warm_engines=not args.no_warm_engines)
+                      precreate_events=not args.lazy_events, warm_engines=not args.no_warm_engines,
+                      timeline=args.timeline is not None)
     n = rep.n
     rep.prime()
 
@@ -837,6 +865,7 @@ def main():
         rep.host_ms, rep.host_seg = [], []
         fpipe.SLOW_CALLS.clear()
         torch.cuda.synchronize(dev)
+        rep.timeline_start()
         t0 = time.perf_counter()
         for s in range(args.warmup, steps_total):
             rep.issue(s)
@@ -847,6 +876,8 @@ def main():
         elapsed_pcie = max_over_ranks(time.perf_counter() - t0, dev, world, args.dist_backend)
         gc.enable()
         rep.check_status(args.warmup)   # no timed step may have been rejected on the device
+        if args.timeline:
+            write_timeline(args.timeline, rep, args.warmup, steps_total, elapsed_pcie)
         snap = rep.results(args.warmup).copy() if args.parity_seconds > 0 else None
         value_pcie = world * n * args.steps / elapsed_pcie
     host_ms = np.asarray(rep.host_ms, dtype=np.float64)
@@ -1013,8 +1044,8 @@ def main():
                 "traffic": traffic,
                 "kernel": "main search phase: fme::k_search_lane (EMI + FracDIF, every PU shape, one "
                           "persistent launch per batch)" if BD == 8 else
-                          "main search phase at bit depth 10: fme::k_search_px<10> (EMI + FracDIF, pixel per lane, "
-                          "one job per workgroup iteration, every PU shape)",
+                          "main search phase at bit depth 10: fme::k_search_lane10 (EMI + FracDIF on int16 samples, "
+                          "one lane per 4x8 / 4x4 unit, every PU shape, one persistent launch per batch)",
                 "kernel_jobs": int(len(small_jobs)),
                 "algorithmic_ops_per_launch": ops_small,
                 "algorithmic_bytes_per_launch": bytes_small,

@@ -274,6 +274,8 @@ struct fme_ctx {
   hipEvent_t ev_done = nullptr; // end of the last batch (fme_refine_status)
   hipEvent_t ev_search = nullptr; // caller's event, recorded before each search launch (fme_set_search_event)
   int search_reserve = 0;         // resident search workgroups left free (fme_set_search_reserve)
+  bool main10_px = false;         // bit depth 10: the pixel kernel instead of the lane kernel
+                                  // (environment FME_MAIN10_SEARCH=px, an A/B switch)
   bool batch_issued = false;
   float last_ms[FME_NUM_TIMINGS] = {};
   double acc_ms[FME_NUM_TIMINGS] = {};
@@ -320,6 +322,10 @@ int fme_create(int device, const fme_config* cfg, fme_ctx** out_ctx) {
   HIP_TRY(c->counts.reserve(kCountWords));
   HIP_TRY(c->d_sched.reserve(1));
   c->sched_p = sched_params();
+  {
+    const char* m10 = std::getenv("FME_MAIN10_SEARCH");
+    c->main10_px = m10 && std::strcmp(m10, "px") == 0;
+  }
   HIP_TRY(hipEventCreateWithFlags(&c->ev_done, hipEventDisableTiming));
   HIP_TRY(c->nn_state.reserve(24));
   HIP_TRY(hipMemset(c->nn_state.p, 0, 24 * sizeof(uint32_t)));
@@ -835,7 +841,10 @@ static int refine_batch(fme_ctx* c, const fme_job* d_jobs, fme_result* d_res, fm
     // the small- and large-PU pixel kernels one after the other: side by side on two streams they
     // took 11.5 ms per 1080p frame against 10.5 in series (profiles/r06_ab.log: their LDS and
     // wave slots compete)
-    HIP_TRY(launch_search_px(a, w, c->cfg.bit_depth, s, nullptr));
+    if (c->main10_px)
+      HIP_TRY(launch_search_px(a, w, c->cfg.bit_depth, s, nullptr));
+    else
+      HIP_TRY(launch_search_lane10(a, w, s));
   } else {
     HIP_TRY(launch_search_lane(a, w, c->search_reserve, s));
   }

@@ -243,6 +243,10 @@ hipError_t launch_search_lane(const BatchArgs& a, const WorkBufs& w, int reserve
 // pictures hold uint16 samples (PicDesc::luma reinterpreted, stride in samples).
 // s_big (may be null: s): the stream of the large-PU kernel, run beside the small-PU one
 hipError_t launch_search_px(const BatchArgs& a, const WorkBufs& w, int bit_depth, hipStream_t s, hipStream_t s_big);
+// Bit depth 10: the lane-per-unit search on int16 samples (fme_lane10.hip), the lane kernel's
+// classes, schedule and records (the default main10 search; FME_MAIN10_SEARCH=px selects the pixel
+// kernel above)
+hipError_t launch_search_lane10(const BatchArgs& a, const WorkBufs& w, hipStream_t s);
 struct NnIn11 {   // NN_pred() inputs of a single call: array_e slots[8], C, PUHeight, PUWidth
   uint32_t v[11];
 };

@@ -158,7 +158,7 @@ class FrameReplay:
     def __init__(self, ctx, base_jobs, pool, lambda_of, n_steps, frames_per_step=1, world=1, rank=0, device=None,
                  group=None, defer_download=True, key_reqs=None, key_count=0, nn_rows=None,
                  download_engine="sdma", download_wgs=8, search_reserve=0, packed=True, copy_streams=1, slots=3,
-                 max_ahead=4, precreate_events=True, warm_engines=True):
+                 max_ahead=4, precreate_events=True, warm_engines=True, timeline=False):
         """ctx: an FmeContext on `device`; base_jobs: one frame's jobs (ref_id = reference
         distance - 1); pool: uint8 [P, H, W] host frames, frame g's pictures are pool[g % P];
         lambda_of(g): frame g's lambda (pool uint16: main10 samples for a bit-depth-10 context,
@@ -279,6 +279,14 @@ class FrameReplay:
         self.host_seg_names = ("upload", "waits", "bind", "refine", "prefetch", "download")
         self.warm_engines = bool(warm_engines)
         self.engines_warmed = None
+        # timeline=True (diagnostic): timing events around each step's uploads, batch and download,
+        # read back by timeline_rows() (the kernel + copy timeline of the pipeline from the HIP
+        # runtime's own clocks)
+        self.tl = None
+        if timeline:
+            self.tl = {kk: [torch.cuda.Event(enable_timing=True) for _ in range(n_steps)]
+                       for kk in ("up0", "up1", "b0", "b1", "d0", "d1")}
+            self.tl_base = torch.cuda.Event(enable_timing=True)
 
     def h2d_bytes_per_step(self):
         """Bytes this rank uploads per step: jobs (+ key bases), key requests, NN rows, its frames'
@@ -448,6 +456,8 @@ class FrameReplay:
         with self.torch.cuda.stream(cp):
             if k >= R:
                 _timed("copy stream wait_event", lambda: cp.wait_event(self.ev_comp[k - R]))   # step k-R is done with the slot
+            if self.tl:
+                self.tl["up0"][k].record(cp)
             _memcpy_async(self.d_jobs[b], self.h_jobs, self.h_jobs.numel(), H2D, cp)
             if self.packed:
                 _memcpy_async(self.d_kb[b], self.h_kb, self.h_kb.numel(), H2D, cp)
@@ -461,6 +471,8 @@ class FrameReplay:
             self._publish_run(base + self.rank * F - 1, F, self.rank, cp)
             if self.world > 1:   # ... and sent to the ranks whose frames reference it
                 self._exchange(k, cp)
+            if self.tl:
+                self.tl["up1"][k].record(cp)
             _timed("ev_in record", lambda: self.ev_in[k].record(cp))
         self.uploaded = k
 
@@ -491,9 +503,13 @@ class FrameReplay:
         if self.defer_download:
             ctx.set_search_event(self.ev_search[k])        # recorded right before this batch's search
         t.append(pc())
+        if self.tl:
+            self.tl["b0"][k].record(comp)
         self._refine(k, self.d_out[b].data_ptr(), self.n, comp)
         if self.world > 1:
             ctx.nn_copy_state_device(self.states[k].data_ptr(), comp.cuda_stream)
+        if self.tl:
+            self.tl["b1"][k].record(comp)
         self.ev_comp[k].record(comp)
         t.append(pc())
         if prefetch and k + 1 < self.steps:
@@ -525,7 +541,11 @@ class FrameReplay:
             after.wait(dn)
         else:
             dn.wait_event(after)
+        if self.tl:
+            self.tl["d0"][k].record(dn)
         self._copy_down(k, dn)
+        if self.tl:
+            self.tl["d1"][k].record(dn)
         self.ev_out[k].record(dn)
 
     def drain(self):
@@ -546,6 +566,22 @@ class FrameReplay:
         for k in range(first_step, self.steps):
             if np.any(self.results(k)["status"] & RES_REJECTED):
                 raise RuntimeError(f"frame replay: step {k}'s batch was rejected on the device")
+
+    def timeline_start(self):
+        """Mark the timeline's zero on the copy and compute streams' device (timeline=True)."""
+        if self.tl:
+            self.tl_base.record(self.s_comp)
+
+    def timeline_rows(self, k0, k1):
+        """Per step k0 .. k1-1: ms from timeline_start() to the start / end of the step's uploads,
+        batch and download (after drain())."""
+        rows = []
+        for k in range(k0, k1):
+            r = {"step": k}
+            for kk in ("up0", "up1", "b0", "b1", "d0", "d1"):
+                r[kk] = round(self.tl_base.elapsed_time(self.tl[kk][k]), 4)
+            rows.append(r)
+        return rows
 
     def results(self, k):
         return self.h_out[k].numpy().view(MV_RESULT_DTYPE)

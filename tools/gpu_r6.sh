@@ -51,6 +51,10 @@ for step in "$@"; do
           run w_c3_ma8 200 $B --steps 30 --parity-seconds 0 --max-ahead 8 && \
           run w_c1 200 $B --workload c1 --steps 30 --parity-seconds 5 && \
           run w_c3_100 200 $B --steps 100 --parity-seconds 0 ;;
+    m10b) run m10tests 400 python -u -m pytest tests/test_gpu_main10.py -m gpu -x -v -p no:cacheprovider --timeout 200 --timeout-method thread && \
+          run m10bench 300 $B --workload c3_qp22_main10 --steps 10 --parity-seconds 10 && \
+          run m10bench_px 300 env FME_MAIN10_SEARCH=px $B --workload c3_qp22_main10 --steps 10 --parity-seconds 0 ;;
+    copytl_rocpd) run copytl_rocpd 300 rocprofv3 --kernel-trace --memory-copy-trace --output-format rocpd -d gpurun_out/copytl_rocpd -o run -- python3 bench.py --no-pi --no-tz --no-mc --no-cpu-baseline --parity-seconds 0 --steps 10 ;;
     logwait) run env_logwait 200 env AMD_LOG_LEVEL=4 AMD_LOG_MASK=294 $B --steps 12 --parity-seconds 0 ;;
     tzc) run tz_counts 200 python -u tools/tz_counts.py ;;
     icache) A="python tools/ab_bench.py . --rounds 2 --reps 2"
@@ -62,6 +66,7 @@ for step in "$@"; do
     benchfull) run benchfull 600 python -u bench.py ;;
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     copytl) run copytl 300 env FME_CRASH_TRACE=1 rocprofv3 --kernel-trace --memory-copy-trace --output-format csv -d gpurun_out/copytl -o run -- python3 bench.py --no-pi --no-tz --no-mc --no-cpu-baseline --parity-seconds 0 --steps 10 ;;
+    copytl_dbg) run copytl_dbg 300 env FME_CRASH_TRACE=1 LD_DEBUG=files rocprofv3 --kernel-trace --memory-copy-trace --output-format csv -d gpurun_out/copytl -o run -- python3 bench.py --no-pi --no-tz --no-mc --no-cpu-baseline --parity-seconds 0 --steps 10 ;;
     copytl_c1) run copytl_c1 300 env FME_CRASH_TRACE=1 rocprofv3 --kernel-trace --memory-copy-trace --output-format csv -d gpurun_out/copytl_c1 -o run -- python3 bench.py --workload c1 --no-cpu-baseline --no-pi --no-tz --no-mc --parity-seconds 0 --steps 10 ;;
     prof) run prof 400 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run -- python3 bench.py --no-cpu-baseline --no-pi --no-tz --no-mc --parity-seconds 0 --no-pcie ;;
     *) echo "unknown step $step"; exit 2 ;;
