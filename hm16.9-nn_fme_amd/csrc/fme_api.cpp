@@ -472,13 +472,13 @@ int fme_bind_picture_device(fme_ctx* c, int id, const uint8_t* d_luma, int strid
 
 int fme_set_picture_chroma(fme_ctx* c, int id, const uint8_t* cb, const uint8_t* cr, int stride, void* stream) {
   if (!c || !cb || !cr) return fail(FME_E_INVALID, "fme_set_picture_chroma: null argument");
-  NEED_8BIT(c, "fme_set_picture_chroma");
   if (id < 0 || id >= FME_MAX_PICTURES) return fail(FME_E_INVALID, "fme_set_picture_chroma: id %d", id);
   if (!c->pics[id].luma) return fail(FME_E_STATE, "fme_set_picture_chroma: picture %d has no luma plane", id);
   const int cw = c->pics[id].width >> 1, ch = c->pics[id].height >> 1;
   if (stride < cw) return fail(FME_E_INVALID, "fme_set_picture_chroma: stride %d < %d", stride, cw);
   HIP_TRY(hipSetDevice(c->device));
-  const size_t bytes = 2 * (size_t)cw * ch;
+  const size_t bps = c->cfg.bit_depth > 8 ? 2 : 1;   // bytes per sample (10-bit: uint16 planes)
+  const size_t bytes = 2 * (size_t)cw * ch * bps;
   if (!c->chroma_owned[id] || c->chroma_bytes[id] < bytes) {
     if (c->chroma_owned[id]) HIP_TRY(hipFree(c->chroma_owned[id]));
     c->chroma_owned[id] = nullptr;
@@ -486,10 +486,10 @@ int fme_set_picture_chroma(fme_ctx* c, int id, const uint8_t* cb, const uint8_t*
     c->chroma_bytes[id] = bytes;
   }
   uint8_t* dcb = c->chroma_owned[id];
-  uint8_t* dcr = dcb + (size_t)cw * ch;
+  uint8_t* dcr = dcb + (size_t)cw * ch * bps;
   hipStream_t s = static_cast<hipStream_t>(stream);
-  HIP_TRY(hipMemcpy2DAsync(dcb, cw, cb, stride, cw, ch, hipMemcpyHostToDevice, s));
-  HIP_TRY(hipMemcpy2DAsync(dcr, cw, cr, stride, cw, ch, hipMemcpyHostToDevice, s));
+  HIP_TRY(hipMemcpy2DAsync(dcb, cw * bps, cb, stride * bps, cw * bps, ch, hipMemcpyHostToDevice, s));
+  HIP_TRY(hipMemcpy2DAsync(dcr, cw * bps, cr, stride * bps, cw * bps, ch, hipMemcpyHostToDevice, s));
   HIP_TRY(hipStreamSynchronize(s));
   c->pics[id].cb = dcb;
   c->pics[id].cr = dcr;
@@ -500,7 +500,6 @@ int fme_set_picture_chroma(fme_ctx* c, int id, const uint8_t* cb, const uint8_t*
 
 int fme_bind_picture_chroma_device(fme_ctx* c, int id, const uint8_t* d_cb, const uint8_t* d_cr, int stride) {
   if (!c || !d_cb || !d_cr) return fail(FME_E_INVALID, "fme_bind_picture_chroma_device: null argument");
-  NEED_8BIT(c, "fme_bind_picture_chroma_device");
   if (id < 0 || id >= FME_MAX_PICTURES) return fail(FME_E_INVALID, "fme_bind_picture_chroma_device: id %d", id);
   if (!c->pics[id].luma) return fail(FME_E_STATE, "fme_bind_picture_chroma_device: picture %d has no luma plane", id);
   if (stride < (c->pics[id].width >> 1)) return fail(FME_E_INVALID, "fme_bind_picture_chroma_device: stride %d", stride);
@@ -1757,7 +1756,6 @@ static const char* mc_job_problem(const fme_ctx* c, const fme_mc_job& j, int wid
 
 static int mc_launch(fme_ctx* c, const fme_mc_job* d_jobs, int n, uint8_t* y, int ys, uint8_t* cb, uint8_t* cr,
                      int cs, int width, int height, hipStream_t s) {
-  NEED_8BIT(c, "fme_motion_compensate");
   HIP_TRY(c->d_mc_invalid.reserve(1));
   HIP_TRY(hipMemsetAsync(c->d_mc_invalid.p, 0, sizeof(int32_t), s));
   if (int e = sync_tables(c, s)) return e;
@@ -1773,6 +1771,7 @@ static int mc_launch(fme_ctx* c, const fme_mc_job* d_jobs, int n, uint8_t* y, in
   a.c_stride = cs;
   a.width = width;
   a.height = height;
+  a.bit_depth = c->cfg.bit_depth;   // 10: uint16 planes, strides in samples (k_mc10)
   if (c->profiling) {
     if (!c->ev_mc[0]) {
       HIP_TRY(hipEventCreate(&c->ev_mc[0]));
@@ -1803,7 +1802,8 @@ int fme_motion_compensate(fme_ctx* c, const fme_mc_job* jobs, int n, uint8_t* y,
   if (n == 0) return FME_OK;
   HIP_TRY(hipSetDevice(c->device));
   hipStream_t s = static_cast<hipStream_t>(stream);
-  const size_t ly = (size_t)width * height, lc = ly / 4;
+  const size_t bps = c->cfg.bit_depth > 8 ? 2 : 1;   // bytes per sample (10-bit: uint16 planes)
+  const size_t ly = (size_t)width * height * bps, lc = ly / 4;
   HIP_TRY(c->d_mc_jobs.reserve(n));
   HIP_TRY(c->d_mc_planes.reserve(ly + 2 * lc));
   uint8_t* dy = c->d_mc_planes.p;
@@ -1811,13 +1811,13 @@ int fme_motion_compensate(fme_ctx* c, const fme_mc_job* jobs, int n, uint8_t* y,
   uint8_t* dcr = dcb + lc;
   const int cw = width / 2, ch = height / 2;
   HIP_TRY(hipMemcpyAsync(c->d_mc_jobs.p, jobs, n * sizeof(fme_mc_job), hipMemcpyHostToDevice, s));
-  HIP_TRY(hipMemcpy2DAsync(dy, width, y, ys, width, height, hipMemcpyHostToDevice, s));
-  HIP_TRY(hipMemcpy2DAsync(dcb, cw, cb, cs, cw, ch, hipMemcpyHostToDevice, s));
-  HIP_TRY(hipMemcpy2DAsync(dcr, cw, cr, cs, cw, ch, hipMemcpyHostToDevice, s));
+  HIP_TRY(hipMemcpy2DAsync(dy, width * bps, y, ys * bps, width * bps, height, hipMemcpyHostToDevice, s));
+  HIP_TRY(hipMemcpy2DAsync(dcb, cw * bps, cb, cs * bps, cw * bps, ch, hipMemcpyHostToDevice, s));
+  HIP_TRY(hipMemcpy2DAsync(dcr, cw * bps, cr, cs * bps, cw * bps, ch, hipMemcpyHostToDevice, s));
   if (int e = mc_launch(c, c->d_mc_jobs.p, n, dy, width, dcb, dcr, cw, width, height, s)) return e;
-  HIP_TRY(hipMemcpy2DAsync(y, ys, dy, width, width, height, hipMemcpyDeviceToHost, s));
-  HIP_TRY(hipMemcpy2DAsync(cb, cs, dcb, cw, cw, ch, hipMemcpyDeviceToHost, s));
-  HIP_TRY(hipMemcpy2DAsync(cr, cs, dcr, cw, cw, ch, hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipMemcpy2DAsync(y, ys * bps, dy, width * bps, width * bps, height, hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipMemcpy2DAsync(cb, cs * bps, dcb, cw * bps, cw * bps, ch, hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipMemcpy2DAsync(cr, cs * bps, dcr, cw * bps, cw * bps, ch, hipMemcpyDeviceToHost, s));
   HIP_TRY(hipStreamSynchronize(s));
   return FME_OK;
 }

@@ -59,6 +59,7 @@ struct McArgs {
   uint8_t* cr;
   int32_t* invalid;           // count of skipped jobs
   int32_t n, y_stride, c_stride, width, height;
+  int32_t bit_depth;          // 8, or 10: y / cb / cr and the pictures hold uint16 samples (strides in samples)
 };
 hipError_t launch_mc(const McArgs& a, hipStream_t s);
 

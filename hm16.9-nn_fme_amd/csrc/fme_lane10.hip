@@ -370,6 +370,15 @@ __device__ __forceinline__ void qpass(uint32_t (&v)[UH + 8][(UW + 8) / 2], const
       __builtin_amdgcn_sched_barrier(0);   // one column at a time (register pressure)
     }
   }
+  second_stages<UW, UH, T, UW, 0, NQ>(HQ, K, met, qy, d);
+}
+
+// The NQ vertical offsets qy[m] over first-stage columns C0 .. C0 + UW - 1 of HQ: a second stage
+// (filter<8, !isFirst, isLast>), key' - pred' and the unit's distortion each, one at a time.
+template <int UW, int UH, int T, int NC, int C0, int NQ>
+__device__ __forceinline__ void second_stages(uint32_t (&HQ)[NC][(UH + 8) / 2], const KeySrc<UW, UH / 2>& K,
+                                              const Metric& met, const int (&qy)[NQ], uint32_t (&d)[NQ]) {
+  constexpr int UJ = UH / 2;
 #pragma unroll
   for (int m = 0; m < NQ; m++) {
     launder(HQ);   // no candidate's values shared with (and kept live for) another
@@ -379,7 +388,7 @@ __device__ __forceinline__ void qpass(uint32_t (&v)[UH + 8][(UW + 8) / 2], const
 #pragma unroll
       for (int x = 0; x < UW; x++)
 #pragma unroll
-        for (int jj = 0; jj < UJ; jj++) X[x][jj] = pk_sub(K.at(x, jj), pk_round1(HQ[x][jj + 2]));
+        for (int jj = 0; jj < UJ; jj++) X[x][jj] = pk_sub(K.at(x, jj), pk_round1(HQ[C0 + x][jj + 2]));
     } else {
       uint32_t ce[5], co[5];
       cpairs(fy, 1 + iy, 64, ce);
@@ -392,7 +401,7 @@ __device__ __forceinline__ void qpass(uint32_t (&v)[UH + 8][(UW + 8) / 2], const
           const int m0 = (y & 1) ? (y - 1) / 2 : y / 2;
           int acc = 512 * 64;
 #pragma unroll
-          for (int t = 0; t < 5; t++) acc = dot2(HQ[x][m0 + t], (y & 1) ? co[t] : ce[t], acc);
+          for (int t = 0; t < 5; t++) acc = dot2(HQ[C0 + x][m0 + t], (y & 1) ? co[t] : ce[t], acc);
           vq[y] = acc;
         }
 #pragma unroll
@@ -401,6 +410,42 @@ __device__ __forceinline__ void qpass(uint32_t (&v)[UH + 8][(UW + 8) / 2], const
     }
     d[m] = unit_dist<UW, UH, T>(X, met);
     __builtin_amdgcn_sched_barrier(0);   // one candidate at a time
+  }
+}
+
+// The six half-pel side candidates (-1, 0/-1/+1) and (+1, 0/-1/+1) from the UW + 1 half columns
+// x - 1/2, x = 0 .. UW, that both sides share (xExtDIFUpSamplingH's filteredBlock[*][2] columns):
+// side -1 reads columns 0 .. UW-1, side +1 columns 1 .. UW.  d = H9 candidates 3, 5, 7, 4, 6, 8.
+template <int UW, int UH, int T>
+__device__ __forceinline__ void half_sides(uint32_t (&v)[UH + 8][(UW + 8) / 2], const KeySrc<UW, UH / 2>& K,
+                                           const Metric& met, uint32_t (&d)[6]) {
+  constexpr int RV = UH + 8;
+  uint32_t HQ[UW + 1][RV / 2];
+  const uint32_t c0 = p16(-1, 4), c1 = p16(-11, 40), c2 = p16(40, -11), c3 = p16(4, -1);
+#pragma unroll
+  for (int k = 0; k <= UW; k++) {   // window samples k .. k+7: the half column between cols k-1, k
+    launder(v);
+#pragma unroll
+    for (int r = 0; r < RV; r += 2) {
+      int h0 = dot2(rpair(v[r], k), c0, 0), h1 = dot2(rpair(v[r + 1], k), c0, 0);
+      h0 = dot2(rpair(v[r], k + 2), c1, h0);
+      h1 = dot2(rpair(v[r + 1], k + 2), c1, h1);
+      h0 = dot2(rpair(v[r], k + 4), c2, h0);
+      h1 = dot2(rpair(v[r + 1], k + 4), c2, h1);
+      h0 = dot2(rpair(v[r], k + 6), c3, h0);
+      h1 = dot2(rpair(v[r + 1], k + 6), c3, h1);
+      HQ[k][r / 2] = pack2(h0 >> 2, h1 >> 2);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  const int qy[3] = {0, -2, 2};
+  uint32_t dl[3], dr[3];
+  second_stages<UW, UH, T, UW + 1, 0, 3>(HQ, K, met, qy, dl);
+  second_stages<UW, UH, T, UW + 1, 1, 3>(HQ, K, met, qy, dr);
+#pragma unroll
+  for (int m = 0; m < 3; m++) {
+    d[m] = dl[m];
+    d[3 + m] = dr[m];
   }
 }
 
@@ -519,6 +564,8 @@ __device__ __attribute__((noinline)) void lane_unit10(const BatchArgs& a, const 
       for (int pos = 0; pos < 9; pos++) {
         const int dx = emi_dx(pos), dy = emi_dy(pos);
         uint32_t e = 0;
+        int sq = 0;       // SSE: sum of d * d
+        uint32_t lo = 0;  // SSE: sum of (d * d) mod 16 = ((d & 7)^2) & 15
 #pragma unroll
         for (int r = 0; r < UH; r++) {
           if (kSadEmi && (r & 1) && (fen == 1 || fen == 3)) continue;   // FEN: even rows (unit rows start even)
@@ -527,12 +574,16 @@ __device__ __attribute__((noinline)) void lane_unit10(const BatchArgs& a, const 
             const uint32_t dd = pk_sub(kraw[r][k], rpair(w[r + 1 + dy], 1 + dx + 2 * k));
             if constexpr (kSadEmi) {
               e = udot2(pk_abs(dd), 0x00010001u, e);
-            } else {   // xGetSSE at bitDepth 10: (d * d) >> 4 per sample
-              const int d0 = sx16(dd), d1 = hx16(dd);
-              e += ((uint32_t)(d0 * d0) >> (2 * kDsh)) + ((uint32_t)(d1 * d1) >> (2 * kDsh));
+            } else {
+              sq = dot2(dd, dd, sq);
+              const uint32_t m = dd & 0x00070007u;
+              const uint32_t f = __builtin_bit_cast(uint32_t, __builtin_bit_cast(v2u, m) * __builtin_bit_cast(v2u, m)) & 0x000F000Fu;
+              lo = udot2(f, 0x00010001u, lo);
             }
           }
         }
+        // xGetSSE at bitDepth 10 sums (d * d) >> 4 per sample: (sum d^2 - sum (d^2 mod 16)) / 16, exactly
+        if constexpr (!kSadEmi) e = ((uint32_t)sq - lo) >> (2 * kDsh);
         e9[pos] += e;
       }
     }
@@ -619,7 +670,7 @@ __device__ __attribute__((noinline)) void lane_unit10(const BatchArgs& a, const 
     }
   };
 
-  // ---- 2. half-pel stage: three passes (horizontal offset -2, 0, +2 quarter-pels) ---------------
+  // ---- 2. half-pel stage: the integer columns' pass, then the six side candidates -------------
   uint32_t hbest = 0xFFFFFFFFu;
   int hbi = 9;
   {
@@ -631,20 +682,14 @@ __device__ __attribute__((noinline)) void lane_unit10(const BatchArgs& a, const 
     take_half<L>(2, d[2], live, ml, mvx, mvy, mvp_x, mvp_y, hbest, hbi);
   }
   {
-    const int qy[3] = {0, -2, 2};
-    uint32_t d[3];
-    over_halves([&](uint32_t (&dd)[3]) FME_AI { qpass<UW, UH, T, -2, 3>(v, K, met, 0, qy, dd); }, d);
+    uint32_t d[6];
+    over_halves([&](uint32_t (&dd)[6]) FME_AI { half_sides<UW, UH, T>(v, K, met, dd); }, d);
     take_half<L>(3, d[0], live, ml, mvx, mvy, mvp_x, mvp_y, hbest, hbi);
     take_half<L>(5, d[1], live, ml, mvx, mvy, mvp_x, mvp_y, hbest, hbi);
     take_half<L>(7, d[2], live, ml, mvx, mvy, mvp_x, mvp_y, hbest, hbi);
-  }
-  {
-    const int qy[3] = {0, -2, 2};
-    uint32_t d[3];
-    over_halves([&](uint32_t (&dd)[3]) FME_AI { qpass<UW, UH, T, 2, 3>(v, K, met, 0, qy, dd); }, d);
-    take_half<L>(4, d[0], live, ml, mvx, mvy, mvp_x, mvp_y, hbest, hbi);
-    take_half<L>(6, d[1], live, ml, mvx, mvy, mvp_x, mvp_y, hbest, hbi);
-    take_half<L>(8, d[2], live, ml, mvx, mvy, mvp_x, mvp_y, hbest, hbi);
+    take_half<L>(4, d[3], live, ml, mvx, mvy, mvp_x, mvp_y, hbest, hbi);
+    take_half<L>(6, d[4], live, ml, mvx, mvy, mvp_x, mvp_y, hbest, hbi);
+    take_half<L>(8, d[5], live, ml, mvx, mvy, mvp_x, mvp_y, hbest, hbi);
   }
   const int hx = h9_dx(hbi), hy = h9_dy(hbi);
 

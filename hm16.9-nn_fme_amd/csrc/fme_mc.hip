@@ -308,6 +308,161 @@ __global__ __launch_bounds__(kMcBlock) void k_mc(McArgs a) {
   }
 }
 
+// ---- bit depth 10 (the main10 configurations): uint16 planes, int samples -----------------------
+// xPredInterBlk at bitDepth 10 (headRoom 4, TComInterpolationFilter.cpp:94-257) in the same
+// two-stage form as the 8-bit kernel: with s' = s - 512 the first stage filter<N, ., isFirst,
+// !isLast> is h = (sum c s - (8192 << 2)) >> 2 = (sum c s') >> 2 (the identity filter gives
+// filterCopy's 16 s'), the second uni (isLast): ((sum c h + 512) >> 10) + 512 clipped to 0..1023,
+// bi (!isLast): (sum c h) >> 6, which is HM's 14-bit value for every fraction pair (a zero fraction
+// is the identity: (64 h) >> 6 = h, (16 sum c s') >> 6 = (sum c s') >> 2).  TComYuv::addAvg at
+// bitDepth 10: (p0 + p1 + 16400) >> 5 clipped (shift 14 + 1 - 10, offset 16 + 2 * 8192).
+struct Plane16 {
+  const uint16_t* p;
+  int stride, w, h;
+};
+typedef __attribute__((address_space(1))) const uint16_t gu16c;
+
+template <int N, int U>
+__device__ __forceinline__ void pred10(const Plane16& pl, int bx, int by, uint32_t hlo, uint32_t hhi, uint32_t vlo,
+                                       uint32_t vhi, bool uni, int (&out)[U][U]) {
+  constexpr int R = U + N - 1;
+  const int x0 = bx - (N / 2 - 1), y0 = by - (N / 2 - 1);
+  int h[R][U];
+#pragma unroll
+  for (int r = 0; r < R; r++) {
+    const gu16c* row = (const gu16c*)(pl.p + (size_t)clamp_i(y0 + r, 0, pl.h - 1) * pl.stride);
+    int sv[R];
+#pragma unroll
+    for (int c = 0; c < R; c++) sv[c] = (int)row[clamp_i(x0 + c, 0, pl.w - 1)] - 512;
+#pragma unroll
+    for (int c = 0; c < U; c++) {
+      int acc = 0;
+#pragma unroll
+      for (int k = 0; k < N; k++) acc += tap_of(hlo, hhi, k) * sv[c + k];
+      h[r][c] = acc >> 2;
+    }
+  }
+#pragma unroll
+  for (int y = 0; y < U; y++)
+#pragma unroll
+    for (int c = 0; c < U; c++) {
+      int sum = 0;
+#pragma unroll
+      for (int k = 0; k < N; k++) sum += h[y + k][c] * tap_of(vlo, vhi, k);
+      out[y][c] = uni ? clamp_i(((sum + 512) >> 10) + 512, 0, 1023) : (sum >> 6);
+    }
+}
+
+__global__ __launch_bounds__(kMcBlock) void k_mc10(McArgs a) {
+  __shared__ McJobInfo info[kMcJobs];
+  __shared__ int first_unit[kMcJobs + 1];
+  const int j0 = blockIdx.x * kMcJobs;
+  const int t = threadIdx.x;
+  if (t < kMcJobs) {   // the job set-up of k_mc
+    McJobInfo& in = info[t];
+    in.units = 0;
+    const int ji = j0 + t;
+    if (ji < a.n) {
+      const fme_mc_job j = a.jobs[ji];
+      if (!mc_job_valid(a, j)) {
+        atomicAdd(a.invalid, 1);
+      } else {
+        int nl = 0, lists[2] = {0, 0};
+        if (j.flags & FME_MC_L0) lists[nl++] = 0;
+        if (j.flags & FME_MC_L1) lists[nl++] = 1;
+        if (nl == 2 && j.ref_id[0] == j.ref_id[1] && j.mv[0][0] == j.mv[1][0] && j.mv[0][1] == j.mv[1][1]) nl = 1;
+        in.nl = nl;
+        for (int k = 0; k < nl; k++) {
+          const int l = lists[k];
+          const PicDesc p = a.pics[j.ref_id[l]];
+          int mx = j.mv[l][0], my = j.mv[l][1];
+          clip_mv(mx, my, p.width, p.height, j.cu_x, j.cu_y);
+          in.lix[k] = mx >> 2;
+          in.liy[k] = my >> 2;
+          in.lfx[k] = mx & 3;
+          in.lfy[k] = my & 3;
+          in.cix[k] = mx >> 3;
+          in.ciy[k] = my >> 3;
+          in.cfx[k] = mx & 7;
+          in.cfy[k] = my & 7;
+          in.pic[k] = p;
+        }
+        in.x = j.x;
+        in.y = j.y;
+        in.ux_n = j.w >> 2;
+        in.units = (j.w >> 2) * (j.h >> 2);
+      }
+    }
+  }
+  __syncthreads();
+  if (t == 0) {
+    int acc = 0;
+    for (int k = 0; k < kMcJobs; k++) {
+      first_unit[k] = acc;
+      acc += info[k].units;
+    }
+    first_unit[kMcJobs] = acc;
+  }
+  __syncthreads();
+  const int total = first_unit[kMcJobs];
+  uint16_t* const oy = reinterpret_cast<uint16_t*>(a.y);
+  uint16_t* const ocb = reinterpret_cast<uint16_t*>(a.cb);
+  uint16_t* const ocr = reinterpret_cast<uint16_t*>(a.cr);
+  for (int g = t; g < total; g += kMcBlock) {
+    int q = 0;
+#pragma unroll
+    for (int k = 1; k < kMcJobs; k++) q += g >= first_unit[k] ? 1 : 0;
+    const McJobInfo& in = info[q];
+    const int u = g - first_unit[q];
+    const int ux = u % in.ux_n, uy = u / in.ux_n;
+    const bool uni = in.nl == 1;
+    {   // luma 4x4
+      const int x = in.x + 4 * ux, y = in.y + 4 * uy;
+      int acc[4][4], o[4][4];
+#pragma unroll
+      for (int k = 0; k < 2; k++) {
+        if (k >= in.nl) break;
+        const PicDesc& p = in.pic[k];
+        uint32_t hlo, hhi, vlo, vhi;
+        luma_taps(in.lfx[k], hlo, hhi);
+        luma_taps(in.lfy[k], vlo, vhi);
+        pred10<8, 4>(Plane16{reinterpret_cast<const uint16_t*>(p.luma), p.stride, p.width, p.height}, x + in.lix[k],
+                     y + in.liy[k], hlo, hhi, vlo, vhi, uni, o);
+#pragma unroll
+        for (int r = 0; r < 4; r++)
+#pragma unroll
+          for (int c = 0; c < 4; c++) acc[r][c] = k == 0 ? o[r][c] : clamp_i((acc[r][c] + o[r][c] + 16400) >> 5, 0, 1023);
+      }
+#pragma unroll
+      for (int r = 0; r < 4; r++)
+#pragma unroll
+        for (int c = 0; c < 4; c++) oy[(size_t)(y + r) * a.y_stride + x + c] = (uint16_t)acc[r][c];
+    }
+#pragma unroll
+    for (int comp = 1; comp <= 2; comp++) {   // chroma 2x2 of Cb and Cr (4:2:0)
+      const int x = (in.x >> 1) + 2 * ux, y = (in.y >> 1) + 2 * uy;
+      int acc[2][2], o[2][2];
+#pragma unroll
+      for (int k = 0; k < 2; k++) {
+        if (k >= in.nl) break;
+        const PicDesc& p = in.pic[k];
+        const Plane16 pl{reinterpret_cast<const uint16_t*>(comp == 1 ? p.cb : p.cr), p.cstride, p.width >> 1,
+                         p.height >> 1};
+        pred10<4, 2>(pl, x + in.cix[k], y + in.ciy[k], chroma_taps(in.cfx[k]), 0u, chroma_taps(in.cfy[k]), 0u, uni, o);
+#pragma unroll
+        for (int r = 0; r < 2; r++)
+#pragma unroll
+          for (int c = 0; c < 2; c++) acc[r][c] = k == 0 ? o[r][c] : clamp_i((acc[r][c] + o[r][c] + 16400) >> 5, 0, 1023);
+      }
+      uint16_t* base = comp == 1 ? ocb : ocr;
+#pragma unroll
+      for (int r = 0; r < 2; r++)
+#pragma unroll
+        for (int c = 0; c < 2; c++) base[(size_t)(y + r) * a.c_stride + x + c] = (uint16_t)acc[r][c];
+    }
+  }
+}
+
 // xGetTemplateCost (TEncSearch.cpp:4397-4436) distortion: clipMv of the candidate, the uni-pred
 // luma prediction xPredInterBlk(COMPONENT_Y, ..., bi = false) and getDistPart(DF_SAD) against the
 // original (plain SAD at every width: setDistParam(UInt, UInt, DFunc) sets no subsampling,
@@ -409,7 +564,10 @@ hipError_t launch_bi_key(const BiKeyArgs& a, hipStream_t s) {
 }
 
 hipError_t launch_mc(const McArgs& a, hipStream_t s) {
-  if (a.n > 0) hipLaunchKernelGGL(k_mc, dim3((a.n + kMcJobs - 1) / kMcJobs), dim3(kMcBlock), 0, s, a);
+  if (a.n > 0 && a.bit_depth > 8)
+    hipLaunchKernelGGL(k_mc10, dim3((a.n + kMcJobs - 1) / kMcJobs), dim3(kMcBlock), 0, s, a);
+  else if (a.n > 0)
+    hipLaunchKernelGGL(k_mc, dim3((a.n + kMcJobs - 1) / kMcJobs), dim3(kMcBlock), 0, s, a);
   return hipGetLastError();
 }
 

@@ -202,8 +202,10 @@ class FmeContext:
         _check(self.lib, self.lib.fme_bind_picture_device(self.h, pid, C.c_void_p(data_ptr), stride, width, height))
 
     def set_picture_chroma(self, pid, cb, cr, stream=None):
-        cb = np.ascontiguousarray(cb, dtype=np.uint8)
-        cr = np.ascontiguousarray(cr, dtype=np.uint8)
+        """4:2:0 chroma planes of picture pid: uint8, or uint16 samples in a bit-depth-10 context."""
+        dt = np.uint16 if self.bit_depth > 8 else np.uint8
+        cb = np.ascontiguousarray(cb, dtype=dt)
+        cr = np.ascontiguousarray(cr, dtype=dt)
         assert cb.shape == cr.shape
         _check(self.lib, self.lib.fme_set_picture_chroma(self.h, pid, _ptr(cb), _ptr(cr), cb.shape[1], stream))
 
@@ -320,8 +322,9 @@ class FmeContext:
         """Predict every job into the (host) planes y, cb, cr in place (fme_motion_compensate)."""
         from .abi import MC_JOB_DTYPE
         jobs = np.ascontiguousarray(mc_jobs, dtype=MC_JOB_DTYPE)
+        dt = np.uint16 if self.bit_depth > 8 else np.uint8   # main10: uint16 planes
         for a in (y, cb, cr):
-            assert a.dtype == np.uint8 and a.flags["C_CONTIGUOUS"]
+            assert a.dtype == dt and a.flags["C_CONTIGUOUS"]
         h, w = y.shape
         _check(self.lib, self.lib.fme_motion_compensate(self.h, _ptr(jobs), len(jobs), _ptr(y), y.shape[1], _ptr(cb),
                                                         _ptr(cr), cb.shape[1], w, h, stream))

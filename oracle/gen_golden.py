@@ -111,6 +111,49 @@ def build_case(name, seed, width, height, n_jobs, hadme, fen, nn_mode, qp, bipre
           f"{int((r_ref['n_emi'] < 8).sum())} with < 8 EMI pushes")
 
 
+def mc10_pictures(width, height, refs, seed):
+    """Reference pictures at bit depth 10: synthetic 10-bit luma, chroma from the 8-bit generator
+    with random low bits (every sample value 0..1023 reachable)."""
+    rng = np.random.default_rng(seed + 1000)
+    pics = {}
+    for k in range(refs):
+        cb, cr = synth.synth_chroma(width, height, k, seed=seed)
+        lo = rng.integers(0, 4, size=(2,) + cb.shape, dtype=np.uint16)
+        pics[k] = (synth.synth_luma_hbd(width, height, k, bit_depth=10, seed=seed),
+                   (cb.astype(np.uint16) << 2) | lo[0], (cr.astype(np.uint16) << 2) | lo[1])
+    return pics
+
+
+def build_mc10_case(name, seed, width, height, bi_frac, mv_amp, identical_frac, fill=0):
+    """Motion compensation at bit depth 10 (cfg *_main10.cfg InternalBitDepth 10): the predicted
+    uint16 planes from _ref's TComInterpolationFilter / TComYuv::addAvg at bitDepth 10 (the C
+    restatement's orc_mc is 8-bit: these fixtures pin the HIP path on the reference alone)."""
+    rng = np.random.default_rng(seed)
+    pics = mc10_pictures(width, height, 3, seed)
+    jobs = synth.make_mc_partition(rng, width, height, [0, 1, 2], bi_frac=bi_frac, mv_amp=mv_amp,
+                                   identical_frac=identical_frac)
+    ref = Reference(bit_depth=10)
+    for k, (y, cb, cr) in pics.items():
+        ref.set_picture_yuv(k, y, cb, cr)
+    y = np.full((height, width), fill, np.uint16)
+    cb = np.full((height // 2, width // 2), fill, np.uint16)
+    cr = cb.copy()
+    ref.mc(jobs, y, cb, cr)
+    path = os.path.join(OUT, f"{name}.npz")
+    np.savez_compressed(
+        path,
+        ref_y=np.stack([pics[k][0] for k in range(3)]),
+        ref_cb=np.stack([pics[k][1] for k in range(3)]),
+        ref_cr=np.stack([pics[k][2] for k in range(3)]),
+        jobs=jobs,
+        fill=np.array([fill], np.uint16),
+        bit_depth=np.array([10], np.int32),
+        pred_y=y, pred_cb=cb, pred_cr=cr,
+    )
+    print(f"{path}: {len(jobs)} PUs, {int(((jobs['flags'] & 3) == 3).sum())} bi-pred, "
+          f"luma {int(y.min())}..{int(y.max())}")
+
+
 def build_mc_case(name, seed, width, height, bi_frac, mv_amp, identical_frac, keep_frac=1.0, fill=0):
     """Motion compensation (TComPrediction::motionCompensation): reference pictures with 4:2:0
     chroma, one frame partition of decided PUs, the predicted planes from _ref (the oracle must
@@ -310,6 +353,13 @@ TZ2_CASES = [
     ("tz_enhanced_far_fen0_sr32", 35, 160, 96, 30, 0, 32, 0.1, 200, 0x08),
 ]
 
+MC10_CASES = [
+    # name, seed, W, H, bi fraction, MV amplitude (quarter-pel), identical-motion fraction, fill
+    ("mc10_ldp_uni", 41, 160, 104, 0.0, 40, 0.0, 0),
+    ("mc10_ra_bi_clip", 42, 168, 96, 0.5, 200, 0.2, 0),
+    ("mc10_bi_near", 43, 128, 80, 0.8, 12, 0.1, 513),
+]
+
 MC_CASES = [
     # name, seed, W, H, bi_frac, mv_amp (pel), identical_frac, keep_frac, fill
     ("mc_ldp_uni", 21, 160, 104, 0.0, 40, 0.0, 1.0, 0),
@@ -373,6 +423,10 @@ def main():
         for c in TZ2_CASES:
             build_tz2_case(*c)
         return 0
+    if "--mc10-only" in sys.argv:
+        for c in MC10_CASES:
+            build_mc10_case(*c)
+        return 0
     if "--ring-only" in sys.argv:
         for c in RING_CASES:
             build_ring_case(*c)
@@ -387,6 +441,8 @@ def main():
     if "--tz-only" not in sys.argv:
         for c in MC_CASES:
             build_mc_case(*c)
+        for c in MC10_CASES:
+            build_mc10_case(*c)
     for c in TZ_CASES:
         build_tz_case(*c)
     for c in TZ2_CASES:

@@ -323,6 +323,10 @@ class Reference:
         lib.ref_refine.argtypes = [_P, _P, _P, C.c_int]
         lib.ref_set_picture_yuv.restype = C.c_int
         lib.ref_set_picture_yuv.argtypes = [_P, C.c_int, _P, C.c_int, _P, _P, C.c_int, C.c_int, C.c_int]
+        lib.ref_set_picture_yuv16.restype = C.c_int
+        lib.ref_set_picture_yuv16.argtypes = [_P, C.c_int, _P, C.c_int, _P, _P, C.c_int, C.c_int, C.c_int]
+        lib.ref_mc16.restype = C.c_int
+        lib.ref_mc16.argtypes = [_P, _P, C.c_int, _P, C.c_int, _P, _P, C.c_int, C.c_int, C.c_int]
         lib.ref_integer_search.restype = C.c_int
         lib.ref_integer_search.argtypes = [_P, _P, _P, _P, C.c_int]
         lib.ref_integer_search_ring.restype = C.c_int
@@ -356,6 +360,12 @@ class Reference:
         self.lib.ref_set_picture(self.h, pid, _ptr(luma), luma.shape[1], luma.shape[1], luma.shape[0])
 
     def set_picture_yuv(self, pid, y, cb, cr):
+        """A 4:2:0 reference picture for mc(): uint8 planes, or uint16 planes at bit depth 10."""
+        if np.asarray(y).dtype == np.uint16:
+            y, cb, cr = (np.ascontiguousarray(a, dtype=np.uint16) for a in (y, cb, cr))
+            self.lib.ref_set_picture_yuv16(self.h, pid, _ptr(y), y.shape[1], _ptr(cb), _ptr(cr), cb.shape[1],
+                                           y.shape[1], y.shape[0])
+            return
         y, cb, cr = (np.ascontiguousarray(a, dtype=np.uint8) for a in (y, cb, cr))
         self.lib.ref_set_picture_yuv(self.h, pid, _ptr(y), y.shape[1], _ptr(cb), _ptr(cr), cb.shape[1], y.shape[1],
                                      y.shape[0])
@@ -400,9 +410,11 @@ class Reference:
         self.lib.ref_set_nn_inputs(self.h, _ptr(rows), len(rows))
 
     def mc(self, mc_jobs, y, cb, cr):
+        """Predictions into the planes y / cb / cr in place (uint8, or uint16 at bit depth 10)."""
         jobs = np.ascontiguousarray(mc_jobs)
         h, w = y.shape
-        rc = self.lib.ref_mc(self.h, _ptr(jobs), len(jobs), _ptr(y), y.shape[1], _ptr(cb), _ptr(cr), cb.shape[1], w, h)
+        f = self.lib.ref_mc16 if y.dtype == np.uint16 else self.lib.ref_mc
+        rc = f(self.h, _ptr(jobs), len(jobs), _ptr(y), y.shape[1], _ptr(cb), _ptr(cr), cb.shape[1], w, h)
         if rc != 0:
             raise RuntimeError(f"ref_mc: invalid job {-1 - rc}")
 

@@ -577,8 +577,9 @@ int ref_refine(void* h, const fme_job* jobs, fme_result* res, int n) {
 
 // ---- motion compensation ---------------------------------------------------------------------
 // 4:2:0 picture for motion compensation: TComPicYuv with margins + extendPicBorder.
-int ref_set_picture_yuv(void* h, int id, const uint8_t* y, int ys, const uint8_t* cb, const uint8_t* cr, int cs,
-                        int w, int hgt) {
+extern "C++" {
+template <typename S>
+static int set_picture_yuv(void* h, int id, const S* y, int ys, const S* cb, const S* cr, int cs, int w, int hgt) {
   RefCtx* c = static_cast<RefCtx*>(h);
   Pic& p = c->pics[id];
   p.yuv420.destroy();
@@ -587,7 +588,7 @@ int ref_set_picture_yuv(void* h, int id, const uint8_t* y, int ys, const uint8_t
     const ComponentID id_ = ComponentID(comp);
     Pel* dst = p.yuv420.getAddr(id_);
     const int ds = p.yuv420.getStride(id_);
-    const uint8_t* src = comp == 0 ? y : (comp == 1 ? cb : cr);
+    const S* src = comp == 0 ? y : (comp == 1 ? cb : cr);
     const int ss = comp ? cs : ys, pw = comp ? w / 2 : w, ph = comp ? hgt / 2 : hgt;
     for (int yy = 0; yy < ph; yy++)
       for (int xx = 0; xx < pw; xx++) dst[yy * ds + xx] = src[(size_t)yy * ss + xx];
@@ -596,6 +597,16 @@ int ref_set_picture_yuv(void* h, int id, const uint8_t* y, int ys, const uint8_t
   p.set420 = true;
   return 0;
 }
+}  // extern "C++"
+int ref_set_picture_yuv(void* h, int id, const uint8_t* y, int ys, const uint8_t* cb, const uint8_t* cr, int cs,
+                        int w, int hgt) {
+  return set_picture_yuv(h, id, y, ys, cb, cr, cs, w, hgt);
+}
+// 10-bit planes (strides in samples): the main10 configurations (ref_set_bit_depth first)
+int ref_set_picture_yuv16(void* h, int id, const uint16_t* y, int ys, const uint16_t* cb, const uint16_t* cr, int cs,
+                          int w, int hgt) {
+  return set_picture_yuv(h, id, y, ys, cb, cr, cs, w, hgt);
+}
 
 // TComPrediction::motionCompensation per job (TComPrediction.cpp:495-560).  TComDataCU /
 // TComPic are not built here, so the CU-level steps are restated: clipMv (TComDataCU.cpp
@@ -603,13 +614,15 @@ int ref_set_picture_yuv(void* h, int id, const uint8_t* y, int ys, const uint8_t
 // offset / fraction / filter order (616-668) over the reference's TComInterpolationFilter
 // (filterHor / filterVer with the component id and CHROMA_420, TComInterpolationFilter.cpp
 // :341-394) on the padded TComPicYuv; bi-prediction averages with TComYuv::addAvg.
-int ref_mc(void* h, const fme_mc_job* jobs, int n, uint8_t* y, int ys, uint8_t* cb, uint8_t* cr, int cs, int width,
-           int height) {
+extern "C++" {
+template <typename S>
+static int mc_run(void* h, const fme_mc_job* jobs, int n, S* y, int ys, S* cb, S* cr, int cs, int width, int height,
+                  int depth) {
   RefCtx* c = static_cast<RefCtx*>(h);
   TComInterpolationFilter f;
   BitDepths bd;
-  bd.recon[CHANNEL_TYPE_LUMA] = 8;
-  bd.recon[CHANNEL_TYPE_CHROMA] = 8;
+  bd.recon[CHANNEL_TYPE_LUMA] = depth;
+  bd.recon[CHANNEL_TYPE_CHROMA] = depth;
   for (int i = 0; i < n; i++) {
     const fme_mc_job& j = jobs[i];
     int lists[2], nl = 0;
@@ -643,14 +656,14 @@ int ref_mc(void* h, const fme_mc_job* jobs, int n, uint8_t* y, int ys, uint8_t* 
         const int xf = mx & ((1 << shH) - 1), yf = my & ((1 << shV) - 1);
         const int cw = j.w >> csx, ch = j.h >> csx;
         if (yf == 0) {
-          f.filterHor(cid, src, rs, dst, dstS, cw, ch, xf, !bi, CHROMA_420, 8);
+          f.filterHor(cid, src, rs, dst, dstS, cw, ch, xf, !bi, CHROMA_420, depth);
         } else if (xf == 0) {
-          f.filterVer(cid, src, rs, dst, dstS, cw, ch, yf, true, !bi, CHROMA_420, 8);
+          f.filterVer(cid, src, rs, dst, dstS, cw, ch, yf, true, !bi, CHROMA_420, depth);
         } else {
           const int nt = comp ? NTAPS_CHROMA : NTAPS_LUMA;
           std::vector<Pel> tmp((size_t)cw * (ch + nt - 1));
-          f.filterHor(cid, src - ((nt >> 1) - 1) * rs, rs, tmp.data(), cw, cw, ch + nt - 1, xf, false, CHROMA_420, 8);
-          f.filterVer(cid, tmp.data() + ((nt >> 1) - 1) * cw, cw, dst, dstS, cw, ch, yf, false, !bi, CHROMA_420, 8);
+          f.filterHor(cid, src - ((nt >> 1) - 1) * rs, rs, tmp.data(), cw, cw, ch + nt - 1, xf, false, CHROMA_420, depth);
+          f.filterVer(cid, tmp.data() + ((nt >> 1) - 1) * cw, cw, dst, dstS, cw, ch, yf, false, !bi, CHROMA_420, depth);
         }
       }
     }
@@ -660,16 +673,27 @@ int ref_mc(void* h, const fme_mc_job* jobs, int n, uint8_t* y, int ys, uint8_t* 
       const int csx = comp ? 1 : 0;
       const Pel* o = out.getAddr(cid);
       const int os = out.getStride(cid);
-      uint8_t* d = comp == 0 ? y : (comp == 1 ? cb : cr);
+      S* d = comp == 0 ? y : (comp == 1 ? cb : cr);
       const int dsd = comp ? cs : ys;
       for (int r = 0; r < (j.h >> csx); r++)
         for (int q = 0; q < (j.w >> csx); q++)
-          d[(size_t)((j.y >> csx) + r) * dsd + (j.x >> csx) + q] = (uint8_t)o[r * os + q];
+          d[(size_t)((j.y >> csx) + r) * dsd + (j.x >> csx) + q] = (S)o[r * os + q];
     }
     for (int k = 0; k < 2; k++) pred[k].destroy();
     out.destroy();
   }
   return 0;
+}
+}  // extern "C++"
+int ref_mc(void* h, const fme_mc_job* jobs, int n, uint8_t* y, int ys, uint8_t* cb, uint8_t* cr, int cs, int width,
+           int height) {
+  return mc_run(h, jobs, n, y, ys, cb, cr, cs, width, height, 8);
+}
+// 10-bit planes (strides in samples) at the context's bit depth (ref_set_bit_depth): xPredInterBlk and
+// addAvg at bitDepth 10 (TComInterpolationFilter.cpp:94-257 headroom 4, TComYuv.cpp:354-415 shift 5)
+int ref_mc16(void* h, const fme_mc_job* jobs, int n, uint16_t* y, int ys, uint16_t* cb, uint16_t* cr, int cs,
+             int width, int height) {
+  return mc_run(h, jobs, n, y, ys, cb, cr, cs, width, height, static_cast<RefCtx*>(h)->s.bd);
 }
 
 // xGetTemplateCost (TEncSearch.cpp:4397-4436) over the reference's own pieces: clipMv, xPredInterBlk's

@@ -35,7 +35,7 @@ def pytest_collection_modifyitems(config, items):
 def golden_cases():
     """Sub-pel refinement fixtures (fme_job -> fme_result)."""
     return sorted(f[:-4] for f in os.listdir(GOLDEN)
-                  if f.endswith(".npz") and not f.startswith(("mc_", "tz_", "ring_", "main10_")))
+                  if f.endswith(".npz") and not f.startswith(("mc_", "mc10_", "tz_", "ring_", "main10_")))
 
 
 def main10_golden_cases():
@@ -59,14 +59,19 @@ def mc_golden_cases():
     return sorted(f[:-4] for f in os.listdir(GOLDEN) if f.endswith(".npz") and f.startswith("mc_"))
 
 
+def mc10_golden_cases():
+    """Motion-compensation fixtures at bit depth 10 (uint16 planes, from oracle/_ref at bitDepth 10)."""
+    return sorted(f[:-4] for f in os.listdir(GOLDEN) if f.endswith(".npz") and f.startswith("mc10_"))
+
+
 def mc_inputs(g):
     """(pictures {id: (Y, Cb, Cr)}, jobs, fresh output planes filled like the fixture's)."""
     import numpy as np
     pics = {k: (g["ref_y"][k], g["ref_cb"][k], g["ref_cr"][k]) for k in range(len(g["ref_y"]))}
     fill = int(g["fill"][0])
     h, w = g["pred_y"].shape
-    planes = (np.full((h, w), fill, np.uint8), np.full((h // 2, w // 2), fill, np.uint8),
-              np.full((h // 2, w // 2), fill, np.uint8))
+    dt = g["pred_y"].dtype   # uint8, or uint16 at bit depth 10 (mc10_*)
+    planes = (np.full((h, w), fill, dt), np.full((h // 2, w // 2), fill, dt), np.full((h // 2, w // 2), fill, dt))
     return pics, g["jobs"], planes
 
 

@@ -46,8 +46,9 @@ def test_main10_golden_split_batches_and_device_path(case):
 
 
 def test_main10_entry_points_outside_the_path_refuse():
-    """A 10-bit context refuses the 8-bit-only kernels with FME_E_UNSUPPORTED (-4) instead of
-    reading 16-bit planes as bytes; 12 bits is refused at creation."""
+    """A 10-bit context refuses the 8-bit-only kernels (integer search, single-call FracDIF) with
+    FME_E_UNSUPPORTED (-4) instead of reading 16-bit planes as bytes; 12 bits is refused at
+    creation.  (Motion compensation runs at 10 bits: tests/test_gpu_mc.py.)"""
     from nnfme.runtime import FmeContext, FmeError
     from nnfme.abi import TZ_EXT_DTYPE
     g = load_golden(main10_golden_cases()[0])

@@ -5,7 +5,7 @@ restatement (orc_mc) on a full 1080p frame partition.  Integer output: bit-exact
 import numpy as np
 import pytest
 
-from conftest import load_golden, mc_golden_cases, mc_inputs
+from conftest import load_golden, mc10_golden_cases, mc_golden_cases, mc_inputs
 from nnfme import synth
 from nnfme.abi import MC_JOB_DTYPE, MC_L0, MC_L1
 
@@ -31,6 +31,56 @@ def test_mc_golden(case):
     pics, jobs, planes = mc_inputs(g)
     _ctx(pics).motion_compensate(jobs, *planes)
     _same(planes, (g["pred_y"], g["pred_cb"], g["pred_cr"]), case)
+
+
+@pytest.mark.parametrize("case", mc10_golden_cases())
+def test_mc10_golden(case):
+    """Bit depth 10 (main10): uint16 planes through fme_motion_compensate against the reference's
+    own filters and addAvg at bitDepth 10 (k_mc10)."""
+    from nnfme.runtime import FmeContext
+    g = load_golden(case)
+    pics, jobs, planes = mc_inputs(g)
+    ctx = FmeContext(nn_mode=0, bit_depth=10)
+    for k, (y, cb, cr) in pics.items():
+        ctx.set_picture_yuv(k, y, cb, cr)
+    ctx.motion_compensate(jobs, *planes)
+    _same(planes, (g["pred_y"], g["pred_cb"], g["pred_cr"]), case)
+
+
+def test_mc10_device_frame_matches_reference():
+    """A 416x240 main10 partition (every PU shape, 40 % bi-pred, MVs up to +-150 quarter-pel so
+    clipMv acts at the borders) with device-resident jobs and uint16 planes, against oracle/_ref
+    at bitDepth 10 run live."""
+    import torch
+    from nnfme.runtime import FmeContext
+    from oracle import Reference
+    W, H = 416, 240
+    rng = np.random.default_rng(5)
+    pics = {}
+    for k in range(3):
+        cb, cr = synth.synth_chroma(W, H, k)
+        lo = rng.integers(0, 4, size=(2,) + cb.shape, dtype=np.uint16)
+        pics[k] = (synth.synth_luma_hbd(W, H, k, bit_depth=10), (cb.astype(np.uint16) << 2) | lo[0],
+                   (cr.astype(np.uint16) << 2) | lo[1])
+    jobs = synth.make_mc_partition(rng, W, H, [0, 1, 2], bi_frac=0.4, mv_amp=150, identical_frac=0.1)
+    ctx = FmeContext(nn_mode=0, bit_depth=10)
+    ref = Reference(bit_depth=10)
+    for k, p in pics.items():
+        ctx.set_picture_yuv(k, *p)
+        ref.set_picture_yuv(k, *p)
+    dev = torch.device("cuda", 0)
+    dj = torch.from_numpy(jobs.view(np.uint8).copy()).to(dev)
+    dy = torch.zeros((H, W), dtype=torch.int16, device=dev)
+    dcb = torch.zeros((H // 2, W // 2), dtype=torch.int16, device=dev)
+    dcr = torch.zeros_like(dcb)
+    s = torch.cuda.current_stream(dev).cuda_stream
+    ctx.motion_compensate_device(dj.data_ptr(), len(jobs), dy.data_ptr(), W, dcb.data_ptr(), dcr.data_ptr(), W // 2,
+                                 W, H, s)
+    assert ctx.mc_invalid_count() == 0
+    exp = (np.zeros((H, W), np.uint16), np.zeros((H // 2, W // 2), np.uint16), np.zeros((H // 2, W // 2), np.uint16))
+    ref.mc(jobs, *exp)
+    got = tuple(t.cpu().numpy().view(np.uint16) for t in (dy, dcb, dcr))
+    _same(got, exp, "416x240 main10")
 
 
 def _frame(W, H, refs, seed):

@@ -5,7 +5,8 @@ import os
 import numpy as np
 import pytest
 
-from conftest import tz_golden_cases, mc_golden_cases, mc_inputs, golden_cases, load_golden, main10_golden_cases
+from conftest import (tz_golden_cases, mc_golden_cases, mc10_golden_cases, mc_inputs, golden_cases, load_golden,
+                      main10_golden_cases)
 from nnfme import synth, weights
 from nnfme.abi import PARITY_FIELDS, compare_results
 from oracle import REF_SO, Oracle, Reference
@@ -124,6 +125,32 @@ def test_mc_oracle_matches_reference_random(seed, bi, amp):
         outs.append((y, cb, cr))
     for a, b in zip(*outs):
         assert np.array_equal(a, b)
+
+
+@pytest.mark.skipif(not HAVE_REF, reason="oracle/_ref not built")
+@pytest.mark.parametrize("case", mc10_golden_cases())
+def test_mc10_golden_is_the_reference(case):
+    """The main10 MC fixtures are oracle/_ref's output at bitDepth 10 (the reference's own
+    TComInterpolationFilter and TComYuv::addAvg): recomputed here, bit for bit."""
+    g = load_golden(case)
+    assert int(g["bit_depth"][0]) == 10
+    pics, jobs, (y, cb, cr) = mc_inputs(g)
+    ref = Reference(bit_depth=10)
+    for k, p in pics.items():
+        ref.set_picture_yuv(k, *p)
+    ref.mc(jobs, y, cb, cr)
+    for got, exp, comp in ((y, g["pred_y"], "Y"), (cb, g["pred_cb"], "Cb"), (cr, g["pred_cr"], "Cr")):
+        assert got.dtype == np.uint16 and np.array_equal(got, exp), f"{case} {comp}"
+
+
+def test_mc10_goldens_cover_bi_clip_and_range():
+    bi = uni = 0
+    for case in mc10_golden_cases():
+        g = load_golden(case)
+        bi += int(((g["jobs"]["flags"] & 3) == 3).sum())
+        uni += int(((g["jobs"]["flags"] & 3) != 3).sum())
+        assert g["pred_y"].max() > 255 and g["pred_y"].max() <= 1023   # really 10-bit samples
+    assert bi > 50 and uni > 50 and len(mc10_golden_cases()) >= 3
 
 
 def test_mc_golden_covers_cases():

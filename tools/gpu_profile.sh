@@ -26,6 +26,12 @@ if [ "${PROF:-1}" = 1 ]; then
   run sq_n 150 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_LDS SQ_WAVES GRBM_GUI_ACTIVE --output-format csv -d $O/sq/n -o run -- $P --steps 2 --warmup 1
   run sq_o 150 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_VMEM --output-format csv -d $O/sq/o -o run -- $P --steps 2 --warmup 1
   python3 tools/pmc_summary.py $O/sq > $O/sq_summary.txt
+  if [ "${M10:-0}" = 1 ]; then   # the main10 search kernel (k_search_lane10): kernel stats and SQ counters
+    run trace10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/trace10 -o run -- $P --workload c3_qp22_main10 --steps 10 --warmup 2
+    run sq10_n 150 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_LDS SQ_WAVES GRBM_GUI_ACTIVE --output-format csv -d $O/sq10/n -o run -- $P --workload c3_qp22_main10 --steps 2 --warmup 1
+    run sq10_o 150 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_VMEM --output-format csv -d $O/sq10/o -o run -- $P --workload c3_qp22_main10 --steps 2 --warmup 1
+    python3 tools/pmc_summary.py $O/sq10 > $O/sq10_summary.txt
+  fi
 fi
 if [ "${WORKLOADS:-1}" = 1 ]; then
   run bench_c1 300 python bench.py --workload c1 --no-pi --no-tz --no-mc --cpu-seconds 12 --cpu-cores -1
