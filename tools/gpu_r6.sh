@@ -57,6 +57,7 @@ for step in "$@"; do
     copytl_rocpd) run copytl_rocpd 300 rocprofv3 --kernel-trace --memory-copy-trace --output-format rocpd -d gpurun_out/copytl_rocpd -o run -- python3 bench.py --no-pi --no-tz --no-mc --no-cpu-baseline --parity-seconds 0 --steps 10 ;;
     tl) run tl_c3 200 $B --steps 20 --parity-seconds 0 --timeline gpurun_out/timeline_c3.txt && \
         run tl_c1 200 $B --workload c1 --steps 20 --parity-seconds 0 --timeline gpurun_out/timeline_c1.txt ;;
+    mc10) run mc10tests 300 python -u -m pytest tests/test_gpu_mc.py tests/test_gpu_main10.py -m gpu -x -v -p no:cacheprovider --timeout 200 --timeout-method thread ;;
     logwait) run env_logwait 200 env AMD_LOG_LEVEL=4 AMD_LOG_MASK=294 $B --steps 12 --parity-seconds 0 ;;
     tzc) run tz_counts 200 python -u tools/tz_counts.py ;;
     icache) A="python tools/ab_bench.py . --rounds 2 --reps 2"
