@@ -274,6 +274,8 @@ struct fme_ctx {
   hipEvent_t ev_done = nullptr; // end of the last batch (fme_refine_status)
   hipEvent_t ev_search = nullptr; // caller's event, recorded before each search launch (fme_set_search_event)
   int search_reserve = 0;         // resident search workgroups left free (fme_set_search_reserve)
+  fme_ctx* single10 = nullptr;    // bit depth 10: the private one-job context of fme_frac_dif_single
+  hipStream_t single10_stream = nullptr;
   bool main10_px = false;         // bit depth 10: the pixel kernel instead of the lane kernel
                                   // (environment FME_MAIN10_SEARCH=px, an A/B switch)
   bool batch_issued = false;
@@ -379,6 +381,8 @@ int fme_destroy(fme_ctx* c) {
   if (!c) return FME_OK;
   (void)hipSetDevice(c->device);
   (void)srv_stop(c);
+  if (c->single10) (void)fme_destroy(c->single10);
+  if (c->single10_stream) (void)hipStreamDestroy(c->single10_stream);
   (void)hipDeviceSynchronize();
   for (int i = 0; i < FME_MAX_PICTURES; i++)
     if (c->pic_owned[i] && c->pics[i].luma) (void)hipFree(const_cast<uint8_t*>(c->pics[i].luma));
@@ -1613,17 +1617,76 @@ static int srv_call(fme_ctx* c, bool uses_nn) {
 // and the reference window around the integer MV (rows -4..h+3, columns -4..w+3 of the padded
 // picture) go into the server's mailbox; the MV predictor is shifted by 4*mv_int so that every
 // MV-cost argument (xPatternRefinement's (cMvTest << scale) - pred) is unchanged.
+// Bit depth 10: the call runs as a one-job batch (the lane kernel k_search_lane10, bit-exact with
+// the main10 batches) on a private 10-bit context with its own stream, so the caller's pictures,
+// lambdas, keys and NN state are untouched: the window (rows -4..h+3, columns -4..w+3 around
+// mv_int) becomes picture 0 with the PU at (4, 4), the key its key block, the MV predictor is
+// shifted by 4*mv_int as for the server.  Latency: a few launches and copies per call.
+static int frac_dif_single10(fme_ctx* c, int lossless, const int16_t* key, int key_stride, int w, int h,
+                             const int16_t* ref, int ref_stride, int mv_int_x, int mv_int_y, int px, int py,
+                             double motion_lambda, int16_t* half_xy, int16_t* qtr_xy, uint32_t* cost) {
+  if (!c->single10) {
+    fme_config cfg = c->cfg;
+    cfg.nn_mode = 0;
+    cfg.max_jobs = 64;
+    fme_ctx* s = nullptr;
+    const int rc = fme_create(c->device, &cfg, &s);
+    if (rc) return rc;
+    c->single10 = s;
+    HIP_TRY(hipStreamCreateWithFlags(&c->single10_stream, hipStreamNonBlocking));
+  }
+  fme_ctx* s = c->single10;
+  const int pw = w + 8, ph = h + 8;
+  const int maxv = (1 << c->cfg.bit_depth) - 1;
+  std::vector<uint16_t> win((size_t)pw * ph);
+  for (int y = 0; y < ph; y++) {
+    const int16_t* src = ref + (ptrdiff_t)(mv_int_y - 4 + y) * ref_stride + (mv_int_x - 4);
+    for (int x = 0; x < pw; x++) win[(size_t)y * pw + x] = (uint16_t)std::min(maxv, std::max(0, (int)src[x]));
+  }
+  std::vector<int16_t> kb((size_t)w * h);
+  for (int y = 0; y < h; y++) std::memcpy(&kb[(size_t)y * w], key + (ptrdiff_t)y * key_stride, (size_t)w * sizeof(int16_t));
+  int rc = fme_set_picture(s, 0, reinterpret_cast<const uint8_t*>(win.data()), pw, pw, ph, c->single10_stream);
+  if (!rc) rc = fme_set_motion_lambda(s, 0, motion_lambda);
+  if (!rc) rc = fme_set_keys(s, kb.data(), kb.size(), c->single10_stream);
+  if (rc) return rc;
+  fme_job j{};
+  j.x = 4;
+  j.y = 4;
+  j.w = (uint8_t)w;
+  j.h = (uint8_t)h;
+  j.org_id = 0;
+  j.ref_id = 0;
+  j.mvp_x = (int16_t)px;
+  j.mvp_y = (int16_t)py;
+  j.lt_x = j.lt_y = -1;
+  j.rb_x = j.rb_y = 1;
+  j.flags = lossless ? FME_JOB_LOSSLESS : 0;
+  j.key_offset = 0;
+  fme_result r{};
+  rc = fme_refine(s, &j, &r, 1, c->single10_stream);
+  if (rc) return rc;
+  if (r.status & FME_RES_REJECTED) return fail(FME_E_INVALID, "fme_frac_dif_single: job rejected");
+  half_xy[0] = r.half_x;
+  half_xy[1] = r.half_y;
+  qtr_xy[0] = r.qtr_x;
+  qtr_xy[1] = r.qtr_y;
+  *cost = r.frac_cost;
+  return FME_OK;
+}
+
 int fme_frac_dif_single(fme_ctx* c, int lossless, const int16_t* key, int key_stride, int w, int h,
                         const int16_t* ref, int ref_stride, int mv_int_x, int mv_int_y, int mvp_x,
                         int mvp_y, double motion_lambda, int16_t* half_xy, int16_t* qtr_xy,
                         uint32_t* cost) {
   if (!c || !key || !ref || !half_xy || !qtr_xy || !cost) return fail(FME_E_INVALID, "fme_frac_dif_single: null argument");
-  NEED_8BIT(c, "fme_frac_dif_single");
   const int cls = class_of(w, h);
   if (cls < 0) return fail(FME_E_UNSUPPORTED, "fme_frac_dif_single: %dx%d", w, h);
   const int px = mvp_x - 4 * mv_int_x, py = mvp_y - 4 * mv_int_y;
   if (px < -32768 || px > 32767 || py < -32768 || py > 32767) return fail(FME_E_INVALID, "fme_frac_dif_single: predictor out of range");
   HIP_TRY(hipSetDevice(c->device));
+  if (c->cfg.bit_depth > 8)
+    return frac_dif_single10(c, lossless, key, key_stride, w, h, ref, ref_stride, mv_int_x, mv_int_y, px, py,
+                             motion_lambda, half_xy, qtr_xy, cost);
   int rc = srv_open(c);
   if (rc) return rc;
   SrvBox* b = c->box;

@@ -31,6 +31,19 @@
 namespace fme {
 
 constexpr int kNumClasses = 24;      // HEVC inter PU shapes 4x8 .. 64x64 incl. AMP
+
+// Order in which an XCD's band visits the PU classes (Schedule::xq position -> class id):
+// 0 = by class id (smallest PUs first), 1 = reversed (largest first), 2 = smallest and largest
+// alternating (0, 23, 1, 22, ...).  A/B on the 1080p batch: 0.876 / 0.880 / 0.884 ms, results
+// identical (profiles/r06_ab.log): the band's first class pays its cold start whichever it is.
+#ifndef FME_LANE_ORDER
+#define FME_LANE_ORDER 0
+#endif
+__host__ __device__ __forceinline__ constexpr int lane_class_at(int pos) {
+  return FME_LANE_ORDER == 1 ? kNumClasses - 1 - pos
+         : FME_LANE_ORDER == 2 ? ((pos & 1) ? kNumClasses - 1 - (pos >> 1) : (pos >> 1))
+                               : pos;
+}
 constexpr int kBlock = 256;          // threads per workgroup (4 wavefronts)
 constexpr int kJobsPerScanBlock = 1024;  // classify / NN kernels: 4 jobs per thread
 constexpr int kKeyedWord = 60;           // counts[]: jobs that read a key block (k_classify)
@@ -150,8 +163,9 @@ struct Schedule {
   // The lane kernel's per-XCD tile queues.  Every class's wave tiles are split into 8 S
   // contiguous bands (S = FME_LANE_SUBBANDS; band B holds tiles [nt B / 8S, nt (B+1) / 8S) of a
   // class with nt tiles), XCD x owns bands x S .. x S + S - 1, and its queue lists them band by
-  // band, class by class inside a band: xq[x][s][c] = the queue's tiles before (band x S + s,
-  // class c); xq[x][s][kNumClasses] = before band s + 1 (xq[x][S-1][kNumClasses] = its length).
+  // band, class by class inside a band in the order lane_class_at: xq[x][s][i] = the queue's tiles
+  // before (band x S + s, class lane_class_at(i)); xq[x][s][kNumClasses] = before band s + 1
+  // (xq[x][S-1][kNumClasses] = its length).
   int32_t xq[8][FME_LANE_SUBBANDS][kNumClasses + 1];
   int32_t invalid;            // jobs rejected by k_classify (the whole batch is then skipped)
   int32_t pad_[3];

@@ -198,7 +198,8 @@ __global__ __launch_bounds__(64) void k_schedule(WorkBufs w, SchedParams p) {
 #pragma unroll 1
     for (int q = 0; q < S; q++) {
       const int B = x * S + q;
-      const int mine = c < kNumClasses ? band_lo(B + 1) - band_lo(B) : 0;
+      const int mine_c = c < kNumClasses ? band_lo(B + 1) - band_lo(B) : 0;   // class c's band tiles
+      const int mine = __shfl(mine_c, c < kNumClasses ? lane_class_at(c) : c);  // position c's
       const int ex = run + wave_excl_scan(mine);
       if (c <= kNumClasses) sc->xq[x][q][c] = ex;
       run = __shfl(ex, kNumClasses);

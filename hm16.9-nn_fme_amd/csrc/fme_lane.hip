@@ -1311,10 +1311,12 @@ void k_search_lane(BatchArgs a, WorkBufs w) {
       int q = 0, c = 0;   // band x S + q of the queue, class c inside it
       while (q < S - 1 && tw >= s_xq[x][q][kNumClasses]) q++;
       while (c < kNumClasses - 1 && tw >= s_xq[x][q][c + 1]) c++;
+      const int ci = c;   // queue position -> class
+      c = lane_class_at(ci);
       const int nt = sc->prefix[c + 1] - sc->prefix[c];
       const int lo = (int)(((long long)nt * (x * S + q)) / (8 * S));   // the band's first tile of class c
       // wave-uniform: kept in an SGPR, so no VGPR of it lives (and is spilled) across the call
-      const int wt = __builtin_amdgcn_readfirstlane(lo + (tw - s_xq[x][q][c]));
+      const int wt = __builtin_amdgcn_readfirstlane(lo + (tw - s_xq[x][q][ci]));
       switch (c) {
         FME_LANE_CLASSES(FME_CASE)
         default: break;

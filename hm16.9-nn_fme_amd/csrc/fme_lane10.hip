@@ -335,10 +335,13 @@ __device__ __forceinline__ void load_window(const PicDesc& pic, int x0, int y0, 
 // and NQ vertical offsets qy[m] (a second stage and a distortion each); v = window rows -4..UH+3,
 // cols -4..UW+3 as pairs.  QX constant (half stage) or kRuntime (qx per lane: the quarter stage).
 constexpr int kRuntime = 99;
+template <int UW, int UH, int T, int NC, int C0, int NQ>
+__device__ __forceinline__ void second_stages(uint32_t (&HQ)[NC][(UH + 8) / 2], const KeySrc<UW, UH / 2>& K,
+                                              const Metric& met, const int (&qy)[NQ], uint32_t (&d)[NQ]);
 template <int UW, int UH, int T, int QX, int NQ>
 __device__ __forceinline__ void qpass(uint32_t (&v)[UH + 8][(UW + 8) / 2], const KeySrc<UW, UH / 2>& K, const Metric& met,
                                       int qx_rt, const int (&qy)[NQ], uint32_t (&d)[NQ]) {
-  constexpr int RV = UH + 8, UJ = UH / 2;
+  constexpr int RV = UH + 8;
   uint32_t HQ[UW][RV / 2];   // first-stage rows (2k, 2k+1) of each column
   if constexpr (QX != kRuntime && (QX & 3) == 0) {   // integer columns: h = 16 s' (filterCopy, isFirst)
     launder(v);
@@ -807,9 +810,11 @@ void k_search_lane10(BatchArgs a, WorkBufs w) {
       int q = 0, c = 0;
       while (q < S - 1 && tw >= s_xq[x][q][kNumClasses]) q++;
       while (c < kNumClasses - 1 && tw >= s_xq[x][q][c + 1]) c++;
+      const int ci = c;   // queue position -> class
+      c = lane_class_at(ci);
       const int nt = sc->prefix[c + 1] - sc->prefix[c];
       const int lo = (int)(((long long)nt * (x * S + q)) / (8 * S));
-      const int wt = __builtin_amdgcn_readfirstlane(lo + (tw - s_xq[x][q][c]));
+      const int wt = __builtin_amdgcn_readfirstlane(lo + (tw - s_xq[x][q][ci]));
       switch (c) {
         FME_L10_CLASSES(FME_CASE10)
         default: break;

@@ -48,10 +48,10 @@ extern "C" {
 typedef struct fme_config {
   int32_t bit_depth;        /* internal luma bit depth: 8, or 10 for the main10
                                configurations (cfg/encoder_*_main10.cfg InternalBitDepth 10):
-                               pictures are then uint16 sample planes (strides in samples) and
-                               the refinement batches (fme_refine*) run the pixel kernel;
-                               integer search, MC, producers, bi-pred key builds and
-                               fme_frac_dif_single return FME_E_UNSUPPORTED at 10 bits       */
+                               pictures are then uint16 sample planes (strides in samples);
+                               the refinement batches (fme_refine*), fme_frac_dif_single and
+                               motion compensation run at 10 bits; integer search, the
+                               producers and bi-pred key builds return FME_E_UNSUPPORTED     */
   int32_t use_hadamard;     /* HadamardME (TAppEncCfg.cpp:760): SATD vs SAD in FracDIF   */
   int32_t nn_mode;          /* 0: standard FracDIF MV (TEncSearch.cpp:4587-4588 variant)
                                1: NN_pred() MV (shipped behaviour, TEncSearch.cpp:4590-4591)
@@ -649,7 +649,9 @@ int fme_pred_inter_phases(fme_ctx* ctx, double* ms, int count);
  *   key/key_stride/w/h = pcPatternKey ROI, ref/ref_stride = piRefY/iRefStride
  *   (host pointer at the PU origin of a padded picture: reads span rows -4..h+3 and
  *   columns -4..w+3 around mv_int), mvp/motion_lambda = the TComRdCost state.
- * Synchronous; latency-bound by construction (one launch per call).                     */
+ * Synchronous; latency-bound by construction (one launch per call).  At bit depth 10 the
+ * call runs as a one-job batch (k_search_lane10) on a private 10-bit context created at the
+ * first such call, key and window in int16 / uint16 samples (a few launches and copies).      */
 int fme_frac_dif_single(fme_ctx* ctx, int lossless, const int16_t* key, int key_stride, int w,
                         int h, const int16_t* ref, int ref_stride, int mv_int_x, int mv_int_y,
                         int mvp_x, int mvp_y, double motion_lambda, int16_t* half_xy,

@@ -1,6 +1,7 @@
 """Bit depth 10 (the main10 configurations: cfg/encoder_lowdelay_P_main10.cfg:58,
 encoder_randomaccess_main10.cfg:60, encoder_lowdelay_main10.cfg:56 InternalBitDepth 10) through
-the HIP path: 16-bit pictures, the pixel-per-lane search kernel (csrc/fme_px.hip), the same NN tail.
+the HIP path: 16-bit pictures, the lane-per-unit search kernel on int16 samples
+(csrc/fme_lane10.hip), the same NN tail; the single-call FracDIF as a one-job batch.
 
 Bit-exact against the main10 goldens (oracle/_ref's TComInterpolationFilter / TComRdCost at
 bitDepth 10, the C oracle agreeing) and, over a whole 416x240 frame in HM's CTU order, every field
@@ -11,7 +12,7 @@ import pytest
 from conftest import load_golden, main10_golden_cases
 from nnfme import synth, weights
 from nnfme.abi import JOB_DTYPE, MV_FIELDS, MV_RESULT_DTYPE, RESULT_DTYPE, compare_results
-from test_gpu_parity import _assert_same, _ctx
+from test_gpu_parity import _assert_same, _ctx, _frac_single_check
 
 pytestmark = pytest.mark.gpu
 
@@ -46,9 +47,9 @@ def test_main10_golden_split_batches_and_device_path(case):
 
 
 def test_main10_entry_points_outside_the_path_refuse():
-    """A 10-bit context refuses the 8-bit-only kernels (integer search, single-call FracDIF) with
-    FME_E_UNSUPPORTED (-4) instead of reading 16-bit planes as bytes; 12 bits is refused at
-    creation.  (Motion compensation runs at 10 bits: tests/test_gpu_mc.py.)"""
+    """A 10-bit context refuses the 8-bit-only kernels (integer search) with FME_E_UNSUPPORTED (-4)
+    instead of reading 16-bit planes as bytes; 12 bits is refused at creation.  (Motion
+    compensation runs at 10 bits: tests/test_gpu_mc.py; the single-call FracDIF below.)"""
     from nnfme.runtime import FmeContext, FmeError
     from nnfme.abi import TZ_EXT_DTYPE
     g = load_golden(main10_golden_cases()[0])
@@ -59,15 +60,31 @@ def test_main10_entry_points_outside_the_path_refuse():
         ctx.integer_search(jobs, ext)
     assert e.value.code == -4
     with pytest.raises(FmeError) as e:
-        key = np.zeros((8, 8), np.int16)
-        ctx.frac_dif_single(key, np.zeros((40, 40), np.int16), (16, 16), (0, 0), (0, 0), 100.0)
-    assert e.value.code == -4
-    with pytest.raises(FmeError) as e:
         FmeContext(bit_depth=12)
     assert e.value.code == -4
     # the NN_pred single call is bit-depth independent
     cls, _ = ctx.nn_pred_single(np.arange(1, 9, dtype=np.uint32) * 1000, 777, 8, 8)
     assert 0 <= cls < 49
+
+
+@pytest.mark.parametrize("case", main10_golden_cases())
+def test_main10_frac_dif_single_every_shape(case):
+    """xPatternSearchFracDIF's single-PU entry point at bit depth 10 (a one-job batch on a private
+    10-bit context): rcMvHalf, rcMvQter and ruiCost equal the main10 goldens' FracDIF fields for
+    every PU shape (up to 4 jobs per shape, keyed bi-pred jobs and lossless jobs included), and the
+    caller's context is untouched (its batch still matches afterwards)."""
+    g = load_golden(case)
+    jobs = g["jobs"]
+    idx = []
+    for (w, h) in synth.ALL_PU_SIZES:
+        sel = np.flatnonzero((jobs["w"] == w) & (jobs["h"] == h))
+        idx += list(sel[:: max(1, len(sel) // 4)][:4])
+    idx += list(np.flatnonzero(jobs["flags"] & 4)[:4])
+    idx += list(np.flatnonzero(jobs["key_offset"] >= 0)[:4])
+    ctx = _ctx(g)
+    _frac_single_check(ctx, g, idx)
+    ctx.nn_reset()
+    _assert_same(ctx.refine(jobs), g["results"], case + " after single calls")
 
 
 def test_main10_frame_every_job_against_reference():
