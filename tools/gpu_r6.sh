@@ -29,6 +29,7 @@ for step in "$@"; do
     stamps) run lane_stamps 200 python -u tools/lane_stamps.py 5 ;;
     pkab) run pkab 300 python -u tools/ab_bench.py . variants/pk16 --rounds 4 ;;
     ordab) run ordab 300 python -u tools/ab_bench.py . variants/ord1 variants/ord2 --rounds 4 ;;
+    pfab) run pfab 300 python -u tools/ab_bench.py . variants/pf --rounds 5 ;;
     u44ab) run u44ab 300 python -u tools/ab_bench.py . variants/u44 --rounds 4 ;;
     pipe2) run q_c3 200 $B --steps 20 --parity-seconds 10 && run q_c3_ma0 200 $B --steps 20 --parity-seconds 0 --max-ahead 0 && \
            run q_c3_ma2 200 $B --steps 20 --parity-seconds 0 --max-ahead 2 && run q_c3_blit 200 $B --steps 20 --parity-seconds 0 --download-engine blit && \
