@@ -46,15 +46,6 @@ int fail(int code, const char* fmt, ...) {
   return code;
 }
 
-// The main10 path (cfg.bit_depth 10) covers the sub-pel refinement batch (fme_refine*, the pixel
-// kernel of fme_px.hip) and NN_pred; the 8-bit-only kernels refuse a 10-bit context.
-#define NEED_8BIT(c, fn)                                                                          \
-  do {                                                                                            \
-    if ((c)->cfg.bit_depth != 8)                                                                  \
-      return fail(FME_E_UNSUPPORTED, "%s: bit_depth %d (the 10-bit path covers fme_refine* and "  \
-                  "fme_nn_pred_single)", fn, (c)->cfg.bit_depth);                                 \
-  } while (0)
-
 #define HIP_TRY(expr)                                                                       \
   do {                                                                                      \
     hipError_t _e = (expr);                                                                 \
@@ -1152,7 +1143,6 @@ int fme_refine_status(fme_ctx* c) {
 static int tz_run(fme_ctx* c, fme_job* d_jobs, const fme_tz_ext* d_ext, uint32_t* d_sad, int n, void* stream,
                   int16_t* d_emi, uint32_t* d_nn_in = nullptr, int ext_stride = (int)sizeof(fme_tz_ext)) {
   if (!c || (n > 0 && (!d_jobs || !d_ext))) return fail(FME_E_INVALID, "fme_integer_search_device: null argument");
-  NEED_8BIT(c, "fme_integer_search");
   if (n < 0) return fail(FME_E_INVALID, "fme_integer_search_device: n = %d", n);
   if (n == 0) return FME_OK;
   HIP_TRY(hipSetDevice(c->device));
@@ -1230,7 +1220,7 @@ static int tz_run(fme_ctx* c, fme_job* d_jobs, const fme_tz_ext* d_ext, uint32_t
       npic = i + 1;
     }
   const long long np = (long long)npic * cw * ch;
-  if (FME_TZ_STAGE && np > 0 && np <= (1LL << 20)) {
+  if (FME_TZ_STAGE && c->cfg.bit_depth == 8 && np > 0 && np <= (1LL << 20)) {   // (10-bit: the unstaged kernels)
     const size_t words = 8 + 12 * (size_t)np;
     if (c->d_tzp.cap < words || c->d_tzp_perm.cap < (size_t)n) {
       rc = drain_ctx(c);   // no launch of an earlier call still reads the old buffers
@@ -1261,9 +1251,9 @@ static int tz_run(fme_ctx* c, fme_job* d_jobs, const fme_tz_ext* d_ext, uint32_t
     HIP_TRY(hipEventRecord(c->ev_fork, s));
     HIP_TRY(hipStreamWaitEvent(c->aux, c->ev_fork, 0));
     HIP_TRY(hipStreamWaitEvent(c->aux2, c->ev_fork, 0));
-    HIP_TRY(launch_tz_wave(ta, sc, 0, keyed, c->aux));
-    HIP_TRY(launch_tz_wave(ta, sc, 1, keyed, c->aux2));
-    HIP_TRY(launch_tz_wave(ta, sc, 2, keyed, s));
+    HIP_TRY(launch_tz_wave(ta, sc, 0, keyed, c->cfg.bit_depth, c->aux));
+    HIP_TRY(launch_tz_wave(ta, sc, 1, keyed, c->cfg.bit_depth, c->aux2));
+    HIP_TRY(launch_tz_wave(ta, sc, 2, keyed, c->cfg.bit_depth, s));
   }
   HIP_TRY(hipEventRecord(c->ev_join, c->aux));
   HIP_TRY(hipEventRecord(c->ev_join2, c->aux2));
@@ -1277,7 +1267,6 @@ static int tz_run(fme_ctx* c, fme_job* d_jobs, const fme_tz_ext* d_ext, uint32_t
 static int tz_run_host(fme_ctx* c, fme_job* jobs, const fme_tz_ext* ext, uint32_t* sad, int n, void* stream,
                        int16_t* emi, uint32_t* nn_in = nullptr, int ext_stride = (int)sizeof(fme_tz_ext)) {
   if (!c || (n > 0 && (!jobs || !ext))) return fail(FME_E_INVALID, "fme_integer_search: null argument");
-  NEED_8BIT(c, "fme_integer_search");
   if (n <= 0) return n == 0 ? FME_OK : fail(FME_E_INVALID, "fme_integer_search: n = %d", n);
   HIP_TRY(hipSetDevice(c->device));
   hipStream_t s = static_cast<hipStream_t>(stream);
@@ -1365,7 +1354,7 @@ static int tz_by_level(fme_ctx* c, std::vector<fme_job>& jobs, std::vector<fme_t
   ta.ext_stride = (int)sizeof(fme_tz_ext);
   ta.emi_mv = c->d_tz_emi.p;
   const TzChain ch{c->d_ch_i32.p, max_level + 1};
-  HIP_TRY(launch_tz_levels(ta, ch, off.data(), s));
+  HIP_TRY(launch_tz_levels(ta, ch, off.data(), c->cfg.bit_depth, s));
   std::vector<int16_t> lemi((size_t)2 * nu);
   HIP_TRY(hipMemcpyAsync(lj.data(), c->d_jobs.p, (size_t)nu * sizeof(fme_job), hipMemcpyDeviceToHost, s));
   HIP_TRY(hipMemcpyAsync(lemi.data(), c->d_tz_emi.p, (size_t)2 * nu * sizeof(int16_t), hipMemcpyDeviceToHost, s));
@@ -2074,7 +2063,6 @@ extern "C" {
 // costs[(i * FME_MAX_REFS + k) * 2 + m]; 0xFFFFFFFF for k >= num_refs or m >= n_cand[k].
 int fme_template_costs(fme_ctx* c, const fme_pu_req* reqs, uint32_t* costs, int n, void* stream) {
   if (!c || (n > 0 && (!reqs || !costs))) return fail(FME_E_INVALID, "fme_template_costs: null argument");
-  NEED_8BIT(c, "fme_template_costs");
   if (n <= 0) return n == 0 ? FME_OK : fail(FME_E_INVALID, "fme_template_costs: n = %d", n);
   HIP_TRY(hipSetDevice(c->device));
   hipStream_t s = static_cast<hipStream_t>(stream);
@@ -2106,7 +2094,7 @@ int fme_template_costs(fme_ctx* c, const fme_pu_req* reqs, uint32_t* costs, int 
   HIP_TRY(c->d_amvp.reserve(tasks.size()));
   HIP_TRY(c->d_amvp_sad.reserve(tasks.size()));
   HIP_TRY(hipMemcpyAsync(c->d_amvp.p, tasks.data(), tasks.size() * sizeof(AmvpTask), hipMemcpyHostToDevice, s));
-  AmvpArgs aa{c->d_amvp.p, c->d_pics.p, c->d_amvp_sad.p, (int32_t)tasks.size()};
+  AmvpArgs aa{c->d_amvp.p, c->d_pics.p, c->d_amvp_sad.p, (int32_t)tasks.size(), c->cfg.bit_depth};
   HIP_TRY(launch_amvp_sad(aa, s));
   HIP_TRY(hipMemcpyAsync(tsad.data(), c->d_amvp_sad.p, tasks.size() * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
   HIP_TRY(hipStreamSynchronize(s));
@@ -2122,7 +2110,6 @@ int fme_template_costs(fme_ctx* c, const fme_pu_req* reqs, uint32_t* costs, int 
 int fme_build_bipred_keys(fme_ctx* c, const fme_bikey_req* reqs, int n, size_t key_count, void* stream) {
   static_assert(sizeof(fme_bikey_req) == sizeof(BiKeyTask), "fme_bikey_req is the kernel's task record");
   if (!c || (n > 0 && !reqs)) return fail(FME_E_INVALID, "fme_build_bipred_keys: null argument");
-  NEED_8BIT(c, "fme_build_bipred_keys");
   if (n < 0) return fail(FME_E_INVALID, "fme_build_bipred_keys: n = %d", n);
   HIP_TRY(hipSetDevice(c->device));
   hipStream_t s = static_cast<hipStream_t>(stream);
@@ -2144,7 +2131,7 @@ int fme_build_bipred_keys(fme_ctx* c, const fme_bikey_req* reqs, int n, size_t k
   if (n == 0) return hipStreamSynchronize(s) == hipSuccess ? FME_OK : fail(FME_E_DEVICE, "fme_build_bipred_keys: sync");
   HIP_TRY(c->d_bikey.reserve((size_t)n));
   HIP_TRY(hipMemcpyAsync(c->d_bikey.p, reqs, (size_t)n * sizeof(BiKeyTask), hipMemcpyHostToDevice, s));
-  BiKeyArgs ka{c->d_bikey.p, c->d_pics.p, c->d_keys.p, (int32_t)n, nullptr, (int64_t)key_count};
+  BiKeyArgs ka{c->d_bikey.p, c->d_pics.p, c->d_keys.p, (int32_t)n, nullptr, (int64_t)key_count, c->cfg.bit_depth};
   HIP_TRY(launch_bi_key(ka, s));
   HIP_TRY(hipStreamSynchronize(s));
   return FME_OK;
@@ -2155,7 +2142,6 @@ int fme_build_bipred_keys(fme_ctx* c, const fme_bikey_req* reqs, int n, size_t k
 // counted, and every later batch whose jobs read keys is rejected until keys are built again.
 int fme_build_bipred_keys_device(fme_ctx* c, const fme_bikey_req* d_reqs, int n, size_t key_count, void* stream) {
   if (!c || (n > 0 && !d_reqs)) return fail(FME_E_INVALID, "fme_build_bipred_keys_device: null argument");
-  NEED_8BIT(c, "fme_build_bipred_keys_device");
   if (n < 0) return fail(FME_E_INVALID, "fme_build_bipred_keys_device: n = %d", n);
   HIP_TRY(hipSetDevice(c->device));
   hipStream_t s = static_cast<hipStream_t>(stream);
@@ -2167,7 +2153,7 @@ int fme_build_bipred_keys_device(fme_ctx* c, const fme_bikey_req* d_reqs, int n,
   HIP_TRY(hipMemsetAsync(c->d_key_invalid.p, 0, sizeof(int32_t), s));
   if (n == 0) return FME_OK;
   BiKeyArgs ka{reinterpret_cast<const BiKeyTask*>(d_reqs), c->d_pics.p, c->d_keys.p, (int32_t)n,
-               c->d_key_invalid.p, (int64_t)key_count};
+               c->d_key_invalid.p, (int64_t)key_count, c->cfg.bit_depth};
   HIP_TRY(launch_bi_key(ka, s));
   return FME_OK;
 }
@@ -2239,7 +2225,7 @@ static int tz_levels_device(fme_ctx* c, const fme_job* jobs, const fme_tz_ext* e
     ta.ext_stride = (int)sizeof(fme_tz_ext);
     ta.emi_mv = c->d_tz_emi.p;
     const TzChain ch{c->d_ch_i32.p, max_level + 1};
-    HIP_TRY(launch_tz_levels(ta, ch, off.data(), s));
+    HIP_TRY(launch_tz_levels(ta, ch, off.data(), c->cfg.bit_depth, s));
   }
   // the searched jobs back in request order for the sub-pel pass, on the device
   HIP_TRY(launch_gather_jobs(c->d_pi_jobs.p, nullptr, c->d_pi_idx.p + nj, c->d_jobs.p, nullptr, nj, s));
@@ -2288,7 +2274,6 @@ int fme_pred_inter_reset(fme_ctx* c) {
 //   4. xCheckBestMVP and the reference choice on the host.
 int fme_pred_inter_p(fme_ctx* c, const fme_pu_req* reqs, fme_pu_res* res, int n, void* stream) {
   if (!c || (n > 0 && (!reqs || !res))) return fail(FME_E_INVALID, "fme_pred_inter_p: null argument");
-  NEED_8BIT(c, "fme_pred_inter_p");
   if (n <= 0) return n == 0 ? FME_OK : fail(FME_E_INVALID, "fme_pred_inter_p: n = %d", n);
   HIP_TRY(hipSetDevice(c->device));
   hipStream_t s = static_cast<hipStream_t>(stream);
@@ -2349,7 +2334,7 @@ int fme_pred_inter_p(fme_ctx* c, const fme_pu_req* reqs, fme_pu_res* res, int n,
     HIP_TRY(c->d_amvp.reserve((size_t)ntasks));
     HIP_TRY(c->d_amvp_sad.reserve((size_t)ntasks));
     HIP_TRY(hipMemcpyAsync(c->d_amvp.p, tasks, (size_t)ntasks * sizeof(AmvpTask), hipMemcpyHostToDevice, s));
-    AmvpArgs aa{c->d_amvp.p, c->d_pics.p, c->d_amvp_sad.p, (int32_t)ntasks};
+    AmvpArgs aa{c->d_amvp.p, c->d_pics.p, c->d_amvp_sad.p, (int32_t)ntasks, c->cfg.bit_depth};
     HIP_TRY(launch_amvp_sad(aa, s));
     HIP_TRY(hipMemcpyAsync(c->h_pi_tsad.p, c->d_amvp_sad.p, (size_t)ntasks * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
     HIP_TRY(hipStreamSynchronize(s));
@@ -2547,7 +2532,6 @@ int fme_pred_inter_p(fme_ctx* c, const fme_pu_req* reqs, fme_pu_res* res, int n,
 
 int fme_pred_inter_b(fme_ctx* c, const fme_pu_req_b* reqs, fme_pu_res_b* res, int n, void* stream) {
   if (!c || (n > 0 && (!reqs || !res))) return fail(FME_E_INVALID, "fme_pred_inter_b: null argument");
-  NEED_8BIT(c, "fme_pred_inter_b");
   if (n <= 0) return n == 0 ? FME_OK : fail(FME_E_INVALID, "fme_pred_inter_b: n = %d", n);
   const int fen = c->cfg.fast_inter_mode;
   HIP_TRY(hipSetDevice(c->device));
@@ -2618,7 +2602,7 @@ int fme_pred_inter_b(fme_ctx* c, const fme_pu_req_b* reqs, fme_pu_res_b* res, in
       HIP_TRY(c->d_amvp.reserve(ntasks));
       HIP_TRY(c->d_amvp_sad.reserve(ntasks));
       HIP_TRY(hipMemcpyAsync(c->d_amvp.p, tasks, ntasks * sizeof(AmvpTask), hipMemcpyHostToDevice, s));
-      AmvpArgs aa{c->d_amvp.p, c->d_pics.p, c->d_amvp_sad.p, (int32_t)ntasks};
+      AmvpArgs aa{c->d_amvp.p, c->d_pics.p, c->d_amvp_sad.p, (int32_t)ntasks, c->cfg.bit_depth};
       HIP_TRY(launch_amvp_sad(aa, s));
       HIP_TRY(hipMemcpyAsync(c->h_pi_tsad.p, c->d_amvp_sad.p, ntasks * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
       HIP_TRY(hipStreamSynchronize(s));
@@ -2994,7 +2978,7 @@ int fme_pred_inter_b(fme_ctx* c, const fme_pu_req_b* reqs, fme_pu_res_b* res, in
     HIP_TRY(c->d_bikey.reserve(keyt.size()));
     HIP_TRY(hipMemcpyAsync(c->d_bikey.p, keyt.data(), keyt.size() * sizeof(BiKeyTask), hipMemcpyHostToDevice, s));
     HIP_TRY(hipMemsetAsync(c->d_key_invalid.p, 0, sizeof(int32_t), s));
-    BiKeyArgs ka{c->d_bikey.p, c->d_pics.p, c->d_keys.p, (int32_t)keyt.size(), nullptr, (int64_t)key_total};
+    BiKeyArgs ka{c->d_bikey.p, c->d_pics.p, c->d_keys.p, (int32_t)keyt.size(), nullptr, (int64_t)key_total, c->cfg.bit_depth};
     HIP_TRY(launch_bi_key(ka, s));
     // the round's bi jobs alone: in call order each sits right after its request's uni jobs, reads
     // the carried NN state there and writes none (TEncSearch.cpp:88-134), so each is refined as an

@@ -90,6 +90,7 @@ struct AmvpArgs {
   const PicDesc* pics;
   uint32_t* sad;
   int32_t n;
+  int32_t bit_depth;          // 8, or 10: uint16 planes (k_amvp_sad<10>)
 };
 hipError_t launch_amvp_sad(const AmvpArgs& a, hipStream_t s);
 
@@ -112,6 +113,7 @@ struct BiKeyArgs {
   int32_t n;
   int32_t* invalid;           // device-resident requests: validated here, rejected ones counted
   int64_t n_keys;             // (then) the key buffer's length
+  int32_t bit_depth;          // 8, or 10: uint16 planes, ClipForBiPredMe to 0..1023 (k_bi_key<10>)
 };
 hipError_t launch_bi_key(const BiKeyArgs& a, hipStream_t s);
 
@@ -213,7 +215,7 @@ struct TzSchedule {
 };
 // keyed: some job of the batch reads a key block (bi-pred): the kernels that hold int16 keys;
 // otherwise the uni-pred form, whose key rows take half the registers
-hipError_t launch_tz_wave(const TzArgs& ta, const TzSchedule& sc, int kid, bool keyed, hipStream_t s);   // prefix in waves
+hipError_t launch_tz_wave(const TzArgs& ta, const TzSchedule& sc, int kid, bool keyed, int bit_depth, hipStream_t s);   // prefix in waves
 // The staged bulk search's groups (fme_tz.hip k_tz_staged): PUs by (unit-shape kernel kid,
 // reference picture, CTU), np = (bound picture ids) * cw * ch groups per kernel.
 struct TzPairs {
@@ -233,7 +235,7 @@ struct TzChain {
   const int32_t* psrc;        // [n]: job whose post-EMI MV is m_integerMv2Nx2N, or -1
   int32_t nlev;
 };
-hipError_t launch_tz_levels(const TzArgs& ta, const TzChain& ch, const int32_t* h_lvl_off, hipStream_t s);
+hipError_t launch_tz_levels(const TzArgs& ta, const TzChain& ch, const int32_t* h_lvl_off, int bit_depth, hipStream_t s);
 
 // Host-side launch helpers (fme_kernels.hip).
 hipError_t launch_classify(const BatchArgs& a, const WorkBufs& w, hipStream_t s);

@@ -499,6 +499,25 @@ __global__ __launch_bounds__(kMcBlock) void k_amvp_sad(AmvpArgs a) {
   if (lane == 0) a.sad[task] = sad;
 }
 
+// Device-resident requests (fme_build_bipred_keys_device, a.invalid set): the host checks' equivalent;
+// a rejected request is counted once (lane 0) and skipped.
+__device__ __forceinline__ bool bi_key_task_ok(const BiKeyArgs& a, const BiKeyTask& t, int lane) {
+  if (!a.invalid) return true;
+  bool shape = false;
+#pragma unroll
+  for (int k = 0; k < kNumClasses; k++) shape |= kClassW[k] == t.w && kClassH[k] == t.h;
+  bool ok = shape && t.org_id < FME_MAX_PICTURES && t.ref_id < FME_MAX_PICTURES && t.key_off >= 0 &&
+            (t.key_off & 3) == 0 && (int64_t)t.key_off + (int64_t)t.w * t.h <= a.n_keys &&
+            (t.clip & ~FME_PU_CLIP_BIPRED) == 0;
+  if (ok) {
+    const PicDesc r = a.pics[t.ref_id], o = a.pics[t.org_id];
+    ok = r.luma && o.luma && r.width == o.width && r.height == o.height && t.x + t.w <= o.width &&
+         t.y + t.h <= o.height;
+  }
+  if (!ok && lane == 0) atomicAdd(a.invalid, 1);
+  return ok;
+}
+
 // xMotionEstimation(bBi) (TEncSearch.cpp:4461-4471): motionCompensation of the other list (luma,
 // uni-pred, 8-bit) and TComYuv::removeHighFreq (TComYuv.cpp:411-455) into the key buffer.  One
 // task per wave: the lanes walk the PU's 4x4 units.
@@ -507,23 +526,7 @@ __global__ __launch_bounds__(kMcBlock) void k_bi_key(BiKeyArgs a) {
   if (task >= a.n) return;   // wave-uniform
   const int lane = (int)(threadIdx.x & 63);
   const BiKeyTask t = a.tasks[task];
-  if (a.invalid) {   // device-resident requests (fme_build_bipred_keys_device): the host checks' equivalent
-    bool shape = false;
-#pragma unroll
-    for (int k = 0; k < kNumClasses; k++) shape |= kClassW[k] == t.w && kClassH[k] == t.h;
-    bool ok = shape && t.org_id < FME_MAX_PICTURES && t.ref_id < FME_MAX_PICTURES && t.key_off >= 0 &&
-              (t.key_off & 3) == 0 && (int64_t)t.key_off + (int64_t)t.w * t.h <= a.n_keys &&
-              (t.clip & ~FME_PU_CLIP_BIPRED) == 0;
-    if (ok) {
-      const PicDesc r = a.pics[t.ref_id], o = a.pics[t.org_id];
-      ok = r.luma && o.luma && r.width == o.width && r.height == o.height && t.x + t.w <= o.width &&
-           t.y + t.h <= o.height;
-    }
-    if (!ok) {
-      if (lane == 0) atomicAdd(a.invalid, 1);
-      return;   // wave-uniform
-    }
-  }
+  if (!bi_key_task_ok(a, t, lane)) return;   // wave-uniform
   const PicDesc ref = a.pics[t.ref_id], org = a.pics[t.org_id];
   int mx = t.mv_x, my = t.mv_y;
   clip_mv(mx, my, ref.width, ref.height, t.cu_x, t.cu_y);
@@ -556,10 +559,84 @@ __global__ __launch_bounds__(kMcBlock) void k_bi_key(BiKeyArgs a) {
   }
 }
 
+// ---- the producers' luma stages at bit depth 10 (uint16 planes; pred10 is k_mc10's uni-pred luma) --
+// xGetTemplateCost's SAD: getDistPart(DF_SAD) at bitDepth 10 sums |d| and shifts the block sum >> 2
+// (xGetSAD*: uiSum >> DISTORTION_PRECISION_ADJUSTMENT(bitDepth - 8), TComRdCost.cpp:370-536).
+__global__ __launch_bounds__(kMcBlock) void k_amvp_sad10(AmvpArgs a) {
+  const int task = (int)(blockIdx.x * (kMcBlock / 64) + (threadIdx.x >> 6));
+  if (task >= a.n) return;   // wave-uniform
+  const int lane = (int)(threadIdx.x & 63);
+  const AmvpTask t = a.tasks[task];
+  const PicDesc ref = a.pics[t.ref_id], org = a.pics[t.org_id];
+  int mx = t.mv_x, my = t.mv_y;
+  clip_mv(mx, my, ref.width, ref.height, t.cu_x, t.cu_y);
+  uint32_t hlo, hhi, vlo, vhi;
+  luma_taps(mx & 3, hlo, hhi);
+  luma_taps(my & 3, vlo, vhi);
+  const Plane16 pl{reinterpret_cast<const uint16_t*>(ref.luma), ref.stride, ref.width, ref.height};
+  const uint16_t* ol = reinterpret_cast<const uint16_t*>(org.luma);
+  const int uxn = t.w >> 2, units = uxn * (t.h >> 2);
+  uint32_t sad = 0;
+  for (int u = lane; u < units; u += 64) {
+    const int x = t.x + 4 * (u % uxn), y = t.y + 4 * (u / uxn);
+    int o[4][4];
+    pred10<8, 4>(pl, x + (mx >> 2), y + (my >> 2), hlo, hhi, vlo, vhi, true, o);
+#pragma unroll
+    for (int r = 0; r < 4; r++) {
+      const gu16c* op = (const gu16c*)(ol + (size_t)(y + r) * org.stride + x);
+#pragma unroll
+      for (int c = 0; c < 4; c++) sad += (uint32_t)abs(o[r][c] - (int)op[c]);
+    }
+  }
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) sad += (uint32_t)__shfl_xor((int)sad, off, 64);
+  if (lane == 0) a.sad[task] = sad >> 2;
+}
+
+// The bi-pred key at bit depth 10: 2 * org - pred (removeHighFreq), ClipBD to 0..1023 with
+// ClipForBiPredMe (TComYuv.cpp:411-455).
+__global__ __launch_bounds__(kMcBlock) void k_bi_key10(BiKeyArgs a) {
+  const int task = (int)(blockIdx.x * (kMcBlock / 64) + (threadIdx.x >> 6));
+  if (task >= a.n) return;   // wave-uniform
+  const int lane = (int)(threadIdx.x & 63);
+  const BiKeyTask t = a.tasks[task];
+  if (!bi_key_task_ok(a, t, lane)) return;   // wave-uniform
+  const PicDesc ref = a.pics[t.ref_id], org = a.pics[t.org_id];
+  int mx = t.mv_x, my = t.mv_y;
+  clip_mv(mx, my, ref.width, ref.height, t.cu_x, t.cu_y);
+  uint32_t hlo, hhi, vlo, vhi;
+  luma_taps(mx & 3, hlo, hhi);
+  luma_taps(my & 3, vlo, vhi);
+  const Plane16 pl{reinterpret_cast<const uint16_t*>(ref.luma), ref.stride, ref.width, ref.height};
+  const uint16_t* ol = reinterpret_cast<const uint16_t*>(org.luma);
+  const int uxn = t.w >> 2, units = uxn * (t.h >> 2);
+  for (int u = lane; u < units; u += 64) {
+    const int ux = u % uxn, uy = u / uxn;
+    const int x = t.x + 4 * ux, y = t.y + 4 * uy;
+    int o[4][4];
+    pred10<8, 4>(pl, x + (mx >> 2), y + (my >> 2), hlo, hhi, vlo, vhi, true, o);
+#pragma unroll
+    for (int r = 0; r < 4; r++) {
+      const gu16c* op = (const gu16c*)(ol + (size_t)(y + r) * org.stride + x);
+      int16_t* kp = a.keys + t.key_off + (size_t)(4 * uy + r) * t.w + 4 * ux;
+      int v[4];
+#pragma unroll
+      for (int c = 0; c < 4; c++) {
+        v[c] = 2 * (int)op[c] - o[r][c];
+        if (t.clip) v[c] = clamp_i(v[c], 0, 1023);
+      }
+      *(uint2*)kp = make_uint2((uint32_t)(uint16_t)v[0] | ((uint32_t)(uint16_t)v[1] << 16),
+                               (uint32_t)(uint16_t)v[2] | ((uint32_t)(uint16_t)v[3] << 16));
+    }
+  }
+}
+
 }  // namespace
 
 hipError_t launch_bi_key(const BiKeyArgs& a, hipStream_t s) {
-  if (a.n > 0) hipLaunchKernelGGL(k_bi_key, dim3((a.n + kMcBlock / 64 - 1) / (kMcBlock / 64)), dim3(kMcBlock), 0, s, a);
+  const dim3 g((a.n + kMcBlock / 64 - 1) / (kMcBlock / 64));
+  if (a.n > 0 && a.bit_depth > 8) hipLaunchKernelGGL(k_bi_key10, g, dim3(kMcBlock), 0, s, a);
+  else if (a.n > 0) hipLaunchKernelGGL(k_bi_key, g, dim3(kMcBlock), 0, s, a);
   return hipGetLastError();
 }
 
@@ -572,7 +649,9 @@ hipError_t launch_mc(const McArgs& a, hipStream_t s) {
 }
 
 hipError_t launch_amvp_sad(const AmvpArgs& a, hipStream_t s) {
-  if (a.n > 0) hipLaunchKernelGGL(k_amvp_sad, dim3((a.n + kMcBlock / 64 - 1) / (kMcBlock / 64)), dim3(kMcBlock), 0, s, a);
+  const dim3 g((a.n + kMcBlock / 64 - 1) / (kMcBlock / 64));
+  if (a.n > 0 && a.bit_depth > 8) hipLaunchKernelGGL(k_amvp_sad10, g, dim3(kMcBlock), 0, s, a);
+  else if (a.n > 0) hipLaunchKernelGGL(k_amvp_sad, g, dim3(kMcBlock), 0, s, a);
   return hipGetLastError();
 }
 

@@ -310,6 +310,68 @@ __device__ __forceinline__ uint32_t unit_part(const uint32_t (&w)[UH][UW / 4 + 1
   return part;
 }
 
+// ---- bit depth 10 (the main10 configurations, InternalBitDepth 10) --------------------------------
+// uint16 planes (strides in samples).  A unit's window row is UW / 2 + 1 dwords of sample pairs from
+// the even column at or left of the candidate; s0 = 1 when the candidate column is odd.
+template <int UW, int UH>
+__device__ __forceinline__ void load_window10(uint32_t (&w)[UH][UW / 2 + 1], uint32_t& s0, const PicDesc& ref,
+                                              int bx, int by, bool sub) {
+  constexpr int ND = UW / 2 + 1;
+  const int xa = bx & ~1;
+  s0 = (uint32_t)(bx - xa);
+  const uint16_t* luma = reinterpret_cast<const uint16_t*>(ref.luma);
+  const bool inside = xa >= 0 && xa + 2 * ND <= ref.width;
+#pragma unroll
+  for (int r = 0; r < UH; r++) {
+    if (sub && (r & 1)) continue;   // FEN: even rows of the PU
+    const uint16_t* row = luma + (size_t)clamp_i(by + r, 0, ref.height - 1) * ref.stride;
+    if (inside) {
+#pragma unroll
+      for (int q = 0; q < ND; q++) w[r][q] = gld32(row + xa + 2 * q);
+    } else {   // the padded picture: columns clamped (TComPicYuv::extendPicBorder)
+      typedef __attribute__((address_space(1))) const uint16_t gu16c;
+#pragma unroll
+      for (int q = 0; q < ND; q++) {
+        const uint32_t a = *(gu16c*)(row + clamp_i(xa + 2 * q, 0, ref.width - 1));
+        const uint32_t b = *(gu16c*)(row + clamp_i(xa + 2 * q + 1, 0, ref.width - 1));
+        w[r][q] = a | (b << 16);
+      }
+    }
+  }
+}
+
+// One unit's share of the bit-depth-10 distortion: SSE sums (d * d) >> 4 per sample
+// (xGetSSE, TComRdCost.cpp:875-1130, DISTORTION_PRECISION_ADJUSTMENT(2 (bitDepth - 8))) as
+// (sum d^2 - sum (d^2 mod 16)) >> 4, with d^2 mod 16 = ((d & 7)^2) & 15; SAD returns the raw sum
+// (<< 1 with FEN subsampling), the block's >> 2 (xGetSAD12/24/48: uiSum >> (bitDepth - 8)) comes
+// after the group sum.  kk: the key as sample pairs (org samples, or the bi-pred int16 key).
+template <int UW, int UH>
+__device__ __forceinline__ uint32_t unit_part10(const uint32_t (&w)[UH][UW / 2 + 1], uint32_t s0,
+                                                const uint32_t (&kk)[UH][UW / 2], bool sad_metric, bool sub) {
+  int sq = 0;
+  uint32_t lo = 0, acc = 0;
+#pragma unroll
+  for (int r = 0; r < UH; r++) {
+    if (sub && (r & 1)) continue;
+#pragma unroll
+    for (int c = 0; c < UW / 2; c++) {
+      const uint32_t pv = s0 ? __builtin_amdgcn_alignbyte(w[r][c + 1], w[r][c], 2u) : w[r][c];
+      const uint32_t dd = pk_sub(kk[r][c], pv);
+      if (sad_metric) {
+        acc = udot2(pk_abs(dd), 0x00010001u, acc);
+      } else {
+        sq = dot2(dd, dd, sq);
+        const uint32_t m = dd & 0x00070007u;
+        typedef uint16_t v2u16 __attribute__((ext_vector_type(2)));
+        const uint32_t f = __builtin_bit_cast(uint32_t, __builtin_bit_cast(v2u16, m) * __builtin_bit_cast(v2u16, m)) & 0x000F000Fu;
+        lo = udot2(f, 0x00010001u, lo);
+      }
+    }
+  }
+  if (sad_metric) return sub ? acc << 1 : acc;
+  return ((uint32_t)sq - lo) >> 4;
+}
+
 // ---- wave-uniform search: one wave per PU ------------------------------------------------------
 // The reference's xTZSearch is a short sequence of candidate LISTS whose points do not depend on
 // each other: the three start points, the first search's diamond rings (dist 1, 2, 4, ... around
@@ -366,7 +428,8 @@ __device__ __forceinline__ uint64_t block_min(uint64_t key) {
 
 // KB: -1 any job; 0 the uni-pred form (no job of the launch reads a key block: the key rows are
 // UW / 4 dwords of bytes, half the registers of the int16 form)
-template <int UW, int UH, int NW = 1, int KB = -1>
+// BD: the luma bit depth (8, or 10: uint16 planes, the key as sample pairs, no staged tile).
+template <int UW, int UH, int NW = 1, int KB = -1, int BD = 8>
 __device__ __forceinline__ void tz_wave(const TzArgs& ta, int jid, const fme_job& j, int PW, int PH, int pred_x,
                                         int pred_y, const TileRef& tile = TileRef{nullptr, 0, 0}) {
   const BatchArgs& a = ta.a;
@@ -387,10 +450,17 @@ __device__ __forceinline__ void tz_wave(const TzArgs& ta, int jid, const fme_job
   const int ox = (int)j.x + ux * UW, oy = (int)j.y + uy * UH;
   constexpr int ND = UW / 4 + 1;
 
-  constexpr int KW = KB == 0 ? UW / 4 : UW / 2;   // key dwords per row
+  constexpr int KW = (KB == 0 && BD == 8) ? UW / 4 : UW / 2;   // key dwords per row
   uint32_t kk[UH][KW];
   int sk2 = 0;
-  if (!kbuf) {
+  if (BD != 8 && !kbuf) {   // 10-bit org samples as pairs
+    const PicDesc org = a.pics[j.org_id];
+    const uint16_t* ol = reinterpret_cast<const uint16_t*>(org.luma);
+#pragma unroll
+    for (int r = 0; r < UH; r++)
+#pragma unroll
+      for (int c = 0; c < KW; c++) kk[r][c] = gld32(ol + (size_t)(oy + r) * org.stride + ox + 2 * c);
+  } else if (!kbuf) {
     const PicDesc org = a.pics[j.org_id];
 #pragma unroll
     for (int r = 0; r < UH; r++) {
@@ -403,7 +473,7 @@ __device__ __forceinline__ void tz_wave(const TzArgs& ta, int jid, const fme_job
 #pragma unroll
       for (int c = UW / 4; c < KW; c++) kk[r][c] = 0;
     }
-  } else if constexpr (KW == UW / 2) {
+  } else if constexpr (KW == UW / 2) {   // bi-pred keys (int16)
     const int16_t* kb = a.keys + (size_t)j.key_offset + (size_t)(uy * UH) * PW + ux * UW;
 #pragma unroll
     for (int r = 0; r < UH; r++)
@@ -424,12 +494,20 @@ __device__ __forceinline__ void tz_wave(const TzArgs& ta, int jid, const fme_job
   auto cost_at = [&](int x, int y, bool v, uint32_t& dist) FME_AI -> uint32_t {
     uint32_t part = 0;
     if (v && real) {
-      uint32_t w[UH][ND];
-      uint32_t s0;
-      load_window<UW, UH>(w, s0, ref, ox + x, oy + y, sub, tile);
-      part = unit_part<UW, UH, KW>(w, s0, kk, sk2, kbuf, sad_metric, sub);
+      if constexpr (BD == 8) {
+        uint32_t w[UH][ND];
+        uint32_t s0;
+        load_window<UW, UH>(w, s0, ref, ox + x, oy + y, sub, tile);
+        part = unit_part<UW, UH, KW>(w, s0, kk, sk2, kbuf, sad_metric, sub);
+      } else {
+        uint32_t w[UH][UW / 2 + 1];
+        uint32_t s0;
+        load_window10<UW, UH>(w, s0, ref, ox + x, oy + y, sub);
+        part = unit_part10<UW, UH>(w, s0, kk, sad_metric, sub);
+      }
     }
-    const uint32_t d = group_sum(part, L);
+    uint32_t d = group_sum(part, L);
+    if (BD != 8 && sad_metric) d >>= BD - 8;   // xGetSAD12/24/48 at bitDepth 10: the block sum >> 2
     dist = v ? d : 0xFFFFFFFFu;
     return v ? d + mv_cost(ml, mv_bits(x, y, 2, j.mvp_x, j.mvp_y)) : 0xFFFFFFFFu;
   };
@@ -819,7 +897,7 @@ __device__ __forceinline__ int tz_entry(const TzSchedule& sc, int kid, int x, in
   return -1;
 }
 
-template <int UW, int UH, int KB>
+template <int UW, int UH, int KB, int BD = 8>
 __global__ __launch_bounds__(kTzNT) __attribute__((amdgpu_waves_per_eu(FME_TZW_WAVES)))
 void k_tz_wave(TzArgs ta, TzSchedule sc, int kid) {
   const int x = (int)blockIdx.x & 7;
@@ -829,7 +907,7 @@ void k_tz_wave(TzArgs ta, TzSchedule sc, int kid) {
   if (q < 0) return;
   const int jid = ta.perm[q];
   const fme_job j = FME_SJOBS ? ta.sjobs[q] : ta.a.jobs[jid];
-  tz_wave<UW, UH, 1, KB>(ta, jid, j, kTzW[c], kTzH[c], tz_ext_at(ta, jid).pred2n_x, tz_ext_at(ta, jid).pred2n_y);
+  tz_wave<UW, UH, 1, KB, BD>(ta, jid, j, kTzW[c], kTzH[c], tz_ext_at(ta, jid).pred2n_x, tz_ext_at(ta, jid).pred2n_y);
 }
 
 // ---- staged bulk search: PUs grouped by (kernel, reference picture, CTU), a group's search area
@@ -984,6 +1062,7 @@ void k_tz_staged(TzArgs ta, TzPairs tp, int kid) {
 #ifndef FME_TZL_WAVES
 #define FME_TZL_WAVES 1   // waves per chain job (A/B: 8 waves 276 ms per P frame, spilling; 1 wave 198 ms)
 #endif
+template <int BD>
 __global__ __launch_bounds__(64 * FME_TZL_WAVES) void k_tz_level(TzArgs ta, TzChain ch, int first) {
   const int q = first + (int)blockIdx.x;
   const int PW = ta.a.jobs[q].w, PH = ta.a.jobs[q].h;   // shapes checked by the host
@@ -996,9 +1075,9 @@ __global__ __launch_bounds__(64 * FME_TZL_WAVES) void k_tz_level(TzArgs ta, TzCh
   }
   const int kid = (PW % 8) ? 0 : ((PH % 8) ? 1 : 2);
   const fme_job j = ta.a.jobs[q];
-  if (kid == 0) tz_wave<4, 8, FME_TZL_WAVES>(ta, q, j, PW, PH, px, py);
-  else if (kid == 1) tz_wave<8, 4, FME_TZL_WAVES>(ta, q, j, PW, PH, px, py);
-  else tz_wave<8, 8, FME_TZL_WAVES>(ta, q, j, PW, PH, px, py);
+  if (kid == 0) tz_wave<4, 8, FME_TZL_WAVES, -1, BD>(ta, q, j, PW, PH, px, py);
+  else if (kid == 1) tz_wave<8, 4, FME_TZL_WAVES, -1, BD>(ta, q, j, PW, PH, px, py);
+  else tz_wave<8, 8, FME_TZL_WAVES, -1, BD>(ta, q, j, PW, PH, px, py);
 }
 
 }  // namespace
@@ -1014,10 +1093,12 @@ extern "C" int fme_debug_tz_counts(unsigned long long* out6, int reset) {
 }
 #endif
 
-hipError_t launch_tz_levels(const TzArgs& ta, const TzChain& ch, const int32_t* h_lvl_off, hipStream_t s) {
+hipError_t launch_tz_levels(const TzArgs& ta, const TzChain& ch, const int32_t* h_lvl_off, int bit_depth, hipStream_t s) {
   for (int lv = 0; lv < ch.nlev; lv++) {
     const int n = h_lvl_off[lv + 1] - h_lvl_off[lv];
-    if (n > 0) hipLaunchKernelGGL(k_tz_level, dim3(n), dim3(64 * FME_TZL_WAVES), 0, s, ta, ch, h_lvl_off[lv]);
+    if (n <= 0) continue;
+    if (bit_depth > 8) hipLaunchKernelGGL(k_tz_level<10>, dim3(n), dim3(64 * FME_TZL_WAVES), 0, s, ta, ch, h_lvl_off[lv]);
+    else hipLaunchKernelGGL(k_tz_level<8>, dim3(n), dim3(64 * FME_TZL_WAVES), 0, s, ta, ch, h_lvl_off[lv]);
   }
   return hipGetLastError();
 }
@@ -1060,7 +1141,7 @@ hipError_t launch_tz_staged(const TzArgs& ta, const TzPairs& tp, int kid, bool k
 }
 
 // Wave-uniform bulk search of kernel kid: sc.prefix in waves (one per PU).
-hipError_t launch_tz_wave(const TzArgs& ta, const TzSchedule& sc, int kid, bool keyed, hipStream_t s) {
+hipError_t launch_tz_wave(const TzArgs& ta, const TzSchedule& sc, int kid, bool keyed, int bit_depth, hipStream_t s) {
   int share = 0;   // the largest per-XCD share of this kernel's PUs (waves)
   for (int x = 0; x < 8; x++) {
     int n = 0;
@@ -1071,7 +1152,11 @@ hipError_t launch_tz_wave(const TzArgs& ta, const TzSchedule& sc, int kid, bool 
   }
   if (share <= 0) return hipSuccess;
   const int blocks = 8 * ((share + kTzNT / 64 - 1) / (kTzNT / 64));
-  if (keyed) {
+  if (bit_depth > 8) {   // one form: the 10-bit key rows are sample pairs either way
+    if (kid == 0) hipLaunchKernelGGL((k_tz_wave<4, 8, -1, 10>), dim3(blocks), dim3(kTzNT), 0, s, ta, sc, 0);
+    else if (kid == 1) hipLaunchKernelGGL((k_tz_wave<8, 4, -1, 10>), dim3(blocks), dim3(kTzNT), 0, s, ta, sc, 1);
+    else hipLaunchKernelGGL((k_tz_wave<8, 8, -1, 10>), dim3(blocks), dim3(kTzNT), 0, s, ta, sc, 2);
+  } else if (keyed) {
     if (kid == 0) hipLaunchKernelGGL((k_tz_wave<4, 8, -1>), dim3(blocks), dim3(kTzNT), 0, s, ta, sc, 0);
     else if (kid == 1) hipLaunchKernelGGL((k_tz_wave<8, 4, -1>), dim3(blocks), dim3(kTzNT), 0, s, ta, sc, 1);
     else hipLaunchKernelGGL((k_tz_wave<8, 8, -1>), dim3(blocks), dim3(kTzNT), 0, s, ta, sc, 2);

@@ -159,9 +159,9 @@ class FmeContext:
 
     def __init__(self, device=0, use_hadamard=1, nn_mode=1, qp=22, fast_inter_mode=1, max_jobs=0,
                  load_nn=True, lib_path=None, net=None, nn_engine=0, bit_depth=8):
-        """bit_depth 10 (the main10 configurations): pictures are uint16 sample planes and the
-        refinement batches run the pixel kernel (fme_px.hip); the other 8-bit-only entry points
-        refuse such a context (FME_E_UNSUPPORTED)."""
+        """bit_depth 10 (the main10 configurations): pictures are uint16 sample planes; every entry
+        point runs at 10 bits (the refinement batches on k_search_lane10, integer search, template
+        costs, bi-pred keys, the producers, motion compensation)."""
         self.lib = load_library(lib_path)
         self.bit_depth = int(bit_depth)
         self.cfg = FmeConfig(self.bit_depth, use_hadamard, nn_mode, qp, fast_inter_mode, max_jobs)

@@ -49,9 +49,10 @@ typedef struct fme_config {
   int32_t bit_depth;        /* internal luma bit depth: 8, or 10 for the main10
                                configurations (cfg/encoder_*_main10.cfg InternalBitDepth 10):
                                pictures are then uint16 sample planes (strides in samples);
-                               the refinement batches (fme_refine*), fme_frac_dif_single and
-                               motion compensation run at 10 bits; integer search, the
-                               producers and bi-pred key builds return FME_E_UNSUPPORTED     */
+                               every entry point runs at 10 bits (refinement, single-call
+                               FracDIF, integer search, template costs, bi-pred keys, the
+                               producers, motion compensation), with TComRdCost's 10-bit
+                               distortion shifts; other depths return FME_E_UNSUPPORTED     */
   int32_t use_hadamard;     /* HadamardME (TAppEncCfg.cpp:760): SATD vs SAD in FracDIF   */
   int32_t nn_mode;          /* 0: standard FracDIF MV (TEncSearch.cpp:4587-4588 variant)
                                1: NN_pred() MV (shipped behaviour, TEncSearch.cpp:4590-4591)

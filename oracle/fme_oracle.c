@@ -57,6 +57,7 @@ static inline int ref_px(const orc_picture* p, int x, int y) {
   return p->luma16 ? p->luma16[(size_t)y * p->stride + x] : p->luma[(size_t)y * p->stride + x];
 }
 static inline int pic_bd(const orc_picture* p) { return p->bd > 8 ? p->bd : 8; }
+static inline int pic_set(const orc_picture* p) { return p->luma != NULL || p->luma16 != NULL; }
 /* headRoom = max(2, IF_INTERNAL_PREC - bitDepth): filterCopy's shift and the filters' headroom
  * (TComInterpolationFilter.cpp:113, 129, 201) - 6 at 8 bits, 4 at 10 */
 static inline int if_headroom(int bd) { return 14 - bd < 2 ? 2 : 14 - bd; }
@@ -1211,10 +1212,15 @@ typedef struct pi_pu {   /* the geometry and slots every xMotionEstimation of on
   int x, y, w, h, cu_x, cu_y, org_id, lambda_id, lossless;
 } pi_pu;
 
-/* motionCompensation's luma part for one list (xPredInterUni, bi = false): 8-bit prediction. */
+/* motionCompensation's luma part for one list (xPredInterUni, bi = false); above 8 bits the
+ * generic quarter-pel predictor at the picture's bit depth (orc_pred_block). */
 static void pi_pred_uni(const orc_ctx* ctx, const pi_pu* g, int ref_id, int mx, int my, int16_t* pred) {
   const orc_picture* ref = &ctx->pics[ref_id];
   mc_clip_mv(&mx, &my, ref->width, ref->height, g->cu_x, g->cu_y);
+  if (pic_bd(ref) > 8) {
+    orc_pred_block(ref, g->x, g->y, g->w, g->h, mx, my, pred);
+    return;
+  }
   mc_pred_blk(ref->luma, ref->stride, ref->width, ref->height, 0, g->x, g->y, g->w, g->h, mx, my, 0, pred, g->w);
 }
 
@@ -1224,9 +1230,10 @@ static uint32_t pi_tmpl(const orc_ctx* ctx, const pi_pu* g, int ref_id, int mx, 
   uint32_t sad = 0;
   for (int y = 0; y < g->h; y++)
     for (int x = 0; x < g->w; x++) {
-      const int d = pred[y * g->w + x] - org->luma[(size_t)(g->y + y) * org->stride + g->x + x];
+      const int d = pred[y * g->w + x] - ref_px(org, g->x + x, g->y + y);
       sad += (uint32_t)(d < 0 ? -d : d);
     }
+  sad >>= pic_bd(org) - 8;   /* xGetSAD*: uiSum >> DISTORTION_PRECISION_ADJUSTMENT(bitDepth - 8) */
   const double ml = ctx->mlambda[g->lambda_id];
   return (uint32_t)((double)sad + ((double)pi_mvp_idx_bits(m, 2) * ml) / 65536.0);
 }
@@ -1350,7 +1357,7 @@ int orc_pred_inter_p(orc_ctx* ctx, const fme_pu_req* reqs, fme_pu_res* res, int 
     fme_pu_res* o = &res[i];
     memset(o, 0, sizeof(*o));
     if (q->num_refs < 1 || q->num_refs > FME_MAX_REFS || q->org_id >= FME_MAX_PICTURES ||
-        !ctx->pics[q->org_id].luma || q->lambda_id >= FME_MAX_LAMBDAS) {
+        !pic_set(&ctx->pics[q->org_id]) || q->lambda_id >= FME_MAX_LAMBDAS) {
       free(pred);
       return FME_E_INVALID;
     }
@@ -1358,7 +1365,7 @@ int orc_pred_inter_p(orc_ctx* ctx, const fme_pu_req* reqs, fme_pu_res* res, int 
     const int range = q->search_range ? q->search_range : 64;
     uint32_t best_cost = 0xFFFFFFFFu;   /* uiCost[0] = max */
     for (int k = 0; k < q->num_refs; k++) {
-      if (q->ref_id[k] >= FME_MAX_PICTURES || !ctx->pics[q->ref_id[k]].luma || q->n_cand[k] < 1 || q->n_cand[k] > 2) {
+      if (q->ref_id[k] >= FME_MAX_PICTURES || !pic_set(&ctx->pics[q->ref_id[k]]) || q->n_cand[k] < 1 || q->n_cand[k] > 2) {
         free(pred);
         return FME_E_INVALID;
       }
@@ -1426,7 +1433,7 @@ static void pi_blk_bits_b(int part_size, int part_idx, int last_mode, uint32_t o
 
 /* xMotionEstimation(bBi)'s key (TEncSearch.cpp:4461-4471): the other list's uni-pred luma
  * prediction (motionCompensation) at (mvx, mvy), key = 2 * org - pred (removeHighFreq, TComYuv.cpp
- * :411-455), clipped to 8 bits with ClipForBiPredMe.  key: w*h. */
+ * :411-455), clipped to the bit depth with ClipForBiPredMe.  key: w*h. */
 void orc_bi_key(const orc_ctx* ctx, int org_id, int ref_id, int x, int y, int w, int h, int cu_x, int cu_y,
                 int mvx, int mvy, int clip, int16_t* key) {
   int16_t pred[64 * 64];
@@ -1435,8 +1442,8 @@ void orc_bi_key(const orc_ctx* ctx, int org_id, int ref_id, int x, int y, int w,
   const orc_picture* org = &ctx->pics[org_id];
   for (int r = 0; r < h; r++)
     for (int c = 0; c < w; c++) {
-      int v = 2 * org->luma[(size_t)(y + r) * org->stride + x + c] - pred[r * w + c];
-      if (clip) v = clampi(v, 0, 255);
+      int v = 2 * ref_px(org, x + c, y + r) - pred[r * w + c];
+      if (clip) v = clampi(v, 0, (1 << pic_bd(org)) - 1);   /* ClipBD */
       key[r * w + c] = (int16_t)v;
     }
 }
@@ -1457,7 +1464,7 @@ int orc_pred_inter_b(orc_ctx* ctx, const fme_pu_req_b* reqs, fme_pu_res_b* res, 
     const fme_pu_req_b* q = &reqs[i];
     fme_pu_res_b* o = &res[i];
     memset(o, 0, sizeof(*o));
-    if (q->org_id >= FME_MAX_PICTURES || !ctx->pics[q->org_id].luma || q->lambda_id >= FME_MAX_LAMBDAS ||
+    if (q->org_id >= FME_MAX_PICTURES || !pic_set(&ctx->pics[q->org_id]) || q->lambda_id >= FME_MAX_LAMBDAS ||
         q->part_size > FME_PART_nRx2N || q->part_idx >= pi_num_parts(q->part_size) ||
         (q->flags & ~(FME_PU_LOSSLESS | FME_PU_FAST_ME_GEN_B | FME_PU_CLIP_BIPRED | FME_PU_MVD_L1_ZERO))) {
       rc = FME_E_INVALID;
@@ -1466,7 +1473,7 @@ int orc_pred_inter_b(orc_ctx* ctx, const fme_pu_req_b* reqs, fme_pu_res_b* res, 
     for (int l = 0; l < 2 && !rc; l++) {
       if (q->num_refs[l] < 1 || q->num_refs[l] > FME_MAX_REFS) rc = FME_E_INVALID;
       for (int k = 0; k < q->num_refs[l] && !rc; k++)
-        if (q->ref_id[l][k] >= FME_MAX_PICTURES || !ctx->pics[q->ref_id[l][k]].luma || q->n_cand[l][k] < 1 ||
+        if (q->ref_id[l][k] >= FME_MAX_PICTURES || !pic_set(&ctx->pics[q->ref_id[l][k]]) || q->n_cand[l][k] < 1 ||
             q->n_cand[l][k] > 2 || (l == 1 && q->l1_to_l0[k] >= q->num_refs[0]))
           rc = FME_E_INVALID;
     }

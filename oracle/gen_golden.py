@@ -206,16 +206,25 @@ def build_mc_case(name, seed, width, height, bi_frac, mv_amp, identical_frac, ke
     print(f"{path}: {len(jobs)} PUs, {nbi} bi-pred, {len(set(zip(jobs['w'], jobs['h'])))} PU shapes")
 
 
-def build_tz_case(name, seed, width, height, calls, fen, search_range, bipred, mvp_noise):
-    """Integer motion estimation (xTZSearch / xPatternSearch) from _ref; the oracle must agree."""
+def tz_pictures(width, height, seed, bit_depth):
+    """The integer-search fixtures' five pictures: 8-bit, or the same field at bit depth 10 (main10)."""
+    if bit_depth > 8:
+        return {i: synth.synth_luma_hbd(width, height, i, bit_depth=bit_depth, seed=seed) for i in range(5)}
+    return {i: synth.synth_luma(width, height, i, seed=seed) for i in range(5)}
+
+
+def build_tz_case(name, seed, width, height, calls, fen, search_range, bipred, mvp_noise, bit_depth=8):
+    """Integer motion estimation (xTZSearch / xPatternSearch) from _ref; the oracle must agree.
+    bit_depth 10: 16-bit pictures, the distortions of TComRdCost at bitDepth 10 (SSE (d * d) >> 4 per
+    sample, SAD >> 2 per block)."""
     rng = np.random.default_rng(seed)
-    pics = {i: synth.synth_luma(width, height, i, seed=seed) for i in range(5)}
+    pics = tz_pictures(width, height, seed, bit_depth)
     lambdas = np.array(synth.LDP_LAMBDA[22], dtype=np.float64)
     jobs, ext = synth.make_tz_jobs(rng, width, height, calls, 4, [0, 1, 2, 3], [0, 1, 2, 3], bipred_frac=bipred,
                                    search_range=search_range, mvp_noise=mvp_noise)
     keys = synth.make_bipred_keys(rng, jobs, pics)
-    ref = Reference(fast_inter_mode=fen)
-    orc = Oracle(fast_inter_mode=fen)
+    ref = Reference(fast_inter_mode=fen, bit_depth=bit_depth)
+    orc = Oracle(fast_inter_mode=fen, bit_depth=bit_depth)
     for eng in (ref, orc):
         for k, v in pics.items():
             eng.set_picture(k, v)
@@ -230,13 +239,14 @@ def build_tz_case(name, seed, width, height, calls, fen, search_range, bipred, m
     path = os.path.join(OUT, f"{name}.npz")
     np.savez_compressed(path, pictures=np.stack([pics[i] for i in range(5)]), lambdas=lambdas, keys=keys,
                         jobs=jobs, ext=ext, mv_x=out_r["mv_x"], mv_y=out_r["mv_y"], sad=sad_r,
-                        config=np.array([fen, search_range], dtype=np.int32))
+                        config=np.array([fen, search_range], dtype=np.int32),
+                        **({"bit_depth": np.array([bit_depth], np.int32)} if bit_depth != 8 else {}))
     far = np.abs(out_r["mv_x"] * 4 - jobs["mvp_x"]) + np.abs(out_r["mv_y"] * 4 - jobs["mvp_y"])
     print(f"{path}: {len(jobs)} jobs, {int((jobs['flags'] & JOB_BIPRED != 0).sum())} bi-pred, "
           f"{int((ext['flags'] != 0).sum())} with a 2Nx2N start, {int((far > 4 * 20).sum())} ending > 20 px from the predictor")
 
 
-def build_tz2_case(name, seed, width, height, calls, fen, search_range, bipred, mvp_noise, mode):
+def build_tz2_case(name, seed, width, height, calls, fen, search_range, bipred, mvp_noise, mode, bit_depth=8):
     """The other FastSearch settings (fme_tz_ext2): FastSearch 0 (FME_TZ_FULL, xPatternSearch for every
     job) or 3 (FME_TZ_ENHANCED, xTZSearch with bExtendedSettings and the neighbour predictors
     m_acMvPredictors) from _ref; the oracle must agree.  The predictors: near the AMVP predictor, some
@@ -244,7 +254,7 @@ def build_tz2_case(name, seed, width, height, calls, fen, search_range, bipred, 
     conditions both ways)."""
     from nnfme.abi import TZ_EXT2_DTYPE
     rng = np.random.default_rng(seed)
-    pics = {i: synth.synth_luma(width, height, i, seed=seed) for i in range(5)}
+    pics = tz_pictures(width, height, seed, bit_depth)
     lambdas = np.array(synth.LDP_LAMBDA[22], dtype=np.float64)
     jobs, ext = synth.make_tz_jobs(rng, width, height, calls, 4, [0, 1, 2, 3], [0, 1, 2, 3], bipred_frac=bipred,
                                    search_range=search_range, mvp_noise=mvp_noise)
@@ -261,8 +271,8 @@ def build_tz2_case(name, seed, width, height, calls, fen, search_range, bipred, 
         far = rng.integers(-4 * 3 * search_range, 4 * 3 * search_range + 1, (n, 3))
         v = np.where(kind == 0, base, np.where(kind == 1, 0, np.where(kind == 2, near, far)))
         ext2["preds"][:, :, c] = np.clip(v, -32768, 32767)
-    ref = Reference(fast_inter_mode=fen)
-    orc = Oracle(fast_inter_mode=fen)
+    ref = Reference(fast_inter_mode=fen, bit_depth=bit_depth)
+    orc = Oracle(fast_inter_mode=fen, bit_depth=bit_depth)
     for eng in (ref, orc):
         for k, v in pics.items():
             eng.set_picture(k, v)
@@ -280,7 +290,8 @@ def build_tz2_case(name, seed, width, height, calls, fen, search_range, bipred, 
     path = os.path.join(OUT, f"{name}.npz")
     np.savez_compressed(path, pictures=np.stack([pics[i] for i in range(5)]), lambdas=lambdas, keys=keys,
                         jobs=jobs, ext=ext2, mv_x=out_r["mv_x"], mv_y=out_r["mv_y"], sad=sad_r,
-                        config=np.array([fen, search_range], dtype=np.int32))
+                        config=np.array([fen, search_range], dtype=np.int32),
+                        **({"bit_depth": np.array([bit_depth], np.int32)} if bit_depth != 8 else {}))
     print(f"{path}: {n} jobs, {int((~uni).sum())} bi-pred, mode 0x{mode:x}, {differ} MVs differ from FastSearch 1")
 
 
@@ -353,6 +364,24 @@ TZ2_CASES = [
     ("tz_enhanced_far_fen0_sr32", 35, 160, 96, 30, 0, 32, 0.1, 200, 0x08),
 ]
 
+TZ10_CASES = [
+    # bit depth 10 (the main10 configurations): FastSearch 1 / 0 / 3 with SSE and the SAD widths
+    # (FEN 0 and the FEN 1 / 3 row subsampling); (TZ_CASES fields, mode or None, bit depth)
+    ("tz10_ldp_fen1", 51, 160, 96, 40, 1, 64, 0.15, 24, None, 10),
+    ("tz10_far_fen0_sr32", 52, 160, 96, 40, 0, 32, 0.1, 200, None, 10),
+    ("tz10_full_sr8_fen3", 53, 128, 96, 10, 3, 8, 0.1, 24, 0x04, 10),
+    ("tz10_enhanced_fen1", 54, 160, 96, 30, 1, 64, 0.1, 24, 0x08, 10),
+]
+
+
+def build_tz10_case(name, seed, width, height, calls, fen, search_range, bipred, mvp_noise, mode, bit_depth):
+    if mode is None:
+        build_tz_case(name, seed, width, height, calls, fen, search_range, bipred, mvp_noise, bit_depth=bit_depth)
+    else:
+        build_tz2_case(name, seed, width, height, calls, fen, search_range, bipred, mvp_noise, mode,
+                       bit_depth=bit_depth)
+
+
 MC10_CASES = [
     # name, seed, W, H, bi fraction, MV amplitude (quarter-pel), identical-motion fraction, fill
     ("mc10_ldp_uni", 41, 160, 104, 0.0, 40, 0.0, 0),
@@ -423,6 +452,10 @@ def main():
         for c in TZ2_CASES:
             build_tz2_case(*c)
         return 0
+    if "--tz10-only" in sys.argv:
+        for c in TZ10_CASES:
+            build_tz10_case(*c)
+        return 0
     if "--mc10-only" in sys.argv:
         for c in MC10_CASES:
             build_mc10_case(*c)
@@ -447,6 +480,8 @@ def main():
         build_tz_case(*c)
     for c in TZ2_CASES:
         build_tz2_case(*c)
+    for c in TZ10_CASES:
+        build_tz10_case(*c)
     return 0
 
 

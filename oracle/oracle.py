@@ -282,13 +282,18 @@ class Oracle:
             raise RuntimeError(f"orc_mc: invalid job {-1 - rc}")
 
     def pred_block(self, luma, x0, y0, w, h, qx, qy):
-        luma = np.ascontiguousarray(luma, dtype=np.uint8)
+        """orc_pred_block on a uint8 plane, or a uint16 plane at the oracle's bit depth."""
+        wide = np.asarray(luma).dtype == np.uint16
+        luma = np.ascontiguousarray(luma, dtype=np.uint16 if wide else np.uint8)
         out = np.zeros((h, w), dtype=np.int16)
-        # build an orc_picture on the fly: {const uint8_t*, int stride, width, height}
+        # build an orc_picture on the fly: {const uint8_t*, int stride, width, height, luma16, bd}
         class Pic(C.Structure):
             _fields_ = [("luma", C.c_void_p), ("stride", C.c_int), ("width", C.c_int), ("height", C.c_int),
                         ("luma16", C.c_void_p), ("bd", C.c_int)]
-        p = Pic(luma.ctypes.data, luma.shape[1], luma.shape[1], luma.shape[0], None, 8)
+        if wide:
+            p = Pic(None, luma.shape[1], luma.shape[1], luma.shape[0], luma.ctypes.data, self.bit_depth)
+        else:
+            p = Pic(luma.ctypes.data, luma.shape[1], luma.shape[1], luma.shape[0], None, 8)
         self.lib.orc_pred_block(C.byref(p), x0, y0, w, h, qx, qy, _ptr(out))
         return out
 

@@ -445,12 +445,12 @@ int ref_pred_block(void* h, int id, int x0, int y0, int w, int hgt, int qx, int 
   TComInterpolationFilter f;
   std::vector<Pel> dst(w * hgt), tmp(w * (hgt + 7));
   if (fy == 0) {
-    f.filterHor(COMPONENT_Y, src, stride, dst.data(), w, w, hgt, fx, true, CHROMA_400, 8);
+    f.filterHor(COMPONENT_Y, src, stride, dst.data(), w, w, hgt, fx, true, CHROMA_400, c->s.bd);
   } else if (fx == 0) {
-    f.filterVer(COMPONENT_Y, src, stride, dst.data(), w, w, hgt, fy, true, true, CHROMA_400, 8);
+    f.filterVer(COMPONENT_Y, src, stride, dst.data(), w, w, hgt, fy, true, true, CHROMA_400, c->s.bd);
   } else {
-    f.filterHor(COMPONENT_Y, src - 3 * stride, stride, tmp.data(), w, w, hgt + 7, fx, false, CHROMA_400, 8);
-    f.filterVer(COMPONENT_Y, tmp.data() + 3 * w, w, dst.data(), w, w, hgt, fy, false, true, CHROMA_400, 8);
+    f.filterHor(COMPONENT_Y, src - 3 * stride, stride, tmp.data(), w, w, hgt + 7, fx, false, CHROMA_400, c->s.bd);
+    f.filterVer(COMPONENT_Y, tmp.data() + 3 * w, w, dst.data(), w, w, hgt, fy, false, true, CHROMA_400, c->s.bd);
   }
   for (int i = 0; i < w * hgt; i++) out[i] = dst[i];
   return 0;
@@ -698,7 +698,8 @@ int ref_mc16(void* h, const fme_mc_job* jobs, int n, uint16_t* y, int ys, uint16
 
 // xGetTemplateCost (TEncSearch.cpp:4397-4436) over the reference's own pieces: clipMv, xPredInterBlk's
 // luma filter order (uni-prediction, isLast) on the padded TComPicYuv, TComRdCost::getDistPart(DF_SAD)
-// (TComRdCost.cpp:327-349) and calcRdCost(bits, SAD, DF_SAD) (57-102) with the slot's lambda.
+// (TComRdCost.cpp:327-349) and calcRdCost(bits, SAD, DF_SAD) (57-102) with the slot's lambda; at the
+// context's luma bit depth (ref_set_bit_depth: main10 filters with headroom 4, SAD >> 2).
 uint32_t ref_template_cost(void* h, int org_id, int ref_id, int x, int y, int w, int hgt, int cu_x, int cu_y,
                            int mvx, int mvy, int bits, int lambda_id) {
   RefCtx* c = static_cast<RefCtx*>(h);
@@ -720,20 +721,20 @@ uint32_t ref_template_cost(void* h, int org_id, int ref_id, int x, int y, int w,
   std::vector<Pel> dst((size_t)w * hgt);
   const int xf = mvx & 3, yf = mvy & 3;
   if (yf == 0) {
-    f.filterHor(COMPONENT_Y, src, rs, dst.data(), w, w, hgt, xf, true, CHROMA_400, 8);
+    f.filterHor(COMPONENT_Y, src, rs, dst.data(), w, w, hgt, xf, true, CHROMA_400, c->s.bd);
   } else if (xf == 0) {
-    f.filterVer(COMPONENT_Y, src, rs, dst.data(), w, w, hgt, yf, true, true, CHROMA_400, 8);
+    f.filterVer(COMPONENT_Y, src, rs, dst.data(), w, w, hgt, yf, true, true, CHROMA_400, c->s.bd);
   } else {
     std::vector<Pel> tmp((size_t)w * (hgt + NTAPS_LUMA - 1));
     f.filterHor(COMPONENT_Y, src - ((NTAPS_LUMA >> 1) - 1) * rs, rs, tmp.data(), w, w, hgt + NTAPS_LUMA - 1, xf, false,
-                CHROMA_400, 8);
+                CHROMA_400, c->s.bd);
     f.filterVer(COMPONENT_Y, tmp.data() + ((NTAPS_LUMA >> 1) - 1) * w, w, dst.data(), w, w, hgt, yf, false, true,
-                CHROMA_400, 8);
+                CHROMA_400, c->s.bd);
   }
   const int os = org.getStride(COMPONENT_Y);
   const Pel* o = org.getAddr(COMPONENT_Y) + y * os + x;
   c->s.setLambda(c->lambda[lambda_id]);
-  const Distortion sad = c->s.rd.getDistPart(8, dst.data(), w, o, os, w, hgt, COMPONENT_Y, DF_SAD);
+  const Distortion sad = c->s.rd.getDistPart(c->s.bd, dst.data(), w, o, os, w, hgt, COMPONENT_Y, DF_SAD);
   return (UInt)c->s.rd.calcRdCost(bits, sad, DF_SAD);
 }
 
@@ -766,22 +767,22 @@ int ref_bi_key(void* h, int org_id, int ref_id, int x, int y, int w, int hgt, in
   const int ds = other.getStride(COMPONENT_Y);
   const int xf = mvx & 3, yf = mvy & 3;
   if (yf == 0) {
-    f.filterHor(COMPONENT_Y, src, rs, dst, ds, w, hgt, xf, true, CHROMA_400, 8);
+    f.filterHor(COMPONENT_Y, src, rs, dst, ds, w, hgt, xf, true, CHROMA_400, c->s.bd);
   } else if (xf == 0) {
-    f.filterVer(COMPONENT_Y, src, rs, dst, ds, w, hgt, yf, true, true, CHROMA_400, 8);
+    f.filterVer(COMPONENT_Y, src, rs, dst, ds, w, hgt, yf, true, true, CHROMA_400, c->s.bd);
   } else {
     std::vector<Pel> tmp((size_t)w * (hgt + NTAPS_LUMA - 1));
     f.filterHor(COMPONENT_Y, src - ((NTAPS_LUMA >> 1) - 1) * rs, rs, tmp.data(), w, w, hgt + NTAPS_LUMA - 1, xf, false,
-                CHROMA_400, 8);
+                CHROMA_400, c->s.bd);
     f.filterVer(COMPONENT_Y, tmp.data() + ((NTAPS_LUMA >> 1) - 1) * w, w, dst, ds, w, hgt, yf, false, true, CHROMA_400,
-                8);
+                c->s.bd);
   }
   const int os = org.getStride(COMPONENT_Y), ts = temp.getStride(COMPONENT_Y);
   const Pel* o = org.getAddr(COMPONENT_Y) + y * os + x;
   Pel* t = temp.getAddr(COMPONENT_Y);
   for (int r = 0; r < hgt; r++)
     for (int q = 0; q < w; q++) t[r * ts + q] = o[r * os + q];
-  const Int bd[MAX_NUM_CHANNEL_TYPE] = {8, 8};
+  const Int bd[MAX_NUM_CHANNEL_TYPE] = {c->s.bd, c->s.bd};
   temp.removeHighFreq(&other, 0, w, hgt, bd, clip != 0);
   for (int r = 0; r < hgt; r++)
     for (int q = 0; q < w; q++) key[r * w + q] = (int16_t)t[r * ts + q];

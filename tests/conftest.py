@@ -35,7 +35,7 @@ def pytest_collection_modifyitems(config, items):
 def golden_cases():
     """Sub-pel refinement fixtures (fme_job -> fme_result)."""
     return sorted(f[:-4] for f in os.listdir(GOLDEN)
-                  if f.endswith(".npz") and not f.startswith(("mc_", "mc10_", "tz_", "ring_", "main10_")))
+                  if f.endswith(".npz") and not f.startswith(("mc_", "mc10_", "tz_", "tz10_", "ring_", "main10_")))
 
 
 def main10_golden_cases():
@@ -51,7 +51,12 @@ def ring_golden_cases():
 
 def tz_golden_cases():
     """Integer motion-estimation fixtures (fme_job + fme_tz_ext -> integer MV, ruiSAD)."""
-    return sorted(f[:-4] for f in os.listdir(GOLDEN) if f.endswith(".npz") and f.startswith("tz_"))
+    return sorted(f[:-4] for f in os.listdir(GOLDEN) if f.endswith(".npz") and f.startswith(("tz_", "tz10_")))
+
+
+def golden_bit_depth(g):
+    """The fixture's luma bit depth (10 for the main10 fixtures, else 8)."""
+    return int(g["bit_depth"][0]) if "bit_depth" in g else 8
 
 
 def mc_golden_cases():

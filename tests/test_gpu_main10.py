@@ -46,23 +46,16 @@ def test_main10_golden_split_batches_and_device_path(case):
         assert np.array_equal(got[f], g["results"][f]), f
 
 
-def test_main10_entry_points_outside_the_path_refuse():
-    """A 10-bit context refuses the 8-bit-only kernels (integer search) with FME_E_UNSUPPORTED (-4)
-    instead of reading 16-bit planes as bytes; 12 bits is refused at creation.  (Motion
-    compensation runs at 10 bits: tests/test_gpu_mc.py; the single-call FracDIF below.)"""
+def test_main10_context_limits():
+    """12 bits is refused at creation with FME_E_UNSUPPORTED (-4); every entry point runs at 10 bits
+    (integer search: test_gpu_tz.py's tz10_* goldens; producers and template costs:
+    test_main10_producers.py; motion compensation: test_gpu_mc.py); NN_pred is bit-depth independent."""
     from nnfme.runtime import FmeContext, FmeError
-    from nnfme.abi import TZ_EXT_DTYPE
     g = load_golden(main10_golden_cases()[0])
     ctx = _ctx(g)
-    jobs = g["jobs"][:4]
-    ext = np.zeros(4, TZ_EXT_DTYPE)
-    with pytest.raises(FmeError) as e:
-        ctx.integer_search(jobs, ext)
-    assert e.value.code == -4
     with pytest.raises(FmeError) as e:
         FmeContext(bit_depth=12)
     assert e.value.code == -4
-    # the NN_pred single call is bit-depth independent
     cls, _ = ctx.nn_pred_single(np.arange(1, 9, dtype=np.uint32) * 1000, 777, 8, 8)
     assert 0 <= cls < 49
 

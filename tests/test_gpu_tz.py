@@ -5,18 +5,19 @@ the reference harness (oracle/_ref) and the C restatement (orc_integer_search). 
 import numpy as np
 import pytest
 
-from conftest import load_golden, tz_golden_cases
+from conftest import golden_bit_depth, load_golden, tz_golden_cases
 from nnfme import synth
 from nnfme.abi import JOB_BIPRED, TZ_EXT_DTYPE
 
 pytestmark = pytest.mark.gpu
 
 
-def _ctx(g=None, fen=1):
+def _ctx(g=None, fen=1, bit_depth=8):
     from nnfme.runtime import FmeContext
     if g is not None:
         fen = int(g["config"][0])
-    ctx = FmeContext(nn_mode=0, fast_inter_mode=fen)
+        bit_depth = golden_bit_depth(g)
+    ctx = FmeContext(nn_mode=0, fast_inter_mode=fen, bit_depth=bit_depth)
     if g is not None:
         for i, p in enumerate(g["pictures"]):
             ctx.set_picture(i, p)
@@ -114,7 +115,7 @@ def test_tz_device_and_timing():
     assert TZ_EXT_DTYPE.itemsize == 12
 
 
-@pytest.mark.parametrize("case", ["tz_enhanced_fen1", "tz_full_sr8_fen1"])
+@pytest.mark.parametrize("case", ["tz_enhanced_fen1", "tz_full_sr8_fen1", "tz10_enhanced_fen1", "tz10_full_sr8_fen3"])
 def test_tz2_device_and_mode_flags(case):
     """FastSearch 0 / 3 (fme_tz_ext2) through the device entry point; the same jobs through the
     12-byte records search with zero neighbour predictors, as the oracle does."""
@@ -136,7 +137,7 @@ def test_tz2_device_and_mode_flags(case):
     assert np.array_equal(ds.cpu().numpy().view(np.uint32), g["sad"])
     base = np.ascontiguousarray(g["ext"]["base"])
     jobs, sad = ctx.integer_search(g["jobs"], base)
-    orc = Oracle(fast_inter_mode=int(g["config"][0]))
+    orc = Oracle(fast_inter_mode=int(g["config"][0]), bit_depth=golden_bit_depth(g))
     for i, p in enumerate(g["pictures"]):
         orc.set_picture(i, p)
     for i, lam in enumerate(g["lambdas"]):

@@ -5,7 +5,7 @@ import os
 import numpy as np
 import pytest
 
-from conftest import (tz_golden_cases, mc_golden_cases, mc10_golden_cases, mc_inputs, golden_cases, load_golden,
+from conftest import (golden_bit_depth, tz_golden_cases, mc_golden_cases, mc10_golden_cases, mc_inputs, golden_cases, load_golden,
                       main10_golden_cases)
 from nnfme import synth, weights
 from nnfme.abi import PARITY_FIELDS, compare_results
@@ -167,7 +167,7 @@ def test_mc_golden_covers_cases():
 
 def _tz_engine(cls, g):
     fen, _ = (int(v) for v in g["config"])
-    eng = cls(fast_inter_mode=fen)
+    eng = cls(fast_inter_mode=fen, bit_depth=golden_bit_depth(g))
     for i, p in enumerate(g["pictures"]):
         eng.set_picture(i, p)
     for i, lam in enumerate(g["lambdas"]):
