@@ -244,9 +244,6 @@ def parity_leg(rep, wl, net, step, state, seconds, max_jobs=0):
     from nnfme.pipeline import ORG0, REFS
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     from oracle import Reference
-    if rep.kreqs is not None:
-        return {"skipped": "bi-pred keys are built on the device per step; the key parity is "
-                           "tests/test_gpu_c4.py's"}
     nn = wl["nn"]
     ref = Reference(use_hadamard=1, nn_mode=nn, fast_inter_mode=1, bit_depth=wl.get("bit_depth", 8))
     if nn == 1:
@@ -261,6 +258,17 @@ def parity_leg(rep, wl, net, step, state, seconds, max_jobs=0):
         ref.set_lambda(j, rep.lambda_of(f0 + j))
     for slot in range(F + REFS - 1):
         ref.set_picture(slot, pool[(f0 - REFS + slot) % P])
+    keys_s = None
+    if rep.kreqs is not None:
+        # the step's removeHighFreq keys, built on the device inside the timed step
+        # (fme_build_bipred_keys_device), restated on the host from the same bound pictures
+        # (synth.bipred_keys, pinned to orc_bi_key / _ref's ref_bi_key by tests/test_pred_inter_b.py)
+        from nnfme import synth
+        tk = time.perf_counter()
+        pics = {ORG0 + j: pool[(f0 + j) % P] for j in range(F)}
+        pics.update({slot: pool[(f0 - REFS + slot) % P] for slot in range(F + REFS - 1)})
+        ref.set_keys(synth.bipred_keys(rep.kreqs, pics, rep.key_count * F))
+        keys_s = round(time.perf_counter() - tk, 2)
     ref.nn_set_state(state)
     jobs, gpu = rep.jobs, rep.results(step)
     n = len(jobs) if max_jobs <= 0 else min(max_jobs, len(jobs))
@@ -292,6 +300,8 @@ def parity_leg(rep, wl, net, step, state, seconds, max_jobs=0):
            "reference": "oracle/_ref (the reference's TLibCommon -O2, TEncSearch order restated; NN "
                         "restated scalar) with the step's pictures, lambdas and carried NN state",
            "seconds": round(time.perf_counter() - t0, 2)}
+    if keys_s is not None:
+        out["keys"] = f"{len(rep.kreqs)} bi-pred key blocks rebuilt on the host ({keys_s} s, synth.bipred_keys)"
     if nn == 2 and wl.get("engine"):
         out["note"] = ("MFMA engine: FMA-chain rounding, not bit-exact by construction (DESIGN.md §3); "
                        "a mismatch is a near-tie class")
@@ -416,12 +426,19 @@ def mc_leg(dev, stream, reps):
     return out
 
 
-def tz_cpu_rate(jobs, ext, keys, pics, seconds):
+def leg_pictures(n, bd):
+    """The legs' synthetic 1080p pictures: 8-bit, or the same fields at bit depth 10 (main10)."""
+    ts = (7, 6, 5, 4, 0, 3)[:n]
+    return {k: (synth.synth_luma(W, H, t) if bd == 8 else synth.synth_luma_hbd(W, H, t, bit_depth=bd))
+            for k, t in zip(range(n), ts)}
+
+
+def tz_cpu_rate(jobs, ext, keys, pics, seconds, bd=8):
     """oracle/_ref integer search (the reference's TComRdCost distortion, xTZSearch restated) on one
     host core over a bounded prefix of the frame's jobs (HM order)."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     from oracle import Reference
-    ref = Reference(fast_inter_mode=1)
+    ref = Reference(fast_inter_mode=1, bit_depth=bd)
     for k, v in pics.items():
         ref.set_picture(k, v)
     for lid, lam in enumerate(synth.LDP_LAMBDA[QP]):
@@ -435,7 +452,7 @@ def tz_cpu_rate(jobs, ext, keys, pics, seconds):
     return done / (time.perf_counter() - t0), done
 
 
-def tz_roofline(jobs, ext, pics, kernel_ms, sample=20000):
+def tz_roofline(jobs, ext, pics, kernel_ms, sample=20000, bd=8):
     """Work of the frame's integer searches, from the oracle's counters on the first `sample` jobs
     (HM order): points tested per search and distortion samples per point.  Each sample is three
     reference integer ops (SSE: difference, square, accumulate; SAD: difference, absolute value,
@@ -443,7 +460,7 @@ def tz_roofline(jobs, ext, pics, kernel_ms, sample=20000):
     tested point), not by ALU or HBM: the fractions say how far from either roof they sit."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     from oracle import Oracle
-    orc = Oracle(nn_mode=0, fast_inter_mode=1)
+    orc = Oracle(nn_mode=0, fast_inter_mode=1, bit_depth=bd)
     for k, v in pics.items():
         orc.set_picture(k, v)
     for lid, lam in enumerate(synth.LDP_LAMBDA[QP]):
@@ -461,21 +478,22 @@ def tz_roofline(jobs, ext, pics, kernel_ms, sample=20000):
             "reference_ops_per_frame": ops, "sample": f"oracle counters over the first {m} searches"}
 
 
-def tz_leg(dev, stream, reps, cpu_seconds):
+def tz_leg(dev, stream, reps, cpu_seconds, bd=8):
     """Integer motion estimation (xTZSearch / bi-pred xPatternSearch) of one 1080p frame's jobs:
     510 CTUs x 423 calls x 4 refs in HM order, HBM-resident jobs, HIP events around the launches."""
     import torch
     from nnfme.runtime import FmeContext
     rng = np.random.default_rng(2024)
-    pics = {k: synth.synth_luma(W, H, t) for k, t in zip(range(5), (7, 6, 5, 4, 0))}
+    pics = leg_pictures(5, bd)
     jobs, ext = synth.make_tz_jobs(rng, W, H, 423, 4, [0, 1, 2, 3], [0, 1, 2, 3])
     out = {"workload": f"{W}x{H} lowdelay_P QP{QP}: {len(jobs)} integer searches (xTZSearch from the AMVP "
-                       f"predictor, 2Nx2N starts for half the non-2Nx2N PUs, SearchRange 64)"}
+                       f"predictor, 2Nx2N starts for half the non-2Nx2N PUs, SearchRange 64)"
+                       + (f", bit depth {bd}" if bd != 8 else "")}
     if cpu_seconds > 0:
-        rate, done = tz_cpu_rate(jobs, ext, None, pics, cpu_seconds)
+        rate, done = tz_cpu_rate(jobs, ext, None, pics, cpu_seconds, bd)
         out["cpu_baseline"] = {"value": rate, "unit": "PU/s", "cores": 1, "kind": "reference",
                                "sample": f"first {done} jobs of the frame on one host core (oracle/_ref)"}
-    ctx = FmeContext(device=dev.index, nn_mode=0, fast_inter_mode=1, max_jobs=len(jobs))
+    ctx = FmeContext(device=dev.index, nn_mode=0, fast_inter_mode=1, max_jobs=len(jobs), bit_depth=bd)
     for k, v in pics.items():
         ctx.set_picture(k, v)
     for lid, lam in enumerate(synth.LDP_LAMBDA[QP]):
@@ -505,15 +523,17 @@ def tz_leg(dev, stream, reps, cpu_seconds):
     out.update({"kernel_ms": t, "pu_per_s_kernels": len(jobs) / (t / 1e3), "ms_per_frame": wall * 1e3,
                 "pu_per_s": len(jobs) / wall, "kernels": "fme::k_tz_staged<4,8>, <8,4>, <8,8>: a workgroup per (kernel, reference, CTU) group with "
                              "its search area in LDS, one wave per PU, three concurrent launches (+ classify, scatter, "
-                             "k_tz_pair_count / _scan / _scatter)"})
-    out["roofline"] = tz_roofline(jobs, ext, pics, t)
+                             "k_tz_pair_count / _scan / _scatter)" if bd == 8 else
+                             "fme::k_tz_wave<4,8,-1,10>, <8,4,-1,10>, <8,8,-1,10>: one wave per PU on uint16 planes "
+                             "(exact shifted SSE), three concurrent launches (+ classify, scatter)"})
+    out["roofline"] = tz_roofline(jobs, ext, pics, t, bd=bd)
     if "cpu_baseline" in out:
         out["speedup_vs_cpu_1core"] = out["pu_per_s"] / out["cpu_baseline"]["value"]
     ctx.close()
     return out
 
 
-def pred_inter_leg(dev, reps, cpu_seconds):
+def pred_inter_leg(dev, reps, cpu_seconds, bd=8):
     """predInterSearch's P-slice PU / reference loop over one 1080p P frame:
     every PU of a full 64 -> 8 CU quadtree with AMP in xCompressCU order, 4 references, the AMVP
     candidate lists of nnfme.synth.make_pu_requests, NN on (fme_pred_inter_p, host request arrays).
@@ -522,15 +542,17 @@ def pred_inter_leg(dev, reps, cpu_seconds):
     from nnfme import weights
     from nnfme.runtime import FmeContext
     rng = np.random.default_rng(2)
-    pics = {i: synth.synth_luma(W, H, t) for i, t in zip(range(5), (7, 6, 5, 4, 0))}
+    pics = leg_pictures(6, bd)
+    pic5 = pics.pop(5)
     reqs = synth.make_pu_requests(rng, W, H, org_id=4, ref_ids=[0, 1, 2, 3], lambda_id=0, max_depth=3)
     nj = int(reqs["num_refs"].astype(np.int64).sum())
     out = {"workload": f"{W}x{H} P frame QP{QP}: {len(reqs)} PU requests = {nj} xMotionEstimation jobs (full 64->8 "
-                       f"quadtree with AMP, 4 refs, AMVP template choice, xCheckBestMVP, reference choice, NN on)"}
+                       f"quadtree with AMP, 4 refs, AMVP template choice, xCheckBestMVP, reference choice, NN on)"
+                       + (f", bit depth {bd}" if bd != 8 else "")}
     if cpu_seconds > 0:
         sys.path.insert(0, os.path.join(ROOT, "oracle"))
         from oracle import Oracle
-        orc = Oracle(nn_mode=1, qp=QP, fast_inter_mode=1)
+        orc = Oracle(nn_mode=1, qp=QP, fast_inter_mode=1, bit_depth=bd)
         orc.load_nn(weights.load_weights(QP))
         for k, v in pics.items():
             orc.set_picture(k, v)
@@ -543,7 +565,7 @@ def pred_inter_leg(dev, reps, cpu_seconds):
         rate = done / (time.perf_counter() - t0)
         out["cpu_baseline"] = {"value": rate, "unit": "PU requests/s", "cores": 1, "kind": "port",
                                "sample": f"first {done} requests of the frame, sequential (oracle/fme_oracle.c)"}
-    ctx = FmeContext(device=dev.index, nn_mode=1, qp=QP, fast_inter_mode=1, max_jobs=nj)
+    ctx = FmeContext(device=dev.index, nn_mode=1, qp=QP, fast_inter_mode=1, max_jobs=nj, bit_depth=bd)
     for k, v in pics.items():
         ctx.set_picture(k, v)
     for lid, lam in enumerate(synth.LDP_LAMBDA[QP]):
@@ -564,7 +586,7 @@ def pred_inter_leg(dev, reps, cpu_seconds):
     if "cpu_baseline" in out:
         out["speedup_vs_cpu_1core"] = out["requests_per_s"] / out["cpu_baseline"]["value"]
     # the B-slice producer on the same frame: L0 = {t-1, t-2}, L1 = {t+1, t+2} (fme_pred_inter_b)
-    pics[5] = synth.synth_luma(W, H, 3)
+    pics[5] = pic5
     ctx.set_picture(5, pics[5])
     reqs_b = synth.make_pu_requests_b(np.random.default_rng(3), W, H, org_id=4, l0=[(0, 1), (1, 2)],
                                       l1=[(5, -1), (2, -2)], lambda_id=0, max_depth=3)
@@ -986,12 +1008,12 @@ def main():
         if rank == 0 and not args.no_mc and W == 1920 and NN != 2 and BD == 8 else None
     single = drop_in_leg(dev) if rank == 0 and not args.no_mc and W == 1920 and NN == 1 and BD == 8 else None
     pi = None
-    if rank == 0 and not args.no_pi and W == 1920 and world == 1 and NN == 1 and BD == 8:
-        pi = pred_inter_leg(dev, reps=2, cpu_seconds=0.0 if args.no_cpu_baseline else 4.0)
+    if rank == 0 and not args.no_pi and W == 1920 and world == 1 and NN == 1:
+        pi = pred_inter_leg(dev, reps=2, cpu_seconds=0.0 if args.no_cpu_baseline else 4.0, bd=BD)
     tz = None
-    if rank == 0 and not args.no_tz and W == 1920 and world == 1 and NN == 1 and BD == 8:
+    if rank == 0 and not args.no_tz and W == 1920 and world == 1 and NN == 1:
         tz = tz_leg(dev, torch.cuda.current_stream(dev), reps=max(3, args.steps // 4),
-                    cpu_seconds=0.0 if args.no_cpu_baseline else 6.0)
+                    cpu_seconds=0.0 if args.no_cpu_baseline else 6.0, bd=BD)
 
     if rank == 0:
         gj = rep.jobs

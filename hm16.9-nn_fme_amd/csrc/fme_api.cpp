@@ -597,7 +597,10 @@ int fme_load_nn_net(fme_ctx* c, const fme_nn_net* n, const double* params, int c
   if (!bytes) return fail(FME_E_UNSUPPORTED, "fme_load_nn_net: no kernel for this net");
   std::vector<unsigned char> packed(bytes);
   nn_deep_pack(*n, params, packed.data());
-  HIP_TRY(hipDeviceSynchronize());   // a batch in flight may still read the previous net
+  {   // a batch of this context in flight may still read the previous net
+    const int rc = drain_ctx(c);
+    if (rc) return rc;
+  }
   HIP_TRY(c->d_net.reserve(bytes));
   HIP_TRY(hipMemcpy(c->d_net.p, packed.data(), bytes, hipMemcpyHostToDevice));
   c->net = *n;
@@ -650,7 +653,10 @@ int fme_nn_get_state(fme_ctx* c, uint32_t* out12) {
     return FME_OK;
   }
   HIP_TRY(hipSetDevice(c->device));
-  HIP_TRY(hipDeviceSynchronize());
+  {
+    const int rc = drain_ctx(c);   // this context's streams only
+    if (rc) return rc;
+  }
   HIP_TRY(hipMemcpy(out12, c->nn_state.p + 12 * c->state_cur, 12 * sizeof(uint32_t), hipMemcpyDeviceToHost));
   return FME_OK;
 }
@@ -1887,7 +1893,10 @@ int fme_mc_invalid_count(fme_ctx* c) {
   if (!c->d_mc_invalid.p) return 0;
   HIP_TRY(hipSetDevice(c->device));
   int32_t v = 0;
-  HIP_TRY(hipDeviceSynchronize());
+  {
+    const int rc = drain_ctx(c);   // this context's streams only
+    if (rc) return rc;
+  }
   HIP_TRY(hipMemcpy(&v, c->d_mc_invalid.p, sizeof(v), hipMemcpyDeviceToHost));
   return v;
 }
