@@ -1226,7 +1226,8 @@ static int tz_run(fme_ctx* c, fme_job* d_jobs, const fme_tz_ext* d_ext, uint32_t
       npic = i + 1;
     }
   const long long np = (long long)npic * cw * ch;
-  if (FME_TZ_STAGE && c->cfg.bit_depth == 8 && np > 0 && np <= (1LL << 20)) {   // (10-bit: the unstaged kernels)
+  const bool stage = c->cfg.bit_depth == 8 || std::getenv("FME_TZ10_UNSTAGED") == nullptr;   // (A/B switch)
+  if (FME_TZ_STAGE && stage && np > 0 && np <= (1LL << 20)) {
     const size_t words = 8 + 12 * (size_t)np;
     if (c->d_tzp.cap < words || c->d_tzp_perm.cap < (size_t)n) {
       rc = drain_ctx(c);   // no launch of an earlier call still reads the old buffers
@@ -1250,9 +1251,9 @@ static int tz_run(fme_ctx* c, fme_job* d_jobs, const fme_tz_ext* d_ext, uint32_t
     HIP_TRY(hipEventRecord(c->ev_fork, s));
     HIP_TRY(hipStreamWaitEvent(c->aux, c->ev_fork, 0));
     HIP_TRY(hipStreamWaitEvent(c->aux2, c->ev_fork, 0));
-    HIP_TRY(launch_tz_staged(ta, tp, 0, keyed, c->aux));
-    HIP_TRY(launch_tz_staged(ta, tp, 1, keyed, c->aux2));
-    HIP_TRY(launch_tz_staged(ta, tp, 2, keyed, s));
+    HIP_TRY(launch_tz_staged(ta, tp, 0, keyed, c->cfg.bit_depth, c->aux));
+    HIP_TRY(launch_tz_staged(ta, tp, 1, keyed, c->cfg.bit_depth, c->aux2));
+    HIP_TRY(launch_tz_staged(ta, tp, 2, keyed, c->cfg.bit_depth, s));
   } else {
     HIP_TRY(hipEventRecord(c->ev_fork, s));
     HIP_TRY(hipStreamWaitEvent(c->aux, c->ev_fork, 0));

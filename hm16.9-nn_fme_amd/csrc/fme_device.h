@@ -228,7 +228,7 @@ struct TzPairs {
   int32_t np, cw, ch;
 };
 hipError_t launch_tz_pairs(const TzArgs& ta, const TzPairs& tp, const uint8_t* cls, int n, hipStream_t s);
-hipError_t launch_tz_staged(const TzArgs& ta, const TzPairs& tp, int kid, bool keyed, hipStream_t s);
+hipError_t launch_tz_staged(const TzArgs& ta, const TzPairs& tp, int kid, bool keyed, int bit_depth, hipStream_t s);
 // The dependency levels of a producer's m_integerMv2Nx2N chain (fme_tz.hip k_tz_level): jobs in
 // level order, level l = jobs [lvl_off[l], lvl_off[l+1]), one launch per level, back to back.
 struct TzChain {

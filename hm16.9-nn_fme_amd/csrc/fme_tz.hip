@@ -219,8 +219,16 @@ constexpr int kTileWD = (64 + 2 * kTileM + 3 + 8 + 3) / 4;   // dwords per row (
 constexpr int kTileH = 64 + 2 * kTileM;
 struct TileRef {
   const uint32_t* lds;   // null: no staged tile
-  int x0, y0;            // picture coordinates of tile dword 0 of row 0 (x0 a multiple of 4)
+  int x0, y0;            // picture coordinates of tile dword 0 of row 0 (x0 a multiple of 4; 10-bit: of 2)
 };
+// Bit depth 10: the tile holds sample pairs (twice the bytes per sample), so its margin is smaller
+// (two 67 KB tiles per CU); windows outside it are read from global memory as before.
+#ifndef FME_TZS_MARGIN10
+#define FME_TZS_MARGIN10 56
+#endif
+constexpr int kTileM10 = FME_TZS_MARGIN10;
+constexpr int kTileWD10 = (64 + 2 * kTileM10 + 1 + 10 + 1) / 2;   // dwords (sample pairs) per row (x0 even)
+constexpr int kTileH10 = 64 + 2 * kTileM10;
 
 // Reference window of one unit at displacement (bx, by) from its origin: UH rows (FEN: even rows
 // only) of ND dwords from the aligned column, and the byte shift s0 of the first sample.
@@ -315,19 +323,31 @@ __device__ __forceinline__ uint32_t unit_part(const uint32_t (&w)[UH][UW / 4 + 1
 // the even column at or left of the candidate; s0 = 1 when the candidate column is odd.
 template <int UW, int UH>
 __device__ __forceinline__ void load_window10(uint32_t (&w)[UH][UW / 2 + 1], uint32_t& s0, const PicDesc& ref,
-                                              int bx, int by, bool sub) {
+                                              int bx, int by, bool sub, const TileRef& t) {
   constexpr int ND = UW / 2 + 1;
   const int xa = bx & ~1;
   s0 = (uint32_t)(bx - xa);
+  if (t.lds && xa >= t.x0 && xa + 2 * ND <= t.x0 + 2 * kTileWD10 && by >= t.y0 && by + UH <= t.y0 + kTileH10) {
+    const uint32_t* p = t.lds + (by - t.y0) * kTileWD10 + ((xa - t.x0) >> 1);
+#pragma unroll
+    for (int r = 0; r < UH; r++) {
+      if (sub && (r & 1)) continue;
+#pragma unroll
+      for (int q = 0; q < ND; q++) w[r][q] = p[r * kTileWD10 + q];
+    }
+    return;
+  }
   const uint16_t* luma = reinterpret_cast<const uint16_t*>(ref.luma);
   const bool inside = xa >= 0 && xa + 2 * ND <= ref.width;
 #pragma unroll
   for (int r = 0; r < UH; r++) {
     if (sub && (r & 1)) continue;   // FEN: even rows of the PU
     const uint16_t* row = luma + (size_t)clamp_i(by + r, 0, ref.height - 1) * ref.stride;
-    if (inside) {
+    if (inside) {   // one vector load per row (dwordx3, or x4 + x1), as the 8-bit windows
+      typedef uint32_t vec_t __attribute__((ext_vector_type(ND), aligned(4)));
+      const vec_t v = *(__attribute__((address_space(1))) const vec_t*)(row + xa);
 #pragma unroll
-      for (int q = 0; q < ND; q++) w[r][q] = gld32(row + xa + 2 * q);
+      for (int q = 0; q < ND; q++) w[r][q] = v[q];
     } else {   // the padded picture: columns clamped (TComPicYuv::extendPicBorder)
       typedef __attribute__((address_space(1))) const uint16_t gu16c;
 #pragma unroll
@@ -361,10 +381,10 @@ __device__ __forceinline__ uint32_t unit_part10(const uint32_t (&w)[UH][UW / 2 +
         acc = udot2(pk_abs(dd), 0x00010001u, acc);
       } else {
         sq = dot2(dd, dd, sq);
-        const uint32_t m = dd & 0x00070007u;
-        typedef uint16_t v2u16 __attribute__((ext_vector_type(2)));
-        const uint32_t f = __builtin_bit_cast(uint32_t, __builtin_bit_cast(v2u16, m) * __builtin_bit_cast(v2u16, m)) & 0x000F000Fu;
-        lo = udot2(f, 0x00010001u, lo);
+        // d^2 mod 16 by d & 7 (0 1 4 9 0 9 4 1) from a byte table: one v_and_or makes the v_perm
+        // selector (byte 0x0C selects zero), the perm gives the pair of residues as u16 halves
+        const uint32_t sel = (dd & 0x00070007u) | 0x0C000C00u;
+        lo = udot2(__builtin_amdgcn_perm(0x01040900u, 0x09040100u, sel), 0x00010001u, lo);
       }
     }
   }
@@ -502,7 +522,7 @@ __device__ __forceinline__ void tz_wave(const TzArgs& ta, int jid, const fme_job
       } else {
         uint32_t w[UH][UW / 2 + 1];
         uint32_t s0;
-        load_window10<UW, UH>(w, s0, ref, ox + x, oy + y, sub);
+        load_window10<UW, UH>(w, s0, ref, ox + x, oy + y, sub, tile);
         part = unit_part10<UW, UH>(w, s0, kk, sad_metric, sub);
       }
     }
@@ -1013,10 +1033,12 @@ __global__ __launch_bounds__(256) void k_tz_pair_scatter(TzArgs ta, TzPairs tp, 
 // One launch per unit-shape kernel, one workgroup per group (the grid an upper bound): stage the
 // group's tile, then search its PUs, one wave per PU.  (The three kernels' searches in one launch,
 // behind a switch, spilled 282 VGPRs: the allocation is the maximum over the three.)
-template <int UW, int UH, int KB>
+template <int UW, int UH, int KB, int BD = 8>
 __global__ __launch_bounds__(FME_TZS_NT) __attribute__((amdgpu_waves_per_eu(FME_TZS_WAVES)))
 void k_tz_staged(TzArgs ta, TzPairs tp, int kid) {
-  __shared__ uint32_t tile[kTileH * kTileWD];
+  constexpr int TH = BD == 8 ? kTileH : kTileH10, TWD = BD == 8 ? kTileWD : kTileWD10;
+  constexpr int TM = BD == 8 ? kTileM : kTileM10;
+  __shared__ uint32_t tile[TH * TWD];
   if ((int)blockIdx.x >= tp.nseg[kid]) return;
   const int key = tp.seg[tp.nseg[3 + kid] + (int)blockIdx.x];
   const int start = tp.off[key], cnt = tp.cnt[key];
@@ -1027,19 +1049,31 @@ void k_tz_staged(TzArgs ta, TzPairs tp, int kid) {
   const PicDesc ref = ta.a.pics[jb.ref_id];
   int mx = jb.mvp_x, my = jb.mvp_y;
   clip_qpel(mx, my, ref.width, ref.height, e0.cu_x, e0.cu_y);
-  const int x0 = (((int)jb.x & ~63) + round4(mx) - kTileM) & ~3;
-  const int y0 = ((int)jb.y & ~63) + round4(my) - kTileM;
-  for (int i = (int)threadIdx.x; i < kTileH * kTileWD; i += FME_TZS_NT) {
-    const int r = i / kTileWD, q = i - r * kTileWD;
-    const uint8_t* row = ref.luma + (size_t)clamp_i(y0 + r, 0, ref.height - 1) * ref.stride;
-    const int x = x0 + 4 * q;
+  const int x0 = (((int)jb.x & ~63) + round4(mx) - TM) & (BD == 8 ? ~3 : ~1);
+  const int y0 = ((int)jb.y & ~63) + round4(my) - TM;
+  for (int i = (int)threadIdx.x; i < TH * TWD; i += FME_TZS_NT) {
+    const int r = i / TWD, q = i - r * TWD;
     uint32_t v;
-    if (x >= 0 && x + 4 <= ref.width) {
-      v = gld32(row + x);
-    } else {
-      v = 0;
+    if constexpr (BD == 8) {
+      const uint8_t* row = ref.luma + (size_t)clamp_i(y0 + r, 0, ref.height - 1) * ref.stride;
+      const int x = x0 + 4 * q;
+      if (x >= 0 && x + 4 <= ref.width) {
+        v = gld32(row + x);
+      } else {
+        v = 0;
 #pragma unroll
-      for (int k = 0; k < 4; k++) v |= gld8(row + clamp_i(x + k, 0, ref.width - 1)) << (8 * k);
+        for (int k = 0; k < 4; k++) v |= gld8(row + clamp_i(x + k, 0, ref.width - 1)) << (8 * k);
+      }
+    } else {   // sample pairs of the uint16 plane
+      typedef __attribute__((address_space(1))) const uint16_t gu16c;
+      const uint16_t* row = reinterpret_cast<const uint16_t*>(ref.luma) + (size_t)clamp_i(y0 + r, 0, ref.height - 1) * ref.stride;
+      const int x = x0 + 2 * q;
+      if (x >= 0 && x + 2 <= ref.width) {
+        v = gld32(row + x);
+      } else {
+        v = (uint32_t)*(gu16c*)(row + clamp_i(x, 0, ref.width - 1)) |
+            ((uint32_t)*(gu16c*)(row + clamp_i(x + 1, 0, ref.width - 1)) << 16);
+      }
     }
     tile[i] = v;
   }
@@ -1050,7 +1084,7 @@ void k_tz_staged(TzArgs ta, TzPairs tp, int kid) {
   for (int p = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6); p < cnt; p += FME_TZS_NT / 64) {
     const int jid = tp.perm[start + p];
     const fme_job j = ta.a.jobs[jid];
-    tz_wave<UW, UH, 1, KB>(ta, jid, j, j.w, j.h, tz_ext_at(ta, jid).pred2n_x, tz_ext_at(ta, jid).pred2n_y, tr);
+    tz_wave<UW, UH, 1, KB, BD>(ta, jid, j, j.w, j.h, tz_ext_at(ta, jid).pred2n_x, tz_ext_at(ta, jid).pred2n_y, tr);
   }
 }
 
@@ -1126,9 +1160,13 @@ hipError_t launch_tz_pairs(const TzArgs& ta, const TzPairs& tp, const uint8_t* c
   return hipGetLastError();
 }
 
-hipError_t launch_tz_staged(const TzArgs& ta, const TzPairs& tp, int kid, bool keyed, hipStream_t s) {
+hipError_t launch_tz_staged(const TzArgs& ta, const TzPairs& tp, int kid, bool keyed, int bit_depth, hipStream_t s) {
   const dim3 g(tp.np), b(FME_TZS_NT);
-  if (keyed) {
+  if (bit_depth > 8) {
+    if (kid == 0) hipLaunchKernelGGL((k_tz_staged<4, 8, -1, 10>), g, b, 0, s, ta, tp, 0);
+    else if (kid == 1) hipLaunchKernelGGL((k_tz_staged<8, 4, -1, 10>), g, b, 0, s, ta, tp, 1);
+    else hipLaunchKernelGGL((k_tz_staged<8, 8, -1, 10>), g, b, 0, s, ta, tp, 2);
+  } else if (keyed) {
     if (kid == 0) hipLaunchKernelGGL((k_tz_staged<4, 8, -1>), g, b, 0, s, ta, tp, 0);
     else if (kid == 1) hipLaunchKernelGGL((k_tz_staged<8, 4, -1>), g, b, 0, s, ta, tp, 1);
     else hipLaunchKernelGGL((k_tz_staged<8, 8, -1>), g, b, 0, s, ta, tp, 2);
