@@ -183,6 +183,10 @@ struct fme_ctx {
   DevBuf<fme_mc_job> d_mc_jobs;
   DevBuf<uint8_t> d_mc_planes;
   DevBuf<int32_t> d_mc_invalid;
+  // weighted prediction (fme_set_wp): [list][picture][Y, Cb, Cr], uploaded before a launch when changed
+  fme_wp_param h_wp[2][FME_MAX_PICTURES][3] = {};
+  bool wp_init = false, wp_dirty = true;
+  DevBuf<fme_wp_param> d_mc_wp;
   hipEvent_t ev_mc[2] = {nullptr, nullptr};
   bool mc_timed = false;
   // integer search: staging for the host entry point, timing events
@@ -379,7 +383,7 @@ int fme_destroy(fme_ctx* c) {
     if (c->pic_owned[i] && c->pics[i].luma) (void)hipFree(const_cast<uint8_t*>(c->pics[i].luma));
   for (int i = 0; i < FME_MAX_PICTURES; i++)
     if (c->chroma_owned[i]) (void)hipFree(c->chroma_owned[i]);
-  c->d_mc_jobs.release(); c->d_mc_planes.release(); c->d_mc_invalid.release();
+  c->d_mc_jobs.release(); c->d_mc_planes.release(); c->d_mc_invalid.release(); c->d_mc_wp.release();
   c->d_tz_ext.release(); c->d_tz_sad.release(); c->d_tz_nn_in.release();
   c->d_amvp.release(); c->d_amvp_sad.release(); c->d_bikey.release(); c->d_key_invalid.release(); c->d_ch_i32.release(); c->d_tz_emi.release();
   c->h_pi_tasks.release(); c->h_pi_tsad.release(); c->h_pi_jobs.release(); c->h_pi_ext.release();
@@ -1801,7 +1805,7 @@ int fme_search_kernel_of_shape(int width, int height) {
 // ---- motion compensation ---------------------------------------------------------------------
 static const char* mc_job_problem(const fme_ctx* c, const fme_mc_job& j, int width, int height) {
   if (j.w < 4 || j.h < 4 || j.w > 64 || j.h > 64 || (j.w & 3) || (j.h & 3)) return "PU size";
-  if (!(j.flags & (FME_MC_L0 | FME_MC_L1)) || (j.flags & ~(FME_MC_L0 | FME_MC_L1))) return "list flags";
+  if (!(j.flags & (FME_MC_L0 | FME_MC_L1)) || (j.flags & ~(FME_MC_L0 | FME_MC_L1 | FME_MC_WP))) return "list flags";
   if ((int)j.x + j.w > width || (int)j.y + j.h > height) return "PU outside the picture";
   for (int l = 0; l < 2; l++) {
     if (!(j.flags & (1u << l))) continue;
@@ -1818,7 +1822,19 @@ static int mc_launch(fme_ctx* c, const fme_mc_job* d_jobs, int n, uint8_t* y, in
   HIP_TRY(c->d_mc_invalid.reserve(1));
   HIP_TRY(hipMemsetAsync(c->d_mc_invalid.p, 0, sizeof(int32_t), s));
   if (int e = sync_tables(c, s)) return e;
+  if (!c->wp_init) {   // the default weights: 1 << 0, offset 0
+    for (auto& l : c->h_wp)
+      for (auto& p : l)
+        for (auto& q : p) q = fme_wp_param{1, 0, 0, {0, 0, 0}};
+    c->wp_init = true;
+  }
+  if (c->wp_dirty) {   // (pageable source: the runtime stages it before returning)
+    HIP_TRY(c->d_mc_wp.reserve(sizeof(c->h_wp) / sizeof(fme_wp_param)));
+    HIP_TRY(hipMemcpyAsync(c->d_mc_wp.p, c->h_wp, sizeof(c->h_wp), hipMemcpyHostToDevice, s));
+    c->wp_dirty = false;
+  }
   McArgs a{};
+  a.wp = c->d_mc_wp.p;
   a.jobs = d_jobs;
   a.pics = c->d_pics.p;
   a.y = y;
@@ -1900,6 +1916,23 @@ int fme_mc_invalid_count(fme_ctx* c) {
   }
   HIP_TRY(hipMemcpy(&v, c->d_mc_invalid.p, sizeof(v), hipMemcpyDeviceToHost));
   return v;
+}
+
+int fme_set_wp(fme_ctx* c, int list, int ref_id, const fme_wp_param* p) {
+  if (!c || !p) return fail(FME_E_INVALID, "fme_set_wp: null argument");
+  if (list < 0 || list > 1 || ref_id < 0 || ref_id >= FME_MAX_PICTURES)
+    return fail(FME_E_INVALID, "fme_set_wp: list %d reference %d", list, ref_id);
+  for (int k = 0; k < 3; k++)
+    if (p[k].log2_denom > 7) return fail(FME_E_INVALID, "fme_set_wp: log2 denominator %d", (int)p[k].log2_denom);
+  if (!c->wp_init) {
+    for (auto& l : c->h_wp)
+      for (auto& q : l)
+        for (auto& r : q) r = fme_wp_param{1, 0, 0, {0, 0, 0}};
+    c->wp_init = true;
+  }
+  for (int k = 0; k < 3; k++) c->h_wp[list][ref_id][k] = p[k];
+  c->wp_dirty = true;
+  return FME_OK;
 }
 
 int fme_mc_last_ms(fme_ctx* c, float* ms) {

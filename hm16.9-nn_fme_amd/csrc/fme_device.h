@@ -73,6 +73,7 @@ struct McArgs {
   int32_t* invalid;           // count of skipped jobs
   int32_t n, y_stride, c_stride, width, height;
   int32_t bit_depth;          // 8, or 10: y / cb / cr and the pictures hold uint16 samples (strides in samples)
+  const fme_wp_param* wp;     // [2][FME_MAX_PICTURES][3] weighted-prediction parameters (FME_MC_WP jobs)
 };
 hipError_t launch_mc(const McArgs& a, hipStream_t s);
 

@@ -158,7 +158,7 @@ struct UnitWin {
 
 __device__ __forceinline__ bool mc_job_valid(const McArgs& a, const fme_mc_job& j) {
   if (j.w < 4 || j.h < 4 || j.w > 64 || j.h > 64 || (j.w & 3) || (j.h & 3)) return false;
-  if (!(j.flags & (FME_MC_L0 | FME_MC_L1)) || (j.flags & ~(FME_MC_L0 | FME_MC_L1))) return false;
+  if (!(j.flags & (FME_MC_L0 | FME_MC_L1)) || (j.flags & ~(FME_MC_L0 | FME_MC_L1 | FME_MC_WP))) return false;
   if ((int)j.x + j.w > a.width || (int)j.y + j.h > a.height) return false;
   for (int l = 0; l < 2; l++) {
     if (!(j.flags & (1u << l))) continue;
@@ -188,7 +188,45 @@ struct McJobInfo {
   int lix[2], liy[2], lfx[2], lfy[2];   // luma integer offsets / fractions per list
   int cix[2], ciy[2], cfx[2], cfy[2];   // chroma (eighth-pel) per list
   PicDesc pic[2];
+  int wp;                              // FME_MC_WP: weighted prediction of the lists' 14-bit values
+  int ww[2][3], wsh[3], woff[3];       // per component: the lists' weights, shift, (summed) offset
 };
+
+// getWpScaling (TComWeightPrediction.cpp:247-324) for the PU's lists, per component: bi-pred
+// w0 / w1, offset o0 + o1, shift log2Wd + 1 (list 0's denominator); uni-pred w, o, shift log2Wd;
+// offsets scaled by 1 << (bitDepth - 8); addWeightBi / addWeightUni then add shiftNum =
+// max(2, 14 - bitDepth) (:103, :160).
+__device__ __forceinline__ void mc_wp_setup(const McArgs& a, const fme_mc_job& j, const int* lists, int nl,
+                                            McJobInfo& in) {
+  const int bd = a.bit_depth > 8 ? a.bit_depth : 8;
+  const int shift_num = 14 - bd > 2 ? 14 - bd : 2;
+#pragma unroll
+  for (int c = 0; c < 3; c++) {
+    const fme_wp_param p0 = a.wp[(lists[0] * FME_MAX_PICTURES + j.ref_id[lists[0]]) * 3 + c];
+    in.ww[0][c] = p0.weight;
+    if (nl == 2) {
+      const fme_wp_param p1 = a.wp[(FME_MAX_PICTURES + j.ref_id[1]) * 3 + c];
+      in.ww[1][c] = p1.weight;
+      in.woff[c] = (p0.offset + p1.offset) * (1 << (bd - 8));
+      in.wsh[c] = p0.log2_denom + 1 + shift_num;
+    } else {
+      in.ww[1][c] = 0;
+      in.woff[c] = p0.offset * (1 << (bd - 8));
+      in.wsh[c] = p0.log2_denom + shift_num;
+    }
+  }
+}
+
+// weightBidir / weightUnidir (TComWeightPrediction.cpp:46-56) on the 14-bit values p0, p1 (HM's
+// stored intermediates, IF_INTERNAL_OFFS 8192 below the sample scale).  The unit-weight branch of
+// addWeightUni (noWeightUnidir with shiftNum) is the same value: w = 1 << d turns
+// (w (p + 8192) + 2^(d + n - 1)) >> (d + n) into (p + 8192 + 2^(n - 1)) >> n exactly.
+__device__ __forceinline__ int mc_wp_sample(const McJobInfo& in, int c, int p0, int p1, int maxv) {
+  const int sh = in.wsh[c], half = 1 << (sh - 1);
+  if (in.nl == 2)
+    return clamp_i((in.ww[0][c] * (p0 + 8192) + in.ww[1][c] * (p1 + 8192) + half + in.woff[c] * half) >> sh, 0, maxv);
+  return clamp_i(((in.ww[0][c] * (p0 + 8192) + half) >> sh) + in.woff[c], 0, maxv);
+}
 
 #ifndef FME_MC_JOBS
 #define FME_MC_JOBS 8
@@ -216,9 +254,11 @@ __global__ __launch_bounds__(kMcBlock) void k_mc(McArgs a) {
         int nl = 0, lists[2] = {0, 0};
         if (j.flags & FME_MC_L0) lists[nl++] = 0;
         if (j.flags & FME_MC_L1) lists[nl++] = 1;
-        if (nl == 2 && j.ref_id[0] == j.ref_id[1] && j.mv[0][0] == j.mv[1][0] && j.mv[0][1] == j.mv[1][1])
-          nl = 1;   // xCheckIdenticalMotion: same picture, same MV -> xPredInterUni(REF_PIC_LIST_0)
+        in.wp = (j.flags & FME_MC_WP) ? 1 : 0;
+        if (nl == 2 && !in.wp && j.ref_id[0] == j.ref_id[1] && j.mv[0][0] == j.mv[1][0] && j.mv[0][1] == j.mv[1][1])
+          nl = 1;   // xCheckIdenticalMotion (not with WPBiPred): same picture, same MV -> xPredInterUni(REF_PIC_LIST_0)
         in.nl = nl;
+        if (in.wp) mc_wp_setup(a, j, lists, nl, in);
         for (int k = 0; k < nl; k++) {
           const int l = lists[k];
           const PicDesc p = a.pics[j.ref_id[l]];
@@ -261,10 +301,11 @@ __global__ __launch_bounds__(kMcBlock) void k_mc(McArgs a) {
     const McJobInfo& in = info[q];
     const int u = g - first_unit[q];
     const int ux = u % in.ux_n, uy = u / in.ux_n;
-    const bool uni = in.nl == 1;
+    const bool wp = in.wp != 0;
+    const bool uni = in.nl == 1 && !wp;   // weighted prediction filters to the 14-bit values (bi form)
     {   // luma 4x4
       const int x = in.x + 4 * ux, y = in.y + 4 * uy;
-      int acc[4][4], o[4][4];
+      int acc[4][4], o[4][4], q0[4][4];
 #pragma unroll
       for (int k = 0; k < 2; k++) {
         if (k >= in.nl) break;
@@ -279,15 +320,23 @@ __global__ __launch_bounds__(kMcBlock) void k_mc(McArgs a) {
 #pragma unroll
         for (int r = 0; r < 4; r++)
 #pragma unroll
-          for (int c = 0; c < 4; c++) acc[r][c] = k == 0 ? o[r][c] : clamp_i((acc[r][c] + o[r][c] + 16448) >> 7, 0, 255);
+          for (int c = 0; c < 4; c++) {
+            if (k == 0) q0[r][c] = o[r][c];
+            acc[r][c] = k == 0 ? o[r][c] : clamp_i((acc[r][c] + o[r][c] + 16448) >> 7, 0, 255);
+          }
       }
+      if (wp)
+#pragma unroll
+        for (int r = 0; r < 4; r++)
+#pragma unroll
+          for (int c = 0; c < 4; c++) acc[r][c] = mc_wp_sample(in, 0, q0[r][c], o[r][c], 255);
 #pragma unroll
       for (int r = 0; r < 4; r++) store_row(a.y + (size_t)(y + r) * a.y_stride + x, acc[r], 4, ys_al);
     }
 #pragma unroll
     for (int comp = 1; comp <= 2; comp++) {   // chroma 2x2 of Cb and Cr (4:2:0)
       const int x = (in.x >> 1) + 2 * ux, y = (in.y >> 1) + 2 * uy;
-      int acc[2][2], o[2][2];
+      int acc[2][2], o[2][2], q0[2][2];
 #pragma unroll
       for (int k = 0; k < 2; k++) {
         if (k >= in.nl) break;
@@ -299,8 +348,16 @@ __global__ __launch_bounds__(kMcBlock) void k_mc(McArgs a) {
 #pragma unroll
         for (int r = 0; r < 2; r++)
 #pragma unroll
-          for (int c = 0; c < 2; c++) acc[r][c] = k == 0 ? o[r][c] : clamp_i((acc[r][c] + o[r][c] + 16448) >> 7, 0, 255);
+          for (int c = 0; c < 2; c++) {
+            if (k == 0) q0[r][c] = o[r][c];
+            acc[r][c] = k == 0 ? o[r][c] : clamp_i((acc[r][c] + o[r][c] + 16448) >> 7, 0, 255);
+          }
       }
+      if (wp)
+#pragma unroll
+        for (int r = 0; r < 2; r++)
+#pragma unroll
+          for (int c = 0; c < 2; c++) acc[r][c] = mc_wp_sample(in, comp, q0[r][c], o[r][c], 255);
       uint8_t* base = comp == 1 ? a.cb : a.cr;
 #pragma unroll
       for (int r = 0; r < 2; r++) store_row(base + (size_t)(y + r) * a.c_stride + x, acc[r], 2, cs_al);
@@ -370,8 +427,10 @@ __global__ __launch_bounds__(kMcBlock) void k_mc10(McArgs a) {
         int nl = 0, lists[2] = {0, 0};
         if (j.flags & FME_MC_L0) lists[nl++] = 0;
         if (j.flags & FME_MC_L1) lists[nl++] = 1;
-        if (nl == 2 && j.ref_id[0] == j.ref_id[1] && j.mv[0][0] == j.mv[1][0] && j.mv[0][1] == j.mv[1][1]) nl = 1;
+        in.wp = (j.flags & FME_MC_WP) ? 1 : 0;
+        if (nl == 2 && !in.wp && j.ref_id[0] == j.ref_id[1] && j.mv[0][0] == j.mv[1][0] && j.mv[0][1] == j.mv[1][1]) nl = 1;
         in.nl = nl;
+        if (in.wp) mc_wp_setup(a, j, lists, nl, in);
         for (int k = 0; k < nl; k++) {
           const int l = lists[k];
           const PicDesc p = a.pics[j.ref_id[l]];
@@ -415,10 +474,11 @@ __global__ __launch_bounds__(kMcBlock) void k_mc10(McArgs a) {
     const McJobInfo& in = info[q];
     const int u = g - first_unit[q];
     const int ux = u % in.ux_n, uy = u / in.ux_n;
-    const bool uni = in.nl == 1;
+    const bool wp = in.wp != 0;
+    const bool uni = in.nl == 1 && !wp;   // weighted prediction filters to the 14-bit values (bi form)
     {   // luma 4x4
       const int x = in.x + 4 * ux, y = in.y + 4 * uy;
-      int acc[4][4], o[4][4];
+      int acc[4][4], o[4][4], q0[4][4];
 #pragma unroll
       for (int k = 0; k < 2; k++) {
         if (k >= in.nl) break;
@@ -431,8 +491,16 @@ __global__ __launch_bounds__(kMcBlock) void k_mc10(McArgs a) {
 #pragma unroll
         for (int r = 0; r < 4; r++)
 #pragma unroll
-          for (int c = 0; c < 4; c++) acc[r][c] = k == 0 ? o[r][c] : clamp_i((acc[r][c] + o[r][c] + 16400) >> 5, 0, 1023);
+          for (int c = 0; c < 4; c++) {
+            if (k == 0) q0[r][c] = o[r][c];
+            acc[r][c] = k == 0 ? o[r][c] : clamp_i((acc[r][c] + o[r][c] + 16400) >> 5, 0, 1023);
+          }
       }
+      if (wp)
+#pragma unroll
+        for (int r = 0; r < 4; r++)
+#pragma unroll
+          for (int c = 0; c < 4; c++) acc[r][c] = mc_wp_sample(in, 0, q0[r][c], o[r][c], 1023);
 #pragma unroll
       for (int r = 0; r < 4; r++)
 #pragma unroll
@@ -441,7 +509,7 @@ __global__ __launch_bounds__(kMcBlock) void k_mc10(McArgs a) {
 #pragma unroll
     for (int comp = 1; comp <= 2; comp++) {   // chroma 2x2 of Cb and Cr (4:2:0)
       const int x = (in.x >> 1) + 2 * ux, y = (in.y >> 1) + 2 * uy;
-      int acc[2][2], o[2][2];
+      int acc[2][2], o[2][2], q0[2][2];
 #pragma unroll
       for (int k = 0; k < 2; k++) {
         if (k >= in.nl) break;
@@ -452,8 +520,16 @@ __global__ __launch_bounds__(kMcBlock) void k_mc10(McArgs a) {
 #pragma unroll
         for (int r = 0; r < 2; r++)
 #pragma unroll
-          for (int c = 0; c < 2; c++) acc[r][c] = k == 0 ? o[r][c] : clamp_i((acc[r][c] + o[r][c] + 16400) >> 5, 0, 1023);
+          for (int c = 0; c < 2; c++) {
+            if (k == 0) q0[r][c] = o[r][c];
+            acc[r][c] = k == 0 ? o[r][c] : clamp_i((acc[r][c] + o[r][c] + 16400) >> 5, 0, 1023);
+          }
       }
+      if (wp)
+#pragma unroll
+        for (int r = 0; r < 2; r++)
+#pragma unroll
+          for (int c = 0; c < 2; c++) acc[r][c] = mc_wp_sample(in, comp, q0[r][c], o[r][c], 1023);
       uint16_t* base = comp == 1 ? ocb : ocr;
 #pragma unroll
       for (int r = 0; r < 2; r++)

@@ -156,6 +156,23 @@ PART_2Nx2N, PART_2NxN, PART_Nx2N, PART_NxN, PART_2NxnU, PART_2NxnD, PART_nLx2N, 
 
 MC_L0 = 0x01
 MC_L1 = 0x02
+MC_WP = 0x04   # explicit weighted prediction (fme_set_wp parameters)
+
+# fme_wp_param: WPScalingParam's iWeight, iOffset (8-bit units), uiLog2WeightDenom per component
+WP_PARAM_DTYPE = np.dtype([("weight", "<i2"), ("offset", "<i2"), ("log2_denom", "u1"), ("reserved", "u1", (3,))])
+assert WP_PARAM_DTYPE.itemsize == 8
+
+
+def wp_params(params):
+    """Three fme_wp_param rows (Y, Cb, Cr) from (weight, offset, log2_denom) triples or a
+    WP_PARAM_DTYPE array."""
+    a = np.asarray(params)
+    if a.dtype == WP_PARAM_DTYPE:
+        return np.ascontiguousarray(a.reshape(3))
+    out = np.zeros(3, WP_PARAM_DTYPE)
+    for k, (w, o, d) in enumerate(np.asarray(params, dtype=np.int64).reshape(3, 3)):
+        out[k] = (int(w), int(o), int(d), (0, 0, 0))
+    return out
 
 CONFIG_FIELDS = ("bit_depth", "use_hadamard", "nn_mode", "qp", "fast_inter_mode", "max_jobs")
 

@@ -16,7 +16,7 @@ from .weights import load_weights
 PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB_PATH = os.environ.get("FME_LIB_PATH") or os.path.join(PKG_ROOT, "libfme_amd.so")
 
-ABI_VERSION = 17
+ABI_VERSION = 18
 TIMING_NAMES = ("classify", "scatter", "search", "nn_tail", "batch", "search_main", "search_aux")
 
 # Every entry point include/fme.h declares (the ABI test checks the .so exports them).
@@ -36,7 +36,7 @@ ABI_SYMBOLS = (
     "fme_set_nn_inputs", "fme_integer_search_ring", "fme_integer_search_ring_device",
     "fme_download_device", "fme_pred_inter_phases", "fme_set_search_reserve",
     "fme_pack_jobs", "fme_unpack_jobs", "fme_refine_packed_device", "fme_refine_mv_packed_device",
-    "fme_integer_search2", "fme_integer_search2_device", "fme_warm_copy_engines",
+    "fme_integer_search2", "fme_integer_search2_device", "fme_warm_copy_engines", "fme_set_wp",
 )
 
 
@@ -92,6 +92,7 @@ def load_library(path=None):
         "fme_motion_compensate": (I, [P, P, I, P, I, P, P, I, I, I, P]),
         "fme_motion_compensate_device": (I, [P, P, I, P, I, P, P, I, I, I, P]),
         "fme_mc_invalid_count": (I, [P]),
+        "fme_set_wp": (I, [P, I, I, P]),
         "fme_mc_last_ms": (I, [P, P]),
         "fme_integer_search": (I, [P, P, P, P, I, P]),
         "fme_integer_search_device": (I, [P, P, P, P, I, P]),
@@ -328,6 +329,13 @@ class FmeContext:
         h, w = y.shape
         _check(self.lib, self.lib.fme_motion_compensate(self.h, _ptr(jobs), len(jobs), _ptr(y), y.shape[1], _ptr(cb),
                                                         _ptr(cr), cb.shape[1], w, h, stream))
+
+    def set_wp(self, lst, ref_id, params):
+        """fme_set_wp: weighted-prediction parameters (Y, Cb, Cr) of reference ref_id in list lst;
+        params: 3 rows of (weight, offset, log2_denom) or a WP_PARAM_DTYPE[3] array."""
+        from .abi import WP_PARAM_DTYPE, wp_params
+        arr = wp_params(params)
+        _check(self.lib, self.lib.fme_set_wp(self.h, int(lst), int(ref_id), _ptr(arr)))
 
     def motion_compensate_device(self, d_jobs, n, d_y, y_stride, d_cb, d_cr, c_stride, width, height, stream=None):
         _check(self.lib, self.lib.fme_motion_compensate_device(self.h, C.c_void_p(d_jobs), n, C.c_void_p(d_y), y_stride,

@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define FME_ABI_VERSION 17
+#define FME_ABI_VERSION 18
 
 /* ---- error codes ---------------------------------------------------------------- */
 #define FME_OK            0
@@ -681,6 +681,12 @@ int fme_nn_pred_single(fme_ctx* ctx, const uint32_t* e, uint32_t c, int pu_h, in
  *   mv[l]        list l's MV in quarter-pel luma units (hor, ver), as stored in the CU          */
 #define FME_MC_L0 0x01u
 #define FME_MC_L1 0x02u
+#define FME_MC_WP 0x04u   /* explicit weighted prediction for this PU: the slice's PPS UseWP (P slice)
+                             or WPBiPred (B slice) (TComPrediction.cpp:509-512, 539-542, 612-619): the
+                             lists' 14-bit predictions go through TComWeightPrediction::addWeightUni /
+                             addWeightBi (TComWeightPrediction.cpp:78-245) with the fme_set_wp
+                             parameters, and identical bi motion is not collapsed (xCheckIdenticalMotion
+                             tests !WPBiPred) */
 
 typedef struct fme_mc_job {
   uint16_t x, y;
@@ -707,6 +713,19 @@ int fme_motion_compensate_device(fme_ctx* ctx, const fme_mc_job* d_jobs, int n, 
                                  int y_stride, uint8_t* d_cb, uint8_t* d_cr, int c_stride, int width,
                                  int height, void* stream);
 int fme_mc_invalid_count(fme_ctx* ctx);
+/* Weighted-prediction parameters of reference `ref_id` in list `list` (0 / 1) for the jobs with
+ * FME_MC_WP, per component Y, Cb, Cr: the slice header's WPScalingParam (TComSlice.h:1239-1254)
+ * iWeight, iOffset (in 8-bit units; scaled by 1 << (bitDepth - 8), high-precision offsets off) and
+ * uiLog2WeightDenom (luma / chroma denominators; a bi-pred PU takes list 0's).  getWpScaling's
+ * derivation (TComWeightPrediction.cpp:247-324) runs in the kernels.  Unset entries are the
+ * default weights (1 << 0, offset 0, denominator 0).  Takes effect for later motion compensation. */
+typedef struct fme_wp_param {
+  int16_t weight;
+  int16_t offset;
+  uint8_t log2_denom;     /* 0..7 */
+  uint8_t reserved[3];
+} fme_wp_param;           /* 8 bytes */
+int fme_set_wp(fme_ctx* ctx, int list, int ref_id, const fme_wp_param* ycbcr);
 /* With profiling on: device milliseconds of the last motion-compensation launch (HIP events on
  * its stream); waits for it. */
 int fme_mc_last_ms(fme_ctx* ctx, float* ms);

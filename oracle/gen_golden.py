@@ -154,6 +154,79 @@ def build_mc10_case(name, seed, width, height, bi_frac, mv_amp, identical_frac, 
           f"luma {int(y.min())}..{int(y.max())}")
 
 
+def wp_table(rng, refs):
+    """Explicit WP parameters [list][ref][Y, Cb, Cr][iWeight, iOffset, uiLog2WeightDenom] as a slice
+    header carries them: one luma and one chroma denominator per slice (0..7), weights
+    2^denom + delta (delta -24..24, some exactly 2^denom to reach addWeightUni's unit-weight branch),
+    offsets -128..127 (8-bit units) with some zero."""
+    t = np.zeros((2, refs, 3, 3), np.int32)
+    dl, dc = int(rng.integers(0, 8)), int(rng.integers(0, 8))
+    for l in range(2):
+        for r in range(refs):
+            for c in range(3):
+                d = dl if c == 0 else dc
+                delta = 0 if rng.random() < 0.25 else int(rng.integers(-24, 25))
+                off = 0 if rng.random() < 0.3 else int(rng.integers(-128, 128))
+                t[l, r, c] = ((1 << d) + delta, off, d)
+    return t
+
+
+def build_mcwp_case(name, seed, width, height, bi_frac, mv_amp, identical_frac, wp_frac, bit_depth=8):
+    """Motion compensation with explicit weighted prediction (FME_MC_WP; PPS UseWP / WPBiPred,
+    TComPrediction.cpp:509-512, 612-619): the planes from _ref, which filters each list to the 14-bit
+    values and runs the reference's own TComWeightPrediction::addWeightUni / addWeightBi
+    (TComWeightPrediction.cpp:78-245) with getWpScaling's derivation; a share of the jobs without
+    the flag (plain averaging) and identical bi motion kept as two lists under WP.  The C oracle's
+    orc_mc has no WP: these fixtures pin the HIP path on the reference alone."""
+    from nnfme.abi import MC_WP
+    rng = np.random.default_rng(seed)
+    if bit_depth > 8:
+        pics = mc10_pictures(width, height, 3, seed)
+    else:
+        pics = {}
+        for k in range(3):
+            cb, cr = synth.synth_chroma(width, height, k, seed=seed)
+            pics[k] = (synth.synth_luma(width, height, k, seed=seed), cb, cr)
+    jobs = synth.make_mc_partition(rng, width, height, [0, 1, 2], bi_frac=bi_frac, mv_amp=mv_amp,
+                                   identical_frac=identical_frac)
+    wpm = rng.random(len(jobs)) < wp_frac
+    jobs["flags"] = np.where(wpm, jobs["flags"] | MC_WP, jobs["flags"])
+    wp = wp_table(rng, 3)
+    ref = Reference(bit_depth=bit_depth)
+    for k, (y, cb, cr) in pics.items():
+        ref.set_picture_yuv(k, y, cb, cr)
+    for l in range(2):
+        for r in range(3):
+            ref.set_wp(l, r, wp[l, r])
+    dt = np.uint16 if bit_depth > 8 else np.uint8
+    y = np.zeros((height, width), dt)
+    cb = np.zeros((height // 2, width // 2), dt)
+    cr = cb.copy()
+    ref.mc(jobs, y, cb, cr)
+    path = os.path.join(OUT, f"{name}.npz")
+    np.savez_compressed(
+        path,
+        ref_y=np.stack([pics[k][0] for k in range(3)]),
+        ref_cb=np.stack([pics[k][1] for k in range(3)]),
+        ref_cr=np.stack([pics[k][2] for k in range(3)]),
+        jobs=jobs, wp=wp, bit_depth=np.array([bit_depth], np.int32),
+        pred_y=y, pred_cb=cb, pred_cr=cr,
+    )
+    bi = (jobs["flags"] & 3) == 3
+    same = bi & (jobs["ref_id"][:, 0] == jobs["ref_id"][:, 1]) & (jobs["mv"][:, 0, 0] == jobs["mv"][:, 1, 0]) & \
+        (jobs["mv"][:, 0, 1] == jobs["mv"][:, 1, 1])
+    print(f"{path}: {len(jobs)} PUs, {int(wpm.sum())} weighted, {int((bi & wpm).sum())} weighted bi-pred, "
+          f"{int((same & wpm).sum())} weighted identical-motion, denominators {int(wp[0, 0, 0, 2])}/{int(wp[0, 0, 1, 2])}")
+
+
+MCWP_CASES = [
+    # name, seed, W, H, bi fraction, MV amplitude, identical-motion fraction, WP fraction, bit depth
+    ("mcwp_p_uni", 61, 160, 104, 0.0, 40, 0.0, 0.9, 8),
+    ("mcwp_b_bi", 62, 168, 96, 0.6, 120, 0.2, 0.8, 8),
+    ("mcwp10_b_bi", 63, 128, 80, 0.6, 60, 0.2, 0.8, 10),
+]
+
+
 def build_mc_case(name, seed, width, height, bi_frac, mv_amp, identical_frac, keep_frac=1.0, fill=0):
     """Motion compensation (TComPrediction::motionCompensation): reference pictures with 4:2:0
     chroma, one frame partition of decided PUs, the predicted planes from _ref (the oracle must
@@ -456,6 +529,10 @@ def main():
         for c in TZ10_CASES:
             build_tz10_case(*c)
         return 0
+    if "--mcwp-only" in sys.argv:
+        for c in MCWP_CASES:
+            build_mcwp_case(*c)
+        return 0
     if "--mc10-only" in sys.argv:
         for c in MC10_CASES:
             build_mc10_case(*c)
@@ -476,6 +553,8 @@ def main():
             build_mc_case(*c)
         for c in MC10_CASES:
             build_mc10_case(*c)
+        for c in MCWP_CASES:
+            build_mcwp_case(*c)
     for c in TZ_CASES:
         build_tz_case(*c)
     for c in TZ2_CASES:

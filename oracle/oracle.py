@@ -345,6 +345,7 @@ class Reference:
         lib.ref_bi_key.argtypes = [_P] + [C.c_int] * 11 + [_P]
         lib.ref_mc.restype = C.c_int
         lib.ref_mc.argtypes = [_P, _P, C.c_int, _P, C.c_int, _P, _P, C.c_int, C.c_int, C.c_int]
+        lib.ref_set_wp.argtypes = [_P, C.c_int, C.c_int, _P]
         self.h = lib.ref_create(use_hadamard, fast_inter_mode, nn_mode)
         if bit_depth != 8:
             lib.ref_set_bit_depth(self.h, bit_depth)
@@ -413,6 +414,12 @@ class Reference:
         rows = np.ascontiguousarray(rows, dtype=np.uint32).reshape(-1, 9)
         self._rows = rows   # the library keeps the pointer: keep the array alive
         self.lib.ref_set_nn_inputs(self.h, _ptr(rows), len(rows))
+
+    def set_wp(self, lst, pid, params):
+        """Explicit weighted-prediction parameters of picture pid in list lst for FME_MC_WP jobs:
+        3 rows (Y, Cb, Cr) of (iWeight, iOffset, uiLog2WeightDenom)."""
+        p = np.ascontiguousarray(np.asarray(params, dtype=np.int32).reshape(9))
+        self.lib.ref_set_wp(self.h, int(lst), int(pid), _ptr(p))
 
     def mc(self, mc_jobs, y, cb, cr):
         """Predictions into the planes y / cb / cr in place (uint8, or uint16 at bit depth 10)."""

@@ -28,6 +28,8 @@
 #include "TLibCommon/TComPrediction.h"
 #include "TLibCommon/TComRdCost.h"
 #include "TLibCommon/TComRom.h"
+#include "TLibCommon/TComSlice.h"
+#include "TLibCommon/TComWeightPrediction.h"
 #include "TLibCommon/TComYuv.h"
 
 #include "../include/fme.h"
@@ -291,6 +293,13 @@ struct RefCtx {
   uint32_t slot[8] = {0};
   uint32_t C = 0, puh = 0, puw = 0;
   std::vector<uint32_t> nn_in;   // FME_JOB_NN_IN rows (ref_set_nn_inputs), 9 per job
+  // explicit WP parameters per [list][picture][component]: iWeight, iOffset, uiLog2WeightDenom
+  int wp[2][FME_MAX_PICTURES][3][3];
+  RefCtx() {
+    for (auto& l : wp)
+      for (auto& p : l)
+        for (auto& c : p) { c[0] = 1; c[1] = 0; c[2] = 0; }
+  }
 };
 
 int nnClass(const float* P, const uint32_t* e, uint32_t c, int H, int W) {
@@ -630,8 +639,11 @@ static int mc_run(void* h, const fme_mc_job* jobs, int n, S* y, int ys, S* cb, S
     if (j.flags & FME_MC_L1) lists[nl++] = 1;
     for (int k = 0; k < nl; k++)
       if (!c->pics[j.ref_id[lists[k]]].set420) return -1 - i;
-    if (nl == 2 && j.ref_id[0] == j.ref_id[1] && j.mv[0][0] == j.mv[1][0] && j.mv[0][1] == j.mv[1][1]) nl = 1;
+    const bool wpf = (j.flags & FME_MC_WP) != 0;   // PPS UseWP (P) / WPBiPred (B)
+    // xCheckIdenticalMotion (TComPrediction.cpp:476-492) collapses only without WPBiPred
+    if (nl == 2 && !wpf && j.ref_id[0] == j.ref_id[1] && j.mv[0][0] == j.mv[1][0] && j.mv[0][1] == j.mv[1][1]) nl = 1;
     const bool bi = nl == 2;
+    const bool inter = bi || wpf;   // the lists' 14-bit values (xPredInterUni(..., bi = true))
     TComYuv pred[2], out;
     for (int k = 0; k < 2; k++) pred[k].create(j.w, j.h, CHROMA_420);
     out.create(j.w, j.h, CHROMA_420);
@@ -644,7 +656,7 @@ static int mc_run(void* h, const fme_mc_job* jobs, int n, S* y, int ys, S* cb, S
         mx = std::min(hmax, std::max(hmin, mx));
         my = std::min(vmax, std::max(vmin, my));
       }
-      TComYuv& dstYuv = bi ? pred[k] : out;
+      TComYuv& dstYuv = inter ? pred[k] : out;
       for (int comp = 0; comp < 3; comp++) {
         const ComponentID cid = ComponentID(comp);
         const int csx = comp ? 1 : 0;
@@ -656,18 +668,53 @@ static int mc_run(void* h, const fme_mc_job* jobs, int n, S* y, int ys, S* cb, S
         const int xf = mx & ((1 << shH) - 1), yf = my & ((1 << shV) - 1);
         const int cw = j.w >> csx, ch = j.h >> csx;
         if (yf == 0) {
-          f.filterHor(cid, src, rs, dst, dstS, cw, ch, xf, !bi, CHROMA_420, depth);
+          f.filterHor(cid, src, rs, dst, dstS, cw, ch, xf, !inter, CHROMA_420, depth);
         } else if (xf == 0) {
-          f.filterVer(cid, src, rs, dst, dstS, cw, ch, yf, true, !bi, CHROMA_420, depth);
+          f.filterVer(cid, src, rs, dst, dstS, cw, ch, yf, true, !inter, CHROMA_420, depth);
         } else {
           const int nt = comp ? NTAPS_CHROMA : NTAPS_LUMA;
           std::vector<Pel> tmp((size_t)cw * (ch + nt - 1));
           f.filterHor(cid, src - ((nt >> 1) - 1) * rs, rs, tmp.data(), cw, cw, ch + nt - 1, xf, false, CHROMA_420, depth);
-          f.filterVer(cid, tmp.data() + ((nt >> 1) - 1) * cw, cw, dst, dstS, cw, ch, yf, false, !bi, CHROMA_420, depth);
+          f.filterVer(cid, tmp.data() + ((nt >> 1) - 1) * cw, cw, dst, dstS, cw, ch, yf, false, !inter, CHROMA_420, depth);
         }
       }
     }
-    if (bi) out.addAvg(&pred[0], &pred[1], 0, j.w, j.h, bd);
+    if (wpf) {
+      // getWpScaling (TComWeightPrediction.cpp:247-324) restated (TComDataCU / TComSlice are not
+      // built here), then the reference's own addWeightBi / addWeightUni
+      WPScalingParam w0[3], w1[3];
+      const int scale = 1 << (depth - 8);   // high-precision offsets off
+      for (int comp = 0; comp < 3; comp++) {
+        for (int k = 0; k < nl; k++) {
+          const int* q = c->wp[lists[k]][j.ref_id[lists[k]]][comp];
+          WPScalingParam& w = (k == 0 ? w0 : w1)[comp];
+          w.bPresentFlag = true;
+          w.iWeight = q[0];
+          w.iOffset = q[1];
+          w.uiLog2WeightDenom = (UInt)q[2];
+          w.w = q[0];
+        }
+        if (bi) {
+          w0[comp].o = w0[comp].iOffset * scale;
+          w1[comp].o = w1[comp].iOffset * scale;
+          w0[comp].offset = w0[comp].o + w1[comp].o;
+          w0[comp].shift = (Int)w0[comp].uiLog2WeightDenom + 1;
+          w0[comp].round = 1 << w0[comp].uiLog2WeightDenom;
+          w1[comp].offset = w0[comp].offset;
+          w1[comp].shift = w0[comp].shift;
+          w1[comp].round = w0[comp].round;
+        } else {
+          w0[comp].offset = w0[comp].iOffset * scale;
+          w0[comp].shift = (Int)w0[comp].uiLog2WeightDenom;
+          w0[comp].round = w0[comp].uiLog2WeightDenom >= 1 ? (1 << (w0[comp].uiLog2WeightDenom - 1)) : 0;
+        }
+      }
+      TComWeightPrediction wpr;
+      if (bi) wpr.addWeightBi(&pred[0], &pred[1], bd, 0, j.w, j.h, w0, w1, &out);
+      else wpr.addWeightUni(&pred[0], bd, 0, j.w, j.h, w0, &out);
+    } else if (bi) {
+      out.addAvg(&pred[0], &pred[1], 0, j.w, j.h, bd);
+    }
     for (int comp = 0; comp < 3; comp++) {
       const ComponentID cid = ComponentID(comp);
       const int csx = comp ? 1 : 0;
@@ -685,6 +732,13 @@ static int mc_run(void* h, const fme_mc_job* jobs, int n, S* y, int ys, S* cb, S
   return 0;
 }
 }  // extern "C++"
+// Explicit weighted-prediction parameters of (list, picture) for FME_MC_WP jobs: per component
+// {iWeight, iOffset, uiLog2WeightDenom} (fme_set_wp).
+void ref_set_wp(void* h, int list, int id, const int* p9) {
+  RefCtx* c = static_cast<RefCtx*>(h);
+  for (int comp = 0; comp < 3; comp++)
+    for (int k = 0; k < 3; k++) c->wp[list][id][comp][k] = p9[3 * comp + k];
+}
 int ref_mc(void* h, const fme_mc_job* jobs, int n, uint8_t* y, int ys, uint8_t* cb, uint8_t* cr, int cs, int width,
            int height) {
   return mc_run(h, jobs, n, y, ys, cb, cr, cs, width, height, 8);

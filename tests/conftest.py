@@ -35,7 +35,7 @@ def pytest_collection_modifyitems(config, items):
 def golden_cases():
     """Sub-pel refinement fixtures (fme_job -> fme_result)."""
     return sorted(f[:-4] for f in os.listdir(GOLDEN)
-                  if f.endswith(".npz") and not f.startswith(("mc_", "mc10_", "tz_", "tz10_", "ring_", "main10_")))
+                  if f.endswith(".npz") and not f.startswith(("mc_", "mc10_", "mcwp", "tz_", "tz10_", "ring_", "main10_")))
 
 
 def main10_golden_cases():

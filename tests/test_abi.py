@@ -19,11 +19,11 @@ def header_functions():
 def test_library_exports_header():
     lib = runtime.load_library()
     names = header_functions()
-    assert len(names) == 60
+    assert len(names) == 61
     assert set(names) == set(runtime.ABI_SYMBOLS)
     for n in names:
         assert hasattr(lib, n), n
-    assert lib.fme_abi_version() == runtime.ABI_VERSION == 17
+    assert lib.fme_abi_version() == runtime.ABI_VERSION == 18
 
 
 def test_struct_layouts():
@@ -42,6 +42,7 @@ def test_struct_layouts():
     assert abi.MV_RESULT_DTYPE.fields["cost"][1] == 4
     assert abi.MV_RESULT_DTYPE.fields["status"][1] == 14
     assert abi.TZ_EXT_DTYPE.itemsize == 12
+    assert abi.WP_PARAM_DTYPE.itemsize == 8 and abi.WP_PARAM_DTYPE.fields["log2_denom"][1] == 4
     assert abi.TZ_EXT_DTYPE.fields["flags"][1] == 8
 
 
