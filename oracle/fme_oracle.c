@@ -758,12 +758,35 @@ static void mc_pred_blk(const uint8_t* plane, int stride, int pw, int ph, int ch
   free(tmp);
 }
 
-int orc_mc(const orc_yuv* pics, const fme_mc_job* jobs, int n, uint8_t* y, int ys, uint8_t* cb, uint8_t* cr,
-           int cs, int width, int height) {
+/* Explicit weighted prediction (TComWeightPrediction.cpp), restated: getWpScaling (247-324) from
+ * wp[list][picture][component] = {iWeight, iOffset (8-bit units), uiLog2WeightDenom}, then
+ * weightBidir / weightUnidir / noWeightUnidir (46-66) as addWeightBi / addWeightUni pick them
+ * (78-245) on the lists' 14-bit values, 8-bit output (shiftNum 6, IF_INTERNAL_OFFS 8192). */
+static int wp_sample(const int (*wp)[FME_MAX_PICTURES][3][3], const fme_mc_job* j, const int* lists, int nl,
+                     int comp, int p0, int p1) {
+  const int shift_num = 6;   /* max(2, IF_INTERNAL_PREC - 8) */
+  const int* a = wp[lists[0]][j->ref_id[lists[0]]][comp];
+  if (nl == 2) {
+    const int* b = wp[1][j->ref_id[1]][comp];
+    const int offset = a[1] + b[1];                     /* o0 + o1, offsetScalingFactor 1 */
+    const int shift = a[2] + 1 + shift_num, round = 1 << (shift - 1);
+    return clampi((a[0] * (p0 + 8192) + b[0] * (p1 + 8192) + round + offset * (1 << (shift - 1))) >> shift, 0, 255);
+  }
+  if (a[0] != (1 << a[2])) {                            /* weightUnidir */
+    const int shift = a[2] + shift_num, round = shift > 0 ? 1 << (shift - 1) : 0;
+    return clampi(((a[0] * (p0 + 8192) + round) >> shift) + a[1], 0, 255);
+  }
+  /* noWeightUnidir / noWeightOffsetUnidir: shiftNum alone */
+  return clampi((((p0 + 8192) + (1 << (shift_num - 1))) >> shift_num) + a[1], 0, 255);
+}
+
+static int mc_run_jobs(const orc_yuv* pics, const fme_mc_job* jobs, int n, uint8_t* y, int ys, uint8_t* cb,
+                       uint8_t* cr, int cs, int width, int height, const int (*wp)[FME_MAX_PICTURES][3][3]) {
   for (int i = 0; i < n; i++) {
     const fme_mc_job* j = &jobs[i];
+    const int wpf = wp && (j->flags & FME_MC_WP);
     if (j->w < 4 || j->h < 4 || j->w > 64 || j->h > 64 || (j->w & 3) || (j->h & 3)) return -1 - i;
-    if (!(j->flags & 3u) || (j->flags & ~3u)) return -1 - i;
+    if (!(j->flags & 3u) || (j->flags & ~(wp ? 7u : 3u))) return -1 - i;
     if (j->x + j->w > width || j->y + j->h > height) return -1 - i;
     for (int l = 0; l < 2; l++)
       if ((j->flags & (1u << l)) &&
@@ -773,8 +796,9 @@ int orc_mc(const orc_yuv* pics, const fme_mc_job* jobs, int n, uint8_t* y, int y
     int lists[2], nl = 0;
     if (j->flags & FME_MC_L0) lists[nl++] = 0;
     if (j->flags & FME_MC_L1) lists[nl++] = 1;
-    /* xCheckIdenticalMotion (TComPrediction.cpp:476-492) */
-    if (nl == 2 && j->ref_id[0] == j->ref_id[1] && j->mv[0][0] == j->mv[1][0] && j->mv[0][1] == j->mv[1][1]) nl = 1;
+    /* xCheckIdenticalMotion (TComPrediction.cpp:476-492; not with WPBiPred) */
+    if (nl == 2 && !wpf && j->ref_id[0] == j->ref_id[1] && j->mv[0][0] == j->mv[1][0] && j->mv[0][1] == j->mv[1][1])
+      nl = 1;
     for (int comp = 0; comp < 3; comp++) {
       const int c = comp ? 1 : 0;
       const int w = j->w >> c, h = j->h >> c, x0 = j->x >> c, y0 = j->y >> c;
@@ -785,7 +809,7 @@ int orc_mc(const orc_yuv* pics, const fme_mc_job* jobs, int n, uint8_t* y, int y
         mc_clip_mv(&mx, &my, p->width, p->height, j->cu_x, j->cu_y);
         const uint8_t* plane = comp == 0 ? p->y : (comp == 1 ? p->cb : p->cr);
         mc_pred_blk(plane, comp ? p->c_stride : p->y_stride, p->width >> c, p->height >> c, c, x0, y0, w, h, mx, my,
-                    nl == 2, pred[k], w);
+                    nl == 2 || wpf, pred[k], w);
       }
       uint8_t* out = comp == 0 ? y : (comp == 1 ? cb : cr);
       const int os = comp ? cs : ys;
@@ -793,12 +817,24 @@ int orc_mc(const orc_yuv* pics, const fme_mc_job* jobs, int n, uint8_t* y, int y
         for (int q = 0; q < w; q++) {
           int v = pred[0][r * w + q];
           /* TComYuv::addAvg (TComYuv.cpp:354-415): shiftNum 7, offset 64 + 2 * 8192 */
-          if (nl == 2) v = clampi((pred[0][r * w + q] + pred[1][r * w + q] + 16448) >> 7, 0, 255);
+          if (wpf) v = wp_sample(wp, j, lists, nl, comp, pred[0][r * w + q], nl == 2 ? pred[1][r * w + q] : 0);
+          else if (nl == 2) v = clampi((pred[0][r * w + q] + pred[1][r * w + q] + 16448) >> 7, 0, 255);
           out[(size_t)(y0 + r) * os + x0 + q] = (uint8_t)v;
         }
     }
   }
   return 0;
+}
+
+int orc_mc(const orc_yuv* pics, const fme_mc_job* jobs, int n, uint8_t* y, int ys, uint8_t* cb, uint8_t* cr,
+           int cs, int width, int height) {
+  return mc_run_jobs(pics, jobs, n, y, ys, cb, cr, cs, width, height, NULL);
+}
+
+/* orc_mc with FME_MC_WP jobs weighted by wp9 = [2][FME_MAX_PICTURES][3 components][3] ints. */
+int orc_mc_wp(const orc_yuv* pics, const fme_mc_job* jobs, int n, const int* wp9, uint8_t* y, int ys, uint8_t* cb,
+              uint8_t* cr, int cs, int width, int height) {
+  return mc_run_jobs(pics, jobs, n, y, ys, cb, cr, cs, width, height, (const int (*)[FME_MAX_PICTURES][3][3])wp9);
 }
 
 /* =====================================================================================

@@ -151,6 +151,11 @@ typedef struct orc_yuv {
  * pics[ref_id] are the reference pictures.  Returns 0, or -1-i for an invalid job i. */
 int orc_mc(const orc_yuv* pics, const fme_mc_job* jobs, int n, uint8_t* y, int y_stride,
            uint8_t* cb, uint8_t* cr, int c_stride, int width, int height);
+/* Motion compensation with explicit weighted prediction for the jobs with FME_MC_WP (8-bit):
+ * wp9 = int[2][FME_MAX_PICTURES][3][3], per list, picture and component {iWeight, iOffset,
+ * uiLog2WeightDenom}. */
+int orc_mc_wp(const orc_yuv* pics, const fme_mc_job* jobs, int n, const int* wp9, uint8_t* y, int ys,
+              uint8_t* cb, uint8_t* cr, int cs, int width, int height);
 
 /* ---- predInterSearch's P-slice PU / reference loop: each request in
  * order, each reference index in order, exactly as TEncSearch.cpp:3746-3866 runs them (AMVP

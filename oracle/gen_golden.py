@@ -177,7 +177,7 @@ def build_mcwp_case(name, seed, width, height, bi_frac, mv_amp, identical_frac, 
     values and runs the reference's own TComWeightPrediction::addWeightUni / addWeightBi
     (TComWeightPrediction.cpp:78-245) with getWpScaling's derivation; a share of the jobs without
     the flag (plain averaging) and identical bi motion kept as two lists under WP.  The C oracle's
-    orc_mc has no WP: these fixtures pin the HIP path on the reference alone."""
+    orc_mc_wp agrees at 8 bits (tests/test_mc_wp.py); the 10-bit fixture rests on the reference."""
     from nnfme.abi import MC_WP
     rng = np.random.default_rng(seed)
     if bit_depth > 8:

@@ -262,8 +262,9 @@ class Oracle:
         r = np.ascontiguousarray(np.asarray(req, dtype=PU_REQ_DTYPE).reshape(1))
         return int(self.lib.orc_template_cost(self.ctx, _ptr(r), int(k), int(m)))
 
-    def mc(self, pics, mc_jobs, y, cb, cr):
-        """orc_mc: pics = {id: (Y, Cb, Cr)} reference pictures; predicts into y/cb/cr in place."""
+    def mc(self, pics, mc_jobs, y, cb, cr, wp=None):
+        """orc_mc: pics = {id: (Y, Cb, Cr)} reference pictures; predicts into y/cb/cr in place.
+        wp: [2][refs][3][3] (iWeight, iOffset, uiLog2WeightDenom) for the FME_MC_WP jobs (orc_mc_wp)."""
         class Yuv(C.Structure):
             _fields_ = [("y", C.c_void_p), ("cb", C.c_void_p), ("cr", C.c_void_p), ("y_stride", C.c_int),
                         ("c_stride", C.c_int), ("width", C.c_int), ("height", C.c_int)]
@@ -276,8 +277,17 @@ class Oracle:
                            py.shape[1], py.shape[0])
         jobs = np.ascontiguousarray(mc_jobs)
         h, w = y.shape
-        rc = self.lib.orc_mc(C.cast(arr, C.c_void_p), _ptr(jobs), len(jobs), _ptr(y), y.shape[1], _ptr(cb), _ptr(cr),
-                             cb.shape[1], w, h)
+        if wp is not None:
+            t = np.zeros((2, 64, 3, 3), np.int32)
+            t[..., 0] = 1
+            wp = np.asarray(wp, dtype=np.int32)
+            t[:, :wp.shape[1]] = wp
+            self.lib.orc_mc_wp.argtypes = [_P, _P, C.c_int, _P, _P, C.c_int, _P, _P, C.c_int, C.c_int, C.c_int]
+            rc = self.lib.orc_mc_wp(C.cast(arr, C.c_void_p), _ptr(jobs), len(jobs), _ptr(t), _ptr(y), y.shape[1],
+                                    _ptr(cb), _ptr(cr), cb.shape[1], w, h)
+        else:
+            rc = self.lib.orc_mc(C.cast(arr, C.c_void_p), _ptr(jobs), len(jobs), _ptr(y), y.shape[1], _ptr(cb), _ptr(cr),
+                                 cb.shape[1], w, h)
         if rc != 0:
             raise RuntimeError(f"orc_mc: invalid job {-1 - rc}")
 

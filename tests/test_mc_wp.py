@@ -5,8 +5,8 @@ TComWeightPrediction::addWeightUni / addWeightBi (TComWeightPrediction.cpp:78-24
 getWpScaling's parameters (247-324), and xCheckIdenticalMotion not collapsing identical bi motion.
 
 Fixtures (tests/golden/mcwp*_*.npz, oracle/gen_golden.py) come from oracle/_ref, which drives the
-reference's own filters and TComWeightPrediction; the C oracle has no WP (parity pinned on the
-reference alone).  Integer planes: bit-exact."""
+reference's own filters and TComWeightPrediction; the C oracle's orc_mc_wp restates it at 8 bits
+and agrees (the 10-bit fixture is pinned on the reference alone).  Integer planes: bit-exact."""
 import os
 
 import numpy as np
@@ -63,6 +63,20 @@ def test_mcwp_goldens_cover_the_branches():
 def test_mcwp_reference_harness_matches_golden(case):
     g = load_golden(case)
     y, cb, cr = _run_ref(_reference(g), g, g["jobs"], g["wp"])
+    assert np.array_equal(y, g["pred_y"]) and np.array_equal(cb, g["pred_cb"]) and np.array_equal(cr, g["pred_cr"])
+
+
+@pytest.mark.parametrize("case", [c for c in CASES if not c.startswith("mcwp10")])
+def test_mcwp_oracle_matches_golden(case):
+    """orc_mc_wp (the C restatement of getWpScaling + weightBidir / weightUnidir / noWeightUnidir,
+    8-bit) against the reference's own TComWeightPrediction run."""
+    from oracle import Oracle
+    g = load_golden(case)
+    pics = {k: (g["ref_y"][k], g["ref_cb"][k], g["ref_cr"][k]) for k in range(len(g["ref_y"]))}
+    y = np.zeros_like(g["pred_y"])
+    cb = np.zeros_like(g["pred_cb"])
+    cr = np.zeros_like(g["pred_cr"])
+    Oracle().mc(pics, g["jobs"], y, cb, cr, wp=g["wp"])
     assert np.array_equal(y, g["pred_y"]) and np.array_equal(cb, g["pred_cb"]) and np.array_equal(cr, g["pred_cr"])
 
 
