@@ -159,9 +159,17 @@ void MotionCompensator::setPictureYuv8(int id, const uint8_t* y, int ys, const u
   check(fme_set_picture_chroma(search_.ctx(), id, cb, cr, cs, nullptr), "fme_set_picture_chroma");
 }
 
+void MotionCompensator::setWp(int list, int id, const int weight[3], const int offset[3], const int log2Denom[3]) {
+  fme_wp_param p[3];
+  for (int c = 0; c < 3; c++) p[c] = fme_wp_param{(int16_t)weight[c], (int16_t)offset[c], (uint8_t)log2Denom[c], {0, 0, 0}};
+  std::lock_guard<std::mutex> lk(search_.mutex());
+  check(fme_set_wp(search_.ctx(), list, id, p), "fme_set_wp");
+}
+
 void MotionCompensator::add(int x, int y, int w, int h, int cuX, int cuY, int refIdL0, const Mv& mvL0, int refIdL1,
-                            const Mv& mvL1) {
+                            const Mv& mvL1, bool weighted) {
   fme_mc_job j = {};
+  if (weighted) j.flags |= FME_MC_WP;
   j.x = (uint16_t)x;
   j.y = (uint16_t)y;
   j.w = (uint8_t)w;

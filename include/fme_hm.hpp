@@ -117,8 +117,13 @@ class MotionCompensator {
                      int height);
   void setPictureYuv8(int id, const uint8_t* y, int yStride, const uint8_t* cb, const uint8_t* cr, int cStride,
                       int width, int height);
-  // Queue one PU: uni-pred when only one of mvL0 / mvL1 is given (refIdL* < 0 for the other).
-  void add(int x, int y, int w, int h, int cuX, int cuY, int refIdL0, const Mv& mvL0, int refIdL1, const Mv& mvL1);
+  // Explicit weighted prediction of reference `id` in list `list` (the slice header's
+  // WPScalingParam iWeight / iOffset / uiLog2WeightDenom for Y, Cb, Cr; fme_set_wp).
+  void setWp(int list, int id, const int weight[3], const int offset[3], const int log2Denom[3]);
+  // Queue one PU: uni-pred when only one of mvL0 / mvL1 is given (refIdL* < 0 for the other);
+  // weighted: the slice's UseWP (P) / WPBiPred (B) (FME_MC_WP).
+  void add(int x, int y, int w, int h, int cuX, int cuY, int refIdL0, const Mv& mvL0, int refIdL1, const Mv& mvL1,
+           bool weighted = false);
   int pending() const { return (int)jobs_.size(); }
   // Predict every queued PU into the 8-bit planes (width x height luma) and clear the queue.
   void run(uint8_t* y, int yStride, uint8_t* cb, uint8_t* cr, int cStride, int width, int height);

@@ -294,6 +294,33 @@ static int run() {
            "orc_mc rejected the jobs");
     EXPECT(gy == oy, "MotionCompensator luma differs from orc_mc");
     EXPECT(gcb == ocb && gcr == ocr, "MotionCompensator chroma differs from orc_mc");
+
+    // the same PUs with explicit weighted prediction (setWp + weighted add) against orc_mc_wp
+    static int wp9[2][FME_MAX_PICTURES][3][3];
+    for (int l = 0; l < 2; l++)
+      for (int i = 0; i < FME_MAX_PICTURES; i++)
+        for (int c = 0; c < 3; c++) { wp9[l][i][c][0] = 1; wp9[l][i][c][1] = 0; wp9[l][i][c][2] = 0; }
+    for (int l = 0; l < 2; l++)
+      for (int i = 10; i < 13; i++) {
+        int w[3], o[3], d[3];
+        for (int c = 0; c < 3; c++) {
+          d[c] = c ? 5 : 3;
+          w[c] = (1 << d[c]) + (int)(rng() % 31) - 15;
+          o[c] = (int)(rng() % 101) - 50;
+          wp9[l][i][c][0] = w[c]; wp9[l][i][c][1] = o[c]; wp9[l][i][c][2] = d[c];
+        }
+        mc.setWp(l, i, w, o, d);
+      }
+    for (fme_mc_job& j : jobs) {
+      j.flags |= FME_MC_WP;
+      mc.add(j.x, j.y, j.w, j.h, j.cu_x, j.cu_y, j.ref_id[0], fme_hm::Mv(j.mv[0][0], j.mv[0][1]),
+             (j.flags & FME_MC_L1) ? j.ref_id[1] : -1, fme_hm::Mv(j.mv[1][0], j.mv[1][1]), true);
+    }
+    mc.run(gy.data(), W, gcb.data(), gcr.data(), W / 2, W, H);
+    EXPECT(orc_mc_wp(yuv, jobs.data(), (int)jobs.size(), &wp9[0][0][0][0], oy.data(), W, ocb.data(), ocr.data(), W / 2,
+                     W, H) == 0, "orc_mc_wp rejected the jobs");
+    EXPECT(gy == oy, "MotionCompensator weighted luma differs from orc_mc_wp");
+    EXPECT(gcb == ocb && gcr == ocr, "MotionCompensator weighted chroma differs from orc_mc_wp");
   }
 
   // ---- InterSearchP: predInterSearch's P-slice PU / reference loop ----------
