@@ -126,3 +126,17 @@ def test_gpu_mcwp_matches_golden(case):
     from nnfme.runtime import FmeError
     with pytest.raises(FmeError):
         ctx.set_wp(2, 0, g["wp"][0, 0])
+
+
+def test_unit_weight_branch_identity():
+    """k_mc / k_mc10 use one uni-pred formula, ((w (p + 8192) + 2^(s-1)) >> s) + o with s = d + shiftNum,
+    where addWeightUni switches to noWeightUnidir ((p + 8192 + 2^(n-1)) >> n) + o when w == 1 << d
+    (TComWeightPrediction.cpp:170-238): the two agree for every 14-bit value, denominator and bit depth."""
+    p = np.arange(-8192, 16384 + 1, dtype=np.int64)
+    for bd in (8, 10):
+        n = max(2, 14 - bd)
+        for d in range(8):
+            s = d + n
+            one = ((1 << d) * (p + 8192) + (1 << (s - 1))) >> s
+            two = (p + 8192 + (1 << (n - 1))) >> n
+            assert np.array_equal(one, two), (bd, d)
